@@ -1,0 +1,96 @@
+// pybind11 module `_nidt_hip`: host entry points of the gfx950 kernels in csrc/kernels/*.hip.
+// Every function takes raw device pointers (uintptr_t), sizes and a hipStream_t (as uintptr_t); shape and dtype
+// validation happens in the Python wrappers (neuroimagedisttraining_amd/ops) before any launch.
+#include <pybind11/pybind11.h>
+#include <cstdint>
+
+namespace nidt {
+// optim.hip
+int64_t clip_sgd_mask_workspace(int64_t C, int64_t P);
+void clip_sgd_mask(uintptr_t w, uintptr_t g, uintptr_t buf, uintptr_t mask, uintptr_t part, uintptr_t coef_out,
+                   uintptr_t wbf, int64_t C, int64_t P, int64_t stride, float lr, float wd, float mom, int first,
+                   float max_norm, uintptr_t stream);
+void weighted_rows_sum(uintptr_t rows, uintptr_t wts, int64_t C, int64_t P, int64_t stride, float beta, uintptr_t out,
+                       uintptr_t stream);
+void broadcast_row(uintptr_t src, int64_t P, int64_t stride, int64_t C, uintptr_t dst, uintptr_t stream);
+// conv3d.hip
+void conv3d_fwd(uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t xs, uintptr_t xt, uintptr_t y, uintptr_t stats,
+                int G, int B, int D, int H, int W, int Cin, int Cout, int pad, uintptr_t stream);
+int conv3d_fwd_nblocks(int B, int D, int H, int W, int pad);
+void conv3d_wgrad(uintptr_t x, uintptr_t xs, uintptr_t xt, uintptr_t dy, uintptr_t part, uintptr_t grad, int64_t ldg,
+                  int64_t off, int G, int B, int D, int H, int W, int Cin, int Cout, int pad, int nsplit, float scale,
+                  uintptr_t stream);
+int conv3d_wgrad_nsplit(int G, int B, int D, int H, int W, int Cin, int Cout, int pad);
+void pack_conv_w(uintptr_t theta, int64_t ldt, int64_t off, int G, int Cout, int Cin, float scale, uintptr_t wp,
+                 uintptr_t wt, uintptr_t stream);
+// bn.hip
+void bn_finalize(uintptr_t stats, int nPB, int BP, int Mg, int G, int C, uintptr_t theta, int64_t ldt, int64_t off_g,
+                 int64_t off_b, uintptr_t bufs, int64_t ldb, int64_t off_rm, int64_t off_rv, int64_t off_nbt,
+                 float momentum, float eps, uintptr_t scale, uintptr_t shift, uintptr_t mean, uintptr_t invstd,
+                 int update_running, uintptr_t stream);
+void bn_eval(int G, int C, uintptr_t theta, int64_t ldt, int64_t off_g, int64_t off_b, uintptr_t bufs, int64_t ldb,
+             int64_t off_rm, int64_t off_rv, float eps, uintptr_t scale, uintptr_t shift, uintptr_t stream);
+void bn_relu_pool(uintptr_t y, uintptr_t scale, uintptr_t shift, uintptr_t out, uintptr_t amax, int NB, int B, int D,
+                  int H, int W, int C, uintptr_t stream);
+void bn_bwd(int pool, uintptr_t y, uintptr_t dsrc, uintptr_t pout, uintptr_t amax, uintptr_t scale, uintptr_t shift,
+            uintptr_t mean, uintptr_t invstd, int NB, int B, int D, int H, int W, int C, uintptr_t part, int nchunk,
+            uintptr_t theta, int64_t ldt, int64_t off_g, uintptr_t grad, int64_t ldg, int64_t goff_g, int64_t goff_b,
+            int64_t goff_convb, uintptr_t coef, uintptr_t dy, uintptr_t stream);
+// conv1.hip
+void polyphase(uintptr_t src, uintptr_t dst, int64_t N, uintptr_t stream);
+void conv1_sample_moments(uintptr_t x8, int64_t N, uintptr_t mom, uintptr_t stream);
+void pack_conv1_w(uintptr_t theta, int64_t ldt, int64_t off, int G, float scale, uintptr_t w8, uintptr_t w125,
+                  uintptr_t stream);
+void conv1_bnstats(uintptr_t mom, uintptr_t idx, int B, int G, uintptr_t Mb, uintptr_t w125, uintptr_t theta,
+                   int64_t ldt, int64_t off_bias, int64_t off_g, int64_t off_b, uintptr_t bufs, int64_t ldb,
+                   int64_t off_rm, int64_t off_rv, int64_t off_nbt, float momentum, float eps, int update_running,
+                   uintptr_t scale, uintptr_t shift, uintptr_t mean, uintptr_t invstd, uintptr_t mu, uintptr_t covw,
+                   uintptr_t stream);
+void conv1_fwd_pool(uintptr_t x8, uintptr_t idx, uintptr_t w8, uintptr_t scale, uintptr_t shift, int NB, int B,
+                    uintptr_t out, uintptr_t amax, uintptr_t stream);
+void conv1_wgrad(uintptr_t x8, uintptr_t idx, uintptr_t dp, uintptr_t pout, uintptr_t amax, int NB, int B,
+                 uintptr_t part, uintptr_t w125, uintptr_t mu, uintptr_t covw, uintptr_t invstd, uintptr_t theta,
+                 int64_t ldt, int64_t off_g, uintptr_t grad, int64_t ldg, int64_t goff_w, int64_t goff_bias,
+                 int64_t goff_g, int64_t goff_b, float wscale, uintptr_t stream);
+// head.hip
+void head(uintptr_t p5, uintptr_t theta, int64_t ldt, int64_t off_w1, int64_t off_b1, int64_t off_w2, int64_t off_b2,
+          uintptr_t y, uintptr_t logits, uintptr_t loss, uintptr_t grad, int64_t ldg, uintptr_t dp5, int G, int B,
+          int train, float keep, uint64_t seed, uintptr_t stream);
+// select.hip
+void saliency_acc(uintptr_t theta, uintptr_t grad, int64_t ld, int64_t P, int G, float alpha, uintptr_t score,
+                  int64_t lds, uintptr_t stream);
+void radix_select_kth(uintptr_t v, int64_t n, int64_t k, uintptr_t state, uintptr_t hist, uintptr_t stream);
+void threshold_mask(uintptr_t v, int64_t n, uintptr_t state, uintptr_t mask, uintptr_t stream);
+void mask_stats(uintptr_t a, uintptr_t b, int64_t n, uintptr_t out, uintptr_t stream);
+}  // namespace nidt
+
+PYBIND11_MODULE(_nidt_hip, m) {
+  m.doc() = "gfx950 (MI355X) HIP kernels of neuroimagedisttraining_amd";
+  m.attr("ARCH") = "gfx950";
+#define DEF(name) m.def(#name, &nidt::name)
+  DEF(clip_sgd_mask_workspace);
+  DEF(clip_sgd_mask);
+  DEF(weighted_rows_sum);
+  DEF(broadcast_row);
+  DEF(conv3d_fwd);
+  DEF(conv3d_fwd_nblocks);
+  DEF(conv3d_wgrad);
+  DEF(conv3d_wgrad_nsplit);
+  DEF(pack_conv_w);
+  DEF(bn_finalize);
+  DEF(bn_eval);
+  DEF(bn_relu_pool);
+  DEF(bn_bwd);
+  DEF(polyphase);
+  DEF(conv1_sample_moments);
+  DEF(pack_conv1_w);
+  DEF(conv1_bnstats);
+  DEF(conv1_fwd_pool);
+  DEF(conv1_wgrad);
+  DEF(head);
+  DEF(saliency_acc);
+  DEF(radix_select_kth);
+  DEF(threshold_mask);
+  DEF(mask_stats);
+#undef DEF
+}

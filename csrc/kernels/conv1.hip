@@ -1,0 +1,547 @@
+// AlexNet3D conv1 (Conv3d(1, 64, k=5, s=2) + BatchNorm3d + ReLU + MaxPool3d(3,3)), salient_models.py:146-150,
+// the layer that carries 53 % of the model's FLOPs at 1x121x145x121.
+//
+// Design (MI355X-first, not a translation of cuDNN's path):
+//  * Input volumes live in HBM as uint8 in a *polyphase* layout [N][61][73][61][8]: voxel (d,h,w) is stored at
+//    (d>>1, h>>1, w>>1) phase ((d&1)<<2 | (h&1)<<1 | (w&1)).  The stride-2 5^3 conv becomes a stride-1 3^3 conv
+//    over 8 "phase channels": every MFMA B fragment (8 consecutive k = the 8 phases of one tap) is one 16-B
+//    contiguous read.  K = 27 taps x 8 phases = 216 (125 live), padded to 224 = 7 k-steps of 32.
+//    uint8 values are exact in bf16, so B = u8 and A = bf16(w/255): conv == sum w * (u8/255).
+//  * BatchNorm batch statistics need no pass over the 253 M-element conv output: with per-sample patch moments
+//    m1 = sum_pos p, m2 = sum_pos p p^T (computed once when the data is loaded; exact int-valued fp64),
+//    mean_c = w_c.mu + b_c and var_c = w_c^T Cov w_c.  The forward kernel therefore fuses conv + BN + ReLU +
+//    max-pool and writes only the pooled bf16 output and a uint8 argmax (the conv1 activation never exists).
+//  * Backward needs no dense activation either: with dz only non-zero at the argmax voxels,
+//      S_c = sum dz p (sparse gather, k_conv1_wgrad), D_c = sum dz,
+//      dgamma = invstd w.(S - D mu),  dbeta = D,
+//      dw = gamma invstd (S - D mu - dgamma invstd Cov w),  db = 0
+//    which is exactly the gradient autograd computes through conv -> BN(train) -> ReLU -> pool.
+#include "common.h"
+
+namespace nidt {
+
+constexpr int kPZ = 61, kPY = 73, kPX = 61;          // polyphase grid of a 121x145x121 volume
+constexpr int kOD = 59, kOH = 71, kOW = 59;          // conv1 output
+constexpr int kPD = 19, kPH = 23, kPW = 19;          // pooled output
+constexpr int kC1 = 64;
+constexpr int kK1 = 224;                              // padded k (27 taps x 8 phases = 216)
+constexpr int kNM = 125 + 125 * 125;                  // per-sample moment vector length
+
+// phase r = (rd<<2)|(rh<<1)|rw ; tap t = jd*9+jh*3+jw ; original k = kd*25+kh*5+kw with kd = 2 jd + rd
+__host__ __device__ __forceinline__ bool tp_valid(int t, int r) {
+  const int jd = t / 9, jh = (t / 3) % 3, jw = t % 3;
+  return (2 * jd + (r >> 2) < 5) && (2 * jh + ((r >> 1) & 1) < 5) && (2 * jw + (r & 1) < 5);
+}
+__host__ __device__ __forceinline__ int tp_to_k(int t, int r) {
+  const int jd = t / 9, jh = (t / 3) % 3, jw = t % 3;
+  return (2 * jd + (r >> 2)) * 25 + (2 * jh + ((r >> 1) & 1)) * 5 + (2 * jw + (r & 1));
+}
+
+// ------------------------------------------------------------------------------------------------
+// polyphase conversion of uint8 volumes [N][121][145][121] -> [N][61][73][61][8]
+__global__ void k_polyphase(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, int64_t N) {
+  const int64_t tot = N * kPZ * kPY * kPX;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < tot; e += (int64_t)gridDim.x * blockDim.x) {
+    int64_t v = e;
+    const int x = (int)(v % kPX); v /= kPX;
+    const int y = (int)(v % kPY); v /= kPY;
+    const int z = (int)(v % kPZ);
+    const int64_t n = v / kPZ;
+    uint32_t lo = 0, hi = 0;
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      const int d = 2 * z + (r >> 2), h = 2 * y + ((r >> 1) & 1), w = 2 * x + (r & 1);
+      uint32_t b = 0;
+      if (d < 121 && h < 145 && w < 121) b = src[((n * 121 + d) * 145 + h) * 121 + w];
+      if (r < 4) lo |= b << (8 * r); else hi |= b << (8 * (r - 4));
+    }
+    *reinterpret_cast<uint2*>(dst + e * 8) = make_uint2(lo, hi);
+  }
+}
+
+void polyphase(uintptr_t src, uintptr_t dst, int64_t N, uintptr_t stream) {
+  const int64_t tot = N * kPZ * kPY * kPX;
+  hipLaunchKernelGGL(k_polyphase, dim3((unsigned)std::min<int64_t>(65536, (tot + 255) / 256)), dim3(256), 0,
+                     as_stream(stream), ptr<const uint8_t>(src), ptr<uint8_t>(dst), N);
+  NIDT_CHECK(hipGetLastError());
+}
+
+// ------------------------------------------------------------------------------------------------
+// per-sample patch moments, exact (integer products summed in fp32 chunks of <= 256 positions, then fp64)
+// grid (N, 59 od); block 256: thread owns an 8x8 block of the (padded 128x128) second-moment matrix.
+__global__ __launch_bounds__(256) void k_conv1_moments_sample(const uint8_t* __restrict__ x8, double* __restrict__ mom) {
+  __shared__ float P[64][129];
+  const int n = blockIdx.x, od = blockIdx.y, tid = threadIdx.x;
+  const int kb1 = tid >> 4, kb2 = tid & 15;
+  const bool active = kb1 <= kb2;  // symmetric: compute upper block triangle only
+  float acc[8][8];
+  double accd[8][8];
+  float s1 = 0.f;
+  double s1d = 0.0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { acc[i][j] = 0.f; accd[i][j] = 0.0; }
+  const uint8_t* xs = x8 + (int64_t)n * kPZ * kPY * kPX * 8;
+  const int npos = kOH * kOW;
+  int since = 0;
+  for (int p0 = 0; p0 < npos; p0 += 64) {
+    __syncthreads();
+    for (int e = tid; e < 64 * 128; e += 256) {
+      const int pl = e >> 7, k = e & 127;
+      const int pos = p0 + pl;
+      float v = 0.f;
+      if (pos < npos && k < 125) {
+        const int oh = pos / kOW, ow = pos - oh * kOW;
+        const int kd = k / 25, kh = (k / 5) % 5, kw = k % 5;
+        const int z = od + (kd >> 1), y = oh + (kh >> 1), xx = ow + (kw >> 1);
+        const int r = ((kd & 1) << 2) | ((kh & 1) << 1) | (kw & 1);
+        v = (float)xs[(((int64_t)z * kPY + y) * kPX + xx) * 8 + r];
+      }
+      P[pl][k] = v;
+    }
+    __syncthreads();
+    if (active) {
+      for (int pl = 0; pl < 64; ++pl) {
+        float a[8], b[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) { a[i] = P[pl][8 * kb1 + i]; b[i] = P[pl][8 * kb2 + i]; }
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) acc[i][j] = fmaf(a[i], b[j], acc[i][j]);
+      }
+    }
+    if (tid < 128) for (int pl = 0; pl < 64; ++pl) s1 += P[pl][tid];
+    since += 64;
+    if (since >= 256 || p0 + 64 >= npos) {  // flush (each fp32 partial <= 256*255*255 < 2^24: exact)
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { accd[i][j] += (double)acc[i][j]; acc[i][j] = 0.f; }
+      s1d += (double)s1;
+      s1 = 0.f;
+      since = 0;
+    }
+  }
+  double* m = mom + (int64_t)n * kNM;
+  if (tid < 125) atomicAdd(m + tid, s1d);
+  if (active) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int k1 = 8 * kb1 + i, k2 = 8 * kb2 + j;
+        if (k1 < 125 && k2 < 125) {
+          atomicAdd(m + 125 + k1 * 125 + k2, accd[i][j]);
+          if (kb1 != kb2) atomicAdd(m + 125 + k2 * 125 + k1, accd[i][j]);
+        }
+      }
+  }
+}
+
+void conv1_sample_moments(uintptr_t x8, int64_t N, uintptr_t mom, uintptr_t stream) {
+  NIDT_CHECK(hipMemsetAsync(ptr<void>(mom), 0, (size_t)N * kNM * sizeof(double), as_stream(stream)));
+  hipLaunchKernelGGL(k_conv1_moments_sample, dim3((unsigned)N, kOD), dim3(256), 0, as_stream(stream),
+                     ptr<const uint8_t>(x8), ptr<double>(mom));
+  NIDT_CHECK(hipGetLastError());
+}
+
+// ------------------------------------------------------------------------------------------------
+// weight packing: theta row g at off: [64][125] fp32 -> w8 [G][64][224] bf16 (x scale), w125 [G][64][125] f32
+// holding the bf16-rounded scaled weights (the exact values the MFMA uses) for the moment math.
+__global__ void k_pack_conv1_w(const float* __restrict__ theta, int64_t ldt, int64_t off, int G, float scale,
+                               uint16_t* __restrict__ w8, float* __restrict__ w125) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= G * kC1 * kK1) return;
+  const int g = i / (kC1 * kK1), rem = i - g * kC1 * kK1, c = rem / kK1, kk = rem - c * kK1;
+  const int t = kk >> 3, r = kk & 7;
+  uint16_t v = 0;
+  if (t < 27 && tp_valid(t, r)) {
+    const int k = tp_to_k(t, r);
+    v = f32_to_bf16(theta[(int64_t)g * ldt + off + c * 125 + k] * scale);
+    w125[((int64_t)g * kC1 + c) * 125 + k] = bf16_to_f32(v);
+  }
+  w8[i] = v;
+}
+
+void pack_conv1_w(uintptr_t theta, int64_t ldt, int64_t off, int G, float scale, uintptr_t w8, uintptr_t w125,
+                  uintptr_t stream) {
+  hipLaunchKernelGGL(k_pack_conv1_w, dim3(ceil_div(G * kC1 * kK1, 256)), dim3(256), 0, as_stream(stream),
+                     ptr<const float>(theta), ldt, off, G, scale, ptr<uint16_t>(w8), ptr<float>(w125));
+  NIDT_CHECK(hipGetLastError());
+}
+
+// ------------------------------------------------------------------------------------------------
+// batch moments: Mb[g][e] = sum_b mom[idx[g*B+b]][e]
+__global__ void k_conv1_batch_moments(const double* __restrict__ mom, const int* __restrict__ idx, int B, int G,
+                                      double* __restrict__ Mb) {
+  const int g = blockIdx.y;
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= kNM) return;
+  double s = 0;
+  for (int b = 0; b < B; ++b) s += mom[(int64_t)idx[g * B + b] * kNM + e];
+  Mb[(int64_t)g * kNM + e] = s;
+}
+
+// BN1 statistics per (g, c) from the batch moments.  block = 128 threads (k1), grid (64, G).
+// Outputs: scale/shift for conv-without-bias; mean (incl. bias) & invstd; covw[g][c][k] = (Cov w)_k; running stats.
+__global__ __launch_bounds__(128) void k_conv1_bnstats(const double* __restrict__ Mb, const float* __restrict__ w125,
+                                                       const float* __restrict__ theta, int64_t ldt, int64_t off_bias,
+                                                       int64_t off_g, int64_t off_b, float* bufs, int64_t ldb,
+                                                       int64_t off_rm, int64_t off_rv, int64_t off_nbt, double Npos,
+                                                       float momentum, float eps, int update_running, float* scale,
+                                                       float* shift, float* mean_o, float* invstd_o, float* mu_o,
+                                                       float* covw_o) {
+  __shared__ double sw[128], smu[128], red[2];
+  const int c = blockIdx.x, g = blockIdx.y, k1 = threadIdx.x;
+  const double* M = Mb + (int64_t)g * kNM;
+  if (k1 < 125) {
+    sw[k1] = w125[((int64_t)g * kC1 + c) * 125 + k1];
+    smu[k1] = M[k1] / Npos;
+  } else {
+    sw[k1] = 0; smu[k1] = 0;
+  }
+  __syncthreads();
+  double t = 0;
+  if (k1 < 125) {
+    for (int k2 = 0; k2 < 125; ++k2) {
+      const double cov = M[125 + k1 * 125 + k2] / Npos - smu[k1] * smu[k2];
+      t += cov * sw[k2];
+    }
+    covw_o[((int64_t)g * kC1 + c) * 125 + k1] = (float)t;
+    if (c == 0) mu_o[(int64_t)g * 125 + k1] = (float)smu[k1];
+  }
+  double v = sw[k1] * t, m = sw[k1] * smu[k1];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) { v += __shfl_xor(v, o, 64); m += __shfl_xor(m, o, 64); }
+  if ((k1 & 63) == 0) { red[k1 >> 6] = v; }
+  __syncthreads();
+  const double var = red[0] + red[1];
+  __syncthreads();
+  if ((k1 & 63) == 0) red[k1 >> 6] = m;
+  __syncthreads();
+  if (k1 == 0) {
+    const double mnb = red[0] + red[1];  // mean of the conv output without bias
+    const float bias = theta[(int64_t)g * ldt + off_bias + c];
+    const float gm = theta[(int64_t)g * ldt + off_g + c], bt = theta[(int64_t)g * ldt + off_b + c];
+    const double vv = var > 0 ? var : 0.0;
+    const float inv = (float)(1.0 / sqrt(vv + (double)eps));
+    const int i = g * kC1 + c;
+    scale[i] = gm * inv;
+    shift[i] = bt - (float)mnb * gm * inv;
+    mean_o[i] = (float)(mnb + bias);
+    invstd_o[i] = inv;
+    if (update_running) {
+      float* rm = bufs + (int64_t)g * ldb + off_rm + c;
+      float* rv = bufs + (int64_t)g * ldb + off_rv + c;
+      *rm = (1.f - momentum) * *rm + momentum * (float)(mnb + bias);
+      *rv = (1.f - momentum) * *rv + momentum * (float)(vv * Npos / (Npos - 1.0));
+      if (c == 0) bufs[(int64_t)g * ldb + off_nbt] += 1.f;
+    }
+  }
+}
+
+void conv1_bnstats(uintptr_t mom, uintptr_t idx, int B, int G, uintptr_t Mb, uintptr_t w125, uintptr_t theta,
+                   int64_t ldt, int64_t off_bias, int64_t off_g, int64_t off_b, uintptr_t bufs, int64_t ldb,
+                   int64_t off_rm, int64_t off_rv, int64_t off_nbt, float momentum, float eps, int update_running,
+                   uintptr_t scale, uintptr_t shift, uintptr_t mean, uintptr_t invstd, uintptr_t mu, uintptr_t covw,
+                   uintptr_t stream) {
+  hipStream_t s = as_stream(stream);
+  hipLaunchKernelGGL(k_conv1_batch_moments, dim3(ceil_div(kNM, 256), G), dim3(256), 0, s, ptr<const double>(mom),
+                     ptr<const int>(idx), B, G, ptr<double>(Mb));
+  NIDT_CHECK(hipGetLastError());
+  const double Npos = (double)B * kOD * kOH * kOW;
+  hipLaunchKernelGGL(k_conv1_bnstats, dim3(kC1, G), dim3(128), 0, s, ptr<const double>(Mb), ptr<const float>(w125),
+                     ptr<const float>(theta), ldt, off_bias, off_g, off_b, ptr<float>(bufs), ldb, off_rm, off_rv,
+                     off_nbt, Npos, momentum, eps, update_running, ptr<float>(scale), ptr<float>(shift),
+                     ptr<float>(mean), ptr<float>(invstd), ptr<float>(mu), ptr<float>(covw));
+  NIDT_CHECK(hipGetLastError());
+}
+
+// ------------------------------------------------------------------------------------------------
+// Fused forward: conv1 (MFMA) -> z = conv*scale + shift -> max over 3x3x3 -> relu.  Block = (n, pd, ph),
+// 4 waves; wave w owns output columns ow = 15w .. 15w+14 (5 pooling windows), lane column = ow offset.
+__global__ __launch_bounds__(256, 2) void k_conv1_fwd_pool(const uint8_t* __restrict__ x8, const int* __restrict__ idx,
+                                                           const uint16_t* __restrict__ w8,
+                                                           const float* __restrict__ scale,
+                                                           const float* __restrict__ shift, int B,
+                                                           uint16_t* __restrict__ out, uint8_t* __restrict__ amax) {
+  constexpr int HX = 64;  // halo x extent
+  __shared__ __attribute__((aligned(16))) uint16_t halo[5 * 5 * HX * 8];
+  const int ph = blockIdx.x, pd = blockIdx.y, n = blockIdx.z;
+  const int g = n / B;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const uint8_t* xs = x8 + (int64_t)idx[n] * kPZ * kPY * kPX * 8;
+  // stage halo: z = 3pd..3pd+4, y = 3ph..3ph+4, x = 0..63 (x >= 61 -> 0), u8 -> bf16
+  for (int e = tid; e < 5 * 5 * HX; e += 256) {
+    const int xh = e % HX, yz = e / HX, yh = yz % 5, zh = yz / 5;
+    const int z = 3 * pd + zh, y = 3 * ph + yh;
+    uint2 v = make_uint2(0, 0);
+    if (xh < kPX) v = *reinterpret_cast<const uint2*>(xs + (((int64_t)z * kPY + y) * kPX + xh) * 8);
+    uint4 o;
+    o.x = ((v.x & 0xffu) ? __float_as_uint((float)(v.x & 0xffu)) >> 16 : 0u) |
+          (((v.x >> 8) & 0xffu) ? (__float_as_uint((float)((v.x >> 8) & 0xffu)) & 0xffff0000u) : 0u);
+    o.y = (((v.x >> 16) & 0xffu) ? __float_as_uint((float)((v.x >> 16) & 0xffu)) >> 16 : 0u) |
+          ((v.x >> 24) ? (__float_as_uint((float)(v.x >> 24)) & 0xffff0000u) : 0u);
+    o.z = ((v.y & 0xffu) ? __float_as_uint((float)(v.y & 0xffu)) >> 16 : 0u) |
+          (((v.y >> 8) & 0xffu) ? (__float_as_uint((float)((v.y >> 8) & 0xffu)) & 0xffff0000u) : 0u);
+    o.w = (((v.y >> 16) & 0xffu) ? __float_as_uint((float)((v.y >> 16) & 0xffu)) >> 16 : 0u) |
+          ((v.y >> 24) ? (__float_as_uint((float)(v.y >> 24)) & 0xffff0000u) : 0u);
+    *reinterpret_cast<uint4*>(&halo[e * 8]) = o;
+  }
+  // wave layout: ch = co half (channels 32ch..32ch+31 = 2 MFMA row tiles), op = pair of 16-column ow tiles.
+  // A fragments (weights) for the wave's 2 co tiles x 7 k-steps stay in registers for the whole block.
+  const int fr = lane & 15, fq = lane >> 4;
+  const int ch = wid & 1, op = wid >> 1;
+  bf16x8 fa[2][7];
+  const uint16_t* wg = w8 + (int64_t)g * kC1 * kK1;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int s = 0; s < 7; ++s)
+      fa[i][s] = *reinterpret_cast<const bf16x8*>(wg + (32 * ch + 16 * i + fr) * kK1 + 32 * s + 8 * fq);
+  float sc[2][4], sh[2][4];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      sc[i][r] = scale[g * kC1 + 32 * ch + 16 * i + 4 * fq + r];
+      sh[i][r] = shift[g * kC1 + 32 * ch + 16 * i + 4 * fq + r];
+    }
+  // per-lane tap offsets (in halo elements) for each k-step: tap t = 4s + fq (t >= 27 -> zero weights; reuse 26)
+  int toff[7];
+#pragma unroll
+  for (int s = 0; s < 7; ++s) {
+    int t = 4 * s + fq;
+    t = t < 27 ? t : 26;
+    toff[s] = (((t / 9) * 5 + (t / 3) % 3) * HX + (t % 3)) * 8;
+  }
+  // output column tiles of this wave: ow = 15*(2op+j) + fr, j = 0,1 (a tile holds 5 pooling windows)
+  const int colbase0 = (15 * (2 * op) + fr) * 8, colbase1 = colbase0 + 15 * 8;
+  __syncthreads();
+  float best[2][2][4];
+  int bidx[2][2][4];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) { best[i][j][r] = -INFINITY; bidx[i][j][r] = 0; }
+  for (int dd = 0; dd < 3; ++dd) {
+    for (int dh = 0; dh < 3; ++dh) {
+      f32x4 acc[2][2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      const int rowoff = ((dd * 5 + dh) * HX) * 8;
+#pragma unroll
+      for (int s = 0; s < 7; ++s) {
+        const bf16x8 fb0 = *reinterpret_cast<const bf16x8*>(&halo[colbase0 + rowoff + toff[s]]);
+        const bf16x8 fb1 = *reinterpret_cast<const bf16x8*>(&halo[colbase1 + rowoff + toff[s]]);
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          acc[i][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][s], fb0, acc[i][0], 0, 0, 0);
+          acc[i][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][s], fb1, acc[i][1], 0, 0, 0);
+        }
+      }
+      const int li = dd * 9 + dh * 3;
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float z = fmaf(acc[i][j][r], sc[i][r], sh[i][r]);
+            if (z > best[i][j][r]) { best[i][j][r] = z; bidx[i][j][r] = li; }
+          }
+    }
+  }
+  // combine the 3 w-columns of each window: lanes fr = 3w', 3w'+1, 3w'+2 (within the 16-lane group)
+  const int wloc = fr / 3, dw = fr - 3 * wloc;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int pw = 5 * (2 * op + j) + wloc;
+    const bool writer = (dw == 0) && (fr < 15) && (pw < kPW);
+    uint32_t pk[2][2], ab[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      ab[i] = 0;
+      float o4[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float v = best[i][j][r];
+        int ix = bidx[i][j][r] + dw;
+        const float v1 = __shfl_down(v, 1, 16), v2 = __shfl_down(v, 2, 16);
+        const int i1 = __shfl_down(ix, 1, 16), i2 = __shfl_down(ix, 2, 16);
+        if (v1 > v || (v1 == v && i1 < ix)) { v = v1; ix = i1; }
+        if (v2 > v || (v2 == v && i2 < ix)) { v = v2; ix = i2; }
+        o4[r] = fmaxf(v, 0.f);
+        ab[i] |= (uint32_t)ix << (8 * r);
+      }
+      pk[i][0] = pack_bf16x2(o4[0], o4[1]);
+      pk[i][1] = pack_bf16x2(o4[2], o4[3]);
+    }
+    if (writer) {
+      const int64_t o = ((((int64_t)n * kPD + pd) * kPH + ph) * kPW + pw) * kC1 + 32 * ch + 4 * fq;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        *reinterpret_cast<uint2*>(out + o + 16 * i) = make_uint2(pk[i][0], pk[i][1]);
+        *reinterpret_cast<uint32_t*>(amax + o + 16 * i) = ab[i];
+      }
+    }
+  }
+}
+
+void conv1_fwd_pool(uintptr_t x8, uintptr_t idx, uintptr_t w8, uintptr_t scale, uintptr_t shift, int NB, int B,
+                    uintptr_t out, uintptr_t amax, uintptr_t stream) {
+  NIDT_REQUIRE(NB % B == 0, "conv1_fwd_pool: NB % B");
+  hipLaunchKernelGGL(k_conv1_fwd_pool, dim3(kPH, kPD, NB), dim3(256), 0, as_stream(stream), ptr<const uint8_t>(x8),
+                     ptr<const int>(idx), ptr<const uint16_t>(w8), ptr<const float>(scale), ptr<const float>(shift), B,
+                     ptr<uint16_t>(out), ptr<uint8_t>(amax));
+  NIDT_CHECK(hipGetLastError());
+}
+
+// ------------------------------------------------------------------------------------------------
+// Sparse wgrad: S[c][k] = sum over pooled voxels of dz * patch(argmax voxel), D[c] = sum dz.
+// Block = (n, pd); loops over ph; thread = (wave w, channel c = lane); wave w takes pw = w, w+4, ...
+// Output slab: part[n*19 + pd][64][126] (125 S entries + D).
+__global__ __launch_bounds__(256) void k_conv1_wgrad(const uint8_t* __restrict__ x8, const int* __restrict__ idx,
+                                                     const uint16_t* __restrict__ dp, const uint16_t* __restrict__ pout,
+                                                     const uint8_t* __restrict__ amax, float* __restrict__ part) {
+  constexpr int HX = 64;
+  __shared__ __attribute__((aligned(16))) uint16_t halo[5 * 5 * HX * 8];
+  __shared__ float red[64][127];
+  const int pd = blockIdx.x, n = blockIdx.y;
+  const int tid = threadIdx.x, c = tid & 63, wid = tid >> 6;
+  const uint8_t* xs = x8 + (int64_t)idx[n] * kPZ * kPY * kPX * 8;
+  float S[125];
+#pragma unroll
+  for (int k = 0; k < 125; ++k) S[k] = 0.f;
+  float Dsum = 0.f;
+  for (int ph = 0; ph < kPH; ++ph) {
+    __syncthreads();
+    for (int e = tid; e < 5 * 5 * HX; e += 256) {
+      const int xh = e % HX, yz = e / HX, yh = yz % 5, zh = yz / 5;
+      const int z = 3 * pd + zh, y = 3 * ph + yh;
+      uint2 v = make_uint2(0, 0);
+      if (xh < kPX) v = *reinterpret_cast<const uint2*>(xs + (((int64_t)z * kPY + y) * kPX + xh) * 8);
+      uint4 o;
+      o.x = (__float_as_uint((float)(v.x & 0xffu)) >> 16) | (__float_as_uint((float)((v.x >> 8) & 0xffu)) & 0xffff0000u);
+      o.y = (__float_as_uint((float)((v.x >> 16) & 0xffu)) >> 16) | (__float_as_uint((float)(v.x >> 24)) & 0xffff0000u);
+      o.z = (__float_as_uint((float)(v.y & 0xffu)) >> 16) | (__float_as_uint((float)((v.y >> 8) & 0xffu)) & 0xffff0000u);
+      o.w = (__float_as_uint((float)((v.y >> 16) & 0xffu)) >> 16) | (__float_as_uint((float)(v.y >> 24)) & 0xffff0000u);
+      *reinterpret_cast<uint4*>(&halo[e * 8]) = o;
+    }
+    __syncthreads();
+    for (int pw = wid; pw < kPW; pw += 4) {
+      const int64_t o = ((((int64_t)n * kPD + pd) * kPH + ph) * kPW + pw) * kC1 + c;
+      const float pv = bf16_to_f32(pout[o]);
+      const float dz = pv > 0.f ? bf16_to_f32(dp[o]) : 0.f;
+      const int a = amax[o];
+      const int ad = a / 9, ah = (a / 3) % 3, aw = a % 3;
+      const int base = ((ad * 5 + ah) * HX + 3 * pw + aw) * 8;
+      Dsum += dz;
+#pragma unroll
+      for (int t = 0; t < 27; ++t) {
+        const int jd = t / 9, jh = (t / 3) % 3, jw = t % 3;
+        const uint4 u = *reinterpret_cast<const uint4*>(&halo[base + ((jd * 5 + jh) * HX + jw) * 8]);
+        const uint32_t w4[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+          if (tp_valid(t, r)) {
+            const uint32_t bits = (r & 1) ? (w4[r >> 1] & 0xffff0000u) : (w4[r >> 1] << 16);
+            S[tp_to_k(t, r)] = fmaf(dz, __uint_as_float(bits), S[tp_to_k(t, r)]);
+          }
+        }
+      }
+    }
+  }
+  // reduce the 4 waves (channel c owned by lane c of every wave) through one [64][127] LDS buffer
+  for (int w = 1; w < 4; ++w) {
+    __syncthreads();
+    if (wid == w) {
+#pragma unroll
+      for (int k = 0; k < 125; ++k) red[c][k] = S[k];
+      red[c][125] = Dsum;
+    }
+    __syncthreads();
+    if (wid == 0) {
+#pragma unroll
+      for (int k = 0; k < 125; ++k) S[k] += red[c][k];
+      Dsum += red[c][125];
+    }
+  }
+  if (wid == 0) {
+    float* o = part + (((int64_t)n * kPD + pd) * kC1 + c) * 126;
+#pragma unroll
+    for (int k = 0; k < 125; ++k) o[k] = S[k];
+    o[125] = Dsum;
+  }
+}
+
+// Reduce slabs per client and apply the closed form.  grid (64 c, G), block 128 (k).
+__global__ __launch_bounds__(128) void k_conv1_wgrad_fin(const float* __restrict__ part, int B,
+                                                         const float* __restrict__ w125, const float* __restrict__ mu,
+                                                         const float* __restrict__ covw,
+                                                         const float* __restrict__ invstd, const float* theta,
+                                                         int64_t ldt, int64_t off_g, float* grad, int64_t ldg,
+                                                         int64_t goff_w, int64_t goff_bias, int64_t goff_g,
+                                                         int64_t goff_b, float wscale) {
+  __shared__ double red[2];
+  __shared__ double sD, sdg;
+  const int c = blockIdx.x, g = blockIdx.y, k = threadIdx.x;
+  const int nslab = B * kPD;
+  double S = 0, D = 0;
+  for (int sl = 0; sl < nslab; ++sl) {
+    const float* o = part + (((int64_t)g * nslab + sl) * kC1 + c) * 126;
+    if (k < 125) S += o[k];
+    if (k == 0) D += o[125];
+  }
+  if (k == 0) sD = D;
+  __syncthreads();
+  D = sD;
+  const int i = g * kC1 + c;
+  const double iv = invstd[i];
+  const double gm = theta[(int64_t)g * ldt + off_g + c];
+  const double muk = k < 125 ? mu[(int64_t)g * 125 + k] : 0.0;
+  const double wk = k < 125 ? w125[(int64_t)i * 125 + k] : 0.0;
+  const double r = k < 125 ? S - D * muk : 0.0;
+  double v = wk * r;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  if ((k & 63) == 0) red[k >> 6] = v;
+  __syncthreads();
+  if (k == 0) sdg = iv * (red[0] + red[1]);
+  __syncthreads();
+  const double dg = sdg;
+  if (k < 125) {
+    const double cw = covw[(int64_t)i * 125 + k];
+    const double dw = gm * iv * (r - dg * iv * cw);
+    grad[(int64_t)g * ldg + goff_w + (int64_t)c * 125 + k] = (float)(dw * wscale);
+  }
+  if (k == 0) {
+    grad[(int64_t)g * ldg + goff_g + c] = (float)dg;
+    grad[(int64_t)g * ldg + goff_b + c] = (float)D;
+    grad[(int64_t)g * ldg + goff_bias + c] = 0.f;
+  }
+}
+
+void conv1_wgrad(uintptr_t x8, uintptr_t idx, uintptr_t dp, uintptr_t pout, uintptr_t amax, int NB, int B,
+                 uintptr_t part, uintptr_t w125, uintptr_t mu, uintptr_t covw, uintptr_t invstd, uintptr_t theta,
+                 int64_t ldt, int64_t off_g, uintptr_t grad, int64_t ldg, int64_t goff_w, int64_t goff_bias,
+                 int64_t goff_g, int64_t goff_b, float wscale, uintptr_t stream) {
+  hipStream_t s = as_stream(stream);
+  hipLaunchKernelGGL(k_conv1_wgrad, dim3(kPD, NB), dim3(256), 0, s, ptr<const uint8_t>(x8), ptr<const int>(idx),
+                     ptr<const uint16_t>(dp), ptr<const uint16_t>(pout), ptr<const uint8_t>(amax), ptr<float>(part));
+  NIDT_CHECK(hipGetLastError());
+  const int G = NB / B;
+  hipLaunchKernelGGL(k_conv1_wgrad_fin, dim3(kC1, G), dim3(128), 0, s, ptr<const float>(part), B,
+                     ptr<const float>(w125), ptr<const float>(mu), ptr<const float>(covw), ptr<const float>(invstd),
+                     ptr<const float>(theta), ldt, off_g, ptr<float>(grad), ldg, goff_w, goff_bias, goff_g, goff_b,
+                     wscale);
+  NIDT_CHECK(hipGetLastError());
+}
+
+}  // namespace nidt

@@ -1,0 +1,85 @@
+"""SNIP saliency and global top-k mask selection (reference ``sailentgrads/snip.py``).
+
+The reference patches every Conv3d/Linear to compute ``F.conv3d(x, w*mask)`` and reads
+``|dL/dmask|`` at ``mask=1``.  Since ``dL/dmask = w * dL/dw_eff`` and ``w_eff = w`` at mask 1,
+this module computes the identical quantity as ``|w ⊙ ∂L/∂w|`` from one ordinary backward pass on a
+throwaway copy of the model (train mode, as in the reference) — no monkey-patching.
+
+Mask rule (``snip.py:80-116``): concatenate all scores, divide by their sum, ``k = int(N*keep)``,
+threshold = k-th largest, keep ``score >= threshold`` (ties kept, Q7).  Non-conv/linear params
+(biases, BN affine) get all-ones masks.  The device path uses the HIP radix-select kernel in
+:mod:`neuroimagedisttraining_amd.ops.topk` when available (bit-identical threshold).
+"""
+from __future__ import annotations
+
+import copy
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+MASKABLE = (nn.Conv1d, nn.Conv2d, nn.Conv3d, nn.Linear)
+
+
+def maskable_weight_names(model):
+    return [name + ".weight" for name, m in model.named_modules() if isinstance(m, MASKABLE)]
+
+
+def snip_scores(model, x, y, loss="bce"):
+    """Per-layer ``|w ⊙ ∂L/∂w|`` for one mini-batch; keys are module names (``features.0``)."""
+    cp = copy.deepcopy(model)
+    cp.train()
+    names = [n for n, m in cp.named_modules() if isinstance(m, MASKABLE)]
+    mods = dict(cp.named_modules())
+    for p in cp.parameters():
+        p.requires_grad_(False)
+    for n in names:
+        mods[n].weight.requires_grad_(True)
+    out = cp(x)
+    out = out[0] if isinstance(out, (list, tuple)) else out
+    if loss == "bce" or (out.dim() == 2 and out.shape[1] == 1):
+        L = F.binary_cross_entropy_with_logits(out.float(), y.view(-1, 1).float())
+    else:
+        L = F.cross_entropy(out.float(), y.long())
+    L.backward()
+    res = {n: (mods[n].weight.detach() * mods[n].weight.grad).abs() for n in names}
+    del cp
+    return res
+
+
+def mean_scores(score_dicts):
+    """Element-wise mean of a list of score dicts (``get_mean_snip_scores`` / ``get_mean_sailency_scores``)."""
+    out = {}
+    for d in score_dicts:
+        for k, v in d.items():
+            out[k] = v.clone() if k not in out else out[k].add_(v)
+    for k in out:
+        out[k].div_(len(score_dicts))
+    return out
+
+
+def global_threshold(all_scores_flat, keep_ratio, use_kernel=True):
+    """k-th largest of normalised scores.  Returns ``(threshold, norm_factor)``."""
+    norm = all_scores_flat.sum()
+    normed = all_scores_flat / norm
+    k = int(normed.numel() * keep_ratio)
+    k = max(1, k)
+    if use_kernel and normed.is_cuda:
+        from ..ops import topk as _tk
+        thr = _tk.kth_largest(normed, k)
+    else:
+        thr = torch.topk(normed, k, sorted=True).values[-1]
+    return thr, norm
+
+
+def mask_from_scores(model, scores, keep_ratio, use_kernel=True):
+    """Returns ``(keep_masks{module}, final_weight_mask{param name})`` as in the reference."""
+    names = list(scores.keys())
+    flat = torch.cat([scores[n].flatten() for n in names])
+    thr, norm = global_threshold(flat, keep_ratio, use_kernel)
+    keep = {n: ((scores[n] / norm) >= thr).float() for n in names}
+    final = {}
+    wnames = {n + ".weight": n for n in names}
+    for pname, p in model.named_parameters():
+        final[pname] = keep[wnames[pname]].to(p.device) if pname in wnames else torch.ones_like(p)
+    return keep, final

@@ -1,0 +1,127 @@
+"""Robust aggregation (reference ``fedml_core/robustness/robust_aggregation.py:4-55``) plus the
+Byzantine-robust aggregators BASELINE.json asks for (Krum, Multi-Krum, coordinate-wise median,
+trimmed mean), which the reference lacks.
+
+Everything operates on flattened parameter vectors; states are flattened with
+:func:`vectorize_weight` (which, unlike the reference's ``torch.cat`` of unflattened tensors —
+quirk Q16 — flattens each tensor first).  For many clients the stacked matrix ``[K, P]`` lives on
+the GPU, so the pairwise-distance Gram and the per-coordinate median run as device ops.
+"""
+from __future__ import annotations
+
+import torch
+
+
+def is_weight_param(k):
+    return "running_mean" not in k and "running_var" not in k and "num_batches_tracked" not in k
+
+
+def vectorize_weight(state_dict):
+    return torch.cat([v.reshape(-1).float() for k, v in state_dict.items() if is_weight_param(k)])
+
+
+def load_model_weight_diff(local_state_dict, weight_diff, global_state_dict):
+    """``w_g + diff`` for weight params; buffers copied from the local state."""
+    sd = local_state_dict.state_dict() if hasattr(local_state_dict, "state_dict") else local_state_dict
+    out, off = {}, 0
+    for k, v in sd.items():
+        if is_weight_param(k):
+            n = v.numel()
+            out[k] = weight_diff[off:off + n].view_as(v).to(v.dtype) + global_state_dict[k]
+            off += n
+        else:
+            out[k] = v
+    return out
+
+
+class RobustAggregator:
+    """Norm-difference clipping and weak-DP noise (``defense_type`` / ``norm_bound`` / ``stddev``)."""
+
+    def __init__(self, args):
+        self.defense_type = getattr(args, "defense_type", "norm_diff_clipping")
+        self.norm_bound = float(getattr(args, "norm_bound", 5.0))
+        self.stddev = float(getattr(args, "stddev", 0.025))
+
+    def norm_diff_clipping(self, local_state_dict, global_state_dict):
+        vl = vectorize_weight(local_state_dict)
+        vg = vectorize_weight(global_state_dict)
+        diff = vl - vg
+        nrm = torch.linalg.vector_norm(diff).item()
+        diff = diff / max(1.0, nrm / self.norm_bound)
+        return load_model_weight_diff(local_state_dict, diff, global_state_dict)
+
+    def add_noise(self, local_weight, device=None):
+        noise = torch.randn(local_weight.size(), device=device or local_weight.device) * self.stddev
+        return local_weight + noise
+
+
+def stack_states(states):
+    keys = list(states[0].keys())
+    shapes = [(k, states[0][k].shape, states[0][k].dtype) for k in keys]
+    M = torch.stack([torch.cat([s[k].reshape(-1).float() for k in keys]) for s in states])
+    return M, shapes
+
+
+def unstack_vector(v, shapes):
+    out, off = {}, 0
+    for k, shp, dt in shapes:
+        n = 1
+        for d in shp:
+            n *= d
+        t = v[off:off + n].view(shp)
+        out[k] = t if dt.is_floating_point else t.round().to(dt)
+        off += n
+    return out
+
+
+def pairwise_sq_dists(M):
+    """``||m_i - m_j||^2`` via the Gram matrix (one GEMM on device)."""
+    g = M @ M.t()
+    d = g.diag()
+    return (d[:, None] + d[None, :] - 2 * g).clamp_(min=0)
+
+
+def krum_scores(M, f):
+    K = M.shape[0]
+    D = pairwise_sq_dists(M)
+    m = max(1, K - f - 2)
+    D = D + torch.diag(torch.full((K,), float("inf"), device=M.device))
+    return torch.topk(D, m, dim=1, largest=False).values.sum(1)
+
+
+def krum(M, f=0, multi=1):
+    """(Multi-)Krum: average of the ``multi`` vectors with the smallest Krum score."""
+    s = krum_scores(M, f)
+    sel = torch.topk(s, max(1, multi), largest=False).indices
+    return M[sel].mean(0), sel
+
+
+def coordinate_median(M):
+    return M.median(dim=0).values if M.shape[0] % 2 == 1 else M.sort(dim=0).values[
+        M.shape[0] // 2 - 1:M.shape[0] // 2 + 1].mean(0)
+
+
+def trimmed_mean(M, trim_ratio=0.1):
+    K = M.shape[0]
+    b = int(K * trim_ratio)
+    if b == 0:
+        return M.mean(0)
+    S = M.sort(dim=0).values
+    return S[b:K - b].mean(0)
+
+
+def robust_aggregate(kind, w_locals, f=0, trim_ratio=0.1):
+    """``w_locals`` = list of ``(n, state)``; returns the aggregated state."""
+    states = [s for _, s in w_locals]
+    M, shapes = stack_states(states)
+    if kind == "krum":
+        v, _ = krum(M, f, 1)
+    elif kind == "multikrum":
+        v, _ = krum(M, f, max(1, M.shape[0] - f))
+    elif kind == "median":
+        v = coordinate_median(M)
+    elif kind == "trimmed_mean":
+        v = trimmed_mean(M, trim_ratio)
+    else:
+        raise ValueError("unknown aggregator %r" % kind)
+    return unstack_vector(v, shapes)

@@ -1,0 +1,220 @@
+"""Client-batched AlexNet3D_Dropout train/eval step on the gfx950 HIP kernels.
+
+One call trains G virtual clients in lockstep: every client has its own fp32 master row in ``theta [G, P]``
+(reference param order, so state_dict keys / masks / SNIP scores line up with
+``fedml_api/model/cv/salient_models.py:142-191``), its own BN running stats row in ``bufs [G, Q]``, and its own
+batch of B volumes.  The forward/backward is an explicit launch sequence (no autograd, no MIOpen):
+
+  conv1+BN1+ReLU+pool1 (fused, BN1 stats from patch moments)  ->  conv2 (MFMA, BN-stat epilogue)
+  -> BN2+ReLU+pool2 -> conv3 -> conv4 (BN3+ReLU fused into its loader) -> conv5 (BN4 fused) -> BN5+ReLU+pool5
+  -> head (dropout MLP + BCEWithLogits, fwd+bwd) -> BN5/conv5 bwd -> ... -> conv1 sparse wgrad + closed form.
+
+Gradients are written (not accumulated) straight into ``grads [G, P]`` at the reference parameter offsets;
+the fused clip+SGD+mask optimizer then updates ``theta`` in place.
+"""
+from __future__ import annotations
+
+import torch
+
+from .. import ops
+
+BN_EPS = 1e-5
+BN_MOM = 0.1
+# (conv idx, bn idx, Cin, Cout, pad, in spatial)
+L2 = (4, 5, 64, 128, 0, (19, 23, 19))
+L3 = (8, 9, 128, 192, 1, (5, 7, 5))
+L4 = (11, 12, 192, 192, 1, (5, 7, 5))
+L5 = (14, 15, 192, 128, 1, (5, 7, 5))
+NM = 125 + 125 * 125
+
+
+def _p(t):
+    return t.data_ptr() if t is not None else 0
+
+
+class HipAlexNet3D:
+    """Owns scratch buffers for a (G, B) shape and runs fused train / eval steps."""
+
+    def __init__(self, players, blayers, device):
+        self.m = ops.ext()
+        self.pl, self.bl = players, blayers
+        self.dev = torch.device(device)
+        self.P, self.Q = players.total, blayers.total
+        self._cache = {}
+        self.o = {n: off for n, off in zip(players.names, players.offsets)}
+        self.ob = {n: off for n, off in zip(blayers.names, blayers.offsets)}
+
+    # ---------------------------------------------------------------------------------------------
+    def _bufs(self, G, B, train):
+        key = (G, B, train)
+        if key in self._cache:
+            return self._cache[key]
+        d, bf, f32, u8 = self.dev, torch.bfloat16, torch.float32, torch.uint8
+        NB = G * B
+        e = lambda *s, dt=bf: torch.empty(s, dtype=dt, device=d)  # noqa: E731
+        b = dict(
+            w1p=e(G, 64, 224), w125=e(G, 64, 125, dt=f32),
+            s1=e(G, 64, dt=f32), t1=e(G, 64, dt=f32), m1=e(G, 64, dt=f32), i1=e(G, 64, dt=f32),
+            Mb=e(G, NM, dt=torch.float64), mu=e(G, 125, dt=f32), covw=e(G, 64, 125, dt=f32),
+            p1=e(NB, 19, 23, 19, 64), a1=e(NB, 19, 23, 19, 64, dt=u8),
+            y2=e(NB, 17, 21, 17, 128), p2=e(NB, 5, 7, 5, 128), a2=e(NB, 5, 7, 5, 128, dt=u8),
+            y3=e(NB, 5, 7, 5, 192), y4=e(NB, 5, 7, 5, 192), y5=e(NB, 5, 7, 5, 128),
+            p5=e(NB, 1, 2, 1, 128), a5=e(NB, 1, 2, 1, 128, dt=u8),
+            logits=e(NB, dt=f32), loss=e(G, dt=f32),
+        )
+        for (ci, bi, cin, cout, pad, sp) in (L2, L3, L4, L5):
+            b["w%dp" % ci] = e(G, cout, 27, cin)
+            b["bias%d" % ci] = e(G, cout, dt=f32)
+            for k in ("s", "t", "m", "i"):
+                b["%s%d" % (k, ci)] = e(G, cout, dt=f32)
+            npb = self.m.conv3d_fwd_nblocks(B, sp[0], sp[1], sp[2], pad)
+            b["st%d" % ci] = e(G, npb, cout, 2, dt=f32)
+            b["npb%d" % ci] = npb
+        if train:
+            for (ci, bi, cin, cout, pad, sp) in (L2, L3, L4, L5):
+                b["w%dt" % ci] = e(G, cin, 27, cout)
+                b["ns%d" % ci] = self.m.conv3d_wgrad_nsplit(G, B, sp[0], sp[1], sp[2], cin, cout, pad)
+            wg_sz = max(b["ns%d" % ci] * G * cout * 27 * cin for (ci, bi, cin, cout, pad, sp) in (L2, L3, L4, L5))
+            b.update(
+                wgpart=e(wg_sz, dt=f32),
+                dp5=e(NB, 1, 2, 1, 128), dy5=e(NB, 5, 7, 5, 128), dx5=e(NB, 5, 7, 5, 192),
+                dy4=e(NB, 5, 7, 5, 192), dx4=e(NB, 5, 7, 5, 192), dy3=e(NB, 5, 7, 5, 192),
+                dx3=e(NB, 5, 7, 5, 128), dy2=e(NB, 17, 21, 17, 128), dp1=e(NB, 19, 23, 19, 64),
+                bnpart=e(G * 64 * 256 * 2, dt=f32), coef=e(G, 192, 3, dt=f32),
+                c1part=e(NB * 19, 64, 126, dt=f32),
+            )
+        self._cache[key] = b
+        return b
+
+    # ---------------------------------------------------------------------------------------------
+    def _pack(self, theta, G, b, train):
+        m, st = self.m, torch.cuda.current_stream().cuda_stream
+        P = theta.stride(0)
+        m.pack_conv1_w(_p(theta), P, self.o["features.0.weight"], G, 1.0 / 255.0, _p(b["w1p"]), _p(b["w125"]), st)
+        for (ci, bi, cin, cout, pad, sp) in (L2, L3, L4, L5):
+            m.pack_conv_w(_p(theta), P, self.o["features.%d.weight" % ci], G, cout, cin, 1.0, _p(b["w%dp" % ci]),
+                          _p(b["w%dt" % ci]) if train else 0, st)
+            o = self.o["features.%d.bias" % ci]
+            b["bias%d" % ci].copy_(theta[:, o:o + cout])
+
+    def _bn(self, ci, bi, C, G, B, sp, theta, bufs, b, train):
+        """BN coefficients for conv ``ci`` (train: from the conv epilogue stats; eval: running stats)."""
+        m, st = self.m, torch.cuda.current_stream().cuda_stream
+        P, Q = theta.stride(0), bufs.stride(0)
+        og, ob = self.o["features.%d.weight" % bi], self.o["features.%d.bias" % bi]
+        orm, orv = self.ob["features.%d.running_mean" % bi], self.ob["features.%d.running_var" % bi]
+        if train:
+            onbt = self.ob["features.%d.num_batches_tracked" % bi]
+            Mg = B * sp[0] * sp[1] * sp[2]
+            m.bn_finalize(_p(b["st%d" % ci]), b["npb%d" % ci], 128, Mg, G, C, _p(theta), P, og, ob, _p(bufs), Q,
+                          orm, orv, onbt, BN_MOM, BN_EPS, _p(b["s%d" % ci]), _p(b["t%d" % ci]), _p(b["m%d" % ci]),
+                          _p(b["i%d" % ci]), 1, st)
+        else:
+            m.bn_eval(G, C, _p(theta), P, og, ob, _p(bufs), Q, orm, orv, BN_EPS, _p(b["s%d" % ci]),
+                      _p(b["t%d" % ci]), st)
+
+    def forward(self, theta, bufs, x8, mom, idx, G, B, train):
+        """Runs the forward; returns the scratch dict (logits in ``b['logits']``)."""
+        assert theta.stride(1) == 1 and bufs.stride(1) == 1 and theta.shape[0] == G and bufs.shape[0] == G
+        assert theta.shape[1] == self.P and bufs.shape[1] == self.Q and theta.dtype == torch.float32
+        assert idx.dtype == torch.int32 and idx.numel() == G * B and x8.dtype == torch.uint8
+        assert x8.dim() == 5 and tuple(x8.shape[1:]) == (61, 73, 61, 8) and x8.is_contiguous()
+        m, st = self.m, torch.cuda.current_stream().cuda_stream
+        b = self._bufs(G, B, train)
+        NB = G * B
+        P, Q = theta.stride(0), bufs.stride(0)
+        self._pack(theta, G, b, train)
+        # ---- conv1 + BN1 + ReLU + pool1 ----
+        if train:
+            assert mom is not None and mom.dtype == torch.float64 and mom.shape[1] == NM
+            m.conv1_bnstats(_p(mom), _p(idx), B, G, _p(b["Mb"]), _p(b["w125"]), _p(theta), P,
+                            self.o["features.0.bias"], self.o["features.1.weight"], self.o["features.1.bias"],
+                            _p(bufs), Q, self.ob["features.1.running_mean"], self.ob["features.1.running_var"],
+                            self.ob["features.1.num_batches_tracked"], BN_MOM, BN_EPS, 1, _p(b["s1"]), _p(b["t1"]),
+                            _p(b["m1"]), _p(b["i1"]), _p(b["mu"]), _p(b["covw"]), st)
+        else:
+            m.bn_eval(G, 64, _p(theta), P, self.o["features.1.weight"], self.o["features.1.bias"], _p(bufs), Q,
+                      self.ob["features.1.running_mean"], self.ob["features.1.running_var"], BN_EPS, _p(b["s1"]),
+                      _p(b["t1"]), st)
+            ob = self.o["features.0.bias"]
+            b["t1"].add_(b["s1"] * theta[:, ob:ob + 64])  # fold conv1 bias: the kernel convolves without it
+        m.conv1_fwd_pool(_p(x8), _p(idx), _p(b["w1p"]), _p(b["s1"]), _p(b["t1"]), NB, B, _p(b["p1"]), _p(b["a1"]), st)
+        # ---- conv2 + BN2 + ReLU + pool2 ----
+        ci, bi, cin, cout, pad, sp = L2
+        m.conv3d_fwd(_p(b["p1"]), _p(b["w4p"]), _p(b["bias4"]), 0, 0, _p(b["y2"]), _p(b["st4"]) if train else 0,
+                     G, B, 19, 23, 19, 64, 128, 0, st)
+        self._bn(4, 5, 128, G, B, (17, 21, 17), theta, bufs, b, train)
+        m.bn_relu_pool(_p(b["y2"]), _p(b["s4"]), _p(b["t4"]), _p(b["p2"]), _p(b["a2"]), NB, B, 17, 21, 17, 128, st)
+        # ---- conv3 ----
+        m.conv3d_fwd(_p(b["p2"]), _p(b["w8p"]), _p(b["bias8"]), 0, 0, _p(b["y3"]), _p(b["st8"]) if train else 0,
+                     G, B, 5, 7, 5, 128, 192, 1, st)
+        self._bn(8, 9, 192, G, B, (5, 7, 5), theta, bufs, b, train)
+        # ---- conv4 (input = relu(bn3(y3)) applied in the loader) ----
+        m.conv3d_fwd(_p(b["y3"]), _p(b["w11p"]), _p(b["bias11"]), _p(b["s8"]), _p(b["t8"]), _p(b["y4"]),
+                     _p(b["st11"]) if train else 0, G, B, 5, 7, 5, 192, 192, 1, st)
+        self._bn(11, 12, 192, G, B, (5, 7, 5), theta, bufs, b, train)
+        # ---- conv5 (input = relu(bn4(y4))) + BN5 + ReLU + pool ----
+        m.conv3d_fwd(_p(b["y4"]), _p(b["w14p"]), _p(b["bias14"]), _p(b["s11"]), _p(b["t11"]), _p(b["y5"]),
+                     _p(b["st14"]) if train else 0, G, B, 5, 7, 5, 192, 128, 1, st)
+        self._bn(14, 15, 128, G, B, (5, 7, 5), theta, bufs, b, train)
+        m.bn_relu_pool(_p(b["y5"]), _p(b["s14"]), _p(b["t14"]), _p(b["p5"]), _p(b["a5"]), NB, B, 5, 7, 5, 128, st)
+        return b
+
+    # ---------------------------------------------------------------------------------------------
+    def train_step(self, theta, bufs, grads, x8, mom, idx, labels, G, B, keep=0.5, seed=0):
+        """Forward + backward for G clients; writes ``grads`` [G,P], updates BN running stats in ``bufs``.
+        Returns the per-client mean loss tensor [G] (device)."""
+        assert grads.shape == theta.shape and grads.stride(1) == 1 and grads.stride(0) == theta.stride(0)
+        assert labels.dtype == torch.float32 and labels.numel() == G * B and B <= 32
+        m, st = self.m, torch.cuda.current_stream().cuda_stream
+        b = self.forward(theta, bufs, x8, mom, idx, G, B, True)
+        NB = G * B
+        P = theta.stride(0)
+        o = self.o
+        m.head(_p(b["p5"]), _p(theta), P, o["classifier.1.weight"], o["classifier.1.bias"], o["classifier.4.weight"],
+               o["classifier.4.bias"], _p(labels), _p(b["logits"]), _p(b["loss"]), _p(grads), grads.stride(0), _p(b["dp5"]), G, B, 1,
+               float(keep), int(seed) & ((1 << 64) - 1), st)
+        nchunk = 64
+
+        def bn_bwd(pool, ci, bi, C, sp, dsrc, pout, amax, dy, y):
+            m.bn_bwd(pool, _p(y), _p(dsrc), _p(pout), _p(amax), _p(b["s%d" % ci]), _p(b["t%d" % ci]),
+                     _p(b["m%d" % ci]), _p(b["i%d" % ci]), NB, B, sp[0], sp[1], sp[2], C, _p(b["bnpart"]), nchunk,
+                     _p(theta), P, o["features.%d.weight" % bi], _p(grads), P, o["features.%d.weight" % bi],
+                     o["features.%d.bias" % bi], o["features.%d.bias" % ci], _p(b["coef"]), _p(dy), st)
+
+        def wgrad(ci, x, xs, xt, dy, sp, cin, cout, pad):
+            m.conv3d_wgrad(_p(x), _p(xs), _p(xt), _p(dy), _p(b["wgpart"]), _p(grads), P, o["features.%d.weight" % ci],
+                           G, B, sp[0], sp[1], sp[2], cin, cout, pad, b["ns%d" % ci], 1.0, st)
+
+        # layer 5: pool5 -> BN5 -> conv5
+        bn_bwd(1, 14, 15, 128, (5, 7, 5), b["dp5"], b["p5"], b["a5"], b["dy5"], b["y5"])
+        wgrad(14, b["y4"], b["s11"], b["t11"], b["dy5"], (5, 7, 5), 192, 128, 1)
+        m.conv3d_fwd(_p(b["dy5"]), _p(b["w14t"]), 0, 0, 0, _p(b["dx5"]), 0, G, B, 5, 7, 5, 128, 192, 1, st)
+        # layer 4
+        bn_bwd(0, 11, 12, 192, (5, 7, 5), b["dx5"], None, None, b["dy4"], b["y4"])
+        wgrad(11, b["y3"], b["s8"], b["t8"], b["dy4"], (5, 7, 5), 192, 192, 1)
+        m.conv3d_fwd(_p(b["dy4"]), _p(b["w11t"]), 0, 0, 0, _p(b["dx4"]), 0, G, B, 5, 7, 5, 192, 192, 1, st)
+        # layer 3
+        bn_bwd(0, 8, 9, 192, (5, 7, 5), b["dx4"], None, None, b["dy3"], b["y3"])
+        wgrad(8, b["p2"], None, None, b["dy3"], (5, 7, 5), 128, 192, 1)
+        m.conv3d_fwd(_p(b["dy3"]), _p(b["w8t"]), 0, 0, 0, _p(b["dx3"]), 0, G, B, 5, 7, 5, 192, 128, 1, st)
+        # layer 2: pool2 -> BN2 -> conv2
+        bn_bwd(1, 4, 5, 128, (17, 21, 17), b["dx3"], b["p2"], b["a2"], b["dy2"], b["y2"])
+        wgrad(4, b["p1"], None, None, b["dy2"], (19, 23, 19), 64, 128, 0)
+        m.conv3d_fwd(_p(b["dy2"]), _p(b["w4t"]), 0, 0, 0, _p(b["dp1"]), 0, G, B, 17, 21, 17, 128, 64, 2, st)
+        # layer 1: sparse wgrad through pool1/ReLU/BN1 (closed form)
+        m.conv1_wgrad(_p(x8), _p(idx), _p(b["dp1"]), _p(b["p1"]), _p(b["a1"]), NB, B, _p(b["c1part"]), _p(b["w125"]),
+                      _p(b["mu"]), _p(b["covw"]), _p(b["i1"]), _p(theta), P, o["features.1.weight"], _p(grads), P,
+                      o["features.0.weight"], o["features.0.bias"], o["features.1.weight"], o["features.1.bias"],
+                      1.0 / 255.0, st)
+        return b["loss"]
+
+    def eval_logits(self, theta, bufs, x8, idx, G, B):
+        """Eval-mode (running-stat BN, no dropout) logits [G*B] for client g's samples idx[g*B:(g+1)*B]."""
+        m, st = self.m, torch.cuda.current_stream().cuda_stream
+        b = self.forward(theta, bufs, x8, None, idx, G, B, False)
+        P = theta.stride(0)
+        o = self.o
+        m.head(_p(b["p5"]), _p(theta), P, o["classifier.1.weight"], o["classifier.1.bias"], o["classifier.4.weight"],
+               o["classifier.4.bias"], 0, _p(b["logits"]), 0, 0, P, 0, G, B, 0, 1.0, 0, st)
+        return b["logits"]

@@ -1,0 +1,523 @@
+"""Client-batched FL executor: many virtual clients per GPU, one process per GPU, RCCL aggregation.
+
+This is the MI355X-native replacement of the reference's sequential client loop
+(``sailentgrads_api.py:86-147`` / ``fedavg_api.py:40-88``): instead of swapping one shared ``nn.Module``'s
+state_dict per client and copying weights host<->device, every rank keeps its shard of clients resident
+as rows of ``theta [C_local, P]`` (params) and ``bufs [C_local, Q]`` (BN running stats) and trains all of
+them in lockstep — one launch sequence per local step for the whole shard.
+
+Round semantics reproduced from the reference (SURVEY.md §2.2 "Shared algorithm behaviors"):
+* client sampling ``np.random.seed(round); choice(total, per_round, replace=False)`` (all if frac=1);
+* every sampled client starts from ``w_global``; SGD(lr * lr_decay**round, momentum, wd) rebuilt per round
+  (momentum never carries over, Q4); ``clip_grad_norm_(10)``; SalientGrads multiplies weights by the global
+  SNIP mask after every step (Q2);
+* one DataLoader(shuffle=True) pass per epoch over the client's train split (last batch may be partial);
+* aggregation: sample-weighted average over ALL state entries incl. BN running stats and
+  ``num_batches_tracked`` (Q3) — a local weighted row-sum followed by ONE all-reduce of P+Q floats;
+* evaluation: global model and each client's last local ("personal") model on that client's test split;
+  logged loss uses sigmoid-then-BCEWithLogits (Q1); metrics are unweighted means over clients (Q5).
+"""
+from __future__ import annotations
+
+import math
+import time
+from dataclasses import dataclass, field
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+from .. import ops
+from ..ops import reference as R
+from ..parallel import runtime as rt
+from .flat import ParamLayout
+
+
+# ------------------------------------------------------------------------------------------------
+@dataclass
+class ClientSplit:
+    """Global sample indices of one client (into the engine's data store)."""
+    train: np.ndarray
+    test: np.ndarray
+
+
+@dataclass
+class FLConfig:
+    comm_round: int = 200
+    epochs: int = 2
+    batch_size: int = 16
+    lr: float = 0.01
+    lr_decay: float = 0.998
+    wd: float = 5e-4
+    momentum: float = 0.0
+    max_norm: float = 10.0
+    frac: float = 1.0
+    dense_ratio: float = 0.5
+    itersnip_iteration: int = 1
+    snip_mask: bool = True
+    dropout_keep: float = 0.5
+    frequency_of_the_test: int = 1
+    seed: int = 1024
+    prox_mu: float = 0.0          # FedProx proximal coefficient (0 = FedAvg/SalientGrads)
+    group: int = 0                # max clients per lockstep launch (0 = all local clients)
+    test_batch: int = 256
+
+
+# ------------------------------------------------------------------------------------------------
+class HipEngine:
+    """AlexNet3D_Dropout on the gfx950 kernels (ABCD-shape volumes, polyphase uint8 store)."""
+
+    def __init__(self, template_model, x8, mom, labels, device):
+        from .alexnet_hip import HipAlexNet3D
+        self.players = ParamLayout.from_tensors(list(template_model.named_parameters()))
+        self.blayers = ParamLayout.from_tensors(list(template_model.named_buffers()))
+        self.net = HipAlexNet3D(self.players, self.blayers, device)
+        self.x8, self.mom, self.labels = x8, mom, labels
+        self.device = torch.device(device)
+        self.m = ops.ext()
+
+    def train_step(self, theta, bufs, grads, idx, G, B, keep, seed):
+        y = self.labels.index_select(0, idx.long())
+        return self.net.train_step(theta, bufs, grads, self.x8, self.mom, idx, y, G, B, keep, seed)
+
+    def eval_logits(self, theta, bufs, idx, G, B):
+        return self.net.eval_logits(theta, bufs, self.x8, idx, G, B)
+
+    # fused optimizer: clip(10) -> SGD(wd, momentum) -> w *= mask (one HIP pass per row)
+    def opt_step(self, theta, grads, mom_buf, mask, lr, wd, momentum, first, max_norm):
+        G, P = theta.shape
+        ws = self.m.clip_sgd_mask_workspace(G, P)
+        if not hasattr(self, "_optws") or self._optws.numel() < ws:
+            self._optws = torch.empty(ws, dtype=torch.float32, device=theta.device)
+        self.m.clip_sgd_mask(theta.data_ptr(), grads.data_ptr(), mom_buf.data_ptr() if mom_buf is not None else 0,
+                             mask.data_ptr() if mask is not None else 0, self._optws.data_ptr(), 0, 0, G, P,
+                             theta.stride(0), float(lr), float(wd), float(momentum), int(first), float(max_norm),
+                             torch.cuda.current_stream().cuda_stream)
+
+    def saliency_acc(self, theta, grads, score, alpha):
+        G, P = theta.shape
+        self.m.saliency_acc(theta.data_ptr(), grads.data_ptr(), theta.stride(0), P, G, float(alpha),
+                            score.data_ptr(), score.stride(0), torch.cuda.current_stream().cuda_stream)
+
+
+class TorchEngine:
+    """Any ``nn.Module`` (reference-semantics eager path; CPU tests, 2D CNN families, baselines).
+
+    ``store``: float tensor ``[N, ...]`` of inputs (already scaled); ``labels``: ``[N]``.
+    ``loss``: ``"bce"`` (class_num=1, logits [B,1]) or ``"ce"`` (multi-class)."""
+
+    def __init__(self, template_model, store, labels, device, loss="bce", dtype=torch.float32):
+        self.model = template_model.to(device)
+        self.players = ParamLayout.from_tensors(list(self.model.named_parameters()))
+        self.blayers = ParamLayout.from_tensors(list(self.model.named_buffers()))
+        self.store, self.labels, self.device, self.loss, self.dtype = store, labels, torch.device(device), loss, dtype
+
+    def _views(self, row, layout):
+        return {n: row[o:o + layout.numel(i)].view(layout.shapes[i])
+                for i, (n, o) in enumerate(zip(layout.names, layout.offsets))}
+
+    def _batch(self, idx):
+        x = self.store.index_select(0, idx.long().to(self.store.device)).to(self.device)
+        if x.dtype == torch.uint8:
+            x = x.to(self.dtype) / 255.0
+        if x.dim() == 4:  # volumes without channel dim
+            x = x.unsqueeze(1)
+        y = self.labels.index_select(0, idx.long().to(self.labels.device)).to(self.device)
+        return x.to(self.dtype), y
+
+    def _loss(self, out, y):
+        if self.loss == "bce":
+            return F.binary_cross_entropy_with_logits(out.float().view(-1, 1), y.float().view(-1, 1))
+        return F.cross_entropy(out.float(), y.long())
+
+    def train_step(self, theta, bufs, grads, idx, G, B, keep, seed):
+        from torch.func import functional_call
+        torch.manual_seed(int(seed) & 0x7fffffff)
+        losses = torch.zeros(G, device=theta.device)
+        self.model.train()
+        for g in range(G):
+            row = theta[g].detach().clone().requires_grad_(True)
+            pv = self._views(row, self.players)
+            bv = self._views(bufs[g], self.blayers)
+            x, y = self._batch(idx[g * B:(g + 1) * B])
+            out = functional_call(self.model, {**pv, **bv}, (x,))
+            if isinstance(out, (list, tuple)):
+                out = out[0]
+            loss = self._loss(out, y)
+            loss.backward()
+            grads[g].copy_(row.grad)
+            losses[g] = loss.detach()
+        return losses
+
+    def eval_logits(self, theta, bufs, idx, G, B):
+        from torch.func import functional_call
+        self.model.eval()
+        outs = []
+        with torch.no_grad():
+            for g in range(G):
+                pv = self._views(theta[g], self.players)
+                bv = self._views(bufs[g].clone(), self.blayers)
+                x, _ = self._batch(idx[g * B:(g + 1) * B])
+                out = functional_call(self.model, {**pv, **bv}, (x,))
+                if isinstance(out, (list, tuple)):
+                    out = out[0]
+                outs.append(out.float())
+        return torch.cat(outs, 0)
+
+    def opt_step(self, theta, grads, mom_buf, mask, lr, wd, momentum, first, max_norm):
+        for g in range(theta.shape[0]):
+            gn = float(grads[g].norm())
+            coef = min(1.0, max_norm / (gn + 1e-6))
+            d = grads[g] * coef + wd * theta[g]
+            if momentum != 0 and mom_buf is not None:
+                if first:
+                    mom_buf[g].copy_(d)
+                else:
+                    mom_buf[g].mul_(momentum).add_(d)
+                d = mom_buf[g]
+            theta[g].add_(d, alpha=-lr)
+            if mask is not None:
+                theta[g].mul_(mask)
+
+    def saliency_acc(self, theta, grads, score, alpha):
+        score.add_((theta * grads).abs() * alpha)
+
+
+# ------------------------------------------------------------------------------------------------
+def padded_rows(n, width, device, align=64, dtype=torch.float32):
+    """``[n, width]`` zero view whose row stride is a multiple of ``align`` floats (16-B aligned rows for the
+    vectorised HIP kernels; P = 2,570,241 for AlexNet3D is odd)."""
+    ld = (width + align - 1) // align * align
+    return torch.zeros((n, ld), dtype=dtype, device=device)[:, :width]
+
+
+def gather_rows(src, ix):
+    out = padded_rows(ix.numel(), src.shape[1], src.device, dtype=src.dtype)
+    out.copy_(src.index_select(0, ix))
+    return out
+
+
+def maskable_flat_mask(layout: ParamLayout, names):
+    """Boolean [P] marking the maskable (conv / linear weight) entries, in layout order."""
+    m = torch.zeros(layout.total, dtype=torch.bool)
+    for i, n in enumerate(layout.names):
+        if n in names:
+            m[layout.offsets[i]:layout.offsets[i] + layout.numel(i)] = True
+    return m
+
+
+def snip_maskable_names(model):
+    out = []
+    for name, mod in model.named_modules():
+        if isinstance(mod, (torch.nn.Conv1d, torch.nn.Conv2d, torch.nn.Conv3d, torch.nn.Linear)):
+            out.append(name + ".weight")
+    return out
+
+
+class FLRunner:
+    """SalientGrads / FedAvg / FedProx over client-sharded, client-batched local training."""
+
+    def __init__(self, engine, splits, cfg: FLConfig, info: rt.DistInfo, template_model, logger=None,
+                 algorithm="salientgrads"):
+        self.e, self.cfg, self.info, self.log = engine, cfg, info, logger
+        self.alg = algorithm
+        self.N = len(splits)
+        self.splits = splits
+        self.device = info.device
+        self.shards = rt.shard_clients([len(s.train) for s in splits], info.world)
+        self.local = self.shards[info.rank]
+        self.C = len(self.local)
+        P, Q = engine.players.total, engine.blayers.total
+        self.P, self.Q = P, Q
+        flat_p = engine.players.flatten_state(dict(template_model.named_parameters()), self.device)
+        flat_b = engine.blayers.flatten_state(dict(template_model.named_buffers()), self.device)
+        self.w_global = flat_p.clone()
+        self.b_global = flat_b.clone()
+        nrow = max(1, self.C)
+        self.theta = padded_rows(nrow, P, self.device)
+        self.theta.copy_(flat_p.unsqueeze(0).expand(nrow, P))
+        self.bufs = padded_rows(nrow, Q, self.device)
+        self.bufs.copy_(flat_b.unsqueeze(0).expand(nrow, Q))
+        self.grads = padded_rows(nrow, P, self.device)
+        self.mom_buf = padded_rows(nrow, P, self.device) if cfg.momentum != 0 else None
+        self.mask = None
+        self.maskable = maskable_flat_mask(engine.players, snip_maskable_names(template_model)).to(self.device)
+        self.stat_info = dict(sum_comm_params=0, sum_training_flops=0, global_test_acc=[], person_test_acc=[],
+                              global_test_loss=[], person_test_loss=[], round_time=[])
+        self.timers = {"train": 0.0, "aggregate": 0.0, "eval": 0.0, "snip": 0.0}
+        self._step_seed = 0
+
+    # ---------------------------------------------------------------------------------------------
+    def _rng(self, *key):
+        return np.random.RandomState(abs(hash((self.cfg.seed,) + tuple(int(k) for k in key))) % (2 ** 31))
+
+    def _groups(self, rows):
+        gmax = self.cfg.group or len(rows)
+        return [rows[i:i + gmax] for i in range(0, len(rows), gmax)]
+
+    def _run_batches(self, rows, clients, round_idx, epoch_tag, fn, n_batches=None):
+        """Iterate lockstep local steps over ``clients`` (global ids) living in ``rows`` (local row ids).
+        ``fn(row_slice_or_index, idx_tensor, G, B)`` is called per (group, step)."""
+        B = self.cfg.batch_size
+        orders = []
+        for c in clients:
+            tr = self.splits[c].train
+            perm = self._rng(round_idx, c, epoch_tag).permutation(len(tr))
+            orders.append(tr[perm])
+        nsteps = max(int(math.ceil(len(o) / B)) for o in orders) if orders else 0
+        if n_batches is not None:
+            nsteps = min(nsteps, n_batches)
+        for s in range(nsteps):
+            by_size = {}
+            for r, o in zip(rows, orders):
+                chunk = o[s * B:(s + 1) * B]
+                if len(chunk):
+                    by_size.setdefault(len(chunk), []).append((r, chunk))
+            for bsz, items in sorted(by_size.items(), reverse=True):
+                for grp in self._groups(items):
+                    rr = [r for r, _ in grp]
+                    idx = torch.from_numpy(np.concatenate([ch for _, ch in grp]).astype(np.int32)).to(self.device)
+                    fn(rr, idx, len(grp), bsz)
+
+    def _with_rows(self, rr, body):
+        """Run ``body(theta, bufs, grads, mom)`` on rows ``rr`` (in place when they are a contiguous run)."""
+        lo, hi = rr[0], rr[-1] + 1
+        if rr == list(range(lo, hi)):
+            return body(self.theta[lo:hi], self.bufs[lo:hi], self.grads[lo:hi],
+                        self.mom_buf[lo:hi] if self.mom_buf is not None else None)
+        ix = torch.tensor(rr, device=self.device)
+        th, bu, gr = gather_rows(self.theta, ix), gather_rows(self.bufs, ix), gather_rows(self.grads, ix)
+        mo = gather_rows(self.mom_buf, ix) if self.mom_buf is not None else None
+        out = body(th, bu, gr, mo)
+        self.theta[ix] = th
+        self.bufs[ix] = bu
+        if mo is not None:
+            self.mom_buf[ix] = mo
+        return out
+
+    # ---------------------------------------------------------------------------------------------
+    def generate_global_mask_snip(self):
+        """IterSNIP saliency on every client (mean over iterations, then clients) -> global top-k mask
+        (``sailentgrads_api.py:47-66``, ``snip.py:21-116``)."""
+        t0 = time.perf_counter()
+        cfg = self.cfg
+        score = torch.zeros((max(1, self.C), self.P), dtype=torch.float32, device=self.device)
+        rows = list(range(self.C))
+        self.theta.copy_(self.w_global.unsqueeze(0).expand_as(self.theta))
+        saved_bufs = self.bufs.clone()
+        for it in range(cfg.itersnip_iteration):
+            # "next(iter(train_loader))": the first batch of a fresh shuffle
+            def fn(rr, idx, G, B):
+                def body(th, bu, gr, mo):
+                    self._step_seed += 1
+                    self.e.train_step(th, bu, gr, idx, G, B, cfg.dropout_keep, (cfg.seed << 20) + self._step_seed)
+                    lo, hi = rr[0], rr[-1] + 1
+                    self.e.saliency_acc(th, gr, score[lo:hi] if rr == list(range(lo, hi)) else score[rr],
+                                        1.0 / cfg.itersnip_iteration)
+                self._with_rows(rr, body)
+            self._run_batches(rows, self.local, -1, it, fn, n_batches=1)
+        self.bufs.copy_(saved_bufs)  # SNIP runs on a model copy: running stats are discarded
+        total = score.sum(0) if self.C else torch.zeros(self.P, device=self.device)
+        rt.all_reduce_buckets(total, self.info)
+        total /= self.N
+        sel = total[self.maskable]
+        sel = sel / sel.sum()
+        k = int(sel.numel() * cfg.dense_ratio)
+        mask = torch.ones(self.P, dtype=torch.float32, device=self.device)
+        if k >= 1:
+            if self.device.type == "cuda":
+                m = self.e.m
+                st = torch.empty(4, dtype=torch.int32, device=self.device)
+                hist = torch.empty(256, dtype=torch.int32, device=self.device)
+                sel = sel.contiguous()
+                m.radix_select_kth(sel.data_ptr(), sel.numel(), k, st.data_ptr(), hist.data_ptr(),
+                                   torch.cuda.current_stream().cuda_stream)
+                keep = torch.empty_like(sel)
+                m.threshold_mask(sel.data_ptr(), sel.numel(), st.data_ptr(), keep.data_ptr(),
+                                 torch.cuda.current_stream().cuda_stream)
+            else:
+                thr = torch.topk(sel, k, sorted=True).values[-1]
+                keep = (sel >= thr).float()
+            mask[self.maskable] = keep
+        self.mask = mask if cfg.snip_mask else torch.ones_like(mask)
+        self.timers["snip"] += time.perf_counter() - t0
+        return self.mask
+
+    # ---------------------------------------------------------------------------------------------
+    def sample_clients(self, round_idx):
+        per_round = max(1, int(self.N * self.cfg.frac))
+        if per_round >= self.N:
+            return list(range(self.N))
+        np.random.seed(round_idx)
+        return sorted(np.random.choice(range(self.N), per_round, replace=False).tolist())
+
+    def local_train(self, round_idx, sampled):
+        cfg = self.cfg
+        loc = [c for c in self.local if c in set(sampled)]
+        rows = [self.local.index(c) for c in loc]
+        if not rows:
+            return
+        for r in rows:
+            self.theta[r].copy_(self.w_global)
+            self.bufs[r].copy_(self.b_global)
+        lr = cfg.lr * (cfg.lr_decay ** round_idx)
+        first = [True]
+        for ep in range(cfg.epochs):
+            def fn(rr, idx, G, B):
+                def body(th, bu, gr, mo):
+                    self._step_seed += 1
+                    if cfg.prox_mu > 0:
+                        w_ref = self.w_global
+                    self.e.train_step(th, bu, gr, idx, G, B, cfg.dropout_keep, (cfg.seed << 20) + self._step_seed)
+                    if cfg.prox_mu > 0:
+                        gr.add_(th - w_ref.unsqueeze(0), alpha=cfg.prox_mu)
+                    self.e.opt_step(th, gr, mo, self.mask if self.alg == "salientgrads" else None, lr, cfg.wd,
+                                    cfg.momentum, first[0], cfg.max_norm)
+                self._with_rows(rr, body)
+                first[0] = False
+            self._run_batches(rows, loc, round_idx, ep, fn)
+
+    def aggregate(self, sampled):
+        """w_global = sum_i n_i/sum n * w_i over sampled clients (params + buffers), one all-reduce."""
+        sset = set(sampled)
+        n_tot = float(sum(len(self.splits[c].train) for c in sampled))
+        Pp = (self.P + 63) // 64 * 64  # keep the buffer section 16-B aligned for the vectorised kernel
+        buf = torch.zeros(Pp + self.Q, dtype=torch.float32, device=self.device)
+        rows = [i for i, c in enumerate(self.local) if c in sset]
+        if rows:
+            w = torch.tensor([len(self.splits[self.local[r]].train) / n_tot for r in rows], dtype=torch.float32,
+                             device=self.device)
+            ix = torch.tensor(rows, device=self.device)
+            if self.device.type == "cuda" and rows == list(range(rows[0], rows[-1] + 1)):
+                m, st = self.e.m, torch.cuda.current_stream().cuda_stream
+                lo = rows[0]
+                m.weighted_rows_sum(self.theta[lo].data_ptr(), w.data_ptr(), len(rows), self.P, self.theta.stride(0),
+                                    0.0, buf.data_ptr(), st)
+                m.weighted_rows_sum(self.bufs[lo].data_ptr(), w.data_ptr(), len(rows), self.Q, self.bufs.stride(0),
+                                    0.0, buf[Pp:].data_ptr(), st)
+            else:
+                buf[:self.P] = (w.view(-1, 1) * self.theta[ix]).sum(0)
+                buf[Pp:] = (w.view(-1, 1) * self.bufs[ix]).sum(0)
+        rt.all_reduce_buckets(buf, self.info)
+        self.w_global.copy_(buf[:self.P])
+        self.b_global.copy_(buf[Pp:])
+
+    def _eval_rows(self, theta, bufs, clients, per_client_rows):
+        """Per-client (correct, loss_sum, total) with reference test semantics (Q1).  Clients that share a
+        model row are evaluated together in chunks of ``test_batch`` samples (one launch sequence each)."""
+        out = np.zeros((len(clients), 3), dtype=np.float64)
+        by_row = {}
+        for j, r in enumerate(per_client_rows):
+            by_row.setdefault(r, []).append(j)
+        for r, js in by_row.items():
+            tests = [self.splits[clients[j]].test for j in js]
+            owner = np.concatenate([np.full(len(t), k) for k, t in enumerate(tests)]).astype(np.int64)
+            allidx = np.concatenate(tests).astype(np.int32) if tests else np.zeros(0, np.int32)
+            if allidx.size == 0:
+                continue
+            th, bu = theta[r:r + 1], bufs[r:r + 1]
+            tb = self.cfg.test_batch
+            acc = torch.zeros((len(js), 3), dtype=torch.float64, device=self.device)
+            own_t = torch.from_numpy(owner).to(self.device)
+            for s in range(0, allidx.size, tb):
+                idx = torch.from_numpy(allidx[s:s + tb]).to(self.device)
+                logits = self.e.eval_logits(th, bu, idx, 1, idx.numel()).view(-1)
+                y = self.e.labels.index_select(0, idx.long()).to(logits.device).float()
+                pred = torch.sigmoid(logits)
+                loss = F.binary_cross_entropy_with_logits(pred, y, reduction="none")
+                correct = ((pred >= 0.5).float() == y).float()
+                o = own_t[s:s + idx.numel()]
+                acc[:, 0].index_add_(0, o, correct.double())
+                acc[:, 1].index_add_(0, o, loss.double())
+                acc[:, 2].index_add_(0, o, torch.ones_like(loss, dtype=torch.float64))
+            out[js] = acc.cpu().numpy()
+        return out
+
+    def _eval_grouped(self, theta, bufs, rows, clients):
+        """Personal models: clients with equal test sizes are evaluated in one grouped launch."""
+        out = np.zeros((len(clients), 3), dtype=np.float64)
+        sizes = {}
+        for j, c in enumerate(clients):
+            sizes.setdefault(len(self.splits[c].test), []).append(j)
+        for n, js in sizes.items():
+            if n == 0:
+                continue
+            if n > self.cfg.test_batch or rows != list(range(rows[0], rows[0] + len(rows))):
+                res = self._eval_rows(theta, bufs, [clients[j] for j in js], [rows[j] for j in js])
+                out[js] = res
+                continue
+            for grp in self._groups(js):
+                rr = [rows[j] for j in grp]
+                lo, hi = rr[0], rr[-1] + 1
+                if rr != list(range(lo, hi)):
+                    out[grp] = self._eval_rows(theta, bufs, [clients[j] for j in grp], rr)
+                    continue
+                idx = torch.from_numpy(np.concatenate([self.splits[clients[j]].test for j in grp]).astype(np.int32))
+                idx = idx.to(self.device)
+                logits = self.e.eval_logits(theta[lo:hi], bufs[lo:hi], idx, len(grp), n).view(len(grp), n)
+                y = self.e.labels.index_select(0, idx.long()).to(logits.device).float().view(len(grp), n)
+                pred = torch.sigmoid(logits)
+                loss = F.binary_cross_entropy_with_logits(pred, y, reduction="none").sum(1)
+                correct = ((pred >= 0.5).float() == y).float().sum(1)
+                res = torch.stack([correct, loss, torch.full_like(loss, n)], 1).double().cpu().numpy()
+                out[grp] = res
+        return out
+
+    def evaluate(self, round_idx):
+        t0 = time.perf_counter()
+        gth = padded_rows(1, self.P, self.device)
+        gth.copy_(self.w_global.unsqueeze(0))
+        gbu = padded_rows(1, self.Q, self.device)
+        gbu.copy_(self.b_global.unsqueeze(0))
+        glob = self._eval_rows(gth, gbu, self.local, [0] * self.C) if self.C else np.zeros((0, 3))
+        pers = self._eval_grouped(self.theta, self.bufs, list(range(self.C)), self.local) if self.C else np.zeros((0, 3))
+        res = torch.zeros((self.N, 6), dtype=torch.float64, device=self.device)
+        if self.C:
+            res[torch.tensor(self.local, device=self.device)] = torch.from_numpy(
+                np.concatenate([glob, pers], 1)).to(self.device)
+        rt.all_reduce_buckets(res, self.info)
+        r = res.cpu().numpy()
+        ok = r[:, 2] > 0
+        g_acc = float(np.mean(r[ok, 0] / r[ok, 2])) if ok.any() else 0.0
+        g_loss = float(np.mean(r[ok, 1] / r[ok, 2])) if ok.any() else 0.0
+        okp = r[:, 5] > 0
+        p_acc = float(np.mean(r[okp, 3] / r[okp, 5])) if okp.any() else 0.0
+        p_loss = float(np.mean(r[okp, 4] / r[okp, 5])) if okp.any() else 0.0
+        self.stat_info["global_test_acc"].append(g_acc)
+        self.stat_info["global_test_loss"].append(g_loss)
+        self.stat_info["person_test_acc"].append(p_acc)
+        self.stat_info["person_test_loss"].append(p_loss)
+        if self.log is not None and self.info.is_main:
+            self.log.info({"global_test_acc": g_acc, "global_test_loss": g_loss})
+            self.log.info({"person_test_acc": p_acc, "person_test_loss": p_loss})
+        self.timers["eval"] += time.perf_counter() - t0
+        return dict(global_test_acc=g_acc, global_test_loss=g_loss, person_test_acc=p_acc, person_test_loss=p_loss)
+
+    def run_round(self, round_idx, sync_timers=False):
+        t0 = time.perf_counter()
+        sampled = self.sample_clients(round_idx)
+        if self.log is not None and self.info.is_main:
+            self.log.info("################Communication round : {}".format(round_idx))
+            self.log.info("client_indexes = " + str(np.array(sampled)))
+        self.local_train(round_idx, sampled)
+        if sync_timers and self.device.type == "cuda":
+            torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        self.aggregate(sampled)
+        if sync_timers and self.device.type == "cuda":
+            torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        self.timers["train"] += t1 - t0
+        self.timers["aggregate"] += t2 - t1
+        res = None
+        if self.cfg.frequency_of_the_test and (round_idx % self.cfg.frequency_of_the_test == 0):
+            res = self.evaluate(round_idx)
+        self.stat_info["round_time"].append(time.perf_counter() - t0)
+        return res
+
+    def train(self):
+        if self.alg == "salientgrads":
+            self.generate_global_mask_snip()
+        for r in range(self.cfg.comm_round):
+            self.run_round(r)
+        return self.stat_info

@@ -1,0 +1,415 @@
+"""GPU numerics tests: every HIP kernel against a plain PyTorch fp32 reference of the same op.
+
+All tests run in one process on the GPU box (``pytest -m gpu``).  Shapes are the real AlexNet3D shapes at the
+ABCD input (1x121x145x121) with small client/batch counts, and every launch's operands are validated on the
+host by the Python wrappers first.
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from neuroimagedisttraining_amd.engine.executor import padded_rows
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def _m():
+    from neuroimagedisttraining_amd import ops
+    return ops.ext()
+
+
+def _st():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _relerr(a, b):
+    a, b = a.double(), b.double()
+    return float((a - b).norm() / (b.norm() + 1e-30))
+
+
+def _cl(x):  # NCDHW -> NDHWC
+    return x.permute(0, 2, 3, 4, 1).contiguous()
+
+
+def _cf(x):  # NDHWC -> NCDHW
+    return x.permute(0, 4, 1, 2, 3).contiguous()
+
+
+# ------------------------------------------------------------------------------------------------
+def test_polyphase_and_moments():
+    from neuroimagedisttraining_amd.ops.reference import polyphase, unpolyphase
+    from neuroimagedisttraining_amd.data.synthetic_fl import conv1_moments_reference, to_hip_store
+    torch.manual_seed(0)
+    vol = torch.randint(0, 256, (2, 121, 145, 121), dtype=torch.uint8, device=DEV)
+    x8, mom = to_hip_store(vol)
+    torch.cuda.synchronize()
+    assert torch.equal(x8, polyphase(vol))
+    assert torch.equal(unpolyphase(x8), vol)
+    ref = conv1_moments_reference(vol[:1].cpu())
+    assert torch.equal(mom[:1].cpu(), ref), "moments must be exact (integer-valued fp64)"
+
+
+@pytest.mark.parametrize("cin,cout,pad,sp,xf", [(64, 128, 0, (19, 23, 19), False), (128, 192, 1, (5, 7, 5), False),
+                                                (192, 192, 1, (5, 7, 5), True), (192, 128, 1, (5, 7, 5), True),
+                                                (128, 64, 2, (17, 21, 17), False)])
+def test_conv3d_fwd_stats(cin, cout, pad, sp, xf):
+    m = _m()
+    G, B = 2, 3
+    torch.manual_seed(1)
+    x = torch.randn(G * B, *sp, cin, device=DEV).bfloat16()
+    w = (torch.randn(G, cout, 27, cin, device=DEV) * 0.05).bfloat16()
+    bias = torch.randn(G, cout, device=DEV)
+    xs = torch.rand(G, cin, device=DEV) + 0.5 if xf else None
+    xt = torch.randn(G, cin, device=DEV) * 0.2 if xf else None
+    Do, Ho, Wo = [s + 2 * pad - 2 for s in sp]
+    y = torch.empty(G * B, Do, Ho, Wo, cout, device=DEV, dtype=torch.bfloat16)
+    npb = m.conv3d_fwd_nblocks(B, *sp, pad)
+    stats = torch.empty(G, npb, cout, 2, device=DEV)
+    m.conv3d_fwd(x.data_ptr(), w.data_ptr(), bias.data_ptr(), xs.data_ptr() if xf else 0, xt.data_ptr() if xf else 0,
+                 y.data_ptr(), stats.data_ptr(), G, B, *sp, cin, cout, pad, _st())
+    torch.cuda.synchronize()
+    ys = []
+    for g in range(G):
+        xin = x[g * B:(g + 1) * B].float()
+        if xf:
+            xin = torch.relu(xin * xs[g] + xt[g]).bfloat16().float()
+        wg = w[g].float().view(cout, 3, 3, 3, cin).permute(0, 4, 1, 2, 3)
+        ys.append(_cl(F.conv3d(_cf(xin), wg, bias[g], 1, pad)))
+    yr = torch.cat(ys, 0)
+    assert _relerr(y.float(), yr) < 1e-2
+    # statistics: merged block stats == batch mean / biased var per (client, channel)
+    Mg = B * Do * Ho * Wo
+    cnt = torch.tensor([min(128, Mg - b * 128) for b in range(npb)], device=DEV, dtype=torch.float64)
+    mean_b, m2_b = stats[..., 0].double(), stats[..., 1].double()
+    mean = (mean_b * cnt.view(1, -1, 1)).sum(1) / Mg
+    var = (m2_b + cnt.view(1, -1, 1) * (mean_b - mean.unsqueeze(1)) ** 2).sum(1) / Mg
+    yr_g = yr.view(G, Mg, cout).double()
+    assert _relerr(mean, yr_g.mean(1)) < 1e-3
+    assert _relerr(var, yr_g.var(1, unbiased=False)) < 1e-3
+
+
+@pytest.mark.parametrize("cin,cout,pad,sp,xf", [(64, 128, 0, (19, 23, 19), False), (128, 192, 1, (5, 7, 5), False),
+                                                (192, 192, 1, (5, 7, 5), True), (192, 128, 1, (5, 7, 5), True)])
+def test_conv3d_wgrad_and_dgrad(cin, cout, pad, sp, xf):
+    m = _m()
+    G, B = 2, 2
+    torch.manual_seed(2)
+    x = torch.randn(G * B, *sp, cin, device=DEV).bfloat16()
+    xs = torch.rand(G, cin, device=DEV) + 0.5 if xf else None
+    xt = torch.randn(G, cin, device=DEV) * 0.2 if xf else None
+    Do, Ho, Wo = [s + 2 * pad - 2 for s in sp]
+    dy = torch.randn(G * B, Do, Ho, Wo, cout, device=DEV).bfloat16()
+    P = cout * cin * 27 + 7
+    grad = torch.zeros(G, P, device=DEV)
+    ns = m.conv3d_wgrad_nsplit(G, B, *sp, cin, cout, pad)
+    part = torch.empty(ns * G * cout * 27 * cin, device=DEV)
+    m.conv3d_wgrad(x.data_ptr(), xs.data_ptr() if xf else 0, xt.data_ptr() if xf else 0, dy.data_ptr(), part.data_ptr(),
+                   grad.data_ptr(), P, 3, G, B, *sp, cin, cout, pad, ns, 1.0, _st())
+    # dgrad through the fwd kernel with flipped/transposed weights (packed from fp32 PyTorch layout)
+    wt32 = torch.randn(G, cout, cin, 3, 3, 3, device=DEV) * 0.05
+    theta = wt32.view(G, -1).contiguous()
+    wp = torch.empty(G, cout, 27, cin, device=DEV, dtype=torch.bfloat16)
+    wtt = torch.empty(G, cin, 27, cout, device=DEV, dtype=torch.bfloat16)
+    m.pack_conv_w(theta.data_ptr(), theta.stride(0), 0, G, cout, cin, 1.0, wp.data_ptr(), wtt.data_ptr(), _st())
+    dx = torch.empty(G * B, *sp, cin, device=DEV, dtype=torch.bfloat16)
+    m.conv3d_fwd(dy.data_ptr(), wtt.data_ptr(), 0, 0, 0, dx.data_ptr(), 0, G, B, Do, Ho, Wo, cout, cin, 2 - pad, _st())
+    torch.cuda.synchronize()
+    for g in range(G):
+        xin = x[g * B:(g + 1) * B].float()
+        if xf:
+            xin = torch.relu(xin * xs[g] + xt[g]).bfloat16().float()
+        xin = _cf(xin).requires_grad_(True)
+        wref = wt32[g].bfloat16().float().requires_grad_(True)
+        out = F.conv3d(xin, wref, None, 1, pad)
+        out.backward(_cf(dy[g * B:(g + 1) * B].float()))
+        dw = grad[g, 3:3 + cout * cin * 27].view(cout, cin, 3, 3, 3)
+        assert _relerr(dw, wref.grad) < 1e-2
+        if not xf:
+            assert _relerr(dx[g * B:(g + 1) * B].float(), _cl(xin.grad)) < 1e-2
+        # wp layout check
+        assert torch.equal(wp[g].view(cout, 3, 3, 3, cin).permute(0, 4, 1, 2, 3), wt32[g].bfloat16())
+
+
+def test_bn_relu_pool_and_bwd():
+    m = _m()
+    G, B, C = 2, 2, 128
+    D, H, W = 17, 21, 17
+    torch.manual_seed(3)
+    y = torch.randn(G * B, D, H, W, C, device=DEV).bfloat16()
+    scale = torch.rand(G, C, device=DEV) + 0.5
+    shift = torch.randn(G, C, device=DEV) * 0.3
+    out = torch.empty(G * B, D // 3, H // 3, W // 3, C, device=DEV, dtype=torch.bfloat16)
+    am = torch.empty_like(out, dtype=torch.uint8)
+    m.bn_relu_pool(y.data_ptr(), scale.data_ptr(), shift.data_ptr(), out.data_ptr(), am.data_ptr(), G * B, B, D, H, W, C,
+                   _st())
+    torch.cuda.synchronize()
+    z = y.float().view(G, B, D, H, W, C) * scale.view(G, 1, 1, 1, 1, C) + shift.view(G, 1, 1, 1, 1, C)
+    zr = _cf(z.view(G * B, D, H, W, C))
+    pr, ir = F.max_pool3d(torch.relu(zr), 3, 3, return_indices=True)
+    assert _relerr(out.float(), _cl(pr)) < 1e-2
+    # backward through pool -> relu -> BN(train) vs autograd
+    gamma = torch.rand(G, C, device=DEV) + 0.5
+    beta = torch.randn(G, C, device=DEV) * 0.3
+    P = 4 * C
+    theta = torch.zeros(G, P, device=DEV)
+    theta[:, :C] = gamma
+    theta[:, C:2 * C] = beta
+    yf = y.float().view(G, B * D * H * W, C).double()
+    mean = yf.mean(1).float()
+    invstd = (1.0 / torch.sqrt(yf.var(1, unbiased=False) + 1e-5)).float()
+    sc = (gamma * invstd).contiguous()
+    sh = (beta - mean * sc).contiguous()
+    m.bn_relu_pool(y.data_ptr(), sc.data_ptr(), sh.data_ptr(), out.data_ptr(), am.data_ptr(), G * B, B, D, H, W, C, _st())
+    dp = torch.randn_like(out, dtype=torch.float32).bfloat16()
+    grad = torch.zeros(G, P, device=DEV)
+    part = torch.empty(G * 64 * C * 2, device=DEV)
+    coef = torch.empty(G, C, 3, device=DEV)
+    dy = torch.empty_like(y)
+    m.bn_bwd(1, y.data_ptr(), dp.data_ptr(), out.data_ptr(), am.data_ptr(), sc.data_ptr(), sh.data_ptr(),
+             mean.data_ptr(), invstd.data_ptr(), G * B, B, D, H, W, C, part.data_ptr(), 64, theta.data_ptr(), P, 0,
+             grad.data_ptr(), P, 0, C, 2 * C, coef.data_ptr(), dy.data_ptr(), _st())
+    torch.cuda.synchronize()
+    for g in range(G):
+        # fp64 CPU autograd oracle (first-max pooling semantics, no library BN/pool kernels involved)
+        yi = _cf(y[g * B:(g + 1) * B].double().cpu()).requires_grad_(True)
+        gm = gamma[g].double().cpu().requires_grad_(True)
+        bt = beta[g].double().cpu().requires_grad_(True)
+        o = F.max_pool3d(torch.relu(F.batch_norm(yi, None, None, gm, bt, True, 0.1, 1e-5)), 3, 3)
+        o.backward(_cf(dp[g * B:(g + 1) * B].double().cpu()))
+        assert _relerr(grad[g, :C].cpu(), gm.grad) < 1e-3
+        assert _relerr(grad[g, C:2 * C].cpu(), bt.grad) < 1e-3
+        assert _relerr(dy[g * B:(g + 1) * B].float().cpu(), _cl(yi.grad)) < 1e-2
+        assert float(grad[g, 2 * C:3 * C].abs().max()) == 0.0  # conv bias grad before BN is exactly 0
+
+
+def _alexnet_setup(G, B, seed=0):
+    from neuroimagedisttraining_amd.data.volumes import make_synthetic_abcd
+    from neuroimagedisttraining_amd.data.synthetic_fl import to_hip_store
+    from neuroimagedisttraining_amd.engine.flat import ParamLayout
+    from neuroimagedisttraining_amd.models.alexnet3d import AlexNet3D_Dropout
+    torch.manual_seed(seed)
+    store = make_synthetic_abcd(G * B, seed=seed + 1, device=DEV)
+    x8, mom = to_hip_store(store.volumes)
+    model = AlexNet3D_Dropout(num_classes=1)
+    pl = ParamLayout.from_tensors(list(model.named_parameters()))
+    bl = ParamLayout.from_tensors(list(model.named_buffers()))
+    from neuroimagedisttraining_amd.engine.executor import padded_rows
+    theta = padded_rows(G, pl.total, DEV)
+    theta.copy_(torch.stack([pl.flatten_state(dict(AlexNet3D_Dropout(num_classes=1).named_parameters()), DEV)
+                             for _ in range(G)]))
+    bufs = padded_rows(G, bl.total, DEV)
+    bufs.copy_(bl.flatten_state(dict(model.named_buffers()), DEV).unsqueeze(0).expand(G, bl.total))
+    # non-trivial BN affine params so the BN backward paths are exercised
+    for i, n in enumerate(pl.names):
+        if n.startswith("features.") and int(n.split(".")[1]) in (1, 5, 9, 12, 15):
+            o, k = pl.offsets[i], pl.numel(i)
+            if n.endswith("weight"):
+                theta[:, o:o + k] = 0.75 + 0.5 * torch.rand(G, k, device=DEV)
+            else:
+                theta[:, o:o + k] = 0.1 * torch.randn(G, k, device=DEV)
+    return store, x8, mom, pl, bl, theta, bufs
+
+
+def _pool_at(h, amax):
+    """max_pool3d(3,3) whose window choices are the HIP kernel's argmax (both sides route gradients alike)."""
+    Bn, C, D, H, W = h.shape
+    Dp, Hp, Wp = D // 3, H // 3, W // 3
+    a = amax.long().permute(0, 4, 1, 2, 3)
+    pd = torch.arange(Dp, device=h.device).view(1, 1, Dp, 1, 1)
+    ph = torch.arange(Hp, device=h.device).view(1, 1, 1, Hp, 1)
+    pw = torch.arange(Wp, device=h.device).view(1, 1, 1, 1, Wp)
+    flat = ((3 * pd + a // 9) * H + 3 * ph + (a // 3) % 3) * W + 3 * pw + a % 3
+    return torch.gather(h.reshape(Bn, C, -1), 2, flat.reshape(Bn, C, -1)).view(Bn, C, Dp, Hp, Wp)
+
+
+def _routed_reference(b, theta, pl, vols, labels, G, B, keep, seed):
+    """fp64 autograd of AlexNet3D_Dropout in which every discrete decision (max-pool argmax, ReLU masks,
+    dropout masks) is taken from the HIP forward.  bf16 activations make near-ties flip those decisions
+    relative to an unconstrained fp64 run (a flip moves a whole gradient entry), so the engine is checked
+    against the same computation graph; the decisions themselves are checked by the forward comparisons."""
+    from neuroimagedisttraining_amd.ops.reference import dropout_keep
+    m1 = torch.from_numpy(dropout_keep(seed, G, B, 256, keep, 0)).to(DEV)
+    m2 = torch.from_numpy(dropout_keep(seed, G, B, 64, keep, 1)).to(DEV)
+    grads, logits = [], []
+    cfg = {0: (2, 0), 4: (1, 0), 8: (1, 1), 11: (1, 1), 14: (1, 1)}
+    for g in range(G):
+        sl = slice(g * B, (g + 1) * B)
+        row = theta[g].detach().double().clone().requires_grad_(True)
+        pv = {n: row[o:o + pl.numel(i)].view(pl.shapes[i]) for i, (n, o) in enumerate(zip(pl.names, pl.offsets))}
+        h = (vols[sl].double() / 255.0).unsqueeze(1)
+        for ci, bi in zip((0, 4, 8, 11, 14), (1, 5, 9, 12, 15)):
+            s_, pd = cfg[ci]
+            y = F.conv3d(h, pv["features.%d.weight" % ci], pv["features.%d.bias" % ci], s_, pd)
+            z = F.batch_norm(y, None, None, pv["features.%d.weight" % bi], pv["features.%d.bias" % bi], True, 0.1, 1e-5)
+            if ci in (0, 4, 14):
+                ours = {0: b["p1"], 4: b["p2"], 14: b["p5"]}[ci][sl]
+                h = _pool_at(z, {0: b["a1"], 4: b["a2"], 14: b["a5"]}[ci][sl]) * (_cf(ours.double()) > 0)
+            else:
+                yb = b["y%d" % {8: 3, 11: 4}[ci]][sl].float()
+                h = z * _cf(((yb * b["s%d" % ci][g] + b["t%d" % ci][g]) > 0).double())
+        f = h.flatten(1) * m1[g].double() / keep
+        fo = _cf(b["p5"][sl].double()).flatten(1) * m1[g].double() / keep
+        z1o = F.linear(fo, pv["classifier.1.weight"].detach(), pv["classifier.1.bias"].detach())
+        zz = F.linear(f, pv["classifier.1.weight"], pv["classifier.1.bias"]) * (z1o > 0) * m2[g].double() / keep
+        out = F.linear(zz, pv["classifier.4.weight"], pv["classifier.4.bias"])
+        F.binary_cross_entropy_with_logits(out, labels[sl].double().view(B, 1)).backward()
+        grads.append(row.grad)
+        logits.append(out.detach().view(-1))
+    return torch.stack(grads), torch.cat(logits)
+
+
+@pytest.mark.parametrize("keep", [1.0, 0.5])
+def test_alexnet_train_step_matches_autograd(keep):
+    from neuroimagedisttraining_amd.engine.alexnet_hip import HipAlexNet3D
+    from neuroimagedisttraining_amd.ops.reference import train_step_reference
+    G, B = 2, 4
+    store, x8, mom, pl, bl, theta, bufs = _alexnet_setup(G, B)
+    net = HipAlexNet3D(pl, bl, DEV)
+    grads = padded_rows(G, pl.total, DEV)
+    bufs_h = padded_rows(G, bl.total, DEV)
+    bufs_h.copy_(bufs)
+    idx = torch.arange(G * B, dtype=torch.int32, device=DEV)
+    loss = net.train_step(theta, bufs_h, grads, x8, mom, idx, store.labels.float(), G, B, keep=keep, seed=77)
+    torch.cuda.synchronize()
+    b = net._cache[(G, B, True)]
+    # (1) unconstrained fp64 reference: forward, loss and BN running statistics
+    bufs_r = bufs.clone()
+    gfree, lr_, logit_r = train_step_reference(pl, bl, theta, bufs_r, store.volumes, store.labels.float(), B,
+                                               keep=keep, seed=77, dtype=torch.float64)
+    assert _relerr(b["logits"], logit_r) < 3e-2
+    assert _relerr(loss, lr_) < 3e-2
+    assert _relerr(bufs_h, bufs_r) < 1e-2
+    # (2) gradients against the decision-routed fp64 graph
+    gr, _ = _routed_reference(b, theta, pl, store.volumes, store.labels, G, B, keep, 77)
+    errs = {}
+    for i, n in enumerate(pl.names):
+        o, k = pl.offsets[i], pl.numel(i)
+        if n.startswith("features.") and n.endswith(".bias") and int(n.split(".")[1]) in (0, 4, 8, 11, 14):
+            assert float(grads[:, o:o + k].abs().max()) == 0.0  # conv bias before train-mode BN: exactly 0
+            continue
+        errs[n] = _relerr(grads[:, o:o + k], gr[:, o:o + k])
+    print("grad rel errors", errs)
+    bad = {n: e for n, e in errs.items() if e > 3e-2}
+    assert not bad, bad
+    # (3) the free-running fp64 gradient still points the same way (cosine over the whole model)
+    cos = F.cosine_similarity(grads.double().flatten(), gfree.double().flatten(), dim=0)
+    assert float(cos) > 0.9, float(cos)
+
+
+def test_conv1_fused_fwd_and_sparse_wgrad():
+    """conv1 -> BN(train, stats from patch moments) -> ReLU -> pool, and the closed-form backward, vs fp64 autograd."""
+    from neuroimagedisttraining_amd.engine.alexnet_hip import HipAlexNet3D
+    m = _m()
+    G, B = 2, 2
+    store, x8, mom, pl, bl, theta, bufs = _alexnet_setup(G, B, seed=9)
+    net = HipAlexNet3D(pl, bl, DEV)
+    idx = torch.arange(G * B, dtype=torch.int32, device=DEV)
+    b = net._bufs(G, B, True)
+    net._pack(theta, G, b, True)
+    o = net.o
+    st = _st()
+    P, Q = theta.stride(0), bufs.stride(0)
+    m.conv1_bnstats(mom.data_ptr(), idx.data_ptr(), B, G, b["Mb"].data_ptr(), b["w125"].data_ptr(), theta.data_ptr(), P,
+                    o["features.0.bias"], o["features.1.weight"], o["features.1.bias"], bufs.data_ptr(), Q,
+                    net.ob["features.1.running_mean"], net.ob["features.1.running_var"],
+                    net.ob["features.1.num_batches_tracked"], 0.1, 1e-5, 0, b["s1"].data_ptr(), b["t1"].data_ptr(),
+                    b["m1"].data_ptr(), b["i1"].data_ptr(), b["mu"].data_ptr(), b["covw"].data_ptr(), st)
+    m.conv1_fwd_pool(x8.data_ptr(), idx.data_ptr(), b["w1p"].data_ptr(), b["s1"].data_ptr(), b["t1"].data_ptr(), G * B, B,
+                     b["p1"].data_ptr(), b["a1"].data_ptr(), st)
+    torch.manual_seed(11)
+    dp = torch.randn(G * B, 19, 23, 19, 64, device=DEV).bfloat16()
+    grads = padded_rows(G, pl.total, DEV)
+    m.conv1_wgrad(x8.data_ptr(), idx.data_ptr(), dp.data_ptr(), b["p1"].data_ptr(), b["a1"].data_ptr(), G * B, B,
+                  b["c1part"].data_ptr(), b["w125"].data_ptr(), b["mu"].data_ptr(), b["covw"].data_ptr(),
+                  b["i1"].data_ptr(), theta.data_ptr(), P, o["features.1.weight"], grads.data_ptr(), P,
+                  o["features.0.weight"], o["features.0.bias"], o["features.1.weight"], o["features.1.bias"],
+                  1.0 / 255.0, st)
+    torch.cuda.synchronize()
+    ow, og, ob = o["features.0.weight"], o["features.1.weight"], o["features.1.bias"]
+    for g in range(G):
+        # the kernel convolves with bf16(w/255): use exactly those weights in the oracle
+        w_eff = (b["w125"][g].double() * 255.0).view(64, 1, 5, 5, 5).detach().clone().requires_grad_(True)
+        gm = theta[g, og:og + 64].double().detach().clone().requires_grad_(True)
+        bt = theta[g, ob:ob + 64].double().detach().clone().requires_grad_(True)
+        x = (store.volumes[g * B:(g + 1) * B].double() / 255.0).unsqueeze(1)
+        y = F.conv3d(x, w_eff, None, 2, 0)
+        z = F.batch_norm(y, None, None, gm, bt, True, 0.1, 1e-5)
+        assert _relerr(b["p1"][g * B:(g + 1) * B].float(), _cl(F.max_pool3d(torch.relu(z), 3, 3).detach())) < 1e-2
+        ours = b["p1"][g * B:(g + 1) * B]
+        pr = _pool_at(z, b["a1"][g * B:(g + 1) * B]) * (_cf(ours.double()) > 0)
+        pr.backward(_cf(dp[g * B:(g + 1) * B].double()))
+        e_w = _relerr(grads[g, ow:ow + 8000], w_eff.grad.view(-1))
+        e_g = _relerr(grads[g, og:og + 64], gm.grad)
+        e_b = _relerr(grads[g, ob:ob + 64], bt.grad)
+        print("conv1 grad errors", e_w, e_g, e_b)
+        assert e_w < 2e-2 and e_g < 2e-2 and e_b < 2e-2, (e_w, e_g, e_b)
+
+
+def test_alexnet_eval_matches_reference():
+    from neuroimagedisttraining_amd.engine.alexnet_hip import HipAlexNet3D
+    from neuroimagedisttraining_amd.ops.reference import eval_logits_reference
+    G, B = 2, 3
+    store, x8, mom, pl, bl, theta, bufs = _alexnet_setup(G, B, seed=5)
+    for i, n in enumerate(bl.names):
+        o, k = bl.offsets[i], bl.numel(i)
+        if n.endswith("running_mean"):
+            bufs[:, o:o + k] = 0.1 * torch.randn(G, k, device=DEV)
+        if n.endswith("running_var"):
+            bufs[:, o:o + k] = 0.5 + torch.rand(G, k, device=DEV)
+    net = HipAlexNet3D(pl, bl, DEV)
+    idx = torch.arange(G * B, dtype=torch.int32, device=DEV)
+    out = net.eval_logits(theta, bufs, x8, idx, G, B)
+    ref = eval_logits_reference(pl, bl, theta, bufs, store.volumes, B, dtype=torch.float64)
+    assert _relerr(out, ref) < 3e-2
+
+
+def test_clip_sgd_mask_matches_reference():
+    m = _m()
+    G, P = 3, 2570241
+    torch.manual_seed(4)
+    from neuroimagedisttraining_amd.engine.executor import padded_rows
+    theta = padded_rows(G, P, DEV)
+    theta.copy_(torch.randn(G, P, device=DEV))
+    grad = padded_rows(G, P, DEV)
+    grad.copy_(torch.randn(G, P, device=DEV) * 0.01)
+    grad[1] *= 1000  # exercises clipping
+    mask = (torch.rand(P, device=DEV) > 0.5).float()
+    ref = theta.clone()
+    from neuroimagedisttraining_amd.ops.reference import clip_sgd_mask_reference
+    clip_sgd_mask_reference(ref, grad.clone(), mask, 0.01, 5e-4)
+    ws = torch.empty(m.clip_sgd_mask_workspace(G, P), device=DEV)
+    m.clip_sgd_mask(theta.data_ptr(), grad.data_ptr(), 0, mask.data_ptr(), ws.data_ptr(), 0, 0, G, P, theta.stride(0),
+                    0.01, 5e-4, 0.0, 1, 10.0, _st())
+    torch.cuda.synchronize()
+    assert _relerr(theta, ref) < 1e-6
+
+
+def test_radix_select_matches_topk():
+    m = _m()
+    torch.manual_seed(5)
+    v = torch.rand(2568064, device=DEV) ** 3
+    v = v / v.sum()
+    k = int(v.numel() * 0.5)
+    st = torch.empty(4, dtype=torch.int32, device=DEV)
+    hist = torch.empty(256, dtype=torch.int32, device=DEV)
+    m.radix_select_kth(v.data_ptr(), v.numel(), k, st.data_ptr(), hist.data_ptr(), _st())
+    mask = torch.empty_like(v)
+    m.threshold_mask(v.data_ptr(), v.numel(), st.data_ptr(), mask.data_ptr(), _st())
+    thr = torch.topk(v, k, sorted=True).values[-1]
+    assert torch.equal(mask, (v >= thr).float())
+
+
+def test_weighted_rows_sum():
+    m = _m()
+    C, P = 5, 1000003
+    from neuroimagedisttraining_amd.engine.executor import padded_rows
+    rows = padded_rows(C, P, DEV)
+    rows.copy_(torch.randn(C, P, device=DEV))
+    w = torch.rand(C, device=DEV)
+    out = torch.empty(P, device=DEV)
+    m.weighted_rows_sum(rows.data_ptr(), w.data_ptr(), C, P, rows.stride(0), 0.0, out.data_ptr(), _st())
+    torch.cuda.synchronize()
+    assert _relerr(out, (w.view(-1, 1) * rows).sum(0)) < 1e-6
