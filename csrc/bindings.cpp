@@ -23,6 +23,7 @@ void conv3d_wgrad(uintptr_t x, uintptr_t xs, uintptr_t xt, uintptr_t dy, uintptr
 int conv3d_wgrad_nsplit(int G, int B, int D, int H, int W, int Cin, int Cout, int pad);
 void pack_conv_w(uintptr_t theta, int64_t ldt, int64_t off, int G, int Cout, int Cin, float scale, uintptr_t wp,
                  uintptr_t wt, uintptr_t stream);
+void bn_relu_apply(uintptr_t y, uintptr_t sc, uintptr_t sh, uintptr_t h, int64_t npos, int C, int S, uintptr_t stream);
 // bn.hip
 void bn_finalize(uintptr_t stats, int nPB, int BP, int Mg, int G, int C, uintptr_t theta, int64_t ldt, int64_t off_g,
                  int64_t off_b, uintptr_t bufs, int64_t ldb, int64_t off_rm, int64_t off_rv, int64_t off_nbt,
@@ -77,6 +78,7 @@ PYBIND11_MODULE(_nidt_hip, m) {
   DEF(conv3d_wgrad);
   DEF(conv3d_wgrad_nsplit);
   DEF(pack_conv_w);
+  DEF(bn_relu_apply);
   DEF(bn_finalize);
   DEF(bn_eval);
   DEF(bn_relu_pool);

@@ -405,14 +405,21 @@ void conv1_fwd_pool(uintptr_t x8, uintptr_t idx, uintptr_t w8, uintptr_t scale, 
 
 // ------------------------------------------------------------------------------------------------
 // Sparse wgrad: S[c][k] = sum over pooled voxels of dz * patch(argmax voxel), D[c] = sum dz.
-// Block = (n, pd); loops over ph; thread = (wave w, channel c = lane); wave w takes pw = w, w+4, ...
+// Block = (n, pd); thread = (wave w, channel c = lane).  The polyphase input halo is staged as raw uint8 (8 B per
+// voxel) for 4 pooled rows (ph) at a time.  Halo strides are padded so that the 27 possible argmax offsets
+// (aw + 3 ah + 9 ad voxels apart) fall on 27 distinct ds_read_b64 bank pairs: the 64 channel-lanes of a wave,
+// which read at their own argmax, never bank-conflict (identical addresses broadcast).
 // Output slab: part[n*19 + pd][64][126] (125 S entries + D).
+constexpr int kWgRows = 4;                       // pooled rows (ph) per stage
+constexpr int kWgHY = 3 * kWgRows + 2;           // halo y extent (14)
+constexpr int kWgRS = 67;                        // row stride in voxels   (67 = 3 mod 32)
+constexpr int kWgZS = 969;                       // plane stride in voxels (969 = 9 mod 32, >= 14*67)
+constexpr int kWgHalo = 5 * kWgZS;               // voxels per halo buffer
+
 __global__ __launch_bounds__(256) void k_conv1_wgrad(const uint8_t* __restrict__ x8, const int* __restrict__ idx,
                                                      const uint16_t* __restrict__ dp, const uint16_t* __restrict__ pout,
                                                      const uint8_t* __restrict__ amax, float* __restrict__ part) {
-  constexpr int HX = 64;
-  __shared__ __attribute__((aligned(16))) uint16_t halo[5 * 5 * HX * 8];
-  __shared__ float red[64][127];
+  __shared__ __attribute__((aligned(16))) uint2 halo[kWgHalo];
   const int pd = blockIdx.x, n = blockIdx.y;
   const int tid = threadIdx.x, c = tid & 63, wid = tid >> 6;
   const uint8_t* xs = x8 + (int64_t)idx[n] * kPZ * kPY * kPX * 8;
@@ -420,64 +427,63 @@ __global__ __launch_bounds__(256) void k_conv1_wgrad(const uint8_t* __restrict__
 #pragma unroll
   for (int k = 0; k < 125; ++k) S[k] = 0.f;
   float Dsum = 0.f;
-  for (int ph = 0; ph < kPH; ++ph) {
+  for (int ph0 = 0; ph0 < kPH; ph0 += kWgRows) {
+    const int nph = min(kWgRows, kPH - ph0);
+    const int ny = 3 * nph + 2;
     __syncthreads();
-    for (int e = tid; e < 5 * 5 * HX; e += 256) {
-      const int xh = e % HX, yz = e / HX, yh = yz % 5, zh = yz / 5;
-      const int z = 3 * pd + zh, y = 3 * ph + yh;
+    for (int e = tid; e < 5 * ny * 64; e += 256) {
+      const int xh = e & 63, r = e >> 6, yh = r % ny, zh = r / ny;
+      const int z = 3 * pd + zh, y = 3 * ph0 + yh;
       uint2 v = make_uint2(0, 0);
       if (xh < kPX) v = *reinterpret_cast<const uint2*>(xs + (((int64_t)z * kPY + y) * kPX + xh) * 8);
-      uint4 o;
-      o.x = (__float_as_uint((float)(v.x & 0xffu)) >> 16) | (__float_as_uint((float)((v.x >> 8) & 0xffu)) & 0xffff0000u);
-      o.y = (__float_as_uint((float)((v.x >> 16) & 0xffu)) >> 16) | (__float_as_uint((float)(v.x >> 24)) & 0xffff0000u);
-      o.z = (__float_as_uint((float)(v.y & 0xffu)) >> 16) | (__float_as_uint((float)((v.y >> 8) & 0xffu)) & 0xffff0000u);
-      o.w = (__float_as_uint((float)((v.y >> 16) & 0xffu)) >> 16) | (__float_as_uint((float)(v.y >> 24)) & 0xffff0000u);
-      *reinterpret_cast<uint4*>(&halo[e * 8]) = o;
+      halo[zh * kWgZS + yh * kWgRS + xh] = v;
     }
     __syncthreads();
-    for (int pw = wid; pw < kPW; pw += 4) {
-      const int64_t o = ((((int64_t)n * kPD + pd) * kPH + ph) * kPW + pw) * kC1 + c;
+    for (int it = wid; it < nph * kPW; it += 4) {
+      const int phl = it / kPW, pw = it - phl * kPW;
+      const int64_t o = ((((int64_t)n * kPD + pd) * kPH + ph0 + phl) * kPW + pw) * kC1 + c;
       const float pv = bf16_to_f32(pout[o]);
       const float dz = pv > 0.f ? bf16_to_f32(dp[o]) : 0.f;
       const int a = amax[o];
       const int ad = a / 9, ah = (a / 3) % 3, aw = a % 3;
-      const int base = ((ad * 5 + ah) * HX + 3 * pw + aw) * 8;
+      const uint2* base = halo + ad * kWgZS + (3 * phl + ah) * kWgRS + 3 * pw + aw;
       Dsum += dz;
 #pragma unroll
       for (int t = 0; t < 27; ++t) {
         const int jd = t / 9, jh = (t / 3) % 3, jw = t % 3;
-        const uint4 u = *reinterpret_cast<const uint4*>(&halo[base + ((jd * 5 + jh) * HX + jw) * 8]);
-        const uint32_t w4[4] = {u.x, u.y, u.z, u.w};
+        const uint2 u = base[jd * kWgZS + jh * kWgRS + jw];
 #pragma unroll
         for (int r = 0; r < 8; ++r) {
           if (tp_valid(t, r)) {
-            const uint32_t bits = (r & 1) ? (w4[r >> 1] & 0xffff0000u) : (w4[r >> 1] << 16);
-            S[tp_to_k(t, r)] = fmaf(dz, __uint_as_float(bits), S[tp_to_k(t, r)]);
+            const uint32_t w = r < 4 ? u.x : u.y;
+            const float xv = (float)((w >> (8 * (r & 3))) & 0xffu);
+            S[tp_to_k(t, r)] = fmaf(dz, xv, S[tp_to_k(t, r)]);
           }
         }
       }
     }
   }
-  // reduce the 4 waves (channel c owned by lane c of every wave) through one [64][127] LDS buffer
+  // reduce the 4 waves (channel c owned by lane c of every wave) through LDS (reusing the halo buffer)
+  float* red = reinterpret_cast<float*>(halo);  // [64][127] floats = 32.5 KB < halo
   for (int w = 1; w < 4; ++w) {
     __syncthreads();
     if (wid == w) {
 #pragma unroll
-      for (int k = 0; k < 125; ++k) red[c][k] = S[k];
-      red[c][125] = Dsum;
+      for (int k = 0; k < 125; ++k) red[c * 127 + k] = S[k];
+      red[c * 127 + 125] = Dsum;
     }
     __syncthreads();
     if (wid == 0) {
 #pragma unroll
-      for (int k = 0; k < 125; ++k) S[k] += red[c][k];
-      Dsum += red[c][125];
+      for (int k = 0; k < 125; ++k) S[k] += red[c * 127 + k];
+      Dsum += red[c * 127 + 125];
     }
   }
   if (wid == 0) {
-    float* o = part + (((int64_t)n * kPD + pd) * kC1 + c) * 126;
+    float* op = part + (((int64_t)n * kPD + pd) * kC1 + c) * 126;
 #pragma unroll
-    for (int k = 0; k < 125; ++k) o[k] = S[k];
-    o[125] = Dsum;
+    for (int k = 0; k < 125; ++k) op[k] = S[k];
+    op[125] = Dsum;
   }
 }
 

@@ -439,19 +439,25 @@ __global__ __launch_bounds__(256, 2) void k_conv_wgrad(ConvWgArgs a) {
   }
 }
 
-// sum the split slabs; write PyTorch layout grad[g][off + (co*Cin + ci)*27 + t] for k = t*Cin + ci (scaled)
-__global__ void k_wgrad_reduce(const float* __restrict__ part, int nsplit, int G, int Cout, int Cin, float* grad,
-                               int64_t ldg, int64_t off, float scale) {
+// sum the split slabs; write PyTorch layout grad[g][off + (co*Cin + ci)*27 + t] for k = t*Cin + ci (scaled).
+// Block = (co, g): the K-row is summed into LDS in k order, then written out in [ci][t] order (coalesced).
+__global__ __launch_bounds__(256) void k_wgrad_reduce(const float* __restrict__ part, int nsplit, int G, int Cout,
+                                                      int Cin, float* grad, int64_t ldg, int64_t off, float scale) {
+  __shared__ float row[27 * 192];
+  const int co = blockIdx.x, g = blockIdx.y;
   const int K = 27 * Cin;
   const int64_t tot = (int64_t)G * Cout * K;
-  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < tot; e += (int64_t)gridDim.x * blockDim.x) {
+  const float* src = part + ((int64_t)g * Cout + co) * K;
+  for (int k = threadIdx.x; k < K; k += 256) {
     float s = 0.f;
-    for (int sp = 0; sp < nsplit; ++sp) s += part[(int64_t)sp * tot + e];
-    const int g = (int)(e / ((int64_t)Cout * K));
-    const int rem = (int)(e - (int64_t)g * Cout * K);
-    const int co = rem / K, k = rem - co * K;
-    const int t = k / Cin, ci = k - t * Cin;
-    grad[(int64_t)g * ldg + off + ((int64_t)co * Cin + ci) * 27 + t] = s * scale;
+    for (int sp = 0; sp < nsplit; ++sp) s += src[(int64_t)sp * tot + k];
+    row[k] = s * scale;
+  }
+  __syncthreads();
+  float* dst = grad + (int64_t)g * ldg + off + (int64_t)co * K;
+  for (int e = threadIdx.x; e < K; e += 256) {
+    const int ci = e / 27, t = e - ci * 27;
+    dst[e] = row[t * Cin + ci];
   }
 }
 
@@ -483,34 +489,82 @@ void conv3d_wgrad(uintptr_t x, uintptr_t xs, uintptr_t xt, uintptr_t dy, uintptr
   if (xs) hipLaunchKernelGGL((k_conv_wgrad<true>), grid, dim3(256), 0, s, a);
   else hipLaunchKernelGGL((k_conv_wgrad<false>), grid, dim3(256), 0, s, a);
   NIDT_CHECK(hipGetLastError());
-  const int64_t tot = (int64_t)G * Cout * a.K;
-  hipLaunchKernelGGL(k_wgrad_reduce, dim3(std::min<int64_t>(4096, (tot + 255) / 256)), dim3(256), 0, s,
-                     ptr<const float>(part), nsplit, G, Cout, Cin, ptr<float>(grad), ldg, off, scale);
+  hipLaunchKernelGGL(k_wgrad_reduce, dim3(Cout, G), dim3(256), 0, s, ptr<const float>(part), nsplit, G, Cout, Cin,
+                     ptr<float>(grad), ldg, off, scale);
   NIDT_CHECK(hipGetLastError());
 }
 
 // ------------------------------------------------------------------------------------------------
 // Pack fp32 PyTorch-layout weights [Cout][Cin][27] (row g of theta at offset off) into
-// wp [G][Cout][27][Cin] bf16 and (optionally) wt [G][Cin][27][Cout] bf16 with the taps flipped (dgrad).
-__global__ void k_pack_conv_w(const float* __restrict__ theta, int64_t ldt, int64_t off, int G, int Cout, int Cin,
-                              float scale, uint16_t* __restrict__ wp, uint16_t* __restrict__ wt) {
-  const int64_t per = (int64_t)Cout * Cin * 27;
-  const int64_t tot = per * G;
-  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < tot; e += (int64_t)gridDim.x * blockDim.x) {
-    const int g = (int)(e / per);
-    const int rem = (int)(e - (int64_t)g * per);
-    const int co = rem / (Cin * 27), r2 = rem - co * Cin * 27, ci = r2 / 27, t = r2 - ci * 27;
-    const uint16_t v = f32_to_bf16(theta[(int64_t)g * ldt + off + rem] * scale);
-    wp[(((int64_t)g * Cout + co) * 27 + t) * Cin + ci] = v;
-    if (wt) wt[(((int64_t)g * Cin + ci) * 27 + (26 - t)) * Cout + co] = v;
+// wp [G][Cout][27][Cin] bf16 (block per (co, g): coalesced read of the [Cin][27] row, LDS transpose) and, for dgrad,
+// wt [G][Cin][27][Cout] with the taps flipped (64x64 LDS-tiled transpose of wp per tap).
+__global__ __launch_bounds__(256) void k_pack_wp(const float* __restrict__ theta, int64_t ldt, int64_t off, int Cout,
+                                                 int Cin, float scale, uint16_t* __restrict__ wp) {
+  __shared__ float row[27 * 192];
+  const int co = blockIdx.x, g = blockIdx.y;
+  const int K = 27 * Cin;
+  const float* src = theta + (int64_t)g * ldt + off + (int64_t)co * K;
+  for (int e = threadIdx.x; e < K; e += 256) row[e] = src[e];
+  __syncthreads();
+  uint16_t* dst = wp + ((int64_t)g * Cout + co) * K;
+  for (int e = threadIdx.x; e < K; e += 256) {
+    const int t = e / Cin, ci = e - t * Cin;
+    dst[e] = f32_to_bf16(row[ci * 27 + t] * scale);
+  }
+}
+
+__global__ __launch_bounds__(256) void k_pack_wt(const uint16_t* __restrict__ wp, int Cout, int Cin,
+                                                 uint16_t* __restrict__ wt) {
+  __shared__ uint16_t tile[64][66];
+  const int ci0 = blockIdx.x * 64, co0 = blockIdx.y * 64;
+  const int g = blockIdx.z / 27, t = blockIdx.z - g * 27;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  for (int r = ty; r < 64; r += 4) {  // r = co offset, tx = ci offset
+    const int co = co0 + r, ci = ci0 + tx;
+    tile[r][tx] = (co < Cout && ci < Cin) ? wp[(((int64_t)g * Cout + co) * 27 + t) * Cin + ci] : 0;
+  }
+  __syncthreads();
+  for (int r = ty; r < 64; r += 4) {  // r = ci offset, tx = co offset
+    const int ci = ci0 + r, co = co0 + tx;
+    if (ci < Cin && co < Cout) wt[(((int64_t)g * Cin + ci) * 27 + (26 - t)) * Cout + co] = tile[tx][r];
   }
 }
 
 void pack_conv_w(uintptr_t theta, int64_t ldt, int64_t off, int G, int Cout, int Cin, float scale, uintptr_t wp,
                  uintptr_t wt, uintptr_t stream) {
-  const int64_t tot = (int64_t)G * Cout * Cin * 27;
-  hipLaunchKernelGGL(k_pack_conv_w, dim3(std::min<int64_t>(8192, (tot + 255) / 256)), dim3(256), 0, as_stream(stream),
-                     ptr<const float>(theta), ldt, off, G, Cout, Cin, scale, ptr<uint16_t>(wp), ptr<uint16_t>(wt));
+  NIDT_REQUIRE(Cin <= 192, "pack_conv_w: Cin <= 192");
+  hipStream_t s = as_stream(stream);
+  hipLaunchKernelGGL(k_pack_wp, dim3(Cout, G), dim3(256), 0, s, ptr<const float>(theta), ldt, off, Cout, Cin, scale,
+                     ptr<uint16_t>(wp));
+  NIDT_CHECK(hipGetLastError());
+  if (wt) {
+    hipLaunchKernelGGL(k_pack_wt, dim3(ceil_div(Cin, 64), ceil_div(Cout, 64), G * 27), dim3(256), 0, s,
+                       ptr<const uint16_t>(wp), Cout, Cin, ptr<uint16_t>(wt));
+    NIDT_CHECK(hipGetLastError());
+  }
+}
+
+// h = relu(y * s + t) in bf16 (materialises BN+ReLU once so the consuming conv and its wgrad read it plain)
+__global__ void k_bn_relu_apply(const uint16_t* __restrict__ y, const float* __restrict__ sc,
+                                const float* __restrict__ sh, uint16_t* __restrict__ h, int64_t npos, int C, int S) {
+  const int C8 = C / 8;
+  const int64_t tot = npos * C8;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < tot; e += (int64_t)gridDim.x * blockDim.x) {
+    const int cg = (int)(e % C8);
+    const int64_t pos = e / C8;
+    const int g = (int)(pos / S);
+    const uint4 v = *reinterpret_cast<const uint4*>(y + pos * C + cg * 8);
+    *reinterpret_cast<uint4*>(h + pos * C + cg * 8) = xform8(v, sc + (int64_t)g * C + cg * 8, sh + (int64_t)g * C + cg * 8, true);
+  }
+}
+
+// y: [G*B*S_per_sample positions][C]; S = positions per client (B * D*H*W)
+void bn_relu_apply(uintptr_t y, uintptr_t sc, uintptr_t sh, uintptr_t h, int64_t npos, int C, int S, uintptr_t stream) {
+  NIDT_REQUIRE(C % 8 == 0, "bn_relu_apply: C % 8");
+  const int64_t tot = npos * (C / 8);
+  hipLaunchKernelGGL(k_bn_relu_apply, dim3((unsigned)std::min<int64_t>(16384, (tot + 255) / 256)), dim3(256), 0,
+                     as_stream(stream), ptr<const uint16_t>(y), ptr<const float>(sc), ptr<const float>(sh),
+                     ptr<uint16_t>(h), npos, C, S);
   NIDT_CHECK(hipGetLastError());
 }
 

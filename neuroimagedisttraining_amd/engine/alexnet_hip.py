@@ -59,6 +59,7 @@ class HipAlexNet3D:
             p1=e(NB, 19, 23, 19, 64), a1=e(NB, 19, 23, 19, 64, dt=u8),
             y2=e(NB, 17, 21, 17, 128), p2=e(NB, 5, 7, 5, 128), a2=e(NB, 5, 7, 5, 128, dt=u8),
             y3=e(NB, 5, 7, 5, 192), y4=e(NB, 5, 7, 5, 192), y5=e(NB, 5, 7, 5, 128),
+            h3=e(NB, 5, 7, 5, 192), h4=e(NB, 5, 7, 5, 192),
             p5=e(NB, 1, 2, 1, 128), a5=e(NB, 1, 2, 1, 128, dt=u8),
             logits=e(NB, dt=f32), loss=e(G, dt=f32),
         )
@@ -149,12 +150,15 @@ class HipAlexNet3D:
         m.conv3d_fwd(_p(b["p2"]), _p(b["w8p"]), _p(b["bias8"]), 0, 0, _p(b["y3"]), _p(b["st8"]) if train else 0,
                      G, B, 5, 7, 5, 128, 192, 1, st)
         self._bn(8, 9, 192, G, B, (5, 7, 5), theta, bufs, b, train)
-        # ---- conv4 (input = relu(bn3(y3)) applied in the loader) ----
-        m.conv3d_fwd(_p(b["y3"]), _p(b["w11p"]), _p(b["bias11"]), _p(b["s8"]), _p(b["t8"]), _p(b["y4"]),
+        # BN3+ReLU materialised once (read by conv4 fwd and by conv4's wgrad im2col 27x)
+        m.bn_relu_apply(_p(b["y3"]), _p(b["s8"]), _p(b["t8"]), _p(b["h3"]), NB * 175, 192, B * 175, st)
+        # ---- conv4 ----
+        m.conv3d_fwd(_p(b["h3"]), _p(b["w11p"]), _p(b["bias11"]), 0, 0, _p(b["y4"]),
                      _p(b["st11"]) if train else 0, G, B, 5, 7, 5, 192, 192, 1, st)
         self._bn(11, 12, 192, G, B, (5, 7, 5), theta, bufs, b, train)
-        # ---- conv5 (input = relu(bn4(y4))) + BN5 + ReLU + pool ----
-        m.conv3d_fwd(_p(b["y4"]), _p(b["w14p"]), _p(b["bias14"]), _p(b["s11"]), _p(b["t11"]), _p(b["y5"]),
+        m.bn_relu_apply(_p(b["y4"]), _p(b["s11"]), _p(b["t11"]), _p(b["h4"]), NB * 175, 192, B * 175, st)
+        # ---- conv5 + BN5 + ReLU + pool ----
+        m.conv3d_fwd(_p(b["h4"]), _p(b["w14p"]), _p(b["bias14"]), 0, 0, _p(b["y5"]),
                      _p(b["st14"]) if train else 0, G, B, 5, 7, 5, 192, 128, 1, st)
         self._bn(14, 15, 128, G, B, (5, 7, 5), theta, bufs, b, train)
         m.bn_relu_pool(_p(b["y5"]), _p(b["s14"]), _p(b["t14"]), _p(b["p5"]), _p(b["a5"]), NB, B, 5, 7, 5, 128, st)
@@ -188,11 +192,11 @@ class HipAlexNet3D:
 
         # layer 5: pool5 -> BN5 -> conv5
         bn_bwd(1, 14, 15, 128, (5, 7, 5), b["dp5"], b["p5"], b["a5"], b["dy5"], b["y5"])
-        wgrad(14, b["y4"], b["s11"], b["t11"], b["dy5"], (5, 7, 5), 192, 128, 1)
+        wgrad(14, b["h4"], None, None, b["dy5"], (5, 7, 5), 192, 128, 1)
         m.conv3d_fwd(_p(b["dy5"]), _p(b["w14t"]), 0, 0, 0, _p(b["dx5"]), 0, G, B, 5, 7, 5, 128, 192, 1, st)
         # layer 4
         bn_bwd(0, 11, 12, 192, (5, 7, 5), b["dx5"], None, None, b["dy4"], b["y4"])
-        wgrad(11, b["y3"], b["s8"], b["t8"], b["dy4"], (5, 7, 5), 192, 192, 1)
+        wgrad(11, b["h3"], None, None, b["dy4"], (5, 7, 5), 192, 192, 1)
         m.conv3d_fwd(_p(b["dy4"]), _p(b["w11t"]), 0, 0, 0, _p(b["dx4"]), 0, G, B, 5, 7, 5, 192, 192, 1, st)
         # layer 3
         bn_bwd(0, 8, 9, 192, (5, 7, 5), b["dx4"], None, None, b["dy3"], b["y3"])
