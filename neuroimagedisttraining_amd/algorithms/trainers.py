@@ -101,19 +101,24 @@ class VolumeTrainer(_TrainerBase):
     def _criterion(self, logits):
         return nn.BCEWithLogitsLoss() if (logits.dim() == 2 and logits.shape[1] == 1) else nn.CrossEntropyLoss()
 
-    def train(self, train_data, device, args, round_idx=0, masks=None, prox_ref=None):
+    def train(self, train_data, device, args, round_idx=0, masks=None, prox_ref=None, mask_mode="weight",
+              epoch_hook=None, epochs=None, prox_lamda=None):
+        """``mask_mode``: "weight" multiplies weights by the mask after each step (SalientGrads / DisPFL),
+        "grad" multiplies gradients before the step (SubAvg).  ``epoch_hook(epoch)`` runs after every epoch.
+        ``prox_lamda`` + ``prox_ref``: Ditto's proximal pull w -= lr*lamda*(w - w_ref) after each step."""
         model = self.model
         model.to(device)
         model.train()
         opt = self._optimizer(args, round_idx)
-        use_mask = masks is not None and bool(getattr(args, "snip_mask", True))
+        use_mask = masks is not None and (mask_mode != "weight" or bool(getattr(args, "snip_mask", True)))
         dev_masks = None
         if use_mask:
             dev_masks = {n: masks[n].to(device) for n, _ in model.named_parameters() if n in masks}
         mu = float(getattr(args, "fedprox_mu", 0.0) or 0.0)
         named = dict(model.named_parameters())
         epoch_losses = []
-        for epoch in range(args.epochs):
+        lr_now = opt.param_groups[0]["lr"]
+        for epoch in range(args.epochs if epochs is None else epochs):
             losses = []
             for batch in train_data:
                 x, y = self._xy(batch, train_data, device)
@@ -128,10 +133,20 @@ class VolumeTrainer(_TrainerBase):
                     prox = sum(((named[k] - prox_ref[k].to(device)) ** 2).sum() for k in named if k in prox_ref)
                     loss = loss + 0.5 * mu * prox
                 loss.backward()
+                if use_mask and mask_mode == "grad":
+                    for n, p in named.items():
+                        m = dev_masks.get(n)
+                        if m is not None and p.grad is not None:
+                            p.grad.mul_(m)
                 torch.nn.utils.clip_grad_norm_(model.parameters(), 10)
                 opt.step()
                 losses.append(loss.detach())
-                if use_mask:
+                if prox_lamda is not None and prox_ref is not None:
+                    with torch.no_grad():
+                        for n, p in named.items():
+                            if n in prox_ref:
+                                p.sub_(lr_now * prox_lamda * (p - prox_ref[n].to(p.device)))
+                if use_mask and mask_mode == "weight":
                     with torch.no_grad():
                         for n, p in named.items():
                             m = dev_masks.get(n)
@@ -140,7 +155,23 @@ class VolumeTrainer(_TrainerBase):
             ep = torch.stack(losses).mean().item() if losses else float("nan")
             epoch_losses.append(ep)
             self.logger.info("Client Index = %s\tEpoch: %d\tLoss: %.6f", self.id, epoch, ep)
+            if epoch_hook is not None:
+                epoch_hook(epoch)
         return epoch_losses
+
+    def screen_gradients(self, train_data, device):
+        """Full (unmasked) gradient on one batch, model in eval mode (``DisPFL/my_model_trainer.py:166-189``)."""
+        model = self.model
+        model.to(device)
+        model.eval()
+        model.zero_grad()
+        batch = next(iter(train_data))
+        x, y = self._xy(batch, train_data, device)
+        out = model(x)
+        out = out[0] if isinstance(out, (list, tuple)) else out
+        logits, t = self._loss_targets(out.float(), y)
+        self._criterion(logits)(logits, t).backward()
+        return {n: p.grad.detach().clone() for n, p in model.named_parameters() if p.grad is not None}
 
     @torch.no_grad()
     def test(self, test_data, device, args):

@@ -1,0 +1,256 @@
+"""Communication backends and the server/client manager skeleton (reference
+``fedml_core/distributed/{communication/{mpi,gRPC,mqtt},server/server_manager.py,client/client_manager.py}``).
+
+Backends (``backend=`` of the managers):
+
+* ``"INPROC"`` — queues inside one process (threads or sequential simulation); zero dependencies.
+* ``"TORCH"`` — control messages between ``torch.distributed`` ranks (the one-process-per-GPU runtime); JSON
+  payload shipped as a uint8 tensor via point-to-point send/recv on the gloo group (RCCL carries the bulk
+  tensors through collectives, not through messages).
+* ``"GRPC"`` — a real gRPC server per rank (``grpcio`` generic unary handler, 100 MB messages, port
+  ``base_port + rank``, peers from an ``ip_config`` CSV ``receiver_id,ip``) — the reference's backend without
+  generated stubs, and importable (the reference's is not, quirk Q17).
+* ``"MPI"`` / ``"MQTT"`` — need ``mpi4py`` / ``paho-mqtt``; they raise a clear ImportError when absent.
+
+The receive loop is event driven (blocking queue get with timeout) rather than the reference's 0.3 s polling.
+"""
+from __future__ import annotations
+
+import csv
+import logging
+import queue
+import threading
+
+import torch
+
+from .message import BaseCommunicationManager, Message, Observer
+
+log = logging.getLogger(__name__)
+
+
+class _Hub:
+    """Process-local mailbox registry for the INPROC backend."""
+    _boxes = {}
+    _lock = threading.Lock()
+
+    @classmethod
+    def box(cls, world, rank):
+        with cls._lock:
+            return cls._boxes.setdefault((world, rank), queue.Queue())
+
+    @classmethod
+    def reset(cls, world=None):
+        with cls._lock:
+            for k in list(cls._boxes):
+                if world is None or k[0] == world:
+                    del cls._boxes[k]
+
+
+class _QueueCommManager(BaseCommunicationManager):
+    def __init__(self):
+        self._observers = []
+        self._running = False
+        self.q = queue.Queue()
+
+    def add_observer(self, observer: Observer):
+        self._observers.append(observer)
+
+    def remove_observer(self, observer: Observer):
+        self._observers.remove(observer)
+
+    def _notify(self, msg: Message):
+        for o in list(self._observers):
+            o.receive_message(msg.get_type(), msg)
+
+    def poll_once(self, timeout=0.0):
+        """Deliver at most one pending message (for sequential simulation); returns True if one was handled."""
+        try:
+            msg = self.q.get(timeout=timeout) if timeout else self.q.get_nowait()
+        except queue.Empty:
+            return False
+        self._notify(msg)
+        return True
+
+    def handle_receive_message(self):
+        self._running = True
+        while self._running:
+            self.poll_once(timeout=0.05)
+
+    def stop_receive_message(self):
+        self._running = False
+
+
+class InProcCommManager(_QueueCommManager):
+    def __init__(self, rank, size, world="default"):
+        super().__init__()
+        self.rank, self.size, self.world = rank, size, world
+        self.q = _Hub.box(world, rank)
+
+    def send_message(self, msg: Message):
+        _Hub.box(self.world, msg.get_receiver_id()).put(msg)
+
+
+class TorchDistCommManager(_QueueCommManager):
+    """Control messages over torch.distributed point-to-point (gloo group)."""
+
+    def __init__(self, rank, size, group=None):
+        super().__init__()
+        import torch.distributed as dist
+        self.dist = dist
+        self.rank, self.size = rank, size
+        self.group = group
+        self._stop = threading.Event()
+        self._rx = threading.Thread(target=self._recv_loop, daemon=True)
+        self._rx.start()
+
+    def send_message(self, msg: Message):
+        data = torch.frombuffer(bytearray(msg.to_json().encode()), dtype=torch.uint8)
+        n = torch.tensor([data.numel()], dtype=torch.int64)
+        self.dist.send(n, dst=msg.get_receiver_id(), group=self.group)
+        self.dist.send(data, dst=msg.get_receiver_id(), group=self.group)
+
+    def _recv_loop(self):
+        while not self._stop.is_set():
+            n = torch.zeros(1, dtype=torch.int64)
+            src = self.dist.recv(n, group=self.group)
+            if int(n.item()) < 0:
+                break
+            buf = torch.empty(int(n.item()), dtype=torch.uint8)
+            self.dist.recv(buf, src=src, group=self.group)
+            m = Message()
+            m.init_from_json_string(bytes(buf.tolist()).decode())
+            self.q.put(m)
+
+    def stop_receive_message(self):
+        super().stop_receive_message()
+        self._stop.set()
+
+
+class GRPCCommManager(_QueueCommManager):
+    """gRPC backend: every rank serves ``/nidt.Comm/sendMessage`` (bytes in, bytes out)."""
+
+    MAX_MSG = 100 * 1024 * 1024
+
+    def __init__(self, host, port, ip_config_path=None, topic="fedml", client_id=0, client_num=0, base_port=50000):
+        super().__init__()
+        import grpc
+        from concurrent import futures
+        self.grpc = grpc
+        self.client_id = client_id
+        self.base_port = base_port
+        self.ip_config = self._read_ip_config(ip_config_path) if ip_config_path else {}
+        opts = [("grpc.max_send_message_length", self.MAX_MSG), ("grpc.max_receive_message_length", self.MAX_MSG)]
+        self.server = grpc.server(futures.ThreadPoolExecutor(max_workers=4), options=opts)
+
+        def handle(request, context):
+            m = Message()
+            m.init_from_json_string(request.decode())
+            self.q.put(m)
+            return b"ok"
+
+        handler = grpc.method_handlers_generic_handler(
+            "nidt.Comm", {"sendMessage": grpc.unary_unary_rpc_method_handler(handle)})
+        self.server.add_generic_rpc_handlers((handler,))
+        self.port = port or (base_port + client_id)
+        self.server.add_insecure_port("%s:%d" % (host, self.port))
+        self.server.start()
+        self.opts = opts
+
+    @staticmethod
+    def _read_ip_config(path):
+        out = {}
+        with open(path) as f:
+            for row in csv.reader(f):
+                if row and row[0].strip().isdigit():
+                    out[int(row[0])] = row[1].strip()
+        return out
+
+    def send_message(self, msg: Message):
+        rid = msg.get_receiver_id()
+        ip = self.ip_config.get(rid, "127.0.0.1")
+        with self.grpc.insecure_channel("%s:%d" % (ip, self.base_port + rid), options=self.opts) as ch:
+            call = ch.unary_unary("/nidt.Comm/sendMessage")
+            call(msg.to_json().encode(), timeout=60)
+
+    def stop_receive_message(self):
+        super().stop_receive_message()
+        self.server.stop(0)
+
+
+def MpiCommunicationManager(*a, **k):  # noqa: N802 (reference class name)
+    try:
+        import mpi4py  # noqa: F401
+    except ImportError as e:
+        raise ImportError("the MPI backend needs mpi4py (not installed); use backend='TORCH' or 'INPROC'") from e
+    raise NotImplementedError("MPI backend: use backend='TORCH' (torch.distributed) on MI355X nodes")
+
+
+def MqttCommManager(*a, **k):  # noqa: N802
+    try:
+        import paho.mqtt.client  # noqa: F401
+    except ImportError as e:
+        raise ImportError("the MQTT backend needs paho-mqtt (not installed); use backend='GRPC' or 'TORCH'") from e
+    raise NotImplementedError("MQTT backend not provided; use backend='GRPC'")
+
+
+def make_comm_manager(backend, rank, size, **kw):
+    backend = (backend or "INPROC").upper()
+    if backend == "INPROC":
+        return InProcCommManager(rank, size, kw.get("world", "default"))
+    if backend == "TORCH":
+        return TorchDistCommManager(rank, size, kw.get("group"))
+    if backend == "GRPC":
+        return GRPCCommManager(kw.get("host", "0.0.0.0"), kw.get("port"), kw.get("ip_config_path"),
+                               client_id=rank, client_num=size, base_port=kw.get("base_port", 50000))
+    if backend == "MPI":
+        return MpiCommunicationManager(kw.get("comm"), rank, size)
+    if backend == "MQTT":
+        return MqttCommManager(kw.get("host"), kw.get("port"), client_id=rank, client_num=size)
+    raise ValueError("unknown backend %r" % backend)
+
+
+class _Manager(Observer):
+    def __init__(self, args, comm=None, rank=0, size=0, backend="INPROC", **kw):
+        self.args = args
+        self.rank = rank
+        self.size = size
+        self.backend = backend
+        self.com_manager = comm if isinstance(comm, BaseCommunicationManager) else \
+            make_comm_manager(backend, rank, size, **kw)
+        self.com_manager.add_observer(self)
+        self.message_handler_dict = {}
+
+    def run(self):
+        self.register_message_receive_handlers()
+        self.com_manager.handle_receive_message()
+
+    def get_sender_id(self):
+        return self.rank
+
+    def receive_message(self, msg_type, msg_params) -> None:
+        handler = self.message_handler_dict.get(msg_type)
+        if handler is None:
+            log.warning("no handler for message type %r", msg_type)
+            return
+        handler(msg_params)
+
+    def send_message(self, message):
+        self.com_manager.send_message(message)
+
+    def register_message_receive_handler(self, msg_type, handler_callback_func):
+        self.message_handler_dict[msg_type] = handler_callback_func
+
+    def register_message_receive_handlers(self) -> None:
+        """Subclasses register their handlers here."""
+
+    def finish(self):
+        """Stop this manager's receive loop (the reference aborts the whole MPI job instead)."""
+        self.com_manager.stop_receive_message()
+
+
+class ServerManager(_Manager):
+    pass
+
+
+class ClientManager(_Manager):
+    pass

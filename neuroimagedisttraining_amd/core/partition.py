@@ -62,7 +62,17 @@ def _sequential_prior_draw(labels, n_clients, priors, n_cls, rng, exhausted):
         quota[c] -= 1
         remaining -= 1
         row = cdf[c]
+        tries = 0
         while True:
+            tries += 1
+            if tries > 1000 and exhausted == "redraw":
+                # The reference redraws forever when a client's prior has (numerically) no mass left on any
+                # class with remaining samples; after 1000 misses draw from the prior restricted to
+                # non-exhausted classes instead (identical behaviour whenever the reference terminates quickly).
+                pr = priors[c] * (left > 0)
+                pr = pr / pr.sum() if pr.sum() > 0 else (left > 0) / max(1, int((left > 0).sum()))
+                row = np.cumsum(pr)
+                tries = -10 ** 9
             k = int(np.argmax(rng.uniform() <= row))
             if left[k] <= 0:
                 if exhausted == "random_refill":

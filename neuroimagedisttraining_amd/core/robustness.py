@@ -122,6 +122,9 @@ def robust_aggregate(kind, w_locals, f=0, trim_ratio=0.1):
         v = coordinate_median(M)
     elif kind == "trimmed_mean":
         v = trimmed_mean(M, trim_ratio)
+    elif kind == "fedavg":
+        n = torch.tensor([float(k) for k, _ in w_locals], dtype=M.dtype, device=M.device)
+        v = (n / n.sum()) @ M
     else:
         raise ValueError("unknown aggregator %r" % kind)
     return unstack_vector(v, shapes)

@@ -1,0 +1,152 @@
+"""CIFAR-10 / CIFAR-100 / Tiny-ImageNet / tabular federated loaders (reference
+``fedml_api/data_preprocessing/{cifar10,cifar100,tiny_imagenet}/{data_loader,data_val_loader}.py``).
+
+There is no network and no dataset files in this environment, so each loader builds a synthetic dataset of the
+real shape and class count (class-conditional smooth patterns + noise, learnable), unless ``data_dir`` holds an
+``.npz`` with ``x_train, y_train, x_test, y_test`` (loaded with ``allow_pickle=False``).  Partitioning and the
+per-client test / validation construction follow the reference exactly:
+
+* train split: ``partition_method`` in {dir, n_cls, my_part, homo, hetero};
+* per-client test set: for each class ``c``, ``ceil(train_count_c / train_total * ceil(|test| / C))`` random
+  test indices of class c (test sets overlap across clients);
+* val loaders (9-tuple): 10 % of *client 0's* size sampled from each client's train indices.
+
+Every loader returns the reference's 8-tuple ``[None, None, None, None, train_num_dict, train_dict, test_dict,
+class_num]`` (val variant: + ``val_dict``).
+"""
+from __future__ import annotations
+
+import logging
+import math
+import os
+
+import numpy as np
+import torch
+from torch.utils.data import DataLoader, TensorDataset
+
+from ..core import partition as P
+
+log = logging.getLogger(__name__)
+
+SPECS = {"cifar10": ((3, 32, 32), 10, 50000, 10000), "cifar100": ((3, 32, 32), 100, 50000, 10000),
+         "tiny": ((3, 64, 64), 200, 100000, 10000), "mnist": ((1, 28, 28), 10, 60000, 10000),
+         "emnist": ((1, 28, 28), 62, 60000, 10000)}
+
+
+def synthetic_images(n, shape, n_cls, seed=0, noise=0.6):
+    """Class-conditional images: a random low-frequency template per class + per-sample noise."""
+    g = torch.Generator().manual_seed(seed)
+    c, h, w = shape
+    coarse = torch.randn(n_cls, c, max(2, h // 8), max(2, w // 8), generator=g)
+    templ = torch.nn.functional.interpolate(coarse, size=(h, w), mode="bilinear", align_corners=False)
+    y = torch.randint(0, n_cls, (n,), generator=g)
+    x = templ[y] + noise * torch.randn(n, c, h, w, generator=g)
+    return x.float(), y.long()
+
+
+def _load_arrays(dataset, data_dir, n_train=None, n_test=None, seed=0):
+    shape, n_cls, ntr, nte = SPECS[dataset]
+    if data_dir and os.path.isfile(data_dir) and data_dir.endswith(".npz"):
+        d = np.load(data_dir, allow_pickle=False)
+        return (torch.from_numpy(d["x_train"]).float(), torch.from_numpy(d["y_train"]).long(),
+                torch.from_numpy(d["x_test"]).float(), torch.from_numpy(d["y_test"]).long(), n_cls)
+    ntr = n_train or ntr
+    nte = n_test or nte
+    xtr, ytr = synthetic_images(ntr, shape, n_cls, seed)
+    xte, yte = synthetic_images(nte, shape, n_cls, seed + 1)
+    log.info("%s: no data files, using synthetic %s images (%d train / %d test)", dataset, shape, ntr, nte)
+    return xtr, ytr, xte, yte, n_cls
+
+
+def _loader(x, y, idx, bs, shuffle):
+    idx = torch.as_tensor(np.asarray(idx, dtype=np.int64))
+    return DataLoader(TensorDataset(x[idx], y[idx]), batch_size=bs, shuffle=shuffle, drop_last=False)
+
+
+def partition_data(y_train, partition, n_clients, alpha, n_cls, rng=None):
+    return P.partition_labels(partition, np.asarray(y_train), n_clients, alpha, n_cls=n_cls, rng=rng)
+
+
+def load_partition_data(dataset, data_dir, partition_method, partition_alpha, client_number, batch_size,
+                        logger=None, n_train=None, n_test=None, seed=0, with_val=False):
+    logger = logger or log
+    xtr, ytr, xte, yte, n_cls = _load_arrays(dataset, data_dir, n_train, n_test, seed)
+    rng = np.random.RandomState(seed)
+    train_map = partition_data(ytr.numpy(), partition_method, client_number, partition_alpha, n_cls, rng)
+    test_map = P.per_client_test_indices(ytr.numpy(), yte.numpy(), train_map, n_cls=n_cls, rng=rng)
+    val_map = {}
+    if with_val:
+        nval = int(0.1 * len(train_map[0]))
+        for c in range(client_number):
+            ix = np.asarray(train_map[c])
+            pick = rng.choice(len(ix), min(nval, len(ix)), replace=False)
+            val_map[c] = ix[pick]
+            train_map[c] = np.delete(ix, pick)
+    num, trn, tst, val = {}, {}, {}, {}
+    for c in range(client_number):
+        num[c] = len(train_map[c])
+        trn[c] = _loader(xtr, ytr, train_map[c], batch_size, True)
+        tst[c] = _loader(xte, yte, test_map[c], batch_size, False)
+        if with_val:
+            val[c] = _loader(xtr, ytr, val_map[c], batch_size, False)
+        logger.info("client_idx = %d, local_train_sample_number = %d", c, num[c])
+    out = [None, None, None, None, num, trn, tst, n_cls]
+    return out + [val] if with_val else out
+
+
+def load_partition_data_cifar10(data_dir, partition_method, partition_alpha, client_number, batch_size, logger=None,
+                                **kw):
+    return load_partition_data("cifar10", data_dir, partition_method, partition_alpha, client_number, batch_size,
+                               logger, **kw)
+
+
+def load_partition_data_cifar100(data_dir, partition_method, partition_alpha, client_number, batch_size,
+                                 logger=None, **kw):
+    return load_partition_data("cifar100", data_dir, partition_method, partition_alpha, client_number, batch_size,
+                               logger, **kw)
+
+
+def load_partition_data_tiny(data_dir, partition_method, partition_alpha, client_number, batch_size, logger=None,
+                             **kw):
+    return load_partition_data("tiny", data_dir, partition_method, partition_alpha, client_number, batch_size,
+                               logger, **kw)
+
+
+def load_partition_data_with_val(dataset, data_dir, partition_method, partition_alpha, client_number, batch_size,
+                                 logger=None, **kw):
+    return load_partition_data(dataset, data_dir, partition_method, partition_alpha, client_number, batch_size,
+                               logger, with_val=True, **kw)
+
+
+# ------------------------------------------------------------------------------------------------ tabular
+def synthetic_tabular(n_clients=2, n_per_client=500, dim=60, n_cls=10, alpha=1.0, beta=1.0, seed=0):
+    """FedProx-style synthetic(alpha, beta) non-IID tabular data: client-specific model and feature shift."""
+    rs = np.random.RandomState(seed)
+    xs, ys = [], []
+    for c in range(n_clients):
+        u = rs.normal(0, alpha)
+        b = rs.normal(0, beta)
+        W = rs.normal(u, 1, (dim, n_cls))
+        bias = rs.normal(u, 1, n_cls)
+        v = rs.normal(b, 1, dim)
+        cov = np.diag(np.power(np.arange(1, dim + 1, dtype=np.float64), -1.2))
+        x = rs.multivariate_normal(v, cov, n_per_client)
+        y = np.argmax(x @ W + bias, 1)
+        xs.append(x.astype(np.float32))
+        ys.append(y.astype(np.int64))
+    return xs, ys
+
+
+def load_partition_data_synthetic_tabular(client_number=2, batch_size=32, n_per_client=500, dim=60, n_cls=10,
+                                          alpha=1.0, beta=1.0, seed=0, test_ratio=0.2):
+    xs, ys = synthetic_tabular(client_number, n_per_client, dim, n_cls, alpha, beta, seed)
+    num, trn, tst = {}, {}, {}
+    for c in range(client_number):
+        n = len(ys[c])
+        nt = int(math.floor(n * test_ratio))
+        x = torch.from_numpy(xs[c])
+        y = torch.from_numpy(ys[c])
+        num[c] = n - nt
+        trn[c] = DataLoader(TensorDataset(x[nt:], y[nt:]), batch_size=batch_size, shuffle=True)
+        tst[c] = DataLoader(TensorDataset(x[:nt], y[:nt]), batch_size=batch_size, shuffle=False)
+    return [None, None, None, None, num, trn, tst, n_cls]

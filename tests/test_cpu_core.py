@@ -1,0 +1,187 @@
+"""CPU unit tests: partitioners, robust aggregation, messages/backends, topologies, secure aggregation, FLOPs."""
+import json
+
+import numpy as np
+import pytest
+import torch
+
+from neuroimagedisttraining_amd.core import partition as P
+from neuroimagedisttraining_amd.core import robustness as RB
+from neuroimagedisttraining_amd.comm import (InProcCommManager, Message, ServerManager, ClientManager,
+                                             SymmetricTopologyManager, AsymmetricTopologyManager, mixing_matrix)
+from neuroimagedisttraining_amd.algorithms import turboaggregate as TA
+from neuroimagedisttraining_amd.algorithms import sparse as SP
+
+
+def _labels(n=2000, c=10, seed=0):
+    return np.random.RandomState(seed).randint(0, c, n)
+
+
+@pytest.mark.parametrize("method", ["dir", "n_cls", "my_part", "hetero"])
+def test_partitioners_cover_and_quota(method):
+    y = _labels()
+    rs = np.random.RandomState(1)
+    m = P.partition_labels(method, y, 10, 0.3 if method != "n_cls" else 2, n_cls=10, rng=rs)
+    assert len(m) == 10
+    tot = sum(len(v) for v in m.values())
+    if method in ("dir", "n_cls", "my_part"):
+        assert all(len(v) == 200 for v in m.values())  # equal quotas (lognormal sigma=0)
+    if method in ("dir", "hetero"):
+        allix = np.concatenate([m[i] for i in range(10)])
+        assert len(np.unique(allix)) == len(allix), "no sample reuse"
+    assert tot >= 1900
+
+
+def test_dir_partition_is_non_iid():
+    y = _labels(5000)
+    m = P.partition_dir(y, 20, 0.1, n_cls=10, rng=np.random.RandomState(3))
+    ent = []
+    for ix in m.values():
+        h = np.bincount(y[ix], minlength=10) / len(ix)
+        ent.append(-(h[h > 0] * np.log(h[h > 0])).sum())
+    assert np.mean(ent) < 0.8 * np.log(10)
+
+
+def test_homo_and_site_partition():
+    m = P.partition_homo(103, 4, rng=np.random.RandomState(0))
+    assert sorted(np.concatenate(list(m.values())).tolist()) == list(range(103))
+    site = np.array([0] * 50 + [1] * 30 + [2] * 20)
+    tr, te, _ = P.partition_by_site(site, max_clients=3)
+    assert len(tr[0]) == 40 and len(te[0]) == 10 and len(tr[2]) == 16
+
+
+def test_robust_aggregators():
+    torch.manual_seed(0)
+    good = [{"w": torch.randn(5) * 0.01 + 1.0} for _ in range(6)]
+    bad = [{"w": torch.full((5,), 100.0)}]
+    wl = [(1, s) for s in good + bad]
+    med = RB.robust_aggregate("median", wl)
+    assert torch.allclose(med["w"], torch.ones(5), atol=0.05)
+    kr = RB.robust_aggregate("krum", wl, f=1)
+    assert float(kr["w"].max()) < 2
+    tm = RB.robust_aggregate("trimmed_mean", wl, trim_ratio=0.2)
+    assert float(tm["w"].max()) < 2
+    avg = RB.robust_aggregate("fedavg", wl) if hasattr(RB, "robust_aggregate") else None
+    if avg is not None:
+        assert float(avg["w"].mean()) > 10
+
+
+def test_message_json_roundtrip_and_inproc_dispatch():
+    m = Message(3, 0, 1)
+    m.add_params(Message.MSG_ARG_KEY_MODEL_PARAMS, {"a.weight": torch.arange(6.).view(2, 3), "n": 4})
+    s = m.to_json()
+    m2 = Message()
+    m2.init_from_json_string(s)
+    assert m2.get_type() == 3 and m2.get_receiver_id() == 1
+    assert torch.equal(m2.get(Message.MSG_ARG_KEY_MODEL_PARAMS)["a.weight"], torch.arange(6.).view(2, 3))
+
+    got = []
+
+    class S(ServerManager):
+        def register_message_receive_handlers(self):
+            self.register_message_receive_handler(7, lambda msg: got.append(msg.get("x")))
+
+    srv = S(None, rank=0, size=2, backend="INPROC", world="t1")
+    srv.register_message_receive_handlers()
+    cli = ClientManager(None, rank=1, size=2, backend="INPROC", world="t1")
+    msg = Message(7, 1, 0)
+    msg.add_params("x", 42)
+    cli.send_message(msg)
+    assert srv.com_manager.poll_once(timeout=1.0)
+    assert got == [42]
+
+
+def test_grpc_backend_roundtrip():
+    pytest.importorskip("grpc")
+    from neuroimagedisttraining_amd.comm import GRPCCommManager
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    base = s.getsockname()[1]
+    s.close()
+    a = GRPCCommManager("127.0.0.1", None, client_id=0, base_port=base)
+    b = GRPCCommManager("127.0.0.1", None, client_id=1, base_port=base)
+    try:
+        m = Message(5, 1, 0)
+        m.add_params("w", torch.ones(3))
+        b.send_message(m)
+        r = a.q.get(timeout=10)
+        assert r.get_type() == 5 and torch.equal(r.get("w"), torch.ones(3))
+    finally:
+        a.stop_receive_message()
+        b.stop_receive_message()
+
+
+def test_topologies_row_stochastic():
+    t = SymmetricTopologyManager(8, 4)
+    W = t.generate_topology()
+    assert np.allclose(W.sum(1), 1) and np.allclose(W, W.T)
+    assert t.get_in_neighbor_idx_list(0) == [1, 2, 6, 7]
+    a = AsymmetricTopologyManager(8, 2, 2, seed=0)
+    W2 = a.generate_topology()
+    assert np.allclose(W2.sum(1), 1)
+    for kind in ("ring", "full", "random"):
+        M = mixing_matrix(kind, 6, round_idx=3, neighbors=2)
+        assert np.allclose(M.sum(1), 1)
+
+
+def test_mpc_bgw_lcc_additive():
+    p = TA.P_DEFAULT
+    rs = np.random.RandomState(0)
+    X = rs.randint(0, 1000, size=(2, 5))
+    sh = TA.BGW_encoding(X, 5, 2, p, rs)
+    rec = TA.BGW_decoding(sh[[0, 2, 4]], [0, 2, 4], p)
+    assert np.array_equal(rec, X % p)
+    X2 = rs.randint(0, 1000, size=(4, 3))
+    enc = TA.LCC_encoding(X2, N=6, K=2, T=1, p=p, rng=rs)
+    dec = TA.LCC_decoding(enc, 1, 6, 2, 1, list(range(6)), p)
+    assert np.array_equal(np.concatenate(list(dec), 0), X2 % p)
+    ss = TA.Gen_Additive_SS(7, 4, p, rs)
+    assert np.all(ss.sum(0) % p == 0)
+    assert TA.modular_inv(3, p) * 3 % p == 1
+
+
+def test_secure_aggregation_equals_fedavg_with_dropout():
+    rs = np.random.RandomState(1)
+    n = 5
+    vecs = [rs.randn(100) for _ in range(n)]
+    wts = rs.dirichlet(np.ones(n))
+    tr = TA.TurboAggregateTrainer(n, seed=3)
+    ups = {i: tr.client_upload(i, vecs[i], wts[i]) for i in range(n)}
+    agg = tr.server_aggregate(ups)
+    ref = sum(w * v for w, v in zip(wts, vecs))
+    assert np.allclose(agg, ref, atol=1e-3)
+    ups.pop(2)
+    agg2 = tr.server_aggregate(ups, dropped=[2])
+    ref2 = sum(wts[i] * vecs[i] for i in range(n) if i != 2)
+    assert np.allclose(agg2, ref2, atol=1e-3)
+
+
+def test_sparse_mask_ops():
+    torch.manual_seed(0)
+    params = {"a": torch.randn(64, 32), "b": torch.randn(10, 64)}
+    sp = SP.erk_sparsities(params, 0.5)
+    masks = SP.init_masks(params, sp)
+    dens = sum(float(m.sum()) for m in masks.values()) / sum(m.numel() for m in masks.values())
+    assert abs(dens - 0.5) < 0.02
+    new, nrm = SP.fire_mask(masks, params, 0, 0.5, 10)
+    assert all(float(new[k].sum()) == float(masks[k].sum()) - nrm[k] for k in masks)
+    grown = SP.regrow_mask(new, nrm, {k: torch.randn_like(v) for k, v in params.items()})
+    assert all(float(grown[k].sum()) == float(masks[k].sum()) for k in masks)
+    d, tot = SP.hamming_distance(masks, grown)
+    assert 0 < d < tot
+    w = {"a.weight": torch.randn(100)}
+    m = {"a.weight": torch.ones(100)}
+    m2 = SP.fake_prune(0.3, w, m)
+    assert abs(float(m2["a.weight"].sum()) - 70) <= 1
+    srv = {"a.weight": torch.zeros(100)}
+    agg = SP.masked_average(srv, [(m, {"a.weight": torch.ones(100)}), (m2, {"a.weight": 3 * torch.ones(100)})])
+    assert torch.all((agg["a.weight"] == 2) | (agg["a.weight"] == 1) | (agg["a.weight"] == 4))
+
+
+def test_flops_counts_conv3d():
+    from neuroimagedisttraining_amd.models import AlexNet3D_Dropout
+    from neuroimagedisttraining_amd.utils.flops import count_inference_flops
+    m = AlexNet3D_Dropout(num_classes=1, in_shape=(69, 69, 69))
+    f = count_inference_flops(m, input_shape=(1, 69, 69, 69), full=True)
+    assert f > 1e8
