@@ -56,7 +56,7 @@ void conv1_wgrad(uintptr_t x8, uintptr_t idx, uintptr_t dp, uintptr_t pout, uint
 // head.hip
 void head(uintptr_t p5, uintptr_t theta, int64_t ldt, int64_t off_w1, int64_t off_b1, int64_t off_w2, int64_t off_b2,
           uintptr_t y, uintptr_t logits, uintptr_t loss, uintptr_t grad, int64_t ldg, uintptr_t dp5, int G, int B,
-          int train, float keep, uint64_t seed, uintptr_t stream);
+          int train, float keep, uint64_t seed, uintptr_t cids, uintptr_t stream);
 // select.hip
 void saliency_acc(uintptr_t theta, uintptr_t grad, int64_t ld, int64_t P, int G, float alpha, uintptr_t score,
                   int64_t lds, uintptr_t stream);

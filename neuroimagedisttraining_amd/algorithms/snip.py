@@ -37,7 +37,7 @@ def snip_scores(model, x, y, loss="bce"):
         mods[n].weight.requires_grad_(True)
     out = cp(x)
     out = out[0] if isinstance(out, (list, tuple)) else out
-    if loss == "bce" or (out.dim() == 2 and out.shape[1] == 1):
+    if out.dim() == 1 or (out.dim() == 2 and out.shape[1] == 1):
         L = F.binary_cross_entropy_with_logits(out.float(), y.view(-1, 1).float())
     else:
         L = F.cross_entropy(out.float(), y.long())

@@ -165,7 +165,7 @@ class HipAlexNet3D:
         return b
 
     # ---------------------------------------------------------------------------------------------
-    def train_step(self, theta, bufs, grads, x8, mom, idx, labels, G, B, keep=0.5, seed=0):
+    def train_step(self, theta, bufs, grads, x8, mom, idx, labels, G, B, keep=0.5, seed=0, cids=None):
         """Forward + backward for G clients; writes ``grads`` [G,P], updates BN running stats in ``bufs``.
         Returns the per-client mean loss tensor [G] (device)."""
         assert grads.shape == theta.shape and grads.stride(1) == 1 and grads.stride(0) == theta.stride(0)
@@ -177,7 +177,7 @@ class HipAlexNet3D:
         o = self.o
         m.head(_p(b["p5"]), _p(theta), P, o["classifier.1.weight"], o["classifier.1.bias"], o["classifier.4.weight"],
                o["classifier.4.bias"], _p(labels), _p(b["logits"]), _p(b["loss"]), _p(grads), grads.stride(0), _p(b["dp5"]), G, B, 1,
-               float(keep), int(seed) & ((1 << 64) - 1), st)
+               float(keep), int(seed) & ((1 << 64) - 1), _p(cids), st)
         nchunk = 64
 
         def bn_bwd(pool, ci, bi, C, sp, dsrc, pout, amax, dy, y):
@@ -220,5 +220,5 @@ class HipAlexNet3D:
         P = theta.stride(0)
         o = self.o
         m.head(_p(b["p5"]), _p(theta), P, o["classifier.1.weight"], o["classifier.1.bias"], o["classifier.4.weight"],
-               o["classifier.4.bias"], 0, _p(b["logits"]), 0, 0, P, 0, G, B, 0, 1.0, 0, st)
+               o["classifier.4.bias"], 0, _p(b["logits"]), 0, 0, P, 0, G, B, 0, 1.0, 0, 0, st)
         return b["logits"]

@@ -76,9 +76,12 @@ class HipEngine:
         self.device = torch.device(device)
         self.m = ops.ext()
 
-    def train_step(self, theta, bufs, grads, idx, G, B, keep, seed):
+    def train_step(self, theta, bufs, grads, idx, G, B, keep, seed, cids=None):
         y = self.labels.index_select(0, idx.long())
-        return self.net.train_step(theta, bufs, grads, self.x8, self.mom, idx, y, G, B, keep, seed)
+        ct = None
+        if cids is not None:
+            ct = torch.as_tensor(list(cids), dtype=torch.int32).to(self.device, non_blocking=True)
+        return self.net.train_step(theta, bufs, grads, self.x8, self.mom, idx, y, G, B, keep, seed, ct)
 
     def eval_logits(self, theta, bufs, idx, G, B):
         return self.net.eval_logits(theta, bufs, self.x8, idx, G, B)
@@ -130,21 +133,29 @@ class TorchEngine:
             return F.binary_cross_entropy_with_logits(out.float().view(-1, 1), y.float().view(-1, 1))
         return F.cross_entropy(out.float(), y.long())
 
-    def train_step(self, theta, bufs, grads, idx, G, B, keep, seed):
+    def train_step(self, theta, bufs, grads, idx, G, B, keep, seed, cids=None):
         from torch.func import functional_call
-        torch.manual_seed(int(seed) & 0x7fffffff)
         losses = torch.zeros(G, device=theta.device)
         self.model.train()
         for g in range(G):
+            # dropout stream keyed by (step seed, global client id): independent of how clients are sharded
+            cid = int(cids[g]) if cids is not None else g
+            torch.manual_seed((int(seed) * 1000003 + cid) & 0x7fffffffffff)
             row = theta[g].detach().clone().requires_grad_(True)
             pv = self._views(row, self.players)
-            bv = self._views(bufs[g], self.blayers)
+            # separate buffer tensors: in-place running-stat updates on views of one row would bump a shared
+            # version counter that autograd checks; results are copied back into the row afterwards
+            bview = self._views(bufs[g], self.blayers)
+            bv = {k: v.clone() for k, v in bview.items()}
             x, y = self._batch(idx[g * B:(g + 1) * B])
             out = functional_call(self.model, {**pv, **bv}, (x,))
             if isinstance(out, (list, tuple)):
                 out = out[0]
             loss = self._loss(out, y)
             loss.backward()
+            with torch.no_grad():
+                for k, v in bv.items():
+                    bview[k].copy_(v)
             grads[g].copy_(row.grad)
             losses[g] = loss.detach()
         return losses
@@ -229,8 +240,9 @@ class FLRunner:
         self.C = len(self.local)
         P, Q = engine.players.total, engine.blayers.total
         self.P, self.Q = P, Q
-        flat_p = engine.players.flatten_state(dict(template_model.named_parameters()), self.device)
-        flat_b = engine.blayers.flatten_state(dict(template_model.named_buffers()), self.device)
+        with torch.no_grad():
+            flat_p = engine.players.flatten_state(dict(template_model.named_parameters()), self.device).detach()
+            flat_b = engine.blayers.flatten_state(dict(template_model.named_buffers()), self.device).detach()
         self.w_global = flat_p.clone()
         self.b_global = flat_b.clone()
         nrow = max(1, self.C)
@@ -310,7 +322,8 @@ class FLRunner:
             def fn(rr, idx, G, B):
                 def body(th, bu, gr, mo):
                     self._step_seed += 1
-                    self.e.train_step(th, bu, gr, idx, G, B, cfg.dropout_keep, (cfg.seed << 20) + self._step_seed)
+                    self.e.train_step(th, bu, gr, idx, G, B, cfg.dropout_keep, (cfg.seed << 20) + self._step_seed,
+                                      cids=[self.local[r] for r in rr])
                     lo, hi = rr[0], rr[-1] + 1
                     self.e.saliency_acc(th, gr, score[lo:hi] if rr == list(range(lo, hi)) else score[rr],
                                         1.0 / cfg.itersnip_iteration)
@@ -368,7 +381,8 @@ class FLRunner:
                     self._step_seed += 1
                     if cfg.prox_mu > 0:
                         w_ref = self.w_global
-                    self.e.train_step(th, bu, gr, idx, G, B, cfg.dropout_keep, (cfg.seed << 20) + self._step_seed)
+                    self.e.train_step(th, bu, gr, idx, G, B, cfg.dropout_keep, (cfg.seed << 20) + self._step_seed,
+                                      cids=[self.local[r] for r in rr])
                     if cfg.prox_mu > 0:
                         gr.add_(th - w_ref.unsqueeze(0), alpha=cfg.prox_mu)
                     self.e.opt_step(th, gr, mo, self.mask if self.alg == "salientgrads" else None, lr, cfg.wd,

@@ -58,12 +58,13 @@ def hash4_np(seed, a, b, c):
     return (z >> np.uint64(32)).astype(np.uint32)
 
 
-def dropout_keep(seed, G, B, nfeat, keep, layer=0):
-    """Boolean keep-mask ``[G, B, nfeat]`` identical to the HIP head kernel's."""
+def dropout_keep(seed, G, B, nfeat, keep, layer=0, cids=None):
+    """Boolean keep-mask ``[G, B, nfeat]`` identical to the HIP head kernel's (streams keyed by global client id)."""
     if keep >= 1.0:
         return np.ones((G, B, nfeat), dtype=bool)
     s = seed if layer == 0 else (seed ^ 0x5bd1e995)
-    g, b, f = np.meshgrid(np.arange(G), np.arange(B), np.arange(nfeat), indexing="ij")
+    cid = np.arange(G) if cids is None else np.asarray(cids)
+    g, b, f = np.meshgrid(cid, np.arange(B), np.arange(nfeat), indexing="ij")
     thr = np.uint64(int(keep * 4294967296.0))
     return hash4_np(s, g, b, f).astype(np.uint64) < thr
 

@@ -1,0 +1,148 @@
+"""CPU end-to-end tests of the FL stack: reference-semantics algorithm APIs on small synthetic data, the
+client-batched executor (TorchEngine) incl. SNIP masks and aggregation, and a 2-rank gloo run that must
+reproduce the 1-rank result exactly (client sharding must not change the math)."""
+import os
+import types
+
+import numpy as np
+import pytest
+import torch
+import torch.nn as nn
+
+from neuroimagedisttraining_amd.algorithms.trainers import ClassificationTrainer, VolumeTrainer
+from neuroimagedisttraining_amd.data.images import load_partition_data, load_partition_data_synthetic_tabular
+from neuroimagedisttraining_amd.models import LeNet5_cifar, LogisticRegression
+
+
+def _args(**kw):
+    a = dict(client_num_in_total=3, client_num_per_round=3, comm_round=2, epochs=1, batch_size=32, lr=0.05,
+             lr_decay=0.998, wd=5e-4, momentum=0.0, client_optimizer="sgd", frequency_of_the_test=1, ci=0,
+             dense_ratio=0.5, anneal_factor=0.5, active=1.0, cs="random", static=False, dis_gradient_check=False,
+             uniform=False, different_initial=False, diff_spa=False, erk_power_scale=1.0, save_masks=False,
+             each_prune_ratio=0.2, dist_thresh=1e-4, acc_thresh=0.0, lamda=0.5, local_epochs=1,
+             itersnip_iteration=1, snip_mask=True, dataset="cifar10", record_mask_diff=True)
+    a.update(kw)
+    return types.SimpleNamespace(**a)
+
+
+def test_fedavg_logistic_regression_two_clients_learns():
+    from neuroimagedisttraining_amd.algorithms.fedavg import FedAvgAPI
+    torch.manual_seed(0)
+    ds = load_partition_data_synthetic_tabular(client_number=2, batch_size=32, n_per_client=400, dim=20, n_cls=5)
+    args = _args(client_num_in_total=2, client_num_per_round=2, comm_round=15, lr=0.1, final_finetune=False)
+    tr = ClassificationTrainer(LogisticRegression(20, 5), args)
+    api = FedAvgAPI(ds, torch.device("cpu"), args, tr)
+    api.train()
+    acc = api.stat_info["global_test_acc"]
+    assert acc[-1] > 0.5 and acc[-1] >= acc[0]
+
+
+@pytest.fixture(scope="module")
+def img_ds():
+    return load_partition_data("cifar10", None, "dir", 0.5, 3, 32, n_train=300, n_test=150, seed=1)
+
+
+@pytest.mark.parametrize("algo", ["dispfl", "subavg", "ditto", "dpsgd", "fedfomo", "local", "salientgrads", "fedavg"])
+def test_algorithms_run(algo, img_ds):
+    from neuroimagedisttraining_amd.algorithms import personalized as PZ
+    from neuroimagedisttraining_amd.algorithms.fedavg import FedAvgAPI
+    from neuroimagedisttraining_amd.algorithms.salientgrads import SailentGradsAPI
+    torch.manual_seed(0)
+    np.random.seed(0)
+    args = _args(client_num_per_round=2 if algo in ("dispfl", "fedfomo") else 3)
+    tr = ClassificationTrainer(LeNet5_cifar(10), args)
+    cls = {"dispfl": PZ.DisPFLAPI, "subavg": PZ.SubAvgAPI, "ditto": PZ.DittoAPI, "dpsgd": PZ.DPSGDAPI,
+           "fedfomo": PZ.FedFomoAPI, "local": PZ.LocalAPI, "salientgrads": SailentGradsAPI, "fedavg": FedAvgAPI}[algo]
+    ds = img_ds
+    if algo == "fedfomo":
+        ds = load_partition_data("cifar10", None, "dir", 0.5, 3, 32, n_train=300, n_test=150, seed=1, with_val=True)
+    api = cls(ds, torch.device("cpu"), args, tr)
+    out = api.train()
+    assert out is not None
+    if algo == "dispfl":
+        m = api.masks[0]
+        dens = sum(float(v.sum()) for v in m.values()) / sum(v.numel() for v in m.values())
+        assert abs(dens - 0.5) < 0.05
+    if algo == "salientgrads":
+        mask = api.mask
+        w = api.w_global
+        for k, v in mask.items():
+            if v.dim() > 1:
+                assert float((w[k] * (1 - v)).abs().max()) == 0.0  # masked weights stay zero
+
+
+# ------------------------------------------------------------------------------------------------ executor
+class Tiny3D(nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.features = nn.Sequential(nn.Conv3d(1, 4, 3, 2), nn.BatchNorm3d(4), nn.ReLU(), nn.MaxPool3d(2, 2),
+                                      nn.Conv3d(4, 8, 3), nn.BatchNorm3d(8), nn.ReLU())
+        self.classifier = nn.Sequential(nn.Dropout(), nn.Linear(8, 1))
+
+    def forward(self, x):
+        return self.classifier(self.features(x).amax((2, 3, 4)))
+
+
+def _runner(rank=0, world=1, clients=4, rounds=2):
+    from neuroimagedisttraining_amd.engine.executor import ClientSplit, FLConfig, FLRunner, TorchEngine
+    from neuroimagedisttraining_amd.parallel import runtime as rt
+    torch.manual_seed(0)
+    g = torch.Generator().manual_seed(5)
+    n_tr, n_te = 10, 4
+    N = clients * (n_tr + n_te)
+    vols = torch.randint(0, 256, (N, 15, 15, 15), dtype=torch.uint8, generator=g)
+    labels = torch.randint(0, 2, (N,), generator=g).float()
+    splits = [ClientSplit(np.arange(c * 14, c * 14 + n_tr), np.arange(c * 14 + n_tr, c * 14 + 14))
+              for c in range(clients)]
+    model = Tiny3D()
+    eng = TorchEngine(model, vols, labels, "cpu")
+    info = rt.DistInfo(rank, world, rank, torch.device("cpu"), "gloo" if world > 1 else "none")
+    cfg = FLConfig(comm_round=rounds, epochs=2, batch_size=4, lr=0.05, dense_ratio=0.5, seed=7)
+    return FLRunner(eng, splits, cfg, info, model)
+
+
+def test_executor_snip_rounds_and_aggregation():
+    r = _runner()
+    mask = r.generate_global_mask_snip()
+    sel = mask[r.maskable]
+    assert abs(float(sel.mean()) - 0.5) < 0.02
+    assert float(mask[~r.maskable].min()) == 1.0
+    res = r.run_round(0)
+    # global = sample-weighted mean of the clients' rows (equal sizes -> plain mean), params and buffers
+    assert torch.allclose(r.w_global, r.theta.mean(0), atol=1e-6)
+    assert torch.allclose(r.b_global, r.bufs.mean(0), atol=1e-5)
+    # SalientGrads: masked weights are exactly zero on every client after local training
+    assert float((r.theta[:, r.maskable] * (1 - mask[r.maskable])).abs().max()) == 0.0
+    assert 0.0 <= res["global_test_acc"] <= 1.0
+
+
+def _dist_worker(rank, world, port, out):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    r = _runner(rank, world)
+    r.generate_global_mask_snip()
+    for k in range(2):
+        r.run_round(k)
+    if rank == 0:
+        torch.save({"w": r.w_global, "acc": r.stat_info["global_test_acc"]}, out)
+    dist.destroy_process_group()
+
+
+def test_two_rank_gloo_matches_single_process(tmp_path):
+    import socket
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    out = str(tmp_path / "w.pt")
+    mp.start_processes(_dist_worker, args=(2, port, out), nprocs=2, join=True, start_method="spawn")
+    got = torch.load(out, weights_only=True)
+    r = _runner()
+    r.generate_global_mask_snip()
+    for k in range(2):
+        r.run_round(k)
+    assert torch.allclose(got["w"], r.w_global, atol=1e-5), float((got["w"] - r.w_global).abs().max())
+    assert np.allclose(got["acc"], r.stat_info["global_test_acc"])
