@@ -1,0 +1,3 @@
+"""Compat shim: reference import path ``fedml_api/standalone/fedavg/my_model_trainer.py``."""
+from neuroimagedisttraining_amd.algorithms.trainers import ClassificationTrainer as MyModelTrainer  # noqa: F401
+from neuroimagedisttraining_amd.algorithms.trainers import VolumeTrainer  # noqa: F401

@@ -1,0 +1,2 @@
+"""Compat shim: reference import path ``fedml_api/standalone/fedfomo/client.py``."""
+from neuroimagedisttraining_amd.algorithms.common import Client  # noqa: F401

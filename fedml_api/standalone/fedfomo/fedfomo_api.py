@@ -1,0 +1,2 @@
+"""Compat shim: reference import path ``fedml_api/standalone/fedfomo/fedfomo_api.py``."""
+from neuroimagedisttraining_amd.algorithms.personalized import FedFomoAPI  # noqa: F401

@@ -1,0 +1,276 @@
+"""Standalone experiment entry points (reference ``fedml_experiments/standalone/<algo>/main_<algo>.py``).
+
+Flags, defaults and the ``args.identity`` string (the log file name, ``LOG/<dataset>/<identity>.log``) follow
+the reference entry points.  Added flags:
+
+* ``--engine {auto,hip,torch}``: SalientGrads / FedAvg / FedProx on 3D-CNN + ABCD-shape data run on the
+  client-batched MI355X executor (HIP kernels, clients sharded over ranks, RCCL aggregation) when ``hip``
+  (``auto`` = hip if a GPU and the extension are available); ``torch`` = the reference-semantics sequential
+  eager path (also the CPU path).
+* ``--synthetic_abcd 1``, ``--n_per_client``: synthetic ABCD-shape cohort (no HDF5 needed).
+* FedProx / robust aggregation: ``--fedprox_mu``, ``--aggregator {fedavg,krum,multikrum,median,trimmed_mean}``,
+  ``--byzantine_f``, ``--trim_ratio``.
+* ``--checkpoint_dir`` / ``--resume`` for the HIP executor.
+
+Run under ``torchrun`` for multi-GPU; single process otherwise.
+"""
+from __future__ import annotations
+
+import argparse
+import logging
+import os
+import random
+
+import numpy as np
+import torch
+
+ALGOS = ("sailentgrads", "fedavg", "fedprox", "dispfl", "subavg", "ditto", "dpsgd", "fedfomo", "local")
+
+_DEFAULTS = {  # per-entry-point defaults that differ
+    "sailentgrads": dict(model="3DCNN", dataset="ABCD", batch_size=16, lr=0.01, epochs=2, client_num_in_total=4,
+                         frac=1.0, comm_round=200, seed=1024, cs="v0"),
+    "fedavg": dict(model="3DCNN", dataset="ABCD", batch_size=16, lr=0.001, epochs=5, client_num_in_total=4,
+                   frac=0.9, comm_round=200, seed=0),
+    "fedprox": dict(model="3DCNN", dataset="ABCD", batch_size=16, lr=0.001, epochs=5, client_num_in_total=128,
+                    frac=1.0, comm_round=200, seed=0, partition_method="dir", fedprox_mu=0.01),
+    "dispfl": dict(model="3DCNN", dataset="ABCD", batch_size=16, lr=0.001, epochs=5, client_num_in_total=21,
+                   frac=0.1, comm_round=10, seed=1024, cs="random"),
+    "subavg": dict(model="resnet18", dataset="cifar10", batch_size=128, lr=0.1, epochs=5, client_num_in_total=100,
+                   frac=0.1, comm_round=1000, seed=0),
+    "ditto": dict(model="resnet18", dataset="cifar10", batch_size=128, lr=0.1, epochs=2, client_num_in_total=100,
+                  frac=0.1, comm_round=1000, seed=0),
+    "dpsgd": dict(model="resnet18", dataset="cifar10", batch_size=128, lr=0.1, epochs=5, client_num_in_total=100,
+                  frac=0.1, comm_round=50, seed=0, cs="ring"),
+    "fedfomo": dict(model="resnet18", dataset="cifar10", batch_size=128, lr=0.1, epochs=5, client_num_in_total=100,
+                    frac=0.1, comm_round=1000, seed=0),
+    "local": dict(model="resnet18", dataset="cifar10", batch_size=128, lr=0.1, epochs=5, client_num_in_total=100,
+                  frac=1.0, comm_round=10, seed=1024),
+}
+
+
+def str2bool(v):
+    return str(v).lower() in ("1", "true", "yes", "y")
+
+
+def add_args(parser, algo):
+    d = _DEFAULTS[algo]
+    a = parser.add_argument
+    a("--model", type=str, default=d["model"])
+    a("--dataset", type=str, default=d["dataset"])
+    a("--data_dir", type=str, default="")
+    a("--partition_method", type=str, default=d.get("partition_method", "dir"))
+    a("--partition_alpha", type=float, default=0.3)
+    a("--batch_size", type=int, default=d["batch_size"])
+    a("--client_optimizer", type=str, default="sgd")
+    a("--lr", type=float, default=d["lr"])
+    a("--lr_decay", type=float, default=0.998)
+    a("--wd", type=float, default=5e-4)
+    a("--momentum", type=float, default=0)
+    a("--epochs", type=int, default=d["epochs"])
+    a("--client_num_in_total", type=int, default=d["client_num_in_total"])
+    a("--frac", type=float, default=d["frac"])
+    a("--comm_round", type=int, default=d["comm_round"])
+    a("--frequency_of_the_test", type=int, default=1)
+    a("--gpu", type=int, default=0)
+    a("--ci", type=int, default=0)
+    a("--seed", type=int, default=d["seed"])
+    a("--tag", type=str, default="test")
+    if algo in ("sailentgrads", "dispfl"):
+        a("--dense_ratio", type=float, default=0.5)
+        a("--anneal_factor", type=float, default=0.5)
+        a("--cs", type=str, default=d["cs"])
+        a("--active", type=float, default=1.0)
+        a("--public_portion", type=float, default=0)
+        a("--erk_power_scale", type=float, default=1)
+        for f in ("dis_gradient_check", "strict_avg", "static", "uniform", "save_masks", "different_initial",
+                  "record_mask_diff", "diff_spa", "global_test"):
+            a("--" + f, action="store_true")
+        a("--dispfl_aggregate", type=int, default=0)
+    if algo == "sailentgrads":
+        a("--itersnip_iteration", type=int, default=1)
+        a("--stratified_sampling", action="store_true")
+        a("--snip_mask", type=str2bool, default=True)  # reference: type=bool (cannot be disabled, Q6)
+        a("--logfile", type=str, default="logfile")
+    if algo == "subavg":
+        a("--dense_ratio", type=float, default=0.5)
+        a("--each_prune_ratio", type=float, default=0.05)
+        a("--dist_thresh", type=float, default=1e-4)
+        a("--acc_thresh", type=float, default=0.5)
+        a("--record_mask_diff", action="store_true")
+    if algo == "ditto":
+        a("--local_epochs", type=int, default=3)
+        a("--lamda", type=float, default=0.5)
+    if algo == "dpsgd":
+        a("--cs", type=str, default=d["cs"])
+        a("--type", type=str, default="epoch")
+    # additions (not in the reference)
+    a("--engine", type=str, default="auto", choices=["auto", "hip", "torch"])
+    a("--synthetic_abcd", type=int, default=1)
+    a("--n_per_client", type=int, default=180)
+    a("--fedprox_mu", type=float, default=d.get("fedprox_mu", 0.0))
+    a("--aggregator", type=str, default="fedavg")
+    a("--byzantine_f", type=int, default=0)
+    a("--trim_ratio", type=float, default=0.1)
+    a("--group", type=int, default=0)
+    a("--checkpoint_dir", type=str, default="")
+    a("--resume", type=int, default=0)
+    a("--log_dir", type=str, default="LOG")
+    return parser
+
+
+def identity(args, algo):
+    part = args.partition_method + ("" if args.partition_method == "homo" else str(args.partition_alpha))
+    args.client_num_per_round = int(args.client_num_in_total * args.frac)
+    if algo == "sailentgrads":
+        s = "SailentGrads-" + args.dataset + "-" + part + "-mdl" + args.model + "customized" + "lowbatch" + "-cs" + args.cs
+        s += "-masks" if args.save_masks else ""
+        s += "-diff_spa" if args.diff_spa else ""
+        s += "-uniform_init" if args.uniform else "-ERK_init"
+        s += "-diff_init" if args.different_initial else "-same_init"
+        s += "-g" if args.global_test else ""
+        s += "-RSM" if args.static else "-DST"
+        s += "-cm%s-total_clnt%s" % (args.comm_round, args.client_num_in_total)
+        s += "-neighbor%s-dr%s-active%s-seed%s-lr%s-batchsize%s-iteration%s-stratified%s" % (
+            args.client_num_per_round, args.dense_ratio, args.active, args.seed, args.lr, args.batch_size,
+            args.itersnip_iteration, args.stratified_sampling)
+        return s
+    if algo in ("fedavg", "fedprox"):
+        s = ("fedavg" if algo == "fedavg" else "fedprox") + "-" + part + "-mdl" + args.model
+        s += "-batchsize%s-cm%s-total_clnt%s-neighbor%s-seed%s-lr%s" % (
+            args.batch_size, args.comm_round, args.client_num_in_total, args.client_num_per_round, args.seed, args.lr)
+        return s + ("-mu%s-agg%s" % (args.fedprox_mu, args.aggregator) if algo == "fedprox" else "")
+    if algo == "dispfl":
+        s = "dispfl-" + args.dataset + "-" + part + "-mdl" + args.model + "-cs" + args.cs
+        s += "-masks" if args.save_masks else ""
+        s += "-diff_spa" if args.diff_spa else ""
+        s += "-uniform_init" if args.uniform else "-ERK_init"
+        s += "-diff_init" if args.different_initial else "-same_init"
+        s += "-g" if args.global_test else ""
+        s += "-RSM" if args.static else "-DST"
+        s += "-cm%s-total_clnt%s-neighbor%s-dr%s-active%s-seed%s" % (
+            args.comm_round, args.client_num_in_total, args.client_num_per_round, args.dense_ratio, args.active,
+            args.seed)
+        return s
+    base = {"subavg": "subavg", "ditto": "ditto", "dpsgd": "dpsgd", "fedfomo": "fedfomo", "local": "local"}[algo]
+    s = base + "-" + args.dataset + "-" + part + "-mdl" + args.model
+    s += "-cm%s-total_clnt%s-neighbor%s-seed%s-lr%s" % (args.comm_round, args.client_num_in_total,
+                                                         args.client_num_per_round, args.seed, args.lr)
+    if algo == "subavg":
+        s += "-dr%s-epr%s" % (args.dense_ratio, args.each_prune_ratio)
+    return s
+
+
+def load_data(args, dataset_name, logger=None):
+    from .data import abcd, images
+    if dataset_name == "ABCD":
+        if args.synthetic_abcd or not args.data_dir:
+            return abcd.load_partition_data_abcd_synthetic(args.client_num_in_total, args.partition_method,
+                                                           args.partition_alpha, args.batch_size,
+                                                           n_per_client=args.n_per_client, seed=args.seed,
+                                                           logger=logger)
+        return abcd.load_partition_data_abcd(args.data_dir, args.partition_method, args.partition_alpha,
+                                             args.client_num_in_total, args.batch_size, logger)
+    if dataset_name in ("cifar10", "cifar100", "tiny"):
+        return images.load_partition_data(dataset_name, args.data_dir, args.partition_method, args.partition_alpha,
+                                          args.client_num_in_total, args.batch_size, logger, seed=args.seed,
+                                          with_val=False)
+    if dataset_name == "synthetic":
+        return images.load_partition_data_synthetic_tabular(args.client_num_in_total, args.batch_size)
+    raise ValueError(dataset_name)
+
+
+def _use_hip(args, algo):
+    if algo not in ("sailentgrads", "fedavg", "fedprox") or args.dataset != "ABCD" or args.model != "3DCNN":
+        return False
+    if args.engine == "torch":
+        return False
+    if args.aggregator != "fedavg":
+        return False
+    try:
+        from . import ops
+        ok = torch.cuda.is_available() and ops.available()
+    except Exception:  # noqa: BLE001
+        ok = False
+    if args.engine == "hip" and not ok:
+        raise RuntimeError("--engine hip needs a GPU and the built HIP extension")
+    return ok
+
+
+def run_hip(args, algo, logger):
+    """SalientGrads / FedAvg / FedProx on the client-batched MI355X executor."""
+    from .data.synthetic_fl import build_fl_volumes, to_hip_store
+    from .engine.executor import ClientSplit, FLConfig, FLRunner, HipEngine
+    from .models.alexnet3d import AlexNet3D_Dropout
+    from .parallel import runtime as rt
+    from .utils import checkpoint as ck
+    info = rt.init_distributed()
+    n_test = max(1, int(round(args.n_per_client * 0.2)))
+    n_train = args.n_per_client - n_test
+    shards = rt.shard_clients([n_train] * args.client_num_in_total, info.world)
+    vol, labels, local_splits = build_fl_volumes(shards[info.rank], args.client_num_in_total, n_train, n_test,
+                                                 info.device, seed=args.seed, alpha=args.partition_alpha)
+    x8, mom = to_hip_store(vol)
+    del vol
+    splits = [local_splits.get(c) or ClientSplit(np.zeros(n_train, np.int64), np.zeros(n_test, np.int64))
+              for c in range(args.client_num_in_total)]
+    model = AlexNet3D_Dropout(num_classes=1)
+    eng = HipEngine(model, x8, mom, labels, info.device)
+    cfg = FLConfig(comm_round=args.comm_round, epochs=args.epochs, batch_size=args.batch_size, lr=args.lr,
+                   lr_decay=args.lr_decay, wd=args.wd, momentum=args.momentum, frac=args.frac,
+                   dense_ratio=getattr(args, "dense_ratio", 1.0), itersnip_iteration=getattr(args, "itersnip_iteration", 1),
+                   snip_mask=getattr(args, "snip_mask", True), frequency_of_the_test=args.frequency_of_the_test,
+                   seed=args.seed, prox_mu=args.fedprox_mu if algo == "fedprox" else 0.0, group=args.group)
+    runner = FLRunner(eng, splits, cfg, info, model, logger=logger,
+                      algorithm="salientgrads" if algo == "sailentgrads" else "fedavg")
+    start = 0
+    if args.resume and args.checkpoint_dir and os.path.exists(os.path.join(args.checkpoint_dir, "global.pt")):
+        start = ck.load_runner(runner, args.checkpoint_dir)
+        logger.info("resumed from %s at round %d", args.checkpoint_dir, start)
+    elif algo == "sailentgrads":
+        runner.generate_global_mask_snip()
+    for r in range(start, cfg.comm_round):
+        runner.run_round(r)
+        if args.checkpoint_dir:
+            ck.save_runner(runner, args.checkpoint_dir, r + 1)
+    rt.shutdown(info)
+    return runner.stat_info
+
+
+def run_reference(args, algo, logger, device):
+    from .algorithms import personalized as PZ
+    from .algorithms.fedavg import FedAvgAPI, FedProxAPI
+    from .algorithms.salientgrads import SailentGradsAPI
+    from .algorithms.trainers import ClassificationTrainer, VolumeTrainer
+    from .models import create_model
+    ds_name = "ABCD" if algo == "sailentgrads" else args.dataset
+    dataset = load_data(args, ds_name, logger)
+    class_num = 1 if ds_name == "ABCD" else dataset[7]
+    in_shape = None
+    model = create_model(args.model, ds_name, class_num, in_shape=in_shape).to(device)
+    trainer = (VolumeTrainer if ds_name == "ABCD" else ClassificationTrainer)(model, args, logger)
+    cls = {"sailentgrads": SailentGradsAPI, "fedavg": FedAvgAPI, "fedprox": FedProxAPI, "dispfl": PZ.DisPFLAPI,
+           "subavg": PZ.SubAvgAPI, "ditto": PZ.DittoAPI, "dpsgd": PZ.DPSGDAPI, "fedfomo": PZ.FedFomoAPI,
+           "local": PZ.LocalAPI}[algo]
+    api = cls(dataset, device, args, trainer, logger)
+    api.train()
+    return api.stat_info
+
+
+def main(algo, argv=None):
+    from .utils.logger import logger_config
+    parser = add_args(argparse.ArgumentParser(description="%s (neuroimagedisttraining_amd)" % algo), algo)
+    args = parser.parse_args(argv)
+    args.identity = identity(args, algo)
+    log_path = os.path.join(args.log_dir, args.dataset, args.identity + ".log")
+    logger = logger_config(log_path=log_path, logging_name=args.identity)
+    logger.info(args)
+    random.seed(args.seed)
+    np.random.seed(args.seed)
+    torch.manual_seed(args.seed)
+    if torch.cuda.is_available():
+        torch.cuda.manual_seed_all(args.seed)
+    if _use_hip(args, algo):
+        return run_hip(args, algo, logger)
+    device = torch.device("cuda:%d" % args.gpu if torch.cuda.is_available() else "cpu")
+    logger.info(device)
+    return run_reference(args, algo, logger, device)

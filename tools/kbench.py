@@ -1,0 +1,100 @@
+"""Per-kernel micro-benchmark at the headline shapes (G clients x B=16, AlexNet3D at 121x145x121).
+
+Runs one full train step to populate every scratch buffer, then re-times each HIP launch of the step in
+isolation (median of N reps with HIP events) and prints achieved TFLOP/s against the useful FLOPs of the op.
+Usage: python tools/kbench.py [G] [reps]
+"""
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def timeit(fn, reps):
+    ts = []
+    for _ in range(3):
+        fn()
+    for _ in range(reps):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        fn()
+        b.record()
+        b.synchronize()
+        ts.append(a.elapsed_time(b))
+    ts.sort()
+    return ts[len(ts) // 2]
+
+
+def main():
+    G = int(sys.argv[1]) if len(sys.argv) > 1 else 64
+    reps = int(sys.argv[2]) if len(sys.argv) > 2 else 10
+    B = 16
+    from neuroimagedisttraining_amd.data.volumes import make_synthetic_abcd
+    from neuroimagedisttraining_amd.data.synthetic_fl import to_hip_store
+    from neuroimagedisttraining_amd.engine.alexnet_hip import HipAlexNet3D
+    from neuroimagedisttraining_amd.engine.executor import padded_rows
+    from neuroimagedisttraining_amd.engine.flat import ParamLayout
+    from neuroimagedisttraining_amd.models.alexnet3d import AlexNet3D_Dropout
+    dev = torch.device("cuda")
+    store = make_synthetic_abcd(min(G * B, 256), seed=1, device=dev)
+    x8, mom = to_hip_store(store.volumes)
+    model = AlexNet3D_Dropout(num_classes=1)
+    pl = ParamLayout.from_tensors(list(model.named_parameters()))
+    bl = ParamLayout.from_tensors(list(model.named_buffers()))
+    with torch.no_grad():
+        theta = padded_rows(G, pl.total, dev)
+        theta.copy_(pl.flatten_state(dict(model.named_parameters()), dev).unsqueeze(0).expand(G, pl.total))
+        bufs = padded_rows(G, bl.total, dev)
+        bufs.copy_(bl.flatten_state(dict(model.named_buffers()), dev).unsqueeze(0).expand(G, bl.total))
+    grads = padded_rows(G, pl.total, dev)
+    net = HipAlexNet3D(pl, bl, dev)
+    idx = (torch.arange(G * B, device=dev) % x8.shape[0]).int()
+    y = store.labels.float().repeat((G * B + store.labels.numel() - 1) // store.labels.numel())[:G * B].contiguous()
+    step = lambda: net.train_step(theta, bufs, grads, x8, mom, idx, y, G, B, 0.5, 1)  # noqa: E731
+    t_step = timeit(step, max(3, reps // 2))
+    b = net._cache[(G, B, True)]
+    m, st = net.m, torch.cuda.current_stream().cuda_stream
+    P = theta.stride(0)
+    o = net.o
+    p = lambda t: t.data_ptr() if t is not None else 0  # noqa: E731
+    rows = []
+
+    def add(name, fn, flops):
+        t = timeit(fn, reps)
+        rows.append((name, t, flops / t / 1e9 if flops else 0.0))
+
+    NB = G * B
+    add("conv1_fwd_pool", lambda: m.conv1_fwd_pool(p(x8), p(idx), p(b["w1p"]), p(b["s1"]), p(b["t1"]), NB, B, p(b["p1"]),
+                                                   p(b["a1"]), st), 2 * 64 * 125 * 57 * 69 * 57 * NB)
+    add("conv1_wgrad", lambda: m.conv1_wgrad(p(x8), p(idx), p(b["dp1"]), p(b["p1"]), p(b["a1"]), NB, B, p(b["c1part"]),
+                                             p(b["w125"]), p(b["mu"]), p(b["covw"]), p(b["i1"]), p(theta), P,
+                                             o["features.1.weight"], p(grads), P, o["features.0.weight"],
+                                             o["features.0.bias"], o["features.1.weight"], o["features.1.bias"],
+                                             1.0 / 255, st), 2 * 64 * 125 * 19 * 23 * 19 * NB)
+    cfgs = [("conv2", "p1", 4, (19, 23, 19), 64, 128, 0), ("conv3", "p2", 8, (5, 7, 5), 128, 192, 1),
+            ("conv4", "h3", 11, (5, 7, 5), 192, 192, 1), ("conv5", "h4", 14, (5, 7, 5), 192, 128, 1)]
+    outs = {4: "y2", 8: "y3", 11: "y4", 14: "y5"}
+    dys = {4: "dy2", 8: "dy3", 11: "dy4", 14: "dy5"}
+    dxs = {4: "dp1", 8: "dx3", 11: "dx4", 14: "dx5"}
+    for name, xin, ci, sp, cin, cout, pad in cfgs:
+        Do = [s + 2 * pad - 2 for s in sp]
+        fl = 2.0 * cin * 27 * cout * Do[0] * Do[1] * Do[2] * NB
+        add(name + "_fwd", lambda xin=xin, ci=ci, sp=sp, cin=cin, cout=cout, pad=pad: m.conv3d_fwd(
+            p(b[xin]), p(b["w%dp" % ci]), p(b["bias%d" % ci]), 0, 0, p(b[outs[ci]]), p(b["st%d" % ci]), G, B, *sp, cin,
+            cout, pad, st), fl)
+        add(name + "_dgrad", lambda ci=ci, sp=sp, cin=cin, cout=cout, pad=pad, Do=Do: m.conv3d_fwd(
+            p(b[dys[ci]]), p(b["w%dt" % ci]), 0, 0, 0, p(b[dxs[ci]]), 0, G, B, *Do, cout, cin, 2 - pad, st), fl)
+        add(name + "_wgrad", lambda xin=xin, ci=ci, sp=sp, cin=cin, cout=cout, pad=pad: m.conv3d_wgrad(
+            p(b[xin]), 0, 0, p(b[dys[ci]]), p(b["wgpart"]), p(grads), P, o["features.%d.weight" % ci], G, B, *sp, cin,
+            cout, pad, b["ns%d" % ci], 1.0, st), fl)
+    tot = sum(r[1] for r in rows)
+    print("G=%d B=%d  full train step %.3f ms  (sum of timed kernels %.3f ms)" % (G, B, t_step, tot))
+    for name, t, tf in rows:
+        print("%-16s %9.3f ms  %8.1f TF/s" % (name, t, tf))
+
+
+if __name__ == "__main__":
+    main()
