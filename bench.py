@@ -28,7 +28,7 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 # Measured on MI355X (1 GPU) with tools/eager_baseline.py: PyTorch-ROCm eager fp32, reference semantics
 # (sequential clients, one shared nn.Module, per-step mask multiply), same 64-client config.  See BASELINE.md.
-EAGER_BASELINE_ROUNDS_PER_S = None
+EAGER_BASELINE_ROUNDS_PER_S = 0.04611  # fp32, steady-state (rounds 1-2), profiles/r1_eager_baseline_steady.txt
 
 
 def parse():

@@ -33,11 +33,14 @@ SPECS = {"cifar10": ((3, 32, 32), 10, 50000, 10000), "cifar100": ((3, 32, 32), 1
          "emnist": ((1, 28, 28), 62, 60000, 10000)}
 
 
-def synthetic_images(n, shape, n_cls, seed=0, noise=0.6):
-    """Class-conditional images: a random low-frequency template per class + per-sample noise."""
-    g = torch.Generator().manual_seed(seed)
+def synthetic_images(n, shape, n_cls, seed=0, noise=0.6, template_seed=12345):
+    """Class-conditional images: a random low-frequency template per class + per-sample noise.
+
+    The class templates depend only on ``template_seed`` so train and test splits share them."""
     c, h, w = shape
-    coarse = torch.randn(n_cls, c, max(2, h // 8), max(2, w // 8), generator=g)
+    gt = torch.Generator().manual_seed(template_seed)
+    coarse = torch.randn(n_cls, c, max(2, h // 8), max(2, w // 8), generator=gt)
+    g = torch.Generator().manual_seed(seed)
     templ = torch.nn.functional.interpolate(coarse, size=(h, w), mode="bilinear", align_corners=False)
     y = torch.randint(0, n_cls, (n,), generator=g)
     x = templ[y] + noise * torch.randn(n, c, h, w, generator=g)
