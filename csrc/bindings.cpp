@@ -19,7 +19,8 @@ void conv3d_fwd(uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t xs, uintptr_
 int conv3d_fwd_nblocks(int B, int D, int H, int W, int pad);
 void conv3d_wgrad(uintptr_t x, uintptr_t xs, uintptr_t xt, uintptr_t dy, uintptr_t part, uintptr_t grad, int64_t ldg,
                   int64_t off, int G, int B, int D, int H, int W, int Cin, int Cout, int pad, int nsplit, float scale,
-                  uintptr_t stream);
+                  uintptr_t ptab, uintptr_t stream);
+void conv3d_pos_table(uintptr_t tab, int B, int D, int H, int W, int pad, uintptr_t stream);
 int conv3d_wgrad_nsplit(int G, int B, int D, int H, int W, int Cin, int Cout, int pad);
 void pack_conv_w(uintptr_t theta, int64_t ldt, int64_t off, int G, int Cout, int Cin, float scale, uintptr_t wp,
                  uintptr_t wt, uintptr_t stream);
@@ -77,6 +78,7 @@ PYBIND11_MODULE(_nidt_hip, m) {
   DEF(conv3d_fwd_nblocks);
   DEF(conv3d_wgrad);
   DEF(conv3d_wgrad_nsplit);
+  DEF(conv3d_pos_table);
   DEF(pack_conv_w);
   DEF(bn_relu_apply);
   DEF(bn_finalize);

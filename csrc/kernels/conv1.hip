@@ -394,10 +394,169 @@ __global__ __launch_bounds__(256, 2) void k_conv1_fwd_pool(const uint8_t* __rest
   }
 }
 
+// k_conv1_fwd_pool_pipe — same math as k_conv1_fwd_pool, but one block walks all 23 pooled rows (ph) of a
+// (sample, pd) slab: the next row's 5x5x64 halo is prefetched into registers (7 x 8 B per thread) while the
+// MFMAs of the current row run, then converted (v_cvt_f32_ubyteN + v_perm: u8 -> exact bf16) into the other
+// LDS buffer — the load latency and the conversion hide behind the matrix work instead of serialising a
+// one-row block.  1-D grid, XCD-remapped so the 19 pd-slabs of a sample (overlapping by 2 z-planes) share
+// an L2.
+__device__ __forceinline__ uint4 u8x8_to_bf16x8(uint2 v) {
+  const float f0 = (float)(v.x & 0xffu), f1 = (float)((v.x >> 8) & 0xffu);
+  const float f2 = (float)((v.x >> 16) & 0xffu), f3 = (float)(v.x >> 24);
+  const float f4 = (float)(v.y & 0xffu), f5 = (float)((v.y >> 8) & 0xffu);
+  const float f6 = (float)((v.y >> 16) & 0xffu), f7 = (float)(v.y >> 24);
+  uint4 o;  // integers 0..255 are exact in bf16: keep the high half of the f32
+  o.x = __builtin_amdgcn_perm(__float_as_uint(f1), __float_as_uint(f0), 0x07060302u);
+  o.y = __builtin_amdgcn_perm(__float_as_uint(f3), __float_as_uint(f2), 0x07060302u);
+  o.z = __builtin_amdgcn_perm(__float_as_uint(f5), __float_as_uint(f4), 0x07060302u);
+  o.w = __builtin_amdgcn_perm(__float_as_uint(f7), __float_as_uint(f6), 0x07060302u);
+  return o;
+}
+
+__global__ __launch_bounds__(256, 2) void k_conv1_fwd_pool_pipe(const uint8_t* __restrict__ x8,
+                                                                const int* __restrict__ idx,
+                                                                const uint16_t* __restrict__ w8,
+                                                                const float* __restrict__ scale,
+                                                                const float* __restrict__ shift, int B,
+                                                                uint16_t* __restrict__ out, uint8_t* __restrict__ amax) {
+  constexpr int HX = 64;
+  constexpr int HALO = 5 * 5 * HX * 8;  // bf16 elements per buffer
+  constexpr int NLD = (5 * 5 * HX + 255) / 256;  // 7 halo voxels per thread
+  __shared__ __attribute__((aligned(16))) uint16_t halo[2 * HALO];
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int pd = bid % kPD, n = bid / kPD;
+  const int g = n / B;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const uint8_t* xs = x8 + (int64_t)idx[n] * kPZ * kPY * kPX * 8;
+  uint2 pre[NLD];
+#define C1_LOAD(PH)                                                                                           \
+  _Pragma("unroll") for (int u_ = 0; u_ < NLD; ++u_) {                                                        \
+    const int e_ = tid + 256 * u_;                                                                            \
+    const int xh_ = e_ & (HX - 1), yz_ = e_ >> 6, yh_ = yz_ % 5, zh_ = yz_ / 5;                                \
+    pre[u_] = make_uint2(0, 0);                                                                               \
+    if (e_ < 5 * 5 * HX && xh_ < kPX)                                                                         \
+      pre[u_] = *reinterpret_cast<const uint2*>(xs + (((int64_t)(3 * pd + zh_) * kPY + 3 * (PH) + yh_) * kPX + xh_) * 8); \
+  }
+#define C1_STORE(BUF)                                                                                         \
+  _Pragma("unroll") for (int u_ = 0; u_ < NLD; ++u_) {                                                        \
+    const int e_ = tid + 256 * u_;                                                                            \
+    if (e_ < 5 * 5 * HX) *reinterpret_cast<uint4*>(&halo[(BUF) * HALO + e_ * 8]) = u8x8_to_bf16x8(pre[u_]);  \
+  }
+  C1_LOAD(0)
+  const int fr = lane & 15, fq = lane >> 4;
+  const int ch = wid & 1, op = wid >> 1;
+  bf16x8 fa[2][7];
+  const uint16_t* wg = w8 + (int64_t)g * kC1 * kK1;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int s = 0; s < 7; ++s)
+      fa[i][s] = *reinterpret_cast<const bf16x8*>(wg + (32 * ch + 16 * i + fr) * kK1 + 32 * s + 8 * fq);
+  float sc[2][4], sh[2][4];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      sc[i][r] = scale[g * kC1 + 32 * ch + 16 * i + 4 * fq + r];
+      sh[i][r] = shift[g * kC1 + 32 * ch + 16 * i + 4 * fq + r];
+    }
+  int toff[7];
+#pragma unroll
+  for (int s = 0; s < 7; ++s) {
+    int t = 4 * s + fq;
+    t = t < 27 ? t : 26;
+    toff[s] = (((t / 9) * 5 + (t / 3) % 3) * HX + (t % 3)) * 8;
+  }
+  const int colbase0 = (15 * (2 * op) + fr) * 8, colbase1 = colbase0 + 15 * 8;
+  const int wloc = fr / 3, dw = fr - 3 * wloc;
+  C1_STORE(0)
+  __syncthreads();
+  for (int ph = 0; ph < kPH; ++ph) {
+    const int cur = ph & 1;
+    if (ph + 1 < kPH) C1_LOAD(ph + 1)
+    const uint16_t* hb = halo + cur * HALO;
+    float best[2][2][4];
+    int bidx[2][2][4];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) { best[i][j][r] = -INFINITY; bidx[i][j][r] = 0; }
+    for (int dd = 0; dd < 3; ++dd) {
+#pragma unroll
+      for (int dh = 0; dh < 3; ++dh) {
+        f32x4 acc[2][2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        const int rowoff = ((dd * 5 + dh) * HX) * 8;
+#pragma unroll
+        for (int s = 0; s < 7; ++s) {
+          const bf16x8 fb0 = *reinterpret_cast<const bf16x8*>(&hb[colbase0 + rowoff + toff[s]]);
+          const bf16x8 fb1 = *reinterpret_cast<const bf16x8*>(&hb[colbase1 + rowoff + toff[s]]);
+#pragma unroll
+          for (int i = 0; i < 2; ++i) {
+            acc[i][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][s], fb0, acc[i][0], 0, 0, 0);
+            acc[i][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][s], fb1, acc[i][1], 0, 0, 0);
+          }
+        }
+        const int li = dd * 9 + dh * 3;
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const float z = fmaf(acc[i][j][r], sc[i][r], sh[i][r]);
+              if (z > best[i][j][r]) { best[i][j][r] = z; bidx[i][j][r] = li; }
+            }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int pw = 5 * (2 * op + j) + wloc;
+      const bool writer = (dw == 0) && (fr < 15) && (pw < kPW);
+      uint32_t pk[2][2], ab[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        ab[i] = 0;
+        float o4[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float v = best[i][j][r];
+          int ix = bidx[i][j][r] + dw;
+          const float v1 = __shfl_down(v, 1, 16), v2 = __shfl_down(v, 2, 16);
+          const int i1 = __shfl_down(ix, 1, 16), i2 = __shfl_down(ix, 2, 16);
+          if (v1 > v || (v1 == v && i1 < ix)) { v = v1; ix = i1; }
+          if (v2 > v || (v2 == v && i2 < ix)) { v = v2; ix = i2; }
+          o4[r] = fmaxf(v, 0.f);
+          ab[i] |= (uint32_t)ix << (8 * r);
+        }
+        pk[i][0] = pack_bf16x2(o4[0], o4[1]);
+        pk[i][1] = pack_bf16x2(o4[2], o4[3]);
+      }
+      if (writer) {
+        const int64_t o = ((((int64_t)n * kPD + pd) * kPH + ph) * kPW + pw) * kC1 + 32 * ch + 4 * fq;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          *reinterpret_cast<uint2*>(out + o + 16 * i) = make_uint2(pk[i][0], pk[i][1]);
+          *reinterpret_cast<uint32_t*>(amax + o + 16 * i) = ab[i];
+        }
+      }
+    }
+    if (ph + 1 < kPH) C1_STORE(cur ^ 1)
+    __syncthreads();
+  }
+#undef C1_LOAD
+#undef C1_STORE
+}
+
 void conv1_fwd_pool(uintptr_t x8, uintptr_t idx, uintptr_t w8, uintptr_t scale, uintptr_t shift, int NB, int B,
                     uintptr_t out, uintptr_t amax, uintptr_t stream) {
   NIDT_REQUIRE(NB % B == 0, "conv1_fwd_pool: NB % B");
-  hipLaunchKernelGGL(k_conv1_fwd_pool, dim3(kPH, kPD, NB), dim3(256), 0, as_stream(stream), ptr<const uint8_t>(x8),
+  hipLaunchKernelGGL(k_conv1_fwd_pool_pipe, dim3(kPD * NB), dim3(256), 0, as_stream(stream), ptr<const uint8_t>(x8),
                      ptr<const int>(idx), ptr<const uint16_t>(w8), ptr<const float>(scale), ptr<const float>(shift), B,
                      ptr<uint16_t>(out), ptr<uint8_t>(amax));
   NIDT_CHECK(hipGetLastError());

@@ -55,6 +55,112 @@ __device__ __forceinline__ uint4 xform8(uint4 v, const float* s, const float* t,
   return make_uint4(u[0], u[1], u[2], u[3]);
 }
 
+// Shared epilogue of the forward kernels: bias, bf16 store, per-block BN statistics (block mean + M2 per
+// channel).  C layout (16x16x32): C[row = 4*fq + r][col = fr]; rows = co, cols = positions.
+template <int BCO, bool BIAS, bool STATS, int TCO, int TP>
+__device__ __forceinline__ void conv_fwd_epilogue(const ConvFwdArgs& a, f32x4 (&acc)[TCO][TP], float* red, int g,
+                                                  int pb, int co0, int wco, int wp, int fr, int fq, int tid) {
+  constexpr int BP = kFwdBP;
+  constexpr int WCO = BCO / 2, WP = BP / 2;
+  float bias_r[TCO][4];
+#pragma unroll
+  for (int i = 0; i < TCO; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      bias_r[i][r] = BIAS ? a.bias[(int64_t)g * a.Cout + co0 + wco * WCO + i * 16 + 4 * fq + r] : 0.f;
+  const int posw = pb * BP + wp * WP + fr;
+#pragma unroll
+  for (int j = 0; j < TP; ++j) {
+    const int m = posw + j * 16;
+    if (m < a.Mg) {
+      uint16_t* yp = a.y + ((int64_t)g * a.Mg + m) * a.Cout + co0 + wco * WCO + 4 * fq;
+#pragma unroll
+      for (int i = 0; i < TCO; ++i) {
+        float v0 = acc[i][j][0] + bias_r[i][0], v1 = acc[i][j][1] + bias_r[i][1];
+        float v2 = acc[i][j][2] + bias_r[i][2], v3 = acc[i][j][3] + bias_r[i][3];
+        uint2 o = make_uint2(pack_bf16x2(v0, v1), pack_bf16x2(v2, v3));
+        *reinterpret_cast<uint2*>(yp + i * 16) = o;
+      }
+    }
+  }
+  if (STATS) {
+    // pass 1: block sums per channel (valid positions only)
+    // red: [2 (wp)][BCO] floats of LDS scratch
+    const int cnt = min(BP, a.Mg - pb * BP);
+    float s_[TCO][4];
+#pragma unroll
+    for (int i = 0; i < TCO; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float s = 0.f;
+#pragma unroll
+        for (int j = 0; j < TP; ++j)
+          if (posw + j * 16 < a.Mg) s += acc[i][j][r] + bias_r[i][r];
+        s += __shfl_xor(s, 1, 64);
+        s += __shfl_xor(s, 2, 64);
+        s += __shfl_xor(s, 4, 64);
+        s += __shfl_xor(s, 8, 64);
+        s_[i][r] = s;
+      }
+    __syncthreads();
+    if (fr == 0) {
+#pragma unroll
+      for (int i = 0; i < TCO; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) red[wp * BCO + wco * WCO + i * 16 + 4 * fq + r] = s_[i][r];
+    }
+    __syncthreads();
+    float mean_[TCO][4];
+#pragma unroll
+    for (int i = 0; i < TCO; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int c = wco * WCO + i * 16 + 4 * fq + r;
+        mean_[i][r] = (red[c] + red[BCO + c]) / (float)cnt;
+      }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < TCO; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float s = 0.f;
+#pragma unroll
+        for (int j = 0; j < TP; ++j)
+          if (posw + j * 16 < a.Mg) {
+            const float d = acc[i][j][r] + bias_r[i][r] - mean_[i][r];
+            s = fmaf(d, d, s);
+          }
+        s += __shfl_xor(s, 1, 64);
+        s += __shfl_xor(s, 2, 64);
+        s += __shfl_xor(s, 4, 64);
+        s += __shfl_xor(s, 8, 64);
+        s_[i][r] = s;
+      }
+    if (fr == 0) {
+#pragma unroll
+      for (int i = 0; i < TCO; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) red[wp * BCO + wco * WCO + i * 16 + 4 * fq + r] = s_[i][r];
+    }
+    __syncthreads();
+    for (int c = tid; c < BCO; c += 256) {
+      float* st = a.stats + (((int64_t)g * a.nPB + pb) * a.Cout + co0 + c) * 2;
+      // recompute mean for this channel from the first pass is not available here; store via second array
+      st[1] = red[c] + red[BCO + c];
+    }
+    // means: write by the owning lanes (every (wco, i, fq, r) channel is owned by the fr==0, wp==0 lanes)
+    if (fr == 0 && wp == 0) {
+#pragma unroll
+      for (int i = 0; i < TCO; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int c = wco * WCO + i * 16 + 4 * fq + r;
+          a.stats[(((int64_t)g * a.nPB + pb) * a.Cout + co0 + c) * 2] = mean_[i][r];
+        }
+    }
+  }
+}
+
 template <int BCO, bool XF, bool BIAS, bool STATS>
 __global__ __launch_bounds__(256, 2) void k_conv_fwd(ConvFwdArgs a) {
   constexpr int BP = kFwdBP;
@@ -158,105 +264,131 @@ __global__ __launch_bounds__(256, 2) void k_conv_fwd(ConvFwdArgs a) {
 #undef CONV_LOAD
 #undef CONV_STORE
 
-  // ---- epilogue: bias, bf16 store, per-block BN statistics ----
-  // C layout (16x16x32): C[row = 4*fq + r][col = fr]; rows = co, cols = positions.
-  float bias_r[TCO][4];
+  conv_fwd_epilogue<BCO, BIAS, STATS, TCO, TP>(a, acc, reinterpret_cast<float*>(&sB[0][0]), g, pb, co0, wco, wp, fr,
+                                               fq, tid);
+}
+
+// ------------------------------------------------------------------------------------------------
+// k_conv_fwd_dma — the Cin % 64 == 0 forward/dgrad path: BK = 64 (one tap x 64 channels per k-step, a
+// 128-B row per position / output channel), both tiles filled by global_load_lds (LDS-DMA, no staging
+// VGPRs, no ds_write).  The LDS image is lane-linear per wave instruction, so the bank swizzle
+// chunk' = chunk ^ ((row >> 1) & 7) is applied to the per-lane SOURCE address and undone on the
+// ds_read_b128 fragment reads (conflict-free for the 16x16x32 fragment pattern: each 16-lane group of a
+// b128 read touches 16 distinct 16-B bank slots).  Out-of-range taps (padding) and positions past the
+// end load from a zero page.  Per-row tap validity is a 27-bit mask computed once per block, so the
+// k-loop's address work is one 64-bit add + select per 16-B chunk.  1-D grid with the XCD remap: the
+// co-tiles of one position tile and neighbouring position tiles share an XCD's L2 (the 27 taps re-read
+// the same input rows).
+__device__ __attribute__((aligned(16))) uint4 g_zero_page[16];
+
+__device__ __forceinline__ int swz_dma(int r) { return (r >> 1) & 7; }
+
+__device__ __forceinline__ void glds16(const void* src, uint16_t* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(lds_wave_base), 16, 0, 0);
+}
+
+template <int BCO, bool BIAS, bool STATS>
+__global__ __launch_bounds__(256, 2) void k_conv_fwd_dma(ConvFwdArgs a, int nCO) {
+  constexpr int BP = kFwdBP, BK = 64;
+  constexpr int WCO = BCO / 2, WP = BP / 2;
+  constexpr int TCO = WCO / 16, TP = WP / 16;
+  constexpr int A_ELEMS = BCO * BK, B_ELEMS = BP * BK, BUF = A_ELEMS + B_ELEMS;
+  constexpr int A_INSTR = BCO / 32;  // 1-KB glds wave-instructions per wave for the A tile
+  __shared__ __attribute__((aligned(16))) uint16_t smem[2 * BUF];
+
+  const int nwg = gridDim.x;
+  const int id = xcd_remap(blockIdx.x, nwg);
+  const int cot = id % nCO, rest = id / nCO;
+  const int pb = rest % a.nPB, g = rest / a.nPB;
+  const int co0 = cot * BCO;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wco = wid >> 1, wp = wid & 1;
+  const int Cin = a.Cin, nck = Cin / BK, nks = 27 * nck;
+  const int lrow = lane >> 3, slot = lane & 7;
+
+  // ---- per-thread B rows: 4 rows (one per glds instruction), fixed over the k loop ----
+  const int S = a.Do * a.Ho * a.Wo;
+  int64_t roff[4];
+  uint32_t tmask[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = 32 * wid + 8 * i + lrow;
+    const int m = pb * BP + row;
+    tmask[i] = 0u;
+    roff[i] = 0;
+    if (m < a.Mg) {
+      const int nl = m / S, s = m - nl * S;
+      const int od = s / (a.Ho * a.Wo), r2 = s - od * a.Ho * a.Wo;
+      const int oh = r2 / a.Wo, ow = r2 - oh * a.Wo;
+      const int d0 = od - a.pad, h0 = oh - a.pad, w0 = ow - a.pad;
+      roff[i] = ((((int64_t)(g * a.B + nl) * a.D + d0) * a.H + h0) * a.W + w0) * Cin + ((slot ^ swz_dma(row)) << 3);
+      for (int t = 0; t < 27; ++t) {
+        const int id_ = d0 + t / 9, ih = h0 + (t / 3) % 3, iw = w0 + t % 3;
+        if (id_ >= 0 && id_ < a.D && ih >= 0 && ih < a.H && iw >= 0 && iw < a.W) tmask[i] |= 1u << t;
+      }
+    }
+  }
+  int64_t aoff[A_INSTR];
+#pragma unroll
+  for (int i = 0; i < A_INSTR; ++i) {
+    const int row = 8 * (wid * A_INSTR + i) + lrow;
+    aoff[i] = ((int64_t)g * a.Cout + co0 + row) * 27 * Cin + ((slot ^ swz_dma(row)) << 3);
+  }
+  const uint16_t* zp = reinterpret_cast<const uint16_t*>(g_zero_page);
+
+#define DMA_ISSUE(KS, BUFI)                                                                                   \
+  {                                                                                                           \
+    const int t_ = (KS) / nck, cc_ = (KS) - t_ * nck;                                                         \
+    const int64_t toff_ = ((((int64_t)(t_ / 9)) * a.H + (t_ / 3) % 3) * a.W + t_ % 3) * Cin + cc_ * BK;       \
+    uint16_t* sA_ = smem + (BUFI) * BUF;                                                                      \
+    uint16_t* sB_ = sA_ + A_ELEMS;                                                                            \
+    _Pragma("unroll") for (int i_ = 0; i_ < A_INSTR; ++i_)                                                    \
+      glds16(a.w + aoff[i_] + (int64_t)t_ * Cin + cc_ * BK, sA_ + (wid * A_INSTR + i_) * 512);                \
+    _Pragma("unroll") for (int i_ = 0; i_ < 4; ++i_) {                                                        \
+      const uint16_t* src_ = ((tmask[i_] >> t_) & 1u) ? a.x + roff[i_] + toff_ : zp;                          \
+      glds16(src_, sB_ + (4 * wid + i_) * 512);                                                               \
+    }                                                                                                         \
+  }
+
+  f32x4 acc[TCO][TP];
 #pragma unroll
   for (int i = 0; i < TCO; ++i)
 #pragma unroll
-    for (int r = 0; r < 4; ++r)
-      bias_r[i][r] = BIAS ? a.bias[(int64_t)g * a.Cout + co0 + wco * WCO + i * 16 + 4 * fq + r] : 0.f;
-  const int posw = pb * BP + wp * WP + fr;
+    for (int j = 0; j < TP; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int fr = lane & 15, fq = lane >> 4;
+  DMA_ISSUE(0, 0)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int ks = 0; ks < nks; ++ks) {
+    const int cur = ks & 1;
+    if (ks + 1 < nks) DMA_ISSUE(ks + 1, cur ^ 1)
+    const uint16_t* sA = smem + cur * BUF;
+    const uint16_t* sB = sA + A_ELEMS;
 #pragma unroll
-  for (int j = 0; j < TP; ++j) {
-    const int m = posw + j * 16;
-    if (m < a.Mg) {
-      uint16_t* yp = a.y + ((int64_t)g * a.Mg + m) * a.Cout + co0 + wco * WCO + 4 * fq;
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 fa[TCO], fb[TP];
 #pragma unroll
       for (int i = 0; i < TCO; ++i) {
-        float v0 = acc[i][j][0] + bias_r[i][0], v1 = acc[i][j][1] + bias_r[i][1];
-        float v2 = acc[i][j][2] + bias_r[i][2], v3 = acc[i][j][3] + bias_r[i][3];
-        uint2 o = make_uint2(pack_bf16x2(v0, v1), pack_bf16x2(v2, v3));
-        *reinterpret_cast<uint2*>(yp + i * 16) = o;
+        const int r = wco * WCO + i * 16 + fr;
+        fa[i] = *reinterpret_cast<const bf16x8*>(&sA[r * BK + (((4 * kk + fq) ^ swz_dma(r)) << 3)]);
       }
+#pragma unroll
+      for (int j = 0; j < TP; ++j) {
+        const int r = wp * WP + j * 16 + fr;
+        fb[j] = *reinterpret_cast<const bf16x8*>(&sB[r * BK + (((4 * kk + fq) ^ swz_dma(r)) << 3)]);
+      }
+#pragma unroll
+      for (int i = 0; i < TCO; ++i)
+#pragma unroll
+        for (int j = 0; j < TP; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
   }
-  if (STATS) {
-    // pass 1: block sums per channel (valid positions only)
-    float* red = reinterpret_cast<float*>(&sB[0][0]);  // [2 (wp)][BCO]
-    const int cnt = min(BP, a.Mg - pb * BP);
-    float s_[TCO][4];
-#pragma unroll
-    for (int i = 0; i < TCO; ++i)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        float s = 0.f;
-#pragma unroll
-        for (int j = 0; j < TP; ++j)
-          if (posw + j * 16 < a.Mg) s += acc[i][j][r] + bias_r[i][r];
-        s += __shfl_xor(s, 1, 64);
-        s += __shfl_xor(s, 2, 64);
-        s += __shfl_xor(s, 4, 64);
-        s += __shfl_xor(s, 8, 64);
-        s_[i][r] = s;
-      }
-    __syncthreads();
-    if (fr == 0) {
-#pragma unroll
-      for (int i = 0; i < TCO; ++i)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) red[wp * BCO + wco * WCO + i * 16 + 4 * fq + r] = s_[i][r];
-    }
-    __syncthreads();
-    float mean_[TCO][4];
-#pragma unroll
-    for (int i = 0; i < TCO; ++i)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int c = wco * WCO + i * 16 + 4 * fq + r;
-        mean_[i][r] = (red[c] + red[BCO + c]) / (float)cnt;
-      }
-    __syncthreads();
-#pragma unroll
-    for (int i = 0; i < TCO; ++i)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        float s = 0.f;
-#pragma unroll
-        for (int j = 0; j < TP; ++j)
-          if (posw + j * 16 < a.Mg) {
-            const float d = acc[i][j][r] + bias_r[i][r] - mean_[i][r];
-            s = fmaf(d, d, s);
-          }
-        s += __shfl_xor(s, 1, 64);
-        s += __shfl_xor(s, 2, 64);
-        s += __shfl_xor(s, 4, 64);
-        s += __shfl_xor(s, 8, 64);
-        s_[i][r] = s;
-      }
-    if (fr == 0) {
-#pragma unroll
-      for (int i = 0; i < TCO; ++i)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) red[wp * BCO + wco * WCO + i * 16 + 4 * fq + r] = s_[i][r];
-    }
-    __syncthreads();
-    for (int c = tid; c < BCO; c += 256) {
-      float* st = a.stats + (((int64_t)g * a.nPB + pb) * a.Cout + co0 + c) * 2;
-      // recompute mean for this channel from the first pass is not available here; store via second array
-      st[1] = red[c] + red[BCO + c];
-    }
-    // means: write by the owning lanes (every (wco, i, fq, r) channel is owned by the fr==0, wp==0 lanes)
-    if (fr == 0 && wp == 0) {
-#pragma unroll
-      for (int i = 0; i < TCO; ++i)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int c = wco * WCO + i * 16 + 4 * fq + r;
-          a.stats[(((int64_t)g * a.nPB + pb) * a.Cout + co0 + c) * 2] = mean_[i][r];
-        }
-    }
-  }
+#undef DMA_ISSUE
+  float* red = reinterpret_cast<float*>(smem);
+  conv_fwd_epilogue<BCO, BIAS, STATS, TCO, TP>(a, acc, red, g, pb, co0, wco, wp, fr, fq, tid);
 }
 
 void conv3d_fwd(uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t xs, uintptr_t xt, uintptr_t y, uintptr_t stats,
@@ -274,8 +406,23 @@ void conv3d_fwd(uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t xs, uintptr_
   a.nPB = ceil_div(a.Mg, kFwdBP);
   const bool xf = xs != 0, hb = bias != 0, st = stats != 0;
   const int bco = (Cout % 128 == 0) ? 128 : 64;
-  dim3 grid(a.nPB, Cout / bco, G);
   hipStream_t s = as_stream(stream);
+  if (!xf && Cin % 64 == 0) {
+    const int nCO = Cout / bco;
+    const int64_t nwg = (int64_t)a.nPB * nCO * G;
+    NIDT_REQUIRE(nwg < (1ll << 31), "conv3d_fwd: grid too large");
+    dim3 g1((unsigned)nwg);
+#define NIDT_DMA(BC, BI, ST) hipLaunchKernelGGL((k_conv_fwd_dma<BC, BI, ST>), g1, dim3(256), 0, s, a, nCO)
+    if (bco == 128) {
+      if (st) NIDT_DMA(128, true, true); else if (hb) NIDT_DMA(128, true, false); else NIDT_DMA(128, false, false);
+    } else {
+      if (st) NIDT_DMA(64, true, true); else if (hb) NIDT_DMA(64, true, false); else NIDT_DMA(64, false, false);
+    }
+#undef NIDT_DMA
+    NIDT_CHECK(hipGetLastError());
+    return;
+  }
+  dim3 grid(a.nPB, Cout / bco, G);
 #define NIDT_FWD(BC, X, BI, ST) hipLaunchKernelGGL((k_conv_fwd<BC, X, BI, ST>), grid, dim3(256), 0, s, a)
   if (bco == 128) {
     if (xf) { if (st) NIDT_FWD(128, true, true, true); else if (hb) NIDT_FWD(128, true, true, false); else NIDT_FWD(128, true, false, false); }
@@ -470,9 +617,163 @@ int conv3d_wgrad_nsplit(int G, int B, int D, int H, int W, int Cin, int Cout, in
   return max(1, min(ns, maxns));
 }
 
+// ------------------------------------------------------------------------------------------------
+// k_conv_wgrad_dma — dW[co][k] = sum_pos dY[pos][co] * X[pos + tap(k)][ci(k)], 64 positions per k-step,
+// both tiles filled by global_load_lds.  A block owns 64 co x 256 k-cols = 4 "groups" of 64 k-cols (each
+// group is one tap x 64 input channels, a 128-B row per position, so every glds wave-instruction reads
+// 8 whole 128-B rows: coalesced).  Wave w stages X group w (8 instructions, rows 8i + lane/8) and two of
+// the eight 8-row slices of dY.  The MFMA operands want the position axis in the k slots: they are read
+// with ds_read_b64_tr_b16 (4 positions x 4 channels per lane).  Rows are 128 B, so the 16-B chunk index is
+// XORed with f(r) = bit1(r)<<1 | bit3(r)<<2 (applied to the glds SOURCE address, undone on the read): every
+// 32-lane group of a tr read then hits 32 distinct 8-B bank slots.  Position table (k_conv_pos_table): per
+// client-local output position, the input-voxel offset of tap 0 and the 27-bit in-bounds tap mask; one
+// global load per lane per step, distributed to the 8 rows a lane stages with __shfl.
+struct ConvWgDmaArgs {
+  const uint16_t* x;    // [G*B, D, H, W, Cin]
+  const uint16_t* dy;   // [G*B, Do, Ho, Wo, Cout] == [G, Mg, Cout]
+  const int2* ptab;     // [Mg] {input voxel offset of tap (0,0,0) relative to the client's first voxel, tap mask}
+  float* part;          // [nsplit, G, Cout, K]
+  int D, H, W, Cin, Cout, Mg, K, nsplit, chunk, G, nKT, nCT;
+  int64_t xclient;      // elements per client in x (B*D*H*W*Cin)
+};
+
+__global__ void k_conv_pos_table(int2* tab, int Mg, int D, int H, int W, int pad) {
+  const int m = blockIdx.x * blockDim.x + threadIdx.x;
+  if (m >= Mg) return;
+  const int Do = D + 2 * pad - 2, Ho = H + 2 * pad - 2, Wo = W + 2 * pad - 2, S = Do * Ho * Wo;
+  const int nl = m / S, s = m - nl * S;
+  const int od = s / (Ho * Wo), r = s - od * Ho * Wo, oh = r / Wo, ow = r - oh * Wo;
+  const int d0 = od - pad, h0 = oh - pad, w0 = ow - pad;
+  uint32_t mask = 0;
+  for (int t = 0; t < 27; ++t) {
+    const int id = d0 + t / 9, ih = h0 + (t / 3) % 3, iw = w0 + t % 3;
+    if (id >= 0 && id < D && ih >= 0 && ih < H && iw >= 0 && iw < W) mask |= 1u << t;
+  }
+  tab[m] = make_int2(((nl * D + d0) * H + h0) * W + w0, (int)mask);
+}
+
+constexpr int kWdPos = 64;                       // positions per k-step
+constexpr int kWdRow = 64;                       // bf16 per 128-B row
+constexpr int kWdGroup = kWdPos * kWdRow;        // one 64-col group: 8 KB
+constexpr int kWdBuf = 5 * kWdGroup;             // 4 X groups + dY
+__device__ __forceinline__ int swz_wd(int r) { return (r & 2) | ((r >> 1) & 4); }
+
+__global__ __launch_bounds__(256, 2) void k_conv_wgrad_dma(ConvWgDmaArgs a) {
+  __shared__ __attribute__((aligned(16))) uint16_t smem[2 * kWdBuf];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int id = xcd_remap(blockIdx.x, gridDim.x);
+  const int kt = id % a.nKT, r1 = id / a.nKT;
+  const int ct = r1 % a.nCT, r2 = r1 / a.nCT;
+  const int sp = r2 % a.nsplit, g = r2 / a.nsplit;
+  const int kc0 = kt * kWgKC, co0 = ct * kWgCO;
+  const int p_begin = sp * a.chunk, p_end = min(a.Mg, p_begin + a.chunk);
+  const int Cin = a.Cin;
+  const uint16_t* zp = reinterpret_cast<const uint16_t*>(g_zero_page);
+  const uint16_t* xg = a.x + (int64_t)g * a.xclient;
+  // this wave's X group: k-cols kc0 + 64w .. +63 = one tap, 64 channels
+  const int kg = kc0 + 64 * wid;
+  const bool gval = kg < a.K;
+  const int gtap = gval ? kg / Cin : 31;  // 31: never set in a tap mask -> zero page
+  const int gcol = gval ? (((gtap / 9) * a.H + (gtap / 3) % 3) * a.W + gtap % 3) * Cin + (kg - gtap * Cin) : 0;
+  const int lr = lane >> 3, ls = lane & 7;
+  int2 tnext = make_int2(0, 0);
+#define WD_FETCH(P0)                                                                                          \
+  {                                                                                                           \
+    const int m_ = (P0) + lane;                                                                               \
+    tnext = m_ < p_end ? a.ptab[m_] : make_int2(0, 0);                                                        \
+  }
+#define WD_ISSUE(P0, BUFI)                                                                                    \
+  {                                                                                                           \
+    uint16_t* sX_ = smem + (BUFI) * kWdBuf + wid * kWdGroup;                                                  \
+    uint16_t* sD_ = smem + (BUFI) * kWdBuf + 4 * kWdGroup;                                                    \
+    _Pragma("unroll") for (int i_ = 0; i_ < 8; ++i_) {                                                        \
+      const int r_ = 8 * i_ + lr;                                                                             \
+      const int off_ = __shfl(tnext.x, r_, 64), msk_ = __shfl(tnext.y, r_, 64);                               \
+      const bool ok_ = ((P0) + r_ < p_end) && ((msk_ >> gtap) & 1);                                           \
+      const uint16_t* src_ = ok_ ? xg + (int64_t)off_ * Cin + gcol + ((ls ^ swz_wd(r_)) << 3) : zp;           \
+      glds16(src_, sX_ + i_ * 512);                                                                           \
+    }                                                                                                         \
+    _Pragma("unroll") for (int i_ = 0; i_ < 2; ++i_) {                                                        \
+      const int r_ = 8 * (2 * wid + i_) + lr;                                                                 \
+      const int m_ = (P0) + r_;                                                                               \
+      const uint16_t* src_ = m_ < p_end ? a.dy + ((int64_t)g * a.Mg + m_) * a.Cout + co0 + ((ls ^ swz_wd(r_)) << 3) : zp; \
+      glds16(src_, sD_ + (2 * wid + i_) * 512);                                                               \
+    }                                                                                                         \
+  }
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // transposed reads: 16-lane group gq covers positions 8gq..8gq+7 (two 4-row reads); lane 4qq+pp reads row qq,
+  // columns 4pp..4pp+3 of a 16-column segment s = chunks 2s + (pp >> 1), half (pp & 1).
+  const int gq = lane >> 4, li = lane & 15, qq = li >> 2, pp = li & 3;
+  const int rr0 = 8 * gq + qq, rr1 = rr0 + 4;
+  const int nsteps = (p_end - p_begin + kWdPos - 1) / kWdPos;
+  if (nsteps > 0) {
+    WD_FETCH(p_begin)
+    WD_ISSUE(p_begin, 0)
+    if (nsteps > 1) WD_FETCH(p_begin + kWdPos)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  for (int st = 0; st < nsteps; ++st) {
+    const int cur = st & 1;
+    if (st + 1 < nsteps) {
+      WD_ISSUE(p_begin + kWdPos * (st + 1), cur ^ 1)
+      if (st + 2 < nsteps) WD_FETCH(p_begin + kWdPos * (st + 2))
+    }
+    const uint16_t* sX = smem + cur * kWdBuf + wid * kWdGroup;
+    const uint16_t* sD = smem + cur * kWdBuf + 4 * kWdGroup;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {  // two 32-position MFMA k-steps
+      const int ra = 32 * kk + rr0, rb = 32 * kk + rr1;
+      bf16x8 fa[4], fb[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int c = 2 * i + (pp >> 1);
+        fa[i] = tr_pair(sD + ra * kWdRow + ((c ^ swz_wd(ra)) << 3) + (pp & 1) * 4,
+                        sD + rb * kWdRow + ((c ^ swz_wd(rb)) << 3) + (pp & 1) * 4);
+        fb[i] = tr_pair(sX + ra * kWdRow + ((c ^ swz_wd(ra)) << 3) + (pp & 1) * 4,
+                        sX + rb * kWdRow + ((c ^ swz_wd(rb)) << 3) + (pp & 1) * 4);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+#undef WD_ISSUE
+#undef WD_FETCH
+  const int fr = lane & 15, fq = lane >> 4;
+  float* out = a.part + (((int64_t)sp * a.G + g) * a.Cout + co0) * a.K;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int k = kc0 + 64 * wid + 16 * j + fr;
+    if (k < a.K) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) out[(int64_t)(16 * i + 4 * fq + r) * a.K + k] = acc[i][j][r];
+    }
+  }
+}
+
+void conv3d_pos_table(uintptr_t tab, int B, int D, int H, int W, int pad, uintptr_t stream) {
+  const int Mg = B * (D + 2 * pad - 2) * (H + 2 * pad - 2) * (W + 2 * pad - 2);
+  NIDT_REQUIRE((int64_t)B * D * H * W < (1ll << 31), "conv3d_pos_table: volume too large for 32-bit offsets");
+  hipLaunchKernelGGL(k_conv_pos_table, dim3(ceil_div(Mg, 256)), dim3(256), 0, as_stream(stream), ptr<int2>(tab), Mg,
+                     D, H, W, pad);
+  NIDT_CHECK(hipGetLastError());
+}
+
 void conv3d_wgrad(uintptr_t x, uintptr_t xs, uintptr_t xt, uintptr_t dy, uintptr_t part, uintptr_t grad, int64_t ldg,
                   int64_t off, int G, int B, int D, int H, int W, int Cin, int Cout, int pad, int nsplit, float scale,
-                  uintptr_t stream) {
+                  uintptr_t ptab, uintptr_t stream) {
   NIDT_REQUIRE(Cin % 64 == 0 && Cin <= 192, "conv3d_wgrad: Cin must be a multiple of 64 and <= 192");
   NIDT_REQUIRE(Cout % kWgCO == 0, "conv3d_wgrad: Cout must be a multiple of 64");
   ConvWgArgs a;
@@ -484,10 +785,22 @@ void conv3d_wgrad(uintptr_t x, uintptr_t xs, uintptr_t xt, uintptr_t dy, uintptr
   a.K = 27 * Cin;
   a.nsplit = nsplit;
   a.chunk = ((ceil_div(a.Mg, nsplit) + 31) / 32) * 32;
-  dim3 grid(ceil_div(a.K, kWgKC), Cout / kWgCO, G * nsplit);
   hipStream_t s = as_stream(stream);
-  if (xs) hipLaunchKernelGGL((k_conv_wgrad<true>), grid, dim3(256), 0, s, a);
-  else hipLaunchKernelGGL((k_conv_wgrad<false>), grid, dim3(256), 0, s, a);
+  if (ptab && !xs) {
+    ConvWgDmaArgs d;
+    d.x = a.x; d.dy = a.dy; d.ptab = ptr<const int2>(ptab); d.part = a.part;
+    d.D = D; d.H = H; d.W = W; d.Cin = Cin; d.Cout = Cout; d.Mg = a.Mg; d.K = a.K; d.nsplit = nsplit; d.G = G;
+    d.chunk = ((ceil_div(a.Mg, nsplit) + kWdPos - 1) / kWdPos) * kWdPos;
+    d.nKT = ceil_div(a.K, kWgKC); d.nCT = Cout / kWgCO;
+    d.xclient = (int64_t)B * D * H * W * Cin;
+    const int64_t nwg = (int64_t)d.nKT * d.nCT * nsplit * G;
+    NIDT_REQUIRE(nwg < (1ll << 31), "conv3d_wgrad: grid too large");
+    hipLaunchKernelGGL(k_conv_wgrad_dma, dim3((unsigned)nwg), dim3(256), 0, s, d);
+  } else {
+    dim3 grid(ceil_div(a.K, kWgKC), Cout / kWgCO, G * nsplit);
+    if (xs) hipLaunchKernelGGL((k_conv_wgrad<true>), grid, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((k_conv_wgrad<false>), grid, dim3(256), 0, s, a);
+  }
   NIDT_CHECK(hipGetLastError());
   hipLaunchKernelGGL(k_wgrad_reduce, dim3(Cout, G), dim3(256), 0, s, ptr<const float>(part), nsplit, G, Cout, Cin,
                      ptr<float>(grad), ldg, off, scale);

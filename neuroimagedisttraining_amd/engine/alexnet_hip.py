@@ -84,6 +84,12 @@ class HipAlexNet3D:
                 bnpart=e(G * 64 * 256 * 2, dt=f32), coef=e(G, 192, 3, dt=f32),
                 c1part=e(NB * 19, 64, 126, dt=f32),
             )
+            # per-layer output-position tables for the LDS-DMA wgrad kernel (shared by all clients and steps)
+            st0 = torch.cuda.current_stream().cuda_stream
+            for (ci, bi, cin, cout, pad, sp) in (L2, L3, L4, L5):
+                mg = B * (sp[0] + 2 * pad - 2) * (sp[1] + 2 * pad - 2) * (sp[2] + 2 * pad - 2)
+                b["pt%d" % ci] = e(mg, 2, dt=torch.int32)
+                self.m.conv3d_pos_table(_p(b["pt%d" % ci]), B, sp[0], sp[1], sp[2], pad, st0)
         self._cache[key] = b
         return b
 
@@ -188,7 +194,7 @@ class HipAlexNet3D:
 
         def wgrad(ci, x, xs, xt, dy, sp, cin, cout, pad):
             m.conv3d_wgrad(_p(x), _p(xs), _p(xt), _p(dy), _p(b["wgpart"]), _p(grads), P, o["features.%d.weight" % ci],
-                           G, B, sp[0], sp[1], sp[2], cin, cout, pad, b["ns%d" % ci], 1.0, st)
+                           G, B, sp[0], sp[1], sp[2], cin, cout, pad, b["ns%d" % ci], 1.0, _p(b["pt%d" % ci]), st)
 
         # layer 5: pool5 -> BN5 -> conv5
         bn_bwd(1, 14, 15, 128, (5, 7, 5), b["dp5"], b["p5"], b["a5"], b["dy5"], b["y5"])

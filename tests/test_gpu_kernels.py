@@ -106,8 +106,17 @@ def test_conv3d_wgrad_and_dgrad(cin, cout, pad, sp, xf):
     grad = torch.zeros(G, P, device=DEV)
     ns = m.conv3d_wgrad_nsplit(G, B, *sp, cin, cout, pad)
     part = torch.empty(ns * G * cout * 27 * cin, device=DEV)
+    Mg = B * Do * Ho * Wo
+    ptab = torch.empty(Mg, 2, device=DEV, dtype=torch.int32)
+    m.conv3d_pos_table(ptab.data_ptr(), B, *sp, pad, _st())
     m.conv3d_wgrad(x.data_ptr(), xs.data_ptr() if xf else 0, xt.data_ptr() if xf else 0, dy.data_ptr(), part.data_ptr(),
-                   grad.data_ptr(), P, 3, G, B, *sp, cin, cout, pad, ns, 1.0, _st())
+                   grad.data_ptr(), P, 3, G, B, *sp, cin, cout, pad, ns, 1.0, ptab.data_ptr(), _st())
+    if not xf:  # the register-staged fallback kernel must agree with the LDS-DMA one
+        grad0 = torch.zeros_like(grad)
+        m.conv3d_wgrad(x.data_ptr(), 0, 0, dy.data_ptr(), part.data_ptr(), grad0.data_ptr(), P, 3, G, B, *sp, cin,
+                       cout, pad, ns, 1.0, 0, _st())
+        torch.cuda.synchronize()
+        assert _relerr(grad0, grad) < 1e-5
     # dgrad through the fwd kernel with flipped/transposed weights (packed from fp32 PyTorch layout)
     wt32 = torch.randn(G, cout, cin, 3, 3, 3, device=DEV) * 0.05
     theta = wt32.view(G, -1).contiguous()

@@ -89,7 +89,7 @@ def main():
             p(b[dys[ci]]), p(b["w%dt" % ci]), 0, 0, 0, p(b[dxs[ci]]), 0, G, B, *Do, cout, cin, 2 - pad, st), fl)
         add(name + "_wgrad", lambda xin=xin, ci=ci, sp=sp, cin=cin, cout=cout, pad=pad: m.conv3d_wgrad(
             p(b[xin]), 0, 0, p(b[dys[ci]]), p(b["wgpart"]), p(grads), P, o["features.%d.weight" % ci], G, B, *sp, cin,
-            cout, pad, b["ns%d" % ci], 1.0, st), fl)
+            cout, pad, b["ns%d" % ci], 1.0, p(b["pt%d" % ci]), st), fl)
     tot = sum(r[1] for r in rows)
     print("G=%d B=%d  full train step %.3f ms  (sum of timed kernels %.3f ms)" % (G, B, t_step, tot))
     for name, t, tf in rows:
