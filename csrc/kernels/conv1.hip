@@ -693,13 +693,132 @@ __global__ __launch_bounds__(128) void k_conv1_wgrad_fin(const float* __restrict
   }
 }
 
+// k_conv1_wgrad_split — the sparse wgrad with the 125 taps split over the 4 waves instead of the cells:
+// every wave walks all cells of the slab for its channel (lane) but accumulates only its ~31 taps, so the
+// accumulators shrink from 125 to <= 32 VGPRs (4+ waves/SIMD instead of 2, which hides the LDS and L2
+// latency of the per-lane argmax gathers) and no cross-wave reduction is needed: each wave writes its own
+// disjoint taps of the slab row.  Polyphase offsets t = 9jd+3jh+jw carry 8/4/2/1 valid taps (j=2 drops
+// the odd phase in that dimension); the sets below balance taps (32/32/30/31).
+__device__ constexpr int kWgSet0[] = {0, 1, 3, 4};
+__device__ constexpr int kWgSet1[] = {9, 10, 12, 13};
+__device__ constexpr int kWgSet2[] = {2, 5, 11, 14, 6, 7, 15, 8};
+__device__ constexpr int kWgSet3[] = {16, 18, 19, 21, 22, 17, 20, 23, 24, 25, 26};
+template <int W> struct WgSet;
+template <> struct WgSet<0> { static constexpr int n = 4; __device__ static constexpr int t(int i) { return kWgSet0[i]; } };
+template <> struct WgSet<1> { static constexpr int n = 4; __device__ static constexpr int t(int i) { return kWgSet1[i]; } };
+template <> struct WgSet<2> { static constexpr int n = 8; __device__ static constexpr int t(int i) { return kWgSet2[i]; } };
+template <> struct WgSet<3> { static constexpr int n = 11; __device__ static constexpr int t(int i) { return kWgSet3[i]; } };
+
+__host__ __device__ constexpr int tp_count(int t) {
+  return (t / 9 < 2 ? 2 : 1) * ((t / 3) % 3 < 2 ? 2 : 1) * (t % 3 < 2 ? 2 : 1);
+}
+
+template <int W>
+__device__ __forceinline__ void conv1_wg_wave(const uint8_t* __restrict__ xs, const uint16_t* __restrict__ dp,
+                                              const uint16_t* __restrict__ pout, const uint8_t* __restrict__ amax,
+                                              float* __restrict__ part, uint2* halo, int n, int pd, int tid, int c) {
+  using SET = WgSet<W>;
+  constexpr int NS = 32;  // >= taps of any set
+  float S[NS];
+#pragma unroll
+  for (int k = 0; k < NS; ++k) S[k] = 0.f;
+  float Dsum = 0.f;
+  const int64_t rowbase = ((int64_t)n * kPD + pd) * kPH;
+  for (int ph0 = 0; ph0 < kPH; ph0 += kWgRows) {
+    const int nph = min(kWgRows, kPH - ph0);
+    const int ny = 3 * nph + 2;
+    __syncthreads();
+    for (int e = tid; e < 5 * ny * 64; e += 256) {
+      const int xh = e & 63, r = e >> 6, yh = r % ny, zh = r / ny;
+      const int z = 3 * pd + zh, y = 3 * ph0 + yh;
+      uint2 v = make_uint2(0, 0);
+      if (xh < kPX) v = *reinterpret_cast<const uint2*>(xs + (((int64_t)z * kPY + y) * kPX + xh) * 8);
+      halo[zh * kWgZS + yh * kWgRS + xh] = v;
+    }
+    __syncthreads();
+    const int ncell = nph * kPW;
+    int64_t o = ((rowbase + ph0) * kPW) * kC1 + c;
+    uint16_t pv_n = pout[o], dp_n = dp[o];
+    uint8_t a_n = amax[o];
+    for (int it = 0; it < ncell; ++it) {
+      const uint16_t pv_c = pv_n, dp_c = dp_n;
+      const int a = a_n;
+      if (it + 1 < ncell) {
+        const int64_t on = o + kC1;
+        pv_n = pout[on];
+        dp_n = dp[on];
+        a_n = amax[on];
+      }
+      o += kC1;
+      const int phl = it / kPW, pw = it - phl * kPW;
+      const float dz = bf16_to_f32(pv_c) > 0.f ? bf16_to_f32(dp_c) : 0.f;
+      if (W == 0) Dsum += dz;
+      const int ad = a / 9, ah = (a / 3) % 3, aw = a % 3;
+      const uint2* base = halo + ad * kWgZS + (3 * phl + ah) * kWgRS + 3 * pw + aw;
+      uint2 u[SET::n];
+#pragma unroll
+      for (int i = 0; i < SET::n; ++i) {
+        constexpr int dummy = 0;
+        (void)dummy;
+        const int t = SET::t(i);
+        u[i] = base[(t / 9) * kWgZS + ((t / 3) % 3) * kWgRS + t % 3];
+      }
+      int slot = 0;
+#pragma unroll
+      for (int i = 0; i < SET::n; ++i) {
+        const int t = SET::t(i);
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+          if (tp_valid(t, r)) {
+            const uint32_t w = r < 4 ? u[i].x : u[i].y;
+            S[slot] = fmaf(dz, (float)((w >> (8 * (r & 3))) & 0xffu), S[slot]);
+            ++slot;
+          }
+        }
+      }
+    }
+  }
+  float* op = part + (((int64_t)n * kPD + pd) * kC1 + c) * 126;
+  int slot = 0;
+#pragma unroll
+  for (int i = 0; i < SET::n; ++i) {
+    const int t = SET::t(i);
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      if (tp_valid(t, r)) {
+        op[tp_to_k(t, r)] = S[slot];
+        ++slot;
+      }
+    }
+  }
+  if (W == 0) op[125] = Dsum;
+}
+
+__global__ __launch_bounds__(256) void k_conv1_wgrad_split(const uint8_t* __restrict__ x8, const int* __restrict__ idx,
+                                                           const uint16_t* __restrict__ dp,
+                                                           const uint16_t* __restrict__ pout,
+                                                           const uint8_t* __restrict__ amax, float* __restrict__ part) {
+  __shared__ __attribute__((aligned(16))) uint2 halo[kWgHalo];
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int pd = bid % kPD, n = bid / kPD;
+  const int tid = threadIdx.x, c = tid & 63, wid = tid >> 6;
+  const uint8_t* xs = x8 + (int64_t)idx[n] * kPZ * kPY * kPX * 8;
+  switch (wid) {
+    case 0: conv1_wg_wave<0>(xs, dp, pout, amax, part, halo, n, pd, tid, c); break;
+    case 1: conv1_wg_wave<1>(xs, dp, pout, amax, part, halo, n, pd, tid, c); break;
+    case 2: conv1_wg_wave<2>(xs, dp, pout, amax, part, halo, n, pd, tid, c); break;
+    default: conv1_wg_wave<3>(xs, dp, pout, amax, part, halo, n, pd, tid, c); break;
+  }
+}
+
 void conv1_wgrad(uintptr_t x8, uintptr_t idx, uintptr_t dp, uintptr_t pout, uintptr_t amax, int NB, int B,
                  uintptr_t part, uintptr_t w125, uintptr_t mu, uintptr_t covw, uintptr_t invstd, uintptr_t theta,
                  int64_t ldt, int64_t off_g, uintptr_t grad, int64_t ldg, int64_t goff_w, int64_t goff_bias,
                  int64_t goff_g, int64_t goff_b, float wscale, uintptr_t stream) {
   hipStream_t s = as_stream(stream);
-  hipLaunchKernelGGL(k_conv1_wgrad, dim3(kPD, NB), dim3(256), 0, s, ptr<const uint8_t>(x8), ptr<const int>(idx),
-                     ptr<const uint16_t>(dp), ptr<const uint16_t>(pout), ptr<const uint8_t>(amax), ptr<float>(part));
+  hipLaunchKernelGGL(k_conv1_wgrad_split, dim3(kPD * NB), dim3(256), 0, s, ptr<const uint8_t>(x8),
+                     ptr<const int>(idx), ptr<const uint16_t>(dp), ptr<const uint16_t>(pout), ptr<const uint8_t>(amax),
+                     ptr<float>(part));
   NIDT_CHECK(hipGetLastError());
   const int G = NB / B;
   hipLaunchKernelGGL(k_conv1_wgrad_fin, dim3(kC1, G), dim3(128), 0, s, ptr<const float>(part), B,
