@@ -57,11 +57,10 @@ __device__ __forceinline__ uint4 xform8(uint4 v, const float* s, const float* t,
 
 // Shared epilogue of the forward kernels: bias, bf16 store, per-block BN statistics (block mean + M2 per
 // channel).  C layout (16x16x32): C[row = 4*fq + r][col = fr]; rows = co, cols = positions.
-template <int BCO, bool BIAS, bool STATS, int TCO, int TP>
+template <int BCO, int BP, int WM, int WN, bool BIAS, bool STATS, int TCO, int TP>
 __device__ __forceinline__ void conv_fwd_epilogue(const ConvFwdArgs& a, f32x4 (&acc)[TCO][TP], float* red, int g,
                                                   int pb, int co0, int wco, int wp, int fr, int fq, int tid) {
-  constexpr int BP = kFwdBP;
-  constexpr int WCO = BCO / 2, WP = BP / 2;
+  constexpr int WCO = BCO / WM, WP = BP / WN;
   float bias_r[TCO][4];
 #pragma unroll
   for (int i = 0; i < TCO; ++i)
@@ -85,7 +84,7 @@ __device__ __forceinline__ void conv_fwd_epilogue(const ConvFwdArgs& a, f32x4 (&
   }
   if (STATS) {
     // pass 1: block sums per channel (valid positions only)
-    // red: [2 (wp)][BCO] floats of LDS scratch
+    // red: [WN (wp)][BCO] floats of LDS scratch
     const int cnt = min(BP, a.Mg - pb * BP);
     float s_[TCO][4];
 #pragma unroll
@@ -116,7 +115,10 @@ __device__ __forceinline__ void conv_fwd_epilogue(const ConvFwdArgs& a, f32x4 (&
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int c = wco * WCO + i * 16 + 4 * fq + r;
-        mean_[i][r] = (red[c] + red[BCO + c]) / (float)cnt;
+        float t = 0.f;
+#pragma unroll
+        for (int q = 0; q < WN; ++q) t += red[q * BCO + c];
+        mean_[i][r] = t / (float)cnt;
       }
     __syncthreads();
 #pragma unroll
@@ -146,7 +148,10 @@ __device__ __forceinline__ void conv_fwd_epilogue(const ConvFwdArgs& a, f32x4 (&
     for (int c = tid; c < BCO; c += 256) {
       float* st = a.stats + (((int64_t)g * a.nPB + pb) * a.Cout + co0 + c) * 2;
       // recompute mean for this channel from the first pass is not available here; store via second array
-      st[1] = red[c] + red[BCO + c];
+      float t = 0.f;
+#pragma unroll
+      for (int q = 0; q < WN; ++q) t += red[q * BCO + c];
+      st[1] = t;
     }
     // means: write by the owning lanes (every (wco, i, fq, r) channel is owned by the fr==0, wp==0 lanes)
     if (fr == 0 && wp == 0) {
@@ -264,8 +269,8 @@ __global__ __launch_bounds__(256, 2) void k_conv_fwd(ConvFwdArgs a) {
 #undef CONV_LOAD
 #undef CONV_STORE
 
-  conv_fwd_epilogue<BCO, BIAS, STATS, TCO, TP>(a, acc, reinterpret_cast<float*>(&sB[0][0]), g, pb, co0, wco, wp, fr,
-                                               fq, tid);
+  conv_fwd_epilogue<BCO, BP, 2, 2, BIAS, STATS, TCO, TP>(a, acc, reinterpret_cast<float*>(&sB[0][0]), g, pb, co0,
+                                                         wco, wp, fr, fq, tid);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -287,13 +292,15 @@ __device__ __forceinline__ void glds16(const void* src, uint16_t* lds_wave_base)
   __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(lds_wave_base), 16, 0, 0);
 }
 
-template <int BCO, bool BIAS, bool STATS>
+template <int BCO, int WN, bool BIAS, bool STATS>
 __global__ __launch_bounds__(256, 2) void k_conv_fwd_dma(ConvFwdArgs a, int nCO) {
-  constexpr int BP = kFwdBP, BK = 64;
-  constexpr int WCO = BCO / 2, WP = BP / 2;
+  // waves: WM (co) x WN (positions); each wave owns (BCO/WM) co x 64 positions
+  constexpr int WM = 4 / WN, BP = 64 * WN, BK = 64;
+  constexpr int WCO = BCO / WM, WP = 64;
   constexpr int TCO = WCO / 16, TP = WP / 16;
   constexpr int A_ELEMS = BCO * BK, B_ELEMS = BP * BK, BUF = A_ELEMS + B_ELEMS;
   constexpr int A_INSTR = BCO / 32;  // 1-KB glds wave-instructions per wave for the A tile
+  constexpr int B_INSTR = BP / 32;   // ... and for the B tile (8 rows each)
   __shared__ __attribute__((aligned(16))) uint16_t smem[2 * BUF];
 
   const int nwg = gridDim.x;
@@ -302,17 +309,17 @@ __global__ __launch_bounds__(256, 2) void k_conv_fwd_dma(ConvFwdArgs a, int nCO)
   const int pb = rest % a.nPB, g = rest / a.nPB;
   const int co0 = cot * BCO;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wco = wid >> 1, wp = wid & 1;
+  const int wco = wid / WN, wp = wid % WN;
   const int Cin = a.Cin, nck = Cin / BK, nks = 27 * nck;
   const int lrow = lane >> 3, slot = lane & 7;
 
-  // ---- per-thread B rows: 4 rows (one per glds instruction), fixed over the k loop ----
+  // ---- per-thread B rows: one per glds instruction, fixed over the k loop ----
   const int S = a.Do * a.Ho * a.Wo;
-  int64_t roff[4];
-  uint32_t tmask[4];
+  int64_t roff[B_INSTR];
+  uint32_t tmask[B_INSTR];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int row = 32 * wid + 8 * i + lrow;
+  for (int i = 0; i < B_INSTR; ++i) {
+    const int row = 8 * (B_INSTR * wid + i) + lrow;
     const int m = pb * BP + row;
     tmask[i] = 0u;
     roff[i] = 0;
@@ -344,9 +351,9 @@ __global__ __launch_bounds__(256, 2) void k_conv_fwd_dma(ConvFwdArgs a, int nCO)
     uint16_t* sB_ = sA_ + A_ELEMS;                                                                            \
     _Pragma("unroll") for (int i_ = 0; i_ < A_INSTR; ++i_)                                                    \
       glds16(a.w + aoff[i_] + (int64_t)t_ * Cin + cc_ * BK, sA_ + (wid * A_INSTR + i_) * 512);                \
-    _Pragma("unroll") for (int i_ = 0; i_ < 4; ++i_) {                                                        \
+    _Pragma("unroll") for (int i_ = 0; i_ < B_INSTR; ++i_) {                                                  \
       const uint16_t* src_ = ((tmask[i_] >> t_) & 1u) ? a.x + roff[i_] + toff_ : zp;                          \
-      glds16(src_, sB_ + (4 * wid + i_) * 512);                                                               \
+      glds16(src_, sB_ + (B_INSTR * wid + i_) * 512);                                                         \
     }                                                                                                         \
   }
 
@@ -388,7 +395,7 @@ __global__ __launch_bounds__(256, 2) void k_conv_fwd_dma(ConvFwdArgs a, int nCO)
   }
 #undef DMA_ISSUE
   float* red = reinterpret_cast<float*>(smem);
-  conv_fwd_epilogue<BCO, BIAS, STATS, TCO, TP>(a, acc, red, g, pb, co0, wco, wp, fr, fq, tid);
+  conv_fwd_epilogue<BCO, BP, WM, WN, BIAS, STATS, TCO, TP>(a, acc, red, g, pb, co0, wco, wp, fr, fq, tid);
 }
 
 void conv3d_fwd(uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t xs, uintptr_t xt, uintptr_t y, uintptr_t stats,
@@ -405,18 +412,26 @@ void conv3d_fwd(uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t xs, uintptr_
   a.Mg = B * a.Do * a.Ho * a.Wo;
   a.nPB = ceil_div(a.Mg, kFwdBP);
   const bool xf = xs != 0, hb = bias != 0, st = stats != 0;
+  NIDT_REQUIRE(!st || hb, "conv3d_fwd: statistics require a bias");
   const int bco = (Cout % 128 == 0) ? 128 : 64;
   hipStream_t s = as_stream(stream);
   if (!xf && Cin % 64 == 0) {
+    // BCO=64 without statistics (dgrad of conv2/4/5): 64 co x 256 positions, waves 1x4 (64x64 each);
+    // otherwise 128 positions per block (the BN statistics are merged per 128-position block).
+    const bool wide = bco == 64 && !st;
+    const int bp = wide ? 256 : kFwdBP;
+    a.nPB = ceil_div(a.Mg, bp);
     const int nCO = Cout / bco;
     const int64_t nwg = (int64_t)a.nPB * nCO * G;
     NIDT_REQUIRE(nwg < (1ll << 31), "conv3d_fwd: grid too large");
     dim3 g1((unsigned)nwg);
-#define NIDT_DMA(BC, BI, ST) hipLaunchKernelGGL((k_conv_fwd_dma<BC, BI, ST>), g1, dim3(256), 0, s, a, nCO)
+#define NIDT_DMA(BC, WN, BI, ST) hipLaunchKernelGGL((k_conv_fwd_dma<BC, WN, BI, ST>), g1, dim3(256), 0, s, a, nCO)
     if (bco == 128) {
-      if (st) NIDT_DMA(128, true, true); else if (hb) NIDT_DMA(128, true, false); else NIDT_DMA(128, false, false);
+      if (st) NIDT_DMA(128, 2, true, true); else if (hb) NIDT_DMA(128, 2, true, false); else NIDT_DMA(128, 2, false, false);
+    } else if (wide) {
+      if (hb) NIDT_DMA(64, 4, true, false); else NIDT_DMA(64, 4, false, false);
     } else {
-      if (st) NIDT_DMA(64, true, true); else if (hb) NIDT_DMA(64, true, false); else NIDT_DMA(64, false, false);
+      NIDT_DMA(64, 2, true, true);
     }
 #undef NIDT_DMA
     NIDT_CHECK(hipGetLastError());
