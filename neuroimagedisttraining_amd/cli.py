@@ -139,25 +139,38 @@ def identity(args, algo):
         s += "-batchsize%s-cm%s-total_clnt%s-neighbor%s-seed%s-lr%s" % (
             args.batch_size, args.comm_round, args.client_num_in_total, args.client_num_per_round, args.seed, args.lr)
         return s + ("-mu%s-agg%s" % (args.fedprox_mu, args.aggregator) if algo == "fedprox" else "")
-    if algo == "dispfl":
-        s = "dispfl-" + args.dataset + "-" + part + "-mdl" + args.model + "-cs" + args.cs
+    if algo == "dispfl":  # main_dispfl.py:203-238
+        s = "DisPFL-" + args.dataset + "-" + part + "-mdl" + args.model + "-cs" + args.cs
         s += "-masks" if args.save_masks else ""
         s += "-diff_spa" if args.diff_spa else ""
         s += "-uniform_init" if args.uniform else "-ERK_init"
         s += "-diff_init" if args.different_initial else "-same_init"
         s += "-g" if args.global_test else ""
         s += "-RSM" if args.static else "-DST"
-        s += "-cm%s-total_clnt%s-neighbor%s-dr%s-active%s-seed%s" % (
-            args.comm_round, args.client_num_in_total, args.client_num_per_round, args.dense_ratio, args.active,
-            args.seed)
+        s += "-cm%s-total_clnt%s-neighbor%s-dr%s-batchsize%s-active%s-lr%s-seed%s" % (
+            args.comm_round, args.client_num_in_total, args.client_num_per_round, args.dense_ratio, args.batch_size,
+            args.active, args.lr, args.seed)
         return s
-    base = {"subavg": "subavg", "ditto": "ditto", "dpsgd": "dpsgd", "fedfomo": "fedfomo", "local": "local"}[algo]
-    s = base + "-" + args.dataset + "-" + part + "-mdl" + args.model
-    s += "-cm%s-total_clnt%s-neighbor%s-seed%s-lr%s" % (args.comm_round, args.client_num_in_total,
-                                                         args.client_num_per_round, args.seed, args.lr)
-    if algo == "subavg":
-        s += "-dr%s-epr%s" % (args.dense_ratio, args.each_prune_ratio)
-    return s
+    if algo == "subavg":  # main_subavg.py:177-186 (no "-" between the name and the partition)
+        return "SubAVG%s-mdl%s-batchsize%s-cm%s-total_clnt%s-neighbor%s-seed%s-dr%s" % (
+            part, args.model, args.batch_size, args.comm_round, args.client_num_in_total, args.client_num_per_round,
+            args.seed, args.dense_ratio)
+    if algo == "ditto":  # main_ditto.py:165-174
+        return "ditto-%s-mdl%s-ge%s-le%s-batchsize%s-lambda%s-cm%s-total_clnt%s-neighbor%s-seed%s" % (
+            part, args.model, args.epochs, args.local_epochs, args.batch_size, args.lamda, args.comm_round,
+            args.client_num_in_total, args.client_num_per_round, args.seed)
+    if algo == "dpsgd":  # main_dpsgd.py:167-175
+        return "dpsgd-%s-%s-mdl%s-cs%s-batchsize%s-cm%s-total_clnt%s-neighbor%s-seed%s-type%s" % (
+            args.dataset, part, args.model, args.cs, args.batch_size, args.comm_round, args.client_num_in_total,
+            args.client_num_per_round, args.seed, args.type)
+    if algo == "fedfomo":  # main_fedfomo.py:170-176
+        return "fedfomo-%s-mdl%s-cm%s-total_clnt%s-batchsize%s-neighbor%s-seed%s" % (
+            part, args.model, args.comm_round, args.client_num_in_total, args.batch_size, args.client_num_per_round,
+            args.seed)
+    if algo == "local":  # main_local.py:163-168
+        return "local-%s-cm%s-total_clnt%s-neighbor%s-seed%s" % (
+            part, args.comm_round, args.client_num_in_total, args.client_num_per_round, args.seed)
+    raise ValueError(algo)
 
 
 def load_data(args, dataset_name, logger=None):
@@ -183,8 +196,6 @@ def _use_hip(args, algo):
     if algo not in ("sailentgrads", "fedavg", "fedprox") or args.dataset != "ABCD" or args.model != "3DCNN":
         return False
     if args.engine == "torch":
-        return False
-    if args.aggregator != "fedavg":
         return False
     try:
         from . import ops
@@ -219,7 +230,8 @@ def run_hip(args, algo, logger):
                    lr_decay=args.lr_decay, wd=args.wd, momentum=args.momentum, frac=args.frac,
                    dense_ratio=getattr(args, "dense_ratio", 1.0), itersnip_iteration=getattr(args, "itersnip_iteration", 1),
                    snip_mask=getattr(args, "snip_mask", True), frequency_of_the_test=args.frequency_of_the_test,
-                   seed=args.seed, prox_mu=args.fedprox_mu if algo == "fedprox" else 0.0, group=args.group)
+                   seed=args.seed, prox_mu=args.fedprox_mu if algo == "fedprox" else 0.0, group=args.group,
+                   aggregator=args.aggregator, byzantine_f=args.byzantine_f, trim_ratio=args.trim_ratio)
     runner = FLRunner(eng, splits, cfg, info, model, logger=logger,
                       algorithm="salientgrads" if algo == "sailentgrads" else "fedavg")
     start = 0

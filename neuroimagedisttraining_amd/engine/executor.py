@@ -61,6 +61,11 @@ class FLConfig:
     prox_mu: float = 0.0          # FedProx proximal coefficient (0 = FedAvg/SalientGrads)
     group: int = 0                # max clients per lockstep launch (0 = all local clients)
     test_batch: int = 256
+    aggregator: str = "fedavg"    # fedavg | krum | multikrum | median | trimmed_mean (BASELINE config 4)
+    byzantine_f: int = 0          # Krum's assumed number of Byzantine clients
+    multikrum_m: int = 0          # Multi-Krum: number of selected clients (0 = K - f)
+    trim_ratio: float = 0.1       # trimmed mean: fraction cut from each end per coordinate
+    sparse_aggregate: bool = True  # SalientGrads: all-reduce only the coordinates kept by the global mask
 
 
 # ------------------------------------------------------------------------------------------------
@@ -392,7 +397,26 @@ class FLRunner:
             self._run_batches(rows, loc, round_idx, ep, fn)
 
     def aggregate(self, sampled):
-        """w_global = sum_i n_i/sum n * w_i over sampled clients (params + buffers), one all-reduce."""
+        if self.cfg.aggregator != "fedavg":
+            return self.aggregate_robust(sampled)
+        return self.aggregate_fedavg(sampled)
+
+    def _compact_index(self, Pp):
+        """Flat indices of the aggregation buffer that can be non-zero: SalientGrads' global mask zeroes the
+        pruned weights on every client after every step, so their weighted sum is exactly 0 and they need
+        not travel (params kept by the mask + all BN buffers)."""
+        key = (Pp, id(self.mask))
+        if getattr(self, "_cidx_key", None) != key:
+            keep = torch.ones(Pp + self.Q, dtype=torch.bool, device=self.device)
+            keep[:self.P] = self.mask > 0
+            keep[self.P:Pp] = False
+            self._cidx = keep.nonzero().view(-1)
+            self._cidx_key = key
+        return self._cidx
+
+    def aggregate_fedavg(self, sampled):
+        """w_global = sum_i n_i/sum n * w_i over sampled clients (params + buffers), one all-reduce (of the
+        mask-compacted coordinates when a SalientGrads mask is active)."""
         sset = set(sampled)
         n_tot = float(sum(len(self.splits[c].train) for c in sampled))
         Pp = (self.P + 63) // 64 * 64  # keep the buffer section 16-B aligned for the vectorised kernel
@@ -412,9 +436,51 @@ class FLRunner:
             else:
                 buf[:self.P] = (w.view(-1, 1) * self.theta[ix]).sum(0)
                 buf[Pp:] = (w.view(-1, 1) * self.bufs[ix]).sum(0)
-        rt.all_reduce_buckets(buf, self.info)
+        sparse = (self.info.enabled and self.cfg.sparse_aggregate and self.alg == "salientgrads"
+                  and self.mask is not None)
+        if sparse:
+            idx = self._compact_index(Pp)
+            packed = buf.index_select(0, idx)
+            rt.all_reduce_buckets(packed, self.info)
+            buf.zero_()
+            buf.index_copy_(0, idx, packed)
+            self.stat_info["aggregate_elems"] = int(idx.numel())
+        else:
+            rt.all_reduce_buckets(buf, self.info)
+            self.stat_info["aggregate_elems"] = int(buf.numel())
         self.w_global.copy_(buf[:self.P])
         self.b_global.copy_(buf[Pp:])
+
+    def aggregate_robust(self, sampled):
+        """Byzantine-robust aggregation (BASELINE config 4): every sampled client's (params, buffers) row is
+        all-gathered to every rank (xGMI all-gather of K x (P+Q) fp32; 128 x 10.3 MB = 1.3 GB fits HBM
+        easily), then Krum / Multi-Krum / coordinate median / trimmed mean run on device with the same
+        deterministic result on all ranks (``core/robustness.py``).  BN buffers follow the selected clients
+        for Krum and are coordinate-aggregated otherwise."""
+        from ..core import robustness as R
+        sset = set(sampled)
+        rows = [i for i, c in enumerate(self.local) if c in sset]
+        ids = torch.tensor([self.local[r] for r in rows], dtype=torch.float32, device=self.device)
+        W = self.P + self.Q
+        loc = torch.cat([self.theta[rows, :self.P], self.bufs[rows, :self.Q]], 1) if rows else \
+            torch.zeros((0, W), device=self.device)
+        allrows = rt.all_gather_cat(loc.reshape(-1).contiguous(), self.info).view(-1, W)
+        allids = rt.all_gather_cat(ids, self.info).long()
+        order = torch.argsort(allids)  # deterministic client order on every rank
+        M = allrows.index_select(0, order)
+        kind = self.cfg.aggregator
+        if kind in ("krum", "multikrum"):
+            m = 1 if kind == "krum" else (self.cfg.multikrum_m or max(1, M.shape[0] - self.cfg.byzantine_f))
+            agg, _ = R.krum(M, f=self.cfg.byzantine_f, multi=m)
+        elif kind == "median":
+            agg = R.coordinate_median(M)
+        elif kind == "trimmed_mean":
+            agg = R.trimmed_mean(M, self.cfg.trim_ratio)
+        else:
+            raise ValueError("unknown aggregator %r" % kind)
+        self.w_global.copy_(agg[:self.P])
+        self.b_global.copy_(agg[self.P:])
+        self.stat_info["aggregate_elems"] = int(M.numel())
 
     def _eval_rows(self, theta, bufs, clients, per_client_rows):
         """Per-client (correct, loss_sum, total) with reference test semantics (Q1).  Clients that share a

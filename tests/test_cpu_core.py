@@ -185,3 +185,38 @@ def test_flops_counts_conv3d():
     m = AlexNet3D_Dropout(num_classes=1, in_shape=(69, 69, 69))
     f = count_inference_flops(m, input_shape=(1, 69, 69, 69), full=True)
     assert f > 1e8
+
+
+@pytest.mark.parametrize("algo,expected", [
+    ("sailentgrads", "SailentGrads-ABCD-dir0.3-mdl3DCNNcustomizedlowbatch-csv0-ERK_init-same_init-DST-cm200-total_clnt4"
+                     "-neighbor4-dr0.5-active1.0-seed1024-lr0.01-batchsize16-iteration1-stratifiedFalse"),
+    ("fedavg", "fedavg-dir0.3-mdl3DCNN-batchsize16-cm200-total_clnt4-neighbor3-seed0-lr0.001"),
+    ("dispfl", "DisPFL-ABCD-dir0.3-mdl3DCNN-csrandom-ERK_init-same_init-DST-cm10-total_clnt21-neighbor2-dr0.5"
+               "-batchsize16-active1.0-lr0.001-seed1024"),
+    ("subavg", "SubAVGdir0.3-mdlresnet18-batchsize128-cm1000-total_clnt100-neighbor10-seed0-dr0.5"),
+    ("ditto", "ditto-dir0.3-mdlresnet18-ge2-le3-batchsize128-lambda0.5-cm1000-total_clnt100-neighbor10-seed0"),
+    ("dpsgd", "dpsgd-cifar10-dir0.3-mdlresnet18-csring-batchsize128-cm50-total_clnt100-neighbor10-seed0-typeepoch"),
+    ("fedfomo", "fedfomo-dir0.3-mdlresnet18-cm1000-total_clnt100-batchsize128-neighbor10-seed0"),
+    ("local", "local-dir0.3-cm10-total_clnt100-neighbor100-seed1024"),
+])
+def test_cli_identity_strings_match_reference(algo, expected):
+    """The identity string is the log file name (LOG/<dataset>/<identity>.log): byte-compatible with the
+    reference entry points' defaults (main_<algo>.py)."""
+    import argparse
+    from neuroimagedisttraining_amd import cli
+    args = cli.add_args(argparse.ArgumentParser(), algo).parse_args([])
+    assert cli.identity(args, algo) == expected
+
+
+def test_alexnet3d_state_dict_keys_match_reference():
+    from neuroimagedisttraining_amd.models.alexnet3d import AlexNet3D_Dropout
+    keys = list(AlexNet3D_Dropout(num_classes=1).state_dict().keys())
+    exp = []
+    for c, b in zip((0, 4, 8, 11, 14), (1, 5, 9, 12, 15)):
+        exp += ["features.%d.weight" % c, "features.%d.bias" % c]
+        exp += ["features.%d.%s" % (b, k) for k in ("weight", "bias", "running_mean", "running_var",
+                                                     "num_batches_tracked")]
+    exp += ["classifier.1.weight", "classifier.1.bias", "classifier.4.weight", "classifier.4.bias"]
+    assert keys == exp
+    n = sum(p.numel() for p in AlexNet3D_Dropout(num_classes=1).parameters())
+    assert n == 2570241  # SURVEY.md §6 workload constants

@@ -83,7 +83,7 @@ class Tiny3D(nn.Module):
         return self.classifier(self.features(x).amax((2, 3, 4)))
 
 
-def _runner(rank=0, world=1, clients=4, rounds=2):
+def _runner(rank=0, world=1, clients=4, rounds=2, **cfg_kw):
     from neuroimagedisttraining_amd.engine.executor import ClientSplit, FLConfig, FLRunner, TorchEngine
     from neuroimagedisttraining_amd.parallel import runtime as rt
     torch.manual_seed(0)
@@ -97,7 +97,7 @@ def _runner(rank=0, world=1, clients=4, rounds=2):
     model = Tiny3D()
     eng = TorchEngine(model, vols, labels, "cpu")
     info = rt.DistInfo(rank, world, rank, torch.device("cpu"), "gloo" if world > 1 else "none")
-    cfg = FLConfig(comm_round=rounds, epochs=2, batch_size=4, lr=0.05, dense_ratio=0.5, seed=7)
+    cfg = FLConfig(comm_round=rounds, epochs=2, batch_size=4, lr=0.05, dense_ratio=0.5, seed=7, **cfg_kw)
     return FLRunner(eng, splits, cfg, info, model)
 
 
@@ -116,12 +116,12 @@ def test_executor_snip_rounds_and_aggregation():
     assert 0.0 <= res["global_test_acc"] <= 1.0
 
 
-def _dist_worker(rank, world, port, out):
+def _dist_worker(rank, world, port, out, cfg_kw=None):
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    r = _runner(rank, world)
+    r = _runner(rank, world, **(cfg_kw or {}))
     r.generate_global_mask_snip()
     for k in range(2):
         r.run_round(k)
@@ -130,7 +130,9 @@ def _dist_worker(rank, world, port, out):
     dist.destroy_process_group()
 
 
-def test_two_rank_gloo_matches_single_process(tmp_path):
+@pytest.mark.parametrize("cfg_kw", [{}, {"aggregator": "median"}])
+def test_two_rank_gloo_matches_single_process(tmp_path, cfg_kw):
+    """2 ranks (clients sharded, mask-compacted all-reduce / all-gathered robust aggregation) == 1 process."""
     import socket
     import torch.multiprocessing as mp
     s = socket.socket()
@@ -138,11 +140,46 @@ def test_two_rank_gloo_matches_single_process(tmp_path):
     port = s.getsockname()[1]
     s.close()
     out = str(tmp_path / "w.pt")
-    mp.start_processes(_dist_worker, args=(2, port, out), nprocs=2, join=True, start_method="spawn")
+    mp.start_processes(_dist_worker, args=(2, port, out, cfg_kw), nprocs=2, join=True, start_method="spawn")
     got = torch.load(out, weights_only=True)
-    r = _runner()
+    r = _runner(**cfg_kw)
     r.generate_global_mask_snip()
     for k in range(2):
         r.run_round(k)
     assert torch.allclose(got["w"], r.w_global, atol=1e-5), float((got["w"] - r.w_global).abs().max())
     assert np.allclose(got["acc"], r.stat_info["global_test_acc"])
+
+
+def test_executor_robust_aggregation_rejects_outlier():
+    from neuroimagedisttraining_amd.core import robustness as R
+    for kind in ("krum", "multikrum", "median", "trimmed_mean"):
+        r = _runner(clients=5, aggregator=kind, byzantine_f=1, trim_ratio=0.2)
+        r.mask = torch.ones(r.P)
+        sampled = list(range(5))
+        r.theta[:, :r.P] = torch.randn(5, r.P) * 0.01
+        r.theta[3, :r.P] += 100.0  # Byzantine client
+        r.aggregate(sampled)
+        assert float(r.w_global.abs().max()) < 1.0, kind
+        M = torch.cat([r.theta[:, :r.P], r.bufs[:, :r.Q]], 1)
+        if kind == "median":
+            assert torch.allclose(r.w_global, R.coordinate_median(M)[:r.P])
+
+
+def test_executor_checkpoint_resume_is_exact(tmp_path):
+    from neuroimagedisttraining_amd.utils import checkpoint as ck
+    a = _runner(rounds=3)
+    a.generate_global_mask_snip()
+    for k in range(3):
+        a.run_round(k)
+    b = _runner(rounds=3)
+    b.generate_global_mask_snip()
+    b.run_round(0)
+    ck.save_runner(b, str(tmp_path), 1)
+    c = _runner(rounds=3)
+    start = ck.load_runner(c, str(tmp_path))
+    assert start == 1
+    for k in range(start, 3):
+        c.run_round(k)
+    assert torch.equal(a.w_global, c.w_global)
+    assert torch.equal(a.theta, c.theta)
+    assert c.stat_info["global_test_acc"][-1] == a.stat_info["global_test_acc"][-1]
