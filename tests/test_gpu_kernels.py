@@ -422,3 +422,37 @@ def test_weighted_rows_sum():
     m.weighted_rows_sum(rows.data_ptr(), w.data_ptr(), C, P, rows.stride(0), 0.0, out.data_ptr(), _st())
     torch.cuda.synchronize()
     assert _relerr(out, (w.view(-1, 1) * rows).sum(0)) < 1e-6
+
+
+@pytest.mark.parametrize("cin,cout,pad,sp", [(64, 128, 0, (9, 11, 9)), (128, 192, 1, (5, 7, 5))])
+def test_torch_library_conv3d_k3_autograd(cin, cout, pad, sp):
+    """nidt::conv3d_k3 custom op (LDS-DMA fwd, dgrad, row-group wgrad) vs F.conv3d autograd per client."""
+    from neuroimagedisttraining_amd.ops import library  # noqa: F401  (registers torch.ops.nidt.*)
+    G, B = 2, 2
+    torch.manual_seed(3)
+    x = torch.randn(G * B, *sp, cin, device=DEV).bfloat16().requires_grad_(True)
+    w = (torch.randn(G, cout, cin, 3, 3, 3, device=DEV) * 0.05).requires_grad_(True)
+    b = torch.randn(G, cout, device=DEV).requires_grad_(True)
+    y = torch.ops.nidt.conv3d_k3(x, w, b, pad)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    for g in range(G):
+        xr = _cf(x[g * B:(g + 1) * B].detach().float()).requires_grad_(True)
+        wr = w[g].detach().bfloat16().float().requires_grad_(True)
+        br = b[g].detach().clone().requires_grad_(True)
+        yr = F.conv3d(xr, wr, br, 1, pad)
+        yr.backward(_cf(dy[g * B:(g + 1) * B].float()))
+        assert _relerr(y[g * B:(g + 1) * B].float(), _cl(yr.detach())) < 1e-2
+        assert _relerr(x.grad[g * B:(g + 1) * B].float(), _cl(xr.grad)) < 1e-2
+        assert _relerr(w.grad[g], wr.grad) < 1e-2
+        assert _relerr(b.grad[g], br.grad) < 1e-3
+
+
+def test_torch_library_kth_and_weighted_sum():
+    from neuroimagedisttraining_amd.ops import library  # noqa: F401
+    v = torch.rand(100003, device=DEV)
+    k = 777
+    assert float(torch.ops.nidt.kth_largest(v, k)) == float(torch.topk(v, k).values[-1])
+    rows = torch.randn(5, 1001, device=DEV)
+    wts = torch.rand(5, device=DEV)
+    assert torch.allclose(torch.ops.nidt.weighted_rows_sum(rows, wts), (wts[:, None] * rows).sum(0), atol=1e-5)
