@@ -41,7 +41,8 @@ void bn_bwd(int pool, uintptr_t y, uintptr_t dsrc, uintptr_t pout, uintptr_t ama
 // conv1.hip
 void polyphase(uintptr_t src, uintptr_t dst, int64_t N, uintptr_t stream);
 void conv1_sample_moments(uintptr_t x8, int64_t N, uintptr_t mom, uintptr_t stream);
-void pack_conv1_w(uintptr_t theta, int64_t ldt, int64_t off, int G, float scale, uintptr_t w8, uintptr_t w125,
+void pack_conv1_w(uintptr_t theta, int64_t ldt, int64_t off, int64_t off_sign, int G, float scale, uintptr_t w8,
+                  uintptr_t w125,
                   uintptr_t stream);
 void conv1_bnstats(uintptr_t mom, uintptr_t idx, int B, int G, uintptr_t Mb, uintptr_t w125, uintptr_t theta,
                    int64_t ldt, int64_t off_bias, int64_t off_g, int64_t off_b, uintptr_t bufs, int64_t ldb,

@@ -150,8 +150,8 @@ void conv1_sample_moments(uintptr_t x8, int64_t N, uintptr_t mom, uintptr_t stre
 // ------------------------------------------------------------------------------------------------
 // weight packing: theta row g at off: [64][125] fp32 -> w8 [G][64][224] bf16 (x scale), w125 [G][64][125] f32
 // holding the bf16-rounded scaled weights (the exact values the MFMA uses) for the moment math.
-__global__ void k_pack_conv1_w(const float* __restrict__ theta, int64_t ldt, int64_t off, int G, float scale,
-                               uint16_t* __restrict__ w8, float* __restrict__ w125) {
+__global__ void k_pack_conv1_w(const float* __restrict__ theta, int64_t ldt, int64_t off, int64_t off_sign, int G,
+                               float scale, uint16_t* __restrict__ w8, float* __restrict__ w125) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= G * kC1 * kK1) return;
   const int g = i / (kC1 * kK1), rem = i - g * kC1 * kK1, c = rem / kK1, kk = rem - c * kK1;
@@ -161,14 +161,16 @@ __global__ void k_pack_conv1_w(const float* __restrict__ theta, int64_t ldt, int
     const int k = tp_to_k(t, r);
     v = f32_to_bf16(theta[(int64_t)g * ldt + off + c * 125 + k] * scale);
     w125[((int64_t)g * kC1 + c) * 125 + k] = bf16_to_f32(v);
+    // the fused forward expects sign(gamma_c) folded into its MFMA weights (exact sign flip)
+    if (off_sign >= 0 && theta[(int64_t)g * ldt + off_sign + c] < 0.f) v ^= 0x8000u;
   }
   w8[i] = v;
 }
 
-void pack_conv1_w(uintptr_t theta, int64_t ldt, int64_t off, int G, float scale, uintptr_t w8, uintptr_t w125,
-                  uintptr_t stream) {
+void pack_conv1_w(uintptr_t theta, int64_t ldt, int64_t off, int64_t off_sign, int G, float scale, uintptr_t w8,
+                  uintptr_t w125, uintptr_t stream) {
   hipLaunchKernelGGL(k_pack_conv1_w, dim3(ceil_div(G * kC1 * kK1, 256)), dim3(256), 0, as_stream(stream),
-                     ptr<const float>(theta), ldt, off, G, scale, ptr<uint16_t>(w8), ptr<float>(w125));
+                     ptr<const float>(theta), ldt, off, off_sign, G, scale, ptr<uint16_t>(w8), ptr<float>(w125));
   NIDT_CHECK(hipGetLastError());
 }
 
@@ -262,138 +264,6 @@ void conv1_bnstats(uintptr_t mom, uintptr_t idx, int B, int G, uintptr_t Mb, uin
 // ------------------------------------------------------------------------------------------------
 // Fused forward: conv1 (MFMA) -> z = conv*scale + shift -> max over 3x3x3 -> relu.  Block = (n, pd, ph),
 // 4 waves; wave w owns output columns ow = 15w .. 15w+14 (5 pooling windows), lane column = ow offset.
-__global__ __launch_bounds__(256, 2) void k_conv1_fwd_pool(const uint8_t* __restrict__ x8, const int* __restrict__ idx,
-                                                           const uint16_t* __restrict__ w8,
-                                                           const float* __restrict__ scale,
-                                                           const float* __restrict__ shift, int B,
-                                                           uint16_t* __restrict__ out, uint8_t* __restrict__ amax) {
-  constexpr int HX = 64;  // halo x extent
-  __shared__ __attribute__((aligned(16))) uint16_t halo[5 * 5 * HX * 8];
-  const int ph = blockIdx.x, pd = blockIdx.y, n = blockIdx.z;
-  const int g = n / B;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const uint8_t* xs = x8 + (int64_t)idx[n] * kPZ * kPY * kPX * 8;
-  // stage halo: z = 3pd..3pd+4, y = 3ph..3ph+4, x = 0..63 (x >= 61 -> 0), u8 -> bf16
-  for (int e = tid; e < 5 * 5 * HX; e += 256) {
-    const int xh = e % HX, yz = e / HX, yh = yz % 5, zh = yz / 5;
-    const int z = 3 * pd + zh, y = 3 * ph + yh;
-    uint2 v = make_uint2(0, 0);
-    if (xh < kPX) v = *reinterpret_cast<const uint2*>(xs + (((int64_t)z * kPY + y) * kPX + xh) * 8);
-    uint4 o;
-    o.x = ((v.x & 0xffu) ? __float_as_uint((float)(v.x & 0xffu)) >> 16 : 0u) |
-          (((v.x >> 8) & 0xffu) ? (__float_as_uint((float)((v.x >> 8) & 0xffu)) & 0xffff0000u) : 0u);
-    o.y = (((v.x >> 16) & 0xffu) ? __float_as_uint((float)((v.x >> 16) & 0xffu)) >> 16 : 0u) |
-          ((v.x >> 24) ? (__float_as_uint((float)(v.x >> 24)) & 0xffff0000u) : 0u);
-    o.z = ((v.y & 0xffu) ? __float_as_uint((float)(v.y & 0xffu)) >> 16 : 0u) |
-          (((v.y >> 8) & 0xffu) ? (__float_as_uint((float)((v.y >> 8) & 0xffu)) & 0xffff0000u) : 0u);
-    o.w = (((v.y >> 16) & 0xffu) ? __float_as_uint((float)((v.y >> 16) & 0xffu)) >> 16 : 0u) |
-          ((v.y >> 24) ? (__float_as_uint((float)(v.y >> 24)) & 0xffff0000u) : 0u);
-    *reinterpret_cast<uint4*>(&halo[e * 8]) = o;
-  }
-  // wave layout: ch = co half (channels 32ch..32ch+31 = 2 MFMA row tiles), op = pair of 16-column ow tiles.
-  // A fragments (weights) for the wave's 2 co tiles x 7 k-steps stay in registers for the whole block.
-  const int fr = lane & 15, fq = lane >> 4;
-  const int ch = wid & 1, op = wid >> 1;
-  bf16x8 fa[2][7];
-  const uint16_t* wg = w8 + (int64_t)g * kC1 * kK1;
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int s = 0; s < 7; ++s)
-      fa[i][s] = *reinterpret_cast<const bf16x8*>(wg + (32 * ch + 16 * i + fr) * kK1 + 32 * s + 8 * fq);
-  float sc[2][4], sh[2][4];
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      sc[i][r] = scale[g * kC1 + 32 * ch + 16 * i + 4 * fq + r];
-      sh[i][r] = shift[g * kC1 + 32 * ch + 16 * i + 4 * fq + r];
-    }
-  // per-lane tap offsets (in halo elements) for each k-step: tap t = 4s + fq (t >= 27 -> zero weights; reuse 26)
-  int toff[7];
-#pragma unroll
-  for (int s = 0; s < 7; ++s) {
-    int t = 4 * s + fq;
-    t = t < 27 ? t : 26;
-    toff[s] = (((t / 9) * 5 + (t / 3) % 3) * HX + (t % 3)) * 8;
-  }
-  // output column tiles of this wave: ow = 15*(2op+j) + fr, j = 0,1 (a tile holds 5 pooling windows)
-  const int colbase0 = (15 * (2 * op) + fr) * 8, colbase1 = colbase0 + 15 * 8;
-  __syncthreads();
-  float best[2][2][4];
-  int bidx[2][2][4];
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) { best[i][j][r] = -INFINITY; bidx[i][j][r] = 0; }
-  for (int dd = 0; dd < 3; ++dd) {
-    for (int dh = 0; dh < 3; ++dh) {
-      f32x4 acc[2][2];
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-      const int rowoff = ((dd * 5 + dh) * HX) * 8;
-#pragma unroll
-      for (int s = 0; s < 7; ++s) {
-        const bf16x8 fb0 = *reinterpret_cast<const bf16x8*>(&halo[colbase0 + rowoff + toff[s]]);
-        const bf16x8 fb1 = *reinterpret_cast<const bf16x8*>(&halo[colbase1 + rowoff + toff[s]]);
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-          acc[i][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][s], fb0, acc[i][0], 0, 0, 0);
-          acc[i][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][s], fb1, acc[i][1], 0, 0, 0);
-        }
-      }
-      const int li = dd * 9 + dh * 3;
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const float z = fmaf(acc[i][j][r], sc[i][r], sh[i][r]);
-            if (z > best[i][j][r]) { best[i][j][r] = z; bidx[i][j][r] = li; }
-          }
-    }
-  }
-  // combine the 3 w-columns of each window: lanes fr = 3w', 3w'+1, 3w'+2 (within the 16-lane group)
-  const int wloc = fr / 3, dw = fr - 3 * wloc;
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int pw = 5 * (2 * op + j) + wloc;
-    const bool writer = (dw == 0) && (fr < 15) && (pw < kPW);
-    uint32_t pk[2][2], ab[2];
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      ab[i] = 0;
-      float o4[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        float v = best[i][j][r];
-        int ix = bidx[i][j][r] + dw;
-        const float v1 = __shfl_down(v, 1, 16), v2 = __shfl_down(v, 2, 16);
-        const int i1 = __shfl_down(ix, 1, 16), i2 = __shfl_down(ix, 2, 16);
-        if (v1 > v || (v1 == v && i1 < ix)) { v = v1; ix = i1; }
-        if (v2 > v || (v2 == v && i2 < ix)) { v = v2; ix = i2; }
-        o4[r] = fmaxf(v, 0.f);
-        ab[i] |= (uint32_t)ix << (8 * r);
-      }
-      pk[i][0] = pack_bf16x2(o4[0], o4[1]);
-      pk[i][1] = pack_bf16x2(o4[2], o4[3]);
-    }
-    if (writer) {
-      const int64_t o = ((((int64_t)n * kPD + pd) * kPH + ph) * kPW + pw) * kC1 + 32 * ch + 4 * fq;
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        *reinterpret_cast<uint2*>(out + o + 16 * i) = make_uint2(pk[i][0], pk[i][1]);
-        *reinterpret_cast<uint32_t*>(amax + o + 16 * i) = ab[i];
-      }
-    }
-  }
-}
-
 // k_conv1_fwd_pool_pipe — same math as k_conv1_fwd_pool, but one block walks all 23 pooled rows (ph) of a
 // (sample, pd) slab: the next row's 5x5x64 halo is prefetched into registers (7 x 8 B per thread) while the
 // MFMAs of the current row run, then converted (v_cvt_f32_ubyteN + v_perm: u8 -> exact bf16) into the other
@@ -452,14 +322,28 @@ __global__ __launch_bounds__(256, 2) void k_conv1_fwd_pool_pipe(const uint8_t* _
 #pragma unroll
     for (int s = 0; s < 7; ++s)
       fa[i][s] = *reinterpret_cast<const bf16x8*>(wg + (32 * ch + 16 * i + fr) * kK1 + 32 * s + 8 * fq);
+  // w8 carries sign(gamma) = sign(sc) per output channel (k_pack_conv1_w, exact), so the argmax of
+  // z = sc*acc + sh is the argmax of the accumulator and the pooled value is |sc| * max + sh.  The 3^3
+  // window's argmax index rides in the 5 low mantissa bits of the running max (v_and_or + v_max per conv
+  // output instead of fma + cmp + 2 selects).
   float sc[2][4], sh[2][4];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      sc[i][r] = scale[g * kC1 + 32 * ch + 16 * i + 4 * fq + r];
+      sc[i][r] = fabsf(scale[g * kC1 + 32 * ch + 16 * i + 4 * fq + r]);
       sh[i][r] = shift[g * kC1 + 32 * ch + 16 * i + 4 * fq + r];
     }
+  // Retire the one-time loads here: an empty asm that "redefines" each register makes the waitcnt pass see
+  // them complete before the row loop, so it does not insert vmcnt waits on the halo prefetch inside the
+  // MFMA loop (which would serialise the prefetch with the matrix work).
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+#pragma unroll
+    for (int s = 0; s < 7; ++s) asm volatile("" : "+v"(fa[i][s]));
+#pragma unroll
+    for (int r = 0; r < 4; ++r) asm volatile("" : "+v"(sc[i][r]), "+v"(sh[i][r]));
+  }
   int toff[7];
 #pragma unroll
   for (int s = 0; s < 7; ++s) {
@@ -476,32 +360,39 @@ __global__ __launch_bounds__(256, 2) void k_conv1_fwd_pool_pipe(const uint8_t* _
     if (ph + 1 < kPH) C1_LOAD(ph + 1)
     const uint16_t* hb = halo + cur * HALO;
     float best[2][2][4];
-    int bidx[2][2][4];
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
       for (int j = 0; j < 2; ++j)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) { best[i][j][r] = -INFINITY; bidx[i][j][r] = 0; }
+        for (int r = 0; r < 4; ++r) best[i][j][r] = -INFINITY;
+#pragma unroll 1
     for (int dd = 0; dd < 3; ++dd) {
+      // 21 k-steps (3 dh rows x 7 tap groups) with the B fragments of step q+1 read before step q's MFMAs
+      bf16x8 nb0 = *reinterpret_cast<const bf16x8*>(&hb[colbase0 + dd * 5 * HX * 8 + toff[0]]);
+      bf16x8 nb1 = *reinterpret_cast<const bf16x8*>(&hb[colbase1 + dd * 5 * HX * 8 + toff[0]]);
+      f32x4 acc[2][2];
 #pragma unroll
-      for (int dh = 0; dh < 3; ++dh) {
-        f32x4 acc[2][2];
+      for (int q = 0; q < 21; ++q) {
+        const int dh = q / 7, s = q % 7;
+        if (s == 0) {
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
+          for (int i = 0; i < 2; ++i)
 #pragma unroll
-          for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-        const int rowoff = ((dd * 5 + dh) * HX) * 8;
-#pragma unroll
-        for (int s = 0; s < 7; ++s) {
-          const bf16x8 fb0 = *reinterpret_cast<const bf16x8*>(&hb[colbase0 + rowoff + toff[s]]);
-          const bf16x8 fb1 = *reinterpret_cast<const bf16x8*>(&hb[colbase1 + rowoff + toff[s]]);
-#pragma unroll
-          for (int i = 0; i < 2; ++i) {
-            acc[i][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][s], fb0, acc[i][0], 0, 0, 0);
-            acc[i][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][s], fb1, acc[i][1], 0, 0, 0);
-          }
+            for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
         }
+        const bf16x8 fb0 = nb0, fb1 = nb1;
+        if (q + 1 < 21) {
+          const int ro = ((dd * 5 + (q + 1) / 7) * HX) * 8 + toff[(q + 1) % 7];
+          nb0 = *reinterpret_cast<const bf16x8*>(&hb[colbase0 + ro]);
+          nb1 = *reinterpret_cast<const bf16x8*>(&hb[colbase1 + ro]);
+        }
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          acc[i][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][s], fb0, acc[i][0], 0, 0, 0);
+          acc[i][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][s], fb1, acc[i][1], 0, 0, 0);
+        }
+        if (s != 6) continue;
         const int li = dd * 9 + dh * 3;
 #pragma unroll
         for (int i = 0; i < 2; ++i)
@@ -509,8 +400,8 @@ __global__ __launch_bounds__(256, 2) void k_conv1_fwd_pool_pipe(const uint8_t* _
           for (int j = 0; j < 2; ++j)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-              const float z = fmaf(acc[i][j][r], sc[i][r], sh[i][r]);
-              if (z > best[i][j][r]) { best[i][j][r] = z; bidx[i][j][r] = li; }
+              const uint32_t e = (__float_as_uint(acc[i][j][r]) & ~31u) | (uint32_t)li;
+              best[i][j][r] = fmaxf(best[i][j][r], __uint_as_float(e));
             }
       }
     }
@@ -525,13 +416,14 @@ __global__ __launch_bounds__(256, 2) void k_conv1_fwd_pool_pipe(const uint8_t* _
         float o4[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          float v = best[i][j][r];
-          int ix = bidx[i][j][r] + dw;
+          const uint32_t bb = __float_as_uint(best[i][j][r]);
+          float v = __uint_as_float(bb & ~31u);
+          int ix = (int)(bb & 31u) + dw;
           const float v1 = __shfl_down(v, 1, 16), v2 = __shfl_down(v, 2, 16);
           const int i1 = __shfl_down(ix, 1, 16), i2 = __shfl_down(ix, 2, 16);
           if (v1 > v || (v1 == v && i1 < ix)) { v = v1; ix = i1; }
           if (v2 > v || (v2 == v && i2 < ix)) { v = v2; ix = i2; }
-          o4[r] = fmaxf(v, 0.f);
+          o4[r] = fmaxf(fmaf(v, sc[i][r], sh[i][r]), 0.f);
           ab[i] |= (uint32_t)ix << (8 * r);
         }
         pk[i][0] = pack_bf16x2(o4[0], o4[1]);

@@ -97,7 +97,8 @@ class HipAlexNet3D:
     def _pack(self, theta, G, b, train):
         m, st = self.m, torch.cuda.current_stream().cuda_stream
         P = theta.stride(0)
-        m.pack_conv1_w(_p(theta), P, self.o["features.0.weight"], G, 1.0 / 255.0, _p(b["w1p"]), _p(b["w125"]), st)
+        m.pack_conv1_w(_p(theta), P, self.o["features.0.weight"], self.o["features.1.weight"], G, 1.0 / 255.0,
+                       _p(b["w1p"]), _p(b["w125"]), st)
         for (ci, bi, cin, cout, pad, sp) in (L2, L3, L4, L5):
             m.pack_conv_w(_p(theta), P, self.o["features.%d.weight" % ci], G, cout, cin, 1.0, _p(b["w%dp" % ci]),
                           _p(b["w%dt" % ci]) if train else 0, st)
