@@ -145,7 +145,7 @@ __device__ __forceinline__ void conv_fwd_epilogue(const ConvFwdArgs& a, f32x4 (&
         for (int r = 0; r < 4; ++r) red[wp * BCO + wco * WCO + i * 16 + 4 * fq + r] = s_[i][r];
     }
     __syncthreads();
-    for (int c = tid; c < BCO; c += 256) {
+    for (int c = tid; c < BCO; c += (int)blockDim.x) {
       float* st = a.stats + (((int64_t)g * a.nPB + pb) * a.Cout + co0 + c) * 2;
       // recompute mean for this channel from the first pass is not available here; store via second array
       float t = 0.f;
@@ -292,15 +292,15 @@ __device__ __forceinline__ void glds16(const void* src, uint16_t* lds_wave_base)
   __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(lds_wave_base), 16, 0, 0);
 }
 
-template <int BCO, int WN, bool BIAS, bool STATS>
-__global__ __launch_bounds__(256, 2) void k_conv_fwd_dma(ConvFwdArgs a, int nCO) {
+template <int BCO, int WM, int WN, bool BIAS, bool STATS>
+__global__ __launch_bounds__(64 * WM * WN, 8 / (WM * WN)) void k_conv_fwd_dma(ConvFwdArgs a, int nCO) {
   // waves: WM (co) x WN (positions); each wave owns (BCO/WM) co x 64 positions
-  constexpr int WM = 4 / WN, BP = 64 * WN, BK = 64;
+  constexpr int NW = WM * WN, BP = 64 * WN, BK = 64;
   constexpr int WCO = BCO / WM, WP = 64;
   constexpr int TCO = WCO / 16, TP = WP / 16;
   constexpr int A_ELEMS = BCO * BK, B_ELEMS = BP * BK, BUF = A_ELEMS + B_ELEMS;
-  constexpr int A_INSTR = BCO / 32;  // 1-KB glds wave-instructions per wave for the A tile
-  constexpr int B_INSTR = BP / 32;   // ... and for the B tile (8 rows each)
+  constexpr int A_INSTR = BCO / (8 * NW);  // 1-KB glds wave-instructions per wave for the A tile
+  constexpr int B_INSTR = BP / (8 * NW);   // ... and for the B tile (8 rows each)
   __shared__ __attribute__((aligned(16))) uint16_t smem[2 * BUF];
 
   const int nwg = gridDim.x;
@@ -416,22 +416,20 @@ void conv3d_fwd(uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t xs, uintptr_
   const int bco = (Cout % 128 == 0) ? 128 : 64;
   hipStream_t s = as_stream(stream);
   if (!xf && Cin % 64 == 0) {
-    // BCO=64 without statistics (dgrad of conv2/4/5): 64 co x 256 positions, waves 1x4 (64x64 each);
-    // otherwise 128 positions per block (the BN statistics are merged per 128-position block).
-    const bool wide = bco == 64 && !st;
-    const int bp = wide ? 256 : kFwdBP;
+    // 256 positions per block: BCO=128 -> 8 waves (2 co x 4 pos, 512 threads), BCO=64 -> 4 waves (1 x 4);
+    // every wave owns a 64x64 output tile (the A tile is re-read from L2 once per 256 positions).
+    const int bp = 256;
     a.nPB = ceil_div(a.Mg, bp);
     const int nCO = Cout / bco;
     const int64_t nwg = (int64_t)a.nPB * nCO * G;
     NIDT_REQUIRE(nwg < (1ll << 31), "conv3d_fwd: grid too large");
     dim3 g1((unsigned)nwg);
-#define NIDT_DMA(BC, WN, BI, ST) hipLaunchKernelGGL((k_conv_fwd_dma<BC, WN, BI, ST>), g1, dim3(256), 0, s, a, nCO)
+#define NIDT_DMA(BC, WM, BI, ST) \
+    hipLaunchKernelGGL((k_conv_fwd_dma<BC, WM, 4, BI, ST>), g1, dim3(256 * WM), 0, s, a, nCO)
     if (bco == 128) {
       if (st) NIDT_DMA(128, 2, true, true); else if (hb) NIDT_DMA(128, 2, true, false); else NIDT_DMA(128, 2, false, false);
-    } else if (wide) {
-      if (hb) NIDT_DMA(64, 4, true, false); else NIDT_DMA(64, 4, false, false);
     } else {
-      NIDT_DMA(64, 2, true, true);
+      if (st) NIDT_DMA(64, 1, true, true); else if (hb) NIDT_DMA(64, 1, true, false); else NIDT_DMA(64, 1, false, false);
     }
 #undef NIDT_DMA
     NIDT_CHECK(hipGetLastError());
@@ -450,9 +448,15 @@ void conv3d_fwd(uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t xs, uintptr_
   NIDT_CHECK(hipGetLastError());
 }
 
-int conv3d_fwd_nblocks(int B, int D, int H, int W, int pad) {
+// positions per block (= per BN-statistics block) of conv3d_fwd for this layer shape
+int conv3d_fwd_bp(int Cin, int Cout, int xf) {
+  (void)Cout;
+  return (!xf && Cin % 64 == 0) ? 256 : kFwdBP;
+}
+
+int conv3d_fwd_nblocks(int B, int D, int H, int W, int pad, int bp) {
   const int Mg = B * (D + 2 * pad - 2) * (H + 2 * pad - 2) * (W + 2 * pad - 2);
-  return ceil_div(Mg, kFwdBP);
+  return ceil_div(Mg, bp);
 }
 
 // ------------------------------------------------------------------------------------------------

@@ -68,9 +68,11 @@ class HipAlexNet3D:
             b["bias%d" % ci] = e(G, cout, dt=f32)
             for k in ("s", "t", "m", "i"):
                 b["%s%d" % (k, ci)] = e(G, cout, dt=f32)
-            npb = self.m.conv3d_fwd_nblocks(B, sp[0], sp[1], sp[2], pad)
+            bp = self.m.conv3d_fwd_bp(cin, cout, 0)
+            npb = self.m.conv3d_fwd_nblocks(B, sp[0], sp[1], sp[2], pad, bp)
             b["st%d" % ci] = e(G, npb, cout, 2, dt=f32)
             b["npb%d" % ci] = npb
+            b["bp%d" % ci] = bp
         if train:
             for (ci, bi, cin, cout, pad, sp) in (L2, L3, L4, L5):
                 b["w%dt" % ci] = e(G, cin, 27, cout)
@@ -114,7 +116,7 @@ class HipAlexNet3D:
         if train:
             onbt = self.ob["features.%d.num_batches_tracked" % bi]
             Mg = B * sp[0] * sp[1] * sp[2]
-            m.bn_finalize(_p(b["st%d" % ci]), b["npb%d" % ci], 128, Mg, G, C, _p(theta), P, og, ob, _p(bufs), Q,
+            m.bn_finalize(_p(b["st%d" % ci]), b["npb%d" % ci], b["bp%d" % ci], Mg, G, C, _p(theta), P, og, ob, _p(bufs), Q,
                           orm, orv, onbt, BN_MOM, BN_EPS, _p(b["s%d" % ci]), _p(b["t%d" % ci]), _p(b["m%d" % ci]),
                           _p(b["i%d" % ci]), 1, st)
         else:

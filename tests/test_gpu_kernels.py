@@ -66,7 +66,8 @@ def test_conv3d_fwd_stats(cin, cout, pad, sp, xf):
     xt = torch.randn(G, cin, device=DEV) * 0.2 if xf else None
     Do, Ho, Wo = [s + 2 * pad - 2 for s in sp]
     y = torch.empty(G * B, Do, Ho, Wo, cout, device=DEV, dtype=torch.bfloat16)
-    npb = m.conv3d_fwd_nblocks(B, *sp, pad)
+    bp = m.conv3d_fwd_bp(cin, cout, 1 if xf else 0)
+    npb = m.conv3d_fwd_nblocks(B, *sp, pad, bp)
     stats = torch.empty(G, npb, cout, 2, device=DEV)
     m.conv3d_fwd(x.data_ptr(), w.data_ptr(), bias.data_ptr(), xs.data_ptr() if xf else 0, xt.data_ptr() if xf else 0,
                  y.data_ptr(), stats.data_ptr(), G, B, *sp, cin, cout, pad, _st())
@@ -82,7 +83,7 @@ def test_conv3d_fwd_stats(cin, cout, pad, sp, xf):
     assert _relerr(y.float(), yr) < 1e-2
     # statistics: merged block stats == batch mean / biased var per (client, channel)
     Mg = B * Do * Ho * Wo
-    cnt = torch.tensor([min(128, Mg - b * 128) for b in range(npb)], device=DEV, dtype=torch.float64)
+    cnt = torch.tensor([min(bp, Mg - b * bp) for b in range(npb)], device=DEV, dtype=torch.float64)
     mean_b, m2_b = stats[..., 0].double(), stats[..., 1].double()
     mean = (mean_b * cnt.view(1, -1, 1)).sum(1) / Mg
     var = (m2_b + cnt.view(1, -1, 1) * (mean_b - mean.unsqueeze(1)) ** 2).sum(1) / Mg
