@@ -292,8 +292,8 @@ __device__ __forceinline__ void glds16(const void* src, uint16_t* lds_wave_base)
   __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(lds_wave_base), 16, 0, 0);
 }
 
-template <int BCO, int WM, int WN, bool BIAS, bool STATS>
-__global__ __launch_bounds__(64 * WM * WN, 8 / (WM * WN)) void k_conv_fwd_dma(ConvFwdArgs a, int nCO) {
+template <int BCO, int WM, int WN, int NST, bool BIAS, bool STATS>
+__global__ __launch_bounds__(64 * WM * WN, (NST == 2 ? 8 : 4) / (WM * WN)) void k_conv_fwd_dma(ConvFwdArgs a, int nCO) {
   // waves: WM (co) x WN (positions); each wave owns (BCO/WM) co x 64 positions
   constexpr int NW = WM * WN, BP = 64 * WN, BK = 64;
   constexpr int WCO = BCO / WM, WP = 64;
@@ -301,7 +301,10 @@ __global__ __launch_bounds__(64 * WM * WN, 8 / (WM * WN)) void k_conv_fwd_dma(Co
   constexpr int A_ELEMS = BCO * BK, B_ELEMS = BP * BK, BUF = A_ELEMS + B_ELEMS;
   constexpr int A_INSTR = BCO / (8 * NW);  // 1-KB glds wave-instructions per wave for the A tile
   constexpr int B_INSTR = BP / (8 * NW);   // ... and for the B tile (8 rows each)
-  __shared__ __attribute__((aligned(16))) uint16_t smem[2 * BUF];
+  constexpr int NI = A_INSTR + B_INSTR;    // glds per wave per stage (the vmcnt unit)
+  // NST LDS stages: NST-1 tiles in flight while one is consumed.  With NST = 3 the loads of two k-steps
+  // stay in flight across the barrier (counted vmcnt + raw s_barrier; a __syncthreads() would drain them).
+  __shared__ __attribute__((aligned(16))) uint16_t smem[NST * BUF];
 
   const int nwg = gridDim.x;
   const int id = xcd_remap(blockIdx.x, nwg);
@@ -365,11 +368,20 @@ __global__ __launch_bounds__(64 * WM * WN, 8 / (WM * WN)) void k_conv_fwd_dma(Co
 
   const int fr = lane & 15, fq = lane >> 4;
   DMA_ISSUE(0, 0)
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
+  if (NST == 3 && nks > 1) {
+    DMA_ISSUE(1, 1)
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NI) : "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __builtin_amdgcn_s_barrier();
+  int cur = 0;
   for (int ks = 0; ks < nks; ++ks) {
-    const int cur = ks & 1;
-    if (ks + 1 < nks) DMA_ISSUE(ks + 1, cur ^ 1)
+    if (ks + NST - 1 < nks) {
+      int nb = cur + NST - 1;
+      nb = nb >= NST ? nb - NST : nb;
+      DMA_ISSUE(ks + NST - 1, nb)
+    }
     const uint16_t* sA = smem + cur * BUF;
     const uint16_t* sB = sA + A_ELEMS;
 #pragma unroll
@@ -390,10 +402,15 @@ __global__ __launch_bounds__(64 * WM * WN, 8 / (WM * WN)) void k_conv_fwd_dma(Co
 #pragma unroll
         for (int j = 0; j < TP; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+    // retire stage ks+1 (this wave's own glds), keep the younger stages in flight, then one barrier so
+    // every wave's part of stage ks+1 has landed and every wave is done reading stage ks.
+    if (NST == 3 && ks + 2 < nks) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(NI) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    cur = cur + 1 == NST ? 0 : cur + 1;
   }
 #undef DMA_ISSUE
+  __syncthreads();
   float* red = reinterpret_cast<float*>(smem);
   conv_fwd_epilogue<BCO, BP, WM, WN, BIAS, STATS, TCO, TP>(a, acc, red, g, pb, co0, wco, wp, fr, fq, tid);
 }
@@ -425,7 +442,7 @@ void conv3d_fwd(uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t xs, uintptr_
     NIDT_REQUIRE(nwg < (1ll << 31), "conv3d_fwd: grid too large");
     dim3 g1((unsigned)nwg);
 #define NIDT_DMA(BC, WM, BI, ST) \
-    hipLaunchKernelGGL((k_conv_fwd_dma<BC, WM, 4, BI, ST>), g1, dim3(256 * WM), 0, s, a, nCO)
+    hipLaunchKernelGGL((k_conv_fwd_dma<BC, WM, 4, 2, BI, ST>), g1, dim3(256 * WM), 0, s, a, nCO)
     if (bco == 128) {
       if (st) NIDT_DMA(128, 2, true, true); else if (hb) NIDT_DMA(128, 2, true, false); else NIDT_DMA(128, 2, false, false);
     } else {
