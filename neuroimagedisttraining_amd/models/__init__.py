@@ -54,6 +54,9 @@ def create_model(model_name, dataset="ABCD", class_num=1, in_shape=None, input_d
         return cnn_cifar10_meta(n_cls=class_num)
     if name in ("lr", "logistic_regression"):
         return LogisticRegression(input_dim, class_num)
+    if name in ("resnet20_meta", "resnet_meta"):
+        from .meta_resnet import resnet20_meta
+        return resnet20_meta(class_num)
     if name == "resnet56_ip":
         return resnet56_ip(class_num)
     if name in ("resnet18_gn", "resnet50_gn"):

@@ -220,3 +220,17 @@ def test_alexnet3d_state_dict_keys_match_reference():
     assert keys == exp
     n = sum(p.numel() for p in AlexNet3D_Dropout(num_classes=1).parameters())
     assert n == 2570241  # SURVEY.md §6 workload constants
+
+
+def test_meta_resnet_generates_weights_for_any_gene():
+    import random
+    from neuroimagedisttraining_amd.models.meta_resnet import MetaResNet20
+    torch.manual_seed(0)
+    m = MetaResNet20(num_classes=10, blocks=2)
+    x = torch.randn(3, 3, 32, 32)
+    rng = random.Random(1)
+    for gene in (m.max_gene(), m.random_gene(rng), [0] * m.gene_length()):
+        out = m(x, gene)
+        assert out.shape == (3, 10)
+    out.sum().backward()
+    assert m.stem.gen.fc2.weight.grad is not None and float(m.stem.gen.fc2.weight.grad.abs().sum()) > 0
