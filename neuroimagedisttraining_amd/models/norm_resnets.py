@@ -306,3 +306,21 @@ def resnet56_ip(num_classes=10):
 
 def resnet110_ip(num_classes=10):
     return ResNet_ip(110, num_classes)
+
+
+def DataParallelWithCallback(module, device_ids=None, output_device=None):  # noqa: N802 (reference name)
+    """Reference ``batchnorm_utils.DataParallelWithCallback`` (single-process ``nn.DataParallel`` whose replicas
+    sync BN through a master callback).  MI355X-native equivalent: one process per GPU — when a process group
+    is initialised the module is wrapped in ``DistributedDataParallel`` (gradients all-reduced over RCCL,
+    :class:`SynchronizedBatchNorm2d` statistics all-reduced in its forward); otherwise it is returned as is."""
+    import torch.distributed as dist
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        dev = next(module.parameters()).device
+        ids = [dev.index] if dev.type == "cuda" else None
+        return torch.nn.parallel.DistributedDataParallel(module, device_ids=ids, output_device=output_device)
+    return module
+
+
+def patch_replication_callback(data_parallel):
+    """No-op: there are no in-process replicas to patch (see :func:`DataParallelWithCallback`)."""
+    return data_parallel
