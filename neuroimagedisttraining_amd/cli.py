@@ -111,6 +111,7 @@ def add_args(parser, algo):
     a("--aggregator", type=str, default="fedavg")
     a("--byzantine_f", type=int, default=0)
     a("--trim_ratio", type=float, default=0.1)
+    a("--update_topk", type=float, default=0.0, help="send only the top-k fraction of each client's update")
     a("--group", type=int, default=0)
     a("--checkpoint_dir", type=str, default="")
     a("--resume", type=int, default=0)
@@ -231,7 +232,8 @@ def run_hip(args, algo, logger):
                    dense_ratio=getattr(args, "dense_ratio", 1.0), itersnip_iteration=getattr(args, "itersnip_iteration", 1),
                    snip_mask=getattr(args, "snip_mask", True), frequency_of_the_test=args.frequency_of_the_test,
                    seed=args.seed, prox_mu=args.fedprox_mu if algo == "fedprox" else 0.0, group=args.group,
-                   aggregator=args.aggregator, byzantine_f=args.byzantine_f, trim_ratio=args.trim_ratio)
+                   aggregator=args.aggregator, byzantine_f=args.byzantine_f, trim_ratio=args.trim_ratio,
+                   update_topk=args.update_topk)
     runner = FLRunner(eng, splits, cfg, info, model, logger=logger,
                       algorithm="salientgrads" if algo == "sailentgrads" else "fedavg")
     start = 0

@@ -66,6 +66,8 @@ class FLConfig:
     multikrum_m: int = 0          # Multi-Krum: number of selected clients (0 = K - f)
     trim_ratio: float = 0.1       # trimmed mean: fraction cut from each end per coordinate
     sparse_aggregate: bool = True  # SalientGrads: all-reduce only the coordinates kept by the global mask
+    update_topk: float = 0.0      # >0: each client sends only its top-k |update| (values + int32 indices,
+                                  # k = update_topk * P) through an RCCL all-gather (BASELINE config 5)
 
 
 # ------------------------------------------------------------------------------------------------
@@ -399,7 +401,40 @@ class FLRunner:
     def aggregate(self, sampled):
         if self.cfg.aggregator != "fedavg":
             return self.aggregate_robust(sampled)
+        if self.cfg.update_topk > 0:
+            return self.aggregate_topk(sampled)
         return self.aggregate_fedavg(sampled)
+
+    def aggregate_topk(self, sampled):
+        """Sparse-update FedAvg: client i contributes n_i/N * topk(theta_i - w_global) (fixed k per client, so
+        the all-gather needs no padding), BN buffers are averaged densely.  Every rank applies the same
+        gathered (index, value) lists in global client order, so all ranks end with the same model."""
+        sset = set(sampled)
+        n_tot = float(sum(len(self.splits[c].train) for c in sampled))
+        k = max(1, int(math.ceil(self.cfg.update_topk * self.P)))
+        rows = [i for i, c in enumerate(self.local) if c in sset]
+        vals = torch.zeros((len(rows), k), dtype=torch.float32, device=self.device)
+        idx = torch.zeros((len(rows), k), dtype=torch.int32, device=self.device)
+        for j, r in enumerate(rows):
+            d = self.theta[r, :self.P] - self.w_global
+            top = torch.topk(d.abs(), k, sorted=False).indices
+            idx[j] = top.int()
+            vals[j] = d.index_select(0, top) * (len(self.splits[self.local[r]].train) / n_tot)
+        cid = torch.tensor([self.local[r] for r in rows], dtype=torch.float32, device=self.device)
+        g_vals = rt.all_gather_cat(vals.view(-1), self.info).view(-1, k)
+        g_idx = rt.all_gather_cat(idx.view(-1), self.info).view(-1, k).long()
+        g_cid = rt.all_gather_cat(cid, self.info)
+        order = torch.argsort(g_cid)
+        upd = torch.zeros(self.P, dtype=torch.float32, device=self.device)
+        for j in order.tolist():  # fixed order: identical fp32 sums on every rank
+            upd.index_add_(0, g_idx[j], g_vals[j])
+        self.w_global.add_(upd)
+        bsum = torch.zeros(self.Q, dtype=torch.float32, device=self.device)
+        for r in rows:
+            bsum.add_(self.bufs[r, :self.Q], alpha=len(self.splits[self.local[r]].train) / n_tot)
+        rt.all_reduce_buckets(bsum, self.info)
+        self.b_global.copy_(bsum)
+        self.stat_info["aggregate_elems"] = int(2 * k * len(sampled))
 
     def _compact_index(self, Pp):
         """Flat indices of the aggregation buffer that can be non-zero: SalientGrads' global mask zeroes the

@@ -130,7 +130,7 @@ def _dist_worker(rank, world, port, out, cfg_kw=None):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("cfg_kw", [{}, {"aggregator": "median"}])
+@pytest.mark.parametrize("cfg_kw", [{}, {"aggregator": "median"}, {"update_topk": 0.1}])
 def test_two_rank_gloo_matches_single_process(tmp_path, cfg_kw):
     """2 ranks (clients sharded, mask-compacted all-reduce / all-gathered robust aggregation) == 1 process."""
     import socket
@@ -183,3 +183,14 @@ def test_executor_checkpoint_resume_is_exact(tmp_path):
     assert torch.equal(a.w_global, c.w_global)
     assert torch.equal(a.theta, c.theta)
     assert c.stat_info["global_test_acc"][-1] == a.stat_info["global_test_acc"][-1]
+
+
+def test_topk_update_aggregation_full_k_equals_fedavg():
+    """update_topk = 1.0 sends every coordinate: identical to dense FedAvg of the params."""
+    a = _runner(update_topk=1.0)
+    b = _runner()
+    for r in (a, b):
+        r.generate_global_mask_snip()
+        r.run_round(0)
+    assert torch.allclose(a.w_global, b.w_global, atol=1e-6)
+    assert torch.allclose(a.b_global, b.b_global, atol=1e-6)
