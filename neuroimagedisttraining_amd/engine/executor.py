@@ -116,8 +116,10 @@ class TorchEngine:
     ``store``: float tensor ``[N, ...]`` of inputs (already scaled); ``labels``: ``[N]``.
     ``loss``: ``"bce"`` (class_num=1, logits [B,1]) or ``"ce"`` (multi-class)."""
 
-    def __init__(self, template_model, store, labels, device, loss="bce", dtype=torch.float32):
+    def __init__(self, template_model, store, labels, device, loss="bce", dtype=torch.float32, amp=False):
         self.model = template_model.to(device)
+        # amp: bf16 autocast for the forward/backward (fp32 master rows, fp32 optimizer) on MIOpen
+        self.amp = bool(amp) and torch.device(device).type == "cuda"
         self.players = ParamLayout.from_tensors(list(self.model.named_parameters()))
         self.blayers = ParamLayout.from_tensors(list(self.model.named_buffers()))
         self.store, self.labels, self.device, self.loss, self.dtype = store, labels, torch.device(device), loss, dtype
@@ -155,7 +157,8 @@ class TorchEngine:
             bview = self._views(bufs[g], self.blayers)
             bv = {k: v.clone() for k, v in bview.items()}
             x, y = self._batch(idx[g * B:(g + 1) * B])
-            out = functional_call(self.model, {**pv, **bv}, (x,))
+            with torch.autocast("cuda", dtype=torch.bfloat16, enabled=self.amp):
+                out = functional_call(self.model, {**pv, **bv}, (x,))
             if isinstance(out, (list, tuple)):
                 out = out[0]
             loss = self._loss(out, y)
@@ -176,7 +179,8 @@ class TorchEngine:
                 pv = self._views(theta[g], self.players)
                 bv = self._views(bufs[g].clone(), self.blayers)
                 x, _ = self._batch(idx[g * B:(g + 1) * B])
-                out = functional_call(self.model, {**pv, **bv}, (x,))
+                with torch.autocast("cuda", dtype=torch.bfloat16, enabled=self.amp):
+                    out = functional_call(self.model, {**pv, **bv}, (x,))
                 if isinstance(out, (list, tuple)):
                     out = out[0]
                 outs.append(out.float())
