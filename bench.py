@@ -45,6 +45,10 @@ def parse():
     ap.add_argument("--dense-ratio", type=float, default=0.5)
     ap.add_argument("--seed", type=int, default=1024)
     ap.add_argument("--no-eval", action="store_true", help="(diagnostic only) skip per-round evaluation")
+    ap.add_argument("--algorithm", default="salientgrads", choices=["salientgrads", "fedavg", "fedprox"],
+                    help="other BASELINE configs: fedavg (config 2: --clients 8), fedprox + --aggregator (config 4)")
+    ap.add_argument("--aggregator", default="fedavg", choices=["fedavg", "krum", "multikrum", "median", "trimmed_mean"])
+    ap.add_argument("--prox-mu", type=float, default=0.01)
     ap.add_argument("--phase-timers", action="store_true")
     return ap.parse_args()
 
@@ -83,10 +87,13 @@ def main():
     engine = HipEngine(model, x8, mom, labels, info.device)
     cfg = FLConfig(comm_round=args.warmup + args.steps, epochs=args.epochs, batch_size=args.batch,
                    dense_ratio=args.dense_ratio, seed=args.seed, group=args.group,
-                   frequency_of_the_test=0 if args.no_eval else 1)
-    runner = FLRunner(engine, splits, cfg, info, model, logger=None, algorithm="salientgrads")
+                   frequency_of_the_test=0 if args.no_eval else 1, aggregator=args.aggregator,
+                   prox_mu=args.prox_mu if args.algorithm == "fedprox" else 0.0)
+    alg = "salientgrads" if args.algorithm == "salientgrads" else "fedavg"
+    runner = FLRunner(engine, splits, cfg, info, model, logger=None, algorithm=alg)
     t0 = time.perf_counter()
-    runner.generate_global_mask_snip()
+    if alg == "salientgrads":
+        runner.generate_global_mask_snip()
     torch.cuda.synchronize()
     t_snip = time.perf_counter() - t0
     for r in range(args.warmup):
@@ -107,9 +114,12 @@ def main():
     dt = rt.max_over_ranks(dt, info)
     ms = dt * 1000.0 / max(1, args.steps)
     value = args.steps / dt
+    headline = args.algorithm == "salientgrads" and args.clients == 64 and args.aggregator == "fedavg"
     if info.is_main:
         out = {
-            "metric": "FL rounds/sec (whole node), 64-client SalientGrads 3D-CNN on ABCD-shape synth",
+            "metric": ("FL rounds/sec (whole node), 64-client SalientGrads 3D-CNN on ABCD-shape synth" if headline else
+                       "FL rounds/sec (whole node), %d-client %s%s 3D-CNN on ABCD-shape synth"
+                       % (args.clients, args.algorithm, "" if args.aggregator == "fedavg" else "+" + args.aggregator)),
             "value": round(value, 4),
             "unit": "rounds/s",
             "n_gpus": info.world,
@@ -118,10 +128,13 @@ def main():
             "ms_per_step": round(ms, 2),
             "higher_is_better": True,
             "scaling": "strong",
-            "vs_baseline": (round(value / EAGER_BASELINE_ROUNDS_PER_S, 2) if EAGER_BASELINE_ROUNDS_PER_S else None),
+            "vs_baseline": (round(value / EAGER_BASELINE_ROUNDS_PER_S, 2)
+                            if EAGER_BASELINE_ROUNDS_PER_S and headline else None),
             "dtype": "bf16",
             "data": "synthetic",
-            "config": {"model": "AlexNet3D_Dropout", "algorithm": "SalientGrads", "clients": args.clients,
+            "config": {"model": "AlexNet3D_Dropout", "algorithm": {"salientgrads": "SalientGrads", "fedavg": "FedAvg",
+                                                                  "fedprox": "FedProx"}[args.algorithm],
+                       "aggregator": args.aggregator, "clients": args.clients,
                        "global_batch": args.batch * args.clients, "batch_per_client": args.batch,
                        "seq_len": None, "input": "1x121x145x121", "epochs": args.epochs,
                        "train_per_client": args.train_per_client, "test_per_client": args.test_per_client,
