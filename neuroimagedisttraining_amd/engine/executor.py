@@ -82,12 +82,17 @@ class HipEngine:
         self.x8, self.mom, self.labels = x8, mom, labels
         self.device = torch.device(device)
         self.m = ops.ext()
+        self._cid_cache = {}
 
     def train_step(self, theta, bufs, grads, idx, G, B, keep, seed, cids=None):
         y = self.labels.index_select(0, idx.long())
         ct = None
         if cids is not None:
-            ct = torch.as_tensor(list(cids), dtype=torch.int32).to(self.device, non_blocking=True)
+            key = tuple(int(c) for c in cids)
+            ct = self._cid_cache.get(key)
+            if ct is None:  # one upload per client group, reused by every step
+                ct = torch.tensor(key, dtype=torch.int32, device=self.device)
+                self._cid_cache[key] = ct
         return self.net.train_step(theta, bufs, grads, self.x8, self.mom, idx, y, G, B, keep, seed, ct)
 
     def eval_logits(self, theta, bufs, idx, G, B):
@@ -290,6 +295,10 @@ class FLRunner:
         nsteps = max(int(math.ceil(len(o) / B)) for o in orders) if orders else 0
         if n_batches is not None:
             nsteps = min(nsteps, n_batches)
+        # Plan every (step, group) launch first and upload all sample indices in ONE pinned, non-blocking
+        # copy: a per-step pageable host->device copy would synchronise the host with the GPU every local
+        # step and expose the next step's launch latency.
+        plan, chunks, off = [], [], 0
         for s in range(nsteps):
             by_size = {}
             for r, o in zip(rows, orders):
@@ -298,9 +307,22 @@ class FLRunner:
                     by_size.setdefault(len(chunk), []).append((r, chunk))
             for bsz, items in sorted(by_size.items(), reverse=True):
                 for grp in self._groups(items):
-                    rr = [r for r, _ in grp]
-                    idx = torch.from_numpy(np.concatenate([ch for _, ch in grp]).astype(np.int32)).to(self.device)
-                    fn(rr, idx, len(grp), bsz)
+                    n = sum(len(ch) for _, ch in grp)
+                    plan.append(([r for r, _ in grp], off, n, len(grp), bsz))
+                    chunks.extend(ch for _, ch in grp)
+                    off += n
+        if not plan:
+            return
+        all_idx = self._upload_i32(np.concatenate(chunks))
+        for rr, o, n, G, bsz in plan:
+            fn(rr, all_idx[o:o + n], G, bsz)
+
+    def _upload_i32(self, arr):
+        """int32 host array -> device tensor through pinned memory, without blocking the host."""
+        t = torch.from_numpy(np.ascontiguousarray(arr, dtype=np.int32))
+        if self.device.type != "cuda":
+            return t
+        return t.pin_memory().to(self.device, non_blocking=True)
 
     def _with_rows(self, rr, body):
         """Run ``body(theta, bufs, grads, mom)`` on rows ``rr`` (in place when they are a contiguous run)."""
@@ -381,9 +403,13 @@ class FLRunner:
         rows = [self.local.index(c) for c in loc]
         if not rows:
             return
-        for r in rows:
-            self.theta[r].copy_(self.w_global)
-            self.bufs[r].copy_(self.b_global)
+        if rows == list(range(rows[0], rows[-1] + 1)):  # one broadcast launch for the whole shard
+            self.theta[rows[0]:rows[-1] + 1].copy_(self.w_global.expand(len(rows), -1))
+            self.bufs[rows[0]:rows[-1] + 1].copy_(self.b_global.expand(len(rows), -1))
+        else:
+            for r in rows:
+                self.theta[r].copy_(self.w_global)
+                self.bufs[r].copy_(self.b_global)
         lr = cfg.lr * (cfg.lr_decay ** round_idx)
         first = [True]
         for ep in range(cfg.epochs):
@@ -538,8 +564,9 @@ class FLRunner:
             tb = self.cfg.test_batch
             acc = torch.zeros((len(js), 3), dtype=torch.float64, device=self.device)
             own_t = torch.from_numpy(owner).to(self.device)
+            all_t = self._upload_i32(allidx)
             for s in range(0, allidx.size, tb):
-                idx = torch.from_numpy(allidx[s:s + tb]).to(self.device)
+                idx = all_t[s:s + tb]
                 logits = self.e.eval_logits(th, bu, idx, 1, idx.numel()).view(-1)
                 y = self.e.labels.index_select(0, idx.long()).to(logits.device).float()
                 pred = torch.sigmoid(logits)
@@ -555,6 +582,7 @@ class FLRunner:
     def _eval_grouped(self, theta, bufs, rows, clients):
         """Personal models: clients with equal test sizes are evaluated in one grouped launch."""
         out = np.zeros((len(clients), 3), dtype=np.float64)
+        pending = []  # (client positions, device result): one device->host copy at the end
         sizes = {}
         for j, c in enumerate(clients):
             sizes.setdefault(len(self.splits[c].test), []).append(j)
@@ -571,15 +599,19 @@ class FLRunner:
                 if rr != list(range(lo, hi)):
                     out[grp] = self._eval_rows(theta, bufs, [clients[j] for j in grp], rr)
                     continue
-                idx = torch.from_numpy(np.concatenate([self.splits[clients[j]].test for j in grp]).astype(np.int32))
-                idx = idx.to(self.device)
+                idx = self._upload_i32(np.concatenate([self.splits[clients[j]].test for j in grp]))
                 logits = self.e.eval_logits(theta[lo:hi], bufs[lo:hi], idx, len(grp), n).view(len(grp), n)
                 y = self.e.labels.index_select(0, idx.long()).to(logits.device).float().view(len(grp), n)
                 pred = torch.sigmoid(logits)
                 loss = F.binary_cross_entropy_with_logits(pred, y, reduction="none").sum(1)
                 correct = ((pred >= 0.5).float() == y).float().sum(1)
-                res = torch.stack([correct, loss, torch.full_like(loss, n)], 1).double().cpu().numpy()
-                out[grp] = res
+                pending.append((grp, torch.stack([correct, loss, torch.full_like(loss, n)], 1).double()))
+        if pending:
+            host = torch.cat([r for _, r in pending], 0).cpu().numpy()
+            o = 0
+            for grp, r in pending:
+                out[grp] = host[o:o + len(grp)]
+                o += len(grp)
         return out
 
     def evaluate(self, round_idx):

@@ -1,21 +1,51 @@
-"""Summarise a rocprofv3 rocpd SQLite database (kernel-trace) into a per-kernel stats table."""
+"""Summarise a rocprofv3 rocpd SQLite database (kernel-trace) into a per-kernel stats table.
+
+``--window-ms W`` restricts the table to dispatches that start in the last W ms of the trace (the timed
+rounds of a bench run come last) and adds a timeline line: wall span, GPU busy time (union of kernel
+intervals), idle fraction and the largest inter-kernel gaps — the launch/sync overhead a hipGraph or
+sync removal would recover.
+"""
+import argparse
 import sqlite3
-import sys
 
 
-def main(db, top=30, out=None):
+def main(db, top=30, out=None, window_ms=None):
     con = sqlite3.connect(db)
     cur = con.cursor()
-    cols = [r[1] for r in cur.execute("pragma table_info(rocpd_kernel_dispatch)")]
-    q = """select s.display_name, count(*), sum(d.end - d.start), avg(d.end - d.start), min(d.end-d.start), max(d.end-d.start)
-           from rocpd_kernel_dispatch d join rocpd_info_kernel_symbol s on d.kernel_id = s.id
-           group by s.display_name order by sum(d.end - d.start) desc"""
-    rows = cur.execute(q).fetchall()
-    tot = sum(r[2] for r in rows)
+    q = """select s.display_name, d.start, d.end
+           from rocpd_kernel_dispatch d join rocpd_info_kernel_symbol s on d.kernel_id = s.id"""
+    ev = cur.execute(q).fetchall()
+    if window_ms:
+        t_end = max(e for _, _, e in ev)
+        ev = [x for x in ev if x[1] >= t_end - window_ms * 1e6]
+    agg = {}
+    for name, s, e in ev:
+        a = agg.setdefault(name, [0, 0, 0])
+        a[0] += 1
+        a[1] += e - s
+    rows = sorted(((n, a[0], a[1]) for n, a in agg.items()), key=lambda r: -r[2])
+    tot = sum(r[2] for r in rows) or 1
     lines = ["%-90s %8s %12s %10s %6s" % ("kernel", "calls", "total_ms", "avg_us", "pct")]
-    for name, n, s, a, mn, mx in rows[:top]:
-        lines.append("%-90s %8d %12.3f %10.2f %6.2f" % (name[:90], n, s / 1e6, a / 1e3, 100.0 * s / tot))
-    lines.append("TOTAL kernel time %.3f ms over %d kernels (%d dispatches)" % (tot / 1e6, len(rows), sum(r[1] for r in rows)))
+    for name, n, s in rows[:top]:
+        lines.append("%-90s %8d %12.3f %10.2f %6.2f" % (name[:90], n, s / 1e6, s / n / 1e3, 100.0 * s / tot))
+    lines.append("TOTAL kernel time %.3f ms over %d kernels (%d dispatches)" % (tot / 1e6, len(rows), len(ev)))
+    if ev:
+        iv = sorted((s, e) for _, s, e in ev)
+        busy, gaps = 0, []
+        cs, ce = iv[0]
+        for s, e in iv[1:]:
+            if s > ce:
+                busy += ce - cs
+                gaps.append(s - ce)
+                cs, ce = s, e
+            else:
+                ce = max(ce, e)
+        busy += ce - cs
+        span = iv[-1][1] - iv[0][0]
+        gaps.sort(reverse=True)
+        lines.append("TIMELINE span %.3f ms, GPU busy %.3f ms, idle %.1f %%, %d gaps (sum %.3f ms; largest us: %s)"
+                     % (span / 1e6, busy / 1e6, 100.0 * (span - busy) / max(span, 1), len(gaps), sum(gaps) / 1e6,
+                        ", ".join("%.0f" % (g / 1e3) for g in gaps[:8])))
     txt = "\n".join(lines)
     print(txt)
     if out:
@@ -23,4 +53,10 @@ def main(db, top=30, out=None):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], out=sys.argv[2] if len(sys.argv) > 2 else None)
+    ap = argparse.ArgumentParser()
+    ap.add_argument("db")
+    ap.add_argument("out", nargs="?")
+    ap.add_argument("--top", type=int, default=30)
+    ap.add_argument("--window-ms", type=float, default=None)
+    a = ap.parse_args()
+    main(a.db, top=a.top, out=a.out, window_ms=a.window_ms)
