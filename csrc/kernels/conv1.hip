@@ -538,8 +538,10 @@ __global__ __launch_bounds__(256) void k_conv1_wgrad(const uint8_t* __restrict__
   }
 }
 
-// Reduce slabs per client and apply the closed form.  grid (64 c, G), block 128 (k).
-__global__ __launch_bounds__(128) void k_conv1_wgrad_fin(const float* __restrict__ part, int B,
+// Reduce slabs per client and apply the closed form.  grid (64 c, G), block 256: the B*19 slabs are split
+// over the 4 waves (lane = k, k + 64; 4 independent loads in flight per lane instead of one dependent chain),
+// merged through LDS in a fixed order (deterministic), then threads 0..127 (k) apply the closed form.
+__global__ __launch_bounds__(256) void k_conv1_wgrad_fin(const float* __restrict__ part, int B,
                                                          const float* __restrict__ w125, const float* __restrict__ mu,
                                                          const float* __restrict__ covw,
                                                          const float* __restrict__ invstd, const float* theta,
@@ -548,17 +550,41 @@ __global__ __launch_bounds__(128) void k_conv1_wgrad_fin(const float* __restrict
                                                          int64_t goff_b, float wscale) {
   __shared__ double red[2];
   __shared__ double sD, sdg;
-  const int c = blockIdx.x, g = blockIdx.y, k = threadIdx.x;
+  __shared__ double wpart[4][128];
+  const int c = blockIdx.x, g = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int nslab = B * kPD;
-  double S = 0, D = 0;
-  for (int sl = 0; sl < nslab; ++sl) {
-    const float* o = part + (((int64_t)g * nslab + sl) * kC1 + c) * 126;
-    if (k < 125) S += o[k];
-    if (k == 0) D += o[125];
+  {
+    const float* base = part + ((int64_t)g * nslab * kC1 + c) * 126;
+    const int64_t sst = (int64_t)kC1 * 126;  // slab stride
+    double a0 = 0, a1 = 0;
+    const bool hi = lane + 64 < 126;
+    int sl = wid;
+    for (; sl + 12 < nslab; sl += 16) {
+      float v0[4], v1[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const float* o = base + (int64_t)(sl + 4 * u) * sst;
+        v0[u] = o[lane];
+        v1[u] = hi ? o[lane + 64] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) { a0 += v0[u]; a1 += v1[u]; }
+    }
+    for (; sl < nslab; sl += 4) {
+      const float* o = base + (int64_t)sl * sst;
+      a0 += o[lane];
+      if (hi) a1 += o[lane + 64];
+    }
+    wpart[wid][lane] = a0;
+    wpart[wid][lane + 64] = a1;
   }
-  if (k == 0) sD = D;
   __syncthreads();
-  D = sD;
+  if (tid >= 128) return;
+  const int k = tid;
+  double S = k < 125 ? ((wpart[0][k] + wpart[1][k]) + (wpart[2][k] + wpart[3][k])) : 0.0;
+  if (k == 0) sD = (wpart[0][125] + wpart[1][125]) + (wpart[2][125] + wpart[3][125]);
+  __syncthreads();
+  double D = sD;
   const int i = g * kC1 + c;
   const double iv = invstd[i];
   const double gm = theta[(int64_t)g * ldt + off_g + c];
@@ -713,7 +739,7 @@ void conv1_wgrad(uintptr_t x8, uintptr_t idx, uintptr_t dp, uintptr_t pout, uint
                      ptr<float>(part));
   NIDT_CHECK(hipGetLastError());
   const int G = NB / B;
-  hipLaunchKernelGGL(k_conv1_wgrad_fin, dim3(kC1, G), dim3(128), 0, s, ptr<const float>(part), B,
+  hipLaunchKernelGGL(k_conv1_wgrad_fin, dim3(kC1, G), dim3(256), 0, s, ptr<const float>(part), B,
                      ptr<const float>(w125), ptr<const float>(mu), ptr<const float>(covw), ptr<const float>(invstd),
                      ptr<const float>(theta), ldt, off_g, ptr<float>(grad), ldg, goff_w, goff_bias, goff_g, goff_b,
                      wscale);

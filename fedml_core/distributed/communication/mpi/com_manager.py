@@ -1,2 +1,3 @@
-"""Compat shim: reference import path ``fedml_core/distributed/communication/mpi/com_manager.py`` -> ``neuroimagedisttraining_amd.comm.managers``."""
-from neuroimagedisttraining_amd.comm.managers import MpiCommunicationManager  # noqa: F401
+"""Compat shim: reference import path ``fedml_core/distributed/communication/mpi/com_manager.py`` ->
+``neuroimagedisttraining_amd.comm.mpi_threads`` (send/receive threads over an mpi4py-like ``comm``)."""
+from neuroimagedisttraining_amd.comm.mpi_threads import MpiCommunicationManager, TorchP2PComm  # noqa: F401

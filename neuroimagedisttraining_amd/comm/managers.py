@@ -10,7 +10,9 @@ Backends (``backend=`` of the managers):
 * ``"GRPC"`` — a real gRPC server per rank (``grpcio`` generic unary handler, 100 MB messages, port
   ``base_port + rank``, peers from an ``ip_config`` CSV ``receiver_id,ip``) — the reference's backend without
   generated stubs, and importable (the reference's is not, quirk Q17).
-* ``"MPI"`` / ``"MQTT"`` — need ``mpi4py`` / ``paho-mqtt``; they raise a clear ImportError when absent.
+* ``"MPI"`` — the reference's send/receive-thread manager (``mpi_threads.py``) over an ``mpi4py``-like ``comm``;
+  without mpi4py it runs over :class:`TorchP2PComm` (torch.distributed point-to-point).
+* ``"MQTT"`` — needs ``paho-mqtt``; raises a clear ImportError when absent.
 
 The receive loop is event driven (blocking queue get with timeout) rather than the reference's 0.3 s polling.
 """
@@ -126,8 +128,30 @@ class TorchDistCommManager(_QueueCommManager):
         self._stop.set()
 
 
+class GRPCCOMMServicer:
+    """Server side of the reference's ``gRPCCommManager`` service (``gRPC/grpc_server.py:9-40``): every
+    ``sendMessage`` request's JSON payload is queued for the owning manager's receive loop."""
+
+    def __init__(self, host, port, client_num, client_id, q=None):
+        self.host, self.port, self.client_num, self.client_id = host, port, client_num, client_id
+        self.node_type = "server" if client_id == 0 else "client"
+        self.message_q = q if q is not None else queue.Queue()
+
+    def sendMessage(self, request, context):  # noqa: N802 (service method name)
+        from .grpc_proto import CommResponse
+        log.debug("client_%d got a message from client_%d (%s)", self.client_id, request.client_id, context.peer())
+        self.message_q.put(request.message)  # queue.Queue is already thread-safe (no global lock needed)
+        return CommResponse(client_id=self.client_id, message="message received")
+
+    def handleReceiveMessage(self, request, context):  # noqa: N802
+        from .grpc_proto import CommResponse
+        return CommResponse(client_id=self.client_id, message="")
+
+
 class GRPCCommManager(_QueueCommManager):
-    """gRPC backend: every rank serves ``/nidt.Comm/sendMessage`` (bytes in, bytes out)."""
+    """gRPC backend speaking the reference's ``gRPCCommManager`` protobuf service (wire compatible with its
+    generated stubs): every rank serves ``sendMessage`` on ``base_port + client_id``; a send opens a channel to
+    the receiver (IP from the ``ip_config`` CSV ``receiver_id,ip``) with 100 MB message limits."""
 
     MAX_MSG = 100 * 1024 * 1024
 
@@ -135,26 +159,33 @@ class GRPCCommManager(_QueueCommManager):
         super().__init__()
         import grpc
         from concurrent import futures
-        self.grpc = grpc
-        self.client_id = client_id
+        from . import grpc_proto
+        self.grpc, self.proto = grpc, grpc_proto
+        self.client_id, self.client_num = client_id, client_num
         self.base_port = base_port
         self.ip_config = self._read_ip_config(ip_config_path) if ip_config_path else {}
-        opts = [("grpc.max_send_message_length", self.MAX_MSG), ("grpc.max_receive_message_length", self.MAX_MSG)]
-        self.server = grpc.server(futures.ThreadPoolExecutor(max_workers=4), options=opts)
-
-        def handle(request, context):
-            m = Message()
-            m.init_from_json_string(request.decode())
-            self.q.put(m)
-            return b"ok"
-
-        handler = grpc.method_handlers_generic_handler(
-            "nidt.Comm", {"sendMessage": grpc.unary_unary_rpc_method_handler(handle)})
-        self.server.add_generic_rpc_handlers((handler,))
+        self.opts = [("grpc.max_send_message_length", self.MAX_MSG),
+                     ("grpc.max_receive_message_length", self.MAX_MSG)]
+        self.server = grpc.server(futures.ThreadPoolExecutor(max_workers=4), options=self.opts)
         self.port = port or (base_port + client_id)
+        self._raw = queue.Queue()
+        self.servicer = GRPCCOMMServicer(host, self.port, client_num, client_id, q=self._raw)
+        grpc_proto.add_gRPCCommManagerServicer_to_server(self.servicer, self.server)
         self.server.add_insecure_port("%s:%d" % (host, self.port))
         self.server.start()
-        self.opts = opts
+        self._stop = threading.Event()
+        self._rx = threading.Thread(target=self._decode_loop, daemon=True)
+        self._rx.start()
+
+    def _decode_loop(self):
+        while not self._stop.is_set():
+            try:
+                s = self._raw.get(timeout=0.05)
+            except queue.Empty:
+                continue
+            m = Message()
+            m.init_from_json_string(s)
+            self.q.put(m)
 
     @staticmethod
     def _read_ip_config(path):
@@ -169,20 +200,16 @@ class GRPCCommManager(_QueueCommManager):
         rid = msg.get_receiver_id()
         ip = self.ip_config.get(rid, "127.0.0.1")
         with self.grpc.insecure_channel("%s:%d" % (ip, self.base_port + rid), options=self.opts) as ch:
-            call = ch.unary_unary("/nidt.Comm/sendMessage")
-            call(msg.to_json().encode(), timeout=60)
+            stub = self.proto.gRPCCommManagerStub(ch)
+            stub.sendMessage(self.proto.CommRequest(client_id=self.client_id, message=msg.to_json()), timeout=60)
 
     def stop_receive_message(self):
         super().stop_receive_message()
+        self._stop.set()
         self.server.stop(0)
 
 
-def MpiCommunicationManager(*a, **k):  # noqa: N802 (reference class name)
-    try:
-        import mpi4py  # noqa: F401
-    except ImportError as e:
-        raise ImportError("the MPI backend needs mpi4py (not installed); use backend='TORCH' or 'INPROC'") from e
-    raise NotImplementedError("MPI backend: use backend='TORCH' (torch.distributed) on MI355X nodes")
+from .mpi_threads import MpiCommunicationManager, TorchP2PComm  # noqa: E402,F401  (mpi4py-style manager)
 
 
 def MqttCommManager(*a, **k):  # noqa: N802

@@ -131,7 +131,15 @@ def load_partition_data_abcd(data_dir, partition_method="site", partition_alpha=
     cohort (and says so) when ``h5py`` or the file is unavailable."""
     path = data_dir
     if path and os.path.isdir(path):
-        path = os.path.join(path, "alldatain8bitsnormalized.h5")
+        nv = os.path.join(path, "alldatain8bitsnormalized.nidtvol")
+        path = nv if os.path.exists(nv) else os.path.join(path, "alldatain8bitsnormalized.h5")
+    if path and str(path).endswith(".nidtvol"):
+        # native NIDTVOL1 cohort (mmap + C++ gather, overlapped H2D when device is a GPU)
+        from .volume_file import VolumeFile
+        vf = VolumeFile(path)
+        store = vf.to_store(device=device)
+        train, test, _ = P.partition_by_site(vf.sites, max_clients=max_clients)
+        return _assemble(store, train, test, batch_size, 2, logger)
     try:
         X, y, site = _read_h5(path)
     except Exception as e:  # noqa: BLE001 - h5py missing or no file: synthetic fallback

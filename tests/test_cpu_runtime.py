@@ -1,0 +1,88 @@
+"""CPU tests of the native host runtime: the C++ NIDTVOL1 volume reader (``csrc/runtime/volume_io.cpp``) and
+its Python pipeline / ABCD-loader integration."""
+import numpy as np
+import pytest
+import torch
+
+from neuroimagedisttraining_amd.data.volume_file import VolumeFile, stream_to_device, write_volume_file
+
+
+def _cohort(n=11, shape=(9, 13, 7), seed=0):
+    rs = np.random.RandomState(seed)
+    return (rs.randint(0, 256, size=(n,) + shape).astype(np.uint8), rs.randint(0, 2, n).astype(np.float32),
+            rs.randint(0, 21, n).astype(np.float32))
+
+
+def test_volume_file_roundtrip_and_gather(tmp_path):
+    X, y, s = _cohort()
+    p = write_volume_file(str(tmp_path / "c.nidtvol"), X, y, s, chunk=4)
+    vf = VolumeFile(p, threads=3)
+    assert len(vf) == 11 and vf.shape == (9, 13, 7)
+    assert np.array_equal(vf.labels, y) and np.array_equal(vf.sites, s)
+    ix = [10, 0, 3, 3, 7]
+    got = vf.gather(ix)
+    assert got.dtype == torch.uint8 and np.array_equal(got.numpy(), X[ix])
+    out = torch.zeros((8,) + X.shape[1:], dtype=torch.uint8)
+    vf.gather([2, 5], out=out)
+    assert np.array_equal(out[:2].numpy(), X[[2, 5]]) and int(out[2:].sum()) == 0
+
+
+def test_volume_file_async_tickets_and_large_subjects(tmp_path):
+    # > 1 MiB per subject: each gather is split into several pieces across the worker pool
+    X, y, s = _cohort(n=5, shape=(64, 130, 130), seed=1)
+    vf = VolumeFile(write_volume_file(str(tmp_path / "big.nidtvol"), X, y, s), threads=4)
+    a = torch.empty((3,) + X.shape[1:], dtype=torch.uint8)
+    b = torch.empty((2,) + X.shape[1:], dtype=torch.uint8)
+    ta = vf.submit([4, 1, 2], a)
+    tb = vf.submit([0, 4], b)
+    vf.prefetch([3])
+    vf.wait(tb)
+    vf.wait(ta)
+    assert np.array_equal(a.numpy(), X[[4, 1, 2]]) and np.array_equal(b.numpy(), X[[0, 4]])
+
+
+def test_volume_file_validation(tmp_path):
+    X, y, s = _cohort(n=3)
+    p = write_volume_file(str(tmp_path / "v.nidtvol"), X, y, s)
+    vf = VolumeFile(p)
+    with pytest.raises(IndexError):
+        vf.gather([3])
+    bad = tmp_path / "bad.nidtvol"
+    bad.write_bytes(b"NOTAVOL!" + open(p, "rb").read()[8:])
+    with pytest.raises(RuntimeError, match="bad magic"):
+        VolumeFile(str(bad))
+    trunc = tmp_path / "trunc.nidtvol"
+    trunc.write_bytes(open(p, "rb").read()[:5000])
+    with pytest.raises(RuntimeError, match="truncated"):
+        VolumeFile(str(trunc))
+    with pytest.raises(TypeError):
+        write_volume_file(str(tmp_path / "f.nidtvol"), X.astype(np.float32), y)
+
+
+def test_stream_to_device_cpu_and_store(tmp_path):
+    X, y, s = _cohort(n=7)
+    vf = VolumeFile(write_volume_file(str(tmp_path / "c.nidtvol"), X, y, s))
+    v = stream_to_device(vf, [6, 2], "cpu", chunk=1)
+    assert np.array_equal(v.numpy(), X[[6, 2]])
+    st = vf.to_store([1, 4, 5])
+    assert len(st) == 3 and np.array_equal(st.volumes.numpy(), X[[1, 4, 5]])
+    assert np.array_equal(st.labels.numpy(), y[[1, 4, 5]])
+
+
+def test_abcd_loader_reads_volume_file_by_site(tmp_path):
+    from neuroimagedisttraining_amd.data.abcd import load_partition_data_abcd
+    rs = np.random.RandomState(3)
+    n = 60
+    X = rs.randint(0, 256, size=(n, 5, 6, 5)).astype(np.uint8)
+    y = rs.randint(0, 2, n).astype(np.float32)
+    site = (np.arange(n) % 4).astype(np.float32)
+    p = write_volume_file(str(tmp_path / "abcd.nidtvol"), X, y, site)
+    ds = load_partition_data_abcd(p, batch_size=4, max_clients=21)
+    num, trn, tst = ds[4], ds[5], ds[6]
+    assert sorted(num) == [0, 1, 2, 3] and sum(num.values()) + sum(len(t.indices) for t in tst.values()) == n
+    store = trn[0].store
+    assert tuple(store.shape) == (5, 6, 5)
+    xb, yb, sb = next(iter(trn[0]))
+    xv, yv = store.fetch(xb)
+    assert xv.shape == (len(xb), 1, 5, 6, 5)
+    assert np.array_equal(np.sort(yv.numpy()), np.sort(y[np.sort(xb.numpy().astype(int))]))

@@ -71,7 +71,37 @@ def build(force=False, verbose=True):
             raise RuntimeError("link failed:\n%s\n%s" % (" ".join(cmd), r.stderr[-4000:]))
         if verbose:
             print("[build_ext] linked", out, flush=True)
+    build_runtime(force, verbose)
     return out
+
+
+def runtime_name(name):
+    suffix = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
+    return os.path.join(ROOT, "neuroimagedisttraining_amd", "runtime", name + suffix)
+
+
+def build_runtime(force=False, verbose=True):
+    """Host-only native runtime modules (csrc/runtime/*.cpp -> neuroimagedisttraining_amd/runtime/<name>.so),
+    built with the system C++ compiler: no GPU toolchain or device needed to build, import or test them."""
+    rdir = os.path.join(ROOT, "csrc", "runtime")
+    cxx = os.environ.get("CXX", "g++")
+    outs = []
+    for f in sorted(os.listdir(rdir)):
+        if not f.endswith(".cpp"):
+            continue
+        src = os.path.join(rdir, f)
+        out = runtime_name("_nidt_" + f[:-4].split("_")[-1])
+        outs.append(out)
+        if not force and os.path.exists(out) and os.path.getmtime(out) >= os.path.getmtime(src):
+            continue
+        cmd = [cxx, "-O3", "-std=c++17", "-shared", "-fPIC", "-pthread", "-Wall", "-Wno-unused-result"] + \
+            _includes()[:2] + [src, "-o", out]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError("runtime build failed:\n%s\n%s" % (" ".join(cmd), r.stderr[-4000:]))
+        if verbose:
+            print("[build_ext] built", out, flush=True)
+    return outs
 
 
 if __name__ == "__main__":
