@@ -148,8 +148,9 @@ void conv1_sample_moments(uintptr_t x8, int64_t N, uintptr_t mom, uintptr_t stre
 }
 
 // ------------------------------------------------------------------------------------------------
-// weight packing: theta row g at off: [64][125] fp32 -> w8 [G][64][224] bf16 (x scale), w125 [G][64][125] f32
-// holding the bf16-rounded scaled weights (the exact values the MFMA uses) for the moment math.
+// weight packing: theta row g at off: [64][125] fp32 -> w8 [G][64][224] f16 bits of f16(w) (the forward's MFMA
+// A operand, against raw uint8 voxels), w125 [G][64][125] f32 = f16(w) * scale (scale = 1/255): the exact
+// effective weights of conv(x / 255) that the moment math (BN statistics) and the closed-form backward use.
 __global__ void k_pack_conv1_w(const float* __restrict__ theta, int64_t ldt, int64_t off, int64_t off_sign, int G,
                                float scale, uint16_t* __restrict__ w8, float* __restrict__ w125) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -159,8 +160,9 @@ __global__ void k_pack_conv1_w(const float* __restrict__ theta, int64_t ldt, int
   uint16_t v = 0;
   if (t < 27 && tp_valid(t, r)) {
     const int k = tp_to_k(t, r);
-    v = f32_to_bf16(theta[(int64_t)g * ldt + off + c * 125 + k] * scale);
-    w125[((int64_t)g * kC1 + c) * 125 + k] = bf16_to_f32(v);
+    const _Float16 h = (_Float16)theta[(int64_t)g * ldt + off + c * 125 + k];
+    v = __builtin_bit_cast(uint16_t, h);
+    w125[((int64_t)g * kC1 + c) * 125 + k] = (float)h * scale;
     // the fused forward expects sign(gamma_c) folded into its MFMA weights (exact sign flip)
     if (off_sign >= 0 && theta[(int64_t)g * ldt + off_sign + c] < 0.f) v ^= 0x8000u;
   }
@@ -262,26 +264,57 @@ void conv1_bnstats(uintptr_t mom, uintptr_t idx, int B, int G, uintptr_t Mb, uin
 }
 
 // ------------------------------------------------------------------------------------------------
-// Fused forward: conv1 (MFMA) -> z = conv*scale + shift -> max over 3x3x3 -> relu.  Block = (n, pd, ph),
-// 4 waves; wave w owns output columns ow = 15w .. 15w+14 (5 pooling windows), lane column = ow offset.
-// k_conv1_fwd_pool_pipe — same math as k_conv1_fwd_pool, but one block walks all 23 pooled rows (ph) of a
-// (sample, pd) slab: the next row's 5x5x64 halo is prefetched into registers (7 x 8 B per thread) while the
-// MFMAs of the current row run, then converted (v_cvt_f32_ubyteN + v_perm: u8 -> exact bf16) into the other
-// LDS buffer — the load latency and the conversion hide behind the matrix work instead of serialising a
-// one-row block.  1-D grid, XCD-remapped so the 19 pd-slabs of a sample (overlapping by 2 z-planes) share
-// an L2.
-__device__ __forceinline__ uint4 u8x8_to_bf16x8(uint2 v) {
-  const float f0 = (float)(v.x & 0xffu), f1 = (float)((v.x >> 8) & 0xffu);
-  const float f2 = (float)((v.x >> 16) & 0xffu), f3 = (float)(v.x >> 24);
-  const float f4 = (float)(v.y & 0xffu), f5 = (float)((v.y >> 8) & 0xffu);
-  const float f6 = (float)((v.y >> 16) & 0xffu), f7 = (float)(v.y >> 24);
-  uint4 o;  // integers 0..255 are exact in bf16: keep the high half of the f32
-  o.x = __builtin_amdgcn_perm(__float_as_uint(f1), __float_as_uint(f0), 0x07060302u);
-  o.y = __builtin_amdgcn_perm(__float_as_uint(f3), __float_as_uint(f2), 0x07060302u);
-  o.z = __builtin_amdgcn_perm(__float_as_uint(f5), __float_as_uint(f4), 0x07060302u);
-  o.w = __builtin_amdgcn_perm(__float_as_uint(f7), __float_as_uint(f6), 0x07060302u);
+// Fused forward: conv1 (MFMA) -> z = conv*scale + shift -> max over 3x3x3 -> relu, k_conv1_fwd_pool_pipe.
+// One block (4 waves) walks all 23 pooled rows (ph) of a (sample, pd) slab; wave w owns 32 output channels
+// (ch = w & 1) x 2 column groups of 15 conv columns (op = w >> 1); the next row's 5x5x64 polyphase halo is
+// prefetched into registers while the MFMAs of the current row run, then written into the other LDS buffer.
+// 1-D grid, XCD-remapped so the 19 pd-slabs of a sample (overlapping by 2 z-planes) share an L2.
+//
+// The kernel is VALU-issue bound, not MFMA bound (rocprofv3 PMC, profiles/r1_pmc_v4.txt: 1330 VALU vs 252
+// MFMA per wave-row), so every per-voxel and per-output VALU op counts:
+//  * operands are f16, not bf16.  A uint8 voxel becomes the f16 magic number 1024 + x with ONE v_perm per two
+//    voxels (exponent byte 0x64 spliced next to each data byte) instead of 8 cvt + 4 perm per 8 voxels; the
+//    weights are f16(w) (11-bit mantissa, more precise than bf16).  The +1024 offset is cancelled exactly by
+//    starting every accumulator at -1024 * sum_k A[c][k] (A = the packed, sign-folded row of channel c), so
+//    acc = sum_k A x = 255 * conv(x/255) with no cancellation in the final value;
+//  * the 3^3 window's argmax index (dd*9 + dh*3 + dw, dw = this lane's column in the window) rides in the 5
+//    low mantissa bits of each candidate: one v_and_or_b32 + one v_max (v_max3 across two dh rows);
+//  * the cross-lane (dw) part of the pool is two DPP row shifts + one v_max3 on the tagged values; the bf16
+//    output is one v_cvt_pk_bf16_f32 per two channels.
+__device__ __forceinline__ uint4 u8x8_to_f16magic(uint2 v) {
+  const uint32_t e = 0x64646464u;  // f16 0x64xx = 1024 + xx
+  uint4 o;
+  o.x = __builtin_amdgcn_perm(e, v.x, 0x04010400u);
+  o.y = __builtin_amdgcn_perm(e, v.x, 0x04030402u);
+  o.z = __builtin_amdgcn_perm(e, v.y, 0x04010400u);
+  o.w = __builtin_amdgcn_perm(e, v.y, 0x04030402u);
   return o;
 }
+
+__device__ __forceinline__ float tag_idx(float acc, uint32_t tag) {
+  return __uint_as_float((__float_as_uint(acc) & ~31u) | tag);
+}
+
+// plain v_max_f32 / v_max3_f32: fmaxf would first "canonicalise" each bit-built operand with an extra
+// v_max(x, x) (IEEE NaN quieting) — one wasted VALU op per candidate in this VALU-bound loop
+__device__ __forceinline__ float vmax2(float a, float b) {
+  float r;
+  asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ float vmax3(float a, float b, float c) {
+  float r;
+  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+
+__device__ __forceinline__ uint32_t pack_bf16x2_hw(float lo, float hi) {
+  typedef __bf16 bf2 __attribute__((ext_vector_type(2)));
+  const bf2 v = {(__bf16)lo, (__bf16)hi};  // v_cvt_pk_bf16_f32 (RNE)
+  return __builtin_bit_cast(uint32_t, v);
+}
+
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 
 __global__ __launch_bounds__(256, 2) void k_conv1_fwd_pool_pipe(const uint8_t* __restrict__ x8,
                                                                 const int* __restrict__ idx,
@@ -290,7 +323,7 @@ __global__ __launch_bounds__(256, 2) void k_conv1_fwd_pool_pipe(const uint8_t* _
                                                                 const float* __restrict__ shift, int B,
                                                                 uint16_t* __restrict__ out, uint8_t* __restrict__ amax) {
   constexpr int HX = 64;
-  constexpr int HALO = 5 * 5 * HX * 8;  // bf16 elements per buffer
+  constexpr int HALO = 5 * 5 * HX * 8;  // f16 elements per buffer
   constexpr int NLD = (5 * 5 * HX + 255) / 256;  // 7 halo voxels per thread
   __shared__ __attribute__((aligned(16))) uint16_t halo[2 * HALO];
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
@@ -310,28 +343,41 @@ __global__ __launch_bounds__(256, 2) void k_conv1_fwd_pool_pipe(const uint8_t* _
 #define C1_STORE(BUF)                                                                                         \
   _Pragma("unroll") for (int u_ = 0; u_ < NLD; ++u_) {                                                        \
     const int e_ = tid + 256 * u_;                                                                            \
-    if (e_ < 5 * 5 * HX) *reinterpret_cast<uint4*>(&halo[(BUF) * HALO + e_ * 8]) = u8x8_to_bf16x8(pre[u_]);  \
+    if (e_ < 5 * 5 * HX) *reinterpret_cast<uint4*>(&halo[(BUF) * HALO + e_ * 8]) = u8x8_to_f16magic(pre[u_]); \
   }
   C1_LOAD(0)
   const int fr = lane & 15, fq = lane >> 4;
   const int ch = wid & 1, op = wid >> 1;
-  bf16x8 fa[2][7];
+  f16x8 fa[2][7];
   const uint16_t* wg = w8 + (int64_t)g * kC1 * kK1;
+  float rs[2] = {0.f, 0.f};  // partial row sums of A (row 32ch + 16i + fr, this lane's k chunks)
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int s = 0; s < 7; ++s)
-      fa[i][s] = *reinterpret_cast<const bf16x8*>(wg + (32 * ch + 16 * i + fr) * kK1 + 32 * s + 8 * fq);
+    for (int s = 0; s < 7; ++s) {
+      fa[i][s] = *reinterpret_cast<const f16x8*>(wg + (32 * ch + 16 * i + fr) * kK1 + 32 * s + 8 * fq);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) rs[i] += (float)fa[i][s][e];
+    }
+  // full row sums (the 4 fq lanes of a row hold disjoint k chunks), then fetch the sums of the C rows this
+  // lane accumulates (rows 4fq + r of each 16-row tile) -> accumulator start values -1024 * sum A
+  f32x4 cinit[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    rs[i] += __shfl_xor(rs[i], 16, 64);
+    rs[i] += __shfl_xor(rs[i], 32, 64);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) cinit[i][r] = -1024.f * __shfl(rs[i], 4 * fq + r, 64);
+  }
   // w8 carries sign(gamma) = sign(sc) per output channel (k_pack_conv1_w, exact), so the argmax of
-  // z = sc*acc + sh is the argmax of the accumulator and the pooled value is |sc| * max + sh.  The 3^3
-  // window's argmax index rides in the 5 low mantissa bits of the running max (v_and_or + v_max per conv
-  // output instead of fma + cmp + 2 selects).
+  // z = sc*acc + sh is the argmax of the accumulator and the pooled value is |sc| * max + sh.  acc is
+  // 255 x the conv of x/255 (f16(w) weights against raw uint8), hence |sc| / 255.
   float sc[2][4], sh[2][4];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      sc[i][r] = fabsf(scale[g * kC1 + 32 * ch + 16 * i + 4 * fq + r]);
+      sc[i][r] = fabsf(scale[g * kC1 + 32 * ch + 16 * i + 4 * fq + r]) * (1.0f / 255.0f);
       sh[i][r] = shift[g * kC1 + 32 * ch + 16 * i + 4 * fq + r];
     }
   // Retire the one-time loads here: an empty asm that "redefines" each register makes the waitcnt pass see
@@ -342,7 +388,7 @@ __global__ __launch_bounds__(256, 2) void k_conv1_fwd_pool_pipe(const uint8_t* _
 #pragma unroll
     for (int s = 0; s < 7; ++s) asm volatile("" : "+v"(fa[i][s]));
 #pragma unroll
-    for (int r = 0; r < 4; ++r) asm volatile("" : "+v"(sc[i][r]), "+v"(sh[i][r]));
+    for (int r = 0; r < 4; ++r) asm volatile("" : "+v"(sc[i][r]), "+v"(sh[i][r]), "+v"(cinit[i][r]));
   }
   int toff[7];
 #pragma unroll
@@ -359,7 +405,7 @@ __global__ __launch_bounds__(256, 2) void k_conv1_fwd_pool_pipe(const uint8_t* _
     const int cur = ph & 1;
     if (ph + 1 < kPH) C1_LOAD(ph + 1)
     const uint16_t* hb = halo + cur * HALO;
-    float best[2][2][4];
+    float best[2][2][4], pend[2][2][4];
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -369,8 +415,8 @@ __global__ __launch_bounds__(256, 2) void k_conv1_fwd_pool_pipe(const uint8_t* _
 #pragma unroll 1
     for (int dd = 0; dd < 3; ++dd) {
       // 21 k-steps (3 dh rows x 7 tap groups) with the B fragments of step q+1 read before step q's MFMAs
-      bf16x8 nb0 = *reinterpret_cast<const bf16x8*>(&hb[colbase0 + dd * 5 * HX * 8 + toff[0]]);
-      bf16x8 nb1 = *reinterpret_cast<const bf16x8*>(&hb[colbase1 + dd * 5 * HX * 8 + toff[0]]);
+      f16x8 nb0 = *reinterpret_cast<const f16x8*>(&hb[colbase0 + dd * 5 * HX * 8 + toff[0]]);
+      f16x8 nb1 = *reinterpret_cast<const f16x8*>(&hb[colbase1 + dd * 5 * HX * 8 + toff[0]]);
       f32x4 acc[2][2];
 #pragma unroll
       for (int q = 0; q < 21; ++q) {
@@ -379,29 +425,31 @@ __global__ __launch_bounds__(256, 2) void k_conv1_fwd_pool_pipe(const uint8_t* _
 #pragma unroll
           for (int i = 0; i < 2; ++i)
 #pragma unroll
-            for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+            for (int j = 0; j < 2; ++j) acc[i][j] = cinit[i];
         }
-        const bf16x8 fb0 = nb0, fb1 = nb1;
+        const f16x8 fb0 = nb0, fb1 = nb1;
         if (q + 1 < 21) {
           const int ro = ((dd * 5 + (q + 1) / 7) * HX) * 8 + toff[(q + 1) % 7];
-          nb0 = *reinterpret_cast<const bf16x8*>(&hb[colbase0 + ro]);
-          nb1 = *reinterpret_cast<const bf16x8*>(&hb[colbase1 + ro]);
+          nb0 = *reinterpret_cast<const f16x8*>(&hb[colbase0 + ro]);
+          nb1 = *reinterpret_cast<const f16x8*>(&hb[colbase1 + ro]);
         }
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
-          acc[i][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][s], fb0, acc[i][0], 0, 0, 0);
-          acc[i][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][s], fb1, acc[i][1], 0, 0, 0);
+          acc[i][0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[i][s], fb0, acc[i][0], 0, 0, 0);
+          acc[i][1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[i][s], fb1, acc[i][1], 0, 0, 0);
         }
         if (s != 6) continue;
-        const int li = dd * 9 + dh * 3;
+        const uint32_t tag = (uint32_t)(dd * 9 + dh * 3 + dw);
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll
           for (int j = 0; j < 2; ++j)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-              const uint32_t e = (__float_as_uint(acc[i][j][r]) & ~31u) | (uint32_t)li;
-              best[i][j][r] = fmaxf(best[i][j][r], __uint_as_float(e));
+              const float e = tag_idx(acc[i][j][r], tag);
+              if (dh == 0) pend[i][j][r] = e;
+              else if (dh == 1) best[i][j][r] = vmax3(best[i][j][r], pend[i][j][r], e);
+              else best[i][j][r] = vmax2(best[i][j][r], e);
             }
       }
     }
@@ -416,18 +464,16 @@ __global__ __launch_bounds__(256, 2) void k_conv1_fwd_pool_pipe(const uint8_t* _
         float o4[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const uint32_t bb = __float_as_uint(best[i][j][r]);
-          float v = __uint_as_float(bb & ~31u);
-          int ix = (int)(bb & 31u) + dw;
-          const float v1 = __shfl_down(v, 1, 16), v2 = __shfl_down(v, 2, 16);
-          const int i1 = __shfl_down(ix, 1, 16), i2 = __shfl_down(ix, 2, 16);
-          if (v1 > v || (v1 == v && i1 < ix)) { v = v1; ix = i1; }
-          if (v2 > v || (v2 == v && i2 < ix)) { v = v2; ix = i2; }
-          o4[r] = fmaxf(fmaf(v, sc[i][r], sh[i][r]), 0.f);
-          ab[i] |= (uint32_t)ix << (8 * r);
+          // max over the window's 3 columns = this lane (dw = 0) and the next two lanes of the 16-lane row
+          const uint32_t b0 = __float_as_uint(best[i][j][r]);
+          const uint32_t b1 = __builtin_amdgcn_update_dpp(0u, b0, 0x101, 0xf, 0xf, false);  // row_shl:1
+          const uint32_t b2 = __builtin_amdgcn_update_dpp(0u, b0, 0x102, 0xf, 0xf, false);  // row_shl:2
+          const uint32_t bb = __float_as_uint(vmax3(__uint_as_float(b0), __uint_as_float(b1), __uint_as_float(b2)));
+          o4[r] = fmaxf(fmaf(__uint_as_float(bb & ~31u), sc[i][r], sh[i][r]), 0.f);
+          ab[i] |= (bb & 31u) << (8 * r);
         }
-        pk[i][0] = pack_bf16x2(o4[0], o4[1]);
-        pk[i][1] = pack_bf16x2(o4[2], o4[3]);
+        pk[i][0] = pack_bf16x2_hw(o4[0], o4[1]);
+        pk[i][1] = pack_bf16x2_hw(o4[2], o4[3]);
       }
       if (writer) {
         const int64_t o = ((((int64_t)n * kPD + pd) * kPH + ph) * kPW + pw) * kC1 + 32 * ch + 4 * fq;
