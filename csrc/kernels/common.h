@@ -57,16 +57,28 @@ __device__ __forceinline__ float block_sum(float v, float* red) {
 
 __device__ __forceinline__ float bf16_to_f32(uint16_t b) { return __uint_as_float(((uint32_t)b) << 16); }
 
-// Round-to-nearest-even f32 -> bf16 bits.
-__device__ __forceinline__ uint16_t f32_to_bf16(float f) {
-  uint32_t u = __float_as_uint(f);
-  if ((u & 0x7f800000u) == 0x7f800000u) return (uint16_t)((u >> 16) | ((u & 0xffff) ? 0x40 : 0));  // inf/nan
-  u += 0x7fffu + ((u >> 16) & 1u);
-  return (uint16_t)(u >> 16);
-}
+// f32 -> bf16 bits, round-to-nearest-even (NaN stays NaN): the gfx950 hardware conversion
+// (v_cvt_pk_bf16_f32), one VALU op per PAIR instead of a ~6-op software rounding per value.
+__device__ __forceinline__ uint16_t f32_to_bf16(float f) { return __builtin_bit_cast(uint16_t, (__bf16)f); }
 
 __device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi) {
-  return (uint32_t)f32_to_bf16(lo) | ((uint32_t)f32_to_bf16(hi) << 16);
+  typedef __bf16 bf2 __attribute__((ext_vector_type(2)));
+  const bf2 v = {(__bf16)lo, (__bf16)hi};
+  return __builtin_bit_cast(uint32_t, v);
+}
+
+// 27-bit in-bounds mask of the 3x3x3 taps (t = 9 jd + 3 jh + jw) of an output position whose window starts at
+// (d0, h0, w0): three 3-bit per-dimension masks combined with shifts (~20 VALU instead of 27 x 6 compares).
+__device__ __forceinline__ uint32_t tap_mask3(int d0, int h0, int w0, int D, int H, int W) {
+  uint32_t md = 0, mh = 0, mw = 0;
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    md |= (uint32_t)((unsigned)(d0 + j) < (unsigned)D) << j;
+    mh |= (uint32_t)((unsigned)(h0 + j) < (unsigned)H) << j;
+    mw |= (uint32_t)((unsigned)(w0 + j) < (unsigned)W) << j;
+  }
+  const uint32_t hw = ((mh & 1u) ? mw : 0u) | ((mh & 2u) ? mw << 3 : 0u) | ((mh & 4u) ? mw << 6 : 0u);
+  return ((md & 1u) ? hw : 0u) | ((md & 2u) ? hw << 9 : 0u) | ((md & 4u) ? hw << 18 : 0u);
 }
 
 inline hipStream_t as_stream(uintptr_t s) { return reinterpret_cast<hipStream_t>(s); }

@@ -308,11 +308,6 @@ __device__ __forceinline__ float vmax3(float a, float b, float c) {
   return r;
 }
 
-__device__ __forceinline__ uint32_t pack_bf16x2_hw(float lo, float hi) {
-  typedef __bf16 bf2 __attribute__((ext_vector_type(2)));
-  const bf2 v = {(__bf16)lo, (__bf16)hi};  // v_cvt_pk_bf16_f32 (RNE)
-  return __builtin_bit_cast(uint32_t, v);
-}
 
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 
@@ -472,8 +467,8 @@ __global__ __launch_bounds__(256, 2) void k_conv1_fwd_pool_pipe(const uint8_t* _
           o4[r] = fmaxf(fmaf(__uint_as_float(bb & ~31u), sc[i][r], sh[i][r]), 0.f);
           ab[i] |= (bb & 31u) << (8 * r);
         }
-        pk[i][0] = pack_bf16x2_hw(o4[0], o4[1]);
-        pk[i][1] = pack_bf16x2_hw(o4[2], o4[3]);
+        pk[i][0] = pack_bf16x2(o4[0], o4[1]);
+        pk[i][1] = pack_bf16x2(o4[2], o4[3]);
       }
       if (writer) {
         const int64_t o = ((((int64_t)n * kPD + pd) * kPH + ph) * kPW + pw) * kC1 + 32 * ch + 4 * fq;

@@ -332,10 +332,7 @@ __global__ __launch_bounds__(64 * WM * WN, (NST == 2 ? 8 : 4) / (WM * WN)) void 
       const int oh = r2 / a.Wo, ow = r2 - oh * a.Wo;
       const int d0 = od - a.pad, h0 = oh - a.pad, w0 = ow - a.pad;
       roff[i] = ((((int64_t)(g * a.B + nl) * a.D + d0) * a.H + h0) * a.W + w0) * Cin + ((slot ^ swz_dma(row)) << 3);
-      for (int t = 0; t < 27; ++t) {
-        const int id_ = d0 + t / 9, ih = h0 + (t / 3) % 3, iw = w0 + t % 3;
-        if (id_ >= 0 && id_ < a.D && ih >= 0 && ih < a.H && iw >= 0 && iw < a.W) tmask[i] |= 1u << t;
-      }
+      tmask[i] = tap_mask3(d0, h0, w0, a.D, a.H, a.W);
     }
   }
   int64_t aoff[A_INSTR];
@@ -681,10 +678,7 @@ __global__ void k_conv_pos_table(int2* tab, int Mg, int D, int H, int W, int pad
   const int od = s / (Ho * Wo), r = s - od * Ho * Wo, oh = r / Wo, ow = r - oh * Wo;
   const int d0 = od - pad, h0 = oh - pad, w0 = ow - pad;
   uint32_t mask = 0;
-  for (int t = 0; t < 27; ++t) {
-    const int id = d0 + t / 9, ih = h0 + (t / 3) % 3, iw = w0 + t % 3;
-    if (id >= 0 && id < D && ih >= 0 && ih < H && iw >= 0 && iw < W) mask |= 1u << t;
-  }
+  mask = tap_mask3(d0, h0, w0, D, H, W);
   tab[m] = make_int2(((nl * D + d0) * H + h0) * W + w0, (int)mask);
 }
 
