@@ -688,9 +688,36 @@ constexpr int kWdGroup = kWdPos * kWdRow;        // one 64-col group: 8 KB
 constexpr int kWdBuf = 5 * kWdGroup;             // 4 X groups + dY
 __device__ __forceinline__ int swz_wd(int r) { return (r & 2) | ((r >> 1) & 4); }
 
+// Raw buffer resources (stride 0, range = bytes): an offset at or past the range reads zeros, which replaces the
+// zero page, the 64-bit address arithmetic and the per-row bounds selects of the global_load_lds version (the
+// issue loop was VALU-bound: 4.8 VALU per MFMA, profiles/r1_pmc_v4.txt).
+typedef int i32x4_t __attribute__((ext_vector_type(4)));
+typedef int i32x2_t __attribute__((ext_vector_type(2)));
+__device__ i32x2_t nidt_raw_buffer_load_v2i32(i32x4_t rsrc, int voffset, int soffset, int aux)
+    __asm("llvm.amdgcn.raw.buffer.load.v2i32");
+__device__ void nidt_raw_buffer_load_lds(i32x4_t rsrc, __attribute__((address_space(3))) uint32_t* lds, int size,
+                                         int voffset, int soffset, int offset, int aux)
+    __asm("llvm.amdgcn.raw.buffer.load.lds");
+constexpr int kBufOOB = (int)0x80000000u;
+
+__device__ __forceinline__ i32x4_t make_rsrc(const void* base, uint32_t bytes) {
+  const uint64_t p = reinterpret_cast<uint64_t>(base);
+  i32x4_t r;
+  r.x = __builtin_amdgcn_readfirstlane((int)(uint32_t)p);
+  r.y = __builtin_amdgcn_readfirstlane((int)(uint32_t)(p >> 32));  // stride 0 (48-bit address)
+  r.z = __builtin_amdgcn_readfirstlane((int)bytes);
+  r.w = 0x00020000;
+  return r;
+}
+
+__device__ __forceinline__ void blds16(i32x4_t rsrc, int voffset, uint16_t* lds_wave_base) {
+  nidt_raw_buffer_load_lds(rsrc, (__attribute__((address_space(3))) uint32_t*)(lds_wave_base), 16, voffset, 0, 0, 0);
+}
+
 __global__ __launch_bounds__(256, 2) void k_conv_wgrad_dma(ConvWgDmaArgs a) {
   __shared__ __attribute__((aligned(16))) uint16_t smem[2 * kWdBuf];
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // uniform: LDS destinations stay in SGPRs
   const int id = xcd_remap(blockIdx.x, gridDim.x);
   const int kt = id % a.nKT, r1 = id / a.nKT;
   const int ct = r1 % a.nCT, r2 = r1 / a.nCT;
@@ -698,38 +725,27 @@ __global__ __launch_bounds__(256, 2) void k_conv_wgrad_dma(ConvWgDmaArgs a) {
   const int kc0 = kt * kWgKC, co0 = ct * kWgCO;
   const int p_begin = sp * a.chunk, p_end = min(a.Mg, p_begin + a.chunk);
   const int Cin = a.Cin;
-  const uint16_t* zp = reinterpret_cast<const uint16_t*>(g_zero_page);
-  const uint16_t* xg = a.x + (int64_t)g * a.xclient;
+  const i32x4_t rx = make_rsrc(a.x + (int64_t)g * a.xclient, (uint32_t)(a.xclient * 2));
+  const i32x4_t rd = make_rsrc(a.dy + (int64_t)g * a.Mg * a.Cout, (uint32_t)((int64_t)a.Mg * a.Cout * 2));
+  const i32x4_t rt = make_rsrc(a.ptab, (uint32_t)a.Mg * 8u);  // rows past Mg read {0, mask 0}: no taps valid
   // this wave's X group: k-cols kc0 + 64w .. +63 = one tap, 64 channels
   const int kg = kc0 + 64 * wid;
   const bool gval = kg < a.K;
-  const int gtap = gval ? kg / Cin : 31;  // 31: never set in a tap mask -> zero page
+  const int gtap = gval ? kg / Cin : 31;  // 31: never set in a tap mask -> out-of-range read -> zeros
   const int gcol = gval ? (((gtap / 9) * a.H + (gtap / 3) % 3) * a.W + gtap % 3) * Cin + (kg - gtap * Cin) : 0;
   const int lr = lane >> 3, ls = lane & 7;
-  int2 tnext = make_int2(0, 0);
-#define WD_FETCH(P0)                                                                                          \
-  {                                                                                                           \
-    const int m_ = (P0) + lane;                                                                               \
-    tnext = m_ < p_end ? a.ptab[m_] : make_int2(0, 0);                                                        \
+  // per-lane constant parts of the byte offsets: X row r = 8i + lr, chunk (ls ^ swz(r)); dY likewise
+  int xcol[8], dcol[2];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) xcol[i] = (gcol + ((ls ^ swz_wd(8 * i + lr)) << 3)) * 2;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int r = 8 * (2 * wid + i) + lr;
+    dcol[i] = (r * a.Cout + co0 + ((ls ^ swz_wd(r)) << 3)) * 2;
   }
-#define WD_ISSUE(P0, BUFI)                                                                                    \
-  {                                                                                                           \
-    uint16_t* sX_ = smem + (BUFI) * kWdBuf + wid * kWdGroup;                                                  \
-    uint16_t* sD_ = smem + (BUFI) * kWdBuf + 4 * kWdGroup;                                                    \
-    _Pragma("unroll") for (int i_ = 0; i_ < 8; ++i_) {                                                        \
-      const int r_ = 8 * i_ + lr;                                                                             \
-      const int off_ = __shfl(tnext.x, r_, 64), msk_ = __shfl(tnext.y, r_, 64);                               \
-      const bool ok_ = ((P0) + r_ < p_end) && ((msk_ >> gtap) & 1);                                           \
-      const uint16_t* src_ = ok_ ? xg + (int64_t)off_ * Cin + gcol + ((ls ^ swz_wd(r_)) << 3) : zp;           \
-      glds16(src_, sX_ + i_ * 512);                                                                           \
-    }                                                                                                         \
-    _Pragma("unroll") for (int i_ = 0; i_ < 2; ++i_) {                                                        \
-      const int r_ = 8 * (2 * wid + i_) + lr;                                                                 \
-      const int m_ = (P0) + r_;                                                                               \
-      const uint16_t* src_ = m_ < p_end ? a.dy + ((int64_t)g * a.Mg + m_) * a.Cout + co0 + ((ls ^ swz_wd(r_)) << 3) : zp; \
-      glds16(src_, sD_ + (2 * wid + i_) * 512);                                                               \
-    }                                                                                                         \
-  }
+  i32x2_t tn[8];  // ptab entries {voxel offset, tap mask} of this lane's 8 X rows, one step ahead
+#define WD_FETCH(P0)                                                                                            {                                                                                                               _Pragma("unroll") for (int i_ = 0; i_ < 8; ++i_)                                                                tn[i_] = nidt_raw_buffer_load_v2i32(rt, ((P0) + 8 * i_ + lr) * 8, 0, 0);                                  }
+#define WD_ISSUE(P0, BUFI)                                                                                      {                                                                                                               uint16_t* sX_ = smem + (BUFI) * kWdBuf + wid * kWdGroup;                                                      uint16_t* sD_ = smem + (BUFI) * kWdBuf + 4 * kWdGroup;                                                        _Pragma("unroll") for (int i_ = 0; i_ < 8; ++i_) {                                                              const bool ok_ = (tn[i_].y >> gtap) & 1;                                                                      blds16(rx, ok_ ? tn[i_].x * (2 * Cin) + xcol[i_] : kBufOOB, sX_ + i_ * 512);                               }                                                                                                             _Pragma("unroll") for (int i_ = 0; i_ < 2; ++i_)                                                                blds16(rd, (P0) * (2 * a.Cout) + dcol[i_], sD_ + (2 * wid + i_) * 512);                                    }
 
   f32x4 acc[4][4];
 #pragma unroll
@@ -823,6 +839,8 @@ void conv3d_wgrad(uintptr_t x, uintptr_t xs, uintptr_t xt, uintptr_t dy, uintptr
     d.chunk = ((ceil_div(a.Mg, nsplit) + kWdPos - 1) / kWdPos) * kWdPos;
     d.nKT = ceil_div(a.K, kWgKC); d.nCT = Cout / kWgCO;
     d.xclient = (int64_t)B * D * H * W * Cin;
+    NIDT_REQUIRE(d.xclient * 2 < (1ll << 31) && (int64_t)a.Mg * Cout * 2 < (1ll << 31),
+                 "conv3d_wgrad: per-client tensors must stay below 2 GiB (32-bit buffer offsets)");
     const int64_t nwg = (int64_t)d.nKT * d.nCT * nsplit * G;
     NIDT_REQUIRE(nwg < (1ll << 31), "conv3d_wgrad: grid too large");
     hipLaunchKernelGGL(k_conv_wgrad_dma, dim3((unsigned)nwg), dim3(256), 0, s, d);
