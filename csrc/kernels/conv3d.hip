@@ -275,21 +275,41 @@ __global__ __launch_bounds__(256, 2) void k_conv_fwd(ConvFwdArgs a) {
 
 // ------------------------------------------------------------------------------------------------
 // k_conv_fwd_dma — the Cin % 64 == 0 forward/dgrad path: BK = 64 (one tap x 64 channels per k-step, a
-// 128-B row per position / output channel), both tiles filled by global_load_lds (LDS-DMA, no staging
+// 128-B row per position / output channel), both tiles filled by buffer_load ... lds (LDS-DMA, no staging
 // VGPRs, no ds_write).  The LDS image is lane-linear per wave instruction, so the bank swizzle
-// chunk' = chunk ^ ((row >> 1) & 7) is applied to the per-lane SOURCE address and undone on the
+// chunk' = chunk ^ ((row >> 1) & 7) is applied to the per-lane SOURCE offset and undone on the
 // ds_read_b128 fragment reads (conflict-free for the 16x16x32 fragment pattern: each 16-lane group of a
 // b128 read touches 16 distinct 16-B bank slots).  Out-of-range taps (padding) and positions past the
-// end load from a zero page.  Per-row tap validity is a 27-bit mask computed once per block, so the
-// k-loop's address work is one 64-bit add + select per 16-B chunk.  1-D grid with the XCD remap: the
-// co-tiles of one position tile and neighbouring position tiles share an XCD's L2 (the 27 taps re-read
-// the same input rows).
-__device__ __attribute__((aligned(16))) uint4 g_zero_page[16];
-
+// end read past the buffer range and get zeros.  Per-row tap validity is a 27-bit mask computed once per
+// block, so the k-loop's address work is one 32-bit add + select per 16-B chunk.  1-D grid with the XCD
+// remap: the co-tiles of one position tile and neighbouring position tiles share an XCD's L2 (the 27
+// taps re-read the same input rows).
 __device__ __forceinline__ int swz_dma(int r) { return (r >> 1) & 7; }
 
-__device__ __forceinline__ void glds16(const void* src, uint16_t* lds_wave_base) {
-  __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(lds_wave_base), 16, 0, 0);
+// Raw buffer resources (stride 0, range = bytes): an offset at or past the range reads zeros, which replaces the
+// zero page, the 64-bit address arithmetic and the per-row bounds selects of the global_load_lds version (the
+// issue loop was VALU-bound: 4.8 VALU per MFMA, profiles/r1_pmc_v4.txt).
+typedef int i32x4_t __attribute__((ext_vector_type(4)));
+typedef int i32x2_t __attribute__((ext_vector_type(2)));
+__device__ i32x2_t nidt_raw_buffer_load_v2i32(i32x4_t rsrc, int voffset, int soffset, int aux)
+    __asm("llvm.amdgcn.raw.buffer.load.v2i32");
+__device__ void nidt_raw_buffer_load_lds(i32x4_t rsrc, __attribute__((address_space(3))) uint32_t* lds, int size,
+                                         int voffset, int soffset, int offset, int aux)
+    __asm("llvm.amdgcn.raw.buffer.load.lds");
+constexpr int kBufOOB = (int)0x80000000u;
+
+__device__ __forceinline__ i32x4_t make_rsrc(const void* base, uint32_t bytes) {
+  const uint64_t p = reinterpret_cast<uint64_t>(base);
+  i32x4_t r;
+  r.x = __builtin_amdgcn_readfirstlane((int)(uint32_t)p);
+  r.y = __builtin_amdgcn_readfirstlane((int)(uint32_t)(p >> 32));  // stride 0 (48-bit address)
+  r.z = __builtin_amdgcn_readfirstlane((int)bytes);
+  r.w = 0x00020000;
+  return r;
+}
+
+__device__ __forceinline__ void blds16(i32x4_t rsrc, int voffset, uint16_t* lds_wave_base) {
+  nidt_raw_buffer_load_lds(rsrc, (__attribute__((address_space(3))) uint32_t*)(lds_wave_base), 16, voffset, 0, 0, 0);
 }
 
 template <int BCO, int WM, int WN, int NST, bool BIAS, bool STATS>
@@ -311,14 +331,16 @@ __global__ __launch_bounds__(64 * WM * WN, (NST == 2 ? 8 : 4) / (WM * WN)) void 
   const int cot = id % nCO, rest = id / nCO;
   const int pb = rest % a.nPB, g = rest / a.nPB;
   const int co0 = cot * BCO;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // uniform: LDS destinations stay in SGPRs
   const int wco = wid / WN, wp = wid % WN;
   const int Cin = a.Cin, nck = Cin / BK, nks = 27 * nck;
   const int lrow = lane >> 3, slot = lane & 7;
 
-  // ---- per-thread B rows: one per glds instruction, fixed over the k loop ----
+  // ---- per-thread B rows: one per LDS-DMA instruction, fixed over the k loop (byte offsets in the client's input;
+  // rows past the end and padding taps read out of range -> zeros) ----
   const int S = a.Do * a.Ho * a.Wo;
-  int64_t roff[B_INSTR];
+  int roff[B_INSTR];
   uint32_t tmask[B_INSTR];
 #pragma unroll
   for (int i = 0; i < B_INSTR; ++i) {
@@ -331,30 +353,32 @@ __global__ __launch_bounds__(64 * WM * WN, (NST == 2 ? 8 : 4) / (WM * WN)) void 
       const int od = s / (a.Ho * a.Wo), r2 = s - od * a.Ho * a.Wo;
       const int oh = r2 / a.Wo, ow = r2 - oh * a.Wo;
       const int d0 = od - a.pad, h0 = oh - a.pad, w0 = ow - a.pad;
-      roff[i] = ((((int64_t)(g * a.B + nl) * a.D + d0) * a.H + h0) * a.W + w0) * Cin + ((slot ^ swz_dma(row)) << 3);
+      // may be negative for padded windows; only taps inside the volume (tmask) are ever read
+      roff[i] = ((((nl * a.D + d0) * a.H + h0) * a.W + w0) * Cin + ((slot ^ swz_dma(row)) << 3)) * 2;
       tmask[i] = tap_mask3(d0, h0, w0, a.D, a.H, a.W);
     }
   }
-  int64_t aoff[A_INSTR];
+  int aoff[A_INSTR];
 #pragma unroll
   for (int i = 0; i < A_INSTR; ++i) {
     const int row = 8 * (wid * A_INSTR + i) + lrow;
-    aoff[i] = ((int64_t)g * a.Cout + co0 + row) * 27 * Cin + ((slot ^ swz_dma(row)) << 3);
+    aoff[i] = ((co0 + row) * 27 * Cin + ((slot ^ swz_dma(row)) << 3)) * 2;
   }
-  const uint16_t* zp = reinterpret_cast<const uint16_t*>(g_zero_page);
+  const int64_t xcl = (int64_t)a.B * a.D * a.H * a.W * Cin;
+  const i32x4_t rxs = make_rsrc(a.x + (int64_t)g * xcl, (uint32_t)(xcl * 2));
+  const i32x4_t rws = make_rsrc(a.w + (int64_t)g * a.Cout * 27 * Cin, (uint32_t)(a.Cout * 27 * Cin * 2));
 
 #define DMA_ISSUE(KS, BUFI)                                                                                   \
   {                                                                                                           \
     const int t_ = (KS) / nck, cc_ = (KS) - t_ * nck;                                                         \
-    const int64_t toff_ = ((((int64_t)(t_ / 9)) * a.H + (t_ / 3) % 3) * a.W + t_ % 3) * Cin + cc_ * BK;       \
+    const int toff_ = (((((t_ / 9)) * a.H + (t_ / 3) % 3) * a.W + t_ % 3) * Cin + cc_ * BK) * 2;              \
+    const int woff_ = (t_ * Cin + cc_ * BK) * 2;                                                              \
     uint16_t* sA_ = smem + (BUFI) * BUF;                                                                      \
     uint16_t* sB_ = sA_ + A_ELEMS;                                                                            \
     _Pragma("unroll") for (int i_ = 0; i_ < A_INSTR; ++i_)                                                    \
-      glds16(a.w + aoff[i_] + (int64_t)t_ * Cin + cc_ * BK, sA_ + (wid * A_INSTR + i_) * 512);                \
-    _Pragma("unroll") for (int i_ = 0; i_ < B_INSTR; ++i_) {                                                  \
-      const uint16_t* src_ = ((tmask[i_] >> t_) & 1u) ? a.x + roff[i_] + toff_ : zp;                          \
-      glds16(src_, sB_ + (B_INSTR * wid + i_) * 512);                                                         \
-    }                                                                                                         \
+      blds16(rws, aoff[i_] + woff_, sA_ + (wid * A_INSTR + i_) * 512);                                        \
+    _Pragma("unroll") for (int i_ = 0; i_ < B_INSTR; ++i_)                                                    \
+      blds16(rxs, ((tmask[i_] >> t_) & 1u) ? roff[i_] + toff_ : kBufOOB, sB_ + (B_INSTR * wid + i_) * 512);   \
   }
 
   f32x4 acc[TCO][TP];
@@ -417,6 +441,8 @@ void conv3d_fwd(uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t xs, uintptr_
   NIDT_REQUIRE(Cin % 32 == 0 && Cin <= 192, "conv3d_fwd: Cin must be a multiple of 32 and <= 192");
   NIDT_REQUIRE(Cout % 64 == 0, "conv3d_fwd: Cout must be a multiple of 64");
   NIDT_REQUIRE(pad >= 0 && pad <= 2, "conv3d_fwd: pad in [0,2]");
+  NIDT_REQUIRE((int64_t)B * D * H * W * Cin * 2 < (1ll << 31),
+               "conv3d_fwd: per-client input must stay below 2 GiB (32-bit buffer offsets)");
   ConvFwdArgs a;
   a.x = ptr<const uint16_t>(x); a.w = ptr<const uint16_t>(w); a.bias = ptr<const float>(bias);
   a.xs = ptr<const float>(xs); a.xt = ptr<const float>(xt); a.y = ptr<uint16_t>(y); a.stats = ptr<float>(stats);
@@ -687,32 +713,6 @@ constexpr int kWdRow = 64;                       // bf16 per 128-B row
 constexpr int kWdGroup = kWdPos * kWdRow;        // one 64-col group: 8 KB
 constexpr int kWdBuf = 5 * kWdGroup;             // 4 X groups + dY
 __device__ __forceinline__ int swz_wd(int r) { return (r & 2) | ((r >> 1) & 4); }
-
-// Raw buffer resources (stride 0, range = bytes): an offset at or past the range reads zeros, which replaces the
-// zero page, the 64-bit address arithmetic and the per-row bounds selects of the global_load_lds version (the
-// issue loop was VALU-bound: 4.8 VALU per MFMA, profiles/r1_pmc_v4.txt).
-typedef int i32x4_t __attribute__((ext_vector_type(4)));
-typedef int i32x2_t __attribute__((ext_vector_type(2)));
-__device__ i32x2_t nidt_raw_buffer_load_v2i32(i32x4_t rsrc, int voffset, int soffset, int aux)
-    __asm("llvm.amdgcn.raw.buffer.load.v2i32");
-__device__ void nidt_raw_buffer_load_lds(i32x4_t rsrc, __attribute__((address_space(3))) uint32_t* lds, int size,
-                                         int voffset, int soffset, int offset, int aux)
-    __asm("llvm.amdgcn.raw.buffer.load.lds");
-constexpr int kBufOOB = (int)0x80000000u;
-
-__device__ __forceinline__ i32x4_t make_rsrc(const void* base, uint32_t bytes) {
-  const uint64_t p = reinterpret_cast<uint64_t>(base);
-  i32x4_t r;
-  r.x = __builtin_amdgcn_readfirstlane((int)(uint32_t)p);
-  r.y = __builtin_amdgcn_readfirstlane((int)(uint32_t)(p >> 32));  // stride 0 (48-bit address)
-  r.z = __builtin_amdgcn_readfirstlane((int)bytes);
-  r.w = 0x00020000;
-  return r;
-}
-
-__device__ __forceinline__ void blds16(i32x4_t rsrc, int voffset, uint16_t* lds_wave_base) {
-  nidt_raw_buffer_load_lds(rsrc, (__attribute__((address_space(3))) uint32_t*)(lds_wave_base), 16, voffset, 0, 0, 0);
-}
 
 __global__ __launch_bounds__(256, 2) void k_conv_wgrad_dma(ConvWgDmaArgs a) {
   __shared__ __attribute__((aligned(16))) uint16_t smem[2 * kWdBuf];
