@@ -17,7 +17,7 @@ void broadcast_row(uintptr_t src, int64_t P, int64_t stride, int64_t C, uintptr_
 void conv3d_fwd(uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t xs, uintptr_t xt, uintptr_t y, uintptr_t stats,
                 int G, int B, int D, int H, int W, int Cin, int Cout, int pad, uintptr_t stream);
 int conv3d_fwd_nblocks(int B, int D, int H, int W, int pad, int bp);
-int conv3d_fwd_bp(int Cin, int Cout, int xf);
+int conv3d_fwd_bp(int Cin, int Cout, int xf, int G, int Mg);
 void conv3d_wgrad(uintptr_t x, uintptr_t xs, uintptr_t xt, uintptr_t dy, uintptr_t part, uintptr_t grad, int64_t ldg,
                   int64_t off, int G, int B, int D, int H, int W, int Cin, int Cout, int pad, int nsplit, float scale,
                   uintptr_t ptab, uintptr_t stream);

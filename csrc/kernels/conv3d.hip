@@ -436,6 +436,8 @@ __global__ __launch_bounds__(64 * WM * WN, (NST == 2 ? 8 : 4) / (WM * WN)) void 
   conv_fwd_epilogue<BCO, BP, WM, WN, BIAS, STATS, TCO, TP>(a, acc, red, g, pb, co0, wco, wp, fr, fq, tid);
 }
 
+int conv3d_fwd_bp(int Cin, int Cout, int xf, int G, int Mg);
+
 void conv3d_fwd(uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t xs, uintptr_t xt, uintptr_t y, uintptr_t stats,
                 int G, int B, int D, int H, int W, int Cin, int Cout, int pad, uintptr_t stream) {
   NIDT_REQUIRE(Cin % 32 == 0 && Cin <= 192, "conv3d_fwd: Cin must be a multiple of 32 and <= 192");
@@ -457,20 +459,27 @@ void conv3d_fwd(uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t xs, uintptr_
   hipStream_t s = as_stream(stream);
   if (!xf && Cin % 64 == 0) {
     // 256 positions per block: BCO=128 -> 8 waves (2 co x 4 pos, 512 threads), BCO=64 -> 4 waves (1 x 4);
-    // every wave owns a 64x64 output tile (the A tile is re-read from L2 once per 256 positions).
-    const int bp = 256;
+    // every wave owns a 64x64 output tile (the A tile is re-read from L2 once per 256 positions).  When that
+    // grid would not fill the chip (few clients per GPU, e.g. 8 clients x the 5x7x5 conv3-5 layers at 8 GPUs)
+    // the block shrinks to one 64-position column of waves (4x the blocks).
+    const int bp = conv3d_fwd_bp(Cin, Cout, 0, G, a.Mg);
     a.nPB = ceil_div(a.Mg, bp);
     const int nCO = Cout / bco;
     const int64_t nwg = (int64_t)a.nPB * nCO * G;
     NIDT_REQUIRE(nwg < (1ll << 31), "conv3d_fwd: grid too large");
     dim3 g1((unsigned)nwg);
-#define NIDT_DMA(BC, WM, BI, ST) \
-    hipLaunchKernelGGL((k_conv_fwd_dma<BC, WM, 4, 2, BI, ST>), g1, dim3(256 * WM), 0, s, a, nCO)
-    if (bco == 128) {
-      if (st) NIDT_DMA(128, 2, true, true); else if (hb) NIDT_DMA(128, 2, true, false); else NIDT_DMA(128, 2, false, false);
-    } else {
-      if (st) NIDT_DMA(64, 1, true, true); else if (hb) NIDT_DMA(64, 1, true, false); else NIDT_DMA(64, 1, false, false);
+#define NIDT_DMA(BC, WM, WN, BI, ST) \
+    hipLaunchKernelGGL((k_conv_fwd_dma<BC, WM, WN, 2, BI, ST>), g1, dim3(64 * WM * WN), 0, s, a, nCO)
+#define NIDT_DMA_WN(WN)                                                                                     \
+    if (bco == 128) {                                                                                       \
+      if (st) NIDT_DMA(128, 2, WN, true, true); else if (hb) NIDT_DMA(128, 2, WN, true, false);             \
+      else NIDT_DMA(128, 2, WN, false, false);                                                              \
+    } else {                                                                                                \
+      if (st) NIDT_DMA(64, 1, WN, true, true); else if (hb) NIDT_DMA(64, 1, WN, true, false);               \
+      else NIDT_DMA(64, 1, WN, false, false);                                                               \
     }
+    if (bp == 256) { NIDT_DMA_WN(4) } else { NIDT_DMA_WN(1) }
+#undef NIDT_DMA_WN
 #undef NIDT_DMA
     NIDT_CHECK(hipGetLastError());
     return;
@@ -488,10 +497,12 @@ void conv3d_fwd(uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t xs, uintptr_
   NIDT_CHECK(hipGetLastError());
 }
 
-// positions per block (= per BN-statistics block) of conv3d_fwd for this layer shape
-int conv3d_fwd_bp(int Cin, int Cout, int xf) {
-  (void)Cout;
-  return (!xf && Cin % 64 == 0) ? 256 : kFwdBP;
+// positions per block (= per BN-statistics block) of conv3d_fwd for this layer shape and client count
+int conv3d_fwd_bp(int Cin, int Cout, int xf, int G, int Mg) {
+  if (xf || Cin % 64 != 0) return kFwdBP;
+  const int bco = (Cout % 128 == 0) ? 128 : 64;
+  const int64_t nwg256 = (int64_t)ceil_div(Mg, 256) * (Cout / bco) * G;
+  return nwg256 < 256 ? 64 : 256;  // fewer blocks than CUs: 64-position blocks (measured: only then a win)
 }
 
 int conv3d_fwd_nblocks(int B, int D, int H, int W, int pad, int bp) {

@@ -68,7 +68,8 @@ class HipAlexNet3D:
             b["bias%d" % ci] = e(G, cout, dt=f32)
             for k in ("s", "t", "m", "i"):
                 b["%s%d" % (k, ci)] = e(G, cout, dt=f32)
-            bp = self.m.conv3d_fwd_bp(cin, cout, 0)
+            mg = B * (sp[0] + 2 * pad - 2) * (sp[1] + 2 * pad - 2) * (sp[2] + 2 * pad - 2)
+            bp = self.m.conv3d_fwd_bp(cin, cout, 0, G, mg)
             npb = self.m.conv3d_fwd_nblocks(B, sp[0], sp[1], sp[2], pad, bp)
             b["st%d" % ci] = e(G, npb, cout, 2, dt=f32)
             b["npb%d" % ci] = npb

@@ -55,9 +55,9 @@ def test_polyphase_and_moments():
 @pytest.mark.parametrize("cin,cout,pad,sp,xf", [(64, 128, 0, (19, 23, 19), False), (128, 192, 1, (5, 7, 5), False),
                                                 (192, 192, 1, (5, 7, 5), True), (192, 128, 1, (5, 7, 5), True),
                                                 (128, 64, 2, (17, 21, 17), False)])
-def test_conv3d_fwd_stats(cin, cout, pad, sp, xf):
+@pytest.mark.parametrize("G,B", [(2, 3), (8, 16)])  # small grid (64-position blocks) and full (256) tiles
+def test_conv3d_fwd_stats(cin, cout, pad, sp, xf, G, B):
     m = _m()
-    G, B = 2, 3
     torch.manual_seed(1)
     x = torch.randn(G * B, *sp, cin, device=DEV).bfloat16()
     w = (torch.randn(G, cout, 27, cin, device=DEV) * 0.05).bfloat16()
@@ -66,7 +66,8 @@ def test_conv3d_fwd_stats(cin, cout, pad, sp, xf):
     xt = torch.randn(G, cin, device=DEV) * 0.2 if xf else None
     Do, Ho, Wo = [s + 2 * pad - 2 for s in sp]
     y = torch.empty(G * B, Do, Ho, Wo, cout, device=DEV, dtype=torch.bfloat16)
-    bp = m.conv3d_fwd_bp(cin, cout, 1 if xf else 0)
+    mg = B * (sp[0] + 2 * pad - 2) * (sp[1] + 2 * pad - 2) * (sp[2] + 2 * pad - 2)
+    bp = m.conv3d_fwd_bp(cin, cout, 1 if xf else 0, G, mg)
     npb = m.conv3d_fwd_nblocks(B, *sp, pad, bp)
     stats = torch.empty(G, npb, cout, 2, device=DEV)
     m.conv3d_fwd(x.data_ptr(), w.data_ptr(), bias.data_ptr(), xs.data_ptr() if xf else 0, xt.data_ptr() if xf else 0,
