@@ -683,7 +683,8 @@ int conv3d_wgrad_nsplit(int G, int B, int D, int H, int W, int Cin, int Cout, in
   const int K = 27 * Cin;
   const int base = G * (Cout / kWgCO) * ceil_div(K, kWgKC);
   int ns = ceil_div(2048, base);
-  const int maxns = max(1, Mg / 512);  // keep >= 16 k-steps per block
+  // keep >= 8 (small K) / 16 (K >= 3000: large fp32 split-K slabs to write and re-read) 64-position steps per block
+  const int maxns = max(1, Mg / (K >= 3000 ? 1024 : 512));
   return max(1, min(ns, maxns));
 }
 
