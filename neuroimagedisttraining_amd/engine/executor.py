@@ -614,14 +614,39 @@ class FLRunner:
                 o += len(grp)
         return out
 
+    def _eval_global_and_personal(self):
+        """Global model and every local client's personal model on that client's test split, in ONE grouped
+        launch sequence of 2C model rows (C personal rows + C copies of the global model).  Compared with
+        evaluating the single global row in test_batch chunks (G = 1) this keeps the kernels at full-client
+        shapes — it matters most at 8 clients per GPU.  Returns (glob, pers) or None when test sizes differ."""
+        C = self.C
+        sizes = {len(self.splits[c].test) for c in self.local}
+        if len(sizes) != 1 or next(iter(sizes)) > self.cfg.test_batch or next(iter(sizes)) == 0:
+            return None
+        if getattr(self, "_eval_rows2", None) is None or self._eval_rows2[0].shape[0] != 2 * C:
+            self._eval_rows2 = (padded_rows(2 * C, self.P, self.device), padded_rows(2 * C, self.Q, self.device))
+        th, bu = self._eval_rows2
+        with torch.no_grad():
+            th[:C].copy_(self.theta[:C])
+            th[C:].copy_(self.w_global.expand(C, -1))
+            bu[:C].copy_(self.bufs[:C])
+            bu[C:].copy_(self.b_global.expand(C, -1))
+        res = self._eval_grouped(th, bu, list(range(2 * C)), self.local + self.local)
+        return res[C:], res[:C]
+
     def evaluate(self, round_idx):
         t0 = time.perf_counter()
-        gth = padded_rows(1, self.P, self.device)
-        gth.copy_(self.w_global.unsqueeze(0))
-        gbu = padded_rows(1, self.Q, self.device)
-        gbu.copy_(self.b_global.unsqueeze(0))
-        glob = self._eval_rows(gth, gbu, self.local, [0] * self.C) if self.C else np.zeros((0, 3))
-        pers = self._eval_grouped(self.theta, self.bufs, list(range(self.C)), self.local) if self.C else np.zeros((0, 3))
+        both = self._eval_global_and_personal() if self.C else None
+        if both is not None:
+            glob, pers = both
+        else:
+            gth = padded_rows(1, self.P, self.device)
+            gth.copy_(self.w_global.unsqueeze(0))
+            gbu = padded_rows(1, self.Q, self.device)
+            gbu.copy_(self.b_global.unsqueeze(0))
+            glob = self._eval_rows(gth, gbu, self.local, [0] * self.C) if self.C else np.zeros((0, 3))
+            pers = self._eval_grouped(self.theta, self.bufs, list(range(self.C)), self.local) if self.C else \
+                np.zeros((0, 3))
         res = torch.zeros((self.N, 6), dtype=torch.float64, device=self.device)
         if self.C:
             res[torch.tensor(self.local, device=self.device)] = torch.from_numpy(
