@@ -497,87 +497,21 @@ void conv1_fwd_pool(uintptr_t x8, uintptr_t idx, uintptr_t w8, uintptr_t scale, 
 
 // ------------------------------------------------------------------------------------------------
 // Sparse wgrad: S[c][k] = sum over pooled voxels of dz * patch(argmax voxel), D[c] = sum dz.
-// Block = (n, pd); thread = (wave w, channel c = lane).  The polyphase input halo is staged as raw uint8 (8 B per
-// voxel) for 4 pooled rows (ph) at a time.  Halo strides are padded so that the 27 possible argmax offsets
-// (aw + 3 ah + 9 ad voxels apart) fall on 27 distinct ds_read_b64 bank pairs: the 64 channel-lanes of a wave,
-// which read at their own argmax, never bank-conflict (identical addresses broadcast).
+// Block = (n, pd); thread = (wave w, channel c = lane).  Per stage of kWgRows pooled rows (ph) the block stages
+// (a) the polyphase input halo as raw uint8 (8 B per voxel) and (b) one 32-bit record per (cell, channel):
+// dz = (pooled > 0 ? dL/dpooled : 0) as bf16 bits in the low half, the halo offset of the argmax patch in the
+// high half.  Staging the per-cell metadata with the whole block's loads in flight at once (instead of each
+// lane walking its cells with a one-cell global prefetch) takes the L2/HBM latency out of the cell loop, which
+// PMC showed parked 42 % of wave time in s_waitcnt.  Halo strides are padded so that the 27 possible argmax
+// offsets (aw + 67 ah + 553 ad voxels apart: 3 and 9 mod 32) fall on 27 distinct ds_read_b64 bank pairs: the
+// 64 channel-lanes of a wave, which read at their own argmax, never bank-conflict.
 // Output slab: part[n*19 + pd][64][126] (125 S entries + D).
-constexpr int kWgRows = 4;                       // pooled rows (ph) per stage
-constexpr int kWgHY = 3 * kWgRows + 2;           // halo y extent (14)
+constexpr int kWgRows = 2;                       // pooled rows (ph) per stage
+constexpr int kWgHY = 3 * kWgRows + 2;           // halo y extent (8)
 constexpr int kWgRS = 67;                        // row stride in voxels   (67 = 3 mod 32)
-constexpr int kWgZS = 969;                       // plane stride in voxels (969 = 9 mod 32, >= 14*67)
+constexpr int kWgZS = 553;                       // plane stride in voxels (553 = 9 mod 32, >= 8*67)
 constexpr int kWgHalo = 5 * kWgZS;               // voxels per halo buffer
-
-__global__ __launch_bounds__(256) void k_conv1_wgrad(const uint8_t* __restrict__ x8, const int* __restrict__ idx,
-                                                     const uint16_t* __restrict__ dp, const uint16_t* __restrict__ pout,
-                                                     const uint8_t* __restrict__ amax, float* __restrict__ part) {
-  __shared__ __attribute__((aligned(16))) uint2 halo[kWgHalo];
-  const int pd = blockIdx.x, n = blockIdx.y;
-  const int tid = threadIdx.x, c = tid & 63, wid = tid >> 6;
-  const uint8_t* xs = x8 + (int64_t)idx[n] * kPZ * kPY * kPX * 8;
-  float S[125];
-#pragma unroll
-  for (int k = 0; k < 125; ++k) S[k] = 0.f;
-  float Dsum = 0.f;
-  for (int ph0 = 0; ph0 < kPH; ph0 += kWgRows) {
-    const int nph = min(kWgRows, kPH - ph0);
-    const int ny = 3 * nph + 2;
-    __syncthreads();
-    for (int e = tid; e < 5 * ny * 64; e += 256) {
-      const int xh = e & 63, r = e >> 6, yh = r % ny, zh = r / ny;
-      const int z = 3 * pd + zh, y = 3 * ph0 + yh;
-      uint2 v = make_uint2(0, 0);
-      if (xh < kPX) v = *reinterpret_cast<const uint2*>(xs + (((int64_t)z * kPY + y) * kPX + xh) * 8);
-      halo[zh * kWgZS + yh * kWgRS + xh] = v;
-    }
-    __syncthreads();
-    for (int it = wid; it < nph * kPW; it += 4) {
-      const int phl = it / kPW, pw = it - phl * kPW;
-      const int64_t o = ((((int64_t)n * kPD + pd) * kPH + ph0 + phl) * kPW + pw) * kC1 + c;
-      const float pv = bf16_to_f32(pout[o]);
-      const float dz = pv > 0.f ? bf16_to_f32(dp[o]) : 0.f;
-      const int a = amax[o];
-      const int ad = a / 9, ah = (a / 3) % 3, aw = a % 3;
-      const uint2* base = halo + ad * kWgZS + (3 * phl + ah) * kWgRS + 3 * pw + aw;
-      Dsum += dz;
-#pragma unroll
-      for (int t = 0; t < 27; ++t) {
-        const int jd = t / 9, jh = (t / 3) % 3, jw = t % 3;
-        const uint2 u = base[jd * kWgZS + jh * kWgRS + jw];
-#pragma unroll
-        for (int r = 0; r < 8; ++r) {
-          if (tp_valid(t, r)) {
-            const uint32_t w = r < 4 ? u.x : u.y;
-            const float xv = (float)((w >> (8 * (r & 3))) & 0xffu);
-            S[tp_to_k(t, r)] = fmaf(dz, xv, S[tp_to_k(t, r)]);
-          }
-        }
-      }
-    }
-  }
-  // reduce the 4 waves (channel c owned by lane c of every wave) through LDS (reusing the halo buffer)
-  float* red = reinterpret_cast<float*>(halo);  // [64][127] floats = 32.5 KB < halo
-  for (int w = 1; w < 4; ++w) {
-    __syncthreads();
-    if (wid == w) {
-#pragma unroll
-      for (int k = 0; k < 125; ++k) red[c * 127 + k] = S[k];
-      red[c * 127 + 125] = Dsum;
-    }
-    __syncthreads();
-    if (wid == 0) {
-#pragma unroll
-      for (int k = 0; k < 125; ++k) S[k] += red[c * 127 + k];
-      Dsum += red[c * 127 + 125];
-    }
-  }
-  if (wid == 0) {
-    float* op = part + (((int64_t)n * kPD + pd) * kC1 + c) * 126;
-#pragma unroll
-    for (int k = 0; k < 125; ++k) op[k] = S[k];
-    op[125] = Dsum;
-  }
-}
+constexpr int kWgMeta = kWgRows * kPW * kC1;     // metadata records per stage
 
 // Reduce slabs per client and apply the closed form.  grid (64 c, G), block 256: the B*19 slabs are split
 // over the 4 waves (lane = k, k + 64; 4 independent loads in flight per lane instead of one dependent chain),
@@ -675,12 +609,13 @@ __host__ __device__ constexpr int tp_count(int t) {
 template <int W>
 __device__ __forceinline__ void conv1_wg_wave(const uint8_t* __restrict__ xs, const uint16_t* __restrict__ dp,
                                               const uint16_t* __restrict__ pout, const uint8_t* __restrict__ amax,
-                                              float* __restrict__ part, uint2* halo, int n, int pd, int tid, int c) {
+                                              float* __restrict__ part, uint2* halo, uint32_t* meta, int n, int pd,
+                                              int tid, int c) {
   using SET = WgSet<W>;
   constexpr int NS = 32;  // >= taps of any set
-  float S[NS];
+  f32x2 S2[NS / 2];
 #pragma unroll
-  for (int k = 0; k < NS; ++k) S[k] = 0.f;
+  for (int k = 0; k < NS / 2; ++k) S2[k] = f32x2{0.f, 0.f};
   float Dsum = 0.f;
   const int64_t rowbase = ((int64_t)n * kPD + pd) * kPH;
   for (int ph0 = 0; ph0 < kPH; ph0 += kWgRows) {
@@ -694,35 +629,33 @@ __device__ __forceinline__ void conv1_wg_wave(const uint8_t* __restrict__ xs, co
       if (xh < kPX) v = *reinterpret_cast<const uint2*>(xs + (((int64_t)z * kPY + y) * kPX + xh) * 8);
       halo[zh * kWgZS + yh * kWgRS + xh] = v;
     }
-    __syncthreads();
     const int ncell = nph * kPW;
-    int64_t o = ((rowbase + ph0) * kPW) * kC1 + c;
-    uint16_t pv_n = pout[o], dp_n = dp[o];
-    uint8_t a_n = amax[o];
+    const int64_t obase = ((rowbase + ph0) * kPW) * kC1;
+    for (int e = tid; e < ncell * kC1; e += 256) {  // (cell, channel) records, channel-fastest: coalesced
+      const int cell = e >> 6;
+      const uint16_t pv = pout[obase + e], g = dp[obase + e];
+      const int a = amax[obase + e];
+      const int phl = cell / kPW, pw = cell - phl * kPW;
+      const int off = (a / 9) * kWgZS + (3 * phl + (a / 3) % 3) * kWgRS + 3 * pw + a % 3;
+      const uint32_t dzb = bf16_to_f32(pv) > 0.f ? (uint32_t)g : 0u;
+      meta[e] = dzb | ((uint32_t)off << 16);
+    }
+    __syncthreads();
     for (int it = 0; it < ncell; ++it) {
-      const uint16_t pv_c = pv_n, dp_c = dp_n;
-      const int a = a_n;
-      if (it + 1 < ncell) {
-        const int64_t on = o + kC1;
-        pv_n = pout[on];
-        dp_n = dp[on];
-        a_n = amax[on];
-      }
-      o += kC1;
-      const int phl = it / kPW, pw = it - phl * kPW;
-      const float dz = bf16_to_f32(pv_c) > 0.f ? bf16_to_f32(dp_c) : 0.f;
+      const uint32_t m = meta[it * kC1 + c];
+      const float dz = bf16_to_f32((uint16_t)(m & 0xffffu));
       if (W == 0) Dsum += dz;
-      const int ad = a / 9, ah = (a / 3) % 3, aw = a % 3;
-      const uint2* base = halo + ad * kWgZS + (3 * phl + ah) * kWgRS + 3 * pw + aw;
+      const uint2* base = halo + (m >> 16);
       uint2 u[SET::n];
 #pragma unroll
       for (int i = 0; i < SET::n; ++i) {
-        constexpr int dummy = 0;
-        (void)dummy;
         const int t = SET::t(i);
         u[i] = base[(t / 9) * kWgZS + ((t / 3) % 3) * kWgRS + t % 3];
       }
+      // consecutive valid taps are paired into packed-FP32 FMAs (v_pk_fma_f32, dz broadcast)
+      const f32x2 dz2 = {dz, dz};
       int slot = 0;
+      float pend = 0.f;
 #pragma unroll
       for (int i = 0; i < SET::n; ++i) {
         const int t = SET::t(i);
@@ -730,11 +663,18 @@ __device__ __forceinline__ void conv1_wg_wave(const uint8_t* __restrict__ xs, co
         for (int r = 0; r < 8; ++r) {
           if (tp_valid(t, r)) {
             const uint32_t w = r < 4 ? u[i].x : u[i].y;
-            S[slot] = fmaf(dz, (float)((w >> (8 * (r & 3))) & 0xffu), S[slot]);
+            const float xv = (float)((w >> (8 * (r & 3))) & 0xffu);
+            if ((slot & 1) == 0) {
+              pend = xv;
+            } else {
+              const f32x2 x2 = {pend, xv};
+              S2[slot >> 1] = __builtin_elementwise_fma(dz2, x2, S2[slot >> 1]);
+            }
             ++slot;
           }
         }
       }
+      if (slot & 1) S2[slot >> 1].x = fmaf(dz, pend, S2[slot >> 1].x);
     }
   }
   float* op = part + (((int64_t)n * kPD + pd) * kC1 + c) * 126;
@@ -745,7 +685,7 @@ __device__ __forceinline__ void conv1_wg_wave(const uint8_t* __restrict__ xs, co
 #pragma unroll
     for (int r = 0; r < 8; ++r) {
       if (tp_valid(t, r)) {
-        op[tp_to_k(t, r)] = S[slot];
+        op[tp_to_k(t, r)] = (slot & 1) ? S2[slot >> 1].y : S2[slot >> 1].x;
         ++slot;
       }
     }
@@ -758,15 +698,16 @@ __global__ __launch_bounds__(256) void k_conv1_wgrad_split(const uint8_t* __rest
                                                            const uint16_t* __restrict__ pout,
                                                            const uint8_t* __restrict__ amax, float* __restrict__ part) {
   __shared__ __attribute__((aligned(16))) uint2 halo[kWgHalo];
+  __shared__ uint32_t meta[kWgMeta];
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
   const int pd = bid % kPD, n = bid / kPD;
   const int tid = threadIdx.x, c = tid & 63, wid = tid >> 6;
   const uint8_t* xs = x8 + (int64_t)idx[n] * kPZ * kPY * kPX * 8;
   switch (wid) {
-    case 0: conv1_wg_wave<0>(xs, dp, pout, amax, part, halo, n, pd, tid, c); break;
-    case 1: conv1_wg_wave<1>(xs, dp, pout, amax, part, halo, n, pd, tid, c); break;
-    case 2: conv1_wg_wave<2>(xs, dp, pout, amax, part, halo, n, pd, tid, c); break;
-    default: conv1_wg_wave<3>(xs, dp, pout, amax, part, halo, n, pd, tid, c); break;
+    case 0: conv1_wg_wave<0>(xs, dp, pout, amax, part, halo, meta, n, pd, tid, c); break;
+    case 1: conv1_wg_wave<1>(xs, dp, pout, amax, part, halo, meta, n, pd, tid, c); break;
+    case 2: conv1_wg_wave<2>(xs, dp, pout, amax, part, halo, meta, n, pd, tid, c); break;
+    default: conv1_wg_wave<3>(xs, dp, pout, amax, part, halo, meta, n, pd, tid, c); break;
   }
 }
 
