@@ -512,6 +512,7 @@ constexpr int kWgRS = 67;                        // row stride in voxels   (67 =
 constexpr int kWgZS = 553;                       // plane stride in voxels (553 = 9 mod 32, >= 8*67)
 constexpr int kWgHalo = 5 * kWgZS;               // voxels per halo buffer
 constexpr int kWgMeta = kWgRows * kPW * kC1;     // metadata records per stage
+__device__ __forceinline__ int bid_slab(int n_pd, int q, int nq) { return n_pd * nq + q; }  // slab of (n, pd, q)
 
 // Reduce slabs per client and apply the closed form.  grid (64 c, G), block 256: the B*19 slabs are split
 // over the 4 waves (lane = k, k + 64; 4 independent loads in flight per lane instead of one dependent chain),
@@ -610,7 +611,7 @@ template <int W>
 __device__ __forceinline__ void conv1_wg_wave(const uint8_t* __restrict__ xs, const uint16_t* __restrict__ dp,
                                               const uint16_t* __restrict__ pout, const uint8_t* __restrict__ amax,
                                               float* __restrict__ part, uint2* halo, uint32_t* meta, int n, int pd,
-                                              int tid, int c) {
+                                              int tid, int c, int ph_begin, int ph_end, int slab) {
   using SET = WgSet<W>;
   constexpr int NS = 32;  // >= taps of any set
   f32x2 S2[NS / 2];
@@ -618,8 +619,8 @@ __device__ __forceinline__ void conv1_wg_wave(const uint8_t* __restrict__ xs, co
   for (int k = 0; k < NS / 2; ++k) S2[k] = f32x2{0.f, 0.f};
   float Dsum = 0.f;
   const int64_t rowbase = ((int64_t)n * kPD + pd) * kPH;
-  for (int ph0 = 0; ph0 < kPH; ph0 += kWgRows) {
-    const int nph = min(kWgRows, kPH - ph0);
+  for (int ph0 = ph_begin; ph0 < ph_end; ph0 += kWgRows) {
+    const int nph = min(kWgRows, ph_end - ph0);
     const int ny = 3 * nph + 2;
     __syncthreads();
     for (int e = tid; e < 5 * ny * 64; e += 256) {
@@ -677,7 +678,7 @@ __device__ __forceinline__ void conv1_wg_wave(const uint8_t* __restrict__ xs, co
       if (slot & 1) S2[slot >> 1].x = fmaf(dz, pend, S2[slot >> 1].x);
     }
   }
-  float* op = part + (((int64_t)n * kPD + pd) * kC1 + c) * 126;
+  float* op = part + ((int64_t)slab * kC1 + c) * 126;
   int slot = 0;
 #pragma unroll
   for (int i = 0; i < SET::n; ++i) {
@@ -693,35 +694,45 @@ __device__ __forceinline__ void conv1_wg_wave(const uint8_t* __restrict__ xs, co
   if (W == 0) op[125] = Dsum;
 }
 
+// grid = NB * 19 * nq: block (n, pd, q) walks pooled rows [q * rq, (q + 1) * rq) of its slab (nq = 2 when one
+// slab per (sample, pd) would give the chip fewer than ~4 blocks per CU: few clients per GPU)
 __global__ __launch_bounds__(256) void k_conv1_wgrad_split(const uint8_t* __restrict__ x8, const int* __restrict__ idx,
                                                            const uint16_t* __restrict__ dp,
                                                            const uint16_t* __restrict__ pout,
-                                                           const uint8_t* __restrict__ amax, float* __restrict__ part) {
+                                                           const uint8_t* __restrict__ amax, float* __restrict__ part,
+                                                           int nq) {
   __shared__ __attribute__((aligned(16))) uint2 halo[kWgHalo];
   __shared__ uint32_t meta[kWgMeta];
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
-  const int pd = bid % kPD, n = bid / kPD;
+  const int q = bid % nq, rest = bid / nq;
+  const int pd = rest % kPD, n = rest / kPD;
+  const int rq = ((kPH + nq - 1) / nq + kWgRows - 1) / kWgRows * kWgRows;
+  const int ph_begin = q * rq, ph_end = min(kPH, ph_begin + rq);
   const int tid = threadIdx.x, c = tid & 63, wid = tid >> 6;
   const uint8_t* xs = x8 + (int64_t)idx[n] * kPZ * kPY * kPX * 8;
   switch (wid) {
-    case 0: conv1_wg_wave<0>(xs, dp, pout, amax, part, halo, meta, n, pd, tid, c); break;
-    case 1: conv1_wg_wave<1>(xs, dp, pout, amax, part, halo, meta, n, pd, tid, c); break;
-    case 2: conv1_wg_wave<2>(xs, dp, pout, amax, part, halo, meta, n, pd, tid, c); break;
-    default: conv1_wg_wave<3>(xs, dp, pout, amax, part, halo, meta, n, pd, tid, c); break;
+    case 0: conv1_wg_wave<0>(xs, dp, pout, amax, part, halo, meta, n, pd, tid, c, ph_begin, ph_end, bid_slab(rest, q, nq)); break;
+    case 1: conv1_wg_wave<1>(xs, dp, pout, amax, part, halo, meta, n, pd, tid, c, ph_begin, ph_end, bid_slab(rest, q, nq)); break;
+    case 2: conv1_wg_wave<2>(xs, dp, pout, amax, part, halo, meta, n, pd, tid, c, ph_begin, ph_end, bid_slab(rest, q, nq)); break;
+    default: conv1_wg_wave<3>(xs, dp, pout, amax, part, halo, meta, n, pd, tid, c, ph_begin, ph_end, bid_slab(rest, q, nq)); break;
   }
 }
+
+int conv1_wgrad_nq(int NB) { return (int64_t)NB * kPD < 4 * 256 * 4 ? 2 : 1; }
 
 void conv1_wgrad(uintptr_t x8, uintptr_t idx, uintptr_t dp, uintptr_t pout, uintptr_t amax, int NB, int B,
                  uintptr_t part, uintptr_t w125, uintptr_t mu, uintptr_t covw, uintptr_t invstd, uintptr_t theta,
                  int64_t ldt, int64_t off_g, uintptr_t grad, int64_t ldg, int64_t goff_w, int64_t goff_bias,
                  int64_t goff_g, int64_t goff_b, float wscale, uintptr_t stream) {
   hipStream_t s = as_stream(stream);
-  hipLaunchKernelGGL(k_conv1_wgrad_split, dim3(kPD * NB), dim3(256), 0, s, ptr<const uint8_t>(x8),
+  const int nq = conv1_wgrad_nq(NB);
+  hipLaunchKernelGGL(k_conv1_wgrad_split, dim3(kPD * NB * nq), dim3(256), 0, s, ptr<const uint8_t>(x8),
                      ptr<const int>(idx), ptr<const uint16_t>(dp), ptr<const uint16_t>(pout), ptr<const uint8_t>(amax),
-                     ptr<float>(part));
+                     ptr<float>(part), nq);
   NIDT_CHECK(hipGetLastError());
   const int G = NB / B;
-  hipLaunchKernelGGL(k_conv1_wgrad_fin, dim3(kC1, G), dim3(256), 0, s, ptr<const float>(part), B,
+  // client g's slabs are contiguous: B samples x 19 pd x nq row ranges
+  hipLaunchKernelGGL(k_conv1_wgrad_fin, dim3(kC1, G), dim3(256), 0, s, ptr<const float>(part), B * nq,
                      ptr<const float>(w125), ptr<const float>(mu), ptr<const float>(covw), ptr<const float>(invstd),
                      ptr<const float>(theta), ldt, off_g, ptr<float>(grad), ldg, goff_w, goff_bias, goff_g, goff_b,
                      wscale);

@@ -85,7 +85,7 @@ class HipAlexNet3D:
                 dy4=e(NB, 5, 7, 5, 192), dx4=e(NB, 5, 7, 5, 192), dy3=e(NB, 5, 7, 5, 192),
                 dx3=e(NB, 5, 7, 5, 128), dy2=e(NB, 17, 21, 17, 128), dp1=e(NB, 19, 23, 19, 64),
                 bnpart=e(G * 64 * 256 * 2, dt=f32), coef=e(G, 192, 3, dt=f32),
-                c1part=e(NB * 19, 64, 126, dt=f32),
+                c1part=e(NB * 19 * self.m.conv1_wgrad_nq(NB), 64, 126, dt=f32),
             )
             # per-layer output-position tables for the LDS-DMA wgrad kernel (shared by all clients and steps)
             st0 = torch.cuda.current_stream().cuda_stream
