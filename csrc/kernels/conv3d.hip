@@ -38,6 +38,7 @@ struct ConvFwdArgs {
 };
 
 constexpr int kFwdBP = 128;  // positions per block
+constexpr int kMaxCin = 512; // LDS-DMA paths (Cin % 64 == 0); the register-staged / transform paths keep 192
 constexpr int kBK = 32;      // k per step
 
 __device__ __forceinline__ int swz_fwd(int r) { return ((r >> 3) & 1) * 3; }
@@ -440,7 +441,9 @@ int conv3d_fwd_bp(int Cin, int Cout, int xf, int G, int Mg);
 
 void conv3d_fwd(uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t xs, uintptr_t xt, uintptr_t y, uintptr_t stats,
                 int G, int B, int D, int H, int W, int Cin, int Cout, int pad, uintptr_t stream) {
-  NIDT_REQUIRE(Cin % 32 == 0 && Cin <= 192, "conv3d_fwd: Cin must be a multiple of 32 and <= 192");
+  NIDT_REQUIRE(Cin % 32 == 0, "conv3d_fwd: Cin must be a multiple of 32");
+  NIDT_REQUIRE((xs == 0 && Cin % 64 == 0) ? Cin <= kMaxCin : Cin <= 192,
+               "conv3d_fwd: Cin <= 512 (LDS-DMA path: Cin % 64 == 0, no input transform), else <= 192");
   NIDT_REQUIRE(Cout % 64 == 0, "conv3d_fwd: Cout must be a multiple of 64");
   NIDT_REQUIRE(pad >= 0 && pad <= 2, "conv3d_fwd: pad in [0,2]");
   NIDT_REQUIRE((int64_t)B * D * H * W * Cin * 2 < (1ll << 31),
@@ -660,7 +663,7 @@ __global__ __launch_bounds__(256, 2) void k_conv_wgrad(ConvWgArgs a) {
 // Block = (co, g): the K-row is summed into LDS in k order, then written out in [ci][t] order (coalesced).
 __global__ __launch_bounds__(256) void k_wgrad_reduce(const float* __restrict__ part, int nsplit, int G, int Cout,
                                                       int Cin, float* grad, int64_t ldg, int64_t off, float scale) {
-  __shared__ float row[27 * 192];
+  __shared__ float row[27 * kMaxCin];
   const int co = blockIdx.x, g = blockIdx.y;
   const int K = 27 * Cin;
   const int64_t tot = (int64_t)G * Cout * K;
@@ -832,7 +835,9 @@ void conv3d_pos_table(uintptr_t tab, int B, int D, int H, int W, int pad, uintpt
 void conv3d_wgrad(uintptr_t x, uintptr_t xs, uintptr_t xt, uintptr_t dy, uintptr_t part, uintptr_t grad, int64_t ldg,
                   int64_t off, int G, int B, int D, int H, int W, int Cin, int Cout, int pad, int nsplit, float scale,
                   uintptr_t ptab, uintptr_t stream) {
-  NIDT_REQUIRE(Cin % 64 == 0 && Cin <= 192, "conv3d_wgrad: Cin must be a multiple of 64 and <= 192");
+  NIDT_REQUIRE(Cin % 64 == 0, "conv3d_wgrad: Cin must be a multiple of 64");
+  NIDT_REQUIRE((ptab && !xs) ? Cin <= kMaxCin : Cin <= 192,
+               "conv3d_wgrad: Cin <= 512 (LDS-DMA path with a position table), else <= 192");
   NIDT_REQUIRE(Cout % kWgCO == 0, "conv3d_wgrad: Cout must be a multiple of 64");
   ConvWgArgs a;
   a.x = ptr<const uint16_t>(x); a.xs = ptr<const float>(xs); a.xt = ptr<const float>(xt);
@@ -873,7 +878,7 @@ void conv3d_wgrad(uintptr_t x, uintptr_t xs, uintptr_t xt, uintptr_t dy, uintptr
 // wt [G][Cin][27][Cout] with the taps flipped (64x64 LDS-tiled transpose of wp per tap).
 __global__ __launch_bounds__(256) void k_pack_wp(const float* __restrict__ theta, int64_t ldt, int64_t off, int Cout,
                                                  int Cin, float scale, uint16_t* __restrict__ wp) {
-  __shared__ float row[27 * 192];
+  __shared__ float row[27 * kMaxCin];
   const int co = blockIdx.x, g = blockIdx.y;
   const int K = 27 * Cin;
   const float* src = theta + (int64_t)g * ldt + off + (int64_t)co * K;
@@ -905,7 +910,7 @@ __global__ __launch_bounds__(256) void k_pack_wt(const uint16_t* __restrict__ wp
 
 void pack_conv_w(uintptr_t theta, int64_t ldt, int64_t off, int G, int Cout, int Cin, float scale, uintptr_t wp,
                  uintptr_t wt, uintptr_t stream) {
-  NIDT_REQUIRE(Cin <= 192, "pack_conv_w: Cin <= 192");
+  NIDT_REQUIRE(Cin <= kMaxCin, "pack_conv_w: Cin <= 512");
   hipStream_t s = as_stream(stream);
   hipLaunchKernelGGL(k_pack_wp, dim3(Cout, G), dim3(256), 0, s, ptr<const float>(theta), ldt, off, Cout, Cin, scale,
                      ptr<uint16_t>(wp));

@@ -39,8 +39,8 @@ def _check_conv(x, w, bias, pad):
     if x.shape[0] % G or x.shape[4] != Cin or tuple(bias.shape) != (G, Cout):
         raise ValueError("nidt::conv3d_k3: shape mismatch x%s w%s bias%s" % (tuple(x.shape), tuple(w.shape),
                                                                           tuple(bias.shape)))
-    if Cin % 64 or Cin > 192 or Cout % 64:
-        raise ValueError("nidt::conv3d_k3: Cin must be a multiple of 64 and <= 192, Cout a multiple of 64")
+    if Cin % 64 or Cin > 512 or Cout % 64 or Cout > 512:
+        raise ValueError("nidt::conv3d_k3: Cin and Cout must be multiples of 64 and <= 512")
     if not 0 <= pad <= 2:
         raise ValueError("nidt::conv3d_k3: pad in [0, 2]")
     if any(s + 2 * pad - 2 <= 0 for s in x.shape[1:4]):

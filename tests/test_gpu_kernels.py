@@ -458,3 +458,42 @@ def test_torch_library_kth_and_weighted_sum():
     rows = torch.randn(5, 1001, device=DEV)
     wts = torch.rand(5, device=DEV)
     assert torch.allclose(torch.ops.nidt.weighted_rows_sum(rows, wts), (wts[:, None] * rows).sum(0), atol=1e-5)
+
+
+@pytest.mark.parametrize("cin,cout,pad", [(64, 64, 1), (256, 256, 1), (512, 512, 1), (128, 256, 0)])
+def test_hip_conv3d_module_matches_conv3d(cin, cout, pad):
+    """HipConv3d (nidt::conv3d_k3, incl. the 512-channel LDS-DMA paths) == F.conv3d fwd + both gradients."""
+    from neuroimagedisttraining_amd.ops.modules import HipConv3d
+    torch.manual_seed(3)
+    conv = HipConv3d(cin, cout, 3, 1, pad, bias=False).to(DEV)
+    x = torch.randn(2, cin, 6, 7, 5, device=DEV).to(memory_format=torch.channels_last_3d)
+    xa = x.clone().requires_grad_(True)
+    y = conv(xa.bfloat16())
+    g = torch.randn_like(y.float())
+    y.float().backward(g)
+    xr = x.bfloat16().float().requires_grad_(True)
+    wr = conv.weight.detach().bfloat16().float().requires_grad_(True)
+    yr = F.conv3d(xr, wr, None, 1, pad)
+    yr.backward(g)
+    assert _relerr(y.float(), yr) < 1e-2
+    assert _relerr(xa.grad, xr.grad) < 2e-2
+    assert _relerr(conv.weight.grad, wr.grad) < 2e-2
+
+
+def test_resnet3d_bottleneck_with_hip_convs_trains():
+    from neuroimagedisttraining_amd.models.resnet3d import resnet3d_50
+    from neuroimagedisttraining_amd.ops.modules import HipConv3d, use_hip_convs
+    torch.manual_seed(0)
+    m = resnet3d_50(num_classes=1, width=16).to(DEV)
+    ref = resnet3d_50(num_classes=1, width=16).to(DEV)
+    ref.load_state_dict(m.state_dict())
+    n = use_hip_convs(m)
+    assert n > 0 and sum(isinstance(c, HipConv3d) for c in m.modules()) == n
+    assert list(m.state_dict().keys()) == list(ref.state_dict().keys())
+    x = torch.randn(2, 1, 32, 36, 32, device=DEV)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        out = m(x)
+        out_ref = ref(x)
+    assert torch.isfinite(out).all() and _relerr(out.float(), out_ref.float()) < 5e-2
+    out.float().sum().backward()
+    assert all(torch.isfinite(p.grad).all() for p in m.parameters() if p.grad is not None)
