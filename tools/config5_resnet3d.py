@@ -31,6 +31,8 @@ def main():
     ap.add_argument("--epochs", type=int, default=1)
     ap.add_argument("--topk", type=float, default=0.01)
     ap.add_argument("--width", type=int, default=64)
+    ap.add_argument("--no-hip-convs", action="store_true",
+                    help="keep every Conv3d on MIOpen (default: eligible 3x3x3 convs run on the HIP kernels)")
     args = ap.parse_args()
     from neuroimagedisttraining_amd.data.synthetic_fl import build_fl_volumes
     from neuroimagedisttraining_amd.engine.executor import ClientSplit, FLConfig, FLRunner, TorchEngine
@@ -44,6 +46,10 @@ def main():
     splits = [local.get(c) or ClientSplit(np.zeros(args.train_per_client, np.int64),
                                           np.zeros(args.test_per_client, np.int64)) for c in range(args.clients)]
     model = resnet3d_50(num_classes=1, checkpoint_stages=True, width=args.width)
+    n_hip = 0
+    if dev.type == "cuda" and not args.no_hip_convs:
+        from neuroimagedisttraining_amd.ops.modules import use_hip_convs
+        n_hip = use_hip_convs(model)  # 13 of the 16 bottleneck 3x3x3 convs -> nidt::conv3d_k3
     eng = TorchEngine(model, vol, labels, dev, loss="bce", amp=True)
     cfg = FLConfig(comm_round=args.rounds, epochs=args.epochs, batch_size=args.batch, lr=0.01, frac=1.0,
                    seed=7, update_topk=args.topk, frequency_of_the_test=1, test_batch=8)
@@ -52,16 +58,21 @@ def main():
         torch.cuda.synchronize()
     t0 = time.perf_counter()
     res = None
+    per_round = []
     for r in range(args.rounds):
+        tr = time.perf_counter()
         res = runner.run_round(r)
-    if dev.type == "cuda":
-        torch.cuda.synchronize()
+        if dev.type == "cuda":
+            torch.cuda.synchronize()
+        per_round.append(rt.max_over_ranks(time.perf_counter() - tr, info))
     dt = rt.max_over_ranks(time.perf_counter() - t0, info)
     peak = torch.cuda.max_memory_allocated() / 2 ** 30 if dev.type == "cuda" else 0.0
     if info.is_main:
         print(json.dumps({"config": "3D ResNet-50 full-res, sparse top-k all-gather", "clients": args.clients,
                           "ranks": info.world, "params": runner.P, "rounds": args.rounds,
-                          "s_per_round": round(dt / args.rounds, 2), "peak_hbm_gib_rank0": round(peak, 1),
+                          "s_per_round": round(dt / args.rounds, 2),
+                          "s_round_each": [round(x, 2) for x in per_round], "hip_convs": n_hip,
+                          "peak_hbm_gib_rank0": round(peak, 1),
                           "update_topk": args.topk, "aggregate_elems": runner.stat_info.get("aggregate_elems"),
                           "metrics": res}), flush=True)
     rt.shutdown(info)
