@@ -9,7 +9,7 @@ namespace nidt {
 int64_t clip_sgd_mask_workspace(int64_t C, int64_t P);
 void clip_sgd_mask(uintptr_t w, uintptr_t g, uintptr_t buf, uintptr_t mask, uintptr_t part, uintptr_t coef_out,
                    uintptr_t wbf, int64_t C, int64_t P, int64_t stride, float lr, float wd, float mom, int first,
-                   float max_norm, uintptr_t stream);
+                   float max_norm, uintptr_t lr_dev, uintptr_t stream);
 void weighted_rows_sum(uintptr_t rows, uintptr_t wts, int64_t C, int64_t P, int64_t stride, float beta, uintptr_t out,
                        uintptr_t stream);
 void broadcast_row(uintptr_t src, int64_t P, int64_t stride, int64_t C, uintptr_t dst, uintptr_t stream);
@@ -60,7 +60,7 @@ void conv1_wgrad(uintptr_t x8, uintptr_t idx, uintptr_t dp, uintptr_t pout, uint
 // head.hip
 void head(uintptr_t p5, uintptr_t theta, int64_t ldt, int64_t off_w1, int64_t off_b1, int64_t off_w2, int64_t off_b2,
           uintptr_t y, uintptr_t logits, uintptr_t loss, uintptr_t grad, int64_t ldg, uintptr_t dp5, int G, int B,
-          int train, float keep, uint64_t seed, uintptr_t cids, uintptr_t stream);
+          int train, float keep, uint64_t seed, uintptr_t cids, uintptr_t seed_dev, uintptr_t stream);
 // select.hip
 void saliency_acc(uintptr_t theta, uintptr_t grad, int64_t ld, int64_t P, int G, float alpha, uintptr_t score,
                   int64_t lds, uintptr_t stream);

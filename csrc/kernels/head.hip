@@ -31,6 +31,7 @@ struct HeadArgs {
   float keep;           // dropout keep probability (1 = no dropout)
   uint64_t seed;
   const int* cids;      // [G] global client ids (dropout streams are per client, independent of sharding)
+  const int64_t* seed_dev;  // optional: device step counter added to seed (hipGraph replays change it on device)
 };
 
 constexpr int kHF = 256, kHH = 64, kHMaxB = 32;
@@ -43,6 +44,7 @@ __global__ __launch_bounds__(256) void k_head(HeadArgs a) {
   __shared__ float DZ2[kHMaxB];
   const int g = blockIdx.x, tid = threadIdx.x;
   const uint32_t cid = a.cids ? (uint32_t)a.cids[g] : (uint32_t)g;
+  const uint64_t seed = a.seed + (a.seed_dev ? (uint64_t)*a.seed_dev : 0ull);
   const float* th = a.theta + (int64_t)g * a.ldt;
   const float* w1 = th + a.off_w1;
   const float* b1 = th + a.off_b1;
@@ -60,7 +62,7 @@ __global__ __launch_bounds__(256) void k_head(HeadArgs a) {
       const int c = f >> 1, h = f & 1;
       const int n = g * a.B + b0 + b;
       float v = bf16_to_f32(a.p5[((int64_t)n * 2 + h) * 128 + c]);
-      if (drop) v = (hash4(a.seed, cid, b0 + b, f) < thr) ? v * inv_keep : 0.f;
+      if (drop) v = (hash4(seed, cid, b0 + b, f) < thr) ? v * inv_keep : 0.f;
       F[b][f] = v;
     }
     __syncthreads();
@@ -71,7 +73,7 @@ __global__ __launch_bounds__(256) void k_head(HeadArgs a) {
       for (int f = 0; f < kHF; ++f) z = fmaf(wr[f], F[b][f], z);
       Z1[b][o] = z;
       float h = fmaxf(z, 0.f);
-      if (drop) h = (hash4(a.seed ^ 0x5bd1e995ull, cid, b0 + b, o) < thr) ? h * inv_keep : 0.f;
+      if (drop) h = (hash4(seed ^ 0x5bd1e995ull, cid, b0 + b, o) < thr) ? h * inv_keep : 0.f;
       Hd[b][o] = h;
     }
     __syncthreads();
@@ -113,7 +115,7 @@ __global__ __launch_bounds__(256) void k_head(HeadArgs a) {
   for (int e = tid; e < nb * kHH; e += 256) {
     const int b = e / kHH, o = e - b * kHH;
     float d = DZ2[b] * w2[o];
-    if (drop) d = (hash4(a.seed ^ 0x5bd1e995ull, cid, b, o) < thr) ? d * inv_keep : 0.f;
+    if (drop) d = (hash4(seed ^ 0x5bd1e995ull, cid, b, o) < thr) ? d * inv_keep : 0.f;
     Z1[b][o] = Z1[b][o] > 0.f ? d : 0.f;
   }
   __syncthreads();
@@ -132,7 +134,7 @@ __global__ __launch_bounds__(256) void k_head(HeadArgs a) {
     const int b = e / kHF, f = e - b * kHF;
     float s = 0.f;
     for (int o = 0; o < kHH; ++o) s = fmaf(Z1[b][o], w1[(int64_t)o * kHF + f], s);
-    if (drop) s = (hash4(a.seed, cid, b, f) < thr) ? s * inv_keep : 0.f;
+    if (drop) s = (hash4(seed, cid, b, f) < thr) ? s * inv_keep : 0.f;
     const int c = f >> 1, h = f & 1;
     a.dp5[(((int64_t)g * a.B + b) * 2 + h) * 128 + c] = f32_to_bf16(s);
   }
@@ -140,11 +142,11 @@ __global__ __launch_bounds__(256) void k_head(HeadArgs a) {
 
 void head(uintptr_t p5, uintptr_t theta, int64_t ldt, int64_t off_w1, int64_t off_b1, int64_t off_w2, int64_t off_b2,
           uintptr_t y, uintptr_t logits, uintptr_t loss, uintptr_t grad, int64_t ldg, uintptr_t dp5, int G, int B,
-          int train, float keep, uint64_t seed, uintptr_t cids, uintptr_t stream) {
+          int train, float keep, uint64_t seed, uintptr_t cids, uintptr_t seed_dev, uintptr_t stream) {
   NIDT_REQUIRE(!train || B <= kHMaxB, "head: training batch per client must be <= 32");
   HeadArgs a{ptr<const uint16_t>(p5), ptr<const float>(theta), ldt, off_w1, off_b1, off_w2, off_b2,
              ptr<const float>(y), ptr<float>(logits), ptr<float>(loss), ptr<float>(grad), ldg, ptr<uint16_t>(dp5),
-             B, 1, train, keep, seed, ptr<const int>(cids)};
+             B, 1, train, keep, seed, ptr<const int>(cids), ptr<const int64_t>(seed_dev)};
   hipLaunchKernelGGL(k_head, dim3(G), dim3(256), 0, as_stream(stream), a);
   NIDT_CHECK(hipGetLastError());
 }

@@ -42,9 +42,11 @@ template <bool HAS_MASK, bool HAS_MOM, bool EMIT_BF16>
 __global__ __launch_bounds__(kOptThreads) void k_clip_sgd_mask(
     float* __restrict__ w, float* __restrict__ g, float* __restrict__ buf, const float* __restrict__ mask,
     const float* __restrict__ part, int nblk, int64_t P, int64_t stride, int64_t chunk, float lr, float wd,
-    float mom, int first, float max_norm, float* __restrict__ coef_out, uint16_t* __restrict__ wbf) {
+    float mom, int first, float max_norm, float* __restrict__ coef_out, uint16_t* __restrict__ wbf,
+    const float* __restrict__ lr_dev) {
   __shared__ float red[kOptThreads / 64];
   const int c = blockIdx.y;
+  if (lr_dev) lr = *lr_dev;  // hipGraph replays: the round's learning rate lives on the device
   float t = 0.f;
   for (int i = threadIdx.x; i < nblk; i += kOptThreads) t += part[(int64_t)c * nblk + i];
   t = block_sum(t, red);
@@ -130,7 +132,7 @@ int64_t clip_sgd_mask_workspace(int64_t C, int64_t P) {
 
 void clip_sgd_mask(uintptr_t w, uintptr_t g, uintptr_t buf, uintptr_t mask, uintptr_t part, uintptr_t coef_out,
                    uintptr_t wbf, int64_t C, int64_t P, int64_t stride, float lr, float wd, float mom, int first,
-                   float max_norm, uintptr_t stream) {
+                   float max_norm, uintptr_t lr_dev, uintptr_t stream) {
   NIDT_REQUIRE(stride % 4 == 0 && stride >= P, "stride must be >= P and a multiple of 4");
   NIDT_REQUIRE((w & 15) == 0 && (g & 15) == 0 && (buf & 15) == 0 && (mask & 15) == 0 && (wbf & 7) == 0,
                "buffers must be 16-byte aligned");
@@ -144,7 +146,7 @@ void clip_sgd_mask(uintptr_t w, uintptr_t g, uintptr_t buf, uintptr_t mask, uint
 #define NIDT_LAUNCH(M, MO, B)                                                                                   \
   hipLaunchKernelGGL((k_clip_sgd_mask<M, MO, B>), grid, dim3(kOptThreads), 0, st, ptr<float>(w), ptr<float>(g),      \
                      ptr<float>(buf), ptr<const float>(mask), ptr<const float>(part), nblk, P, stride, chunk, lr, wd,   \
-                     mom, first, max_norm, ptr<float>(coef_out), ptr<uint16_t>(wbf))
+                     mom, first, max_norm, ptr<float>(coef_out), ptr<uint16_t>(wbf), ptr<const float>(lr_dev))
   if (hm && hmo && hb) NIDT_LAUNCH(true, true, true);
   else if (hm && hmo && !hb) NIDT_LAUNCH(true, true, false);
   else if (hm && !hmo && hb) NIDT_LAUNCH(true, false, true);

@@ -175,9 +175,10 @@ class HipAlexNet3D:
         return b
 
     # ---------------------------------------------------------------------------------------------
-    def train_step(self, theta, bufs, grads, x8, mom, idx, labels, G, B, keep=0.5, seed=0, cids=None):
+    def train_step(self, theta, bufs, grads, x8, mom, idx, labels, G, B, keep=0.5, seed=0, cids=None, seed_dev=None):
         """Forward + backward for G clients; writes ``grads`` [G,P], updates BN running stats in ``bufs``.
-        Returns the per-client mean loss tensor [G] (device)."""
+        Returns the per-client mean loss tensor [G] (device).  ``seed_dev`` (int64 device scalar, optional) is
+        added to ``seed`` inside the kernel, so a captured hipGraph can advance the dropout stream on device."""
         assert grads.shape == theta.shape and grads.stride(1) == 1 and grads.stride(0) == theta.stride(0)
         assert labels.dtype == torch.float32 and labels.numel() == G * B and B <= 32
         m, st = self.m, torch.cuda.current_stream().cuda_stream
@@ -187,7 +188,7 @@ class HipAlexNet3D:
         o = self.o
         m.head(_p(b["p5"]), _p(theta), P, o["classifier.1.weight"], o["classifier.1.bias"], o["classifier.4.weight"],
                o["classifier.4.bias"], _p(labels), _p(b["logits"]), _p(b["loss"]), _p(grads), grads.stride(0), _p(b["dp5"]), G, B, 1,
-               float(keep), int(seed) & ((1 << 64) - 1), _p(cids), st)
+               float(keep), int(seed) & ((1 << 64) - 1), _p(cids), _p(seed_dev), st)
         nchunk = 64
 
         def bn_bwd(pool, ci, bi, C, sp, dsrc, pout, amax, dy, y):
@@ -230,5 +231,5 @@ class HipAlexNet3D:
         P = theta.stride(0)
         o = self.o
         m.head(_p(b["p5"]), _p(theta), P, o["classifier.1.weight"], o["classifier.1.bias"], o["classifier.4.weight"],
-               o["classifier.4.bias"], 0, _p(b["logits"]), 0, 0, P, 0, G, B, 0, 1.0, 0, 0, st)
+               o["classifier.4.bias"], 0, _p(b["logits"]), 0, 0, P, 0, G, B, 0, 1.0, 0, 0, 0, st)
         return b["logits"]

@@ -68,6 +68,7 @@ class FLConfig:
     sparse_aggregate: bool = True  # SalientGrads: all-reduce only the coordinates kept by the global mask
     update_topk: float = 0.0      # >0: each client sends only its top-k |update| (values + int32 indices,
                                   # k = update_topk * P) through an RCCL all-gather (BASELINE config 5)
+    hip_graphs: bool = True       # capture each lockstep local step (train + optimizer) in a hipGraph and replay it
 
 
 # ------------------------------------------------------------------------------------------------
@@ -84,7 +85,9 @@ class HipEngine:
         self.m = ops.ext()
         self._cid_cache = {}
 
-    def train_step(self, theta, bufs, grads, idx, G, B, keep, seed, cids=None):
+    supports_graphs = True
+
+    def train_step(self, theta, bufs, grads, idx, G, B, keep, seed, cids=None, seed_dev=None):
         y = self.labels.index_select(0, idx.long())
         ct = None
         if cids is not None:
@@ -93,13 +96,13 @@ class HipEngine:
             if ct is None:  # one upload per client group, reused by every step
                 ct = torch.tensor(key, dtype=torch.int32, device=self.device)
                 self._cid_cache[key] = ct
-        return self.net.train_step(theta, bufs, grads, self.x8, self.mom, idx, y, G, B, keep, seed, ct)
+        return self.net.train_step(theta, bufs, grads, self.x8, self.mom, idx, y, G, B, keep, seed, ct, seed_dev)
 
     def eval_logits(self, theta, bufs, idx, G, B):
         return self.net.eval_logits(theta, bufs, self.x8, idx, G, B)
 
     # fused optimizer: clip(10) -> SGD(wd, momentum) -> w *= mask (one HIP pass per row)
-    def opt_step(self, theta, grads, mom_buf, mask, lr, wd, momentum, first, max_norm):
+    def opt_step(self, theta, grads, mom_buf, mask, lr, wd, momentum, first, max_norm, lr_dev=None):
         G, P = theta.shape
         ws = self.m.clip_sgd_mask_workspace(G, P)
         if not hasattr(self, "_optws") or self._optws.numel() < ws:
@@ -107,7 +110,7 @@ class HipEngine:
         self.m.clip_sgd_mask(theta.data_ptr(), grads.data_ptr(), mom_buf.data_ptr() if mom_buf is not None else 0,
                              mask.data_ptr() if mask is not None else 0, self._optws.data_ptr(), 0, 0, G, P,
                              theta.stride(0), float(lr), float(wd), float(momentum), int(first), float(max_norm),
-                             torch.cuda.current_stream().cuda_stream)
+                             lr_dev.data_ptr() if lr_dev is not None else 0, torch.cuda.current_stream().cuda_stream)
 
     def saliency_acc(self, theta, grads, score, alpha):
         G, P = theta.shape
@@ -274,6 +277,8 @@ class FLRunner:
                               global_test_loss=[], person_test_loss=[], round_time=[])
         self.timers = {"train": 0.0, "aggregate": 0.0, "eval": 0.0, "snip": 0.0}
         self._step_seed = 0
+        self._graphs = {}          # (rows, G, B) -> captured local step (None until the shape repeats)
+        self._lr_dev = self._seed_dev = None
 
     # ---------------------------------------------------------------------------------------------
     def _rng(self, *key):
@@ -386,6 +391,7 @@ class FLRunner:
                 keep = (sel >= thr).float()
             mask[self.maskable] = keep
         self.mask = mask if cfg.snip_mask else torch.ones_like(mask)
+        self._graphs = {}  # captured local steps reference the mask tensor
         self.timers["snip"] += time.perf_counter() - t0
         return self.mask
 
@@ -412,8 +418,20 @@ class FLRunner:
                 self.bufs[r].copy_(self.b_global)
         lr = cfg.lr * (cfg.lr_decay ** round_idx)
         first = [True]
+        use_graphs = (cfg.hip_graphs and getattr(self.e, "supports_graphs", False) and self.device.type == "cuda"
+                      and cfg.momentum == 0)
+        if use_graphs:
+            if self._lr_dev is None:
+                self._lr_dev = torch.zeros(1, dtype=torch.float32, device=self.device)
+                self._seed_dev = torch.zeros(1, dtype=torch.int64, device=self.device)
+            self._lr_dev.fill_(lr)
         for ep in range(cfg.epochs):
             def fn(rr, idx, G, B):
+                if use_graphs and rr == list(range(rr[0], rr[-1] + 1)):
+                    self._graph_step(rr, idx, G, B)
+                    first[0] = False
+                    return
+
                 def body(th, bu, gr, mo):
                     self._step_seed += 1
                     if cfg.prox_mu > 0:
@@ -427,6 +445,54 @@ class FLRunner:
                 self._with_rows(rr, body)
                 first[0] = False
             self._run_batches(rows, loc, round_idx, ep, fn)
+
+    def _graph_step(self, rr, idx, G, B):
+        """One lockstep local step (forward+backward of G clients, FedProx term, clip+SGD+mask) as a replayed
+        hipGraph.  The ~45 kernel launches of a step become one graph launch; everything that changes between
+        steps lives in device memory the graph reads: the sample indices (copied into a static buffer), the
+        dropout stream counter and the round's learning rate.  The first step of a (rows, G, B) shape runs
+        eagerly (it also allocates every scratch buffer the graph will reuse), the second is captured and
+        replayed, later ones only replay — same kernels, same arguments, same results as the eager path."""
+        cfg = self.cfg
+        lo, hi = rr[0], rr[-1] + 1
+        key = (lo, hi, G, B)
+        self._step_seed += 1
+        ent = self._graphs.get(key, "new")
+        th, bu, gr = self.theta[lo:hi], self.bufs[lo:hi], self.grads[lo:hi]
+        mask = self.mask if self.alg == "salientgrads" else None
+        cids = [self.local[r] for r in rr]
+        base = cfg.seed << 20
+
+        def step(idx_t, seed_dev):
+            self.e.train_step(th, bu, gr, idx_t, G, B, cfg.dropout_keep, base, cids=cids, seed_dev=seed_dev)
+            if cfg.prox_mu > 0:
+                gr.add_(th - self.w_global.unsqueeze(0), alpha=cfg.prox_mu)
+            self.e.opt_step(th, gr, None, mask, 0.0, cfg.wd, 0.0, True, cfg.max_norm, lr_dev=self._lr_dev)
+
+        self._seed_dev.fill_(self._step_seed)
+        if ent == "new":  # eager warm-up step: allocates the per-shape scratch the capture will reuse
+            step(idx, self._seed_dev)
+            self._graphs[key] = None
+            return
+        if ent is None:
+            idx_buf = torch.empty(G * B, dtype=torch.int32, device=self.device)
+            idx_buf.copy_(idx)
+            torch.cuda.current_stream().synchronize()
+            g = torch.cuda.CUDAGraph()
+            try:
+                with torch.cuda.graph(g):
+                    step(idx_buf, self._seed_dev)
+            except Exception:  # noqa: BLE001 - capture unsupported here: stay eager for this shape
+                self._graphs[key] = False
+                step(idx, self._seed_dev)
+                return
+            ent = self._graphs[key] = (g, idx_buf)
+        elif ent is False:
+            step(idx, self._seed_dev)
+            return
+        g, idx_buf = ent
+        idx_buf.copy_(idx)
+        g.replay()
 
     def aggregate(self, sampled):
         if self.cfg.aggregator != "fedavg":

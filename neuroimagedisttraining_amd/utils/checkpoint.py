@@ -46,6 +46,8 @@ def load_runner(runner, directory):
     runner.b_global.copy_(glob["b_global"].to(runner.device))
     if glob["mask"] is not None:
         runner.mask = glob["mask"].to(runner.device)
+        if hasattr(runner, "_graphs"):
+            runner._graphs = {}  # captured steps reference the previous mask tensor
     if "step_seed" in glob:  # dropout stream position (bit-exact resume)
         runner._step_seed = int(glob["step_seed"])
     runner.theta.copy_(shard["theta"].to(runner.device))

@@ -393,7 +393,7 @@ def test_clip_sgd_mask_matches_reference():
     clip_sgd_mask_reference(ref, grad.clone(), mask, 0.01, 5e-4)
     ws = torch.empty(m.clip_sgd_mask_workspace(G, P), device=DEV)
     m.clip_sgd_mask(theta.data_ptr(), grad.data_ptr(), 0, mask.data_ptr(), ws.data_ptr(), 0, 0, G, P, theta.stride(0),
-                    0.01, 5e-4, 0.0, 1, 10.0, _st())
+                    0.01, 5e-4, 0.0, 1, 10.0, 0, _st())
     torch.cuda.synchronize()
     assert _relerr(theta, ref) < 1e-6
 
@@ -497,3 +497,31 @@ def test_resnet3d_bottleneck_with_hip_convs_trains():
     assert torch.isfinite(out).all() and _relerr(out.float(), out_ref.float()) < 5e-2
     out.float().sum().backward()
     assert all(torch.isfinite(p.grad).all() for p in m.parameters() if p.grad is not None)
+
+
+def test_hip_graph_local_steps_match_eager():
+    """FLRunner with hipGraph-captured local steps == the eager launch sequence, bit for bit (same kernels, same
+    arguments; only the step-varying scalars move to device memory)."""
+    from neuroimagedisttraining_amd.data.synthetic_fl import build_fl_volumes, to_hip_store
+    from neuroimagedisttraining_amd.engine.executor import FLConfig, FLRunner, HipEngine
+    from neuroimagedisttraining_amd.models.alexnet3d import AlexNet3D_Dropout
+    from neuroimagedisttraining_amd.parallel import runtime as rt
+    info = rt.DistInfo(device=torch.device(DEV))
+    vol, labels, splits = build_fl_volumes(list(range(3)), 3, 32, 8, DEV, seed=5)
+    x8, mom = to_hip_store(vol)
+    outs = []
+    for graphs in (False, True):
+        torch.manual_seed(0)
+        model = AlexNet3D_Dropout(num_classes=1)
+        eng = HipEngine(model, x8, mom, labels, DEV)
+        cfg = FLConfig(comm_round=2, epochs=2, batch_size=16, dense_ratio=0.5, seed=3, hip_graphs=graphs)
+        r = FLRunner(eng, [splits[c] for c in range(3)], cfg, info, model, algorithm="salientgrads")
+        r.generate_global_mask_snip()
+        for k in range(2):
+            r.run_round(k)
+        torch.cuda.synchronize()
+        if graphs:
+            assert any(isinstance(v, tuple) for v in r._graphs.values()), "no step was captured"
+        outs.append((r.w_global.clone(), r.b_global.clone(), r.stat_info["global_test_acc"]))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    assert outs[0][2] == outs[1][2]
