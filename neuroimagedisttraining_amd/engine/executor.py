@@ -480,7 +480,8 @@ class FLRunner:
             torch.cuda.current_stream().synchronize()
             g = torch.cuda.CUDAGraph()
             try:
-                with torch.cuda.graph(g):
+                # thread_local: the RCCL watchdog thread of a multi-GPU run may query events during the capture
+                with torch.cuda.graph(g, capture_error_mode="thread_local"):
                     step(idx_buf, self._seed_dev)
             except Exception:  # noqa: BLE001 - capture unsupported here: stay eager for this shape
                 self._graphs[key] = False
