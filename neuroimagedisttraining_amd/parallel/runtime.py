@@ -54,11 +54,13 @@ def init_distributed(prefer_gpu=True, timeout_s=600) -> DistInfo:
     backend = "none"
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        backend = "nccl" if use_gpu else "gloo"
+        # NIDT_DIST_BACKEND=gloo rehearses the multi-rank GPU path on ONE GPU (several ranks on cuda:0, gloo
+        # collectives on device tensors) where RCCL refuses two ranks on the same device
+        backend = os.environ.get("NIDT_DIST_BACKEND") or ("nccl" if use_gpu else "gloo")
         if not dist.is_initialized():
             kw = dict(backend=backend, rank=rank, world_size=world,
                       timeout=datetime.timedelta(seconds=timeout_s))
-            if use_gpu:
+            if use_gpu and backend == "nccl":
                 kw["device_id"] = device
             dist.init_process_group(**kw)
     return DistInfo(rank, world, local, device, backend)
