@@ -12,7 +12,8 @@ Backends (``backend=`` of the managers):
   generated stubs, and importable (the reference's is not, quirk Q17).
 * ``"MPI"`` — the reference's send/receive-thread manager (``mpi_threads.py``) over an ``mpi4py``-like ``comm``;
   without mpi4py it runs over :class:`TorchP2PComm` (torch.distributed point-to-point).
-* ``"MQTT"`` — needs ``paho-mqtt``; raises a clear ImportError when absent.
+* ``"MQTT"`` — the reference's topic scheme over a built-in MQTT 3.1.1 client (``mqtt.py``; any broker, or
+  the in-process :class:`MqttBroker`).
 
 The receive loop is event driven (blocking queue get with timeout) rather than the reference's 0.3 s polling.
 """
@@ -212,12 +213,7 @@ class GRPCCommManager(_QueueCommManager):
 from .mpi_threads import MpiCommunicationManager, TorchP2PComm  # noqa: E402,F401  (mpi4py-style manager)
 
 
-def MqttCommManager(*a, **k):  # noqa: N802
-    try:
-        import paho.mqtt.client  # noqa: F401
-    except ImportError as e:
-        raise ImportError("the MQTT backend needs paho-mqtt (not installed); use backend='GRPC' or 'TORCH'") from e
-    raise NotImplementedError("MQTT backend not provided; use backend='GRPC'")
+from .mqtt import MqttBroker, MqttClient, MqttCommManager  # noqa: E402,F401  (MQTT 3.1.1, no paho needed)
 
 
 def make_comm_manager(backend, rank, size, **kw):
@@ -232,7 +228,8 @@ def make_comm_manager(backend, rank, size, **kw):
     if backend == "MPI":
         return MpiCommunicationManager(kw.get("comm"), rank, size)
     if backend == "MQTT":
-        return MqttCommManager(kw.get("host"), kw.get("port"), client_id=rank, client_num=size)
+        return MqttCommManager(kw.get("host"), kw.get("port"), kw.get("topic", "fedml"), client_id=rank,
+                               client_num=kw.get("client_num", size - 1))
     raise ValueError("unknown backend %r" % backend)
 
 

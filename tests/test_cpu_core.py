@@ -112,6 +112,42 @@ def test_grpc_backend_roundtrip():
         b.stop_receive_message()
 
 
+def test_mqtt_backend_roundtrip_with_builtin_broker():
+    """Reference topic scheme (server 0 <-> clients 1..N) over the built-in MQTT 3.1.1 client and broker."""
+    from neuroimagedisttraining_amd.comm import MqttCommManager
+    from neuroimagedisttraining_amd.comm.mqtt import MqttBroker, topic_matches
+    assert topic_matches("fedml/+/x", "fedml/3/x") and topic_matches("a/#", "a/b/c") and not topic_matches("a", "a/b")
+    broker = MqttBroker()
+    srv = MqttCommManager("127.0.0.1", broker.port, client_id=0, client_num=2)
+    c1 = MqttCommManager("127.0.0.1", broker.port, client_id=1, client_num=2)
+    c2 = MqttCommManager("127.0.0.1", broker.port, client_id=2, client_num=2)
+    try:
+        for c in (c1, c2):
+            m = Message(3, c.client_id, 0)
+            m.add_params("w", torch.full((4,), float(c.client_id)))
+            c.send_message(m)
+        got = sorted((srv.q.get(timeout=10) for _ in range(2)), key=lambda r: r.get_sender_id())
+        assert [r.get_sender_id() for r in got] == [1, 2]
+        assert torch.equal(got[1].get("w"), torch.full((4,), 2.0))
+        m = Message(4, 0, 2)
+        m.add_params("round", 7)
+        srv.send_message(m)
+        r = c2.q.get(timeout=10)
+        assert r.get_type() == 4 and r.get("round") == 7 and c1.q.empty()
+        seen = []
+
+        class Obs:
+            def receive_message(self, t, p):
+                seen.append((t, p.get("round")))
+        c2.add_observer(Obs())
+        srv.send_message(m)
+        assert c2.poll_once(timeout=10.0) and seen == [(4, 7)]
+    finally:
+        for c in (srv, c1, c2):
+            c.stop_receive_message()
+        broker.close()
+
+
 def test_topologies_row_stochastic():
     t = SymmetricTopologyManager(8, 4)
     W = t.generate_topology()
