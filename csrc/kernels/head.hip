@@ -42,6 +42,7 @@ __global__ __launch_bounds__(256) void k_head(HeadArgs a) {
   __shared__ float Hd[kHMaxB][kHH + 1];
   __shared__ float Z2[kHMaxB];
   __shared__ float DZ2[kHMaxB];
+  __shared__ float W1s[kHH][kHF + 1];  // w1 staged once (the dot products below read it ~nb times)
   const int g = blockIdx.x, tid = threadIdx.x;
   const uint32_t cid = a.cids ? (uint32_t)a.cids[g] : (uint32_t)g;
   const uint64_t seed = a.seed + (a.seed_dev ? (uint64_t)*a.seed_dev : 0ull);
@@ -53,6 +54,7 @@ __global__ __launch_bounds__(256) void k_head(HeadArgs a) {
   const float inv_keep = a.keep > 0.f ? 1.f / a.keep : 0.f;
   const uint32_t thr = a.keep >= 1.f ? 0xffffffffu : (uint32_t)(a.keep * 4294967296.0);
   const bool drop = a.train && a.keep < 1.f;
+  for (int e = tid; e < kHH * kHF; e += 256) W1s[e / kHF][e % kHF] = w1[e];  // rows are not 16-B aligned
   // train mode processes the whole batch in one chunk (B <= 32 asserted on the host)
   for (int b0 = 0; b0 < a.B; b0 += kHMaxB) {
     const int nb = min(kHMaxB, a.B - b0);
@@ -69,8 +71,8 @@ __global__ __launch_bounds__(256) void k_head(HeadArgs a) {
     for (int e = tid; e < nb * kHH; e += 256) {
       const int b = e / kHH, o = e - b * kHH;
       float z = b1[o];
-      const float* wr = w1 + (int64_t)o * kHF;
-      for (int f = 0; f < kHF; ++f) z = fmaf(wr[f], F[b][f], z);
+#pragma unroll 8
+      for (int f = 0; f < kHF; ++f) z = fmaf(W1s[o][f], F[b][f], z);
       Z1[b][o] = z;
       float h = fmaxf(z, 0.f);
       if (drop) h = (hash4(seed ^ 0x5bd1e995ull, cid, b0 + b, o) < thr) ? h * inv_keep : 0.f;
@@ -133,7 +135,8 @@ __global__ __launch_bounds__(256) void k_head(HeadArgs a) {
   for (int e = tid; e < nb * kHF; e += 256) {
     const int b = e / kHF, f = e - b * kHF;
     float s = 0.f;
-    for (int o = 0; o < kHH; ++o) s = fmaf(Z1[b][o], w1[(int64_t)o * kHF + f], s);
+#pragma unroll 8
+    for (int o = 0; o < kHH; ++o) s = fmaf(Z1[b][o], W1s[o][f], s);
     if (drop) s = (hash4(seed, cid, b, f) < thr) ? s * inv_keep : 0.f;
     const int c = f >> 1, h = f & 1;
     a.dp5[(((int64_t)g * a.B + b) * 2 + h) * 128 + c] = f32_to_bf16(s);

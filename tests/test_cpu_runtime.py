@@ -1,5 +1,7 @@
 """CPU tests of the native host runtime: the C++ NIDTVOL1 volume reader (``csrc/runtime/volume_io.cpp``) and
 its Python pipeline / ABCD-loader integration."""
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -86,3 +88,24 @@ def test_abcd_loader_reads_volume_file_by_site(tmp_path):
     xv, yv = store.fetch(xb)
     assert xv.shape == (len(xb), 1, 5, 6, 5)
     assert np.array_equal(np.sort(yv.numpy()), np.sort(y[np.sort(xb.numpy().astype(int))]))
+
+
+@pytest.mark.parametrize("san", ["thread", "address,undefined"])
+def test_volume_reader_sanitizer_stress(san, tmp_path):
+    """Race detection for the native runtime: the reader core (worker pool, ticket registry, completion
+    signalling, destructor draining queued gathers) under ThreadSanitizer and AddressSanitizer+UBSan, host only."""
+    import shutil
+    import subprocess
+    cxx = shutil.which("g++")
+    if cxx is None:
+        pytest.skip("no host C++ compiler")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = str(tmp_path / "stress")
+    cmd = [cxx, "-std=c++17", "-O1", "-g", "-pthread", "-fsanitize=" + san, "-fno-sanitize-recover=all",
+           "-fno-omit-frame-pointer", os.path.join(root, "csrc/runtime/tests/volume_io_stress.cpp"), "-o", exe]
+    b = subprocess.run(cmd, capture_output=True, text=True)
+    if b.returncode != 0 and "sanitize" in b.stderr:
+        pytest.skip("sanitizer runtime unavailable: " + b.stderr[-200:])
+    assert b.returncode == 0, b.stderr[-2000:]
+    r = subprocess.run([exe, str(tmp_path), "4", "25"], capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0 and "volume_io_stress ok" in r.stdout, (r.stdout + r.stderr)[-3000:]

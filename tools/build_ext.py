@@ -92,7 +92,8 @@ def build_runtime(force=False, verbose=True):
         src = os.path.join(rdir, f)
         out = runtime_name("_nidt_" + f[:-4].split("_")[-1])
         outs.append(out)
-        if not force and os.path.exists(out) and os.path.getmtime(out) >= os.path.getmtime(src):
+        deps = [src] + [os.path.join(rdir, h) for h in os.listdir(rdir) if h.endswith(".h")]
+        if not force and os.path.exists(out) and os.path.getmtime(out) >= max(map(os.path.getmtime, deps)):
             continue
         cmd = [cxx, "-O3", "-std=c++17", "-shared", "-fPIC", "-pthread", "-Wall", "-Wno-unused-result"] + \
             _includes()[:2] + [src, "-o", out]
