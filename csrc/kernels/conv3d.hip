@@ -19,6 +19,9 @@
 //                  [Cout][Cin][3][3][3] layout straight into the flat per-client gradient rows.
 //  * k_pack_conv_w — fp32 flat master weights -> bf16 [G][Cout][27][Cin] (+ flipped/transposed copy
 //                  for dgrad), scaled by an optional factor.
+#include <cmath>
+#include <cstdlib>
+
 #include "common.h"
 
 namespace nidt {
@@ -681,14 +684,40 @@ __global__ __launch_bounds__(256) void k_wgrad_reduce(const float* __restrict__ 
   }
 }
 
+// Split-K factor for the wgrad: blocks are equally long (chunk positions each), so the run time is
+// waves x block time with waves = ceil(blocks / slots), slots = 256 CUs x 2 resident blocks (80 KB LDS each),
+// plus the fp32 slab traffic (ns x G x Cout x K, written once and read once by k_wgrad_reduce).  The model
+// (one 64-position step ~1.28 us per block slot, ~12 steps of prologue/epilogue, ~5 TB/s slab traffic) picks the
+// ns with the smallest estimate; ties go to the smaller ns.  NIDT_WG_NSPLIT_LEGACY=1 restores the old rule
+// (ceil(2048 / tiles), capped) for A/B measurements.
 int conv3d_wgrad_nsplit(int G, int B, int D, int H, int W, int Cin, int Cout, int pad) {
   const int Mg = B * (D + 2 * pad - 2) * (H + 2 * pad - 2) * (W + 2 * pad - 2);
   const int K = 27 * Cin;
   const int base = G * (Cout / kWgCO) * ceil_div(K, kWgKC);
-  int ns = ceil_div(2048, base);
-  // keep >= 8 (small K) / 16 (K >= 3000: large fp32 split-K slabs to write and re-read) 64-position steps per block
-  const int maxns = max(1, Mg / (K >= 3000 ? 1024 : 512));
-  return max(1, min(ns, maxns));
+  static const bool legacy = [] {
+    const char* e = getenv("NIDT_WG_NSPLIT_LEGACY");
+    return e && e[0] == '1';
+  }();
+  if (legacy) {
+    const int ns = ceil_div(2048, base);
+    const int maxns = max(1, Mg / (K >= 3000 ? 1024 : 512));
+    return max(1, min(ns, maxns));
+  }
+  constexpr double kSlots = 512.0, kStepUs = 1.28, kOverheadSteps = 12.0, kBytesPerUs = 5.0e6;
+  const double slab_bytes = 8.0 * G * Cout * K;  // fp32 write + read per split
+  const int maxns = max(1, min(64, Mg / 512));  // keep >= 8 steps per block
+  int best = 1;
+  double best_t = 1e30;
+  for (int ns = 1; ns <= maxns; ++ns) {
+    const double waves = ceil((double)base * ns / kSlots);
+    const double steps = ceil(ceil((double)Mg / ns) / 64.0);
+    const double t = waves * (steps + kOverheadSteps) * kStepUs + ns * slab_bytes / kBytesPerUs;
+    if (t < best_t * 0.995) {
+      best_t = t;
+      best = ns;
+    }
+  }
+  return best;
 }
 
 // ------------------------------------------------------------------------------------------------
