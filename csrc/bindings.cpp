@@ -9,7 +9,7 @@ namespace nidt {
 int64_t clip_sgd_mask_workspace(int64_t C, int64_t P);
 void clip_sgd_mask(uintptr_t w, uintptr_t g, uintptr_t buf, uintptr_t mask, uintptr_t part, uintptr_t coef_out,
                    uintptr_t wbf, int64_t C, int64_t P, int64_t stride, float lr, float wd, float mom, int first,
-                   float max_norm, uintptr_t lr_dev, uintptr_t stream);
+                   float max_norm, uintptr_t lr_dev, int keep_grad, uintptr_t stream);
 void weighted_rows_sum(uintptr_t rows, uintptr_t wts, int64_t C, int64_t P, int64_t stride, float beta, uintptr_t out,
                        uintptr_t stream);
 void broadcast_row(uintptr_t src, int64_t P, int64_t stride, int64_t C, uintptr_t dst, uintptr_t stream);

@@ -43,7 +43,7 @@ __global__ __launch_bounds__(kOptThreads) void k_clip_sgd_mask(
     float* __restrict__ w, float* __restrict__ g, float* __restrict__ buf, const float* __restrict__ mask,
     const float* __restrict__ part, int nblk, int64_t P, int64_t stride, int64_t chunk, float lr, float wd,
     float mom, int first, float max_norm, float* __restrict__ coef_out, uint16_t* __restrict__ wbf,
-    const float* __restrict__ lr_dev) {
+    const float* __restrict__ lr_dev, int keep_grad) {
   __shared__ float red[kOptThreads / 64];
   const int c = blockIdx.y;
   if (lr_dev) lr = *lr_dev;  // hipGraph replays: the round's learning rate lives on the device
@@ -87,7 +87,7 @@ __global__ __launch_bounds__(kOptThreads) void k_clip_sgd_mask(
       ww[j] = fmaf(-lr, d, ww[j]);
       if (HAS_MASK) ww[j] *= mm[j];
     }
-    *reinterpret_cast<float4*>(gr + i) = make_float4(gg[0], gg[1], gg[2], gg[3]);
+    if (keep_grad) *reinterpret_cast<float4*>(gr + i) = make_float4(gg[0], gg[1], gg[2], gg[3]);
     *reinterpret_cast<float4*>(wr + i) = make_float4(ww[0], ww[1], ww[2], ww[3]);
     if (HAS_MOM) *reinterpret_cast<float4*>(br + i) = make_float4(bb[0], bb[1], bb[2], bb[3]);
     if (EMIT_BF16) {
@@ -98,7 +98,7 @@ __global__ __launch_bounds__(kOptThreads) void k_clip_sgd_mask(
   }
   for (int64_t i = e4 + threadIdx.x; i < e; i += kOptThreads) {
     float gj = gr[i] * coef;
-    gr[i] = gj;
+    if (keep_grad) gr[i] = gj;
     float d = fmaf(wd, wr[i], gj);
     if (HAS_MOM) {
       float b = first ? d : fmaf(mom, br[i], d);
@@ -132,7 +132,7 @@ int64_t clip_sgd_mask_workspace(int64_t C, int64_t P) {
 
 void clip_sgd_mask(uintptr_t w, uintptr_t g, uintptr_t buf, uintptr_t mask, uintptr_t part, uintptr_t coef_out,
                    uintptr_t wbf, int64_t C, int64_t P, int64_t stride, float lr, float wd, float mom, int first,
-                   float max_norm, uintptr_t lr_dev, uintptr_t stream) {
+                   float max_norm, uintptr_t lr_dev, int keep_grad, uintptr_t stream) {
   NIDT_REQUIRE(stride % 4 == 0 && stride >= P, "stride must be >= P and a multiple of 4");
   NIDT_REQUIRE((w & 15) == 0 && (g & 15) == 0 && (buf & 15) == 0 && (mask & 15) == 0 && (wbf & 7) == 0,
                "buffers must be 16-byte aligned");
@@ -146,7 +146,8 @@ void clip_sgd_mask(uintptr_t w, uintptr_t g, uintptr_t buf, uintptr_t mask, uint
 #define NIDT_LAUNCH(M, MO, B)                                                                                   \
   hipLaunchKernelGGL((k_clip_sgd_mask<M, MO, B>), grid, dim3(kOptThreads), 0, st, ptr<float>(w), ptr<float>(g),      \
                      ptr<float>(buf), ptr<const float>(mask), ptr<const float>(part), nblk, P, stride, chunk, lr, wd,   \
-                     mom, first, max_norm, ptr<float>(coef_out), ptr<uint16_t>(wbf), ptr<const float>(lr_dev))
+                     mom, first, max_norm, ptr<float>(coef_out), ptr<uint16_t>(wbf), ptr<const float>(lr_dev),  \
+                     keep_grad)
   if (hm && hmo && hb) NIDT_LAUNCH(true, true, true);
   else if (hm && hmo && !hb) NIDT_LAUNCH(true, true, false);
   else if (hm && !hmo && hb) NIDT_LAUNCH(true, false, true);

@@ -102,7 +102,9 @@ class HipEngine:
         return self.net.eval_logits(theta, bufs, self.x8, idx, G, B)
 
     # fused optimizer: clip(10) -> SGD(wd, momentum) -> w *= mask (one HIP pass per row)
-    def opt_step(self, theta, grads, mom_buf, mask, lr, wd, momentum, first, max_norm, lr_dev=None):
+    def opt_step(self, theta, grads, mom_buf, mask, lr, wd, momentum, first, max_norm, lr_dev=None, keep_grad=False):
+        """Fused clip + SGD (+ momentum) + mask.  The clipped gradient is only written back with ``keep_grad`` (the
+        local step overwrites ``grads`` next time; skipping the write saves 4 B/param of HBM traffic)."""
         G, P = theta.shape
         ws = self.m.clip_sgd_mask_workspace(G, P)
         if not hasattr(self, "_optws") or self._optws.numel() < ws:
@@ -110,7 +112,8 @@ class HipEngine:
         self.m.clip_sgd_mask(theta.data_ptr(), grads.data_ptr(), mom_buf.data_ptr() if mom_buf is not None else 0,
                              mask.data_ptr() if mask is not None else 0, self._optws.data_ptr(), 0, 0, G, P,
                              theta.stride(0), float(lr), float(wd), float(momentum), int(first), float(max_norm),
-                             lr_dev.data_ptr() if lr_dev is not None else 0, torch.cuda.current_stream().cuda_stream)
+                             lr_dev.data_ptr() if lr_dev is not None else 0, int(keep_grad),
+                             torch.cuda.current_stream().cuda_stream)
 
     def saliency_acc(self, theta, grads, score, alpha):
         G, P = theta.shape

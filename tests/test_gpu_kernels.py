@@ -392,10 +392,22 @@ def test_clip_sgd_mask_matches_reference():
     from neuroimagedisttraining_amd.ops.reference import clip_sgd_mask_reference
     clip_sgd_mask_reference(ref, grad.clone(), mask, 0.01, 5e-4)
     ws = torch.empty(m.clip_sgd_mask_workspace(G, P), device=DEV)
+    g0 = grad.clone()
+    th0 = theta.clone()
     m.clip_sgd_mask(theta.data_ptr(), grad.data_ptr(), 0, mask.data_ptr(), ws.data_ptr(), 0, 0, G, P, theta.stride(0),
-                    0.01, 5e-4, 0.0, 1, 10.0, 0, _st())
+                    0.01, 5e-4, 0.0, 1, 10.0, 0, 1, _st())
     torch.cuda.synchronize()
     assert _relerr(theta, ref) < 1e-6
+    n1 = float(g0[1, :P].double().norm())
+    assert _relerr(grad[1, :P], g0[1, :P] * (10.0 / (n1 + 1e-6))) < 1e-5  # keep_grad: clipped gradient written back
+    # keep_grad = 0: identical weights, gradient untouched
+    grad2 = padded_rows(G, P, DEV)  # same row stride as theta (the kernel takes one stride)
+    grad2.copy_(g0)
+    theta.copy_(th0)
+    m.clip_sgd_mask(theta.data_ptr(), grad2.data_ptr(), 0, mask.data_ptr(), ws.data_ptr(), 0, 0, G, P, theta.stride(0),
+                    0.01, 5e-4, 0.0, 1, 10.0, 0, 0, _st())
+    torch.cuda.synchronize()
+    assert _relerr(theta, ref) < 1e-6 and torch.equal(grad2, g0)
 
 
 def test_radix_select_matches_topk():
