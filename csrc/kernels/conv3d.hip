@@ -317,7 +317,7 @@ __device__ __forceinline__ void blds16(i32x4_t rsrc, int voffset, uint16_t* lds_
 }
 
 template <int BCO, int WM, int WN, int NST, bool BIAS, bool STATS>
-__global__ __launch_bounds__(64 * WM * WN, (NST == 2 ? 8 : 4) / (WM * WN)) void k_conv_fwd_dma(ConvFwdArgs a, int nCO) {
+__global__ __launch_bounds__(64 * WM * WN, ((NST == 2 ? 8 : 4) / (WM * WN)) > 0 ? (NST == 2 ? 8 : 4) / (WM * WN) : 1) void k_conv_fwd_dma(ConvFwdArgs a, int nCO) {
   // waves: WM (co) x WN (positions); each wave owns (BCO/WM) co x 64 positions
   constexpr int NW = WM * WN, BP = 64 * WN, BK = 64;
   constexpr int WCO = BCO / WM, WP = 64;
@@ -392,12 +392,16 @@ __global__ __launch_bounds__(64 * WM * WN, (NST == 2 ? 8 : 4) / (WM * WN)) void 
     for (int j = 0; j < TP; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int fr = lane & 15, fq = lane >> 4;
+  // prologue: stages 0 .. NST-2 in flight, wait for stage 0 only
   DMA_ISSUE(0, 0)
-  if (NST == 3 && nks > 1) {
-    DMA_ISSUE(1, 1)
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NI) : "memory");
-  } else {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int s_ = 1; s_ < NST - 1; ++s_)
+    if (s_ < nks) DMA_ISSUE(s_, s_)
+  {
+    const int younger = min(NST - 2, nks - 1);
+    if (younger >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NI) : "memory");
+    else if (younger == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NI) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   __builtin_amdgcn_s_barrier();
   int cur = 0;
@@ -429,8 +433,12 @@ __global__ __launch_bounds__(64 * WM * WN, (NST == 2 ? 8 : 4) / (WM * WN)) void 
     }
     // retire stage ks+1 (this wave's own glds), keep the younger stages in flight, then one barrier so
     // every wave's part of stage ks+1 has landed and every wave is done reading stage ks.
-    if (NST == 3 && ks + 2 < nks) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(NI) : "memory");
-    else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    {
+      const int younger = min(NST - 2, nks - ks - 2);  // stages issued after ks+1 that may stay in flight
+      if (younger >= 2) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(2 * NI) : "memory");
+      else if (younger == 1) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(NI) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    }
     __builtin_amdgcn_s_barrier();
     cur = cur + 1 == NST ? 0 : cur + 1;
   }
@@ -474,8 +482,18 @@ void conv3d_fwd(uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t xs, uintptr_
     const int64_t nwg = (int64_t)a.nPB * nCO * G;
     NIDT_REQUIRE(nwg < (1ll << 31), "conv3d_fwd: grid too large");
     dim3 g1((unsigned)nwg);
-#define NIDT_DMA(BC, WM, WN, BI, ST) \
-    hipLaunchKernelGGL((k_conv_fwd_dma<BC, WM, WN, 2, BI, ST>), g1, dim3(64 * WM * WN), 0, s, a, nCO)
+    // small grids (64-position blocks: conv3-5 at 8 clients per GPU) run at ~1 wave per SIMD: a third LDS stage
+    // keeps two k-steps of LDS-DMA in flight to cover the load latency the missing waves cannot hide.
+    static const int nst_env = [] {
+      const char* e = getenv("NIDT_FWD_NST");
+      return e ? atoi(e) : 0;
+    }();
+    const int nst = nst_env ? nst_env : (bp == 64 ? 3 : 2);  // measured: 3 stages only pay with 64-position blocks
+#define NIDT_DMA(BC, WM, WN, BI, ST)                                                                        \
+    do {                                                                                                    \
+      if (nst == 3) hipLaunchKernelGGL((k_conv_fwd_dma<BC, WM, WN, 3, BI, ST>), g1, dim3(64 * WM * WN), 0, s, a, nCO); \
+      else hipLaunchKernelGGL((k_conv_fwd_dma<BC, WM, WN, 2, BI, ST>), g1, dim3(64 * WM * WN), 0, s, a, nCO); \
+    } while (0)
 #define NIDT_DMA_WN(WN)                                                                                     \
     if (bco == 128) {                                                                                       \
       if (st) NIDT_DMA(128, 2, WN, true, true); else if (hb) NIDT_DMA(128, 2, WN, true, false);             \
@@ -508,7 +526,11 @@ int conv3d_fwd_bp(int Cin, int Cout, int xf, int G, int Mg) {
   if (xf || Cin % 64 != 0) return kFwdBP;
   const int bco = (Cout % 128 == 0) ? 128 : 64;
   const int64_t nwg256 = (int64_t)ceil_div(Mg, 256) * (Cout / bco) * G;
-  return nwg256 < 256 ? 64 : 256;  // fewer blocks than CUs: 64-position blocks (measured: only then a win)
+  static const int thresh = [] {
+    const char* e = getenv("NIDT_FWD_BP_THRESH");
+    return e ? atoi(e) : 256;
+  }();
+  return nwg256 < thresh ? 64 : 256;  // fewer blocks than CUs: 64-position blocks (measured: only then a win)
 }
 
 int conv3d_fwd_nblocks(int B, int D, int H, int W, int pad, int bp) {

@@ -35,8 +35,9 @@ struct HeadArgs {
 };
 
 constexpr int kHF = 256, kHH = 64, kHMaxB = 32;
+constexpr int kHT = 1024;  // 16 waves per client: the head is latency-bound (one block per client)
 
-__global__ __launch_bounds__(256) void k_head(HeadArgs a) {
+__global__ __launch_bounds__(kHT) void k_head(HeadArgs a) {
   __shared__ float F[kHMaxB][kHF + 1];
   __shared__ float Z1[kHMaxB][kHH + 1];
   __shared__ float Hd[kHMaxB][kHH + 1];
@@ -54,12 +55,12 @@ __global__ __launch_bounds__(256) void k_head(HeadArgs a) {
   const float inv_keep = a.keep > 0.f ? 1.f / a.keep : 0.f;
   const uint32_t thr = a.keep >= 1.f ? 0xffffffffu : (uint32_t)(a.keep * 4294967296.0);
   const bool drop = a.train && a.keep < 1.f;
-  for (int e = tid; e < kHH * kHF; e += 256) W1s[e / kHF][e % kHF] = w1[e];  // rows are not 16-B aligned
+  for (int e = tid; e < kHH * kHF; e += kHT) W1s[e / kHF][e % kHF] = w1[e];  // rows are not 16-B aligned
   // train mode processes the whole batch in one chunk (B <= 32 asserted on the host)
   for (int b0 = 0; b0 < a.B; b0 += kHMaxB) {
     const int nb = min(kHMaxB, a.B - b0);
     __syncthreads();
-    for (int e = tid; e < nb * kHF; e += 256) {
+    for (int e = tid; e < nb * kHF; e += kHT) {
       const int b = e / kHF, f = e - b * kHF;
       const int c = f >> 1, h = f & 1;
       const int n = g * a.B + b0 + b;
@@ -68,7 +69,7 @@ __global__ __launch_bounds__(256) void k_head(HeadArgs a) {
       F[b][f] = v;
     }
     __syncthreads();
-    for (int e = tid; e < nb * kHH; e += 256) {
+    for (int e = tid; e < nb * kHH; e += kHT) {
       const int b = e / kHH, o = e - b * kHH;
       float z = b1[o];
 #pragma unroll 8
@@ -114,7 +115,7 @@ __global__ __launch_bounds__(256) void k_head(HeadArgs a) {
   }
   // dz1 (overwrite Z1)
   __syncthreads();
-  for (int e = tid; e < nb * kHH; e += 256) {
+  for (int e = tid; e < nb * kHH; e += kHT) {
     const int b = e / kHH, o = e - b * kHH;
     float d = DZ2[b] * w2[o];
     if (drop) d = (hash4(seed ^ 0x5bd1e995ull, cid, b, o) < thr) ? d * inv_keep : 0.f;
@@ -126,13 +127,13 @@ __global__ __launch_bounds__(256) void k_head(HeadArgs a) {
     for (int b = 0; b < nb; ++b) s += Z1[b][tid];
     gr[a.off_b1 + tid] = s;
   }
-  for (int e = tid; e < kHH * kHF; e += 256) {
+  for (int e = tid; e < kHH * kHF; e += kHT) {
     const int o = e / kHF, f = e - o * kHF;
     float s = 0.f;
     for (int b = 0; b < nb; ++b) s = fmaf(Z1[b][o], F[b][f], s);
     gr[a.off_w1 + e] = s;
   }
-  for (int e = tid; e < nb * kHF; e += 256) {
+  for (int e = tid; e < nb * kHF; e += kHT) {
     const int b = e / kHF, f = e - b * kHF;
     float s = 0.f;
 #pragma unroll 8
@@ -150,7 +151,7 @@ void head(uintptr_t p5, uintptr_t theta, int64_t ldt, int64_t off_w1, int64_t of
   HeadArgs a{ptr<const uint16_t>(p5), ptr<const float>(theta), ldt, off_w1, off_b1, off_w2, off_b2,
              ptr<const float>(y), ptr<float>(logits), ptr<float>(loss), ptr<float>(grad), ldg, ptr<uint16_t>(dp5),
              B, 1, train, keep, seed, ptr<const int>(cids), ptr<const int64_t>(seed_dev)};
-  hipLaunchKernelGGL(k_head, dim3(G), dim3(256), 0, as_stream(stream), a);
+  hipLaunchKernelGGL(k_head, dim3(G), dim3(kHT), 0, as_stream(stream), a);
   NIDT_CHECK(hipGetLastError());
 }
 
