@@ -1,2 +1,2 @@
 """Compat shim: reference import path ``fedml_api/standalone/turboaggregate/TA_client.py``."""
-from neuroimagedisttraining_amd.algorithms.common import Client as TA_Client  # noqa: F401
+from neuroimagedisttraining_amd.algorithms.turboaggregate import TA_Client  # noqa: F401

@@ -202,3 +202,32 @@ class TurboAggregateTrainer:
                 m_ik = r if i < k else (-r) % self.p
                 s = (s - m_ik) % self.p
         return dequantize(s, self.scale, self.p)
+
+
+class TA_Client:  # noqa: N801 (reference name)
+    """Turbo-Aggregate participant (reference ``turboaggregate/TA_client.py:8-26``): local data handles plus the
+    ``isdrop`` flag the protocol uses to simulate a client that drops out after uploading nothing; the
+    server side recovers the masks of dropped clients in :meth:`TurboAggregateTrainer.server_aggregate`."""
+
+    def __init__(self, local_training_data, local_test_data, local_sample_number, args, device, client_idx=0):
+        self.local_training_data = local_training_data
+        self.local_test_data = local_test_data
+        self.local_sample_number = local_sample_number
+        self.args, self.device, self.client_idx = args, device, client_idx
+        import torch.nn as nn
+        self.criterion = nn.CrossEntropyLoss()
+        self.isdrop = False
+
+    def set_dropout(self, isdrop):
+        self.isdrop = bool(isdrop)
+
+    def get_sample_number(self):
+        return self.local_sample_number
+
+
+def secure_round(trainer, clients, vectors, weights):
+    """One Turbo-Aggregate round over ``TA_Client`` objects: every client that is not marked dropped uploads its
+    masked, weighted update; the server removes the dropped clients' masks and returns the weighted sum."""
+    uploads = {i: trainer.client_upload(i, vectors[i], weights[i]) for i, c in enumerate(clients) if not c.isdrop}
+    dropped = [i for i, c in enumerate(clients) if c.isdrop]
+    return trainer.server_aggregate(uploads, dropped=dropped)

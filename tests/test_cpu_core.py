@@ -191,6 +191,12 @@ def test_secure_aggregation_equals_fedavg_with_dropout():
     agg2 = tr.server_aggregate(ups, dropped=[2])
     ref2 = sum(wts[i] * vecs[i] for i in range(n) if i != 2)
     assert np.allclose(agg2, ref2, atol=1e-3)
+    # reference-style clients with the isdrop flag (TA_client.py:20-26)
+    from fedml_api.standalone.turboaggregate.TA_client import TA_Client
+    clients = [TA_Client(None, None, 10, None, "cpu", i) for i in range(n)]
+    clients[4].set_dropout(True)
+    agg3 = TA.secure_round(tr, clients, vecs, wts)
+    assert np.allclose(agg3, sum(wts[i] * vecs[i] for i in range(4)), atol=1e-3)
 
 
 def test_sparse_mask_ops():
