@@ -514,10 +514,12 @@ constexpr int kWgHalo = 5 * kWgZS;               // voxels per halo buffer
 constexpr int kWgMeta = kWgRows * kPW * kC1;     // metadata records per stage
 __device__ __forceinline__ int bid_slab(int n_pd, int q, int nq) { return n_pd * nq + q; }  // slab of (n, pd, q)
 
-// Reduce slabs per client and apply the closed form.  grid (64 c, G), block 256: the B*19 slabs are split
-// over the 4 waves (lane = k, k + 64; 4 independent loads in flight per lane instead of one dependent chain),
-// merged through LDS in a fixed order (deterministic), then threads 0..127 (k) apply the closed form.
-__global__ __launch_bounds__(256) void k_conv1_wgrad_fin(const float* __restrict__ part, int B,
+// Reduce slabs per client and apply the closed form.  grid (64 c, G), block 1024: the B*19*nq slabs are split
+// over the 16 waves (lane = k, k + 64; 4 independent loads in flight per lane; 16 waves per block because at few
+// clients per GPU there are only 64*G blocks to cover the L2/HBM latency), merged through LDS in a fixed order
+// (deterministic), then threads 0..127 (k) apply the closed form.
+constexpr int kFinW = 16;
+__global__ __launch_bounds__(64 * kFinW) void k_conv1_wgrad_fin(const float* __restrict__ part, int B,
                                                          const float* __restrict__ w125, const float* __restrict__ mu,
                                                          const float* __restrict__ covw,
                                                          const float* __restrict__ invstd, const float* theta,
@@ -526,7 +528,7 @@ __global__ __launch_bounds__(256) void k_conv1_wgrad_fin(const float* __restrict
                                                          int64_t goff_b, float wscale) {
   __shared__ double red[2];
   __shared__ double sD, sdg;
-  __shared__ double wpart[4][128];
+  __shared__ double wpart[kFinW][128];
   const int c = blockIdx.x, g = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int nslab = B * kPD;
   {
@@ -535,18 +537,18 @@ __global__ __launch_bounds__(256) void k_conv1_wgrad_fin(const float* __restrict
     double a0 = 0, a1 = 0;
     const bool hi = lane + 64 < 126;
     int sl = wid;
-    for (; sl + 12 < nslab; sl += 16) {
+    for (; sl + 3 * kFinW < nslab; sl += 4 * kFinW) {
       float v0[4], v1[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        const float* o = base + (int64_t)(sl + 4 * u) * sst;
+        const float* o = base + (int64_t)(sl + kFinW * u) * sst;
         v0[u] = o[lane];
         v1[u] = hi ? o[lane + 64] : 0.f;
       }
 #pragma unroll
       for (int u = 0; u < 4; ++u) { a0 += v0[u]; a1 += v1[u]; }
     }
-    for (; sl < nslab; sl += 4) {
+    for (; sl < nslab; sl += kFinW) {
       const float* o = base + (int64_t)sl * sst;
       a0 += o[lane];
       if (hi) a1 += o[lane + 64];
@@ -555,10 +557,21 @@ __global__ __launch_bounds__(256) void k_conv1_wgrad_fin(const float* __restrict
     wpart[wid][lane + 64] = a1;
   }
   __syncthreads();
+  if (tid < 128) {  // fixed-order tree over the 16 wave partials
+    double t[kFinW];
+#pragma unroll
+    for (int w = 0; w < kFinW; ++w) t[w] = wpart[w][tid];
+#pragma unroll
+    for (int h = kFinW / 2; h > 0; h >>= 1)
+#pragma unroll
+      for (int w = 0; w < h; ++w) t[w] += t[w + h];
+    wpart[0][tid] = t[0];
+  }
+  __syncthreads();
   if (tid >= 128) return;
   const int k = tid;
-  double S = k < 125 ? ((wpart[0][k] + wpart[1][k]) + (wpart[2][k] + wpart[3][k])) : 0.0;
-  if (k == 0) sD = (wpart[0][125] + wpart[1][125]) + (wpart[2][125] + wpart[3][125]);
+  double S = k < 125 ? wpart[0][k] : 0.0;
+  if (k == 0) sD = wpart[0][125];
   __syncthreads();
   double D = sD;
   const int i = g * kC1 + c;
@@ -732,7 +745,7 @@ void conv1_wgrad(uintptr_t x8, uintptr_t idx, uintptr_t dp, uintptr_t pout, uint
   NIDT_CHECK(hipGetLastError());
   const int G = NB / B;
   // client g's slabs are contiguous: B samples x 19 pd x nq row ranges
-  hipLaunchKernelGGL(k_conv1_wgrad_fin, dim3(kC1, G), dim3(256), 0, s, ptr<const float>(part), B * nq,
+  hipLaunchKernelGGL(k_conv1_wgrad_fin, dim3(kC1, G), dim3(64 * kFinW), 0, s, ptr<const float>(part), B * nq,
                      ptr<const float>(w125), ptr<const float>(mu), ptr<const float>(covw), ptr<const float>(invstd),
                      ptr<const float>(theta), ldt, off_g, ptr<float>(grad), ldg, goff_w, goff_bias, goff_g, goff_b,
                      wscale);
