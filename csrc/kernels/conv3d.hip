@@ -38,6 +38,9 @@ struct ConvFwdArgs {
   int B, D, H, W, Cin, Do, Ho, Wo, Cout, pad;
   int Mg;               // output positions per client
   int nPB;              // position blocks per client (grid.x)
+  int ksplit = 1;       // split-K factor (LDS-DMA path): > 1 writes fp32 partials, k_fwd_splitk_fin finishes
+  int G = 0;            // clients (split-K partial indexing)
+  float* part = nullptr;  // [ksplit, G, Mg, Cout] fp32 partial sums
 };
 
 constexpr int kFwdBP = 128;  // positions per block
@@ -333,12 +336,14 @@ __global__ __launch_bounds__(64 * WM * WN, ((NST == 2 ? 8 : 4) / (WM * WN)) > 0 
   const int nwg = gridDim.x;
   const int id = xcd_remap(blockIdx.x, nwg);
   const int cot = id % nCO, rest = id / nCO;
-  const int pb = rest % a.nPB, g = rest / a.nPB;
+  const int pb = rest % a.nPB, rest2 = rest / a.nPB;
+  const int sp = rest2 % a.ksplit, g = rest2 / a.ksplit;
   const int co0 = cot * BCO;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // uniform: LDS destinations stay in SGPRs
   const int wco = wid / WN, wp = wid % WN;
   const int Cin = a.Cin, nck = Cin / BK, nks = 27 * nck;
+  const int ks0 = nks * sp / a.ksplit, ks1 = nks * (sp + 1) / a.ksplit;  // this split's k-steps
   const int lrow = lane >> 3, slot = lane & 7;
 
   // ---- per-thread B rows: one per LDS-DMA instruction, fixed over the k loop (byte offsets in the client's input;
@@ -393,20 +398,20 @@ __global__ __launch_bounds__(64 * WM * WN, ((NST == 2 ? 8 : 4) / (WM * WN)) > 0 
 
   const int fr = lane & 15, fq = lane >> 4;
   // prologue: stages 0 .. NST-2 in flight, wait for stage 0 only
-  DMA_ISSUE(0, 0)
+  DMA_ISSUE(ks0, 0)
 #pragma unroll
   for (int s_ = 1; s_ < NST - 1; ++s_)
-    if (s_ < nks) DMA_ISSUE(s_, s_)
+    if (ks0 + s_ < ks1) DMA_ISSUE(ks0 + s_, s_)
   {
-    const int younger = min(NST - 2, nks - 1);
+    const int younger = min(NST - 2, ks1 - ks0 - 1);
     if (younger >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NI) : "memory");
     else if (younger == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NI) : "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   __builtin_amdgcn_s_barrier();
   int cur = 0;
-  for (int ks = 0; ks < nks; ++ks) {
-    if (ks + NST - 1 < nks) {
+  for (int ks = ks0; ks < ks1; ++ks) {
+    if (ks + NST - 1 < ks1) {
       int nb = cur + NST - 1;
       nb = nb >= NST ? nb - NST : nb;
       DMA_ISSUE(ks + NST - 1, nb)
@@ -434,7 +439,7 @@ __global__ __launch_bounds__(64 * WM * WN, ((NST == 2 ? 8 : 4) / (WM * WN)) > 0 
     // retire stage ks+1 (this wave's own glds), keep the younger stages in flight, then one barrier so
     // every wave's part of stage ks+1 has landed and every wave is done reading stage ks.
     {
-      const int younger = min(NST - 2, nks - ks - 2);  // stages issued after ks+1 that may stay in flight
+      const int younger = min(NST - 2, ks1 - ks - 2);  // stages issued after ks+1 that may stay in flight
       if (younger >= 2) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(2 * NI) : "memory");
       else if (younger == 1) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(NI) : "memory");
       else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
@@ -443,15 +448,111 @@ __global__ __launch_bounds__(64 * WM * WN, ((NST == 2 ? 8 : 4) / (WM * WN)) > 0 
     cur = cur + 1 == NST ? 0 : cur + 1;
   }
 #undef DMA_ISSUE
+  if (a.ksplit > 1) {  // raw fp32 partials; bias, bf16 output and statistics come from k_fwd_splitk_fin
+    const int posw = pb * BP + wp * WP + fr;
+#pragma unroll
+    for (int j = 0; j < TP; ++j) {
+      const int m = posw + j * 16;
+      if (m < a.Mg) {
+        float* pp = a.part + (((int64_t)sp * a.G + g) * a.Mg + m) * a.Cout + co0 +
+                    wco * WCO + 4 * fq;
+#pragma unroll
+        for (int i = 0; i < TCO; ++i)
+          *reinterpret_cast<float4*>(pp + i * 16) = make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
+      }
+    }
+    return;
+  }
   __syncthreads();
   float* red = reinterpret_cast<float*>(smem);
   conv_fwd_epilogue<BCO, BP, WM, WN, BIAS, STATS, TCO, TP>(a, acc, red, g, pb, co0, wco, wp, fr, fq, tid);
 }
 
+// Finish a split-K forward: y = bf16(sum of the partials + bias) and the same per-block BN statistics as the
+// fused epilogue (block mean and M2 per channel over the block's BP positions, fp32 values before rounding).
+// Block (pb, g), 1024 threads: lane -> channel c = lane + 64 u, wave -> positions m0 + wave + 16 v; the 16 wave
+// partial sums are combined in a fixed order (deterministic).
+constexpr int kFinPG = 16;      // position groups (waves)
+constexpr int kFinMaxCU = 4;    // Cout <= 256
+constexpr int kFinMaxPV = 16;   // positions per group (BP = 256)
+template <bool BIAS, bool STATS>
+__global__ __launch_bounds__(1024) void k_fwd_splitk_fin(const float* __restrict__ part, int ksplit,
+                                                         const float* __restrict__ bias, uint16_t* __restrict__ y,
+                                                         float* __restrict__ stats, int G, int Mg, int Cout, int BP,
+                                                         int nPB) {
+  __shared__ float red[kFinPG][256];
+  __shared__ float smean[256];
+  const int pb = blockIdx.x, g = blockIdx.y;
+  const int lane = threadIdx.x & 63, pg = threadIdx.x >> 6;
+  const int m0 = pb * BP, cnt = min(BP, Mg - m0);
+  const int ncu = Cout / 64;
+  const int64_t pst = (int64_t)G * Mg * Cout;
+  float v[kFinMaxCU][kFinMaxPV];
+  float s[kFinMaxCU];
+#pragma unroll
+  for (int u = 0; u < kFinMaxCU; ++u) {
+    s[u] = 0.f;
+    if (u >= ncu) continue;
+    const int c = lane + 64 * u;
+    const float bv = BIAS ? bias[(int64_t)g * Cout + c] : 0.f;
+#pragma unroll
+    for (int q = 0; q < kFinMaxPV; ++q) {
+      const int m = pg + kFinPG * q;
+      v[u][q] = 0.f;
+      if (m < cnt) {
+        const int64_t o = ((int64_t)g * Mg + m0 + m) * Cout + c;
+        float acc = 0.f;
+        for (int sp = 0; sp < ksplit; ++sp) acc += part[sp * pst + o];
+        const float t = acc + bv;
+        v[u][q] = t;
+        y[o] = f32_to_bf16(t);
+        s[u] += t;
+      }
+    }
+  }
+  if (!STATS) return;
+#pragma unroll
+  for (int u = 0; u < kFinMaxCU; ++u)
+    if (u < ncu) red[pg][lane + 64 * u] = s[u];
+  __syncthreads();
+  for (int c = threadIdx.x; c < Cout; c += 1024) {
+    float t = 0.f;
+    for (int q = 0; q < kFinPG; ++q) t += red[q][c];
+    smean[c] = t / (float)cnt;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < kFinMaxCU; ++u) {
+    if (u >= ncu) continue;
+    const float mu = smean[lane + 64 * u];
+    float q2 = 0.f;
+#pragma unroll
+    for (int q = 0; q < kFinMaxPV; ++q)
+      if (pg + kFinPG * q < cnt) {
+        const float d = v[u][q] - mu;
+        q2 = fmaf(d, d, q2);
+      }
+    s[u] = q2;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < kFinMaxCU; ++u)
+    if (u < ncu) red[pg][lane + 64 * u] = s[u];
+  __syncthreads();
+  for (int c = threadIdx.x; c < Cout; c += 1024) {
+    float t = 0.f;
+    for (int q = 0; q < kFinPG; ++q) t += red[q][c];
+    float* st = stats + (((int64_t)g * nPB + pb) * Cout + c) * 2;
+    st[0] = smean[c];
+    st[1] = t;
+  }
+}
+
 int conv3d_fwd_bp(int Cin, int Cout, int xf, int G, int Mg);
 
-void conv3d_fwd(uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t xs, uintptr_t xt, uintptr_t y, uintptr_t stats,
-                int G, int B, int D, int H, int W, int Cin, int Cout, int pad, uintptr_t stream) {
+static void conv3d_fwd_impl(uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t xs, uintptr_t xt, uintptr_t y,
+                            uintptr_t stats, int G, int B, int D, int H, int W, int Cin, int Cout, int pad,
+                            uintptr_t stream, int ksplit, uintptr_t part) {
   NIDT_REQUIRE(Cin % 32 == 0, "conv3d_fwd: Cin must be a multiple of 32");
   NIDT_REQUIRE((xs == 0 && Cin % 64 == 0) ? Cin <= kMaxCin : Cin <= 192,
                "conv3d_fwd: Cin <= 512 (LDS-DMA path: Cin % 64 == 0, no input transform), else <= 192");
@@ -467,6 +568,7 @@ void conv3d_fwd(uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t xs, uintptr_
   NIDT_REQUIRE(a.Do > 0 && a.Ho > 0 && a.Wo > 0, "conv3d_fwd: empty output");
   a.Mg = B * a.Do * a.Ho * a.Wo;
   a.nPB = ceil_div(a.Mg, kFwdBP);
+  a.G = G;
   const bool xf = xs != 0, hb = bias != 0, st = stats != 0;
   NIDT_REQUIRE(!st || hb, "conv3d_fwd: statistics require a bias");
   const int bco = (Cout % 128 == 0) ? 128 : 64;
@@ -479,7 +581,12 @@ void conv3d_fwd(uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t xs, uintptr_
     const int bp = conv3d_fwd_bp(Cin, Cout, 0, G, a.Mg);
     a.nPB = ceil_div(a.Mg, bp);
     const int nCO = Cout / bco;
-    const int64_t nwg = (int64_t)a.nPB * nCO * G;
+    if (ksplit > 1) {
+      NIDT_REQUIRE(part != 0 && bp == 256 && Cout <= 256, "conv3d_fwd_splitk: needs a partial buffer, 256-position blocks, Cout <= 256");
+      a.ksplit = ksplit;
+      a.part = ptr<float>(part);
+    }
+    const int64_t nwg = (int64_t)a.nPB * nCO * G * a.ksplit;
     NIDT_REQUIRE(nwg < (1ll << 31), "conv3d_fwd: grid too large");
     dim3 g1((unsigned)nwg);
     // small grids (64-position blocks: conv3-5 at 8 clients per GPU) run at ~1 wave per SIMD: a third LDS stage
@@ -506,8 +613,16 @@ void conv3d_fwd(uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t xs, uintptr_
 #undef NIDT_DMA_WN
 #undef NIDT_DMA
     NIDT_CHECK(hipGetLastError());
+    if (a.ksplit > 1) {
+      const dim3 fg(a.nPB, G);
+      if (st) hipLaunchKernelGGL((k_fwd_splitk_fin<true, true>), fg, dim3(1024), 0, s, a.part, a.ksplit, a.bias, a.y, a.stats, G, a.Mg, Cout, bp, a.nPB);
+      else if (hb) hipLaunchKernelGGL((k_fwd_splitk_fin<true, false>), fg, dim3(1024), 0, s, a.part, a.ksplit, a.bias, a.y, a.stats, G, a.Mg, Cout, bp, a.nPB);
+      else hipLaunchKernelGGL((k_fwd_splitk_fin<false, false>), fg, dim3(1024), 0, s, a.part, a.ksplit, a.bias, a.y, a.stats, G, a.Mg, Cout, bp, a.nPB);
+      NIDT_CHECK(hipGetLastError());
+    }
     return;
   }
+  NIDT_REQUIRE(ksplit <= 1, "conv3d_fwd: split-K needs the LDS-DMA path (Cin % 64 == 0, no input transform)");
   dim3 grid(a.nPB, Cout / bco, G);
 #define NIDT_FWD(BC, X, BI, ST) hipLaunchKernelGGL((k_conv_fwd<BC, X, BI, ST>), grid, dim3(256), 0, s, a)
   if (bco == 128) {
@@ -519,6 +634,37 @@ void conv3d_fwd(uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t xs, uintptr_
   }
 #undef NIDT_FWD
   NIDT_CHECK(hipGetLastError());
+}
+
+void conv3d_fwd(uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t xs, uintptr_t xt, uintptr_t y, uintptr_t stats,
+                int G, int B, int D, int H, int W, int Cin, int Cout, int pad, uintptr_t stream) {
+  conv3d_fwd_impl(x, w, bias, xs, xt, y, stats, G, B, D, H, W, Cin, Cout, pad, stream, 1, 0);
+}
+
+// Split-K forward for grids that would not fill the chip (few clients per GPU x the 5x7x5 conv3-5 layers):
+// ksplit blocks share one output tile, each over 1/ksplit of the 27*Cin reduction, writing fp32 partials
+// [ksplit, G, Mg, Cout] (part); k_fwd_splitk_fin adds them (fixed order), the bias, and emits y and the BN stats.
+void conv3d_fwd_splitk(uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t y, uintptr_t stats, uintptr_t part,
+                       int ksplit, int G, int B, int D, int H, int W, int Cin, int Cout, int pad, uintptr_t stream) {
+  conv3d_fwd_impl(x, w, bias, 0, 0, y, stats, G, B, D, H, W, Cin, Cout, pad, stream, ksplit, part);
+}
+
+// Split-K factor for conv3d_fwd_splitk.  Off by default: measured at 8 clients per GPU (conv3-5, 264-block grids)
+// the split (2 x 27 k-steps + the finish kernel) made the train step slower, 3.97 -> 4.16 ms
+// (profiles/r1_ab_fwd_splitk.txt).  NIDT_FWD_KSPLIT=k enables it where it applies (256-position blocks,
+// Cout <= 256, fewer than two resident blocks per CU).
+int conv3d_fwd_ksplit(int Cin, int Cout, int G, int Mg) {
+  if (Cin % 64 != 0 || Cout > 256 || Cout % 64 != 0) return 1;
+  if (conv3d_fwd_bp(Cin, Cout, 0, G, Mg) != 256) return 1;
+  static const int env = [] {
+    const char* e = getenv("NIDT_FWD_KSPLIT");
+    return e ? atoi(e) : 0;
+  }();
+  const int bco = (Cout % 128 == 0) ? 128 : 64;
+  const int64_t nwg = (int64_t)ceil_div(Mg, 256) * (Cout / bco) * G;
+  if (env <= 1 || nwg >= 512) return 1;
+  int ks = env;
+  return std::max(1, std::min(ks, 27 * Cin / 64 / 8));
 }
 
 // positions per block (= per BN-statistics block) of conv3d_fwd for this layer shape and client count

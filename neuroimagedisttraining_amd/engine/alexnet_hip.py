@@ -74,6 +74,17 @@ class HipAlexNet3D:
             b["st%d" % ci] = e(G, npb, cout, 2, dt=f32)
             b["npb%d" % ci] = npb
             b["bp%d" % ci] = bp
+        # split-K for the forward/dgrad convs whose grids would not fill the chip (few clients per GPU)
+        fp_sz = 0
+        for (ci, bi, cin, cout, pad, sp) in (L2, L3, L4, L5):
+            out = tuple(d + 2 * pad - 2 for d in sp)
+            for tag, (c_in, c_out, vol, pd) in (("f", (cin, cout, sp, pad)), ("d", (cout, cin, out, 2 - pad))):
+                mg = B * (vol[0] + 2 * pd - 2) * (vol[1] + 2 * pd - 2) * (vol[2] + 2 * pd - 2)
+                ks = self.m.conv3d_fwd_ksplit(c_in, c_out, G, mg)
+                b["ks%s%d" % (tag, ci)] = ks
+                if ks > 1:
+                    fp_sz = max(fp_sz, ks * G * mg * c_out)
+        b["fpart"] = e(max(fp_sz, 1), dt=f32)
         if train:
             for (ci, bi, cin, cout, pad, sp) in (L2, L3, L4, L5):
                 b["w%dt" % ci] = e(G, cin, 27, cout)
@@ -95,6 +106,15 @@ class HipAlexNet3D:
                 self.m.conv3d_pos_table(_p(b["pt%d" % ci]), B, sp[0], sp[1], sp[2], pad, st0)
         self._cache[key] = b
         return b
+
+    def _conv(self, b, key, x, w, bias, y, stats, G, B, D, H, W, cin, cout, pad, st):
+        """conv3d_fwd, or its split-K form when ``b[key]`` (chosen at allocation) is > 1."""
+        ks = b[key]
+        if ks > 1:
+            self.m.conv3d_fwd_splitk(_p(x), _p(w), _p(bias), _p(y), _p(stats), _p(b["fpart"]), ks, G, B, D, H, W, cin,
+                                     cout, pad, st)
+        else:
+            self.m.conv3d_fwd(_p(x), _p(w), _p(bias), 0, 0, _p(y), _p(stats), G, B, D, H, W, cin, cout, pad, st)
 
     # ---------------------------------------------------------------------------------------------
     def _pack(self, theta, G, b, train):
@@ -152,24 +172,24 @@ class HipAlexNet3D:
         m.conv1_fwd_pool(_p(x8), _p(idx), _p(b["w1p"]), _p(b["s1"]), _p(b["t1"]), NB, B, _p(b["p1"]), _p(b["a1"]), st)
         # ---- conv2 + BN2 + ReLU + pool2 ----
         ci, bi, cin, cout, pad, sp = L2
-        m.conv3d_fwd(_p(b["p1"]), _p(b["w4p"]), _p(b["bias4"]), 0, 0, _p(b["y2"]), _p(b["st4"]) if train else 0,
-                     G, B, 19, 23, 19, 64, 128, 0, st)
+        self._conv(b, "ksf4", b["p1"], b["w4p"], b["bias4"], b["y2"], b["st4"] if train else None,
+                   G, B, 19, 23, 19, 64, 128, 0, st)
         self._bn(4, 5, 128, G, B, (17, 21, 17), theta, bufs, b, train)
         m.bn_relu_pool(_p(b["y2"]), _p(b["s4"]), _p(b["t4"]), _p(b["p2"]), _p(b["a2"]), NB, B, 17, 21, 17, 128, st)
         # ---- conv3 ----
-        m.conv3d_fwd(_p(b["p2"]), _p(b["w8p"]), _p(b["bias8"]), 0, 0, _p(b["y3"]), _p(b["st8"]) if train else 0,
-                     G, B, 5, 7, 5, 128, 192, 1, st)
+        self._conv(b, "ksf8", b["p2"], b["w8p"], b["bias8"], b["y3"], b["st8"] if train else None,
+                   G, B, 5, 7, 5, 128, 192, 1, st)
         self._bn(8, 9, 192, G, B, (5, 7, 5), theta, bufs, b, train)
         # BN3+ReLU materialised once (read by conv4 fwd and by conv4's wgrad im2col 27x)
         m.bn_relu_apply(_p(b["y3"]), _p(b["s8"]), _p(b["t8"]), _p(b["h3"]), NB * 175, 192, B * 175, st)
         # ---- conv4 ----
-        m.conv3d_fwd(_p(b["h3"]), _p(b["w11p"]), _p(b["bias11"]), 0, 0, _p(b["y4"]),
-                     _p(b["st11"]) if train else 0, G, B, 5, 7, 5, 192, 192, 1, st)
+        self._conv(b, "ksf11", b["h3"], b["w11p"], b["bias11"], b["y4"], b["st11"] if train else None,
+                   G, B, 5, 7, 5, 192, 192, 1, st)
         self._bn(11, 12, 192, G, B, (5, 7, 5), theta, bufs, b, train)
         m.bn_relu_apply(_p(b["y4"]), _p(b["s11"]), _p(b["t11"]), _p(b["h4"]), NB * 175, 192, B * 175, st)
         # ---- conv5 + BN5 + ReLU + pool ----
-        m.conv3d_fwd(_p(b["h4"]), _p(b["w14p"]), _p(b["bias14"]), 0, 0, _p(b["y5"]),
-                     _p(b["st14"]) if train else 0, G, B, 5, 7, 5, 192, 128, 1, st)
+        self._conv(b, "ksf14", b["h4"], b["w14p"], b["bias14"], b["y5"], b["st14"] if train else None,
+                   G, B, 5, 7, 5, 192, 128, 1, st)
         self._bn(14, 15, 128, G, B, (5, 7, 5), theta, bufs, b, train)
         m.bn_relu_pool(_p(b["y5"]), _p(b["s14"]), _p(b["t14"]), _p(b["p5"]), _p(b["a5"]), NB, B, 5, 7, 5, 128, st)
         return b
@@ -204,19 +224,19 @@ class HipAlexNet3D:
         # layer 5: pool5 -> BN5 -> conv5
         bn_bwd(1, 14, 15, 128, (5, 7, 5), b["dp5"], b["p5"], b["a5"], b["dy5"], b["y5"])
         wgrad(14, b["h4"], None, None, b["dy5"], (5, 7, 5), 192, 128, 1)
-        m.conv3d_fwd(_p(b["dy5"]), _p(b["w14t"]), 0, 0, 0, _p(b["dx5"]), 0, G, B, 5, 7, 5, 128, 192, 1, st)
+        self._conv(b, "ksd14", b["dy5"], b["w14t"], None, b["dx5"], None, G, B, 5, 7, 5, 128, 192, 1, st)
         # layer 4
         bn_bwd(0, 11, 12, 192, (5, 7, 5), b["dx5"], None, None, b["dy4"], b["y4"])
         wgrad(11, b["h3"], None, None, b["dy4"], (5, 7, 5), 192, 192, 1)
-        m.conv3d_fwd(_p(b["dy4"]), _p(b["w11t"]), 0, 0, 0, _p(b["dx4"]), 0, G, B, 5, 7, 5, 192, 192, 1, st)
+        self._conv(b, "ksd11", b["dy4"], b["w11t"], None, b["dx4"], None, G, B, 5, 7, 5, 192, 192, 1, st)
         # layer 3
         bn_bwd(0, 8, 9, 192, (5, 7, 5), b["dx4"], None, None, b["dy3"], b["y3"])
         wgrad(8, b["p2"], None, None, b["dy3"], (5, 7, 5), 128, 192, 1)
-        m.conv3d_fwd(_p(b["dy3"]), _p(b["w8t"]), 0, 0, 0, _p(b["dx3"]), 0, G, B, 5, 7, 5, 192, 128, 1, st)
+        self._conv(b, "ksd8", b["dy3"], b["w8t"], None, b["dx3"], None, G, B, 5, 7, 5, 192, 128, 1, st)
         # layer 2: pool2 -> BN2 -> conv2
         bn_bwd(1, 4, 5, 128, (17, 21, 17), b["dx3"], b["p2"], b["a2"], b["dy2"], b["y2"])
         wgrad(4, b["p1"], None, None, b["dy2"], (19, 23, 19), 64, 128, 0)
-        m.conv3d_fwd(_p(b["dy2"]), _p(b["w4t"]), 0, 0, 0, _p(b["dp1"]), 0, G, B, 17, 21, 17, 128, 64, 2, st)
+        self._conv(b, "ksd4", b["dy2"], b["w4t"], None, b["dp1"], None, G, B, 17, 21, 17, 128, 64, 2, st)
         # layer 1: sparse wgrad through pool1/ReLU/BN1 (closed form)
         m.conv1_wgrad(_p(x8), _p(idx), _p(b["dp1"]), _p(b["p1"]), _p(b["a1"]), NB, B, _p(b["c1part"]), _p(b["w125"]),
                       _p(b["mu"]), _p(b["covw"]), _p(b["i1"]), _p(theta), P, o["features.1.weight"], _p(grads), P,

@@ -93,6 +93,45 @@ def test_conv3d_fwd_stats(cin, cout, pad, sp, xf, G, B):
     assert _relerr(var, yr_g.var(1, unbiased=False)) < 1e-3
 
 
+@pytest.mark.parametrize("cin,cout,G", [(128, 192, 8), (192, 192, 8), (192, 128, 24)])
+@pytest.mark.parametrize("ksplit,stats_on", [(2, True), (3, True), (2, False)])
+def test_conv3d_fwd_splitk(cin, cout, G, ksplit, stats_on):
+    """Split-K forward (few clients per GPU): fp32 partials + finish kernel == fp32 oracle; BN block stats too."""
+    m = _m()
+    B, pad, sp = 16, 1, (5, 7, 5)
+    torch.manual_seed(3)
+    x = torch.randn(G * B, *sp, cin, device=DEV).bfloat16()
+    w = (torch.randn(G, cout, 27, cin, device=DEV) * 0.05).bfloat16()
+    bias = torch.randn(G, cout, device=DEV)
+    Mg = B * 5 * 7 * 5
+    bp = m.conv3d_fwd_bp(cin, cout, 0, G, Mg)
+    assert bp == 256
+    npb = m.conv3d_fwd_nblocks(B, *sp, pad, bp)
+    y = torch.empty(G * B, *sp, cout, device=DEV, dtype=torch.bfloat16)
+    stats = torch.empty(G, npb, cout, 2, device=DEV)
+    part = torch.empty(ksplit * G * Mg * cout, device=DEV)
+    m.conv3d_fwd_splitk(x.data_ptr(), w.data_ptr(), bias.data_ptr(), y.data_ptr(), stats.data_ptr() if stats_on else 0,
+                        part.data_ptr(), ksplit, G, B, *sp, cin, cout, pad, _st())
+    y1 = torch.empty_like(y)
+    m.conv3d_fwd(x.data_ptr(), w.data_ptr(), bias.data_ptr(), 0, 0, y1.data_ptr(), 0, G, B, *sp, cin, cout, pad, _st())
+    torch.cuda.synchronize()
+    ys = []
+    for g in range(G):
+        wg = w[g].float().view(cout, 3, 3, 3, cin).permute(0, 4, 1, 2, 3)
+        ys.append(_cl(F.conv3d(_cf(x[g * B:(g + 1) * B].float()), wg, bias[g], 1, pad)))
+    yr = torch.cat(ys, 0)
+    assert _relerr(y.float(), yr) < 1e-2
+    assert (y.float() - y1.float()).abs().max() <= 2e-2 * yr.abs().max()  # same as the unsplit kernel up to rounding
+    if stats_on:
+        cnt = torch.tensor([min(bp, Mg - b * bp) for b in range(npb)], device=DEV, dtype=torch.float64)
+        mean_b, m2_b = stats[..., 0].double(), stats[..., 1].double()
+        mean = (mean_b * cnt.view(1, -1, 1)).sum(1) / Mg
+        var = (m2_b + cnt.view(1, -1, 1) * (mean_b - mean.unsqueeze(1)) ** 2).sum(1) / Mg
+        yr_g = yr.view(G, Mg, cout).double()
+        assert _relerr(mean, yr_g.mean(1)) < 1e-3
+        assert _relerr(var, yr_g.var(1, unbiased=False)) < 1e-3
+
+
 @pytest.mark.parametrize("cin,cout,pad,sp,xf", [(64, 128, 0, (19, 23, 19), False), (128, 192, 1, (5, 7, 5), False),
                                                 (192, 192, 1, (5, 7, 5), True), (192, 128, 1, (5, 7, 5), True)])
 def test_conv3d_wgrad_and_dgrad(cin, cout, pad, sp, xf):
