@@ -831,24 +831,32 @@ __global__ __launch_bounds__(256, 2) void k_conv_wgrad(ConvWgArgs a) {
 }
 
 // sum the split slabs; write PyTorch layout grad[g][off + (co*Cin + ci)*27 + t] for k = t*Cin + ci (scaled).
-// Block = (co, g): the K-row is summed into LDS in k order, then written out in [ci][t] order (coalesced).
+// Block = (co, g): the K-row is summed into LDS (16-B loads), then written out in [ci][t] order (coalesced).
+// The LDS row is padded to a (Cin + 1) stride per tap: the transposed read row[t][ci] with t fastest across
+// lanes would otherwise hit one bank ~27 times (Cin is a multiple of 32).  Dynamic LDS sized to the layer
+// (27 (Cin + 1) floats) instead of the 512-channel maximum: more resident blocks to cover the HBM latency.
 __global__ __launch_bounds__(256) void k_wgrad_reduce(const float* __restrict__ part, int nsplit, int G, int Cout,
                                                       int Cin, float* grad, int64_t ldg, int64_t off, float scale) {
-  __shared__ float row[27 * kMaxCin];
+  extern __shared__ float row[];  // [27][Cin + 1]
   const int co = blockIdx.x, g = blockIdx.y;
-  const int K = 27 * Cin;
+  const int K = 27 * Cin, RS = Cin + 1;
   const int64_t tot = (int64_t)G * Cout * K;
-  const float* src = part + ((int64_t)g * Cout + co) * K;
-  for (int k = threadIdx.x; k < K; k += 256) {
-    float s = 0.f;
-    for (int sp = 0; sp < nsplit; ++sp) s += src[(int64_t)sp * tot + k];
-    row[k] = s * scale;
+  const float* src = part + ((int64_t)g * Cout + co) * K;  // 16-B aligned: K = 27 * 64 * n
+  for (int k = 4 * threadIdx.x; k < K; k += 4 * 256) {
+    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int sp = 0; sp < nsplit; ++sp) {
+      const float4 v = *reinterpret_cast<const float4*>(src + (int64_t)sp * tot + k);
+      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    }
+    const int t = k / Cin, ci = k - t * Cin;  // k .. k+3 share the tap (Cin % 4 == 0)
+    float* r = row + t * RS + ci;
+    r[0] = s.x * scale; r[1] = s.y * scale; r[2] = s.z * scale; r[3] = s.w * scale;
   }
   __syncthreads();
   float* dst = grad + (int64_t)g * ldg + off + (int64_t)co * K;
   for (int e = threadIdx.x; e < K; e += 256) {
     const int ci = e / 27, t = e - ci * 27;
-    dst[e] = row[t * Cin + ci];
+    dst[e] = row[t * RS + ci];
   }
 }
 
@@ -1064,7 +1072,8 @@ void conv3d_wgrad(uintptr_t x, uintptr_t xs, uintptr_t xt, uintptr_t dy, uintptr
     else hipLaunchKernelGGL((k_conv_wgrad<false>), grid, dim3(256), 0, s, a);
   }
   NIDT_CHECK(hipGetLastError());
-  hipLaunchKernelGGL(k_wgrad_reduce, dim3(Cout, G), dim3(256), 0, s, ptr<const float>(part), nsplit, G, Cout, Cin,
+  hipLaunchKernelGGL(k_wgrad_reduce, dim3(Cout, G), dim3(256), 27 * (Cin + 1) * sizeof(float), s,
+                     ptr<const float>(part), nsplit, G, Cout, Cin,
                      ptr<float>(grad), ldg, off, scale);
   NIDT_CHECK(hipGetLastError());
 }
@@ -1075,16 +1084,16 @@ void conv3d_wgrad(uintptr_t x, uintptr_t xs, uintptr_t xt, uintptr_t dy, uintptr
 // wt [G][Cin][27][Cout] with the taps flipped (64x64 LDS-tiled transpose of wp per tap).
 __global__ __launch_bounds__(256) void k_pack_wp(const float* __restrict__ theta, int64_t ldt, int64_t off, int Cout,
                                                  int Cin, float scale, uint16_t* __restrict__ wp) {
-  __shared__ float row[27 * kMaxCin];
+  extern __shared__ float row[];  // [Cin][27], dynamic: sized to the layer (not the 512-channel maximum)
   const int co = blockIdx.x, g = blockIdx.y;
   const int K = 27 * Cin;
   const float* src = theta + (int64_t)g * ldt + off + (int64_t)co * K;
   for (int e = threadIdx.x; e < K; e += 256) row[e] = src[e];
   __syncthreads();
-  uint16_t* dst = wp + ((int64_t)g * Cout + co) * K;
-  for (int e = threadIdx.x; e < K; e += 256) {
+  uint16_t* dst = wp + ((int64_t)g * Cout + co) * K;  // K even: 4-B aligned pairs
+  for (int e = 2 * threadIdx.x; e < K; e += 2 * 256) {  // e, e+1 share the tap (Cin even)
     const int t = e / Cin, ci = e - t * Cin;
-    dst[e] = f32_to_bf16(row[ci * 27 + t] * scale);
+    *reinterpret_cast<uint32_t*>(dst + e) = pack_bf16x2(row[ci * 27 + t] * scale, row[(ci + 1) * 27 + t] * scale);
   }
 }
 
@@ -1109,8 +1118,8 @@ void pack_conv_w(uintptr_t theta, int64_t ldt, int64_t off, int G, int Cout, int
                  uintptr_t wt, uintptr_t stream) {
   NIDT_REQUIRE(Cin <= kMaxCin, "pack_conv_w: Cin <= 512");
   hipStream_t s = as_stream(stream);
-  hipLaunchKernelGGL(k_pack_wp, dim3(Cout, G), dim3(256), 0, s, ptr<const float>(theta), ldt, off, Cout, Cin, scale,
-                     ptr<uint16_t>(wp));
+  hipLaunchKernelGGL(k_pack_wp, dim3(Cout, G), dim3(256), 27 * Cin * sizeof(float), s, ptr<const float>(theta), ldt,
+                     off, Cout, Cin, scale, ptr<uint16_t>(wp));
   NIDT_CHECK(hipGetLastError());
   if (wt) {
     hipLaunchKernelGGL(k_pack_wt, dim3(ceil_div(Cin, 64), ceil_div(Cout, 64), G * 27), dim3(256), 0, s,
