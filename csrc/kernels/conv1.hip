@@ -190,6 +190,11 @@ __global__ void k_conv1_batch_moments(const double* __restrict__ mom, const int*
 
 // BN1 statistics per (g, c) from the batch moments.  block = 128 threads (k1), grid (64, G).
 // Outputs: scale/shift for conv-without-bias; mean (incl. bias) & invstd; covw[g][c][k] = (Cov w)_k; running stats.
+// Block = (group of kBnCPB channels, client): the 125x125 patch covariance row k1 is formed once per thread and
+// applied to the block's channel filters (one block per channel re-reads the client's 125 KB moment matrix 64
+// times; 8 channels per block when there are >= 32 clients, else 1 to keep the grid wide).  Per channel the
+// arithmetic and reduction order are the same either way.
+template <int kBnCPB>
 __global__ __launch_bounds__(128) void k_conv1_bnstats(const double* __restrict__ Mb, const float* __restrict__ w125,
                                                        const float* __restrict__ theta, int64_t ldt, int64_t off_bias,
                                                        int64_t off_g, int64_t off_b, float* bufs, int64_t ldb,
@@ -197,36 +202,38 @@ __global__ __launch_bounds__(128) void k_conv1_bnstats(const double* __restrict_
                                                        float momentum, float eps, int update_running, float* scale,
                                                        float* shift, float* mean_o, float* invstd_o, float* mu_o,
                                                        float* covw_o) {
-  __shared__ double sw[128], smu[128], red[2];
-  const int c = blockIdx.x, g = blockIdx.y, k1 = threadIdx.x;
+  __shared__ double sw[kBnCPB][128], smu[128], red[kBnCPB][2][2];
+  const int c0 = blockIdx.x * kBnCPB, g = blockIdx.y, k1 = threadIdx.x;
   const double* M = Mb + (int64_t)g * kNM;
-  if (k1 < 125) {
-    sw[k1] = w125[((int64_t)g * kC1 + c) * 125 + k1];
-    smu[k1] = M[k1] / Npos;
-  } else {
-    sw[k1] = 0; smu[k1] = 0;
-  }
+  smu[k1] = k1 < 125 ? M[k1] / Npos : 0.0;
+#pragma unroll
+  for (int cc = 0; cc < kBnCPB; ++cc) sw[cc][k1] = k1 < 125 ? (double)w125[((int64_t)g * kC1 + c0 + cc) * 125 + k1] : 0.0;
   __syncthreads();
-  double t = 0;
+  double t[kBnCPB];
+#pragma unroll
+  for (int cc = 0; cc < kBnCPB; ++cc) t[cc] = 0;
   if (k1 < 125) {
     for (int k2 = 0; k2 < 125; ++k2) {
       const double cov = M[125 + k1 * 125 + k2] / Npos - smu[k1] * smu[k2];
-      t += cov * sw[k2];
-    }
-    covw_o[((int64_t)g * kC1 + c) * 125 + k1] = (float)t;
-    if (c == 0) mu_o[(int64_t)g * 125 + k1] = (float)smu[k1];
-  }
-  double v = sw[k1] * t, m = sw[k1] * smu[k1];
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) { v += __shfl_xor(v, o, 64); m += __shfl_xor(m, o, 64); }
-  if ((k1 & 63) == 0) { red[k1 >> 6] = v; }
+      for (int cc = 0; cc < kBnCPB; ++cc) t[cc] += cov * sw[cc][k2];
+    }
+#pragma unroll
+    for (int cc = 0; cc < kBnCPB; ++cc) covw_o[((int64_t)g * kC1 + c0 + cc) * 125 + k1] = (float)t[cc];
+    if (c0 == 0) mu_o[(int64_t)g * 125 + k1] = (float)smu[k1];
+  }
+#pragma unroll
+  for (int cc = 0; cc < kBnCPB; ++cc) {
+    double v = sw[cc][k1] * t[cc], m = sw[cc][k1] * smu[k1];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) { v += __shfl_xor(v, o, 64); m += __shfl_xor(m, o, 64); }
+    if ((k1 & 63) == 0) { red[cc][0][k1 >> 6] = v; red[cc][1][k1 >> 6] = m; }
+  }
   __syncthreads();
-  const double var = red[0] + red[1];
-  __syncthreads();
-  if ((k1 & 63) == 0) red[k1 >> 6] = m;
-  __syncthreads();
-  if (k1 == 0) {
-    const double mnb = red[0] + red[1];  // mean of the conv output without bias
+  if (k1 < kBnCPB) {
+    const int c = c0 + k1;
+    const double var = red[k1][0][0] + red[k1][0][1];
+    const double mnb = red[k1][1][0] + red[k1][1][1];  // mean of the conv output without bias
     const float bias = theta[(int64_t)g * ldt + off_bias + c];
     const float gm = theta[(int64_t)g * ldt + off_g + c], bt = theta[(int64_t)g * ldt + off_b + c];
     const double vv = var > 0 ? var : 0.0;
@@ -256,10 +263,14 @@ void conv1_bnstats(uintptr_t mom, uintptr_t idx, int B, int G, uintptr_t Mb, uin
                      ptr<const int>(idx), B, G, ptr<double>(Mb));
   NIDT_CHECK(hipGetLastError());
   const double Npos = (double)B * kOD * kOH * kOW;
-  hipLaunchKernelGGL(k_conv1_bnstats, dim3(kC1, G), dim3(128), 0, s, ptr<const double>(Mb), ptr<const float>(w125),
-                     ptr<const float>(theta), ldt, off_bias, off_g, off_b, ptr<float>(bufs), ldb, off_rm, off_rv,
-                     off_nbt, Npos, momentum, eps, update_running, ptr<float>(scale), ptr<float>(shift),
-                     ptr<float>(mean), ptr<float>(invstd), ptr<float>(mu), ptr<float>(covw));
+#define NIDT_BNSTATS(CPB)                                                                                      \
+  hipLaunchKernelGGL(k_conv1_bnstats<CPB>, dim3(kC1 / CPB, G), dim3(128), 0, s, ptr<const double>(Mb),           \
+                     ptr<const float>(w125), ptr<const float>(theta), ldt, off_bias, off_g, off_b, ptr<float>(bufs), \
+                     ldb, off_rm, off_rv, off_nbt, Npos, momentum, eps, update_running, ptr<float>(scale),          \
+                     ptr<float>(shift), ptr<float>(mean), ptr<float>(invstd), ptr<float>(mu), ptr<float>(covw))
+  if (G >= 32) NIDT_BNSTATS(8);
+  else NIDT_BNSTATS(1);
+#undef NIDT_BNSTATS
   NIDT_CHECK(hipGetLastError());
 }
 
