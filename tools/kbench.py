@@ -94,6 +94,25 @@ def main():
     print("G=%d B=%d  full train step %.3f ms  (sum of timed kernels %.3f ms)" % (G, B, t_step, tot))
     for name, t, tf in rows:
         print("%-16s %9.3f ms  %8.1f TF/s" % (name, t, tf))
+    # eval-mode forward at the round's evaluation shape (2G rows: personal + global copies, 36 test samples each)
+    if os.environ.get("KBENCH_EVAL", "1") == "1":
+        G2, B2 = 2 * G, 36
+        th2, bu2 = padded_rows(G2, pl.total, dev), padded_rows(G2, bl.total, dev)
+        th2.copy_(theta[:1].expand(G2, -1))
+        bu2.copy_(bufs[:1].expand(G2, -1))
+        idx2 = (torch.arange(G2 * B2, device=dev) % x8.shape[0]).int()
+        t_ev = timeit(lambda: net.eval_logits(th2, bu2, x8, idx2, G2, B2), 3)
+        t_tr = timeit(lambda: net.eval_logits(theta, bufs, x8, idx, G, B), 5)
+        be = net._cache[(G2, B2, False)]
+        t_c1 = timeit(lambda: m.conv1_fwd_pool(p(x8), p(idx2), p(be["w1p"]), p(be["s1"]), p(be["t1"]), G2 * B2, B2,
+                                               p(be["p1"]), p(be["a1"]), st), 3)
+        bt = net._cache[(G, B, False)]
+        t_c1t = timeit(lambda: m.conv1_fwd_pool(p(x8), p(idx), p(bt["w1p"]), p(bt["s1"]), p(bt["t1"]), G * B, B,
+                                                p(bt["p1"]), p(bt["a1"]), st), 5)
+        print("eval forward %dx%d: %.3f ms (%.2f us/sample; conv1 %.3f ms = %.2f us/sample) | eval forward %dx%d: "
+              "%.3f ms (%.2f us/sample; conv1 %.3f ms = %.2f us/sample)"
+              % (G2, B2, t_ev, 1e3 * t_ev / (G2 * B2), t_c1, 1e3 * t_c1 / (G2 * B2), G, B, t_tr,
+                 1e3 * t_tr / (G * B), t_c1t, 1e3 * t_c1t / (G * B)))
 
 
 if __name__ == "__main__":
