@@ -609,7 +609,7 @@ static void conv3d_fwd_impl(uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t 
       if (st) NIDT_DMA(64, 1, WN, true, true); else if (hb) NIDT_DMA(64, 1, WN, true, false);               \
       else NIDT_DMA(64, 1, WN, false, false);                                                               \
     }
-    if (bp == 256) { NIDT_DMA_WN(4) } else { NIDT_DMA_WN(1) }
+    if (bp == 256) { NIDT_DMA_WN(4) } else if (bp == 128) { NIDT_DMA_WN(2) } else { NIDT_DMA_WN(1) }
 #undef NIDT_DMA_WN
 #undef NIDT_DMA
     NIDT_CHECK(hipGetLastError());
@@ -676,7 +676,15 @@ int conv3d_fwd_bp(int Cin, int Cout, int xf, int G, int Mg) {
     const char* e = getenv("NIDT_FWD_BP_THRESH");
     return e ? atoi(e) : 256;
   }();
-  return nwg256 < thresh ? 64 : 256;  // fewer blocks than CUs: 64-position blocks (measured: only then a win)
+  if (nwg256 < thresh) return 64;  // fewer blocks than CUs: 64-position blocks (measured: only then a win)
+  // one 4-wave 64-channel block per CU (e.g. conv3-5 at 8 clients per GPU: 264 blocks): 128-position blocks of
+  // 2 waves put two blocks on every CU instead
+  static const int bp128 = [] {
+    const char* e = getenv("NIDT_FWD_BP128");
+    return e ? atoi(e) : 1;
+  }();
+  if (bp128 && bco == 64 && nwg256 < 512) return 128;
+  return 256;
 }
 
 int conv3d_fwd_nblocks(int B, int D, int H, int W, int pad, int bp) {

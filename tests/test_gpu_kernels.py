@@ -55,7 +55,7 @@ def test_polyphase_and_moments():
 @pytest.mark.parametrize("cin,cout,pad,sp,xf", [(64, 128, 0, (19, 23, 19), False), (128, 192, 1, (5, 7, 5), False),
                                                 (192, 192, 1, (5, 7, 5), True), (192, 128, 1, (5, 7, 5), True),
                                                 (128, 64, 2, (17, 21, 17), False)])
-@pytest.mark.parametrize("G,B", [(2, 3), (8, 16)])  # small grid (64-position blocks) and full (256) tiles
+@pytest.mark.parametrize("G,B", [(2, 3), (8, 16), (16, 16)])  # 64-, 128- (5x7x5 at G=8) and 256-position blocks
 def test_conv3d_fwd_stats(cin, cout, pad, sp, xf, G, B):
     m = _m()
     torch.manual_seed(1)
@@ -93,7 +93,7 @@ def test_conv3d_fwd_stats(cin, cout, pad, sp, xf, G, B):
     assert _relerr(var, yr_g.var(1, unbiased=False)) < 1e-3
 
 
-@pytest.mark.parametrize("cin,cout,G", [(128, 192, 8), (192, 192, 8), (192, 128, 24)])
+@pytest.mark.parametrize("cin,cout,G", [(128, 192, 16), (192, 192, 16), (192, 128, 24)])
 @pytest.mark.parametrize("ksplit,stats_on", [(2, True), (3, True), (2, False)])
 def test_conv3d_fwd_splitk(cin, cout, G, ksplit, stats_on):
     """Split-K forward (few clients per GPU): fp32 partials + finish kernel == fp32 oracle; BN block stats too."""
