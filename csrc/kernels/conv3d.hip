@@ -882,6 +882,11 @@ int conv3d_wgrad_nsplit(int G, int B, int D, int H, int W, int Cin, int Cout, in
     const char* e = getenv("NIDT_WG_NSPLIT_LEGACY");
     return e && e[0] == '1';
   }();
+  static const int force = [] {  // A/B experiments only: one split factor for every layer
+    const char* e = getenv("NIDT_WG_NSPLIT_FORCE");
+    return e ? atoi(e) : 0;
+  }();
+  if (force > 0) return std::max(1, std::min(force, std::max(1, Mg / 64)));
   if (legacy) {
     const int ns = ceil_div(2048, base);
     const int maxns = max(1, Mg / (K >= 3000 ? 1024 : 512));
