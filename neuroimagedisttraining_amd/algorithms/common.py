@@ -23,7 +23,9 @@ log = logging.getLogger(__name__)
 def client_sampling(round_idx, client_num_in_total, client_num_per_round):
     if client_num_in_total == client_num_per_round:
         return list(range(client_num_in_total))
-    n = min(client_num_per_round, client_num_in_total)
+    # at least one client: int(total * frac) is 0 for small federations with the reference's default frac 0.1,
+    # where the reference aggregates an empty list and crashes (the identity string keeps the reference's count)
+    n = max(1, min(client_num_per_round, client_num_in_total))
     np.random.seed(round_idx)
     return list(np.random.choice(range(client_num_in_total), n, replace=False))
 

@@ -7,7 +7,8 @@ the reference entry points.  Added flags:
   client-batched MI355X executor (HIP kernels, clients sharded over ranks, RCCL aggregation) when ``hip``
   (``auto`` = hip if a GPU and the extension are available); ``torch`` = the reference-semantics sequential
   eager path (also the CPU path).
-* ``--synthetic_abcd 1``, ``--n_per_client``: synthetic ABCD-shape cohort (no HDF5 needed).
+* ``--synthetic_abcd 1``, ``--n_per_client``: synthetic ABCD-shape cohort (no HDF5 needed);
+  ``--synthetic_size N``: N synthetic train images (N/5 test) for CIFAR/Tiny without data files.
 * FedProx / robust aggregation: ``--fedprox_mu``, ``--aggregator {fedavg,krum,multikrum,median,trimmed_mean}``,
   ``--byzantine_f``, ``--trim_ratio``.
 * ``--checkpoint_dir`` / ``--resume`` for the HIP executor.
@@ -107,6 +108,7 @@ def add_args(parser, algo):
     a("--engine", type=str, default="auto", choices=["auto", "hip", "torch"])
     a("--synthetic_abcd", type=int, default=1)
     a("--n_per_client", type=int, default=180)
+    a("--synthetic_size", type=int, default=0)  # 2D datasets without files: synthetic train images (0 = full size)
     a("--fedprox_mu", type=float, default=d.get("fedprox_mu", 0.0))
     a("--aggregator", type=str, default="fedavg")
     a("--byzantine_f", type=int, default=0)
@@ -185,9 +187,10 @@ def load_data(args, dataset_name, logger=None):
         return abcd.load_partition_data_abcd(args.data_dir, args.partition_method, args.partition_alpha,
                                              args.client_num_in_total, args.batch_size, logger)
     if dataset_name in ("cifar10", "cifar100", "tiny"):
+        n = getattr(args, "synthetic_size", 0) or None
         return images.load_partition_data(dataset_name, args.data_dir, args.partition_method, args.partition_alpha,
                                           args.client_num_in_total, args.batch_size, logger, seed=args.seed,
-                                          with_val=False)
+                                          with_val=False, n_train=n, n_test=n // 5 if n else None)
     if dataset_name == "synthetic":
         return images.load_partition_data_synthetic_tabular(args.client_num_in_total, args.batch_size)
     raise ValueError(dataset_name)
