@@ -276,3 +276,39 @@ def test_meta_resnet_generates_weights_for_any_gene():
         assert out.shape == (3, 10)
     out.sum().backward()
     assert m.stem.gen.fc2.weight.grad is not None and float(m.stem.gen.fc2.weight.grad.abs().sum()) > 0
+
+
+def test_model_zoo_forward_shapes():
+    """Every reference model family builds and runs forward + backward at its dataset's input shape."""
+    import importlib
+    A3 = importlib.import_module("neuroimagedisttraining_amd.models.alexnet3d")
+    NR = importlib.import_module("neuroimagedisttraining_amd.models.norm_resnets")
+    R3 = importlib.import_module("neuroimagedisttraining_amd.models.resnet3d")
+    Z = importlib.import_module("neuroimagedisttraining_amd.models.zoo2d")
+    torch.manual_seed(0)
+    x32 = torch.randn(2, 3, 32, 32)
+    cases = [
+        (Z.customized_resnet18(class_num=10), x32, (2, 10)),
+        (Z.vgg11(10), x32, (2, 10)),
+        (Z.vgg16(10), x32, (2, 10)),
+        (Z.LeNet5_cifar(), x32, (2, 10)),
+        (Z.cnn_cifar10(), x32, (2, 10)),
+        (Z.cnn_cifar100(), x32, (2, 100)),
+        (Z.cnn_cifar10_meta(), x32, (2, 10)),
+        (Z.CNN_DropOut(), torch.randn(2, 1, 28, 28), (2, 10)),
+        (Z.CNN_OriginalFedAvg(), torch.randn(2, 1, 28, 28), (2, 10)),
+        (Z.LeNet5(), torch.randn(2, 1, 28, 28), (2, 10)),
+        (NR.resnet18_gn(num_classes=10), torch.randn(2, 3, 64, 64), (2, 10)),
+        (NR.resnet29_ip(num_classes=10), x32, (2, 10)),
+        (R3.resnet3d_18(num_classes=1, width=8), torch.randn(2, 1, 32, 32, 32), (2, 1)),
+        (A3.AlexNet3D_Dropout(num_classes=1, in_shape=(80, 96, 80)), torch.randn(2, 1, 80, 96, 80), (2, 1)),
+    ]
+    for model, x, shape in cases:
+        out = model(x)
+        out = out[0] if isinstance(out, (list, tuple)) else out
+        assert tuple(out.shape) == shape, (type(model).__name__, tuple(out.shape))
+        out.float().sum().backward()
+    # SyncBN without a process group behaves as BatchNorm
+    bn = NR.SynchronizedBatchNorm3d(4)
+    y = bn(torch.randn(3, 4, 5, 5, 5))
+    assert y.shape == (3, 4, 5, 5, 5) and abs(float(y.mean())) < 1e-5
