@@ -550,6 +550,19 @@ __global__ __launch_bounds__(1024) void k_fwd_splitk_fin(const float* __restrict
 
 int conv3d_fwd_bp(int Cin, int Cout, int xf, int G, int Mg);
 
+// launch one k_conv_fwd_dma variant; the 3-stage pipeline only where 3 LDS stages fit in 160 KB
+template <int BC, int WM, int WN, bool BI, bool ST>
+static void launch_fwd_dma(int nst, dim3 g, hipStream_t s, const ConvFwdArgs& a, int nCO) {
+  constexpr int kStageBytes = (BC + 64 * WN) * 64 * 2;
+  if constexpr (3 * kStageBytes <= 160 * 1024) {
+    if (nst == 3) {
+      hipLaunchKernelGGL((k_conv_fwd_dma<BC, WM, WN, 3, BI, ST>), g, dim3(64 * WM * WN), 0, s, a, nCO);
+      return;
+    }
+  }
+  hipLaunchKernelGGL((k_conv_fwd_dma<BC, WM, WN, 2, BI, ST>), g, dim3(64 * WM * WN), 0, s, a, nCO);
+}
+
 static void conv3d_fwd_impl(uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t xs, uintptr_t xt, uintptr_t y,
                             uintptr_t stats, int G, int B, int D, int H, int W, int Cin, int Cout, int pad,
                             uintptr_t stream, int ksplit, uintptr_t part) {
@@ -596,11 +609,7 @@ static void conv3d_fwd_impl(uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t 
       return e ? atoi(e) : 0;
     }();
     const int nst = nst_env ? nst_env : (bp == 64 ? 3 : 2);  // measured: 3 stages only pay with 64-position blocks
-#define NIDT_DMA(BC, WM, WN, BI, ST)                                                                        \
-    do {                                                                                                    \
-      if (nst == 3) hipLaunchKernelGGL((k_conv_fwd_dma<BC, WM, WN, 3, BI, ST>), g1, dim3(64 * WM * WN), 0, s, a, nCO); \
-      else hipLaunchKernelGGL((k_conv_fwd_dma<BC, WM, WN, 2, BI, ST>), g1, dim3(64 * WM * WN), 0, s, a, nCO); \
-    } while (0)
+#define NIDT_DMA(BC, WM, WN, BI, ST) launch_fwd_dma<BC, WM, WN, BI, ST>(nst, g1, s, a, nCO)
 #define NIDT_DMA_WN(WN)                                                                                     \
     if (bco == 128) {                                                                                       \
       if (st) NIDT_DMA(128, 2, WN, true, true); else if (hb) NIDT_DMA(128, 2, WN, true, false);             \
@@ -609,7 +618,7 @@ static void conv3d_fwd_impl(uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t 
       if (st) NIDT_DMA(64, 1, WN, true, true); else if (hb) NIDT_DMA(64, 1, WN, true, false);               \
       else NIDT_DMA(64, 1, WN, false, false);                                                               \
     }
-    if (bp == 256) { NIDT_DMA_WN(4) } else if (bp == 128) { NIDT_DMA_WN(2) } else { NIDT_DMA_WN(1) }
+    if (bp == 256) { NIDT_DMA_WN(4) } else if (bp == 512) { NIDT_DMA_WN(8) } else if (bp == 128) { NIDT_DMA_WN(2) } else { NIDT_DMA_WN(1) }
 #undef NIDT_DMA_WN
 #undef NIDT_DMA
     NIDT_CHECK(hipGetLastError());
@@ -684,6 +693,13 @@ int conv3d_fwd_bp(int Cin, int Cout, int xf, int G, int Mg) {
     return e ? atoi(e) : 1;
   }();
   if (bp128 && bco == 64 && nwg256 < 512) return 128;
+  // large grids: 512-position blocks (16 waves for 128 channels, 160 KB of LDS) raise the MFMA work per byte of
+  // LDS-DMA by 20 % and give each SIMD 4 waves.  NIDT_FWD_BP512=1 enables it (A/B).
+  static const int bp512 = [] {
+    const char* e = getenv("NIDT_FWD_BP512");
+    return e ? atoi(e) : 0;
+  }();
+  if (bp512 && nwg256 >= 4096) return 512;
   return 256;
 }
 
