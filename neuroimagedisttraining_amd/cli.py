@@ -108,7 +108,8 @@ def add_args(parser, algo):
     a("--engine", type=str, default="auto", choices=["auto", "hip", "torch"])
     a("--synthetic_abcd", type=int, default=1)
     a("--n_per_client", type=int, default=180)
-    a("--synthetic_size", type=int, default=0)  # 2D datasets without files: synthetic train images (0 = full size)
+    a("--synthetic_size", type=int, default=0)
+    a("--heartbeat_s", type=float, default=0.0)  # >0: multi-rank failure detection (comm/failure.py)  # 2D datasets without files: synthetic train images (0 = full size)
     a("--fedprox_mu", type=float, default=d.get("fedprox_mu", 0.0))
     a("--aggregator", type=str, default="fedavg")
     a("--byzantine_f", type=int, default=0)
@@ -236,7 +237,7 @@ def run_hip(args, algo, logger):
                    snip_mask=getattr(args, "snip_mask", True), frequency_of_the_test=args.frequency_of_the_test,
                    seed=args.seed, prox_mu=args.fedprox_mu if algo == "fedprox" else 0.0, group=args.group,
                    aggregator=args.aggregator, byzantine_f=args.byzantine_f, trim_ratio=args.trim_ratio,
-                   update_topk=args.update_topk)
+                   update_topk=args.update_topk, heartbeat_s=args.heartbeat_s)
     runner = FLRunner(eng, splits, cfg, info, model, logger=logger,
                       algorithm="salientgrads" if algo == "sailentgrads" else "fedavg")
     start = 0

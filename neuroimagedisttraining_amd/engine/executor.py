@@ -69,6 +69,8 @@ class FLConfig:
     update_topk: float = 0.0      # >0: each client sends only its top-k |update| (values + int32 indices,
                                   # k = update_topk * P) through an RCCL all-gather (BASELINE config 5)
     hip_graphs: bool = True       # capture each lockstep local step (train + optimizer) in a hipGraph and replay it
+    heartbeat_s: float = 0.0      # >0: ranks publish heartbeats every heartbeat_s through the process group's store and
+                                  # each round fails fast (comm.failure.PeerFailure) if a peer is silent for 30x that
 
 
 # ------------------------------------------------------------------------------------------------
@@ -739,8 +741,22 @@ class FLRunner:
         self.timers["eval"] += time.perf_counter() - t0
         return dict(global_test_acc=g_acc, global_test_loss=g_loss, person_test_acc=p_acc, person_test_loss=p_loss)
 
+    def _heartbeat(self):
+        """Lazily started failure detector (multi-rank runs with ``cfg.heartbeat_s`` > 0), else None."""
+        if self.cfg.heartbeat_s <= 0 or self.info.world <= 1:
+            return None
+        if getattr(self, "_hb", None) is None:
+            from ..comm.failure import HeartbeatMonitor, default_store
+            store = default_store()
+            self._hb = HeartbeatMonitor(store, self.info.rank, self.info.world, self.cfg.heartbeat_s,
+                                        30.0 * self.cfg.heartbeat_s) if store is not None else False
+        return self._hb or None
+
     def run_round(self, round_idx, sync_timers=False):
         t0 = time.perf_counter()
+        hb = self._heartbeat()
+        if hb is not None:
+            hb.check_or_raise()  # before the round's collectives: a dead peer would block them until the timeout
         sampled = self.sample_clients(round_idx)
         if self.log is not None and self.info.is_main:
             self.log.info("################Communication round : {}".format(round_idx))

@@ -1,6 +1,8 @@
 """CPU unit tests: partitioners, robust aggregation, messages/backends, topologies, secure aggregation, FLOPs."""
 import json
 
+import time
+
 import numpy as np
 import pytest
 import torch
@@ -312,3 +314,33 @@ def test_model_zoo_forward_shapes():
     bn = NR.SynchronizedBatchNorm3d(4)
     y = bn(torch.randn(3, 4, 5, 5, 5))
     assert y.shape == (3, 4, 5, 5, 5) and abs(float(y.mean())) < 1e-5
+
+
+def test_heartbeat_failure_detector_reports_silent_rank():
+    """Store-based heartbeats: a rank that stops publishing is reported dead after the timeout; live ranks are not."""
+    import socket
+    import torch.distributed as dist
+    from neuroimagedisttraining_amd.comm.failure import HeartbeatMonitor, PeerFailure
+    sk = socket.socket()
+    sk.bind(("127.0.0.1", 0))
+    port = sk.getsockname()[1]
+    sk.close()
+    master = dist.TCPStore("127.0.0.1", port, 3, True, wait_for_workers=False)
+    stores = [master] + [dist.TCPStore("127.0.0.1", port, 3, False) for _ in range(2)]
+    mons = [HeartbeatMonitor(stores[r], r, 3, interval_s=0.05, timeout_s=0.6) for r in range(3)]
+    try:
+        assert mons[0].wait_all_alive(5.0)
+        assert mons[0].dead_ranks() == [] and mons[1].dead_ranks() == []
+        time.sleep(0.3)
+        assert mons[0].dead_ranks() == []
+        mons[2].stop()                      # rank 2 "dies"
+        t_end = time.time() + 5
+        while time.time() < t_end and not (mons[0].dead_ranks() == [2] and mons[1].dead_ranks() == [2]):
+            time.sleep(0.1)  # each observer times a silent peer from its own last observed change
+        assert mons[0].dead_ranks() == [2] and mons[1].dead_ranks() == [2]
+        with pytest.raises(PeerFailure) as ei:
+            mons[1].check_or_raise()
+        assert ei.value.dead == [2]
+    finally:
+        for m in mons:
+            m.stop()

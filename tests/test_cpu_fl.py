@@ -130,7 +130,7 @@ def _dist_worker(rank, world, port, out, cfg_kw=None):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("cfg_kw", [{}, {"aggregator": "median"}, {"update_topk": 0.1}])
+@pytest.mark.parametrize("cfg_kw", [{}, {"aggregator": "median"}, {"update_topk": 0.1}, {"heartbeat_s": 0.05}])
 def test_two_rank_gloo_matches_single_process(tmp_path, cfg_kw):
     """2 ranks (clients sharded, mask-compacted all-reduce / all-gathered robust aggregation) == 1 process."""
     import socket
