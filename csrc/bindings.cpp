@@ -19,6 +19,8 @@ void conv3d_fwd(uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t xs, uintptr_
 void conv3d_fwd_splitk(uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t y, uintptr_t stats, uintptr_t part,
                        int ksplit, int G, int B, int D, int H, int W, int Cin, int Cout, int pad, uintptr_t stream);
 int conv3d_fwd_ksplit(int Cin, int Cout, int G, int Mg);
+void conv3d_fwd_bld(uintptr_t x, uintptr_t w, uintptr_t bias, int64_t bias_ld, uintptr_t y, uintptr_t stats, int G, int B,
+                    int D, int H, int W, int Cin, int Cout, int pad, uintptr_t stream);
 int conv3d_fwd_nblocks(int B, int D, int H, int W, int pad, int bp);
 int conv3d_fwd_bp(int Cin, int Cout, int xf, int G, int Mg);
 void conv3d_wgrad(uintptr_t x, uintptr_t xs, uintptr_t xt, uintptr_t dy, uintptr_t part, uintptr_t grad, int64_t ldg,
@@ -83,6 +85,7 @@ PYBIND11_MODULE(_nidt_hip, m) {
   DEF(conv3d_fwd);
   DEF(conv3d_fwd_splitk);
   DEF(conv3d_fwd_ksplit);
+  DEF(conv3d_fwd_bld);
   DEF(conv3d_fwd_nblocks);
   DEF(conv3d_fwd_bp);
   DEF(conv3d_wgrad);

@@ -40,6 +40,7 @@ struct ConvFwdArgs {
   int nPB;              // position blocks per client (grid.x)
   int ksplit = 1;       // split-K factor (LDS-DMA path): > 1 writes fp32 partials, k_fwd_splitk_fin finishes
   int G = 0;            // clients (split-K partial indexing)
+  int64_t bias_ld = 0;  // bias row stride per client (0 = Cout; the flat parameter row stride to read theta directly)
   float* part = nullptr;  // [ksplit, G, Mg, Cout] fp32 partial sums
 };
 
@@ -73,7 +74,8 @@ __device__ __forceinline__ void conv_fwd_epilogue(const ConvFwdArgs& a, f32x4 (&
   for (int i = 0; i < TCO; ++i)
 #pragma unroll
     for (int r = 0; r < 4; ++r)
-      bias_r[i][r] = BIAS ? a.bias[(int64_t)g * a.Cout + co0 + wco * WCO + i * 16 + 4 * fq + r] : 0.f;
+      bias_r[i][r] = BIAS ? a.bias[(int64_t)g * (a.bias_ld ? a.bias_ld : a.Cout) + co0 + wco * WCO + i * 16 + 4 * fq + r]
+                          : 0.f;
   const int posw = pb * BP + wp * WP + fr;
 #pragma unroll
   for (int j = 0; j < TP; ++j) {
@@ -479,7 +481,7 @@ template <bool BIAS, bool STATS>
 __global__ __launch_bounds__(1024) void k_fwd_splitk_fin(const float* __restrict__ part, int ksplit,
                                                          const float* __restrict__ bias, uint16_t* __restrict__ y,
                                                          float* __restrict__ stats, int G, int Mg, int Cout, int BP,
-                                                         int nPB) {
+                                                         int nPB, int64_t bias_ld) {
   __shared__ float red[kFinPG][256];
   __shared__ float smean[256];
   const int pb = blockIdx.x, g = blockIdx.y;
@@ -494,7 +496,7 @@ __global__ __launch_bounds__(1024) void k_fwd_splitk_fin(const float* __restrict
     s[u] = 0.f;
     if (u >= ncu) continue;
     const int c = lane + 64 * u;
-    const float bv = BIAS ? bias[(int64_t)g * Cout + c] : 0.f;
+    const float bv = BIAS ? bias[(int64_t)g * bias_ld + c] : 0.f;
 #pragma unroll
     for (int q = 0; q < kFinMaxPV; ++q) {
       const int m = pg + kFinPG * q;
@@ -565,7 +567,7 @@ static void launch_fwd_dma(int nst, dim3 g, hipStream_t s, const ConvFwdArgs& a,
 
 static void conv3d_fwd_impl(uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t xs, uintptr_t xt, uintptr_t y,
                             uintptr_t stats, int G, int B, int D, int H, int W, int Cin, int Cout, int pad,
-                            uintptr_t stream, int ksplit, uintptr_t part) {
+                            uintptr_t stream, int ksplit, uintptr_t part, int64_t bias_ld = 0) {
   NIDT_REQUIRE(Cin % 32 == 0, "conv3d_fwd: Cin must be a multiple of 32");
   NIDT_REQUIRE((xs == 0 && Cin % 64 == 0) ? Cin <= kMaxCin : Cin <= 192,
                "conv3d_fwd: Cin <= 512 (LDS-DMA path: Cin % 64 == 0, no input transform), else <= 192");
@@ -582,6 +584,7 @@ static void conv3d_fwd_impl(uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t 
   a.Mg = B * a.Do * a.Ho * a.Wo;
   a.nPB = ceil_div(a.Mg, kFwdBP);
   a.G = G;
+  a.bias_ld = bias_ld;
   const bool xf = xs != 0, hb = bias != 0, st = stats != 0;
   NIDT_REQUIRE(!st || hb, "conv3d_fwd: statistics require a bias");
   const int bco = (Cout % 128 == 0) ? 128 : 64;
@@ -624,9 +627,9 @@ static void conv3d_fwd_impl(uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t 
     NIDT_CHECK(hipGetLastError());
     if (a.ksplit > 1) {
       const dim3 fg(a.nPB, G);
-      if (st) hipLaunchKernelGGL((k_fwd_splitk_fin<true, true>), fg, dim3(1024), 0, s, a.part, a.ksplit, a.bias, a.y, a.stats, G, a.Mg, Cout, bp, a.nPB);
-      else if (hb) hipLaunchKernelGGL((k_fwd_splitk_fin<true, false>), fg, dim3(1024), 0, s, a.part, a.ksplit, a.bias, a.y, a.stats, G, a.Mg, Cout, bp, a.nPB);
-      else hipLaunchKernelGGL((k_fwd_splitk_fin<false, false>), fg, dim3(1024), 0, s, a.part, a.ksplit, a.bias, a.y, a.stats, G, a.Mg, Cout, bp, a.nPB);
+      if (st) hipLaunchKernelGGL((k_fwd_splitk_fin<true, true>), fg, dim3(1024), 0, s, a.part, a.ksplit, a.bias, a.y, a.stats, G, a.Mg, Cout, bp, a.nPB, a.bias_ld ? a.bias_ld : (int64_t)Cout);
+      else if (hb) hipLaunchKernelGGL((k_fwd_splitk_fin<true, false>), fg, dim3(1024), 0, s, a.part, a.ksplit, a.bias, a.y, a.stats, G, a.Mg, Cout, bp, a.nPB, a.bias_ld ? a.bias_ld : (int64_t)Cout);
+      else hipLaunchKernelGGL((k_fwd_splitk_fin<false, false>), fg, dim3(1024), 0, s, a.part, a.ksplit, a.bias, a.y, a.stats, G, a.Mg, Cout, bp, a.nPB, a.bias_ld ? a.bias_ld : (int64_t)Cout);
       NIDT_CHECK(hipGetLastError());
     }
     return;
@@ -653,6 +656,13 @@ void conv3d_fwd(uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t xs, uintptr_
 // Split-K forward for grids that would not fill the chip (few clients per GPU x the 5x7x5 conv3-5 layers):
 // ksplit blocks share one output tile, each over 1/ksplit of the 27*Cin reduction, writing fp32 partials
 // [ksplit, G, Mg, Cout] (part); k_fwd_splitk_fin adds them (fixed order), the bias, and emits y and the BN stats.
+// Forward whose per-client bias rows live at stride bias_ld (e.g. read straight from the flat parameter rows
+// theta[g][off_bias ..] instead of a per-step copy into a contiguous [G, Cout] buffer).
+void conv3d_fwd_bld(uintptr_t x, uintptr_t w, uintptr_t bias, int64_t bias_ld, uintptr_t y, uintptr_t stats, int G, int B,
+                    int D, int H, int W, int Cin, int Cout, int pad, uintptr_t stream) {
+  conv3d_fwd_impl(x, w, bias, 0, 0, y, stats, G, B, D, H, W, Cin, Cout, pad, stream, 1, 0, bias_ld);
+}
+
 void conv3d_fwd_splitk(uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t y, uintptr_t stats, uintptr_t part,
                        int ksplit, int G, int B, int D, int H, int W, int Cin, int Cout, int pad, uintptr_t stream) {
   conv3d_fwd_impl(x, w, bias, 0, 0, y, stats, G, B, D, H, W, Cin, Cout, pad, stream, ksplit, part);

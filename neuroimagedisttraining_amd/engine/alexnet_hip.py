@@ -107,9 +107,18 @@ class HipAlexNet3D:
         self._cache[key] = b
         return b
 
-    def _conv(self, b, key, x, w, bias, y, stats, G, B, D, H, W, cin, cout, pad, st):
-        """conv3d_fwd, or its split-K form when ``b[key]`` (chosen at allocation) is > 1."""
+    def _conv(self, b, key, x, w, bias, y, stats, G, B, D, H, W, cin, cout, pad, st, theta=None, ci=None):
+        """conv3d_fwd, or its split-K form when ``b[key]`` (chosen at allocation) is > 1.  With ``theta`` the bias
+        of conv ``ci`` is read straight from the flat parameter rows (row stride P), no per-step copy."""
         ks = b[key]
+        if theta is not None and ks <= 1:
+            o = self.o["features.%d.bias" % ci]
+            self.m.conv3d_fwd_bld(_p(x), _p(w), theta.data_ptr() + 4 * o, theta.stride(0), _p(y), _p(stats), G, B, D,
+                                  H, W, cin, cout, pad, st)
+            return
+        if theta is not None:
+            o = self.o["features.%d.bias" % ci]
+            bias.copy_(theta[:, o:o + cout])
         if ks > 1:
             self.m.conv3d_fwd_splitk(_p(x), _p(w), _p(bias), _p(y), _p(stats), _p(b["fpart"]), ks, G, B, D, H, W, cin,
                                      cout, pad, st)
@@ -125,8 +134,6 @@ class HipAlexNet3D:
         for (ci, bi, cin, cout, pad, sp) in (L2, L3, L4, L5):
             m.pack_conv_w(_p(theta), P, self.o["features.%d.weight" % ci], G, cout, cin, 1.0, _p(b["w%dp" % ci]),
                           _p(b["w%dt" % ci]) if train else 0, st)
-            o = self.o["features.%d.bias" % ci]
-            b["bias%d" % ci].copy_(theta[:, o:o + cout])
 
     def _bn(self, ci, bi, C, G, B, sp, theta, bufs, b, train):
         """BN coefficients for conv ``ci`` (train: from the conv epilogue stats; eval: running stats)."""
@@ -173,23 +180,23 @@ class HipAlexNet3D:
         # ---- conv2 + BN2 + ReLU + pool2 ----
         ci, bi, cin, cout, pad, sp = L2
         self._conv(b, "ksf4", b["p1"], b["w4p"], b["bias4"], b["y2"], b["st4"] if train else None,
-                   G, B, 19, 23, 19, 64, 128, 0, st)
+                   G, B, 19, 23, 19, 64, 128, 0, st, theta, 4)
         self._bn(4, 5, 128, G, B, (17, 21, 17), theta, bufs, b, train)
         m.bn_relu_pool(_p(b["y2"]), _p(b["s4"]), _p(b["t4"]), _p(b["p2"]), _p(b["a2"]), NB, B, 17, 21, 17, 128, st)
         # ---- conv3 ----
         self._conv(b, "ksf8", b["p2"], b["w8p"], b["bias8"], b["y3"], b["st8"] if train else None,
-                   G, B, 5, 7, 5, 128, 192, 1, st)
+                   G, B, 5, 7, 5, 128, 192, 1, st, theta, 8)
         self._bn(8, 9, 192, G, B, (5, 7, 5), theta, bufs, b, train)
         # BN3+ReLU materialised once (read by conv4 fwd and by conv4's wgrad im2col 27x)
         m.bn_relu_apply(_p(b["y3"]), _p(b["s8"]), _p(b["t8"]), _p(b["h3"]), NB * 175, 192, B * 175, st)
         # ---- conv4 ----
         self._conv(b, "ksf11", b["h3"], b["w11p"], b["bias11"], b["y4"], b["st11"] if train else None,
-                   G, B, 5, 7, 5, 192, 192, 1, st)
+                   G, B, 5, 7, 5, 192, 192, 1, st, theta, 11)
         self._bn(11, 12, 192, G, B, (5, 7, 5), theta, bufs, b, train)
         m.bn_relu_apply(_p(b["y4"]), _p(b["s11"]), _p(b["t11"]), _p(b["h4"]), NB * 175, 192, B * 175, st)
         # ---- conv5 + BN5 + ReLU + pool ----
         self._conv(b, "ksf14", b["h4"], b["w14p"], b["bias14"], b["y5"], b["st14"] if train else None,
-                   G, B, 5, 7, 5, 192, 128, 1, st)
+                   G, B, 5, 7, 5, 192, 128, 1, st, theta, 14)
         self._bn(14, 15, 128, G, B, (5, 7, 5), theta, bufs, b, train)
         m.bn_relu_pool(_p(b["y5"]), _p(b["s14"]), _p(b["t14"]), _p(b["p5"]), _p(b["a5"]), NB, B, 5, 7, 5, 128, st)
         return b
