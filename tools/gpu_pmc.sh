@@ -3,6 +3,7 @@
 set -o pipefail
 mkdir -p gpurun_out/pmc
 export PYTHONUNBUFFERED=1
+export KBENCH_EVAL=0
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 RE='k_conv1_fwd_pool_pipe|k_conv1_wgrad_split|k_conv_fwd_dma|k_conv_wgrad_dma'
 i=0
