@@ -109,3 +109,25 @@ def test_volume_reader_sanitizer_stress(san, tmp_path):
     assert b.returncode == 0, b.stderr[-2000:]
     r = subprocess.run([exe, str(tmp_path), "4", "25"], capture_output=True, text=True, timeout=240)
     assert r.returncode == 0 and "volume_io_stress ok" in r.stdout, (r.stdout + r.stderr)[-3000:]
+
+
+def test_abcd_preprocessing_matches_notebook_semantics(tmp_path):
+    """Preprocess_ABCD.ipynb: mean-image > 0.2 mask, masked per-subject min-max, uint8 truncation, category codes
+    for sex and LabelEncoder codes for site; written as a NIDTVOL1 file the native reader serves."""
+    from neuroimagedisttraining_amd.data.preprocess import preprocess_cohort
+    rs = np.random.RandomState(0)
+    vols = rs.rand(5, 6, 7, 6).astype(np.float32) * 0.6
+    vols[:, :2] = 0.05  # low-mean region falls outside the mask
+    female = np.array(["1", "0", "1", "", "0"], dtype=object)
+    site = np.array(["site21", "site02", "site02", "site10", "site21"])
+    q, y, s = preprocess_cohort(vols, female, site, out_path=str(tmp_path / "c.nidtvol"))
+    mask = vols.mean(0) > 0.2
+    for i in range(5):
+        v = vols[i].astype(np.float64) * mask
+        ref = ((v - v.min()) / (v.max() - v.min()) * 255).astype(np.uint8)
+        assert np.array_equal(q[i], ref)
+    assert (q[:, :2] == 0).all()
+    assert y.tolist() == [1, 0, 1, -1, 0] and s.tolist() == [2, 0, 0, 1, 2]
+    vf = VolumeFile(str(tmp_path / "c.nidtvol"))
+    assert np.array_equal(vf.gather(np.array([3, 1])).numpy(), q[[3, 1]])
+    assert np.asarray(vf.labels).tolist() == [1, 0, 1, -1, 0]
