@@ -13,6 +13,10 @@ void clip_sgd_mask(uintptr_t w, uintptr_t g, uintptr_t buf, uintptr_t mask, uint
 void weighted_rows_sum(uintptr_t rows, uintptr_t wts, int64_t C, int64_t P, int64_t stride, float beta, uintptr_t out,
                        uintptr_t stream);
 void broadcast_row(uintptr_t src, int64_t P, int64_t stride, int64_t C, uintptr_t dst, uintptr_t stream);
+void local_opt(uintptr_t w, uintptr_t g, uintptr_t buf, int64_t ld, uintptr_t mbits, int64_t mstride, int mask_mode,
+               uintptr_t ref, int64_t ref_ld, float mu, uintptr_t pref, int64_t pref_ld, float lamda, uintptr_t part,
+               int64_t C, int64_t P, float lr, float wd, float mom, float max_norm, uintptr_t lr_dev, int keep_grad,
+               uintptr_t stream);
 // conv3d.hip
 void conv3d_fwd(uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t xs, uintptr_t xt, uintptr_t y, uintptr_t stats,
                 int G, int B, int D, int H, int W, int Cin, int Cout, int pad, uintptr_t stream);
@@ -37,13 +41,14 @@ void bn_finalize(uintptr_t stats, int nPB, int BP, int Mg, int G, int C, uintptr
                  float momentum, float eps, uintptr_t scale, uintptr_t shift, uintptr_t mean, uintptr_t invstd,
                  int update_running, uintptr_t stream);
 void bn_eval(int G, int C, uintptr_t theta, int64_t ldt, int64_t off_g, int64_t off_b, uintptr_t bufs, int64_t ldb,
-             int64_t off_rm, int64_t off_rv, float eps, uintptr_t scale, uintptr_t shift, uintptr_t stream);
+             int64_t off_rm, int64_t off_rv, float eps, uintptr_t scale, uintptr_t shift, uintptr_t mean,
+             uintptr_t invstd, uintptr_t stream);
 void bn_relu_pool(uintptr_t y, uintptr_t scale, uintptr_t shift, uintptr_t out, uintptr_t amax, int NB, int B, int D,
                   int H, int W, int C, uintptr_t stream);
 void bn_bwd(int pool, uintptr_t y, uintptr_t dsrc, uintptr_t pout, uintptr_t amax, uintptr_t scale, uintptr_t shift,
             uintptr_t mean, uintptr_t invstd, int NB, int B, int D, int H, int W, int C, uintptr_t part, int nchunk,
             uintptr_t theta, int64_t ldt, int64_t off_g, uintptr_t grad, int64_t ldg, int64_t goff_g, int64_t goff_b,
-            int64_t goff_convb, uintptr_t coef, uintptr_t dy, uintptr_t stream);
+            int64_t goff_convb, uintptr_t coef, uintptr_t dy, int eval_mode, uintptr_t stream);
 // conv1.hip
 void polyphase(uintptr_t src, uintptr_t dst, int64_t N, uintptr_t stream);
 void conv1_sample_moments(uintptr_t x8, int64_t N, uintptr_t mom, uintptr_t stream);
@@ -61,7 +66,7 @@ int conv1_wgrad_nq(int NB);
 void conv1_wgrad(uintptr_t x8, uintptr_t idx, uintptr_t dp, uintptr_t pout, uintptr_t amax, int NB, int B,
                  uintptr_t part, uintptr_t w125, uintptr_t mu, uintptr_t covw, uintptr_t invstd, uintptr_t theta,
                  int64_t ldt, int64_t off_g, uintptr_t grad, int64_t ldg, int64_t goff_w, int64_t goff_bias,
-                 int64_t goff_g, int64_t goff_b, float wscale, uintptr_t stream);
+                 int64_t goff_g, int64_t goff_b, float wscale, uintptr_t emean, uintptr_t stream);
 // head.hip
 void head(uintptr_t p5, uintptr_t theta, int64_t ldt, int64_t off_w1, int64_t off_b1, int64_t off_w2, int64_t off_b2,
           uintptr_t y, uintptr_t logits, uintptr_t loss, uintptr_t grad, int64_t ldg, uintptr_t dp5, int G, int B,
@@ -72,6 +77,19 @@ void saliency_acc(uintptr_t theta, uintptr_t grad, int64_t ld, int64_t P, int G,
 void radix_select_kth(uintptr_t v, int64_t n, int64_t k, uintptr_t state, uintptr_t hist, uintptr_t stream);
 void threshold_mask(uintptr_t v, int64_t n, uintptr_t state, uintptr_t mask, uintptr_t stream);
 void mask_stats(uintptr_t a, uintptr_t b, int64_t n, uintptr_t out, uintptr_t stream);
+// sparse.hip
+void seg_count(uintptr_t tiles, int ntiles, uintptr_t A, uintptr_t Bm, int64_t mstride, uintptr_t v, int64_t ldv,
+               int mode, int S, uintptr_t out, uintptr_t stream);
+void seg_select(uintptr_t tiles, uintptr_t tile_first, int ntiles, uintptr_t v, int64_t ldv, uintptr_t bits,
+                int64_t mstride, uintptr_t cids, uint64_t seed, int R, int S, int mode, uintptr_t state,
+                uintptr_t hist, uintptr_t ties, int query_only, uintptr_t stream);
+void seg_prune(uintptr_t tiles, int ntiles, uintptr_t v, int64_t ldv, uintptr_t out, int64_t mstride, uintptr_t thr,
+               uintptr_t prune, int S, uintptr_t stream);
+void masked_rows_sum(uintptr_t rows, int64_t ld, uintptr_t bits, int64_t mstride, int R, int64_t n, uintptr_t sum,
+                     uintptr_t cnt, uintptr_t stream);
+void mix_rows(uintptr_t src, uintptr_t wts, uintptr_t rowptr, uintptr_t dst, int R, int64_t n, uintptr_t stream);
+int pair_sqdist_nblk(int64_t n);
+void pair_sqdist(uintptr_t pa, uintptr_t pb, int K, int64_t n, uintptr_t part, uintptr_t stream);
 }  // namespace nidt
 
 PYBIND11_MODULE(_nidt_hip, m) {
@@ -109,5 +127,13 @@ PYBIND11_MODULE(_nidt_hip, m) {
   DEF(radix_select_kth);
   DEF(threshold_mask);
   DEF(mask_stats);
+  DEF(local_opt);
+  DEF(seg_count);
+  DEF(seg_select);
+  DEF(seg_prune);
+  DEF(masked_rows_sum);
+  DEF(mix_rows);
+  DEF(pair_sqdist_nblk);
+  DEF(pair_sqdist);
 #undef DEF
 }

@@ -83,22 +83,29 @@ void bn_finalize(uintptr_t stats, int nPB, int BP, int Mg, int G, int C, uintptr
   NIDT_CHECK(hipGetLastError());
 }
 
-__global__ void k_bn_eval(int G, int C, BNPtrs p, float eps, float* scale, float* shift) {
+// eval-mode coefficients; mean_o / invstd_o (optional) receive the running mean and 1/sqrt(running_var + eps) for an
+// eval-mode backward (DisPFL screen_gradients runs the model in eval(): DisPFL/my_model_trainer.py:166-189)
+__global__ void k_bn_eval(int G, int C, BNPtrs p, float eps, float* scale, float* shift, float* mean_o,
+                          float* invstd_o) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= G * C) return;
   const int g = i / C, c = i - g * C;
   const float rm = p.bufs[(int64_t)g * p.ldb + p.off_rm + c], rv = p.bufs[(int64_t)g * p.ldb + p.off_rv + c];
   const float gm = p.theta[(int64_t)g * p.ldt + p.off_g + c], bt = p.theta[(int64_t)g * p.ldt + p.off_b + c];
+  const float inv = 1.f / sqrtf(rv + eps);
   const float sc = gm / sqrtf(rv + eps);
   scale[i] = sc;
   shift[i] = bt - rm * sc;
+  if (mean_o) mean_o[i] = rm;
+  if (invstd_o) invstd_o[i] = inv;
 }
 
 void bn_eval(int G, int C, uintptr_t theta, int64_t ldt, int64_t off_g, int64_t off_b, uintptr_t bufs, int64_t ldb,
-             int64_t off_rm, int64_t off_rv, float eps, uintptr_t scale, uintptr_t shift, uintptr_t stream) {
+             int64_t off_rm, int64_t off_rv, float eps, uintptr_t scale, uintptr_t shift, uintptr_t mean,
+             uintptr_t invstd, uintptr_t stream) {
   BNPtrs p{ptr<const float>(theta), ldt, off_g, off_b, ptr<float>(bufs), ldb, off_rm, off_rv, 0};
   hipLaunchKernelGGL(k_bn_eval, dim3(ceil_div(G * C, 256)), dim3(256), 0, as_stream(stream), G, C, p, eps,
-                     ptr<float>(scale), ptr<float>(shift));
+                     ptr<float>(scale), ptr<float>(shift), ptr<float>(mean), ptr<float>(invstd));
   NIDT_CHECK(hipGetLastError());
 }
 
@@ -274,7 +281,8 @@ __global__ __launch_bounds__(256) void k_bn_bwd_fin(const float* __restrict__ pa
                                                     double Ncount, const float* __restrict__ mean,
                                                     const float* __restrict__ invstd, const float* theta, int64_t ldt,
                                                     int64_t off_g, float* grad, int64_t ldg, int64_t goff_g,
-                                                    int64_t goff_b, int64_t goff_convb, float* __restrict__ coef) {
+                                                    int64_t goff_b, int64_t goff_convb, float* __restrict__ coef,
+                                                    int eval_mode) {
   const int i = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (i >= G * C) return;
   const int g = i / C, c = i - g * C;
@@ -293,6 +301,13 @@ __global__ __launch_bounds__(256) void k_bn_bwd_fin(const float* __restrict__ pa
   const double iv = invstd[i], mu = mean[i];
   grad[(int64_t)g * ldg + goff_g + c] = (float)sdx;
   grad[(int64_t)g * ldg + goff_b + c] = (float)sdz;
+  if (eval_mode) {  // running statistics are constants: dy = gamma * invstd * dz, conv bias grad = sum dy
+    if (goff_convb >= 0) grad[(int64_t)g * ldg + goff_convb + c] = (float)(gm * iv * sdz);
+    coef[i * 3 + 0] = (float)(gm * iv);
+    coef[i * 3 + 1] = 0.f;
+    coef[i * 3 + 2] = 0.f;
+    return;
+  }
   if (goff_convb >= 0) grad[(int64_t)g * ldg + goff_convb + c] = 0.f;
   // dy = gm*iv*(dz - sdz/N - xhat*sdx/N), xhat = (y - mu)*iv
   const double A = gm * iv;
@@ -378,7 +393,7 @@ __global__ __launch_bounds__(256) void k_bn_bwd_dx(BwdSrc s, const float* __rest
 void bn_bwd(int pool, uintptr_t y, uintptr_t dsrc, uintptr_t pout, uintptr_t amax, uintptr_t scale, uintptr_t shift,
             uintptr_t mean, uintptr_t invstd, int NB, int B, int D, int H, int W, int C, uintptr_t part, int nchunk,
             uintptr_t theta, int64_t ldt, int64_t off_g, uintptr_t grad, int64_t ldg, int64_t goff_g, int64_t goff_b,
-            int64_t goff_convb, uintptr_t coef, uintptr_t dy, uintptr_t stream) {
+            int64_t goff_convb, uintptr_t coef, uintptr_t dy, int eval_mode, uintptr_t stream) {
   NIDT_REQUIRE(C % 8 == 0 && C <= 256, "bn_bwd: C");
   BwdSrc s{ptr<const uint16_t>(y), ptr<const uint16_t>(dsrc), ptr<const uint16_t>(pout), ptr<const uint8_t>(amax),
            ptr<const float>(scale), ptr<const float>(shift), ptr<const float>(mean), ptr<const float>(invstd),
@@ -392,7 +407,7 @@ void bn_bwd(int pool, uintptr_t y, uintptr_t dsrc, uintptr_t pout, uintptr_t ama
   const double Ncount = (double)B * D * H * W;
   hipLaunchKernelGGL(k_bn_bwd_fin, dim3(ceil_div(G * C, 4)), dim3(256), 0, st, ptr<const float>(part), nchunk, G, C,
                      Ncount, ptr<const float>(mean), ptr<const float>(invstd), ptr<const float>(theta), ldt, off_g,
-                     ptr<float>(grad), ldg, goff_g, goff_b, goff_convb, ptr<float>(coef));
+                     ptr<float>(grad), ldg, goff_g, goff_b, goff_convb, ptr<float>(coef), eval_mode);
   NIDT_CHECK(hipGetLastError());
   NIDT_REQUIRE((int64_t)D * H * W * C < (1ll << 31), "bn_bwd: per-sample tensor too large for 32-bit offsets");
   const int S = D * H * W, npl = 256 / (C / 8);

@@ -536,7 +536,7 @@ __global__ __launch_bounds__(64 * kFinW) void k_conv1_wgrad_fin(const float* __r
                                                          const float* __restrict__ invstd, const float* theta,
                                                          int64_t ldt, int64_t off_g, float* grad, int64_t ldg,
                                                          int64_t goff_w, int64_t goff_bias, int64_t goff_g,
-                                                         int64_t goff_b, float wscale) {
+                                                         int64_t goff_b, float wscale, const float* __restrict__ emean) {
   __shared__ double red[2];
   __shared__ double sD, sdg;
   __shared__ double wpart[kFinW][128];
@@ -590,24 +590,26 @@ __global__ __launch_bounds__(64 * kFinW) void k_conv1_wgrad_fin(const float* __r
   const double gm = theta[(int64_t)g * ldt + off_g + c];
   const double muk = k < 125 ? mu[(int64_t)g * 125 + k] : 0.0;
   const double wk = k < 125 ? w125[(int64_t)i * 125 + k] : 0.0;
-  const double r = k < 125 ? S - D * muk : 0.0;
+  // eval mode (emean != null, running statistics): y = w.p + b, z = gamma*(y - rm)*iv + beta, so
+  // dW = gamma*iv*S, dbias = gamma*iv*D, dgamma = iv*(w.S - D*(rm - b)) with emean = rm - b
+  const bool ev = emean != nullptr;
+  const double r = k < 125 ? (ev ? S : S - D * muk) : 0.0;
   double v = wk * r;
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   if ((k & 63) == 0) red[k >> 6] = v;
   __syncthreads();
-  if (k == 0) sdg = iv * (red[0] + red[1]);
+  if (k == 0) sdg = ev ? iv * (red[0] + red[1] - D * (double)emean[i]) : iv * (red[0] + red[1]);
   __syncthreads();
   const double dg = sdg;
   if (k < 125) {
-    const double cw = covw[(int64_t)i * 125 + k];
-    const double dw = gm * iv * (r - dg * iv * cw);
+    const double dw = ev ? gm * iv * r : gm * iv * (r - dg * iv * covw[(int64_t)i * 125 + k]);
     grad[(int64_t)g * ldg + goff_w + (int64_t)c * 125 + k] = (float)(dw * wscale);
   }
   if (k == 0) {
     grad[(int64_t)g * ldg + goff_g + c] = (float)dg;
     grad[(int64_t)g * ldg + goff_b + c] = (float)D;
-    grad[(int64_t)g * ldg + goff_bias + c] = 0.f;
+    grad[(int64_t)g * ldg + goff_bias + c] = ev ? (float)(gm * iv * D) : 0.f;
   }
 }
 
@@ -747,7 +749,7 @@ int conv1_wgrad_nq(int NB) { return (int64_t)NB * kPD < 4 * 256 * 4 ? 2 : 1; }
 void conv1_wgrad(uintptr_t x8, uintptr_t idx, uintptr_t dp, uintptr_t pout, uintptr_t amax, int NB, int B,
                  uintptr_t part, uintptr_t w125, uintptr_t mu, uintptr_t covw, uintptr_t invstd, uintptr_t theta,
                  int64_t ldt, int64_t off_g, uintptr_t grad, int64_t ldg, int64_t goff_w, int64_t goff_bias,
-                 int64_t goff_g, int64_t goff_b, float wscale, uintptr_t stream) {
+                 int64_t goff_g, int64_t goff_b, float wscale, uintptr_t emean, uintptr_t stream) {
   hipStream_t s = as_stream(stream);
   const int nq = conv1_wgrad_nq(NB);
   hipLaunchKernelGGL(k_conv1_wgrad_split, dim3(kPD * NB * nq), dim3(256), 0, s, ptr<const uint8_t>(x8),
@@ -759,7 +761,7 @@ void conv1_wgrad(uintptr_t x8, uintptr_t idx, uintptr_t dp, uintptr_t pout, uint
   hipLaunchKernelGGL(k_conv1_wgrad_fin, dim3(kC1, G), dim3(64 * kFinW), 0, s, ptr<const float>(part), B * nq,
                      ptr<const float>(w125), ptr<const float>(mu), ptr<const float>(covw), ptr<const float>(invstd),
                      ptr<const float>(theta), ldt, off_g, ptr<float>(grad), ldg, goff_w, goff_bias, goff_g, goff_b,
-                     wscale);
+                     wscale, ptr<const float>(emean));
   NIDT_CHECK(hipGetLastError());
 }
 

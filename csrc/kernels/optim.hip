@@ -160,6 +160,176 @@ void clip_sgd_mask(uintptr_t w, uintptr_t g, uintptr_t buf, uintptr_t mask, uint
   NIDT_CHECK(hipGetLastError());
 }
 
+// ------------------------------------------------------------------------------------------------
+// Generalised fused local step for every algorithm of the harness, per client row c:
+//   g' = g * m_c            (mask_mode GRAD: SubAvg masks gradients before clipping, subavg/my_model_trainer.py:66-68)
+//   g' += mu * (w - ref_c)  (FedProx proximal gradient, inside the clipped norm like a loss term)
+//   coef = min(1, max_norm / (||g'|| + 1e-6));  d = coef g' + wd w;  buf = mom buf + d (buf zeroed at round start)
+//   w -= lr d
+//   w -= lr * lamda * (w - pref_c)   (Ditto personal pull after the step, ditto/my_model_trainer.py:63-64)
+//   w *= m_c                (mask_mode WEIGHT: SalientGrads / DisPFL re-zero masked weights, Q2)
+// Masks are bit rows (uint32 words, bit i of word i>>5); mstride = 0 shares one mask row between all clients
+// (SalientGrads' global SNIP mask).  ref/pref row strides may be 0 (w_global shared by every client).
+struct LocalOpt {
+  float* w; float* g; float* buf; int64_t ld;
+  const uint32_t* mbits; int64_t mstride;
+  const float* ref; int64_t ref_ld; float mu;
+  const float* pref; int64_t pref_ld; float lamda;
+  float lr, wd, mom, max_norm;
+  const float* lr_dev;
+  int keep_grad;
+};
+
+enum { kMaskNone = 0, kMaskWeight = 1, kMaskGrad = 2 };
+
+template <int MASK>
+__device__ __forceinline__ uint32_t mask4(const LocalOpt& a, int c, int64_t i) {
+  if (MASK == kMaskNone) return 0xfu;
+  return (a.mbits[(int64_t)c * a.mstride + (i >> 5)] >> (i & 31)) & 0xfu;
+}
+
+template <int MASK>
+__global__ __launch_bounds__(kOptThreads) void k_local_sqnorm(LocalOpt a, int64_t P, int64_t chunk,
+                                                              float* __restrict__ part, int nblk) {
+  __shared__ float red[kOptThreads / 64];
+  const int c = blockIdx.y;
+  const int64_t s = (int64_t)blockIdx.x * chunk;
+  const int64_t e = s + chunk < P ? s + chunk : P;
+  const float* gr = a.g + (int64_t)c * a.ld;
+  const float* wr = a.w + (int64_t)c * a.ld;
+  const float* rr = a.mu != 0.f ? a.ref + (int64_t)c * a.ref_ld : nullptr;
+  float acc = 0.f;
+  const int64_t e4 = s + ((e - s) & ~int64_t(3));
+  for (int64_t i = s + 4 * threadIdx.x; i < e4; i += 4 * kOptThreads) {
+    const float4 gv = *reinterpret_cast<const float4*>(gr + i);
+    float gg[4] = {gv.x, gv.y, gv.z, gv.w};
+    if (MASK == kMaskGrad) {
+      const uint32_t m = mask4<MASK>(a, c, i);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) gg[j] = ((m >> j) & 1u) ? gg[j] : 0.f;
+    }
+    if (rr) {
+      const float4 wv = *reinterpret_cast<const float4*>(wr + i), rv = *reinterpret_cast<const float4*>(rr + i);
+      gg[0] = fmaf(a.mu, wv.x - rv.x, gg[0]); gg[1] = fmaf(a.mu, wv.y - rv.y, gg[1]);
+      gg[2] = fmaf(a.mu, wv.z - rv.z, gg[2]); gg[3] = fmaf(a.mu, wv.w - rv.w, gg[3]);
+    }
+    acc += gg[0] * gg[0] + gg[1] * gg[1] + gg[2] * gg[2] + gg[3] * gg[3];
+  }
+  for (int64_t i = e4 + threadIdx.x; i < e; i += kOptThreads) {
+    float gj = gr[i];
+    if (MASK == kMaskGrad && !((a.mbits[(int64_t)c * a.mstride + (i >> 5)] >> (i & 31)) & 1u)) gj = 0.f;
+    if (rr) gj = fmaf(a.mu, wr[i] - rr[i], gj);
+    acc += gj * gj;
+  }
+  const float t = block_sum(acc, red);
+  if (threadIdx.x == 0) part[(int64_t)c * nblk + blockIdx.x] = t;
+}
+
+template <int MASK, bool HAS_MOM>
+__global__ __launch_bounds__(kOptThreads) void k_local_step(LocalOpt a, const float* __restrict__ part, int nblk,
+                                                            int64_t P, int64_t chunk) {
+  __shared__ float red[kOptThreads / 64];
+  const int c = blockIdx.y;
+  const float lr = a.lr_dev ? *a.lr_dev : a.lr;
+  float t = 0.f;
+  for (int i = threadIdx.x; i < nblk; i += kOptThreads) t += part[(int64_t)c * nblk + i];
+  t = block_sum(t, red);
+  float coef = a.max_norm / (sqrtf(t) + 1e-6f);
+  coef = coef < 1.f ? coef : 1.f;
+  const int64_t s = (int64_t)blockIdx.x * chunk;
+  const int64_t e = s + chunk < P ? s + chunk : P;
+  float* wr = a.w + (int64_t)c * a.ld;
+  float* gr = a.g + (int64_t)c * a.ld;
+  float* br = HAS_MOM ? a.buf + (int64_t)c * a.ld : nullptr;
+  const float* rr = a.mu != 0.f ? a.ref + (int64_t)c * a.ref_ld : nullptr;
+  const float* pr = a.lamda != 0.f ? a.pref + (int64_t)c * a.pref_ld : nullptr;
+  const float pull = lr * a.lamda;
+  auto one = [&](float& ww, float& gg, float& bb, float rv, float pv, bool m) {
+    float gj = (MASK == kMaskGrad && !m) ? 0.f : gg;
+    if (rr) gj = fmaf(a.mu, ww - rv, gj);
+    gj *= coef;
+    gg = gj;
+    float d = fmaf(a.wd, ww, gj);
+    if (HAS_MOM) {
+      bb = fmaf(a.mom, bb, d);
+      d = bb;
+    }
+    ww = fmaf(-lr, d, ww);
+    if (pr) ww = fmaf(-pull, ww - pv, ww);
+    if (MASK == kMaskWeight && !m) ww = 0.f;
+  };
+  const int64_t e4 = s + ((e - s) & ~int64_t(3));
+  for (int64_t i = s + 4 * threadIdx.x; i < e4; i += 4 * kOptThreads) {
+    const float4 gv = *reinterpret_cast<const float4*>(gr + i);
+    const float4 wv = *reinterpret_cast<const float4*>(wr + i);
+    float gg[4] = {gv.x, gv.y, gv.z, gv.w}, ww[4] = {wv.x, wv.y, wv.z, wv.w};
+    float bb[4] = {0.f, 0.f, 0.f, 0.f}, rv[4] = {0.f, 0.f, 0.f, 0.f}, pv[4] = {0.f, 0.f, 0.f, 0.f};
+    if (HAS_MOM) {
+      const float4 v = *reinterpret_cast<const float4*>(br + i);
+      bb[0] = v.x; bb[1] = v.y; bb[2] = v.z; bb[3] = v.w;
+    }
+    if (rr) {
+      const float4 v = *reinterpret_cast<const float4*>(rr + i);
+      rv[0] = v.x; rv[1] = v.y; rv[2] = v.z; rv[3] = v.w;
+    }
+    if (pr) {
+      const float4 v = *reinterpret_cast<const float4*>(pr + i);
+      pv[0] = v.x; pv[1] = v.y; pv[2] = v.z; pv[3] = v.w;
+    }
+    const uint32_t m = mask4<MASK>(a, c, i);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) one(ww[j], gg[j], bb[j], rv[j], pv[j], (m >> j) & 1u);
+    if (a.keep_grad) *reinterpret_cast<float4*>(gr + i) = make_float4(gg[0], gg[1], gg[2], gg[3]);
+    *reinterpret_cast<float4*>(wr + i) = make_float4(ww[0], ww[1], ww[2], ww[3]);
+    if (HAS_MOM) *reinterpret_cast<float4*>(br + i) = make_float4(bb[0], bb[1], bb[2], bb[3]);
+  }
+  for (int64_t i = e4 + threadIdx.x; i < e; i += kOptThreads) {
+    float ww = wr[i], gg = gr[i], bb = HAS_MOM ? br[i] : 0.f;
+    const bool m = MASK == kMaskNone ? true : ((a.mbits[(int64_t)c * a.mstride + (i >> 5)] >> (i & 31)) & 1u);
+    one(ww, gg, bb, rr ? rr[i] : 0.f, pr ? pr[i] : 0.f, m);
+    if (a.keep_grad) gr[i] = gg;
+    wr[i] = ww;
+    if (HAS_MOM) br[i] = bb;
+  }
+}
+
+void local_opt(uintptr_t w, uintptr_t g, uintptr_t buf, int64_t ld, uintptr_t mbits, int64_t mstride, int mask_mode,
+               uintptr_t ref, int64_t ref_ld, float mu, uintptr_t pref, int64_t pref_ld, float lamda, uintptr_t part,
+               int64_t C, int64_t P, float lr, float wd, float mom, float max_norm, uintptr_t lr_dev, int keep_grad,
+               uintptr_t stream) {
+  NIDT_REQUIRE(ld % 4 == 0 && ld >= P, "local_opt: row stride must be >= P and a multiple of 4");
+  NIDT_REQUIRE((w & 15) == 0 && (g & 15) == 0 && (buf & 15) == 0, "local_opt: 16-byte alignment");
+  NIDT_REQUIRE(mask_mode == kMaskNone || (mbits != 0 && mstride % 4 == 0 && (mbits & 15) == 0), "local_opt: mask");
+  NIDT_REQUIRE(mu == 0.f || (ref != 0 && ref_ld % 4 == 0 && (ref & 15) == 0), "local_opt: prox reference");
+  NIDT_REQUIRE(lamda == 0.f || (pref != 0 && pref_ld % 4 == 0 && (pref & 15) == 0), "local_opt: pull reference");
+  if (C == 0) return;
+  LocalOpt a{ptr<float>(w), ptr<float>(g), ptr<float>(buf), ld, ptr<const uint32_t>(mbits), mstride,
+             ptr<const float>(ref), ref_ld, mu, ptr<const float>(pref), pref_ld, lamda, lr, wd, mom, max_norm,
+             ptr<const float>(lr_dev), keep_grad};
+  int nblk;
+  const int64_t chunk = opt_chunk(P, &nblk);
+  hipStream_t st = as_stream(stream);
+  dim3 grid(nblk, (unsigned)C);
+  if (mask_mode == kMaskGrad)
+    hipLaunchKernelGGL(k_local_sqnorm<kMaskGrad>, grid, dim3(kOptThreads), 0, st, a, P, chunk, ptr<float>(part), nblk);
+  else
+    hipLaunchKernelGGL(k_local_sqnorm<kMaskNone>, grid, dim3(kOptThreads), 0, st, a, P, chunk, ptr<float>(part), nblk);
+  const bool hm = buf != 0 && mom != 0.f;
+#define NIDT_LS(M, MO)                                                                                            \
+  hipLaunchKernelGGL((k_local_step<M, MO>), grid, dim3(kOptThreads), 0, st, a, ptr<const float>(part), nblk, P, chunk)
+  switch (mask_mode * 2 + (hm ? 1 : 0)) {
+    case 0: NIDT_LS(kMaskNone, false); break;
+    case 1: NIDT_LS(kMaskNone, true); break;
+    case 2: NIDT_LS(kMaskWeight, false); break;
+    case 3: NIDT_LS(kMaskWeight, true); break;
+    case 4: NIDT_LS(kMaskGrad, false); break;
+    case 5: NIDT_LS(kMaskGrad, true); break;
+    default: NIDT_REQUIRE(false, "local_opt: mask_mode");
+  }
+#undef NIDT_LS
+  NIDT_CHECK(hipGetLastError());
+}
+
 // ---- weighted reduction over the client axis: out[p] = sum_c wts[c] * rows[c, p] (+ beta*out) ----
 __global__ __launch_bounds__(256) void k_weighted_rows_sum(const float* __restrict__ rows, const float* __restrict__ wts,
                                                            int C, int64_t P, int64_t stride, float beta,

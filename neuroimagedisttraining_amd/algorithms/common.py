@@ -129,10 +129,15 @@ class APIBase:
         self.logger = logger or log
         self.device = device
         self.args = args
-        (self.train_data_num_in_total, self.test_data_num_in_total, self.train_global, self.test_global,
-         self.train_data_local_num_dict, self.train_data_local_dict, self.test_data_local_dict,
-         self.class_counts) = dataset[:8]
-        self.val_data_local_dict = dataset[8] if len(dataset) > 8 else None
+        if len(dataset) > 8:  # 9-tuple of the val loaders: (..., num, train, val, test, class_num)
+            (self.train_data_num_in_total, self.test_data_num_in_total, self.train_global, self.test_global,
+             self.train_data_local_num_dict, self.train_data_local_dict, self.val_data_local_dict,
+             self.test_data_local_dict, self.class_counts) = dataset[:9]
+        else:
+            (self.train_data_num_in_total, self.test_data_num_in_total, self.train_global, self.test_global,
+             self.train_data_local_num_dict, self.train_data_local_dict, self.test_data_local_dict,
+             self.class_counts) = dataset[:8]
+            self.val_data_local_dict = None
         self.model_trainer = model_trainer
         self.client_list = []
         self._setup_clients()

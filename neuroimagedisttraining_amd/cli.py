@@ -191,7 +191,8 @@ def load_data(args, dataset_name, logger=None):
         n = getattr(args, "synthetic_size", 0) or None
         return images.load_partition_data(dataset_name, args.data_dir, args.partition_method, args.partition_alpha,
                                           args.client_num_in_total, args.batch_size, logger, seed=args.seed,
-                                          with_val=False, n_train=n, n_test=n // 5 if n else None)
+                                          with_val=getattr(args, "algo", "") == "fedfomo", n_train=n,
+                                          n_test=n // 5 if n else None)
     if dataset_name == "synthetic":
         return images.load_partition_data_synthetic_tabular(args.client_num_in_total, args.batch_size)
     raise ValueError(dataset_name)

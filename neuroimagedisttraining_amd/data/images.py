@@ -93,8 +93,9 @@ def load_partition_data(dataset, data_dir, partition_method, partition_alpha, cl
         if with_val:
             val[c] = _loader(xtr, ytr, val_map[c], batch_size, False)
         logger.info("client_idx = %d, local_train_sample_number = %d", c, num[c])
-    out = [None, None, None, None, num, trn, tst, n_cls]
-    return out + [val] if with_val else out
+    if with_val:  # reference 9-tuple order: (..., num, train, val, test, class_num) (cifar10/data_val_loader.py:325)
+        return [None, None, None, None, num, trn, val, tst, n_cls]
+    return [None, None, None, None, num, trn, tst, n_cls]
 
 
 def load_partition_data_cifar10(data_dir, partition_method, partition_alpha, client_number, batch_size, logger=None,

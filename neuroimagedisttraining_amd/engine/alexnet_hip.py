@@ -136,7 +136,8 @@ class HipAlexNet3D:
                           _p(b["w%dt" % ci]) if train else 0, st)
 
     def _bn(self, ci, bi, C, G, B, sp, theta, bufs, b, train):
-        """BN coefficients for conv ``ci`` (train: from the conv epilogue stats; eval: running stats)."""
+        """BN coefficients for conv ``ci`` (train: from the conv epilogue stats; eval: running stats, which also
+        leaves the running mean / invstd in ``m``/``i`` for an eval-mode backward)."""
         m, st = self.m, torch.cuda.current_stream().cuda_stream
         P, Q = theta.stride(0), bufs.stride(0)
         og, ob = self.o["features.%d.weight" % bi], self.o["features.%d.bias" % bi]
@@ -149,10 +150,12 @@ class HipAlexNet3D:
                           _p(b["i%d" % ci]), 1, st)
         else:
             m.bn_eval(G, C, _p(theta), P, og, ob, _p(bufs), Q, orm, orv, BN_EPS, _p(b["s%d" % ci]),
-                      _p(b["t%d" % ci]), st)
+                      _p(b["t%d" % ci]), _p(b["m%d" % ci]), _p(b["i%d" % ci]), st)
 
-    def forward(self, theta, bufs, x8, mom, idx, G, B, train):
-        """Runs the forward; returns the scratch dict (logits in ``b['logits']``)."""
+    def forward(self, theta, bufs, x8, mom, idx, G, B, train, bn_train=None):
+        """Runs the forward; returns the scratch dict (logits in ``b['logits']``).  ``train`` keeps what the backward
+        needs; ``bn_train`` (default = ``train``) selects batch statistics (+ running-stat update) vs running stats."""
+        bn_train = train if bn_train is None else bn_train
         assert theta.stride(1) == 1 and bufs.stride(1) == 1 and theta.shape[0] == G and bufs.shape[0] == G
         assert theta.shape[1] == self.P and bufs.shape[1] == self.Q and theta.dtype == torch.float32
         assert idx.dtype == torch.int32 and idx.numel() == G * B and x8.dtype == torch.uint8
@@ -163,7 +166,7 @@ class HipAlexNet3D:
         P, Q = theta.stride(0), bufs.stride(0)
         self._pack(theta, G, b, train)
         # ---- conv1 + BN1 + ReLU + pool1 ----
-        if train:
+        if bn_train:
             assert mom is not None and mom.dtype == torch.float64 and mom.shape[1] == NM
             m.conv1_bnstats(_p(mom), _p(idx), B, G, _p(b["Mb"]), _p(b["w125"]), _p(theta), P,
                             self.o["features.0.bias"], self.o["features.1.weight"], self.o["features.1.bias"],
@@ -173,43 +176,49 @@ class HipAlexNet3D:
         else:
             m.bn_eval(G, 64, _p(theta), P, self.o["features.1.weight"], self.o["features.1.bias"], _p(bufs), Q,
                       self.ob["features.1.running_mean"], self.ob["features.1.running_var"], BN_EPS, _p(b["s1"]),
-                      _p(b["t1"]), st)
+                      _p(b["t1"]), _p(b["m1"]), _p(b["i1"]), st)
             ob = self.o["features.0.bias"]
             b["t1"].add_(b["s1"] * theta[:, ob:ob + 64])  # fold conv1 bias: the kernel convolves without it
         m.conv1_fwd_pool(_p(x8), _p(idx), _p(b["w1p"]), _p(b["s1"]), _p(b["t1"]), NB, B, _p(b["p1"]), _p(b["a1"]), st)
         # ---- conv2 + BN2 + ReLU + pool2 ----
         ci, bi, cin, cout, pad, sp = L2
-        self._conv(b, "ksf4", b["p1"], b["w4p"], b["bias4"], b["y2"], b["st4"] if train else None,
+        self._conv(b, "ksf4", b["p1"], b["w4p"], b["bias4"], b["y2"], b["st4"] if bn_train else None,
                    G, B, 19, 23, 19, 64, 128, 0, st, theta, 4)
-        self._bn(4, 5, 128, G, B, (17, 21, 17), theta, bufs, b, train)
+        self._bn(4, 5, 128, G, B, (17, 21, 17), theta, bufs, b, bn_train)
         m.bn_relu_pool(_p(b["y2"]), _p(b["s4"]), _p(b["t4"]), _p(b["p2"]), _p(b["a2"]), NB, B, 17, 21, 17, 128, st)
         # ---- conv3 ----
-        self._conv(b, "ksf8", b["p2"], b["w8p"], b["bias8"], b["y3"], b["st8"] if train else None,
+        self._conv(b, "ksf8", b["p2"], b["w8p"], b["bias8"], b["y3"], b["st8"] if bn_train else None,
                    G, B, 5, 7, 5, 128, 192, 1, st, theta, 8)
-        self._bn(8, 9, 192, G, B, (5, 7, 5), theta, bufs, b, train)
+        self._bn(8, 9, 192, G, B, (5, 7, 5), theta, bufs, b, bn_train)
         # BN3+ReLU materialised once (read by conv4 fwd and by conv4's wgrad im2col 27x)
         m.bn_relu_apply(_p(b["y3"]), _p(b["s8"]), _p(b["t8"]), _p(b["h3"]), NB * 175, 192, B * 175, st)
         # ---- conv4 ----
-        self._conv(b, "ksf11", b["h3"], b["w11p"], b["bias11"], b["y4"], b["st11"] if train else None,
+        self._conv(b, "ksf11", b["h3"], b["w11p"], b["bias11"], b["y4"], b["st11"] if bn_train else None,
                    G, B, 5, 7, 5, 192, 192, 1, st, theta, 11)
-        self._bn(11, 12, 192, G, B, (5, 7, 5), theta, bufs, b, train)
+        self._bn(11, 12, 192, G, B, (5, 7, 5), theta, bufs, b, bn_train)
         m.bn_relu_apply(_p(b["y4"]), _p(b["s11"]), _p(b["t11"]), _p(b["h4"]), NB * 175, 192, B * 175, st)
         # ---- conv5 + BN5 + ReLU + pool ----
-        self._conv(b, "ksf14", b["h4"], b["w14p"], b["bias14"], b["y5"], b["st14"] if train else None,
+        self._conv(b, "ksf14", b["h4"], b["w14p"], b["bias14"], b["y5"], b["st14"] if bn_train else None,
                    G, B, 5, 7, 5, 192, 128, 1, st, theta, 14)
-        self._bn(14, 15, 128, G, B, (5, 7, 5), theta, bufs, b, train)
+        self._bn(14, 15, 128, G, B, (5, 7, 5), theta, bufs, b, bn_train)
         m.bn_relu_pool(_p(b["y5"]), _p(b["s14"]), _p(b["t14"]), _p(b["p5"]), _p(b["a5"]), NB, B, 5, 7, 5, 128, st)
         return b
 
     # ---------------------------------------------------------------------------------------------
-    def train_step(self, theta, bufs, grads, x8, mom, idx, labels, G, B, keep=0.5, seed=0, cids=None, seed_dev=None):
+    def train_step(self, theta, bufs, grads, x8, mom, idx, labels, G, B, keep=0.5, seed=0, cids=None, seed_dev=None,
+                   bn_train=True):
         """Forward + backward for G clients; writes ``grads`` [G,P], updates BN running stats in ``bufs``.
         Returns the per-client mean loss tensor [G] (device).  ``seed_dev`` (int64 device scalar, optional) is
-        added to ``seed`` inside the kernel, so a captured hipGraph can advance the dropout stream on device."""
+        added to ``seed`` inside the kernel, so a captured hipGraph can advance the dropout stream on device.
+        ``bn_train=False``: gradient of the model in ``eval()`` mode (running-stat BN, no dropout, no running-stat
+        update) — DisPFL's ``screen_gradients`` (``DisPFL/my_model_trainer.py:166-189``)."""
         assert grads.shape == theta.shape and grads.stride(1) == 1 and grads.stride(0) == theta.stride(0)
         assert labels.dtype == torch.float32 and labels.numel() == G * B and B <= 32
         m, st = self.m, torch.cuda.current_stream().cuda_stream
-        b = self.forward(theta, bufs, x8, mom, idx, G, B, True)
+        if not bn_train:
+            keep = 1.0
+        ev = 0 if bn_train else 1
+        b = self.forward(theta, bufs, x8, mom, idx, G, B, True, bn_train=bn_train)
         NB = G * B
         P = theta.stride(0)
         o = self.o
@@ -222,7 +231,7 @@ class HipAlexNet3D:
             m.bn_bwd(pool, _p(y), _p(dsrc), _p(pout), _p(amax), _p(b["s%d" % ci]), _p(b["t%d" % ci]),
                      _p(b["m%d" % ci]), _p(b["i%d" % ci]), NB, B, sp[0], sp[1], sp[2], C, _p(b["bnpart"]), nchunk,
                      _p(theta), P, o["features.%d.weight" % bi], _p(grads), P, o["features.%d.weight" % bi],
-                     o["features.%d.bias" % bi], o["features.%d.bias" % ci], _p(b["coef"]), _p(dy), st)
+                     o["features.%d.bias" % bi], o["features.%d.bias" % ci], _p(b["coef"]), _p(dy), ev, st)
 
         def wgrad(ci, x, xs, xt, dy, sp, cin, cout, pad):
             m.conv3d_wgrad(_p(x), _p(xs), _p(xt), _p(dy), _p(b["wgpart"]), _p(grads), P, o["features.%d.weight" % ci],
@@ -244,11 +253,15 @@ class HipAlexNet3D:
         bn_bwd(1, 4, 5, 128, (17, 21, 17), b["dx3"], b["p2"], b["a2"], b["dy2"], b["y2"])
         wgrad(4, b["p1"], None, None, b["dy2"], (19, 23, 19), 64, 128, 0)
         self._conv(b, "ksd4", b["dy2"], b["w4t"], None, b["dp1"], None, G, B, 17, 21, 17, 128, 64, 2, st)
-        # layer 1: sparse wgrad through pool1/ReLU/BN1 (closed form)
+        # layer 1: sparse wgrad through pool1/ReLU/BN1 (closed form; eval mode: running mean minus the conv bias)
+        emean = None
+        if not bn_train:
+            ob1 = o["features.0.bias"]
+            emean = (b["m1"] - theta[:, ob1:ob1 + 64]).contiguous()
         m.conv1_wgrad(_p(x8), _p(idx), _p(b["dp1"]), _p(b["p1"]), _p(b["a1"]), NB, B, _p(b["c1part"]), _p(b["w125"]),
                       _p(b["mu"]), _p(b["covw"]), _p(b["i1"]), _p(theta), P, o["features.1.weight"], _p(grads), P,
                       o["features.0.weight"], o["features.0.bias"], o["features.1.weight"], o["features.1.bias"],
-                      1.0 / 255.0, st)
+                      1.0 / 255.0, _p(emean), st)
         return b["loss"]
 
     def eval_logits(self, theta, bufs, x8, idx, G, B):

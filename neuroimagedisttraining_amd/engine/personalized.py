@@ -1,0 +1,610 @@
+"""Personalized and decentralized FL algorithms on the client-batched executor (HIP kernels on MI355X).
+
+Every algorithm of the reference harness besides SalientGrads / FedAvg runs here with the same building blocks as
+:class:`~.runner.FLRunner`: client rows resident on the GPU, lockstep local steps (hipGraphs), the fused optimizer
+(per-client bit masks in weight or gradient mode, Ditto's pull), per-(client, layer) mask kernels, and RCCL for
+everything that crosses ranks (all-reduce of partial sums, point-to-point neighbour rows, metric gathers).
+
+* :class:`DisPFLRunner`  — ``DisPFL/dispfl_api.py:46-184``, ``DisPFL/client.py:32-99``: ERK / uniform per-client
+  masks over all parameters, masked local training, eval-mode ``screen_gradients``, cosine-annealed fire (smallest
+  |w| among active) + regrow (largest |g| among inactive, or random) per layer on device (K15), mask Hamming
+  bookkeeping (K18), client dropout ``--active``.  Neighbour aggregation is commented out in the reference (Q10),
+  so every client continues its own model; ``dispfl_aggregate`` enables the masked neighbour average.
+* :class:`SubAvgRunner`  — ``subavg/subavg_api.py:43-139``, ``subavg/client.py:36-63``: gradient-masked training,
+  ``fake_prune`` percentiles at the first and last epoch (K16), prune when the mask moved and the pruned model is
+  accurate enough on the local training data, server average of each coordinate over the clients keeping it.
+* :class:`DittoRunner`   — ``ditto/ditto_api.py:40-105``: FedAvg global model + personal models pulled towards the
+  round's global model after every step (fused in the optimizer, K20).
+* :class:`DPSGDRunner`   — ``dpsgd/dpsgd_api.py:41-178``: neighbour averaging (ring / random / full) as one row-mixing
+  launch, neighbours on other ranks fetched point-to-point, global mean for evaluation, fine-tune every 100 rounds.
+* :class:`FedFomoRunner` — ``fedfomo/fedfomo_api.py:53-217``: first-order model optimisation — validation losses of
+  the candidate models (grouped evaluation launches), parameter distances (one kernel over all pairs), affinity-driven
+  neighbour choice and the weighted neighbour update (row mixing).
+* :class:`LocalRunner`   — ``local/local_api.py:51-84``: local-only training.
+
+Host-side random decisions (client dropout, neighbour choice) are drawn from dedicated generators on every rank in
+the reference's order, so all ranks agree without communication.
+"""
+from __future__ import annotations
+
+import math
+import random
+import time
+from dataclasses import replace
+
+import numpy as np
+import torch
+
+from ..algorithms import sparse as SP
+from ..parallel import runtime as rt
+from . import masks as MK
+from .executor import padded_rows
+from .runner import MASK_GRAD, MASK_WEIGHT, FLRunner, RowSet, StepSpec
+
+
+def _sparsities(params, dense_ratio, cfg):
+    dist = "uniform" if cfg.uniform else "ERK"
+    return SP.erk_sparsities(params, dense_ratio, erk_power_scale=cfg.erk_power_scale, distribution=dist)
+
+
+class PersonalizedRunner(FLRunner):
+    """Shared machinery: personal rows, per-client mask bit rows, neighbour row exchange, local evaluations."""
+
+    def __init__(self, engine, splits, cfg, info, template_model, logger=None, algorithm="local"):
+        super().__init__(engine, splits, cfg, info, template_model, logger, algorithm)
+        self.mspace = MK.MaskSpace(engine.players)  # masks cover every parameter (the reference's named_parameters)
+        self.mbits = None
+        self.np_rng = np.random.RandomState(cfg.seed)
+        self.py_rng = random.Random(cfg.seed)
+        for k in ("old_mask_test_acc", "new_mask_test_acc", "test_acc", "test_loss", "mask_dis_matrix"):
+            self.stat_info.setdefault(k, [])
+        self.rowset = RowSet(self.theta, self.bufs)
+
+    # ---------------------------------------------------------------------------------------------- helpers
+    def all_rows(self):
+        return list(range(self.C)), list(self.local)
+
+    def snapshot(self, rs=None):
+        rs = rs or self.rowset
+        return RowSet(rs.theta.clone(), rs.bufs.clone())
+
+    def fetch(self, needs, src):
+        """{client: (theta_row [P], bufs_row [Q])} for every client in ``needs[self.rank]``: local clients are views
+        of ``src``, remote ones arrive point-to-point from their owners (same ``needs`` on every rank)."""
+        P, Q = self.P, self.Q
+        recv = rt.exchange_rows(self.info, self.owner, needs,
+                                lambda c: torch.cat([src.theta[self.row_of[c], :P], src.bufs[self.row_of[c], :Q]]),
+                                P + Q, self.device)
+        out = {}
+        for c in needs[self.info.rank]:
+            if c in self.row_of:
+                out[c] = (src.theta[self.row_of[c]], src.bufs[self.row_of[c]])
+            else:
+                v = recv[c]
+                out[c] = (v[:P], v[P:])
+        return out
+
+    def pool(self, entries):
+        """Stack (theta_row, bufs_row) pairs into a fresh row set (16-B aligned rows for the kernels)."""
+        th = padded_rows(max(1, len(entries)), self.P, self.device)
+        bu = padded_rows(max(1, len(entries)), self.Q, self.device)
+        for i, (t, b) in enumerate(entries):
+            th[i].copy_(t[:self.P])
+            bu[i].copy_(b[:self.Q])
+        return RowSet(th, bu)
+
+    def eval_local(self, rs, rows, clients, which="test"):
+        """[N, 3] (correct, loss_sum, total) of model rows[j] on clients[j] (this rank's part), gathered."""
+        res = self.eval_grouped(rs.theta, rs.bufs, rows, clients, which) if rows else np.zeros((0, 3))
+        return self.gather_metrics(clients, res)
+
+    def log_test(self, r, key=None, tag="test"):
+        acc, loss = self.mean_acc_loss(r)
+        if key:
+            self.stat_info[key].append(acc)
+        if self.log is not None and self.info.is_main:
+            self.log.info({"%s_acc" % tag: acc, "%s_loss" % tag: loss})
+        return acc, loss
+
+    def count_nonzero_rows(self, rs, rows):
+        """count_communication_params of whole states (params + buffers) per row (host ints)."""
+        if not rows:
+            return np.zeros(0, dtype=np.int64)
+        ix = torch.tensor(rows, device=self.device)
+        nz = torch.count_nonzero(rs.theta[ix], dim=1) + torch.count_nonzero(rs.bufs[ix], dim=1)
+        return nz.cpu().numpy().astype(np.int64)
+
+    def local_masks_from(self, per_client_float):
+        """list of N flat float masks [P] (host or device) -> this rank's bit rows [C, W]."""
+        m = torch.stack([per_client_float[c].to(self.device) for c in self.local]) if self.C else \
+            torch.zeros((1, self.P), device=self.device)
+        return MK.pack_bits(m)
+
+    def flat_mask(self, named_masks):
+        """{name: tensor} mask dict -> flat [P] float (ones for names without a mask)."""
+        lay = self.e.players
+        out = torch.ones(self.P, dtype=torch.float32)
+        for i, n in enumerate(lay.names):
+            if n in named_masks:
+                out[lay.offsets[i]:lay.offsets[i] + lay.numel(i)] = named_masks[n].reshape(-1).float().cpu()
+        return out
+
+    def finish(self):
+        return None
+
+    def train(self):
+        for r in range(self.cfg.comm_round):
+            self.run_round(r)
+        self.finish()
+        return self.stat_info
+
+
+# ================================================================================================== Local
+class LocalRunner(PersonalizedRunner):
+    """Local-only baseline: sampled clients continue their own model (``local/local_api.py:51-84``)."""
+
+    def run_round(self, round_idx, sync_timers=False):
+        t0 = time.perf_counter()
+        self._round_start(round_idx)
+        sampled = self.sample_clients(round_idx)
+        rows, loc = self._local_rows(sampled)
+        self.train_rows(self.rowset, rows, loc, round_idx, self.cfg.epochs)
+        t1 = time.perf_counter()
+        self.timers["train"] += t1 - t0
+        self.stat_info["sum_training_flops"] += int(self.cfg.epochs * sum(self.sizes[c] for c in sampled))
+        r = self.eval_local(self.rowset, rows, loc)  # client.train tests right after training (local/client.py)
+        acc, _ = self.log_test(r, "person_test_acc")
+        self.timers["eval"] += time.perf_counter() - t1
+        self.stat_info["round_time"].append(time.perf_counter() - t0)
+        return {"person_test_acc": acc}
+
+
+# ================================================================================================== Ditto
+class DittoRunner(PersonalizedRunner):
+    """FedAvg global model + personal models with the proximal pull ``w -= lr*lamda*(w - w_global)`` after every
+    step for ``local_epochs`` (``ditto/ditto_api.py:40-78``, ``ditto/my_model_trainer.py:38-68``)."""
+
+    def __init__(self, *a, **kw):
+        super().__init__(*a, **kw)
+        self.pers = RowSet(padded_rows(max(1, self.C), self.P, self.device),
+                           padded_rows(max(1, self.C), self.Q, self.device))
+        self.pers.theta.copy_(self.w_global.expand_as(self.pers.theta))
+        self.pers.bufs.copy_(self.b_global.expand_as(self.pers.bufs))
+        self._pull_ref = torch.zeros_like(self.w_global)
+
+    def run_round(self, round_idx, sync_timers=False):
+        t0 = time.perf_counter()
+        self._round_start(round_idx)
+        sampled = self.sample_clients(round_idx)
+        self._pull_ref.copy_(self.w_global)  # the round's global model (deepcopy(w_global) in the reference)
+        self.local_train(round_idx, sampled)  # global-model training from w_global
+        rows, loc = self._local_rows(sampled)
+        spec = StepSpec(lamda=self.cfg.lamda, pref=self._pull_ref)
+        self.train_rows(self.pers, rows, loc, round_idx, self.cfg.local_epochs or self.cfg.epochs, spec, tag=1)
+        t1 = time.perf_counter()
+        self.aggregate(sampled)
+        t2 = time.perf_counter()
+        self.timers["train"] += t1 - t0
+        self.timers["aggregate"] += t2 - t1
+        res = None
+        if self._eval_due(round_idx):
+            r = self.eval_local(self.pers, *self.all_rows())
+            acc, loss = self.log_test(r, "person_test_acc")
+            res = {"person_test_acc": acc, "person_test_loss": loss}
+        self.timers["eval"] += time.perf_counter() - t2
+        self.stat_info["round_time"].append(time.perf_counter() - t0)
+        return res
+
+
+# ================================================================================================== D-PSGD
+class DPSGDRunner(PersonalizedRunner):
+    """Decentralized SGD: every client averages its neighbours' last models, then trains (``dpsgd_api.py:41-103``)."""
+
+    def neighbours(self, round_idx, c):
+        N, K, cs = self.N, max(1, int(self.N * self.cfg.frac)), self.cfg.cs
+        if N == K:
+            return list(range(N))
+        if cs == "random":
+            np.random.seed(round_idx + c)
+            idx = np.random.choice(range(N), min(K, N), replace=False)
+            while c in idx:
+                idx = np.random.choice(range(N), min(K, N), replace=False)
+            nei = list(idx)
+        elif cs == "ring":
+            nei = [(c - 1 + N) % N, (c + 1) % N]
+        elif cs == "full":
+            nei = [j for j in range(N) if j != c]
+        else:
+            raise ValueError("unknown cs %r" % cs)
+        return sorted(int(j) for j in list(nei) + [c])
+
+    def run_round(self, round_idx, sync_timers=False):
+        t0 = time.perf_counter()
+        self._round_start(round_idx)
+        nei = {c: self.neighbours(round_idx, c) for c in range(self.N)}
+        needs = [sorted({j for c in self.shards[r] for j in nei[c]}) for r in range(self.info.world)]
+        last = self.snapshot()
+        src = self.fetch(needs, last)
+        plan = []
+        for c in self.local:  # w_local = mean of the neighbourhood's last models (params and buffers)
+            i = self.row_of[c]
+            w = 1.0 / len(nei[c])
+            plan.append((self.theta[i], [(src[j][0], w) for j in nei[c]]))
+        MK.mix_rows(plan, self.P)
+        MK.mix_rows([(self.bufs[self.row_of[c]], [(src[j][1], 1.0 / len(nei[c])) for j in nei[c]])
+                     for c in self.local], self.Q)
+        del src, last
+        rows, loc = self.all_rows()
+        self.train_rows(self.rowset, rows, loc, round_idx, self.cfg.epochs)
+        t1 = time.perf_counter()
+        # global model = uniform mean of all personal models (evaluation only)
+        buf, Pp = self.weighted_partial(self.theta, self.bufs, rows, [1.0 / self.N] * len(rows))
+        rt.all_reduce_buckets(buf, self.info)
+        self.w_global.copy_(buf[:self.P])
+        self.b_global.copy_(buf[Pp:])
+        t2 = time.perf_counter()
+        self.timers["train"] += t1 - t0
+        self.timers["aggregate"] += t2 - t1
+        self.stat_info["sum_training_flops"] += int(self.cfg.epochs * self.sizes.sum())
+        res = self.evaluate(round_idx)
+        if round_idx % 100 == 99:  # fine-tune evaluation (dpsgd_api.py:89-101); state is unchanged
+            self.finetune_round()
+        self.stat_info["round_time"].append(time.perf_counter() - t0)
+        return res
+
+
+# ================================================================================================== FedFomo
+class FedFomoRunner(PersonalizedRunner):
+    """FedFomo (``fedfomo/fedfomo_api.py:53-217``): after local training, client c weighs each candidate j by
+    ``(L_val(theta_c^old) - L_val(theta_j)) / ||theta_j - theta_c^old||`` and moves to
+    ``theta_c^old + sum_j w_j^+ (theta_j - theta_c^old) / sum w^+`` (its own new model stands in for j = c)."""
+
+    def __init__(self, *a, **kw):
+        super().__init__(*a, **kw)
+        N = self.N
+        self.weights_locals = np.full((N, N), 1.0 / N)
+        self.p_choose = np.ones((N, N))
+
+    def choose(self, c):
+        N, K = self.N, max(1, int(self.N * self.cfg.frac))
+        if N == K:
+            return list(range(N))
+        p = self.p_choose[c]
+        p[c] = 0
+        if self.py_rng.random() >= 0.5:
+            idx = np.argsort(p)[-K:]
+        else:
+            idx = self.np_rng.choice(range(N), K, replace=False)
+            while c in idx:
+                idx = self.np_rng.choice(range(N), K, replace=False)
+        return sorted(int(j) for j in list(idx) + [c])
+
+    def run_round(self, round_idx, sync_timers=False):
+        t0 = time.perf_counter()
+        self._round_start(round_idx)
+        last = self.snapshot()
+        rows, loc = self.all_rows()
+        self.train_rows(self.rowset, rows, loc, round_idx, self.cfg.epochs)
+        self.stat_info["sum_training_flops"] += int(self.cfg.epochs * self.sizes.sum())
+        t1 = time.perf_counter()
+        after_train = self.eval_local(self.rowset, rows, loc)
+        nei = {c: self.choose(c) for c in range(self.N)}  # same generator sequence on every rank
+        needs = [sorted({j for c in self.shards[r] for j in nei[c]}) for r in range(self.info.world)]
+        src = self.fetch(needs, last)
+        # candidate pool: [old own models (C) | new own models (C) | remote candidates]
+        remote = [j for j in needs[self.info.rank] if j not in self.row_of]
+        pool = RowSet(torch.cat([last.theta[:self.C], self.theta[:self.C]]),
+                      torch.cat([last.bufs[:self.C], self.bufs[:self.C]]))
+        if remote:
+            ext = self.pool([src[j] for j in remote])
+            pool = RowSet(torch.cat([pool.theta, ext.theta[:len(remote)]]), torch.cat([pool.bufs, ext.bufs[:len(remote)]]))
+        prow = {("old", c): self.row_of[c] for c in self.local}
+        prow.update({("new", c): self.C + self.row_of[c] for c in self.local})
+        for k, j in enumerate(remote):
+            prow[("old", j)] = 2 * self.C + k
+        # validation losses: (model row, client whose val split) pairs, grouped launches
+        pairs = []
+        for c in self.local:
+            pairs.append((prow[("old", c)], c))
+            for j in nei[c]:
+                pairs.append((prow[("new", c)] if j == c else prow[("old", j)], c))
+        which = "val" if self.splits[self.local[0]].val is not None else "test"
+        met = self.eval_grouped(pool.theta, pool.bufs, [p for p, _ in pairs], [c for _, c in pairs], which)
+        # parameter distances ||theta_j - theta_c^old|| over the whole state (params and buffers)
+        dpairs = []
+        for c in self.local:
+            base = prow[("old", c)]
+            for j in nei[c]:
+                dpairs.append((prow[("new", c)] if j == c else prow[("old", j)], base))
+        d2 = MK.pair_sqdist([(pool.theta[a], pool.theta[b]) for a, b in dpairs], self.P) + \
+            MK.pair_sqdist([(pool.bufs[a], pool.bufs[b]) for a, b in dpairs], self.Q)
+        d2 = d2.cpu().numpy()
+        wl = np.zeros((self.N, self.N))
+        k = kd = 0
+        plan_t, plan_b = [], []
+        for c in self.local:
+            loss_cur = met[k, 1]
+            k += 1
+            w_row = self.weights_locals[c].copy()
+            for j in nei[c]:
+                lj = met[k, 1]
+                k += 1
+                dist = math.sqrt(max(float(d2[kd]), 0.0))
+                kd += 1
+                w_row[j] = 0.0 if dist == 0 else (loss_cur - lj) / dist
+            wl[c] = w_row
+        # every rank needs every client's new weight row (next round's neighbour choice): one all-reduce
+        wl_all = torch.from_numpy(wl).to(self.device)
+        rt.all_reduce_buckets(wl_all, self.info)
+        wl_all = wl_all.cpu().numpy()
+        self.weights_locals = wl_all
+        self.p_choose = self.p_choose + wl_all
+        new_t = {c: self.theta[self.row_of[c]] for c in self.local}
+        new_b = {c: self.bufs[self.row_of[c]] for c in self.local}
+        out = RowSet(padded_rows(max(1, self.C), self.P, self.device), padded_rows(max(1, self.C), self.Q, self.device))
+        for c in self.local:
+            i = self.row_of[c]
+            wpos = np.maximum(self.weights_locals[c][nei[c]], 0)
+            tot = float(np.sum(wpos))
+            if tot == 0.0:  # no useful neighbour: keep the round-start model (fedfomo_api.py:204-205)
+                plan_t.append((out.theta[i], [(last.theta[i], 1.0)]))
+                plan_b.append((out.bufs[i], [(last.bufs[i], 1.0)]))
+                continue
+            a = wpos / tot
+            terms_t = [(last.theta[i], 1.0 - float(a.sum()))]
+            terms_b = [(last.bufs[i], 1.0 - float(a.sum()))]
+            for j, aj in zip(nei[c], a):
+                if aj == 0:
+                    continue
+                terms_t.append((new_t[c] if j == c else src[j][0], float(aj)))
+                terms_b.append((new_b[c] if j == c else src[j][1], float(aj)))
+            plan_t.append((out.theta[i], terms_t))
+            plan_b.append((out.bufs[i], terms_b))
+        MK.mix_rows(plan_t, self.P)
+        MK.mix_rows(plan_b, self.Q)
+        self.theta[:self.C].copy_(out.theta[:self.C])
+        self.bufs[:self.C].copy_(out.bufs[:self.C])
+        t2 = time.perf_counter()
+        after_agg = self.eval_local(self.rowset, rows, loc)
+        self.log_test(after_train, "old_mask_test_acc")
+        acc, loss = self.log_test(after_agg, "person_test_acc")
+        self.timers["train"] += t1 - t0
+        self.timers["aggregate"] += t2 - t1
+        self.timers["eval"] += time.perf_counter() - t2
+        self.stat_info["round_time"].append(time.perf_counter() - t0)
+        return {"person_test_acc": acc, "person_test_loss": loss}
+
+
+# ================================================================================================== DisPFL
+class DisPFLRunner(PersonalizedRunner):
+    """Decentralized sparse personalized FL with dynamic masks (``DisPFL/dispfl_api.py:46-184``)."""
+
+    def __init__(self, engine, splits, cfg, info, template_model, logger=None, algorithm="dispfl", mask_gen=None):
+        super().__init__(engine, splits, cfg, info, template_model, logger, algorithm)
+        params = {n: p.detach().cpu() for n, p in template_model.named_parameters()}
+        N = self.N
+        self.w_spa = [cfg.dense_ratio] * N
+        gen = mask_gen if mask_gen is not None else torch.Generator().manual_seed(cfg.seed + 17)
+        if not cfg.different_initial:
+            base = SP.init_masks(params, _sparsities(params, cfg.dense_ratio, cfg), generator=gen)
+            masks = [base] * N
+        elif not cfg.diff_spa:
+            masks = [SP.init_masks(params, _sparsities(params, cfg.dense_ratio, cfg), generator=gen) for _ in range(N)]
+        else:
+            p_divide = [0.2, 0.4, 0.6, 0.8, 1.0]
+            masks = []
+            for i in range(N):
+                self.w_spa[i] = p_divide[i % 5]
+                masks.append(SP.init_masks(params, _sparsities(params, p_divide[i % 5], cfg), generator=gen))
+        flat = {c: self.flat_mask(masks[c]) for c in self.local}
+        self.mbits = self.local_masks_from(flat)
+        self.shared_bits = self.mbits.clone()  # mask_pers_shared: the mask each client last trained with
+        # w_per = w_global * mask (every parameter is masked)
+        if self.C:
+            self.theta[:self.C].mul_(MK.unpack_bits(self.mbits[:self.C], self.P))
+        self.dist_locals = np.zeros((N, N))
+
+    def benefit_choose(self, c, active):
+        N, K = self.N, max(1, int(self.N * self.cfg.frac))
+        if N == K:
+            return list(range(N))
+        # the reference forces cs = "random" (dispfl_api.py:201), drawing from the global numpy stream
+        idx = self.np_rng.choice(range(N), min(K, N), replace=False)
+        while c in idx:
+            idx = self.np_rng.choice(range(N), min(K, N), replace=False)
+        return [int(j) for j in idx]
+
+    def run_round(self, round_idx, sync_timers=False):
+        cfg = self.cfg
+        t0 = time.perf_counter()
+        self._round_start(round_idx)
+        N = self.N
+        active = self.np_rng.choice([0, 1], size=N, p=[1.0 - cfg.active, cfg.active])
+        rows, loc = self.all_rows()
+        # mask movement since the last round (hamming(shared_last[c], local[c])), K18 on device
+        if self.C:
+            moved = self.mspace.hamming(self.shared_bits[:self.C], self.mbits[:self.C]).sum(1).cpu().numpy()
+            for j, c in enumerate(self.local):
+                self.dist_locals[c][c] = moved[j]
+        nei = {}
+        for c in range(N):
+            nb = [] if active[c] == 0 else self.benefit_choose(c, active)
+            if N != max(1, int(N * cfg.frac)):
+                nb = list(nb) + [c]
+            nei[c] = sorted(int(j) for j in nb)
+        last = self.snapshot() if cfg.dispfl_aggregate else None
+        if cfg.dispfl_aggregate:
+            self._aggregate_neighbours(nei, active, last)
+        self.shared_bits.copy_(self.mbits)
+        before = self.eval_local(self.rowset, rows, loc)  # test of w_local before training
+        w_old = self.snapshot()
+        spec = StepSpec(mask_mode=MASK_WEIGHT, bits=self.mbits[:self.C])
+        self.train_rows(self.rowset, rows, loc, round_idx, cfg.epochs, spec)
+        t1 = time.perf_counter()
+        after = self.eval_local(self.rowset, rows, loc)
+        if not cfg.static and self.C:
+            drop = cfg.anneal_factor / 2 * (1 + np.cos((round_idx * np.pi) / cfg.comm_round))
+            nnz = self.mspace.popcount(self.mbits[:self.C])
+            k = torch.ceil(torch.tensor(drop, dtype=torch.float32) * nnz.float()).to(torch.int64)
+            k = torch.minimum(k, nnz)
+            self.mspace.select(MK.FIRE, self.theta, self.mbits, k.to(self.device))
+            if not cfg.dis_gradient_check:
+                self.local_grad(self.rowset, rows, loc, round_idx, bn_train=False)
+                self.mspace.select(MK.REGROW_ABS, self.grads, self.mbits, k.to(self.device))
+            else:
+                self.mspace.select(MK.REGROW_RAND, None, self.mbits, k.to(self.device), cids=loc,
+                                   seed=(cfg.seed << 20) + round_idx)
+        upd = self.count_nonzero_rows(RowSet(self.theta - w_old.theta, self.bufs - w_old.bufs), rows)
+        self.stat_info["sum_comm_params"] += int(self.count_nonzero_rows(w_old, rows).sum() + upd.sum())
+        self.timers["train"] += t1 - t0
+        t2 = time.perf_counter()
+        acc, _ = self.log_test(after, "old_mask_test_acc")
+        self.log_test(before, "new_mask_test_acc")
+        self.stat_info["person_test_acc"].append(acc)
+        self.timers["eval"] += time.perf_counter() - t2
+        self.stat_info["round_time"].append(time.perf_counter() - t0)
+        return {"person_test_acc": acc}
+
+    def _aggregate_neighbours(self, nei, active, last):
+        """The DisPFL paper's masked neighbour average (commented out in the reference, ``dispfl_api.py:138-142``):
+        per coordinate, the mean over the neighbours whose shared mask keeps it, times the client's own mask."""
+        needs = [sorted({j for c in self.shards[r] if active[c] for j in nei[c]}) for r in range(self.info.world)]
+        src = self.fetch(needs, last)
+        all_bits = self._all_bits(self.shared_bits)
+        for c in self.local:
+            if not active[c] or not nei[c]:
+                continue
+            i = self.row_of[c]
+            m = MK.unpack_bits(all_bits[nei[c]], self.P)
+            num = sum(src[j][0][:self.P] * m[k] for k, j in enumerate(nei[c]))
+            cnt = m.sum(0)
+            avg = torch.where(cnt > 0, num / cnt.clamp_min(1), torch.zeros_like(num))
+            self.theta[i, :self.P] = avg * MK.unpack_bits(self.mbits[i:i + 1], self.P)[0]
+            self.bufs[i, :self.Q] = sum(src[j][1][:self.Q] for j in nei[c]) / len(nei[c])
+
+    def _all_bits(self, bits):
+        """[N, W] mask bit rows of every client (all-reduce of the zero-padded local rows)."""
+        out = torch.zeros((self.N, self.W), dtype=torch.int64, device=self.device)
+        if self.C:
+            out[torch.tensor(self.local, device=self.device)] = bits[:self.C].to(torch.int64)
+        rt.all_reduce_buckets(out, self.info)
+        return out.to(torch.int32)
+
+    def finish(self):
+        all_bits = self._all_bits(self.mbits)
+        mat = []
+        for i in range(self.N):
+            d = self.mspace.hamming(all_bits[i:i + 1].expand(self.N, -1).contiguous(), all_bits).sum(1)
+            mat.append(d.cpu().tolist())
+        self.stat_info["mask_dis_matrix"] = mat
+        if self.cfg.save_masks:
+            self.stat_info["final_masks"] = MK.unpack_bits(all_bits, self.P).bool().cpu()
+        return None
+
+
+# ================================================================================================== SubAvg
+class SubAvgRunner(PersonalizedRunner):
+    """Sub-FedAvg unstructured pruning (``subavg/subavg_api.py:43-139``, ``subavg/client.py:36-63``)."""
+
+    def __init__(self, *a, **kw):
+        super().__init__(*a, **kw)
+        self.mbits = MK.pack_bits(torch.ones((max(1, self.C), self.P), device=self.device))
+        names = self.e.players.names
+        self.prune_names = [n for n in names if "weight" in n and "bn" not in n]  # prune_func.py:23
+
+    def _real_prune_rows(self, rs, rows, bits_rows):
+        ix = torch.tensor(rows, device=self.device)
+        rs.theta[ix, :self.P] = rs.theta[ix, :self.P] * MK.unpack_bits(bits_rows, self.P)
+
+    def run_round(self, round_idx, sync_timers=False):
+        cfg = self.cfg
+        t0 = time.perf_counter()
+        self._round_start(round_idx)
+        sampled = self.sample_clients(round_idx)
+        rows, loc = self._local_rows(sampled)
+        hooks = {}
+        if rows:
+            ix = torch.tensor(rows, device=self.device)
+            old_bits = self.mbits[ix].clone()
+            self.theta[ix] = self.w_global.unsqueeze(0).expand(len(rows), -1)
+            self.bufs[ix] = self.b_global.unsqueeze(0).expand(len(rows), -1)
+            self._real_prune_rows(self.rowset, rows, old_bits)  # w_per = real_prune(w_global, mask)
+            nz = self.count_nonzero_rows(self.rowset, rows)
+            dense = nz / float(self.P + self.Q)  # print_pruning over the whole state
+            self.stat_info["sum_comm_params"] += int(nz.sum())
+
+            def hook(ep, view, clients):  # fake_prune after the first and the last epoch (the training masks)
+                if ep == 0:
+                    hooks["m1"] = self.mspace.percentile_prune(view.theta, old_bits, cfg.each_prune_ratio,
+                                                               self.prune_names)
+                if ep == cfg.epochs - 1:
+                    hooks["m2"] = self.mspace.percentile_prune(view.theta, old_bits, cfg.each_prune_ratio,
+                                                               self.prune_names)
+            spec = StepSpec(mask_mode=MASK_GRAD, bits=self.mbits)
+            self.train_rows(self.rowset, rows, loc, round_idx, cfg.epochs, spec, epoch_hook=hook)
+            m1, m2 = hooks["m1"], hooks["m2"]
+            ham = self.mspace.hamming(m1, m2).double().cpu().numpy()
+            dist = (ham / self.mspace.seg_len[None, :]).mean(1)  # mean over every parameter (scipy hamming)
+            cand = [j for j in range(len(rows)) if dist[j] > cfg.dist_thresh and dense[j] > cfg.dense_ratio]
+            final_bits = old_bits.clone()
+            if cand:
+                pr = self.pool([(self.theta[rows[j]], self.bufs[rows[j]]) for j in cand])
+                cb = torch.stack([m2[j] for j in cand])
+                pr.theta[:len(cand), :self.P].mul_(MK.unpack_bits(cb, self.P))
+                met = self.eval_grouped(pr.theta, pr.bufs, list(range(len(cand))), [loc[j] for j in cand], "train")
+                for q, j in enumerate(cand):
+                    if met[q, 0] / max(1.0, met[q, 2]) > cfg.acc_thresh:
+                        self.theta[rows[j], :self.P].copy_(pr.theta[q, :self.P])
+                        final_bits[j] = m2[j]
+            self.stat_info["sum_comm_params"] += int(self.count_nonzero_rows(self.rowset, rows).sum())
+        t1 = time.perf_counter()
+        # masked average with the masks the clients trained with (subavg_api.py:123-139)
+        s = torch.zeros(self.P, dtype=torch.float32, device=self.device)
+        cnt = torch.zeros(self.P, dtype=torch.float32, device=self.device)
+        sb = torch.zeros(self.Q, dtype=torch.float32, device=self.device)
+        cb = torch.zeros(self.Q, dtype=torch.float32, device=self.device)
+        if rows:
+            sc = self._scratch_rows(len(rows))
+            sc.theta[:len(rows)].copy_(self.theta[ix])
+            sc.bufs[:len(rows)].copy_(self.bufs[ix])
+            MK.masked_rows_sum(sc.theta[:len(rows)], self.P, old_bits, s, cnt)
+            MK.masked_rows_sum(sc.bufs[:len(rows)], self.Q, None, sb, cb)
+        red = torch.cat([s, cnt, sb, cb])
+        rt.all_reduce_buckets(red, self.info)
+        s, cnt, sb, cb = red.split([self.P, self.P, self.Q, self.Q])
+        self.w_global.copy_(torch.where(cnt > 0, s / cnt, self.w_global))
+        self.b_global.copy_(torch.where(cb > 0, sb / cb, self.b_global))
+        t2 = time.perf_counter()
+        res = None
+        if self._eval_due(round_idx):  # every client tests real_prune(w_global, its current mask)
+            er = self._eval_buffers(max(1, self.C))
+            th, bu = er
+            th.copy_(self.w_global.expand_as(th))
+            bu.copy_(self.b_global.expand_as(bu))
+            if self.C:
+                th[:self.C, :self.P].mul_(MK.unpack_bits(self.mbits[:self.C], self.P))
+            r = self.eval_local(RowSet(th, bu), *self.all_rows())
+            acc, loss = self.log_test(r, "test_acc")
+            self.stat_info["person_test_acc"].append(acc)
+            res = {"test_acc": acc, "test_loss": loss}
+        if rows:
+            self.mbits[ix] = final_bits
+        self.timers["train"] += t1 - t0
+        self.timers["aggregate"] += t2 - t1
+        self.timers["eval"] += time.perf_counter() - t2
+        self.stat_info["sum_training_flops"] += int(cfg.epochs * sum(self.sizes[c] for c in sampled))
+        self.stat_info["round_time"].append(time.perf_counter() - t0)
+        return res
+
+
+RUNNERS = {"dispfl": DisPFLRunner, "subavg": SubAvgRunner, "ditto": DittoRunner, "dpsgd": DPSGDRunner,
+           "fedfomo": FedFomoRunner, "local": LocalRunner}
+
+
+def make_runner(algorithm, engine, splits, cfg, info, template_model, logger=None, **kw):
+    """Runner of any algorithm of the harness on the client-batched executor."""
+    if algorithm in RUNNERS:
+        return RUNNERS[algorithm](engine, splits, cfg, info, template_model, logger, algorithm=algorithm, **kw)
+    alg = {"sailentgrads": "salientgrads", "salientgrads": "salientgrads", "fedavg": "fedavg",
+           "fedprox": "fedavg"}[algorithm]
+    return FLRunner(engine, splits, cfg, info, template_model, logger, algorithm=alg)

@@ -1,0 +1,774 @@
+"""Client-batched FL runner: many virtual clients per GPU, one process per GPU, RCCL collectives.
+
+This replaces the reference's sequential client loop (``sailentgrads_api.py:86-147``, ``fedavg_api.py:40-88``):
+instead of swapping one shared ``nn.Module``'s state_dict per client and copying weights host<->device, every rank
+keeps its clients resident as rows of ``theta [C_local, P]`` (params) and ``bufs [C_local, Q]`` (BN running stats)
+and trains all of them in lockstep — one launch sequence (or one replayed hipGraph) per local step.
+
+Layout decisions that keep every launch dense:
+
+* rows are ordered by training-set size (descending).  At local step ``s`` the clients whose batch has the same
+  size (full batches, then each partial last-batch size) therefore form *contiguous* row ranges, so ragged
+  federations (unequal sites, ``drop_last=False`` partial batches, ``ABCD/data_loader.py:195``) train without
+  gather/scatter copies and keep hipGraph capture;
+* a round that trains a subset of the local rows (``frac < 1``) gathers them once into a scratch row set, trains
+  there and scatters back (one copy per round, not per step);
+* everything a step needs besides its launch arguments lives on device (sample indices, learning rate, dropout
+  counter), so steps replay as hipGraphs;
+* the optimizer is one fused kernel for every algorithm (``StepSpec``): shared or per-client bit masks applied to
+  weights (SalientGrads / DisPFL) or gradients (SubAvg), FedProx's proximal gradient and Ditto's personal pull.
+
+Round semantics reproduced from the reference (SURVEY.md §2.2 "Shared algorithm behaviors"):
+* sampling ``np.random.seed(round); choice(total, per_round, replace=False)`` (all if frac = 1);
+* every sampled client starts from ``w_global``; SGD(lr * lr_decay**round, momentum, wd) rebuilt per round
+  (momentum rows are zeroed at the start of each local training, Q4); ``clip_grad_norm_(10)``;
+* one DataLoader(shuffle=True) pass per epoch over the client's train split (last batch may be partial);
+* aggregation: sample-weighted average over ALL state entries incl. BN running stats and
+  ``num_batches_tracked`` (Q3) — a local weighted row-sum followed by ONE all-reduce of P+Q floats;
+* evaluation: global model and each client's last local ("personal") model on that client's test split;
+  logged loss uses sigmoid-then-BCEWithLogits (Q1); metrics are unweighted means over clients (Q5).
+The personalized / decentralized algorithms build on this class (``engine/personalized.py``).
+"""
+from __future__ import annotations
+
+import math
+import time
+from dataclasses import dataclass, replace
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+from ..parallel import runtime as rt
+from . import masks as MK
+from .executor import (ClientSplit, FLConfig, gather_rows, maskable_flat_mask, padded_rows,  # noqa: F401
+                       snip_maskable_names)
+
+MASK_NONE, MASK_WEIGHT, MASK_GRAD = 0, 1, 2
+
+
+@dataclass
+class StepSpec:
+    """What the fused optimizer does after each local step (see ``optim.hip`` ``local_opt``)."""
+    mask_mode: int = MASK_NONE
+    bits: torch.Tensor = None      # [R, W] bit rows aligned with the trained rows, or [1, W] when ``shared``
+    shared: bool = False
+    prox_mu: float = 0.0           # FedProx: g += mu (w - ref)
+    ref: torch.Tensor = None       # [P] shared reference row
+    lamda: float = 0.0             # Ditto: w -= lr lamda (w - pref) after the step
+    pref: torch.Tensor = None      # [P] shared pull reference
+
+    def rows(self, lo, hi):
+        if self.bits is None or self.shared:
+            return self
+        return replace(self, bits=self.bits[lo:hi])
+
+    def key(self):
+        return (self.mask_mode, None if self.bits is None else (self.bits.data_ptr(), self.shared), self.prox_mu,
+                None if self.ref is None else self.ref.data_ptr(), self.lamda,
+                None if self.pref is None else self.pref.data_ptr())
+
+
+@dataclass
+class RowSet:
+    theta: torch.Tensor            # [R, P] fp32 (16-B aligned row stride)
+    bufs: torch.Tensor             # [R, Q]
+
+    def rows(self, lo, hi):
+        return RowSet(self.theta[lo:hi], self.bufs[lo:hi])
+
+
+def _contiguous(rows):
+    return bool(rows) and rows == list(range(rows[0], rows[-1] + 1))
+
+
+class FLRunner:
+    """SalientGrads / FedAvg / FedProx over client-sharded, client-batched local training (and the base of the
+    personalized runners)."""
+
+    def __init__(self, engine, splits, cfg: FLConfig, info: rt.DistInfo, template_model, logger=None,
+                 algorithm="salientgrads"):
+        self.e, self.cfg, self.info, self.log = engine, cfg, info, logger
+        self.alg = algorithm
+        self.N = len(splits)
+        self.splits = splits
+        self.device = info.device
+        self.sizes = np.array([len(s.train) for s in splits], dtype=np.int64)
+        self.shards = rt.shard_clients(list(self.sizes), info.world)
+        # rows ordered by train size (desc), ties by client id: equal-size step groups are contiguous row ranges
+        self.local = sorted(self.shards[info.rank], key=lambda c: (-int(self.sizes[c]), c))
+        self.row_of = {c: i for i, c in enumerate(self.local)}
+        self.owner = np.zeros(self.N, dtype=np.int64)
+        for r, sh in enumerate(self.shards):
+            self.owner[list(sh)] = r
+        self.C = len(self.local)
+        P, Q = engine.players.total, engine.blayers.total
+        self.P, self.Q = P, Q
+        self.W = MK.mask_words(P)
+        with torch.no_grad():
+            flat_p = engine.players.flatten_state(dict(template_model.named_parameters()), self.device).detach()
+            flat_b = engine.blayers.flatten_state(dict(template_model.named_buffers()), self.device).detach()
+        self.w_global = flat_p.clone()
+        self.b_global = flat_b.clone()
+        nrow = max(1, self.C)
+        self.theta = padded_rows(nrow, P, self.device)
+        self.theta.copy_(flat_p.unsqueeze(0).expand(nrow, P))
+        self.bufs = padded_rows(nrow, Q, self.device)
+        self.bufs.copy_(flat_b.unsqueeze(0).expand(nrow, Q))
+        self.grads = padded_rows(nrow, P, self.device)
+        self.mom_buf = padded_rows(nrow, P, self.device) if cfg.momentum != 0 else None
+        self.mask = None              # SalientGrads global mask, float [P]
+        self.mask_bits = None         # the same as one shared bit row [1, W]
+        self.maskable = maskable_flat_mask(engine.players, snip_maskable_names(template_model)).to(self.device)
+        self.stat_info = dict(sum_comm_params=0, sum_training_flops=0, global_test_acc=[], person_test_acc=[],
+                              global_test_loss=[], person_test_loss=[], round_time=[])
+        self.timers = {"train": 0.0, "aggregate": 0.0, "eval": 0.0, "snip": 0.0}
+        self._graphs = {}             # step key -> captured local step (None until the shape repeats, False = eager)
+        self._lr_dev = self._seed_dev = None
+        self._scratch = None
+        self._eval_cache = None
+
+    # ---------------------------------------------------------------------------------------------- helpers
+    def _rng(self, *key):
+        return np.random.RandomState(abs(hash((self.cfg.seed,) + tuple(int(k) for k in key))) % (2 ** 31))
+
+    def _groups(self, items):
+        gmax = self.cfg.group or len(items)
+        return [items[i:i + gmax] for i in range(0, len(items), gmax)]
+
+    def _upload_i32(self, arr):
+        """int32 host array -> device tensor through pinned memory, without blocking the host."""
+        t = torch.from_numpy(np.ascontiguousarray(arr, dtype=np.int32))
+        if self.device.type != "cuda":
+            return t
+        return t.pin_memory().to(self.device, non_blocking=True)
+
+    def _sync(self):
+        if self.device.type == "cuda":
+            torch.cuda.synchronize()
+
+    def _step_seed(self, round_idx, tag, ep, s):
+        """Dropout stream position of one local step: a function of (round, training tag, epoch, step) only, so it
+        does not depend on how clients are grouped or sharded (client ids key the per-client streams)."""
+        return ((((round_idx + 2) * 64 + tag) * 64 + ep) * 8192 + s) & ((1 << 40) - 1)
+
+    def _order(self, c, round_idx, tag, ep):
+        """Sample order of one epoch of client c (DataLoader(shuffle=True))."""
+        tr = self.splits[c].train
+        return tr[self._rng(round_idx, c, tag, ep).permutation(len(tr))]
+
+    def _stratified_batch(self, c, it, B):
+        """A label-stratified mini-batch of client c (IterSNIP ``--stratified_sampling``): per class
+        round(B * n_class / n) samples (largest remainders), drawn without replacement."""
+        tr = self.splits[c].train
+        y = self.e.labels.index_select(0, torch.as_tensor(tr, dtype=torch.long).to(self.e.labels.device))
+        y = y.cpu().numpy()
+        rs = self._rng(-7, c, it)
+        B = min(B, len(tr))
+        cls, cnt = np.unique(y, return_counts=True)
+        q = B * cnt / cnt.sum()
+        take = np.floor(q).astype(int)
+        for i in np.argsort(-(q - take), kind="stable")[:B - take.sum()]:
+            take[i] += 1
+        out = []
+        for k, n in zip(cls, take):
+            pool = tr[y == k]
+            out.append(pool[rs.permutation(len(pool))[:n]])
+        b = np.concatenate(out)
+        return b[rs.permutation(len(b))]
+
+    # ---------------------------------------------------------------------------------------------- planning
+    def _plan(self, clients, chunks_of):
+        """Lockstep launch plan over clients listed in row order.  ``chunks_of(j, c)`` -> list of per-step index
+        arrays of client j.  Returns (plan, idx) where plan items are (r0, r1, step, offset, n, G, B) with rows
+        relative to the listed clients and all sample indices uploaded in ONE pinned non-blocking copy."""
+        chunks = [chunks_of(j, c) for j, c in enumerate(clients)]
+        nsteps = max((len(ch) for ch in chunks), default=0)
+        plan, flat, off = [], [], 0
+        for s in range(nsteps):
+            run = None
+            items = []
+            for j, ch in enumerate(chunks):
+                if s < len(ch) and len(ch[s]):
+                    items.append((j, ch[s]))
+            # contiguous runs of equal batch size (rows are size sorted, so equal sizes are adjacent)
+            runs = []
+            for j, ch in items:
+                if run and run[-1][0] == j - 1 and len(run[-1][1]) == len(ch):
+                    run.append((j, ch))
+                else:
+                    run = [(j, ch)]
+                    runs.append(run)
+            for run in runs:
+                for grp in self._groups(run):
+                    n = sum(len(ch) for _, ch in grp)
+                    plan.append((grp[0][0], grp[-1][0] + 1, s, off, n, len(grp), len(grp[0][1])))
+                    flat.extend(ch for _, ch in grp)
+                    off += n
+        if not plan:
+            return [], None
+        return plan, self._upload_i32(np.concatenate(flat))
+
+    def _epoch_chunks(self, round_idx, tag, ep, n_batches=None):
+        B = self.cfg.batch_size
+
+        def f(j, c):
+            o = self._order(c, round_idx, tag, ep)
+            ch = [o[i:i + B] for i in range(0, len(o), B)]
+            return ch[:n_batches] if n_batches is not None else ch
+        return f
+
+    # ---------------------------------------------------------------------------------------------- training
+    def _scratch_rows(self, k):
+        if self._scratch is None or self._scratch.theta.shape[0] < k:
+            n = max(k, self.C, 1)
+            self._scratch = RowSet(padded_rows(n, self.P, self.device), padded_rows(n, self.Q, self.device))
+            self._scratch_bits = torch.zeros((n, self.W), dtype=torch.int32, device=self.device)
+            self._graphs = {}
+        return self._scratch
+
+    def _zero_mom(self, k):
+        if self.mom_buf is not None:
+            self.mom_buf[:k].zero_()
+
+    def train_rows(self, rs, rows, clients, round_idx, epochs, spec=None, tag=0, epoch_hook=None, lr=None):
+        """Local SGD (``epochs`` DataLoader passes) of ``clients`` living in rows ``rows`` of row set ``rs`` (rows
+        listed in increasing order = the size-sorted row order).  ``epoch_hook(ep, view, clients)`` runs after every
+        epoch on the rows being trained."""
+        if not rows:
+            return
+        spec = spec or StepSpec()
+        if _contiguous(rows):
+            lo, hi = rows[0], rows[-1] + 1
+            self._train_view(rs.rows(lo, hi), clients, round_idx, epochs, spec.rows(lo, hi), tag, epoch_hook, lr)
+            return
+        ix = torch.tensor(rows, device=self.device)
+        k = len(rows)
+        sc = self._scratch_rows(k)
+        view = sc.rows(0, k)
+        view.theta.copy_(rs.theta.index_select(0, ix))
+        view.bufs.copy_(rs.bufs.index_select(0, ix))
+        sspec = spec
+        if spec.bits is not None and not spec.shared:
+            self._scratch_bits[:k].copy_(spec.bits.index_select(0, ix))
+            sspec = replace(spec, bits=self._scratch_bits[:k])
+        self._train_view(view, clients, round_idx, epochs, sspec, tag, epoch_hook, lr)
+        rs.theta[ix] = view.theta
+        rs.bufs[ix] = view.bufs
+        if spec.bits is not None and not spec.shared:
+            spec.bits[ix] = self._scratch_bits[:k]  # epoch hooks may have changed the trained masks
+
+    def _train_view(self, view, clients, round_idx, epochs, spec, tag, epoch_hook, lr):
+        cfg = self.cfg
+        lr = cfg.lr * (cfg.lr_decay ** round_idx) if lr is None else lr
+        self._zero_mom(len(clients))
+        use_graphs = cfg.hip_graphs and getattr(self.e, "supports_graphs", False) and self.device.type == "cuda"
+        if self._lr_dev is None:
+            self._lr_dev = torch.zeros(1, dtype=torch.float32, device=self.device)
+            self._seed_dev = torch.zeros(1, dtype=torch.int64, device=self.device)
+        self._lr_dev.fill_(lr)
+        for ep in range(epochs):
+            plan, idx = self._plan(clients, self._epoch_chunks(round_idx, tag, ep))
+            for r0, r1, s, off, n, G, B in plan:
+                seed = self._step_seed(round_idx, tag, ep, s)
+                cids = clients[r0:r1]
+                sub = view.rows(r0, r1)
+                if use_graphs:
+                    self._graph_step(sub, r0, idx[off:off + n], G, B, spec.rows(r0, r1), cids, seed)
+                else:
+                    self._seed_dev.fill_(seed)
+                    self._step(sub, r0, idx[off:off + n], G, B, spec.rows(r0, r1), cids, lr)
+            if epoch_hook is not None:
+                epoch_hook(ep, view, clients)
+
+    def _step(self, sub, r0, idx, G, B, spec, cids, lr, seed_dev=None, lr_dev=None):
+        cfg = self.cfg
+        gr = self.grads[r0:r0 + G]
+        mo = self.mom_buf[r0:r0 + G] if self.mom_buf is not None else None
+        self.e.train_step(sub.theta, sub.bufs, gr, idx, G, B, cfg.dropout_keep, cfg.seed << 40, cids=cids,
+                          seed_dev=self._seed_dev if seed_dev is None else seed_dev)
+        self.e.local_opt(sub.theta, gr, mo, spec, lr, cfg.wd, cfg.momentum, cfg.max_norm,
+                         lr_dev=self._lr_dev if lr_dev is None else lr_dev)
+
+    def _graph_step(self, sub, r0, idx, G, B, spec, cids, seed):
+        """One lockstep local step (forward+backward of G clients + fused optimizer) as a replayed hipGraph.  The
+        ~45 kernel launches of a step become one graph launch; everything that changes between steps lives in
+        device memory the graph reads: the sample indices (copied into a static buffer), the dropout stream
+        counter and the round's learning rate.  The first step of a shape runs eagerly (it also allocates every
+        scratch buffer the graph will reuse), the second is captured and replayed, later ones only replay — same
+        kernels, same arguments, same results as the eager path."""
+        key = (sub.theta.data_ptr(), r0, G, B, tuple(int(c) for c in cids), spec.key())
+        ent = self._graphs.get(key, "new")
+        self._seed_dev.fill_(seed)
+        if ent == "new":
+            self._step(sub, r0, idx, G, B, spec, cids, 0.0)
+            self._graphs[key] = None
+            return
+        if ent is None:
+            idx_buf = torch.empty(G * B, dtype=torch.int32, device=self.device)
+            idx_buf.copy_(idx)
+            torch.cuda.current_stream().synchronize()
+            g = torch.cuda.CUDAGraph()
+            try:
+                # thread_local: the RCCL watchdog thread of a multi-GPU run may query events during the capture
+                with torch.cuda.graph(g, capture_error_mode="thread_local"):
+                    self._step(sub, r0, idx_buf, G, B, spec, cids, 0.0)
+            except Exception:  # noqa: BLE001 - capture unsupported here: stay eager for this shape
+                self._graphs[key] = False
+                self._step(sub, r0, idx, G, B, spec, cids, 0.0)
+                return
+            ent = self._graphs[key] = (g, idx_buf)
+        elif ent is False:
+            self._step(sub, r0, idx, G, B, spec, cids, 0.0)
+            return
+        g, idx_buf = ent
+        idx_buf.copy_(idx)
+        g.replay()
+
+    def local_grad(self, rs, rows, clients, round_idx, bn_train=True, tag=11):
+        """Gradient of the first batch of a fresh shuffle (``next(iter(train_loader))``) into ``self.grads`` rows
+        [0, len(rows)); ``bn_train=False`` = model.eval() (DisPFL ``screen_gradients``).  Running stats untouched
+        (the steps run on copies of the buffer rows)."""
+        plan, idx = self._plan(clients, self._epoch_chunks(round_idx, tag, 0, n_batches=1))
+        seed_dev = self._seed_dev_or_zero()
+        for r0, r1, s, off, n, G, B in plan:
+            t = torch.tensor(rows[r0:r1], device=self.device)
+            th, bu = gather_rows(rs.theta, t), gather_rows(rs.bufs, t)
+            seed_dev.fill_(self._step_seed(round_idx, tag, 0, s))
+            self.e.train_step(th, bu, self.grads[r0:r1], idx[off:off + n], G, B, self.cfg.dropout_keep,
+                              self.cfg.seed << 40, cids=clients[r0:r1], seed_dev=seed_dev, bn_train=bn_train)
+
+    def _seed_dev_or_zero(self):
+        if self._seed_dev is None:
+            self._seed_dev = torch.zeros(1, dtype=torch.int64, device=self.device)
+            self._lr_dev = torch.zeros(1, dtype=torch.float32, device=self.device)
+        return self._seed_dev
+
+    # ---------------------------------------------------------------------------------------------- SNIP
+    def generate_global_mask_snip(self):
+        """IterSNIP saliency on every client (mean over iterations, then clients) -> global top-k mask
+        (``sailentgrads_api.py:47-66``, ``snip.py:21-116``).  ``stratified_sampling``: each iteration uses a
+        label-stratified mini-batch (the intent of ``sailentgrads/client.py:33-43``)."""
+        t0 = time.perf_counter()
+        cfg = self.cfg
+        score = torch.zeros((max(1, self.C), self.P), dtype=torch.float32, device=self.device)
+        self.theta.copy_(self.w_global.unsqueeze(0).expand_as(self.theta))
+        saved_bufs = self.bufs.clone()
+        clients = self.local
+        seed_dev = self._seed_dev_or_zero()
+        for it in range(cfg.itersnip_iteration):
+            if cfg.stratified_sampling:
+                plan, idx = self._plan(clients, lambda j, c: [self._stratified_batch(c, it, cfg.batch_size)])
+            else:  # "next(iter(train_loader))": the first batch of a fresh shuffle
+                plan, idx = self._plan(clients, self._epoch_chunks(-1, 0, it, n_batches=1))
+            for r0, r1, s, off, n, G, B in plan:
+                seed_dev.fill_(self._step_seed(-1, 1, it, s))
+                th, bu, gr = self.theta[r0:r1], self.bufs[r0:r1], self.grads[r0:r1]
+                self.e.train_step(th, bu, gr, idx[off:off + n], G, B, cfg.dropout_keep, cfg.seed << 40,
+                                  cids=clients[r0:r1], seed_dev=seed_dev)
+                self.e.saliency_acc(th, gr, score[r0:r1], 1.0 / cfg.itersnip_iteration)
+        self.bufs.copy_(saved_bufs)  # SNIP runs on a model copy: running stats are discarded
+        total = score.sum(0) if self.C else torch.zeros(self.P, device=self.device)
+        rt.all_reduce_buckets(total, self.info)
+        total /= self.N
+        sel = total[self.maskable]
+        sel = sel / sel.sum()
+        k = int(sel.numel() * cfg.dense_ratio)
+        mask = torch.ones(self.P, dtype=torch.float32, device=self.device)
+        if k >= 1:
+            if self.device.type == "cuda":
+                m = self.e.m
+                st = torch.empty(4, dtype=torch.int32, device=self.device)
+                hist = torch.empty(256, dtype=torch.int32, device=self.device)
+                sel = sel.contiguous()
+                m.radix_select_kth(sel.data_ptr(), sel.numel(), k, st.data_ptr(), hist.data_ptr(),
+                                   torch.cuda.current_stream().cuda_stream)
+                keep = torch.empty_like(sel)
+                m.threshold_mask(sel.data_ptr(), sel.numel(), st.data_ptr(), keep.data_ptr(),
+                                 torch.cuda.current_stream().cuda_stream)
+            else:
+                thr = torch.topk(sel, k, sorted=True).values[-1]
+                keep = (sel >= thr).float()
+            mask[self.maskable] = keep
+        self.set_mask(mask if cfg.snip_mask else torch.ones_like(mask))
+        self.timers["snip"] += time.perf_counter() - t0
+        return self.mask
+
+    def set_mask(self, mask):
+        self.mask = mask
+        self.mask_bits = MK.pack_bits(mask.view(1, -1))
+        self._graphs = {}  # captured local steps reference the mask tensor
+
+    # ---------------------------------------------------------------------------------------------- rounds
+    def sample_clients(self, round_idx):
+        per_round = max(1, int(self.N * self.cfg.frac))
+        if per_round >= self.N:
+            return list(range(self.N))
+        np.random.seed(round_idx)
+        return sorted(np.random.choice(range(self.N), per_round, replace=False).tolist())
+
+    def _local_rows(self, clients):
+        """(rows, clients) of the given global clients that live on this rank, in row order."""
+        cs = sorted((c for c in clients if c in self.row_of), key=lambda c: self.row_of[c])
+        return [self.row_of[c] for c in cs], cs
+
+    def _fedavg_spec(self):
+        spec = StepSpec()
+        if self.alg == "salientgrads" and self.mask_bits is not None:
+            spec = replace(spec, mask_mode=MASK_WEIGHT, bits=self.mask_bits, shared=True)
+        if self.cfg.prox_mu > 0:
+            spec = replace(spec, prox_mu=self.cfg.prox_mu, ref=self.w_global)
+        return spec
+
+    def local_train(self, round_idx, sampled, lr=None):
+        rows, loc = self._local_rows(sampled)
+        if not rows:
+            return
+        if _contiguous(rows):  # one broadcast launch for the whole run
+            self.theta[rows[0]:rows[-1] + 1].copy_(self.w_global.expand(len(rows), -1))
+            self.bufs[rows[0]:rows[-1] + 1].copy_(self.b_global.expand(len(rows), -1))
+        else:
+            ix = torch.tensor(rows, device=self.device)
+            self.theta[ix] = self.w_global.unsqueeze(0).expand(len(rows), -1)
+            self.bufs[ix] = self.b_global.unsqueeze(0).expand(len(rows), -1)
+        self.train_rows(RowSet(self.theta, self.bufs), rows, loc, round_idx, self.cfg.epochs, self._fedavg_spec(),
+                        lr=lr)
+
+    def aggregate(self, sampled):
+        if self.cfg.aggregator != "fedavg":
+            return self.aggregate_robust(sampled)
+        if self.cfg.update_topk > 0:
+            return self.aggregate_topk(sampled)
+        return self.aggregate_fedavg(sampled)
+
+    def aggregate_topk(self, sampled):
+        """Sparse-update FedAvg: client i contributes n_i/N * topk(theta_i - w_global) (fixed k per client, so
+        the all-gather needs no padding), BN buffers are averaged densely.  Every rank applies the same
+        gathered (index, value) lists in global client order, so all ranks end with the same model."""
+        n_tot = float(sum(self.sizes[c] for c in sampled))
+        k = max(1, int(math.ceil(self.cfg.update_topk * self.P)))
+        rows, loc = self._local_rows(sampled)
+        vals = torch.zeros((len(rows), k), dtype=torch.float32, device=self.device)
+        idx = torch.zeros((len(rows), k), dtype=torch.int32, device=self.device)
+        for j, r in enumerate(rows):
+            d = self.theta[r, :self.P] - self.w_global
+            top = torch.topk(d.abs(), k, sorted=False).indices
+            idx[j] = top.int()
+            vals[j] = d.index_select(0, top) * (self.sizes[self.local[r]] / n_tot)
+        cid = torch.tensor(loc, dtype=torch.float32, device=self.device)
+        g_vals = rt.all_gather_cat(vals.view(-1), self.info).view(-1, k)
+        g_idx = rt.all_gather_cat(idx.view(-1), self.info).view(-1, k).long()
+        g_cid = rt.all_gather_cat(cid, self.info)
+        order = torch.argsort(g_cid)
+        upd = torch.zeros(self.P, dtype=torch.float32, device=self.device)
+        for j in order.tolist():  # fixed order: identical fp32 sums on every rank
+            upd.index_add_(0, g_idx[j], g_vals[j])
+        self.w_global.add_(upd)
+        bsum = torch.zeros(self.Q, dtype=torch.float32, device=self.device)
+        for r in rows:
+            bsum.add_(self.bufs[r, :self.Q], alpha=self.sizes[self.local[r]] / n_tot)
+        rt.all_reduce_buckets(bsum, self.info)
+        self.b_global.copy_(bsum)
+        self.stat_info["aggregate_elems"] = int(2 * k * len(sampled))
+
+    def _compact_index(self, Pp):
+        """Flat indices of the aggregation buffer that can be non-zero: SalientGrads' global mask zeroes the
+        pruned weights on every client after every step, so their weighted sum is exactly 0 and they need
+        not travel (params kept by the mask + all BN buffers)."""
+        key = (Pp, id(self.mask))
+        if getattr(self, "_cidx_key", None) != key:
+            keep = torch.ones(Pp + self.Q, dtype=torch.bool, device=self.device)
+            keep[:self.P] = self.mask > 0
+            keep[self.P:Pp] = False
+            self._cidx = keep.nonzero().view(-1)
+            self._cidx_key = key
+        return self._cidx
+
+    def weighted_partial(self, theta, bufs, rows, weights):
+        """[Pp + Q] buffer = sum_j weights[j] * (theta[rows[j]], bufs[rows[j]]) (local partial of a FedAvg)."""
+        Pp = (self.P + 63) // 64 * 64  # keep the buffer section 16-B aligned for the vectorised kernel
+        buf = torch.zeros(Pp + self.Q, dtype=torch.float32, device=self.device)
+        if rows:
+            w = torch.tensor(weights, dtype=torch.float32, device=self.device)
+            if self.device.type == "cuda" and _contiguous(rows):
+                m, st = self.e.m, torch.cuda.current_stream().cuda_stream
+                lo = rows[0]
+                m.weighted_rows_sum(theta[lo].data_ptr(), w.data_ptr(), len(rows), self.P, theta.stride(0), 0.0,
+                                    buf.data_ptr(), st)
+                m.weighted_rows_sum(bufs[lo].data_ptr(), w.data_ptr(), len(rows), self.Q, bufs.stride(0), 0.0,
+                                    buf[Pp:].data_ptr(), st)
+            else:
+                ix = torch.tensor(rows, device=self.device)
+                buf[:self.P] = (w.view(-1, 1) * theta[ix]).sum(0)
+                buf[Pp:] = (w.view(-1, 1) * bufs[ix]).sum(0)
+        return buf, Pp
+
+    def aggregate_fedavg(self, sampled):
+        """w_global = sum_i n_i/sum n * w_i over sampled clients (params + buffers), one all-reduce (of the
+        mask-compacted coordinates when a SalientGrads mask is active)."""
+        n_tot = float(sum(self.sizes[c] for c in sampled))
+        rows, loc = self._local_rows(sampled)
+        buf, Pp = self.weighted_partial(self.theta, self.bufs, rows, [self.sizes[c] / n_tot for c in loc])
+        sparse = (self.info.enabled and self.cfg.sparse_aggregate and self.alg == "salientgrads"
+                  and self.mask is not None)
+        if sparse:
+            idx = self._compact_index(Pp)
+            packed = buf.index_select(0, idx)
+            rt.all_reduce_buckets(packed, self.info)
+            buf.zero_()
+            buf.index_copy_(0, idx, packed)
+            self.stat_info["aggregate_elems"] = int(idx.numel())
+        else:
+            rt.all_reduce_buckets(buf, self.info)
+            self.stat_info["aggregate_elems"] = int(buf.numel())
+        self.w_global.copy_(buf[:self.P])
+        self.b_global.copy_(buf[Pp:])
+
+    def aggregate_robust(self, sampled):
+        """Byzantine-robust aggregation (BASELINE config 4): every sampled client's (params, buffers) row is
+        all-gathered to every rank (xGMI all-gather of K x (P+Q) fp32; 128 x 10.3 MB = 1.3 GB fits HBM
+        easily), then Krum / Multi-Krum / coordinate median / trimmed mean run on device with the same
+        deterministic result on all ranks (``core/robustness.py``).  BN buffers follow the selected clients
+        for Krum and are coordinate-aggregated otherwise."""
+        from ..core import robustness as R
+        rows, loc = self._local_rows(sampled)
+        ids = torch.tensor(loc, dtype=torch.float32, device=self.device)
+        W = self.P + self.Q
+        lm = torch.cat([self.theta[rows, :self.P], self.bufs[rows, :self.Q]], 1) if rows else \
+            torch.zeros((0, W), device=self.device)
+        allrows = rt.all_gather_cat(lm.reshape(-1).contiguous(), self.info).view(-1, W)
+        allids = rt.all_gather_cat(ids, self.info).long()
+        order = torch.argsort(allids)  # deterministic client order on every rank
+        M = allrows.index_select(0, order)
+        kind = self.cfg.aggregator
+        if kind in ("krum", "multikrum"):
+            m = 1 if kind == "krum" else (self.cfg.multikrum_m or max(1, M.shape[0] - self.cfg.byzantine_f))
+            agg, _ = R.krum(M, f=self.cfg.byzantine_f, multi=m)
+        elif kind == "median":
+            agg = R.coordinate_median(M)
+        elif kind == "trimmed_mean":
+            agg = R.trimmed_mean(M, self.cfg.trim_ratio)
+        else:
+            raise ValueError("unknown aggregator %r" % kind)
+        self.w_global.copy_(agg[:self.P])
+        self.b_global.copy_(agg[self.P:])
+        self.stat_info["aggregate_elems"] = int(M.numel())
+
+    # ---------------------------------------------------------------------------------------------- evaluation
+    def _split_of(self, c, which):
+        s = self.splits[c]
+        return {"test": s.test, "train": s.train, "val": getattr(s, "val", None)}[which]
+
+    def _eval_chunk_metrics(self, logits, y):
+        """Per-sample (correct, loss) of logits [..., K] (K = 1: binary head) against labels [...]."""
+        if logits.shape[-1] > 1:  # multi-class models (CrossEntropy trainers of the 2D baselines)
+            loss = F.cross_entropy(logits.reshape(-1, logits.shape[-1]).float(), y.reshape(-1).long(),
+                                   reduction="none").view(y.shape)
+            correct = (logits.argmax(-1) == y.long()).float()
+            return correct, loss
+        logits = logits[..., 0]
+        pred = torch.sigmoid(logits)
+        x = logits if self.cfg.fix_eval_loss else pred  # Q1: the reference feeds probabilities to BCEWithLogits
+        loss = F.binary_cross_entropy_with_logits(x, y, reduction="none")
+        correct = ((pred >= 0.5).float() == y).float()
+        return correct, loss
+
+    def _eval_rows(self, theta, bufs, clients, per_client_rows, which="test"):
+        """Per-client (correct, loss_sum, total) with reference test semantics (Q1).  Clients that share a
+        model row are evaluated together in chunks of ``test_batch`` samples (one launch sequence each)."""
+        out = np.zeros((len(clients), 3), dtype=np.float64)
+        by_row = {}
+        for j, r in enumerate(per_client_rows):
+            by_row.setdefault(r, []).append(j)
+        for r, js in by_row.items():
+            tests = [self._split_of(clients[j], which) for j in js]
+            owner = np.concatenate([np.full(len(t), k) for k, t in enumerate(tests)]).astype(np.int64)
+            allidx = np.concatenate(tests).astype(np.int32) if tests else np.zeros(0, np.int32)
+            if allidx.size == 0:
+                continue
+            th, bu = theta[r:r + 1], bufs[r:r + 1]
+            tb = self.cfg.test_batch
+            acc = torch.zeros((len(js), 3), dtype=torch.float64, device=self.device)
+            own_t = torch.from_numpy(owner).to(self.device)
+            all_t = self._upload_i32(allidx)
+            for s in range(0, allidx.size, tb):
+                idx = all_t[s:s + tb]
+                logits = self.e.eval_logits(th, bu, idx, 1, idx.numel()).view(idx.numel(), -1)
+                y = self.e.labels.index_select(0, idx.long().to(self.e.labels.device)).to(logits.device).float()
+                correct, loss = self._eval_chunk_metrics(logits, y)
+                o = own_t[s:s + idx.numel()]
+                acc[:, 0].index_add_(0, o, correct.double())
+                acc[:, 1].index_add_(0, o, loss.double())
+                acc[:, 2].index_add_(0, o, torch.ones_like(loss, dtype=torch.float64))
+            out[js] = acc.cpu().numpy()
+        return out
+
+    def eval_grouped(self, theta, bufs, rows, clients, which="test"):
+        """Model row rows[j] on client clients[j]'s split: clients with equal split sizes are evaluated in grouped
+        launches (G rows x n samples); one device->host copy at the end."""
+        out = np.zeros((len(clients), 3), dtype=np.float64)
+        pending = []
+        sizes = {}
+        for j, c in enumerate(clients):
+            sizes.setdefault(len(self._split_of(c, which)), []).append(j)
+        for n, js in sizes.items():
+            if n == 0:
+                continue
+            if n > self.cfg.test_batch:
+                out[js] = self._eval_rows(theta, bufs, [clients[j] for j in js], [rows[j] for j in js], which)
+                continue
+            for grp in self._groups(js):
+                rr = [rows[j] for j in grp]
+                if _contiguous(rr):
+                    th, bu = theta[rr[0]:rr[-1] + 1], bufs[rr[0]:rr[-1] + 1]
+                else:
+                    t = torch.tensor(rr, device=self.device)
+                    th, bu = gather_rows(theta, t), gather_rows(bufs, t)
+                idx = self._upload_i32(np.concatenate([self._split_of(clients[j], which) for j in grp]))
+                logits = self.e.eval_logits(th, bu, idx, len(grp), n).view(len(grp), n, -1)
+                y = self.e.labels.index_select(0, idx.long().to(self.e.labels.device)).to(logits.device).float()
+                y = y.view(len(grp), n)
+                correct, loss = self._eval_chunk_metrics(logits, y)
+                pending.append((grp, torch.stack([correct.sum(1), loss.sum(1),
+                                                  torch.full_like(loss[:, 0], float(n))], 1).double()))
+        if pending:
+            host = torch.cat([r for _, r in pending], 0).cpu().numpy()
+            o = 0
+            for grp, _ in pending:
+                out[grp] = host[o:o + len(grp)]
+                o += len(grp)
+        return out
+
+    def _eval_buffers(self, k):
+        if self._eval_cache is None or self._eval_cache[0].shape[0] < k:
+            self._eval_cache = (padded_rows(k, self.P, self.device), padded_rows(k, self.Q, self.device))
+        th, bu = self._eval_cache
+        return th[:k], bu[:k]
+
+    def _eval_global_and_personal(self, theta=None, bufs=None):
+        """Global model and every local client's personal model on that client's test split, in ONE grouped
+        launch sequence of 2C model rows (C personal rows + C copies of the global model) — full-client kernel
+        shapes instead of a G = 1 global evaluation."""
+        C = self.C
+        theta = self.theta if theta is None else theta
+        bufs = self.bufs if bufs is None else bufs
+        th, bu = self._eval_buffers(2 * C)
+        with torch.no_grad():
+            th[:C].copy_(theta[:C])
+            th[C:].copy_(self.w_global.expand(C, -1))
+            bu[:C].copy_(bufs[:C])
+            bu[C:].copy_(self.b_global.expand(C, -1))
+        res = self.eval_grouped(th, bu, list(range(2 * C)), self.local + self.local)
+        return res[C:], res[:C]
+
+    def gather_metrics(self, clients, arr):
+        """Per-client metric rows of this rank's clients -> [N, k] numpy on every rank (one all-reduce)."""
+        k = arr.shape[1] if arr.ndim == 2 else 1
+        res = torch.zeros((self.N, k), dtype=torch.float64, device=self.device)
+        if len(clients):
+            res[torch.tensor(list(clients), device=self.device)] = torch.from_numpy(
+                np.asarray(arr, dtype=np.float64).reshape(len(clients), k)).to(self.device)
+        rt.all_reduce_buckets(res, self.info)
+        return res.cpu().numpy()
+
+    @staticmethod
+    def mean_acc_loss(r, cols=(0, 1, 2)):
+        ok = r[:, cols[2]] > 0
+        if not ok.any():
+            return 0.0, 0.0
+        return float(np.mean(r[ok, cols[0]] / r[ok, cols[2]])), float(np.mean(r[ok, cols[1]] / r[ok, cols[2]]))
+
+    def evaluate(self, round_idx, theta=None, bufs=None):
+        t0 = time.perf_counter()
+        glob, pers = self._eval_global_and_personal(theta, bufs) if self.C else (np.zeros((0, 3)), np.zeros((0, 3)))
+        r = self.gather_metrics(self.local, np.concatenate([glob, pers], 1))
+        g_acc, g_loss = self.mean_acc_loss(r, (0, 1, 2))
+        p_acc, p_loss = self.mean_acc_loss(r, (3, 4, 5))
+        self.stat_info["global_test_acc"].append(g_acc)
+        self.stat_info["global_test_loss"].append(g_loss)
+        self.stat_info["person_test_acc"].append(p_acc)
+        self.stat_info["person_test_loss"].append(p_loss)
+        if self.log is not None and self.info.is_main:
+            self.log.info("################global_test_on_all_clients : {}".format(round_idx))
+            self.log.info({"global_test_acc": g_acc, "global_test_loss": g_loss})
+            self.log.info({"person_test_acc": p_acc, "person_test_loss": p_loss})
+        self.timers["eval"] += time.perf_counter() - t0
+        return dict(global_test_acc=g_acc, global_test_loss=g_loss, person_test_acc=p_acc, person_test_loss=p_loss)
+
+    # ---------------------------------------------------------------------------------------------- driver
+    def _heartbeat(self):
+        """Lazily started failure detector (multi-rank runs with ``cfg.heartbeat_s`` > 0), else None."""
+        if self.cfg.heartbeat_s <= 0 or self.info.world <= 1:
+            return None
+        if getattr(self, "_hb", None) is None:
+            from ..comm.failure import HeartbeatMonitor, default_store
+            store = default_store()
+            self._hb = HeartbeatMonitor(store, self.info.rank, self.info.world, self.cfg.heartbeat_s,
+                                        30.0 * self.cfg.heartbeat_s) if store is not None else False
+        return self._hb or None
+
+    def _round_start(self, round_idx):
+        hb = self._heartbeat()
+        if hb is not None:
+            hb.check_or_raise()  # before the round's collectives: a dead peer would block them until the timeout
+        if self.log is not None and self.info.is_main:
+            self.log.info("################Communication round : {}".format(round_idx))
+
+    def _eval_due(self, round_idx):
+        f = self.cfg.frequency_of_the_test
+        return bool(f) and (round_idx % f == 0 or round_idx == self.cfg.comm_round - 1)
+
+    def run_round(self, round_idx, sync_timers=False):
+        t0 = time.perf_counter()
+        self._round_start(round_idx)
+        sampled = self.sample_clients(round_idx)
+        if self.log is not None and self.info.is_main:
+            self.log.info("client_indexes = " + str(np.array(sampled)))
+        self.local_train(round_idx, sampled)
+        if sync_timers:
+            self._sync()
+        t1 = time.perf_counter()
+        self.aggregate(sampled)
+        if sync_timers:
+            self._sync()
+        t2 = time.perf_counter()
+        self.timers["train"] += t1 - t0
+        self.timers["aggregate"] += t2 - t1
+        self.stat_info["sum_training_flops"] += int(self.cfg.epochs * sum(self.sizes[c] for c in sampled))
+        res = None
+        if self._eval_due(round_idx):
+            res = self.evaluate(round_idx)
+            if sync_timers:
+                self._sync()
+        self.stat_info["round_time"].append(time.perf_counter() - t0)
+        return res
+
+    def finetune_round(self):
+        """FedAvg's final "fine-tune" pass (``fedavg_api.py:78-88``): every client trains one more local round from
+        the final w_global (the reference passes round -1, so lr = lr / lr_decay) and the global model plus these
+        fine-tuned personal models are evaluated; w_global is unchanged."""
+        rows, loc = self._local_rows(range(self.N))
+        if not rows:
+            return self.evaluate(-1)
+        fin = RowSet(padded_rows(self.C, self.P, self.device), padded_rows(self.C, self.Q, self.device))
+        fin.theta.copy_(self.w_global.expand(self.C, -1))
+        fin.bufs.copy_(self.b_global.expand(self.C, -1))
+        self.train_rows(fin, rows, loc, -1, self.cfg.epochs, self._fedavg_spec(), tag=3)
+        return self.evaluate(-1, fin.theta, fin.bufs)
+
+    def train(self):
+        if self.alg == "salientgrads":
+            self.generate_global_mask_snip()
+        for r in range(self.cfg.comm_round):
+            self.run_round(r)
+        self.finish()
+        return self.stat_info
+
+    def finish(self):
+        """Reference round tail: SalientGrads re-evaluates (``sailentgrads_api.py:147``), FedAvg fine-tunes every
+        client once more and evaluates (``fedavg_api.py:78-88``)."""
+        if not self.cfg.final_round:
+            return None
+        if self.alg == "salientgrads":
+            return self.evaluate(-1)
+        return self.finetune_round()

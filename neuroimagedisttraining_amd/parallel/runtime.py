@@ -122,6 +122,34 @@ def all_gather_cat(t: torch.Tensor, info: DistInfo):
     return torch.cat([b[:s] for b, s in zip(bufs, sizes)])
 
 
+def exchange_rows(info: DistInfo, owner, needs, row_of, width, device, dtype=torch.float32):
+    """Point-to-point fetch of client rows (gossip neighbours, FedFomo candidates) — RCCL send/recv over xGMI
+    instead of an all-gather of every client.
+
+    ``owner[c]``: rank holding client c; ``needs[r]``: clients rank r needs (every rank passes the same ``needs``,
+    so both sides of each transfer agree on the schedule); ``row_of(c)`` -> 1-D tensor [width] of a client this rank
+    owns.  Returns {c: tensor [width]} for this rank's remote needs.  All transfers go out as one batched group."""
+    if not info.enabled:
+        return {}
+    import torch.distributed as dist
+    p2p, recv = [], {}
+    for r in range(info.world):
+        for c in sorted(set(needs[r])):
+            o = int(owner[c])
+            if o == r:
+                continue
+            if o == info.rank:
+                p2p.append(dist.P2POp(dist.isend, row_of(c).contiguous(), r))
+            if r == info.rank:
+                buf = torch.empty(width, dtype=dtype, device=device)
+                recv[c] = buf
+                p2p.append(dist.P2POp(dist.irecv, buf, o))
+    if p2p:
+        for q in dist.batch_isend_irecv(p2p):
+            q.wait()
+    return recv
+
+
 def barrier(info: DistInfo):
     if info.enabled:
         if info.backend == "nccl":

@@ -28,7 +28,7 @@ def save_runner(runner, directory, next_round):
     if runner.info.is_main:
         glob = {"w_global": runner.w_global.detach().cpu(), "b_global": runner.b_global.detach().cpu(),
                 "mask": None if runner.mask is None else runner.mask.detach().cpu(),
-                "next_round": torch.tensor(next_round), "step_seed": torch.tensor(runner._step_seed)}
+                "next_round": torch.tensor(next_round)}
         _atomic_save(glob, os.path.join(directory, "global.pt"))
         with open(os.path.join(directory, "stat_info.json.tmp"), "w") as f:
             json.dump({k: v for k, v in runner.stat_info.items() if isinstance(v, (list, int, float))}, f)
@@ -45,11 +45,7 @@ def load_runner(runner, directory):
     runner.w_global.copy_(glob["w_global"].to(runner.device))
     runner.b_global.copy_(glob["b_global"].to(runner.device))
     if glob["mask"] is not None:
-        runner.mask = glob["mask"].to(runner.device)
-        if hasattr(runner, "_graphs"):
-            runner._graphs = {}  # captured steps reference the previous mask tensor
-    if "step_seed" in glob:  # dropout stream position (bit-exact resume)
-        runner._step_seed = int(glob["step_seed"])
+        runner.set_mask(glob["mask"].to(runner.device))
     runner.theta.copy_(shard["theta"].to(runner.device))
     runner.bufs.copy_(shard["bufs"].to(runner.device))
     p = os.path.join(directory, "stat_info.json")

@@ -220,7 +220,7 @@ def test_bn_relu_pool_and_bwd():
     dy = torch.empty_like(y)
     m.bn_bwd(1, y.data_ptr(), dp.data_ptr(), out.data_ptr(), am.data_ptr(), sc.data_ptr(), sh.data_ptr(),
              mean.data_ptr(), invstd.data_ptr(), G * B, B, D, H, W, C, part.data_ptr(), 64, theta.data_ptr(), P, 0,
-             grad.data_ptr(), P, 0, C, 2 * C, coef.data_ptr(), dy.data_ptr(), _st())
+             grad.data_ptr(), P, 0, C, 2 * C, coef.data_ptr(), dy.data_ptr(), 0, _st())
     torch.cuda.synchronize()
     for g in range(G):
         # fp64 CPU autograd oracle (first-max pooling semantics, no library BN/pool kernels involved)
@@ -376,7 +376,7 @@ def test_conv1_fused_fwd_and_sparse_wgrad():
                   b["c1part"].data_ptr(), b["w125"].data_ptr(), b["mu"].data_ptr(), b["covw"].data_ptr(),
                   b["i1"].data_ptr(), theta.data_ptr(), P, o["features.1.weight"], grads.data_ptr(), P,
                   o["features.0.weight"], o["features.0.bias"], o["features.1.weight"], o["features.1.bias"],
-                  1.0 / 255.0, st)
+                  1.0 / 255.0, 0, st)
     torch.cuda.synchronize()
     ow, og, ob = o["features.0.weight"], o["features.1.weight"], o["features.1.bias"]
     for g in range(G):

@@ -73,7 +73,7 @@ def main():
                                              p(b["w125"]), p(b["mu"]), p(b["covw"]), p(b["i1"]), p(theta), P,
                                              o["features.1.weight"], p(grads), P, o["features.0.weight"],
                                              o["features.0.bias"], o["features.1.weight"], o["features.1.bias"],
-                                             1.0 / 255, st), 2 * 64 * 125 * 19 * 23 * 19 * NB)
+                                             1.0 / 255, 0, st), 2 * 64 * 125 * 19 * 23 * 19 * NB)
     cfgs = [("conv2", "p1", 4, (19, 23, 19), 64, 128, 0), ("conv3", "p2", 8, (5, 7, 5), 128, 192, 1),
             ("conv4", "h3", 11, (5, 7, 5), 192, 192, 1), ("conv5", "h4", 14, (5, 7, 5), 192, 128, 1)]
     outs = {4: "y2", 8: "y3", 11: "y4", 14: "y5"}
