@@ -10,6 +10,10 @@ and every client's personal model on its 36-sample test split (frequency_of_the_
 The 64 clients are sharded over the N GPUs (strong scaling: total work per round is fixed as N grows).
 The SNIP mask phase runs once before the warmup rounds (as in the reference, it is not per round).
 
+``--algorithm`` selects any other algorithm of the harness on the same executor (fedavg / fedprox [+ robust
+``--aggregator``], dispfl, subavg, ditto, dpsgd, fedfomo, local) and ``--size-skew A`` gives the clients
+Dirichlet(A) sizes with the same total sample count (ragged federations).
+
 Data: synthetic ABCD-shape (1x121x145x121 uint8) volumes with a non-IID (Dirichlet 0.3) label prior per
 client, generated on device; random-init AlexNet3D_Dropout weights.  Compute: bf16 MFMA with fp32 accumulate,
 fp32 master weights / optimizer / BN statistics.
@@ -26,9 +30,13 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
-# Measured on MI355X (1 GPU) with tools/eager_baseline.py: PyTorch-ROCm eager fp32, reference semantics
+# Measured on MI355X (1 GPU) with tools/eager_baseline.py: PyTorch-ROCm eager, reference semantics
 # (sequential clients, one shared nn.Module, per-step mask multiply), same 64-client config.  See BASELINE.md.
-EAGER_BASELINE_ROUNDS_PER_S = 0.04611  # fp32, steady-state (rounds 1-2), profiles/r1_eager_baseline_steady.txt
+EAGER_BASELINE_ROUNDS_PER_S = 0.04611       # fp32 (the reference's precision), profiles/r1_eager_baseline_steady.txt
+EAGER_BF16_BASELINE_ROUNDS_PER_S = 0.0640   # same eager path under bf16 autocast (equal-precision comparison)
+ALGOS = ["salientgrads", "fedavg", "fedprox", "dispfl", "subavg", "ditto", "dpsgd", "fedfomo", "local"]
+NAMES = {"salientgrads": "SalientGrads", "fedavg": "FedAvg", "fedprox": "FedProx", "dispfl": "DisPFL",
+         "subavg": "SubAvg", "ditto": "Ditto", "dpsgd": "D-PSGD", "fedfomo": "FedFomo", "local": "Local"}
 
 
 def parse():
@@ -44,55 +52,59 @@ def parse():
     ap.add_argument("--group", type=int, default=0, help="max clients per lockstep launch (0 = all local)")
     ap.add_argument("--dense-ratio", type=float, default=0.5)
     ap.add_argument("--seed", type=int, default=1024)
+    ap.add_argument("--frac", type=float, default=1.0)
+    ap.add_argument("--size-skew", type=float, default=0.0, help="Dirichlet alpha of per-client sizes (0 = equal)")
     ap.add_argument("--no-eval", action="store_true", help="(diagnostic only) skip per-round evaluation")
-    ap.add_argument("--algorithm", default="salientgrads", choices=["salientgrads", "fedavg", "fedprox"],
-                    help="other BASELINE configs: fedavg (config 2: --clients 8), fedprox + --aggregator (config 4)")
+    ap.add_argument("--algorithm", default="salientgrads", choices=ALGOS)
     ap.add_argument("--aggregator", default="fedavg", choices=["fedavg", "krum", "multikrum", "median", "trimmed_mean"])
     ap.add_argument("--prox-mu", type=float, default=0.01)
-    ap.add_argument("--phase-timers", action="store_true")
+    ap.add_argument("--cs", default="ring", help="D-PSGD topology")
+    ap.add_argument("--phase-timers", action="store_true", help="synchronised per-phase timers (adds syncs)")
     return ap.parse_args()
 
 
 def main():
     args = parse()
+    import numpy as np
     from neuroimagedisttraining_amd.parallel import runtime as rt
-    from neuroimagedisttraining_amd.engine.executor import FLConfig, FLRunner, HipEngine
-    from neuroimagedisttraining_amd.data.synthetic_fl import build_fl_volumes, to_hip_store
+    from neuroimagedisttraining_amd.engine.executor import ClientSplit, FLConfig, HipEngine
+    from neuroimagedisttraining_amd.engine.personalized import make_runner
+    from neuroimagedisttraining_amd.data.synthetic_fl import build_fl_volumes, skewed_sizes, to_hip_store
     from neuroimagedisttraining_amd.models.alexnet3d import AlexNet3D_Dropout
 
     info = rt.init_distributed(prefer_gpu=True)
     assert info.device.type == "cuda", "bench.py needs a GPU"
     torch.manual_seed(args.seed)
-    shards = rt.shard_clients([args.train_per_client] * args.clients, info.world)
+    per = args.train_per_client + args.test_per_client
+    tot = skewed_sizes(args.clients, per, args.size_skew, seed=args.seed)
+    n_test = [max(1, int(round(t * args.test_per_client / per))) for t in tot]
+    n_train = [t - e for t, e in zip(tot, n_test)]
+    shards = rt.shard_clients(n_train, info.world)
     local = shards[info.rank]
     t0 = time.perf_counter()
-    vol, labels, splits_local = build_fl_volumes(local, args.clients, args.train_per_client, args.test_per_client,
-                                                 info.device, seed=args.seed)
+    vol, labels, splits_local = build_fl_volumes(local, args.clients, n_train, n_test, info.device, seed=args.seed)
     x8, mom = to_hip_store(vol)
     del vol
+    if args.algorithm == "fedfomo":  # validation split: 10 % of client 0's train size (data_val_loader.py:275)
+        nval = int(0.1 * n_train[0])
+        splits_local = {c: ClientSplit(s.train[nval:], s.test, s.train[:nval]) for c, s in splits_local.items()}
+        n_train = [n - nval for n in n_train]
     torch.cuda.synchronize()
     t_data = time.perf_counter() - t0
 
     # splits indexed by global client id; non-local clients only need their sizes (sampling weights)
-    import numpy as np
-    from neuroimagedisttraining_amd.engine.executor import ClientSplit
-    splits = []
-    for c in range(args.clients):
-        if c in splits_local:
-            splits.append(splits_local[c])
-        else:
-            splits.append(ClientSplit(train=np.zeros(args.train_per_client, dtype=np.int64),
-                                      test=np.zeros(args.test_per_client, dtype=np.int64)))
+    splits = [splits_local[c] if c in splits_local else
+              ClientSplit(train=np.zeros(n_train[c], dtype=np.int64), test=np.zeros(n_test[c], dtype=np.int64))
+              for c in range(args.clients)]
     model = AlexNet3D_Dropout(num_classes=1)
     engine = HipEngine(model, x8, mom, labels, info.device)
     cfg = FLConfig(comm_round=args.warmup + args.steps, epochs=args.epochs, batch_size=args.batch,
-                   dense_ratio=args.dense_ratio, seed=args.seed, group=args.group,
+                   dense_ratio=args.dense_ratio, seed=args.seed, group=args.group, frac=args.frac,
                    frequency_of_the_test=0 if args.no_eval else 1, aggregator=args.aggregator,
-                   prox_mu=args.prox_mu if args.algorithm == "fedprox" else 0.0)
-    alg = "salientgrads" if args.algorithm == "salientgrads" else "fedavg"
-    runner = FLRunner(engine, splits, cfg, info, model, logger=None, algorithm=alg)
+                   prox_mu=args.prox_mu if args.algorithm == "fedprox" else 0.0, cs=args.cs, final_round=False)
+    runner = make_runner(args.algorithm, engine, splits, cfg, info, model, logger=None)
     t0 = time.perf_counter()
-    if alg == "salientgrads":
+    if runner.alg == "salientgrads":
         runner.generate_global_mask_snip()
     torch.cuda.synchronize()
     t_snip = time.perf_counter() - t0
@@ -108,18 +120,24 @@ def main():
     for r in range(args.warmup, args.warmup + args.steps):
         res = runner.run_round(r, sync_timers=args.phase_timers)
     torch.cuda.synchronize()
+    t_local = time.perf_counter() - t0   # this rank's own work (before waiting for the slowest rank)
     rt.barrier(info)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
+    per_rank = rt.all_gather_cat(torch.tensor([t_local], dtype=torch.float64, device=info.device), info)
+    per_rank = [round(float(x), 4) for x in per_rank.cpu()]
     dt = rt.max_over_ranks(dt, info)
     ms = dt * 1000.0 / max(1, args.steps)
     value = args.steps / dt
-    headline = args.algorithm == "salientgrads" and args.clients == 64 and args.aggregator == "fedavg"
+    headline = (args.algorithm == "salientgrads" and args.clients == 64 and args.aggregator == "fedavg"
+                and args.size_skew == 0 and args.frac == 1.0)
     if info.is_main:
         out = {
             "metric": ("FL rounds/sec (whole node), 64-client SalientGrads 3D-CNN on ABCD-shape synth" if headline else
-                       "FL rounds/sec (whole node), %d-client %s%s 3D-CNN on ABCD-shape synth"
-                       % (args.clients, args.algorithm, "" if args.aggregator == "fedavg" else "+" + args.aggregator)),
+                       "FL rounds/sec (whole node), %d-client %s%s 3D-CNN on ABCD-shape synth%s"
+                       % (args.clients, NAMES[args.algorithm],
+                          "" if args.aggregator == "fedavg" else "+" + args.aggregator,
+                          "" if args.size_skew == 0 else " (size skew %.2f)" % args.size_skew)),
             "value": round(value, 4),
             "unit": "rounds/s",
             "n_gpus": info.world,
@@ -128,22 +146,25 @@ def main():
             "ms_per_step": round(ms, 2),
             "higher_is_better": True,
             "scaling": "strong",
-            "vs_baseline": (round(value / EAGER_BASELINE_ROUNDS_PER_S, 2)
-                            if EAGER_BASELINE_ROUNDS_PER_S and headline else None),
+            "vs_baseline": (round(value / EAGER_BASELINE_ROUNDS_PER_S, 2) if headline else None),
+            "vs_bf16_eager": (round(value / EAGER_BF16_BASELINE_ROUNDS_PER_S, 2) if headline else None),
             "dtype": "bf16",
             "data": "synthetic",
-            "config": {"model": "AlexNet3D_Dropout", "algorithm": {"salientgrads": "SalientGrads", "fedavg": "FedAvg",
-                                                                  "fedprox": "FedProx"}[args.algorithm],
-                       "aggregator": args.aggregator, "clients": args.clients,
+            "config": {"model": "AlexNet3D_Dropout", "algorithm": NAMES[args.algorithm],
+                       "aggregator": args.aggregator, "clients": args.clients, "frac": args.frac,
                        "global_batch": args.batch * args.clients, "batch_per_client": args.batch,
                        "seq_len": None, "input": "1x121x145x121", "epochs": args.epochs,
                        "train_per_client": args.train_per_client, "test_per_client": args.test_per_client,
+                       "size_skew": args.size_skew, "samples_train_total": int(sum(n_train)),
                        "dense_ratio": args.dense_ratio, "eval_every_round": not args.no_eval,
                        "parallelism": "clients-sharded-dp%d" % info.world},
             "setup_s": {"data": round(t_data, 2), "snip_mask": round(t_snip, 2)},
-            "phase_s": {k: round(v, 3) for k, v in runner.timers.items()},
+            "rank_busy_s": per_rank,
+            "rank_imbalance": round(max(per_rank) / (sum(per_rank) / len(per_rank)), 3) if per_rank else None,
             "last_round_metrics": res,
         }
+        if args.phase_timers:
+            out["phase_s"] = {k: round(v, 3) for k, v in runner.timers.items()}
         print(json.dumps(out), flush=True)
     rt.shutdown(info)
 

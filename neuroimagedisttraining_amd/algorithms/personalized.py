@@ -26,12 +26,6 @@ import torch
 
 from .common import APIBase, client_sampling, summarize, weighted_average, uniform_average
 from . import sparse as SP
-from ..comm.topology import mixing_matrix
-
-
-def _mask_params(trainer):
-    names = set(SP.weight_mask_names(trainer.model))
-    return {n: p for n, p in trainer.model.named_parameters() if n in names}
 
 
 # ------------------------------------------------------------------------------------------------ DisPFL
@@ -40,12 +34,13 @@ class DisPFLAPI(APIBase):
     def _benefit_choose(self, round_idx, cur_clnt, total, per_round, dist_local=None, total_dist=None, cs=None,
                         active=None):
         if total == per_round:
-            return np.array([i for i in range(total) if i != cur_clnt])
-        # the reference forces cs = "random" (dispfl_api.py:201)
-        np.random.seed(round_idx + cur_clnt)
-        cand = [i for i in range(total) if i != cur_clnt and (active is None or active[i] == 1)]
-        k = min(per_round, len(cand))
-        return np.random.choice(cand, k, replace=False) if k > 0 else np.array([], dtype=int)
+            return np.array(list(range(total)))
+        # the reference forces cs = "random" (dispfl_api.py:201) and draws from the (global) numpy stream
+        k = min(per_round, total)
+        idx = self.np_rng.choice(range(total), k, replace=False)
+        while cur_clnt in idx:
+            idx = self.np_rng.choice(range(total), k, replace=False)
+        return idx
 
     def _aggregate_func(self, clnt, nei, w_per_mdls, masks):
         """Masked neighbour average (used only with ``dispfl_aggregate``)."""
@@ -64,23 +59,29 @@ class DisPFLAPI(APIBase):
     def train(self):
         a = self.args
         tr = self.model_trainer
-        params = _mask_params(tr)
+        # masks cover every named parameter (get_trainable_params, DisPFL/my_model_trainer.py:125-129)
+        params = {n: p.detach().cpu() for n, p in tr.model.named_parameters()}
         N = a.client_num_in_total
+        self.np_rng = np.random.RandomState(getattr(a, "seed", 0))
+        gen = torch.Generator().manual_seed(getattr(a, "seed", 0) + 17)  # mask init stream (same as the executor's DisPFLRunner)
         dense = [a.dense_ratio] * N
         dist = "uniform" if getattr(a, "uniform", False) else "ERK"
-        sp = SP.erk_sparsities(params, a.dense_ratio, erk_power_scale=getattr(a, "erk_power_scale", 1.0),
-                               distribution=dist)
+        eps = getattr(a, "erk_power_scale", 1.0)
+        sp = SP.erk_sparsities(params, a.dense_ratio, erk_power_scale=eps, distribution=dist)
         if not getattr(a, "different_initial", False):
-            base = SP.init_masks(params, sp)
+            base = SP.init_masks(params, sp, generator=gen)
             masks = [SP.copy_masks(base) for _ in range(N)]
         elif not getattr(a, "diff_spa", False):
-            masks = [SP.init_masks(params, sp) for _ in range(N)]
+            masks = [SP.init_masks(params, sp, generator=gen) for _ in range(N)]
         else:
             p_divide = [0.2, 0.4, 0.6, 0.8, 1.0]
             masks = []
             for i in range(N):
                 dense[i] = p_divide[i % 5]
-                masks.append(SP.init_masks(params, SP.erk_sparsities(params, dense[i], distribution=dist)))
+                masks.append(SP.init_masks(params, SP.erk_sparsities(params, dense[i], erk_power_scale=eps,
+                                                                     distribution=dist), generator=gen))
+        dev = next(tr.model.parameters()).device
+        masks = [{k: v.to(dev) for k, v in m.items()} for m in masks]
         w_global = tr.get_model_params()
         w_per = []
         for c in range(N):
@@ -94,18 +95,23 @@ class DisPFLAPI(APIBase):
         for round_idx in range(a.comm_round):
             t0 = time.perf_counter()
             self.logger.info("################Communication round : %d", round_idx)
-            active = np.random.choice([0, 1], size=N, p=[1.0 - a.active, a.active])
+            active = self.np_rng.choice([0, 1], size=N, p=[1.0 - a.active, a.active])
             w_last = copy.deepcopy(w_per)
             shared_last = [SP.copy_masks(m) for m in shared]
             after, before = [], []
             for c in range(N):
                 d, tot = SP.hamming_distance(shared_last[c], masks[c])
                 dist_locals[c][c] = d
-                nei = np.array([]) if active[c] == 0 else self._benefit_choose(
+                nei = np.array([], dtype=int) if active[c] == 0 else self._benefit_choose(
                     round_idx, c, N, a.client_num_per_round, dist_locals[c], tot, a.cs, active)
+                if N != a.client_num_per_round:
+                    nei = np.append(nei, c)
+                nei = np.sort(nei).astype(int)
                 for j in nei:
-                    dist_locals[c][int(j)], _ = SP.hamming_distance(masks[c], shared_last[int(j)])
-                w_local = self._aggregate_func(c, [int(j) for j in nei], w_last, shared_last) if (agg and len(nei)) \
+                    if int(j) != c:
+                        dist_locals[c][int(j)], _ = SP.hamming_distance(masks[c], shared_last[int(j)])
+                w_local = self._aggregate_func(c, [int(j) for j in nei], w_last, shared_last) if (agg and len(nei)
+                                                                                                  and active[c]) \
                     else copy.deepcopy(w_last[c])
                 shared[c] = SP.copy_masks(masks[c])
                 client = self.client_list[c]
@@ -120,6 +126,8 @@ class DisPFLAPI(APIBase):
                 if not getattr(a, "static", False):
                     grad = None if getattr(a, "dis_gradient_check", False) else \
                         tr.screen_gradients(client.local_training_data, self.device)
+                    if grad is not None:
+                        grad = {k: v.to(dev) for k, v in grad.items()}
                     new_m, num_remove = SP.fire_mask(masks[c], w_new, round_idx, a.anneal_factor, a.comm_round)
                     masks[c] = SP.regrow_mask(new_m, num_remove, grad)
                 w_per[c] = w_new
@@ -152,8 +160,7 @@ class SubAvgAPI(APIBase):
     def train(self):
         a = self.args
         tr = self.model_trainer
-        params = _mask_params(tr)
-        masks = {n: torch.ones_like(p) for n, p in params.items()}
+        masks = {n: torch.ones_like(p).detach() for n, p in tr.model.named_parameters()}  # every parameter (init_masks)
         N = a.client_num_in_total
         mask_pers = [SP.copy_masks(masks) for _ in range(N)]
         w_global = tr.get_model_params()
@@ -243,8 +250,22 @@ class DittoAPI(APIBase):
 class DPSGDAPI(APIBase):
 
     def _benefit_choose(self, round_idx, cur_clnt, total, per_round, cs="ring"):
-        w = mixing_matrix(cs, total, round_idx=round_idx, neighbors=per_round)
-        return [j for j in np.nonzero(w[cur_clnt])[0].tolist() if j != cur_clnt]
+        """Neighbourhood incl. the client itself (``dpsgd_api.py:116-139`` + the append in ``train``)."""
+        if total == per_round:
+            return list(range(total))
+        if cs == "random":
+            np.random.seed(round_idx + cur_clnt)
+            idx = np.random.choice(range(total), min(per_round, total), replace=False)
+            while cur_clnt in idx:
+                idx = np.random.choice(range(total), min(per_round, total), replace=False)
+            nei = list(idx)
+        elif cs == "ring":
+            nei = [(cur_clnt - 1 + total) % total, (cur_clnt + 1) % total]
+        elif cs == "full":
+            nei = [j for j in range(total) if j != cur_clnt]
+        else:
+            raise ValueError(cs)
+        return sorted(int(j) for j in nei + [cur_clnt])
 
     def train(self):
         a = self.args
@@ -259,15 +280,14 @@ class DPSGDAPI(APIBase):
             last = copy.deepcopy(w_per)
             for c in range(N):
                 nei = self._benefit_choose(round_idx, c, N, a.client_num_per_round, cs)
-                w_local = uniform_average([last[j] for j in sorted(set(nei) | {c})])
+                w_local = uniform_average([last[j] for j in nei])
                 client = self.client_list[c]
                 tr.set_model_params(w_local)
                 tr.set_id(c)
                 tr.train(client.local_training_data, self.device, a, round_idx)
                 w_per[c] = tr.get_model_params()
             w_global = uniform_average(w_per)
-            if round_idx == a.comm_round - 1 or round_idx % max(1, a.frequency_of_the_test) == 0:
-                self._test_on_all_clients(w_global, w_per, round_idx)
+            self._test_on_all_clients(w_global, w_per, round_idx)
             self.stat_info["round_time_s"].append(time.perf_counter() - t0)
         self.w_global, self.w_per_mdls = w_global, w_per
         return w_global
@@ -275,68 +295,84 @@ class DPSGDAPI(APIBase):
 
 # ------------------------------------------------------------------------------------------------ FedFomo
 class FedFomoAPI(APIBase):
+    """Reference ``fedfomo_api.py:53-217``: train from the last model, choose neighbours (argsort of the affinity
+    ``p_choose`` half of the time, random otherwise), weigh them by validation-loss improvement per unit distance
+    (the client's own freshly trained model stands in for itself), move to the weighted combination."""
 
-    def _benefit_choose(self, round_idx, cur_clnt, total, per_round, affinity):
+    def _benefit_choose(self, round_idx, cur_clnt, total, per_round, p_choose):
         if total == per_round:
-            return [i for i in range(total) if i != cur_clnt]
-        np.random.seed(round_idx + cur_clnt)
-        k = min(per_round, total - 1)
-        top = [int(i) for i in np.argsort(-affinity[cur_clnt]) if i != cur_clnt][:k // 2]
-        rest = [i for i in range(total) if i != cur_clnt and i not in top]
-        rnd = list(np.random.choice(rest, k - len(top), replace=False)) if k - len(top) > 0 else []
-        return sorted(top + [int(r) for r in rnd])
+            return list(range(total))
+        p_choose[cur_clnt] = 0
+        if self.py_rng.random() >= 0.5:
+            idx = np.argsort(p_choose)[-per_round:]
+        else:
+            idx = self.np_rng.choice(range(total), per_round, replace=False)
+            while cur_clnt in idx:
+                idx = self.np_rng.choice(range(total), per_round, replace=False)
+        return sorted(int(j) for j in list(idx) + [cur_clnt])
 
-    def _updates_weight_local(self, c, nei, w_per, w_old):
-        """w_j = (L_val(theta_old) - L_val(theta_j)) / ||theta_j - theta_old||, negatives clipped."""
+    def _val(self, c, w):
         client = self.client_list[c]
-        base = client.val_test(w_old) if client.local_val_data is not None else client.local_test(w_old, False)
-        l0 = base["test_loss"] / max(1, base["test_total"])
-        ws = []
-        for j in nei:
-            m = client.val_test(w_per[j]) if client.local_val_data is not None else client.local_test(w_per[j], False)
-            lj = m["test_loss"] / max(1, m["test_total"])
-            d = np.sqrt(max(SP.model_difference({k: v.float() for k, v in w_per[j].items()},
-                                                {k: v.float() for k, v in w_old.items()}), 1e-12))
-            ws.append((l0 - lj) / d)
-        return np.asarray(ws, dtype=np.float64)
+        m = client.val_test(w) if client.local_val_data is not None else client.local_test(w, False)
+        return m["test_loss"]
 
-    def _aggregate_func(self, w_old, nei, weights, w_per):
-        pos = np.maximum(weights, 0)
-        if pos.sum() <= 0:
-            return copy.deepcopy(w_old)
+    def _updates_weight_local(self, c, nei, last, weight_local, w_new):
+        loss_cur = self._val(c, last[c])
+        for j in nei:
+            src = w_new if j == c else last[j]
+            lj = self._val(c, src)
+            d = np.sqrt(max(SP.model_difference({k: v.float() for k, v in src.items()},
+                                                {k: v.float() for k, v in last[c].items()}), 0.0))
+            weight_local[j] = 0.0 if d == 0 else (loss_cur - lj) / d
+        return weight_local
+
+    def _aggregate_func(self, c, nei, last, weights, w_new):
+        wpos = np.maximum(weights[nei], 0)
+        tot = float(np.sum(wpos))
+        if tot == 0.0:
+            return copy.deepcopy(last[c])
         out = {}
-        for k, v in w_old.items():
+        for k, v in last[c].items():
             acc = v.float().clone()
-            for j, wj in zip(nei, pos):
-                if wj > 0:
-                    acc += (wj / pos.sum()) * (w_per[j][k].float() - v.float())
+            for j, wj in zip(nei, wpos):
+                src = w_new if j == c else last[j]
+                acc += (src[k].float() - v.float()) * (wj / tot)
             out[k] = acc.to(v.dtype) if v.is_floating_point() else acc.round().to(v.dtype)  # fixes quirk Q12
         return out
 
     def train(self):
+        import random
         a = self.args
         tr = self.model_trainer
         N = a.client_num_in_total
+        self.np_rng = np.random.RandomState(getattr(a, "seed", 0))
+        self.py_rng = random.Random(getattr(a, "seed", 0))
         w_global = tr.get_model_params()
         w_per = [copy.deepcopy(w_global) for _ in range(N)]
-        affinity = np.zeros((N, N))
+        weights_locals = np.full((N, N), 1.0 / N)
+        p_choose = np.ones((N, N))
         for round_idx in range(a.comm_round):
             t0 = time.perf_counter()
             self.logger.info("################Communication round : %d", round_idx)
             last = copy.deepcopy(w_per)
+            after_train, after_agg = [], []
             for c in range(N):
                 client = self.client_list[c]
                 tr.set_model_params(last[c])
                 tr.set_id(c)
                 tr.train(client.local_training_data, self.device, a, round_idx)
                 w_new = tr.get_model_params()
-                nei = self._benefit_choose(round_idx, c, N, a.client_num_per_round, affinity)
-                wts = self._updates_weight_local(c, nei, last, w_new)
-                for j, wj in zip(nei, wts):
-                    affinity[c][j] += wj
-                w_per[c] = self._aggregate_func(w_new, nei, wts, last)
-            if round_idx == a.comm_round - 1 or round_idx % max(1, a.frequency_of_the_test) == 0:
-                self._local_test_on_all_clients(w_per, round_idx, key="person_test_acc")
+                after_train.append(tr.test(client.local_test_data, self.device, a))
+                nei = self._benefit_choose(round_idx, c, N, a.client_num_per_round, p_choose[c])
+                weights_locals[c] = self._updates_weight_local(c, nei, last, weights_locals[c].copy(), w_new)
+                p_choose[c] = p_choose[c] + weights_locals[c]
+                w_per[c] = self._aggregate_func(c, nei, last, weights_locals[c], w_new)
+                after_agg.append(client.local_test(w_per[c], True))
+            acc0, _ = summarize(after_train)
+            acc, loss = summarize(after_agg)
+            self.stat_info["old_mask_test_acc"].append(acc0)
+            self.stat_info["person_test_acc"].append(acc)
+            self.logger.info({"test_acc": acc, "test_loss": loss})
             self.stat_info["round_time_s"].append(time.perf_counter() - t0)
         self.w_per_mdls = w_per
         return w_per

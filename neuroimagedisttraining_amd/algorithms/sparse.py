@@ -58,24 +58,28 @@ def cosine_annealing(alpha, round_idx, total_rounds):
 
 
 def fire_mask(masks, weights, round_idx, anneal_factor, comm_round):
-    """Drop the ``ceil(drop_ratio * nnz)`` smallest-|w| active weights per layer (cosine-annealed drop ratio)."""
+    """Drop the ``ceil(drop_ratio * nnz)`` smallest-|w| active weights per layer (cosine-annealed drop ratio).
+
+    As in ``DisPFL/client.py:71-82``: ``num_non_zeros`` is a float32 tensor, so the product with the drop ratio is
+    float32; the sort is stable (ties go to the lowest index, like the device kernel)."""
     drop_ratio = cosine_annealing(anneal_factor, round_idx, comm_round)
     new, num_remove = {}, {}
     for n, m in masks.items():
-        nnz = float(m.sum())
-        k = int(math.ceil(drop_ratio * nnz))
+        nnz = m.float().sum()
+        k = int(math.ceil(float(torch.tensor(drop_ratio, dtype=torch.float32) * nnz)))
         num_remove[n] = k
         w = weights[n].to(m.device)
         score = torch.where(m > 0, w.abs(), torch.full_like(w, 1e5))
         out = m.clone().view(-1)
         if k > 0:
-            out[torch.topk(score.view(-1), k, largest=False).indices] = 0
+            out[torch.sort(score.view(-1), stable=True).indices[:k]] = 0
         new[n] = out.view_as(m)
     return new, num_remove
 
 
 def regrow_mask(masks, num_remove, gradient=None, generator=None):
-    """Re-activate ``num_remove`` inactive weights per layer: top-|g| (gradient regrowth) or uniformly at random."""
+    """Re-activate ``num_remove`` inactive weights per layer: top-|g| (gradient regrowth, stable descending sort) or
+    uniformly at random (``DisPFL/client.py:86-99``)."""
     new = {}
     for n, m in masks.items():
         out = m.clone().view(-1)
@@ -84,7 +88,7 @@ def regrow_mask(masks, num_remove, gradient=None, generator=None):
             if gradient is not None:
                 g = gradient[n].to(m.device).abs().view(-1)
                 score = torch.where(out == 0, g, torch.full_like(g, -1e5))
-                out[torch.topk(score, k).indices] = 1
+                out[torch.sort(score, descending=True, stable=True).indices[:k]] = 1
             else:
                 inactive = (out == 0).float()
                 k = min(k, int(inactive.sum()))
@@ -109,18 +113,18 @@ def model_difference(a, b):
 
 # -------------------------------------------------------------------------------------- SubAvg (prune_func)
 def fake_prune(each_prune_ratio, param_dict, mask):
-    """New mask zeroing weights below the ``each_prune_ratio`` percentile of alive |w| per weight layer."""
+    """New mask zeroing weights below the ``each_prune_ratio`` percentile of alive |w| per weight layer
+    (``subavg/prune_func.py:9-30``: numpy.percentile on the float32 alive values, float32 interpolation)."""
     new = dict(mask)
     for n, t in param_dict.items():
         if "weight" in n and "bn" not in n and n in mask:
-            alive = (t * mask[n].to(t.device))
-            alive = alive[alive != 0].abs().float()
-            if alive.numel() == 0:
+            tt = t.detach().float().cpu().numpy()
+            mm = mask[n].detach().float().cpu().numpy()
+            alive = tt[np.nonzero(tt * mm)]
+            if alive.size == 0:
                 continue
-            # numpy.percentile linear interpolation == torch.quantile 'linear'
-            thr = torch.quantile(alive.cpu().double(), each_prune_ratio).item() if alive.numel() > 16_000_000 else \
-                torch.quantile(alive.double(), each_prune_ratio).item()
-            new[n] = torch.where(t.abs() < thr, torch.zeros_like(mask[n]), mask[n].to(t.device))
+            thr = np.percentile(np.abs(alive), each_prune_ratio * 100)
+            new[n] = torch.from_numpy(np.where(np.abs(tt) < thr, 0, mm).astype(np.float32)).to(mask[n].device)
     return new
 
 

@@ -3,11 +3,12 @@
 Flags, defaults and the ``args.identity`` string (the log file name, ``LOG/<dataset>/<identity>.log``) follow
 the reference entry points.  Added flags:
 
-* ``--engine {auto,hip,torch}``: SalientGrads / FedAvg / FedProx on 3D-CNN + ABCD-shape data run on the
-  client-batched MI355X executor (HIP kernels, clients sharded over ranks, RCCL aggregation) when ``hip``
-  (``auto`` = hip if a GPU and the extension are available); ``torch`` = the reference-semantics sequential
-  eager path (also the CPU path).
-* ``--synthetic_abcd 1``, ``--n_per_client``: synthetic ABCD-shape cohort (no HDF5 needed);
+* ``--engine {auto,hip,torch}``: every algorithm (SalientGrads, FedAvg, FedProx, DisPFL, SubAvg, Ditto, D-PSGD,
+  FedFomo, Local) on 3D-CNN + ABCD-shape data runs on the client-batched MI355X executor (HIP kernels, clients
+  sharded over ranks, RCCL collectives) when ``hip`` (``auto`` = hip if a GPU and the extension are available);
+  ``torch`` = the reference-semantics sequential eager path (also the CPU path).
+* ``--synthetic_abcd 1``, ``--n_per_client``: synthetic ABCD-shape cohort (no HDF5 needed); ``--synthetic_abcd 0
+  --data_dir <cohort.nidtvol | dir>`` trains on the real cohort (site clients) on either path;
   ``--synthetic_size N``: N synthetic train images (N/5 test) for CIFAR/Tiny without data files.
 * FedProx / robust aggregation: ``--fedprox_mu``, ``--aggregator {fedavg,krum,multikrum,median,trimmed_mean}``,
   ``--byzantine_f``, ``--trim_ratio``.
@@ -199,7 +200,11 @@ def load_data(args, dataset_name, logger=None):
 
 
 def _use_hip(args, algo):
-    if algo not in ("sailentgrads", "fedavg", "fedprox") or args.dataset != "ABCD" or args.model != "3DCNN":
+    """Every algorithm of the harness runs on the client-batched MI355X executor for the 3D-CNN on ABCD-shape data."""
+    if args.dataset != "ABCD" or args.model != "3DCNN":
+        if args.engine == "hip":
+            raise RuntimeError("--engine hip supports --model 3DCNN --dataset ABCD (AlexNet3D_Dropout on the HIP "
+                               "kernels); use --engine torch for other models")
         return False
     if args.engine == "torch":
         return False
@@ -213,44 +218,123 @@ def _use_hip(args, algo):
     return ok
 
 
-def run_hip(args, algo, logger):
-    """SalientGrads / FedAvg / FedProx on the client-batched MI355X executor."""
+def _resolve_cohort(data_dir):
+    """NIDTVOL1 cohort file for ``--data_dir`` (a ``.nidtvol`` file or a directory holding
+    ``alldatain8bitsnormalized.nidtvol``); raises instead of silently substituting synthetic data."""
+    path = data_dir
+    if os.path.isdir(path):
+        path = os.path.join(path, "alldatain8bitsnormalized.nidtvol")
+    if not os.path.exists(path) or not str(path).endswith(".nidtvol"):
+        raise FileNotFoundError(
+            "--synthetic_abcd 0 needs a NIDTVOL1 cohort (got --data_dir %r); convert the reference HDF5 once with "
+            "`python -m neuroimagedisttraining_amd.data.volume_file convert alldatain8bitsnormalized.h5 "
+            "alldatain8bitsnormalized.nidtvol`" % data_dir)
+    return path
+
+
+def hip_cohort(args, info, logger=None, with_val=False):
+    """(x8, mom, labels, splits) for the HIP engine: this rank's clients' subjects resident in HBM in the engine's
+    polyphase layout, ``splits[c]`` indexing that local store (non-local clients keep only their sizes).
+
+    * real cohort (``--synthetic_abcd 0``): the reference ABCD loader's site-as-client split (21 sites, seeded
+      80/20, ``ABCD/data_loader.py:67-102,157-212``) read from a NIDTVOL1 file by the native reader and streamed
+      into HBM (gather / H2D / polyphase overlapped, ``data/volume_file.py``);
+    * synthetic cohort (default): ``--n_per_client`` ABCD-shape volumes per client with a Dirichlet label prior.
+    ``with_val``: 10 % of client 0's train size moved from every client's train split into a validation split
+    (``cifar10/data_val_loader.py:275-278``; FedFomo)."""
+    from .core import partition as PT
     from .data.synthetic_fl import build_fl_volumes, to_hip_store
-    from .engine.executor import ClientSplit, FLConfig, FLRunner, HipEngine
+    from .engine.executor import ClientSplit
+    from .parallel import runtime as rt
+    N = args.client_num_in_total
+    if not args.synthetic_abcd:
+        from .data.volume_file import VolumeFile, stream_to_device
+        vf = VolumeFile(_resolve_cohort(args.data_dir))
+        train, test, _ = PT.partition_by_site(vf.sites, max_clients=21)
+        if len(train) != N:
+            (logger or logging.getLogger(__name__)).info(
+                "ABCD site split gives %d clients (--client_num_in_total %d ignored, quirk Q9)", len(train), N)
+            N = args.client_num_in_total = len(train)
+            args.client_num_per_round = int(N * args.frac)
+        tr = [np.asarray(train[c]) for c in range(N)]
+        te = [np.asarray(test[c]) for c in range(N)]
+        shards = rt.shard_clients([len(t) for t in tr], info.world)
+        mine = shards[info.rank]
+        subj = np.concatenate([np.concatenate([tr[c], te[c]]) for c in mine]) if mine else np.zeros(0, np.int64)
+        x8, mom = stream_to_device(vf, subj, info.device, hip_store=True)
+        labels = torch.from_numpy(vf.labels[subj].astype(np.float32)).to(info.device)
+        local, off = {}, 0
+        for c in mine:
+            local[c] = ClientSplit(np.arange(off, off + len(tr[c])), np.arange(off + len(tr[c]),
+                                                                              off + len(tr[c]) + len(te[c])))
+            off += len(tr[c]) + len(te[c])
+        sizes = [(len(tr[c]), len(te[c])) for c in range(N)]
+    else:
+        n_test = max(1, int(round(args.n_per_client * 0.2)))
+        n_train = args.n_per_client - n_test
+        shards = rt.shard_clients([n_train] * N, info.world)
+        vol, labels, local = build_fl_volumes(shards[info.rank], N, n_train, n_test, info.device, seed=args.seed,
+                                              alpha=args.partition_alpha)
+        x8, mom = to_hip_store(vol)
+        del vol
+        sizes = [(n_train, n_test)] * N
+    if with_val:
+        nval = int(0.1 * sizes[0][0])
+        for c, sp in local.items():
+            local[c] = ClientSplit(sp.train[nval:], sp.test, sp.train[:nval])
+        sizes = [(a - nval, b) for a, b in sizes]
+    splits = [local.get(c) or ClientSplit(np.zeros(sizes[c][0], np.int64), np.zeros(sizes[c][1], np.int64))
+              for c in range(N)]
+    return x8, mom, labels, splits
+
+
+def fl_config(args, algo):
+    """FLConfig from the reference flags of any entry point."""
+    from .engine.executor import FLConfig
+    g = lambda k, d=None: getattr(args, k, d)  # noqa: E731
+    return FLConfig(comm_round=args.comm_round, epochs=args.epochs, batch_size=args.batch_size, lr=args.lr,
+                    lr_decay=args.lr_decay, wd=args.wd, momentum=args.momentum, frac=args.frac,
+                    dense_ratio=g("dense_ratio", 1.0), itersnip_iteration=g("itersnip_iteration", 1),
+                    snip_mask=g("snip_mask", True), frequency_of_the_test=args.frequency_of_the_test, seed=args.seed,
+                    prox_mu=args.fedprox_mu if algo == "fedprox" else 0.0, group=args.group,
+                    aggregator=args.aggregator, byzantine_f=args.byzantine_f, trim_ratio=args.trim_ratio,
+                    update_topk=args.update_topk, heartbeat_s=args.heartbeat_s,
+                    stratified_sampling=bool(g("stratified_sampling", False)),
+                    cs=g("cs", "ring") if algo == "dpsgd" else "random", lamda=g("lamda", 0.5),
+                    local_epochs=g("local_epochs", 0) or 0, anneal_factor=g("anneal_factor", 0.5),
+                    active=g("active", 1.0), static=bool(g("static", False)),
+                    dis_gradient_check=bool(g("dis_gradient_check", False)), uniform=bool(g("uniform", False)),
+                    different_initial=bool(g("different_initial", False)), diff_spa=bool(g("diff_spa", False)),
+                    erk_power_scale=g("erk_power_scale", 1.0), save_masks=bool(g("save_masks", False)),
+                    dispfl_aggregate=bool(g("dispfl_aggregate", 0)), each_prune_ratio=g("each_prune_ratio", 0.05),
+                    dist_thresh=g("dist_thresh", 1e-4), acc_thresh=g("acc_thresh", 0.5))
+
+
+def run_hip(args, algo, logger):
+    """Any algorithm of the harness on the client-batched MI355X executor (HIP kernels, clients sharded over
+    ranks, RCCL collectives)."""
+    from .engine.executor import HipEngine
+    from .engine.personalized import make_runner
     from .models.alexnet3d import AlexNet3D_Dropout
     from .parallel import runtime as rt
     from .utils import checkpoint as ck
     info = rt.init_distributed()
-    n_test = max(1, int(round(args.n_per_client * 0.2)))
-    n_train = args.n_per_client - n_test
-    shards = rt.shard_clients([n_train] * args.client_num_in_total, info.world)
-    vol, labels, local_splits = build_fl_volumes(shards[info.rank], args.client_num_in_total, n_train, n_test,
-                                                 info.device, seed=args.seed, alpha=args.partition_alpha)
-    x8, mom = to_hip_store(vol)
-    del vol
-    splits = [local_splits.get(c) or ClientSplit(np.zeros(n_train, np.int64), np.zeros(n_test, np.int64))
-              for c in range(args.client_num_in_total)]
+    x8, mom, labels, splits = hip_cohort(args, info, logger, with_val=algo == "fedfomo")
     model = AlexNet3D_Dropout(num_classes=1)
     eng = HipEngine(model, x8, mom, labels, info.device)
-    cfg = FLConfig(comm_round=args.comm_round, epochs=args.epochs, batch_size=args.batch_size, lr=args.lr,
-                   lr_decay=args.lr_decay, wd=args.wd, momentum=args.momentum, frac=args.frac,
-                   dense_ratio=getattr(args, "dense_ratio", 1.0), itersnip_iteration=getattr(args, "itersnip_iteration", 1),
-                   snip_mask=getattr(args, "snip_mask", True), frequency_of_the_test=args.frequency_of_the_test,
-                   seed=args.seed, prox_mu=args.fedprox_mu if algo == "fedprox" else 0.0, group=args.group,
-                   aggregator=args.aggregator, byzantine_f=args.byzantine_f, trim_ratio=args.trim_ratio,
-                   update_topk=args.update_topk, heartbeat_s=args.heartbeat_s)
-    runner = FLRunner(eng, splits, cfg, info, model, logger=logger,
-                      algorithm="salientgrads" if algo == "sailentgrads" else "fedavg")
+    cfg = fl_config(args, algo)
+    runner = make_runner(algo, eng, splits, cfg, info, model, logger=logger)
     start = 0
-    if args.resume and args.checkpoint_dir and os.path.exists(os.path.join(args.checkpoint_dir, "global.pt")):
+    if args.resume and args.checkpoint_dir and ck.latest_round(args.checkpoint_dir) is not None:
         start = ck.load_runner(runner, args.checkpoint_dir)
         logger.info("resumed from %s at round %d", args.checkpoint_dir, start)
-    elif algo == "sailentgrads":
+    elif runner.alg == "salientgrads":
         runner.generate_global_mask_snip()
     for r in range(start, cfg.comm_round):
         runner.run_round(r)
         if args.checkpoint_dir:
             ck.save_runner(runner, args.checkpoint_dir, r + 1)
+    runner.finish()
     rt.shutdown(info)
     return runner.stat_info
 
@@ -263,7 +347,7 @@ def run_reference(args, algo, logger, device):
     from .models import create_model
     ds_name = "ABCD" if algo == "sailentgrads" else args.dataset
     dataset = load_data(args, ds_name, logger)
-    class_num = 1 if ds_name == "ABCD" else dataset[7]
+    class_num = 1 if ds_name == "ABCD" else dataset[8 if len(dataset) > 8 else 7]
     in_shape = None
     model = create_model(args.model, ds_name, class_num, in_shape=in_shape).to(device)
     trainer = (VolumeTrainer if ds_name == "ABCD" else ClassificationTrainer)(model, args, logger)
@@ -279,6 +363,7 @@ def main(algo, argv=None):
     from .utils.logger import logger_config
     parser = add_args(argparse.ArgumentParser(description="%s (neuroimagedisttraining_amd)" % algo), algo)
     args = parser.parse_args(argv)
+    args.algo = algo
     args.identity = identity(args, algo)
     log_path = os.path.join(args.log_dir, args.dataset, args.identity + ".log")
     logger = logger_config(log_path=log_path, logging_name=args.identity)

@@ -28,19 +28,38 @@ def client_labels(n_clients, n_per_client, alpha=0.3, seed=0):
     return labs
 
 
-def build_fl_volumes(local_clients, n_clients, n_train, n_test, device, seed=0, alpha=0.3, shape=(121, 145, 121)):
-    """Generate the local clients' volumes.  Returns (vol_u8 [N_local, D,H,W], labels [N_local] f32 (device),
-    splits dict client -> ClientSplit of indices into the local store)."""
-    per = n_train + n_test
-    labs = client_labels(n_clients, per, alpha, seed)
+def skewed_sizes(n_clients, per_client, alpha, seed=0, minimum=2):
+    """Per-client sizes with Dirichlet(alpha) quotas and the same total as ``n_clients * per_client`` (unequal
+    sites, like the reference's 270-807-subject ABCD site clients).  ``alpha <= 0``: equal sizes."""
+    if alpha <= 0:
+        return [per_client] * n_clients
+    q = np.random.RandomState(seed + 31).dirichlet([alpha] * n_clients)
+    tot = n_clients * per_client
+    s = np.maximum(minimum, np.floor(q * (tot - minimum * n_clients)).astype(np.int64) + minimum)
+    s[np.argmax(s)] += tot - int(s.sum())
+    return [int(x) for x in s]
+
+
+def build_fl_volumes(local_clients, n_clients, n_train, n_test, device, seed=0, alpha=0.3, shape=(121, 145, 121),
+                     label_signal=0.35):
+    """Generate the local clients' volumes.  ``n_train`` / ``n_test``: per-client ints or lists (unequal clients).
+    Returns (vol_u8 [N_local, D,H,W], labels [N_local] f32 (device), splits dict client -> ClientSplit of indices
+    into the local store).  ``label_signal`` sets how separable the classes are (0.35: easy; ~0.05: the fp32
+    reference reaches only ~0.8 accuracy, so numerics regressions show in the accuracy trajectory)."""
+    ntr = list(n_train) if hasattr(n_train, "__len__") else [n_train] * n_clients
+    nte = list(n_test) if hasattr(n_test, "__len__") else [n_test] * n_clients
+    maxper = max(a + b for a, b in zip(ntr, nte))
+    labs = client_labels(n_clients, maxper, alpha, seed)
     vols, ys, splits = [], [], {}
     off = 0
     for c in local_clients:
+        per = ntr[c] + nte[c]
         st = make_synthetic_abcd(per, shape=shape, n_sites=21, seed=seed * 100003 + c, device=device,
-                                 labels=labs[c], site=np.full(per, c % 21, dtype=np.float32))
+                                 labels=labs[c][:per], site=np.full(per, c % 21, dtype=np.float32),
+                                 label_signal=label_signal)
         vols.append(st.volumes)
         ys.append(st.labels)
-        splits[c] = ClientSplit(train=np.arange(off, off + n_train), test=np.arange(off + n_train, off + per))
+        splits[c] = ClientSplit(train=np.arange(off, off + ntr[c]), test=np.arange(off + ntr[c], off + per))
         off += per
     vol = torch.cat(vols, 0) if vols else torch.zeros((0,) + tuple(shape), dtype=torch.uint8, device=device)
     y = torch.cat(ys, 0) if ys else torch.zeros(0, device=device)

@@ -197,6 +197,10 @@ class TorchEngine:
         if seed_dev is not None:
             seed = int(seed) + int(seed_dev.item())
         self.model.train(bn_train)
+        if keep >= 1.0:  # dropout off (the HIP head's keep = 1), BN still in training mode
+            for mod in self.model.modules():
+                if isinstance(mod, torch.nn.Dropout):
+                    mod.eval()
         for g in range(G):
             # dropout stream keyed by (step seed, global client id): independent of how clients are sharded
             cid = int(cids[g]) if cids is not None else g

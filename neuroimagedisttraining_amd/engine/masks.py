@@ -168,6 +168,8 @@ class MaskSpace:
         number of candidates of its segment."""
         R = bits.shape[0]
         k = k.to(torch.int64)
+        assert k.shape == (R, self.S) and bits.shape[1] >= (self.P + 31) // 32 and bits.stride(1) == 1
+        assert v is None or (v.shape[0] >= R and v.shape[1] >= self.P and v.stride(1) == 1)
         if _hip(bits):
             dev = bits.device
             tiles, first, nt = self.tiles(R, dev)
@@ -278,6 +280,8 @@ def masked_rows_sum(rows, n, bits, sum_, cnt):
     if R == 0:
         return
     if _hip(rows):
+        assert rows.stride(1) == 1 and rows.shape[1] >= n and sum_.numel() >= n and cnt.numel() >= n
+        assert bits is None or (bits.shape[0] == R and bits.shape[1] * 32 >= n and bits.stride(1) == 1)
         ops.ext().masked_rows_sum(rows.data_ptr(), rows.stride(0), bits.data_ptr() if bits is not None else 0,
                                   bits.stride(0) if bits is not None else 0, R, n, sum_.data_ptr(), cnt.data_ptr(),
                                   _st())
@@ -296,6 +300,8 @@ def mix_rows(plan, n):
         return
     dev = plan[0][0].device
     if _hip(plan[0][0]):
+        assert all(d.data_ptr() % 16 == 0 and all(t.data_ptr() % 16 == 0 for t, _ in terms) for d, terms in plan), \
+            "mix_rows: rows must be 16-byte aligned"
         src, wts, rp, dst = [], [], [0], []
         for d, terms in plan:
             dst.append(d.data_ptr())
@@ -322,6 +328,7 @@ def pair_sqdist(pairs, n):
         return torch.zeros(0, dtype=torch.float64)
     dev = pairs[0][0].device
     if _hip(pairs[0][0]):
+        assert all(a.data_ptr() % 16 == 0 and b.data_ptr() % 16 == 0 for a, b in pairs), "pair_sqdist: alignment"
         m = ops.ext()
         nb = m.pair_sqdist_nblk(n)
         part = torch.empty((len(pairs), nb), dtype=torch.float32, device=dev)

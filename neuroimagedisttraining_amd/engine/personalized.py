@@ -65,23 +65,45 @@ class PersonalizedRunner(FLRunner):
         return list(range(self.C)), list(self.local)
 
     def snapshot(self, rs=None):
+        """Copy of a row set with 16-B aligned rows (``clone`` of the padded views would pack rows at stride P)."""
         rs = rs or self.rowset
-        return RowSet(rs.theta.clone(), rs.bufs.clone())
+        n = rs.theta.shape[0]
+        out = RowSet(padded_rows(n, self.P, self.device), padded_rows(n, self.Q, self.device))
+        out.theta.copy_(rs.theta)
+        out.bufs.copy_(rs.bufs)
+        return out
+
+    def cat_rows(self, *sets):
+        """Concatenate row sets into one padded row set."""
+        n = sum(s.theta.shape[0] for s in sets)
+        out = RowSet(padded_rows(max(1, n), self.P, self.device), padded_rows(max(1, n), self.Q, self.device))
+        o = 0
+        for s in sets:
+            k = s.theta.shape[0]
+            out.theta[o:o + k].copy_(s.theta)
+            out.bufs[o:o + k].copy_(s.bufs)
+            o += k
+        return out
 
     def fetch(self, needs, src):
         """{client: (theta_row [P], bufs_row [Q])} for every client in ``needs[self.rank]``: local clients are views
         of ``src``, remote ones arrive point-to-point from their owners (same ``needs`` on every rank)."""
         P, Q = self.P, self.Q
-        recv = rt.exchange_rows(self.info, self.owner, needs,
-                                lambda c: torch.cat([src.theta[self.row_of[c], :P], src.bufs[self.row_of[c], :Q]]),
-                                P + Q, self.device)
+        Pp = (P + 63) // 64 * 64  # the buffer section of a received row starts 16-B aligned (vector kernels)
+
+        def row(c):
+            v = torch.zeros(Pp + Q, dtype=torch.float32, device=self.device)
+            v[:P] = src.theta[self.row_of[c], :P]
+            v[Pp:] = src.bufs[self.row_of[c], :Q]
+            return v
+        recv = rt.exchange_rows(self.info, self.owner, needs, row, Pp + Q, self.device)
         out = {}
         for c in needs[self.info.rank]:
             if c in self.row_of:
                 out[c] = (src.theta[self.row_of[c]], src.bufs[self.row_of[c]])
             else:
                 v = recv[c]
-                out[c] = (v[:P], v[P:])
+                out[c] = (v[:P], v[Pp:])
         return out
 
     def pool(self, entries):
@@ -293,11 +315,10 @@ class FedFomoRunner(PersonalizedRunner):
         src = self.fetch(needs, last)
         # candidate pool: [old own models (C) | new own models (C) | remote candidates]
         remote = [j for j in needs[self.info.rank] if j not in self.row_of]
-        pool = RowSet(torch.cat([last.theta[:self.C], self.theta[:self.C]]),
-                      torch.cat([last.bufs[:self.C], self.bufs[:self.C]]))
+        parts = [last.rows(0, self.C), self.rowset.rows(0, self.C)]
         if remote:
-            ext = self.pool([src[j] for j in remote])
-            pool = RowSet(torch.cat([pool.theta, ext.theta[:len(remote)]]), torch.cat([pool.bufs, ext.bufs[:len(remote)]]))
+            parts.append(self.pool([src[j] for j in remote]).rows(0, len(remote)))
+        pool = self.cat_rows(*parts)
         prow = {("old", c): self.row_of[c] for c in self.local}
         prow.update({("new", c): self.C + self.row_of[c] for c in self.local})
         for k, j in enumerate(remote):

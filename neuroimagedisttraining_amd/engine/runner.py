@@ -39,6 +39,7 @@ import numpy as np
 import torch
 import torch.nn.functional as F
 
+from .. import ops
 from ..parallel import runtime as rt
 from . import masks as MK
 from .executor import (ClientSplit, FLConfig, gather_rows, maskable_flat_mask, padded_rows,  # noqa: F401
@@ -377,7 +378,7 @@ class FLRunner:
         mask = torch.ones(self.P, dtype=torch.float32, device=self.device)
         if k >= 1:
             if self.device.type == "cuda":
-                m = self.e.m
+                m = ops.ext()
                 st = torch.empty(4, dtype=torch.int32, device=self.device)
                 hist = torch.empty(256, dtype=torch.int32, device=self.device)
                 sel = sel.contiguous()
@@ -491,7 +492,7 @@ class FLRunner:
         if rows:
             w = torch.tensor(weights, dtype=torch.float32, device=self.device)
             if self.device.type == "cuda" and _contiguous(rows):
-                m, st = self.e.m, torch.cuda.current_stream().cuda_stream
+                m, st = ops.ext(), torch.cuda.current_stream().cuda_stream
                 lo = rows[0]
                 m.weighted_rows_sum(theta[lo].data_ptr(), w.data_ptr(), len(rows), self.P, theta.stride(0), 0.0,
                                     buf.data_ptr(), st)

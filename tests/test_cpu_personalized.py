@@ -1,0 +1,258 @@
+"""CPU tests of the client-batched personalized runners and the mask layer.
+
+* mask ops (torch twins of the HIP kernels) against the reference-style per-layer dict ops of
+  ``algorithms/sparse.py`` (fire / regrow with torch.sort, numpy.percentile fake_prune, masked average);
+* every runner (DisPFL, SubAvg, Ditto, D-PSGD, FedFomo, Local, SalientGrads, FedAvg) with ragged client sizes and
+  partial last batches: 2 gloo ranks (and 3 for the neighbour-exchange algorithms) == 1 process.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.nn as nn
+
+
+class Tiny3D(nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.features = nn.Sequential(nn.Conv3d(1, 4, 3, 2), nn.BatchNorm3d(4), nn.ReLU(), nn.MaxPool3d(2, 2),
+                                      nn.Conv3d(4, 8, 3), nn.BatchNorm3d(8), nn.ReLU())
+        self.classifier = nn.Sequential(nn.Dropout(), nn.Linear(8, 1))
+
+    def forward(self, x):
+        return self.classifier(self.features(x).amax((2, 3, 4)))
+
+
+# ------------------------------------------------------------------------------------------------ mask layer
+def _space():
+    from neuroimagedisttraining_amd.engine.flat import ParamLayout
+    from neuroimagedisttraining_amd.engine import masks as MK
+    m = Tiny3D()
+    pl = ParamLayout.from_tensors(list(m.named_parameters()))
+    return m, pl, MK.MaskSpace(pl)
+
+
+def test_fire_regrow_match_reference_dict_ops():
+    from neuroimagedisttraining_amd.algorithms import sparse as SP
+    from neuroimagedisttraining_amd.engine import masks as MK
+    model, pl, ms = _space()
+    torch.manual_seed(0)
+    P = pl.total
+    w = torch.randn(1, P)
+    w[0, ::5] = torch.round(w[0, ::5])  # ties
+    g = torch.randn(1, P)
+    m = (torch.rand(1, P) < 0.5).float()
+    named = lambda flat: {n: flat[0, o:o + pl.numel(i)].view(pl.shapes[i])  # noqa: E731
+                          for i, (n, o) in enumerate(zip(pl.names, pl.offsets))}
+    new, num_remove = SP.fire_mask(named(m), named(w), 3, 0.5, 10)
+    new = SP.regrow_mask(new, num_remove, named(g))
+    bits = MK.pack_bits(m)
+    nnz = ms.popcount(bits)
+    k = torch.ceil(torch.tensor(SP.cosine_annealing(0.5, 3, 10), dtype=torch.float32) * nnz.float()).long()
+    assert [int(x) for x in k[0]] == [num_remove[n] for n in pl.names]
+    ms.select(MK.FIRE, w, bits, k)
+    ms.select(MK.REGROW_ABS, g, bits, k)
+    got = MK.unpack_bits(bits, P)[0]
+    exp = torch.cat([new[n].reshape(-1) for n in pl.names])
+    assert torch.equal(got, exp)
+
+
+def test_percentile_prune_matches_numpy_fake_prune():
+    from neuroimagedisttraining_amd.algorithms import sparse as SP
+    from neuroimagedisttraining_amd.engine import masks as MK
+    model, pl, ms = _space()
+    torch.manual_seed(1)
+    P = pl.total
+    w = torch.randn(2, P)
+    w[1, ::3] = 0
+    m = (torch.rand(2, P) < 0.7).float()
+    names = [n for n in pl.names if "weight" in n and "bn" not in n]
+    out = MK.unpack_bits(ms.percentile_prune(w, MK.pack_bits(m), 0.2, names), P)
+    for r in range(2):
+        sd = {n: w[r, o:o + pl.numel(i)].view(pl.shapes[i]) for i, (n, o) in enumerate(zip(pl.names, pl.offsets))}
+        mk = {n: m[r, o:o + pl.numel(i)].view(pl.shapes[i]) for i, (n, o) in enumerate(zip(pl.names, pl.offsets))}
+        ref = SP.fake_prune(0.2, sd, mk)
+        assert torch.equal(out[r], torch.cat([ref[n].reshape(-1).float() for n in pl.names]))
+
+
+def test_masked_average_matches_subavg_aggregate():
+    from neuroimagedisttraining_amd.algorithms import sparse as SP
+    from neuroimagedisttraining_amd.engine import masks as MK
+    model, pl, ms = _space()
+    torch.manual_seed(2)
+    P = pl.total
+    rows = torch.randn(3, P)
+    m = (torch.rand(3, P) < 0.5).float()
+    rows = rows * m
+    s, c = torch.zeros(P), torch.zeros(P)
+    MK.masked_rows_sum(rows, P, MK.pack_bits(m), s, c)
+    srv = torch.randn(P)
+    ours = torch.where(c > 0, s / c, srv)
+    named = lambda v: {n: v[o:o + pl.numel(i)].view(pl.shapes[i]).clone()  # noqa: E731
+                       for i, (n, o) in enumerate(zip(pl.names, pl.offsets))}
+    ref = SP.masked_average(named(srv), [(named(m[i]), named(rows[i])) for i in range(3)])
+    assert torch.allclose(ours, torch.cat([ref[n].reshape(-1) for n in pl.names]), atol=1e-6)
+
+
+# ------------------------------------------------------------------------------------------------ runners
+SIZES = [10, 7, 14, 10, 6, 11]
+
+
+def _runner(algo, rank=0, world=1, rounds=2, sizes=None, **kw):
+    from neuroimagedisttraining_amd.engine.executor import ClientSplit, FLConfig, TorchEngine
+    from neuroimagedisttraining_amd.engine.personalized import make_runner
+    from neuroimagedisttraining_amd.parallel import runtime as rt
+    torch.manual_seed(0)
+    g = torch.Generator().manual_seed(5)
+    splits, off = [], 0
+    for s in (sizes or SIZES):
+        tr = np.arange(off, off + s)
+        splits.append(ClientSplit(tr, np.arange(off + s, off + s + 4), tr[:3]))
+        off += s + 4
+    vols = torch.randint(0, 256, (off, 15, 15, 15), dtype=torch.uint8, generator=g)
+    labels = torch.randint(0, 2, (off,), generator=g).float()
+    model = Tiny3D()
+    eng = TorchEngine(model, vols, labels, "cpu")
+    info = rt.DistInfo(rank, world, rank, torch.device("cpu"), "gloo" if world > 1 else "none")
+    cfg = dict(comm_round=rounds, epochs=2, batch_size=4, lr=0.05, dense_ratio=0.5, seed=7, acc_thresh=0.0,
+               each_prune_ratio=0.2, local_epochs=1, dist_thresh=0.0)
+    cfg.update(kw)
+    return make_runner(algo, eng, splits, FLConfig(**cfg), info, model)
+
+
+def _collect(r):
+    """Per-client model rows (global client order) + headline metrics."""
+    rows = {c: r.theta[r.row_of[c], :r.P].clone() for c in r.local}
+    bits = {c: r.mbits[r.row_of[c]].clone() for c in r.local} if getattr(r, "mbits", None) is not None else {}
+    pers = {c: r.pers.theta[r.row_of[c], :r.P].clone() for c in r.local} if hasattr(r, "pers") else {}
+    return {"rows": rows, "bits": bits, "pers": pers, "w": r.w_global.clone(),
+            "stats": {k: v for k, v in r.stat_info.items() if isinstance(v, list) and v and
+                      isinstance(v[0], float) and "time" not in k}}
+
+
+def _drive(r, rounds):
+    if r.alg == "salientgrads":
+        r.generate_global_mask_snip()
+    for k in range(rounds):
+        r.run_round(k)
+    r.finish()
+
+
+def _worker(rank, world, port, out, algo, kw, ckpt=None):
+    """ckpt = (directory, mode): "save" runs round 0 and checkpoints; "resume" loads and runs round 1."""
+    import torch.distributed as dist
+    from neuroimagedisttraining_amd.utils import checkpoint as ck
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    r = _runner(algo, rank, world, **kw)
+    if ckpt is None:
+        _drive(r, 2)
+    elif ckpt[1] == "save":
+        if r.alg == "salientgrads":
+            r.generate_global_mask_snip()
+        r.run_round(0)
+        ck.save_runner(r, ckpt[0], 1)
+    else:
+        start = ck.load_runner(r, ckpt[0])
+        for k in range(start, 2):
+            r.run_round(k)
+        r.finish()
+    torch.save(_collect(r), out + ".%d" % rank)
+    dist.destroy_process_group()
+
+
+def _spawn(world, out, algo, kw, ckpt=None):
+    import torch.multiprocessing as mp
+    mp.start_processes(_worker, args=(world, _port(), out, algo, kw, ckpt), nprocs=world, join=True,
+                       start_method="spawn")
+    got = {"rows": {}, "bits": {}, "pers": {}}
+    for rk in range(world):
+        d = torch.load(out + ".%d" % rk, weights_only=True)
+        for key in ("rows", "bits", "pers"):
+            got[key].update(d[key])
+        if rk == 0:
+            got["w"], got["stats"] = d["w"], d["stats"]
+    return got
+
+
+def _same(got, ref, n, algo, atol=1e-5):
+    for c in range(n):
+        assert torch.allclose(got["rows"][c], ref["rows"][c], atol=atol), (algo, c)
+        if ref["bits"]:
+            assert torch.equal(got["bits"][c], ref["bits"][c]), (algo, c)
+        if ref["pers"]:
+            assert torch.allclose(got["pers"][c], ref["pers"][c], atol=atol), (algo, c)
+    assert torch.allclose(got["w"], ref["w"], atol=atol)
+    for k, v in ref["stats"].items():
+        assert np.allclose(got["stats"][k], v, atol=1e-6), (algo, k)
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+CASES = [("dispfl", 2, {}), ("dispfl", 3, {"frac": 0.5, "active": 0.8, "dis_gradient_check": True}),
+         ("subavg", 2, {"frac": 0.5}), ("ditto", 2, {"frac": 0.5}), ("dpsgd", 3, {"frac": 0.5, "cs": "ring"}),
+         ("dpsgd", 2, {"frac": 0.5, "cs": "random"}), ("fedfomo", 3, {"frac": 0.5}), ("local", 2, {"frac": 0.5}),
+         ("salientgrads", 2, {}), ("fedavg", 3, {"frac": 0.5})]
+
+
+@pytest.mark.parametrize("algo,world,kw", CASES)
+def test_runner_multirank_matches_single_process(algo, world, kw, tmp_path):
+    """Clients sharded over gloo ranks (neighbour rows exchanged point-to-point, partial sums all-reduced) give the
+    same per-client models, masks and metrics as one process."""
+    got = _spawn(world, str(tmp_path / "r"), algo, kw)
+    r = _runner(algo, **kw)
+    _drive(r, 2)
+    _same(got, _collect(r), len(SIZES), algo)
+
+
+def test_hundred_clients_four_ranks_frac_quarter_matches_single_process(tmp_path):
+    """100 clients, frac 0.25 (25 sampled per round, unevenly spread over the 4 ranks' shards) == 1 process."""
+    kw = {"sizes": [6 + (c % 5) * 2 for c in range(100)], "frac": 0.25, "epochs": 1}
+    got = _spawn(4, str(tmp_path / "r"), "fedavg", kw)
+    r = _runner("fedavg", **kw)
+    _drive(r, 2)
+    _same(got, _collect(r), 100, "fedavg")
+
+
+@pytest.mark.parametrize("algo", ["salientgrads", "dispfl", "fedfomo"])
+def test_checkpoint_from_four_ranks_resumes_on_two_exactly(algo, tmp_path):
+    """Round 0 on 4 ranks -> checkpoint -> resume round 1 on 2 ranks == 2 uninterrupted rounds in one process
+    (client rows keyed by id, RNG streams and affinities restored, round tagged shards + latest pointer)."""
+    d = str(tmp_path / "ck")
+    _spawn(4, str(tmp_path / "a"), algo, {}, ckpt=(d, "save"))
+    got = _spawn(2, str(tmp_path / "b"), algo, {}, ckpt=(d, "resume"))
+    r = _runner(algo)
+    _drive(r, 2)
+    _same(got, _collect(r), len(SIZES), algo)
+
+
+def test_dispfl_masks_keep_density_and_masked_weights_zero():
+    from neuroimagedisttraining_amd.engine import masks as MK
+    r = _runner("dispfl", rounds=3)
+    d0 = r.mspace.popcount(r.mbits).sum(1)
+    _drive(r, 3)
+    assert torch.equal(r.mspace.popcount(r.mbits).sum(1), d0)  # fire k == regrow k per layer
+    m = MK.unpack_bits(r.mbits, r.P)
+    # weights outside the mask they were trained with are zero; after fire/regrow only newly regrown ones may be 0
+    moved = r.mspace.hamming(r.shared_bits, r.mbits).sum()
+    assert int(moved) > 0
+    assert float((r.theta[:, :r.P] * (1 - MK.unpack_bits(r.shared_bits, r.P))).abs().max()) == 0.0
+    assert m.shape == (r.C, r.P)
+
+
+def test_subavg_prunes_and_aggregates_over_mask_counts():
+    from neuroimagedisttraining_amd.engine import masks as MK
+    r = _runner("subavg", rounds=3, dense_ratio=0.1, acc_thresh=-1.0)
+    _drive(r, 3)
+    dens = MK.unpack_bits(r.mbits, r.P).mean(1)
+    assert float(dens.min()) < 1.0  # something was pruned (percentile 0.2 per weight layer)
+    assert np.isfinite(r.w_global.numpy()).all()

@@ -1,0 +1,315 @@
+"""GPU tests of the personalized-algorithm machinery: the sparse-mask kernels (``sparse.hip``) bit-exact against
+their torch twins / numpy's percentile, the fused ``local_opt`` kernel against the reference-order torch step, the
+eval-mode backward against fp64 autograd of the model in ``eval()``, and every algorithm runner on the HIP engine
+against the same runner on the fp32 PyTorch engine (ragged client sizes, partial last batches, G >= 4)."""
+import os
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+os.environ.setdefault("MIOPEN_FIND_MODE", "FAST")  # the fp32 oracle engine: skip MIOpen's exhaustive search
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _relerr(a, b):
+    a, b = a.double(), b.double()
+    return float((a - b).norm() / (b.norm() + 1e-30))
+
+
+def _layout():
+    from neuroimagedisttraining_amd.engine.flat import ParamLayout
+    from neuroimagedisttraining_amd.models.alexnet3d import AlexNet3D_Dropout
+    m = AlexNet3D_Dropout(num_classes=1)
+    return m, ParamLayout.from_tensors(list(m.named_parameters())), ParamLayout.from_tensors(list(m.named_buffers()))
+
+
+# ------------------------------------------------------------------------------------------------ mask kernels
+def test_mask_counts_select_and_prune_match_torch():
+    from neuroimagedisttraining_amd.engine import masks as MK
+    from neuroimagedisttraining_amd.engine.executor import padded_rows
+    _, pl, _ = _layout()
+    ms = MK.MaskSpace(pl)
+    R, P = 3, pl.total
+    g = torch.Generator(device=DEV).manual_seed(0)
+    v = padded_rows(R, P, DEV)
+    v.copy_(torch.randn(R, P, device=DEV, generator=g))
+    v[1] = torch.round(v[1] * 4) / 4  # heavy ties: tie-breaking must follow index order
+    v[2, ::7] = 0.0
+    m = (torch.rand(R, P, device=DEV, generator=g) < 0.6)
+    bits = MK.pack_bits(m)
+    assert torch.equal(MK.unpack_bits(bits, P).bool(), m)
+    cpu = lambda t: t.cpu()  # noqa: E731
+    # K17 / K18 counts
+    assert torch.equal(ms.popcount(bits).cpu(), ms.popcount(cpu(bits)))
+    other = MK.pack_bits(torch.rand(R, P, device=DEV, generator=g) < 0.5)
+    assert torch.equal(ms.hamming(bits, other).cpu(), ms.hamming(cpu(bits), cpu(other)))
+    assert torch.equal(ms.alive_count(bits, v).cpu(), ms.alive_count(cpu(bits), cpu(v)))
+    # K15 selection: fire on |w| (smallest active), regrow on |g| (largest inactive) and random regrow
+    nnz = ms.popcount(bits)
+    k = torch.ceil(torch.tensor(0.3, dtype=torch.float32) * nnz.float()).long()
+    for mode, vals in ((MK.FIRE, v), (MK.REGROW_ABS, v), (MK.REGROW_RAND, None)):
+        kk = k if mode == MK.FIRE else torch.minimum(k, ms.popcount(MK.pack_bits(~m)))
+        a, b = bits.clone(), cpu(bits).clone()
+        ms.select(mode, vals, a, kk.to(DEV), cids=[5, 9, 11], seed=123)
+        ms.select(mode, cpu(vals) if vals is not None else None, b, kk.cpu(), cids=[5, 9, 11], seed=123)
+        assert torch.equal(a.cpu(), b), mode
+        delta = ms.popcount(a).cpu() - nnz.cpu()
+        assert torch.equal(delta, -kk.cpu() if mode == MK.FIRE else kk.cpu())
+    # K16 percentile prune == numpy.percentile per layer (subavg/prune_func.py:9-30)
+    names = [n for n in pl.names if "weight" in n]
+    out = ms.percentile_prune(v, bits, 0.05, names)
+    ref = ms.percentile_prune(cpu(v), cpu(bits), 0.05, names)
+    assert torch.equal(out.cpu(), ref)
+    mm = MK.unpack_bits(cpu(bits), P).bool()
+    vv = cpu(v)[:, :P]
+    for r in range(R):
+        for i, n in enumerate(pl.names):
+            o, cnt = pl.offsets[i], pl.numel(i)
+            t = vv[r, o:o + cnt].numpy()
+            alive = t[np.nonzero(t * mm[r, o:o + cnt].numpy())]
+            exp = mm[r, o:o + cnt].numpy().copy()
+            if n in names and alive.size:
+                pv = np.percentile(np.abs(alive), 0.05 * 100)
+                exp = np.where(np.abs(t) < pv, 0, exp)
+            got = MK.unpack_bits(ref[r:r + 1], P)[0, o:o + cnt].numpy()
+            assert np.array_equal(got, exp.astype(got.dtype)), (r, n)
+
+
+def test_row_ops_match_torch():
+    from neuroimagedisttraining_amd.engine import masks as MK
+    from neuroimagedisttraining_amd.engine.executor import padded_rows
+    R, n = 5, 1000003
+    rows = padded_rows(R, n, DEV)
+    rows.copy_(torch.randn(R, n, device=DEV))
+    bits = MK.pack_bits(torch.rand(R, n, device=DEV) < 0.5)
+    s, c = torch.zeros(n, device=DEV), torch.zeros(n, device=DEV)
+    MK.masked_rows_sum(rows, n, bits, s, c)
+    s2, c2 = torch.zeros(n), torch.zeros(n)
+    MK.masked_rows_sum(rows.cpu(), n, bits.cpu(), s2, c2)
+    assert _relerr(s.cpu(), s2) < 1e-6 and torch.equal(c.cpu(), c2)
+    out = padded_rows(2, n, DEV)
+    plan = [(out[0], [(rows[0], 0.25), (rows[3], 0.75)]), (out[1], [(rows[1], 1.0), (rows[2], -2.0), (rows[4], 0.5)])]
+    MK.mix_rows(plan, n)
+    assert _relerr(out[0], 0.25 * rows[0] + 0.75 * rows[3]) < 1e-6
+    assert _relerr(out[1], rows[1] - 2 * rows[2] + 0.5 * rows[4]) < 1e-6
+    d = MK.pair_sqdist([(rows[0], rows[1]), (rows[2], rows[2]), (rows[4], rows[0])], n)
+    ref = torch.stack([((rows[0] - rows[1]).double() ** 2).sum(), torch.zeros((), dtype=torch.float64, device=DEV),
+                       ((rows[4] - rows[0]).double() ** 2).sum()]).cpu()
+    assert torch.allclose(d.cpu(), ref, rtol=1e-5)
+
+
+@pytest.mark.parametrize("mode,mu,lamda,mom,shared", [(0, 0.0, 0.0, 0.0, False), (1, 0.0, 0.0, 0.0, True),
+                                                      (1, 0.0, 0.0, 0.9, False), (2, 0.0, 0.0, 0.0, False),
+                                                      (0, 0.01, 0.0, 0.0, False), (0, 0.0, 0.5, 0.9, False)])
+def test_local_opt_matches_reference_order(mode, mu, lamda, mom, shared):
+    """Fused clip + SGD (+ momentum) with shared / per-row bit masks (weight or gradient mode), FedProx proximal
+    gradient and Ditto pull == the reference-order torch step of TorchEngine."""
+    from neuroimagedisttraining_amd.engine import masks as MK
+    from neuroimagedisttraining_amd.engine.executor import HipEngine, TorchEngine, padded_rows
+    from neuroimagedisttraining_amd.engine.runner import StepSpec
+    G, P = 4, 2570241
+    torch.manual_seed(4)
+    theta = padded_rows(G, P, DEV)
+    theta.copy_(torch.randn(G, P, device=DEV))
+    grad = padded_rows(G, P, DEV)
+    grad.copy_(torch.randn(G, P, device=DEV) * 0.01)
+    grad[1] *= 1000  # clipping
+    mb = padded_rows(G, P, DEV)
+    mb.copy_(torch.randn(G, P, device=DEV))
+    bits = MK.pack_bits(torch.rand(1 if shared else G, P, device=DEV) < 0.5)
+    ref = torch.randn(P, device=DEV)
+    spec = StepSpec(mask_mode=mode, bits=bits if mode else None, shared=shared, prox_mu=mu, ref=ref if mu else None,
+                    lamda=lamda, pref=ref if lamda else None)
+    eng = HipEngine.__new__(HipEngine)
+    from neuroimagedisttraining_amd import ops
+    eng.m = ops.ext()
+    t_theta, t_grad, t_mb = theta.clone(), grad.clone(), mb.clone()
+    eng.local_opt(theta, grad, mb if mom else None, spec, 0.01, 5e-4, mom, 10.0, keep_grad=True)
+    TorchEngine.local_opt(None, t_theta, t_grad, t_mb if mom else None, spec, 0.01, 5e-4, mom, 10.0, keep_grad=True)
+    torch.cuda.synchronize()
+    assert _relerr(theta, t_theta) < 1e-6
+    assert _relerr(grad, t_grad) < 1e-5
+    if mom:
+        assert _relerr(mb, t_mb) < 1e-6
+    if mode == 1:
+        mk = MK.unpack_bits(bits, P).expand(G, P)
+        assert float((theta[:, :P] * (1 - mk)).abs().max()) == 0.0
+
+
+# ------------------------------------------------------------------------------------------------ eval-mode grad
+def test_eval_mode_gradient_matches_autograd():
+    """bn_train=False (DisPFL screen_gradients): gradient of the model in eval() — running-stat BN (incl. gamma < 0),
+    no dropout — against fp64 autograd with the HIP forward's pooling / ReLU decisions."""
+    from test_gpu_kernels import _alexnet_setup, _cf, _pool_at
+    from neuroimagedisttraining_amd.engine.alexnet_hip import HipAlexNet3D
+    from neuroimagedisttraining_amd.engine.executor import padded_rows
+    G, B = 2, 3
+    store, x8, mom, pl, bl, theta, bufs = _alexnet_setup(G, B, seed=3)
+    for i, n in enumerate(bl.names):
+        o, k = bl.offsets[i], bl.numel(i)
+        if n.endswith("running_mean"):
+            bufs[:, o:o + k] = 0.1 * torch.randn(G, k, device=DEV)
+        if n.endswith("running_var"):
+            bufs[:, o:o + k] = 0.5 + torch.rand(G, k, device=DEV)
+    for i, n in enumerate(pl.names):  # some negative gammas
+        if n in ("features.1.weight", "features.9.weight"):
+            o = pl.offsets[i]
+            theta[:, o:o + 8] *= -1
+    net = HipAlexNet3D(pl, bl, DEV)
+    grads = padded_rows(G, pl.total, DEV)
+    b0 = bufs.clone()
+    idx = torch.arange(G * B, dtype=torch.int32, device=DEV)
+    net.train_step(theta, bufs, grads, x8, mom, idx, store.labels.float(), G, B, keep=0.5, seed=3, bn_train=False)
+    torch.cuda.synchronize()
+    assert torch.equal(bufs, b0), "eval-mode step must not touch running statistics"
+    b = net._cache[(G, B, True)]
+    errs = {}
+    for g in range(G):
+        sl = slice(g * B, (g + 1) * B)
+        row = theta[g].detach().double().clone().requires_grad_(True)
+        pv = {n: row[o:o + pl.numel(i)].view(pl.shapes[i]) for i, (n, o) in enumerate(zip(pl.names, pl.offsets))}
+        bv = {n: bufs[g, o:o + bl.numel(i)].double().view(bl.shapes[i]) for i, (n, o) in
+              enumerate(zip(bl.names, bl.offsets))}
+        h = (store.volumes[sl].double() / 255.0).unsqueeze(1)
+        for ci, bi, s_, pd in ((0, 1, 2, 0), (4, 5, 1, 0), (8, 9, 1, 1), (11, 12, 1, 1), (14, 15, 1, 1)):
+            y = F.conv3d(h, pv["features.%d.weight" % ci], pv["features.%d.bias" % ci], s_, pd)
+            z = F.batch_norm(y, bv["features.%d.running_mean" % bi], bv["features.%d.running_var" % bi],
+                             pv["features.%d.weight" % bi], pv["features.%d.bias" % bi], False, 0.1, 1e-5)
+            if ci in (0, 4, 14):
+                ours = {0: b["p1"], 4: b["p2"], 14: b["p5"]}[ci][sl]
+                h = _pool_at(z, {0: b["a1"], 4: b["a2"], 14: b["a5"]}[ci][sl]) * (_cf(ours.double()) > 0)
+            else:
+                yb = b["y%d" % {8: 3, 11: 4}[ci]][sl].float()
+                h = z * _cf(((yb * b["s%d" % ci][g] + b["t%d" % ci][g]) > 0).double())
+        f = h.flatten(1)
+        z1 = F.linear(f, pv["classifier.1.weight"], pv["classifier.1.bias"])
+        out = F.linear(torch.relu(z1), pv["classifier.4.weight"], pv["classifier.4.bias"])
+        F.binary_cross_entropy_with_logits(out, store.labels[sl].double().view(B, 1)).backward()
+        for i, n in enumerate(pl.names):
+            o, k = pl.offsets[i], pl.numel(i)
+            errs.setdefault(n, []).append(_relerr(grads[g, o:o + k], row.grad[o:o + k]))
+    bad = {n: e for n, e in errs.items() if max(e) > 3e-2}
+    assert not bad, bad
+
+
+# ------------------------------------------------------------------------------------------------ runners
+def _fed(sizes, n_test=6, n_val=4, seed=11):
+    from neuroimagedisttraining_amd.data.volumes import make_synthetic_abcd
+    from neuroimagedisttraining_amd.data.synthetic_fl import to_hip_store
+    from neuroimagedisttraining_amd.engine.executor import ClientSplit
+    tot = sum(s + n_test for s in sizes)
+    st = make_synthetic_abcd(tot, seed=seed, device=DEV)
+    splits, off = [], 0
+    for s in sizes:
+        tr = np.arange(off, off + s)
+        splits.append(ClientSplit(tr, np.arange(off + s, off + s + n_test), tr[:n_val]))
+        off += s + n_test
+    x8, mom = to_hip_store(st.volumes)
+    return st, x8, mom, splits
+
+
+def _run(algo, engine_kind, fed, rounds=2, **kw):
+    from neuroimagedisttraining_amd.engine.executor import FLConfig, HipEngine, TorchEngine
+    from neuroimagedisttraining_amd.engine.personalized import make_runner
+    from neuroimagedisttraining_amd.models.alexnet3d import AlexNet3D_Dropout
+    from neuroimagedisttraining_amd.parallel import runtime as rt
+    st, x8, mom, splits = fed
+    torch.manual_seed(0)
+    model = AlexNet3D_Dropout(num_classes=1)
+    if engine_kind == "hip":
+        eng = HipEngine(model, x8, mom, st.labels.float(), DEV)
+    else:
+        eng = TorchEngine(model, st.volumes, st.labels.float(), DEV)
+    cfg = dict(comm_round=rounds, epochs=2, batch_size=8, lr=0.01, dense_ratio=0.5, seed=3, dropout_keep=1.0,
+               frac=1.0, acc_thresh=0.0, each_prune_ratio=0.2, local_epochs=1, dist_thresh=0.0, test_batch=64)
+    cfg.update(kw)
+    info = rt.DistInfo(device=torch.device(DEV))
+    r = make_runner(algo, eng, splits, FLConfig(**cfg), info, model)
+    w0 = r.theta.clone()
+    if algo == "salientgrads":
+        r.generate_global_mask_snip()
+    for k in range(rounds):
+        r.run_round(k)
+    torch.cuda.synchronize()
+    return r, w0
+
+
+ALGOS = ["salientgrads", "fedavg", "local", "ditto", "dpsgd", "fedfomo", "dispfl", "subavg"]
+SIZES = [20, 12, 20, 9, 16, 11, 20, 13]
+
+
+def _extra(algo):
+    return {"frac": 0.5, "cs": "ring"} if algo in ("dpsgd", "subavg") else {}
+
+
+@pytest.mark.parametrize("algo", ALGOS)
+def test_runner_hip_graphs_bit_identical_to_eager(algo):
+    """Every algorithm's lockstep steps replayed as hipGraphs (per-row masks, grad masks, pull references, ragged
+    group shapes) == the eager launch sequence, bit for bit, including the masks the selection kernels produce."""
+    fed = _fed(SIZES)
+    a, _ = _run(algo, "hip", fed, hip_graphs=True, dropout_keep=0.5, **_extra(algo))
+    b, _ = _run(algo, "hip", fed, hip_graphs=False, dropout_keep=0.5, **_extra(algo))
+    assert any(isinstance(v, tuple) for v in a._graphs.values()), "no step was captured"
+    assert torch.equal(a.theta, b.theta) and torch.equal(a.bufs, b.bufs)
+    assert torch.equal(a.w_global, b.w_global)
+    if getattr(a, "mbits", None) is not None:
+        assert torch.equal(a.mbits, b.mbits)
+    if hasattr(a, "pers"):
+        assert torch.equal(a.pers.theta, b.pers.theta)
+
+
+@pytest.mark.parametrize("algo", ALGOS)
+def test_runner_hip_tracks_torch_engine(algo):
+    """HIP engine (bf16 MFMA operands) vs the same runner on the fp32 PyTorch engine: 8 clients of unequal sizes
+    (partial last batches, size-sorted lockstep groups), 2 rounds.  bf16 activations flip max-pool / ReLU decisions,
+    so a single step's gradient already differs from fp32 by ~10-20 % in L2 (free-running cosine ~0.9-0.99,
+    test_gpu_kernels) and trajectories drift apart; they are compared by evaluation loss / accuracy, by the
+    direction of the updates and (DisPFL / SubAvg) by mask agreement.  Exactness of the HIP path itself is
+    covered by the kernel tests, the graph-vs-eager test above and the selection reproduction test below."""
+    fed = _fed(SIZES)
+    a, w0 = _run(algo, "hip", fed, **_extra(algo))
+    b, _ = _run(algo, "torch", fed, **_extra(algo))
+    upd_a = (a.theta[:, :a.P] - w0[:, :a.P]).double()
+    upd_b = (b.theta[:, :b.P] - w0[:, :b.P]).double()
+    cos = F.cosine_similarity(upd_a.flatten(), upd_b.flatten(), dim=0)
+    print(algo, "update cosine", float(cos), "rel err", _relerr(upd_a, upd_b))
+    assert float(cos) > 0.25
+    if algo in ("dispfl", "subavg"):
+        from neuroimagedisttraining_amd.engine import masks as MK
+        agree = float((MK.unpack_bits(a.mbits, a.P) == MK.unpack_bits(b.mbits, b.P)).float().mean())
+        print(algo, "mask agreement", agree)
+        assert agree > 0.9
+    for key in ("global_test_loss", "person_test_loss", "test_loss"):
+        if a.stat_info.get(key):
+            print(algo, key, a.stat_info[key], b.stat_info[key])
+            assert abs(a.stat_info[key][-1] - b.stat_info[key][-1]) <= 0.05 * abs(b.stat_info[key][-1]) + 0.02
+    for key in ("global_test_acc", "person_test_acc"):
+        if a.stat_info.get(key):
+            assert abs(a.stat_info[key][-1] - b.stat_info[key][-1]) <= 0.3
+
+
+def test_dispfl_fire_regrow_on_hip_equals_torch_selection():
+    """The DisPFL round's on-device fire / regrow equals the torch twin (stable sorts per layer) applied to the same
+    HIP-trained weights and eval-mode gradients; density per layer is preserved."""
+    from neuroimagedisttraining_amd.engine import masks as MK
+    fed = _fed(SIZES[:4])
+    r, _ = _run("dispfl", "hip", fed, rounds=1)
+    before = r.shared_bits.clone()
+    assert torch.equal(r.mspace.popcount(before), r.mspace.popcount(r.mbits))
+    rows, loc = r.all_rows()
+    r.local_grad(r.rowset, rows, loc, 0, bn_train=False)
+    drop = r.cfg.anneal_factor / 2 * (1 + np.cos(0))
+    nnz = r.mspace.popcount(before)
+    k = torch.ceil(torch.tensor(drop, dtype=torch.float32) * nnz.float()).long()
+    mine = before.clone()
+    r.mspace.select(MK.FIRE, r.theta, mine, k.to(DEV))
+    r.mspace.select(MK.REGROW_ABS, r.grads, mine, k.to(DEV))
+    assert torch.equal(mine, r.mbits), "the round's masks must be reproducible from its weights and gradients"
+    ref = before.cpu().clone()
+    r.mspace.select(MK.FIRE, r.theta.cpu(), ref, k.cpu())
+    r.mspace.select(MK.REGROW_ABS, r.grads.cpu(), ref, k.cpu())
+    assert torch.equal(mine.cpu(), ref)
