@@ -320,6 +320,9 @@ def run_hip(args, algo, logger):
     from .utils import checkpoint as ck
     info = rt.init_distributed()
     x8, mom, labels, splits = hip_cohort(args, info, logger, with_val=algo == "fedfomo")
+    logger.info("HIP cohort: %s, %d clients, train sizes %s" % (
+        "NIDTVOL1 %s" % _resolve_cohort(args.data_dir) if not args.synthetic_abcd else "synthetic ABCD-shape",
+        len(splits), [len(s.train) for s in splits]))
     model = AlexNet3D_Dropout(num_classes=1)
     eng = HipEngine(model, x8, mom, labels, info.device)
     cfg = fl_config(args, algo)

@@ -83,6 +83,10 @@ def make_synthetic_abcd(n_subjects, shape=ABCD_SHAPE, n_sites=21, seed=0, device
     w = 1.0 / np.arange(1, n_sites + 1) ** 0.5
     site_draw = rs.choice(n_sites, size=n_subjects, p=w / w.sum()).astype(np.float32)
     site = site_draw if site is None else np.asarray(site, dtype=np.float32)
+    if len(site) != n_subjects or len(labels) != n_subjects:
+        raise ValueError("labels / site must have one entry per subject")
+    if site.size and (site.min() < 0 or site.max() >= n_sites):  # indexes the per-site gain table on device
+        raise ValueError("site ids must lie in [0, n_sites=%d)" % n_sites)
     rs = np.random.RandomState(12345)  # scanner effects are a property of the site, shared by all clients
     site_gain = 1.0 + site_shift * rs.randn(n_sites).astype(np.float32)
     site_bias = site_shift * 0.5 * rs.randn(n_sites).astype(np.float32)
