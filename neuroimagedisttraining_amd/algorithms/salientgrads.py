@@ -9,7 +9,7 @@
 
 This is the torch-eager, sequential-client implementation with reference semantics (and the
 test oracle).  The production path — all clients of a GPU training in lockstep on HIP kernels,
-RCCL aggregation across GPUs — is :class:`neuroimagedisttraining_amd.engine.FederatedEngine`.
+RCCL aggregation across GPUs — is :class:`neuroimagedisttraining_amd.engine.runner.FLRunner`.
 """
 from __future__ import annotations
 

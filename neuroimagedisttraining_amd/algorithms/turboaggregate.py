@@ -98,24 +98,29 @@ def LCC_decoding_with_points(f_eval, eval_points, target_points, p):  # noqa: N8
     return LCC_encoding_with_points(f_eval, target_points, eval_points, p)
 
 
+def lcc_points(n, p):
+    """The reference's evaluation points: n consecutive integers centred on 0, mod p
+    (``stt = -floor(n/2)``, ``mpc_function.py:121-125``)."""
+    s = -int(np.floor(n / 2))
+    return [int(v) % p for v in range(s, s + n)]
+
+
 def LCC_encoding(X, N, K, T, p, rng=None):  # noqa: N802
-    """Split X [m, d] into K row blocks, append T random blocks, LCC-encode for N workers."""
+    """Split X [m, d] into K row blocks, append T random blocks, LCC-encode for N workers.  Data blocks sit at the
+    reference's centred points beta (K + T of them) and worker j evaluates at the centred point alpha_j (N of
+    them), so the shares equal the reference's (``mpc_function.py:111-135``)."""
     rng = np.random if rng is None else rng
     X = np.asarray(X, dtype=np.int64) % p
     m = X.shape[0] // K
     blocks = [X[i * m:(i + 1) * m] for i in range(K)] + [rng.randint(p, size=(m,) + X.shape[1:]) for _ in range(T)]
-    beta = list(range(1, K + T + 1))
-    alpha = list(range(K + T + 1, K + T + 1 + N))
-    return LCC_encoding_with_points(np.stack(blocks), alpha, beta, p)
+    return LCC_encoding_with_points(np.stack(blocks), lcc_points(N, p), lcc_points(K + T, p), p)
 
 
 def LCC_encoding_w_Random(X, R_, N, K, T, p):  # noqa: N802
     X = np.asarray(X, dtype=np.int64) % p
     m = X.shape[0] // K
     blocks = [X[i * m:(i + 1) * m] for i in range(K)] + [np.asarray(R_[t], dtype=np.int64) for t in range(T)]
-    beta = list(range(1, K + T + 1))
-    alpha = list(range(K + T + 1, K + T + 1 + N))
-    return LCC_encoding_with_points(np.stack(blocks), alpha, beta, p)
+    return LCC_encoding_with_points(np.stack(blocks), lcc_points(N, p), lcc_points(K + T, p), p)
 
 
 def LCC_encoding_w_Random_partial(X, R_, N, K, T, p, worker_idx):  # noqa: N802
@@ -123,11 +128,14 @@ def LCC_encoding_w_Random_partial(X, R_, N, K, T, p, worker_idx):  # noqa: N802
 
 
 def LCC_decoding(f_eval, f_deg, N, K, T, worker_idx, p):  # noqa: N802
-    """Decode the K data blocks from ``(K+T-1)*f_deg + 1`` worker evaluations."""
-    alpha = [K + T + 1 + int(i) for i in worker_idx]
-    beta = list(range(1, K + 1))
+    """Interpolate the K data blocks from the evaluations of workers ``worker_idx`` (reference
+    ``mpc_function.py:195-212``: targets are the K centred points, sources the workers' centred points).  As in
+    the reference, the targets coincide with the encoder's first K points only when floor(K/2) ==
+    floor((K+T)/2) (e.g. T = 1 with even K); :func:`LCC_decoding_with_points` takes explicit points."""
+    alpha = lcc_points(N, p)
+    ev = [alpha[int(i)] for i in worker_idx]
     need = (K + T - 1) * f_deg + 1
-    return LCC_decoding_with_points(np.asarray(f_eval)[:need], alpha[:need], beta, p)
+    return LCC_decoding_with_points(np.asarray(f_eval)[:need], ev[:need], lcc_points(K, p), p)
 
 
 def Gen_Additive_SS(d, n_out, p, rng=None):  # noqa: N802

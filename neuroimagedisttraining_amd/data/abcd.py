@@ -156,9 +156,13 @@ def load_partition_data_abcd(data_dir, partition_method="site", partition_alpha=
     return _assemble(store, train, test, batch_size, 2, logger)
 
 
-def load_partition_data_abcd_rescale(store: VolumeStore, client_number, batch_size, logger=None,
-                                     split_ratio=0.2, seed=42):
-    """Merge all subjects, seeded 80/20 split, then contiguous equal shards per client."""
+def load_partition_data_abcd_rescale(data_dir, partition_method="site", partition_alpha=0.3, client_number=21,
+                                     batch_size=16, logger=None, split_ratio=0.2, seed=42, store=None, device="cpu"):
+    """Reference signature (``ABCD/data_loader.py:216``): merge every subject of the cohort at ``data_dir`` (or an
+    in-memory ``store``), seeded 80/20 split, then ``client_number`` contiguous equal shards (IID by order); the
+    test shards are the matching slices of the test pool."""
+    if store is None:
+        store = _load_store(data_dir, device, logger)
     n = len(store)
     ix = np.arange(n)
     np.random.RandomState(seed).shuffle(ix)
@@ -167,3 +171,22 @@ def load_partition_data_abcd_rescale(store: VolumeStore, client_number, batch_si
     train = {c: s for c, s in enumerate(np.array_split(tr, client_number))}
     test = {c: s for c, s in enumerate(np.array_split(te, client_number))}
     return _assemble(store, train, test, batch_size, 2, logger)
+
+
+def _load_store(data_dir, device="cpu", logger=None):
+    """VolumeStore of a cohort path (NIDTVOL1 file / directory, or HDF5 with h5py); synthetic if absent."""
+    path = data_dir
+    if path and os.path.isdir(path):
+        nv = os.path.join(path, "alldatain8bitsnormalized.nidtvol")
+        path = nv if os.path.exists(nv) else os.path.join(path, "alldatain8bitsnormalized.h5")
+    if path and str(path).endswith(".nidtvol") and os.path.exists(path):
+        from .volume_file import VolumeFile
+        return VolumeFile(path).to_store(device=device)
+    try:
+        X, y, site = _read_h5(path)
+    except Exception as e:  # noqa: BLE001
+        (logger or log).warning("ABCD cohort unavailable (%s); using a synthetic ABCD-shape cohort", e)
+        return make_synthetic_abcd(21 * 40, seed=0, device=device)
+    return VolumeStore(torch.from_numpy(np.ascontiguousarray(X)).to(torch.uint8).to(device),
+                       torch.from_numpy(np.asarray(y, np.float32)).to(device),
+                       torch.from_numpy(np.asarray(site, np.float32)).to(device))

@@ -11,11 +11,12 @@ the grey-matter maps as a float array, an ``.npy`` memory map, or any iterable o
    ``LabelEncoder`` (sorted unique site names) (cells 27-28).
 
 The result is written as a NIDTVOL1 file (:func:`data.volume_file.write_volume_file`), which the native
-reader memory-maps (the notebook saved an HDF5 with keys ``X``, ``y``, ``site``).  The volumes are processed
-one subject at a time, so a cohort never has to fit in host memory twice.
+reader memory-maps (the notebook saved an HDF5 with keys ``X``, ``y``, ``site``).  The volumes are quantised and
+written one subject at a time, so the cohort is never resident in host memory (the float cohort is 97 GB).
 
-CLI: ``python -m neuroimagedisttraining_amd.data.preprocess cohort.npz out.nidtvol`` with ``X`` (float
-[N, D, H, W]), ``female`` and ``site`` arrays in the npz (loaded with ``allow_pickle=False``).
+CLI: ``python -m neuroimagedisttraining_amd.data.preprocess <X.npy> <labels.npz> out.nidtvol`` with the float
+grey-matter maps ``X`` [N, D, H, W] as a ``.npy`` (memory-mapped, ``mmap_mode='r'``) and ``female`` / ``site``
+arrays in the npz (loaded with ``allow_pickle=False``).
 """
 from __future__ import annotations
 
@@ -62,27 +63,46 @@ def label_encode(values):
     return np.array([index[x] for x in vals], dtype=np.int64), cats
 
 
-def preprocess_cohort(volumes, female, site, out_path=None, threshold=0.2):
-    """Mask, quantise and label a cohort; returns ``(uint8 volumes [N, D, H, W], y, site_codes)`` and, with
-    ``out_path``, also writes the NIDTVOL1 file.  ``volumes`` must be re-iterable (array or memory map)."""
+def preprocess_cohort(volumes, female, site, out_path=None, threshold=0.2, drop_missing=True):
+    """Mask, quantise and label a cohort.
+
+    ``volumes`` must be re-iterable (array, ``np.load(..., mmap_mode='r')`` memory map, or a sequence of
+    per-subject arrays): pass 1 computes the mean-image mask, pass 2 quantises one subject at a time.  With
+    ``out_path`` each quantised subject is streamed straight into the NIDTVOL1 file (host memory holds one subject,
+    never the cohort) and ``(None, y, site_codes)`` is returned; without it the uint8 cohort is returned.
+    ``drop_missing``: subjects whose sex is missing (category code -1) are left out instead of being written with
+    label -1, which a BCE loss would consume as a target."""
     mask = brain_mask(volumes, threshold)
-    q = np.stack([quantize_subject(v, mask) for v in volumes])
     y, _ = category_codes(female)
     s, _ = label_encode(site)
-    if out_path is not None:
-        from .volume_file import write_volume_file
-        write_volume_file(out_path, q, y.astype(np.float32), s.astype(np.float32))
-    return q, y, s
+    keep = np.nonzero(y >= 0)[0] if drop_missing else np.arange(len(y))
+    if out_path is None:
+        q = np.stack([quantize_subject(volumes[i], mask) for i in keep]) if len(keep) else None
+        return q, y[keep], s[keep]
+    from .volume_file import write_volume_file
+    shape = tuple(np.asarray(volumes[int(keep[0])]).shape) if len(keep) else tuple(np.asarray(volumes[0]).shape)
+
+    class _Quantised:  # sliceable view that quantises on demand (the writer streams `chunk` subjects at a time)
+        def __init__(self):
+            self.shape = (len(keep),) + shape
+
+        def __getitem__(self, sl):
+            return np.stack([quantize_subject(volumes[int(i)], mask) for i in keep[sl]])
+
+    write_volume_file(out_path, _Quantised(), y[keep].astype(np.float32), s[keep].astype(np.float32), chunk=1)
+    return None, y[keep], s[keep]
 
 
 def main(argv=None):
     argv = sys.argv[1:] if argv is None else argv
-    if len(argv) != 2:
+    if len(argv) != 3:
         print(__doc__)
         return 2
-    d = np.load(argv[0], allow_pickle=False)
-    q, y, s = preprocess_cohort(d["X"], d["female"], d["site"], out_path=argv[1])
-    print("wrote %s: %d subjects %s, %d sites" % (argv[1], q.shape[0], tuple(q.shape[1:]), len(set(s.tolist()))))
+    X = np.load(argv[0], mmap_mode="r", allow_pickle=False)
+    d = np.load(argv[1], allow_pickle=False)
+    _, y, s = preprocess_cohort(X, d["female"], d["site"], out_path=argv[2])
+    print("wrote %s: %d subjects (%d dropped: missing sex) %s, %d sites" % (
+        argv[2], len(y), X.shape[0] - len(y), tuple(X.shape[1:]), len(set(s.tolist()))))
     return 0
 
 

@@ -174,6 +174,24 @@ def test_mpc_bgw_lcc_additive():
     enc = TA.LCC_encoding(X2, N=6, K=2, T=1, p=p, rng=rs)
     dec = TA.LCC_decoding(enc, 1, 6, 2, 1, list(range(6)), p)
     assert np.array_equal(np.concatenate(list(dec), 0), X2 % p)
+    # shares equal the reference's: worker j holds the Lagrange interpolant through the blocks at the centred
+    # points beta = {-1, 0, 1} evaluated at the centred alpha_j = j - 3 (mpc_function.py:121-125)
+    beta, alpha = [-1, 0, 1], [j - 3 for j in range(6)]
+    rs2 = np.random.RandomState(5)
+    enc = TA.LCC_encoding(X2, N=6, K=2, T=1, p=p, rng=rs2)
+    rnd = np.random.RandomState(5).randint(p, size=(2, 3))
+    blocks = [X2[:2] % p, X2[2:] % p, rnd]
+    for j, a in enumerate(alpha):
+        want = np.zeros((2, 3), dtype=np.int64)
+        for k, b in enumerate(beta):
+            num = den = 1
+            for o in beta:
+                if o != b:
+                    num = num * ((a - o) % p) % p
+                    den = den * ((b - o) % p) % p
+            coef = num * pow(den, p - 2, p) % p
+            want = (want + coef * blocks[k]) % p
+        assert np.array_equal(enc[j], want), j
     ss = TA.Gen_Additive_SS(7, 4, p, rs)
     assert np.all(ss.sum(0) % p == 0)
     assert TA.modular_inv(3, p) * 3 % p == 1

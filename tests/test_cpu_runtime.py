@@ -120,7 +120,7 @@ def test_abcd_preprocessing_matches_notebook_semantics(tmp_path):
     vols[:, :2] = 0.05  # low-mean region falls outside the mask
     female = np.array(["1", "0", "1", "", "0"], dtype=object)
     site = np.array(["site21", "site02", "site02", "site10", "site21"])
-    q, y, s = preprocess_cohort(vols, female, site, out_path=str(tmp_path / "c.nidtvol"))
+    q, y, s = preprocess_cohort(vols, female, site, drop_missing=False)
     mask = vols.mean(0) > 0.2
     for i in range(5):
         v = vols[i].astype(np.float64) * mask
@@ -128,6 +128,31 @@ def test_abcd_preprocessing_matches_notebook_semantics(tmp_path):
         assert np.array_equal(q[i], ref)
     assert (q[:, :2] == 0).all()
     assert y.tolist() == [1, 0, 1, -1, 0] and s.tolist() == [2, 0, 0, 1, 2]
+    # streamed into the file from a memory-mapped .npy; the subject with missing sex is dropped
+    np.save(tmp_path / "X.npy", vols)
+    _, y2, s2 = preprocess_cohort(np.load(tmp_path / "X.npy", mmap_mode="r"), female, site,
+                                  out_path=str(tmp_path / "c.nidtvol"))
+    assert y2.tolist() == [1, 0, 1, 0] and s2.tolist() == [2, 0, 0, 2]
     vf = VolumeFile(str(tmp_path / "c.nidtvol"))
-    assert np.array_equal(vf.gather(np.array([3, 1])).numpy(), q[[3, 1]])
-    assert np.asarray(vf.labels).tolist() == [1, 0, 1, -1, 0]
+    assert np.array_equal(vf.gather(np.array([3, 1])).numpy(), q[[4, 1]])
+    assert np.asarray(vf.labels).tolist() == [1, 0, 1, 0]
+
+
+def test_abcd_rescale_loader_reference_signature(tmp_path):
+    """load_partition_data_abcd_rescale(data_dir, partition_method, partition_alpha, client_number, batch_size,
+    logger) like ABCD/data_loader.py:216: every subject in exactly one train or test shard, contiguous equal
+    train shards of the seeded 80/20 split."""
+    import numpy as np
+    import torch
+    from neuroimagedisttraining_amd.data.abcd import load_partition_data_abcd_rescale
+    from neuroimagedisttraining_amd.data.volume_file import write_volume_file
+    n = 50
+    vols = torch.randint(0, 256, (n, 6, 7, 6), dtype=torch.uint8)
+    path = str(tmp_path / "alldatain8bitsnormalized.nidtvol")
+    write_volume_file(path, vols, np.arange(n) % 2, np.arange(n) % 5)
+    ds = load_partition_data_abcd_rescale(str(tmp_path), "site", 0.3, 4, 8, None)
+    num, trn, tst = ds[4], ds[5], ds[6]
+    tr = np.concatenate([trn[c].indices for c in range(4)])
+    te = np.concatenate([tst[c].indices for c in range(4)])
+    assert sorted(np.concatenate([tr, te]).tolist()) == list(range(n))
+    assert len(te) == int(n * 0.2) and [num[c] for c in range(4)] == [10, 10, 10, 10]
