@@ -183,13 +183,21 @@ def test_conv3d_wgrad_and_dgrad(cin, cout, pad, sp, xf):
         assert torch.equal(wp[g].view(cout, 3, 3, 3, cin).permute(0, 4, 1, 2, 3), wt32[g].bfloat16())
 
 
+def _signed_gamma(G, C):
+    """gamma in (0.5, 1.5) with ~1/4 negative and a few ~0 entries (training can drive gamma through zero)."""
+    g = torch.rand(G, C, device=DEV) + 0.5
+    g[:, ::4] *= -1
+    g[:, 5::16] = 1e-4
+    return g
+
+
 def test_bn_relu_pool_and_bwd():
     m = _m()
     G, B, C = 2, 2, 128
     D, H, W = 17, 21, 17
     torch.manual_seed(3)
     y = torch.randn(G * B, D, H, W, C, device=DEV).bfloat16()
-    scale = torch.rand(G, C, device=DEV) + 0.5
+    scale = _signed_gamma(G, C)
     shift = torch.randn(G, C, device=DEV) * 0.3
     out = torch.empty(G * B, D // 3, H // 3, W // 3, C, device=DEV, dtype=torch.bfloat16)
     am = torch.empty_like(out, dtype=torch.uint8)
@@ -201,7 +209,7 @@ def test_bn_relu_pool_and_bwd():
     pr, ir = F.max_pool3d(torch.relu(zr), 3, 3, return_indices=True)
     assert _relerr(out.float(), _cl(pr)) < 1e-2
     # backward through pool -> relu -> BN(train) vs autograd
-    gamma = torch.rand(G, C, device=DEV) + 0.5
+    gamma = _signed_gamma(G, C)
     beta = torch.randn(G, C, device=DEV) * 0.3
     P = 4 * C
     theta = torch.zeros(G, P, device=DEV)
@@ -235,7 +243,7 @@ def test_bn_relu_pool_and_bwd():
         assert float(grad[g, 2 * C:3 * C].abs().max()) == 0.0  # conv bias grad before BN is exactly 0
 
 
-def _alexnet_setup(G, B, seed=0):
+def _alexnet_setup(G, B, seed=0, signed_gamma=False):
     from neuroimagedisttraining_amd.data.volumes import make_synthetic_abcd
     from neuroimagedisttraining_amd.data.synthetic_fl import to_hip_store
     from neuroimagedisttraining_amd.engine.flat import ParamLayout
@@ -258,6 +266,9 @@ def _alexnet_setup(G, B, seed=0):
             o, k = pl.offsets[i], pl.numel(i)
             if n.endswith("weight"):
                 theta[:, o:o + k] = 0.75 + 0.5 * torch.rand(G, k, device=DEV)
+                if signed_gamma:  # negative and near-zero gammas (sign folding of the fused conv1 forward)
+                    theta[:, o:o + k:4] *= -1
+                    theta[:, o + 5:o + k:16] = 1e-3
             else:
                 theta[:, o:o + k] = 0.1 * torch.randn(G, k, device=DEV)
     return store, x8, mom, pl, bl, theta, bufs
@@ -311,12 +322,12 @@ def _routed_reference(b, theta, pl, vols, labels, G, B, keep, seed):
     return torch.stack(grads), torch.cat(logits)
 
 
-@pytest.mark.parametrize("keep", [1.0, 0.5])
-def test_alexnet_train_step_matches_autograd(keep):
+@pytest.mark.parametrize("keep,G,B,signed", [(1.0, 2, 4, False), (0.5, 2, 4, False), (0.5, 2, 4, True),
+                                              (0.5, 8, 16, True)])
+def test_alexnet_train_step_matches_autograd(keep, G, B, signed):
     from neuroimagedisttraining_amd.engine.alexnet_hip import HipAlexNet3D
     from neuroimagedisttraining_amd.ops.reference import train_step_reference
-    G, B = 2, 4
-    store, x8, mom, pl, bl, theta, bufs = _alexnet_setup(G, B)
+    store, x8, mom, pl, bl, theta, bufs = _alexnet_setup(G, B, signed_gamma=signed)
     net = HipAlexNet3D(pl, bl, DEV)
     grads = padded_rows(G, pl.total, DEV)
     bufs_h = padded_rows(G, bl.total, DEV)
@@ -349,12 +360,14 @@ def test_alexnet_train_step_matches_autograd(keep):
     assert float(cos) > 0.9, float(cos)
 
 
-def test_conv1_fused_fwd_and_sparse_wgrad():
-    """conv1 -> BN(train, stats from patch moments) -> ReLU -> pool, and the closed-form backward, vs fp64 autograd."""
+@pytest.mark.parametrize("signed", [False, True])
+def test_conv1_fused_fwd_and_sparse_wgrad(signed):
+    """conv1 -> BN(train, stats from patch moments) -> ReLU -> pool, and the closed-form backward, vs fp64 autograd
+    (``signed``: negative and near-zero gammas — the fused forward folds sign(gamma) into its weights)."""
     from neuroimagedisttraining_amd.engine.alexnet_hip import HipAlexNet3D
     m = _m()
     G, B = 2, 2
-    store, x8, mom, pl, bl, theta, bufs = _alexnet_setup(G, B, seed=9)
+    store, x8, mom, pl, bl, theta, bufs = _alexnet_setup(G, B, seed=9, signed_gamma=signed)
     net = HipAlexNet3D(pl, bl, DEV)
     idx = torch.arange(G * B, dtype=torch.int32, device=DEV)
     b = net._bufs(G, B, True)
@@ -398,11 +411,12 @@ def test_conv1_fused_fwd_and_sparse_wgrad():
         assert e_w < 2e-2 and e_g < 2e-2 and e_b < 2e-2, (e_w, e_g, e_b)
 
 
-def test_alexnet_eval_matches_reference():
+@pytest.mark.parametrize("signed", [False, True])
+def test_alexnet_eval_matches_reference(signed):
     from neuroimagedisttraining_amd.engine.alexnet_hip import HipAlexNet3D
     from neuroimagedisttraining_amd.ops.reference import eval_logits_reference
     G, B = 2, 3
-    store, x8, mom, pl, bl, theta, bufs = _alexnet_setup(G, B, seed=5)
+    store, x8, mom, pl, bl, theta, bufs = _alexnet_setup(G, B, seed=5, signed_gamma=signed)
     for i, n in enumerate(bl.names):
         o, k = bl.offsets[i], bl.numel(i)
         if n.endswith("running_mean"):

@@ -9,7 +9,6 @@ import pytest
 import torch
 import torch.nn.functional as F
 
-os.environ.setdefault("MIOPEN_FIND_MODE", "FAST")  # the fp32 oracle engine: skip MIOpen's exhaustive search
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"

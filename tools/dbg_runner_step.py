@@ -2,7 +2,6 @@
 import os, sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests"))
-os.environ.setdefault("MIOPEN_FIND_MODE", "FAST")
 import numpy as np, torch
 from test_gpu_personalized import _fed, _run, _relerr
 from neuroimagedisttraining_amd.engine.executor import HipEngine, TorchEngine, padded_rows
