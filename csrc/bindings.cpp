@@ -35,6 +35,22 @@ int conv3d_wgrad_nsplit(int G, int B, int D, int H, int W, int Cin, int Cout, in
 void pack_conv_w(uintptr_t theta, int64_t ldt, int64_t off, int G, int Cout, int Cin, float scale, uintptr_t wp,
                  uintptr_t wt, uintptr_t stream);
 void bn_relu_apply(uintptr_t y, uintptr_t sc, uintptr_t sh, uintptr_t h, int64_t npos, int C, int S, uintptr_t stream);
+void conv_fwd_g(uintptr_t x, uintptr_t w, uintptr_t y, int G, int B, int D, int H, int W, int Cin, int Cout, int kt,
+                int st, int pad, int padd, uintptr_t stream);
+void conv_pos_table_g(uintptr_t tab, int B, int D, int H, int W, int kt, int st, int pad, int padd, uintptr_t stream);
+void conv_wgrad_g(uintptr_t x, uintptr_t dy, uintptr_t part, uintptr_t grad, int64_t ldg, int64_t off, int G, int B,
+                  int D, int H, int W, int Cin, int Cout, int kt, int st, int pad, int padd, int nsplit, float scale,
+                  uintptr_t ptab, uintptr_t stream);
+int conv_wgrad_nsplit_g(int G, int B, int D, int H, int W, int Cin, int Cout, int kt, int st, int pad, int padd);
+void pack_conv_wk(uintptr_t theta, int64_t ldt, int64_t off, int G, int Cout, int Cin, int kt, int cin_src,
+                  float scale, uintptr_t wp, uintptr_t wt, uintptr_t stream);
+// gn.hip
+void gn_fwd(uintptr_t t, uintptr_t res, uintptr_t theta, int64_t ldt, int64_t off_w, int64_t off_b, uintptr_t y,
+            uintptr_t stats, int N, int B, int S, int C, int relu, uintptr_t stream);
+void gn_bwd(uintptr_t dy, int dy_bf16, uintptr_t mask, uintptr_t t, uintptr_t stats, uintptr_t theta, int64_t ldt,
+            int64_t off_w, uintptr_t dt, uintptr_t part, int N, int B, int S, int C, uintptr_t stream);
+void gn_param_grads(uintptr_t part, int G, int B, int C, uintptr_t grads, int64_t ldg, int64_t off_w, int64_t off_b,
+                    uintptr_t stream);
 // bn.hip
 void bn_finalize(uintptr_t stats, int nPB, int BP, int Mg, int G, int C, uintptr_t theta, int64_t ldt, int64_t off_g,
                  int64_t off_b, uintptr_t bufs, int64_t ldb, int64_t off_rm, int64_t off_rv, int64_t off_nbt,
@@ -111,6 +127,14 @@ PYBIND11_MODULE(_nidt_hip, m) {
   DEF(conv3d_pos_table);
   DEF(pack_conv_w);
   DEF(bn_relu_apply);
+  DEF(conv_fwd_g);
+  DEF(conv_pos_table_g);
+  DEF(conv_wgrad_g);
+  DEF(conv_wgrad_nsplit_g);
+  DEF(pack_conv_wk);
+  DEF(gn_fwd);
+  DEF(gn_bwd);
+  DEF(gn_param_grads);
   DEF(bn_finalize);
   DEF(bn_eval);
   DEF(bn_relu_pool);

@@ -42,6 +42,9 @@ struct ConvFwdArgs {
   int G = 0;            // clients (split-K partial indexing)
   int64_t bias_ld = 0;  // bias row stride per client (0 = Cout; the flat parameter row stride to read theta directly)
   float* part = nullptr;  // [ksplit, G, Mg, Cout] fp32 partial sums
+  // geometry (LDS-DMA path): kt taps per output (27 = 3x3x3, 9 = 1x3x3 (2-D convs as D = 1 volumes), 1 = 1x1x1),
+  // stride st in every dimension, depth padding padd (the h/w padding is pad)
+  int kt = 27, st = 1, padd = 0;
 };
 
 constexpr int kFwdBP = 128;  // positions per block
@@ -344,7 +347,7 @@ __global__ __launch_bounds__(64 * WM * WN, ((NST == 2 ? 8 : 4) / (WM * WN)) > 0 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // uniform: LDS destinations stay in SGPRs
   const int wco = wid / WN, wp = wid % WN;
-  const int Cin = a.Cin, nck = Cin / BK, nks = 27 * nck;
+  const int Cin = a.Cin, nck = Cin / BK, nks = a.kt * nck;
   const int ks0 = nks * sp / a.ksplit, ks1 = nks * (sp + 1) / a.ksplit;  // this split's k-steps
   const int lrow = lane >> 3, slot = lane & 7;
 
@@ -363,7 +366,7 @@ __global__ __launch_bounds__(64 * WM * WN, ((NST == 2 ? 8 : 4) / (WM * WN)) > 0 
       const int nl = m / S, s = m - nl * S;
       const int od = s / (a.Ho * a.Wo), r2 = s - od * a.Ho * a.Wo;
       const int oh = r2 / a.Wo, ow = r2 - oh * a.Wo;
-      const int d0 = od - a.pad, h0 = oh - a.pad, w0 = ow - a.pad;
+      const int d0 = od * a.st - a.padd, h0 = oh * a.st - a.pad, w0 = ow * a.st - a.pad;
       // may be negative for padded windows; only taps inside the volume (tmask) are ever read
       roff[i] = ((((nl * a.D + d0) * a.H + h0) * a.W + w0) * Cin + ((slot ^ swz_dma(row)) << 3)) * 2;
       tmask[i] = tap_mask3(d0, h0, w0, a.D, a.H, a.W);
@@ -373,11 +376,11 @@ __global__ __launch_bounds__(64 * WM * WN, ((NST == 2 ? 8 : 4) / (WM * WN)) > 0 
 #pragma unroll
   for (int i = 0; i < A_INSTR; ++i) {
     const int row = 8 * (wid * A_INSTR + i) + lrow;
-    aoff[i] = ((co0 + row) * 27 * Cin + ((slot ^ swz_dma(row)) << 3)) * 2;
+    aoff[i] = ((co0 + row) * a.kt * Cin + ((slot ^ swz_dma(row)) << 3)) * 2;
   }
   const int64_t xcl = (int64_t)a.B * a.D * a.H * a.W * Cin;
   const i32x4_t rxs = make_rsrc(a.x + (int64_t)g * xcl, (uint32_t)(xcl * 2));
-  const i32x4_t rws = make_rsrc(a.w + (int64_t)g * a.Cout * 27 * Cin, (uint32_t)(a.Cout * 27 * Cin * 2));
+  const i32x4_t rws = make_rsrc(a.w + (int64_t)g * a.Cout * a.kt * Cin, (uint32_t)(a.Cout * a.kt * Cin * 2));
 
 #define DMA_ISSUE(KS, BUFI)                                                                                   \
   {                                                                                                           \
@@ -565,21 +568,34 @@ static void launch_fwd_dma(int nst, dim3 g, hipStream_t s, const ConvFwdArgs& a,
   hipLaunchKernelGGL((k_conv_fwd_dma<BC, WM, WN, 2, BI, ST>), g, dim3(64 * WM * WN), 0, s, a, nCO);
 }
 
+// output extent of one dimension: taps k (3 or 1), stride st, padding p
+static inline int conv_out_dim(int n, int k, int st, int p) { return (n + 2 * p - k) / st + 1; }
+
 static void conv3d_fwd_impl(uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t xs, uintptr_t xt, uintptr_t y,
                             uintptr_t stats, int G, int B, int D, int H, int W, int Cin, int Cout, int pad,
-                            uintptr_t stream, int ksplit, uintptr_t part, int64_t bias_ld = 0) {
+                            uintptr_t stream, int ksplit, uintptr_t part, int64_t bias_ld = 0, int kt = 27,
+                            int stride = 1, int padd = -1) {
   NIDT_REQUIRE(Cin % 32 == 0, "conv3d_fwd: Cin must be a multiple of 32");
   NIDT_REQUIRE((xs == 0 && Cin % 64 == 0) ? Cin <= kMaxCin : Cin <= 192,
                "conv3d_fwd: Cin <= 512 (LDS-DMA path: Cin % 64 == 0, no input transform), else <= 192");
   NIDT_REQUIRE(Cout % 64 == 0, "conv3d_fwd: Cout must be a multiple of 64");
   NIDT_REQUIRE(pad >= 0 && pad <= 2, "conv3d_fwd: pad in [0,2]");
+  NIDT_REQUIRE(kt == 27 || kt == 9 || kt == 1, "conv3d_fwd: taps 27 (3x3x3), 9 (1x3x3) or 1 (1x1x1)");
+  NIDT_REQUIRE(stride == 1 || stride == 2, "conv3d_fwd: stride 1 or 2");
+  if (padd < 0) padd = pad;
+  NIDT_REQUIRE(padd >= 0 && padd <= 2 && (kt == 27 || padd == 0) && (kt != 1 || pad == 0),
+               "conv3d_fwd: padding must fit the kernel extent");
+  NIDT_REQUIRE((kt == 27 && stride == 1 && padd == pad) || (xs == 0 && Cin % 64 == 0),
+               "conv3d_fwd: 9/1-tap or strided convs need the LDS-DMA path (Cin % 64 == 0, no input transform)");
   NIDT_REQUIRE((int64_t)B * D * H * W * Cin * 2 < (1ll << 31),
                "conv3d_fwd: per-client input must stay below 2 GiB (32-bit buffer offsets)");
   ConvFwdArgs a;
   a.x = ptr<const uint16_t>(x); a.w = ptr<const uint16_t>(w); a.bias = ptr<const float>(bias);
   a.xs = ptr<const float>(xs); a.xt = ptr<const float>(xt); a.y = ptr<uint16_t>(y); a.stats = ptr<float>(stats);
   a.B = B; a.D = D; a.H = H; a.W = W; a.Cin = Cin; a.Cout = Cout; a.pad = pad;
-  a.Do = D + 2 * pad - 2; a.Ho = H + 2 * pad - 2; a.Wo = W + 2 * pad - 2;
+  a.kt = kt; a.st = stride; a.padd = padd;
+  const int kd = kt == 27 ? 3 : 1, khw = kt == 1 ? 1 : 3;
+  a.Do = conv_out_dim(D, kd, stride, padd); a.Ho = conv_out_dim(H, khw, stride, pad); a.Wo = conv_out_dim(W, khw, stride, pad);
   NIDT_REQUIRE(a.Do > 0 && a.Ho > 0 && a.Wo > 0, "conv3d_fwd: empty output");
   a.Mg = B * a.Do * a.Ho * a.Wo;
   a.nPB = ceil_div(a.Mg, kFwdBP);
@@ -661,6 +677,14 @@ void conv3d_fwd(uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t xs, uintptr_
 void conv3d_fwd_bld(uintptr_t x, uintptr_t w, uintptr_t bias, int64_t bias_ld, uintptr_t y, uintptr_t stats, int G, int B,
                     int D, int H, int W, int Cin, int Cout, int pad, uintptr_t stream) {
   conv3d_fwd_impl(x, w, bias, 0, 0, y, stats, G, B, D, H, W, Cin, Cout, pad, stream, 1, 0, bias_ld);
+}
+
+// General client-grouped conv forward (no bias / statistics): kt taps (27, 9 = 2-D 3x3 on D = 1 volumes, 1 = 1x1),
+// stride st (1 or 2), h/w padding pad, depth padding padd.  w: [G][Cout][kt][Cin] bf16 (pack_conv_wk).
+void conv_fwd_g(uintptr_t x, uintptr_t w, uintptr_t y, int G, int B, int D, int H, int W, int Cin, int Cout, int kt,
+                int st, int pad, int padd, uintptr_t stream) {
+  NIDT_REQUIRE(Cin % 64 == 0, "conv_fwd_g: Cin must be a multiple of 64 (pad the channels)");
+  conv3d_fwd_impl(x, w, 0, 0, 0, y, 0, G, B, D, H, W, Cin, Cout, pad, stream, 1, 0, 0, kt, st, padd);
 }
 
 void conv3d_fwd_splitk(uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t y, uintptr_t stats, uintptr_t part,
@@ -870,10 +894,11 @@ __global__ __launch_bounds__(256, 2) void k_conv_wgrad(ConvWgArgs a) {
 // lanes would otherwise hit one bank ~27 times (Cin is a multiple of 32).  Dynamic LDS sized to the layer
 // (27 (Cin + 1) floats) instead of the 512-channel maximum: more resident blocks to cover the HBM latency.
 __global__ __launch_bounds__(256) void k_wgrad_reduce(const float* __restrict__ part, int nsplit, int G, int Cout,
-                                                      int Cin, float* grad, int64_t ldg, int64_t off, float scale) {
-  extern __shared__ float row[];  // [27][Cin + 1]
+                                                      int Cin, int kt, float* grad, int64_t ldg, int64_t off,
+                                                      float scale) {
+  extern __shared__ float row[];  // [kt][Cin + 1]
   const int co = blockIdx.x, g = blockIdx.y;
-  const int K = 27 * Cin, RS = Cin + 1;
+  const int K = kt * Cin, RS = Cin + 1;
   const int64_t tot = (int64_t)G * Cout * K;
   const float* src = part + ((int64_t)g * Cout + co) * K;  // 16-B aligned: K = 27 * 64 * n
   for (int k = 4 * threadIdx.x; k < K; k += 4 * 256) {
@@ -889,7 +914,7 @@ __global__ __launch_bounds__(256) void k_wgrad_reduce(const float* __restrict__ 
   __syncthreads();
   float* dst = grad + (int64_t)g * ldg + off + (int64_t)co * K;
   for (int e = threadIdx.x; e < K; e += 256) {
-    const int ci = e / 27, t = e - ci * 27;
+    const int ci = e / kt, t = e - ci * kt;
     dst[e] = row[t * RS + ci];
   }
 }
@@ -900,9 +925,19 @@ __global__ __launch_bounds__(256) void k_wgrad_reduce(const float* __restrict__ 
 // (one 64-position step ~1.28 us per block slot, ~12 steps of prologue/epilogue, ~5 TB/s slab traffic) picks the
 // ns with the smallest estimate; ties go to the smaller ns.  NIDT_WG_NSPLIT_LEGACY=1 restores the old rule
 // (ceil(2048 / tiles), capped) for A/B measurements.
+static int wgrad_nsplit_mk(int G, int Mg, int K, int Cout);
+
 int conv3d_wgrad_nsplit(int G, int B, int D, int H, int W, int Cin, int Cout, int pad) {
-  const int Mg = B * (D + 2 * pad - 2) * (H + 2 * pad - 2) * (W + 2 * pad - 2);
-  const int K = 27 * Cin;
+  return wgrad_nsplit_mk(G, B * (D + 2 * pad - 2) * (H + 2 * pad - 2) * (W + 2 * pad - 2), 27 * Cin, Cout);
+}
+
+int conv_wgrad_nsplit_g(int G, int B, int D, int H, int W, int Cin, int Cout, int kt, int st, int pad, int padd) {
+  const int kd = kt == 27 ? 3 : 1, khw = kt == 1 ? 1 : 3;
+  const int Mg = B * conv_out_dim(D, kd, st, padd) * conv_out_dim(H, khw, st, pad) * conv_out_dim(W, khw, st, pad);
+  return wgrad_nsplit_mk(G, Mg, kt * Cin, Cout);
+}
+
+static int wgrad_nsplit_mk(int G, int Mg, int K, int Cout) {
   const int base = G * (Cout / kWgCO) * ceil_div(K, kWgKC);
   static const bool legacy = [] {
     const char* e = getenv("NIDT_WG_NSPLIT_LEGACY");
@@ -955,13 +990,14 @@ struct ConvWgDmaArgs {
   int64_t xclient;      // elements per client in x (B*D*H*W*Cin)
 };
 
-__global__ void k_conv_pos_table(int2* tab, int Mg, int D, int H, int W, int pad) {
+__global__ void k_conv_pos_table(int2* tab, int Mg, int D, int H, int W, int Do, int Ho, int Wo, int st, int padd,
+                                 int pad) {
   const int m = blockIdx.x * blockDim.x + threadIdx.x;
   if (m >= Mg) return;
-  const int Do = D + 2 * pad - 2, Ho = H + 2 * pad - 2, Wo = W + 2 * pad - 2, S = Do * Ho * Wo;
+  const int S = Do * Ho * Wo;
   const int nl = m / S, s = m - nl * S;
   const int od = s / (Ho * Wo), r = s - od * Ho * Wo, oh = r / Wo, ow = r - oh * Wo;
-  const int d0 = od - pad, h0 = oh - pad, w0 = ow - pad;
+  const int d0 = od * st - padd, h0 = oh * st - pad, w0 = ow * st - pad;
   uint32_t mask = 0;
   mask = tap_mask3(d0, h0, w0, D, H, W);
   tab[m] = make_int2(((nl * D + d0) * H + h0) * W + w0, (int)mask);
@@ -1068,18 +1104,30 @@ __global__ __launch_bounds__(256, 2) void k_conv_wgrad_dma(ConvWgDmaArgs a) {
   }
 }
 
-void conv3d_pos_table(uintptr_t tab, int B, int D, int H, int W, int pad, uintptr_t stream) {
-  const int Mg = B * (D + 2 * pad - 2) * (H + 2 * pad - 2) * (W + 2 * pad - 2);
+// positions table of a general conv (kt taps, stride st, h/w padding pad, depth padding padd): Mg = B*Do*Ho*Wo rows
+void conv_pos_table_g(uintptr_t tab, int B, int D, int H, int W, int kt, int st, int pad, int padd, uintptr_t stream) {
+  const int kd = kt == 27 ? 3 : 1, khw = kt == 1 ? 1 : 3;
+  const int Do = conv_out_dim(D, kd, st, padd), Ho = conv_out_dim(H, khw, st, pad), Wo = conv_out_dim(W, khw, st, pad);
+  NIDT_REQUIRE(Do > 0 && Ho > 0 && Wo > 0, "conv_pos_table: empty output");
+  const int Mg = B * Do * Ho * Wo;
   NIDT_REQUIRE((int64_t)B * D * H * W < (1ll << 31), "conv3d_pos_table: volume too large for 32-bit offsets");
   hipLaunchKernelGGL(k_conv_pos_table, dim3(ceil_div(Mg, 256)), dim3(256), 0, as_stream(stream), ptr<int2>(tab), Mg,
-                     D, H, W, pad);
+                     D, H, W, Do, Ho, Wo, st, padd, pad);
   NIDT_CHECK(hipGetLastError());
 }
 
-void conv3d_wgrad(uintptr_t x, uintptr_t xs, uintptr_t xt, uintptr_t dy, uintptr_t part, uintptr_t grad, int64_t ldg,
-                  int64_t off, int G, int B, int D, int H, int W, int Cin, int Cout, int pad, int nsplit, float scale,
-                  uintptr_t ptab, uintptr_t stream) {
+void conv3d_pos_table(uintptr_t tab, int B, int D, int H, int W, int pad, uintptr_t stream) {
+  conv_pos_table_g(tab, B, D, H, W, 27, 1, pad, pad, stream);
+}
+
+static void conv_wgrad_impl(uintptr_t x, uintptr_t xs, uintptr_t xt, uintptr_t dy, uintptr_t part, uintptr_t grad,
+                            int64_t ldg, int64_t off, int G, int B, int D, int H, int W, int Cin, int Cout, int pad,
+                            int nsplit, float scale, uintptr_t ptab, uintptr_t stream, int kt, int st, int padd) {
   NIDT_REQUIRE(Cin % 64 == 0, "conv3d_wgrad: Cin must be a multiple of 64");
+  NIDT_REQUIRE(kt == 27 || kt == 9 || kt == 1, "conv_wgrad: taps 27, 9 or 1");
+  NIDT_REQUIRE((kt == 27 && st == 1 && padd == pad) || (ptab && !xs),
+               "conv_wgrad: 9/1-tap or strided convs need the LDS-DMA path (position table, no input transform)");
+  NIDT_REQUIRE(nsplit >= 1, "conv_wgrad: nsplit >= 1");
   NIDT_REQUIRE((ptab && !xs) ? Cin <= kMaxCin : Cin <= 192,
                "conv3d_wgrad: Cin <= 512 (LDS-DMA path with a position table), else <= 192");
   NIDT_REQUIRE(Cout % kWgCO == 0, "conv3d_wgrad: Cout must be a multiple of 64");
@@ -1087,9 +1135,13 @@ void conv3d_wgrad(uintptr_t x, uintptr_t xs, uintptr_t xt, uintptr_t dy, uintptr
   a.x = ptr<const uint16_t>(x); a.xs = ptr<const float>(xs); a.xt = ptr<const float>(xt);
   a.dy = ptr<const uint16_t>(dy); a.part = ptr<float>(part);
   a.B = B; a.D = D; a.H = H; a.W = W; a.Cin = Cin; a.Cout = Cout; a.pad = pad; a.G = G;
-  a.Do = D + 2 * pad - 2; a.Ho = H + 2 * pad - 2; a.Wo = W + 2 * pad - 2;
+  {
+    const int kd = kt == 27 ? 3 : 1, khw = kt == 1 ? 1 : 3;
+    a.Do = conv_out_dim(D, kd, st, padd); a.Ho = conv_out_dim(H, khw, st, pad); a.Wo = conv_out_dim(W, khw, st, pad);
+  }
+  NIDT_REQUIRE(a.Do > 0 && a.Ho > 0 && a.Wo > 0, "conv_wgrad: empty output");
   a.Mg = B * a.Do * a.Ho * a.Wo;
-  a.K = 27 * Cin;
+  a.K = kt * Cin;
   a.nsplit = nsplit;
   a.chunk = ((ceil_div(a.Mg, nsplit) + 31) / 32) * 32;
   hipStream_t s = as_stream(stream);
@@ -1111,10 +1163,27 @@ void conv3d_wgrad(uintptr_t x, uintptr_t xs, uintptr_t xt, uintptr_t dy, uintptr
     else hipLaunchKernelGGL((k_conv_wgrad<false>), grid, dim3(256), 0, s, a);
   }
   NIDT_CHECK(hipGetLastError());
-  hipLaunchKernelGGL(k_wgrad_reduce, dim3(Cout, G), dim3(256), 27 * (Cin + 1) * sizeof(float), s,
-                     ptr<const float>(part), nsplit, G, Cout, Cin,
+  hipLaunchKernelGGL(k_wgrad_reduce, dim3(Cout, G), dim3(256), kt * (Cin + 1) * sizeof(float), s,
+                     ptr<const float>(part), nsplit, G, Cout, Cin, kt,
                      ptr<float>(grad), ldg, off, scale);
   NIDT_CHECK(hipGetLastError());
+}
+
+void conv3d_wgrad(uintptr_t x, uintptr_t xs, uintptr_t xt, uintptr_t dy, uintptr_t part, uintptr_t grad, int64_t ldg,
+                  int64_t off, int G, int B, int D, int H, int W, int Cin, int Cout, int pad, int nsplit, float scale,
+                  uintptr_t ptab, uintptr_t stream) {
+  conv_wgrad_impl(x, xs, xt, dy, part, grad, ldg, off, G, B, D, H, W, Cin, Cout, pad, nsplit, scale, ptab, stream, 27, 1,
+                  pad);
+}
+
+// General wgrad (position table from conv_pos_table_g with the same geometry): grad rows get PyTorch-layout
+// [Cout][Cin][kt] fp32 at offset off (times scale).
+void conv_wgrad_g(uintptr_t x, uintptr_t dy, uintptr_t part, uintptr_t grad, int64_t ldg, int64_t off, int G, int B,
+                  int D, int H, int W, int Cin, int Cout, int kt, int st, int pad, int padd, int nsplit, float scale,
+                  uintptr_t ptab, uintptr_t stream) {
+  NIDT_REQUIRE(ptab != 0, "conv_wgrad_g: needs a position table");
+  conv_wgrad_impl(x, 0, 0, dy, part, grad, ldg, off, G, B, D, H, W, Cin, Cout, pad, nsplit, scale, ptab, stream, kt, st,
+                  padd);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1122,49 +1191,58 @@ void conv3d_wgrad(uintptr_t x, uintptr_t xs, uintptr_t xt, uintptr_t dy, uintptr
 // wp [G][Cout][27][Cin] bf16 (block per (co, g): coalesced read of the [Cin][27] row, LDS transpose) and, for dgrad,
 // wt [G][Cin][27][Cout] with the taps flipped (64x64 LDS-tiled transpose of wp per tap).
 __global__ __launch_bounds__(256) void k_pack_wp(const float* __restrict__ theta, int64_t ldt, int64_t off, int Cout,
-                                                 int Cin, float scale, uint16_t* __restrict__ wp) {
-  extern __shared__ float row[];  // [Cin][27], dynamic: sized to the layer (not the 512-channel maximum)
+                                                 int Cin, int kt, int cin_src, float scale, uint16_t* __restrict__ wp) {
+  extern __shared__ float row[];  // [Cin][kt], dynamic: sized to the layer (not the 512-channel maximum)
   const int co = blockIdx.x, g = blockIdx.y;
-  const int K = 27 * Cin;
-  const float* src = theta + (int64_t)g * ldt + off + (int64_t)co * K;
-  for (int e = threadIdx.x; e < K; e += 256) row[e] = src[e];
+  const int K = kt * Cin, Ks = kt * cin_src;  // source rows may carry fewer input channels (zero-padded here)
+  const float* src = theta + (int64_t)g * ldt + off + (int64_t)co * Ks;
+  for (int e = threadIdx.x; e < K; e += 256) row[e] = e < Ks ? src[e] : 0.f;
   __syncthreads();
   uint16_t* dst = wp + ((int64_t)g * Cout + co) * K;  // K even: 4-B aligned pairs
   for (int e = 2 * threadIdx.x; e < K; e += 2 * 256) {  // e, e+1 share the tap (Cin even)
     const int t = e / Cin, ci = e - t * Cin;
-    *reinterpret_cast<uint32_t*>(dst + e) = pack_bf16x2(row[ci * 27 + t] * scale, row[(ci + 1) * 27 + t] * scale);
+    *reinterpret_cast<uint32_t*>(dst + e) = pack_bf16x2(row[ci * kt + t] * scale, row[(ci + 1) * kt + t] * scale);
   }
 }
 
-__global__ __launch_bounds__(256) void k_pack_wt(const uint16_t* __restrict__ wp, int Cout, int Cin,
+__global__ __launch_bounds__(256) void k_pack_wt(const uint16_t* __restrict__ wp, int Cout, int Cin, int kt,
                                                  uint16_t* __restrict__ wt) {
   __shared__ uint16_t tile[64][66];
   const int ci0 = blockIdx.x * 64, co0 = blockIdx.y * 64;
-  const int g = blockIdx.z / 27, t = blockIdx.z - g * 27;
+  const int g = blockIdx.z / kt, t = blockIdx.z - g * kt;
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
   for (int r = ty; r < 64; r += 4) {  // r = co offset, tx = ci offset
     const int co = co0 + r, ci = ci0 + tx;
-    tile[r][tx] = (co < Cout && ci < Cin) ? wp[(((int64_t)g * Cout + co) * 27 + t) * Cin + ci] : 0;
+    tile[r][tx] = (co < Cout && ci < Cin) ? wp[(((int64_t)g * Cout + co) * kt + t) * Cin + ci] : 0;
   }
   __syncthreads();
   for (int r = ty; r < 64; r += 4) {  // r = ci offset, tx = co offset
     const int ci = ci0 + r, co = co0 + tx;
-    if (ci < Cin && co < Cout) wt[(((int64_t)g * Cin + ci) * 27 + (26 - t)) * Cout + co] = tile[tx][r];
+    if (ci < Cin && co < Cout) wt[(((int64_t)g * Cin + ci) * kt + (kt - 1 - t)) * Cout + co] = tile[tx][r];
+  }
+}
+
+// General pack: theta rows hold [Cout][cin_src][kt] fp32 (PyTorch layout); wp [G][Cout][kt][Cin] bf16 with input
+// channels cin_src..Cin-1 zero (channel-padded first layers), wt (dgrad, optional) [G][Cin][kt][Cout] tap-flipped.
+void pack_conv_wk(uintptr_t theta, int64_t ldt, int64_t off, int G, int Cout, int Cin, int kt, int cin_src,
+                  float scale, uintptr_t wp, uintptr_t wt, uintptr_t stream) {
+  NIDT_REQUIRE(Cin <= kMaxCin && Cin % 2 == 0, "pack_conv_w: Cin even, <= 512");
+  NIDT_REQUIRE(kt == 27 || kt == 9 || kt == 1, "pack_conv_w: taps 27, 9 or 1");
+  NIDT_REQUIRE(cin_src >= 1 && cin_src <= Cin, "pack_conv_w: 1 <= cin_src <= Cin");
+  hipStream_t s = as_stream(stream);
+  hipLaunchKernelGGL(k_pack_wp, dim3(Cout, G), dim3(256), kt * Cin * sizeof(float), s, ptr<const float>(theta), ldt,
+                     off, Cout, Cin, kt, cin_src, scale, ptr<uint16_t>(wp));
+  NIDT_CHECK(hipGetLastError());
+  if (wt) {
+    hipLaunchKernelGGL(k_pack_wt, dim3(ceil_div(Cin, 64), ceil_div(Cout, 64), G * kt), dim3(256), 0, s,
+                       ptr<const uint16_t>(wp), Cout, Cin, kt, ptr<uint16_t>(wt));
+    NIDT_CHECK(hipGetLastError());
   }
 }
 
 void pack_conv_w(uintptr_t theta, int64_t ldt, int64_t off, int G, int Cout, int Cin, float scale, uintptr_t wp,
                  uintptr_t wt, uintptr_t stream) {
-  NIDT_REQUIRE(Cin <= kMaxCin, "pack_conv_w: Cin <= 512");
-  hipStream_t s = as_stream(stream);
-  hipLaunchKernelGGL(k_pack_wp, dim3(Cout, G), dim3(256), 27 * Cin * sizeof(float), s, ptr<const float>(theta), ldt,
-                     off, Cout, Cin, scale, ptr<uint16_t>(wp));
-  NIDT_CHECK(hipGetLastError());
-  if (wt) {
-    hipLaunchKernelGGL(k_pack_wt, dim3(ceil_div(Cin, 64), ceil_div(Cout, 64), G * 27), dim3(256), 0, s,
-                       ptr<const uint16_t>(wp), Cout, Cin, ptr<uint16_t>(wt));
-    NIDT_CHECK(hipGetLastError());
-  }
+  pack_conv_wk(theta, ldt, off, G, Cout, Cin, 27, Cin, scale, wp, wt, stream);
 }
 
 // h = relu(y * s + t) in bf16 (materialises BN+ReLU once so the consuming conv and its wgrad read it plain)

@@ -1,0 +1,342 @@
+// GroupNorm(32) forward / backward for client-grouped channels-last activations [N = G*B][S][C] (bf16), the
+// normalisation of the reference's CIFAR ResNet-18-GN (fedml_api/model/cv/resnet.py:91-124: BatchNorm swapped for
+// GroupNorm(32, C), per-client affine).
+//
+// One block (512 threads) per sample.  The whole sample (S*C <= 65536 elements: 32x32x64 at layer 1) stays in
+// registers as packed bf16 (<= 16 x 16-B chunks per thread), so the activation is read from HBM once: statistics
+// (two-pass: mean, then sum of squared deviations), normalisation, affine, optional residual add and ReLU are
+// applied from registers.  Each thread owns one 8-channel chunk column (512 % (C/8) == 0), so per-channel partial
+// sums reduce through LDS in a fixed order (deterministic, no atomics, no library workspaces: hipGraph-safe).
+// The backward recomputes x-hat from the saved (mean, rstd), forms the per-channel sums A_c = sum dy and
+// B_c = sum dy * xhat (= the per-sample dbeta / dgamma partials), from them the group means of dy*gamma and
+// dy*gamma*xhat, and writes dt in bf16; k_gn_param_grads sums the per-sample partials of each client into its
+// gradient row.
+#include "common.h"
+
+namespace nidt {
+
+constexpr int kGnThreads = 512;
+constexpr int kGnGroups = 32;
+constexpr float kGnEps = 1e-5f;
+
+__device__ __forceinline__ void unpack8(const uint4 v, float* f) {
+  const uint32_t u[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    f[2 * j] = __uint_as_float(u[j] << 16);
+    f[2 * j + 1] = __uint_as_float(u[j] & 0xffff0000u);
+  }
+}
+
+// Per-channel sums of this thread's 8-channel partials -> per-group totals in grp[32] (valid after the call).
+// part: this thread's 8 values; sm: LDS [512][9] scratch; chs: LDS [512]; grp: LDS [32].
+__device__ __forceinline__ void gn_reduce_groups(const float* part, float* sm, float* chs, float* grp, int C,
+                                                 int nch) {
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) sm[tid * 9 + e] = part[e];
+  __syncthreads();
+  const int rows = kGnThreads / nch;
+  for (int c = tid; c < C; c += kGnThreads) {
+    const int j = c >> 3, e = c & 7;
+    float s = 0.f;
+    for (int r = 0; r < rows; ++r) s += sm[(r * nch + j) * 9 + e];
+    chs[c] = s;
+  }
+  __syncthreads();
+  if (tid < kGnGroups) {
+    const int cg = C / kGnGroups;
+    float s = 0.f;
+    for (int i = 0; i < cg; ++i) s += chs[tid * cg + i];
+    grp[tid] = s;
+  }
+  __syncthreads();
+}
+
+template <int NV, bool RES, bool RELU>
+__global__ __launch_bounds__(kGnThreads) void k_gn_fwd(const uint16_t* __restrict__ t, const uint16_t* __restrict__ res,
+                                                       const float* __restrict__ theta, int64_t ldt, int64_t off_w,
+                                                       int64_t off_b, uint16_t* __restrict__ y,
+                                                       float* __restrict__ stats, int B, int S, int C) {
+  __shared__ float sm[kGnThreads * 9];
+  __shared__ float chs[512];
+  __shared__ float grp[kGnGroups], gmean[kGnGroups], grstd[kGnGroups];
+  const int n = blockIdx.x, g = n / B, tid = threadIdx.x;
+  const int nch = C >> 3, nchunk = S * nch;
+  const int64_t base = (int64_t)n * S * C;
+  const int j = tid % nch;  // this thread's channel chunk (512 % nch == 0)
+  const int cg = C / kGnGroups;
+  uint4 v[NV];
+  float part[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) part[e] = 0.f;
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const int q = tid + k * kGnThreads;
+    v[k] = q < nchunk ? *reinterpret_cast<const uint4*>(t + base + (int64_t)q * 8) : make_uint4(0, 0, 0, 0);
+    float f[8];
+    unpack8(v[k], f);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) part[e] += f[e];
+  }
+  gn_reduce_groups(part, sm, chs, grp, C, nch);
+  if (tid < kGnGroups) gmean[tid] = grp[tid] / (float)(S * cg);
+  __syncthreads();
+  float mu[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    mu[e] = gmean[(8 * j + e) / cg];
+    part[e] = 0.f;
+  }
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const int q = tid + k * kGnThreads;
+    if (q < nchunk) {
+      float f[8];
+      unpack8(v[k], f);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float d = f[e] - mu[e];
+        part[e] = fmaf(d, d, part[e]);
+      }
+    }
+  }
+  gn_reduce_groups(part, sm, chs, grp, C, nch);
+  if (tid < kGnGroups) {
+    const float rs = rsqrtf(grp[tid] / (float)(S * cg) + kGnEps);
+    grstd[tid] = rs;
+    stats[((int64_t)n * kGnGroups + tid) * 2] = gmean[tid];
+    stats[((int64_t)n * kGnGroups + tid) * 2 + 1] = rs;
+  }
+  __syncthreads();
+  float sc[8], sh[8];
+  const float* gw = theta + (int64_t)g * ldt + off_w;
+  const float* gb = theta + (int64_t)g * ldt + off_b;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const int c = 8 * j + e;
+    const float rs = grstd[c / cg];
+    sc[e] = gw[c] * rs;
+    sh[e] = gb[c] - mu[e] * sc[e];
+  }
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const int q = tid + k * kGnThreads;
+    if (q < nchunk) {
+      float f[8], r[8];
+      unpack8(v[k], f);
+      if (RES) unpack8(*reinterpret_cast<const uint4*>(res + base + (int64_t)q * 8), r);
+      uint32_t o[4];
+#pragma unroll
+      for (int e = 0; e < 8; e += 2) {
+        float a0 = fmaf(f[e], sc[e], sh[e]), a1 = fmaf(f[e + 1], sc[e + 1], sh[e + 1]);
+        if (RES) {
+          a0 += r[e];
+          a1 += r[e + 1];
+        }
+        if (RELU) {
+          a0 = fmaxf(a0, 0.f);
+          a1 = fmaxf(a1, 0.f);
+        }
+        o[e >> 1] = pack_bf16x2(a0, a1);
+      }
+      *reinterpret_cast<uint4*>(y + base + (int64_t)q * 8) = make_uint4(o[0], o[1], o[2], o[3]);
+    }
+  }
+}
+
+// dy: fp32 (DYB = false) or bf16; mask (optional, bf16 post-ReLU activation): dy *= (mask > 0)
+template <int NV, bool DYB, bool MASK>
+__global__ __launch_bounds__(kGnThreads) void k_gn_bwd(const void* __restrict__ dyv, const uint16_t* __restrict__ mask,
+                                                       const uint16_t* __restrict__ t, const float* __restrict__ stats,
+                                                       const float* __restrict__ theta, int64_t ldt, int64_t off_w,
+                                                       uint16_t* __restrict__ dt, float* __restrict__ part_out, int B,
+                                                       int S, int C) {
+  __shared__ float sm[kGnThreads * 9];
+  __shared__ float chs[512];
+  __shared__ float grp[kGnGroups], gm1[kGnGroups], gm2[kGnGroups];
+  __shared__ float chA[512];
+  const int n = blockIdx.x, g = n / B, tid = threadIdx.x;
+  const int nch = C >> 3, nchunk = S * nch;
+  const int64_t base = (int64_t)n * S * C;
+  const int j = tid % nch;
+  const int cg = C / kGnGroups;
+  float mu[8], rs[8], gw[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const int c = 8 * j + e;
+    mu[e] = stats[((int64_t)n * kGnGroups + c / cg) * 2];
+    rs[e] = stats[((int64_t)n * kGnGroups + c / cg) * 2 + 1];
+    gw[e] = theta[(int64_t)g * ldt + off_w + c];
+  }
+  auto load_dy = [&](int q, float* d) {
+    if (DYB) {
+      unpack8(*reinterpret_cast<const uint4*>(reinterpret_cast<const uint16_t*>(dyv) + base + (int64_t)q * 8), d);
+    } else {
+      const float4* p = reinterpret_cast<const float4*>(reinterpret_cast<const float*>(dyv) + base + (int64_t)q * 8);
+      const float4 a = p[0], b = p[1];
+      d[0] = a.x; d[1] = a.y; d[2] = a.z; d[3] = a.w; d[4] = b.x; d[5] = b.y; d[6] = b.z; d[7] = b.w;
+    }
+    if (MASK) {
+      float m[8];
+      unpack8(*reinterpret_cast<const uint4*>(mask + base + (int64_t)q * 8), m);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) d[e] = m[e] > 0.f ? d[e] : 0.f;
+    }
+  };
+  uint4 v[NV];
+  float pa[8], pb[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) pa[e] = pb[e] = 0.f;
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const int q = tid + k * kGnThreads;
+    v[k] = make_uint4(0, 0, 0, 0);
+    if (q < nchunk) {
+      v[k] = *reinterpret_cast<const uint4*>(t + base + (int64_t)q * 8);
+      float f[8], d[8];
+      unpack8(v[k], f);
+      load_dy(q, d);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        pa[e] += d[e];
+        pb[e] = fmaf(d[e], (f[e] - mu[e]) * rs[e], pb[e]);
+      }
+    }
+  }
+  // per-channel A_c (= dbeta partial) and B_c (= dgamma partial); group sums of gamma-weighted values
+  gn_reduce_groups(pa, sm, chs, grp, C, nch);
+  for (int c = tid; c < C; c += kGnThreads) chA[c] = chs[c];
+  __syncthreads();
+  float pbw[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) pbw[e] = pb[e];
+  gn_reduce_groups(pbw, sm, chs, grp, C, nch);  // chs = B_c
+  for (int c = tid; c < C; c += kGnThreads) {
+    part_out[((int64_t)n * C + c) * 2] = chA[c];
+    part_out[((int64_t)n * C + c) * 2 + 1] = chs[c];
+  }
+  if (tid < kGnGroups) {
+    float s1 = 0.f, s2 = 0.f;
+    const float* gwr = theta + (int64_t)g * ldt + off_w;
+    for (int i = 0; i < cg; ++i) {
+      const int c = tid * cg + i;
+      s1 = fmaf(gwr[c], chA[c], s1);
+      s2 = fmaf(gwr[c], chs[c], s2);
+    }
+    gm1[tid] = s1 / (float)(S * cg);
+    gm2[tid] = s2 / (float)(S * cg);
+  }
+  __syncthreads();
+  float m1[8], m2[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    m1[e] = gm1[(8 * j + e) / cg];
+    m2[e] = gm2[(8 * j + e) / cg];
+  }
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const int q = tid + k * kGnThreads;
+    if (q < nchunk) {
+      float f[8], d[8];
+      unpack8(v[k], f);
+      load_dy(q, d);
+      uint32_t o[4];
+#pragma unroll
+      for (int e = 0; e < 8; e += 2) {
+        const float x0 = (f[e] - mu[e]) * rs[e], x1 = (f[e + 1] - mu[e + 1]) * rs[e + 1];
+        const float r0 = rs[e] * (d[e] * gw[e] - m1[e] - x0 * m2[e]);
+        const float r1 = rs[e + 1] * (d[e + 1] * gw[e + 1] - m1[e + 1] - x1 * m2[e + 1]);
+        o[e >> 1] = pack_bf16x2(r0, r1);
+      }
+      *reinterpret_cast<uint4*>(dt + base + (int64_t)q * 8) = make_uint4(o[0], o[1], o[2], o[3]);
+    }
+  }
+}
+
+// grads[g][off_w + c] = sum_b part[g*B + b][c][1] (dgamma), grads[g][off_b + c] = sum_b part[..][c][0] (dbeta)
+__global__ void k_gn_param_grads(const float* __restrict__ part, int B, int C, float* __restrict__ grads, int64_t ldg,
+                                 int64_t off_w, int64_t off_b) {
+  const int g = blockIdx.x;
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    float a = 0.f, b = 0.f;
+    for (int i = 0; i < B; ++i) {
+      const float* p = part + (((int64_t)g * B + i) * C + c) * 2;
+      a += p[0];
+      b += p[1];
+    }
+    grads[(int64_t)g * ldg + off_w + c] = b;
+    grads[(int64_t)g * ldg + off_b + c] = a;
+  }
+}
+
+static int gn_nv(int S, int C) {
+  const int chunks = S * C / 8;
+  const int nv = ceil_div(chunks, kGnThreads);
+  return nv <= 1 ? 1 : nv <= 2 ? 2 : nv <= 4 ? 4 : nv <= 8 ? 8 : 16;
+}
+
+static void gn_check(int N, int B, int S, int C, const char* who) {
+  NIDT_REQUIRE(N > 0 && B > 0 && N % B == 0, std::string(who) + ": N % B");
+  NIDT_REQUIRE(C % kGnGroups == 0 && C % 64 == 0 && C <= 512 && (kGnThreads % (C / 8)) == 0,
+               std::string(who) + ": C must be a multiple of 64, <= 512");
+  NIDT_REQUIRE((int64_t)S * C <= 16 * 8 * kGnThreads, std::string(who) + ": S*C <= 65536 (one sample per block)");
+}
+
+void gn_fwd(uintptr_t t, uintptr_t res, uintptr_t theta, int64_t ldt, int64_t off_w, int64_t off_b, uintptr_t y,
+            uintptr_t stats, int N, int B, int S, int C, int relu, uintptr_t stream) {
+  gn_check(N, B, S, C, "gn_fwd");
+  hipStream_t s = as_stream(stream);
+  const int nv = gn_nv(S, C);
+#define GNF(NVV, R, L)                                                                                         \
+  hipLaunchKernelGGL((k_gn_fwd<NVV, R, L>), dim3(N), dim3(kGnThreads), 0, s, ptr<const uint16_t>(t),            \
+                     ptr<const uint16_t>(res), ptr<const float>(theta), ldt, off_w, off_b, ptr<uint16_t>(y),     \
+                     ptr<float>(stats), B, S, C)
+#define GNF_RL(NVV)                                                                                            \
+  if (res) { if (relu) GNF(NVV, true, true); else GNF(NVV, true, false); }                                     \
+  else { if (relu) GNF(NVV, false, true); else GNF(NVV, false, false); }
+  switch (nv) {
+    case 1: GNF_RL(1) break;
+    case 2: GNF_RL(2) break;
+    case 4: GNF_RL(4) break;
+    case 8: GNF_RL(8) break;
+    default: GNF_RL(16) break;
+  }
+#undef GNF_RL
+#undef GNF
+  NIDT_CHECK(hipGetLastError());
+}
+
+void gn_bwd(uintptr_t dy, int dy_bf16, uintptr_t mask, uintptr_t t, uintptr_t stats, uintptr_t theta, int64_t ldt,
+            int64_t off_w, uintptr_t dt, uintptr_t part, int N, int B, int S, int C, uintptr_t stream) {
+  gn_check(N, B, S, C, "gn_bwd");
+  hipStream_t s = as_stream(stream);
+  const int nv = gn_nv(S, C);
+#define GNB(NVV, DB, M)                                                                                        \
+  hipLaunchKernelGGL((k_gn_bwd<NVV, DB, M>), dim3(N), dim3(kGnThreads), 0, s, ptr<const void>(dy),              \
+                     ptr<const uint16_t>(mask), ptr<const uint16_t>(t), ptr<const float>(stats),               \
+                     ptr<const float>(theta), ldt, off_w, ptr<uint16_t>(dt), ptr<float>(part), B, S, C)
+#define GNB_DM(NVV)                                                                                            \
+  if (dy_bf16) { if (mask) GNB(NVV, true, true); else GNB(NVV, true, false); }                                 \
+  else { if (mask) GNB(NVV, false, true); else GNB(NVV, false, false); }
+  switch (nv) {
+    case 1: GNB_DM(1) break;
+    case 2: GNB_DM(2) break;
+    case 4: GNB_DM(4) break;
+    case 8: GNB_DM(8) break;
+    default: GNB_DM(16) break;
+  }
+#undef GNB_DM
+#undef GNB
+  NIDT_CHECK(hipGetLastError());
+}
+
+void gn_param_grads(uintptr_t part, int G, int B, int C, uintptr_t grads, int64_t ldg, int64_t off_w, int64_t off_b,
+                    uintptr_t stream) {
+  NIDT_REQUIRE(C <= 512, "gn_param_grads: C <= 512");
+  hipLaunchKernelGGL(k_gn_param_grads, dim3(G), dim3(256), 0, as_stream(stream), ptr<const float>(part), B, C,
+                     ptr<float>(grads), ldg, off_w, off_b);
+  NIDT_CHECK(hipGetLastError());
+}
+
+}  // namespace nidt

@@ -277,7 +277,7 @@ class MaskSpace:
 def masked_rows_sum(rows, n, bits, sum_, cnt):
     """sum_[p] += sum_r rows[r, p]; cnt[p] += sum_r bit(r, p) (bits None: every row counts)."""
     R = rows.shape[0]
-    if R == 0:
+    if R == 0 or n == 0:  # n = 0: models without buffers (GroupNorm ResNets)
         return
     if _hip(rows):
         assert rows.stride(1) == 1 and rows.shape[1] >= n and sum_.numel() >= n and cnt.numel() >= n
@@ -296,7 +296,7 @@ def masked_rows_sum(rows, n, bits, sum_, cnt):
 def mix_rows(plan, n):
     """``plan``: list of ``(dst_row, [(src_row, weight), ...])`` 1-D fp32 tensors of length >= n; dst rows must not
     alias sources.  One launch for every output row."""
-    if not plan:
+    if not plan or n == 0:
         return
     dev = plan[0][0].device
     if _hip(plan[0][0]):
@@ -327,6 +327,8 @@ def pair_sqdist(pairs, n):
     if not pairs:
         return torch.zeros(0, dtype=torch.float64)
     dev = pairs[0][0].device
+    if n == 0:
+        return torch.zeros(len(pairs), dtype=torch.float64, device=dev)
     if _hip(pairs[0][0]):
         assert all(a.data_ptr() % 16 == 0 and b.data_ptr() % 16 == 0 for a, b in pairs), "pair_sqdist: alignment"
         m = ops.ext()

@@ -125,6 +125,7 @@ class FLRunner:
                               global_test_loss=[], person_test_loss=[], round_time=[])
         self.timers = {"train": 0.0, "aggregate": 0.0, "eval": 0.0, "snip": 0.0}
         self._graphs = {}             # step key -> captured local step (None until the shape repeats, False = eager)
+        self.max_graphs = 64
         self._lr_dev = self._seed_dev = None
         self._scratch = None
         self._eval_cache = None
@@ -302,6 +303,10 @@ class FLRunner:
         ent = self._graphs.get(key, "new")
         self._seed_dev.fill_(seed)
         if ent == "new":
+            # bounded cache: with client sampling (frac < 1) every round brings new client groups; the oldest
+            # captured graphs (and the memory pools they hold) are released first
+            while len(self._graphs) >= self.max_graphs:
+                self._graphs.pop(next(iter(self._graphs)))
             self._step(sub, r0, idx, G, B, spec, cids, 0.0)
             self._graphs[key] = None
             return
@@ -496,8 +501,9 @@ class FLRunner:
                 lo = rows[0]
                 m.weighted_rows_sum(theta[lo].data_ptr(), w.data_ptr(), len(rows), self.P, theta.stride(0), 0.0,
                                     buf.data_ptr(), st)
-                m.weighted_rows_sum(bufs[lo].data_ptr(), w.data_ptr(), len(rows), self.Q, bufs.stride(0), 0.0,
-                                    buf[Pp:].data_ptr(), st)
+                if self.Q:  # GroupNorm models carry no buffers
+                    m.weighted_rows_sum(bufs[lo].data_ptr(), w.data_ptr(), len(rows), self.Q, bufs.stride(0), 0.0,
+                                        buf[Pp:].data_ptr(), st)
             else:
                 ix = torch.tensor(rows, device=self.device)
                 buf[:self.P] = (w.view(-1, 1) * theta[ix]).sum(0)

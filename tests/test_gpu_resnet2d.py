@@ -1,0 +1,154 @@
+"""GPU tests of the client-batched ResNet-18-GN (CIFAR) path: the generalised conv kernels (9-tap 2-D 3x3 at stride
+1/2, 1x1 stride-2 projections, the channel-padded stem) against fp32 PyTorch convolutions, and the full lockstep
+train step against the engine's fp32 CPU twin (itself checked against per-client autograd in
+tests/test_cpu_resnet2d.py)."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def _dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch.device("cuda")
+
+
+def _rel(a, b):
+    return float((a.float() - b.float()).norm() / (b.float().norm() + 1e-12))
+
+
+CONVS = [  # (cin, cout, k, stride, pad, hw)
+    (64, 64, 3, 1, 1, 32),
+    (3, 64, 3, 1, 1, 32),
+    (64, 128, 3, 2, 1, 32),
+    (64, 128, 1, 2, 0, 32),
+    (128, 256, 3, 2, 1, 16),
+    (256, 256, 3, 1, 1, 8),
+    (256, 512, 1, 2, 0, 8),
+    (512, 512, 3, 1, 1, 4),
+]
+
+
+@pytest.mark.parametrize("cin,cout,k,stride,pad,hw", CONVS)
+def test_grouped_conv2d_fwd_dgrad_wgrad(cin, cout, k, stride, pad, hw):
+    from neuroimagedisttraining_amd.engine.resnet2d_hip import GroupedConv
+    dev = _dev()
+    torch.manual_seed(cin * 7 + cout + k + stride)
+    G, B = 3, 2
+    conv = GroupedConv(0, cout, cin, k, stride, pad, hip=True)
+    P = conv.numel
+    ld = (P + 63) // 64 * 64
+    theta = torch.zeros(G, ld, device=dev)[:, :P]
+    theta.copy_(torch.randn(G, P, device=dev) * (2.0 / (cin * k * k)) ** 0.5)
+    x = torch.zeros(G * B, hw, hw, conv.cin_p, device=dev, dtype=torch.bfloat16)
+    x[..., :cin] = torch.randn(G * B, hw, hw, cin, device=dev).to(torch.bfloat16)
+    y = conv.fwd(x, theta, G)
+    # fp32 reference on the same (bf16-rounded) operands
+    xr = x[..., :cin].float().permute(0, 3, 1, 2).requires_grad_(True)
+    wr = theta.view(G, cout, cin, k, k).to(torch.bfloat16).float().requires_grad_(True)
+    ref = torch.cat([F.conv2d(xr[g * B:(g + 1) * B], wr[g], stride=stride, padding=pad) for g in range(G)])
+    assert tuple(y.shape) == (G * B, ref.shape[2], ref.shape[3], cout)
+    assert _rel(y.permute(0, 3, 1, 2), ref) < 1e-2
+    dy = torch.randn_like(y.float()).to(torch.bfloat16)
+    ref.backward(dy.float().permute(0, 3, 1, 2))
+    grads = torch.zeros(G, ld, device=dev)[:, :P]
+    dx = conv.bwd(dy, x, theta, grads, G, need_dx=(cin % 64 == 0))
+    torch.cuda.synchronize()
+    assert _rel(grads.view(G, cout, cin, k, k), wr.grad) < 2e-2
+    if dx is not None:
+        assert tuple(dx.shape) == tuple(x.shape)
+        assert _rel(dx.permute(0, 3, 1, 2)[:, :cin], xr.grad) < 2e-2
+
+
+def test_resnet18gn_train_step_matches_cpu_twin():
+    from neuroimagedisttraining_amd.engine.executor import padded_rows
+    from neuroimagedisttraining_amd.engine.resnet2d_hip import ResNetHipEngine, synthetic_cifar
+    from neuroimagedisttraining_amd.models import customized_resnet18
+    dev = _dev()
+    torch.manual_seed(0)
+    G, B = 4, 8
+    x8, y = synthetic_cifar(G * B, seed=3)
+    m = customized_resnet18(class_num=10)
+    hip = ResNetHipEngine(m, x8, y, dev)
+    cpu = ResNetHipEngine(m, x8, y, "cpu")
+    P = hip.players.total
+    th = torch.cat([torch.cat([p.detach().reshape(-1) for p in customized_resnet18(class_num=10).parameters()])[None]
+                    for _ in range(G)])
+    th_d, gr_d = padded_rows(G, P, dev), padded_rows(G, P, dev)
+    th_c, gr_c = padded_rows(G, P, "cpu"), padded_rows(G, P, "cpu")
+    th_d.copy_(th)
+    th_c.copy_(th)
+    idx = torch.arange(G * B, dtype=torch.int32)
+    ld = hip.train_step(th_d, None, gr_d, idx.to(dev), G, B, 1.0, 0)
+    lc = cpu.train_step(th_c, None, gr_c, idx, G, B, 1.0, 0)
+    torch.cuda.synchronize()
+    assert torch.allclose(ld.cpu(), lc, atol=3e-2), (ld, lc)
+    for g in range(G):
+        a, b = gr_d[g].cpu(), gr_c[g]
+        cos = float(a @ b / (a.norm() * b.norm()))
+        assert cos > 0.98, (g, cos)
+    lg = hip.eval_logits(th_d, None, idx.to(dev), G, B)
+    assert lg.shape == (G * B, 10) and torch.isfinite(lg).all()
+
+
+def test_resnet18gn_hip_runners_graphs_match_eager():
+    """SubAvg and DisPFL on the ResNet engine: hipGraph-replayed local steps == eager, bit for bit."""
+    from neuroimagedisttraining_amd.engine.executor import ClientSplit, FLConfig
+    from neuroimagedisttraining_amd.engine.personalized import make_runner
+    from neuroimagedisttraining_amd.engine.resnet2d_hip import ResNetHipEngine, synthetic_cifar
+    from neuroimagedisttraining_amd.models import customized_resnet18
+    from neuroimagedisttraining_amd.parallel import runtime as rt
+    dev = _dev()
+    info = rt.init_distributed(prefer_gpu=True)
+    C, ntr, nte = 4, 20, 8
+    x8, y = synthetic_cifar(C * (ntr + nte), seed=5)
+    splits = [ClientSplit(train=np.arange(c * (ntr + nte), c * (ntr + nte) + ntr - 3 * c),
+                          test=np.arange(c * (ntr + nte) + ntr, (c + 1) * (ntr + nte))) for c in range(C)]
+    for alg in ("subavg", "dispfl"):
+        outs = []
+        for graphs in (False, True):
+            torch.manual_seed(0)
+            m = customized_resnet18(class_num=10)
+            eng = ResNetHipEngine(m, x8, y, dev)
+            cfg = FLConfig(comm_round=2, epochs=2, batch_size=8, dense_ratio=0.3, seed=1, frac=0.5, lr=0.05,
+                           frequency_of_the_test=1, final_round=False, hip_graphs=graphs)
+            r = make_runner(alg, eng, splits, cfg, info, m)
+            for k in range(2):
+                r.run_round(k)
+            torch.cuda.synchronize()
+            outs.append(r.theta.clone())
+        assert torch.isfinite(outs[0]).all()
+        assert torch.equal(outs[0], outs[1]), alg
+
+
+@pytest.mark.parametrize("hw,C", [(32, 64), (16, 128), (8, 256), (4, 512)])
+@pytest.mark.parametrize("res,dy_bf16", [(False, True), (True, False)])
+def test_groupnorm_kernels_match_torch(hw, C, res, dy_bf16):
+    """gn.hip forward (affine + residual + ReLU) and backward (ReLU mask, dgamma/dbeta rows) vs the fp32 CPU
+    twin on the same bf16 inputs."""
+    from neuroimagedisttraining_amd.engine.resnet2d_hip import GroupNormG
+    dev = _dev()
+    torch.manual_seed(hw + C)
+    G, B = 3, 2
+    N = G * B
+    theta = torch.zeros(G, 2 * C + 64, device=dev)
+    theta[:, :C] = torch.randn(G, C, device=dev)           # signed gammas
+    theta[:, C:2 * C] = torch.randn(G, C, device=dev)
+    t = (torch.randn(N, hw, hw, C, device=dev) * 3 + 1).to(torch.bfloat16)
+    r = torch.randn(N, hw, hw, C, device=dev).to(torch.bfloat16) if res else None
+    hipgn, cpugn = GroupNormG(0, C, C, hip=True), GroupNormG(0, C, C, hip=False)
+    y, st = hipgn.fwd(t, theta, G, res=r, relu=True)
+    yc, stc = cpugn.fwd(t.cpu(), theta.cpu(), G, res=r.cpu() if res else None, relu=True)
+    assert _rel(y.cpu(), yc) < 1e-2
+    dy = torch.randn(N, hw, hw, C, device=dev)
+    dy = dy.to(torch.bfloat16) if dy_bf16 else dy
+    gh = torch.zeros_like(theta)
+    gc = torch.zeros_like(theta.cpu())
+    dt = hipgn.bwd(dy, y, t, st, theta, gh, G)
+    dtc = cpugn.bwd(dy.cpu(), yc, t.cpu(), stc, theta.cpu(), gc, G)
+    torch.cuda.synchronize()
+    assert _rel(dt.cpu(), dtc) < 2e-2
+    assert _rel(gh.cpu()[:, :2 * C], gc[:, :2 * C]) < 1e-3

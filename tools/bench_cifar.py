@@ -1,0 +1,120 @@
+"""Rounds/s of the reference's only timed configs: ResNet-18-GN on CIFAR-10, 100 clients, on the client-batched
+HIP engine (engine/resnet2d_hip.py: hand-written grouped conv kernels, lockstep clients, hipGraph steps).
+
+Reference jobs (1x V100): SubAvg ``subavg/subavgsparsitywithoutiteration70sps.sh`` (finished 500 rounds inside
+72 h -> >= 0.0019 rounds/s, ``subavg/error3437295.err``) and DisPFL ``DisPFL/dispflsparsitywithoutiteration70sps.sh``
+(did not finish 500 rounds in the 2-3 day limit -> < 0.0029 rounds/s, ``DisPFL/error3469448.err``): resnet18,
+cifar10, dir 0.3, batch 16, lr 0.1, lr_decay 0.998, 5 local epochs, dense_ratio 0.3, 100 clients, frac 0.1.
+
+Data: CIFAR-10-shape synthetic uint8 images (50,000 train / 10,000 test, weak class signal), partitioned with the
+reference's ``dir`` partitioner (alpha 0.3: 500 train images per client, label-skewed) and per-client test sets
+drawn from the train label histogram; random-init weights.  No augmentation (the reference's RandomCrop/Flip run
+in its CPU DataLoader).  Usage: ``python tools/bench_cifar.py --algorithm subavg --rounds 3 --warmup 1``.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+V100_BOUNDS = {"subavg": (">=", 0.0019, "subavg/error3437295.err:2-12"),
+               "dispfl": ("<", 0.0029, "DisPFL/error3469448.err:3")}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--algorithm", default="subavg")
+    ap.add_argument("--clients", type=int, default=100)
+    ap.add_argument("--frac", type=float, default=0.1)
+    ap.add_argument("--epochs", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=16)
+    ap.add_argument("--lr", type=float, default=0.1)
+    ap.add_argument("--dense-ratio", type=float, default=0.3)
+    ap.add_argument("--n-train", type=int, default=50000)
+    ap.add_argument("--n-test", type=int, default=10000)
+    ap.add_argument("--rounds", type=int, default=2)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--seed", type=int, default=2022)
+    ap.add_argument("--no-eval", action="store_true")
+    args = ap.parse_args()
+
+    from neuroimagedisttraining_amd.core import partition as Pt
+    from neuroimagedisttraining_amd.engine.executor import ClientSplit, FLConfig
+    from neuroimagedisttraining_amd.engine.personalized import make_runner
+    from neuroimagedisttraining_amd.engine.resnet2d_hip import ResNetHipEngine, synthetic_cifar
+    from neuroimagedisttraining_amd.models import customized_resnet18
+    from neuroimagedisttraining_amd.parallel import runtime as rt
+
+    info = rt.init_distributed(prefer_gpu=True)
+    torch.manual_seed(args.seed)
+    t0 = time.perf_counter()
+    x8, y = synthetic_cifar(args.n_train + args.n_test, seed=args.seed)
+    ytr, yte = y[:args.n_train].numpy(), y[args.n_train:].numpy()
+    rng = np.random.RandomState(args.seed)
+    train_map = Pt.partition_labels("dir", ytr, args.clients, 0.3, n_cls=10, rng=rng)
+    test_map = Pt.per_client_test_indices(ytr, yte, train_map, n_cls=10, rng=rng)
+    splits = []
+    for c in range(args.clients):
+        tr = np.asarray(train_map[c], dtype=np.int64)
+        te = np.asarray(test_map[c], dtype=np.int64) + args.n_train
+        if args.algorithm == "fedfomo":  # 10 % validation split (data_val_loader.py)
+            nv = int(0.1 * len(tr))
+            splits.append(ClientSplit(train=tr[nv:], test=te, val=tr[:nv]))
+        else:
+            splits.append(ClientSplit(train=tr, test=te))
+    model = customized_resnet18(class_num=10)
+    engine = ResNetHipEngine(model, x8, y, info.device)
+    cfg = FLConfig(comm_round=args.warmup + args.rounds, epochs=args.epochs, batch_size=args.batch, lr=args.lr,
+                   lr_decay=0.998, dense_ratio=args.dense_ratio, seed=args.seed, frac=args.frac,
+                   frequency_of_the_test=0 if args.no_eval else 1, final_round=False)
+    runner = make_runner(args.algorithm, engine, splits, cfg, info, model, logger=None)
+    torch.cuda.synchronize()
+    t_setup = time.perf_counter() - t0
+    if runner.alg == "salientgrads":
+        runner.generate_global_mask_snip()
+    walls = []
+    for r in range(args.warmup):
+        t1 = time.perf_counter()
+        runner.run_round(r)
+        torch.cuda.synchronize()
+        walls.append(time.perf_counter() - t1)
+        print("warmup round %d: %.2f s" % (r, walls[-1]), flush=True)
+    rt.barrier(info)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    res = None
+    for r in range(args.warmup, args.warmup + args.rounds):
+        t1 = time.perf_counter()
+        res = runner.run_round(r)
+        torch.cuda.synchronize()
+        print("round %d: %.2f s" % (r, time.perf_counter() - t1), flush=True)
+    rt.barrier(info)
+    torch.cuda.synchronize()
+    dt = rt.max_over_ranks(time.perf_counter() - t0, info)
+    value = args.rounds / dt
+    bound = V100_BOUNDS.get(args.algorithm)
+    if info.is_main:
+        print(json.dumps({
+            "metric": "FL rounds/sec, %d-client %s ResNet-18-GN on CIFAR-10-shape synth" % (args.clients,
+                                                                                             args.algorithm),
+            "value": round(value, 4), "unit": "rounds/s", "n_gpus": info.world, "rounds": args.rounds,
+            "warmup": args.warmup, "s_per_round": round(dt / args.rounds, 3), "dtype": "bf16",
+            "data": "synthetic", "setup_s": round(t_setup, 1), "warmup_round_s": [round(w, 2) for w in walls],
+            "reference_v100": ({"bound": bound[0] + str(bound[1]), "source": bound[2],
+                                "vs_bound": round(value / bound[1], 1)} if bound else None),
+            "config": {"model": "resnet18 (GroupNorm32)", "clients": args.clients, "frac": args.frac,
+                       "epochs": args.epochs, "batch": args.batch, "lr": args.lr, "dense_ratio": args.dense_ratio,
+                       "partition": "dir 0.3", "train_images": args.n_train, "eval_every_round": not args.no_eval},
+            "last_round_metrics": res}), flush=True)
+    rt.shutdown(info)
+
+
+if __name__ == "__main__":
+    main()
