@@ -51,6 +51,7 @@ void gn_bwd(uintptr_t dy, int dy_bf16, uintptr_t mask, uintptr_t t, uintptr_t st
             int64_t off_w, uintptr_t dt, uintptr_t part, int N, int B, int S, int C, uintptr_t stream);
 void gn_param_grads(uintptr_t part, int G, int B, int C, uintptr_t grads, int64_t ldg, int64_t off_w, int64_t off_b,
                     uintptr_t stream);
+void res_grad(uintptr_t out, uintptr_t dx1, uintptr_t dx2, uintptr_t da, uintptr_t mask, int64_t n, uintptr_t stream);
 // bn.hip
 void bn_finalize(uintptr_t stats, int nPB, int BP, int Mg, int G, int C, uintptr_t theta, int64_t ldt, int64_t off_g,
                  int64_t off_b, uintptr_t bufs, int64_t ldb, int64_t off_rm, int64_t off_rv, int64_t off_nbt,
@@ -135,6 +136,7 @@ PYBIND11_MODULE(_nidt_hip, m) {
   DEF(gn_fwd);
   DEF(gn_bwd);
   DEF(gn_param_grads);
+  DEF(res_grad);
   DEF(bn_finalize);
   DEF(bn_eval);
   DEF(bn_relu_pool);

@@ -270,6 +270,39 @@ __global__ void k_gn_param_grads(const float* __restrict__ part, int B, int C, f
   }
 }
 
+// Residual-stream gradient of a basic block: out = dx1 + (dx2 if given, else da * (mask > 0)); dx1/dx2 bf16 (the two
+// convolutions' data gradients), da fp32 (the block output gradient), mask bf16 (the block's post-ReLU output).
+// One pass instead of the four elementwise torch ops (two up-casts, a compare-multiply, an add).
+__global__ void k_res_grad(float* __restrict__ out, const uint16_t* __restrict__ dx1, const uint16_t* __restrict__ dx2,
+                           const float* __restrict__ da, const uint16_t* __restrict__ mask, int64_t n8) {
+  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n8; q += (int64_t)gridDim.x * blockDim.x) {
+    float a[8], b[8];
+    unpack8(*reinterpret_cast<const uint4*>(dx1 + q * 8), a);
+    if (dx2) {
+      unpack8(*reinterpret_cast<const uint4*>(dx2 + q * 8), b);
+    } else {
+      float m[8];
+      unpack8(*reinterpret_cast<const uint4*>(mask + q * 8), m);
+      const float4 d0 = *reinterpret_cast<const float4*>(da + q * 8), d1 = *reinterpret_cast<const float4*>(da + q * 8 + 4);
+      const float d[8] = {d0.x, d0.y, d0.z, d0.w, d1.x, d1.y, d1.z, d1.w};
+#pragma unroll
+      for (int e = 0; e < 8; ++e) b[e] = m[e] > 0.f ? d[e] : 0.f;
+    }
+    float4* o = reinterpret_cast<float4*>(out + q * 8);
+    o[0] = make_float4(a[0] + b[0], a[1] + b[1], a[2] + b[2], a[3] + b[3]);
+    o[1] = make_float4(a[4] + b[4], a[5] + b[5], a[6] + b[6], a[7] + b[7]);
+  }
+}
+
+void res_grad(uintptr_t out, uintptr_t dx1, uintptr_t dx2, uintptr_t da, uintptr_t mask, int64_t n, uintptr_t stream) {
+  NIDT_REQUIRE(n % 8 == 0 && (dx2 || (da && mask)), "res_grad: n % 8 == 0 and (dx2 or da+mask)");
+  const int64_t n8 = n / 8;
+  hipLaunchKernelGGL(k_res_grad, dim3((unsigned)std::min<int64_t>(8192, (n8 + 255) / 256)), dim3(256), 0,
+                     as_stream(stream), ptr<float>(out), ptr<const uint16_t>(dx1), ptr<const uint16_t>(dx2),
+                     ptr<const float>(da), ptr<const uint16_t>(mask), n8);
+  NIDT_CHECK(hipGetLastError());
+}
+
 static int gn_nv(int S, int C) {
   const int chunks = S * C / 8;
   const int nv = ceil_div(chunks, kGnThreads);

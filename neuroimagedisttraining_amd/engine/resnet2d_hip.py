@@ -48,6 +48,8 @@ class GroupedConv:
         self.cin_p = cin if cin % 64 == 0 else (cin + 63) // 64 * 64
         self.hip = hip
         self.numel = cout * cin * k * k
+        self.need_dgrad = self.cin_p == self.cin  # the (channel-padded) stem needs no input gradient
+        self._packed = None
 
     def out_hw(self, h, w):
         return ((h + 2 * self.pad - self.k) // self.stride + 1, (w + 2 * self.pad - self.k) // self.stride + 1)
@@ -66,13 +68,16 @@ class GroupedConv:
         return theta[:, self.off:self.off + self.numel].reshape(G * self.cout, self.cin, self.k, self.k)
 
     # ---------------------------------------------------------------- forward
-    def fwd(self, x, theta, G):
+    def fwd(self, x, theta, G, train=False):
+        """``train``: also pack the transposed (dgrad) weights now and keep both for :meth:`bwd` of this step
+        (one packing pass per conv per step instead of re-packing in the backward)."""
         N, H, W, C = x.shape
         assert C == self.cin_p and N % G == 0, (x.shape, self.cin_p, G)
         Ho, Wo = self.out_hw(H, W)
         if not self.hip:
             return self._torch_fwd(x, self._wtorch(theta, G), G)
-        wp, _ = self._wp(theta, G, False)
+        wp, wt = self._wp(theta, G, train and self.need_dgrad)
+        self._packed = (theta.data_ptr(), G, wt) if train else None
         y = torch.empty(N, Ho, Wo, self.cout, device=x.device, dtype=torch.bfloat16)
         ops.ext().conv_fwd_g(x.data_ptr(), wp.data_ptr(), y.data_ptr(), G, N // G, 1, H, W, self.cin_p, self.cout,
                              self.kt, self.stride, self.pad, 0, _stream())
@@ -112,7 +117,11 @@ class GroupedConv:
                 full.view(G, self.cout, self.cin_p, self.kt)[:, :, :self.cin])
         if not need_dx:
             return None
-        _, wt = self._wp(theta, G, True)
+        pk, self._packed = self._packed, None
+        if pk is not None and pk[0] == theta.data_ptr() and pk[1] == G and pk[2] is not None:
+            wt = pk[2]
+        else:
+            _, wt = self._wp(theta, G, True)
         dx = torch.empty(N, H, W, self.cin_p, device=x.device, dtype=torch.bfloat16)
         if self.stride == 1:
             m.conv_fwd_g(dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), G, B, 1, Ho, Wo, self.cout, self.cin_p, self.kt,
@@ -261,18 +270,18 @@ class GroupedResNet18GN:
         return x.to(self.act).contiguous()
 
     # ------------------------------------------------------------------ forward
-    def forward(self, x, theta, G, keep=False):
+    def forward(self, x, theta, G, train=False):
         saved = []
-        t = self.stem.fwd(x, theta, G)
+        t = self.stem.fwd(x, theta, G, train)
         a, st = self.stem_gn.fwd(t, theta, G, relu=True)
         saved.append((x, t, st, a))
         for blk in self.blocks:
             xin = a
-            t1 = blk["c1"].fwd(xin, theta, G)
+            t1 = blk["c1"].fwd(xin, theta, G, train)
             h1, s1 = blk["n1"].fwd(t1, theta, G, relu=True)
-            t2 = blk["c2"].fwd(h1, theta, G)
+            t2 = blk["c2"].fwd(h1, theta, G, train)
             if "cs" in blk:
-                ts = blk["cs"].fwd(xin, theta, G)
+                ts = blk["cs"].fwd(xin, theta, G, train)
                 ysc, ss = blk["ns"].fwd(ts, theta, G)
             else:
                 ts, ss, ysc = None, None, xin
@@ -290,7 +299,7 @@ class GroupedResNet18GN:
 
     # ------------------------------------------------------------------ train step
     def train_step(self, theta, grads, x, y, G, B):
-        logits, pooled, saved = self.forward(x, theta, G)
+        logits, pooled, saved = self.forward(x, theta, G, train=True)
         lg = logits.view(G, B, self.ncls)
         logp = torch.log_softmax(lg, dim=-1)
         yl = y.long().view(G, B)
@@ -310,13 +319,19 @@ class GroupedResNet18GN:
             dt2 = blk["n2"].bwd(da, a, t2, s2, theta, grads, G)
             dh1 = blk["c2"].bwd(dt2, h1, theta, grads, G, True)
             dt1 = blk["n1"].bwd(dh1, h1, t1, s1, theta, grads, G)
-            dx = blk["c1"].bwd(dt1, xin, theta, grads, G, True).float()
+            dx1 = blk["c1"].bwd(dt1, xin, theta, grads, G, True)
+            dx2 = None
             if "cs" in blk:
                 dts = blk["ns"].bwd(da, a, ts, ss, theta, grads, G)
-                dx = dx + blk["cs"].bwd(dts, xin, theta, grads, G, True).float()
+                dx2 = blk["cs"].bwd(dts, xin, theta, grads, G, True)
+            if self.hip:
+                out = torch.empty(dx1.shape, device=dx1.device, dtype=torch.float32)
+                ops.ext().res_grad(out.data_ptr(), dx1.data_ptr(), dx2.data_ptr() if dx2 is not None else 0,
+                                   0 if dx2 is not None else da.data_ptr(), 0 if dx2 is not None else a.data_ptr(),
+                                   out.numel(), _stream())
+                da = out
             else:
-                dx = dx + da * (a > 0)
-            da = dx
+                da = dx1.float() + (dx2.float() if dx2 is not None else da * (a > 0))
         x0, t0, st0, a0 = saved[0]
         dt0 = self.stem_gn.bwd(da, a0, t0, st0, theta, grads, G)
         self.stem.bwd(dt0, x0, theta, grads, G, False)
