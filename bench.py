@@ -60,6 +60,9 @@ def parse():
     ap.add_argument("--prox-mu", type=float, default=0.01)
     ap.add_argument("--cs", default="ring", help="D-PSGD topology")
     ap.add_argument("--phase-timers", action="store_true", help="synchronised per-phase timers (adds syncs)")
+    ap.add_argument("--rebalance", type=int, default=-1,
+                    help="1: replicate the cohort on every rank and move sampled clients to even the per-round load "
+                         "(default: on when frac < 1 on several ranks)")
     return ap.parse_args()
 
 
@@ -80,7 +83,9 @@ def main():
     n_test = [max(1, int(round(t * args.test_per_client / per))) for t in tot]
     n_train = [t - e for t, e in zip(tot, n_test)]
     shards = rt.shard_clients(n_train, info.world)
-    local = shards[info.rank]
+    rebalance = (args.frac < 1.0 and info.world > 1) if args.rebalance < 0 else bool(args.rebalance)
+    # rebalancing lets any rank train any client: every rank holds the whole (synthetic) cohort (~24 GB of HBM)
+    local = list(range(args.clients)) if rebalance else shards[info.rank]
     t0 = time.perf_counter()
     vol, labels, splits_local = build_fl_volumes(local, args.clients, n_train, n_test, info.device, seed=args.seed)
     x8, mom = to_hip_store(vol)
@@ -101,7 +106,8 @@ def main():
     cfg = FLConfig(comm_round=args.warmup + args.steps, epochs=args.epochs, batch_size=args.batch,
                    dense_ratio=args.dense_ratio, seed=args.seed, group=args.group, frac=args.frac,
                    frequency_of_the_test=0 if args.no_eval else 1, aggregator=args.aggregator,
-                   prox_mu=args.prox_mu if args.algorithm == "fedprox" else 0.0, cs=args.cs, final_round=False)
+                   prox_mu=args.prox_mu if args.algorithm == "fedprox" else 0.0, cs=args.cs, final_round=False,
+                   rebalance=rebalance)
     runner = make_runner(args.algorithm, engine, splits, cfg, info, model, logger=None)
     t0 = time.perf_counter()
     if runner.alg == "salientgrads":
@@ -157,6 +163,7 @@ def main():
                        "train_per_client": args.train_per_client, "test_per_client": args.test_per_client,
                        "size_skew": args.size_skew, "samples_train_total": int(sum(n_train)),
                        "dense_ratio": args.dense_ratio, "eval_every_round": not args.no_eval,
+                       "rebalance": rebalance,
                        "parallelism": "clients-sharded-dp%d" % info.world},
             "setup_s": {"data": round(t_data, 2), "snip_mask": round(t_snip, 2)},
             "rank_busy_s": per_rank,

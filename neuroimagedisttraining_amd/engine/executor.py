@@ -93,6 +93,9 @@ class FLConfig:
     each_prune_ratio: float = 0.05    # SubAvg fake_prune percentile
     dist_thresh: float = 1e-4         # SubAvg: prune only if the mask moved more than this
     acc_thresh: float = 0.5           # SubAvg: and the pruned model's local training accuracy exceeds this
+    rebalance: bool = False       # multi-rank, frac < 1: before each round move the sampled clients' state (rows, masks)
+                                  # so every rank trains about the same number of samples; needs every rank to hold
+                                  # every client's data (replicated cohort: it fits in 288 GB of HBM)
     heartbeat_s: float = 0.0      # >0: ranks publish heartbeats every heartbeat_s through the process group's store and
                                   # each round fails fast (comm.failure.PeerFailure) if a peer is silent for 30x that
 

@@ -61,6 +61,14 @@ class PersonalizedRunner(FLRunner):
         self.rowset = RowSet(self.theta, self.bufs)
 
     # ---------------------------------------------------------------------------------------------- helpers
+    def _row_state(self):
+        out = super()._row_state()
+        for name in ("mbits", "shared_bits"):
+            t = getattr(self, name, None)
+            if t is not None:
+                out.append((name, t))
+        return out
+
     def all_rows(self):
         return list(range(self.C)), list(self.local)
 
@@ -169,6 +177,7 @@ class LocalRunner(PersonalizedRunner):
         t0 = time.perf_counter()
         self._round_start(round_idx)
         sampled = self.sample_clients(round_idx)
+        self.rebalance(sampled)
         rows, loc = self._local_rows(sampled)
         self.train_rows(self.rowset, rows, loc, round_idx, self.cfg.epochs)
         t1 = time.perf_counter()
@@ -194,10 +203,14 @@ class DittoRunner(PersonalizedRunner):
         self.pers.bufs.copy_(self.b_global.expand_as(self.pers.bufs))
         self._pull_ref = torch.zeros_like(self.w_global)
 
+    def _row_state(self):
+        return super()._row_state() + [("pers.theta", self.pers.theta), ("pers.bufs", self.pers.bufs)]
+
     def run_round(self, round_idx, sync_timers=False):
         t0 = time.perf_counter()
         self._round_start(round_idx)
         sampled = self.sample_clients(round_idx)
+        self.rebalance(sampled)
         self._pull_ref.copy_(self.w_global)  # the round's global model (deepcopy(w_global) in the reference)
         self.local_train(round_idx, sampled)  # global-model training from w_global
         rows, loc = self._local_rows(sampled)
@@ -542,6 +555,7 @@ class SubAvgRunner(PersonalizedRunner):
         t0 = time.perf_counter()
         self._round_start(round_idx)
         sampled = self.sample_clients(round_idx)
+        self.rebalance(sampled)
         rows, loc = self._local_rows(sampled)
         hooks = {}
         if rows:

@@ -413,6 +413,93 @@ class FLRunner:
         np.random.seed(round_idx)
         return sorted(np.random.choice(range(self.N), per_round, replace=False).tolist())
 
+    # ---------------------------------------------------------------------------------------------- rebalancing
+    def _row_state(self):
+        """Per-client device state that moves with a client: (attribute path, tensor [rows, width]).  Subclasses
+        add theirs (mask bits, personal models)."""
+        return [("theta", self.theta), ("bufs", self.bufs)]
+
+    def balanced_owner(self, sampled):
+        """Owner map for this round: start from the current owners and move sampled clients from the most to the
+        least loaded rank (load = training samples of its sampled clients) while that lowers the larger of the two
+        loads; the move picked is the one leaving the pair most even (ties: lowest client id).  Identical on every
+        rank (pure function of the sizes, the sample and the current owners)."""
+        own = self.owner.copy()
+        load = np.zeros(self.info.world, dtype=np.int64)
+        for c in sampled:
+            load[own[c]] += self.sizes[c]
+        for _ in range(len(sampled)):
+            hi, lo = int(np.argmax(load)), int(np.argmin(load))
+            if hi == lo:
+                break
+            best = None
+            for c in sorted(c for c in sampled if own[c] == hi):
+                peak = max(load[hi] - self.sizes[c], load[lo] + self.sizes[c])
+                if peak < load[hi] and (best is None or peak < best[0]):
+                    best = (peak, c)
+            if best is None:
+                break
+            c = best[1]
+            own[c] = lo
+            load[hi] -= self.sizes[c]
+            load[lo] += self.sizes[c]
+        return own
+
+    def rebalance(self, sampled):
+        """Sampling-aware load balance (``cfg.rebalance``, multi-rank): migrate the state of sampled clients to the
+        ranks :meth:`balanced_owner` picks — rows go point to point (RCCL send/recv), ownership moves with them and
+        stays there until a later round moves it again.  Results do not depend on where a client trains."""
+        if not (self.cfg.rebalance and self.info.enabled and self.info.world > 1):
+            return
+        self.migrate(self.balanced_owner(sampled))
+
+    def migrate(self, new_owner):
+        new_owner = np.asarray(new_owner, dtype=np.int64)
+        moving = [c for c in range(self.N) if new_owner[c] != self.owner[c]]
+        if not moving:
+            return
+        me = self.info.rank
+        needs = [[c for c in moving if new_owner[c] == r] for r in range(self.info.world)]
+        new_local = sorted((c for c in range(self.N) if new_owner[c] == me), key=lambda c: (-int(self.sizes[c]), c))
+        n = max(1, len(new_local))
+        new_state = {}
+        for path, t in self._row_state():
+            width = t.shape[1]
+            recv = rt.exchange_rows(self.info, self.owner, needs, lambda c, t=t: t[self.row_of[c]], width,
+                                    self.device, t.dtype)
+            nt = padded_rows(n, width, self.device, dtype=t.dtype) if t.dtype == torch.float32 else \
+                torch.zeros((n, width), dtype=t.dtype, device=self.device)
+            keep = [(i, self.row_of[c]) for i, c in enumerate(new_local) if c in self.row_of]
+            if keep:
+                di = torch.tensor([i for i, _ in keep], device=self.device)
+                si = torch.tensor([j for _, j in keep], device=self.device)
+                nt[di] = t[si]
+            for i, c in enumerate(new_local):
+                if c not in self.row_of:
+                    nt[i].copy_(recv[c])
+            new_state[path] = nt
+        for path, nt in new_state.items():
+            obj = self
+            parts = path.split(".")
+            for p_ in parts[:-1]:
+                obj = getattr(obj, p_)
+            setattr(obj, parts[-1], nt)
+        self.owner = new_owner
+        self.shards = [[c for c in range(self.N) if new_owner[c] == r] for r in range(self.info.world)]
+        self.local = new_local
+        self.row_of = {c: i for i, c in enumerate(new_local)}
+        self.C = len(new_local)
+        self.grads = padded_rows(n, self.P, self.device)
+        self.mom_buf = padded_rows(n, self.P, self.device) if self.cfg.momentum != 0 else None
+        self._after_migrate()
+
+    def _after_migrate(self):
+        self._graphs = {}
+        self._scratch = None
+        self._eval_cache = None
+        if hasattr(self, "rowset"):
+            self.rowset = RowSet(self.theta, self.bufs)
+
     def _local_rows(self, clients):
         """(rows, clients) of the given global clients that live on this rank, in row order."""
         cs = sorted((c for c in clients if c in self.row_of), key=lambda c: self.row_of[c])
@@ -731,6 +818,7 @@ class FLRunner:
         sampled = self.sample_clients(round_idx)
         if self.log is not None and self.info.is_main:
             self.log.info("client_indexes = " + str(np.array(sampled)))
+        self.rebalance(sampled)
         self.local_train(round_idx, sampled)
         if sync_timers:
             self._sync()

@@ -256,3 +256,41 @@ def test_subavg_prunes_and_aggregates_over_mask_counts():
     dens = MK.unpack_bits(r.mbits, r.P).mean(1)
     assert float(dens.min()) < 1.0  # something was pruned (percentile 0.2 per weight layer)
     assert np.isfinite(r.w_global.numpy()).all()
+
+
+REBALANCE_CASES = [("fedavg", 4, {"sizes": [6 + (c % 5) * 2 for c in range(100)], "frac": 0.25, "epochs": 1}),
+                   ("salientgrads", 3, {"frac": 0.5}), ("subavg", 2, {"frac": 0.5}), ("ditto", 2, {"frac": 0.5}),
+                   ("local", 3, {"frac": 0.5})]
+
+
+@pytest.mark.parametrize("algo,world,kw", REBALANCE_CASES)
+def test_rebalanced_multirank_matches_single_process(algo, world, kw, tmp_path):
+    """Sampling-aware rebalancing (sampled clients' rows / masks / personal models migrate point-to-point to the
+    least loaded ranks each round) changes where clients train, not what they compute."""
+    kw = dict(kw, rebalance=True)
+    got = _spawn(world, str(tmp_path / "r"), algo, kw)
+    r = _runner(algo, **kw)
+    _drive(r, 2)
+    # fp32 partial sums are all-reduced from different per-rank groupings: w_global agrees to ~1e-7, rows to ~2e-5
+    _same(got, _collect(r), len(kw.get("sizes", SIZES)), algo, atol=5e-5)
+
+
+def test_balanced_owner_evens_the_sampled_load():
+    from neuroimagedisttraining_amd.engine.runner import FLRunner
+    from neuroimagedisttraining_amd.parallel import runtime as rt
+    r = FLRunner.__new__(FLRunner)
+    r.N = 12
+    r.sizes = np.array([30, 5, 5, 5, 20, 20, 4, 4, 9, 9, 9, 9], dtype=np.int64)
+    r.owner = np.array([0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 2, 2], dtype=np.int64)
+    r.info = rt.DistInfo(0, 3, 0, torch.device("cpu"), "gloo")
+    sampled = [0, 1, 2, 3, 4, 5, 8]
+    own = r.balanced_owner(sampled)
+    load = np.zeros(3, dtype=np.int64)
+    before = np.zeros(3, dtype=np.int64)
+    for c in sampled:
+        load[own[c]] += r.sizes[c]
+        before[r.owner[c]] += r.sizes[c]
+    assert load.max() < before.max() and load.sum() == before.sum()
+    assert load.max() - load.min() <= max(r.sizes[c] for c in sampled)
+    assert all(own[c] == r.owner[c] for c in range(r.N) if c not in sampled)  # only sampled clients move
+    assert np.array_equal(own, r.balanced_owner(sampled))                       # deterministic
