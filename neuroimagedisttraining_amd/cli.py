@@ -110,6 +110,7 @@ def add_args(parser, algo):
     a("--synthetic_abcd", type=int, default=1)
     a("--n_per_client", type=int, default=180)
     a("--synthetic_size", type=int, default=0)
+    a("--rebalance", type=int, default=0)  # 1: (HIP, multi-rank, frac < 1) replicate the cohort, even per-round load
     a("--heartbeat_s", type=float, default=0.0)  # >0: multi-rank failure detection (comm/failure.py)  # 2D datasets without files: synthetic train images (0 = full size)
     a("--fedprox_mu", type=float, default=d.get("fedprox_mu", 0.0))
     a("--aggregator", type=str, default="fedavg")
@@ -259,7 +260,7 @@ def hip_cohort(args, info, logger=None, with_val=False):
         tr = [np.asarray(train[c]) for c in range(N)]
         te = [np.asarray(test[c]) for c in range(N)]
         shards = rt.shard_clients([len(t) for t in tr], info.world)
-        mine = shards[info.rank]
+        mine = list(range(N)) if getattr(args, "rebalance", 0) else shards[info.rank]
         subj = np.concatenate([np.concatenate([tr[c], te[c]]) for c in mine]) if mine else np.zeros(0, np.int64)
         x8, mom = stream_to_device(vf, subj, info.device, hip_store=True)
         labels = torch.from_numpy(vf.labels[subj].astype(np.float32)).to(info.device)
@@ -273,7 +274,8 @@ def hip_cohort(args, info, logger=None, with_val=False):
         n_test = max(1, int(round(args.n_per_client * 0.2)))
         n_train = args.n_per_client - n_test
         shards = rt.shard_clients([n_train] * N, info.world)
-        vol, labels, local = build_fl_volumes(shards[info.rank], N, n_train, n_test, info.device, seed=args.seed,
+        mine = list(range(N)) if getattr(args, "rebalance", 0) else shards[info.rank]
+        vol, labels, local = build_fl_volumes(mine, N, n_train, n_test, info.device, seed=args.seed,
                                               alpha=args.partition_alpha)
         x8, mom = to_hip_store(vol)
         del vol
@@ -299,6 +301,7 @@ def fl_config(args, algo):
                     prox_mu=args.fedprox_mu if algo == "fedprox" else 0.0, group=args.group,
                     aggregator=args.aggregator, byzantine_f=args.byzantine_f, trim_ratio=args.trim_ratio,
                     update_topk=args.update_topk, heartbeat_s=args.heartbeat_s,
+                    rebalance=bool(g("rebalance", 0)),
                     stratified_sampling=bool(g("stratified_sampling", False)),
                     cs=g("cs", "ring") if algo == "dpsgd" else "random", lamda=g("lamda", 0.5),
                     local_epochs=g("local_epochs", 0) or 0, anneal_factor=g("anneal_factor", 0.5),
