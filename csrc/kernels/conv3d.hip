@@ -1009,38 +1009,61 @@ constexpr int kWdGroup = kWdPos * kWdRow;        // one 64-col group: 8 KB
 constexpr int kWdBuf = 5 * kWdGroup;             // 4 X groups + dY
 __device__ __forceinline__ int swz_wd(int r) { return (r & 2) | ((r >> 1) & 4); }
 
-__global__ __launch_bounds__(256, 2) void k_conv_wgrad_dma(ConvWgDmaArgs a) {
-  __shared__ __attribute__((aligned(16))) uint16_t smem[2 * kWdBuf];
+// NCH = 64-channel output halves per block: 1 -> 4 waves (64 co x 256 k-cols), 2 -> 8 waves (128 co x 256 k-cols:
+// the X tile of a k-step feeds twice the MFMAs, 48 KB of LDS-DMA per 256 MFMAs instead of 40 KB per 128).
+// Wave (wc, wk) = (wid / 4, wid % 4) computes co half wc x X group wk; it stages 8/NCH of group wk's 8 X
+// instructions and dY half wc's slices 2wk, 2wk+1.
+template <int NCH>
+__global__ __launch_bounds__(256 * NCH, 2 / NCH) void k_conv_wgrad_dma(ConvWgDmaArgs a) {
+  constexpr int BUFE = (4 + NCH) * kWdGroup;  // elements per stage: 4 X groups + NCH dY halves
+  constexpr int XI = 8 / NCH;                  // X instructions per wave per stage
+  __shared__ __attribute__((aligned(16))) uint16_t smem[2 * BUFE];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // uniform: LDS destinations stay in SGPRs
+  const int wc = wid >> 2, wk = wid & 3;
   const int id = xcd_remap(blockIdx.x, gridDim.x);
   const int kt = id % a.nKT, r1 = id / a.nKT;
   const int ct = r1 % a.nCT, r2 = r1 / a.nCT;
   const int sp = r2 % a.nsplit, g = r2 / a.nsplit;
-  const int kc0 = kt * kWgKC, co0 = ct * kWgCO;
+  const int kc0 = kt * kWgKC, co0 = ct * (kWgCO * NCH);
   const int p_begin = sp * a.chunk, p_end = min(a.Mg, p_begin + a.chunk);
   const int Cin = a.Cin;
   const i32x4_t rx = make_rsrc(a.x + (int64_t)g * a.xclient, (uint32_t)(a.xclient * 2));
   const i32x4_t rd = make_rsrc(a.dy + (int64_t)g * a.Mg * a.Cout, (uint32_t)((int64_t)a.Mg * a.Cout * 2));
   const i32x4_t rt = make_rsrc(a.ptab, (uint32_t)a.Mg * 8u);  // rows past Mg read {0, mask 0}: no taps valid
-  // this wave's X group: k-cols kc0 + 64w .. +63 = one tap, 64 channels
-  const int kg = kc0 + 64 * wid;
+  // this wave's X group: k-cols kc0 + 64 wk .. +63 = one tap, 64 channels
+  const int kg = kc0 + 64 * wk;
   const bool gval = kg < a.K;
   const int gtap = gval ? kg / Cin : 31;  // 31: never set in a tap mask -> out-of-range read -> zeros
   const int gcol = gval ? (((gtap / 9) * a.H + (gtap / 3) % 3) * a.W + gtap % 3) * Cin + (kg - gtap * Cin) : 0;
   const int lr = lane >> 3, ls = lane & 7;
+  const int xi0 = wc * XI;  // this wave's first X instruction (row block) of group wk
   // per-lane constant parts of the byte offsets: X row r = 8i + lr, chunk (ls ^ swz(r)); dY likewise
-  int xcol[8], dcol[2];
+  int xcol[XI], dcol[2];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) xcol[i] = (gcol + ((ls ^ swz_wd(8 * i + lr)) << 3)) * 2;
+  for (int i = 0; i < XI; ++i) xcol[i] = (gcol + ((ls ^ swz_wd(8 * (xi0 + i) + lr)) << 3)) * 2;
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
-    const int r = 8 * (2 * wid + i) + lr;
-    dcol[i] = (r * a.Cout + co0 + ((ls ^ swz_wd(r)) << 3)) * 2;
+    const int r = 8 * (2 * wk + i) + lr;
+    dcol[i] = (r * a.Cout + co0 + 64 * wc + ((ls ^ swz_wd(r)) << 3)) * 2;
   }
-  i32x2_t tn[8];  // ptab entries {voxel offset, tap mask} of this lane's 8 X rows, one step ahead
-#define WD_FETCH(P0)                                                                                            {                                                                                                               _Pragma("unroll") for (int i_ = 0; i_ < 8; ++i_)                                                                tn[i_] = nidt_raw_buffer_load_v2i32(rt, ((P0) + 8 * i_ + lr) * 8, 0, 0);                                  }
-#define WD_ISSUE(P0, BUFI)                                                                                      {                                                                                                               uint16_t* sX_ = smem + (BUFI) * kWdBuf + wid * kWdGroup;                                                      uint16_t* sD_ = smem + (BUFI) * kWdBuf + 4 * kWdGroup;                                                        _Pragma("unroll") for (int i_ = 0; i_ < 8; ++i_) {                                                              const bool ok_ = (tn[i_].y >> gtap) & 1;                                                                      blds16(rx, ok_ ? tn[i_].x * (2 * Cin) + xcol[i_] : kBufOOB, sX_ + i_ * 512);                               }                                                                                                             _Pragma("unroll") for (int i_ = 0; i_ < 2; ++i_)                                                                blds16(rd, (P0) * (2 * a.Cout) + dcol[i_], sD_ + (2 * wid + i_) * 512);                                    }
+  i32x2_t tn[XI];  // ptab entries {voxel offset, tap mask} of this lane's X rows, one step ahead
+#define WD_FETCH(P0)                                                                                          \
+  {                                                                                                           \
+    _Pragma("unroll") for (int i_ = 0; i_ < XI; ++i_)                                                         \
+      tn[i_] = nidt_raw_buffer_load_v2i32(rt, ((P0) + 8 * (xi0 + i_) + lr) * 8, 0, 0);                        \
+  }
+#define WD_ISSUE(P0, BUFI)                                                                                    \
+  {                                                                                                           \
+    uint16_t* sX_ = smem + (BUFI) * BUFE + wk * kWdGroup;                                                     \
+    uint16_t* sD_ = smem + (BUFI) * BUFE + (4 + wc) * kWdGroup;                                               \
+    _Pragma("unroll") for (int i_ = 0; i_ < XI; ++i_) {                                                       \
+      const bool ok_ = (tn[i_].y >> gtap) & 1;                                                                \
+      blds16(rx, ok_ ? tn[i_].x * (2 * Cin) + xcol[i_] : kBufOOB, sX_ + (xi0 + i_) * 512);                    \
+    }                                                                                                         \
+    _Pragma("unroll") for (int i_ = 0; i_ < 2; ++i_)                                                          \
+      blds16(rd, (P0) * (2 * a.Cout) + dcol[i_], sD_ + (2 * wk + i_) * 512);                                  \
+  }
 
   f32x4 acc[4][4];
 #pragma unroll
@@ -1066,8 +1089,8 @@ __global__ __launch_bounds__(256, 2) void k_conv_wgrad_dma(ConvWgDmaArgs a) {
       WD_ISSUE(p_begin + kWdPos * (st + 1), cur ^ 1)
       if (st + 2 < nsteps) WD_FETCH(p_begin + kWdPos * (st + 2))
     }
-    const uint16_t* sX = smem + cur * kWdBuf + wid * kWdGroup;
-    const uint16_t* sD = smem + cur * kWdBuf + 4 * kWdGroup;
+    const uint16_t* sX = smem + cur * BUFE + wk * kWdGroup;
+    const uint16_t* sD = smem + cur * BUFE + (4 + wc) * kWdGroup;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {  // two 32-position MFMA k-steps
       const int ra = 32 * kk + rr0, rb = 32 * kk + rr1;
@@ -1091,10 +1114,10 @@ __global__ __launch_bounds__(256, 2) void k_conv_wgrad_dma(ConvWgDmaArgs a) {
 #undef WD_ISSUE
 #undef WD_FETCH
   const int fr = lane & 15, fq = lane >> 4;
-  float* out = a.part + (((int64_t)sp * a.G + g) * a.Cout + co0) * a.K;
+  float* out = a.part + (((int64_t)sp * a.G + g) * a.Cout + co0 + 64 * wc) * a.K;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    const int k = kc0 + 64 * wid + 16 * j + fr;
+    const int k = kc0 + 64 * wk + 16 * j + fr;
     if (k < a.K) {
 #pragma unroll
       for (int i = 0; i < 4; ++i)
@@ -1150,13 +1173,22 @@ static void conv_wgrad_impl(uintptr_t x, uintptr_t xs, uintptr_t xt, uintptr_t d
     d.x = a.x; d.dy = a.dy; d.ptab = ptr<const int2>(ptab); d.part = a.part;
     d.D = D; d.H = H; d.W = W; d.Cin = Cin; d.Cout = Cout; d.Mg = a.Mg; d.K = a.K; d.nsplit = nsplit; d.G = G;
     d.chunk = ((ceil_div(a.Mg, nsplit) + kWdPos - 1) / kWdPos) * kWdPos;
-    d.nKT = ceil_div(a.K, kWgKC); d.nCT = Cout / kWgCO;
+    // NIDT_WG_NCH=2: 128-channel blocks where Cout allows (8 waves, the X tile feeds both halves).  Measured slower
+    // than two resident 64-channel blocks per CU (conv2 wgrad 3.91 -> 4.14 ms at 64 clients, 0.505 -> 0.542 ms
+    // at 8; profiles/r2_ab_wgrad_nch.txt): the kernel is latency/barrier bound, not L2->LDS bandwidth bound.
+    static const int nch_env = [] {
+      const char* e = getenv("NIDT_WG_NCH");
+      return e ? atoi(e) : 0;
+    }();
+    const int nch = (Cout % 128 == 0 && nch_env == 2) ? 2 : 1;
+    d.nKT = ceil_div(a.K, kWgKC); d.nCT = Cout / (kWgCO * nch);
     d.xclient = (int64_t)B * D * H * W * Cin;
     NIDT_REQUIRE(d.xclient * 2 < (1ll << 31) && (int64_t)a.Mg * Cout * 2 < (1ll << 31),
                  "conv3d_wgrad: per-client tensors must stay below 2 GiB (32-bit buffer offsets)");
     const int64_t nwg = (int64_t)d.nKT * d.nCT * nsplit * G;
     NIDT_REQUIRE(nwg < (1ll << 31), "conv3d_wgrad: grid too large");
-    hipLaunchKernelGGL(k_conv_wgrad_dma, dim3((unsigned)nwg), dim3(256), 0, s, d);
+    if (nch == 2) hipLaunchKernelGGL(k_conv_wgrad_dma<2>, dim3((unsigned)nwg), dim3(512), 0, s, d);
+    else hipLaunchKernelGGL(k_conv_wgrad_dma<1>, dim3((unsigned)nwg), dim3(256), 0, s, d);
   } else {
     dim3 grid(ceil_div(a.K, kWgKC), Cout / kWgCO, G * nsplit);
     if (xs) hipLaunchKernelGGL((k_conv_wgrad<true>), grid, dim3(256), 0, s, a);
