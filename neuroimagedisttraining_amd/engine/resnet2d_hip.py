@@ -357,6 +357,7 @@ class ResNetHipEngine:
         if self.net.hip:
             ops.ext()  # fail loudly on a GPU box without the extension
         self.supports_graphs = self.device.type == "cuda"
+        self.graph_cache_limit = 24  # each captured step holds its own activation pool
         self._opt = None
 
     def _batch(self, idx):

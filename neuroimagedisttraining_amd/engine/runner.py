@@ -125,7 +125,9 @@ class FLRunner:
                               global_test_loss=[], person_test_loss=[], round_time=[])
         self.timers = {"train": 0.0, "aggregate": 0.0, "eval": 0.0, "snip": 0.0}
         self._graphs = {}             # step key -> captured local step (None until the shape repeats, False = eager)
-        self.max_graphs = 64
+        # captured steps kept (LRU); engines whose graphs own their activation memory (torch-allocated, e.g. the
+        # ResNet engine) set a small limit, the AlexNet engine's graphs only reference its persistent buffers
+        self.max_graphs = int(getattr(engine, "graph_cache_limit", 512))
         self._lr_dev = self._seed_dev = None
         self._scratch = None
         self._eval_cache = None
