@@ -52,6 +52,17 @@ void gn_bwd(uintptr_t dy, int dy_bf16, uintptr_t mask, uintptr_t t, uintptr_t st
 void gn_param_grads(uintptr_t part, int G, int B, int C, uintptr_t grads, int64_t ldg, int64_t off_w, int64_t off_b,
                     uintptr_t stream);
 void res_grad(uintptr_t out, uintptr_t dx1, uintptr_t dx2, uintptr_t da, uintptr_t mask, int64_t n, uintptr_t stream);
+// bnr.hip
+int bnr_workspace(int G, int64_t M, int C);
+void bnr_stats(uintptr_t t, int G, int64_t M, int C, float eps, float mom, uintptr_t ws, uintptr_t stats,
+               uintptr_t bufs, int64_t ldb, int64_t off_rm, int64_t off_rv, int64_t off_nbt, uintptr_t stream);
+void bnr_eval_stats(int G, int C, float eps, uintptr_t bufs, int64_t ldb, int64_t off_rm, int64_t off_rv,
+                    uintptr_t stats, uintptr_t stream);
+void bnr_apply(uintptr_t t, uintptr_t res, uintptr_t stats, uintptr_t theta, int64_t ldt, int64_t off_w, int64_t off_b,
+               uintptr_t y, int G, int64_t M, int C, int relu, uintptr_t stream);
+void bnr_bwd(uintptr_t t, uintptr_t dy, int dy_bf16, uintptr_t mask, uintptr_t stats, uintptr_t theta, int64_t ldt,
+             int64_t off_w, int64_t off_b, uintptr_t grads, int64_t ldg, uintptr_t ws, uintptr_t coef, uintptr_t dt,
+             int G, int64_t M, int C, int eval_mode, uintptr_t stream);
 // bn.hip
 void bn_finalize(uintptr_t stats, int nPB, int BP, int Mg, int G, int C, uintptr_t theta, int64_t ldt, int64_t off_g,
                  int64_t off_b, uintptr_t bufs, int64_t ldb, int64_t off_rm, int64_t off_rv, int64_t off_nbt,
@@ -137,6 +148,11 @@ PYBIND11_MODULE(_nidt_hip, m) {
   DEF(gn_bwd);
   DEF(gn_param_grads);
   DEF(res_grad);
+  DEF(bnr_workspace);
+  DEF(bnr_stats);
+  DEF(bnr_eval_stats);
+  DEF(bnr_apply);
+  DEF(bnr_bwd);
   DEF(bn_finalize);
   DEF(bn_eval);
   DEF(bn_relu_pool);

@@ -1,0 +1,323 @@
+// BatchNorm3d (training and eval mode) for client-grouped channels-last activations [G][M = B*D*H*W][C] (bf16), the
+// normalisation of the 3D ResNets (fedml_api/model/cv/salient_models.py:8-139 BasicBlock/Bottleneck; the config-5
+// ResNet-50): per-client statistics over the client's batch, per-client affine and running statistics (rows of
+// theta / bufs).
+//
+// Statistics are two-stage and deterministic: k_bnr_partial reduces a chunk of positions of one client for every
+// channel (thread = 8-channel chunk x position row; LDS merge of the rows in a fixed order) into fp32 partial sums,
+// k_bnr_finalize combines the chunks in fp64 per (client, channel) and updates the running mean / unbiased variance
+// (momentum 0.1) and num_batches_tracked exactly like nn.BatchNorm3d.  The apply kernel fuses the residual add and
+// ReLU; the backward reuses the partial kernel for sum(dy) and sum(dy * xhat) (ReLU mask folded in) and writes
+// dgamma / dbeta straight into the client's gradient row.  No atomics, no library workspaces: hipGraph-safe.
+#include "common.h"
+
+namespace nidt {
+
+constexpr int kBnrThreads = 256;
+constexpr int kBnrChunk = 2048;  // positions per partial block
+
+__device__ __forceinline__ void bnr_unpack8(const uint4 v, float* f) {
+  const uint32_t u[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    f[2 * j] = __uint_as_float(u[j] << 16);
+    f[2 * j + 1] = __uint_as_float(u[j] & 0xffff0000u);
+  }
+}
+
+// MODE 0: part = (sum t, sum t^2); MODE 1: part = (sum dy', sum dy' * xhat) with dy' = dy * (mask > 0) (mask optional),
+// xhat = (t - mean) * rstd from stats [G][C][2].  dy: fp32 (DYB false) or bf16.
+template <int MODE, bool DYB>
+__global__ __launch_bounds__(kBnrThreads) void k_bnr_partial(const uint16_t* __restrict__ t, const void* __restrict__ dyv,
+                                                             const uint16_t* __restrict__ mask,
+                                                             const float* __restrict__ stats, int M, int C,
+                                                             float* __restrict__ part) {
+  __shared__ float sm[kBnrThreads * 17];
+  const int chunk = blockIdx.x, g = blockIdx.y, nchunk = gridDim.x, tid = threadIdx.x;
+  const int nch = C >> 3, rows = kBnrThreads / nch;
+  const int j = tid % nch, r = tid / nch;
+  const int p0 = chunk * kBnrChunk, p1 = min(M, p0 + kBnrChunk);
+  const int64_t base = (int64_t)g * M * C;
+  float a[8], b[8], mu[8], rs[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    a[e] = b[e] = 0.f;
+    if (MODE == 1) {
+      mu[e] = stats[((int64_t)g * C + 8 * j + e) * 2];
+      rs[e] = stats[((int64_t)g * C + 8 * j + e) * 2 + 1];
+    }
+  }
+  if (r < rows) {
+    for (int p = p0 + r; p < p1; p += rows) {
+      const int64_t o = base + (int64_t)p * C + 8 * j;
+      float f[8];
+      bnr_unpack8(*reinterpret_cast<const uint4*>(t + o), f);
+      if (MODE == 0) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          a[e] += f[e];
+          b[e] = fmaf(f[e], f[e], b[e]);
+        }
+      } else {
+        float d[8];
+        if (DYB) {
+          bnr_unpack8(*reinterpret_cast<const uint4*>(reinterpret_cast<const uint16_t*>(dyv) + o), d);
+        } else {
+          const float4* q = reinterpret_cast<const float4*>(reinterpret_cast<const float*>(dyv) + o);
+          const float4 x0 = q[0], x1 = q[1];
+          d[0] = x0.x; d[1] = x0.y; d[2] = x0.z; d[3] = x0.w; d[4] = x1.x; d[5] = x1.y; d[6] = x1.z; d[7] = x1.w;
+        }
+        if (mask) {
+          float mk[8];
+          bnr_unpack8(*reinterpret_cast<const uint4*>(mask + o), mk);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) d[e] = mk[e] > 0.f ? d[e] : 0.f;
+        }
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          a[e] += d[e];
+          b[e] = fmaf(d[e], (f[e] - mu[e]) * rs[e], b[e]);
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    sm[tid * 17 + e] = a[e];
+    sm[tid * 17 + 8 + e] = b[e];
+  }
+  __syncthreads();
+  for (int c = tid; c < C; c += kBnrThreads) {
+    const int jj = c >> 3, e = c & 7;
+    float sa = 0.f, sb = 0.f;
+    for (int rr = 0; rr < rows; ++rr) {
+      sa += sm[(rr * nch + jj) * 17 + e];
+      sb += sm[(rr * nch + jj) * 17 + 8 + e];
+    }
+    float* o = part + (((int64_t)chunk * gridDim.y + g) * C + c) * 2;
+    o[0] = sa;
+    o[1] = sb;
+  }
+  (void)nchunk;
+}
+
+// per (client, channel): stats = (mean, rstd); running stats rows updated (train mode)
+__global__ void k_bnr_finalize(const float* __restrict__ part, int nchunk, int G, int C, int M, float eps, float mom,
+                               float* __restrict__ stats, float* bufs, int64_t ldb, int64_t off_rm, int64_t off_rv,
+                               int64_t off_nbt) {
+  const int g = blockIdx.x;
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    double s = 0.0, q = 0.0;
+    for (int k = 0; k < nchunk; ++k) {
+      const float* p = part + (((int64_t)k * G + g) * C + c) * 2;
+      s += p[0];
+      q += p[1];
+    }
+    const double mean = s / M;
+    const double var = fmax(q / M - mean * mean, 0.0);
+    stats[((int64_t)g * C + c) * 2] = (float)mean;
+    stats[((int64_t)g * C + c) * 2 + 1] = (float)(1.0 / sqrt(var + eps));
+    if (bufs) {
+      float* rm = bufs + (int64_t)g * ldb + off_rm;
+      float* rv = bufs + (int64_t)g * ldb + off_rv;
+      const double unb = M > 1 ? var * M / (M - 1) : var;
+      rm[c] = (float)((1.0 - mom) * rm[c] + mom * mean);
+      rv[c] = (float)((1.0 - mom) * rv[c] + mom * unb);
+      if (c == 0 && off_nbt >= 0) bufs[(int64_t)g * ldb + off_nbt] += 1.f;
+    }
+  }
+}
+
+// eval mode: stats from the running statistics rows
+__global__ void k_bnr_eval_stats(int G, int C, float eps, const float* __restrict__ bufs, int64_t ldb, int64_t off_rm,
+                                 int64_t off_rv, float* __restrict__ stats) {
+  const int g = blockIdx.x;
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    stats[((int64_t)g * C + c) * 2] = bufs[(int64_t)g * ldb + off_rm + c];
+    stats[((int64_t)g * C + c) * 2 + 1] = rsqrtf(bufs[(int64_t)g * ldb + off_rv + c] + eps);
+  }
+}
+
+template <bool RES, bool RELU>
+__global__ __launch_bounds__(256) void k_bnr_apply(const uint16_t* __restrict__ t, const uint16_t* __restrict__ res,
+                                                   const float* __restrict__ stats, const float* __restrict__ theta,
+                                                   int64_t ldt, int64_t off_w, int64_t off_b, uint16_t* __restrict__ y,
+                                                   int64_t M, int C) {
+  const int nch = C >> 3;
+  const int64_t per = M * nch, tot = per * gridDim.y;
+  (void)tot;
+  const int g = blockIdx.y;
+  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < per; q += (int64_t)gridDim.x * blockDim.x) {
+    const int j = (int)(q % nch);
+    const int64_t o = ((int64_t)g * M * nch + q) * 8;
+    float f[8], rr[8];
+    bnr_unpack8(*reinterpret_cast<const uint4*>(t + o), f);
+    if (RES) bnr_unpack8(*reinterpret_cast<const uint4*>(res + o), rr);
+    uint32_t out[4];
+#pragma unroll
+    for (int e = 0; e < 8; e += 2) {
+      float v[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int c = 8 * j + e + h;
+        const float mu = stats[((int64_t)g * C + c) * 2], rs = stats[((int64_t)g * C + c) * 2 + 1];
+        const float sc = theta[(int64_t)g * ldt + off_w + c] * rs;
+        float x = fmaf(f[e + h] - mu, sc, theta[(int64_t)g * ldt + off_b + c]);
+        if (RES) x += rr[e + h];
+        if (RELU) x = fmaxf(x, 0.f);
+        v[h] = x;
+      }
+      out[e >> 1] = pack_bf16x2(v[0], v[1]);
+    }
+    *reinterpret_cast<uint4*>(y + o) = make_uint4(out[0], out[1], out[2], out[3]);
+  }
+}
+
+// dgamma / dbeta rows from the backward partials; coef [G][C][2] = (sum dy'/M, sum dy'*xhat/M)
+__global__ void k_bnr_bwd_fin(const float* __restrict__ part, int nchunk, int G, int C, int M, float* __restrict__ grads,
+                              int64_t ldg, int64_t off_w, int64_t off_b, float* __restrict__ coef) {
+  const int g = blockIdx.x;
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    double a = 0.0, b = 0.0;
+    for (int k = 0; k < nchunk; ++k) {
+      const float* p = part + (((int64_t)k * G + g) * C + c) * 2;
+      a += p[0];
+      b += p[1];
+    }
+    grads[(int64_t)g * ldg + off_w + c] = (float)b;
+    grads[(int64_t)g * ldg + off_b + c] = (float)a;
+    coef[((int64_t)g * C + c) * 2] = (float)(a / M);
+    coef[((int64_t)g * C + c) * 2 + 1] = (float)(b / M);
+  }
+}
+
+// dt = rstd * gamma * (dy' - mean(dy') - xhat * mean(dy' xhat))   (eval mode: coef = 0 -> rstd * gamma * dy')
+template <bool DYB>
+__global__ __launch_bounds__(256) void k_bnr_bwd_apply(const uint16_t* __restrict__ t, const void* __restrict__ dyv,
+                                                       const uint16_t* __restrict__ mask,
+                                                       const float* __restrict__ stats, const float* __restrict__ coef,
+                                                       const float* __restrict__ theta, int64_t ldt, int64_t off_w,
+                                                       uint16_t* __restrict__ dt, int64_t M, int C) {
+  const int nch = C >> 3;
+  const int64_t per = M * nch;
+  const int g = blockIdx.y;
+  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < per; q += (int64_t)gridDim.x * blockDim.x) {
+    const int j = (int)(q % nch);
+    const int64_t o = ((int64_t)g * M * nch + q) * 8;
+    float f[8], d[8];
+    bnr_unpack8(*reinterpret_cast<const uint4*>(t + o), f);
+    if (DYB) {
+      bnr_unpack8(*reinterpret_cast<const uint4*>(reinterpret_cast<const uint16_t*>(dyv) + o), d);
+    } else {
+      const float4* p = reinterpret_cast<const float4*>(reinterpret_cast<const float*>(dyv) + o);
+      const float4 x0 = p[0], x1 = p[1];
+      d[0] = x0.x; d[1] = x0.y; d[2] = x0.z; d[3] = x0.w; d[4] = x1.x; d[5] = x1.y; d[6] = x1.z; d[7] = x1.w;
+    }
+    if (mask) {
+      float mk[8];
+      bnr_unpack8(*reinterpret_cast<const uint4*>(mask + o), mk);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) d[e] = mk[e] > 0.f ? d[e] : 0.f;
+    }
+    uint32_t out[4];
+#pragma unroll
+    for (int e = 0; e < 8; e += 2) {
+      float v[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int c = 8 * j + e + h;
+        const float mu = stats[((int64_t)g * C + c) * 2], rs = stats[((int64_t)g * C + c) * 2 + 1];
+        const float m1 = coef ? coef[((int64_t)g * C + c) * 2] : 0.f;
+        const float m2 = coef ? coef[((int64_t)g * C + c) * 2 + 1] : 0.f;
+        const float xh = (f[e + h] - mu) * rs;
+        v[h] = rs * theta[(int64_t)g * ldt + off_w + c] * (d[e + h] - m1 - xh * m2);
+      }
+      out[e >> 1] = pack_bf16x2(v[0], v[1]);
+    }
+    *reinterpret_cast<uint4*>(dt + o) = make_uint4(out[0], out[1], out[2], out[3]);
+  }
+}
+
+static void bnr_check(int G, int64_t M, int C, const char* who) {
+  NIDT_REQUIRE(G > 0 && M > 0 && C % 8 == 0 && C <= 2048 && kBnrThreads % (C / 8) == 0,
+               std::string(who) + ": C a power-of-two multiple of 8, <= 2048");
+  NIDT_REQUIRE(M < (1ll << 31), std::string(who) + ": positions per client < 2^31");
+}
+
+static int bnr_nchunk(int64_t M) { return (int)((M + kBnrChunk - 1) / kBnrChunk); }
+
+int bnr_workspace(int G, int64_t M, int C) { return bnr_nchunk(M) * G * C * 2; }
+
+// training-mode statistics (+ running stats) -> stats [G][C][2]; ws: bnr_workspace floats
+void bnr_stats(uintptr_t t, int G, int64_t M, int C, float eps, float mom, uintptr_t ws, uintptr_t stats,
+               uintptr_t bufs, int64_t ldb, int64_t off_rm, int64_t off_rv, int64_t off_nbt, uintptr_t stream) {
+  bnr_check(G, M, C, "bnr_stats");
+  NIDT_REQUIRE(C / 8 <= kBnrThreads, "bnr_stats: C <= 2048");
+  hipStream_t s = as_stream(stream);
+  const int nc = bnr_nchunk(M);
+  hipLaunchKernelGGL((k_bnr_partial<0, false>), dim3(nc, G), dim3(kBnrThreads), 0, s, ptr<const uint16_t>(t), nullptr,
+                     nullptr, nullptr, (int)M, C, ptr<float>(ws));
+  NIDT_CHECK(hipGetLastError());
+  hipLaunchKernelGGL(k_bnr_finalize, dim3(G), dim3(256), 0, s, ptr<const float>(ws), nc, G, C, (int)M, eps, mom,
+                     ptr<float>(stats), ptr<float>(bufs), ldb, off_rm, off_rv, off_nbt);
+  NIDT_CHECK(hipGetLastError());
+}
+
+void bnr_eval_stats(int G, int C, float eps, uintptr_t bufs, int64_t ldb, int64_t off_rm, int64_t off_rv,
+                    uintptr_t stats, uintptr_t stream) {
+  hipLaunchKernelGGL(k_bnr_eval_stats, dim3(G), dim3(256), 0, as_stream(stream), G, C, eps, ptr<const float>(bufs), ldb,
+                     off_rm, off_rv, ptr<float>(stats));
+  NIDT_CHECK(hipGetLastError());
+}
+
+static dim3 bnr_grid(int G, int64_t M, int C) {
+  const int64_t per = M * (C / 8);
+  return dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(4096 / std::max(1, G) + 1, (per + 255) / 256)), G);
+}
+
+void bnr_apply(uintptr_t t, uintptr_t res, uintptr_t stats, uintptr_t theta, int64_t ldt, int64_t off_w, int64_t off_b,
+               uintptr_t y, int G, int64_t M, int C, int relu, uintptr_t stream) {
+  bnr_check(G, M, C, "bnr_apply");
+  hipStream_t s = as_stream(stream);
+  const dim3 grid = bnr_grid(G, M, C);
+#define BNRA(R, L)                                                                                             \
+  hipLaunchKernelGGL((k_bnr_apply<R, L>), grid, dim3(256), 0, s, ptr<const uint16_t>(t), ptr<const uint16_t>(res), \
+                     ptr<const float>(stats), ptr<const float>(theta), ldt, off_w, off_b, ptr<uint16_t>(y), M, C)
+  if (res) { if (relu) BNRA(true, true); else BNRA(true, false); }
+  else { if (relu) BNRA(false, true); else BNRA(false, false); }
+#undef BNRA
+  NIDT_CHECK(hipGetLastError());
+}
+
+// backward: dgamma/dbeta rows (train mode) and dt.  eval_mode: BN used running stats (no statistics gradient).
+void bnr_bwd(uintptr_t t, uintptr_t dy, int dy_bf16, uintptr_t mask, uintptr_t stats, uintptr_t theta, int64_t ldt,
+             int64_t off_w, int64_t off_b, uintptr_t grads, int64_t ldg, uintptr_t ws, uintptr_t coef, uintptr_t dt,
+             int G, int64_t M, int C, int eval_mode, uintptr_t stream) {
+  bnr_check(G, M, C, "bnr_bwd");
+  NIDT_REQUIRE(C / 8 <= kBnrThreads, "bnr_bwd: C <= 2048");
+  hipStream_t s = as_stream(stream);
+  const int nc = bnr_nchunk(M);
+  if (dy_bf16)
+    hipLaunchKernelGGL((k_bnr_partial<1, true>), dim3(nc, G), dim3(kBnrThreads), 0, s, ptr<const uint16_t>(t),
+                       ptr<const void>(dy), ptr<const uint16_t>(mask), ptr<const float>(stats), (int)M, C, ptr<float>(ws));
+  else
+    hipLaunchKernelGGL((k_bnr_partial<1, false>), dim3(nc, G), dim3(kBnrThreads), 0, s, ptr<const uint16_t>(t),
+                       ptr<const void>(dy), ptr<const uint16_t>(mask), ptr<const float>(stats), (int)M, C, ptr<float>(ws));
+  NIDT_CHECK(hipGetLastError());
+  hipLaunchKernelGGL(k_bnr_bwd_fin, dim3(G), dim3(256), 0, s, ptr<const float>(ws), nc, G, C, (int)M, ptr<float>(grads),
+                     ldg, off_w, off_b, ptr<float>(coef));
+  NIDT_CHECK(hipGetLastError());
+  const dim3 grid = bnr_grid(G, M, C);
+  const float* cf = eval_mode ? nullptr : ptr<const float>(coef);
+  if (dy_bf16)
+    hipLaunchKernelGGL(k_bnr_bwd_apply<true>, grid, dim3(256), 0, s, ptr<const uint16_t>(t), ptr<const void>(dy),
+                       ptr<const uint16_t>(mask), ptr<const float>(stats), cf, ptr<const float>(theta), ldt, off_w,
+                       ptr<uint16_t>(dt), M, C);
+  else
+    hipLaunchKernelGGL(k_bnr_bwd_apply<false>, grid, dim3(256), 0, s, ptr<const uint16_t>(t), ptr<const void>(dy),
+                       ptr<const uint16_t>(mask), ptr<const float>(stats), cf, ptr<const float>(theta), ldt, off_w,
+                       ptr<uint16_t>(dt), M, C);
+  NIDT_CHECK(hipGetLastError());
+}
+
+}  // namespace nidt

@@ -576,8 +576,8 @@ static void conv3d_fwd_impl(uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t 
                             uintptr_t stream, int ksplit, uintptr_t part, int64_t bias_ld = 0, int kt = 27,
                             int stride = 1, int padd = -1) {
   NIDT_REQUIRE(Cin % 32 == 0, "conv3d_fwd: Cin must be a multiple of 32");
-  NIDT_REQUIRE((xs == 0 && Cin % 64 == 0) ? Cin <= kMaxCin : Cin <= 192,
-               "conv3d_fwd: Cin <= 512 (LDS-DMA path: Cin % 64 == 0, no input transform), else <= 192");
+  NIDT_REQUIRE((xs == 0 && Cin % 64 == 0) ? (int64_t)Cin * kt <= 27 * kMaxCin : Cin <= 192,
+               "conv3d_fwd: taps x Cin <= 27 x 512 (LDS-DMA path: Cin % 64 == 0, no input transform), else Cin <= 192");
   NIDT_REQUIRE(Cout % 64 == 0, "conv3d_fwd: Cout must be a multiple of 64");
   NIDT_REQUIRE(pad >= 0 && pad <= 2, "conv3d_fwd: pad in [0,2]");
   NIDT_REQUIRE(kt == 27 || kt == 9 || kt == 1, "conv3d_fwd: taps 27 (3x3x3), 9 (1x3x3) or 1 (1x1x1)");
@@ -1151,8 +1151,8 @@ static void conv_wgrad_impl(uintptr_t x, uintptr_t xs, uintptr_t xt, uintptr_t d
   NIDT_REQUIRE((kt == 27 && st == 1 && padd == pad) || (ptab && !xs),
                "conv_wgrad: 9/1-tap or strided convs need the LDS-DMA path (position table, no input transform)");
   NIDT_REQUIRE(nsplit >= 1, "conv_wgrad: nsplit >= 1");
-  NIDT_REQUIRE((ptab && !xs) ? Cin <= kMaxCin : Cin <= 192,
-               "conv3d_wgrad: Cin <= 512 (LDS-DMA path with a position table), else <= 192");
+  NIDT_REQUIRE((ptab && !xs) ? (int64_t)Cin * kt <= 27 * kMaxCin : Cin <= 192,
+               "conv3d_wgrad: taps x Cin <= 27 x 512 (LDS-DMA path with a position table), else Cin <= 192");
   NIDT_REQUIRE(Cout % kWgCO == 0, "conv3d_wgrad: Cout must be a multiple of 64");
   ConvWgArgs a;
   a.x = ptr<const uint16_t>(x); a.xs = ptr<const float>(xs); a.xt = ptr<const float>(xt);
@@ -1258,7 +1258,7 @@ __global__ __launch_bounds__(256) void k_pack_wt(const uint16_t* __restrict__ wp
 // channels cin_src..Cin-1 zero (channel-padded first layers), wt (dgrad, optional) [G][Cin][kt][Cout] tap-flipped.
 void pack_conv_wk(uintptr_t theta, int64_t ldt, int64_t off, int G, int Cout, int Cin, int kt, int cin_src,
                   float scale, uintptr_t wp, uintptr_t wt, uintptr_t stream) {
-  NIDT_REQUIRE(Cin <= kMaxCin && Cin % 2 == 0, "pack_conv_w: Cin even, <= 512");
+  NIDT_REQUIRE((int64_t)Cin * kt <= 27 * kMaxCin && Cin % 2 == 0, "pack_conv_w: Cin even, taps x Cin <= 27 x 512");
   NIDT_REQUIRE(kt == 27 || kt == 9 || kt == 1, "pack_conv_w: taps 27, 9 or 1");
   NIDT_REQUIRE(cin_src >= 1 && cin_src <= Cin, "pack_conv_w: 1 <= cin_src <= Cin");
   hipStream_t s = as_stream(stream);

@@ -1,0 +1,403 @@
+"""Client-batched 3D ResNet (BASELINE config 5: Bottleneck ResNet-50 on full-resolution 1x121x145x121 volumes) on the
+gfx950 kernels: G clients' local steps in one lockstep pass over rows of the flat ``[C, P]`` parameter matrix.
+
+* every bottleneck convolution — 1x1x1 (the GEMM path: ``conv_fwd_g`` with one tap), 3x3x3 at stride 1 and 2, the
+  1x1x1 stride-2 projections — runs on the client-grouped LDS-DMA implicit-GEMM kernels of ``conv3d.hip``; data
+  gradients use the same kernels on tap-flipped transposed weights (stride 2: zero-upsampled gradient, cropped;
+  1x1 stride 2: scattered to the even voxels), weight gradients the position-table wgrad kernel straight into the
+  client's gradient row;
+* BatchNorm3d (train and eval mode, per-client statistics / affine / running stats) is ``bnr.hip``, with the
+  residual add and ReLU fused into the apply and the ReLU mask into the backward;
+* the stem (7x7x7 stride-2 conv with ONE input channel, BN, ReLU, 3x3x3 max-pool) is not a GEMM shape the conv
+  kernels serve: it runs as one client-grouped PyTorch segment (grouped conv over all clients of the launch,
+  per-client batch statistics) differentiated by autograd;
+* the head (global average pool, fc -> 1, BCE) is a few batched torch ops.
+
+Reference model: ``fedml_api/model/cv/salient_models.py:8-139`` (3D ResNet blocks); the 4-stage ResNet-50 is this
+framework's config-5 model (``models/resnet3d.py``).
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+
+from .. import ops
+from .flat import ParamLayout
+
+BN_EPS = 1e-5
+BN_MOM = 0.1
+
+
+def _stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+class GConv3:
+    """Client-grouped Conv3d (k = 1 or 3, stride 1/2, no bias) on channels-last ``[N, D, H, W, C]`` bf16."""
+
+    def __init__(self, off, cout, cin, k, stride, pad, hip=True):
+        assert k in (1, 3) and cin % 64 == 0 and cout % 64 == 0, (k, cin, cout)
+        self.off, self.cout, self.cin, self.k, self.stride, self.pad = off, cout, cin, k, stride, pad
+        self.hip = hip
+        self.kt = 27 if k == 3 else 1
+        self.numel = cout * cin * self.kt
+        self._packed = None
+
+    def out_dims(self, d, h, w):
+        f = lambda n: (n + 2 * self.pad - self.k) // self.stride + 1  # noqa: E731
+        return f(d), f(h), f(w)
+
+    def _wp(self, theta, G, transposed):
+        wp = torch.empty(G, self.cout, self.kt, self.cin, device=theta.device, dtype=torch.bfloat16)
+        wt = torch.empty(G, self.cin, self.kt, self.cout, device=theta.device, dtype=torch.bfloat16) \
+            if transposed else None
+        ops.ext().pack_conv_wk(theta.data_ptr(), theta.stride(0), self.off, G, self.cout, self.cin, self.kt, self.cin,
+                               1.0, wp.data_ptr(), wt.data_ptr() if transposed else 0, _stream())
+        return wp, wt
+
+    def _torch_fwd(self, x, w, G):
+        N, D, H, W, C = x.shape
+        B = N // G
+        xc = x.reshape(G, B, D, H, W, C).permute(1, 0, 5, 2, 3, 4).reshape(B, G * C, D, H, W)
+        y = F.conv3d(xc, w.reshape(G * self.cout, self.cin, self.k, self.k, self.k), stride=self.stride,
+                     padding=self.pad, groups=G)
+        return y.view(B, G, self.cout, *y.shape[2:]).permute(1, 0, 3, 4, 5, 2).reshape(N, *y.shape[2:], self.cout)
+
+    def fwd(self, x, theta, G, train=False):
+        N, D, H, W, C = x.shape
+        assert C == self.cin and N % G == 0 and x.is_contiguous()
+        if not self.hip:
+            return self._torch_fwd(x, theta[:, self.off:self.off + self.numel], G)
+        Do, Ho, Wo = self.out_dims(D, H, W)
+        wp, wt = self._wp(theta, G, train)
+        self._packed = (theta.data_ptr(), G, wt) if train else None
+        y = torch.empty(N, Do, Ho, Wo, self.cout, device=x.device, dtype=torch.bfloat16)
+        ops.ext().conv_fwd_g(x.data_ptr(), wp.data_ptr(), y.data_ptr(), G, N // G, D, H, W, self.cin, self.cout,
+                             self.kt, self.stride, self.pad, self.pad if self.kt == 27 else 0, _stream())
+        return y
+
+    def bwd(self, dy, x, theta, grads, G, need_dx=True):
+        if not self.hip:
+            w = theta[:, self.off:self.off + self.numel].detach().clone().requires_grad_(True)
+            xx = x.detach().clone().requires_grad_(need_dx)
+            with torch.enable_grad():
+                y = self._torch_fwd(xx, w, G)
+                outs = torch.autograd.grad(y, [w, xx] if need_dx else [w], dy.to(y.dtype))
+            grads[:, self.off:self.off + self.numel].copy_(outs[0])
+            return outs[1] if need_dx else None
+        m, st = ops.ext(), _stream()
+        N, D, H, W, _ = x.shape
+        B = N // G
+        Do, Ho, Wo = dy.shape[1:4]
+        dy = dy.contiguous()
+        padd = self.pad if self.kt == 27 else 0
+        ns = m.conv_wgrad_nsplit_g(G, B, D, H, W, self.cin, self.cout, self.kt, self.stride, self.pad, padd)
+        part = torch.empty(ns * G * self.cout * self.kt * self.cin, device=x.device, dtype=torch.float32)
+        ptab = torch.empty(B * Do * Ho * Wo, 2, device=x.device, dtype=torch.int32)
+        m.conv_pos_table_g(ptab.data_ptr(), B, D, H, W, self.kt, self.stride, self.pad, padd, st)
+        m.conv_wgrad_g(x.data_ptr(), dy.data_ptr(), part.data_ptr(), grads.data_ptr(), grads.stride(0), self.off, G,
+                       B, D, H, W, self.cin, self.cout, self.kt, self.stride, self.pad, padd, ns, 1.0, ptab.data_ptr(),
+                       st)
+        if not need_dx:
+            return None
+        pk, self._packed = self._packed, None
+        wt = pk[2] if (pk is not None and pk[0] == theta.data_ptr() and pk[1] == G and pk[2] is not None) else \
+            self._wp(theta, G, True)[1]
+        if self.stride == 1:
+            dx = torch.empty(N, D, H, W, self.cin, device=x.device, dtype=torch.bfloat16)
+            p2 = self.k - 1 - self.pad
+            m.conv_fwd_g(dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), G, B, Do, Ho, Wo, self.cout, self.cin, self.kt,
+                         1, p2, p2 if self.kt == 27 else 0, st)
+            return dx
+        if self.k == 3:
+            # stride 2, pad 1: dX = conv(zero-upsampled dY [2Do, 2Ho, 2Wo], flipped W^T, pad 1), cropped to D x H x W
+            up = torch.zeros(N, 2 * Do, 2 * Ho, 2 * Wo, self.cout, device=x.device, dtype=torch.bfloat16)
+            up[:, ::2, ::2, ::2] = dy
+            full = torch.empty(N, 2 * Do, 2 * Ho, 2 * Wo, self.cin, device=x.device, dtype=torch.bfloat16)
+            m.conv_fwd_g(up.data_ptr(), wt.data_ptr(), full.data_ptr(), G, B, 2 * Do, 2 * Ho, 2 * Wo, self.cout,
+                         self.cin, 27, 1, 1, 1, st)
+            if (2 * Do, 2 * Ho, 2 * Wo) == (D, H, W):
+                return full
+            return full[:, :D, :H, :W].contiguous()
+        # 1x1 stride 2: dX at the even voxels = W^T dY, zero elsewhere
+        sub = torch.empty(N, Do, Ho, Wo, self.cin, device=x.device, dtype=torch.bfloat16)
+        m.conv_fwd_g(dy.data_ptr(), wt.data_ptr(), sub.data_ptr(), G, B, Do, Ho, Wo, self.cout, self.cin, 1, 1, 0, 0,
+                     st)
+        dx = torch.zeros(N, D, H, W, self.cin, device=x.device, dtype=torch.bfloat16)
+        dx[:, ::2, ::2, ::2] = sub
+        return dx
+
+
+class GBN3:
+    """Client-grouped BatchNorm3d on ``[G*B, D, H, W, C]`` (``bnr.hip``); affine rows in theta, running stats in
+    the buffer rows."""
+
+    def __init__(self, off_w, off_b, C, off_rm, off_rv, off_nbt, hip=True):
+        self.off_w, self.off_b, self.C = off_w, off_b, C
+        self.off_rm, self.off_rv, self.off_nbt = off_rm, off_rv, off_nbt
+        self.hip = hip
+
+    def _torch_fwd(self, t, theta, bufs, G, train, res, relu):
+        C = self.C
+        tf = t.float().reshape(G, -1, C)
+        M = tf.shape[1]
+        if train:
+            mean = tf.mean(1)
+            var = (tf - mean[:, None]).square().mean(1)
+            rm = bufs[:, self.off_rm:self.off_rm + C]
+            rv = bufs[:, self.off_rv:self.off_rv + C]
+            rm.copy_((1 - BN_MOM) * rm + BN_MOM * mean)
+            rv.copy_((1 - BN_MOM) * rv + BN_MOM * var * (M / max(1, M - 1)))
+            if self.off_nbt >= 0:
+                bufs[:, self.off_nbt] += 1
+        else:
+            mean = bufs[:, self.off_rm:self.off_rm + C].clone()
+            var = bufs[:, self.off_rv:self.off_rv + C].clone()
+        rstd = torch.rsqrt(var + BN_EPS)
+        y = (tf - mean[:, None]) * (rstd * theta[:, self.off_w:self.off_w + C])[:, None] + \
+            theta[:, self.off_b:self.off_b + C][:, None]
+        y = y.reshape(t.shape)
+        if res is not None:
+            y = y + res.float()
+        if relu:
+            y = torch.relu(y)
+        return y.to(t.dtype), torch.stack([mean, rstd], -1)
+
+    def fwd(self, t, theta, bufs, G, train, res=None, relu=False):
+        if not self.hip:
+            return self._torch_fwd(t, theta, bufs, G, train, res, relu)
+        m, st = ops.ext(), _stream()
+        N = t.shape[0]
+        M = t.numel() // (self.C * G)
+        stats = torch.empty(G, self.C, 2, device=t.device, dtype=torch.float32)
+        if train:
+            ws = torch.empty(m.bnr_workspace(G, M, self.C), device=t.device, dtype=torch.float32)
+            m.bnr_stats(t.data_ptr(), G, M, self.C, BN_EPS, BN_MOM, ws.data_ptr(), stats.data_ptr(),
+                        bufs.data_ptr() if bufs is not None else 0, bufs.stride(0) if bufs is not None else 0,
+                        self.off_rm, self.off_rv, self.off_nbt, st)
+        else:
+            m.bnr_eval_stats(G, self.C, BN_EPS, bufs.data_ptr(), bufs.stride(0), self.off_rm, self.off_rv,
+                             stats.data_ptr(), st)
+        y = torch.empty_like(t)
+        r = res.contiguous() if res is not None else None
+        m.bnr_apply(t.data_ptr(), r.data_ptr() if r is not None else 0, stats.data_ptr(), theta.data_ptr(),
+                    theta.stride(0), self.off_w, self.off_b, y.data_ptr(), G, M, self.C, int(relu), st)
+        assert N % G == 0
+        return y, stats
+
+    def bwd(self, dy, mask, t, stats, theta, grads, G, eval_mode=False):
+        if not self.hip:
+            C = self.C
+            d = dy.float().reshape(G, -1, C)
+            if mask is not None:
+                d = d * (mask.reshape(G, -1, C) > 0)
+            mean, rstd = stats[..., 0], stats[..., 1]
+            xh = (t.float().reshape(G, -1, C) - mean[:, None]) * rstd[:, None]
+            A, Bs = d.sum(1), (d * xh).sum(1)
+            grads[:, self.off_w:self.off_w + C].copy_(Bs)
+            grads[:, self.off_b:self.off_b + C].copy_(A)
+            M = d.shape[1]
+            g = theta[:, self.off_w:self.off_w + C]
+            if eval_mode:
+                dt = (rstd * g)[:, None] * d
+            else:
+                dt = (rstd * g)[:, None] * (d - (A / M)[:, None] - xh * (Bs / M)[:, None])
+            return dt.reshape(t.shape).to(t.dtype)
+        m, st = ops.ext(), _stream()
+        M = t.numel() // (self.C * G)
+        dy = dy.contiguous()
+        ws = torch.empty(m.bnr_workspace(G, M, self.C), device=t.device, dtype=torch.float32)
+        coef = torch.empty(G, self.C, 2, device=t.device, dtype=torch.float32)
+        dt = torch.empty_like(t)
+        m.bnr_bwd(t.data_ptr(), dy.data_ptr(), int(dy.dtype == torch.bfloat16),
+                  mask.data_ptr() if mask is not None else 0, stats.data_ptr(), theta.data_ptr(), theta.stride(0),
+                  self.off_w, self.off_b, grads.data_ptr(), grads.stride(0), ws.data_ptr(), coef.data_ptr(),
+                  dt.data_ptr(), G, M, self.C, int(eval_mode), st)
+        return dt
+
+
+class GroupedResNet3D:
+    """Forward/backward graph of ``models.resnet3d.ResNet3D`` (Bottleneck) for G clients at once."""
+
+    def __init__(self, players: ParamLayout, blayers: ParamLayout, device, hip=None):
+        self.device = torch.device(device)
+        self.hip = (self.device.type == "cuda") if hip is None else hip
+        self.act = torch.bfloat16 if self.hip else torch.float32
+        off = {n: o for n, o in zip(players.names, players.offsets)}
+        shp = dict(zip(players.names, players.shapes))
+        boff = {n: o for n, o in zip(blayers.names, blayers.offsets)}
+        self.off, self.shp, self.boff = off, shp, boff
+
+        def conv(name, stride):
+            co, ci, k = shp[name][0], shp[name][1], shp[name][2]
+            return GConv3(off[name], co, ci, k, stride, (k - 1) // 2, self.hip)
+
+        def bn(prefix):
+            return GBN3(off[prefix + ".weight"], off[prefix + ".bias"], shp[prefix + ".weight"][0],
+                        boff[prefix + ".running_mean"], boff[prefix + ".running_var"],
+                        boff.get(prefix + ".num_batches_tracked", -1), self.hip)
+
+        self.blocks = []
+        li = 1
+        while ("layer%d.0.conv1.weight" % li) in off:
+            bi = 0
+            while ("layer%d.%d.conv1.weight" % (li, bi)) in off:
+                p = "layer%d.%d." % (li, bi)
+                stride = 2 if (li > 1 and bi == 0) else 1
+                blk = {"c1": conv(p + "conv1.weight", 1), "n1": bn(p + "bn1"),
+                       "c2": conv(p + "conv2.weight", stride), "n2": bn(p + "bn2"),
+                       "c3": conv(p + "conv3.weight", 1), "n3": bn(p + "bn3")}
+                if p + "downsample.0.weight" in off:
+                    blk["cd"] = conv(p + "downsample.0.weight", stride)
+                    blk["nd"] = bn(p + "downsample.1")
+                self.blocks.append(blk)
+                bi += 1
+            li += 1
+        self.fc_w, self.fc_b = off["fc.weight"], off["fc.bias"]
+        self.ncls, self.feat = shp["fc.weight"]
+        self.stem_c = shp["conv1.weight"][0]
+
+    # ------------------------------------------------------------------ stem (torch, autograd)
+    def _stem(self, x8, theta, bufs, G, train):
+        """uint8 volumes [N, D, H, W] -> pooled stem activation [N, d, h, w, C] bf16 (+ autograd handles)."""
+        N = x8.shape[0]
+        B = N // G
+        C = self.stem_c
+        o = self.off
+        w = theta[:, o["conv1.weight"]:o["conv1.weight"] + C * 343].reshape(G * C, 1, 7, 7, 7)
+        gam = theta[:, o["bn1.weight"]:o["bn1.weight"] + C].reshape(G * C)
+        bet = theta[:, o["bn1.bias"]:o["bn1.bias"] + C].reshape(G * C)
+        leaf = [w.detach().clone().requires_grad_(train), gam.detach().clone().requires_grad_(train),
+                bet.detach().clone().requires_grad_(train)]
+        rm = bufs[:, self.boff["bn1.running_mean"]:self.boff["bn1.running_mean"] + C].reshape(G * C).clone()
+        rv = bufs[:, self.boff["bn1.running_var"]:self.boff["bn1.running_var"] + C].reshape(G * C).clone()
+        xin = (x8.to(self.act) / 255.0).view(G, B, *x8.shape[1:]).transpose(0, 1)  # [B, G, D, H, W]
+        with torch.set_grad_enabled(train):
+            s = F.conv3d(xin, leaf[0].to(self.act), stride=2, padding=3, groups=G)          # [B, G*C, ...]
+            s = F.batch_norm(s.float(), rm, rv, leaf[1], leaf[2], training=train, momentum=BN_MOM, eps=BN_EPS)
+            s = F.max_pool3d(torch.relu(s), 3, 2, 1)
+            d, h, ww = s.shape[2:]
+            out = s.view(B, G, C, d, h, ww).permute(1, 0, 3, 4, 5, 2).reshape(N, d, h, ww, C)
+        if train:
+            bufs[:, self.boff["bn1.running_mean"]:self.boff["bn1.running_mean"] + C].copy_(rm.view(G, C))
+            bufs[:, self.boff["bn1.running_var"]:self.boff["bn1.running_var"] + C].copy_(rv.view(G, C))
+            if "bn1.num_batches_tracked" in self.boff:
+                bufs[:, self.boff["bn1.num_batches_tracked"]] += 1
+        return out.to(self.act).contiguous(), (out, leaf)
+
+    # ------------------------------------------------------------------ forward
+    def forward(self, x8, theta, bufs, G, train):
+        a, stem = self._stem(x8, theta, bufs, G, train)
+        saved = []
+        for blk in self.blocks:
+            xin = a
+            t1 = blk["c1"].fwd(xin, theta, G, train)
+            h1, s1 = blk["n1"].fwd(t1, theta, bufs, G, train, relu=True)
+            t2 = blk["c2"].fwd(h1, theta, G, train)
+            h2, s2 = blk["n2"].fwd(t2, theta, bufs, G, train, relu=True)
+            t3 = blk["c3"].fwd(h2, theta, G, train)
+            if "cd" in blk:
+                td = blk["cd"].fwd(xin, theta, G, train)
+                yd, sd = blk["nd"].fwd(td, theta, bufs, G, train)
+            else:
+                td, sd, yd = None, None, xin
+            a, s3 = blk["n3"].fwd(t3, theta, bufs, G, train, res=yd, relu=True)
+            if train:
+                saved.append((xin, t1, s1, h1, t2, s2, h2, t3, s3, td, sd, a))
+        N = a.shape[0]
+        C = a.shape[-1]
+        pooled = a.float().view(N, -1, C).mean(1)
+        fw = theta[:, self.fc_w:self.fc_w + self.ncls * self.feat].view(G, self.ncls, self.feat)
+        fb = theta[:, self.fc_b:self.fc_b + self.ncls]
+        B = N // G
+        logits = (pooled.view(G, B, 1, C) * fw.view(G, 1, self.ncls, C)).sum(-1) + fb.view(G, 1, self.ncls)
+        return logits.reshape(N, self.ncls), pooled, saved, stem
+
+    def train_step(self, theta, bufs, grads, x8, y, G, B, bn_train=True):
+        logits, pooled, saved, stem = self.forward(x8, theta, bufs, G, True)
+        lg = logits.view(G, B)
+        yt = y.float().view(G, B)
+        losses = F.binary_cross_entropy_with_logits(lg, yt, reduction="none").mean(1)
+        dlog = (torch.sigmoid(lg) - yt) / B                                           # [G, B]
+        fw = theta[:, self.fc_w:self.fc_w + self.feat].view(G, self.feat)
+        grads[:, self.fc_w:self.fc_w + self.feat].copy_((dlog.unsqueeze(2) * pooled.view(G, B, self.feat)).sum(1))
+        grads[:, self.fc_b:self.fc_b + 1].copy_(dlog.sum(1, keepdim=True))
+        a = saved[-1][-1]
+        N = a.shape[0]
+        S = a[0].numel() // a.shape[-1]
+        dpool = (dlog.unsqueeze(2) * fw.unsqueeze(1)).reshape(N, 1, self.feat) / float(S)
+        da = dpool.expand(N, S, self.feat).reshape(a.shape).contiguous()
+        for blk, sv in zip(reversed(self.blocks), reversed(saved)):
+            xin, t1, s1, h1, t2, s2, h2, t3, s3, td, sd, a = sv
+            dt3 = blk["n3"].bwd(da, a, t3, s3, theta, grads, G)
+            dh2 = blk["c3"].bwd(dt3, h2, theta, grads, G)
+            dt2 = blk["n2"].bwd(dh2, h2, t2, s2, theta, grads, G)
+            dh1 = blk["c2"].bwd(dt2, h1, theta, grads, G)
+            dt1 = blk["n1"].bwd(dh1, h1, t1, s1, theta, grads, G)
+            dx1 = blk["c1"].bwd(dt1, xin, theta, grads, G)
+            dx2 = None
+            if "cd" in blk:
+                dtd = blk["nd"].bwd(da, a, td, sd, theta, grads, G)
+                dx2 = blk["cd"].bwd(dtd, xin, theta, grads, G)
+            if self.hip:
+                out = torch.empty(dx1.shape, device=dx1.device, dtype=torch.float32)
+                ops.ext().res_grad(out.data_ptr(), dx1.data_ptr(), dx2.data_ptr() if dx2 is not None else 0,
+                                   0 if dx2 is not None else da.data_ptr(), 0 if dx2 is not None else a.data_ptr(),
+                                   out.numel(), _stream())
+                da = out
+            else:
+                da = dx1.float() + (dx2.float() if dx2 is not None else da * (a > 0))
+        out, leaf = stem
+        gw, gg, gb = torch.autograd.grad(out, leaf, da.to(out.dtype))
+        C = self.stem_c
+        o = self.off
+        grads[:, o["conv1.weight"]:o["conv1.weight"] + C * 343].copy_(gw.reshape(G, -1))
+        grads[:, o["bn1.weight"]:o["bn1.weight"] + C].copy_(gg.view(G, C))
+        grads[:, o["bn1.bias"]:o["bn1.bias"] + C].copy_(gb.view(G, C))
+        return losses.detach()
+
+
+class ResNet3DHipEngine:
+    """Engine API (train_step / eval_logits / local_opt / saliency_acc) of the client-batched 3D ResNet on uint8
+    ABCD-shape volumes ``[N, D, H, W]`` (labels {0, 1}, BCE head with one logit)."""
+
+    supports_graphs = False  # the stem segment allocates autograd state; launches here are few and large
+
+    def __init__(self, template_model, volumes_u8, labels, device, hip=None):
+        self.device = torch.device(device)
+        self.players = ParamLayout.from_tensors(list(template_model.named_parameters()))
+        self.blayers = ParamLayout.from_tensors(list(template_model.named_buffers()))
+        self.net = GroupedResNet3D(self.players, self.blayers, self.device, hip=hip)
+        self.x8 = volumes_u8
+        self.labels = labels.to(self.device)
+        if self.net.hip:
+            ops.ext()  # fail loudly without the extension
+        self._opt = None
+
+    def _x(self, idx):
+        return self.x8.index_select(0, idx.long().to(self.x8.device)).to(self.device, non_blocking=True)
+
+    def train_step(self, theta, bufs, grads, idx, G, B, keep, seed, cids=None, seed_dev=None, bn_train=True):
+        y = self.labels.index_select(0, idx.long())
+        return self.net.train_step(theta, bufs, grads, self._x(idx), y, G, B, bn_train)
+
+    def eval_logits(self, theta, bufs, idx, G, B):
+        with torch.no_grad():
+            logits, _, _, _ = self.net.forward(self._x(idx), theta, bufs, G, False)
+        return logits.float()
+
+    def _delegate(self):
+        if self._opt is None:
+            from .executor import HipEngine
+            self._opt = HipEngine.__new__(HipEngine)
+            self._opt.m = ops.ext()
+        return self._opt
+
+    def local_opt(self, theta, grads, mom_buf, spec, lr, wd, momentum, max_norm, lr_dev=None, keep_grad=False):
+        from .executor import HipEngine
+        HipEngine.local_opt(self._delegate(), theta, grads, mom_buf, spec, lr, wd, momentum, max_norm, lr_dev=lr_dev,
+                            keep_grad=keep_grad)
+
+    def saliency_acc(self, theta, grads, score, alpha):
+        from .executor import HipEngine
+        HipEngine.saliency_acc(self._delegate(), theta, grads, score, alpha)

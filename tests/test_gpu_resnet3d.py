@@ -1,0 +1,169 @@
+"""GPU tests of the client-batched 3D ResNet (config 5) path: BatchNorm3d kernels (bnr.hip), the generalised conv
+kernels at 3D shapes (1x1x1 GEMM up to 2048 channels, 3x3x3 stride 2 on odd extents, 1x1x1 stride-2 projections)
+against fp32 PyTorch, and a whole lockstep train step of a Bottleneck ResNet-50 against per-client autograd."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def _dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch.device("cuda")
+
+
+def _rel(a, b):
+    a, b = a.detach().float(), b.detach().float()
+    return float((a - b).norm() / (b.norm() + 1e-12))
+
+
+CONVS = [  # cin, cout, k, stride, (D, H, W)
+    (64, 64, 3, 1, (9, 11, 9)),
+    (64, 128, 3, 2, (9, 11, 9)),
+    (128, 64, 1, 1, (8, 10, 8)),
+    (256, 512, 1, 2, (9, 11, 9)),
+    (1024, 2048, 1, 1, (3, 4, 3)),
+    (512, 512, 3, 1, (4, 5, 4)),
+]
+
+
+@pytest.mark.parametrize("cin,cout,k,stride,dims", CONVS)
+def test_gconv3_fwd_dgrad_wgrad(cin, cout, k, stride, dims):
+    from neuroimagedisttraining_amd.engine.resnet3d_hip import GConv3
+    dev = _dev()
+    torch.manual_seed(cin + cout + k)
+    G, B = 2, 2
+    conv = GConv3(0, cout, cin, k, stride, (k - 1) // 2)
+    P = conv.numel
+    theta = torch.zeros(G, P + (-P) % 64, device=dev)[:, :P]
+    theta.copy_(torch.randn(G, P, device=dev) * (2.0 / (cin * k ** 3)) ** 0.5)
+    x = torch.randn(G * B, *dims, cin, device=dev).to(torch.bfloat16)
+    y = conv.fwd(x, theta, G, train=True)
+    xr = x.float().permute(0, 4, 1, 2, 3).requires_grad_(True)
+    wr = theta.view(G, cout, cin, k, k, k).to(torch.bfloat16).float().requires_grad_(True)
+    ref = torch.cat([F.conv3d(xr[g * B:(g + 1) * B], wr[g], stride=stride, padding=(k - 1) // 2) for g in range(G)])
+    assert tuple(y.shape) == (G * B, *ref.shape[2:], cout)
+    assert _rel(y.permute(0, 4, 1, 2, 3), ref) < 1e-2
+    dy = torch.randn(y.shape, device=dev).to(torch.bfloat16)
+    ref.backward(dy.float().permute(0, 4, 1, 2, 3))
+    grads = torch.zeros_like(theta)
+    dx = conv.bwd(dy, x, theta, grads, G)
+    torch.cuda.synchronize()
+    assert _rel(grads.view(G, cout, cin, k, k, k), wr.grad) < 2e-2
+    assert tuple(dx.shape) == tuple(x.shape)
+    assert _rel(dx.permute(0, 4, 1, 2, 3), xr.grad) < 2e-2
+
+
+@pytest.mark.parametrize("C,dims,res", [(64, (6, 7, 6), True), (256, (3, 4, 3), False), (2048, (1, 2, 1), True)])
+def test_bnr_train_eval_fwd_bwd_match_torch(C, dims, res):
+    from neuroimagedisttraining_amd.engine.resnet3d_hip import GBN3
+    dev = _dev()
+    torch.manual_seed(C)
+    G, B = 3, 2
+    theta = torch.zeros(G, 2 * C + 64, device=dev)
+    theta[:, :C] = torch.randn(G, C, device=dev)
+    theta[:, C:2 * C] = torch.randn(G, C, device=dev)
+    bufs = torch.zeros(G, 2 * C + 64, device=dev)
+    bufs[:, C:2 * C] = 1.0
+    bn = GBN3(0, C, C, 0, C, 2 * C)
+    t = (torch.randn(G * B, *dims, C, device=dev) * 2 + 0.5).to(torch.bfloat16)
+    r = torch.randn_like(t.float()).to(torch.bfloat16) if res else None
+    y, st = bn.fwd(t, theta, bufs, G, True, res=r, relu=True)
+    tr = t.float().requires_grad_(True)
+    gam = theta[:, :C].clone().requires_grad_(True)
+    bet = theta[:, C:2 * C].clone().requires_grad_(True)
+    rm = torch.zeros(G, C, device=dev)
+    rv = torch.ones(G, C, device=dev)
+    outs = []
+    for g in range(G):
+        xg = tr[g * B:(g + 1) * B].permute(0, 4, 1, 2, 3)
+        o = F.batch_norm(xg, rm[g], rv[g], gam[g], bet[g], training=True, momentum=0.1, eps=1e-5)
+        o = o.permute(0, 2, 3, 4, 1)
+        if res:
+            o = o + r[g * B:(g + 1) * B].float()
+        outs.append(torch.relu(o))
+    ref = torch.cat(outs)
+    assert _rel(y, ref) < 1e-2
+    assert torch.allclose(bufs[:, :C], rm, atol=1e-4, rtol=1e-3) and torch.allclose(bufs[:, C:2 * C], rv, atol=1e-3,
+                                                                                     rtol=1e-3)
+    assert torch.all(bufs[:, 2 * C] == 1.0)
+    dy = torch.randn(y.shape, device=dev)
+    ref.backward(dy)
+    grads = torch.zeros_like(theta)
+    dt = bn.bwd(dy, y, t, st, theta, grads, G)
+    torch.cuda.synchronize()
+    assert _rel(dt, tr.grad) < 2e-2
+    assert _rel(grads[:, :C], gam.grad) < 1e-2 and _rel(grads[:, C:2 * C], bet.grad) < 1e-2
+    # eval mode: running statistics
+    ye, _ = bn.fwd(t, theta, bufs, G, False)
+    refe = torch.cat([F.batch_norm(t[g * B:(g + 1) * B].float().permute(0, 4, 1, 2, 3), bufs[g, :C], bufs[g, C:2 * C],
+                                   theta[g, :C], theta[g, C:2 * C], training=False, eps=1e-5).permute(0, 2, 3, 4, 1)
+                      for g in range(G)])
+    assert _rel(ye, refe) < 1e-2
+
+
+def _bf16_faithful(model, conv_dtype=torch.bfloat16):
+    """Round the reference's activations to bf16 where the HIP path stores them (conv outputs, ReLU outputs, the
+    projection BN output), so the comparison checks the wiring, not bf16 error growth through 16 blocks with
+    batch statistics over a few voxels."""
+    def rnd(mod, inp, out):
+        return out.to(conv_dtype).float()
+    for name, mod in model.named_modules():
+        if isinstance(mod, (torch.nn.Conv3d, torch.nn.ReLU)) or name.endswith("downsample.1"):
+            mod.register_forward_hook(rnd)
+    return model
+
+
+def test_resnet3d_lockstep_step_matches_per_client_autograd():
+    """A 4-stage Bottleneck 3D ResNet (one block per stage, every block with a projection) on 72x80x72 volumes:
+    enough voxels per BatchNorm statistic that bf16 rounding does not swamp the comparison (the full ResNet-50 is
+    wiring-checked in fp32 by tests/test_cpu_resnet3d.py; its deepest BN layers see 16 voxels per channel)."""
+    from torch.func import functional_call
+    from neuroimagedisttraining_amd.engine.executor import padded_rows
+    from neuroimagedisttraining_amd.engine.resnet3d_hip import ResNet3DHipEngine
+    from neuroimagedisttraining_amd.models.resnet3d import Bottleneck, ResNet3D
+    dev = _dev()
+    torch.manual_seed(0)
+    G, B = 2, 2
+    vol = torch.randint(0, 256, (G * B, 72, 80, 72), dtype=torch.uint8, device=dev)
+    lab = torch.tensor([0.0, 1.0, 1.0, 0.0], device=dev)
+    resnet3d_50 = lambda num_classes: ResNet3D(Bottleneck, [1, 1, 1, 1], num_classes)  # noqa: E731
+    m = resnet3d_50(num_classes=1)
+    eng = ResNet3DHipEngine(m, vol, lab, dev)
+    L, Lb = eng.players, eng.blayers
+    flat = torch.cat([p.detach().reshape(-1) for p in m.parameters()]).to(dev)
+    bflat = torch.cat([b.detach().float().reshape(-1) for b in m.buffers()]).to(dev)
+    th, gr = padded_rows(G, L.total, dev), padded_rows(G, L.total, dev)
+    bu = padded_rows(G, Lb.total, dev)
+    th.copy_(flat.expand(G, -1))
+    bu.copy_(bflat.expand(G, -1))
+    idx = torch.arange(G * B, dtype=torch.int32, device=dev)
+    losses = eng.train_step(th, bu, gr, idx, G, B, 1.0, 0)
+    torch.cuda.synchronize()
+    mref = _bf16_faithful(resnet3d_50(num_classes=1).to(dev))
+    mref.train()
+    conv_names = {n + ".weight" for n, mod in mref.named_modules() if isinstance(mod, torch.nn.Conv3d)}
+    for g in range(G):
+        row = flat.clone().requires_grad_(True)
+        pv = {n: (row[o:o + L.numel(i)].view(L.shapes[i]).to(torch.bfloat16).float() if n in conv_names else
+                  row[o:o + L.numel(i)].view(L.shapes[i])) for i, (n, o) in enumerate(zip(L.names, L.offsets))}
+        bv = {n: bflat[o:o + Lb.numel(i)].view(Lb.shapes[i]).clone().to(Lb.dtypes[i])
+              for i, (n, o) in enumerate(zip(Lb.names, Lb.offsets))}
+        x = (vol[g * B:(g + 1) * B].float().unsqueeze(1) / 255.0).to(torch.bfloat16).float()
+        out = functional_call(mref, {**pv, **bv}, (x,))
+        loss = F.binary_cross_entropy_with_logits(out.view(-1), lab[g * B:(g + 1) * B])
+        loss.backward()
+        assert abs(float(loss) - float(losses[g])) < 0.02, (float(loss), float(losses[g]))
+        for i, (n, o) in enumerate(zip(L.names, L.offsets)):
+            if n.endswith("conv2.weight") or n in ("conv1.weight", "fc.weight"):
+                a, b = gr[g, o:o + L.numel(i)], row.grad[o:o + L.numel(i)]
+                cos = float(a @ b / (a.norm() * b.norm()))
+                assert cos > 0.9, (n, cos)
+        # running statistics advanced like nn.BatchNorm3d
+        for i, (n, o) in enumerate(zip(Lb.names, Lb.offsets)):
+            if n.endswith("running_mean"):
+                assert torch.allclose(bu[g, o:o + Lb.numel(i)], bv[n].float(), atol=2e-2, rtol=5e-2), n
+    lg = eng.eval_logits(th, bu, idx, G, B)
+    assert lg.shape == (G * B, 1) and torch.isfinite(lg).all()

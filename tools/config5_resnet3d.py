@@ -1,9 +1,11 @@
 """BASELINE config 5: 3D ResNet-50 on full-resolution 1x121x145x121 volumes, many clients, sparse update exchange.
 
 Clients are sharded over the ranks (one process per GPU, RCCL); every client trains a 3D ResNet-50 (Bottleneck
-[3,4,6,3], stage activation checkpointing, bf16 autocast) on its own synthetic ABCD-shape volumes through the
-generic TorchEngine, and the server update is FedAvg over top-k sparsified client updates exchanged with a
-fixed-size all-gather (``FLConfig.update_topk``).  Client rows (params, grads, BN buffers) stay resident in HBM:
+[3,4,6,3]) on its own synthetic ABCD-shape volumes and the server update is FedAvg over top-k sparsified client
+updates exchanged with a fixed-size all-gather (``FLConfig.update_topk``).  ``--engine hip`` (default): the
+client-batched engine (engine/resnet3d_hip.py: ``--group`` clients per lockstep launch, every bottleneck conv and
+BatchNorm on the hand-written kernels); ``--engine torch``: the generic per-client TorchEngine (bf16 autocast,
+stage checkpointing; ``--no-hip-convs`` = all MIOpen), the comparison row.  Client rows (params, grads, BN buffers) stay resident in HBM:
 the script reports the per-GPU peak so the 288 GB sizing can be checked (256 clients x 46 M params x 8 B of
 fp32 params + grads = 94 GB on one GPU, 12 GB per GPU on 8).
 
@@ -31,6 +33,8 @@ def main():
     ap.add_argument("--epochs", type=int, default=1)
     ap.add_argument("--topk", type=float, default=0.01)
     ap.add_argument("--width", type=int, default=64)
+    ap.add_argument("--engine", default="hip", choices=["hip", "torch"])
+    ap.add_argument("--group", type=int, default=32, help="clients per lockstep launch (hip engine)")
     ap.add_argument("--no-hip-convs", action="store_true",
                     help="keep every Conv3d on MIOpen (default: eligible 3x3x3 convs run on the HIP kernels)")
     args = ap.parse_args()
@@ -45,14 +49,21 @@ def main():
                                           args.test_per_client, dev, seed=7)
     splits = [local.get(c) or ClientSplit(np.zeros(args.train_per_client, np.int64),
                                           np.zeros(args.test_per_client, np.int64)) for c in range(args.clients)]
-    model = resnet3d_50(num_classes=1, checkpoint_stages=True, width=args.width)
     n_hip = 0
-    if dev.type == "cuda" and not args.no_hip_convs:
-        from neuroimagedisttraining_amd.ops.modules import use_hip_convs
-        n_hip = use_hip_convs(model)  # 13 of the 16 bottleneck 3x3x3 convs -> nidt::conv3d_k3
-    eng = TorchEngine(model, vol, labels, dev, loss="bce", amp=True)
+    if args.engine == "hip":
+        from neuroimagedisttraining_amd.engine.resnet3d_hip import ResNet3DHipEngine
+        model = resnet3d_50(num_classes=1, width=args.width)
+        eng = ResNet3DHipEngine(model, vol, labels, dev)
+        n_hip = "all bottleneck convs + BN (client-batched)"
+    else:
+        model = resnet3d_50(num_classes=1, checkpoint_stages=True, width=args.width)
+        if dev.type == "cuda" and not args.no_hip_convs:
+            from neuroimagedisttraining_amd.ops.modules import use_hip_convs
+            n_hip = use_hip_convs(model)  # 13 of the 16 bottleneck 3x3x3 convs -> nidt::conv3d_k3
+        eng = TorchEngine(model, vol, labels, dev, loss="bce", amp=True)
     cfg = FLConfig(comm_round=args.rounds, epochs=args.epochs, batch_size=args.batch, lr=0.01, frac=1.0,
-                   seed=7, update_topk=args.topk, frequency_of_the_test=1, test_batch=8)
+                   seed=7, update_topk=args.topk, frequency_of_the_test=1, test_batch=8,
+                   group=args.group if args.engine == "hip" else 0)
     runner = FLRunner(eng, splits, cfg, info, model, algorithm="fedavg")
     if dev.type == "cuda":
         torch.cuda.synchronize()
@@ -68,7 +79,8 @@ def main():
     dt = rt.max_over_ranks(time.perf_counter() - t0, info)
     peak = torch.cuda.max_memory_allocated() / 2 ** 30 if dev.type == "cuda" else 0.0
     if info.is_main:
-        print(json.dumps({"config": "3D ResNet-50 full-res, sparse top-k all-gather", "clients": args.clients,
+        print(json.dumps({"config": "3D ResNet-50 full-res, sparse top-k all-gather", "engine": args.engine,
+                          "group": args.group if args.engine == "hip" else None, "clients": args.clients,
                           "ranks": info.world, "params": runner.P, "rounds": args.rounds,
                           "s_per_round": round(dt / args.rounds, 2),
                           "s_round_each": [round(x, 2) for x in per_round], "hip_convs": n_hip,
