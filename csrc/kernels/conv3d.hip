@@ -568,6 +568,17 @@ static void launch_fwd_dma(int nst, dim3 g, hipStream_t s, const ConvFwdArgs& a,
   hipLaunchKernelGGL((k_conv_fwd_dma<BC, WM, WN, 2, BI, ST>), g, dim3(64 * WM * WN), 0, s, a, nCO);
 }
 
+// output channels per forward block: 128 (8 waves, one resident block per CU) where Cout allows, else 64 (4 waves,
+// two blocks per CU).  NIDT_FWD_BCO=64 forces 64-channel blocks everywhere (A/B).
+static int fwd_bco(int Cout) {
+  static const int env = [] {
+    const char* e = getenv("NIDT_FWD_BCO");
+    return e ? atoi(e) : 0;
+  }();
+  if (env == 64) return 64;
+  return (Cout % 128 == 0) ? 128 : 64;
+}
+
 // output extent of one dimension: taps k (3 or 1), stride st, padding p
 static inline int conv_out_dim(int n, int k, int st, int p) { return (n + 2 * p - k) / st + 1; }
 
@@ -603,7 +614,7 @@ static void conv3d_fwd_impl(uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t 
   a.bias_ld = bias_ld;
   const bool xf = xs != 0, hb = bias != 0, st = stats != 0;
   NIDT_REQUIRE(!st || hb, "conv3d_fwd: statistics require a bias");
-  const int bco = (Cout % 128 == 0) ? 128 : 64;
+  const int bco = fwd_bco(Cout);
   hipStream_t s = as_stream(stream);
   if (!xf && Cin % 64 == 0) {
     // 256 positions per block: BCO=128 -> 8 waves (2 co x 4 pos, 512 threads), BCO=64 -> 4 waves (1 x 4);
@@ -703,7 +714,7 @@ int conv3d_fwd_ksplit(int Cin, int Cout, int G, int Mg) {
     const char* e = getenv("NIDT_FWD_KSPLIT");
     return e ? atoi(e) : 0;
   }();
-  const int bco = (Cout % 128 == 0) ? 128 : 64;
+  const int bco = fwd_bco(Cout);
   const int64_t nwg = (int64_t)ceil_div(Mg, 256) * (Cout / bco) * G;
   if (env <= 1 || nwg >= 512) return 1;
   int ks = env;
@@ -713,7 +724,7 @@ int conv3d_fwd_ksplit(int Cin, int Cout, int G, int Mg) {
 // positions per block (= per BN-statistics block) of conv3d_fwd for this layer shape and client count
 int conv3d_fwd_bp(int Cin, int Cout, int xf, int G, int Mg) {
   if (xf || Cin % 64 != 0) return kFwdBP;
-  const int bco = (Cout % 128 == 0) ? 128 : 64;
+  const int bco = fwd_bco(Cout);
   const int64_t nwg256 = (int64_t)ceil_div(Mg, 256) * (Cout / bco) * G;
   static const int thresh = [] {
     const char* e = getenv("NIDT_FWD_BP_THRESH");

@@ -42,6 +42,9 @@ def main(root, out=None):
         if c.get("SQ_BUSY_CYCLES") and c.get("SQ_VALU_MFMA_BUSY_CYCLES"):
             # SQ_VALU_MFMA_BUSY_CYCLES is summed over SIMDs; SQ_BUSY_CYCLES over SEs (quad-cycles per SE)
             d.append("mfma_busy_per_simd_cycles=%.0f" % (c["SQ_VALU_MFMA_BUSY_CYCLES"] / 1024))
+            if c.get("GRBM_GUI_ACTIVE"):
+                # MFMA pipe busy fraction: busy cycles over 1024 SIMDs x elapsed cycles (GRBM_GUI_ACTIVE sums 8 XCDs)
+                d.append("MFMA_busy=%.1f%%" % (100.0 * c["SQ_VALU_MFMA_BUSY_CYCLES"] / (1024 * c["GRBM_GUI_ACTIVE"] / 8)))
         if c.get("SQ_INSTS_MFMA"):
             d.append("valu/mfma=%.2f lds/mfma=%.2f" % (c.get("SQ_INSTS_VALU", 0) / c["SQ_INSTS_MFMA"],
                                                       c.get("SQ_INSTS_LDS", 0) / c["SQ_INSTS_MFMA"]))
