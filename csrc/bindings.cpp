@@ -52,6 +52,8 @@ void gn_bwd(uintptr_t dy, int dy_bf16, uintptr_t mask, uintptr_t t, uintptr_t st
 void gn_param_grads(uintptr_t part, int G, int B, int C, uintptr_t grads, int64_t ldg, int64_t off_w, int64_t off_b,
                     uintptr_t stream);
 void res_grad(uintptr_t out, uintptr_t dx1, uintptr_t dx2, uintptr_t da, uintptr_t mask, int64_t n, uintptr_t stream);
+// mpc.hip
+void modp_matmul(uintptr_t A, uintptr_t B, uintptr_t C, int M, int K, int64_t N, int64_t p, uintptr_t stream);
 // bnr.hip
 int bnr_workspace(int G, int64_t M, int C);
 void bnr_stats(uintptr_t t, int G, int64_t M, int C, float eps, float mom, uintptr_t ws, uintptr_t stats,
@@ -148,6 +150,7 @@ PYBIND11_MODULE(_nidt_hip, m) {
   DEF(gn_bwd);
   DEF(gn_param_grads);
   DEF(res_grad);
+  DEF(modp_matmul);
   DEF(bnr_workspace);
   DEF(bnr_stats);
   DEF(bnr_eval_stats);

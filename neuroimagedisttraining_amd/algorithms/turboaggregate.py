@@ -44,10 +44,31 @@ def gen_Lagrange_coeffs(alpha_s, beta_s, p, is_K1=0):  # noqa: N802
     return U
 
 
+# model-sized encodings (U [N x K] @ X [K x d], d in the millions) go to the gfx950 kernel when a GPU is present
+DEVICE_MIN_ELEMS = 1 << 16
+
+
+def matmul_mod_device(A, B, p, device="cuda"):
+    """(A @ B) mod p on the GPU (``mpc.hip`` ``modp_matmul``): int64 operands reduced to [0, p), p < 2^32."""
+    import torch
+    from .. import ops
+    A = torch.as_tensor(np.asarray(A, dtype=np.int64) % p).to(device).contiguous()
+    B = torch.as_tensor(np.asarray(B, dtype=np.int64) % p).to(device).contiguous()
+    C = torch.empty((A.shape[0], B.shape[1]), dtype=torch.int64, device=device)
+    ops.ext().modp_matmul(A.data_ptr(), B.data_ptr(), C.data_ptr(), A.shape[0], A.shape[1], B.shape[1], int(p),
+                          torch.cuda.current_stream().cuda_stream)
+    return C.cpu().numpy()
+
+
 def _matmul_mod(A, B, p):
-    """(A @ B) mod p without int64 overflow (row-by-row accumulation of reduced products)."""
+    """(A @ B) mod p without int64 overflow (row-by-row accumulation of reduced products); large products on the
+    GPU kernel."""
     A = np.asarray(A, dtype=np.int64) % p
     B = np.asarray(B, dtype=np.int64) % p
+    if B.size >= DEVICE_MIN_ELEMS and p < (1 << 32):
+        import torch
+        if torch.cuda.is_available():
+            return matmul_mod_device(A, B, p)
     out = np.zeros((A.shape[0], B.shape[1]), dtype=np.int64)
     for k in range(A.shape[1]):
         out = (out + (A[:, k:k + 1] * B[k:k + 1, :]) % p) % p

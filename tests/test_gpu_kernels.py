@@ -590,3 +590,19 @@ def test_hip_graph_local_steps_match_eager():
         outs.append((r.w_global.clone(), r.b_global.clone(), r.stat_info["global_test_acc"]))
     assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
     assert outs[0][2] == outs[1][2]
+
+
+def test_modp_matmul_matches_numpy():
+    """K22: TurboAggregate's mod-p encoding product on the GPU == the exact host reference."""
+    import numpy as np
+    from neuroimagedisttraining_amd.algorithms import turboaggregate as TA
+    rng = np.random.RandomState(0)
+    p = 2 ** 31 - 1
+    A = rng.randint(0, p, size=(7, 5)).astype(np.int64)
+    B = rng.randint(0, p, size=(5, 70001)).astype(np.int64)
+    ref = np.zeros((7, 70001), dtype=np.int64)
+    for k in range(5):
+        ref = (ref + (A[:, k:k + 1] * B[k:k + 1, :]) % p) % p
+    got = TA.matmul_mod_device(A, B, p)
+    assert np.array_equal(got, ref)
+    assert np.array_equal(TA._matmul_mod(A, B, p), ref)  # dispatches to the device above the size threshold
