@@ -121,6 +121,7 @@ def main():
     torch.cuda.synchronize()
     for k in runner.timers:
         runner.timers[k] = 0.0
+    runner.record_train_events, runner.train_events = True, []
     t0 = time.perf_counter()
     res = None
     for r in range(args.warmup, args.warmup + args.steps):
@@ -132,6 +133,10 @@ def main():
     dt = time.perf_counter() - t0
     per_rank = rt.all_gather_cat(torch.tensor([t_local], dtype=torch.float64, device=info.device), info)
     per_rank = [round(float(x), 4) for x in per_rank.cpu()]
+    # GPU time each rank spent in local training (CUDA events, no syncs in the timed loop): the load balance
+    t_train = sum(a.elapsed_time(b) for a, b in runner.train_events) / 1000.0
+    per_rank_train = rt.all_gather_cat(torch.tensor([t_train], dtype=torch.float64, device=info.device), info)
+    per_rank_train = [round(float(x), 4) for x in per_rank_train.cpu()]
     dt = rt.max_over_ranks(dt, info)
     ms = dt * 1000.0 / max(1, args.steps)
     value = args.steps / dt
@@ -166,8 +171,10 @@ def main():
                        "rebalance": rebalance,
                        "parallelism": "clients-sharded-dp%d" % info.world},
             "setup_s": {"data": round(t_data, 2), "snip_mask": round(t_snip, 2)},
-            "rank_busy_s": per_rank,
-            "rank_imbalance": round(max(per_rank) / (sum(per_rank) / len(per_rank)), 3) if per_rank else None,
+            "rank_wall_s": per_rank,
+            "rank_train_gpu_s": per_rank_train,
+            "rank_imbalance": (round(max(per_rank_train) / (sum(per_rank_train) / len(per_rank_train)), 3)
+                               if per_rank_train and sum(per_rank_train) > 0 else None),
             "last_round_metrics": res,
         }
         if args.phase_timers:

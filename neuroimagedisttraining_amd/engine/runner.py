@@ -128,6 +128,8 @@ class FLRunner:
         # captured steps kept (LRU); engines whose graphs own their activation memory (torch-allocated, e.g. the
         # ResNet engine) set a small limit, the AlexNet engine's graphs only reference its persistent buffers
         self.max_graphs = int(getattr(engine, "graph_cache_limit", 512))
+        self.record_train_events = False  # bench: CUDA events around every local-training call (no host syncs)
+        self.train_events = []
         self._lr_dev = self._seed_dev = None
         self._scratch = None
         self._eval_cache = None
@@ -242,6 +244,16 @@ class FLRunner:
         if not rows:
             return
         spec = spec or StepSpec()
+        if self.record_train_events and self.device.type == "cuda":  # per-rank GPU time of local training (bench)
+            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            ev[0].record()
+            self._train_rows(rs, rows, clients, round_idx, epochs, spec, tag, epoch_hook, lr)
+            ev[1].record()
+            self.train_events.append(ev)
+            return
+        self._train_rows(rs, rows, clients, round_idx, epochs, spec, tag, epoch_hook, lr)
+
+    def _train_rows(self, rs, rows, clients, round_idx, epochs, spec, tag, epoch_hook, lr):
         if _contiguous(rows):
             lo, hi = rows[0], rows[-1] + 1
             self._train_view(rs.rows(lo, hi), clients, round_idx, epochs, spec.rows(lo, hi), tag, epoch_hook, lr)
@@ -453,7 +465,9 @@ class FLRunner:
         stays there until a later round moves it again.  Results do not depend on where a client trains."""
         if not (self.cfg.rebalance and self.info.enabled and self.info.world > 1):
             return
+        t0 = time.perf_counter()
         self.migrate(self.balanced_owner(sampled))
+        self.timers["migrate"] = self.timers.get("migrate", 0.0) + time.perf_counter() - t0
 
     def migrate(self, new_owner):
         new_owner = np.asarray(new_owner, dtype=np.int64)

@@ -132,6 +132,9 @@ def exchange_rows(info: DistInfo, owner, needs, row_of, width, device, dtype=tor
     if not info.enabled:
         return {}
     import torch.distributed as dist
+    # gloo moves device tensors through slow internal staging: stage through host memory ourselves (the RCCL
+    # path sends the device rows directly over xGMI)
+    stage = info.backend == "gloo" and torch.device(device).type == "cuda"
     p2p, recv = [], {}
     for r in range(info.world):
         for c in sorted(set(needs[r])):
@@ -139,14 +142,17 @@ def exchange_rows(info: DistInfo, owner, needs, row_of, width, device, dtype=tor
             if o == r:
                 continue
             if o == info.rank:
-                p2p.append(dist.P2POp(dist.isend, row_of(c).contiguous(), r))
+                t = row_of(c).contiguous()
+                p2p.append(dist.P2POp(dist.isend, t.cpu() if stage else t, r))
             if r == info.rank:
-                buf = torch.empty(width, dtype=dtype, device=device)
+                buf = torch.empty(width, dtype=dtype, device="cpu" if stage else device)
                 recv[c] = buf
                 p2p.append(dist.P2POp(dist.irecv, buf, o))
     if p2p:
         for q in dist.batch_isend_irecv(p2p):
             q.wait()
+    if stage:
+        recv = {c: b.to(device) for c, b in recv.items()}
     return recv
 
 
