@@ -559,11 +559,18 @@ class FLRunner:
         rows, loc = self._local_rows(sampled)
         vals = torch.zeros((len(rows), k), dtype=torch.float32, device=self.device)
         idx = torch.zeros((len(rows), k), dtype=torch.int32, device=self.device)
-        for j, r in enumerate(rows):
-            d = self.theta[r, :self.P] - self.w_global
-            top = torch.topk(d.abs(), k, sorted=False).indices
-            idx[j] = top.int()
-            vals[j] = d.index_select(0, top) * (self.sizes[self.local[r]] / n_tot)
+        # batched top-k over chunks of rows (one selection launch per chunk instead of per client; chunks bound the
+        # [rows, P] temporaries: 8 x 46 M fp32 = 1.5 GB for the 3D ResNet-50)
+        chunk = max(1, min(len(rows), int(2e9 // (4 * max(1, self.P)))))
+        for j0 in range(0, len(rows), chunk):
+            rr = rows[j0:j0 + chunk]
+            ix = torch.tensor(rr, device=self.device)
+            d = self.theta.index_select(0, ix)[:, :self.P] - self.w_global
+            top = torch.topk(d.abs(), k, dim=1, sorted=False).indices
+            wts = torch.tensor([self.sizes[self.local[r]] / n_tot for r in rr], dtype=torch.float32,
+                               device=self.device)
+            idx[j0:j0 + len(rr)] = top.int()
+            vals[j0:j0 + len(rr)] = d.gather(1, top) * wts[:, None]
         cid = torch.tensor(loc, dtype=torch.float32, device=self.device)
         g_vals = rt.all_gather_cat(vals.view(-1), self.info).view(-1, k)
         g_idx = rt.all_gather_cat(idx.view(-1), self.info).view(-1, k).long()
