@@ -1119,7 +1119,10 @@ __global__ __launch_bounds__(256 * NCH, 2 / NCH) void k_conv_wgrad_dma(ConvWgDma
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // retire this step's LDS-DMA (next stage) but leave the XI position-table loads for step st+2 in flight: they
+    // are the youngest vector-memory ops and are only consumed by the next step's DMA issue
+    if (st + 2 < nsteps) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(XI) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
 #undef WD_ISSUE
