@@ -37,6 +37,9 @@ void pack_conv_w(uintptr_t theta, int64_t ldt, int64_t off, int G, int Cout, int
 void bn_relu_apply(uintptr_t y, uintptr_t sc, uintptr_t sh, uintptr_t h, int64_t npos, int C, int S, uintptr_t stream);
 void conv_fwd_g(uintptr_t x, uintptr_t w, uintptr_t y, int G, int B, int D, int H, int W, int Cin, int Cout, int kt,
                 int st, int pad, int padd, uintptr_t stream);
+int conv_fwd_g_ksplit(int G, int B, int D, int H, int W, int Cin, int Cout, int kt, int st, int pad, int padd);
+void conv_fwd_gk(uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t part, int ksplit, int G, int B, int D, int H, int W,
+                 int Cin, int Cout, int kt, int st, int pad, int padd, uintptr_t stream);
 void conv_pos_table_g(uintptr_t tab, int B, int D, int H, int W, int kt, int st, int pad, int padd, uintptr_t stream);
 void conv_wgrad_g(uintptr_t x, uintptr_t dy, uintptr_t part, uintptr_t grad, int64_t ldg, int64_t off, int G, int B,
                   int D, int H, int W, int Cin, int Cout, int kt, int st, int pad, int padd, int nsplit, float scale,
@@ -142,6 +145,8 @@ PYBIND11_MODULE(_nidt_hip, m) {
   DEF(pack_conv_w);
   DEF(bn_relu_apply);
   DEF(conv_fwd_g);
+  DEF(conv_fwd_g_ksplit);
+  DEF(conv_fwd_gk);
   DEF(conv_pos_table_g);
   DEF(conv_wgrad_g);
   DEF(conv_wgrad_nsplit_g);

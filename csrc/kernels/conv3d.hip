@@ -473,6 +473,19 @@ __global__ __launch_bounds__(64 * WM * WN, ((NST == 2 ? 8 : 4) / (WM * WN)) > 0 
   conv_fwd_epilogue<BCO, BP, WM, WN, BIAS, STATS, TCO, TP>(a, acc, red, g, pb, co0, wco, wp, fr, fq, tid);
 }
 
+// Finish of a split-K forward without bias / statistics: y = bf16(sum over the ksplit slabs), 4 values per thread
+__global__ __launch_bounds__(256) void k_fwd_splitk_sum(const float* __restrict__ part, int ksplit, int64_t n4,
+                                                        uint16_t* __restrict__ y) {
+  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n4; q += (int64_t)gridDim.x * blockDim.x) {
+    float4 acc = reinterpret_cast<const float4*>(part)[q];
+    for (int sp = 1; sp < ksplit; ++sp) {
+      const float4 v = reinterpret_cast<const float4*>(part)[sp * n4 + q];
+      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    }
+    reinterpret_cast<uint2*>(y)[q] = make_uint2(pack_bf16x2(acc.x, acc.y), pack_bf16x2(acc.z, acc.w));
+  }
+}
+
 // Finish a split-K forward: y = bf16(sum of the partials + bias) and the same per-block BN statistics as the
 // fused epilogue (block mean and M2 per channel over the block's BP positions, fp32 values before rounding).
 // Block (pb, g), 1024 threads: lane -> channel c = lane + 64 u, wave -> positions m0 + wave + 16 v; the 16 wave
@@ -625,7 +638,8 @@ static void conv3d_fwd_impl(uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t 
     a.nPB = ceil_div(a.Mg, bp);
     const int nCO = Cout / bco;
     if (ksplit > 1) {
-      NIDT_REQUIRE(part != 0 && bp == 256 && Cout <= 256, "conv3d_fwd_splitk: needs a partial buffer, 256-position blocks, Cout <= 256");
+      NIDT_REQUIRE(part != 0 && ((!hb && !st) || (bp == 256 && Cout <= 256)),
+                   "conv3d_fwd_splitk: needs a partial buffer (with bias/statistics: 256-position blocks, Cout <= 256)");
       a.ksplit = ksplit;
       a.part = ptr<float>(part);
     }
@@ -652,7 +666,12 @@ static void conv3d_fwd_impl(uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t 
 #undef NIDT_DMA_WN
 #undef NIDT_DMA
     NIDT_CHECK(hipGetLastError());
-    if (a.ksplit > 1) {
+    if (a.ksplit > 1 && !hb && !st) {  // plain sum of the partial slabs -> bf16
+      const int64_t n4 = (int64_t)G * a.Mg * Cout / 4;
+      hipLaunchKernelGGL(k_fwd_splitk_sum, dim3((unsigned)std::min<int64_t>(8192, (n4 + 255) / 256)), dim3(256), 0, s,
+                         a.part, a.ksplit, n4, a.y);
+      NIDT_CHECK(hipGetLastError());
+    } else if (a.ksplit > 1) {
       const dim3 fg(a.nPB, G);
       if (st) hipLaunchKernelGGL((k_fwd_splitk_fin<true, true>), fg, dim3(1024), 0, s, a.part, a.ksplit, a.bias, a.y, a.stats, G, a.Mg, Cout, bp, a.nPB, a.bias_ld ? a.bias_ld : (int64_t)Cout);
       else if (hb) hipLaunchKernelGGL((k_fwd_splitk_fin<true, false>), fg, dim3(1024), 0, s, a.part, a.ksplit, a.bias, a.y, a.stats, G, a.Mg, Cout, bp, a.nPB, a.bias_ld ? a.bias_ld : (int64_t)Cout);
@@ -688,6 +707,34 @@ void conv3d_fwd(uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t xs, uintptr_
 void conv3d_fwd_bld(uintptr_t x, uintptr_t w, uintptr_t bias, int64_t bias_ld, uintptr_t y, uintptr_t stats, int G, int B,
                     int D, int H, int W, int Cin, int Cout, int pad, uintptr_t stream) {
   conv3d_fwd_impl(x, w, bias, 0, 0, y, stats, G, B, D, H, W, Cin, Cout, pad, stream, 1, 0, bias_ld);
+}
+
+// Split-K factor of the general forward: grids that cannot fill the chip (few output tiles: deep layers at small
+// spatial size, few clients per GPU) but have long reductions get their k-steps split over ksplit blocks (>= 12
+// k-steps each), finished by k_fwd_splitk_sum.  NIDT_FWDG_KSPLIT=1 disables it (A/B), =k forces k.
+int conv_fwd_g_ksplit(int G, int B, int D, int H, int W, int Cin, int Cout, int kt, int st, int pad, int padd) {
+  static const int env = [] {
+    const char* e = getenv("NIDT_FWDG_KSPLIT");
+    return e ? atoi(e) : 0;
+  }();
+  const int kd = kt == 27 ? 3 : 1, khw = kt == 1 ? 1 : 3;
+  const int Mg = B * conv_out_dim(D, kd, st, padd) * conv_out_dim(H, khw, st, pad) * conv_out_dim(W, khw, st, pad);
+  const int nks = kt * Cin / 64;
+  if (env > 0) return std::max(1, std::min(env, nks));
+  const int bco = fwd_bco(Cout);
+  const int bp = conv3d_fwd_bp(Cin, Cout, 0, G, Mg);
+  const int64_t nwg = (int64_t)ceil_div(Mg, bp) * (Cout / bco) * G;
+  const int64_t slots = 256 * (bco == 128 ? 1 : 2);
+  if (nwg >= slots || nks < 24) return 1;
+  const int ks = (int)std::min<int64_t>(std::min<int64_t>(ceil_div(2 * slots, nwg), nks / 12), 8);
+  return std::max(1, ks);
+}
+
+// General client-grouped conv forward with split-K partials (part: ksplit * G * Mg * Cout fp32, ksplit > 1)
+void conv_fwd_gk(uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t part, int ksplit, int G, int B, int D, int H, int W,
+                 int Cin, int Cout, int kt, int st, int pad, int padd, uintptr_t stream) {
+  NIDT_REQUIRE(Cin % 64 == 0, "conv_fwd_gk: Cin must be a multiple of 64 (pad the channels)");
+  conv3d_fwd_impl(x, w, 0, 0, 0, y, 0, G, B, D, H, W, Cin, Cout, pad, stream, ksplit, part, 0, kt, st, padd);
 }
 
 // General client-grouped conv forward (no bias / statistics): kt taps (27, 9 = 2-D 3x3 on D = 1 volumes, 1 = 1x1),

@@ -38,6 +38,20 @@ def _stream():
     return torch.cuda.current_stream().cuda_stream
 
 
+def conv_fwd(x_ptr, w_ptr, y_ptr, G, B, D, H, W, Cin, Cout, kt, st, pad, padd, device):
+    """Client-grouped conv forward (``conv_fwd_g``), split over the reduction when the output grid is too small to
+    fill the chip (``conv_fwd_g_ksplit``: deep layers at small spatial size, few clients per GPU)."""
+    m = ops.ext()
+    ks = m.conv_fwd_g_ksplit(G, B, D, H, W, Cin, Cout, kt, st, pad, padd)
+    if ks <= 1:
+        m.conv_fwd_g(x_ptr, w_ptr, y_ptr, G, B, D, H, W, Cin, Cout, kt, st, pad, padd, _stream())
+        return
+    kd, khw = (3 if kt == 27 else 1), (1 if kt == 1 else 3)
+    Mg = B * ((D + 2 * padd - kd) // st + 1) * ((H + 2 * pad - khw) // st + 1) * ((W + 2 * pad - khw) // st + 1)
+    part = torch.empty(ks * G * Mg * Cout, device=device, dtype=torch.float32)
+    m.conv_fwd_gk(x_ptr, w_ptr, y_ptr, part.data_ptr(), ks, G, B, D, H, W, Cin, Cout, kt, st, pad, padd, _stream())
+
+
 class GroupedConv:
     """One conv layer of the client-grouped network (weights = rows of theta at ``off``, PyTorch layout
     ``[Cout, cin, k, k]``).  ``cin_p`` = channels of the activation tensor (cin zero-padded to 64)."""
@@ -79,8 +93,8 @@ class GroupedConv:
         wp, wt = self._wp(theta, G, train and self.need_dgrad)
         self._packed = (theta.data_ptr(), G, wt) if train else None
         y = torch.empty(N, Ho, Wo, self.cout, device=x.device, dtype=torch.bfloat16)
-        ops.ext().conv_fwd_g(x.data_ptr(), wp.data_ptr(), y.data_ptr(), G, N // G, 1, H, W, self.cin_p, self.cout,
-                             self.kt, self.stride, self.pad, 0, _stream())
+        conv_fwd(x.data_ptr(), wp.data_ptr(), y.data_ptr(), G, N // G, 1, H, W, self.cin_p, self.cout,
+                 self.kt, self.stride, self.pad, 0, x.device)
         return y
 
     def _torch_fwd(self, x, w, G):
@@ -124,21 +138,21 @@ class GroupedConv:
             _, wt = self._wp(theta, G, True)
         dx = torch.empty(N, H, W, self.cin_p, device=x.device, dtype=torch.bfloat16)
         if self.stride == 1:
-            m.conv_fwd_g(dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), G, B, 1, Ho, Wo, self.cout, self.cin_p, self.kt,
-                         1, self.k - 1 - self.pad, 0, st)
+            conv_fwd(dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), G, B, 1, Ho, Wo, self.cout, self.cin_p, self.kt,
+                         1, self.k - 1 - self.pad, 0, x.device)
         elif self.k == 3:
             # stride 2: dX = conv(zero-upsampled dY, flipped W^T, pad k-1-pad) (H = 2 Ho for the even CIFAR maps)
             assert H == 2 * Ho and W == 2 * Wo and self.pad == 1, (H, W, Ho, Wo)
             up = torch.zeros(N, H, W, self.cout, device=x.device, dtype=torch.bfloat16)
             up[:, ::2, ::2] = dy
-            m.conv_fwd_g(up.data_ptr(), wt.data_ptr(), dx.data_ptr(), G, B, 1, H, W, self.cout, self.cin_p, self.kt,
-                         1, 1, 0, st)
+            conv_fwd(up.data_ptr(), wt.data_ptr(), dx.data_ptr(), G, B, 1, H, W, self.cout, self.cin_p, self.kt,
+                         1, 1, 0, x.device)
         else:
             # 1x1 stride 2: only the even pixels were read: dX there = W^T dY, zero elsewhere
             assert self.k == 1 and self.pad == 0 and (H + 1) // 2 == Ho and (W + 1) // 2 == Wo
             sub = torch.empty(N, Ho, Wo, self.cin_p, device=x.device, dtype=torch.bfloat16)
-            m.conv_fwd_g(dy.data_ptr(), wt.data_ptr(), sub.data_ptr(), G, B, 1, Ho, Wo, self.cout, self.cin_p, 1, 1,
-                         0, 0, st)
+            conv_fwd(dy.data_ptr(), wt.data_ptr(), sub.data_ptr(), G, B, 1, Ho, Wo, self.cout, self.cin_p, 1, 1,
+                         0, 0, x.device)
             dx.zero_()
             dx[:, ::2, ::2] = sub
         return dx

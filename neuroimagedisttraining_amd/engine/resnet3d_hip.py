@@ -32,6 +32,20 @@ def _stream():
     return torch.cuda.current_stream().cuda_stream
 
 
+def conv_fwd(x_ptr, w_ptr, y_ptr, G, B, D, H, W, Cin, Cout, kt, st, pad, padd, device):
+    """Client-grouped conv forward (``conv_fwd_g``), split over the reduction when the output grid is too small to
+    fill the chip (``conv_fwd_g_ksplit``: deep layers at small spatial size, few clients per GPU)."""
+    m = ops.ext()
+    ks = m.conv_fwd_g_ksplit(G, B, D, H, W, Cin, Cout, kt, st, pad, padd)
+    if ks <= 1:
+        m.conv_fwd_g(x_ptr, w_ptr, y_ptr, G, B, D, H, W, Cin, Cout, kt, st, pad, padd, _stream())
+        return
+    kd, khw = (3 if kt == 27 else 1), (1 if kt == 1 else 3)
+    Mg = B * ((D + 2 * padd - kd) // st + 1) * ((H + 2 * pad - khw) // st + 1) * ((W + 2 * pad - khw) // st + 1)
+    part = torch.empty(ks * G * Mg * Cout, device=device, dtype=torch.float32)
+    m.conv_fwd_gk(x_ptr, w_ptr, y_ptr, part.data_ptr(), ks, G, B, D, H, W, Cin, Cout, kt, st, pad, padd, _stream())
+
+
 class GConv3:
     """Client-grouped Conv3d (k = 1 or 3, stride 1/2, no bias) on channels-last ``[N, D, H, W, C]`` bf16."""
 
@@ -72,8 +86,8 @@ class GConv3:
         wp, wt = self._wp(theta, G, train)
         self._packed = (theta.data_ptr(), G, wt) if train else None
         y = torch.empty(N, Do, Ho, Wo, self.cout, device=x.device, dtype=torch.bfloat16)
-        ops.ext().conv_fwd_g(x.data_ptr(), wp.data_ptr(), y.data_ptr(), G, N // G, D, H, W, self.cin, self.cout,
-                             self.kt, self.stride, self.pad, self.pad if self.kt == 27 else 0, _stream())
+        conv_fwd(x.data_ptr(), wp.data_ptr(), y.data_ptr(), G, N // G, D, H, W, self.cin, self.cout,
+                 self.kt, self.stride, self.pad, self.pad if self.kt == 27 else 0, x.device)
         return y
 
     def bwd(self, dy, x, theta, grads, G, need_dx=True):
@@ -106,23 +120,23 @@ class GConv3:
         if self.stride == 1:
             dx = torch.empty(N, D, H, W, self.cin, device=x.device, dtype=torch.bfloat16)
             p2 = self.k - 1 - self.pad
-            m.conv_fwd_g(dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), G, B, Do, Ho, Wo, self.cout, self.cin, self.kt,
-                         1, p2, p2 if self.kt == 27 else 0, st)
+            conv_fwd(dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), G, B, Do, Ho, Wo, self.cout, self.cin, self.kt,
+                         1, p2, p2 if self.kt == 27 else 0, x.device)
             return dx
         if self.k == 3:
             # stride 2, pad 1: dX = conv(zero-upsampled dY [2Do, 2Ho, 2Wo], flipped W^T, pad 1), cropped to D x H x W
             up = torch.zeros(N, 2 * Do, 2 * Ho, 2 * Wo, self.cout, device=x.device, dtype=torch.bfloat16)
             up[:, ::2, ::2, ::2] = dy
             full = torch.empty(N, 2 * Do, 2 * Ho, 2 * Wo, self.cin, device=x.device, dtype=torch.bfloat16)
-            m.conv_fwd_g(up.data_ptr(), wt.data_ptr(), full.data_ptr(), G, B, 2 * Do, 2 * Ho, 2 * Wo, self.cout,
-                         self.cin, 27, 1, 1, 1, st)
+            conv_fwd(up.data_ptr(), wt.data_ptr(), full.data_ptr(), G, B, 2 * Do, 2 * Ho, 2 * Wo, self.cout,
+                         self.cin, 27, 1, 1, 1, x.device)
             if (2 * Do, 2 * Ho, 2 * Wo) == (D, H, W):
                 return full
             return full[:, :D, :H, :W].contiguous()
         # 1x1 stride 2: dX at the even voxels = W^T dY, zero elsewhere
         sub = torch.empty(N, Do, Ho, Wo, self.cin, device=x.device, dtype=torch.bfloat16)
-        m.conv_fwd_g(dy.data_ptr(), wt.data_ptr(), sub.data_ptr(), G, B, Do, Ho, Wo, self.cout, self.cin, 1, 1, 0, 0,
-                     st)
+        conv_fwd(dy.data_ptr(), wt.data_ptr(), sub.data_ptr(), G, B, Do, Ho, Wo, self.cout, self.cin, 1, 1, 0, 0,
+                 x.device)
         dx = torch.zeros(N, D, H, W, self.cin, device=x.device, dtype=torch.bfloat16)
         dx[:, ::2, ::2, ::2] = sub
         return dx

@@ -63,6 +63,41 @@ def test_grouped_conv2d_fwd_dgrad_wgrad(cin, cout, k, stride, pad, hw):
         assert _rel(dx.permute(0, 3, 1, 2)[:, :cin], xr.grad) < 2e-2
 
 
+@pytest.mark.parametrize("cin,cout,k,stride,pad,hw", [(512, 512, 3, 1, 1, 4), (256, 256, 3, 1, 1, 8),
+                                                      (256, 512, 3, 2, 1, 8)])
+def test_conv_fwd_splitk_matches_single_pass(cin, cout, k, stride, pad, hw):
+    """Split-K forward (``conv_fwd_gk``, partial sums + k_fwd_splitk_sum) at several split factors against the
+    single-pass kernel and fp32 PyTorch; the small-grid deep layers pick ks > 1 by themselves."""
+    from neuroimagedisttraining_amd import ops
+    from neuroimagedisttraining_amd.engine.resnet2d_hip import GroupedConv, _stream
+    dev = _dev()
+    m = ops.ext()
+    torch.manual_seed(cin + cout + stride)
+    G, B = 3, 2
+    conv = GroupedConv(0, cout, cin, k, stride, pad, hip=True)
+    kt = k * k
+    assert m.conv_fwd_g_ksplit(G, B, 1, hw, hw, cin, cout, kt, stride, pad, 0) > 1
+    theta = torch.randn(G, conv.numel, device=dev) * (2.0 / (cin * kt)) ** 0.5
+    wp, _ = conv._wp(theta, G, False)
+    x = torch.randn(G * B, hw, hw, cin, device=dev).to(torch.bfloat16)
+    Ho, Wo = conv.out_hw(hw, hw)
+    y1 = torch.empty(G * B, Ho, Wo, cout, device=dev, dtype=torch.bfloat16)
+    m.conv_fwd_g(x.data_ptr(), wp.data_ptr(), y1.data_ptr(), G, B, 1, hw, hw, cin, cout, kt, stride, pad, 0,
+                 _stream())
+    xr = x.float().permute(0, 3, 1, 2)
+    wr = theta.view(G, cout, cin, k, k).to(torch.bfloat16).float()
+    ref = torch.cat([F.conv2d(xr[g * B:(g + 1) * B], wr[g], stride=stride, padding=pad) for g in range(G)])
+    for ks in (2, 5, 8):
+        part = torch.full((ks * G * B * Ho * Wo * cout,), float("nan"), device=dev)
+        yk = torch.empty_like(y1)
+        m.conv_fwd_gk(x.data_ptr(), wp.data_ptr(), yk.data_ptr(), part.data_ptr(), ks, G, B, 1, hw, hw, cin, cout, kt,
+                      stride, pad, 0, _stream())
+        torch.cuda.synchronize()
+        assert torch.isfinite(yk.float()).all(), ks
+        assert _rel(yk, y1) < 1e-2, ks
+        assert _rel(yk.permute(0, 3, 1, 2), ref) < 1e-2, ks
+
+
 def test_resnet18gn_train_step_matches_cpu_twin():
     from neuroimagedisttraining_amd.engine.executor import padded_rows
     from neuroimagedisttraining_amd.engine.resnet2d_hip import ResNetHipEngine, synthetic_cifar
