@@ -633,6 +633,21 @@ __host__ __device__ constexpr int tp_count(int t) {
   return (t / 9 < 2 ? 2 : 1) * ((t / 3) % 3 < 2 ? 2 : 1) * (t % 3 < 2 ? 2 : 1);
 }
 
+// byte b of w as fp32: one v_cvt_f32_ubyteN.  Written out because the compiler merges the two dwords of a
+// ds_read_b64 into one 64-bit value for some tap sets and then converts (w64 >> 8n) & 0xff through the u64->f32
+// sequence (lshl_b64, min, or, cvt_f32_u32, ldexp: ~5 VALU per byte, ~20 extra per cell on waves 1-2, which
+// pace the block's per-stage barrier).
+__device__ __forceinline__ float u8f(uint32_t w, int b) {
+  float f;
+  switch (b) {
+    case 0: asm("v_cvt_f32_ubyte0 %0, %1" : "=v"(f) : "v"(w)); break;
+    case 1: asm("v_cvt_f32_ubyte1 %0, %1" : "=v"(f) : "v"(w)); break;
+    case 2: asm("v_cvt_f32_ubyte2 %0, %1" : "=v"(f) : "v"(w)); break;
+    default: asm("v_cvt_f32_ubyte3 %0, %1" : "=v"(f) : "v"(w)); break;
+  }
+  return f;
+}
+
 template <int W>
 __device__ __forceinline__ void conv1_wg_wave(const uint8_t* __restrict__ xs, const uint16_t* __restrict__ dp,
                                               const uint16_t* __restrict__ pout, const uint8_t* __restrict__ amax,
@@ -689,8 +704,7 @@ __device__ __forceinline__ void conv1_wg_wave(const uint8_t* __restrict__ xs, co
 #pragma unroll
         for (int r = 0; r < 8; ++r) {
           if (tp_valid(t, r)) {
-            const uint32_t w = r < 4 ? u[i].x : u[i].y;
-            const float xv = (float)((w >> (8 * (r & 3))) & 0xffu);
+            const float xv = u8f(r < 4 ? u[i].x : u[i].y, r & 3);
             if ((slot & 1) == 0) {
               pend = xv;
             } else {
