@@ -60,6 +60,8 @@ def parse():
     ap.add_argument("--prox-mu", type=float, default=0.01)
     ap.add_argument("--cs", default="ring", help="D-PSGD topology")
     ap.add_argument("--phase-timers", action="store_true", help="synchronised per-phase timers (adds syncs)")
+    ap.add_argument("--step-streams", type=int, default=4,
+                    help="side streams for the extra (ragged) launches of one lockstep step (1 = serial)")
     ap.add_argument("--rebalance", type=int, default=-1,
                     help="1: replicate the cohort on every rank and move sampled clients to even the per-round load "
                          "(default: on when frac < 1 on several ranks)")
@@ -107,7 +109,7 @@ def main():
                    dense_ratio=args.dense_ratio, seed=args.seed, group=args.group, frac=args.frac,
                    frequency_of_the_test=0 if args.no_eval else 1, aggregator=args.aggregator,
                    prox_mu=args.prox_mu if args.algorithm == "fedprox" else 0.0, cs=args.cs, final_round=False,
-                   rebalance=rebalance)
+                   rebalance=rebalance, step_streams=args.step_streams)
     runner = make_runner(args.algorithm, engine, splits, cfg, info, model, logger=None)
     t0 = time.perf_counter()
     if runner.alg == "salientgrads":

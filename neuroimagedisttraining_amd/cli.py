@@ -4,8 +4,10 @@ Flags, defaults and the ``args.identity`` string (the log file name, ``LOG/<data
 the reference entry points.  Added flags:
 
 * ``--engine {auto,hip,torch}``: every algorithm (SalientGrads, FedAvg, FedProx, DisPFL, SubAvg, Ditto, D-PSGD,
-  FedFomo, Local) on 3D-CNN + ABCD-shape data runs on the client-batched MI355X executor (HIP kernels, clients
-  sharded over ranks, RCCL collectives) when ``hip`` (``auto`` = hip if a GPU and the extension are available);
+  FedFomo, Local) runs on the client-batched MI355X executor (HIP kernels, clients sharded over ranks, RCCL
+  collectives) when ``hip`` (``auto`` = hip if a GPU and the extension are available) for 3DCNN (AlexNet3D) and
+  3D ResNet-50 (``--model resnet3d_50``) on ABCD-shape volumes and ResNet-18-GN (``--model resnet18``) on
+  CIFAR-10/100 — the reference defaults of every entry point;
   ``torch`` = the reference-semantics sequential eager path (also the CPU path).
 * ``--synthetic_abcd 1``, ``--n_per_client``: synthetic ABCD-shape cohort (no HDF5 needed); ``--synthetic_abcd 0
   --data_dir <cohort.nidtvol | dir>`` trains on the real cohort (site clients) on either path;
@@ -200,12 +202,32 @@ def load_data(args, dataset_name, logger=None):
     raise ValueError(dataset_name)
 
 
+RESNET3D_NAMES = ("resnet3d_50", "3dresnet50")
+IMAGE_DATASETS = ("cifar10", "cifar100")
+
+
+def hip_family(args):
+    """Model family of the client-batched MI355X executor for these flags, or None (eager only):
+    ``alexnet3d`` (3DCNN on ABCD: engine/executor.HipEngine), ``resnet2d`` (resnet18 = ResNet-18-GN on 32x32
+    CIFAR-10/100: engine/resnet2d_hip), ``resnet3d`` (3D ResNet-50 on ABCD: engine/resnet3d_hip)."""
+    model = args.model.lower()
+    if args.dataset == "ABCD" and model in ("3dcnn", "alexnet3d", "alexnet3d_dropout"):
+        return "alexnet3d"
+    if args.dataset in IMAGE_DATASETS and model == "resnet18":
+        return "resnet2d"
+    if args.dataset == "ABCD" and model in RESNET3D_NAMES:
+        return "resnet3d"
+    return None
+
+
 def _use_hip(args, algo):
-    """Every algorithm of the harness runs on the client-batched MI355X executor for the 3D-CNN on ABCD-shape data."""
-    if args.dataset != "ABCD" or args.model != "3DCNN":
+    """Every algorithm of the harness runs on the client-batched MI355X executor for the model families of
+    :func:`hip_family` (the reference defaults of every entry point: 3DCNN + ABCD, resnet18 + cifar10)."""
+    if hip_family(args) is None:
         if args.engine == "hip":
-            raise RuntimeError("--engine hip supports --model 3DCNN --dataset ABCD (AlexNet3D_Dropout on the HIP "
-                               "kernels); use --engine torch for other models")
+            raise RuntimeError("--engine hip supports --model 3DCNN / %s --dataset ABCD and --model resnet18 "
+                               "--dataset %s; use --engine torch for other models"
+                               % (" / ".join(RESNET3D_NAMES), " / ".join(IMAGE_DATASETS)))
         return False
     if args.engine == "torch":
         return False
@@ -233,9 +255,10 @@ def _resolve_cohort(data_dir):
     return path
 
 
-def hip_cohort(args, info, logger=None, with_val=False):
+def hip_cohort(args, info, logger=None, with_val=False, raw=False):
     """(x8, mom, labels, splits) for the HIP engine: this rank's clients' subjects resident in HBM in the engine's
-    polyphase layout, ``splits[c]`` indexing that local store (non-local clients keep only their sizes).
+    polyphase layout (``raw``: plain uint8 ``[N, D, H, W]`` volumes, ``mom`` None — the 3D ResNet engine),
+    ``splits[c]`` indexing that local store (non-local clients keep only their sizes).
 
     * real cohort (``--synthetic_abcd 0``): the reference ABCD loader's site-as-client split (21 sites, seeded
       80/20, ``ABCD/data_loader.py:67-102,157-212``) read from a NIDTVOL1 file by the native reader and streamed
@@ -262,7 +285,10 @@ def hip_cohort(args, info, logger=None, with_val=False):
         shards = rt.shard_clients([len(t) for t in tr], info.world)
         mine = list(range(N)) if getattr(args, "rebalance", 0) else shards[info.rank]
         subj = np.concatenate([np.concatenate([tr[c], te[c]]) for c in mine]) if mine else np.zeros(0, np.int64)
-        x8, mom = stream_to_device(vf, subj, info.device, hip_store=True)
+        if raw:
+            x8, mom = stream_to_device(vf, subj, info.device), None
+        else:
+            x8, mom = stream_to_device(vf, subj, info.device, hip_store=True)
         labels = torch.from_numpy(vf.labels[subj].astype(np.float32)).to(info.device)
         local, off = {}, 0
         for c in mine:
@@ -277,7 +303,10 @@ def hip_cohort(args, info, logger=None, with_val=False):
         mine = list(range(N)) if getattr(args, "rebalance", 0) else shards[info.rank]
         vol, labels, local = build_fl_volumes(mine, N, n_train, n_test, info.device, seed=args.seed,
                                               alpha=args.partition_alpha)
-        x8, mom = to_hip_store(vol)
+        if raw:
+            x8, mom = vol, None
+        else:
+            x8, mom = to_hip_store(vol)
         del vol
         sizes = [(n_train, n_test)] * N
     if with_val:
@@ -313,21 +342,92 @@ def fl_config(args, algo):
                     dist_thresh=g("dist_thresh", 1e-4), acc_thresh=g("acc_thresh", 0.5))
 
 
+def image_cohort(args, info, with_val=False):
+    """(x8, labels, splits) for the client-batched ResNet-18-GN engine: the CIFAR-10/100 train and test images as
+    uint8 ``[N, 32, 32, 3]`` in one device store (train first, test at ``+n_train``), split exactly as the eager
+    loaders do (``data/images.load_partition_data``: same partitioner, same RandomState stream, per-client test
+    sets drawn from the train label histogram, FedFomo's 10 % validation split).
+
+    Pixels: an ``.npz`` (``--data_dir``) holding uint8 HWC images is used as is (the engine applies the reference's
+    CIFAR mean/std normalisation); float images (the synthetic loader's, or a float ``.npz``) are taken to be
+    normalised NCHW tensors and mapped back to uint8 pixels."""
+    from .core import partition as PT
+    from .data import images
+    from .engine.executor import ClientSplit
+    from .engine.resnet2d_hip import CIFAR_MEAN, CIFAR_STD
+    n = getattr(args, "synthetic_size", 0) or None
+    xtr, ytr, xte, yte, n_cls = images._load_arrays(args.dataset, args.data_dir, n, n // 5 if n else None,
+                                                     args.seed)
+    if args.data_dir and args.data_dir.endswith(".npz"):
+        d = np.load(args.data_dir, allow_pickle=False)
+        if d["x_train"].dtype == np.uint8 and d["x_train"].shape[-1] == 3:
+            xtr, xte = torch.from_numpy(d["x_train"]), torch.from_numpy(d["x_test"])
+
+    def to_u8(x):
+        if x.dtype == torch.uint8:
+            return x
+        mean = torch.tensor(CIFAR_MEAN).view(1, 3, 1, 1)
+        std = torch.tensor(CIFAR_STD).view(1, 3, 1, 1)
+        return ((x * std + mean) * 255.0).round().clamp(0, 255).to(torch.uint8).permute(0, 2, 3, 1).contiguous()
+
+    xtr, xte = to_u8(xtr), to_u8(xte)
+    assert tuple(xtr.shape[1:]) == (32, 32, 3), xtr.shape
+    N = args.client_num_in_total
+    rng = np.random.RandomState(args.seed)
+    train_map = images.partition_data(ytr.numpy(), args.partition_method, N, args.partition_alpha, n_cls, rng)
+    test_map = PT.per_client_test_indices(ytr.numpy(), yte.numpy(), train_map, n_cls=n_cls, rng=rng)
+    ntr = len(ytr)
+    splits = []
+    nval = int(0.1 * len(train_map[0])) if with_val else 0
+    for c in range(N):
+        tr = np.asarray(train_map[c], dtype=np.int64)
+        te = np.asarray(test_map[c], dtype=np.int64) + ntr
+        if with_val:
+            pick = rng.choice(len(tr), min(nval, len(tr)), replace=False)
+            splits.append(ClientSplit(train=np.delete(tr, pick), test=te, val=tr[pick]))
+        else:
+            splits.append(ClientSplit(train=tr, test=te))
+    x8 = torch.cat([xtr, xte]).to(info.device)
+    y = torch.cat([ytr, yte]).long().to(info.device)
+    return x8, y, splits, n_cls
+
+
+def build_hip_engine(args, algo, info, logger=None):
+    """(engine, template model, client splits) of the client-batched executor for this model family."""
+    fam = hip_family(args)
+    if fam == "resnet2d":
+        from .engine.resnet2d_hip import ResNetHipEngine
+        from .models import customized_resnet18
+        x8, y, splits, n_cls = image_cohort(args, info, with_val=algo == "fedfomo")
+        model = customized_resnet18(class_num=n_cls)
+        desc = "%s %s images (%d clients)" % ("synthetic" if not args.data_dir else args.data_dir, args.dataset,
+                                              len(splits))
+        return ResNetHipEngine(model, x8, y, info.device), model, splits, desc
+    if fam == "resnet3d":
+        from .engine.resnet3d_hip import ResNet3DHipEngine
+        from .models.resnet3d import resnet3d_50
+        x8, _, labels, splits = hip_cohort(args, info, logger, with_val=algo == "fedfomo", raw=True)
+        model = resnet3d_50(num_classes=1)
+        desc = "NIDTVOL1 %s" % _resolve_cohort(args.data_dir) if not args.synthetic_abcd else "synthetic ABCD-shape"
+        return ResNet3DHipEngine(model, x8, labels, info.device), model, splits, desc
+    from .engine.executor import HipEngine
+    from .models.alexnet3d import AlexNet3D_Dropout
+    x8, mom, labels, splits = hip_cohort(args, info, logger, with_val=algo == "fedfomo")
+    model = AlexNet3D_Dropout(num_classes=1)
+    desc = "NIDTVOL1 %s" % _resolve_cohort(args.data_dir) if not args.synthetic_abcd else "synthetic ABCD-shape"
+    return HipEngine(model, x8, mom, labels, info.device), model, splits, desc
+
+
 def run_hip(args, algo, logger):
     """Any algorithm of the harness on the client-batched MI355X executor (HIP kernels, clients sharded over
-    ranks, RCCL collectives)."""
-    from .engine.executor import HipEngine
+    ranks, RCCL collectives) for the model families of :func:`hip_family`."""
     from .engine.personalized import make_runner
-    from .models.alexnet3d import AlexNet3D_Dropout
     from .parallel import runtime as rt
     from .utils import checkpoint as ck
     info = rt.init_distributed()
-    x8, mom, labels, splits = hip_cohort(args, info, logger, with_val=algo == "fedfomo")
-    logger.info("HIP cohort: %s, %d clients, train sizes %s" % (
-        "NIDTVOL1 %s" % _resolve_cohort(args.data_dir) if not args.synthetic_abcd else "synthetic ABCD-shape",
-        len(splits), [len(s.train) for s in splits]))
-    model = AlexNet3D_Dropout(num_classes=1)
-    eng = HipEngine(model, x8, mom, labels, info.device)
+    eng, model, splits, desc = build_hip_engine(args, algo, info, logger)
+    logger.info("HIP cohort (%s): %s, %d clients, train sizes %s" % (
+        hip_family(args), desc, len(splits), [len(s.train) for s in splits]))
     cfg = fl_config(args, algo)
     runner = make_runner(algo, eng, splits, cfg, info, model, logger=logger)
     start = 0

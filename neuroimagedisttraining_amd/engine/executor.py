@@ -73,6 +73,7 @@ class FLConfig:
     update_topk: float = 0.0      # >0: each client sends only its top-k |update| (values + int32 indices,
                                   # k = update_topk * P) through an RCCL all-gather (BASELINE config 5)
     hip_graphs: bool = True       # capture each lockstep local step (train + optimizer) in a hipGraph and replay it
+    step_streams: int = 4         # side HIP streams for the extra launches of one lockstep step (ragged clients)
     stratified_sampling: bool = False  # IterSNIP: label-stratified SNIP batches (sailentgrads/client.py:33-43)
     fix_eval_loss: bool = False   # evaluation loss on logits instead of the reference's sigmoid-then-BCEWithLogits (Q1)
     final_round: bool = True      # reference round tail: SalientGrads final eval, FedAvg fine-tune round + eval
@@ -136,9 +137,15 @@ class HipEngine:
         mode), FedProx proximal gradient, clip(10), SGD(wd, momentum), Ditto pull — one norm pass + one update
         pass over the rows.  The clipped gradient is written back only with ``keep_grad``."""
         G, P = theta.shape
-        ws = self.m.clip_sgd_mask_workspace(G, P)
-        if not hasattr(self, "_optws") or self._optws.numel() < ws:
-            self._optws = torch.empty(ws, dtype=torch.float32, device=theta.device)
+        # one workspace per row group, never freed or shared: captured graphs keep its address, and the launches of
+        # one step may run concurrently on side streams (runner step_streams)
+        if not hasattr(self, "_optws"):
+            self._optws = {}
+        wkey = (theta.data_ptr(), G, P)
+        ows = self._optws.get(wkey)
+        if ows is None:
+            ows = self._optws[wkey] = torch.empty(self.m.clip_sgd_mask_workspace(G, P), dtype=torch.float32,
+                                                  device=theta.device)
         bits = spec.bits
         if spec.mask_mode:
             assert bits is not None and bits.dtype == torch.int32 and bits.stride(1) == 1
@@ -152,7 +159,7 @@ class HipEngine:
                          ref.stride(0) if (ref is not None and ref.dim() == 2) else 0, float(spec.prox_mu),
                          pref.data_ptr() if pref is not None else 0,
                          pref.stride(0) if (pref is not None and pref.dim() == 2) else 0, float(spec.lamda),
-                         self._optws.data_ptr(), G, P, float(lr), float(wd), float(momentum), float(max_norm),
+                         ows.data_ptr(), G, P, float(lr), float(wd), float(momentum), float(max_norm),
                          lr_dev.data_ptr() if lr_dev is not None else 0, int(keep_grad),
                          torch.cuda.current_stream().cuda_stream)
 

@@ -283,19 +283,60 @@ class FLRunner:
             self._lr_dev = torch.zeros(1, dtype=torch.float32, device=self.device)
             self._seed_dev = torch.zeros(1, dtype=torch.int64, device=self.device)
         self._lr_dev.fill_(lr)
+        side = self._side_streams() if use_graphs else None
         for ep in range(epochs):
             plan, idx = self._plan(clients, self._epoch_chunks(round_idx, tag, ep))
+            main, cur, lanes_used = torch.cuda.current_stream() if side else None, -1, set()
+            partial_steps = {it[2] for it in plan if it[6] < cfg.batch_size} if side else ()
             for r0, r1, s, off, n, G, B in plan:
+                if s != cur:  # fork point of this step: main has enqueued every earlier step
+                    cur = s
+                    fork = main.record_event() if s in partial_steps else None
                 seed = self._step_seed(round_idx, tag, ep, s)
                 cids = clients[r0:r1]
                 sub = view.rows(r0, r1)
-                if use_graphs:
+                if side and B < cfg.batch_size:
+                    # a partial last batch: these clients are done with the epoch after this launch, so it runs
+                    # on a side lane, overlapped with the following full-batch steps (see _lane)
+                    st, sdev = self._lane(G, B)
+                    st.wait_event(fork)
+                    lanes_used.add(st)
+                    with torch.cuda.stream(st):
+                        sdev.fill_(seed)
+                        self._graph_step(sub, r0, idx[off:off + n], G, B, spec.rows(r0, r1), cids, seed, fill=False,
+                                         seed_dev=sdev)
+                elif use_graphs:
                     self._graph_step(sub, r0, idx[off:off + n], G, B, spec.rows(r0, r1), cids, seed)
                 else:
                     self._seed_dev.fill_(seed)
                     self._step(sub, r0, idx[off:off + n], G, B, spec.rows(r0, r1), cids, lr)
+            for st in lanes_used:
+                main.wait_stream(st)
+            self.concurrent_steps = getattr(self, "concurrent_steps", 0) + len(lanes_used)
             if epoch_hook is not None:
                 epoch_hook(ep, view, clients)
+
+    def _side_streams(self):
+        if self.cfg.step_streams <= 1:
+            return None
+        if getattr(self, "_streams", None) is None:
+            self._streams = [torch.cuda.Stream(device=self.device) for _ in range(self.cfg.step_streams)]
+            self._lane_seed = [torch.zeros(1, dtype=torch.int64, device=self.device) for _ in self._streams]
+        return self._streams
+
+    def _lane(self, G, B):
+        """Side stream (+ its own dropout-seed scalar) of a partial-batch launch shape.
+
+        Ragged federations (unequal sizes, drop_last=False) add, at many lockstep steps, launches of the few
+        clients whose partial last batch falls there: tiny, latency-bound grids.  Such a client trains no further
+        in this epoch, so its launch only has to follow the full-batch launches that wrote its rows before (the
+        current stream, forked with an event) and finish before the epoch ends (joined then): it overlaps the
+        next full-batch steps instead of adding its latency to the step chain.  A shape always maps to the same
+        lane, because launches of one (G, B) share the engine's scratch buffers for that shape; each lane has its
+        own seed scalar, which its captured graphs read (the current stream rewrites the main one every step).
+        Results equal the serial order: launches in flight together touch disjoint rows."""
+        k = hash((int(G), int(B))) % len(self._streams)
+        return self._streams[k], self._lane_seed[k]
 
     def _step(self, sub, r0, idx, G, B, spec, cids, lr, seed_dev=None, lr_dev=None):
         cfg = self.cfg
@@ -306,22 +347,26 @@ class FLRunner:
         self.e.local_opt(sub.theta, gr, mo, spec, lr, cfg.wd, cfg.momentum, cfg.max_norm,
                          lr_dev=self._lr_dev if lr_dev is None else lr_dev)
 
-    def _graph_step(self, sub, r0, idx, G, B, spec, cids, seed):
+    def _graph_step(self, sub, r0, idx, G, B, spec, cids, seed, fill=True, seed_dev=None):
         """One lockstep local step (forward+backward of G clients + fused optimizer) as a replayed hipGraph.  The
         ~45 kernel launches of a step become one graph launch; everything that changes between steps lives in
         device memory the graph reads: the sample indices (copied into a static buffer), the dropout stream
         counter and the round's learning rate.  The first step of a shape runs eagerly (it also allocates every
         scratch buffer the graph will reuse), the second is captured and replayed, later ones only replay — same
         kernels, same arguments, same results as the eager path."""
-        key = (sub.theta.data_ptr(), r0, G, B, tuple(int(c) for c in cids), spec.key())
+        sdev = self._seed_dev if seed_dev is None else seed_dev
+        key = (sub.theta.data_ptr(), r0, G, B, tuple(int(c) for c in cids), spec.key(), sdev.data_ptr())
         ent = self._graphs.get(key, "new")
-        self._seed_dev.fill_(seed)
+        if fill:
+            sdev.fill_(seed)
         if ent == "new":
             # bounded cache: with client sampling (frac < 1) every round brings new client groups; the oldest
             # captured graphs (and the memory pools they hold) are released first
+            if len(self._graphs) >= self.max_graphs and getattr(self, "_streams", None):
+                torch.cuda.synchronize(self.device)  # an evicted graph may still run on a side stream
             while len(self._graphs) >= self.max_graphs:
                 self._graphs.pop(next(iter(self._graphs)))
-            self._step(sub, r0, idx, G, B, spec, cids, 0.0)
+            self._step(sub, r0, idx, G, B, spec, cids, 0.0, seed_dev=sdev)
             self._graphs[key] = None
             return
         if ent is None:
@@ -332,14 +377,14 @@ class FLRunner:
             try:
                 # thread_local: the RCCL watchdog thread of a multi-GPU run may query events during the capture
                 with torch.cuda.graph(g, capture_error_mode="thread_local"):
-                    self._step(sub, r0, idx_buf, G, B, spec, cids, 0.0)
+                    self._step(sub, r0, idx_buf, G, B, spec, cids, 0.0, seed_dev=sdev)
             except Exception:  # noqa: BLE001 - capture unsupported here: stay eager for this shape
                 self._graphs[key] = False
-                self._step(sub, r0, idx, G, B, spec, cids, 0.0)
+                self._step(sub, r0, idx, G, B, spec, cids, 0.0, seed_dev=sdev)
                 return
             ent = self._graphs[key] = (g, idx_buf)
         elif ent is False:
-            self._step(sub, r0, idx, G, B, spec, cids, 0.0)
+            self._step(sub, r0, idx, G, B, spec, cids, 0.0, seed_dev=sdev)
             return
         g, idx_buf = ent
         idx_buf.copy_(idx)

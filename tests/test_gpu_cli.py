@@ -49,3 +49,30 @@ def test_cli_every_algorithm_runs_on_hip(algo, tmp_path):
     out = cli.main(algo, argv)
     vals = [v for k, v in out.items() if k.endswith("test_acc") and isinstance(v, list) and v]
     assert vals and all(0.0 <= x <= 1.0 for x in vals[0])
+
+
+@pytest.mark.parametrize("algo", ["subavg", "dispfl", "ditto", "dpsgd", "fedfomo", "local", "fedavg"])
+def test_cli_resnet18_cifar_runs_on_hip(algo, tmp_path):
+    """The CIFAR entry points' default model (resnet18 = ResNet-18-GN, cifar10) runs on the client-batched
+    ResNet engine (engine/resnet2d_hip.py), not the eager loop."""
+    from neuroimagedisttraining_amd import cli
+    argv = ["--model", "resnet18", "--dataset", "cifar10", "--client_num_in_total", "4", "--comm_round", "2",
+            "--epochs", "1", "--batch_size", "16", "--synthetic_size", "640", "--frac", "0.5", "--engine", "hip",
+            "--log_dir", str(tmp_path)]
+    out = cli.main(algo, argv)
+    vals = [v for k, v in out.items() if k.endswith("test_acc") and isinstance(v, list) and v]
+    assert vals and all(0.0 <= x <= 1.0 for x in vals[0])
+    log = next((tmp_path / "cifar10").glob("*.log")).read_text()
+    assert "HIP cohort (resnet2d)" in log
+
+
+def test_cli_resnet3d50_runs_on_hip(tmp_path):
+    """--model resnet3d_50 on ABCD-shape volumes runs on the client-batched 3D ResNet engine (config 5 family)."""
+    from neuroimagedisttraining_amd import cli
+    argv = ["--model", "resnet3d_50", "--dataset", "ABCD", "--client_num_in_total", "2", "--comm_round", "1",
+            "--epochs", "1", "--batch_size", "2", "--n_per_client", "3", "--frac", "1.0", "--engine", "hip",
+            "--log_dir", str(tmp_path)]
+    out = cli.main("fedavg", argv)
+    assert len(out["global_test_acc"]) >= 1
+    log = next((tmp_path / "ABCD").glob("*.log")).read_text()
+    assert "HIP cohort (resnet3d)" in log

@@ -253,6 +253,8 @@ def test_runner_hip_graphs_bit_identical_to_eager(algo):
     a, _ = _run(algo, "hip", fed, hip_graphs=True, dropout_keep=0.5, **_extra(algo))
     b, _ = _run(algo, "hip", fed, hip_graphs=False, dropout_keep=0.5, **_extra(algo))
     assert any(isinstance(v, tuple) for v in a._graphs.values()), "no step was captured"
+    # ragged steps ran their extra launches concurrently on side streams (runner step_streams)
+    assert getattr(a, "concurrent_steps", 0) > 0 or algo in ("dpsgd", "subavg")
     assert torch.equal(a.theta, b.theta) and torch.equal(a.bufs, b.bufs)
     assert torch.equal(a.w_global, b.w_global)
     if getattr(a, "mbits", None) is not None:
