@@ -638,8 +638,8 @@ static void conv3d_fwd_impl(uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t 
     a.nPB = ceil_div(a.Mg, bp);
     const int nCO = Cout / bco;
     if (ksplit > 1) {
-      NIDT_REQUIRE(part != 0 && ((!hb && !st) || (bp == 256 && Cout <= 256)),
-                   "conv3d_fwd_splitk: needs a partial buffer (with bias/statistics: 256-position blocks, Cout <= 256)");
+      NIDT_REQUIRE(part != 0 && ((!hb && !st) || (bp <= 256 && Cout <= 256)),
+                   "conv3d_fwd_splitk: needs a partial buffer (with bias/statistics: <= 256-position blocks, Cout <= 256)");
       a.ksplit = ksplit;
       a.part = ptr<float>(part);
     }
@@ -750,22 +750,25 @@ void conv3d_fwd_splitk(uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t y, ui
   conv3d_fwd_impl(x, w, bias, 0, 0, y, stats, G, B, D, H, W, Cin, Cout, pad, stream, ksplit, part);
 }
 
-// Split-K factor for conv3d_fwd_splitk.  Off by default: measured at 8 clients per GPU (conv3-5, 264-block grids)
-// the split (2 x 27 k-steps + the finish kernel) made the train step slower, 3.97 -> 4.16 ms
-// (profiles/r1_ab_fwd_splitk.txt).  NIDT_FWD_KSPLIT=k enables it where it applies (256-position blocks,
-// Cout <= 256, fewer than two resident blocks per CU).
+// Split-K factor for conv3d_fwd_splitk (forward with bias + BN block statistics, and the dgrad convs): only grids
+// with fewer blocks than CUs and a long reduction, i.e. the 5x7x5 conv3-5 layers at one or two clients per launch
+// (the partial-batch launches of ragged federations): there a block runs 36-81 sequential k-steps on a third of
+// the chip.  ks = min(ceil(512 / blocks), k-steps / 12, 8), finished by k_fwd_splitk_fin / k_fwd_splitk_sum.
+// Measured at 8 clients per GPU (264-block grids) a split made the step slower (3.97 -> 4.16 ms,
+// profiles/r1_ab_fwd_splitk.txt), hence the < 256-block rule.  NIDT_FWD_KSPLIT=1 disables it, =k > 1 forces k.
 int conv3d_fwd_ksplit(int Cin, int Cout, int G, int Mg) {
   if (Cin % 64 != 0 || Cout > 256 || Cout % 64 != 0) return 1;
-  if (conv3d_fwd_bp(Cin, Cout, 0, G, Mg) != 256) return 1;
   static const int env = [] {
     const char* e = getenv("NIDT_FWD_KSPLIT");
     return e ? atoi(e) : 0;
   }();
-  const int bco = fwd_bco(Cout);
-  const int64_t nwg = (int64_t)ceil_div(Mg, 256) * (Cout / bco) * G;
-  if (env <= 1 || nwg >= 512) return 1;
-  int ks = env;
-  return std::max(1, std::min(ks, 27 * Cin / 64 / 8));
+  const int nks = 27 * Cin / 64;
+  if (env == 1) return 1;
+  if (env > 1) return std::max(1, std::min(env, nks / 8));
+  const int bp = conv3d_fwd_bp(Cin, Cout, 0, G, Mg);
+  const int64_t nwg = (int64_t)ceil_div(Mg, bp) * (Cout / fwd_bco(Cout)) * G;
+  if (nwg >= 256 || nks < 24) return 1;
+  return (int)std::max<int64_t>(1, std::min<int64_t>(std::min<int64_t>(ceil_div(512, nwg), nks / 12), 8));
 }
 
 // positions per block (= per BN-statistics block) of conv3d_fwd for this layer shape and client count

@@ -79,6 +79,11 @@ class RowSet:
         return RowSet(self.theta[lo:hi], self.bufs[lo:hi])
 
 
+def _nullctx():
+    import contextlib
+    return contextlib.nullcontext()
+
+
 def _contiguous(rows):
     return bool(rows) and rows == list(range(rows[0], rows[-1] + 1))
 
@@ -773,6 +778,11 @@ class FLRunner:
         sizes = {}
         for j, c in enumerate(clients):
             sizes.setdefault(len(self._split_of(c, which)), []).append(j)
+        # ragged test sets (one launch per distinct size, most of them a client or two: latency-bound) run on the
+        # side lanes, a shape per lane (the engine's eval scratch is per shape); eval-mode launches are independent
+        lanes = self._side_streams() if (self.device.type == "cuda" and len(sizes) > 2) else None
+        main, used = (torch.cuda.current_stream(), set()) if lanes else (None, None)
+        fork = main.record_event() if lanes else None
         for n, js in sizes.items():
             if n == 0:
                 continue
@@ -780,19 +790,28 @@ class FLRunner:
                 out[js] = self._eval_rows(theta, bufs, [clients[j] for j in js], [rows[j] for j in js], which)
                 continue
             for grp in self._groups(js):
-                rr = [rows[j] for j in grp]
-                if _contiguous(rr):
-                    th, bu = theta[rr[0]:rr[-1] + 1], bufs[rr[0]:rr[-1] + 1]
-                else:
-                    t = torch.tensor(rr, device=self.device)
-                    th, bu = gather_rows(theta, t), gather_rows(bufs, t)
-                idx = self._upload_i32(np.concatenate([self._split_of(clients[j], which) for j in grp]))
-                logits = self.e.eval_logits(th, bu, idx, len(grp), n).view(len(grp), n, -1)
-                y = self.e.labels.index_select(0, idx.long().to(self.e.labels.device)).to(logits.device).float()
-                y = y.view(len(grp), n)
-                correct, loss = self._eval_chunk_metrics(logits, y)
-                pending.append((grp, torch.stack([correct.sum(1), loss.sum(1),
-                                                  torch.full_like(loss[:, 0], float(n))], 1).double()))
+                st = self._lane(len(grp), n)[0] if lanes else None
+                if st is not None and st not in used:
+                    st.wait_event(fork)
+                    used.add(st)
+                with torch.cuda.stream(st) if st is not None else _nullctx():
+                    rr = [rows[j] for j in grp]
+                    if _contiguous(rr):
+                        th, bu = theta[rr[0]:rr[-1] + 1], bufs[rr[0]:rr[-1] + 1]
+                    else:
+                        t = torch.tensor(rr, device=self.device)
+                        th, bu = gather_rows(theta, t), gather_rows(bufs, t)
+                    idx = self._upload_i32(np.concatenate([self._split_of(clients[j], which) for j in grp]))
+                    logits = self.e.eval_logits(th, bu, idx, len(grp), n).view(len(grp), n, -1)
+                    y = self.e.labels.index_select(0, idx.long().to(self.e.labels.device)).to(logits.device).float()
+                    y = y.view(len(grp), n)
+                    correct, loss = self._eval_chunk_metrics(logits, y)
+                    res = torch.stack([correct.sum(1), loss.sum(1), torch.full_like(loss[:, 0], float(n))], 1).double()
+                if st is not None:
+                    res.record_stream(main)  # consumed on the current stream after the join
+                pending.append((grp, res))
+        for st in used or ():
+            main.wait_stream(st)
         if pending:
             host = torch.cat([r for _, r in pending], 0).cpu().numpy()
             o = 0

@@ -93,10 +93,11 @@ def test_conv3d_fwd_stats(cin, cout, pad, sp, xf, G, B):
     assert _relerr(var, yr_g.var(1, unbiased=False)) < 1e-3
 
 
-@pytest.mark.parametrize("cin,cout,G", [(128, 192, 16), (192, 192, 16), (192, 128, 24)])
-@pytest.mark.parametrize("ksplit,stats_on", [(2, True), (3, True), (2, False)])
+@pytest.mark.parametrize("cin,cout,G", [(128, 192, 16), (192, 192, 16), (192, 128, 24), (128, 192, 1), (192, 128, 2)])
+@pytest.mark.parametrize("ksplit,stats_on", [(2, True), (3, True), (2, False), (4, True)])
 def test_conv3d_fwd_splitk(cin, cout, G, ksplit, stats_on):
-    """Split-K forward (few clients per GPU): fp32 partials + finish kernel == fp32 oracle; BN block stats too."""
+    """Split-K forward (few clients per GPU): fp32 partials + finish kernel == fp32 oracle; BN block stats too
+    (256-position blocks, and the 64-position blocks of one- or two-client launches, which pick ks > 1 themselves)."""
     m = _m()
     B, pad, sp = 16, 1, (5, 7, 5)
     torch.manual_seed(3)
@@ -105,7 +106,9 @@ def test_conv3d_fwd_splitk(cin, cout, G, ksplit, stats_on):
     bias = torch.randn(G, cout, device=DEV)
     Mg = B * 5 * 7 * 5
     bp = m.conv3d_fwd_bp(cin, cout, 0, G, Mg)
-    assert bp == 256
+    assert bp == (256 if G >= 16 else 64)
+    if G <= 2:
+        assert m.conv3d_fwd_ksplit(cin, cout, G, Mg) > 1
     npb = m.conv3d_fwd_nblocks(B, *sp, pad, bp)
     y = torch.empty(G * B, *sp, cout, device=DEV, dtype=torch.bfloat16)
     stats = torch.empty(G, npb, cout, 2, device=DEV)

@@ -200,13 +200,14 @@ def _fed(sizes, n_test=6, n_val=4, seed=11):
     from neuroimagedisttraining_amd.data.volumes import make_synthetic_abcd
     from neuroimagedisttraining_amd.data.synthetic_fl import to_hip_store
     from neuroimagedisttraining_amd.engine.executor import ClientSplit
-    tot = sum(s + n_test for s in sizes)
+    nte = list(n_test) if hasattr(n_test, "__len__") else [n_test] * len(sizes)
+    tot = sum(s + t for s, t in zip(sizes, nte))
     st = make_synthetic_abcd(tot, seed=seed, device=DEV)
     splits, off = [], 0
-    for s in sizes:
+    for s, t in zip(sizes, nte):
         tr = np.arange(off, off + s)
-        splits.append(ClientSplit(tr, np.arange(off + s, off + s + n_test), tr[:n_val]))
-        off += s + n_test
+        splits.append(ClientSplit(tr, np.arange(off + s, off + s + t), tr[:n_val]))
+        off += s + t
     x8, mom = to_hip_store(st.volumes)
     return st, x8, mom, splits
 
@@ -249,9 +250,9 @@ def _extra(algo):
 def test_runner_hip_graphs_bit_identical_to_eager(algo):
     """Every algorithm's lockstep steps replayed as hipGraphs (per-row masks, grad masks, pull references, ragged
     group shapes) == the eager launch sequence, bit for bit, including the masks the selection kernels produce."""
-    fed = _fed(SIZES)
+    fed = _fed(SIZES, n_test=[6, 4, 7, 5, 6, 3, 8, 5])  # ragged test sets: evaluated on the side lanes
     a, _ = _run(algo, "hip", fed, hip_graphs=True, dropout_keep=0.5, **_extra(algo))
-    b, _ = _run(algo, "hip", fed, hip_graphs=False, dropout_keep=0.5, **_extra(algo))
+    b, _ = _run(algo, "hip", fed, hip_graphs=False, dropout_keep=0.5, step_streams=1, **_extra(algo))
     assert any(isinstance(v, tuple) for v in a._graphs.values()), "no step was captured"
     # ragged steps ran their extra launches concurrently on side streams (runner step_streams)
     assert getattr(a, "concurrent_steps", 0) > 0 or algo in ("dpsgd", "subavg")
@@ -261,6 +262,9 @@ def test_runner_hip_graphs_bit_identical_to_eager(algo):
         assert torch.equal(a.mbits, b.mbits)
     if hasattr(a, "pers"):
         assert torch.equal(a.pers.theta, b.pers.theta)
+    # ragged test sets evaluated on the side lanes == serially
+    for k in ("global_test_acc", "global_test_loss", "person_test_acc", "person_test_loss"):
+        assert a.stat_info[k] == b.stat_info[k], k
 
 
 @pytest.mark.parametrize("algo", ALGOS)
