@@ -648,7 +648,47 @@ __device__ __forceinline__ float u8f(uint32_t w, int b) {
   return f;
 }
 
-template <int W>
+// one cell of the sparse wgrad: its (dz, argmax offset) record and the 8-phase halo voxels of the wave's taps
+template <class SET>
+__device__ __forceinline__ void conv1_wg_load(const uint32_t* meta, const uint2* halo, int it, int c, float& dz,
+                                              uint2 (&u)[SET::n]) {
+  const uint32_t m = meta[it * kC1 + c];
+  dz = bf16_to_f32((uint16_t)(m & 0xffffu));
+  const uint2* base = halo + (m >> 16);
+#pragma unroll
+  for (int i = 0; i < SET::n; ++i) {
+    const int t = SET::t(i);
+    u[i] = base[(t / 9) * kWgZS + ((t / 3) % 3) * kWgRS + t % 3];
+  }
+}
+
+// S += dz * x over the wave's valid taps; consecutive taps are paired into packed-FP32 FMAs (v_pk_fma_f32)
+template <class SET>
+__device__ __forceinline__ void conv1_wg_fma(float dz, const uint2 (&u)[SET::n], f32x2* S2) {
+  const f32x2 dz2 = {dz, dz};
+  int slot = 0;
+  float pend = 0.f;
+#pragma unroll
+  for (int i = 0; i < SET::n; ++i) {
+    const int t = SET::t(i);
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      if (tp_valid(t, r)) {
+        const float xv = u8f(r < 4 ? u[i].x : u[i].y, r & 3);
+        if ((slot & 1) == 0) {
+          pend = xv;
+        } else {
+          const f32x2 x2 = {pend, xv};
+          S2[slot >> 1] = __builtin_elementwise_fma(dz2, x2, S2[slot >> 1]);
+        }
+        ++slot;
+      }
+    }
+  }
+  if (slot & 1) S2[slot >> 1].x = fmaf(dz, pend, S2[slot >> 1].x);
+}
+
+template <int W, int UNR>
 __device__ __forceinline__ void conv1_wg_wave(const uint8_t* __restrict__ xs, const uint16_t* __restrict__ dp,
                                               const uint16_t* __restrict__ pout, const uint8_t* __restrict__ amax,
                                               float* __restrict__ part, uint2* halo, uint32_t* meta, int n, int pd,
@@ -683,39 +723,26 @@ __device__ __forceinline__ void conv1_wg_wave(const uint8_t* __restrict__ xs, co
       meta[e] = dzb | ((uint32_t)off << 16);
     }
     __syncthreads();
-    for (int it = 0; it < ncell; ++it) {
-      const uint32_t m = meta[it * kC1 + c];
-      const float dz = bf16_to_f32((uint16_t)(m & 0xffffu));
-      if (W == 0) Dsum += dz;
-      const uint2* base = halo + (m >> 16);
+    // UNR cells per iteration: every cell's metadata and halo reads are issued before any of their FMAs, so the
+    // LDS latency of cell it+1 hides behind cell it's arithmetic inside one wave
+    int it = 0;
+    for (; it + UNR <= ncell; it += UNR) {
+      float dz[UNR];
+      uint2 u[UNR][SET::n];
+#pragma unroll
+      for (int q = 0; q < UNR; ++q) conv1_wg_load<SET>(meta, halo, it + q, c, dz[q], u[q]);
+#pragma unroll
+      for (int q = 0; q < UNR; ++q) {
+        if (W == 0) Dsum += dz[q];
+        conv1_wg_fma<SET>(dz[q], u[q], S2);
+      }
+    }
+    for (; it < ncell; ++it) {
+      float dz;
       uint2 u[SET::n];
-#pragma unroll
-      for (int i = 0; i < SET::n; ++i) {
-        const int t = SET::t(i);
-        u[i] = base[(t / 9) * kWgZS + ((t / 3) % 3) * kWgRS + t % 3];
-      }
-      // consecutive valid taps are paired into packed-FP32 FMAs (v_pk_fma_f32, dz broadcast)
-      const f32x2 dz2 = {dz, dz};
-      int slot = 0;
-      float pend = 0.f;
-#pragma unroll
-      for (int i = 0; i < SET::n; ++i) {
-        const int t = SET::t(i);
-#pragma unroll
-        for (int r = 0; r < 8; ++r) {
-          if (tp_valid(t, r)) {
-            const float xv = u8f(r < 4 ? u[i].x : u[i].y, r & 3);
-            if ((slot & 1) == 0) {
-              pend = xv;
-            } else {
-              const f32x2 x2 = {pend, xv};
-              S2[slot >> 1] = __builtin_elementwise_fma(dz2, x2, S2[slot >> 1]);
-            }
-            ++slot;
-          }
-        }
-      }
-      if (slot & 1) S2[slot >> 1].x = fmaf(dz, pend, S2[slot >> 1].x);
+      conv1_wg_load<SET>(meta, halo, it, c, dz, u);
+      if (W == 0) Dsum += dz;
+      conv1_wg_fma<SET>(dz, u, S2);
     }
   }
   float* op = part + ((int64_t)slab * kC1 + c) * 126;
@@ -736,6 +763,7 @@ __device__ __forceinline__ void conv1_wg_wave(const uint8_t* __restrict__ xs, co
 
 // grid = NB * 19 * nq: block (n, pd, q) walks pooled rows [q * rq, (q + 1) * rq) of its slab (nq = 2 when one
 // slab per (sample, pd) would give the chip fewer than ~4 blocks per CU: few clients per GPU)
+template <int UNR>
 __global__ __launch_bounds__(256) void k_conv1_wgrad_split(const uint8_t* __restrict__ x8, const int* __restrict__ idx,
                                                            const uint16_t* __restrict__ dp,
                                                            const uint16_t* __restrict__ pout,
@@ -751,10 +779,10 @@ __global__ __launch_bounds__(256) void k_conv1_wgrad_split(const uint8_t* __rest
   const int tid = threadIdx.x, c = tid & 63, wid = tid >> 6;
   const uint8_t* xs = x8 + (int64_t)idx[n] * kPZ * kPY * kPX * 8;
   switch (wid) {
-    case 0: conv1_wg_wave<0>(xs, dp, pout, amax, part, halo, meta, n, pd, tid, c, ph_begin, ph_end, bid_slab(rest, q, nq)); break;
-    case 1: conv1_wg_wave<1>(xs, dp, pout, amax, part, halo, meta, n, pd, tid, c, ph_begin, ph_end, bid_slab(rest, q, nq)); break;
-    case 2: conv1_wg_wave<2>(xs, dp, pout, amax, part, halo, meta, n, pd, tid, c, ph_begin, ph_end, bid_slab(rest, q, nq)); break;
-    default: conv1_wg_wave<3>(xs, dp, pout, amax, part, halo, meta, n, pd, tid, c, ph_begin, ph_end, bid_slab(rest, q, nq)); break;
+    case 0: conv1_wg_wave<0, UNR>(xs, dp, pout, amax, part, halo, meta, n, pd, tid, c, ph_begin, ph_end, bid_slab(rest, q, nq)); break;
+    case 1: conv1_wg_wave<1, UNR>(xs, dp, pout, amax, part, halo, meta, n, pd, tid, c, ph_begin, ph_end, bid_slab(rest, q, nq)); break;
+    case 2: conv1_wg_wave<2, UNR>(xs, dp, pout, amax, part, halo, meta, n, pd, tid, c, ph_begin, ph_end, bid_slab(rest, q, nq)); break;
+    default: conv1_wg_wave<3, UNR>(xs, dp, pout, amax, part, halo, meta, n, pd, tid, c, ph_begin, ph_end, bid_slab(rest, q, nq)); break;
   }
 }
 
@@ -766,9 +794,17 @@ void conv1_wgrad(uintptr_t x8, uintptr_t idx, uintptr_t dp, uintptr_t pout, uint
                  int64_t goff_g, int64_t goff_b, float wscale, uintptr_t emean, uintptr_t stream) {
   hipStream_t s = as_stream(stream);
   const int nq = conv1_wgrad_nq(NB);
-  hipLaunchKernelGGL(k_conv1_wgrad_split, dim3(kPD * NB * nq), dim3(256), 0, s, ptr<const uint8_t>(x8),
-                     ptr<const int>(idx), ptr<const uint16_t>(dp), ptr<const uint16_t>(pout), ptr<const uint8_t>(amax),
-                     ptr<float>(part), nq);
+  // NIDT_C1WG_UNROLL=2|4: unrolled cell loop (A/B: loads of the next cell overlap the current cell's FMAs)
+  static const int unr = [] {
+    const char* e = getenv("NIDT_C1WG_UNROLL");
+    return e ? atoi(e) : 1;
+  }();
+#define NIDT_C1WG(U)                                                                                                \
+  hipLaunchKernelGGL(k_conv1_wgrad_split<U>, dim3(kPD * NB * nq), dim3(256), 0, s, ptr<const uint8_t>(x8),          \
+                     ptr<const int>(idx), ptr<const uint16_t>(dp), ptr<const uint16_t>(pout), ptr<const uint8_t>(amax), \
+                     ptr<float>(part), nq)
+  if (unr == 4) NIDT_C1WG(4); else if (unr == 2) NIDT_C1WG(2); else NIDT_C1WG(1);
+#undef NIDT_C1WG
   NIDT_CHECK(hipGetLastError());
   const int G = NB / B;
   // client g's slabs are contiguous: B samples x 19 pd x nq row ranges
