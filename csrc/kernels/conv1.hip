@@ -16,6 +16,8 @@
 //      dgamma = invstd w.(S - D mu),  dbeta = D,
 //      dw = gamma invstd (S - D mu - dgamma invstd Cov w),  db = 0
 //    which is exactly the gradient autograd computes through conv -> BN(train) -> ReLU -> pool.
+#include <cstdlib>
+
 #include "common.h"
 
 namespace nidt {
@@ -322,6 +324,7 @@ __device__ __forceinline__ float vmax3(float a, float b, float c) {
 
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 
+template <int PF>  // B-fragment prefetch distance in k-steps
 __global__ __launch_bounds__(256, 2) void k_conv1_fwd_pool_pipe(const uint8_t* __restrict__ x8,
                                                                 const int* __restrict__ idx,
                                                                 const uint16_t* __restrict__ w8,
@@ -420,9 +423,15 @@ __global__ __launch_bounds__(256, 2) void k_conv1_fwd_pool_pipe(const uint8_t* _
         for (int r = 0; r < 4; ++r) best[i][j][r] = -INFINITY;
 #pragma unroll 1
     for (int dd = 0; dd < 3; ++dd) {
-      // 21 k-steps (3 dh rows x 7 tap groups) with the B fragments of step q+1 read before step q's MFMAs
-      f16x8 nb0 = *reinterpret_cast<const f16x8*>(&hb[colbase0 + dd * 5 * HX * 8 + toff[0]]);
-      f16x8 nb1 = *reinterpret_cast<const f16x8*>(&hb[colbase1 + dd * 5 * HX * 8 + toff[0]]);
+      // 21 k-steps (3 dh rows x 7 tap groups); the B fragments are read PF steps ahead of their MFMAs (a ring of
+      // PF + 1 register pairs), so an LDS read's latency is covered by PF steps of matrix work, not one
+      f16x8 rb0[PF + 1], rb1[PF + 1];
+#pragma unroll
+      for (int p = 0; p < PF; ++p) {
+        const int ro = ((dd * 5 + p / 7) * HX) * 8 + toff[p % 7];
+        rb0[p] = *reinterpret_cast<const f16x8*>(&hb[colbase0 + ro]);
+        rb1[p] = *reinterpret_cast<const f16x8*>(&hb[colbase1 + ro]);
+      }
       f32x4 acc[2][2];
 #pragma unroll
       for (int q = 0; q < 21; ++q) {
@@ -433,17 +442,18 @@ __global__ __launch_bounds__(256, 2) void k_conv1_fwd_pool_pipe(const uint8_t* _
 #pragma unroll
             for (int j = 0; j < 2; ++j) acc[i][j] = cinit[i];
         }
-        const f16x8 fb0 = nb0, fb1 = nb1;
-        if (q + 1 < 21) {
-          const int ro = ((dd * 5 + (q + 1) / 7) * HX) * 8 + toff[(q + 1) % 7];
-          nb0 = *reinterpret_cast<const f16x8*>(&hb[colbase0 + ro]);
-          nb1 = *reinterpret_cast<const f16x8*>(&hb[colbase1 + ro]);
+        if (q + PF < 21) {
+          const int qn = q + PF, ro = ((dd * 5 + qn / 7) * HX) * 8 + toff[qn % 7];
+          rb0[qn % (PF + 1)] = *reinterpret_cast<const f16x8*>(&hb[colbase0 + ro]);
+          rb1[qn % (PF + 1)] = *reinterpret_cast<const f16x8*>(&hb[colbase1 + ro]);
         }
+        const f16x8 fb0 = rb0[q % (PF + 1)], fb1 = rb1[q % (PF + 1)];
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
           acc[i][0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[i][s], fb0, acc[i][0], 0, 0, 0);
           acc[i][1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[i][s], fb1, acc[i][1], 0, 0, 0);
         }
+        if (PF > 1) asm volatile("" ::: "memory");  // keep step q+PF's LDS reads in step q (no re-hoisting)
         if (s != 6) continue;
         const uint32_t tag = (uint32_t)(dd * 9 + dh * 3 + dw);
 #pragma unroll
@@ -500,9 +510,17 @@ __global__ __launch_bounds__(256, 2) void k_conv1_fwd_pool_pipe(const uint8_t* _
 void conv1_fwd_pool(uintptr_t x8, uintptr_t idx, uintptr_t w8, uintptr_t scale, uintptr_t shift, int NB, int B,
                     uintptr_t out, uintptr_t amax, uintptr_t stream) {
   NIDT_REQUIRE(NB % B == 0, "conv1_fwd_pool: NB % B");
-  hipLaunchKernelGGL(k_conv1_fwd_pool_pipe, dim3(kPD * NB), dim3(256), 0, as_stream(stream), ptr<const uint8_t>(x8),
-                     ptr<const int>(idx), ptr<const uint16_t>(w8), ptr<const float>(scale), ptr<const float>(shift), B,
-                     ptr<uint16_t>(out), ptr<uint8_t>(amax));
+  // B-fragment prefetch distance (k-steps); NIDT_C1_PF=1/2/3 selects it (A/B), default 2
+  static const int pf = [] {
+    const char* e = getenv("NIDT_C1_PF");
+    return e ? atoi(e) : 2;
+  }();
+#define NIDT_C1(PF)                                                                                              \
+  hipLaunchKernelGGL(k_conv1_fwd_pool_pipe<PF>, dim3(kPD * NB), dim3(256), 0, as_stream(stream), ptr<const uint8_t>(x8), \
+                     ptr<const int>(idx), ptr<const uint16_t>(w8), ptr<const float>(scale), ptr<const float>(shift), B, \
+                     ptr<uint16_t>(out), ptr<uint8_t>(amax))
+  if (pf == 1) NIDT_C1(1); else if (pf == 3) NIDT_C1(3); else NIDT_C1(2);
+#undef NIDT_C1
   NIDT_CHECK(hipGetLastError());
 }
 
