@@ -20,7 +20,9 @@
 //  * k_pack_conv_w — fp32 flat master weights -> bf16 [G][Cout][27][Cin] (+ flipped/transposed copy
 //                  for dgrad), scaled by an optional factor.
 #include <cmath>
+#include <array>
 #include <cstdlib>
+#include <map>
 
 #include "common.h"
 
@@ -305,6 +307,8 @@ typedef int i32x4_t __attribute__((ext_vector_type(4)));
 typedef int i32x2_t __attribute__((ext_vector_type(2)));
 __device__ i32x2_t nidt_raw_buffer_load_v2i32(i32x4_t rsrc, int voffset, int soffset, int aux)
     __asm("llvm.amdgcn.raw.buffer.load.v2i32");
+__device__ int nidt_raw_buffer_load_i32(i32x4_t rsrc, int voffset, int soffset, int aux)
+    __asm("llvm.amdgcn.raw.buffer.load.i32");
 __device__ void nidt_raw_buffer_load_lds(i32x4_t rsrc, __attribute__((address_space(3))) uint32_t* lds, int size,
                                          int voffset, int soffset, int offset, int aux)
     __asm("llvm.amdgcn.raw.buffer.load.lds");
@@ -998,8 +1002,15 @@ int conv_wgrad_nsplit_g(int G, int B, int D, int H, int W, int Cin, int Cout, in
   return wgrad_nsplit_mk(G, Mg, kt * Cin, Cout);
 }
 
+static int wgrad_nsplit_base(int base, int G, int Mg, int K, int Cout, double step_us, double overhead_steps);
+
 static int wgrad_nsplit_mk(int G, int Mg, int K, int Cout) {
-  const int base = G * (Cout / kWgCO) * ceil_div(K, kWgKC);
+  return wgrad_nsplit_base(G * (Cout / kWgCO) * ceil_div(K, kWgKC), G, Mg, K, Cout, 1.28, 12.0);
+}
+
+// base = output tiles (blocks per split) of the wgrad kernel in use; step_us / overhead_steps = its cost per
+// 64-position step per block slot and its fixed cost in steps
+static int wgrad_nsplit_base(int base, int G, int Mg, int K, int Cout, double step_us, double overhead_steps) {
   static const bool legacy = [] {
     const char* e = getenv("NIDT_WG_NSPLIT_LEGACY");
     return e && e[0] == '1';
@@ -1014,7 +1025,8 @@ static int wgrad_nsplit_mk(int G, int Mg, int K, int Cout) {
     const int maxns = max(1, Mg / (K >= 3000 ? 1024 : 512));
     return max(1, min(ns, maxns));
   }
-  constexpr double kSlots = 512.0, kStepUs = 1.28, kOverheadSteps = 12.0, kBytesPerUs = 5.0e6;
+  constexpr double kSlots = 512.0, kBytesPerUs = 5.0e6;
+  const double kStepUs = step_us, kOverheadSteps = overhead_steps;
   const double slab_bytes = 8.0 * G * Cout * K;  // fp32 write + read per split
   const int maxns = max(1, min(64, Mg / 512));  // keep >= 8 steps per block
   int best = 1;
@@ -1189,6 +1201,268 @@ __global__ __launch_bounds__(256 * NCH, 2 / NCH) void k_conv_wgrad_dma(ConvWgDma
         for (int r = 0; r < 4; ++r) out[(int64_t)(16 * i + 4 * fq + r) * a.K + k] = acc[i][j][r];
     }
   }
+}
+
+// ------------------------------------------------------------------------------------------------
+// k_conv_wgrad_tri — wgrad of an unpadded 3x3x3 stride-1 conv (AlexNet3D conv2: 64 -> 128 channels on 19x23x19)
+// with the X operand staged once per k-step for THREE taps.
+//
+// k_conv_wgrad_dma stages, per 64-position k-step, one [64 positions][64 channels] X tile per tap of its 4-tap
+// k-column block plus the dY tile: 40 KB of LDS-DMA per 128 MFMAs, ~78 B/clk/CU at the matrix rate against the
+// ~33 B/clk/CU one CU pulls from L2 by LDS-DMA (MI355X_MICROARCH.md, gather into LDS), so it runs at 29 % MFMA
+// busy with its waves parked on the DMA 55 % of the time (profiles/r2_pmc_alexnet_g64.txt).  The taps kw = 0,1,2
+// of one (kd, kh) read input rows b(p) + kw: for 64 consecutive output positions the union of those rows is a
+// few runs of consecutive input rows (<= 80 for conv2; one run per output row band, split only where the band
+// crosses a depth slice or a sample).  A block here owns 128 output channels x one (kd, kh, 64-channel chunk)
+// triplet = 192 k-columns; per k-step it stages the union (<= 80 rows) and the dY tile (64 x 128 channels):
+// 26 KB per 192 MFMAs, 2.3x fewer bytes per MFMA.  Wave (wc, kw) computes co half wc x tap kw; its X fragment
+// rows are union row idx(p) + kw.  Step table (k_wgrad_step_table, per 64-position step of a client): the union
+// rows' voxel offsets of tap (0,0,0) (-1 = unused -> read out of range -> 0) and idx(p) per position.
+constexpr int kWtU = 80;            // union rows per step (cap)
+constexpr int kWtST = kWtU + 64;    // ints per step-table entry
+struct ConvWgTriArgs {
+  const uint16_t* x;    // [G*B, D, H, W, Cin]
+  const uint16_t* dy;   // [G, Mg, Cout]
+  const int* stab;      // [nsteps][kWtST]
+  float* part;          // [nsplit, G, Cout, K]
+  int D, H, W, Cin, Cout, Mg, K, nsplit, chunk, G, nKT, nCT, nstab;
+  int64_t xclient;
+};
+
+__global__ __launch_bounds__(64) void k_wgrad_step_table(int* tab, int Mg, int D, int H, int W) {
+  __shared__ int b[64];
+  const int Do = D - 2, Ho = H - 2, Wo = W - 2, S = Do * Ho * Wo;
+  const int s = blockIdx.x, p = threadIdx.x, m = 64 * s + p;
+  int base = -1;
+  if (m < Mg) {
+    const int nl = m / S, r = m - nl * S, od = r / (Ho * Wo), r2 = r - od * Ho * Wo, oh = r2 / Wo, ow = r2 - oh * Wo;
+    base = ((nl * D + od) * H + oh) * W + ow;
+  }
+  b[p] = base;
+  __syncthreads();
+  if (p != 0) return;
+  int* rows = tab + (int64_t)s * kWtST;
+  int* idx = rows + kWtU;
+  int cnt = 0, last = -10;
+  for (int q = 0; q < 64; ++q) {  // bases increase with q: rows of the current run are contiguous up to `last`
+    const int bq = b[q];
+    if (bq < 0) { idx[q] = 0; continue; }
+    int first;
+    if (cnt > 0 && bq <= last) { idx[q] = cnt - 1 - (last - bq); first = last + 1; }
+    else { idx[q] = cnt; first = bq; }
+    for (int r = first; r <= bq + 2; ++r) {
+      if (cnt < kWtU) rows[cnt] = r;
+      ++cnt;
+    }
+    last = max(last, bq + 2);
+  }
+  for (int u = cnt; u < kWtU; ++u) rows[u] = -1;
+}
+
+// largest union of one 64-position step (same rule as k_wgrad_step_table), cached per shape
+static int wgrad_tri_umax(int B, int D, int H, int W) {
+  static std::map<std::array<int, 4>, int> cache;
+  const std::array<int, 4> key{B, D, H, W};
+  auto it = cache.find(key);
+  if (it != cache.end()) return it->second;
+  const int Do = D - 2, Ho = H - 2, Wo = W - 2, S = Do * Ho * Wo, Mg = B * S;
+  int mx = 0;
+  for (int s0 = 0; s0 < Mg; s0 += 64) {
+    int cnt = 0, last = -10;
+    for (int m = s0; m < std::min(s0 + 64, Mg); ++m) {
+      const int nl = m / S, r = m - nl * S, od = r / (Ho * Wo), r2 = r - od * Ho * Wo, oh = r2 / Wo, ow = r2 - oh * Wo;
+      const int bq = ((nl * D + od) * H + oh) * W + ow;
+      const int first = (cnt > 0 && bq <= last) ? last + 1 : bq;
+      cnt += std::max(0, bq + 3 - first);
+      last = std::max(last, bq + 2);
+    }
+    mx = std::max(mx, cnt);
+  }
+  cache[key] = mx;
+  return mx;
+}
+
+__global__ __launch_bounds__(384, 2) void k_conv_wgrad_tri(ConvWgTriArgs a) {
+  constexpr int NW = 6, XG = kWtU * kWdRow, BUFE = XG + 2 * kWdGroup;
+  constexpr int XP = kWtU / 8, XPW = (XP + NW - 1) / NW;  // union pieces (8 rows each) per wave
+  constexpr int DP = 16, DPW = (DP + NW - 1) / NW;        // dY pieces (8 positions x 64 co) per wave
+  __shared__ __attribute__((aligned(16))) uint16_t smem[2 * BUFE];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wc = wid / 3, kw = wid - 3 * wc;
+  const int id = xcd_remap(blockIdx.x, gridDim.x);
+  const int kt = id % a.nKT, r1 = id / a.nKT;
+  const int ct = r1 % a.nCT, r2 = r1 / a.nCT;
+  const int sp = r2 % a.nsplit, g = r2 / a.nsplit;
+  const int Cin = a.Cin, nck = Cin / 64;
+  const int trip = kt / nck, cc = kt - trip * nck;  // trip = kd * 3 + kh
+  const int kd = trip / 3, kh = trip - 3 * kd;
+  const int co0 = ct * 128;
+  const int p_begin = sp * a.chunk, p_end = min(a.Mg, p_begin + a.chunk);
+  const i32x4_t rx = make_rsrc(a.x + (int64_t)g * a.xclient, (uint32_t)(a.xclient * 2));
+  const i32x4_t rd = make_rsrc(a.dy + (int64_t)g * a.Mg * a.Cout, (uint32_t)((int64_t)a.Mg * a.Cout * 2));
+  const i32x4_t rt = make_rsrc(a.stab, (uint32_t)a.nstab * kWtST * 4u);
+  const int lr = lane >> 3, ls = lane & 7;
+  const int xadd = (kd * a.H + kh) * a.W;  // voxel offset of tap (kd, kh, 0)
+  // per-lane constant parts: union row u of piece xp = wid*XPW + i, dY row / co of piece dp = wid*DPW + i
+  int xcol[XPW], dcol[DPW], dls[DPW];
+#pragma unroll
+  for (int i = 0; i < XPW; ++i) {
+    const int u = 8 * (wid * XPW + i) + lr;
+    xcol[i] = (cc * 64 + ((ls ^ swz_wd(u)) << 3)) * 2;
+  }
+#pragma unroll
+  for (int i = 0; i < DPW; ++i) {
+    const int dp = min(wid * DPW + i, DP - 1), h = dp >> 3, sl = dp & 7, r = 8 * sl + lr;
+    dcol[i] = (r * a.Cout + co0 + 64 * h + ((ls ^ swz_wd(r)) << 3)) * 2;
+    dls[i] = h * kWdGroup + sl * 512;
+  }
+  const int gq = lane >> 4, li = lane & 15, qq = li >> 2, pp = li & 3;
+  const int rr0 = 8 * gq + qq, rr1 = rr0 + 4;
+  int trow[XPW], tix[4], tixn[4];
+#define WT_FETCH_ROWS(S)                                                                                      \
+  {                                                                                                           \
+    _Pragma("unroll") for (int i_ = 0; i_ < XPW; ++i_)                                                        \
+      trow[i_] = nidt_raw_buffer_load_i32(rt, ((S) * kWtST + 8 * (wid * XPW + i_) + lr) * 4, 0, 0);             \
+  }
+#define WT_FETCH_IDX(S, DST)                                                                                  \
+  {                                                                                                           \
+    _Pragma("unroll") for (int k_ = 0; k_ < 4; ++k_)                                                          \
+      DST[k_] = nidt_raw_buffer_load_i32(rt, ((S) * kWtST + kWtU + 32 * (k_ >> 1) + ((k_ & 1) ? rr1 : rr0)) * 4, \
+                                         0, 0);                                                               \
+  }
+#define WT_ISSUE(S, BUFI)                                                                                     \
+  {                                                                                                           \
+    uint16_t* sX_ = smem + (BUFI) * BUFE;                                                                     \
+    uint16_t* sD_ = sX_ + XG;                                                                                 \
+    _Pragma("unroll") for (int i_ = 0; i_ < XPW; ++i_)                                                        \
+      if (wid * XPW + i_ < XP)                                                                                \
+        blds16(rx, trow[i_] >= 0 ? (trow[i_] + xadd) * (2 * Cin) + xcol[i_] : kBufOOB,                      \
+               sX_ + (wid * XPW + i_) * 512);                                                                 \
+    _Pragma("unroll") for (int i_ = 0; i_ < DPW; ++i_)                                                        \
+      if (wid * DPW + i_ < DP) blds16(rd, (S) * 64 * (2 * a.Cout) + dcol[i_], sD_ + dls[i_]);               \
+  }
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int s0 = p_begin / 64, nsteps = (p_end - p_begin + 63) / 64;
+  if (nsteps > 0) {
+    WT_FETCH_ROWS(s0)
+    WT_FETCH_IDX(s0, tixn)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    WT_ISSUE(s0, 0)
+    if (nsteps > 1) WT_FETCH_ROWS(s0 + 1)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  for (int st = 0; st < nsteps; ++st) {
+    const int cur = st & 1;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) tix[k] = tixn[k];
+    if (st + 1 < nsteps) {
+      WT_ISSUE(s0 + st + 1, cur ^ 1)
+      if (st + 2 < nsteps) WT_FETCH_ROWS(s0 + st + 2)
+      WT_FETCH_IDX(s0 + st + 1, tixn)
+    }
+    const uint16_t* sX = smem + cur * BUFE;
+    const uint16_t* sD = sX + XG + wc * kWdGroup;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int ra = 32 * kk + rr0, rb = 32 * kk + rr1;
+      const int xa = tix[2 * kk] + kw, xb = tix[2 * kk + 1] + kw;
+      bf16x8 fa[4], fb[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int c = 2 * i + (pp >> 1);
+        fa[i] = tr_pair(sD + ra * kWdRow + ((c ^ swz_wd(ra)) << 3) + (pp & 1) * 4,
+                        sD + rb * kWdRow + ((c ^ swz_wd(rb)) << 3) + (pp & 1) * 4);
+        fb[i] = tr_pair(sX + xa * kWdRow + ((c ^ swz_wd(xa)) << 3) + (pp & 1) * 4,
+                        sX + xb * kWdRow + ((c ^ swz_wd(xb)) << 3) + (pp & 1) * 4);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    }
+    // retire the next stage's LDS-DMA; the step-table loads issued after it (rows for st+2, idx for st+1) may stay
+    if (st + 2 < nsteps) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(XPW + 4) : "memory");
+    else if (st + 1 < nsteps) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+#undef WT_ISSUE
+#undef WT_FETCH_IDX
+#undef WT_FETCH_ROWS
+  const int fr = lane & 15, fq = lane >> 4;
+  float* out = a.part + (((int64_t)sp * a.G + g) * a.Cout + co0 + 64 * wc) * a.K;
+  const int kcol = ((kd * 9 + kh * 3 + kw) * Cin) + cc * 64;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int k = kcol + 16 * j + fr;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) out[(int64_t)(16 * i + 4 * fq + r) * a.K + k] = acc[i][j][r];
+  }
+}
+
+// split factor of k_conv_wgrad_tri: the wgrad cost model over its own tiles (9 x Cin/64 triplets x Cout/128 x G)
+int conv3d_wgrad_tri_nsplit(int G, int B, int D, int H, int W, int Cin, int Cout) {
+  const int Mg = B * (D - 2) * (H - 2) * (W - 2);
+  // measured at 64 clients: ns 4 / 6 / 8 / 12 -> 3.27 / 3.28 / 3.09 / 3.12 ms (profiles/r2_ab_wgrad_tri.txt)
+  return wgrad_nsplit_base(G * (Cout / 128) * 9 * (Cin / 64), G, Mg, 27 * Cin, Cout, 1.0, 0.0);
+}
+
+// step table for k_conv_wgrad_tri: nsteps = ceil(Mg / 64) entries of kWtST ints (conv3d_wgrad_tri_table_size)
+int conv3d_wgrad_tri_table_size(int B, int D, int H, int W) {
+  const int Mg = B * (D - 2) * (H - 2) * (W - 2);
+  return ceil_div(Mg, 64) * kWtST;
+}
+
+void conv3d_wgrad_tri_table(uintptr_t tab, int B, int D, int H, int W, uintptr_t stream) {
+  const int Mg = B * (D - 2) * (H - 2) * (W - 2);
+  hipLaunchKernelGGL(k_wgrad_step_table, dim3(ceil_div(Mg, 64)), dim3(64), 0, as_stream(stream), ptr<int>(tab), Mg, D,
+                     H, W);
+  NIDT_CHECK(hipGetLastError());
+}
+
+// k_conv_wgrad_tri applies (unpadded 3x3x3, 128-channel output blocks, every step's union <= kWtU rows) and is not
+// switched off (NIDT_WG_TRI=0 -> k_conv_wgrad_dma, A/B)
+int conv3d_wgrad_tri_ok(int B, int D, int H, int W, int Cin, int Cout, int pad) {
+  static const int env = [] {
+    const char* e = getenv("NIDT_WG_TRI");
+    return e ? atoi(e) : 1;
+  }();
+  if (!env || pad != 0 || Cin % 64 != 0 || Cout % 128 != 0 || D < 3 || H < 3 || W < 3) return 0;
+  return wgrad_tri_umax(B, D, H, W) <= kWtU ? 1 : 0;
+}
+
+void conv3d_wgrad_tri(uintptr_t x, uintptr_t dy, uintptr_t part, uintptr_t grad, int64_t ldg, int64_t off, int G, int B,
+                      int D, int H, int W, int Cin, int Cout, int nsplit, float scale, uintptr_t stab, uintptr_t stream) {
+  NIDT_REQUIRE(conv3d_wgrad_tri_ok(B, D, H, W, Cin, Cout, 0), "conv3d_wgrad_tri: shape not eligible");
+  NIDT_REQUIRE(stab != 0 && nsplit >= 1, "conv3d_wgrad_tri: needs the step table");
+  ConvWgTriArgs d;
+  d.x = ptr<const uint16_t>(x); d.dy = ptr<const uint16_t>(dy); d.stab = ptr<const int>(stab); d.part = ptr<float>(part);
+  d.D = D; d.H = H; d.W = W; d.Cin = Cin; d.Cout = Cout;
+  d.Mg = B * (D - 2) * (H - 2) * (W - 2);
+  d.K = 27 * Cin; d.nsplit = nsplit; d.G = G;
+  d.chunk = ((ceil_div(d.Mg, nsplit) + 63) / 64) * 64;
+  d.nKT = 9 * (Cin / 64); d.nCT = Cout / 128;
+  d.nstab = ceil_div(d.Mg, 64);
+  d.xclient = (int64_t)B * D * H * W * Cin;
+  NIDT_REQUIRE(d.xclient * 2 < (1ll << 31) && (int64_t)d.Mg * Cout * 2 < (1ll << 31),
+               "conv3d_wgrad_tri: per-client tensors must stay below 2 GiB (32-bit buffer offsets)");
+  const int64_t nwg = (int64_t)d.nKT * d.nCT * nsplit * G;
+  hipStream_t s = as_stream(stream);
+  hipLaunchKernelGGL(k_conv_wgrad_tri, dim3((unsigned)nwg), dim3(384), 0, s, d);
+  NIDT_CHECK(hipGetLastError());
+  hipLaunchKernelGGL(k_wgrad_reduce, dim3(Cout, G), dim3(256), 27 * (Cin + 1) * sizeof(float), s, ptr<const float>(part),
+                     nsplit, G, Cout, Cin, 27, ptr<float>(grad), ldg, off, scale);
+  NIDT_CHECK(hipGetLastError());
 }
 
 // positions table of a general conv (kt taps, stride st, h/w padding pad, depth padding padd): Mg = B*Do*Ho*Wo rows

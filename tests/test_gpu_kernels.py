@@ -161,6 +161,16 @@ def test_conv3d_wgrad_and_dgrad(cin, cout, pad, sp, xf):
                        cout, pad, ns, 1.0, 0, _st())
         torch.cuda.synchronize()
         assert _relerr(grad0, grad) < 1e-5
+    if m.conv3d_wgrad_tri_ok(B, *sp, cin, cout, pad):  # three-tap union staging (conv2): same sums, other order
+        stab = torch.empty(m.conv3d_wgrad_tri_table_size(B, *sp), device=DEV, dtype=torch.int32)
+        m.conv3d_wgrad_tri_table(stab.data_ptr(), B, *sp, _st())
+        for ns_t in sorted({1, ns, 3}):
+            part_t = torch.empty(ns_t * G * cout * 27 * cin, device=DEV)
+            grad_t = torch.zeros_like(grad)
+            m.conv3d_wgrad_tri(x.data_ptr(), dy.data_ptr(), part_t.data_ptr(), grad_t.data_ptr(), P, 3, G, B, *sp, cin,
+                               cout, ns_t, 1.0, stab.data_ptr(), _st())
+            torch.cuda.synchronize()
+            assert _relerr(grad_t, grad) < 1e-4, ns_t
     # dgrad through the fwd kernel with flipped/transposed weights (packed from fp32 PyTorch layout)
     wt32 = torch.randn(G, cout, cin, 3, 3, 3, device=DEV) * 0.05
     theta = wt32.view(G, -1).contiguous()
