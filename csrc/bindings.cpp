@@ -32,12 +32,14 @@ void conv3d_wgrad(uintptr_t x, uintptr_t xs, uintptr_t xt, uintptr_t dy, uintptr
                   uintptr_t ptab, uintptr_t stream);
 void conv3d_pos_table(uintptr_t tab, int B, int D, int H, int W, int pad, uintptr_t stream);
 int conv3d_wgrad_nsplit(int G, int B, int D, int H, int W, int Cin, int Cout, int pad);
-int conv3d_wgrad_tri_table_size(int B, int D, int H, int W);
-int conv3d_wgrad_tri_nsplit(int G, int B, int D, int H, int W, int Cin, int Cout);
-void conv3d_wgrad_tri_table(uintptr_t tab, int B, int D, int H, int W, uintptr_t stream);
+int conv3d_wgrad_tri_table_size(int B, int D, int H, int W, int pad);
+int conv3d_wgrad_tri_nsplit(int G, int B, int D, int H, int W, int Cin, int Cout, int pad);
+void conv3d_wgrad_tri_table(uintptr_t tab, int B, int D, int H, int W, int pad, uintptr_t stream);
 int conv3d_wgrad_tri_ok(int B, int D, int H, int W, int Cin, int Cout, int pad);
+int conv3d_wgrad_tri_pick(int G, int B, int D, int H, int W, int Cin, int Cout, int pad);
 void conv3d_wgrad_tri(uintptr_t x, uintptr_t dy, uintptr_t part, uintptr_t grad, int64_t ldg, int64_t off, int G, int B,
-                      int D, int H, int W, int Cin, int Cout, int nsplit, float scale, uintptr_t stab, uintptr_t stream);
+                      int D, int H, int W, int Cin, int Cout, int pad, int nsplit, float scale, uintptr_t stab,
+                      uintptr_t stream);
 void pack_conv_w(uintptr_t theta, int64_t ldt, int64_t off, int G, int Cout, int Cin, float scale, uintptr_t wp,
                  uintptr_t wt, uintptr_t stream);
 void bn_relu_apply(uintptr_t y, uintptr_t sc, uintptr_t sh, uintptr_t h, int64_t npos, int C, int S, uintptr_t stream);
@@ -151,6 +153,7 @@ PYBIND11_MODULE(_nidt_hip, m) {
   DEF(conv3d_wgrad_tri_nsplit);
   DEF(conv3d_wgrad_tri_table);
   DEF(conv3d_wgrad_tri_ok);
+  DEF(conv3d_wgrad_tri_pick);
   DEF(conv3d_wgrad_tri);
   DEF(conv3d_pos_table);
   DEF(pack_conv_w);

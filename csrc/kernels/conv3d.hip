@@ -1002,15 +1002,17 @@ int conv_wgrad_nsplit_g(int G, int B, int D, int H, int W, int Cin, int Cout, in
   return wgrad_nsplit_mk(G, Mg, kt * Cin, Cout);
 }
 
-static int wgrad_nsplit_base(int base, int G, int Mg, int K, int Cout, double step_us, double overhead_steps);
+static int wgrad_nsplit_base(int base, int G, int Mg, int K, int Cout, double step_us, double overhead_steps,
+                             double slots);
 
 static int wgrad_nsplit_mk(int G, int Mg, int K, int Cout) {
-  return wgrad_nsplit_base(G * (Cout / kWgCO) * ceil_div(K, kWgKC), G, Mg, K, Cout, 1.28, 12.0);
+  return wgrad_nsplit_base(G * (Cout / kWgCO) * ceil_div(K, kWgKC), G, Mg, K, Cout, 1.28, 12.0, 512.0);
 }
 
 // base = output tiles (blocks per split) of the wgrad kernel in use; step_us / overhead_steps = its cost per
 // 64-position step per block slot and its fixed cost in steps
-static int wgrad_nsplit_base(int base, int G, int Mg, int K, int Cout, double step_us, double overhead_steps) {
+static int wgrad_nsplit_base(int base, int G, int Mg, int K, int Cout, double step_us, double overhead_steps,
+                             double slots) {
   static const bool legacy = [] {
     const char* e = getenv("NIDT_WG_NSPLIT_LEGACY");
     return e && e[0] == '1';
@@ -1025,7 +1027,8 @@ static int wgrad_nsplit_base(int base, int G, int Mg, int K, int Cout, double st
     const int maxns = max(1, Mg / (K >= 3000 ? 1024 : 512));
     return max(1, min(ns, maxns));
   }
-  constexpr double kSlots = 512.0, kBytesPerUs = 5.0e6;
+  constexpr double kBytesPerUs = 5.0e6;
+  const double kSlots = slots;  // resident blocks chip-wide
   const double kStepUs = step_us, kOverheadSteps = overhead_steps;
   const double slab_bytes = 8.0 * G * Cout * K;  // fp32 write + read per split
   const int maxns = max(1, min(64, Mg / 512));  // keep >= 8 steps per block
@@ -1204,74 +1207,88 @@ __global__ __launch_bounds__(256 * NCH, 2 / NCH) void k_conv_wgrad_dma(ConvWgDma
 }
 
 // ------------------------------------------------------------------------------------------------
-// k_conv_wgrad_tri — wgrad of an unpadded 3x3x3 stride-1 conv (AlexNet3D conv2: 64 -> 128 channels on 19x23x19)
-// with the X operand staged once per k-step for THREE taps.
+// k_conv_wgrad_tri — wgrad of a 3x3x3 stride-1 conv (AlexNet3D conv2-5) with the X operand staged once per
+// k-step for THREE taps.
 //
 // k_conv_wgrad_dma stages, per 64-position k-step, one [64 positions][64 channels] X tile per tap of its 4-tap
 // k-column block plus the dY tile: 40 KB of LDS-DMA per 128 MFMAs, ~78 B/clk/CU at the matrix rate against the
 // ~33 B/clk/CU one CU pulls from L2 by LDS-DMA (MI355X_MICROARCH.md, gather into LDS), so it runs at 29 % MFMA
 // busy with its waves parked on the DMA 55 % of the time (profiles/r2_pmc_alexnet_g64.txt).  The taps kw = 0,1,2
-// of one (kd, kh) read input rows b(p) + kw: for 64 consecutive output positions the union of those rows is a
-// few runs of consecutive input rows (<= 80 for conv2; one run per output row band, split only where the band
-// crosses a depth slice or a sample).  A block here owns 128 output channels x one (kd, kh, 64-channel chunk)
-// triplet = 192 k-columns; per k-step it stages the union (<= 80 rows) and the dY tile (64 x 128 channels):
-// 26 KB per 192 MFMAs, 2.3x fewer bytes per MFMA.  Wave (wc, kw) computes co half wc x tap kw; its X fragment
-// rows are union row idx(p) + kw.  Step table (k_wgrad_step_table, per 64-position step of a client): the union
-// rows' voxel offsets of tap (0,0,0) (-1 = unused -> read out of range -> 0) and idx(p) per position.
-constexpr int kWtU = 80;            // union rows per step (cap)
-constexpr int kWtST = kWtU + 64;    // ints per step-table entry
+// of one (kd, kh) read padded-input rows b(p) + kw: for 64 consecutive output positions the union of those rows
+// is a few runs of consecutive padded rows (74 for conv2, 92 for the padded 5x7x5 conv3-5; one run per band of
+// output rows, split where the band crosses a depth slice or a sample).  A block owns 64 NCH output channels x
+// one (kd, kh, 64-channel chunk) triplet = 192 k-columns; per k-step it stages the union (<= U rows) and the dY
+// tile: conv2 (NCH 2) 26 KB per 192 MFMAs, 2.3x fewer bytes per MFMA.  Wave (wc, kw) computes co block wc x tap
+// kw; its X fragment rows are union row idx(p) + kw.  Step table (k_wgrad_step_table, per 64-position step of a
+// client): per union row {voxel offset of its (kd, kh) = (0, 0) source, padded (d, h, w) code} and idx(p); a
+// row whose source for this block's (kd, kh) lies in the padding reads out of range -> 0.
+template <int U>
+struct WtTab {
+  static constexpr int kST = 2 * U + 64;  // ints per step entry: int2 rows[U], int idx[64]
+};
 struct ConvWgTriArgs {
   const uint16_t* x;    // [G*B, D, H, W, Cin]
   const uint16_t* dy;   // [G, Mg, Cout]
-  const int* stab;      // [nsteps][kWtST]
+  const int* stab;      // [nsteps][2U + 64]
   float* part;          // [nsplit, G, Cout, K]
-  int D, H, W, Cin, Cout, Mg, K, nsplit, chunk, G, nKT, nCT, nstab;
+  int D, H, W, Cin, Cout, Mg, K, nsplit, chunk, G, nKT, nCT, nstab, pad;
   int64_t xclient;
 };
 
-__global__ __launch_bounds__(64) void k_wgrad_step_table(int* tab, int Mg, int D, int H, int W) {
+static inline int wt_umax_cap(int umax) { return umax <= 80 ? 80 : (umax <= 96 ? 96 : 0); }
+
+__global__ __launch_bounds__(64) void k_wgrad_step_table(int* tab, int U, int Mg, int D, int H, int W, int pad) {
   __shared__ int b[64];
-  const int Do = D - 2, Ho = H - 2, Wo = W - 2, S = Do * Ho * Wo;
+  const int Dp = D + 2 * pad, Hp = H + 2 * pad, Wp = W + 2 * pad, Do = Dp - 2, Ho = Hp - 2, Wo = Wp - 2;
+  const int S = Do * Ho * Wo, VOL = Dp * Hp * Wp + 8;  // sample n's padded rows live at n * VOL + padded index
   const int s = blockIdx.x, p = threadIdx.x, m = 64 * s + p;
-  int base = -1;
+  int key = -1;
   if (m < Mg) {
     const int nl = m / S, r = m - nl * S, od = r / (Ho * Wo), r2 = r - od * Ho * Wo, oh = r2 / Wo, ow = r2 - oh * Wo;
-    base = ((nl * D + od) * H + oh) * W + ow;
+    key = nl * VOL + (od * Hp + oh) * Wp + ow;
   }
-  b[p] = base;
+  b[p] = key;
   __syncthreads();
   if (p != 0) return;
-  int* rows = tab + (int64_t)s * kWtST;
-  int* idx = rows + kWtU;
+  int* rows = tab + (int64_t)s * (2 * U + 64);
+  int* idx = rows + 2 * U;
   int cnt = 0, last = -10;
-  for (int q = 0; q < 64; ++q) {  // bases increase with q: rows of the current run are contiguous up to `last`
+  for (int q = 0; q < 64; ++q) {  // keys increase with q: rows of the current run are contiguous up to `last`
     const int bq = b[q];
     if (bq < 0) { idx[q] = 0; continue; }
     int first;
     if (cnt > 0 && bq <= last) { idx[q] = cnt - 1 - (last - bq); first = last + 1; }
     else { idx[q] = cnt; first = bq; }
     for (int r = first; r <= bq + 2; ++r) {
-      if (cnt < kWtU) rows[cnt] = r;
+      if (cnt < U) {
+        const int n = r / VOL, l = r - n * VOL, dp = l / (Hp * Wp), l2 = l - dp * Hp * Wp, hp = l2 / Wp, wp = l2 - hp * Wp;
+        rows[2 * cnt] = ((n * D + dp - pad) * H + hp - pad) * W + wp - pad;
+        rows[2 * cnt + 1] = dp | (hp << 10) | (wp << 20);
+      }
       ++cnt;
     }
     last = max(last, bq + 2);
   }
-  for (int u = cnt; u < kWtU; ++u) rows[u] = -1;
+  for (int u = cnt; u < U; ++u) {
+    rows[2 * u] = 0;
+    rows[2 * u + 1] = 1023;  // depth code out of every range: never read
+  }
 }
 
 // largest union of one 64-position step (same rule as k_wgrad_step_table), cached per shape
-static int wgrad_tri_umax(int B, int D, int H, int W) {
-  static std::map<std::array<int, 4>, int> cache;
-  const std::array<int, 4> key{B, D, H, W};
+static int wgrad_tri_umax(int B, int D, int H, int W, int pad) {
+  static std::map<std::array<int, 5>, int> cache;
+  const std::array<int, 5> key{B, D, H, W, pad};
   auto it = cache.find(key);
   if (it != cache.end()) return it->second;
-  const int Do = D - 2, Ho = H - 2, Wo = W - 2, S = Do * Ho * Wo, Mg = B * S;
+  const int Dp = D + 2 * pad, Hp = H + 2 * pad, Wp = W + 2 * pad, Do = Dp - 2, Ho = Hp - 2, Wo = Wp - 2;
+  const int S = Do * Ho * Wo, Mg = B * S, VOL = Dp * Hp * Wp + 8;
   int mx = 0;
   for (int s0 = 0; s0 < Mg; s0 += 64) {
     int cnt = 0, last = -10;
     for (int m = s0; m < std::min(s0 + 64, Mg); ++m) {
       const int nl = m / S, r = m - nl * S, od = r / (Ho * Wo), r2 = r - od * Ho * Wo, oh = r2 / Wo, ow = r2 - oh * Wo;
-      const int bq = ((nl * D + od) * H + oh) * W + ow;
+      const int bq = nl * VOL + (od * Hp + oh) * Wp + ow;
       const int first = (cnt > 0 && bq <= last) ? last + 1 : bq;
       cnt += std::max(0, bq + 3 - first);
       last = std::max(last, bq + 2);
@@ -1282,10 +1299,11 @@ static int wgrad_tri_umax(int B, int D, int H, int W) {
   return mx;
 }
 
-__global__ __launch_bounds__(384, 2) void k_conv_wgrad_tri(ConvWgTriArgs a) {
-  constexpr int NW = 6, XG = kWtU * kWdRow, BUFE = XG + 2 * kWdGroup;
-  constexpr int XP = kWtU / 8, XPW = (XP + NW - 1) / NW;  // union pieces (8 rows each) per wave
-  constexpr int DP = 16, DPW = (DP + NW - 1) / NW;        // dY pieces (8 positions x 64 co) per wave
+template <int NCH, int U, bool PADDED>
+__global__ __launch_bounds__(192 * NCH, 2) void k_conv_wgrad_tri(ConvWgTriArgs a) {
+  constexpr int NW = 3 * NCH, XG = U * kWdRow, BUFE = XG + NCH * kWdGroup, ST = WtTab<U>::kST;
+  constexpr int XP = U / 8, XPW = (XP + NW - 1) / NW;       // union pieces (8 rows each) per wave
+  constexpr int DP = 8 * NCH, DPW = (DP + NW - 1) / NW;     // dY pieces (8 positions x 64 co) per wave
   __shared__ __attribute__((aligned(16))) uint16_t smem[2 * BUFE];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1297,14 +1315,14 @@ __global__ __launch_bounds__(384, 2) void k_conv_wgrad_tri(ConvWgTriArgs a) {
   const int Cin = a.Cin, nck = Cin / 64;
   const int trip = kt / nck, cc = kt - trip * nck;  // trip = kd * 3 + kh
   const int kd = trip / 3, kh = trip - 3 * kd;
-  const int co0 = ct * 128;
+  const int co0 = ct * 64 * NCH;
   const int p_begin = sp * a.chunk, p_end = min(a.Mg, p_begin + a.chunk);
   const i32x4_t rx = make_rsrc(a.x + (int64_t)g * a.xclient, (uint32_t)(a.xclient * 2));
   const i32x4_t rd = make_rsrc(a.dy + (int64_t)g * a.Mg * a.Cout, (uint32_t)((int64_t)a.Mg * a.Cout * 2));
-  const i32x4_t rt = make_rsrc(a.stab, (uint32_t)a.nstab * kWtST * 4u);
+  const i32x4_t rt = make_rsrc(a.stab, (uint32_t)a.nstab * ST * 4u);
   const int lr = lane >> 3, ls = lane & 7;
-  const int xadd = (kd * a.H + kh) * a.W;  // voxel offset of tap (kd, kh, 0)
-  // per-lane constant parts: union row u of piece xp = wid*XPW + i, dY row / co of piece dp = wid*DPW + i
+  const int xadd = (kd * a.H + kh) * a.W;                   // voxel offset of tap (kd, kh, 0)
+  const int dlo = a.pad - kd, hlo = a.pad - kh;             // code ranges of sources inside the volume
   int xcol[XPW], dcol[DPW], dls[DPW];
 #pragma unroll
   for (int i = 0; i < XPW; ++i) {
@@ -1319,16 +1337,17 @@ __global__ __launch_bounds__(384, 2) void k_conv_wgrad_tri(ConvWgTriArgs a) {
   }
   const int gq = lane >> 4, li = lane & 15, qq = li >> 2, pp = li & 3;
   const int rr0 = 8 * gq + qq, rr1 = rr0 + 4;
-  int trow[XPW], tix[4], tixn[4];
+  i32x2_t trow[XPW];
+  int tix[4], tixn[4];
 #define WT_FETCH_ROWS(S)                                                                                      \
   {                                                                                                           \
     _Pragma("unroll") for (int i_ = 0; i_ < XPW; ++i_)                                                        \
-      trow[i_] = nidt_raw_buffer_load_i32(rt, ((S) * kWtST + 8 * (wid * XPW + i_) + lr) * 4, 0, 0);             \
+      trow[i_] = nidt_raw_buffer_load_v2i32(rt, ((S) * ST + 2 * (8 * (wid * XPW + i_) + lr)) * 4, 0, 0);      \
   }
 #define WT_FETCH_IDX(S, DST)                                                                                  \
   {                                                                                                           \
     _Pragma("unroll") for (int k_ = 0; k_ < 4; ++k_)                                                          \
-      DST[k_] = nidt_raw_buffer_load_i32(rt, ((S) * kWtST + kWtU + 32 * (k_ >> 1) + ((k_ & 1) ? rr1 : rr0)) * 4, \
+      DST[k_] = nidt_raw_buffer_load_i32(rt, ((S) * ST + 2 * U + 32 * (k_ >> 1) + ((k_ & 1) ? rr1 : rr0)) * 4, \
                                          0, 0);                                                               \
   }
 #define WT_ISSUE(S, BUFI)                                                                                     \
@@ -1336,9 +1355,14 @@ __global__ __launch_bounds__(384, 2) void k_conv_wgrad_tri(ConvWgTriArgs a) {
     uint16_t* sX_ = smem + (BUFI) * BUFE;                                                                     \
     uint16_t* sD_ = sX_ + XG;                                                                                 \
     _Pragma("unroll") for (int i_ = 0; i_ < XPW; ++i_)                                                        \
-      if (wid * XPW + i_ < XP)                                                                                \
-        blds16(rx, trow[i_] >= 0 ? (trow[i_] + xadd) * (2 * Cin) + xcol[i_] : kBufOOB,                      \
-               sX_ + (wid * XPW + i_) * 512);                                                                 \
+      if (wid * XPW + i_ < XP) {                                                                              \
+        const int c_ = trow[i_].y;                                                                            \
+        const bool ok_ = PADDED ? ((unsigned)((c_ & 1023) - dlo) < (unsigned)a.D &&                            \
+                                   (unsigned)(((c_ >> 10) & 1023) - hlo) < (unsigned)a.H &&                   \
+                                   (unsigned)((c_ >> 20) - a.pad) < (unsigned)a.W)                            \
+                                : (c_ & 1023) != 1023;                                                        \
+        blds16(rx, ok_ ? (trow[i_].x + xadd) * (2 * Cin) + xcol[i_] : kBufOOB, sX_ + (wid * XPW + i_) * 512);  \
+      }                                                                                                       \
     _Pragma("unroll") for (int i_ = 0; i_ < DPW; ++i_)                                                        \
       if (wid * DPW + i_ < DP) blds16(rd, (S) * 64 * (2 * a.Cout) + dcol[i_], sD_ + dls[i_]);               \
   }
@@ -1410,55 +1434,101 @@ __global__ __launch_bounds__(384, 2) void k_conv_wgrad_tri(ConvWgTriArgs a) {
   }
 }
 
-// split factor of k_conv_wgrad_tri: the wgrad cost model over its own tiles (9 x Cin/64 triplets x Cout/128 x G)
-int conv3d_wgrad_tri_nsplit(int G, int B, int D, int H, int W, int Cin, int Cout) {
-  const int Mg = B * (D - 2) * (H - 2) * (W - 2);
-  // measured at 64 clients: ns 4 / 6 / 8 / 12 -> 3.27 / 3.28 / 3.09 / 3.12 ms (profiles/r2_ab_wgrad_tri.txt)
-  return wgrad_nsplit_base(G * (Cout / 128) * 9 * (Cin / 64), G, Mg, 27 * Cin, Cout, 1.0, 0.0);
+static inline int conv_out_n(int n, int pad) { return n + 2 * pad - 2; }
+
+// output channels per k_conv_wgrad_tri block: 64 (3 waves).  NIDT_WG_TRI_NCH=2 gives 128-channel blocks (6 waves)
+// where Cout allows (A/B: slower on every AlexNet layer, conv2 3.28 vs 3.06 ms at 64 clients,
+// profiles/r2_ab_wgrad_tri.txt)
+static int wt_nch(int Cout) {
+  static const int env = [] {
+    const char* e = getenv("NIDT_WG_TRI_NCH");
+    return e ? atoi(e) : 1;
+  }();
+  return (Cout % 128 == 0 && env == 2) ? 2 : 1;
 }
 
-// step table for k_conv_wgrad_tri: nsteps = ceil(Mg / 64) entries of kWtST ints (conv3d_wgrad_tri_table_size)
-int conv3d_wgrad_tri_table_size(int B, int D, int H, int W) {
-  const int Mg = B * (D - 2) * (H - 2) * (W - 2);
-  return ceil_div(Mg, 64) * kWtST;
+// split factor of k_conv_wgrad_tri: the wgrad cost model over its own tiles (9 x Cin/64 triplets x co blocks x G)
+int conv3d_wgrad_tri_nsplit(int G, int B, int D, int H, int W, int Cin, int Cout, int pad) {
+  const int Mg = B * conv_out_n(D, pad) * conv_out_n(H, pad) * conv_out_n(W, pad);
+  const int nch = wt_nch(Cout);
+  // step cost ~1 us per block slot, no fixed term (128-channel blocks at 64 clients, conv2: ns 4 / 6 / 8 / 12 ->
+  // 3.27 / 3.28 / 3.09 / 3.12 ms, profiles/r2_ab_wgrad_tri.txt)
+  const int U = wt_umax_cap(wgrad_tri_umax(B, D, H, W, pad));
+  const int lds = 2 * (U * 128 + nch * 8192);  // bytes per block; 4 waves per SIMD by registers
+  const int per_cu = std::max(1, std::min(163840 / std::max(lds, 1), 16 / (3 * nch)));
+  return wgrad_nsplit_base(G * (Cout / (64 * nch)) * 9 * (Cin / 64), G, Mg, 27 * Cin, Cout, 1.0, 0.0, 256.0 * per_cu);
 }
 
-void conv3d_wgrad_tri_table(uintptr_t tab, int B, int D, int H, int W, uintptr_t stream) {
-  const int Mg = B * (D - 2) * (H - 2) * (W - 2);
-  hipLaunchKernelGGL(k_wgrad_step_table, dim3(ceil_div(Mg, 64)), dim3(64), 0, as_stream(stream), ptr<int>(tab), Mg, D,
-                     H, W);
+// step table for k_conv_wgrad_tri: ceil(Mg / 64) entries of 2U + 64 ints
+int conv3d_wgrad_tri_table_size(int B, int D, int H, int W, int pad) {
+  const int Mg = B * conv_out_n(D, pad) * conv_out_n(H, pad) * conv_out_n(W, pad);
+  const int U = wt_umax_cap(wgrad_tri_umax(B, D, H, W, pad));
+  NIDT_REQUIRE(U > 0, "conv3d_wgrad_tri_table_size: shape not eligible");
+  return ceil_div(Mg, 64) * (2 * U + 64);
+}
+
+void conv3d_wgrad_tri_table(uintptr_t tab, int B, int D, int H, int W, int pad, uintptr_t stream) {
+  const int Mg = B * conv_out_n(D, pad) * conv_out_n(H, pad) * conv_out_n(W, pad);
+  const int U = wt_umax_cap(wgrad_tri_umax(B, D, H, W, pad));
+  NIDT_REQUIRE(U > 0, "conv3d_wgrad_tri_table: shape not eligible");
+  NIDT_REQUIRE(D + 2 * pad < 1024 && H + 2 * pad < 1024 && W + 2 * pad < 1024, "conv3d_wgrad_tri_table: extents < 1024");
+  hipLaunchKernelGGL(k_wgrad_step_table, dim3(ceil_div(Mg, 64)), dim3(64), 0, as_stream(stream), ptr<int>(tab), U, Mg,
+                     D, H, W, pad);
   NIDT_CHECK(hipGetLastError());
 }
 
-// k_conv_wgrad_tri applies (unpadded 3x3x3, 128-channel output blocks, every step's union <= kWtU rows) and is not
-// switched off (NIDT_WG_TRI=0 -> k_conv_wgrad_dma, A/B)
+// k_conv_wgrad_tri applies (3x3x3 stride 1, pad <= 2, 64-channel multiples, every step's union <= 96 rows) and is
+// not switched off (NIDT_WG_TRI=0 -> k_conv_wgrad_dma everywhere, A/B; NIDT_WG_TRI=2 -> only unpadded convs)
 int conv3d_wgrad_tri_ok(int B, int D, int H, int W, int Cin, int Cout, int pad) {
   static const int env = [] {
     const char* e = getenv("NIDT_WG_TRI");
     return e ? atoi(e) : 1;
   }();
-  if (!env || pad != 0 || Cin % 64 != 0 || Cout % 128 != 0 || D < 3 || H < 3 || W < 3) return 0;
-  return wgrad_tri_umax(B, D, H, W) <= kWtU ? 1 : 0;
+  if (!env || (env == 2 && pad != 0) || pad < 0 || pad > 2 || Cin % 64 != 0 || Cout % 64 != 0) return 0;
+  if (conv_out_n(D, pad) < 1 || conv_out_n(H, pad) < 1 || conv_out_n(W, pad) < 1) return 0;
+  return wt_umax_cap(wgrad_tri_umax(B, D, H, W, pad)) > 0 ? 1 : 0;
+}
+
+// k_conv_wgrad_tri is the faster choice for this layer and client count: always for unpadded convs (conv2); padded
+// convs only with >= 64 K output positions per launch (the 5x7x5 conv3-5 at 64 clients: 0.47/0.64/0.45 ->
+// 0.37/0.52/0.36 ms; at 8 clients the 4-tap kernel is as fast or faster, 0.074/0.079/0.074 vs 0.076/0.090/0.074)
+int conv3d_wgrad_tri_pick(int G, int B, int D, int H, int W, int Cin, int Cout, int pad) {
+  if (!conv3d_wgrad_tri_ok(B, D, H, W, Cin, Cout, pad)) return 0;
+  const int64_t pos = (int64_t)G * B * conv_out_n(D, pad) * conv_out_n(H, pad) * conv_out_n(W, pad);
+  return (pad == 0 || pos >= 65536) ? 1 : 0;
 }
 
 void conv3d_wgrad_tri(uintptr_t x, uintptr_t dy, uintptr_t part, uintptr_t grad, int64_t ldg, int64_t off, int G, int B,
-                      int D, int H, int W, int Cin, int Cout, int nsplit, float scale, uintptr_t stab, uintptr_t stream) {
-  NIDT_REQUIRE(conv3d_wgrad_tri_ok(B, D, H, W, Cin, Cout, 0), "conv3d_wgrad_tri: shape not eligible");
+                      int D, int H, int W, int Cin, int Cout, int pad, int nsplit, float scale, uintptr_t stab,
+                      uintptr_t stream) {
+  NIDT_REQUIRE(conv3d_wgrad_tri_ok(B, D, H, W, Cin, Cout, pad), "conv3d_wgrad_tri: shape not eligible");
   NIDT_REQUIRE(stab != 0 && nsplit >= 1, "conv3d_wgrad_tri: needs the step table");
+  const int U = wt_umax_cap(wgrad_tri_umax(B, D, H, W, pad));
   ConvWgTriArgs d;
   d.x = ptr<const uint16_t>(x); d.dy = ptr<const uint16_t>(dy); d.stab = ptr<const int>(stab); d.part = ptr<float>(part);
-  d.D = D; d.H = H; d.W = W; d.Cin = Cin; d.Cout = Cout;
-  d.Mg = B * (D - 2) * (H - 2) * (W - 2);
+  d.D = D; d.H = H; d.W = W; d.Cin = Cin; d.Cout = Cout; d.pad = pad;
+  d.Mg = B * conv_out_n(D, pad) * conv_out_n(H, pad) * conv_out_n(W, pad);
   d.K = 27 * Cin; d.nsplit = nsplit; d.G = G;
   d.chunk = ((ceil_div(d.Mg, nsplit) + 63) / 64) * 64;
-  d.nKT = 9 * (Cin / 64); d.nCT = Cout / 128;
+  const int nch = wt_nch(Cout);
+  d.nKT = 9 * (Cin / 64); d.nCT = Cout / (64 * nch);
   d.nstab = ceil_div(d.Mg, 64);
   d.xclient = (int64_t)B * D * H * W * Cin;
   NIDT_REQUIRE(d.xclient * 2 < (1ll << 31) && (int64_t)d.Mg * Cout * 2 < (1ll << 31),
                "conv3d_wgrad_tri: per-client tensors must stay below 2 GiB (32-bit buffer offsets)");
   const int64_t nwg = (int64_t)d.nKT * d.nCT * nsplit * G;
+  NIDT_REQUIRE(nwg < (1ll << 31), "conv3d_wgrad_tri: grid too large");
   hipStream_t s = as_stream(stream);
-  hipLaunchKernelGGL(k_conv_wgrad_tri, dim3((unsigned)nwg), dim3(384), 0, s, d);
+  const dim3 grid((unsigned)nwg);
+#define NIDT_TRI(NC, UU)                                                                                       \
+  if (pad) hipLaunchKernelGGL((k_conv_wgrad_tri<NC, UU, true>), grid, dim3(192 * NC), 0, s, d);                \
+  else hipLaunchKernelGGL((k_conv_wgrad_tri<NC, UU, false>), grid, dim3(192 * NC), 0, s, d);
+  if (nch == 2) {
+    if (U == 80) { NIDT_TRI(2, 80) } else { NIDT_TRI(2, 96) }
+  } else {
+    if (U == 80) { NIDT_TRI(1, 80) } else { NIDT_TRI(1, 96) }
+  }
+#undef NIDT_TRI
   NIDT_CHECK(hipGetLastError());
   hipLaunchKernelGGL(k_wgrad_reduce, dim3(Cout, G), dim3(256), 27 * (Cin + 1) * sizeof(float), s, ptr<const float>(part),
                      nsplit, G, Cout, Cin, 27, ptr<float>(grad), ldg, off, scale);

@@ -89,11 +89,11 @@ class HipAlexNet3D:
             for (ci, bi, cin, cout, pad, sp) in (L2, L3, L4, L5):
                 b["w%dt" % ci] = e(G, cin, 27, cout)
                 b["ns%d" % ci] = self.m.conv3d_wgrad_nsplit(G, B, sp[0], sp[1], sp[2], cin, cout, pad)
-            # conv2 wgrad: three-tap union staging (k_conv_wgrad_tri, its own split factor) where the shape allows
-            ci, bi, cin, cout, pad, sp = L2
-            b["tri4"] = bool(self.m.conv3d_wgrad_tri_ok(B, *sp, cin, cout, pad))
-            if b["tri4"]:
-                b["ns4"] = self.m.conv3d_wgrad_tri_nsplit(G, B, *sp, cin, cout)
+            # wgrad with three-tap union staging (k_conv_wgrad_tri, its own split factor) where the shape allows
+            for (ci, bi, cin, cout, pad, sp) in (L2, L3, L4, L5):
+                b["tri%d" % ci] = bool(self.m.conv3d_wgrad_tri_pick(G, B, *sp, cin, cout, pad))
+                if b["tri%d" % ci]:
+                    b["ns%d" % ci] = self.m.conv3d_wgrad_tri_nsplit(G, B, *sp, cin, cout, pad)
             wg_sz = max(b["ns%d" % ci] * G * cout * 27 * cin for (ci, bi, cin, cout, pad, sp) in (L2, L3, L4, L5))
             b.update(
                 wgpart=e(wg_sz, dt=f32),
@@ -109,9 +109,10 @@ class HipAlexNet3D:
                 mg = B * (sp[0] + 2 * pad - 2) * (sp[1] + 2 * pad - 2) * (sp[2] + 2 * pad - 2)
                 b["pt%d" % ci] = e(mg, 2, dt=torch.int32)
                 self.m.conv3d_pos_table(_p(b["pt%d" % ci]), B, sp[0], sp[1], sp[2], pad, st0)
-            if b["tri4"]:
-                b["stab4"] = e(self.m.conv3d_wgrad_tri_table_size(B, *L2[5]), dt=torch.int32)
-                self.m.conv3d_wgrad_tri_table(_p(b["stab4"]), B, *L2[5], st0)
+            for (ci, bi, cin, cout, pad, sp) in (L2, L3, L4, L5):
+                if b["tri%d" % ci]:
+                    b["stab%d" % ci] = e(self.m.conv3d_wgrad_tri_table_size(B, *sp, pad), dt=torch.int32)
+                    self.m.conv3d_wgrad_tri_table(_p(b["stab%d" % ci]), B, *sp, pad, st0)
         self._cache[key] = b
         return b
 
@@ -242,9 +243,9 @@ class HipAlexNet3D:
                      o["features.%d.bias" % bi], o["features.%d.bias" % ci], _p(b["coef"]), _p(dy), ev, st)
 
         def wgrad(ci, x, xs, xt, dy, sp, cin, cout, pad):
-            if b.get("tri%d" % ci):
+            if b.get("tri%d" % ci) and xs is None:
                 m.conv3d_wgrad_tri(_p(x), _p(dy), _p(b["wgpart"]), _p(grads), P, o["features.%d.weight" % ci], G, B,
-                                   sp[0], sp[1], sp[2], cin, cout, b["ns%d" % ci], 1.0, _p(b["stab%d" % ci]), st)
+                                   sp[0], sp[1], sp[2], cin, cout, pad, b["ns%d" % ci], 1.0, _p(b["stab%d" % ci]), st)
                 return
             m.conv3d_wgrad(_p(x), _p(xs), _p(xt), _p(dy), _p(b["wgpart"]), _p(grads), P, o["features.%d.weight" % ci],
                            G, B, sp[0], sp[1], sp[2], cin, cout, pad, b["ns%d" % ci], 1.0, _p(b["pt%d" % ci]), st)

@@ -161,14 +161,14 @@ def test_conv3d_wgrad_and_dgrad(cin, cout, pad, sp, xf):
                        cout, pad, ns, 1.0, 0, _st())
         torch.cuda.synchronize()
         assert _relerr(grad0, grad) < 1e-5
-    if m.conv3d_wgrad_tri_ok(B, *sp, cin, cout, pad):  # three-tap union staging (conv2): same sums, other order
-        stab = torch.empty(m.conv3d_wgrad_tri_table_size(B, *sp), device=DEV, dtype=torch.int32)
-        m.conv3d_wgrad_tri_table(stab.data_ptr(), B, *sp, _st())
+    if not xf and m.conv3d_wgrad_tri_ok(B, *sp, cin, cout, pad):  # three-tap union staging: same sums, other order
+        stab = torch.empty(m.conv3d_wgrad_tri_table_size(B, *sp, pad), device=DEV, dtype=torch.int32)
+        m.conv3d_wgrad_tri_table(stab.data_ptr(), B, *sp, pad, _st())
         for ns_t in sorted({1, ns, 3}):
             part_t = torch.empty(ns_t * G * cout * 27 * cin, device=DEV)
             grad_t = torch.zeros_like(grad)
             m.conv3d_wgrad_tri(x.data_ptr(), dy.data_ptr(), part_t.data_ptr(), grad_t.data_ptr(), P, 3, G, B, *sp, cin,
-                               cout, ns_t, 1.0, stab.data_ptr(), _st())
+                               cout, pad, ns_t, 1.0, stab.data_ptr(), _st())
             torch.cuda.synchronize()
             assert _relerr(grad_t, grad) < 1e-4, ns_t
     # dgrad through the fwd kernel with flipped/transposed weights (packed from fp32 PyTorch layout)
@@ -194,6 +194,34 @@ def test_conv3d_wgrad_and_dgrad(cin, cout, pad, sp, xf):
             assert _relerr(dx[g * B:(g + 1) * B].float(), _cl(xin.grad)) < 1e-2
         # wp layout check
         assert torch.equal(wp[g].view(cout, 3, 3, 3, cin).permute(0, 4, 1, 2, 3), wt32[g].bfloat16())
+
+
+@pytest.mark.parametrize("cin,cout,pad,sp", [(64, 128, 0, (19, 23, 19)), (128, 192, 1, (5, 7, 5)),
+                                             (192, 128, 1, (5, 7, 5)), (128, 64, 2, (5, 7, 5))])
+def test_conv3d_wgrad_tri_matches_fp32(cin, cout, pad, sp):
+    """Three-tap union wgrad (k_conv_wgrad_tri) at B = 16 (steps crossing depth slices and samples, padded
+    geometries, 64- and 128-channel blocks) against the fp32 autograd weight gradient."""
+    m = _m()
+    G, B = 2, 16
+    assert m.conv3d_wgrad_tri_ok(B, *sp, cin, cout, pad)
+    torch.manual_seed(4)
+    x = torch.randn(G * B, *sp, cin, device=DEV).bfloat16()
+    Do, Ho, Wo = [s + 2 * pad - 2 for s in sp]
+    dy = torch.randn(G * B, Do, Ho, Wo, cout, device=DEV).bfloat16()
+    P = cout * cin * 27 + 5
+    stab = torch.empty(m.conv3d_wgrad_tri_table_size(B, *sp, pad), device=DEV, dtype=torch.int32)
+    m.conv3d_wgrad_tri_table(stab.data_ptr(), B, *sp, pad, _st())
+    ns = m.conv3d_wgrad_tri_nsplit(G, B, *sp, cin, cout, pad)
+    part = torch.empty(ns * G * cout * 27 * cin, device=DEV)
+    grad = torch.zeros(G, P, device=DEV)
+    m.conv3d_wgrad_tri(x.data_ptr(), dy.data_ptr(), part.data_ptr(), grad.data_ptr(), P, 5, G, B, *sp, cin, cout, pad,
+                       ns, 1.0, stab.data_ptr(), _st())
+    torch.cuda.synchronize()
+    for g in range(G):
+        xin = _cf(x[g * B:(g + 1) * B].float())
+        wref = torch.zeros(cout, cin, 3, 3, 3, device=DEV, requires_grad=True)
+        F.conv3d(xin, wref, None, 1, pad).backward(_cf(dy[g * B:(g + 1) * B].float()))
+        assert _relerr(grad[g, 5:5 + cout * cin * 27].view(cout, cin, 3, 3, 3), wref.grad) < 1e-4
 
 
 def _signed_gamma(G, C):

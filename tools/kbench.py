@@ -88,9 +88,9 @@ def main():
         add(name + "_dgrad", lambda ci=ci, sp=sp, cin=cin, cout=cout, pad=pad, Do=Do: m.conv3d_fwd(
             p(b[dys[ci]]), p(b["w%dt" % ci]), 0, 0, 0, p(b[dxs[ci]]), 0, G, B, *Do, cout, cin, 2 - pad, st), fl)
         if b.get("tri%d" % ci):  # the engine's conv2 wgrad (three-tap union staging)
-            add(name + "_wgrad", lambda xin=xin, ci=ci, sp=sp, cin=cin, cout=cout: m.conv3d_wgrad_tri(
+            add(name + "_wgrad", lambda xin=xin, ci=ci, sp=sp, cin=cin, cout=cout, pad=pad: m.conv3d_wgrad_tri(
                 p(b[xin]), p(b[dys[ci]]), p(b["wgpart"]), p(grads), P, o["features.%d.weight" % ci], G, B, *sp, cin,
-                cout, b["ns%d" % ci], 1.0, p(b["stab%d" % ci]), st), fl)
+                cout, pad, b["ns%d" % ci], 1.0, p(b["stab%d" % ci]), st), fl)
             continue
         add(name + "_wgrad", lambda xin=xin, ci=ci, sp=sp, cin=cin, cout=cout, pad=pad: m.conv3d_wgrad(
             p(b[xin]), 0, 0, p(b[dys[ci]]), p(b["wgpart"]), p(grads), P, o["features.%d.weight" % ci], G, B, *sp, cin,
