@@ -7,7 +7,6 @@ export PYTHONUNBUFFERED=1
 timeout -k 10 400 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_gpu_resnet2d.py \
   > gpurun_out/resnet/pytest.txt 2>&1 || { tail -40 gpurun_out/resnet/pytest.txt; exit 1; }
 tail -3 gpurun_out/resnet/pytest.txt
-timeout -k 10 120 python -u tools/dbg_resnet_graph3.py > gpurun_out/resnet/graph_poison.txt 2>&1 || exit 1
 cat gpurun_out/resnet/graph_poison.txt | grep -v amdgpu.ids
 timeout -k 10 300 python -u tools/bench_cifar.py --algorithm subavg --rounds 2 --warmup 1 \
   > gpurun_out/resnet/bench_subavg.txt 2>&1 || { tail -30 gpurun_out/resnet/bench_subavg.txt; exit 1; }
