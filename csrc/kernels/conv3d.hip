@@ -477,6 +477,133 @@ __global__ __launch_bounds__(64 * WM * WN, ((NST == 2 ? 8 : 4) / (WM * WN)) > 0 
   conv_fwd_epilogue<BCO, BP, WM, WN, BIAS, STATS, TCO, TP>(a, acc, red, g, pb, co0, wco, wp, fr, fq, tid);
 }
 
+// ------------------------------------------------------------------------------------------------
+// k_conv_fwd_tri — 3x3x3 stride-1 forward/dgrad with the B operand staged once per (kd, kh, 64-channel chunk)
+// triplet for the three kw taps.  k_conv_fwd_dma fetches a [BP positions][64 channels] B tile per tap; with the
+// B fetch removed from its k-loop (diagnostic build) the conv2 dgrad ran 3.79 -> 2.62 ms and conv2 fwd 3.33 ->
+// 2.77 ms at 64 clients, so the per-tap B traffic, not the MFMA work, sets their pace.  The rows the three kw taps
+// of a band of BP consecutive output positions read form a union of runs of consecutive padded-input rows (288
+// for conv2 fwd/dgrad, 360 for the padded 5x7x5 convs, vs 3 x 256); the block stages that union once per triplet
+// (single buffer: it is reloaded after the triplet's last tap, while the other block on the CU computes) and
+// double-buffers only the per-tap weight tile.  Union table (k_union_table with P = BP): per band the union rows'
+// sources and each position's union row; tap kw of position p reads union row idx(p) + kw.  Block numbering,
+// statistics blocks and epilogue are those of k_conv_fwd_dma (BP = 256), so the BN buffers are unchanged.
+template <int BCO, int WM, int WN, int U, bool PADDED, bool BIAS, bool STATS>
+__global__ __launch_bounds__(64 * WM * WN, 2) void k_conv_fwd_tri(ConvFwdArgs a, int nCO, const int* __restrict__ utab) {
+  constexpr int NW = WM * WN, BP = 64 * WN, BK = 64;
+  constexpr int WCO = BCO / WM, WP = 64, TCO = WCO / 16, TP = WP / 16;
+  constexpr int A_ELEMS = BCO * BK, ST = 2 * U + BP;
+  constexpr int A_INSTR = BCO / (8 * NW);
+  constexpr int UP = U / 8, UPW = (UP + NW - 1) / NW;  // union pieces (8 rows) per wave
+  static_assert(A_INSTR >= 1 && U % 8 == 0, "tile split");
+  __shared__ __attribute__((aligned(16))) uint16_t smem[2 * A_ELEMS + U * BK];
+  uint16_t* const sAb = smem;
+  uint16_t* const sU = smem + 2 * A_ELEMS;
+
+  const int nwg = gridDim.x;
+  const int id = xcd_remap(blockIdx.x, nwg);
+  const int cot = id % nCO, rest = id / nCO;
+  const int pb = rest % a.nPB, g = rest / a.nPB;
+  const int co0 = cot * BCO;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wco = wid / WN, wp = wid % WN;
+  const int Cin = a.Cin, nck = Cin / BK, ntr = 9 * nck, nks = 3 * ntr;
+  const int lrow = lane >> 3, slot = lane & 7;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int* ent = utab + (int64_t)pb * ST;
+  int uoff[UPW], ucode[UPW];
+#pragma unroll
+  for (int i = 0; i < UPW; ++i) {
+    const int u = 8 * (wid * UPW + i) + lrow;
+    uoff[i] = 0;
+    ucode[i] = 1023;
+    if (wid * UPW + i < UP) {
+      uoff[i] = ent[2 * u] * (Cin * 2) + ((slot ^ swz_dma(u)) << 4);
+      ucode[i] = ent[2 * u + 1];
+    }
+  }
+  int hrow[TP];
+#pragma unroll
+  for (int j = 0; j < TP; ++j) hrow[j] = ent[2 * U + wp * WP + j * 16 + fr];
+  int aoff[A_INSTR];
+#pragma unroll
+  for (int i = 0; i < A_INSTR; ++i) {
+    const int row = 8 * (wid * A_INSTR + i) + lrow;
+    aoff[i] = ((co0 + row) * 27 * Cin + ((slot ^ swz_dma(row)) << 3)) * 2;
+  }
+  const int64_t xcl = (int64_t)a.B * a.D * a.H * a.W * Cin;
+  const i32x4_t rxs = make_rsrc(a.x + (int64_t)g * xcl, (uint32_t)(xcl * 2));
+  const i32x4_t rws = make_rsrc(a.w + (int64_t)g * a.Cout * 27 * Cin, (uint32_t)(a.Cout * 27 * Cin * 2));
+
+  auto issue_a = [&](int ks, int buf) {  // weight tile of tap kw of triplet q = ks / 3
+    const int q = ks / 3, kw = ks - 3 * q, trip = q / nck, cc = q - trip * nck;
+    const int woff = ((trip * 3 + kw) * Cin + cc * BK) * 2;  // tap = kd*9 + kh*3 + kw = trip*3 + kw
+    uint16_t* sA = sAb + buf * A_ELEMS;
+#pragma unroll
+    for (int i = 0; i < A_INSTR; ++i) blds16(rws, aoff[i] + woff, sA + (wid * A_INSTR + i) * 512);
+  };
+  auto issue_u = [&](int q) {  // union rows of triplet q (its (kd, kh) shift and 64-channel chunk)
+    const int trip = q / nck, cc = q - trip * nck, kd = trip / 3, kh = trip - 3 * kd;
+    const int add = ((kd * a.H + kh) * a.W) * (Cin * 2) + cc * (BK * 2);
+    const int dlo = a.pad - kd, hlo = a.pad - kh;
+#pragma unroll
+    for (int i = 0; i < UPW; ++i) {
+      if (wid * UPW + i >= UP) continue;
+      const int c = ucode[i];
+      const bool ok = PADDED ? ((unsigned)((c & 1023) - dlo) < (unsigned)a.D &&
+                                (unsigned)(((c >> 10) & 1023) - hlo) < (unsigned)a.H &&
+                                (unsigned)((c >> 20) - a.pad) < (unsigned)a.W)
+                             : (c & 1023) != 1023;
+      blds16(rxs, ok ? uoff[i] + add : kBufOOB, sU + (wid * UPW + i) * 512);
+    }
+  };
+
+  f32x4 acc[TCO][TP];
+#pragma unroll
+  for (int i = 0; i < TCO; ++i)
+#pragma unroll
+    for (int j = 0; j < TP; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  issue_u(0);
+  issue_a(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  for (int ks = 0; ks < nks; ++ks) {
+    const int q = ks / 3, kw = ks - 3 * q;
+    if (ks + 1 < nks) issue_a(ks + 1, (ks + 1) & 1);
+    const uint16_t* sA = sAb + (ks & 1) * A_ELEMS;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 fa[TCO], fb[TP];
+#pragma unroll
+      for (int i = 0; i < TCO; ++i) {
+        const int r = wco * WCO + i * 16 + fr;
+        fa[i] = *reinterpret_cast<const bf16x8*>(&sA[r * BK + (((4 * kk + fq) ^ swz_dma(r)) << 3)]);
+      }
+#pragma unroll
+      for (int j = 0; j < TP; ++j) {
+        const int r = hrow[j] + kw;
+        fb[j] = *reinterpret_cast<const bf16x8*>(&sU[r * BK + (((4 * kk + fq) ^ swz_dma(r)) << 3)]);
+      }
+#pragma unroll
+      for (int i = 0; i < TCO; ++i)
+#pragma unroll
+        for (int j = 0; j < TP; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (kw == 2 && q + 1 < ntr) {  // every wave is done with this triplet's union: reload it for the next one
+      issue_u(q + 1);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+    }
+  }
+  __syncthreads();
+  conv_fwd_epilogue<BCO, BP, WM, WN, BIAS, STATS, TCO, TP>(a, acc, reinterpret_cast<float*>(smem), g, pb, co0, wco, wp, fr,
+                                                         fq, tid);
+}
+
 // Finish of a split-K forward without bias / statistics: y = bf16(sum over the ksplit slabs), 4 values per thread
 __global__ __launch_bounds__(256) void k_fwd_splitk_sum(const float* __restrict__ part, int ksplit, int64_t n4,
                                                         uint16_t* __restrict__ y) {
@@ -800,6 +927,89 @@ int conv3d_fwd_bp(int Cin, int Cout, int xf, int G, int Mg) {
   }();
   if (bp512 && nwg256 >= 4096) return 512;
   return 256;
+}
+
+static int union_umax(int B, int D, int H, int W, int pad, int P);
+__global__ void k_union_table(int* tab, int U, int P, int Mg, int D, int H, int W, int pad);
+
+static inline int ft_ucap(int umax) { return umax <= 320 ? 320 : (umax <= 384 ? 384 : 0); }
+
+// k_conv_fwd_tri is used for this forward/dgrad (3x3x3 stride 1, 256-position blocks, union <= 384 rows, no split-K,
+// and measured faster for the shape): NIDT_FWD_TRI=0 turns it off (A/B against k_conv_fwd_dma)
+// the shape is supported by k_conv_fwd_tri (any client count; 256-position blocks)
+int conv3d_fwd_tri_ok(int B, int D, int H, int W, int Cin, int Cout, int pad) {
+  if (Cin % 64 != 0 || Cout % 64 != 0 || pad < 0 || pad > 2 || (int64_t)Cin * 27 > 27 * kMaxCin) return 0;
+  const int Mg = B * (D + 2 * pad - 2) * (H + 2 * pad - 2) * (W + 2 * pad - 2);
+  if (D + 2 * pad < 3 || H + 2 * pad < 3 || W + 2 * pad < 3 || Mg <= 0) return 0;
+  return ft_ucap(union_umax(B, D, H, W, pad, 256)) > 0 ? 1 : 0;
+}
+
+int conv3d_fwd_tri_pick(int G, int B, int D, int H, int W, int Cin, int Cout, int pad) {
+  static const int env = [] {
+    const char* e = getenv("NIDT_FWD_TRI");
+    return e ? atoi(e) : 1;
+  }();
+  if (!env || !conv3d_fwd_tri_ok(B, D, H, W, Cin, Cout, pad)) return 0;
+  const int Mg = B * (D + 2 * pad - 2) * (H + 2 * pad - 2) * (W + 2 * pad - 2);
+  if (conv3d_fwd_bp(Cin, Cout, 0, G, Mg) != 256 || conv3d_fwd_ksplit(Cin, Cout, G, Mg) > 1) return 0;
+  const int U = ft_ucap(union_umax(B, D, H, W, pad, 256));
+  // measured (profiles/r2_ab_fwd_tri.txt): conv2 fwd (unpadded) 3.25 -> 2.71 ms at 64 clients, 0.43 -> 0.34 at 8;
+  // conv2 dgrad (pad 2, 320-row unions) 3.80 -> 3.67 at 64 clients but 0.48 -> 0.49 at 8; the padded 5x7x5 convs
+  // (384-row unions) 5-25 % slower.  So: unpadded always, padded only with 320-row unions and >= 4 M positions.
+  if (pad == 0) return 1;
+  return (U <= 320 && (int64_t)G * Mg >= (4ll << 20)) ? 1 : 0;
+}
+
+int conv3d_fwd_tri_table_size(int B, int D, int H, int W, int pad) {
+  const int Mg = B * (D + 2 * pad - 2) * (H + 2 * pad - 2) * (W + 2 * pad - 2);
+  const int U = ft_ucap(union_umax(B, D, H, W, pad, 256));
+  NIDT_REQUIRE(U > 0, "conv3d_fwd_tri_table_size: shape not eligible");
+  return ceil_div(Mg, 256) * (2 * U + 256);
+}
+
+void conv3d_fwd_tri_table(uintptr_t tab, int B, int D, int H, int W, int pad, uintptr_t stream) {
+  const int Mg = B * (D + 2 * pad - 2) * (H + 2 * pad - 2) * (W + 2 * pad - 2);
+  const int U = ft_ucap(union_umax(B, D, H, W, pad, 256));
+  NIDT_REQUIRE(U > 0, "conv3d_fwd_tri_table: shape not eligible");
+  NIDT_REQUIRE(D + 2 * pad < 1024 && H + 2 * pad < 1024 && W + 2 * pad < 1024, "conv3d_fwd_tri_table: extents < 1024");
+  hipLaunchKernelGGL(k_union_table, dim3(ceil_div(Mg, 256)), dim3(256), 0, as_stream(stream), ptr<int>(tab), U, 256, Mg,
+                     D, H, W, pad);
+  NIDT_CHECK(hipGetLastError());
+}
+
+// forward (bias + BN block statistics optional; bias rows at stride bias_ld, 0 = Cout) through k_conv_fwd_tri
+void conv3d_fwd_tri(uintptr_t x, uintptr_t w, uintptr_t bias, int64_t bias_ld, uintptr_t y, uintptr_t stats, int G,
+                    int B, int D, int H, int W, int Cin, int Cout, int pad, uintptr_t utab, uintptr_t stream) {
+  NIDT_REQUIRE(conv3d_fwd_tri_ok(B, D, H, W, Cin, Cout, pad) && utab != 0, "conv3d_fwd_tri: shape not supported");
+  NIDT_REQUIRE((int64_t)B * D * H * W * Cin * 2 < (1ll << 31), "conv3d_fwd_tri: per-client input below 2 GiB");
+  const bool hb = bias != 0, st = stats != 0;
+  NIDT_REQUIRE(!st || hb, "conv3d_fwd_tri: statistics require a bias");
+  ConvFwdArgs a;
+  a.x = ptr<const uint16_t>(x); a.w = ptr<const uint16_t>(w); a.bias = ptr<const float>(bias);
+  a.xs = nullptr; a.xt = nullptr; a.y = ptr<uint16_t>(y); a.stats = ptr<float>(stats);
+  a.B = B; a.D = D; a.H = H; a.W = W; a.Cin = Cin; a.Cout = Cout; a.pad = pad; a.padd = pad; a.kt = 27; a.st = 1;
+  a.Do = D + 2 * pad - 2; a.Ho = H + 2 * pad - 2; a.Wo = W + 2 * pad - 2;
+  a.Mg = B * a.Do * a.Ho * a.Wo;
+  a.nPB = ceil_div(a.Mg, 256);
+  a.G = G;
+  a.bias_ld = bias_ld;
+  const int U = ft_ucap(union_umax(B, D, H, W, pad, 256));
+  const int bco = fwd_bco(Cout), nCO = Cout / bco;
+  const dim3 grid((unsigned)((int64_t)a.nPB * nCO * G));
+  hipStream_t s = as_stream(stream);
+  const int* tab = ptr<const int>(utab);
+#define NIDT_FT(BC, WM, UU, PD, BI, STT) \
+  hipLaunchKernelGGL((k_conv_fwd_tri<BC, WM, 4, UU, PD, BI, STT>), grid, dim3(256 * WM), 0, s, a, nCO, tab)
+#define NIDT_FT_B(BC, WM, UU, PD) \
+  if (st) NIDT_FT(BC, WM, UU, PD, true, true); else if (hb) NIDT_FT(BC, WM, UU, PD, true, false); else NIDT_FT(BC, WM, UU, PD, false, false);
+#define NIDT_FT_U(BC, WM)                                                                                        \
+  if (pad) { if (U == 320) { NIDT_FT_B(BC, WM, 320, true) } else { NIDT_FT_B(BC, WM, 384, true) } }             \
+  else { if (U == 320) { NIDT_FT_B(BC, WM, 320, false) } else { NIDT_FT_B(BC, WM, 384, false) } }
+  if (bco == 128) { NIDT_FT_U(128, 2) } else { NIDT_FT_U(64, 1) }
+#undef NIDT_FT_U
+#undef NIDT_FT_B
+#undef NIDT_FT
+  NIDT_CHECK(hipGetLastError());
 }
 
 int conv3d_fwd_nblocks(int B, int D, int H, int W, int pad, int bp) {
@@ -1219,7 +1429,7 @@ __global__ __launch_bounds__(256 * NCH, 2 / NCH) void k_conv_wgrad_dma(ConvWgDma
 // output rows, split where the band crosses a depth slice or a sample).  A block owns 64 NCH output channels x
 // one (kd, kh, 64-channel chunk) triplet = 192 k-columns; per k-step it stages the union (<= U rows) and the dY
 // tile: conv2 (NCH 2) 26 KB per 192 MFMAs, 2.3x fewer bytes per MFMA.  Wave (wc, kw) computes co block wc x tap
-// kw; its X fragment rows are union row idx(p) + kw.  Step table (k_wgrad_step_table, per 64-position step of a
+// kw; its X fragment rows are union row idx(p) + kw.  Step table (k_union_table, per 64-position step of a
 // client): per union row {voxel offset of its (kd, kh) = (0, 0) source, padded (d, h, w) code} and idx(p); a
 // row whose source for this block's (kd, kh) lies in the padding reads out of range -> 0.
 template <int U>
@@ -1237,23 +1447,28 @@ struct ConvWgTriArgs {
 
 static inline int wt_umax_cap(int umax) { return umax <= 80 ? 80 : (umax <= 96 ? 96 : 0); }
 
-__global__ __launch_bounds__(64) void k_wgrad_step_table(int* tab, int U, int Mg, int D, int H, int W, int pad) {
-  __shared__ int b[64];
+// Union table of a 3x3x3 stride-1 conv (pad in every dimension), one entry per band of P consecutive output positions
+// of a client: int2 rows[U] = {voxel offset of the union row's (kd, kh) = (0, 0) source, padded (d, h, w) code},
+// int idx[P] = union row of each position's tap (0, 0, 0).  The union is the set of padded-input rows b(p) + kw
+// (kw = 0..2) over the band, in increasing order; rows past the union get a depth code that no range admits.
+// One block of P threads per band (P <= 256); one thread merges the runs (allocation time only).
+__global__ __launch_bounds__(256) void k_union_table(int* tab, int U, int P, int Mg, int D, int H, int W, int pad) {
+  __shared__ int b[256];
   const int Dp = D + 2 * pad, Hp = H + 2 * pad, Wp = W + 2 * pad, Do = Dp - 2, Ho = Hp - 2, Wo = Wp - 2;
   const int S = Do * Ho * Wo, VOL = Dp * Hp * Wp + 8;  // sample n's padded rows live at n * VOL + padded index
-  const int s = blockIdx.x, p = threadIdx.x, m = 64 * s + p;
+  const int s = blockIdx.x, p = threadIdx.x, m = P * s + p;
   int key = -1;
-  if (m < Mg) {
+  if (p < P && m < Mg) {
     const int nl = m / S, r = m - nl * S, od = r / (Ho * Wo), r2 = r - od * Ho * Wo, oh = r2 / Wo, ow = r2 - oh * Wo;
     key = nl * VOL + (od * Hp + oh) * Wp + ow;
   }
-  b[p] = key;
+  if (p < P) b[p] = key;
   __syncthreads();
   if (p != 0) return;
-  int* rows = tab + (int64_t)s * (2 * U + 64);
+  int* rows = tab + (int64_t)s * (2 * U + P);
   int* idx = rows + 2 * U;
   int cnt = 0, last = -10;
-  for (int q = 0; q < 64; ++q) {  // keys increase with q: rows of the current run are contiguous up to `last`
+  for (int q = 0; q < P; ++q) {  // keys increase with q: rows of the current run are contiguous up to `last`
     const int bq = b[q];
     if (bq < 0) { idx[q] = 0; continue; }
     int first;
@@ -1275,18 +1490,18 @@ __global__ __launch_bounds__(64) void k_wgrad_step_table(int* tab, int U, int Mg
   }
 }
 
-// largest union of one 64-position step (same rule as k_wgrad_step_table), cached per shape
-static int wgrad_tri_umax(int B, int D, int H, int W, int pad) {
-  static std::map<std::array<int, 5>, int> cache;
-  const std::array<int, 5> key{B, D, H, W, pad};
+// largest union of one P-position band (same rule as k_union_table), cached per shape
+static int union_umax(int B, int D, int H, int W, int pad, int P) {
+  static std::map<std::array<int, 6>, int> cache;
+  const std::array<int, 6> key{B, D, H, W, pad, P};
   auto it = cache.find(key);
   if (it != cache.end()) return it->second;
   const int Dp = D + 2 * pad, Hp = H + 2 * pad, Wp = W + 2 * pad, Do = Dp - 2, Ho = Hp - 2, Wo = Wp - 2;
   const int S = Do * Ho * Wo, Mg = B * S, VOL = Dp * Hp * Wp + 8;
   int mx = 0;
-  for (int s0 = 0; s0 < Mg; s0 += 64) {
+  for (int s0 = 0; s0 < Mg; s0 += P) {
     int cnt = 0, last = -10;
-    for (int m = s0; m < std::min(s0 + 64, Mg); ++m) {
+    for (int m = s0; m < std::min(s0 + P, Mg); ++m) {
       const int nl = m / S, r = m - nl * S, od = r / (Ho * Wo), r2 = r - od * Ho * Wo, oh = r2 / Wo, ow = r2 - oh * Wo;
       const int bq = nl * VOL + (od * Hp + oh) * Wp + ow;
       const int first = (cnt > 0 && bq <= last) ? last + 1 : bq;
@@ -1298,6 +1513,8 @@ static int wgrad_tri_umax(int B, int D, int H, int W, int pad) {
   cache[key] = mx;
   return mx;
 }
+
+static int wgrad_tri_umax(int B, int D, int H, int W, int pad) { return union_umax(B, D, H, W, pad, 64); }
 
 template <int NCH, int U, bool PADDED>
 __global__ __launch_bounds__(192 * NCH, 2) void k_conv_wgrad_tri(ConvWgTriArgs a) {
@@ -1472,7 +1689,7 @@ void conv3d_wgrad_tri_table(uintptr_t tab, int B, int D, int H, int W, int pad, 
   const int U = wt_umax_cap(wgrad_tri_umax(B, D, H, W, pad));
   NIDT_REQUIRE(U > 0, "conv3d_wgrad_tri_table: shape not eligible");
   NIDT_REQUIRE(D + 2 * pad < 1024 && H + 2 * pad < 1024 && W + 2 * pad < 1024, "conv3d_wgrad_tri_table: extents < 1024");
-  hipLaunchKernelGGL(k_wgrad_step_table, dim3(ceil_div(Mg, 64)), dim3(64), 0, as_stream(stream), ptr<int>(tab), U, Mg,
+  hipLaunchKernelGGL(k_union_table, dim3(ceil_div(Mg, 64)), dim3(64), 0, as_stream(stream), ptr<int>(tab), U, 64, Mg,
                      D, H, W, pad);
   NIDT_CHECK(hipGetLastError());
 }

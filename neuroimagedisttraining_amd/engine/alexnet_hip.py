@@ -85,6 +85,18 @@ class HipAlexNet3D:
                 if ks > 1:
                     fp_sz = max(fp_sz, ks * G * mg * c_out)
         b["fpart"] = e(max(fp_sz, 1), dt=f32)
+        # forward / dgrad convs with the three-tap union B staging (k_conv_fwd_tri) and their union tables
+        st0 = torch.cuda.current_stream().cuda_stream
+        for (ci, bi, cin, cout, pad, sp) in (L2, L3, L4, L5):
+            out = tuple(d + 2 * pad - 2 for d in sp)
+            for tag, (c_in, c_out, vol, pd) in (("f", (cin, cout, sp, pad)), ("d", (cout, cin, out, 2 - pad))):
+                if tag == "d" and not train:
+                    continue
+                kname = "ks%s%d" % (tag, ci)
+                if b[kname] <= 1 and self.m.conv3d_fwd_tri_pick(G, B, *vol, c_in, c_out, pd):
+                    tab = e(self.m.conv3d_fwd_tri_table_size(B, *vol, pd), dt=torch.int32)
+                    self.m.conv3d_fwd_tri_table(_p(tab), B, *vol, pd, st0)
+                    b["ft" + kname] = tab
         if train:
             for (ci, bi, cin, cout, pad, sp) in (L2, L3, L4, L5):
                 b["w%dt" % ci] = e(G, cin, 27, cout)
@@ -120,6 +132,15 @@ class HipAlexNet3D:
         """conv3d_fwd, or its split-K form when ``b[key]`` (chosen at allocation) is > 1.  With ``theta`` the bias
         of conv ``ci`` is read straight from the flat parameter rows (row stride P), no per-step copy."""
         ks = b[key]
+        ft = b.get("ft" + key)
+        if ft is not None:  # union-staged B operand (k_conv_fwd_tri)
+            if theta is not None:
+                o = self.o["features.%d.bias" % ci]
+                bptr, bld = theta.data_ptr() + 4 * o, theta.stride(0)
+            else:
+                bptr, bld = _p(bias), 0
+            self.m.conv3d_fwd_tri(_p(x), _p(w), bptr, bld, _p(y), _p(stats), G, B, D, H, W, cin, cout, pad, _p(ft), st)
+            return
         if theta is not None and ks <= 1:
             o = self.o["features.%d.bias" % ci]
             self.m.conv3d_fwd_bld(_p(x), _p(w), theta.data_ptr() + 4 * o, theta.stride(0), _p(y), _p(stats), G, B, D,

@@ -91,6 +91,22 @@ def test_conv3d_fwd_stats(cin, cout, pad, sp, xf, G, B):
     yr_g = yr.view(G, Mg, cout).double()
     assert _relerr(mean, yr_g.mean(1)) < 1e-3
     assert _relerr(var, yr_g.var(1, unbiased=False)) < 1e-3
+    if not xf and bp == 256 and m.conv3d_fwd_tri_ok(B, *sp, cin, cout, pad):
+        # union-staged B operand (k_conv_fwd_tri) against the per-tap kernel and, without bias, the fp32 oracle
+        tab = torch.empty(m.conv3d_fwd_tri_table_size(B, *sp, pad), device=DEV, dtype=torch.int32)
+        m.conv3d_fwd_tri_table(tab.data_ptr(), B, *sp, pad, _st())
+        y3 = torch.empty_like(y)
+        st3 = torch.empty_like(stats)
+        m.conv3d_fwd_tri(x.data_ptr(), w.data_ptr(), bias.data_ptr(), 0, y3.data_ptr(), st3.data_ptr(), G, B, *sp, cin,
+                         cout, pad, tab.data_ptr(), _st())
+        y4 = torch.empty_like(y)  # no bias / statistics (the dgrad form)
+        m.conv3d_fwd_tri(x.data_ptr(), w.data_ptr(), 0, 0, y4.data_ptr(), 0, G, B, *sp, cin, cout, pad, tab.data_ptr(),
+                         _st())
+        torch.cuda.synchronize()
+        # same products; the k order differs when Cin > 64 (triplet-major vs tap-major) -> fp32 rounding only
+        assert (y3.float() - y.float()).abs().max() <= 1e-2 * y.float().abs().max()
+        assert _relerr(st3, stats) < 1e-4
+        assert _relerr(y4.float(), (yr.view(G, -1, cout) - bias.view(G, 1, cout)).view_as(yr)) < 1e-2
 
 
 @pytest.mark.parametrize("cin,cout,G", [(128, 192, 16), (192, 192, 16), (192, 128, 24), (128, 192, 1), (192, 128, 2)])

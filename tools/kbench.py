@@ -82,11 +82,12 @@ def main():
     for name, xin, ci, sp, cin, cout, pad in cfgs:
         Do = [s + 2 * pad - 2 for s in sp]
         fl = 2.0 * cin * 27 * cout * Do[0] * Do[1] * Do[2] * NB
-        add(name + "_fwd", lambda xin=xin, ci=ci, sp=sp, cin=cin, cout=cout, pad=pad: m.conv3d_fwd(
-            p(b[xin]), p(b["w%dp" % ci]), p(b["bias%d" % ci]), 0, 0, p(b[outs[ci]]), p(b["st%d" % ci]), G, B, *sp, cin,
+        # the engine's own launch choice (union-staged k_conv_fwd_tri, split-K or k_conv_fwd_dma)
+        add(name + "_fwd", lambda xin=xin, ci=ci, sp=sp, cin=cin, cout=cout, pad=pad: net._conv(
+            b, "ksf%d" % ci, b[xin], b["w%dp" % ci], b["bias%d" % ci], b[outs[ci]], b["st%d" % ci], G, B, *sp, cin,
             cout, pad, st), fl)
-        add(name + "_dgrad", lambda ci=ci, sp=sp, cin=cin, cout=cout, pad=pad, Do=Do: m.conv3d_fwd(
-            p(b[dys[ci]]), p(b["w%dt" % ci]), 0, 0, 0, p(b[dxs[ci]]), 0, G, B, *Do, cout, cin, 2 - pad, st), fl)
+        add(name + "_dgrad", lambda ci=ci, sp=sp, cin=cin, cout=cout, pad=pad, Do=Do: net._conv(
+            b, "ksd%d" % ci, b[dys[ci]], b["w%dt" % ci], None, b[dxs[ci]], None, G, B, *Do, cout, cin, 2 - pad, st), fl)
         if b.get("tri%d" % ci):  # the engine's conv2 wgrad (three-tap union staging)
             add(name + "_wgrad", lambda xin=xin, ci=ci, sp=sp, cin=cin, cout=cout, pad=pad: m.conv3d_wgrad_tri(
                 p(b[xin]), p(b[dys[ci]]), p(b["wgpart"]), p(grads), P, o["features.%d.weight" % ci], G, B, *sp, cin,
