@@ -1,4 +1,6 @@
 #!/bin/bash
+# NOTE: NIDT_FWD_DIAG existed only in the temporary diagnostic build recorded in profiles/r2_ab_fwd_tri.txt (B-tile
+# LDS-DMA skipped in the k-loop); on the tree this script just repeats the normal timings.
 set -o pipefail
 mkdir -p gpurun_out/fdiag; rm -f gpurun_out/fdiag/*
 export PYTHONUNBUFFERED=1 KBENCH_EVAL=0
