@@ -2,7 +2,7 @@
 # full state check: whole GPU suite (pytest.ini timeouts), smoke(), the driver's 1-GPU bench line, kbench at 64 / 8
 # clients, and a rocprofv3 kernel-trace of two bench rounds (summary only comes back)
 set -o pipefail
-mkdir -p gpurun_out/s2
+mkdir -p gpurun_out/s2; rm -rf gpurun_out/s2/*
 export PYTHONUNBUFFERED=1
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 timeout -k 10 900 python -u -m pytest tests -m gpu -v -s --timeout-method thread > gpurun_out/s2/pytest.txt 2>&1
