@@ -954,10 +954,11 @@ int conv3d_fwd_tri_pick(int G, int B, int D, int H, int W, int Cin, int Cout, in
   if (conv3d_fwd_bp(Cin, Cout, 0, G, Mg) != 256 || conv3d_fwd_ksplit(Cin, Cout, G, Mg) > 1) return 0;
   const int U = ft_ucap(union_umax(B, D, H, W, pad, 256));
   // measured (profiles/r2_ab_fwd_tri.txt): conv2 fwd (unpadded) 3.25 -> 2.71 ms at 64 clients, 0.43 -> 0.34 at 8;
-  // conv2 dgrad (pad 2, 320-row unions) 3.80 -> 3.67 at 64 clients but 0.48 -> 0.49 at 8; the padded 5x7x5 convs
-  // (384-row unions) 5-25 % slower.  So: unpadded always, padded only with 320-row unions and >= 4 M positions.
-  if (pad == 0) return 1;
-  return (U <= 320 && (int64_t)G * Mg >= (4ll << 20)) ? 1 : 0;
+  // conv2 dgrad (pad 2, 320-row unions) 3.80 -> 3.67 on one box but 3.65 -> 3.68 on another (and 8-wave 64-channel
+  // blocks 3.85), 0.48 -> 0.49 at 8 clients; the padded 5x7x5 convs (384-row unions) 5-25 % slower.  So: unpadded
+  // convs only (the single union buffer's per-triplet reload is not hidden for the 4-wave 64-channel blocks).
+  (void)U;
+  return pad == 0 ? 1 : 0;
 }
 
 int conv3d_fwd_tri_table_size(int B, int D, int H, int W, int pad) {
