@@ -140,6 +140,8 @@ def main():
     per_rank_train = rt.all_gather_cat(torch.tensor([t_train], dtype=torch.float64, device=info.device), info)
     per_rank_train = [round(float(x), 4) for x in per_rank_train.cpu()]
     dt = rt.max_over_ranks(dt, info)
+    # caching-allocator peak of any rank (every engine buffer, incl. one scratch set per distinct (G, B) launch shape)
+    peak_gib = rt.max_over_ranks(torch.cuda.max_memory_allocated(info.device) / 2 ** 30, info)
     ms = dt * 1000.0 / max(1, args.steps)
     value = args.steps / dt
     headline = (args.algorithm == "salientgrads" and args.clients == 64 and args.aggregator == "fedavg"
@@ -177,6 +179,7 @@ def main():
             "rank_train_gpu_s": per_rank_train,
             "rank_imbalance": (round(max(per_rank_train) / (sum(per_rank_train) / len(per_rank_train)), 3)
                                if per_rank_train and sum(per_rank_train) > 0 else None),
+            "peak_hbm_gib": round(peak_gib, 2),
             "last_round_metrics": res,
         }
         if args.phase_timers:

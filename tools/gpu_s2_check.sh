@@ -20,3 +20,5 @@ ms=$(python3 -c "import json; print([json.loads(l) for l in open('gpurun_out/s2/
 python3 tools/prof_summary.py "$db" gpurun_out/s2/round_kernels.txt --window-ms $ms --top 30 > /dev/null || exit 1
 rm -rf /tmp/prof_s2
 head -12 gpurun_out/s2/round_kernels.txt
+timeout -k 10 240 python -u bench.py --steps 3 --warmup 1 --size-skew 1.0 > gpurun_out/s2/bench_skew1.txt 2>&1 || exit 1
+grep '^{' gpurun_out/s2/bench_skew1.txt | cut -c1-200
