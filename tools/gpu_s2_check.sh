@@ -13,6 +13,7 @@ tail -1 gpurun_out/s2/smoke.txt
 timeout -k 10 240 python -u bench.py --steps 5 --warmup 2 > gpurun_out/s2/bench.txt 2>&1 || exit 1
 grep '^{' gpurun_out/s2/bench.txt | cut -c1-300
 for G in 64 8; do timeout -k 10 120 python tools/kbench.py $G 10 > gpurun_out/s2/kbench$G.txt 2>&1 || exit 1; done
+grep -H "conv2_fwd\|full train" gpurun_out/s2/kbench*.txt
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d /tmp/prof_s2 -o run -- python3 bench.py --steps 1 --warmup 1 \
   > gpurun_out/s2/prof_bench.txt 2>&1 || exit 1
 db=$(find /tmp/prof_s2 -name "*.db" | head -1)
