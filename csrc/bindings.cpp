@@ -34,6 +34,7 @@ void conv3d_pos_table(uintptr_t tab, int B, int D, int H, int W, int pad, uintpt
 int conv3d_wgrad_nsplit(int G, int B, int D, int H, int W, int Cin, int Cout, int pad);
 int conv3d_wgrad_tri_table_size(int B, int D, int H, int W, int pad);
 int conv3d_fwd_tri_ok(int B, int D, int H, int W, int Cin, int Cout, int pad);
+int conv3d_union_umax(int B, int D, int H, int W, int pad, int P);
 int conv3d_fwd_tri_pick(int G, int B, int D, int H, int W, int Cin, int Cout, int pad);
 int conv3d_fwd_tri_table_size(int B, int D, int H, int W, int pad);
 void conv3d_fwd_tri_table(uintptr_t tab, int B, int D, int H, int W, int pad, uintptr_t stream);
@@ -157,6 +158,7 @@ PYBIND11_MODULE(_nidt_hip, m) {
   DEF(conv3d_wgrad_nsplit);
   DEF(conv3d_wgrad_tri_table_size);
   DEF(conv3d_fwd_tri_ok);
+  DEF(conv3d_union_umax);
   DEF(conv3d_fwd_tri_pick);
   DEF(conv3d_fwd_tri_table_size);
   DEF(conv3d_fwd_tri_table);

@@ -1525,6 +1525,9 @@ static int union_umax(int B, int D, int H, int W, int pad, int P) {
 
 static int wgrad_tri_umax(int B, int D, int H, int W, int pad) { return union_umax(B, D, H, W, pad, 64); }
 
+// largest union (rows) of a P-position band: exposed for host-side tests of the union rule
+int conv3d_union_umax(int B, int D, int H, int W, int pad, int P) { return union_umax(B, D, H, W, pad, P); }
+
 template <int NCH, int U, bool PADDED>
 __global__ __launch_bounds__(192 * NCH, 2) void k_conv_wgrad_tri(ConvWgTriArgs a) {
   constexpr int NW = 3 * NCH, XG = U * kWdRow, BUFE = XG + NCH * kWdGroup, ST = WtTab<U>::kST;

@@ -1,0 +1,65 @@
+"""Host-side rules of the union-staged conv kernels (``csrc/kernels/conv3d.hip``: ``k_conv_wgrad_tri``,
+``k_conv_fwd_tri``): the union size of a band of output positions (which decides eligibility and the kernel's U) against
+an independent Python model of the padded-input rows the three kw taps read, and the launch-choice rules measured in
+``profiles/r2_ab_wgrad_tri.txt`` / ``profiles/r2_ab_fwd_tri.txt``.  Runs on the CPU (host functions of the built
+extension; skipped when it is not built)."""
+import pytest
+
+
+def _ext():
+    from neuroimagedisttraining_amd import ops
+    try:
+        return ops.ext()
+    except Exception as e:  # noqa: BLE001 - extension not built in this environment
+        pytest.skip("HIP extension not built: %s" % e)
+
+
+def _union_rows(B, D, H, W, pad, P):
+    """Largest number of distinct padded-input rows {b(p) + kw} over the bands of P consecutive output positions."""
+    Dp, Hp, Wp = D + 2 * pad, H + 2 * pad, W + 2 * pad
+    Do, Ho, Wo = Dp - 2, Hp - 2, Wp - 2
+    S, vol = Do * Ho * Wo, Dp * Hp * Wp
+    mg = B * S
+    best = 0
+    for m0 in range(0, mg, P):
+        rows = set()
+        for m in range(m0, min(m0 + P, mg)):
+            n, r = divmod(m, S)
+            od, r = divmod(r, Ho * Wo)
+            oh, ow = divmod(r, Wo)
+            base = n * vol + (od * Hp + oh) * Wp + ow
+            rows.update((base, base + 1, base + 2))
+        best = max(best, len(rows))
+    return best
+
+
+@pytest.mark.parametrize("shape", [(16, 19, 23, 19, 0), (3, 19, 23, 19, 0), (16, 17, 21, 17, 2), (16, 5, 7, 5, 1),
+                                   (2, 5, 7, 5, 2), (1, 9, 6, 11, 1)])
+@pytest.mark.parametrize("P", [64, 256])
+def test_union_size_matches_python_model(shape, P):
+    m = _ext()
+    assert m.conv3d_union_umax(*shape, P) == _union_rows(*shape, P)
+
+
+def test_union_kernel_choices():
+    m = _ext()
+    conv2 = (16, 19, 23, 19, 64, 128, 0)        # AlexNet3D conv2 forward / wgrad geometry (B=16)
+    conv2_dgrad = (16, 17, 21, 17, 128, 64, 2)  # its data gradient: a pad-2 forward
+    conv4 = (16, 5, 7, 5, 192, 192, 1)
+    for G in (64, 8, 1):
+        assert m.conv3d_wgrad_tri_pick(G, *conv2) == 1          # unpadded wgrad: always
+        assert m.conv3d_fwd_tri_ok(*conv2_dgrad) == 1           # supported ...
+        assert m.conv3d_fwd_tri_pick(G, *conv2_dgrad) == 0      # ... but not chosen (no consistent gain)
+    assert m.conv3d_fwd_tri_pick(64, *conv2) == 1
+    assert m.conv3d_wgrad_tri_pick(64, *conv4) == 1             # padded wgrad: only with >= 64 K positions
+    assert m.conv3d_wgrad_tri_pick(8, *conv4) == 0
+    assert m.conv3d_fwd_tri_pick(64, *conv4) == 0               # padded forwards stay on the per-tap kernel
+    # split factors stay within the model's bounds and keep >= 8 steps per block
+    for G in (64, 8, 1):
+        ns = m.conv3d_wgrad_tri_nsplit(G, *conv2)
+        assert 1 <= ns <= 64 and 16 * 17 * 21 * 17 // ns >= 512
+    # table sizes: one entry per band, 2U + P ints with U a multiple of 8 covering the largest union
+    n_bands = -(-16 * 17 * 21 * 17 // 64)
+    per = m.conv3d_wgrad_tri_table_size(16, 19, 23, 19, 0) // n_bands
+    assert per * n_bands == m.conv3d_wgrad_tri_table_size(16, 19, 23, 19, 0)
+    assert (per - 64) % 16 == 0 and (per - 64) // 2 >= m.conv3d_union_umax(16, 19, 23, 19, 0, 64)
