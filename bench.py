@@ -62,9 +62,9 @@ def parse():
     ap.add_argument("--phase-timers", action="store_true", help="synchronised per-phase timers (adds syncs)")
     ap.add_argument("--step-streams", type=int, default=4,
                     help="side streams for the extra (ragged) launches of one lockstep step (1 = serial)")
-    ap.add_argument("--rebalance", type=int, default=-1,
-                    help="1: replicate the cohort on every rank and move sampled clients to even the per-round load "
-                         "(default: on when frac < 1 on several ranks)")
+    ap.add_argument("--rebalance", type=int, default=0,
+                    help="1: move sampled clients (state and samples) between ranks to even the per-round load "
+                         "(off by default: no measurement has shown a net gain, profiles/r2_s2_rehearse_2ranks.txt)")
     return ap.parse_args()
 
 
@@ -85,13 +85,13 @@ def main():
     n_test = [max(1, int(round(t * args.test_per_client / per))) for t in tot]
     n_train = [t - e for t, e in zip(tot, n_test)]
     shards = rt.shard_clients(n_train, info.world)
-    rebalance = (args.frac < 1.0 and info.world > 1) if args.rebalance < 0 else bool(args.rebalance)
-    # rebalancing lets any rank train any client: every rank holds the whole (synthetic) cohort (~24 GB of HBM)
-    local = list(range(args.clients)) if rebalance else shards[info.rank]
+    rebalance = bool(args.rebalance)
+    local = shards[info.rank]  # data is sharded like the clients (rebalancing moves a client's samples with it)
     t0 = time.perf_counter()
     vol, labels, splits_local = build_fl_volumes(local, args.clients, n_train, n_test, info.device, seed=args.seed)
     x8, mom = to_hip_store(vol)
     del vol
+    nval = None
     if args.algorithm == "fedfomo":  # validation split: 10 % of client 0's train size (data_val_loader.py:275)
         nval = int(0.1 * n_train[0])
         splits_local = {c: ClientSplit(s.train[nval:], s.test, s.train[:nval]) for c, s in splits_local.items()}
@@ -101,7 +101,8 @@ def main():
 
     # splits indexed by global client id; non-local clients only need their sizes (sampling weights)
     splits = [splits_local[c] if c in splits_local else
-              ClientSplit(train=np.zeros(n_train[c], dtype=np.int64), test=np.zeros(n_test[c], dtype=np.int64))
+              ClientSplit(train=np.zeros(n_train[c], dtype=np.int64), test=np.zeros(n_test[c], dtype=np.int64),
+                          val=None if nval is None else np.zeros(nval, dtype=np.int64))
               for c in range(args.clients)]
     model = AlexNet3D_Dropout(num_classes=1)
     engine = HipEngine(model, x8, mom, labels, info.device)

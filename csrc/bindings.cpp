@@ -2,7 +2,9 @@
 // Every function takes raw device pointers (uintptr_t), sizes and a hipStream_t (as uintptr_t); shape and dtype
 // validation happens in the Python wrappers (neuroimagedisttraining_amd/ops) before any launch.
 #include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
 #include <cstdint>
+#include <vector>
 
 namespace nidt {
 // optim.hip
@@ -70,6 +72,19 @@ void gn_bwd(uintptr_t dy, int dy_bf16, uintptr_t mask, uintptr_t t, uintptr_t st
 void gn_param_grads(uintptr_t part, int G, int B, int C, uintptr_t grads, int64_t ldg, int64_t off_w, int64_t off_b,
                     uintptr_t stream);
 void res_grad(uintptr_t out, uintptr_t dx1, uintptr_t dx2, uintptr_t da, uintptr_t mask, int64_t n, uintptr_t stream);
+void res_grad_s2(uintptr_t out, uintptr_t dx1, uintptr_t dx2s, int N, int H, int W, int C, uintptr_t stream);
+// img.hip
+void img_input(uintptr_t src, uintptr_t idx, uintptr_t out, int N, int H, int W, int CP, float m0, float m1, float m2,
+               float s0, float s1, float s2, int aug, int pad, uintptr_t seed_dev, int64_t seed_base, uintptr_t cids,
+               int B, uintptr_t stream);
+// pack.hip
+void pack_convs(uintptr_t desc, int nd, int nplain, int ntrans, int lds, uintptr_t theta, int64_t ldt, int G,
+                uintptr_t out, uintptr_t stream);
+int pack_desc_bytes();
+// conv3d.hip (sub-pixel stride-2 data gradient)
+void conv_dgrad_s2_g(uintptr_t dy, uintptr_t w, uintptr_t dx, int G, int B, int D, int H, int W, int Cin, int Cout,
+                     int kt, int Dx, int Hx, int Wx, uintptr_t stream);
+std::vector<int> conv_tap_slots(int kt, int stride);
 // mpc.hip
 void modp_matmul(uintptr_t A, uintptr_t B, uintptr_t C, int M, int K, int64_t N, int64_t p, uintptr_t stream);
 // bnr.hip
@@ -182,6 +197,12 @@ PYBIND11_MODULE(_nidt_hip, m) {
   DEF(gn_bwd);
   DEF(gn_param_grads);
   DEF(res_grad);
+  DEF(res_grad_s2);
+  DEF(img_input);
+  DEF(pack_convs);
+  DEF(pack_desc_bytes);
+  DEF(conv_dgrad_s2_g);
+  DEF(conv_tap_slots);
   DEF(modp_matmul);
   DEF(bnr_workspace);
   DEF(bnr_stats);

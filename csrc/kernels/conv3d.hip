@@ -24,6 +24,8 @@
 #include <cstdlib>
 #include <map>
 
+#include <vector>
+
 #include "common.h"
 
 namespace nidt {
@@ -47,6 +49,12 @@ struct ConvFwdArgs {
   // geometry (LDS-DMA path): kt taps per output (27 = 3x3x3, 9 = 1x3x3 (2-D convs as D = 1 volumes), 1 = 1x1x1),
   // stride st in every dimension, depth padding padd (the h/w padding is pad)
   int kt = 27, st = 1, padd = 0;
+  // sub-pixel (phase) data gradient of a stride-2 conv (LDS-DMA path, conv_dgrad_s2_g): nph > 0 phases, each a
+  // stride-1 conv over the dy grid with pnt[ph] taps — window taps ptap[pt0[ph] + j] (geometry and padding mask),
+  // weights at tap slots pt0[ph] + j of w [Cout][kt][Cin] — whose output (od, oh, ow) lands at (2od + bit2(poff),
+  // 2oh + bit1(poff), 2ow + bit0(poff)) of the [Dx][Hx][Wx] output (positions outside are skipped)
+  int nph = 0, Dx = 0, Hx = 0, Wx = 0;
+  unsigned char pnt[8] = {0}, pt0[8] = {0}, poff[8] = {0}, ptap[28] = {0};
 };
 
 constexpr int kFwdBP = 128;  // positions per block
@@ -72,7 +80,8 @@ __device__ __forceinline__ uint4 xform8(uint4 v, const float* s, const float* t,
 // channel).  C layout (16x16x32): C[row = 4*fq + r][col = fr]; rows = co, cols = positions.
 template <int BCO, int BP, int WM, int WN, bool BIAS, bool STATS, int TCO, int TP>
 __device__ __forceinline__ void conv_fwd_epilogue(const ConvFwdArgs& a, f32x4 (&acc)[TCO][TP], float* red, int g,
-                                                  int pb, int co0, int wco, int wp, int fr, int fq, int tid) {
+                                                  int pb, int co0, int wco, int wp, int fr, int fq, int tid,
+                                                  int ph = 0) {
   constexpr int WCO = BCO / WM, WP = BP / WN;
   float bias_r[TCO][4];
 #pragma unroll
@@ -86,7 +95,16 @@ __device__ __forceinline__ void conv_fwd_epilogue(const ConvFwdArgs& a, f32x4 (&
   for (int j = 0; j < TP; ++j) {
     const int m = posw + j * 16;
     if (m < a.Mg) {
-      uint16_t* yp = a.y + ((int64_t)g * a.Mg + m) * a.Cout + co0 + wco * WCO + 4 * fq;
+      int64_t yo = (int64_t)g * a.Mg + m;
+      if (a.nph) {  // phase output: scatter to the strided positions of the full-resolution gradient
+        const int S = a.Do * a.Ho * a.Wo, nl = m / S, sr = m - nl * S;
+        const int od = sr / (a.Ho * a.Wo), r2 = sr - od * a.Ho * a.Wo, oh = r2 / a.Wo, ow = r2 - oh * a.Wo;
+        const int po = a.poff[ph];
+        const int zd = a.Dx > 1 ? 2 * od + ((po >> 2) & 1) : od, zh = 2 * oh + ((po >> 1) & 1), zw = 2 * ow + (po & 1);
+        if (zd >= a.Dx || zh >= a.Hx || zw >= a.Wx) continue;
+        yo = (((int64_t)g * a.B + nl) * a.Dx + zd) * a.Hx * a.Wx + (int64_t)zh * a.Wx + zw;
+      }
+      uint16_t* yp = a.y + yo * a.Cout + co0 + wco * WCO + 4 * fq;
 #pragma unroll
       for (int i = 0; i < TCO; ++i) {
         float v0 = acc[i][j][0] + bias_r[i][0], v1 = acc[i][j][1] + bias_r[i][1];
@@ -346,12 +364,15 @@ __global__ __launch_bounds__(64 * WM * WN, ((NST == 2 ? 8 : 4) / (WM * WN)) > 0 
   const int id = xcd_remap(blockIdx.x, nwg);
   const int cot = id % nCO, rest = id / nCO;
   const int pb = rest % a.nPB, rest2 = rest / a.nPB;
-  const int sp = rest2 % a.ksplit, g = rest2 / a.ksplit;
+  const int nph = a.nph > 0 ? a.nph : 1;
+  const int sp = rest2 % a.ksplit, gp = rest2 / a.ksplit;
+  const int ph = gp % nph, g = gp / nph;
+  const int ntap = a.nph ? (int)a.pnt[ph] : a.kt, tbase = a.nph ? (int)a.pt0[ph] : 0;
   const int co0 = cot * BCO;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // uniform: LDS destinations stay in SGPRs
   const int wco = wid / WN, wp = wid % WN;
-  const int Cin = a.Cin, nck = Cin / BK, nks = a.kt * nck;
+  const int Cin = a.Cin, nck = Cin / BK, nks = ntap * nck;
   const int ks0 = nks * sp / a.ksplit, ks1 = nks * (sp + 1) / a.ksplit;  // this split's k-steps
   const int lrow = lane >> 3, slot = lane & 7;
 
@@ -388,9 +409,10 @@ __global__ __launch_bounds__(64 * WM * WN, ((NST == 2 ? 8 : 4) / (WM * WN)) > 0 
 
 #define DMA_ISSUE(KS, BUFI)                                                                                   \
   {                                                                                                           \
-    const int t_ = (KS) / nck, cc_ = (KS) - t_ * nck;                                                         \
+    const int l_ = (KS) / nck, cc_ = (KS) - l_ * nck;                                                         \
+    const int t_ = a.nph ? (int)a.ptap[tbase + l_] : l_;  /* window tap: geometry + padding mask */           \
     const int toff_ = (((((t_ / 9)) * a.H + (t_ / 3) % 3) * a.W + t_ % 3) * Cin + cc_ * BK) * 2;              \
-    const int woff_ = (t_ * Cin + cc_ * BK) * 2;                                                              \
+    const int woff_ = ((tbase + l_) * Cin + cc_ * BK) * 2;  /* weight tap slot */                             \
     uint16_t* sA_ = smem + (BUFI) * BUF;                                                                      \
     uint16_t* sB_ = sA_ + A_ELEMS;                                                                            \
     _Pragma("unroll") for (int i_ = 0; i_ < A_INSTR; ++i_)                                                    \
@@ -474,7 +496,7 @@ __global__ __launch_bounds__(64 * WM * WN, ((NST == 2 ? 8 : 4) / (WM * WN)) > 0 
   }
   __syncthreads();
   float* red = reinterpret_cast<float*>(smem);
-  conv_fwd_epilogue<BCO, BP, WM, WN, BIAS, STATS, TCO, TP>(a, acc, red, g, pb, co0, wco, wp, fr, fq, tid);
+  conv_fwd_epilogue<BCO, BP, WM, WN, BIAS, STATS, TCO, TP>(a, acc, red, g, pb, co0, wco, wp, fr, fq, tid, ph);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -734,10 +756,55 @@ static int fwd_bco(int Cout) {
 // output extent of one dimension: taps k (3 or 1), stride st, padding p
 static inline int conv_out_dim(int n, int k, int st, int p) { return (n + 2 * p - k) / st + 1; }
 
+struct PhasePlan;
 static void conv3d_fwd_impl(uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t xs, uintptr_t xt, uintptr_t y,
                             uintptr_t stats, int G, int B, int D, int H, int W, int Cin, int Cout, int pad,
                             uintptr_t stream, int ksplit, uintptr_t part, int64_t bias_ld = 0, int kt = 27,
-                            int stride = 1, int padd = -1) {
+                            int stride = 1, int padd = -1, const PhasePlan* pp = nullptr, int Dx = 0, int Hx = 0,
+                            int Wx = 0);
+
+// Sub-pixel decomposition of the data gradient of a k=3, pad=1, stride-2 conv: per dimension, output phase 0 (even
+// positions 2i) takes kernel tap k=1 from dy row i (window index 1 of a pad-1 3-window), phase 1 (2i+1) takes k=0
+// from dy row i+1 (window 2) and k=2 from row i (window 1).  A 3x3(x3) conv therefore splits into 4 (8) stride-1
+// convs over the dy grid with 1,2,2,4 (,2,4,4,8) taps — 9 (27) taps in all instead of 9 (27) taps on a 4x (8x)
+// larger zero-upsampled grid.  Slots number the taps phase-major (phase = d,h,w bits), window order inside.
+struct PhasePlan {
+  int nph = 0;
+  int pnt[8] = {0}, pt0[8] = {0}, poff[8] = {0}, ptap[27] = {0};
+  int slot_of_tap[27] = {0};  // fwd kernel tap (kd*9 + kh*3 + kw) -> slot
+};
+
+static PhasePlan conv_s2_phase_plan(int kt) {
+  PhasePlan pl;
+  const int nd = kt == 27 ? 2 : 1;  // depth phases (2-D convs run as D = 1 volumes: one depth tap, window 0)
+  static const int nk[2] = {1, 2}, kk[2][2] = {{1, -1}, {0, 2}}, ww[2][2] = {{1, -1}, {2, 1}};
+  int slot = 0;
+  for (int ad = 0; ad < nd; ++ad)
+    for (int ah = 0; ah < 2; ++ah)
+      for (int aw = 0; aw < 2; ++aw) {
+        const int p = pl.nph++;
+        pl.pt0[p] = slot;
+        pl.poff[p] = (ad << 2) | (ah << 1) | aw;
+        const int ndt = kt == 27 ? nk[ad] : 1;
+        for (int i = 0; i < ndt; ++i)
+          for (int j = 0; j < nk[ah]; ++j)
+            for (int l = 0; l < nk[aw]; ++l) {
+              const int kd = kt == 27 ? kk[ad][i] : 0, wd = kt == 27 ? ww[ad][i] : 0;
+              const int t_fwd = kd * 9 + kk[ah][j] * 3 + kk[aw][l];
+              const int t_win = wd * 9 + ww[ah][j] * 3 + ww[aw][l];
+              pl.ptap[slot] = t_win;
+              pl.slot_of_tap[t_fwd] = slot;
+              ++slot;
+            }
+        pl.pnt[p] = slot - pl.pt0[p];
+      }
+  return pl;
+}
+
+static void conv3d_fwd_impl(uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t xs, uintptr_t xt, uintptr_t y,
+                            uintptr_t stats, int G, int B, int D, int H, int W, int Cin, int Cout, int pad,
+                            uintptr_t stream, int ksplit, uintptr_t part, int64_t bias_ld, int kt,
+                            int stride, int padd, const PhasePlan* pp, int Dx, int Hx, int Wx) {
   NIDT_REQUIRE(Cin % 32 == 0, "conv3d_fwd: Cin must be a multiple of 32");
   NIDT_REQUIRE((xs == 0 && Cin % 64 == 0) ? (int64_t)Cin * kt <= 27 * kMaxCin : Cin <= 192,
                "conv3d_fwd: taps x Cin <= 27 x 512 (LDS-DMA path: Cin % 64 == 0, no input transform), else Cin <= 192");
@@ -764,6 +831,15 @@ static void conv3d_fwd_impl(uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t 
   a.nPB = ceil_div(a.Mg, kFwdBP);
   a.G = G;
   a.bias_ld = bias_ld;
+  if (pp) {
+    NIDT_REQUIRE(stride == 1 && bias == 0 && stats == 0 && xs == 0 && ksplit <= 1 && Cin % 64 == 0,
+                 "conv_dgrad_s2: phase convs are plain stride-1 LDS-DMA convs without split-K");
+    a.nph = pp->nph; a.Dx = Dx; a.Hx = Hx; a.Wx = Wx;
+    for (int p = 0; p < pp->nph; ++p) {
+      a.pnt[p] = (unsigned char)pp->pnt[p]; a.pt0[p] = (unsigned char)pp->pt0[p]; a.poff[p] = (unsigned char)pp->poff[p];
+    }
+    for (int t = 0; t < kt; ++t) a.ptap[t] = (unsigned char)pp->ptap[t];
+  }
   const bool xf = xs != 0, hb = bias != 0, st = stats != 0;
   NIDT_REQUIRE(!st || hb, "conv3d_fwd: statistics require a bias");
   const int bco = fwd_bco(Cout);
@@ -773,7 +849,7 @@ static void conv3d_fwd_impl(uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t 
     // every wave owns a 64x64 output tile (the A tile is re-read from L2 once per 256 positions).  When that
     // grid would not fill the chip (few clients per GPU, e.g. 8 clients x the 5x7x5 conv3-5 layers at 8 GPUs)
     // the block shrinks to one 64-position column of waves (4x the blocks).
-    const int bp = conv3d_fwd_bp(Cin, Cout, 0, G, a.Mg);
+    const int bp = conv3d_fwd_bp(Cin, Cout, 0, G * (a.nph > 0 ? a.nph : 1), a.Mg);
     a.nPB = ceil_div(a.Mg, bp);
     const int nCO = Cout / bco;
     if (ksplit > 1) {
@@ -782,7 +858,7 @@ static void conv3d_fwd_impl(uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t 
       a.ksplit = ksplit;
       a.part = ptr<float>(part);
     }
-    const int64_t nwg = (int64_t)a.nPB * nCO * G * a.ksplit;
+    const int64_t nwg = (int64_t)a.nPB * nCO * G * a.ksplit * (a.nph > 0 ? a.nph : 1);
     NIDT_REQUIRE(nwg < (1ll << 31), "conv3d_fwd: grid too large");
     dim3 g1((unsigned)nwg);
     // small grids (64-position blocks: conv3-5 at 8 clients per GPU) run at ~1 wave per SIMD: a third LDS stage
@@ -831,6 +907,35 @@ static void conv3d_fwd_impl(uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t 
   }
 #undef NIDT_FWD
   NIDT_CHECK(hipGetLastError());
+}
+
+// Data gradient of a k=3, pad=1, stride-2 client-grouped conv by sub-pixel phases (conv_s2_phase_plan): dy
+// [G*B][D][H][W][Cin] (the forward's output grid and channels), w [G][Cout][kt][Cin] with the taps in slot order
+// (pack_convs), dx [G*B][Dx][Hx][Wx][Cout] written completely (every position belongs to exactly one phase) — no
+// zero-upsampled copy of dy and no memset.  kt = 9 (2-D, D = 1) or 27.
+void conv_dgrad_s2_g(uintptr_t dy, uintptr_t w, uintptr_t dx, int G, int B, int D, int H, int W, int Cin, int Cout,
+                     int kt, int Dx, int Hx, int Wx, uintptr_t stream) {
+  NIDT_REQUIRE(kt == 9 || kt == 27, "conv_dgrad_s2_g: 3x3 (kt 9) or 3x3x3 (kt 27) kernels");
+  NIDT_REQUIRE(Hx <= 2 * H && Hx >= 2 * H - 1 && Wx <= 2 * W && Wx >= 2 * W - 1 &&
+               (kt == 9 ? (D == 1 && Dx == 1) : (Dx <= 2 * D && Dx >= 2 * D - 1)),
+               "conv_dgrad_s2_g: dx extent must be the stride-2 input of the dy grid");
+  static const PhasePlan pl9 = conv_s2_phase_plan(9), pl27 = conv_s2_phase_plan(27);
+  conv3d_fwd_impl(dy, w, 0, 0, 0, dx, 0, G, B, D, H, W, Cin, Cout, 1, stream, 1, 0, 0, kt, 1, kt == 27 ? 1 : 0,
+                  kt == 27 ? &pl27 : &pl9, Dx, Hx, Wx);
+}
+
+// tap slot permutation of the dgrad weight image (pack_convs): stride 1 -> flipped taps, stride 2 (k = 3) -> the
+// sub-pixel phase order, 1x1 -> identity
+std::vector<int> conv_tap_slots(int kt, int stride) {
+  std::vector<int> out(kt);
+  if (kt == 1) { out[0] = 0; return out; }
+  if (stride == 1) {
+    for (int t = 0; t < kt; ++t) out[t] = kt - 1 - t;
+    return out;
+  }
+  const PhasePlan pl = conv_s2_phase_plan(kt);
+  for (int t = 0; t < kt; ++t) out[t] = pl.slot_of_tap[t];
+  return out;
 }
 
 void conv3d_fwd(uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t xs, uintptr_t xt, uintptr_t y, uintptr_t stats,

@@ -254,6 +254,184 @@ __global__ __launch_bounds__(kGnThreads) void k_gn_bwd(const void* __restrict__ 
   }
 }
 
+// Streaming variants for samples larger than the register-resident limit (S*C > 65536, e.g. the 64x64x64 maps of
+// the Tiny-ImageNet ResNet-18): the same arithmetic and reduction order per element, with the sample re-read from
+// memory in each pass (mean, squared deviations, apply) instead of held in registers.
+template <bool RES, bool RELU>
+__global__ __launch_bounds__(kGnThreads) void k_gn_fwd_stream(const uint16_t* __restrict__ t,
+                                                              const uint16_t* __restrict__ res,
+                                                              const float* __restrict__ theta, int64_t ldt,
+                                                              int64_t off_w, int64_t off_b, uint16_t* __restrict__ y,
+                                                              float* __restrict__ stats, int B, int S, int C) {
+  __shared__ float sm[kGnThreads * 9];
+  __shared__ float chs[512];
+  __shared__ float grp[kGnGroups], gmean[kGnGroups], grstd[kGnGroups];
+  const int n = blockIdx.x, g = n / B, tid = threadIdx.x;
+  const int nch = C >> 3, nchunk = S * nch;
+  const int64_t base = (int64_t)n * S * C;
+  const int j = tid % nch;
+  const int cg = C / kGnGroups;
+  float part[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) part[e] = 0.f;
+  for (int q = tid; q < nchunk; q += kGnThreads) {
+    float f[8];
+    unpack8(*reinterpret_cast<const uint4*>(t + base + (int64_t)q * 8), f);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) part[e] += f[e];
+  }
+  gn_reduce_groups(part, sm, chs, grp, C, nch);
+  if (tid < kGnGroups) gmean[tid] = grp[tid] / (float)(S * cg);
+  __syncthreads();
+  float mu[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    mu[e] = gmean[(8 * j + e) / cg];
+    part[e] = 0.f;
+  }
+  for (int q = tid; q < nchunk; q += kGnThreads) {
+    float f[8];
+    unpack8(*reinterpret_cast<const uint4*>(t + base + (int64_t)q * 8), f);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float d = f[e] - mu[e];
+      part[e] = fmaf(d, d, part[e]);
+    }
+  }
+  gn_reduce_groups(part, sm, chs, grp, C, nch);
+  if (tid < kGnGroups) {
+    const float rs = rsqrtf(grp[tid] / (float)(S * cg) + kGnEps);
+    grstd[tid] = rs;
+    stats[((int64_t)n * kGnGroups + tid) * 2] = gmean[tid];
+    stats[((int64_t)n * kGnGroups + tid) * 2 + 1] = rs;
+  }
+  __syncthreads();
+  float sc[8], sh[8];
+  const float* gw = theta + (int64_t)g * ldt + off_w;
+  const float* gb = theta + (int64_t)g * ldt + off_b;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const int c = 8 * j + e;
+    sc[e] = gw[c] * grstd[c / cg];
+    sh[e] = gb[c] - mu[e] * sc[e];
+  }
+  for (int q = tid; q < nchunk; q += kGnThreads) {
+    float f[8], r[8];
+    unpack8(*reinterpret_cast<const uint4*>(t + base + (int64_t)q * 8), f);
+    if (RES) unpack8(*reinterpret_cast<const uint4*>(res + base + (int64_t)q * 8), r);
+    uint32_t o[4];
+#pragma unroll
+    for (int e = 0; e < 8; e += 2) {
+      float a0 = fmaf(f[e], sc[e], sh[e]), a1 = fmaf(f[e + 1], sc[e + 1], sh[e + 1]);
+      if (RES) {
+        a0 += r[e];
+        a1 += r[e + 1];
+      }
+      if (RELU) {
+        a0 = fmaxf(a0, 0.f);
+        a1 = fmaxf(a1, 0.f);
+      }
+      o[e >> 1] = pack_bf16x2(a0, a1);
+    }
+    *reinterpret_cast<uint4*>(y + base + (int64_t)q * 8) = make_uint4(o[0], o[1], o[2], o[3]);
+  }
+}
+
+template <bool DYB, bool MASK>
+__global__ __launch_bounds__(kGnThreads) void k_gn_bwd_stream(const void* __restrict__ dyv,
+                                                              const uint16_t* __restrict__ mask,
+                                                              const uint16_t* __restrict__ t,
+                                                              const float* __restrict__ stats,
+                                                              const float* __restrict__ theta, int64_t ldt,
+                                                              int64_t off_w, uint16_t* __restrict__ dt,
+                                                              float* __restrict__ part_out, int B, int S, int C) {
+  __shared__ float sm[kGnThreads * 9];
+  __shared__ float chs[512];
+  __shared__ float grp[kGnGroups], gm1[kGnGroups], gm2[kGnGroups];
+  __shared__ float chA[512];
+  const int n = blockIdx.x, g = n / B, tid = threadIdx.x;
+  const int nch = C >> 3, nchunk = S * nch;
+  const int64_t base = (int64_t)n * S * C;
+  const int j = tid % nch;
+  const int cg = C / kGnGroups;
+  float mu[8], rs[8], gw[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const int c = 8 * j + e;
+    mu[e] = stats[((int64_t)n * kGnGroups + c / cg) * 2];
+    rs[e] = stats[((int64_t)n * kGnGroups + c / cg) * 2 + 1];
+    gw[e] = theta[(int64_t)g * ldt + off_w + c];
+  }
+  auto load_dy = [&](int q, float* d) {
+    if (DYB) {
+      unpack8(*reinterpret_cast<const uint4*>(reinterpret_cast<const uint16_t*>(dyv) + base + (int64_t)q * 8), d);
+    } else {
+      const float4* p = reinterpret_cast<const float4*>(reinterpret_cast<const float*>(dyv) + base + (int64_t)q * 8);
+      const float4 a = p[0], b = p[1];
+      d[0] = a.x; d[1] = a.y; d[2] = a.z; d[3] = a.w; d[4] = b.x; d[5] = b.y; d[6] = b.z; d[7] = b.w;
+    }
+    if (MASK) {
+      float m[8];
+      unpack8(*reinterpret_cast<const uint4*>(mask + base + (int64_t)q * 8), m);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) d[e] = m[e] > 0.f ? d[e] : 0.f;
+    }
+  };
+  float pa[8], pb[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) pa[e] = pb[e] = 0.f;
+  for (int q = tid; q < nchunk; q += kGnThreads) {
+    float f[8], d[8];
+    unpack8(*reinterpret_cast<const uint4*>(t + base + (int64_t)q * 8), f);
+    load_dy(q, d);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      pa[e] += d[e];
+      pb[e] = fmaf(d[e], (f[e] - mu[e]) * rs[e], pb[e]);
+    }
+  }
+  gn_reduce_groups(pa, sm, chs, grp, C, nch);
+  for (int c = tid; c < C; c += kGnThreads) chA[c] = chs[c];
+  __syncthreads();
+  gn_reduce_groups(pb, sm, chs, grp, C, nch);
+  for (int c = tid; c < C; c += kGnThreads) {
+    part_out[((int64_t)n * C + c) * 2] = chA[c];
+    part_out[((int64_t)n * C + c) * 2 + 1] = chs[c];
+  }
+  if (tid < kGnGroups) {
+    float s1 = 0.f, s2 = 0.f;
+    const float* gwr = theta + (int64_t)g * ldt + off_w;
+    for (int i = 0; i < cg; ++i) {
+      const int c = tid * cg + i;
+      s1 = fmaf(gwr[c], chA[c], s1);
+      s2 = fmaf(gwr[c], chs[c], s2);
+    }
+    gm1[tid] = s1 / (float)(S * cg);
+    gm2[tid] = s2 / (float)(S * cg);
+  }
+  __syncthreads();
+  float m1[8], m2[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    m1[e] = gm1[(8 * j + e) / cg];
+    m2[e] = gm2[(8 * j + e) / cg];
+  }
+  for (int q = tid; q < nchunk; q += kGnThreads) {
+    float f[8], d[8];
+    unpack8(*reinterpret_cast<const uint4*>(t + base + (int64_t)q * 8), f);
+    load_dy(q, d);
+    uint32_t o[4];
+#pragma unroll
+    for (int e = 0; e < 8; e += 2) {
+      const float x0 = (f[e] - mu[e]) * rs[e], x1 = (f[e + 1] - mu[e + 1]) * rs[e + 1];
+      const float r0 = rs[e] * (d[e] * gw[e] - m1[e] - x0 * m2[e]);
+      const float r1 = rs[e + 1] * (d[e + 1] * gw[e + 1] - m1[e + 1] - x1 * m2[e + 1]);
+      o[e >> 1] = pack_bf16x2(r0, r1);
+    }
+    *reinterpret_cast<uint4*>(dt + base + (int64_t)q * 8) = make_uint4(o[0], o[1], o[2], o[3]);
+  }
+}
+
 // grads[g][off_w + c] = sum_b part[g*B + b][c][1] (dgamma), grads[g][off_b + c] = sum_b part[..][c][0] (dbeta)
 __global__ void k_gn_param_grads(const float* __restrict__ part, int B, int C, float* __restrict__ grads, int64_t ldg,
                                  int64_t off_w, int64_t off_b) {
@@ -303,6 +481,42 @@ void res_grad(uintptr_t out, uintptr_t dx1, uintptr_t dx2, uintptr_t da, uintptr
   NIDT_CHECK(hipGetLastError());
 }
 
+// Residual-stream gradient of a downsampling block: out = dx1 + (dx2 at the even pixels), with the 1x1 stride-2
+// shortcut's data gradient given at half resolution (dx2s [N][Ho][Wo][C], Ho = ceil(H/2)): the shortcut conv read
+// only the even pixels, so no full-size zero-filled scatter of its gradient is needed.
+__global__ void k_res_grad_s2(float* __restrict__ out, const uint16_t* __restrict__ dx1,
+                              const uint16_t* __restrict__ dx2s, int64_t n8, int H, int W, int C) {
+  const int C8 = C / 8, Ho = (H + 1) / 2, Wo = (W + 1) / 2;
+  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n8; q += (int64_t)gridDim.x * blockDim.x) {
+    const int c8 = (int)(q % C8);
+    const int64_t pix = q / C8;
+    const int x = (int)(pix % W);
+    const int64_t r = pix / W;
+    const int y = (int)(r % H);
+    const int64_t n = r / H;
+    float a[8], b[8];
+    unpack8(*reinterpret_cast<const uint4*>(dx1 + q * 8), a);
+    if (((x | y) & 1) == 0) {
+      unpack8(*reinterpret_cast<const uint4*>(dx2s + (((n * Ho + (y >> 1)) * Wo + (x >> 1)) * C8 + c8) * 8), b);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) b[e] = 0.f;
+    }
+    float4* o = reinterpret_cast<float4*>(out + q * 8);
+    o[0] = make_float4(a[0] + b[0], a[1] + b[1], a[2] + b[2], a[3] + b[3]);
+    o[1] = make_float4(a[4] + b[4], a[5] + b[5], a[6] + b[6], a[7] + b[7]);
+  }
+}
+
+void res_grad_s2(uintptr_t out, uintptr_t dx1, uintptr_t dx2s, int N, int H, int W, int C, uintptr_t stream) {
+  NIDT_REQUIRE(C % 8 == 0, "res_grad_s2: C % 8 == 0");
+  const int64_t n8 = (int64_t)N * H * W * C / 8;
+  hipLaunchKernelGGL(k_res_grad_s2, dim3((unsigned)std::min<int64_t>(8192, (n8 + 255) / 256)), dim3(256), 0,
+                     as_stream(stream), ptr<float>(out), ptr<const uint16_t>(dx1), ptr<const uint16_t>(dx2s), n8, H,
+                     W, C);
+  NIDT_CHECK(hipGetLastError());
+}
+
 static int gn_nv(int S, int C) {
   const int chunks = S * C / 8;
   const int nv = ceil_div(chunks, kGnThreads);
@@ -313,13 +527,25 @@ static void gn_check(int N, int B, int S, int C, const char* who) {
   NIDT_REQUIRE(N > 0 && B > 0 && N % B == 0, std::string(who) + ": N % B");
   NIDT_REQUIRE(C % kGnGroups == 0 && C % 64 == 0 && C <= 512 && (kGnThreads % (C / 8)) == 0,
                std::string(who) + ": C must be a multiple of 64, <= 512");
-  NIDT_REQUIRE((int64_t)S * C <= 16 * 8 * kGnThreads, std::string(who) + ": S*C <= 65536 (one sample per block)");
 }
+
+static bool gn_streaming(int S, int C) { return (int64_t)S * C > 16 * 8 * kGnThreads; }
 
 void gn_fwd(uintptr_t t, uintptr_t res, uintptr_t theta, int64_t ldt, int64_t off_w, int64_t off_b, uintptr_t y,
             uintptr_t stats, int N, int B, int S, int C, int relu, uintptr_t stream) {
   gn_check(N, B, S, C, "gn_fwd");
   hipStream_t s = as_stream(stream);
+  if (gn_streaming(S, C)) {
+#define GNFS(R, L)                                                                                             \
+  hipLaunchKernelGGL((k_gn_fwd_stream<R, L>), dim3(N), dim3(kGnThreads), 0, s, ptr<const uint16_t>(t),          \
+                     ptr<const uint16_t>(res), ptr<const float>(theta), ldt, off_w, off_b, ptr<uint16_t>(y),     \
+                     ptr<float>(stats), B, S, C)
+    if (res) { if (relu) GNFS(true, true); else GNFS(true, false); }
+    else { if (relu) GNFS(false, true); else GNFS(false, false); }
+#undef GNFS
+    NIDT_CHECK(hipGetLastError());
+    return;
+  }
   const int nv = gn_nv(S, C);
 #define GNF(NVV, R, L)                                                                                         \
   hipLaunchKernelGGL((k_gn_fwd<NVV, R, L>), dim3(N), dim3(kGnThreads), 0, s, ptr<const uint16_t>(t),            \
@@ -344,6 +570,17 @@ void gn_bwd(uintptr_t dy, int dy_bf16, uintptr_t mask, uintptr_t t, uintptr_t st
             int64_t off_w, uintptr_t dt, uintptr_t part, int N, int B, int S, int C, uintptr_t stream) {
   gn_check(N, B, S, C, "gn_bwd");
   hipStream_t s = as_stream(stream);
+  if (gn_streaming(S, C)) {
+#define GNBS(DB, M)                                                                                            \
+  hipLaunchKernelGGL((k_gn_bwd_stream<DB, M>), dim3(N), dim3(kGnThreads), 0, s, ptr<const void>(dy),            \
+                     ptr<const uint16_t>(mask), ptr<const uint16_t>(t), ptr<const float>(stats),               \
+                     ptr<const float>(theta), ldt, off_w, ptr<uint16_t>(dt), ptr<float>(part), B, S, C)
+    if (dy_bf16) { if (mask) GNBS(true, true); else GNBS(true, false); }
+    else { if (mask) GNBS(false, true); else GNBS(false, false); }
+#undef GNBS
+    NIDT_CHECK(hipGetLastError());
+    return;
+  }
   const int nv = gn_nv(S, C);
 #define GNB(NVV, DB, M)                                                                                        \
   hipLaunchKernelGGL((k_gn_bwd<NVV, DB, M>), dim3(N), dim3(kGnThreads), 0, s, ptr<const void>(dy),              \

@@ -1,0 +1,99 @@
+// Batched per-step weight packing of a client-grouped network: every conv layer of G clients' fp32 parameter rows
+// (PyTorch layout [Cout][cin][taps]) becomes the bf16 MFMA A-operand images of the conv kernels in TWO launches per
+// step (all layers at once), instead of two launches per layer:
+//   plain  wp[g][Cout][kt][Cin_p]   (forward; input channels cin..Cin_p-1 zero),
+//   dgrad  wt[g][Cin_p][kt][Cout]   with the taps in slot order: slot_of_tap = kt-1-t for a stride-1 conv (the
+//          flipped kernel), the sub-pixel phase order of conv_s2_phase_plan (conv3d.hip) for a stride-2 3x3(x3)
+//          conv, identity for 1x1.
+// The layer of a block comes from a small descriptor table (prefix block counts), so one grid covers layers of
+// different shapes; the transposes go through a padded 64x64 LDS tile (coalesced reads and writes).
+#include "common.h"
+
+namespace nidt {
+
+struct PackDesc {
+  int64_t src_off;   // element offset of the layer in a theta row
+  int64_t wp_off;    // element offset of wp (all G clients) in the packed buffer
+  int64_t wt_off;    // ... of wt, or -1 (no dgrad image)
+  int cout, cin_p, cin_src, kt;
+  int blk_plain;     // first block of this layer in the plain grid (Cout blocks per layer)
+  int blk_t;         // first block in the transpose grid (ceil(Cin_p/64) * ceil(Cout/64) * kt blocks per layer)
+  int slot[27];
+};
+static_assert(sizeof(PackDesc) % 8 == 0, "PackDesc alignment");
+
+__device__ __forceinline__ int find_layer(const PackDesc* d, int n, int b, bool plain) {
+  int i = 0;
+  while (i + 1 < n && (plain ? d[i + 1].blk_plain : d[i + 1].blk_t) <= b) ++i;
+  return i;
+}
+
+// plain: block (layer row co, client g); the fp32 source row [cin_src][kt] is staged in LDS
+__global__ __launch_bounds__(256) void k_pack_plain(const PackDesc* __restrict__ desc, int nd,
+                                                    const float* __restrict__ theta, int64_t ldt, int G,
+                                                    uint16_t* __restrict__ out) {
+  extern __shared__ float row[];
+  const int li = find_layer(desc, nd, blockIdx.x, true);
+  const PackDesc& d = desc[li];
+  const int co = blockIdx.x - d.blk_plain, g = blockIdx.y;
+  const int Cin = d.cin_p, kt = d.kt, K = kt * Cin, Ks = kt * d.cin_src;
+  const float* src = theta + (int64_t)g * ldt + d.src_off + (int64_t)co * Ks;
+  for (int e = threadIdx.x; e < Ks; e += 256) row[e] = src[e];
+  __syncthreads();
+  uint16_t* dst = out + d.wp_off + ((int64_t)g * d.cout + co) * K;
+  for (int e = 2 * threadIdx.x; e < K; e += 2 * 256) {  // e, e+1: same tap (Cin even)
+    const int t = e / Cin, ci = e - t * Cin;
+    const float a = ci < d.cin_src ? row[ci * kt + t] : 0.f;
+    const float b = ci + 1 < d.cin_src ? row[(ci + 1) * kt + t] : 0.f;
+    *reinterpret_cast<uint32_t*>(dst + e) = pack_bf16x2(a, b);
+  }
+}
+
+// transposed: block (64 ci x 64 co tile, tap t, client g) reads the plain image written by k_pack_plain
+__global__ __launch_bounds__(256) void k_pack_trans(const PackDesc* __restrict__ desc, int nd, int G,
+                                                    uint16_t* __restrict__ out) {
+  __shared__ uint16_t tile[64][66];
+  const int li = find_layer(desc, nd, blockIdx.x, false);
+  const PackDesc& d = desc[li];
+  const int Cin = d.cin_p, Cout = d.cout, kt = d.kt;
+  const int nci = (Cin + 63) / 64, nco = (Cout + 63) / 64;
+  int b = blockIdx.x - d.blk_t;
+  const int t = b % kt;
+  b /= kt;
+  const int ci0 = (b % nci) * 64, co0 = (b / nci) * 64;
+  const int g = blockIdx.y;
+  const uint16_t* wp = out + d.wp_off + (int64_t)g * Cout * kt * Cin;
+  uint16_t* wt = out + d.wt_off + (int64_t)g * Cin * kt * Cout;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  for (int r = ty; r < 64; r += 4) {  // r = co offset, tx = ci offset
+    const int co = co0 + r, ci = ci0 + tx;
+    tile[r][tx] = (co < Cout && ci < Cin) ? wp[((int64_t)co * kt + t) * Cin + ci] : 0;
+  }
+  __syncthreads();
+  const int s = d.slot[t];
+  for (int r = ty; r < 64; r += 4) {  // r = ci offset, tx = co offset
+    const int ci = ci0 + r, co = co0 + tx;
+    if (ci < Cin && co < Cout) wt[((int64_t)ci * kt + s) * Cout + co] = tile[tx][r];
+  }
+  (void)nco;
+}
+
+// desc: device table of nd PackDesc; nplain / ntrans: total blocks of the two grids; lds: bytes for the largest
+// plain source row (max kt * cin_src * 4)
+void pack_convs(uintptr_t desc, int nd, int nplain, int ntrans, int lds, uintptr_t theta, int64_t ldt, int G,
+                uintptr_t out, uintptr_t stream) {
+  NIDT_REQUIRE(nd > 0 && G > 0 && lds > 0 && lds <= 160 * 1024, "pack_convs: bad table");
+  hipStream_t s = as_stream(stream);
+  hipLaunchKernelGGL(k_pack_plain, dim3(nplain, G), dim3(256), lds, s, ptr<const PackDesc>(desc), nd,
+                     ptr<const float>(theta), ldt, G, ptr<uint16_t>(out));
+  NIDT_CHECK(hipGetLastError());
+  if (ntrans > 0) {
+    hipLaunchKernelGGL(k_pack_trans, dim3(ntrans, G), dim3(256), 0, s, ptr<const PackDesc>(desc), nd, G,
+                       ptr<uint16_t>(out));
+    NIDT_CHECK(hipGetLastError());
+  }
+}
+
+int pack_desc_bytes() { return (int)sizeof(PackDesc); }
+
+}  // namespace nidt

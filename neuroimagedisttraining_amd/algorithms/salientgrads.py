@@ -34,15 +34,40 @@ class SailentGradsAPI(APIBase):
         return final
 
     def client_score(self, c):
+        """IterSNIP scores of client ``c`` (``sailentgrads/client.py:30-53``): the mean over
+        ``itersnip_iteration`` mini-batches of ``|w * dL/dw|``.  Each iteration takes the first batch of a fresh
+        shuffle, or with ``--stratified_sampling`` a label-stratified batch (:func:`snip.stratified_batch`, the
+        same draw as the client-batched runner's, so both paths select the same global mask)."""
         client = self.client_list[c]
         loader = client.local_training_data
         iters = int(getattr(self.args, "itersnip_iteration", 1))
+        stratified = bool(getattr(self.args, "stratified_sampling", False))
         scores = []
-        for _ in range(iters):
-            batch = next(iter(loader))
-            x, y = self.model_trainer._xy(batch, loader, self.device)
+        for it in range(iters):
+            if stratified:
+                x, y = self._stratified_xy(c, loader, it)
+            else:
+                batch = next(iter(loader))
+                x, y = self.model_trainer._xy(batch, loader, self.device)
             scores.append(S.snip_scores(self.model_trainer.model.to(self.device), x, y))
         return S.mean_scores(scores)
+
+    def _stratified_xy(self, c, loader, it):
+        """(x, y) of the stratified IterSNIP batch of client ``c`` at iteration ``it``."""
+        rng = S.stratified_rng(getattr(self.args, "seed", 0), c, it)
+        B = int(getattr(loader, "batch_size", None) or self.args.batch_size)
+        store = getattr(loader, "store", None)
+        if store is not None and hasattr(loader, "indices"):  # ABCD IndexLoader: subject indices into a store
+            idx = S.stratified_batch(loader.indices, loader._y, B, rng)
+            return store.fetch(torch.from_numpy(idx.astype(np.float32)), device=self.device)
+        # generic DataLoader: stratify over the positions of its dataset
+        ds = loader.dataset
+        ys = np.asarray([float(np.asarray(ds[i][1]).reshape(-1)[0]) for i in range(len(ds))])
+        pos = S.stratified_batch(np.arange(len(ds)), ys, B, rng)
+        xs, yl = zip(*(ds[int(i)] for i in pos))
+        x = torch.stack([torch.as_tensor(v) for v in xs]).to(self.device)
+        y = torch.as_tensor(np.asarray([np.asarray(v).reshape(-1)[0] for v in yl])).to(self.device)
+        return x, y
 
     def train(self):
         mask = self.generate_global_mask_snip()

@@ -47,6 +47,36 @@ def snip_scores(model, x, y, loss="bce"):
     return res
 
 
+def stratified_rng(seed, client, it):
+    """RNG of IterSNIP iteration ``it`` of ``client`` under ``--stratified_sampling``: a pure function of
+    (run seed, client id, iteration), shared by the eager API and the client-batched runner so both draw the
+    same mini-batches (and hence the same global mask) independently of sharding."""
+    import numpy as np
+    return np.random.RandomState(abs(hash((int(seed), -7, int(client), int(it)))) % (2 ** 31))
+
+
+def stratified_batch(indices, labels, batch_size, rng):
+    """A label-stratified mini-batch of a client's train ``indices`` (``labels[i]`` = label of ``indices[i]``):
+    per class round(B * n_class / n) samples with the largest-remainder rule (the counts sum to B), drawn
+    without replacement, returned in a random order.  This is the intent of the reference's stratified IterSNIP
+    branch (``sailentgrads/client.py:33-43``: StratifiedKFold over the client's samples) at mini-batch size."""
+    import numpy as np
+    indices = np.asarray(indices)
+    y = np.asarray(labels).reshape(-1)
+    B = min(int(batch_size), len(indices))
+    cls, cnt = np.unique(y, return_counts=True)
+    q = B * cnt / cnt.sum()
+    take = np.floor(q).astype(int)
+    for i in np.argsort(-(q - take), kind="stable")[:B - take.sum()]:
+        take[i] += 1
+    out = []
+    for k, n in zip(cls, take):
+        pool = indices[y == k]
+        out.append(pool[rng.permutation(len(pool))[:n]])
+    b = np.concatenate(out) if out else indices[:0]
+    return b[rng.permutation(len(b))]
+
+
 def mean_scores(score_dicts):
     """Element-wise mean of a list of score dicts (``get_mean_snip_scores`` / ``get_mean_sailency_scores``)."""
     out = {}

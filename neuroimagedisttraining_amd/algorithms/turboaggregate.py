@@ -153,10 +153,24 @@ def LCC_decoding(f_eval, f_deg, N, K, T, worker_idx, p):  # noqa: N802
     ``mpc_function.py:195-212``: targets are the K centred points, sources the workers' centred points).  As in
     the reference, the targets coincide with the encoder's first K points only when floor(K/2) ==
     floor((K+T)/2) (e.g. T = 1 with even K); :func:`LCC_decoding_with_points` takes explicit points."""
+    if (K // 2) != ((K + T) // 2):
+        import warnings
+        warnings.warn("LCC_decoding(K=%d, T=%d): the reference's targets lcc_points(K) differ from the encoder's data "
+                      "points; use LCC_decode_blocks to recover the encoded blocks" % (K, T), stacklevel=2)
     alpha = lcc_points(N, p)
     ev = [alpha[int(i)] for i in worker_idx]
     need = (K + T - 1) * f_deg + 1
     return LCC_decoding_with_points(np.asarray(f_eval)[:need], ev[:need], lcc_points(K, p), p)
+
+
+def LCC_decode_blocks(f_eval, f_deg, N, K, T, worker_idx, p):  # noqa: N802
+    """Recover the K data blocks that :func:`LCC_encoding` placed at its first K points beta (of K + T) from the
+    evaluations of workers ``worker_idx`` — the decoder that matches the encoder for every K, T (the
+    reference-compatible :func:`LCC_decoding` does only when floor(K/2) == floor((K+T)/2))."""
+    alpha = lcc_points(N, p)
+    ev = [alpha[int(i)] for i in worker_idx]
+    need = (K + T - 1) * f_deg + 1
+    return LCC_decoding_with_points(np.asarray(f_eval)[:need], ev[:need], lcc_points(K + T, p)[:K], p)
 
 
 def Gen_Additive_SS(d, n_out, p, rng=None):  # noqa: N802

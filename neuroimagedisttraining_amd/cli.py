@@ -14,7 +14,8 @@ the reference entry points.  Added flags:
   ``--synthetic_size N``: N synthetic train images (N/5 test) for CIFAR/Tiny without data files.
 * FedProx / robust aggregation: ``--fedprox_mu``, ``--aggregator {fedavg,krum,multikrum,median,trimmed_mean}``,
   ``--byzantine_f``, ``--trim_ratio``.
-* ``--checkpoint_dir`` / ``--resume`` for the HIP executor.
+* ``--checkpoint_dir`` / ``--checkpoint_every`` / ``--keep_last`` / ``--resume`` for the HIP executor (background-written,
+  indexed, world-size independent checkpoints: ``utils/checkpoint.py``).
 
 Run under ``torchrun`` for multi-GPU; single process otherwise.
 """
@@ -112,8 +113,9 @@ def add_args(parser, algo):
     a("--synthetic_abcd", type=int, default=1)
     a("--n_per_client", type=int, default=180)
     a("--synthetic_size", type=int, default=0)
-    a("--rebalance", type=int, default=0)  # 1: (HIP, multi-rank, frac < 1) replicate the cohort, even per-round load
-    a("--heartbeat_s", type=float, default=0.0)  # >0: multi-rank failure detection (comm/failure.py)  # 2D datasets without files: synthetic train images (0 = full size)
+    a("--rebalance", type=int, default=0)  # 1: (HIP, multi-rank, frac < 1) move sampled clients + samples to even the load
+    a("--heartbeat_s", type=float, default=0.0)  # >0: multi-rank failure detection (comm/failure.py)
+    a("--augment", type=int, default=1)  # image datasets: the reference's train-time RandomCrop(pad 4) + flip
     a("--fedprox_mu", type=float, default=d.get("fedprox_mu", 0.0))
     a("--aggregator", type=str, default="fedavg")
     a("--byzantine_f", type=int, default=0)
@@ -121,6 +123,8 @@ def add_args(parser, algo):
     a("--update_topk", type=float, default=0.0, help="send only the top-k fraction of each client's update")
     a("--group", type=int, default=0)
     a("--checkpoint_dir", type=str, default="")
+    a("--checkpoint_every", type=int, default=1, help="save every N rounds (and after the last round)")
+    a("--keep_last", type=int, default=2, help="complete checkpoint rounds kept on disk (0 = all)")
     a("--resume", type=int, default=0)
     a("--log_dir", type=str, default="LOG")
     return parser
@@ -196,20 +200,21 @@ def load_data(args, dataset_name, logger=None):
         return images.load_partition_data(dataset_name, args.data_dir, args.partition_method, args.partition_alpha,
                                           args.client_num_in_total, args.batch_size, logger, seed=args.seed,
                                           with_val=getattr(args, "algo", "") == "fedfomo", n_train=n,
-                                          n_test=n // 5 if n else None)
+                                          n_test=n // 5 if n else None, augment=bool(getattr(args, "augment", 1)))
     if dataset_name == "synthetic":
         return images.load_partition_data_synthetic_tabular(args.client_num_in_total, args.batch_size)
     raise ValueError(dataset_name)
 
 
 RESNET3D_NAMES = ("resnet3d_50", "3dresnet50")
-IMAGE_DATASETS = ("cifar10", "cifar100")
+IMAGE_DATASETS = ("cifar10", "cifar100", "tiny")
 
 
 def hip_family(args):
     """Model family of the client-batched MI355X executor for these flags, or None (eager only):
     ``alexnet3d`` (3DCNN on ABCD: engine/executor.HipEngine), ``resnet2d`` (resnet18 = ResNet-18-GN on 32x32
-    CIFAR-10/100: engine/resnet2d_hip), ``resnet3d`` (3D ResNet-50 on ABCD: engine/resnet3d_hip)."""
+    CIFAR-10/100 or 64x64 Tiny-ImageNet — ``customized_resnet18`` / ``tiny_resnet18``: engine/resnet2d_hip),
+    ``resnet3d`` (3D ResNet-50 on ABCD: engine/resnet3d_hip)."""
     model = args.model.lower()
     if args.dataset == "ABCD" and model in ("3dcnn", "alexnet3d", "alexnet3d_dropout"):
         return "alexnet3d"
@@ -283,7 +288,7 @@ def hip_cohort(args, info, logger=None, with_val=False, raw=False):
         tr = [np.asarray(train[c]) for c in range(N)]
         te = [np.asarray(test[c]) for c in range(N)]
         shards = rt.shard_clients([len(t) for t in tr], info.world)
-        mine = list(range(N)) if getattr(args, "rebalance", 0) else shards[info.rank]
+        mine = shards[info.rank]  # rebalancing moves a client's samples with it: the store is never replicated
         subj = np.concatenate([np.concatenate([tr[c], te[c]]) for c in mine]) if mine else np.zeros(0, np.int64)
         if raw:
             x8, mom = stream_to_device(vf, subj, info.device), None
@@ -300,7 +305,7 @@ def hip_cohort(args, info, logger=None, with_val=False, raw=False):
         n_test = max(1, int(round(args.n_per_client * 0.2)))
         n_train = args.n_per_client - n_test
         shards = rt.shard_clients([n_train] * N, info.world)
-        mine = list(range(N)) if getattr(args, "rebalance", 0) else shards[info.rank]
+        mine = shards[info.rank]
         vol, labels, local = build_fl_volumes(mine, N, n_train, n_test, info.device, seed=args.seed,
                                               alpha=args.partition_alpha)
         if raw:
@@ -309,12 +314,14 @@ def hip_cohort(args, info, logger=None, with_val=False, raw=False):
             x8, mom = to_hip_store(vol)
         del vol
         sizes = [(n_train, n_test)] * N
+    nval = None
     if with_val:
         nval = int(0.1 * sizes[0][0])
         for c, sp in local.items():
             local[c] = ClientSplit(sp.train[nval:], sp.test, sp.train[:nval])
         sizes = [(a - nval, b) for a, b in sizes]
-    splits = [local.get(c) or ClientSplit(np.zeros(sizes[c][0], np.int64), np.zeros(sizes[c][1], np.int64))
+    splits = [local.get(c) or ClientSplit(np.zeros(sizes[c][0], np.int64), np.zeros(sizes[c][1], np.int64),
+                                          None if nval is None else np.zeros(nval, np.int64))
               for c in range(N)]
     return x8, mom, labels, splits
 
@@ -343,18 +350,18 @@ def fl_config(args, algo):
 
 
 def image_cohort(args, info, with_val=False):
-    """(x8, labels, splits) for the client-batched ResNet-18-GN engine: the CIFAR-10/100 train and test images as
-    uint8 ``[N, 32, 32, 3]`` in one device store (train first, test at ``+n_train``), split exactly as the eager
-    loaders do (``data/images.load_partition_data``: same partitioner, same RandomState stream, per-client test
-    sets drawn from the train label histogram, FedFomo's 10 % validation split).
+    """(x8, labels, splits, n_cls) for the client-batched ResNet-18-GN engine: the CIFAR-10/100 (32x32) or
+    Tiny-ImageNet (64x64) train and test images as uint8 ``[N, S, S, 3]`` in one device store (train first, test at
+    ``+n_train``), split exactly as the eager loaders do (``data/images.load_partition_data``: same partitioner, same
+    RandomState stream, per-client test sets drawn from the train label histogram, FedFomo's 10 % validation split).
 
-    Pixels: an ``.npz`` (``--data_dir``) holding uint8 HWC images is used as is (the engine applies the reference's
-    CIFAR mean/std normalisation); float images (the synthetic loader's, or a float ``.npz``) are taken to be
-    normalised NCHW tensors and mapped back to uint8 pixels."""
+    Pixels: an ``.npz`` (``--data_dir``) holding uint8 HWC images is used as is (the engine applies the dataset's
+    mean/std normalisation, ``images.NORM``); float images (the synthetic loader's, or a float ``.npz``) are taken
+    to be normalised NCHW tensors and mapped back to uint8 pixels."""
     from .core import partition as PT
     from .data import images
     from .engine.executor import ClientSplit
-    from .engine.resnet2d_hip import CIFAR_MEAN, CIFAR_STD
+    MEAN, STD = images.NORM[args.dataset]
     n = getattr(args, "synthetic_size", 0) or None
     xtr, ytr, xte, yte, n_cls = images._load_arrays(args.dataset, args.data_dir, n, n // 5 if n else None,
                                                      args.seed)
@@ -366,12 +373,13 @@ def image_cohort(args, info, with_val=False):
     def to_u8(x):
         if x.dtype == torch.uint8:
             return x
-        mean = torch.tensor(CIFAR_MEAN).view(1, 3, 1, 1)
-        std = torch.tensor(CIFAR_STD).view(1, 3, 1, 1)
+        mean = torch.tensor(MEAN).view(1, 3, 1, 1)
+        std = torch.tensor(STD).view(1, 3, 1, 1)
         return ((x * std + mean) * 255.0).round().clamp(0, 255).to(torch.uint8).permute(0, 2, 3, 1).contiguous()
 
     xtr, xte = to_u8(xtr), to_u8(xte)
-    assert tuple(xtr.shape[1:]) == (32, 32, 3), xtr.shape
+    side = 64 if args.dataset == "tiny" else 32
+    assert tuple(xtr.shape[1:]) == (side, side, 3), xtr.shape
     N = args.client_num_in_total
     rng = np.random.RandomState(args.seed)
     train_map = images.partition_data(ytr.numpy(), args.partition_method, N, args.partition_alpha, n_cls, rng)
@@ -396,13 +404,18 @@ def build_hip_engine(args, algo, info, logger=None):
     """(engine, template model, client splits) of the client-batched executor for this model family."""
     fam = hip_family(args)
     if fam == "resnet2d":
+        from .data.images import NORM
         from .engine.resnet2d_hip import ResNetHipEngine
-        from .models import customized_resnet18
+        from .models import customized_resnet18, tiny_resnet18
         x8, y, splits, n_cls = image_cohort(args, info, with_val=algo == "fedfomo")
-        model = customized_resnet18(class_num=n_cls)
+        # main_subavg.py:149-152: resnet18 is tiny_resnet18 on Tiny-ImageNet (AdaptiveAvgPool2d), else
+        # customized_resnet18 — same parameters, the engine pools the whole final map in both
+        model = (tiny_resnet18 if args.dataset == "tiny" else customized_resnet18)(class_num=n_cls)
         desc = "%s %s images (%d clients)" % ("synthetic" if not args.data_dir else args.data_dir, args.dataset,
                                               len(splits))
-        return ResNetHipEngine(model, x8, y, info.device), model, splits, desc
+        mean, std = NORM[args.dataset]
+        eng = ResNetHipEngine(model, x8, y, info.device, mean=mean, std=std, augment=bool(getattr(args, "augment", 1)))
+        return eng, model, splits, desc
     if fam == "resnet3d":
         from .engine.resnet3d_hip import ResNet3DHipEngine
         from .models.resnet3d import resnet3d_50
@@ -436,10 +449,14 @@ def run_hip(args, algo, logger):
         logger.info("resumed from %s at round %d", args.checkpoint_dir, start)
     elif runner.alg == "salientgrads":
         runner.generate_global_mask_snip()
+    saver = (ck.Checkpointer(args.checkpoint_dir, info, every=args.checkpoint_every, keep_last=args.keep_last)
+             if args.checkpoint_dir else None)
     for r in range(start, cfg.comm_round):
         runner.run_round(r)
-        if args.checkpoint_dir:
-            ck.save_runner(runner, args.checkpoint_dir, r + 1)
+        if saver is not None:
+            saver.maybe_save(runner, r + 1, last=r + 1 == cfg.comm_round)
+    if saver is not None:
+        saver.close()
     runner.finish()
     rt.shutdown(info)
     return runner.stat_info

@@ -22,7 +22,7 @@ import os
 
 import numpy as np
 import torch
-from torch.utils.data import DataLoader, TensorDataset
+from torch.utils.data import DataLoader, Dataset, TensorDataset
 
 from ..core import partition as P
 
@@ -61,9 +61,47 @@ def _load_arrays(dataset, data_dir, n_train=None, n_test=None, seed=0):
     return xtr, ytr, xte, yte, n_cls
 
 
-def _loader(x, y, idx, bs, shuffle):
+# Normalize constants of the reference loaders (cifar10/data_loader.py:43-44, cifar100/data_loader.py:30-31,
+# tiny_imagenet/data_loader.py:49-50); the images handled here are already normalised with them
+NORM = {"cifar10": ((0.49139968, 0.48215827, 0.44653124), (0.24703233, 0.24348505, 0.26158768)),
+        "cifar100": ((0.5071, 0.4865, 0.4409), (0.2673, 0.2564, 0.2762)),
+        "tiny": ((0.5, 0.5, 0.5), (0.5, 0.5, 0.5))}
+AUG_PAD = 4
+
+
+class AugmentedTensorDataset(Dataset):
+    """Train-time augmentation of the reference image loaders on normalised CHW tensors: RandomCrop(size, padding=4)
+    then RandomHorizontalFlip(0.5) (``cifar10/data_loader.py:46-52``, ``tiny_imagenet/data_loader.py:51-57``).
+    The reference pads the uint8 PIL image with 0 before normalising, so the padding here is the normalised value of
+    a black pixel, -mean/std per channel.  Draws follow torchvision: top, then left, each ``torch.randint(0, 2 pad +
+    1)``, then ``torch.rand(1) < 0.5`` for the flip (global torch RNG, as the reference's DataLoader workers)."""
+
+    def __init__(self, x, y, mean, std, pad=AUG_PAD):
+        self.x, self.y, self.pad = x, y, int(pad)
+        self.fill = (-torch.tensor(mean, dtype=x.dtype) / torch.tensor(std, dtype=x.dtype)).view(-1, 1, 1)
+
+    def __len__(self):
+        return len(self.y)
+
+    def __getitem__(self, i):
+        img = self.x[i]
+        C, H, W = img.shape
+        p = self.pad
+        top = int(torch.randint(0, 2 * p + 1, (1,)))
+        left = int(torch.randint(0, 2 * p + 1, (1,)))
+        padded = self.fill[:C].expand(C, H + 2 * p, W + 2 * p).clone()
+        padded[:, p:p + H, p:p + W] = img
+        out = padded[:, top:top + H, left:left + W]
+        if float(torch.rand(1)) < 0.5:
+            out = out.flip(-1)
+        return out.contiguous(), self.y[i]
+
+
+def _loader(x, y, idx, bs, shuffle, augment=None):
+    """``augment``: (mean, std) of the dataset -> train-time RandomCrop + RandomHorizontalFlip."""
     idx = torch.as_tensor(np.asarray(idx, dtype=np.int64))
-    return DataLoader(TensorDataset(x[idx], y[idx]), batch_size=bs, shuffle=shuffle, drop_last=False)
+    ds = AugmentedTensorDataset(x[idx], y[idx], *augment) if augment is not None else TensorDataset(x[idx], y[idx])
+    return DataLoader(ds, batch_size=bs, shuffle=shuffle, drop_last=False)
 
 
 def partition_data(y_train, partition, n_clients, alpha, n_cls, rng=None):
@@ -71,8 +109,11 @@ def partition_data(y_train, partition, n_clients, alpha, n_cls, rng=None):
 
 
 def load_partition_data(dataset, data_dir, partition_method, partition_alpha, client_number, batch_size,
-                        logger=None, n_train=None, n_test=None, seed=0, with_val=False):
+                        logger=None, n_train=None, n_test=None, seed=0, with_val=False, augment=True):
+    """``augment``: the reference's train-time RandomCrop(pad 4) + RandomHorizontalFlip on the train loaders of the
+    image datasets (validation and test loaders are never augmented)."""
     logger = logger or log
+    aug = NORM.get(dataset) if augment else None
     xtr, ytr, xte, yte, n_cls = _load_arrays(dataset, data_dir, n_train, n_test, seed)
     rng = np.random.RandomState(seed)
     train_map = partition_data(ytr.numpy(), partition_method, client_number, partition_alpha, n_cls, rng)
@@ -88,7 +129,7 @@ def load_partition_data(dataset, data_dir, partition_method, partition_alpha, cl
     num, trn, tst, val = {}, {}, {}, {}
     for c in range(client_number):
         num[c] = len(train_map[c])
-        trn[c] = _loader(xtr, ytr, train_map[c], batch_size, True)
+        trn[c] = _loader(xtr, ytr, train_map[c], batch_size, True, aug)
         tst[c] = _loader(xte, yte, test_map[c], batch_size, False)
         if with_val:
             val[c] = _loader(xtr, ytr, val_map[c], batch_size, False)

@@ -95,8 +95,8 @@ class FLConfig:
     dist_thresh: float = 1e-4         # SubAvg: prune only if the mask moved more than this
     acc_thresh: float = 0.5           # SubAvg: and the pruned model's local training accuracy exceeds this
     rebalance: bool = False       # multi-rank, frac < 1: before each round move the sampled clients' state (rows, masks)
-                                  # so every rank trains about the same number of samples; needs every rank to hold
-                                  # every client's data (replicated cohort: it fits in 288 GB of HBM)
+                                  # and their samples (engine.sample_fields) so every rank trains about the same
+                                  # number of samples; the data stays sharded like the clients
     heartbeat_s: float = 0.0      # >0: ranks publish heartbeats every heartbeat_s through the process group's store and
                                   # each round fails fast (comm.failure.PeerFailure) if a peer is silent for 30x that
 
@@ -104,6 +104,7 @@ class FLConfig:
 # ------------------------------------------------------------------------------------------------
 class HipEngine:
     """AlexNet3D_Dropout on the gfx950 kernels (ABCD-shape volumes, polyphase uint8 store)."""
+    sample_fields = ("x8", "mom", "labels")  # per-sample store rows (they travel with a migrating client)
 
     def __init__(self, template_model, x8, mom, labels, device):
         from .alexnet_hip import HipAlexNet3D
@@ -174,6 +175,7 @@ class TorchEngine:
 
     ``store``: float tensor ``[N, ...]`` of inputs (already scaled); ``labels``: ``[N]``.
     ``loss``: ``"bce"`` (class_num=1, logits [B,1]) or ``"ce"`` (multi-class)."""
+    sample_fields = ("store", "labels")
 
     def __init__(self, template_model, store, labels, device, loss="bce", dtype=torch.float32, amp=False):
         self.model = template_model.to(device)

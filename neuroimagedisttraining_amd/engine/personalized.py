@@ -342,7 +342,7 @@ class FedFomoRunner(PersonalizedRunner):
             pairs.append((prow[("old", c)], c))
             for j in nei[c]:
                 pairs.append((prow[("new", c)] if j == c else prow[("old", j)], c))
-        which = "val" if self.splits[self.local[0]].val is not None else "test"
+        which = "val" if getattr(self.splits[0], "val", None) is not None else "test"  # same rule on every rank
         met = self.eval_grouped(pool.theta, pool.bufs, [p for p, _ in pairs], [c for _, c in pairs], which)
         # parameter distances ||theta_j - theta_c^old|| over the whole state (params and buffers)
         dpairs = []

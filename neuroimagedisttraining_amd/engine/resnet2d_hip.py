@@ -1,23 +1,33 @@
-"""Client-batched ResNet-18-GN (CIFAR) on the gfx950 conv kernels: G clients' local steps in one lockstep pass.
+"""Client-batched ResNet-18-GN (CIFAR-10/100, Tiny-ImageNet) on the gfx950 conv kernels: G clients' local steps in
+one lockstep pass.
 
-The reference trains its CIFAR baselines (SubAvg / DisPFL / D-PSGD / FedFomo with ``customized_resnet18``,
-``fedml_api/model/cv/resnet.py:91-124``: CIFAR ResNet-18, GroupNorm(32) everywhere, avg_pool2d(4) head) one
-client after another through cuDNN.  Here every client of a launch group is a row of the flat ``[C, P]``
-parameter matrix and each layer runs ONCE for all of them:
+The reference trains its image baselines (SubAvg / DisPFL / D-PSGD / FedFomo / Ditto / Local with
+``customized_resnet18`` on CIFAR, ``fedml_api/model/cv/resnet.py:91-124``, and ``tiny_resnet18`` on Tiny-ImageNet,
+``resnet.py:134-214``: ResNet-18 with GroupNorm(32) everywhere) one client after another through cuDNN.  Here every
+client of a launch group is a row of the flat ``[C, P]`` parameter matrix and each layer runs ONCE for all of them:
 
+* input: one fused kernel (``img.hip``) gathers the batch's uint8 images, applies the reference's train-time
+  RandomCrop(pad 4) + RandomHorizontalFlip with per-(step, client, sample) draws made on device, normalises and
+  zero-pads the channels (``data_loader.py:46-52`` of the cifar10 / cifar100 / tiny loaders);
+* weights: every layer's bf16 MFMA images (forward, and the data-gradient image in its tap-slot order) are packed
+  in two launches per step (``pack.hip``);
 * every convolution (3x3 stride 1/2, the 1x1 stride-2 projection shortcuts, the stem) is the client-grouped
   LDS-DMA implicit-GEMM kernel of ``conv3d.hip`` run on D = 1 volumes with 9 taps (``conv_fwd_g``); the stem's
   3 input channels are zero-padded to 64 (one more layer-1-sized GEMM instead of a separate kernel);
-* the data gradient is the same kernel on tap-flipped transposed weights (stride 2: on the zero-upsampled
-  gradient; 1x1 stride 2: scattered to the even pixels), the weight gradient is the position-table wgrad
-  kernel writing PyTorch-layout fp32 straight into the client's gradient row (``conv_wgrad_g``);
+* data gradients: stride 1 = the same kernel on tap-flipped transposed weights; stride 2 (3x3) = four sub-pixel
+  phase convs over the dy grid with 1/2/2/4 taps written straight into the interleaved dX positions
+  (``conv_dgrad_s2_g``: 4x fewer MACs than a conv over the zero-upsampled gradient, no memset); 1x1 stride 2 = the
+  half-resolution W^T dY that ``res_grad_s2`` adds at the even pixels.  The weight gradient is the position-table
+  wgrad kernel writing PyTorch-layout fp32 straight into the client's gradient row (``conv_wgrad_g``);
 * activations are bf16 channels-last ``[G*B, H, W, C]``; GroupNorm (+ the residual add and ReLU, fused) is the
-  one-block-per-sample ``gn.hip`` kernel pair; the head and the loss are small fp32 torch ops over the whole group
-  (one launch per op, not per client).  The backward is written out explicitly (no autograd graph) and every op
-  is deterministic and workspace-free, so the step is hipGraph-capturable.
+  one-block-per-sample ``gn.hip`` kernel pair (streaming variant for the 64x64 Tiny maps); the head and the loss are
+  small fp32 torch ops over the whole group (one launch per op, not per client).  The backward is written out
+  explicitly (no autograd graph) and every op is deterministic and workspace-free, so the step is
+  hipGraph-capturable.
 
-A CPU twin (``device.type == 'cpu'``) runs the same graph with fp32 torch convolutions (grouped by client); the
-CPU tests compare it with per-client autograd through the reference-shaped ``nn.Module``.
+A CPU twin (``device.type == 'cpu'``) runs the same graph with fp32 torch convolutions (grouped by client) and the
+same augmentation draws; the CPU tests compare it with per-client autograd through the reference-shaped
+``nn.Module``.
 """
 from __future__ import annotations
 
@@ -28,8 +38,11 @@ import torch.nn.functional as F
 from .. import ops
 from .flat import ParamLayout
 
-CIFAR_MEAN = (0.4914, 0.4822, 0.4465)   # reference cifar10/data_loader.py normalisation
-CIFAR_STD = (0.2470, 0.2435, 0.2616)
+CIFAR_MEAN = (0.49139968, 0.48215827, 0.44653124)   # reference cifar10/data_loader.py:43-44 normalisation
+CIFAR_STD = (0.24703233, 0.24348505, 0.26158768)
+TINY_MEAN = (0.5, 0.5, 0.5)                          # reference tiny_imagenet/data_loader.py:49-50
+TINY_STD = (0.5, 0.5, 0.5)
+AUG_PAD = 4                                          # RandomCrop(S, padding=4) of every image loader
 GN_GROUPS = 32
 GN_EPS = 1e-5
 
@@ -38,6 +51,48 @@ def _stream():
     return torch.cuda.current_stream().cuda_stream
 
 
+# ------------------------------------------------------------------------------------------------ augmentation
+_M64 = (1 << 64) - 1
+
+
+def mix64(seed, a, b):
+    """The splitmix64 finaliser of ``img.hip`` (exact twin, Python ints)."""
+    z = (int(seed) ^ ((0x9e3779b97f4a7c15 * (((int(a) & 0xffffffff) << 32) ^ int(b))) & _M64)) & _M64
+    z = ((z ^ (z >> 30)) * 0xbf58476d1ce4e5b9) & _M64
+    z = ((z ^ (z >> 27)) * 0x94d049bb133111eb) & _M64
+    return z ^ (z >> 31)
+
+
+def aug_draws(seed, cids, B, pad=AUG_PAD):
+    """Per-sample (crop y offset, crop x offset, flip) of a lockstep step: sample j of client cids[g] draws from
+    mix64(step seed, client id, j) — offsets uniform in [0, 2 pad] (torchvision RandomCrop(padding=pad)), flip with
+    p = 1/2 (RandomHorizontalFlip).  Returns int64 arrays [len(cids) * B]."""
+    span = 2 * pad + 1
+    oy, ox, fl = [], [], []
+    for c in cids:
+        for j in range(B):
+            h = mix64(seed, c, j)
+            lo, hi = h & 0xffffffff, h >> 32
+            oy.append(lo % span)
+            ox.append((lo // span) % span)
+            fl.append(hi & 1)
+    return np.array(oy), np.array(ox), np.array(fl)
+
+
+def augment_u8(img, oy, ox, flip, pad=AUG_PAD):
+    """torchvision RandomCrop(size, padding=pad) + RandomHorizontalFlip of uint8 HWC images [N, H, W, 3] with given
+    draws (the CPU twin of the fused HIP input stage; padded pixels are 0)."""
+    N, H, W, _ = img.shape
+    padded = torch.zeros(N, H + 2 * pad, W + 2 * pad, 3, dtype=img.dtype, device=img.device)
+    padded[:, pad:pad + H, pad:pad + W] = img
+    out = torch.empty_like(img)
+    for n in range(N):
+        crop = padded[n, int(oy[n]):int(oy[n]) + H, int(ox[n]):int(ox[n]) + W]
+        out[n] = crop.flip(1) if int(flip[n]) else crop
+    return out
+
+
+# ------------------------------------------------------------------------------------------------ convolutions
 def conv_fwd(x_ptr, w_ptr, y_ptr, G, B, D, H, W, Cin, Cout, kt, st, pad, padd, device):
     """Client-grouped conv forward (``conv_fwd_g``), split over the reduction when the output grid is too small to
     fill the chip (``conv_fwd_g_ksplit``: deep layers at small spatial size, few clients per GPU)."""
@@ -52,6 +107,30 @@ def conv_fwd(x_ptr, w_ptr, y_ptr, G, B, D, H, W, Cin, Cout, kt, st, pad, padd, d
     m.conv_fwd_gk(x_ptr, w_ptr, y_ptr, part.data_ptr(), ks, G, B, D, H, W, Cin, Cout, kt, st, pad, padd, _stream())
 
 
+def tap_slots(kt, stride):
+    """Tap order of a layer's data-gradient weight image (``conv_tap_slots`` in conv3d.hip): stride 1 -> flipped,
+    stride 2 (3x3) -> sub-pixel phase order, 1x1 -> identity."""
+    if torch.cuda.is_available():
+        try:
+            return list(ops.ext().conv_tap_slots(kt, stride))
+        except Exception:  # noqa: BLE001 - CPU twin without the extension
+            pass
+    if kt == 1:
+        return [0]
+    if stride == 1:
+        return [kt - 1 - t for t in range(kt)]
+    # 2-D sub-pixel phases (conv_s2_phase_plan): per dim phase 0 <- k=1, phase 1 <- k=0, k=2
+    lists = {0: [1], 1: [0, 2]}
+    out, slot = [0] * kt, 0
+    for ah in (0, 1):
+        for aw in (0, 1):
+            for kh in lists[ah]:
+                for kw in lists[aw]:
+                    out[kh * 3 + kw] = slot
+                    slot += 1
+    return out
+
+
 class GroupedConv:
     """One conv layer of the client-grouped network (weights = rows of theta at ``off``, PyTorch layout
     ``[Cout, cin, k, k]``).  ``cin_p`` = channels of the activation tensor (cin zero-padded to 64)."""
@@ -63,35 +142,39 @@ class GroupedConv:
         self.hip = hip
         self.numel = cout * cin * k * k
         self.need_dgrad = self.cin_p == self.cin  # the (channel-padded) stem needs no input gradient
-        self._packed = None
+        self.slots = tap_slots(self.kt, stride)
+        self.wp = self.wt = None  # packed images of the current step (WeightPacker.pack)
 
     def out_hw(self, h, w):
         return ((h + 2 * self.pad - self.k) // self.stride + 1, (w + 2 * self.pad - self.k) // self.stride + 1)
 
     # ---------------------------------------------------------------- weights
     def _wp(self, theta, G, transposed):
+        """Standalone per-layer packing (kernel tests); the network packs every layer at once (WeightPacker)."""
         m = ops.ext()
         wp = torch.empty(G, self.cout, self.kt, self.cin_p, device=theta.device, dtype=torch.bfloat16)
         wt = torch.empty(G, self.cin_p, self.kt, self.cout, device=theta.device, dtype=torch.bfloat16) \
             if transposed else None
-        m.pack_conv_wk(theta.data_ptr(), theta.stride(0), self.off, G, self.cout, self.cin_p, self.kt, self.cin, 1.0,
-                       wp.data_ptr(), wt.data_ptr() if transposed else 0, _stream())
+        WeightPacker([self], theta.device).pack_into(theta, G, wp, wt)
         return wp, wt
 
     def _wtorch(self, theta, G):
         return theta[:, self.off:self.off + self.numel].reshape(G * self.cout, self.cin, self.k, self.k)
 
     # ---------------------------------------------------------------- forward
-    def fwd(self, x, theta, G, train=False):
-        """``train``: also pack the transposed (dgrad) weights now and keep both for :meth:`bwd` of this step
-        (one packing pass per conv per step instead of re-packing in the backward)."""
+    def fwd(self, x, theta, G, train=False, packed=False):
+        """``packed``: the network's WeightPacker has packed this step's images (``self.wp`` / ``self.wt``);
+        otherwise (standalone layer) the layer packs its own, incl. the dgrad image when ``train``."""
         N, H, W, C = x.shape
         assert C == self.cin_p and N % G == 0, (x.shape, self.cin_p, G)
         Ho, Wo = self.out_hw(H, W)
         if not self.hip:
             return self._torch_fwd(x, self._wtorch(theta, G), G)
-        wp, wt = self._wp(theta, G, train and self.need_dgrad)
-        self._packed = (theta.data_ptr(), G, wt) if train else None
+        if not packed:
+            wp, wt = self._wp(theta, G, train and self.need_dgrad)
+            self.wp = (wp, G, theta.data_ptr())
+            self.wt = (wt, G, theta.data_ptr()) if wt is not None else None
+        wp = self.wp[0]
         y = torch.empty(N, Ho, Wo, self.cout, device=x.device, dtype=torch.bfloat16)
         conv_fwd(x.data_ptr(), wp.data_ptr(), y.data_ptr(), G, N // G, 1, H, W, self.cin_p, self.cout,
                  self.kt, self.stride, self.pad, 0, x.device)
@@ -107,7 +190,9 @@ class GroupedConv:
 
     # ---------------------------------------------------------------- backward
     def bwd(self, dy, x, theta, grads, G, need_dx, scratch=None):
-        """dW -> grads rows (PyTorch layout at ``off``); returns dX ``[N, H, W, cin_p]`` (or None)."""
+        """dW -> grads rows (PyTorch layout at ``off``); returns dX ``[N, H, W, cin_p]`` (or None).  For the 1x1
+        stride-2 projection the returned gradient is the half-resolution one of the even pixels (``res_grad_s2``
+        adds it into the residual stream)."""
         if not self.hip:
             return self._torch_bwd(dy, x, theta, grads, G, need_dx)
         m, st = ops.ext(), _stream()
@@ -131,31 +216,30 @@ class GroupedConv:
                 full.view(G, self.cout, self.cin_p, self.kt)[:, :, :self.cin])
         if not need_dx:
             return None
-        pk, self._packed = self._packed, None
-        if pk is not None and pk[0] == theta.data_ptr() and pk[1] == G and pk[2] is not None:
-            wt = pk[2]
-        else:
-            _, wt = self._wp(theta, G, True)
-        dx = torch.empty(N, H, W, self.cin_p, device=x.device, dtype=torch.bfloat16)
+        wt = self.wt
+        if wt is None or wt[1] != G or wt[2] != theta.data_ptr():  # backward without a training forward
+            wt = (self._wp(theta, G, True)[1], G, theta.data_ptr())
+        wt = wt[0]
+        self.wt = None
         if self.stride == 1:
+            dx = torch.empty(N, H, W, self.cin_p, device=x.device, dtype=torch.bfloat16)
             conv_fwd(dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), G, B, 1, Ho, Wo, self.cout, self.cin_p, self.kt,
-                         1, self.k - 1 - self.pad, 0, x.device)
-        elif self.k == 3:
-            # stride 2: dX = conv(zero-upsampled dY, flipped W^T, pad k-1-pad) (H = 2 Ho for the even CIFAR maps)
-            assert H == 2 * Ho and W == 2 * Wo and self.pad == 1, (H, W, Ho, Wo)
-            up = torch.zeros(N, H, W, self.cout, device=x.device, dtype=torch.bfloat16)
-            up[:, ::2, ::2] = dy
-            conv_fwd(up.data_ptr(), wt.data_ptr(), dx.data_ptr(), G, B, 1, H, W, self.cout, self.cin_p, self.kt,
-                         1, 1, 0, x.device)
-        else:
-            # 1x1 stride 2: only the even pixels were read: dX there = W^T dY, zero elsewhere
-            assert self.k == 1 and self.pad == 0 and (H + 1) // 2 == Ho and (W + 1) // 2 == Wo
-            sub = torch.empty(N, Ho, Wo, self.cin_p, device=x.device, dtype=torch.bfloat16)
-            conv_fwd(dy.data_ptr(), wt.data_ptr(), sub.data_ptr(), G, B, 1, Ho, Wo, self.cout, self.cin_p, 1, 1,
-                         0, 0, x.device)
-            dx.zero_()
-            dx[:, ::2, ::2] = sub
-        return dx
+                     1, self.k - 1 - self.pad, 0, x.device)
+            return dx
+        if self.k == 3:
+            # sub-pixel phases: 4 stride-1 convs over the dy grid with 1/2/2/4 taps, written straight into the
+            # interleaved positions of dX (no zero-upsampled copy of dy: 4x fewer MACs, no memset / scatter)
+            assert self.pad == 1 and H in (2 * Ho, 2 * Ho - 1) and W in (2 * Wo, 2 * Wo - 1), (H, W, Ho, Wo)
+            dx = torch.empty(N, H, W, self.cin_p, device=x.device, dtype=torch.bfloat16)
+            m.conv_dgrad_s2_g(dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), G, B, 1, Ho, Wo, self.cout, self.cin_p,
+                              self.kt, 1, H, W, st)
+            return dx
+        # 1x1 stride 2: only the even pixels were read -> half-resolution gradient W^T dY (res_grad_s2 scatters)
+        assert self.k == 1 and self.pad == 0 and (H + 1) // 2 == Ho and (W + 1) // 2 == Wo
+        sub = torch.empty(N, Ho, Wo, self.cin_p, device=x.device, dtype=torch.bfloat16)
+        conv_fwd(dy.data_ptr(), wt.data_ptr(), sub.data_ptr(), G, B, 1, Ho, Wo, self.cout, self.cin_p, 1, 1,
+                 0, 0, x.device)
+        return sub
 
     def _torch_bwd(self, dy, x, theta, grads, G, need_dx):
         w = self._wtorch(theta, G).detach().clone().requires_grad_(True)
@@ -164,7 +248,84 @@ class GroupedConv:
             y = self._torch_fwd(xx, w, G)
             outs = torch.autograd.grad(y, [w, xx] if need_dx else [w], dy.to(y.dtype))
         grads[:, self.off:self.off + self.numel].copy_(outs[0].reshape(G, -1))
-        return outs[1] if need_dx else None
+        if not need_dx:
+            return None
+        dx = outs[1]
+        if self.stride == 2 and self.k == 1:  # same contract as the HIP path: the even pixels only
+            dx = dx[:, ::2, ::2].contiguous()
+        return dx
+
+
+# descriptor of pack.hip (PackDesc): int64 src_off, wp_off, wt_off; int32 cout, cin_p, cin_src, kt, blk_plain, blk_t,
+# slot[27]; 160 bytes with the struct's 8-B alignment
+_PACK_DTYPE = np.dtype({"names": ["src_off", "wp_off", "wt_off", "cout", "cin_p", "cin_src", "kt", "blk_plain",
+                                  "blk_t", "slot"],
+                        "formats": ["<i8", "<i8", "<i8", "<i4", "<i4", "<i4", "<i4", "<i4", "<i4", ("<i4", 27)],
+                        "offsets": [0, 8, 16, 24, 28, 32, 36, 40, 44, 48], "itemsize": 160})
+
+
+class WeightPacker:
+    """Per-step bf16 MFMA images of every conv layer of G clients in two launches (``pack.hip`` ``pack_convs``): the
+    forward image of each layer and, for training steps, the data-gradient image (taps in the layer's slot order).
+    Buffers are persistent per launch shape, so a captured step's graph writes and reads the same memory."""
+
+    def __init__(self, convs, device):
+        self.convs, self.device = list(convs), torch.device(device)
+        self._plans = {}
+
+    def _plan(self, G, train, key=None):
+        key = (G, train) if key is None else key
+        if key in self._plans:
+            return self._plans[key]
+        if ops.ext().pack_desc_bytes() != _PACK_DTYPE.itemsize:
+            raise RuntimeError("pack.hip PackDesc layout changed")
+        desc = np.zeros(len(self.convs), dtype=_PACK_DTYPE)
+        off = nplain = ntrans = 0
+        views = []
+        for i, c in enumerate(self.convs):
+            d = desc[i]
+            d["src_off"], d["cout"], d["cin_p"], d["cin_src"], d["kt"] = c.off, c.cout, c.cin_p, c.cin, c.kt
+            d["blk_plain"], d["blk_t"] = nplain, ntrans
+            nplain += c.cout
+            n_img = G * c.cout * c.kt * c.cin_p
+            d["wp_off"] = off
+            vp = (off, (G, c.cout, c.kt, c.cin_p))
+            off += n_img
+            vt = None
+            if train and c.need_dgrad:
+                d["wt_off"] = off
+                vt = (off, (G, c.cin_p, c.kt, c.cout))
+                off += n_img
+                ntrans += ((c.cin_p + 63) // 64) * ((c.cout + 63) // 64) * c.kt
+            else:
+                d["wt_off"] = -1
+            d["slot"][:c.kt] = c.slots
+            views.append((vp, vt))
+        lds = max(c.kt * c.cin * 4 for c in self.convs)
+        buf = torch.empty(max(1, off), dtype=torch.bfloat16, device=self.device)
+        tab = torch.from_numpy(desc.view(np.uint8).copy()).to(self.device)
+        plan = (tab, nplain, ntrans, lds, buf, views)
+        self._plans[key] = plan
+        return plan
+
+    def pack(self, theta, G, train, key=None):
+        """Pack every layer for this step and hand each conv its views (``conv.wp`` / ``conv.wt``)."""
+        tab, nplain, ntrans, lds, buf, views = self._plan(G, train, key)
+        ops.ext().pack_convs(tab.data_ptr(), len(self.convs), nplain, ntrans, lds, theta.data_ptr(), theta.stride(0),
+                             G, buf.data_ptr(), _stream())
+        for c, (vp, vt) in zip(self.convs, views):
+            c.wp = (buf[vp[0]:vp[0] + int(np.prod(vp[1]))].view(vp[1]), G, theta.data_ptr())
+            c.wt = (buf[vt[0]:vt[0] + int(np.prod(vt[1]))].view(vt[1]), G, theta.data_ptr()) if vt else None
+
+    def pack_into(self, theta, G, wp, wt):
+        """Single-layer packing into caller-provided tensors (tests, standalone layers)."""
+        tab, nplain, ntrans, lds, buf, views = self._plan(G, wt is not None, key=("one", G, wt is not None))
+        ops.ext().pack_convs(tab.data_ptr(), 1, nplain, ntrans, lds, theta.data_ptr(), theta.stride(0), G,
+                             buf.data_ptr(), _stream())
+        (vp, vt), = views
+        wp.copy_(buf[vp[0]:vp[0] + wp.numel()].view(wp.shape))
+        if wt is not None:
+            wt.copy_(buf[vt[0]:vt[0] + wt.numel()].view(wt.shape))
 
 
 class GroupNormG:
@@ -237,9 +398,12 @@ class GroupNormG:
 
 
 class GroupedResNet18GN:
-    """The forward/backward graph of ``customized_resnet18`` for G clients at once (see module docstring)."""
+    """The forward/backward graph of ``customized_resnet18`` (32x32 CIFAR, avg_pool2d(4) over the final 4x4 map) and
+    ``tiny_resnet18`` (64x64 Tiny-ImageNet, AdaptiveAvgPool2d over the final 8x8 map) for G clients at once — the two
+    share every parameter and differ only in input size and pooling window, which is the whole final map in both
+    (see module docstring).  ``mean``/``std``: the dataset's Normalize constants."""
 
-    def __init__(self, players: ParamLayout, device, hip=None):
+    def __init__(self, players: ParamLayout, device, hip=None, mean=CIFAR_MEAN, std=CIFAR_STD):
         self.device = torch.device(device)
         self.hip = (self.device.type == "cuda") if hip is None else hip
         self.act = torch.bfloat16 if self.hip else torch.float32
@@ -269,16 +433,40 @@ class GroupedResNet18GN:
                 self.blocks.append(blk)
         self.lw_off, self.lb_off = off["linear.weight"], off["linear.bias"]
         self.ncls, self.feat = shp["linear.weight"]
-        mean = torch.tensor(CIFAR_MEAN, dtype=torch.float32).view(1, 1, 1, 3)
-        std = torch.tensor(CIFAR_STD, dtype=torch.float32).view(1, 1, 1, 3)
-        self.norm_scale = (1.0 / (255.0 * std)).to(self.device)
-        self.norm_shift = (-mean / std).to(self.device)
+        self.mean, self.std = tuple(float(v) for v in mean), tuple(float(v) for v in std)
+        m_ = torch.tensor(self.mean, dtype=torch.float32).view(1, 1, 1, 3)
+        s_ = torch.tensor(self.std, dtype=torch.float32).view(1, 1, 1, 3)
+        self.norm_scale = (1.0 / (255.0 * s_)).to(self.device)
+        self.norm_shift = (-m_ / s_).to(self.device)
+        convs = [self.stem] + [b[k] for b in self.blocks for k in ("c1", "c2", "cs") if k in b]
+        self.packer = WeightPacker(convs, self.device) if self.hip else None
 
     # ------------------------------------------------------------------ input
-    def input(self, x8):
-        """uint8 [N, 32, 32, 3] -> normalised activation [N, 32, 32, cin_p] (channels zero-padded)."""
-        x = x8.float() * self.norm_scale + self.norm_shift
+    def input(self, x8, idx, aug=None):
+        """Gather + (train-time augmentation) + normalise + channel-pad the uint8 HWC images ``x8[idx]`` into the
+        stem's activation [N, H, W, cin_p].  ``aug`` = (seed_dev, seed_base, cids_dev, cids, B) or None; the HIP path
+        is one fused kernel (``img.hip``), the CPU twin draws the same crops/flips (:func:`aug_draws`)."""
+        N = idx.numel()
+        H, W = int(x8.shape[1]), int(x8.shape[2])
         cp = self.stem.cin_p
+        if self.hip:
+            out = torch.empty(N, H, W, cp, device=self.device, dtype=torch.bfloat16)
+            idx32 = idx if idx.dtype == torch.int32 else idx.int()
+            if aug is not None:
+                seed_dev, seed_base, cids_dev, _, B = aug
+                ops.ext().img_input(x8.data_ptr(), idx32.data_ptr(), out.data_ptr(), N, H, W, cp, *self.mean,
+                                    *self.std, 1, AUG_PAD, seed_dev.data_ptr(), int(seed_base), cids_dev.data_ptr(),
+                                    B, _stream())
+            else:
+                ops.ext().img_input(x8.data_ptr(), idx32.data_ptr(), out.data_ptr(), N, H, W, cp, *self.mean,
+                                    *self.std, 0, AUG_PAD, 0, 0, 0, 1, _stream())
+            return out
+        img = x8.index_select(0, idx.long().to(x8.device))
+        if aug is not None:
+            seed_dev, seed_base, _, cids, B = aug
+            oy, ox, fl = aug_draws(int(seed_base) + int(seed_dev.reshape(-1)[0]), cids, B)
+            img = augment_u8(img, oy, ox, fl)
+        x = img.float() * self.norm_scale.to(img.device) + self.norm_shift.to(img.device)
         if cp != 3:
             x = F.pad(x, (0, cp - 3))
         return x.to(self.act).contiguous()
@@ -286,27 +474,30 @@ class GroupedResNet18GN:
     # ------------------------------------------------------------------ forward
     def forward(self, x, theta, G, train=False):
         saved = []
-        t = self.stem.fwd(x, theta, G, train)
+        packed = self.packer is not None
+        if packed:
+            self.packer.pack(theta, G, train, key=(G, x.shape[0] // G, train))
+        t = self.stem.fwd(x, theta, G, train, packed)
         a, st = self.stem_gn.fwd(t, theta, G, relu=True)
         saved.append((x, t, st, a))
         for blk in self.blocks:
             xin = a
-            t1 = blk["c1"].fwd(xin, theta, G, train)
+            t1 = blk["c1"].fwd(xin, theta, G, train, packed)
             h1, s1 = blk["n1"].fwd(t1, theta, G, relu=True)
-            t2 = blk["c2"].fwd(h1, theta, G, train)
+            t2 = blk["c2"].fwd(h1, theta, G, train, packed)
             if "cs" in blk:
-                ts = blk["cs"].fwd(xin, theta, G, train)
+                ts = blk["cs"].fwd(xin, theta, G, train, packed)
                 ysc, ss = blk["ns"].fwd(ts, theta, G)
             else:
                 ts, ss, ysc = None, None, xin
             a, s2 = blk["n2"].fwd(t2, theta, G, res=ysc, relu=True)
             saved.append((xin, t1, s1, h1, t2, s2, ts, ss, a))
         N, H, W, C = a.shape
-        pooled = a.float().view(N, H * W, C).mean(1)  # avg_pool2d(4) on the 4x4 map
+        pooled = a.float().view(N, H * W, C).mean(1)  # avg_pool2d(4) on 4x4 (CIFAR) / adaptive 1x1 on 8x8 (Tiny)
         B = N // G
         lw = theta[:, self.lw_off:self.lw_off + self.ncls * self.feat].view(G, self.ncls, self.feat)
         lb = theta[:, self.lb_off:self.lb_off + self.ncls]
-        # the 512 -> 10 head as broadcast multiply-reduce, not bmm: BLAS calls keep library workspaces that a
+        # the 512 -> K head as broadcast multiply-reduce, not bmm: BLAS calls keep library workspaces that a
         # replayed hipGraph would share with eager work
         logits = (pooled.view(G, B, 1, C) * lw.view(G, 1, self.ncls, C)).sum(-1) + lb.view(G, 1, self.ncls)
         return logits.view(N, self.ncls), pooled, saved
@@ -338,12 +529,20 @@ class GroupedResNet18GN:
             if "cs" in blk:
                 dts = blk["ns"].bwd(da, a, ts, ss, theta, grads, G)
                 dx2 = blk["cs"].bwd(dts, xin, theta, grads, G, True)
+            half = dx2 is not None and blk["cs"].stride == 2  # 1x1 stride-2 projection: even-pixel gradient
             if self.hip:
                 out = torch.empty(dx1.shape, device=dx1.device, dtype=torch.float32)
-                ops.ext().res_grad(out.data_ptr(), dx1.data_ptr(), dx2.data_ptr() if dx2 is not None else 0,
-                                   0 if dx2 is not None else da.data_ptr(), 0 if dx2 is not None else a.data_ptr(),
-                                   out.numel(), _stream())
+                if half:
+                    Nn, Hh, Ww, Cc = dx1.shape
+                    ops.ext().res_grad_s2(out.data_ptr(), dx1.data_ptr(), dx2.data_ptr(), Nn, Hh, Ww, Cc, _stream())
+                else:
+                    ops.ext().res_grad(out.data_ptr(), dx1.data_ptr(), dx2.data_ptr() if dx2 is not None else 0,
+                                       0 if dx2 is not None else da.data_ptr(),
+                                       0 if dx2 is not None else a.data_ptr(), out.numel(), _stream())
                 da = out
+            elif half:
+                da = dx1.float().clone()
+                da[:, ::2, ::2] += dx2.float()
             else:
                 da = dx1.float() + (dx2.float() if dx2 is not None else da * (a > 0))
         x0, t0, st0, a0 = saved[0]
@@ -358,33 +557,50 @@ class GroupedResNet18GN:
 
 class ResNetHipEngine:
     """Engine API of :class:`~.executor.HipEngine` (train_step / eval_logits / local_opt / saliency_acc) for the
-    client-batched ResNet-18-GN on CIFAR-shape uint8 images ``[N, 32, 32, 3]``."""
+    client-batched ResNet-18-GN on uint8 HWC images: CIFAR-10/100 ``[N, 32, 32, 3]`` (``customized_resnet18``) or
+    Tiny-ImageNet ``[N, 64, 64, 3]`` (``tiny_resnet18``).  ``augment``: the reference's train-time RandomCrop(pad 4)
+    + RandomHorizontalFlip, drawn on device per (step, client, sample) and fused into the input stage."""
+    sample_fields = ("x8", "labels")
 
-    def __init__(self, template_model, images_u8, labels, device, hip=None):
+    def __init__(self, template_model, images_u8, labels, device, hip=None, mean=None, std=None, augment=True):
         self.device = torch.device(device)
         self.players = ParamLayout.from_tensors(list(template_model.named_parameters()))
         self.blayers = ParamLayout.from_tensors(list(template_model.named_buffers()))
         assert self.blayers.total == 0, "GroupNorm ResNet carries no buffers"
-        self.net = GroupedResNet18GN(self.players, self.device, hip=hip)
+        hw = int(images_u8.shape[1])
+        if mean is None:
+            mean, std = (TINY_MEAN, TINY_STD) if hw == 64 else (CIFAR_MEAN, CIFAR_STD)
+        self.net = GroupedResNet18GN(self.players, self.device, hip=hip, mean=mean, std=std)
         self.x8 = images_u8.to(self.device)
         self.labels = labels.to(self.device)
+        self.augment = bool(augment)
         if self.net.hip:
             ops.ext()  # fail loudly on a GPU box without the extension
         self.supports_graphs = self.device.type == "cuda"
         self.graph_cache_limit = 24  # each captured step holds its own activation pool
         self._opt = None
+        self._cid_cache = {}
 
-    def _batch(self, idx):
-        ix = idx.long()
-        return self.net.input(self.x8.index_select(0, ix)), self.labels.index_select(0, ix)
+    def _cids_dev(self, cids):
+        key = tuple(int(c) for c in cids)
+        ct = self._cid_cache.get(key)
+        if ct is None:  # one upload per client group (in the eager first step of a shape, before any capture)
+            ct = torch.tensor(key, dtype=torch.int32, device=self.device)
+            self._cid_cache[key] = ct
+        return ct
 
     def train_step(self, theta, bufs, grads, idx, G, B, keep, seed, cids=None, seed_dev=None, bn_train=True):
-        x, y = self._batch(idx)
+        aug = None
+        if self.augment and seed_dev is not None:
+            cids = list(range(G)) if cids is None else [int(c) for c in cids]
+            aug = (seed_dev, int(seed), self._cids_dev(cids), cids, B)
+        x = self.net.input(self.x8, idx, aug)
+        y = self.labels.index_select(0, idx.long())
         return self.net.train_step(theta, grads, x, y, G, B)
 
     def eval_logits(self, theta, bufs, idx, G, B):
         with torch.no_grad():
-            x, _ = self._batch(idx)
+            x = self.net.input(self.x8, idx)
             return self.net.eval_logits(theta, x, G).float()
 
     def _delegate(self):

@@ -374,6 +374,7 @@ class GroupedResNet3D:
 class ResNet3DHipEngine:
     """Engine API (train_step / eval_logits / local_opt / saliency_acc) of the client-batched 3D ResNet on uint8
     ABCD-shape volumes ``[N, D, H, W]`` (labels {0, 1}, BCE head with one logit)."""
+    sample_fields = ("x8", "labels")
 
     supports_graphs = False  # the stem segment allocates autograd state; launches here are few and large
 

@@ -171,22 +171,10 @@ class FLRunner:
     def _stratified_batch(self, c, it, B):
         """A label-stratified mini-batch of client c (IterSNIP ``--stratified_sampling``): per class
         round(B * n_class / n) samples (largest remainders), drawn without replacement."""
+        from ..algorithms.snip import stratified_batch, stratified_rng
         tr = self.splits[c].train
         y = self.e.labels.index_select(0, torch.as_tensor(tr, dtype=torch.long).to(self.e.labels.device))
-        y = y.cpu().numpy()
-        rs = self._rng(-7, c, it)
-        B = min(B, len(tr))
-        cls, cnt = np.unique(y, return_counts=True)
-        q = B * cnt / cnt.sum()
-        take = np.floor(q).astype(int)
-        for i in np.argsort(-(q - take), kind="stable")[:B - take.sum()]:
-            take[i] += 1
-        out = []
-        for k, n in zip(cls, take):
-            pool = tr[y == k]
-            out.append(pool[rs.permutation(len(pool))[:n]])
-        b = np.concatenate(out)
-        return b[rs.permutation(len(b))]
+        return stratified_batch(tr, y.cpu().numpy(), B, stratified_rng(self.cfg.seed, c, it))
 
     # ---------------------------------------------------------------------------------------------- planning
     def _plan(self, clients, chunks_of):
@@ -528,6 +516,7 @@ class FLRunner:
         needs = [[c for c in moving if new_owner[c] == r] for r in range(self.info.world)]
         new_local = sorted((c for c in range(self.N) if new_owner[c] == me), key=lambda c: (-int(self.sizes[c]), c))
         n = max(1, len(new_local))
+        self._migrate_samples(needs, new_local)
         new_state = {}
         for path, t in self._row_state():
             width = t.shape[1]
@@ -558,6 +547,50 @@ class FLRunner:
         self.grads = padded_rows(n, self.P, self.device)
         self.mom_buf = padded_rows(n, self.P, self.device) if self.cfg.momentum != 0 else None
         self._after_migrate()
+
+    def _sample_rows(self, c):
+        """Store rows of client c's samples in a fixed order: train, test, then validation."""
+        sp = self.splits[c]
+        parts = [sp.train, sp.test] + ([sp.val] if sp.val is not None else [])
+        return np.concatenate([np.asarray(p, dtype=np.int64) for p in parts])
+
+    def _migrate_samples(self, needs, new_local):
+        """Move the per-sample store rows (``engine.sample_fields``: volumes, moments, labels) of migrating clients
+        with their state, point to point, and rebuild each rank's store to hold exactly its clients' samples (the
+        data is sharded like the clients, never replicated).  Splits are re-based in the same order, so a client
+        draws the same batches wherever it trains."""
+        fields = getattr(self.e, "sample_fields", None)
+        if not fields:
+            return
+        from .executor import ClientSplit
+        rows = {c: self._sample_rows(c) for c in self.local}
+        ns = {c: len(self.splits[c].train) + len(self.splits[c].test) +
+              (0 if self.splits[c].val is None else len(self.splits[c].val)) for c in range(self.N)}
+        for f in fields:
+            F = getattr(self.e, f)
+            rest = tuple(F.shape[1:])
+            re_ = int(np.prod(rest)) if rest else 1
+            recv = rt.exchange_rows(self.info, self.owner, needs,
+                                    lambda c, F=F: F.index_select(0, torch.as_tensor(rows[c], device=F.device)).reshape(-1),
+                                    lambda c, re_=re_: ns[c] * re_, F.device, F.dtype)
+            parts = [F.index_select(0, torch.as_tensor(rows[c], device=F.device)) if c in rows
+                     else recv[c].view((ns[c],) + rest) for c in new_local]
+            setattr(self.e, f, torch.cat(parts) if parts else F[:0].clone())
+            del F, parts, recv
+        splits, off = list(self.splits), 0
+        for c in range(self.N):
+            sp = self.splits[c]
+            ntr, nte = len(sp.train), len(sp.test)
+            nva = None if sp.val is None else len(sp.val)
+            splits[c] = ClientSplit(np.zeros(ntr, np.int64), np.zeros(nte, np.int64),
+                                    None if nva is None else np.zeros(nva, np.int64))
+        for c in new_local:
+            sp = splits[c]
+            ntr, nte, nva = len(sp.train), len(sp.test), 0 if sp.val is None else len(sp.val)
+            splits[c] = ClientSplit(np.arange(off, off + ntr), np.arange(off + ntr, off + ntr + nte),
+                                    None if sp.val is None else np.arange(off + ntr + nte, off + ntr + nte + nva))
+            off += ntr + nte + nva
+        self.splits = splits
 
     def _after_migrate(self):
         self._graphs = {}
@@ -600,36 +633,52 @@ class FLRunner:
             return self.aggregate_topk(sampled)
         return self.aggregate_fedavg(sampled)
 
+    def _topk_space(self):
+        """One selection segment spanning the whole parameter row (the segmented radix select of ``sparse.hip``
+        then picks a per-row top-k)."""
+        if getattr(self, "_tk_space", None) is None:
+            from types import SimpleNamespace
+            lay = SimpleNamespace(names=["all"], offsets=[0], total=self.P, numel=lambda i: self.P)
+            self._tk_space = MK.MaskSpace(lay)
+        return self._tk_space
+
     def aggregate_topk(self, sampled):
         """Sparse-update FedAvg: client i contributes n_i/N * topk(theta_i - w_global) (fixed k per client, so
-        the all-gather needs no padding), BN buffers are averaged densely.  Every rank applies the same
-        gathered (index, value) lists in global client order, so all ranks end with the same model."""
+        every rank knows every rank's payload size), BN buffers are averaged densely.
+
+        * selection: the segmented radix select (``MaskSpace.select`` REGROW_ABS over one row-wide segment, exact
+          k with deterministic ties) on chunks of rows, instead of ``torch.topk``;
+        * exchange: ONE all-gather of [client id | k values | k indices (int32 bits)] rows with sizes known on
+          every rank (no size exchange, no host sync);
+        * combine: every rank orders the gathered lists by client id and reduces duplicates with a sort-based
+          coalesce (sequential per-index sums in client order, no atomics), so all ranks get identical fp32 sums."""
         n_tot = float(sum(self.sizes[c] for c in sampled))
         k = max(1, int(math.ceil(self.cfg.update_topk * self.P)))
         rows, loc = self._local_rows(sampled)
-        vals = torch.zeros((len(rows), k), dtype=torch.float32, device=self.device)
-        idx = torch.zeros((len(rows), k), dtype=torch.int32, device=self.device)
-        # batched top-k over chunks of rows (one selection launch per chunk instead of per client; chunks bound the
-        # [rows, P] temporaries: 8 x 46 M fp32 = 1.5 GB for the 3D ResNet-50)
+        rec = torch.zeros((len(rows), 1 + 2 * k), dtype=torch.float32, device=self.device)
+        space = self._topk_space()
+        # chunks bound the [rows, P] temporaries: 8 x 46 M fp32 = 1.5 GB for the 3D ResNet-50
         chunk = max(1, min(len(rows), int(2e9 // (4 * max(1, self.P)))))
         for j0 in range(0, len(rows), chunk):
             rr = rows[j0:j0 + chunk]
             ix = torch.tensor(rr, device=self.device)
-            d = self.theta.index_select(0, ix)[:, :self.P] - self.w_global
-            top = torch.topk(d.abs(), k, dim=1, sorted=False).indices
+            d = padded_rows(len(rr), self.P, self.device)
+            torch.sub(self.theta.index_select(0, ix)[:, :self.P], self.w_global, out=d)
+            bits = torch.zeros((len(rr), self.W), dtype=torch.int32, device=self.device)
+            space.select(MK.REGROW_ABS, d, bits, torch.full((len(rr), 1), k, dtype=torch.int64))
+            top = MK.unpack_bits(bits, self.P, torch.bool).nonzero()[:, 1].view(len(rr), k)  # exactly k per row
             wts = torch.tensor([self.sizes[self.local[r]] / n_tot for r in rr], dtype=torch.float32,
                                device=self.device)
-            idx[j0:j0 + len(rr)] = top.int()
-            vals[j0:j0 + len(rr)] = d.gather(1, top) * wts[:, None]
-        cid = torch.tensor(loc, dtype=torch.float32, device=self.device)
-        g_vals = rt.all_gather_cat(vals.view(-1), self.info).view(-1, k)
-        g_idx = rt.all_gather_cat(idx.view(-1), self.info).view(-1, k).long()
-        g_cid = rt.all_gather_cat(cid, self.info)
-        order = torch.argsort(g_cid)
-        upd = torch.zeros(self.P, dtype=torch.float32, device=self.device)
-        for j in order.tolist():  # fixed order: identical fp32 sums on every rank
-            upd.index_add_(0, g_idx[j], g_vals[j])
-        self.w_global.add_(upd)
+            rec[j0:j0 + len(rr), 0] = torch.tensor([self.local[r] for r in rr], dtype=torch.float32,
+                                                   device=self.device)
+            rec[j0:j0 + len(rr), 1:1 + k] = d.gather(1, top) * wts[:, None]
+            rec[j0:j0 + len(rr), 1 + k:] = top.to(torch.int32).view(torch.float32)
+        per_rank = [sum(1 for c in sampled if self.owner[c] == r) * (1 + 2 * k) for r in range(self.info.world)]
+        g = rt.all_gather_sized(rec.view(-1), per_rank, self.info).view(-1, 1 + 2 * k)
+        g = g.index_select(0, torch.argsort(g[:, 0]))  # fixed client order on every rank
+        g_idx = g[:, 1 + k:].contiguous().view(torch.int32).to(torch.int64).reshape(1, -1)
+        upd = torch.sparse_coo_tensor(g_idx, g[:, 1:1 + k].reshape(-1), (self.P,)).coalesce()
+        self.w_global.index_add_(0, upd.indices()[0], upd.values())
         bsum = torch.zeros(self.Q, dtype=torch.float32, device=self.device)
         for r in rows:
             bsum.add_(self.bufs[r, :self.Q], alpha=self.sizes[self.local[r]] / n_tot)

@@ -122,13 +122,27 @@ def all_gather_cat(t: torch.Tensor, info: DistInfo):
     return torch.cat([b[:s] for b, s in zip(bufs, sizes)])
 
 
+def all_gather_sized(t: torch.Tensor, sizes, info: DistInfo):
+    """All-gather 1-D tensors whose per-rank lengths ``sizes`` every rank already knows (e.g. k values per sampled
+    client of each rank): one padded all-gather, no size exchange and no host sync."""
+    if not info.enabled:
+        return t
+    m = max(int(s) for s in sizes)
+    pad = torch.zeros(max(1, m), device=t.device, dtype=t.dtype)
+    pad[:t.numel()] = t.view(-1)
+    bufs = [torch.empty_like(pad) for _ in range(info.world)]
+    dist.all_gather(bufs, pad)
+    return torch.cat([b[:int(s)] for b, s in zip(bufs, sizes)])
+
+
 def exchange_rows(info: DistInfo, owner, needs, row_of, width, device, dtype=torch.float32):
     """Point-to-point fetch of client rows (gossip neighbours, FedFomo candidates) — RCCL send/recv over xGMI
     instead of an all-gather of every client.
 
     ``owner[c]``: rank holding client c; ``needs[r]``: clients rank r needs (every rank passes the same ``needs``,
     so both sides of each transfer agree on the schedule); ``row_of(c)`` -> 1-D tensor [width] of a client this rank
-    owns.  Returns {c: tensor [width]} for this rank's remote needs.  All transfers go out as one batched group."""
+    owns; ``width``: an int, or a function of the client (variable-length payloads, e.g. a client's sample rows).
+    Returns {c: tensor [width]} for this rank's remote needs.  All transfers go out as one batched group."""
     if not info.enabled:
         return {}
     import torch.distributed as dist
@@ -145,7 +159,8 @@ def exchange_rows(info: DistInfo, owner, needs, row_of, width, device, dtype=tor
                 t = row_of(c).contiguous()
                 p2p.append(dist.P2POp(dist.isend, t.cpu() if stage else t, r))
             if r == info.rank:
-                buf = torch.empty(width, dtype=dtype, device="cpu" if stage else device)
+                w = width(c) if callable(width) else width
+                buf = torch.empty(w, dtype=dtype, device="cpu" if stage else device)
                 recv[c] = buf
                 p2p.append(dist.P2POp(dist.irecv, buf, o))
     if p2p:

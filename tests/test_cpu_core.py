@@ -192,6 +192,14 @@ def test_mpc_bgw_lcc_additive():
             coef = num * pow(den, p - 2, p) % p
             want = (want + coef * blocks[k]) % p
         assert np.array_equal(enc[j], want), j
+    # odd K: the reference-compatible decoder's targets differ from the encoder's points (it warns); the matching
+    # decoder recovers the blocks for any K, T
+    X3 = rs.randint(0, 1000, size=(3, 4))
+    enc = TA.LCC_encoding(X3, N=7, K=3, T=1, p=p, rng=rs)
+    with pytest.warns(UserWarning):
+        TA.LCC_decoding(enc, 1, 7, 3, 1, list(range(7)), p)
+    dec = TA.LCC_decode_blocks(enc[[6, 1, 4, 0]], 1, 7, 3, 1, [6, 1, 4, 0], p)  # any K + T workers
+    assert np.array_equal(np.concatenate(list(dec), 0), X3 % p)
     ss = TA.Gen_Additive_SS(7, 4, p, rs)
     assert np.all(ss.sum(0) % p == 0)
     assert TA.modular_inv(3, p) * 3 % p == 1

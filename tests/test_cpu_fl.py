@@ -130,7 +130,7 @@ def _dist_worker(rank, world, port, out, cfg_kw=None):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("cfg_kw", [{}, {"aggregator": "median"}, {"update_topk": 0.1}, {"heartbeat_s": 0.05}])
+@pytest.mark.parametrize("cfg_kw", [{}, {"aggregator": "median"}, {"update_topk": 0.1}, {"heartbeat_s": 0.5}])
 def test_two_rank_gloo_matches_single_process(tmp_path, cfg_kw):
     """2 ranks (clients sharded, mask-compacted all-reduce / all-gathered robust aggregation) == 1 process."""
     import socket
@@ -208,3 +208,68 @@ def test_cli_entry_points_run_end_to_end(algo, tmp_path):
     assert out is not None
     logs = list((tmp_path / "cifar10").glob("*.log"))
     assert len(logs) == 1 and logs[0].stat().st_size > 0
+
+
+class Tiny3DNoDrop(nn.Module):
+    """Tiny 3D CNN without dropout (SNIP scores of the two paths are then deterministic functions of the batch)."""
+
+    def __init__(self):
+        super().__init__()
+        self.features = nn.Sequential(nn.Conv3d(1, 4, 3, 2), nn.BatchNorm3d(4), nn.ReLU(), nn.Conv3d(4, 8, 3))
+        self.classifier = nn.Linear(8, 1)
+
+    def forward(self, x):
+        return self.classifier(self.features(x).amax((2, 3, 4)))
+
+
+def test_stratified_itersnip_eager_and_runner_select_the_same_mask():
+    """--stratified_sampling --itersnip_iteration 3: the reference-semantics SailentGradsAPI and the client-batched
+    FLRunner draw the same label-stratified batches (snip.stratified_batch, RNG keyed by (seed, client, iter)) and
+    select the same global SNIP mask; a stratified batch holds each class in proportion (largest remainders)."""
+    from neuroimagedisttraining_amd.algorithms import snip as S
+    from neuroimagedisttraining_amd.algorithms.salientgrads import SailentGradsAPI
+    from neuroimagedisttraining_amd.data.abcd import _assemble
+    from neuroimagedisttraining_amd.data.volumes import VolumeStore
+    from neuroimagedisttraining_amd.engine.executor import ClientSplit, FLConfig, FLRunner, TorchEngine
+    from neuroimagedisttraining_amd.parallel import runtime as rt
+    g = torch.Generator().manual_seed(11)
+    clients, n_tr, n_te, B = 3, 20, 5, 8
+    N = clients * (n_tr + n_te)
+    vols = torch.randint(0, 256, (N, 13, 13, 13), dtype=torch.uint8, generator=g)
+    labels = (torch.rand(N, generator=g) < 0.3).float()
+    train = {c: np.arange(c * 25, c * 25 + n_tr) for c in range(clients)}
+    test = {c: np.arange(c * 25 + n_tr, c * 25 + 25) for c in range(clients)}
+    # the stratified draw itself: class counts proportional to the client's label histogram
+    y0 = labels[train[0]].numpy()
+    b = S.stratified_batch(train[0], y0, B, S.stratified_rng(5, 0, 0))
+    assert len(set(b.tolist())) == B and set(b.tolist()) <= set(train[0].tolist())
+    want = B * np.bincount(y0.astype(int), minlength=2) / len(y0)
+    got = np.bincount(labels[b].numpy().astype(int), minlength=2)
+    assert np.all(np.abs(got - want) < 1.0)
+
+    torch.manual_seed(3)
+    model = Tiny3DNoDrop()
+    store = VolumeStore(vols, labels, torch.zeros(N))
+    ds = _assemble(store, train, test, B, seed=5)
+    args = _args(client_num_in_total=clients, client_num_per_round=clients, batch_size=B, itersnip_iteration=3,
+                 stratified_sampling=True, seed=5)
+    import copy
+    api = SailentGradsAPI(ds, torch.device("cpu"), args, VolumeTrainer(copy.deepcopy(model), args))
+    eager = api.generate_global_mask_snip()
+
+    splits = [ClientSplit(train[c], test[c]) for c in range(clients)]
+    eng = TorchEngine(copy.deepcopy(model), vols, labels, "cpu")
+    info = rt.DistInfo(0, 1, 0, torch.device("cpu"), "none")
+    cfg = FLConfig(comm_round=1, epochs=1, batch_size=B, dense_ratio=0.5, seed=5, itersnip_iteration=3,
+                   stratified_sampling=True)
+    r = FLRunner(eng, splits, cfg, info, copy.deepcopy(model))
+    flat = r.generate_global_mask_snip()
+    pl = eng.players
+    n_diff = n_tot = 0
+    for i, name in enumerate(pl.names):
+        m = flat[pl.offsets[i]:pl.offsets[i] + pl.numel(i)].view(pl.shapes[i])
+        n_diff += int((m != eager[name]).sum())
+        n_tot += m.numel()
+    # identical batches and scores; only fp32 summation order differs (a borderline tie may flip)
+    print("mask mismatches", n_diff, "of", n_tot)
+    assert n_diff <= max(1, n_tot // 1000), (n_diff, n_tot)

@@ -155,11 +155,30 @@ def _worker(rank, world, port, out, algo, kw, ckpt=None):
             r.generate_global_mask_snip()
         r.run_round(0)
         ck.save_runner(r, ckpt[0], 1)
+    elif ckpt[1] == "save_async":  # background-written saves after rounds 0 and 1, keep only the newest
+        if r.alg == "salientgrads":
+            r.generate_global_mask_snip()
+        saver = ck.Checkpointer(ckpt[0], r.info, every=1, keep_last=1, async_write=True)
+        for k in range(2):
+            r.run_round(k)
+            saver.maybe_save(r, k + 1)
+        saver.close()
     else:
-        start = ck.load_runner(r, ckpt[0])
+        loaded = []
+        real_load = torch.load
+
+        def spy(path, *a, **k):
+            loaded.append(os.path.basename(str(path)))
+            return real_load(path, *a, **k)
+        torch.load = spy
+        try:
+            start = ck.load_runner(r, ckpt[0])
+        finally:
+            torch.load = real_load
         for k in range(start, 2):
             r.run_round(k)
         r.finish()
+        torch.save({"loaded": loaded, "local": list(r.local)}, out + ".loaded.%d" % rank)
     torch.save(_collect(r), out + ".%d" % rank)
     dist.destroy_process_group()
 
@@ -235,6 +254,30 @@ def test_checkpoint_from_four_ranks_resumes_on_two_exactly(algo, tmp_path):
     _same(got, _collect(r), len(SIZES), algo)
 
 
+def test_async_indexed_checkpoint_four_ranks_resumes_on_two(tmp_path):
+    """Background-written saves (pinned snapshot, writer thread, lagged barrier + ``latest`` commit) with
+    keep_last=1 on 4 ranks; stale shards of a larger crashed run in the round directory; resume on 2 ranks:
+    each rank opens only the shards its clients live in (client index), and the state equals 2 rounds in one
+    process."""
+    d = tmp_path / "ck"
+    _spawn(4, str(tmp_path / "a"), "dispfl", {}, ckpt=(str(d), "save_async"))
+    assert sorted(p.name for p in d.iterdir()) == ["latest", "round_2"]  # round_1 pruned
+    assert (d / "latest").read_text() == "2"
+    # a crashed 8-rank run left shards 4..7 of its own round 2 behind: never read (index names shards 0..3)
+    for k in range(4, 8):
+        torch.save({"junk": torch.zeros(1)}, d / "round_2" / ("clients_rank%d.pt" % k))
+    got = _spawn(2, str(tmp_path / "b"), "dispfl", {}, ckpt=(str(d), "resume"))
+    g = torch.load(d / "round_2" / "global.pt", weights_only=True)
+    index = g["index"].tolist()
+    for rk in range(2):
+        rec = torch.load(str(tmp_path / "b") + ".loaded.%d" % rk, weights_only=True)
+        shards = sorted(n for n in rec["loaded"] if n.startswith("clients_rank"))
+        assert shards == sorted({"clients_rank%d.pt" % index[c] for c in rec["local"]}), (rk, shards)
+    r = _runner("dispfl")
+    _drive(r, 2)
+    _same(got, _collect(r), len(SIZES), "dispfl")
+
+
 def test_dispfl_masks_keep_density_and_masked_weights_zero():
     from neuroimagedisttraining_amd.engine import masks as MK
     r = _runner("dispfl", rounds=3)
@@ -273,6 +316,68 @@ def test_rebalanced_multirank_matches_single_process(algo, world, kw, tmp_path):
     _drive(r, 2)
     # fp32 partial sums are all-reduced from different per-rank groupings: w_global agrees to ~1e-7, rows to ~2e-5
     _same(got, _collect(r), len(kw.get("sizes", SIZES)), algo, atol=5e-5)
+
+
+def _worker_sharded(rank, world, port, out, algo, kw):
+    """A rank that holds ONLY its shard's samples (placeholder splits for the other clients), as bench.py and the
+    CLI load them: rebalancing must move sample rows with the migrating clients."""
+    import torch.distributed as dist
+    from neuroimagedisttraining_amd.engine.executor import ClientSplit
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    r = _runner(algo, rank, world, **kw)
+    full = r.e.store
+    mine = [c for c in range(r.N) if r.owner[c] == rank]
+    rows = np.concatenate([r._sample_rows(c) for c in mine])
+    r.e.store = full[torch.as_tensor(rows)].clone()
+    r.e.labels = r.e.labels[torch.as_tensor(rows)].clone()
+    splits, off = [], 0
+    for c, sp in enumerate(r.splits):
+        ntr, nte, nva = len(sp.train), len(sp.test), 0 if sp.val is None else len(sp.val)
+        if c in mine:
+            splits.append(ClientSplit(np.arange(off, off + ntr), np.arange(off + ntr, off + ntr + nte),
+                                      None if sp.val is None else np.arange(off + ntr + nte, off + ntr + nte + nva)))
+            off += ntr + nte + nva
+        else:
+            splits.append(ClientSplit(np.zeros(ntr, np.int64), np.zeros(nte, np.int64),
+                                      None if sp.val is None else np.zeros(nva, np.int64)))
+    r.splits = splits
+    held = [len(r.e.store)]
+    _drive(r, 2)
+    held.append(len(r.e.store))
+    d = _collect(r)
+    d["held"] = held
+    torch.save(d, out + ".%d" % rank)
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("algo,world,kw", [
+    ("fedavg", 4, {"sizes": [6 + (c % 5) * 2 for c in range(40)], "frac": 0.25, "epochs": 1}),
+    ("fedfomo", 4, {"sizes": [6 + (c % 5) * 2 for c in range(16)], "frac": 0.5})])
+def test_rebalancing_moves_samples_with_clients_on_sharded_stores(algo, world, kw, tmp_path):
+    """4 gloo ranks, each holding only its own clients' samples: sampling-aware rebalancing migrates the sampled
+    clients' sample rows (volumes + labels, train/test/val) with their state; every rank's store stays the size of
+    its current clients (no replicated cohort) and the models equal the 1-process run."""
+    import torch.multiprocessing as mp
+    kw = dict(kw, rebalance=True)
+    out = str(tmp_path / "r")
+    mp.start_processes(_worker_sharded, args=(world, _port(), out, algo, kw), nprocs=world, join=True,
+                       start_method="spawn")
+    got = {"rows": {}, "bits": {}, "pers": {}}
+    total = 0
+    for rk in range(world):
+        d = torch.load(out + ".%d" % rk, weights_only=True)
+        for key in ("rows", "bits", "pers"):
+            got[key].update(d[key])
+        if rk == 0:
+            got["w"], got["stats"] = d["w"], d["stats"]
+        total += d["held"][1]
+    n_all = sum(s + 4 + 3 for s in kw["sizes"])  # train + test + val rows of every client (_runner: val = 3)
+    assert total == n_all  # the stores partition the cohort after migration
+    r = _runner(algo, **kw)
+    _drive(r, 2)
+    _same(got, _collect(r), len(kw["sizes"]), algo, atol=5e-5)
 
 
 def test_balanced_owner_evens_the_sampled_load():
