@@ -150,17 +150,59 @@ void conv1_sample_moments(uintptr_t x8, int64_t N, uintptr_t mom, uintptr_t stre
 }
 
 // ------------------------------------------------------------------------------------------------
-// weight packing: theta row g at off: [64][125] fp32 -> w8 [G][64][224] f16 bits of f16(w) (the forward's MFMA
-// A operand, against raw uint8 voxels), w125 [G][64][125] f32 = f16(w) * scale (scale = 1/255): the exact
-// effective weights of conv(x / 255) that the moment math (BN statistics) and the closed-form backward use.
+// 128-slot K packing of the forward (4 MFMA k-steps instead of 7).  The 27 polyphase tap groups t = 9 jd + 3 jh +
+// jw carry 8 valid phases when every j < 2 (8 groups "F"), 4 when one j = 2 (D: jd, H: jh, W: jw; 4 groups each),
+// 2 when two are (DH, DW, HW; 2 each) and 1 for jd = jh = jw = 2 — 125 taps.  Each lane group fq of a k-step holds
+// 8 consecutive k: k-steps 0-1 = the 8 F groups (one 16-B halo read each); k-step 2 = D[fq] (phases 0-3: the first
+// 8 bytes) + H[fq] (phases 0,1,4,5: dwords 0 and 2); k-step 3 = W[fq] (phases 0,2,4,6: the low halves of the 4
+// dwords, two v_perm) + two 2-phase groups (or DHW) picked by one v_cndmask + v_perm each.  Only 3 of 128 slots are
+// empty (vs 99 of 224 in the 27 x 8 layout).
+__device__ constexpr int kC1F[8] = {0, 1, 3, 4, 9, 10, 12, 13};
+__device__ constexpr int kC1D[4] = {18, 19, 21, 22};
+__device__ constexpr int kC1H[4] = {6, 7, 15, 16};
+__device__ constexpr int kC1W[4] = {2, 5, 11, 14};
+__device__ constexpr int kC1X1[4] = {24, 20, 8, 26};   // DH0, DW0, HW0, DHW
+__device__ constexpr int kC1X2[4] = {25, 23, 17, 26};  // DH1, DW1, HW1, (empty)
+__device__ constexpr int kC1XR[4][2] = {{0, 1}, {0, 2}, {0, 4}, {0, -1}};
+
+// (tap group, phase) of slot kk of the 128-slot layout, or t = -1 for an empty slot
+__device__ __forceinline__ void c1_slot128(int kk, int& t, int& r) {
+  const int st = kk >> 5, fq = (kk >> 3) & 3, e = kk & 7;
+  t = -1;
+  r = 0;
+  if (st < 2) { t = kC1F[4 * st + fq]; r = e; return; }
+  if (st == 2) {
+    if (e < 4) { t = kC1D[fq]; r = e; }
+    else { t = kC1H[fq]; r = (e - 4 < 2) ? e - 4 : e - 4 + 2; }
+    return;
+  }
+  if (e < 4) { t = kC1W[fq]; r = 2 * e; return; }
+  const int x = (e - 4) >> 1, h = e & 1;
+  if (x == 1 && fq == 3) return;
+  const int rr = kC1XR[fq][h];
+  if (rr < 0) return;
+  t = x == 0 ? kC1X1[fq] : kC1X2[fq];
+  r = rr;
+}
+
+// weight packing: theta row g at off: [64][125] fp32 -> w8 [G][64][KS] f16 bits of f16(w) (the forward's MFMA
+// A operand, against raw uint8 voxels; KS = 128 slots, or 224 = 27 x 8 for the legacy layout), w125 [G][64][125]
+// f32 = f16(w) * scale (scale = 1/255): the exact effective weights of conv(x / 255) that the moment math (BN
+// statistics) and the closed-form backward use.
 __global__ void k_pack_conv1_w(const float* __restrict__ theta, int64_t ldt, int64_t off, int64_t off_sign, int G,
-                               float scale, uint16_t* __restrict__ w8, float* __restrict__ w125) {
+                               float scale, int KS, uint16_t* __restrict__ w8, float* __restrict__ w125) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= G * kC1 * kK1) return;
-  const int g = i / (kC1 * kK1), rem = i - g * kC1 * kK1, c = rem / kK1, kk = rem - c * kK1;
-  const int t = kk >> 3, r = kk & 7;
+  if (i >= G * kC1 * KS) return;
+  const int g = i / (kC1 * KS), rem = i - g * kC1 * KS, c = rem / KS, kk = rem - c * KS;
+  int t, r;
+  if (KS == 128) {
+    c1_slot128(kk, t, r);
+  } else {
+    t = kk >> 3;
+    r = kk & 7;
+  }
   uint16_t v = 0;
-  if (t < 27 && tp_valid(t, r)) {
+  if (t >= 0 && t < 27 && tp_valid(t, r)) {
     const int k = tp_to_k(t, r);
     const _Float16 h = (_Float16)theta[(int64_t)g * ldt + off + c * 125 + k];
     v = __builtin_bit_cast(uint16_t, h);
@@ -171,10 +213,21 @@ __global__ void k_pack_conv1_w(const float* __restrict__ theta, int64_t ldt, int
   w8[i] = v;
 }
 
+// K slots of the forward's packed weights: 128 (default) or the legacy 27 x 8 = 224 (NIDT_C1_K224=1, A/B)
+int conv1_kslots() {
+  static const int ks = [] {
+    const char* e = getenv("NIDT_C1_K224");
+    return (e && atoi(e) == 1) ? kK1 : 128;
+  }();
+  return ks;
+}
+
 void pack_conv1_w(uintptr_t theta, int64_t ldt, int64_t off, int64_t off_sign, int G, float scale, uintptr_t w8,
                   uintptr_t w125, uintptr_t stream) {
-  hipLaunchKernelGGL(k_pack_conv1_w, dim3(ceil_div(G * kC1 * kK1, 256)), dim3(256), 0, as_stream(stream),
-                     ptr<const float>(theta), ldt, off, off_sign, G, scale, ptr<uint16_t>(w8), ptr<float>(w125));
+  const int KS = conv1_kslots();
+  // w125 entries of empty taps are never read; every valid (t, r) appears in exactly one slot of either layout
+  hipLaunchKernelGGL(k_pack_conv1_w, dim3(ceil_div(G * kC1 * KS, 256)), dim3(256), 0, as_stream(stream),
+                     ptr<const float>(theta), ldt, off, off_sign, G, scale, KS, ptr<uint16_t>(w8), ptr<float>(w125));
   NIDT_CHECK(hipGetLastError());
 }
 
@@ -324,7 +377,33 @@ __device__ __forceinline__ float vmax3(float a, float b, float c) {
 
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 
-template <int PF>  // B-fragment prefetch distance in k-steps
+// B fragment of k-step s (of KS per (dd, dh) row) for one output column: the lane's 8 consecutive k of the packed
+// layout read from the f16 halo at row offset ro.  KS = 7: tap group 4 s + fq, one 16-B read.  KS = 4: the
+// 128-slot layout of c1_slot128 (ga/gh/gx1/gx2: the lane's group offsets; xsrc2: lane picks dword 2 instead of 1
+// of its 2-phase groups; xsel1/xsel2: v_perm selectors of those groups).
+template <int KS>
+__device__ __forceinline__ f16x8 c1_bfrag(const uint16_t* hb, int s, int ro, const int* ga, int gh, int gx1, int gx2,
+                                          bool xsrc2, uint32_t xsel1, uint32_t xsel2) {
+  if (KS == 7 || s < 2) return *reinterpret_cast<const f16x8*>(&hb[ro + ga[s]]);
+  if (s == 2) {
+    const uint2 d = *reinterpret_cast<const uint2*>(&hb[ro + ga[2]]);  // D: phases 0-3
+    const uint32_t h0 = *reinterpret_cast<const uint32_t*>(&hb[ro + gh]);      // H: phases 0,1
+    const uint32_t h2 = *reinterpret_cast<const uint32_t*>(&hb[ro + gh + 4]);  // H: phases 4,5
+    const uint4 v = make_uint4(d.x, d.y, h0, h2);
+    return __builtin_bit_cast(f16x8, v);
+  }
+  const uint4 w = *reinterpret_cast<const uint4*>(&hb[ro + ga[3]]);
+  const uint4 a = *reinterpret_cast<const uint4*>(&hb[ro + gx1]);
+  const uint4 b = *reinterpret_cast<const uint4*>(&hb[ro + gx2]);
+  uint4 v;
+  v.x = __builtin_amdgcn_perm(w.y, w.x, 0x05040100u);  // phases 0, 2 (low halves)
+  v.y = __builtin_amdgcn_perm(w.w, w.z, 0x05040100u);  // phases 4, 6
+  v.z = __builtin_amdgcn_perm(xsrc2 ? a.z : a.y, a.x, xsel1);
+  v.w = __builtin_amdgcn_perm(xsrc2 ? b.z : b.y, b.x, xsel2);
+  return __builtin_bit_cast(f16x8, v);
+}
+
+template <int PF, int KS>  // PF: B-fragment prefetch distance in k-steps; KS: k-steps per (dd, dh) row (7 or 4)
 __global__ __launch_bounds__(256, 2) void k_conv1_fwd_pool_pipe(const uint8_t* __restrict__ x8,
                                                                 const int* __restrict__ idx,
                                                                 const uint16_t* __restrict__ w8,
@@ -357,14 +436,15 @@ __global__ __launch_bounds__(256, 2) void k_conv1_fwd_pool_pipe(const uint8_t* _
   C1_LOAD(0)
   const int fr = lane & 15, fq = lane >> 4;
   const int ch = wid & 1, op = wid >> 1;
-  f16x8 fa[2][7];
-  const uint16_t* wg = w8 + (int64_t)g * kC1 * kK1;
+  constexpr int KW = KS * 32;  // packed slots per channel row
+  f16x8 fa[2][KS];
+  const uint16_t* wg = w8 + (int64_t)g * kC1 * KW;
   float rs[2] = {0.f, 0.f};  // partial row sums of A (row 32ch + 16i + fr, this lane's k chunks)
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int s = 0; s < 7; ++s) {
-      fa[i][s] = *reinterpret_cast<const f16x8*>(wg + (32 * ch + 16 * i + fr) * kK1 + 32 * s + 8 * fq);
+    for (int s = 0; s < KS; ++s) {
+      fa[i][s] = *reinterpret_cast<const f16x8*>(wg + (32 * ch + 16 * i + fr) * KW + 32 * s + 8 * fq);
 #pragma unroll
       for (int e = 0; e < 8; ++e) rs[i] += (float)fa[i][s][e];
     }
@@ -395,16 +475,34 @@ __global__ __launch_bounds__(256, 2) void k_conv1_fwd_pool_pipe(const uint8_t* _
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
 #pragma unroll
-    for (int s = 0; s < 7; ++s) asm volatile("" : "+v"(fa[i][s]));
+    for (int s = 0; s < KS; ++s) asm volatile("" : "+v"(fa[i][s]));
 #pragma unroll
     for (int r = 0; r < 4; ++r) asm volatile("" : "+v"(sc[i][r]), "+v"(sh[i][r]), "+v"(cinit[i][r]));
   }
-  int toff[7];
+  // halo offsets of this lane's tap groups (relative to the (dd, dh) row and the output column)
+  auto goff = [](int t) { return (((t / 9) * 5 + (t / 3) % 3) * HX + (t % 3)) * 8; };
+  int toff[KS];
+  int gh = 0, gx1 = 0, gx2 = 0;
+  bool xsrc2 = false;
+  uint32_t xsel1 = 0, xsel2 = 0;
+  if (KS == 7) {
 #pragma unroll
-  for (int s = 0; s < 7; ++s) {
-    int t = 4 * s + fq;
-    t = t < 27 ? t : 26;
-    toff[s] = (((t / 9) * 5 + (t / 3) % 3) * HX + (t % 3)) * 8;
+    for (int s = 0; s < KS; ++s) {
+      int t = 4 * s + fq;
+      t = t < 27 ? t : 26;
+      toff[s] = goff(t);
+    }
+  } else {
+    toff[0] = goff(kC1F[fq]);
+    toff[1] = goff(kC1F[4 + fq]);
+    toff[2] = goff(kC1D[fq]);
+    toff[3 % KS] = goff(kC1W[fq]);
+    gh = goff(kC1H[fq]);
+    gx1 = goff(kC1X1[fq]);
+    gx2 = goff(kC1X2[fq]);
+    xsrc2 = fq == 2;
+    xsel1 = fq == 0 ? 0x03020100u : fq == 3 ? 0x0c0c0100u : 0x05040100u;
+    xsel2 = fq == 0 ? 0x03020100u : fq == 3 ? 0x0c0c0c0cu : 0x05040100u;
   }
   const int colbase0 = (15 * (2 * op) + fr) * 8, colbase1 = colbase0 + 15 * 8;
   const int wloc = fr / 3, dw = fr - 3 * wloc;
@@ -423,29 +521,30 @@ __global__ __launch_bounds__(256, 2) void k_conv1_fwd_pool_pipe(const uint8_t* _
         for (int r = 0; r < 4; ++r) best[i][j][r] = -INFINITY;
 #pragma unroll 1
     for (int dd = 0; dd < 3; ++dd) {
-      // 21 k-steps (3 dh rows x 7 tap groups); the B fragments are read PF steps ahead of their MFMAs (a ring of
-      // PF + 1 register pairs), so an LDS read's latency is covered by PF steps of matrix work, not one
+      // 3 KS k-steps (3 dh rows x KS); the B fragments are read PF steps ahead of their MFMAs (a ring of PF + 1
+      // register pairs), so an LDS read's latency is covered by PF steps of matrix work, not one
+      constexpr int NQ = 3 * KS;
       f16x8 rb0[PF + 1], rb1[PF + 1];
 #pragma unroll
       for (int p = 0; p < PF; ++p) {
-        const int ro = ((dd * 5 + p / 7) * HX) * 8 + toff[p % 7];
-        rb0[p] = *reinterpret_cast<const f16x8*>(&hb[colbase0 + ro]);
-        rb1[p] = *reinterpret_cast<const f16x8*>(&hb[colbase1 + ro]);
+        const int ro = ((dd * 5 + p / KS) * HX) * 8;
+        rb0[p] = c1_bfrag<KS>(hb + colbase0, p % KS, ro, toff, gh, gx1, gx2, xsrc2, xsel1, xsel2);
+        rb1[p] = c1_bfrag<KS>(hb + colbase1, p % KS, ro, toff, gh, gx1, gx2, xsrc2, xsel1, xsel2);
       }
       f32x4 acc[2][2];
 #pragma unroll
-      for (int q = 0; q < 21; ++q) {
-        const int dh = q / 7, s = q % 7;
+      for (int q = 0; q < NQ; ++q) {
+        const int dh = q / KS, s = q % KS;
         if (s == 0) {
 #pragma unroll
           for (int i = 0; i < 2; ++i)
 #pragma unroll
             for (int j = 0; j < 2; ++j) acc[i][j] = cinit[i];
         }
-        if (q + PF < 21) {
-          const int qn = q + PF, ro = ((dd * 5 + qn / 7) * HX) * 8 + toff[qn % 7];
-          rb0[qn % (PF + 1)] = *reinterpret_cast<const f16x8*>(&hb[colbase0 + ro]);
-          rb1[qn % (PF + 1)] = *reinterpret_cast<const f16x8*>(&hb[colbase1 + ro]);
+        if (q + PF < NQ) {
+          const int qn = q + PF, ro = ((dd * 5 + qn / KS) * HX) * 8;
+          rb0[qn % (PF + 1)] = c1_bfrag<KS>(hb + colbase0, qn % KS, ro, toff, gh, gx1, gx2, xsrc2, xsel1, xsel2);
+          rb1[qn % (PF + 1)] = c1_bfrag<KS>(hb + colbase1, qn % KS, ro, toff, gh, gx1, gx2, xsrc2, xsel1, xsel2);
         }
         const f16x8 fb0 = rb0[q % (PF + 1)], fb1 = rb1[q % (PF + 1)];
 #pragma unroll
@@ -454,7 +553,7 @@ __global__ __launch_bounds__(256, 2) void k_conv1_fwd_pool_pipe(const uint8_t* _
           acc[i][1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[i][s], fb1, acc[i][1], 0, 0, 0);
         }
         if (PF > 1) asm volatile("" ::: "memory");  // keep step q+PF's LDS reads in step q (no re-hoisting)
-        if (s != 6) continue;
+        if (s != KS - 1) continue;
         const uint32_t tag = (uint32_t)(dd * 9 + dh * 3 + dw);
 #pragma unroll
         for (int i = 0; i < 2; ++i)
@@ -515,11 +614,15 @@ void conv1_fwd_pool(uintptr_t x8, uintptr_t idx, uintptr_t w8, uintptr_t scale, 
     const char* e = getenv("NIDT_C1_PF");
     return e ? atoi(e) : 2;
   }();
-#define NIDT_C1(PF)                                                                                              \
-  hipLaunchKernelGGL(k_conv1_fwd_pool_pipe<PF>, dim3(kPD * NB), dim3(256), 0, as_stream(stream), ptr<const uint8_t>(x8), \
-                     ptr<const int>(idx), ptr<const uint16_t>(w8), ptr<const float>(scale), ptr<const float>(shift), B, \
-                     ptr<uint16_t>(out), ptr<uint8_t>(amax))
-  if (pf == 1) NIDT_C1(1); else if (pf == 3) NIDT_C1(3); else NIDT_C1(2);
+#define NIDT_C1(PF, KSS)                                                                                       \
+  hipLaunchKernelGGL((k_conv1_fwd_pool_pipe<PF, KSS>), dim3(kPD * NB), dim3(256), 0, as_stream(stream),           \
+                     ptr<const uint8_t>(x8), ptr<const int>(idx), ptr<const uint16_t>(w8), ptr<const float>(scale),  \
+                     ptr<const float>(shift), B, ptr<uint16_t>(out), ptr<uint8_t>(amax))
+  if (conv1_kslots() == 128) {
+    if (pf == 1) NIDT_C1(1, 4); else if (pf == 3) NIDT_C1(3, 4); else NIDT_C1(2, 4);
+  } else {
+    if (pf == 1) NIDT_C1(1, 7); else if (pf == 3) NIDT_C1(3, 7); else NIDT_C1(2, 7);
+  }
 #undef NIDT_C1
   NIDT_CHECK(hipGetLastError());
 }
