@@ -72,7 +72,7 @@ void gn_bwd(uintptr_t dy, int dy_bf16, uintptr_t mask, uintptr_t t, uintptr_t st
 void gn_param_grads(uintptr_t part, int G, int B, int C, uintptr_t grads, int64_t ldg, int64_t off_w, int64_t off_b,
                     uintptr_t stream);
 void res_grad(uintptr_t out, uintptr_t dx1, uintptr_t dx2, uintptr_t da, uintptr_t mask, int64_t n, uintptr_t stream);
-void res_grad_s2(uintptr_t out, uintptr_t dx1, uintptr_t dx2s, int N, int H, int W, int C, uintptr_t stream);
+void res_grad_s2(uintptr_t out, uintptr_t dx1, uintptr_t dx2s, int N, int D, int H, int W, int C, uintptr_t stream);
 // img.hip
 void img_input(uintptr_t src, uintptr_t idx, uintptr_t out, int N, int H, int W, int CP, float m0, float m1, float m2,
                float s0, float s1, float s2, int aug, int pad, uintptr_t seed_dev, int64_t seed_base, uintptr_t cids,
@@ -154,6 +154,17 @@ void masked_rows_sum(uintptr_t rows, int64_t ld, uintptr_t bits, int64_t mstride
 void mix_rows(uintptr_t src, uintptr_t wts, uintptr_t rowptr, uintptr_t dst, int R, int64_t n, uintptr_t stream);
 int pair_sqdist_nblk(int64_t n);
 void pair_sqdist(uintptr_t pa, uintptr_t pb, int K, int64_t n, uintptr_t part, uintptr_t stream);
+void stem_polyphase(uintptr_t src, uintptr_t idx, int N, int D, int H, int W, uintptr_t xp, uintptr_t xq,
+                    uintptr_t stream);
+void stem_fwd(uintptr_t xp, uintptr_t theta, int64_t ldt, int64_t off_w, int N, int B, int D, int H, int W, uintptr_t wk,
+              uintptr_t y, uintptr_t stats, uintptr_t stream);
+void stem_pool(uintptr_t y, uintptr_t scale, uintptr_t shift, int N, int B, int D, int H, int W, uintptr_t out,
+               uintptr_t amax, uintptr_t stream);
+void stem_bwd(uintptr_t dpool, uintptr_t amax, uintptr_t y, uintptr_t xq, uintptr_t scale, uintptr_t shift,
+              uintptr_t mean, uintptr_t invstd, int N, int B, int D, int H, int W, uintptr_t theta, int64_t ldt,
+              int64_t off_g, uintptr_t grad, int64_t ldg, int64_t goff_w, int64_t goff_g, int64_t goff_b, uintptr_t dz,
+              uintptr_t part, uintptr_t coef, uintptr_t slab, uintptr_t stream);
+std::vector<int64_t> stem_sizes(int N, int D, int H, int W);
 }  // namespace nidt
 
 PYBIND11_MODULE(_nidt_hip, m) {
@@ -235,5 +246,10 @@ PYBIND11_MODULE(_nidt_hip, m) {
   DEF(mix_rows);
   DEF(pair_sqdist_nblk);
   DEF(pair_sqdist);
+  DEF(stem_polyphase);
+  DEF(stem_fwd);
+  DEF(stem_pool);
+  DEF(stem_bwd);
+  DEF(stem_sizes);
 #undef DEF
 }

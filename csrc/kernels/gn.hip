@@ -481,23 +481,27 @@ void res_grad(uintptr_t out, uintptr_t dx1, uintptr_t dx2, uintptr_t da, uintptr
   NIDT_CHECK(hipGetLastError());
 }
 
-// Residual-stream gradient of a downsampling block: out = dx1 + (dx2 at the even pixels), with the 1x1 stride-2
-// shortcut's data gradient given at half resolution (dx2s [N][Ho][Wo][C], Ho = ceil(H/2)): the shortcut conv read
-// only the even pixels, so no full-size zero-filled scatter of its gradient is needed.
+// Residual-stream gradient of a downsampling block: out = dx1 + (dx2 at the even pixels), with the 1x1(x1) stride-2
+// shortcut's data gradient given at half resolution (dx2s [N][Do][Ho][Wo][C], Ho = ceil(H/2); D = 1 for 2-D maps):
+// the shortcut conv read only the even positions, so no full-size zero-filled scatter of its gradient is needed.
 __global__ void k_res_grad_s2(float* __restrict__ out, const uint16_t* __restrict__ dx1,
-                              const uint16_t* __restrict__ dx2s, int64_t n8, int H, int W, int C) {
-  const int C8 = C / 8, Ho = (H + 1) / 2, Wo = (W + 1) / 2;
+                              const uint16_t* __restrict__ dx2s, int64_t n8, int D, int H, int W, int C) {
+  const int C8 = C / 8, Do = D > 1 ? (D + 1) / 2 : 1, Ho = (H + 1) / 2, Wo = (W + 1) / 2;
   for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n8; q += (int64_t)gridDim.x * blockDim.x) {
     const int c8 = (int)(q % C8);
     const int64_t pix = q / C8;
     const int x = (int)(pix % W);
-    const int64_t r = pix / W;
+    int64_t r = pix / W;
     const int y = (int)(r % H);
-    const int64_t n = r / H;
+    r /= H;
+    const int z = (int)(r % D);
+    const int64_t n = r / D;
+    const int zz = D > 1 ? z : 0;
     float a[8], b[8];
     unpack8(*reinterpret_cast<const uint4*>(dx1 + q * 8), a);
-    if (((x | y) & 1) == 0) {
-      unpack8(*reinterpret_cast<const uint4*>(dx2s + (((n * Ho + (y >> 1)) * Wo + (x >> 1)) * C8 + c8) * 8), b);
+    if (((x | y | zz) & 1) == 0) {
+      const int64_t o = (((n * Do + (zz >> 1)) * Ho + (y >> 1)) * Wo + (x >> 1)) * C8 + c8;
+      unpack8(*reinterpret_cast<const uint4*>(dx2s + o * 8), b);
     } else {
 #pragma unroll
       for (int e = 0; e < 8; ++e) b[e] = 0.f;
@@ -508,12 +512,12 @@ __global__ void k_res_grad_s2(float* __restrict__ out, const uint16_t* __restric
   }
 }
 
-void res_grad_s2(uintptr_t out, uintptr_t dx1, uintptr_t dx2s, int N, int H, int W, int C, uintptr_t stream) {
-  NIDT_REQUIRE(C % 8 == 0, "res_grad_s2: C % 8 == 0");
-  const int64_t n8 = (int64_t)N * H * W * C / 8;
+void res_grad_s2(uintptr_t out, uintptr_t dx1, uintptr_t dx2s, int N, int D, int H, int W, int C, uintptr_t stream) {
+  NIDT_REQUIRE(C % 8 == 0 && D >= 1, "res_grad_s2: C % 8 == 0");
+  const int64_t n8 = (int64_t)N * D * H * W * C / 8;
   hipLaunchKernelGGL(k_res_grad_s2, dim3((unsigned)std::min<int64_t>(8192, (n8 + 255) / 256)), dim3(256), 0,
-                     as_stream(stream), ptr<float>(out), ptr<const uint16_t>(dx1), ptr<const uint16_t>(dx2s), n8, H,
-                     W, C);
+                     as_stream(stream), ptr<float>(out), ptr<const uint16_t>(dx1), ptr<const uint16_t>(dx2s), n8, D,
+                     H, W, C);
   NIDT_CHECK(hipGetLastError());
 }
 

@@ -534,7 +534,7 @@ class GroupedResNet18GN:
                 out = torch.empty(dx1.shape, device=dx1.device, dtype=torch.float32)
                 if half:
                     Nn, Hh, Ww, Cc = dx1.shape
-                    ops.ext().res_grad_s2(out.data_ptr(), dx1.data_ptr(), dx2.data_ptr(), Nn, Hh, Ww, Cc, _stream())
+                    ops.ext().res_grad_s2(out.data_ptr(), dx1.data_ptr(), dx2.data_ptr(), Nn, 1, Hh, Ww, Cc, _stream())
                 else:
                     ops.ext().res_grad(out.data_ptr(), dx1.data_ptr(), dx2.data_ptr() if dx2 is not None else 0,
                                        0 if dx2 is not None else da.data_ptr(),

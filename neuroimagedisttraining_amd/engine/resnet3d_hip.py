@@ -2,15 +2,19 @@
 gfx950 kernels: G clients' local steps in one lockstep pass over rows of the flat ``[C, P]`` parameter matrix.
 
 * every bottleneck convolution — 1x1x1 (the GEMM path: ``conv_fwd_g`` with one tap), 3x3x3 at stride 1 and 2, the
-  1x1x1 stride-2 projections — runs on the client-grouped LDS-DMA implicit-GEMM kernels of ``conv3d.hip``; data
-  gradients use the same kernels on tap-flipped transposed weights (stride 2: zero-upsampled gradient, cropped;
-  1x1 stride 2: scattered to the even voxels), weight gradients the position-table wgrad kernel straight into the
-  client's gradient row;
+  1x1x1 stride-2 projections — runs on the client-grouped LDS-DMA implicit-GEMM kernels of ``conv3d.hip``, with
+  every layer's bf16 MFMA images packed in two launches per step (``pack.hip``); data gradients: stride 1 = the
+  same kernels on tap-flipped transposed weights, 3x3x3 stride 2 = eight sub-pixel phase convs over the dy grid
+  written straight into dX (``conv_dgrad_s2_g``: 8x fewer MACs than the zero-upsampled form, no memset or crop),
+  1x1x1 stride 2 = the half-resolution gradient of the even voxels added by ``res_grad_s2``; weight gradients the
+  position-table wgrad kernel straight into the client's gradient row;
 * BatchNorm3d (train and eval mode, per-client statistics / affine / running stats) is ``bnr.hip``, with the
   residual add and ReLU fused into the apply and the ReLU mask into the backward;
-* the stem (7x7x7 stride-2 conv with ONE input channel, BN, ReLU, 3x3x3 max-pool) is not a GEMM shape the conv
-  kernels serve: it runs as one client-grouped PyTorch segment (grouped conv over all clients of the launch,
-  per-client batch statistics) differentiated by autograd;
+* the stem (7x7x7 stride-2 conv with ONE input channel, BN, ReLU, 3x3x3 max-pool) is ``stem.hip``: the uint8
+  volume in polyphase form turns the stride-2 7^3 conv into a stride-1 4^3 conv over 8 phase channels (512 MFMA
+  k-slots), fused with the per-block BN statistics (merged by ``bn.hip``'s finalize), a BN+ReLU+pool kernel that
+  keeps a uint8 argmax, and the backward (unpool + ReLU mask + BN sums, the BN coefficients, an MFMA weight
+  gradient over x-shifted phase rows); the CPU twin (``hip=False``) is the same graph in PyTorch;
 * the head (global average pool, fc -> 1, BCE) is a few batched torch ops.
 
 Reference model: ``fedml_api/model/cv/salient_models.py:8-139`` (3D ResNet blocks); the 4-stage ResNet-50 is this
@@ -47,26 +51,32 @@ def conv_fwd(x_ptr, w_ptr, y_ptr, G, B, D, H, W, Cin, Cout, kt, st, pad, padd, d
 
 
 class GConv3:
-    """Client-grouped Conv3d (k = 1 or 3, stride 1/2, no bias) on channels-last ``[N, D, H, W, C]`` bf16."""
+    """Client-grouped Conv3d (k = 1 or 3, stride 1/2, no bias) on channels-last ``[N, D, H, W, C]`` bf16.  Weight
+    images come from the network's :class:`~.resnet2d_hip.WeightPacker` (two launches per step for all layers;
+    the dgrad image in this layer's tap-slot order)."""
 
     def __init__(self, off, cout, cin, k, stride, pad, hip=True):
         assert k in (1, 3) and cin % 64 == 0 and cout % 64 == 0, (k, cin, cout)
         self.off, self.cout, self.cin, self.k, self.stride, self.pad = off, cout, cin, k, stride, pad
         self.hip = hip
         self.kt = 27 if k == 3 else 1
+        self.cin_p = cin
+        self.need_dgrad = True
         self.numel = cout * cin * self.kt
-        self._packed = None
+        self.slots = list(ops.ext().conv_tap_slots(self.kt, stride)) if hip else None
+        self.wp = self.wt = None
 
     def out_dims(self, d, h, w):
         f = lambda n: (n + 2 * self.pad - self.k) // self.stride + 1  # noqa: E731
         return f(d), f(h), f(w)
 
     def _wp(self, theta, G, transposed):
+        """Standalone packing of this layer (tests); the network packs every layer at once."""
+        from .resnet2d_hip import WeightPacker
         wp = torch.empty(G, self.cout, self.kt, self.cin, device=theta.device, dtype=torch.bfloat16)
         wt = torch.empty(G, self.cin, self.kt, self.cout, device=theta.device, dtype=torch.bfloat16) \
             if transposed else None
-        ops.ext().pack_conv_wk(theta.data_ptr(), theta.stride(0), self.off, G, self.cout, self.cin, self.kt, self.cin,
-                               1.0, wp.data_ptr(), wt.data_ptr() if transposed else 0, _stream())
+        WeightPacker([self], theta.device).pack_into(theta, G, wp, wt)
         return wp, wt
 
     def _torch_fwd(self, x, w, G):
@@ -77,14 +87,17 @@ class GConv3:
                      padding=self.pad, groups=G)
         return y.view(B, G, self.cout, *y.shape[2:]).permute(1, 0, 3, 4, 5, 2).reshape(N, *y.shape[2:], self.cout)
 
-    def fwd(self, x, theta, G, train=False):
+    def fwd(self, x, theta, G, train=False, packed=False):
         N, D, H, W, C = x.shape
         assert C == self.cin and N % G == 0 and x.is_contiguous()
         if not self.hip:
             return self._torch_fwd(x, theta[:, self.off:self.off + self.numel], G)
         Do, Ho, Wo = self.out_dims(D, H, W)
-        wp, wt = self._wp(theta, G, train)
-        self._packed = (theta.data_ptr(), G, wt) if train else None
+        if not packed:
+            wp, wt = self._wp(theta, G, train)
+            self.wp = (wp, G, theta.data_ptr())
+            self.wt = (wt, G, theta.data_ptr()) if wt is not None else None
+        wp = self.wp[0]
         y = torch.empty(N, Do, Ho, Wo, self.cout, device=x.device, dtype=torch.bfloat16)
         conv_fwd(x.data_ptr(), wp.data_ptr(), y.data_ptr(), G, N // G, D, H, W, self.cin, self.cout,
                  self.kt, self.stride, self.pad, self.pad if self.kt == 27 else 0, x.device)
@@ -98,7 +111,11 @@ class GConv3:
                 y = self._torch_fwd(xx, w, G)
                 outs = torch.autograd.grad(y, [w, xx] if need_dx else [w], dy.to(y.dtype))
             grads[:, self.off:self.off + self.numel].copy_(outs[0])
-            return outs[1] if need_dx else None
+            if not need_dx:
+                return None
+            if self.k == 1 and self.stride == 2:  # same contract as the HIP path: the even voxels only
+                return outs[1][:, ::2, ::2, ::2].contiguous()
+            return outs[1]
         m, st = ops.ext(), _stream()
         N, D, H, W, _ = x.shape
         B = N // G
@@ -114,9 +131,8 @@ class GConv3:
                        st)
         if not need_dx:
             return None
-        pk, self._packed = self._packed, None
-        wt = pk[2] if (pk is not None and pk[0] == theta.data_ptr() and pk[1] == G and pk[2] is not None) else \
-            self._wp(theta, G, True)[1]
+        pk, self.wt = self.wt, None
+        wt = pk[0] if (pk is not None and pk[2] == theta.data_ptr() and pk[1] == G) else self._wp(theta, G, True)[1]
         if self.stride == 1:
             dx = torch.empty(N, D, H, W, self.cin, device=x.device, dtype=torch.bfloat16)
             p2 = self.k - 1 - self.pad
@@ -124,22 +140,18 @@ class GConv3:
                          1, p2, p2 if self.kt == 27 else 0, x.device)
             return dx
         if self.k == 3:
-            # stride 2, pad 1: dX = conv(zero-upsampled dY [2Do, 2Ho, 2Wo], flipped W^T, pad 1), cropped to D x H x W
-            up = torch.zeros(N, 2 * Do, 2 * Ho, 2 * Wo, self.cout, device=x.device, dtype=torch.bfloat16)
-            up[:, ::2, ::2, ::2] = dy
-            full = torch.empty(N, 2 * Do, 2 * Ho, 2 * Wo, self.cin, device=x.device, dtype=torch.bfloat16)
-            conv_fwd(up.data_ptr(), wt.data_ptr(), full.data_ptr(), G, B, 2 * Do, 2 * Ho, 2 * Wo, self.cout,
-                         self.cin, 27, 1, 1, 1, x.device)
-            if (2 * Do, 2 * Ho, 2 * Wo) == (D, H, W):
-                return full
-            return full[:, :D, :H, :W].contiguous()
-        # 1x1 stride 2: dX at the even voxels = W^T dY, zero elsewhere
+            # stride 2, pad 1: 8 sub-pixel phase convs over the dy grid (1..8 taps each, 27 in all) written straight
+            # into the interleaved voxels of dX — 8x fewer MACs than a conv over the zero-upsampled dy, no memset,
+            # no crop copy (conv_dgrad_s2_g; odd extents: the last odd-phase plane has no dy plane beyond it)
+            dx = torch.empty(N, D, H, W, self.cin, device=x.device, dtype=torch.bfloat16)
+            ops.ext().conv_dgrad_s2_g(dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), G, B, Do, Ho, Wo, self.cout,
+                                      self.cin, 27, D, H, W, st)
+            return dx
+        # 1x1 stride 2: the half-resolution W^T dY of the even voxels (res_grad_s2 adds it into the residual stream)
         sub = torch.empty(N, Do, Ho, Wo, self.cin, device=x.device, dtype=torch.bfloat16)
         conv_fwd(dy.data_ptr(), wt.data_ptr(), sub.data_ptr(), G, B, Do, Ho, Wo, self.cout, self.cin, 1, 1, 0, 0,
                  x.device)
-        dx = torch.zeros(N, D, H, W, self.cin, device=x.device, dtype=torch.bfloat16)
-        dx[:, ::2, ::2, ::2] = sub
-        return dx
+        return sub
 
 
 class GBN3:
@@ -270,10 +282,82 @@ class GroupedResNet3D:
         self.fc_w, self.fc_b = off["fc.weight"], off["fc.bias"]
         self.ncls, self.feat = shp["fc.weight"]
         self.stem_c = shp["conv1.weight"][0]
+        if self.hip:
+            from .resnet2d_hip import WeightPacker
+            self.packer = WeightPacker([b[k] for b in self.blocks for k in ("c1", "c2", "c3", "cd") if k in b],
+                                       self.device)
+        else:
+            self.packer = None
 
-    # ------------------------------------------------------------------ stem (torch, autograd)
-    def _stem(self, x8, theta, bufs, G, train):
-        """uint8 volumes [N, D, H, W] -> pooled stem activation [N, d, h, w, C] bf16 (+ autograd handles)."""
+    # ------------------------------------------------------------------ stem
+    def _stem(self, x8, theta, bufs, G, train, idx=None):
+        """uint8 volumes -> pooled stem activation [N, 31, 37, 31, C] (+ what the backward needs).  HIP: ``x8`` is
+        the volume store and ``idx`` the samples of this step (None: all of ``x8``, in order)."""
+        if self.hip:
+            return self._stem_hip(x8, idx, theta, bufs, G, train)
+        return self._stem_torch(x8, theta, bufs, G, train)
+
+    def _stem_hip(self, x8, idx, theta, bufs, G, train):
+        m, st = ops.ext(), _stream()
+        dev = theta.device
+        assert x8.dim() == 4 and x8.dtype == torch.uint8 and x8.device == dev and x8.is_contiguous(), \
+            "stem.hip reads contiguous uint8 [N, D, H, W] volumes on the compute device"
+        D, H, W = x8.shape[1:]
+        assert self.stem_c == 64 and W <= 128, "stem.hip: 64 channels, output rows of at most 64 voxels"
+        Od, Oh, Ow = (D - 1) // 2 + 1, (H - 1) // 2 + 1, (W - 1) // 2 + 1
+        Qd, Qh, Qw = (Od - 1) // 2 + 1, (Oh - 1) // 2 + 1, (Ow - 1) // 2 + 1
+        if idx is None:
+            idx = torch.arange(x8.shape[0], device=dev, dtype=torch.int32)
+        idx = idx.to(device=dev, dtype=torch.int32).contiguous()
+        N = idx.numel()
+        assert N % G == 0
+        B = N // G
+        C, o, bo = self.stem_c, self.off, self.boff
+        sz = m.stem_sizes(N, D, H, W)
+        xp = torch.empty(sz[0], device=dev, dtype=torch.uint8)
+        xq = torch.empty(sz[0], device=dev, dtype=torch.uint8) if train else None
+        m.stem_polyphase(x8.data_ptr(), idx.data_ptr(), N, D, H, W, xp.data_ptr(), xq.data_ptr() if train else 0, st)
+        y = torch.empty(N, Od, Oh, Ow, C, device=dev, dtype=torch.bfloat16)
+        stats = torch.empty(sz[3], device=dev, dtype=torch.float32)
+        wk = torch.empty(G * sz[5], device=dev, dtype=torch.bfloat16)
+        m.stem_fwd(xp.data_ptr(), theta.data_ptr(), theta.stride(0), o["conv1.weight"], N, B, D, H, W, wk.data_ptr(),
+                   y.data_ptr(), stats.data_ptr(), st)
+        del xp
+        coef = torch.empty(4, G * C, device=dev, dtype=torch.float32)  # scale, shift, mean, invstd
+        ptrs = [coef[i].data_ptr() for i in range(4)]
+        nbt = bo.get("bn1.num_batches_tracked", -1)
+        if train:
+            upd = bufs is not None and nbt >= 0
+            m.bn_finalize(stats.data_ptr(), B * Od, Oh * Ow, B * Od * Oh * Ow, G, C, theta.data_ptr(),
+                          theta.stride(0), o["bn1.weight"], o["bn1.bias"], bufs.data_ptr() if upd else 0,
+                          bufs.stride(0) if upd else 0, bo["bn1.running_mean"], bo["bn1.running_var"], nbt, BN_MOM,
+                          BN_EPS, *ptrs, int(upd), st)
+        else:
+            m.bn_eval(G, C, theta.data_ptr(), theta.stride(0), o["bn1.weight"], o["bn1.bias"], bufs.data_ptr(),
+                      bufs.stride(0), bo["bn1.running_mean"], bo["bn1.running_var"], BN_EPS, *ptrs, st)
+        out = torch.empty(N, Qd, Qh, Qw, C, device=dev, dtype=torch.bfloat16)
+        amax = torch.empty(N, Qd, Qh, Qw, C, device=dev, dtype=torch.uint8)
+        m.stem_pool(y.data_ptr(), ptrs[0], ptrs[1], N, B, D, H, W, out.data_ptr(), amax.data_ptr(), st)
+        return out, ((y, xq, amax, coef, N, B, (D, H, W)) if train else None)
+
+    def _stem_hip_bwd(self, saved, da, theta, grads, G):
+        y, xq, amax, coef, N, B, (D, H, W) = saved
+        m, st = ops.ext(), _stream()
+        dev = theta.device
+        sz = m.stem_sizes(N, D, H, W)
+        o = self.off
+        da = da.float().contiguous()
+        dz = torch.empty_like(y)
+        part = torch.empty(sz[3], device=dev, dtype=torch.float32)
+        bcoef = torch.empty(G * self.stem_c * 3, device=dev, dtype=torch.float32)
+        slab = torch.empty(sz[4], device=dev, dtype=torch.float32)
+        m.stem_bwd(da.data_ptr(), amax.data_ptr(), y.data_ptr(), xq.data_ptr(), coef[0].data_ptr(),
+                   coef[1].data_ptr(), coef[2].data_ptr(), coef[3].data_ptr(), N, B, D, H, W, theta.data_ptr(),
+                   theta.stride(0), o["bn1.weight"], grads.data_ptr(), grads.stride(0), o["conv1.weight"],
+                   o["bn1.weight"], o["bn1.bias"], dz.data_ptr(), part.data_ptr(), bcoef.data_ptr(), slab.data_ptr(),
+                   st)
+
+    def _stem_torch(self, x8, theta, bufs, G, train):
         N = x8.shape[0]
         B = N // G
         C = self.stem_c
@@ -300,18 +384,22 @@ class GroupedResNet3D:
         return out.to(self.act).contiguous(), (out, leaf)
 
     # ------------------------------------------------------------------ forward
-    def forward(self, x8, theta, bufs, G, train):
-        a, stem = self._stem(x8, theta, bufs, G, train)
+    def forward(self, x8, theta, bufs, G, train, idx=None):
+        packed = self.packer is not None
+        N = x8.shape[0] if idx is None else idx.numel()
+        if packed:  # every bottleneck layer's MFMA images for this step, two launches
+            self.packer.pack(theta, G, train, key=(G, N // G, train))
+        a, stem = self._stem(x8, theta, bufs, G, train, idx)
         saved = []
         for blk in self.blocks:
             xin = a
-            t1 = blk["c1"].fwd(xin, theta, G, train)
+            t1 = blk["c1"].fwd(xin, theta, G, train, packed)
             h1, s1 = blk["n1"].fwd(t1, theta, bufs, G, train, relu=True)
-            t2 = blk["c2"].fwd(h1, theta, G, train)
+            t2 = blk["c2"].fwd(h1, theta, G, train, packed)
             h2, s2 = blk["n2"].fwd(t2, theta, bufs, G, train, relu=True)
-            t3 = blk["c3"].fwd(h2, theta, G, train)
+            t3 = blk["c3"].fwd(h2, theta, G, train, packed)
             if "cd" in blk:
-                td = blk["cd"].fwd(xin, theta, G, train)
+                td = blk["cd"].fwd(xin, theta, G, train, packed)
                 yd, sd = blk["nd"].fwd(td, theta, bufs, G, train)
             else:
                 td, sd, yd = None, None, xin
@@ -327,8 +415,8 @@ class GroupedResNet3D:
         logits = (pooled.view(G, B, 1, C) * fw.view(G, 1, self.ncls, C)).sum(-1) + fb.view(G, 1, self.ncls)
         return logits.reshape(N, self.ncls), pooled, saved, stem
 
-    def train_step(self, theta, bufs, grads, x8, y, G, B, bn_train=True):
-        logits, pooled, saved, stem = self.forward(x8, theta, bufs, G, True)
+    def train_step(self, theta, bufs, grads, x8, y, G, B, bn_train=True, idx=None):
+        logits, pooled, saved, stem = self.forward(x8, theta, bufs, G, True, idx)
         lg = logits.view(G, B)
         yt = y.float().view(G, B)
         losses = F.binary_cross_entropy_with_logits(lg, yt, reduction="none").mean(1)
@@ -353,14 +441,26 @@ class GroupedResNet3D:
             if "cd" in blk:
                 dtd = blk["nd"].bwd(da, a, td, sd, theta, grads, G)
                 dx2 = blk["cd"].bwd(dtd, xin, theta, grads, G)
+            half = dx2 is not None and blk["cd"].stride == 2  # 1x1x1 stride-2 projection: even-voxel gradient
             if self.hip:
                 out = torch.empty(dx1.shape, device=dx1.device, dtype=torch.float32)
-                ops.ext().res_grad(out.data_ptr(), dx1.data_ptr(), dx2.data_ptr() if dx2 is not None else 0,
-                                   0 if dx2 is not None else da.data_ptr(), 0 if dx2 is not None else a.data_ptr(),
-                                   out.numel(), _stream())
+                if half:
+                    Nn, Dd, Hh, Ww, Cc = dx1.shape
+                    ops.ext().res_grad_s2(out.data_ptr(), dx1.data_ptr(), dx2.data_ptr(), Nn, Dd, Hh, Ww, Cc,
+                                          _stream())
+                else:
+                    ops.ext().res_grad(out.data_ptr(), dx1.data_ptr(), dx2.data_ptr() if dx2 is not None else 0,
+                                       0 if dx2 is not None else da.data_ptr(),
+                                       0 if dx2 is not None else a.data_ptr(), out.numel(), _stream())
                 da = out
+            elif half:
+                da = dx1.float().clone()
+                da[:, ::2, ::2, ::2] += dx2.float()
             else:
                 da = dx1.float() + (dx2.float() if dx2 is not None else da * (a > 0))
+        if self.hip:
+            self._stem_hip_bwd(stem, da, theta, grads, G)
+            return losses.detach()
         out, leaf = stem
         gw, gg, gb = torch.autograd.grad(out, leaf, da.to(out.dtype))
         C = self.stem_c
@@ -376,7 +476,7 @@ class ResNet3DHipEngine:
     ABCD-shape volumes ``[N, D, H, W]`` (labels {0, 1}, BCE head with one logit)."""
     sample_fields = ("x8", "labels")
 
-    supports_graphs = False  # the stem segment allocates autograd state; launches here are few and large
+    supports_graphs = False  # launches here are few and large (seconds per step at config-5 shapes)
 
     def __init__(self, template_model, volumes_u8, labels, device, hip=None):
         self.device = torch.device(device)
@@ -389,16 +489,25 @@ class ResNet3DHipEngine:
             ops.ext()  # fail loudly without the extension
         self._opt = None
 
+    def _src(self, idx):
+        """(volumes, sample index) for the network: a device-resident store is read in place by the HIP stem's
+        polyphase gather; otherwise the step's samples are gathered to the device first."""
+        if self.net.hip and self.x8.device == self.device:
+            return self.x8, idx
+        return self._x(idx), None
+
     def _x(self, idx):
         return self.x8.index_select(0, idx.long().to(self.x8.device)).to(self.device, non_blocking=True)
 
     def train_step(self, theta, bufs, grads, idx, G, B, keep, seed, cids=None, seed_dev=None, bn_train=True):
         y = self.labels.index_select(0, idx.long())
-        return self.net.train_step(theta, bufs, grads, self._x(idx), y, G, B, bn_train)
+        x, sel = self._src(idx)
+        return self.net.train_step(theta, bufs, grads, x, y, G, B, bn_train, idx=sel)
 
     def eval_logits(self, theta, bufs, idx, G, B):
         with torch.no_grad():
-            logits, _, _, _ = self.net.forward(self._x(idx), theta, bufs, G, False)
+            x, sel = self._src(idx)
+            logits, _, _, _ = self.net.forward(x, theta, bufs, G, False, idx=sel)
         return logits.float()
 
     def _delegate(self):

@@ -66,6 +66,21 @@ def test_cli_resnet18_cifar_runs_on_hip(algo, tmp_path):
     assert "HIP cohort (resnet2d)" in log
 
 
+@pytest.mark.parametrize("algo", ["subavg", "dispfl", "ditto", "dpsgd", "fedfomo", "local", "fedavg"])
+def test_cli_resnet18_tiny_runs_on_hip(algo, tmp_path):
+    """The Tiny-ImageNet presets (``fedml_experiments/standalone/*/tiny.sh``: resnet18 = tiny_resnet18, 64x64, 200
+    classes) run on the client-batched ResNet engine with the fused augmentation."""
+    from neuroimagedisttraining_amd import cli
+    argv = ["--model", "resnet18", "--dataset", "tiny", "--client_num_in_total", "4", "--comm_round", "2",
+            "--epochs", "1", "--batch_size", "16", "--synthetic_size", "400", "--frac", "0.5", "--engine", "hip",
+            "--log_dir", str(tmp_path)]
+    out = cli.main(algo, argv)
+    vals = [v for k, v in out.items() if k.endswith("test_acc") and isinstance(v, list) and v]
+    assert vals and all(0.0 <= x <= 1.0 for x in vals[0])
+    log = next((tmp_path / "tiny").glob("*.log")).read_text()
+    assert "HIP cohort (resnet2d)" in log
+
+
 def test_cli_resnet3d50_runs_on_hip(tmp_path):
     """--model resnet3d_50 on ABCD-shape volumes runs on the client-batched 3D ResNet engine (config 5 family)."""
     from neuroimagedisttraining_amd import cli

@@ -220,10 +220,16 @@ def _run(algo, engine_kind, fed, rounds=2, **kw):
     st, x8, mom, splits = fed
     torch.manual_seed(0)
     model = AlexNet3D_Dropout(num_classes=1)
+    perturb = kw.pop("perturb", 0.0)
+    if perturb:  # chaos control: the same run with the initial weights moved at rounding level
+        g = torch.Generator().manual_seed(99)
+        with torch.no_grad():
+            for p in model.parameters():
+                p.mul_(1 + perturb * torch.randn(p.shape, generator=g))
     if engine_kind == "hip":
         eng = HipEngine(model, x8, mom, st.labels.float(), DEV)
     else:
-        eng = TorchEngine(model, st.volumes, st.labels.float(), DEV)
+        eng = TorchEngine(model, st.volumes, st.labels.float(), DEV, amp=engine_kind == "amp")
     cfg = dict(comm_round=rounds, epochs=2, batch_size=8, lr=0.01, dense_ratio=0.5, seed=3, dropout_keep=1.0,
                frac=1.0, acc_thresh=0.0, each_prune_ratio=0.2, local_epochs=1, dist_thresh=0.0, test_batch=64)
     cfg.update(kw)

@@ -26,6 +26,8 @@ CONVS = [  # cin, cout, k, stride, (D, H, W)
     (256, 512, 1, 2, (9, 11, 9)),
     (1024, 2048, 1, 1, (3, 4, 3)),
     (512, 512, 3, 1, (4, 5, 4)),
+    (64, 128, 3, 2, (8, 10, 8)),    # even extents: every sub-pixel phase full
+    (128, 256, 1, 2, (8, 9, 8)),
 ]
 
 
@@ -52,8 +54,32 @@ def test_gconv3_fwd_dgrad_wgrad(cin, cout, k, stride, dims):
     dx = conv.bwd(dy, x, theta, grads, G)
     torch.cuda.synchronize()
     assert _rel(grads.view(G, cout, cin, k, k, k), wr.grad) < 2e-2
+    if k == 1 and stride == 2:  # half-resolution gradient of the even voxels (res_grad_s2 adds it)
+        g_ = xr.grad
+        assert float(g_[:, :, 1::2].abs().max()) == 0 and float(g_[:, :, :, 1::2].abs().max()) == 0
+        assert float(g_[:, :, :, :, 1::2].abs().max()) == 0
+        assert tuple(dx.shape) == (G * B, *ref.shape[2:], cin)
+        assert _rel(dx.permute(0, 4, 1, 2, 3), g_[:, :, ::2, ::2, ::2]) < 2e-2
+        return
     assert tuple(dx.shape) == tuple(x.shape)
     assert _rel(dx.permute(0, 4, 1, 2, 3), xr.grad) < 2e-2
+
+
+@pytest.mark.parametrize("dims", [(9, 11, 9), (8, 10, 8)])
+def test_res_grad_s2_3d_matches_torch(dims):
+    from neuroimagedisttraining_amd import ops
+    dev = _dev()
+    N, C = 3, 64
+    D, H, W = dims
+    dx1 = torch.randn(N, D, H, W, C, device=dev).to(torch.bfloat16)
+    sub = torch.randn(N, (D + 1) // 2, (H + 1) // 2, (W + 1) // 2, C, device=dev).to(torch.bfloat16)
+    out = torch.empty(N, D, H, W, C, device=dev)
+    ops.ext().res_grad_s2(out.data_ptr(), dx1.data_ptr(), sub.data_ptr(), N, D, H, W, C,
+                          torch.cuda.current_stream().cuda_stream)
+    want = dx1.float().clone()
+    want[:, ::2, ::2, ::2] += sub.float()
+    torch.cuda.synchronize()
+    assert torch.equal(out, want)
 
 
 @pytest.mark.parametrize("C,dims,res", [(64, (6, 7, 6), True), (256, (3, 4, 3), False), (2048, (1, 2, 1), True)])
@@ -167,3 +193,67 @@ def test_resnet3d_lockstep_step_matches_per_client_autograd():
                 assert torch.allclose(bu[g, o:o + Lb.numel(i)], bv[n].float(), atol=2e-2, rtol=5e-2), n
     lg = eng.eval_logits(th, bu, idx, G, B)
     assert lg.shape == (G * B, 1) and torch.isfinite(lg).all()
+
+
+@pytest.mark.parametrize("G,B,dims", [(2, 1, (121, 145, 121)), (2, 2, (21, 26, 22)), (3, 1, (9, 128, 13))])
+def test_stem_hip_fwd_bwd_match_torch(G, B, dims):
+    """stem.hip (polyphase 7^3/s2 conv on MFMA + BN statistics, BN+ReLU+3^3/s2 max-pool, the backward with the MFMA
+    weight gradient) against fp32 PyTorch autograd of Conv3d(1, 64, 7, 2, 3) -> BatchNorm3d -> ReLU -> MaxPool3d,
+    per client; full ABCD extents and odd/even small ones.  The reference rounds the weights and the conv output
+    to bf16 where the HIP path stores them."""
+    from neuroimagedisttraining_amd.engine.resnet3d_hip import GroupedResNet3D
+    from neuroimagedisttraining_amd.engine.executor import padded_rows
+    from neuroimagedisttraining_amd.engine.flat import ParamLayout
+    from neuroimagedisttraining_amd.models.resnet3d import Bottleneck, ResNet3D
+    dev = _dev()
+    torch.manual_seed(G * 100 + dims[0])
+    m = ResNet3D(Bottleneck, [1, 1, 1, 1], 1)
+    L = ParamLayout.from_tensors(list(m.named_parameters()))
+    Lb = ParamLayout.from_tensors(list(m.named_buffers()))
+    net = GroupedResNet3D(L, Lb, dev)
+    N = G * B
+    th = padded_rows(G, L.total, dev)
+    th.copy_(torch.randn(G, L.total, device=dev) * 0.05)
+    o = dict(zip(L.names, L.offsets))
+    th[:, o["bn1.weight"]:o["bn1.weight"] + 64] = 1 + 0.2 * torch.randn(G, 64, device=dev)
+    bu = padded_rows(G, Lb.total, dev)
+    bo = dict(zip(Lb.names, Lb.offsets))
+    bu[:, bo["bn1.running_var"]:bo["bn1.running_var"] + 64] = 1.0
+    store = torch.randint(0, 256, (N + 3, *dims), dtype=torch.uint8, device=dev)
+    idx = torch.randperm(N + 3, device=dev)[:N].to(torch.int32)
+    out, saved = net._stem_hip(store, idx, th, bu, G, True)
+    da = torch.randn(out.shape, device=dev)
+    gr = torch.zeros_like(th)
+    net._stem_hip_bwd(saved, da, th, gr, G)
+    torch.cuda.synchronize()
+    x = store[idx.long()].float().unsqueeze(1) / 255.0
+    for g in range(G):
+        w = th[g, o["conv1.weight"]:o["conv1.weight"] + 64 * 343].view(64, 1, 7, 7, 7).to(torch.bfloat16).float()
+        w.requires_grad_(True)
+        gam = th[g, o["bn1.weight"]:o["bn1.weight"] + 64].clone().requires_grad_(True)
+        bet = th[g, o["bn1.bias"]:o["bn1.bias"] + 64].clone().requires_grad_(True)
+        rm, rv = torch.zeros(64, device=dev), torch.ones(64, device=dev)
+        c = F.conv3d(x[g * B:(g + 1) * B], w, stride=2, padding=3)
+        c = c + (c.to(torch.bfloat16).float() - c).detach()  # bf16 store, straight-through gradient
+        z = F.max_pool3d(torch.relu(F.batch_norm(c, rm, rv, gam, bet, True, 0.1, 1e-5)), 3, 2, 1)
+        ref = z.permute(0, 2, 3, 4, 1)
+        assert tuple(out[g * B:(g + 1) * B].shape) == tuple(ref.shape)
+        assert _rel(out[g * B:(g + 1) * B], ref) < 1e-2, g
+        ref.backward(da[g * B:(g + 1) * B])
+        gw = gr[g, o["conv1.weight"]:o["conv1.weight"] + 64 * 343].view(64, 1, 7, 7, 7)
+        assert _rel(gw, w.grad) < 2e-2, (g, _rel(gw, w.grad))
+        assert _rel(gr[g, o["bn1.weight"]:o["bn1.weight"] + 64], gam.grad) < 2e-2
+        assert _rel(gr[g, o["bn1.bias"]:o["bn1.bias"] + 64], bet.grad) < 1e-2
+        assert torch.allclose(bu[g, bo["bn1.running_mean"]:bo["bn1.running_mean"] + 64], rm, atol=1e-4, rtol=1e-3)
+        assert torch.allclose(bu[g, bo["bn1.running_var"]:bo["bn1.running_var"] + 64], rv, atol=1e-4, rtol=1e-3)
+    # eval mode: the running statistics just written
+    oute, none = net._stem_hip(store, idx, th, bu, G, False)
+    assert none is None
+    for g in range(G):
+        w = th[g, o["conv1.weight"]:o["conv1.weight"] + 64 * 343].view(64, 1, 7, 7, 7).to(torch.bfloat16).float()
+        c = F.conv3d(x[g * B:(g + 1) * B], w, stride=2, padding=3).to(torch.bfloat16).float()
+        z = F.batch_norm(c, bu[g, bo["bn1.running_mean"]:bo["bn1.running_mean"] + 64],
+                         bu[g, bo["bn1.running_var"]:bo["bn1.running_var"] + 64],
+                         th[g, o["bn1.weight"]:o["bn1.weight"] + 64], th[g, o["bn1.bias"]:o["bn1.bias"] + 64], False)
+        ref = F.max_pool3d(torch.relu(z), 3, 2, 1).permute(0, 2, 3, 4, 1)
+        assert _rel(oute[g * B:(g + 1) * B], ref) < 1e-2

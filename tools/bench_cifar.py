@@ -6,10 +6,13 @@ Reference jobs (1x V100): SubAvg ``subavg/subavgsparsitywithoutiteration70sps.sh
 (did not finish 500 rounds in the 2-3 day limit -> < 0.0029 rounds/s, ``DisPFL/error3469448.err``): resnet18,
 cifar10, dir 0.3, batch 16, lr 0.1, lr_decay 0.998, 5 local epochs, dense_ratio 0.3, 100 clients, frac 0.1.
 
-Data: CIFAR-10-shape synthetic uint8 images (50,000 train / 10,000 test, weak class signal), partitioned with the
-reference's ``dir`` partitioner (alpha 0.3: 500 train images per client, label-skewed) and per-client test sets
-drawn from the train label histogram; random-init weights.  No augmentation (the reference's RandomCrop/Flip run
-in its CPU DataLoader).  Usage: ``python tools/bench_cifar.py --algorithm subavg --rounds 3 --warmup 1``.
+Data: CIFAR-10-shape synthetic uint8 images (50,000 train / 10,000 test, weak class signal) — or with ``--dataset
+tiny`` Tiny-ImageNet-shape 64x64 images (100,000 / 10,000, 200 classes; ``tiny_resnet18``, the reference's
+``fedml_experiments/standalone/*/tiny.sh`` presets use batch 128) — partitioned with the reference's ``dir``
+partitioner (alpha 0.3) and per-client test sets drawn from the train label histogram; random-init weights.  The
+reference's train-time RandomCrop(pad 4) + RandomHorizontalFlip run fused into the engine's input stage (on device,
+per step / client / sample draws); ``--no-augment`` turns them off.
+Usage: ``python tools/bench_cifar.py --algorithm subavg --rounds 3 --warmup 1``.
 """
 from __future__ import annotations
 
@@ -43,23 +46,40 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--seed", type=int, default=2022)
     ap.add_argument("--no-eval", action="store_true")
+    ap.add_argument("--dataset", default="cifar10", choices=["cifar10", "tiny"])
+    ap.add_argument("--no-augment", action="store_true")
     args = ap.parse_args()
+    tiny = args.dataset == "tiny"
+    if tiny and args.n_train == 50000:
+        args.n_train = 100000
 
     from neuroimagedisttraining_amd.core import partition as Pt
     from neuroimagedisttraining_amd.engine.executor import ClientSplit, FLConfig
     from neuroimagedisttraining_amd.engine.personalized import make_runner
     from neuroimagedisttraining_amd.engine.resnet2d_hip import ResNetHipEngine, synthetic_cifar
-    from neuroimagedisttraining_amd.models import customized_resnet18
+    from neuroimagedisttraining_amd.models import customized_resnet18, tiny_resnet18
     from neuroimagedisttraining_amd.parallel import runtime as rt
 
     info = rt.init_distributed(prefer_gpu=True)
     torch.manual_seed(args.seed)
     t0 = time.perf_counter()
-    x8, y = synthetic_cifar(args.n_train + args.n_test, seed=args.seed)
+    n_cls = 200 if tiny else 10
+    if tiny:  # 64x64 Tiny-ImageNet-shape images with a weak class signal (same generator rule as synthetic_cifar)
+        g = np.random.default_rng(args.seed)
+        lab = g.integers(0, n_cls, size=args.n_train + args.n_test)
+        proto = g.integers(0, 256, size=(n_cls, 64, 64, 3)).astype(np.float32)
+        x8 = torch.empty(len(lab), 64, 64, 3, dtype=torch.uint8)
+        for s0 in range(0, len(lab), 10000):
+            sl = slice(s0, s0 + 10000)
+            base = g.integers(0, 256, size=(len(lab[sl]), 64, 64, 3)).astype(np.float32)
+            x8[sl] = torch.from_numpy(np.clip(0.7 * base + 0.3 * proto[lab[sl]], 0, 255).astype(np.uint8))
+        y = torch.from_numpy(lab.astype(np.int64))
+    else:
+        x8, y = synthetic_cifar(args.n_train + args.n_test, seed=args.seed)
     ytr, yte = y[:args.n_train].numpy(), y[args.n_train:].numpy()
     rng = np.random.RandomState(args.seed)
-    train_map = Pt.partition_labels("dir", ytr, args.clients, 0.3, n_cls=10, rng=rng)
-    test_map = Pt.per_client_test_indices(ytr, yte, train_map, n_cls=10, rng=rng)
+    train_map = Pt.partition_labels("dir", ytr, args.clients, 0.3, n_cls=n_cls, rng=rng)
+    test_map = Pt.per_client_test_indices(ytr, yte, train_map, n_cls=n_cls, rng=rng)
     splits = []
     for c in range(args.clients):
         tr = np.asarray(train_map[c], dtype=np.int64)
@@ -69,8 +89,8 @@ def main():
             splits.append(ClientSplit(train=tr[nv:], test=te, val=tr[:nv]))
         else:
             splits.append(ClientSplit(train=tr, test=te))
-    model = customized_resnet18(class_num=10)
-    engine = ResNetHipEngine(model, x8, y, info.device)
+    model = (tiny_resnet18 if tiny else customized_resnet18)(class_num=n_cls)
+    engine = ResNetHipEngine(model, x8, y, info.device, augment=not args.no_augment)
     cfg = FLConfig(comm_round=args.warmup + args.rounds, epochs=args.epochs, batch_size=args.batch, lr=args.lr,
                    lr_decay=0.998, dense_ratio=args.dense_ratio, seed=args.seed, frac=args.frac,
                    frequency_of_the_test=0 if args.no_eval else 1, final_round=False)
@@ -102,16 +122,17 @@ def main():
     bound = V100_BOUNDS.get(args.algorithm)
     if info.is_main:
         print(json.dumps({
-            "metric": "FL rounds/sec, %d-client %s ResNet-18-GN on CIFAR-10-shape synth" % (args.clients,
-                                                                                             args.algorithm),
+            "metric": "FL rounds/sec, %d-client %s ResNet-18-GN on %s-shape synth" % (
+                args.clients, args.algorithm, "Tiny-ImageNet" if tiny else "CIFAR-10"),
             "value": round(value, 4), "unit": "rounds/s", "n_gpus": info.world, "rounds": args.rounds,
             "warmup": args.warmup, "s_per_round": round(dt / args.rounds, 3), "dtype": "bf16",
             "data": "synthetic", "setup_s": round(t_setup, 1), "warmup_round_s": [round(w, 2) for w in walls],
             "reference_v100": ({"bound": bound[0] + str(bound[1]), "source": bound[2],
-                                "vs_bound": round(value / bound[1], 1)} if bound else None),
+                                "vs_bound": round(value / bound[1], 1)} if (bound and not tiny) else None),
             "config": {"model": "resnet18 (GroupNorm32)", "clients": args.clients, "frac": args.frac,
                        "epochs": args.epochs, "batch": args.batch, "lr": args.lr, "dense_ratio": args.dense_ratio,
-                       "partition": "dir 0.3", "train_images": args.n_train, "eval_every_round": not args.no_eval},
+                       "partition": "dir 0.3", "train_images": args.n_train, "eval_every_round": not args.no_eval,
+                       "dataset": args.dataset, "augment": not args.no_augment},
             "last_round_metrics": res}), flush=True)
     rt.shutdown(info)
 
