@@ -30,11 +30,11 @@ constexpr int kK1 = 224;                              // padded k (27 taps x 8 p
 constexpr int kNM = 125 + 125 * 125;                  // per-sample moment vector length
 
 // phase r = (rd<<2)|(rh<<1)|rw ; tap t = jd*9+jh*3+jw ; original k = kd*25+kh*5+kw with kd = 2 jd + rd
-__host__ __device__ __forceinline__ bool tp_valid(int t, int r) {
+__host__ __device__ constexpr bool tp_valid(int t, int r) {
   const int jd = t / 9, jh = (t / 3) % 3, jw = t % 3;
   return (2 * jd + (r >> 2) < 5) && (2 * jh + ((r >> 1) & 1) < 5) && (2 * jw + (r & 1) < 5);
 }
-__host__ __device__ __forceinline__ int tp_to_k(int t, int r) {
+__host__ __device__ constexpr int tp_to_k(int t, int r) {
   const int jd = t / 9, jh = (t / 3) % 3, jw = t % 3;
   return (2 * jd + (r >> 2)) * 25 + (2 * jh + ((r >> 1) & 1)) * 5 + (2 * jw + (r & 1));
 }
@@ -776,10 +776,15 @@ __device__ __forceinline__ void conv1_wg_load(const uint32_t* meta, const uint2*
   const uint32_t m = meta[it * kC1 + c];
   dz = bf16_to_f32((uint16_t)(m & 0xffffu));
   const uint2* base = halo + (m >> 16);
+  // volatile 8-B LDS reads (lds_u64, below): one ds_read_b64 per tap group, in this order.  Plain loads of
+  // neighbouring voxels are merged by the compiler into ds_read2_b64, which costs 8 LDS cycles for 16 B (two
+  // ds_read_b64: 4) and banks by (a/4) mod 32, so the padded strides no longer keep the 27 argmax offsets apart
 #pragma unroll
   for (int i = 0; i < SET::n; ++i) {
     const int t = SET::t(i);
-    u[i] = base[(t / 9) * kWgZS + ((t / 3) % 3) * kWgRS + t % 3];
+    const uint64_t v = ((const volatile __attribute__((address_space(3))) uint64_t*)base)[(t / 9) * kWgZS +
+                                                                                        ((t / 3) % 3) * kWgRS + t % 3];
+    u[i] = make_uint2((uint32_t)v, (uint32_t)(v >> 32));
   }
 }
 
@@ -907,6 +912,236 @@ __global__ __launch_bounds__(256) void k_conv1_wgrad_split(const uint8_t* __rest
   }
 }
 
+// k_conv1_wgrad_dot — the same sparse wgrad with CELL-PAIRED bf16 dot products: uint8 inputs are exact in bf16, so
+// the halo is staged once per stage as bf16 (two planes of 4 phases, each an 8-B voxel read with the padded strides
+// above: the 27 argmax offsets stay on 27 distinct bank pairs), and each lane takes two cells at a time:
+// v_perm_b32 interleaves the two cells' values of a tap into one bf16 pair and v_dot2c_f32_bf16 adds both products
+// to the tap's fp32 accumulator — 1 VALU per MAC (one perm + one dot2 per two MACs) instead of 1.5
+// (v_cvt_f32_ubyte per value + half a v_pk_fma_f32).  The dz pair (bf16, as stored) is one perm per cell pair.
+__device__ __forceinline__ uint32_t bf2_pack(float lo, float hi) {  // exact for integers < 257
+  return __builtin_amdgcn_perm(__float_as_uint(hi), __float_as_uint(lo), 0x07060302u);
+}
+typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ float dot2bf(uint32_t a, uint32_t b, float c) {
+  return __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2v, a), __builtin_bit_cast(bf16x2v, b), c, false);
+}
+
+// the 8-B halo reads of one cell for a wave's tap set: phases 0-3 (hlo) of every group that has a live tap there,
+// then phases 4-7 (hhi)
+template <class SET>
+__device__ constexpr int wd_nreads() {
+  int n = 0;
+  for (int h = 0; h < 2; ++h)
+    for (int i = 0; i < SET::n; ++i) {
+      bool need = false;
+      for (int r = 0; r < 4; ++r) need = need || tp_valid(SET::t(i), 4 * h + r);
+      n += need ? 1 : 0;
+    }
+  return n;
+}
+
+// volatile 8-B reads: one ds_read_b64 each (2 LDS cycles, 64-bank rule), issued in this order.  Plain loads of
+// neighbouring voxels get merged into ds_read2_b64 (8 cycles for the same 16 B, 32-bank rule: the padded strides
+// no longer separate the argmax offsets) or split into ds_read2_b32.
+typedef const volatile __attribute__((address_space(3))) uint64_t lds_u64;
+template <class SET, int NR>
+__device__ __forceinline__ void conv1_wd_load(const uint2* hlo, const uint2* hhi, uint32_t m, uint64_t (&v)[NR]) {
+  int k = 0;
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int i = 0; i < SET::n; ++i) {
+      const int t = SET::t(i);
+      bool need = false;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) need = need || tp_valid(t, 4 * h + r);
+      if (!need) continue;
+      const int off = (t / 9) * kWgZS + ((t / 3) % 3) * kWgRS + t % 3;
+      v[k++] = ((lds_u64*)((h ? hhi : hlo) + (m >> 16)))[off];
+    }
+}
+
+template <class SET, int NR>
+__device__ __forceinline__ void conv1_wd_fma(uint32_t dzp, const uint64_t (&a)[NR], const uint64_t (&b)[NR], float* S) {
+  int k = 0, slot = 0;
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int i = 0; i < SET::n; ++i) {
+      const int t = SET::t(i);
+      bool need = false;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) need = need || tp_valid(t, 4 * h + r);
+      if (!need) continue;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const uint32_t aj = (uint32_t)(a[k] >> (32 * j)), bj = (uint32_t)(b[k] >> (32 * j));
+        if (tp_valid(t, 4 * h + 2 * j)) {
+          S[slot] = dot2bf(dzp, __builtin_amdgcn_perm(bj, aj, 0x05040100u), S[slot]);
+          ++slot;
+        }
+        if (tp_valid(t, 4 * h + 2 * j + 1)) {
+          S[slot] = dot2bf(dzp, __builtin_amdgcn_perm(bj, aj, 0x07060302u), S[slot]);
+          ++slot;
+        }
+      }
+      ++k;
+    }
+}
+
+// slot order of the accumulators: phases 0-3 of every group of the set, then phases 4-7 (conv1_wd_half order)
+template <class SET>
+__device__ __forceinline__ void conv1_wd_store(const float* S, float* op) {
+  int slot = 0;
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int i = 0; i < SET::n; ++i) {
+      const int t = SET::t(i);
+      bool need = false;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) need = need || tp_valid(t, 4 * h + r);
+      if (!need) continue;
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (tp_valid(t, 4 * h + r)) op[tp_to_k(t, 4 * h + r)] = S[slot++];
+    }
+}
+
+template <int W>
+__device__ __forceinline__ void conv1_wd_wave(const uint8_t* __restrict__ xs, const uint16_t* __restrict__ dp,
+                                              const uint16_t* __restrict__ pout, const uint8_t* __restrict__ amax,
+                                              float* __restrict__ part, uint2* hlo, uint2* hhi, uint32_t* meta, int n,
+                                              int pd, int tid, int c, int ph_begin, int ph_end, int slab) {
+  using SET = WgSet<W>;
+  constexpr int NS = 32;
+  float S[NS];
+#pragma unroll
+  for (int k = 0; k < NS; ++k) S[k] = 0.f;
+  float Dsum = 0.f;
+  const int64_t rowbase = ((int64_t)n * kPD + pd) * kPH;
+  // the next stage's global reads (halo voxels, pooled value / gradient / argmax per (cell, channel)) are issued into
+  // registers before this stage's dot products and written to LDS after them: with 54 KB of LDS per block only 2
+  // blocks share a CU, too few to cover the staging latency by switching blocks
+  constexpr int kHV = (5 * kWgHY * 64 + 255) / 256, kMV = (kWgMeta + 255) / 256;
+  uint2 hv[kHV];
+  uint16_t pvr[kMV], gvr[kMV];
+  uint8_t avr[kMV];
+  auto prefetch = [&](int ph0) {
+    const int nph = min(kWgRows, ph_end - ph0), ny = 3 * nph + 2, ncell = nph * kPW;
+    const int64_t obase = ((rowbase + ph0) * kPW) * kC1;
+#pragma unroll
+    for (int k = 0; k < kHV; ++k) {
+      const int e = tid + 256 * k;
+      const int xh = e & 63, r = e >> 6, yh = r % ny, zh = r / ny;
+      hv[k] = make_uint2(0, 0);
+      if (e < 5 * ny * 64 && xh < kPX)
+        hv[k] = *reinterpret_cast<const uint2*>(xs + (((int64_t)(3 * pd + zh) * kPY + 3 * ph0 + yh) * kPX + xh) * 8);
+    }
+#pragma unroll
+    for (int k = 0; k < kMV; ++k) {
+      const int e = tid + 256 * k;
+      if (e < ncell * kC1) {
+        pvr[k] = pout[obase + e];
+        gvr[k] = dp[obase + e];
+        avr[k] = amax[obase + e];
+      }
+    }
+  };
+  auto commit = [&](int ph0) {
+    const int nph = min(kWgRows, ph_end - ph0), ny = 3 * nph + 2, ncell = nph * kPW;
+#pragma unroll
+    for (int k = 0; k < kHV; ++k) {
+      const int e = tid + 256 * k;
+      if (e < 5 * ny * 64) {
+        const int xh = e & 63, r = e >> 6, yh = r % ny, zh = r / ny;
+        const int hi = zh * kWgZS + yh * kWgRS + xh;
+        const uint2 v = hv[k];
+        hlo[hi] = make_uint2(bf2_pack(u8f(v.x, 0), u8f(v.x, 1)), bf2_pack(u8f(v.x, 2), u8f(v.x, 3)));
+        hhi[hi] = make_uint2(bf2_pack(u8f(v.y, 0), u8f(v.y, 1)), bf2_pack(u8f(v.y, 2), u8f(v.y, 3)));
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < kMV; ++k) {
+      const int e = tid + 256 * k;
+      if (e < ncell * kC1) {
+        const int cell = e >> 6, a = avr[k];
+        const int phl = cell / kPW, pw = cell - phl * kPW;
+        const int off = (a / 9) * kWgZS + (3 * phl + (a / 3) % 3) * kWgRS + 3 * pw + a % 3;
+        const uint32_t dzb = bf16_to_f32(pvr[k]) > 0.f ? (uint32_t)gvr[k] : 0u;
+        meta[e] = dzb | ((uint32_t)off << 16);
+      }
+    }
+  };
+  prefetch(ph_begin);
+  for (int ph0 = ph_begin; ph0 < ph_end; ph0 += kWgRows) {
+    const int nph = min(kWgRows, ph_end - ph0);
+    const int ncell = nph * kPW;
+    __syncthreads();  // previous stage's reads done
+    commit(ph0);
+    __syncthreads();
+    if (ph0 + kWgRows < ph_end) prefetch(ph0 + kWgRows);
+    // two cells per step; the next pair's halo reads are issued before this pair's dot products (registers X/Y
+    // alternate, so no copies)
+    constexpr int NR = wd_nreads<SET>();
+    auto pair_meta = [&](int it, uint32_t& m0, uint32_t& m1) {
+      m0 = meta[it * kC1 + c];
+      m1 = it + 1 < ncell ? meta[(it + 1) * kC1 + c] : (m0 & 0xffff0000u);  // odd tail: dz = 0
+    };
+    auto pair_fma = [&](uint32_t m0, uint32_t m1, const uint64_t (&a)[NR], const uint64_t (&b)[NR]) {
+      if (W == 0) Dsum += bf16_to_f32((uint16_t)(m0 & 0xffffu)) + bf16_to_f32((uint16_t)(m1 & 0xffffu));
+      conv1_wd_fma<SET, NR>(__builtin_amdgcn_perm(m1, m0, 0x05040100u), a, b, S);  // dz pair (dz0, dz1)
+    };
+    uint64_t xa[NR], xb[NR], ya[NR], yb[NR];
+    uint32_t xm0, xm1, ym0, ym1;
+    pair_meta(0, xm0, xm1);
+    conv1_wd_load<SET, NR>(hlo, hhi, xm0, xa);
+    conv1_wd_load<SET, NR>(hlo, hhi, xm1, xb);
+    for (int it = 0; it < ncell; it += 4) {
+      const bool more1 = it + 2 < ncell, more2 = it + 4 < ncell;
+      if (more1) {
+        pair_meta(it + 2, ym0, ym1);
+        conv1_wd_load<SET, NR>(hlo, hhi, ym0, ya);
+        conv1_wd_load<SET, NR>(hlo, hhi, ym1, yb);
+      }
+      pair_fma(xm0, xm1, xa, xb);
+      if (!more1) break;
+      if (more2) {
+        pair_meta(it + 4, xm0, xm1);
+        conv1_wd_load<SET, NR>(hlo, hhi, xm0, xa);
+        conv1_wd_load<SET, NR>(hlo, hhi, xm1, xb);
+      }
+      pair_fma(ym0, ym1, ya, yb);
+    }
+  }
+  float* op = part + ((int64_t)slab * kC1 + c) * 126;
+  conv1_wd_store<SET>(S, op);
+  if (W == 0) op[125] = Dsum;
+}
+
+__global__ __launch_bounds__(256, 2) void k_conv1_wgrad_dot(const uint8_t* __restrict__ x8, const int* __restrict__ idx,
+                                                         const uint16_t* __restrict__ dp,
+                                                         const uint16_t* __restrict__ pout,
+                                                         const uint8_t* __restrict__ amax, float* __restrict__ part,
+                                                         int nq) {
+  __shared__ __attribute__((aligned(256))) uint2 hlo[kWgHalo];
+  __shared__ __attribute__((aligned(256))) uint2 hhi[kWgHalo];
+  __shared__ uint32_t meta[kWgMeta];
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int q = bid % nq, rest = bid / nq;
+  const int pd = rest % kPD, n = rest / kPD;
+  const int rq = ((kPH + nq - 1) / nq + kWgRows - 1) / kWgRows * kWgRows;
+  const int ph_begin = q * rq, ph_end = min(kPH, ph_begin + rq);
+  const int tid = threadIdx.x, c = tid & 63, wid = tid >> 6;
+  const uint8_t* xs = x8 + (int64_t)idx[n] * kPZ * kPY * kPX * 8;
+  switch (wid) {
+    case 0: conv1_wd_wave<0>(xs, dp, pout, amax, part, hlo, hhi, meta, n, pd, tid, c, ph_begin, ph_end, bid_slab(rest, q, nq)); break;
+    case 1: conv1_wd_wave<1>(xs, dp, pout, amax, part, hlo, hhi, meta, n, pd, tid, c, ph_begin, ph_end, bid_slab(rest, q, nq)); break;
+    case 2: conv1_wd_wave<2>(xs, dp, pout, amax, part, hlo, hhi, meta, n, pd, tid, c, ph_begin, ph_end, bid_slab(rest, q, nq)); break;
+    default: conv1_wd_wave<3>(xs, dp, pout, amax, part, hlo, hhi, meta, n, pd, tid, c, ph_begin, ph_end, bid_slab(rest, q, nq)); break;
+  }
+}
+
 int conv1_wgrad_nq(int NB) { return (int64_t)NB * kPD < 4 * 256 * 4 ? 2 : 1; }
 
 void conv1_wgrad(uintptr_t x8, uintptr_t idx, uintptr_t dp, uintptr_t pout, uintptr_t amax, int NB, int B,
@@ -920,11 +1155,21 @@ void conv1_wgrad(uintptr_t x8, uintptr_t idx, uintptr_t dp, uintptr_t pout, uint
     const char* e = getenv("NIDT_C1WG_UNROLL");
     return e ? atoi(e) : 1;
   }();
+  // NIDT_C1WG_DOT=1: the cell-paired bf16 dot-product kernel (A/B record: 4.52 ms vs 3.98 ms for this one at
+  // 64 clients, profiles/r3_ab_conv1_wgrad_dot.txt — v_dot2c_f32_bf16 does not issue at the v_fma rate)
+  static const bool dot = [] {
+    const char* e = getenv("NIDT_C1WG_DOT");
+    return e && atoi(e) == 1;
+  }();
 #define NIDT_C1WG(U)                                                                                                \
   hipLaunchKernelGGL(k_conv1_wgrad_split<U>, dim3(kPD * NB * nq), dim3(256), 0, s, ptr<const uint8_t>(x8),          \
                      ptr<const int>(idx), ptr<const uint16_t>(dp), ptr<const uint16_t>(pout), ptr<const uint8_t>(amax), \
                      ptr<float>(part), nq)
-  if (unr == 4) NIDT_C1WG(4); else if (unr == 2) NIDT_C1WG(2); else NIDT_C1WG(1);
+  if (dot)
+    hipLaunchKernelGGL(k_conv1_wgrad_dot, dim3(kPD * NB * nq), dim3(256), 0, s, ptr<const uint8_t>(x8),
+                       ptr<const int>(idx), ptr<const uint16_t>(dp), ptr<const uint16_t>(pout),
+                       ptr<const uint8_t>(amax), ptr<float>(part), nq);
+  else if (unr == 4) NIDT_C1WG(4); else if (unr == 2) NIDT_C1WG(2); else NIDT_C1WG(1);
 #undef NIDT_C1WG
   NIDT_CHECK(hipGetLastError());
   const int G = NB / B;

@@ -144,6 +144,7 @@ class GroupedConv:
         self.need_dgrad = self.cin_p == self.cin  # the (channel-padded) stem needs no input gradient
         self.slots = tap_slots(self.kt, stride)
         self.wp = self.wt = None  # packed images of the current step (WeightPacker.pack)
+        self._ptabs = {}  # wgrad output-position tables per (B, H, W)
 
     def out_hw(self, h, w):
         return ((h + 2 * self.pad - self.k) // self.stride + 1, (w + 2 * self.pad - self.k) // self.stride + 1)
@@ -202,8 +203,7 @@ class GroupedConv:
         dy = dy.contiguous()
         ns = m.conv_wgrad_nsplit_g(G, B, 1, H, W, self.cin_p, self.cout, self.kt, self.stride, self.pad, 0)
         part = torch.empty(ns * G * self.cout * self.kt * self.cin_p, device=x.device, dtype=torch.float32)
-        ptab = torch.empty(B * Ho * Wo, 2, device=x.device, dtype=torch.int32)
-        m.conv_pos_table_g(ptab.data_ptr(), B, 1, H, W, self.kt, self.stride, self.pad, 0, st)
+        ptab = self._pos_table(B, H, W, Ho, Wo, x.device)
         if self.cin_p == self.cin:
             m.conv_wgrad_g(x.data_ptr(), dy.data_ptr(), part.data_ptr(), grads.data_ptr(), grads.stride(0), self.off,
                            G, B, 1, H, W, self.cin_p, self.cout, self.kt, self.stride, self.pad, 0, ns, 1.0,
@@ -240,6 +240,18 @@ class GroupedConv:
         conv_fwd(dy.data_ptr(), wt.data_ptr(), sub.data_ptr(), G, B, 1, Ho, Wo, self.cout, self.cin_p, 1, 1,
                  0, 0, x.device)
         return sub
+
+    def _pos_table(self, B, H, W, Ho, Wo, device):
+        """Output-position table of the wgrad kernel: a function of the shape only, built once per (B, H, W) outside
+        graph capture (inside a capture it is rebuilt by the captured launch, as before)."""
+        key = (B, H, W)
+        tab = self._ptabs.get(key)
+        if tab is None:
+            tab = torch.empty(B * Ho * Wo, 2, device=device, dtype=torch.int32)
+            ops.ext().conv_pos_table_g(tab.data_ptr(), B, 1, H, W, self.kt, self.stride, self.pad, 0, _stream())
+            if not torch.cuda.is_current_stream_capturing():
+                self._ptabs[key] = tab
+        return tab
 
     def _torch_bwd(self, dy, x, theta, grads, G, need_dx):
         w = self._wtorch(theta, G).detach().clone().requires_grad_(True)

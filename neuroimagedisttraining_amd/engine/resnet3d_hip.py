@@ -65,6 +65,7 @@ class GConv3:
         self.numel = cout * cin * self.kt
         self.slots = list(ops.ext().conv_tap_slots(self.kt, stride)) if hip else None
         self.wp = self.wt = None
+        self._ptabs = {}
 
     def out_dims(self, d, h, w):
         f = lambda n: (n + 2 * self.pad - self.k) // self.stride + 1  # noqa: E731
@@ -124,8 +125,13 @@ class GConv3:
         padd = self.pad if self.kt == 27 else 0
         ns = m.conv_wgrad_nsplit_g(G, B, D, H, W, self.cin, self.cout, self.kt, self.stride, self.pad, padd)
         part = torch.empty(ns * G * self.cout * self.kt * self.cin, device=x.device, dtype=torch.float32)
-        ptab = torch.empty(B * Do * Ho * Wo, 2, device=x.device, dtype=torch.int32)
-        m.conv_pos_table_g(ptab.data_ptr(), B, D, H, W, self.kt, self.stride, self.pad, padd, st)
+        key = (B, D, H, W)
+        ptab = self._ptabs.get(key)
+        if ptab is None:  # a function of the shape only: built once per (B, D, H, W)
+            ptab = torch.empty(B * Do * Ho * Wo, 2, device=x.device, dtype=torch.int32)
+            m.conv_pos_table_g(ptab.data_ptr(), B, D, H, W, self.kt, self.stride, self.pad, padd, st)
+            if not torch.cuda.is_current_stream_capturing():
+                self._ptabs[key] = ptab
         m.conv_wgrad_g(x.data_ptr(), dy.data_ptr(), part.data_ptr(), grads.data_ptr(), grads.stride(0), self.off, G,
                        B, D, H, W, self.cin, self.cout, self.kt, self.stride, self.pad, padd, ns, 1.0, ptab.data_ptr(),
                        st)

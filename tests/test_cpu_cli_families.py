@@ -25,7 +25,8 @@ def _args(algo, argv):
     ("ditto", ["--dataset", "cifar100"], "resnet2d"),
     ("fedavg", ["--model", "resnet3d_50"], "resnet3d"),
     ("subavg", ["--model", "vgg11"], None),
-    ("local", ["--dataset", "tiny"], None),
+    ("local", ["--dataset", "tiny"], "resnet2d"),  # tiny_resnet18 (64x64, 200 classes) on the same engine
+    ("local", ["--dataset", "tiny", "--model", "vgg16"], None),
 ])
 def test_hip_family_routes_reference_defaults(algo, argv, fam):
     from neuroimagedisttraining_amd import cli
@@ -48,7 +49,7 @@ def test_image_cohort_matches_eager_loader_splits(algo):
     args = _args(algo, ["--client_num_in_total", "5", "--synthetic_size", "500", "--seed", "3"])
     x8, y, splits, n_cls = cli.image_cohort(args, DistInfo(), with_val=algo == "fedfomo")
     ds = images.load_partition_data("cifar10", "", "dir", 0.3, 5, 16, n_train=500, n_test=100, seed=3,
-                                    with_val=algo == "fedfomo")
+                                    with_val=algo == "fedfomo", augment=False)  # un-augmented pixels to compare
     assert n_cls == 10 and x8.dtype == torch.uint8 and tuple(x8.shape) == (600, 32, 32, 3)
     num, trn = ds[4], ds[5]
     tst = ds[7] if algo == "fedfomo" else ds[6]

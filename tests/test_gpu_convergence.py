@@ -1,8 +1,9 @@
 """Convergence parity of the bf16 HIP engine against the fp32 PyTorch engine over a multi-round federation.
 
 The default synthetic cohort is too easy to reveal a numerics regression (accuracy saturates at 1.0), so this test
-uses a weak label signal: the fp32 reference only reaches ~0.7-0.9 accuracy, and the HIP engine's global
-loss / accuracy trajectories must track it.  6 clients, SalientGrads (SNIP mask + masked FedAvg), 20 rounds, every
+uses a weak label signal: the fp32 reference needs ~10 rounds to leave the majority-class plateau, and the HIP
+engine's global loss / accuracy trajectories must track it (round by round before the transition, without lagging
+after it).  6 clients, SalientGrads (SNIP mask + masked FedAvg), 20 rounds, every
 round evaluated."""
 import os
 
@@ -50,10 +51,16 @@ def test_hip_bf16_tracks_fp32_over_twenty_rounds():
     print("bf16 acc ", np.round(acc_h, 3).tolist())
     print("fp32 loss", np.round(loss_t, 4).tolist())
     print("bf16 loss", np.round(loss_h, 4).tolist())
-    # learning is unstable at the transition (both engines oscillate between the majority class and ~0.9 for a few
-    # rounds), so trajectories are compared on window means, the early rounds point by point
+    # learning is chaotic at the transition off the majority-class plateau (rounds ~10-15): two fp32 runs whose
+    # initial weights differ by 1e-6 relative noise end up to 6.7 % apart in loss there, bf16 autocast 4.8 %
+    # (tools/convergence_ablation.py, profiles/r3_convergence_ablation.txt).  Before it the trajectories are
+    # deterministic functions of the numerics and are compared round by round; after it, on window means, one-sided
+    # where the question is "does bf16 lag fp32".
     assert np.mean(acc_t[-10:]) < 0.97, "cohort too easy: the comparison would not see a numerics regression"
     assert acc_t[-5:].max() > 0.85 and acc_h[-5:].max() > 0.85, "both engines must learn the task"
-    assert abs(np.mean(acc_h[-10:]) - np.mean(acc_t[-10:])) <= 0.08
-    assert np.max(np.abs(loss_h[:10] - loss_t[:10]) / loss_t[:10]) <= 0.02
-    assert abs(np.mean(loss_h[-5:]) - np.mean(loss_t[-5:])) / np.mean(loss_t[-5:]) <= 0.1
+    assert np.max(np.abs(loss_h[:10] - loss_t[:10]) / loss_t[:10]) <= 0.03       # ablation: 0.018 (chaos ctl 0.017)
+    first = lambda a: int(np.argmax(a >= 0.7)) if (a >= 0.7).any() else len(a)  # noqa: E731
+    assert first(acc_h) <= first(acc_t) + 2, "bf16 leaves the plateau later than fp32"
+    assert np.mean(acc_h[-5:]) >= np.mean(acc_t[-5:]) - 0.05                     # no accuracy lag
+    assert abs(np.mean(acc_h[-5:]) - np.mean(acc_t[-5:])) <= 0.1
+    assert np.mean(loss_h[-5:]) <= 1.05 * np.mean(loss_t[-5:])                   # no loss lag

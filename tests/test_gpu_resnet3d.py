@@ -170,6 +170,8 @@ def test_resnet3d_lockstep_step_matches_per_client_autograd():
     torch.cuda.synchronize()
     mref = _bf16_faithful(resnet3d_50(num_classes=1).to(dev))
     mref.train()
+    ctx = torch.backends.cudnn.flags(enabled=False)  # native BN backward (see test_stem_hip_fwd_bwd_match_torch)
+    ctx.__enter__()
     conv_names = {n + ".weight" for n, mod in mref.named_modules() if isinstance(mod, torch.nn.Conv3d)}
     for g in range(G):
         row = flat.clone().requires_grad_(True)
@@ -177,7 +179,7 @@ def test_resnet3d_lockstep_step_matches_per_client_autograd():
                   row[o:o + L.numel(i)].view(L.shapes[i])) for i, (n, o) in enumerate(zip(L.names, L.offsets))}
         bv = {n: bflat[o:o + Lb.numel(i)].view(Lb.shapes[i]).clone().to(Lb.dtypes[i])
               for i, (n, o) in enumerate(zip(Lb.names, Lb.offsets))}
-        x = (vol[g * B:(g + 1) * B].float().unsqueeze(1) / 255.0).to(torch.bfloat16).float()
+        x = vol[g * B:(g + 1) * B].float().unsqueeze(1) / 255.0  # the HIP stem reads exact uint8 values
         out = functional_call(mref, {**pv, **bv}, (x,))
         loss = F.binary_cross_entropy_with_logits(out.view(-1), lab[g * B:(g + 1) * B])
         loss.backward()
@@ -191,6 +193,7 @@ def test_resnet3d_lockstep_step_matches_per_client_autograd():
         for i, (n, o) in enumerate(zip(Lb.names, Lb.offsets)):
             if n.endswith("running_mean"):
                 assert torch.allclose(bu[g, o:o + Lb.numel(i)], bv[n].float(), atol=2e-2, rtol=5e-2), n
+    ctx.__exit__(None, None, None)
     lg = eng.eval_logits(th, bu, idx, G, B)
     assert lg.shape == (G * B, 1) and torch.isfinite(lg).all()
 
@@ -227,6 +230,11 @@ def test_stem_hip_fwd_bwd_match_torch(G, B, dims):
     net._stem_hip_bwd(saved, da, th, gr, G)
     torch.cuda.synchronize()
     x = store[idx.long()].float().unsqueeze(1) / 255.0
+    # PyTorch's native kernels, not MIOpen: MIOpen's BatchNorm backward misses part of dbeta for some channels at
+    # these small shapes (sum of the BN-output gradient != beta.grad by a constant), which the weight gradient of
+    # the conv below amplifies (tools/debug/stem_debug.py, profiles/r3_stem_debug.txt)
+    ctx = torch.backends.cudnn.flags(enabled=False)
+    ctx.__enter__()
     for g in range(G):
         w = th[g, o["conv1.weight"]:o["conv1.weight"] + 64 * 343].view(64, 1, 7, 7, 7).to(torch.bfloat16).float()
         w.requires_grad_(True)
@@ -257,3 +265,4 @@ def test_stem_hip_fwd_bwd_match_torch(G, B, dims):
                          th[g, o["bn1.weight"]:o["bn1.weight"] + 64], th[g, o["bn1.bias"]:o["bn1.bias"] + 64], False)
         ref = F.max_pool3d(torch.relu(z), 3, 2, 1).permute(0, 2, 3, 4, 1)
         assert _rel(oute[g * B:(g + 1) * B], ref) < 1e-2
+    ctx.__exit__(None, None, None)
