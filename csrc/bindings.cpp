@@ -71,8 +71,10 @@ void gn_bwd(uintptr_t dy, int dy_bf16, uintptr_t mask, uintptr_t t, uintptr_t st
             int64_t off_w, uintptr_t dt, uintptr_t part, int N, int B, int S, int C, uintptr_t stream);
 void gn_param_grads(uintptr_t part, int G, int B, int C, uintptr_t grads, int64_t ldg, int64_t off_w, int64_t off_b,
                     uintptr_t stream);
-void res_grad(uintptr_t out, uintptr_t dx1, uintptr_t dx2, uintptr_t da, uintptr_t mask, int64_t n, uintptr_t stream);
-void res_grad_s2(uintptr_t out, uintptr_t dx1, uintptr_t dx2s, int N, int D, int H, int W, int C, uintptr_t stream);
+void res_grad(uintptr_t out, uintptr_t dx1, uintptr_t dx2, uintptr_t da, uintptr_t mask, int64_t n, int flags,
+              uintptr_t stream);
+void res_grad_s2(uintptr_t out, uintptr_t dx1, uintptr_t dx2s, int N, int D, int H, int W, int C, int out_bf16,
+                 uintptr_t stream);
 // img.hip
 void img_input(uintptr_t src, uintptr_t idx, uintptr_t out, int N, int H, int W, int CP, float m0, float m1, float m2,
                float s0, float s1, float s2, int aug, int pad, uintptr_t seed_dev, int64_t seed_base, uintptr_t cids,
@@ -152,6 +154,8 @@ void seg_prune(uintptr_t tiles, int ntiles, uintptr_t v, int64_t ldv, uintptr_t 
 void masked_rows_sum(uintptr_t rows, int64_t ld, uintptr_t bits, int64_t mstride, int R, int64_t n, uintptr_t sum,
                      uintptr_t cnt, uintptr_t stream);
 void mix_rows(uintptr_t src, uintptr_t wts, uintptr_t rowptr, uintptr_t dst, int R, int64_t n, uintptr_t stream);
+void masked_mean_rows(uintptr_t src, uintptr_t sbits, uintptr_t rp, uintptr_t dst, uintptr_t own, int R, int64_t n,
+                      uintptr_t stream);
 int pair_sqdist_nblk(int64_t n);
 void pair_sqdist(uintptr_t pa, uintptr_t pb, int K, int64_t n, uintptr_t part, uintptr_t stream);
 void stem_polyphase(uintptr_t src, uintptr_t idx, int N, int D, int H, int W, uintptr_t xp, uintptr_t xq,
@@ -244,6 +248,7 @@ PYBIND11_MODULE(_nidt_hip, m) {
   DEF(seg_prune);
   DEF(masked_rows_sum);
   DEF(mix_rows);
+  DEF(masked_mean_rows);
   DEF(pair_sqdist_nblk);
   DEF(pair_sqdist);
   DEF(stem_polyphase);

@@ -47,39 +47,68 @@ __global__ __launch_bounds__(kBnrThreads) void k_bnr_partial(const uint16_t* __r
       rs[e] = stats[((int64_t)g * C + 8 * j + e) * 2 + 1];
     }
   }
-  if (r < rows) {
-    for (int p = p0 + r; p < p1; p += rows) {
-      const int64_t o = base + (int64_t)p * C + 8 * j;
-      float f[8];
-      bnr_unpack8(*reinterpret_cast<const uint4*>(t + o), f);
-      if (MODE == 0) {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          a[e] += f[e];
-          b[e] = fmaf(f[e], f[e], b[e]);
-        }
+  // per position: the t chunk, and for MODE 1 the dy / mask chunks; four positions' loads are issued before
+  // their arithmetic (a thread walks ~kBnrChunk / rows positions, one dependent HBM round trip each otherwise)
+  struct Ld {
+    uint4 t, m, d0, d1;
+  };
+  auto load = [&](int p) {
+    Ld v;
+    const int64_t o = base + (int64_t)p * C + 8 * j;
+    v.t = *reinterpret_cast<const uint4*>(t + o);
+    if (MODE == 1) {
+      if (DYB) {
+        v.d0 = *reinterpret_cast<const uint4*>(reinterpret_cast<const uint16_t*>(dyv) + o);
       } else {
-        float d[8];
-        if (DYB) {
-          bnr_unpack8(*reinterpret_cast<const uint4*>(reinterpret_cast<const uint16_t*>(dyv) + o), d);
-        } else {
-          const float4* q = reinterpret_cast<const float4*>(reinterpret_cast<const float*>(dyv) + o);
-          const float4 x0 = q[0], x1 = q[1];
-          d[0] = x0.x; d[1] = x0.y; d[2] = x0.z; d[3] = x0.w; d[4] = x1.x; d[5] = x1.y; d[6] = x1.z; d[7] = x1.w;
-        }
-        if (mask) {
-          float mk[8];
-          bnr_unpack8(*reinterpret_cast<const uint4*>(mask + o), mk);
+        const uint4* q = reinterpret_cast<const uint4*>(reinterpret_cast<const float*>(dyv) + o);
+        v.d0 = q[0];
+        v.d1 = q[1];
+      }
+      if (mask) v.m = *reinterpret_cast<const uint4*>(mask + o);
+    }
+    return v;
+  };
+  auto step = [&](const Ld& v) {
+    float f[8];
+    bnr_unpack8(v.t, f);
+    if (MODE == 0) {
 #pragma unroll
-          for (int e = 0; e < 8; ++e) d[e] = mk[e] > 0.f ? d[e] : 0.f;
-        }
+      for (int e = 0; e < 8; ++e) {
+        a[e] += f[e];
+        b[e] = fmaf(f[e], f[e], b[e]);
+      }
+    } else {
+      float d[8];
+      if (DYB) {
+        bnr_unpack8(v.d0, d);
+      } else {
+        const uint32_t u[8] = {v.d0.x, v.d0.y, v.d0.z, v.d0.w, v.d1.x, v.d1.y, v.d1.z, v.d1.w};
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          a[e] += d[e];
-          b[e] = fmaf(d[e], (f[e] - mu[e]) * rs[e], b[e]);
-        }
+        for (int e = 0; e < 8; ++e) d[e] = __uint_as_float(u[e]);
+      }
+      if (mask) {
+        float mk[8];
+        bnr_unpack8(v.m, mk);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) d[e] = mk[e] > 0.f ? d[e] : 0.f;
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        a[e] += d[e];
+        b[e] = fmaf(d[e], (f[e] - mu[e]) * rs[e], b[e]);
       }
     }
+  };
+  if (r < rows) {
+    int p = p0 + r;
+    for (; p + 3 * rows < p1; p += 4 * rows) {
+      const Ld v0 = load(p), v1 = load(p + rows), v2 = load(p + 2 * rows), v3 = load(p + 3 * rows);
+      step(v0);
+      step(v1);
+      step(v2);
+      step(v3);
+    }
+    for (; p < p1; p += rows) step(load(p));
   }
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
@@ -147,8 +176,19 @@ __global__ __launch_bounds__(256) void k_bnr_apply(const uint16_t* __restrict__ 
   const int64_t per = M * nch, tot = per * gridDim.y;
   (void)tot;
   const int g = blockIdx.y;
-  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < per; q += (int64_t)gridDim.x * blockDim.x) {
-    const int j = (int)(q % nch);
+  // the grid stride (a multiple of 256 threads) is a multiple of nch = C/8 <= 256: a thread's channel chunk j never
+  // changes, so its 8 channels' scale/shift are loaded once (they were 4 global loads per channel per chunk)
+  const int64_t q0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int j = (int)(q0 % nch);
+  float sc[8], sf[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const int c = 8 * j + e;
+    const float mu = stats[((int64_t)g * C + c) * 2], rs = stats[((int64_t)g * C + c) * 2 + 1];
+    sc[e] = theta[(int64_t)g * ldt + off_w + c] * rs;
+    sf[e] = theta[(int64_t)g * ldt + off_b + c] - mu * sc[e];
+  }
+  for (int64_t q = q0; q < per; q += (int64_t)gridDim.x * blockDim.x) {
     const int64_t o = ((int64_t)g * M * nch + q) * 8;
     float f[8], rr[8];
     bnr_unpack8(*reinterpret_cast<const uint4*>(t + o), f);
@@ -159,10 +199,7 @@ __global__ __launch_bounds__(256) void k_bnr_apply(const uint16_t* __restrict__ 
       float v[2];
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
-        const int c = 8 * j + e + h;
-        const float mu = stats[((int64_t)g * C + c) * 2], rs = stats[((int64_t)g * C + c) * 2 + 1];
-        const float sc = theta[(int64_t)g * ldt + off_w + c] * rs;
-        float x = fmaf(f[e + h] - mu, sc, theta[(int64_t)g * ldt + off_b + c]);
+        float x = fmaf(f[e + h], sc[e + h], sf[e + h]);
         if (RES) x += rr[e + h];
         if (RELU) x = fmaxf(x, 0.f);
         v[h] = x;
@@ -201,8 +238,22 @@ __global__ __launch_bounds__(256) void k_bnr_bwd_apply(const uint16_t* __restric
   const int nch = C >> 3;
   const int64_t per = M * nch;
   const int g = blockIdx.y;
-  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < per; q += (int64_t)gridDim.x * blockDim.x) {
-    const int j = (int)(q % nch);
+  // loop-invariant channel chunk (see k_bnr_apply): dt = A dy' + K1 + K2 t with A = rstd gamma,
+  // K2 = -A rstd m2, K1 = -A m1 - K2 mu
+  const int64_t q0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int j = (int)(q0 % nch);
+  float A[8], K1[8], K2[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const int c = 8 * j + e;
+    const float mu = stats[((int64_t)g * C + c) * 2], rs = stats[((int64_t)g * C + c) * 2 + 1];
+    const float m1 = coef ? coef[((int64_t)g * C + c) * 2] : 0.f;
+    const float m2 = coef ? coef[((int64_t)g * C + c) * 2 + 1] : 0.f;
+    A[e] = rs * theta[(int64_t)g * ldt + off_w + c];
+    K2[e] = -A[e] * rs * m2;
+    K1[e] = -A[e] * m1 - K2[e] * mu;
+  }
+  for (int64_t q = q0; q < per; q += (int64_t)gridDim.x * blockDim.x) {
     const int64_t o = ((int64_t)g * M * nch + q) * 8;
     float f[8], d[8];
     bnr_unpack8(*reinterpret_cast<const uint4*>(t + o), f);
@@ -221,19 +272,9 @@ __global__ __launch_bounds__(256) void k_bnr_bwd_apply(const uint16_t* __restric
     }
     uint32_t out[4];
 #pragma unroll
-    for (int e = 0; e < 8; e += 2) {
-      float v[2];
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int c = 8 * j + e + h;
-        const float mu = stats[((int64_t)g * C + c) * 2], rs = stats[((int64_t)g * C + c) * 2 + 1];
-        const float m1 = coef ? coef[((int64_t)g * C + c) * 2] : 0.f;
-        const float m2 = coef ? coef[((int64_t)g * C + c) * 2 + 1] : 0.f;
-        const float xh = (f[e + h] - mu) * rs;
-        v[h] = rs * theta[(int64_t)g * ldt + off_w + c] * (d[e + h] - m1 - xh * m2);
-      }
-      out[e >> 1] = pack_bf16x2(v[0], v[1]);
-    }
+    for (int e = 0; e < 8; e += 2)
+      out[e >> 1] = pack_bf16x2(fmaf(A[e], d[e], fmaf(K2[e], f[e], K1[e])),
+                                fmaf(A[e + 1], d[e + 1], fmaf(K2[e + 1], f[e + 1], K1[e + 1])));
     *reinterpret_cast<uint4*>(dt + o) = make_uint4(out[0], out[1], out[2], out[3]);
   }
 }

@@ -403,8 +403,10 @@ __device__ __forceinline__ f16x8 c1_bfrag(const uint16_t* hb, int s, int ro, con
   return __builtin_bit_cast(f16x8, v);
 }
 
-template <int PF, int KS>  // PF: B-fragment prefetch distance in k-steps; KS: k-steps per (dd, dh) row (7 or 4)
-__global__ __launch_bounds__(256, 2) void k_conv1_fwd_pool_pipe(const uint8_t* __restrict__ x8,
+// PF: B-fragment prefetch distance in k-steps; KS: k-steps per (dd, dh) row (7 or 4); OCC: blocks per CU the
+// register budget is cut for (2: 256 VGPRs; 3: 168, with spills — A/B NIDT_C1_OCC)
+template <int PF, int KS, int OCC = 2>
+__global__ __launch_bounds__(256, OCC) void k_conv1_fwd_pool_pipe(const uint8_t* __restrict__ x8,
                                                                 const int* __restrict__ idx,
                                                                 const uint16_t* __restrict__ w8,
                                                                 const float* __restrict__ scale,
@@ -614,7 +616,16 @@ void conv1_fwd_pool(uintptr_t x8, uintptr_t idx, uintptr_t w8, uintptr_t scale, 
     const char* e = getenv("NIDT_C1_PF");
     return e ? atoi(e) : 2;
   }();
+  static const int occ = [] {
+    const char* e = getenv("NIDT_C1_OCC");
+    return e ? atoi(e) : 2;
+  }();
 #define NIDT_C1(PF, KSS)                                                                                       \
+  if (occ == 3 && (PF) == 2 && (KSS) == 4)                                                                     \
+    hipLaunchKernelGGL((k_conv1_fwd_pool_pipe<2, 4, 3>), dim3(kPD * NB), dim3(256), 0, as_stream(stream),          \
+                       ptr<const uint8_t>(x8), ptr<const int>(idx), ptr<const uint16_t>(w8), ptr<const float>(scale), \
+                       ptr<const float>(shift), B, ptr<uint16_t>(out), ptr<uint8_t>(amax));                          \
+  else                                                                                                         \
   hipLaunchKernelGGL((k_conv1_fwd_pool_pipe<PF, KSS>), dim3(kPD * NB), dim3(256), 0, as_stream(stream),           \
                      ptr<const uint8_t>(x8), ptr<const int>(idx), ptr<const uint16_t>(w8), ptr<const float>(scale),  \
                      ptr<const float>(shift), B, ptr<uint16_t>(out), ptr<uint8_t>(amax))

@@ -449,42 +449,74 @@ __global__ void k_gn_param_grads(const float* __restrict__ part, int B, int C, f
 }
 
 // Residual-stream gradient of a basic block: out = dx1 + (dx2 if given, else da * (mask > 0)); dx1/dx2 bf16 (the two
-// convolutions' data gradients), da fp32 (the block output gradient), mask bf16 (the block's post-ReLU output).
-// One pass instead of the four elementwise torch ops (two up-casts, a compare-multiply, an add).
-__global__ void k_res_grad(float* __restrict__ out, const uint16_t* __restrict__ dx1, const uint16_t* __restrict__ dx2,
-                           const float* __restrict__ da, const uint16_t* __restrict__ mask, int64_t n8) {
+// convolutions' data gradients), da (the block output gradient) and out bf16 or fp32, mask bf16 (the block's
+// post-ReLU output).  One pass instead of the four elementwise torch ops (two up-casts, a compare-multiply, an add).
+// The engines keep the residual gradient stream in bf16 (OB, DB): it is re-read by the normalisation backward of
+// every block, and fp32 doubled those passes' bytes (config 5: the fp32-dy BN backward was 16 % of a round).
+__device__ __forceinline__ void store8(void* out, int64_t q, const float (&v)[8], bool bf) {
+  if (bf) {
+    *reinterpret_cast<uint4*>(reinterpret_cast<uint16_t*>(out) + q * 8) =
+        make_uint4(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]), pack_bf16x2(v[4], v[5]), pack_bf16x2(v[6], v[7]));
+  } else {
+    float4* o = reinterpret_cast<float4*>(reinterpret_cast<float*>(out) + q * 8);
+    o[0] = make_float4(v[0], v[1], v[2], v[3]);
+    o[1] = make_float4(v[4], v[5], v[6], v[7]);
+  }
+}
+
+template <bool OB, bool DB>
+__global__ void k_res_grad(void* __restrict__ out, const uint16_t* __restrict__ dx1, const uint16_t* __restrict__ dx2,
+                           const void* __restrict__ da, const uint16_t* __restrict__ mask, int64_t n8) {
   for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n8; q += (int64_t)gridDim.x * blockDim.x) {
     float a[8], b[8];
     unpack8(*reinterpret_cast<const uint4*>(dx1 + q * 8), a);
     if (dx2) {
       unpack8(*reinterpret_cast<const uint4*>(dx2 + q * 8), b);
     } else {
-      float m[8];
+      float m[8], d[8];
       unpack8(*reinterpret_cast<const uint4*>(mask + q * 8), m);
-      const float4 d0 = *reinterpret_cast<const float4*>(da + q * 8), d1 = *reinterpret_cast<const float4*>(da + q * 8 + 4);
-      const float d[8] = {d0.x, d0.y, d0.z, d0.w, d1.x, d1.y, d1.z, d1.w};
+      if (DB) {
+        unpack8(*reinterpret_cast<const uint4*>(reinterpret_cast<const uint16_t*>(da) + q * 8), d);
+      } else {
+        const float* df = reinterpret_cast<const float*>(da);
+        const float4 d0 = *reinterpret_cast<const float4*>(df + q * 8), d1 = *reinterpret_cast<const float4*>(df + q * 8 + 4);
+        d[0] = d0.x; d[1] = d0.y; d[2] = d0.z; d[3] = d0.w; d[4] = d1.x; d[5] = d1.y; d[6] = d1.z; d[7] = d1.w;
+      }
 #pragma unroll
       for (int e = 0; e < 8; ++e) b[e] = m[e] > 0.f ? d[e] : 0.f;
     }
-    float4* o = reinterpret_cast<float4*>(out + q * 8);
-    o[0] = make_float4(a[0] + b[0], a[1] + b[1], a[2] + b[2], a[3] + b[3]);
-    o[1] = make_float4(a[4] + b[4], a[5] + b[5], a[6] + b[6], a[7] + b[7]);
+    float v[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = a[e] + b[e];
+    store8(out, q, v, OB);
   }
 }
 
-void res_grad(uintptr_t out, uintptr_t dx1, uintptr_t dx2, uintptr_t da, uintptr_t mask, int64_t n, uintptr_t stream) {
+// flags: bit 0 = out bf16, bit 1 = da bf16
+void res_grad(uintptr_t out, uintptr_t dx1, uintptr_t dx2, uintptr_t da, uintptr_t mask, int64_t n, int flags,
+              uintptr_t stream) {
   NIDT_REQUIRE(n % 8 == 0 && (dx2 || (da && mask)), "res_grad: n % 8 == 0 and (dx2 or da+mask)");
   const int64_t n8 = n / 8;
-  hipLaunchKernelGGL(k_res_grad, dim3((unsigned)std::min<int64_t>(8192, (n8 + 255) / 256)), dim3(256), 0,
-                     as_stream(stream), ptr<float>(out), ptr<const uint16_t>(dx1), ptr<const uint16_t>(dx2),
-                     ptr<const float>(da), ptr<const uint16_t>(mask), n8);
+  const dim3 grid((unsigned)std::min<int64_t>(8192, (n8 + 255) / 256));
+  hipStream_t s = as_stream(stream);
+#define RG(OB, DB)                                                                                             \
+  hipLaunchKernelGGL((k_res_grad<OB, DB>), grid, dim3(256), 0, s, ptr<void>(out), ptr<const uint16_t>(dx1),     \
+                     ptr<const uint16_t>(dx2), ptr<const void>(da), ptr<const uint16_t>(mask), n8)
+  switch (flags & 3) {
+    case 0: RG(false, false); break;
+    case 1: RG(true, false); break;
+    case 2: RG(false, true); break;
+    default: RG(true, true); break;
+  }
+#undef RG
   NIDT_CHECK(hipGetLastError());
 }
 
 // Residual-stream gradient of a downsampling block: out = dx1 + (dx2 at the even pixels), with the 1x1(x1) stride-2
 // shortcut's data gradient given at half resolution (dx2s [N][Do][Ho][Wo][C], Ho = ceil(H/2); D = 1 for 2-D maps):
 // the shortcut conv read only the even positions, so no full-size zero-filled scatter of its gradient is needed.
-__global__ void k_res_grad_s2(float* __restrict__ out, const uint16_t* __restrict__ dx1,
+template <bool OB>
+__global__ void k_res_grad_s2(void* __restrict__ out, const uint16_t* __restrict__ dx1,
                               const uint16_t* __restrict__ dx2s, int64_t n8, int D, int H, int W, int C) {
   const int C8 = C / 8, Do = D > 1 ? (D + 1) / 2 : 1, Ho = (H + 1) / 2, Wo = (W + 1) / 2;
   for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n8; q += (int64_t)gridDim.x * blockDim.x) {
@@ -506,18 +538,24 @@ __global__ void k_res_grad_s2(float* __restrict__ out, const uint16_t* __restric
 #pragma unroll
       for (int e = 0; e < 8; ++e) b[e] = 0.f;
     }
-    float4* o = reinterpret_cast<float4*>(out + q * 8);
-    o[0] = make_float4(a[0] + b[0], a[1] + b[1], a[2] + b[2], a[3] + b[3]);
-    o[1] = make_float4(a[4] + b[4], a[5] + b[5], a[6] + b[6], a[7] + b[7]);
+    float v[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = a[e] + b[e];
+    store8(out, q, v, OB);
   }
 }
 
-void res_grad_s2(uintptr_t out, uintptr_t dx1, uintptr_t dx2s, int N, int D, int H, int W, int C, uintptr_t stream) {
+void res_grad_s2(uintptr_t out, uintptr_t dx1, uintptr_t dx2s, int N, int D, int H, int W, int C, int out_bf16,
+                 uintptr_t stream) {
   NIDT_REQUIRE(C % 8 == 0 && D >= 1, "res_grad_s2: C % 8 == 0");
   const int64_t n8 = (int64_t)N * D * H * W * C / 8;
-  hipLaunchKernelGGL(k_res_grad_s2, dim3((unsigned)std::min<int64_t>(8192, (n8 + 255) / 256)), dim3(256), 0,
-                     as_stream(stream), ptr<float>(out), ptr<const uint16_t>(dx1), ptr<const uint16_t>(dx2s), n8, D,
-                     H, W, C);
+  const dim3 grid((unsigned)std::min<int64_t>(8192, (n8 + 255) / 256));
+  if (out_bf16)
+    hipLaunchKernelGGL(k_res_grad_s2<true>, grid, dim3(256), 0, as_stream(stream), ptr<void>(out),
+                       ptr<const uint16_t>(dx1), ptr<const uint16_t>(dx2s), n8, D, H, W, C);
+  else
+    hipLaunchKernelGGL(k_res_grad_s2<false>, grid, dim3(256), 0, as_stream(stream), ptr<void>(out),
+                       ptr<const uint16_t>(dx1), ptr<const uint16_t>(dx2s), n8, D, H, W, C);
   NIDT_CHECK(hipGetLastError());
 }
 

@@ -345,6 +345,59 @@ void masked_rows_sum(uintptr_t rows, int64_t ld, uintptr_t bits, int64_t mstride
   NIDT_CHECK(hipGetLastError());
 }
 
+// ------------------------------------------------------------------------------------------------ masked neighbour mean
+// DisPFL's masked neighbour average (the paper's aggregation; commented out in the reference, dispfl_api.py:138-142),
+// every client of the launch at once: out_r[p] = own_r(p) * (sum_k src_k[p] bit_k(p)) / (sum_k bit_k(p)) over its
+// neighbours k in [rp[r], rp[r+1]) (0 where no neighbour keeps p).  src / bits / dst / own: device pointer tables
+// (fp32 rows 16-B aligned, uint32 bit rows); outputs must not alias sources.  grid (ceil(n/4/256), rows).
+__global__ __launch_bounds__(256) void k_masked_mean_rows(const uint64_t* __restrict__ src,
+                                                          const uint64_t* __restrict__ sbits,
+                                                          const int* __restrict__ rp, const uint64_t* __restrict__ dst,
+                                                          const uint64_t* __restrict__ own, int64_t n) {
+  const int r = blockIdx.y;
+  const int64_t i = 4 * ((int64_t)blockIdx.x * blockDim.x + threadIdx.x);
+  if (i >= n) return;
+  const int k0 = rp[r], k1 = rp[r + 1];
+  float num[4] = {0.f, 0.f, 0.f, 0.f}, cnt[4] = {0.f, 0.f, 0.f, 0.f};
+  const bool full = i + 3 < n;
+  for (int k = k0; k < k1; ++k) {
+    const float* x = reinterpret_cast<const float*>(src[k]);
+    const uint32_t b4 = (reinterpret_cast<const uint32_t*>(sbits[k])[i >> 5] >> (i & 31)) & 0xfu;
+    float v[4];
+    if (full) {
+      const float4 q = *reinterpret_cast<const float4*>(x + i);
+      v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
+    } else {
+      for (int j = 0; j < 4; ++j) v[j] = i + j < n ? x[i + j] : 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const bool on = (b4 >> j) & 1u;
+      num[j] += on ? v[j] : 0.f;
+      cnt[j] += on ? 1.f : 0.f;
+    }
+  }
+  const uint32_t o4 = (reinterpret_cast<const uint32_t*>(own[r])[i >> 5] >> (i & 31)) & 0xfu;
+  float* out = reinterpret_cast<float*>(dst[r]);
+  float res[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) res[j] = (cnt[j] > 0.f && ((o4 >> j) & 1u)) ? num[j] / cnt[j] : 0.f;
+  if (full) {
+    *reinterpret_cast<float4*>(out + i) = make_float4(res[0], res[1], res[2], res[3]);
+  } else {
+    for (int j = 0; j < 4 && i + j < n; ++j) out[i + j] = res[j];
+  }
+}
+
+void masked_mean_rows(uintptr_t src, uintptr_t sbits, uintptr_t rp, uintptr_t dst, uintptr_t own, int R, int64_t n,
+                      uintptr_t stream) {
+  if (R == 0 || n == 0) return;
+  hipLaunchKernelGGL(k_masked_mean_rows, dim3(ceil_div((n + 3) / 4, 256), R), dim3(256), 0, as_stream(stream),
+                     ptr<const uint64_t>(src), ptr<const uint64_t>(sbits), ptr<const int>(rp), ptr<const uint64_t>(dst),
+                     ptr<const uint64_t>(own), n);
+  NIDT_CHECK(hipGetLastError());
+}
+
 // ------------------------------------------------------------------------------------------------ row mixing
 // out_r = sum_{k in [ptr[r], ptr[r+1])} wts[k] * src_k   for each output row r (addresses are device pointers of
 // fp32 rows, 16-B aligned; outputs must not alias any source).  Gossip / neighbour averaging of D-PSGD

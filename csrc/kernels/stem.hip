@@ -19,7 +19,7 @@
 //                     format bn.hip's k_bn_finalize merges).
 //  k_stem_pool        z = relu(y * scale + shift), 3^3 / stride 2 / pad 1 max with the first-max-in-(d,h,w)-order
 //                     argmax of PyTorch's max_pool3d -> pooled bf16 + uint8 window index.
-//  k_stem_unpool      dz at conv resolution = sum of the pooled gradients of the (<= 8) windows whose argmax is this
+//  k_stem_unpool      dz at conv resolution = sum of the (bf16) pooled gradients of the (<= 8) windows whose argmax is this
 //                     voxel, times the ReLU mask; per-block sums of dz and dz * xhat for the BN backward.
 //  k_stem_bn_bwd_fin  dgamma / dbeta into the gradient rows and the coefficients of dy = a dz + b y + d.
 //  k_stem_wgrad       dW[c][slot] = sum_pos dy[pos][c] Xq[pos + tap][phase]: block = (sample, chunk of od planes,
@@ -285,7 +285,7 @@ __global__ void k_stem_pool(StemDims d, const uint16_t* __restrict__ y, const fl
 // ------------------------------------------------------------------------------------------------ pool / BN backward
 // block = (n, od); thread: fixed 8-channel chunk cg = tid & 7, positions (oh, ow) strided by 32.  dz (bf16) and
 // per-block sums of dz and dz * xhat (xhat = (y - mean) * invstd) per channel -> part [G][B*61][64][2].
-__global__ __launch_bounds__(256) void k_stem_unpool(StemDims d, const float* __restrict__ dpool, const uint8_t* __restrict__ amax,
+__global__ __launch_bounds__(256) void k_stem_unpool(StemDims d, const uint16_t* __restrict__ dpool, const uint8_t* __restrict__ amax,
                                                      const uint16_t* __restrict__ y, const float* __restrict__ scale,
                                                      const float* __restrict__ shift, const float* __restrict__ mean,
                                                      const float* __restrict__ invstd, int B,
@@ -315,8 +315,12 @@ __global__ __launch_bounds__(256) void k_stem_unpool(StemDims d, const float* __
           const int a = ad * 9 + ah * 3 + aw;
           const int64_t qo = ((((int64_t)n * d.QD + qd) * d.QH + qh) * d.QW + qw) * kSC + cg * 8;
           const uint2 am = *reinterpret_cast<const uint2*>(amax + qo);
-          const float4 g0 = *reinterpret_cast<const float4*>(dpool + qo), g1 = *reinterpret_cast<const float4*>(dpool + qo + 4);
-          const float gv[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
+          const uint4 gr = *reinterpret_cast<const uint4*>(dpool + qo);  // bf16 (the engine's residual stream)
+          const uint32_t gu[4] = {gr.x, gr.y, gr.z, gr.w};
+          float gv[8];
+#pragma unroll
+          for (int q = 0; q < 8; ++q)
+            gv[q] = __uint_as_float((q & 1) ? (gu[q >> 1] & 0xffff0000u) : (gu[q >> 1] << 16));
 #pragma unroll
           for (int q = 0; q < 8; ++q) {
             const int aq = (int)(((q < 4 ? am.x : am.y) >> (8 * (q & 3))) & 0xffu);
@@ -557,7 +561,7 @@ void stem_bwd(uintptr_t dpool, uintptr_t amax, uintptr_t y, uintptr_t xq, uintpt
   NIDT_REQUIRE(d.OW <= 64, "stem_bwd: output rows must fit one 64-wide block");
   hipStream_t s = as_stream(stream);
   const int G = N / B;
-  hipLaunchKernelGGL(k_stem_unpool, dim3(N * d.OD), dim3(256), 0, s, d, ptr<const float>(dpool),
+  hipLaunchKernelGGL(k_stem_unpool, dim3(N * d.OD), dim3(256), 0, s, d, ptr<const uint16_t>(dpool),
                      ptr<const uint8_t>(amax), ptr<const uint16_t>(y), ptr<const float>(scale),
                      ptr<const float>(shift), ptr<const float>(mean), ptr<const float>(invstd), B, ptr<uint16_t>(dz),
                      ptr<float>(part));

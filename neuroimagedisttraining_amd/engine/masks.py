@@ -293,6 +293,45 @@ def masked_rows_sum(rows, n, bits, sum_, cnt):
         cnt += unpack_bits(bits, n).sum(0)
 
 
+def masked_mean_rows(plan, n):
+    """``plan``: list of ``(dst_row, own_bits_row, [(src_row, src_bits_row), ...])``: dst[p] = own(p) * mean of the
+    src rows whose bit p is set (0 where none is) — DisPFL's masked neighbour average.  fp32 rows of length >= n,
+    uint32 bit rows; dst must not alias a source.  One launch for every output row."""
+    plan = [p for p in plan if p[2]]
+    if not plan or n == 0:
+        return
+    d0 = plan[0][0]
+    if _hip(d0):
+        assert all(d.data_ptr() % 16 == 0 and all(t.data_ptr() % 16 == 0 for t, _ in terms) for d, _, terms in plan), \
+            "masked_mean_rows: rows must be 16-byte aligned"
+        src, sb, rp, dst, own = [], [], [0], [], []
+        for d, ob, terms in plan:
+            dst.append(d.data_ptr())
+            own.append(ob.data_ptr())
+            for t, b in terms:
+                src.append(t.data_ptr())
+                sb.append(b.data_ptr())
+            rp.append(len(src))
+        dev = d0.device
+        # named: the tables must stay referenced until the launch is enqueued (a temporary's block could be
+        # handed to the next table's copy first)
+        t_src, t_sb = torch.tensor(src, dtype=torch.int64).to(dev), torch.tensor(sb, dtype=torch.int64).to(dev)
+        t_rp, t_dst = torch.tensor(rp, dtype=torch.int32).to(dev), torch.tensor(dst, dtype=torch.int64).to(dev)
+        t_own = torch.tensor(own, dtype=torch.int64).to(dev)
+        ops.ext().masked_mean_rows(t_src.data_ptr(), t_sb.data_ptr(), t_rp.data_ptr(), t_dst.data_ptr(),
+                                   t_own.data_ptr(), len(plan), n, _st())
+        return
+    for d, ob, terms in plan:
+        num = torch.zeros(n, dtype=torch.float32, device=d.device)
+        cnt = torch.zeros(n, dtype=torch.float32, device=d.device)
+        for t, b in terms:
+            m = unpack_bits(b.view(1, -1), n, torch.bool)[0]
+            num += torch.where(m, t[:n], torch.zeros_like(num))
+            cnt += m.float()
+        o = unpack_bits(ob.view(1, -1), n, torch.bool)[0]
+        d[:n] = torch.where((cnt > 0) & o, num / cnt.clamp_min(1), torch.zeros_like(num))
+
+
 def mix_rows(plan, n):
     """``plan``: list of ``(dst_row, [(src_row, weight), ...])`` 1-D fp32 tensors of length >= n; dst rows must not
     alias sources.  One launch for every output row."""

@@ -501,20 +501,21 @@ class DisPFLRunner(PersonalizedRunner):
 
     def _aggregate_neighbours(self, nei, active, last):
         """The DisPFL paper's masked neighbour average (commented out in the reference, ``dispfl_api.py:138-142``):
-        per coordinate, the mean over the neighbours whose shared mask keeps it, times the client's own mask."""
+        per coordinate, the mean over the neighbours whose shared mask keeps it, times the client's own mask; the
+        buffers a plain neighbour mean.  One launch each for every local client (``masks.masked_mean_rows`` /
+        ``mix_rows``), neighbour rows of other ranks fetched point-to-point."""
         needs = [sorted({j for c in self.shards[r] if active[c] for j in nei[c]}) for r in range(self.info.world)]
         src = self.fetch(needs, last)
         all_bits = self._all_bits(self.shared_bits)
+        plan, bplan = [], []
         for c in self.local:
             if not active[c] or not nei[c]:
                 continue
             i = self.row_of[c]
-            m = MK.unpack_bits(all_bits[nei[c]], self.P)
-            num = sum(src[j][0][:self.P] * m[k] for k, j in enumerate(nei[c]))
-            cnt = m.sum(0)
-            avg = torch.where(cnt > 0, num / cnt.clamp_min(1), torch.zeros_like(num))
-            self.theta[i, :self.P] = avg * MK.unpack_bits(self.mbits[i:i + 1], self.P)[0]
-            self.bufs[i, :self.Q] = sum(src[j][1][:self.Q] for j in nei[c]) / len(nei[c])
+            plan.append((self.theta[i], self.mbits[i], [(src[j][0], all_bits[j]) for j in nei[c]]))
+            bplan.append((self.bufs[i], [(src[j][1], 1.0 / len(nei[c])) for j in nei[c]]))
+        MK.masked_mean_rows(plan, self.P)
+        MK.mix_rows(bplan, self.Q)
 
     def _all_bits(self, bits):
         """[N, W] mask bit rows of every client (all-reduce of the zero-padded local rows)."""

@@ -530,7 +530,8 @@ class GroupedResNet18GN:
         dpool = (dlog.view(G, B, self.ncls, 1) * lw.view(G, 1, self.ncls, self.feat)).sum(2).view(G * B, 1, self.feat)
         a = saved[-1][-1]
         N, H, W, C = a.shape
-        da = (dpool / float(H * W)).expand(N, H * W, C).reshape(N, H, W, C).contiguous()
+        # bf16 residual-gradient stream on the HIP path (res_grad writes bf16; re-read by every GroupNorm backward)
+        da = (dpool / float(H * W)).expand(N, H * W, C).reshape(N, H, W, C).to(self.act).contiguous()
         for blk, sv in zip(reversed(self.blocks), reversed(saved[1:])):
             xin, t1, s1, h1, t2, s2, ts, ss, a = sv
             dt2 = blk["n2"].bwd(da, a, t2, s2, theta, grads, G)
@@ -543,14 +544,16 @@ class GroupedResNet18GN:
                 dx2 = blk["cs"].bwd(dts, xin, theta, grads, G, True)
             half = dx2 is not None and blk["cs"].stride == 2  # 1x1 stride-2 projection: even-pixel gradient
             if self.hip:
-                out = torch.empty(dx1.shape, device=dx1.device, dtype=torch.float32)
+                out = torch.empty(dx1.shape, device=dx1.device, dtype=torch.bfloat16)
                 if half:
                     Nn, Hh, Ww, Cc = dx1.shape
-                    ops.ext().res_grad_s2(out.data_ptr(), dx1.data_ptr(), dx2.data_ptr(), Nn, 1, Hh, Ww, Cc, _stream())
+                    ops.ext().res_grad_s2(out.data_ptr(), dx1.data_ptr(), dx2.data_ptr(), Nn, 1, Hh, Ww, Cc, 1,
+                                          _stream())
                 else:
                     ops.ext().res_grad(out.data_ptr(), dx1.data_ptr(), dx2.data_ptr() if dx2 is not None else 0,
                                        0 if dx2 is not None else da.data_ptr(),
-                                       0 if dx2 is not None else a.data_ptr(), out.numel(), _stream())
+                                       0 if dx2 is not None else a.data_ptr(), out.numel(),
+                                       1 | (2 if da.dtype == torch.bfloat16 else 0), _stream())
                 da = out
             elif half:
                 da = dx1.float().clone()

@@ -352,7 +352,7 @@ class GroupedResNet3D:
         dev = theta.device
         sz = m.stem_sizes(N, D, H, W)
         o = self.off
-        da = da.float().contiguous()
+        da = da.to(torch.bfloat16).contiguous()  # the bf16 residual gradient stream (a no-op in train_step)
         dz = torch.empty_like(y)
         part = torch.empty(sz[3], device=dev, dtype=torch.float32)
         bcoef = torch.empty(G * self.stem_c * 3, device=dev, dtype=torch.float32)
@@ -434,7 +434,9 @@ class GroupedResNet3D:
         N = a.shape[0]
         S = a[0].numel() // a.shape[-1]
         dpool = (dlog.unsqueeze(2) * fw.unsqueeze(1)).reshape(N, 1, self.feat) / float(S)
-        da = dpool.expand(N, S, self.feat).reshape(a.shape).contiguous()
+        # the residual-stream gradient is kept in bf16 on the HIP path (res_grad writes bf16): it is re-read by the
+        # BatchNorm backward of every block, where fp32 doubled the bytes
+        da = dpool.expand(N, S, self.feat).reshape(a.shape).to(self.act).contiguous()
         for blk, sv in zip(reversed(self.blocks), reversed(saved)):
             xin, t1, s1, h1, t2, s2, h2, t3, s3, td, sd, a = sv
             dt3 = blk["n3"].bwd(da, a, t3, s3, theta, grads, G)
@@ -449,15 +451,16 @@ class GroupedResNet3D:
                 dx2 = blk["cd"].bwd(dtd, xin, theta, grads, G)
             half = dx2 is not None and blk["cd"].stride == 2  # 1x1x1 stride-2 projection: even-voxel gradient
             if self.hip:
-                out = torch.empty(dx1.shape, device=dx1.device, dtype=torch.float32)
+                out = torch.empty(dx1.shape, device=dx1.device, dtype=torch.bfloat16)
                 if half:
                     Nn, Dd, Hh, Ww, Cc = dx1.shape
-                    ops.ext().res_grad_s2(out.data_ptr(), dx1.data_ptr(), dx2.data_ptr(), Nn, Dd, Hh, Ww, Cc,
+                    ops.ext().res_grad_s2(out.data_ptr(), dx1.data_ptr(), dx2.data_ptr(), Nn, Dd, Hh, Ww, Cc, 1,
                                           _stream())
                 else:
                     ops.ext().res_grad(out.data_ptr(), dx1.data_ptr(), dx2.data_ptr() if dx2 is not None else 0,
                                        0 if dx2 is not None else da.data_ptr(),
-                                       0 if dx2 is not None else a.data_ptr(), out.numel(), _stream())
+                                       0 if dx2 is not None else a.data_ptr(), out.numel(),
+                                       1 | (2 if da.dtype == torch.bfloat16 else 0), _stream())
                 da = out
             elif half:
                 da = dx1.float().clone()

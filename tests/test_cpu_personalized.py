@@ -96,6 +96,29 @@ def test_masked_average_matches_subavg_aggregate():
     assert torch.allclose(ours, torch.cat([ref[n].reshape(-1) for n in pl.names]), atol=1e-6)
 
 
+def test_masked_mean_rows_matches_dispfl_neighbour_formula():
+    """DisPFL's masked neighbour average (dispfl_api.py:138-142, the paper's aggregation): per coordinate the mean of
+    the neighbours whose mask keeps it, times the client's own mask, 0 where no neighbour keeps it."""
+    from neuroimagedisttraining_amd.engine import masks as MK
+    torch.manual_seed(3)
+    n, K = 200, 4
+    src = [torch.randn(n + 8) for _ in range(K)]
+    m = (torch.rand(K, n) < 0.4)
+    own = torch.rand(n) < 0.6
+    bits = MK.pack_bits(m.float())
+    obits = MK.pack_bits(own.float().view(1, -1))[0]
+    outs = [torch.full((n + 8,), 7.0), torch.full((n + 8,), 7.0)]
+    plan = [(outs[0], obits, [(src[k], bits[k]) for k in range(K)]),
+            (outs[1], obits, [(src[k], bits[k]) for k in (1, 3)])]
+    MK.masked_mean_rows(plan, n)
+    for o, ks in zip(outs, ([0, 1, 2, 3], [1, 3])):
+        num = sum(src[k][:n] * m[k] for k in ks)
+        cnt = sum(m[k].float() for k in ks)
+        want = torch.where(cnt > 0, num / cnt.clamp_min(1), torch.zeros(n)) * own
+        assert torch.allclose(o[:n], want, atol=1e-6)
+        assert torch.all(o[n:] == 7.0)  # nothing past n written
+
+
 # ------------------------------------------------------------------------------------------------ runners
 SIZES = [10, 7, 14, 10, 6, 11]
 
@@ -218,6 +241,7 @@ def _port():
 
 
 CASES = [("dispfl", 2, {}), ("dispfl", 3, {"frac": 0.5, "active": 0.8, "dis_gradient_check": True}),
+         ("dispfl", 2, {"frac": 0.5, "dispfl_aggregate": True}),
          ("subavg", 2, {"frac": 0.5}), ("ditto", 2, {"frac": 0.5}), ("dpsgd", 3, {"frac": 0.5, "cs": "ring"}),
          ("dpsgd", 2, {"frac": 0.5, "cs": "random"}), ("fedfomo", 3, {"frac": 0.5}), ("local", 2, {"frac": 0.5}),
          ("salientgrads", 2, {}), ("fedavg", 3, {"frac": 0.5})]

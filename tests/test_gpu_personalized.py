@@ -284,11 +284,18 @@ def test_runner_hip_tracks_torch_engine(algo):
     fed = _fed(SIZES)
     a, w0 = _run(algo, "hip", fed, **_extra(algo))
     b, _ = _run(algo, "torch", fed, **_extra(algo))
+    c, _ = _run(algo, "amp", fed, **_extra(algo))  # the same fp32 engine under bf16 autocast (MIOpen bf16 convs)
     upd_a = (a.theta[:, :a.P] - w0[:, :a.P]).double()
     upd_b = (b.theta[:, :b.P] - w0[:, :b.P]).double()
-    cos = F.cosine_similarity(upd_a.flatten(), upd_b.flatten(), dim=0)
-    print(algo, "update cosine", float(cos), "rel err", _relerr(upd_a, upd_b))
-    assert float(cos) > 0.25
+    upd_c = (c.theta[:, :c.P] - w0[:, :c.P]).double()
+    cos = float(F.cosine_similarity(upd_a.flatten(), upd_b.flatten(), dim=0))
+    cos_amp = float(F.cosine_similarity(upd_c.flatten(), upd_b.flatten(), dim=0))
+    print(algo, "update cosine", cos, "bf16-autocast cosine", cos_amp, "rel err", _relerr(upd_a, upd_b))
+    # Two rounds of this cohort are chaotic: two fp32 runs whose initial weights differ by 1e-6 relative noise reach
+    # update cosines of only 0.53 (FedAvg), 0.74 (Local), 0.99 (SalientGrads) (tools/chaos_cosine.py,
+    # profiles/r3_chaos_cosine.txt), so a fixed floor near 1 cannot hold for any bf16 engine.  The criterion: the HIP
+    # engine's update is at least as close to fp32's as PyTorch's own bf16 autocast path is.
+    assert cos >= cos_amp - 0.05 and cos > 0.25, (cos, cos_amp)
     if algo in ("dispfl", "subavg"):
         from neuroimagedisttraining_amd.engine import masks as MK
         agree = float((MK.unpack_bits(a.mbits, a.P) == MK.unpack_bits(b.mbits, b.P)).float().mean())
@@ -324,3 +331,23 @@ def test_dispfl_fire_regrow_on_hip_equals_torch_selection():
     r.mspace.select(MK.FIRE, r.theta.cpu(), ref, k.cpu())
     r.mspace.select(MK.REGROW_ABS, r.grads.cpu(), ref, k.cpu())
     assert torch.equal(mine.cpu(), ref)
+
+
+def test_masked_mean_rows_hip_equals_torch():
+    """DisPFL masked neighbour mean (sparse.hip k_masked_mean_rows) == the torch twin, incl. a ragged tail."""
+    from neuroimagedisttraining_amd.engine import masks as MK
+    torch.manual_seed(4)
+    n, K = 10007, 5
+    srcs = [torch.randn(n + 61, device=DEV) for _ in range(K)]
+    m = torch.rand(K, n, device=DEV) < 0.5
+    bits = MK.pack_bits(m.float())
+    own = MK.pack_bits((torch.rand(1, n, device=DEV) < 0.7).float())[0]
+    mk = lambda: [torch.zeros(n + 61, device=DEV) for _ in range(2)]  # noqa: E731
+    a, b = mk(), mk()
+    plans = lambda o: [(o[0], own, [(srcs[k], bits[k]) for k in range(K)]), (o[1], own, [(srcs[2], bits[2])])]  # noqa
+    MK.masked_mean_rows(plans(a), n)
+    cpu = [(d.cpu(), ob.cpu(), [(t.cpu(), bb.cpu()) for t, bb in terms]) for d, ob, terms in plans(b)]
+    MK.masked_mean_rows(cpu, n)
+    torch.cuda.synchronize()
+    for x, (y, _, _) in zip(a, cpu):
+        assert torch.allclose(x.cpu(), y, atol=1e-6)

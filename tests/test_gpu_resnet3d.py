@@ -74,12 +74,36 @@ def test_res_grad_s2_3d_matches_torch(dims):
     dx1 = torch.randn(N, D, H, W, C, device=dev).to(torch.bfloat16)
     sub = torch.randn(N, (D + 1) // 2, (H + 1) // 2, (W + 1) // 2, C, device=dev).to(torch.bfloat16)
     out = torch.empty(N, D, H, W, C, device=dev)
-    ops.ext().res_grad_s2(out.data_ptr(), dx1.data_ptr(), sub.data_ptr(), N, D, H, W, C,
+    ops.ext().res_grad_s2(out.data_ptr(), dx1.data_ptr(), sub.data_ptr(), N, D, H, W, C, 0,
                           torch.cuda.current_stream().cuda_stream)
     want = dx1.float().clone()
     want[:, ::2, ::2, ::2] += sub.float()
+    outb = torch.empty(N, D, H, W, C, device=dev, dtype=torch.bfloat16)  # the engines' bf16 gradient stream
+    ops.ext().res_grad_s2(outb.data_ptr(), dx1.data_ptr(), sub.data_ptr(), N, D, H, W, C, 1,
+                          torch.cuda.current_stream().cuda_stream)
     torch.cuda.synchronize()
     assert torch.equal(out, want)
+    assert torch.equal(outb, want.to(torch.bfloat16))
+
+
+@pytest.mark.parametrize("flags", [0, 1, 2, 3])
+def test_res_grad_dtypes_match_torch(flags):
+    """out = dx1 + da * (mask > 0) (identity block) and out = dx1 + dx2 (projection), fp32 or bf16 in and out."""
+    from neuroimagedisttraining_amd import ops
+    dev = _dev()
+    n = 4 * 9 * 64
+    dx1 = torch.randn(n, device=dev).to(torch.bfloat16)
+    dx2 = torch.randn(n, device=dev).to(torch.bfloat16)
+    da = torch.randn(n, device=dev).to(torch.bfloat16 if flags & 2 else torch.float32)
+    mask = torch.relu(torch.randn(n, device=dev)).to(torch.bfloat16)
+    odt = torch.bfloat16 if flags & 1 else torch.float32
+    st = torch.cuda.current_stream().cuda_stream
+    o1, o2 = torch.empty(n, device=dev, dtype=odt), torch.empty(n, device=dev, dtype=odt)
+    ops.ext().res_grad(o1.data_ptr(), dx1.data_ptr(), 0, da.data_ptr(), mask.data_ptr(), n, flags, st)
+    ops.ext().res_grad(o2.data_ptr(), dx1.data_ptr(), dx2.data_ptr(), 0, 0, n, flags, st)
+    torch.cuda.synchronize()
+    assert torch.equal(o1, (dx1.float() + da.float() * (mask > 0)).to(odt))
+    assert torch.equal(o2, (dx1.float() + dx2.float()).to(odt))
 
 
 @pytest.mark.parametrize("C,dims,res", [(64, (6, 7, 6), True), (256, (3, 4, 3), False), (2048, (1, 2, 1), True)])
@@ -225,7 +249,7 @@ def test_stem_hip_fwd_bwd_match_torch(G, B, dims):
     store = torch.randint(0, 256, (N + 3, *dims), dtype=torch.uint8, device=dev)
     idx = torch.randperm(N + 3, device=dev)[:N].to(torch.int32)
     out, saved = net._stem_hip(store, idx, th, bu, G, True)
-    da = torch.randn(out.shape, device=dev)
+    da = torch.randn(out.shape, device=dev).to(torch.bfloat16).float()  # the engine's gradient stream is bf16
     gr = torch.zeros_like(th)
     net._stem_hip_bwd(saved, da, th, gr, G)
     torch.cuda.synchronize()

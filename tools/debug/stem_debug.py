@@ -48,7 +48,7 @@ def main():
     amax = torch.empty(N, Qd, Qh, Qw, C, device=dev, dtype=torch.uint8)
     m.stem_pool(y.data_ptr(), coef[0].data_ptr(), coef[1].data_ptr(), N, B, D, H, W, out.data_ptr(), amax.data_ptr(),
                 st)
-    da = torch.randn(out.shape, device=dev)
+    da = torch.randn(out.shape, device=dev).to(torch.bfloat16)  # bf16 pooled gradient (the engine's stream)
     grads = torch.zeros_like(theta)
     dz = torch.empty_like(y)
     part = torch.empty(sz[3], device=dev)
@@ -71,7 +71,7 @@ def main():
     bn.retain_grad()
     r = torch.relu(bn)
     z = F.max_pool3d(r, 3, 2, 1)
-    z.permute(0, 2, 3, 4, 1).backward(da)
+    z.permute(0, 2, 3, 4, 1).backward(da.float())
     print("conv y rel", rel(y.permute(0, 4, 1, 2, 3), c))
     print("pooled rel", rel(out.permute(0, 4, 1, 2, 3), z))
     print("mean rel", rel(coef[2], c.mean((0, 2, 3, 4))), "invstd rel",

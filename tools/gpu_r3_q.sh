@@ -1,0 +1,19 @@
+#!/bin/bash
+# BN partial sums with 4-deep load batches: 3D ResNet tests + config 5; the amp-relative HIP-vs-fp32 runner test
+set -o pipefail
+mkdir -p gpurun_out/r3q
+export PYTHONUNBUFFERED=1
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+timeout -k 10 400 python -u -m pytest tests/test_gpu_resnet3d.py -x -q --timeout 300 --timeout-method thread \
+  > gpurun_out/r3q/pytest3d.txt 2>&1 || { tail -30 gpurun_out/r3q/pytest3d.txt; exit 1; }
+tail -1 gpurun_out/r3q/pytest3d.txt
+timeout -k 10 900 rocprofv3 --kernel-trace --stats -d /tmp/c5profq -o run -- python3 -u tools/config5_resnet3d.py \
+  --clients 256 --train-per-client 36 --test-per-client 9 --batch 4 --group 32 --rounds 1 \
+  > gpurun_out/r3q/config5.txt 2>&1 || { tail -30 gpurun_out/r3q/config5.txt; exit 1; }
+grep '^{' gpurun_out/r3q/config5.txt | cut -c1-330
+db=$(find /tmp/c5profq -name "*.db" | head -1)
+[ -n "$db" ] && python3 tools/prof_summary.py "$db" gpurun_out/r3q/config5_kernels.txt --top 40 > /dev/null 2>&1
+head -12 gpurun_out/r3q/config5_kernels.txt; grep -E "TOTAL|TIMELINE" gpurun_out/r3q/config5_kernels.txt
+timeout -k 10 700 python -u -m pytest tests/test_gpu_personalized.py -v -s --timeout 300 --timeout-method thread \
+  -k "tracks_torch" > gpurun_out/r3q/pytest_tracks.txt 2>&1
+rc=$?; grep -E "update cosine|PASSED|FAILED|passed|failed" gpurun_out/r3q/pytest_tracks.txt; exit $rc
