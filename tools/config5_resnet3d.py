@@ -35,6 +35,9 @@ def main():
     ap.add_argument("--width", type=int, default=64)
     ap.add_argument("--engine", default="hip", choices=["hip", "torch"])
     ap.add_argument("--group", type=int, default=32, help="clients per lockstep launch (hip engine)")
+    ap.add_argument("--test-batch", type=int, default=None,
+                    help="eval chunk (default 16 on the hip engine: a client's 9 test volumes in one grouped launch of "
+                         "--group clients instead of per-client chunks; 8 on the torch engine)")
     ap.add_argument("--no-hip-convs", action="store_true",
                     help="keep every Conv3d on MIOpen (default: eligible 3x3x3 convs run on the HIP kernels)")
     args = ap.parse_args()
@@ -62,7 +65,8 @@ def main():
             n_hip = use_hip_convs(model)  # 13 of the 16 bottleneck 3x3x3 convs -> nidt::conv3d_k3
         eng = TorchEngine(model, vol, labels, dev, loss="bce", amp=True)
     cfg = FLConfig(comm_round=args.rounds, epochs=args.epochs, batch_size=args.batch, lr=0.01, frac=1.0,
-                   seed=7, update_topk=args.topk, frequency_of_the_test=1, test_batch=8,
+                   seed=7, update_topk=args.topk, frequency_of_the_test=1,
+                   test_batch=args.test_batch or (16 if args.engine == "hip" else 8),
                    group=args.group if args.engine == "hip" else 0)
     runner = FLRunner(eng, splits, cfg, info, model, algorithm="fedavg")
     if dev.type == "cuda":
