@@ -217,7 +217,10 @@ def hip_family(args):
     ``resnet3d`` (3D ResNet-50 on ABCD: engine/resnet3d_hip)."""
     model = args.model.lower()
     if args.dataset == "ABCD" and model in ("3dcnn", "alexnet3d", "alexnet3d_dropout"):
-        return "alexnet3d"
+        # the AlexNet3D kernels are built for the ABCD volume (1x121x145x121: polyphase 61x73x61 store, conv1's
+        # compile-time tiling); a cohort file of another shape runs on the eager engine (loudly, see _use_hip)
+        shape = _cohort_shape(args)
+        return "alexnet3d" if shape in (None, ABCD_SHAPE) else None
     if args.dataset in IMAGE_DATASETS and model == "resnet18":
         return "resnet2d"
     if args.dataset == "ABCD" and model in RESNET3D_NAMES:
@@ -225,14 +228,32 @@ def hip_family(args):
     return None
 
 
+ABCD_SHAPE = (121, 145, 121)
+
+
+def _cohort_shape(args):
+    """Volume shape of the ``--data_dir`` cohort file (None: synthetic ABCD-shape data or no readable file)."""
+    if getattr(args, "synthetic_abcd", True) or not getattr(args, "data_dir", None):
+        return None
+    try:
+        from .data.volume_file import VolumeFile
+        return tuple(VolumeFile(_resolve_cohort(args.data_dir)).shape)
+    except Exception:  # noqa: BLE001 - unreadable here: the loader reports it
+        return None
+
+
 def _use_hip(args, algo):
     """Every algorithm of the harness runs on the client-batched MI355X executor for the model families of
     :func:`hip_family` (the reference defaults of every entry point: 3DCNN + ABCD, resnet18 + cifar10)."""
     if hip_family(args) is None:
+        shape = _cohort_shape(args) if args.dataset == "ABCD" else None
+        why = ("the cohort's volumes are %s, the AlexNet3D kernels need %s" % (shape, ABCD_SHAPE)
+               if shape not in (None, ABCD_SHAPE) else
+               "--engine hip supports --model 3DCNN / %s --dataset ABCD and --model resnet18 --dataset %s"
+               % (" / ".join(RESNET3D_NAMES), " / ".join(IMAGE_DATASETS)))
         if args.engine == "hip":
-            raise RuntimeError("--engine hip supports --model 3DCNN / %s --dataset ABCD and --model resnet18 "
-                               "--dataset %s; use --engine torch for other models"
-                               % (" / ".join(RESNET3D_NAMES), " / ".join(IMAGE_DATASETS)))
+            raise RuntimeError(why + "; use --engine torch")
+        logging.getLogger(__name__).warning("running on the eager PyTorch engine: %s", why)
         return False
     if args.engine == "torch":
         return False

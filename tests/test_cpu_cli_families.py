@@ -79,3 +79,29 @@ def test_run_hip_resnet18_cifar_on_cpu_twin(tmp_path):
     out = cli.run_hip(args, "subavg", logging.getLogger("test"))
     vals = [v for k, v in out.items() if k.endswith("test_acc") and isinstance(v, list) and v]
     assert vals and all(0.0 <= x <= 1.0 for x in vals[0])
+
+
+def test_alexnet_hip_routing_checks_the_cohort_volume_shape(tmp_path, caplog):
+    """A cohort file whose volumes are not 1x121x145x121 cannot run on the AlexNet3D kernels: the entry point says so
+    and runs eagerly (or refuses --engine hip) instead of failing inside the engine; ABCD-shape files route to HIP."""
+    from neuroimagedisttraining_amd import cli
+    from neuroimagedisttraining_amd.data.volume_file import write_volume_file
+    g = np.random.default_rng(0)
+    odd = write_volume_file(str(tmp_path / "odd.nidtvol"), g.integers(0, 255, (4, 20, 24, 20), dtype=np.uint8),
+                            np.array([0, 1, 0, 1]), np.array([0, 0, 1, 1]))
+    args = _args("sailentgrads", ["--data_dir", odd])
+    args.synthetic_abcd = False
+    assert cli._cohort_shape(args) == (20, 24, 20)
+    assert cli.hip_family(args) is None
+    args.engine = "hip"
+    with pytest.raises(RuntimeError, match="AlexNet3D kernels need"):
+        cli._use_hip(args, "sailentgrads")
+    args.engine = "auto"
+    with caplog.at_level(logging.WARNING):
+        assert not cli._use_hip(args, "sailentgrads")
+    assert "eager PyTorch engine" in caplog.text
+    ok = write_volume_file(str(tmp_path / "abcd.nidtvol"), g.integers(0, 255, (2, 121, 145, 121), dtype=np.uint8),
+                           np.array([0, 1]), np.array([0, 1]))
+    args2 = _args("sailentgrads", ["--data_dir", ok])
+    args2.synthetic_abcd = False
+    assert cli.hip_family(args2) == "alexnet3d"
