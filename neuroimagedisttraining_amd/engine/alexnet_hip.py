@@ -14,6 +14,8 @@ the fused clip+SGD+mask optimizer then updates ``theta`` in place.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from .. import ops
@@ -26,6 +28,11 @@ L3 = (8, 9, 128, 192, 1, (5, 7, 5))
 L4 = (11, 12, 192, 192, 1, (5, 7, 5))
 L5 = (14, 15, 192, 128, 1, (5, 7, 5))
 NM = 125 + 125 * 125
+# weight gradients on a forked branch of the step (see train_step) with NIDT_AX_WGRAD_STREAM=1: measured no faster
+# (kbench 23.3 vs 23.2 ms per 64-client step, bench 2.08-2.10 vs 2.10-2.11 r/s: profiles/r3_ab_wgrad_stream.txt).
+# NIDT_WG2_EARLY=1 forks the conv2 wgrad before the conv2 dgrad instead of after it (beside the conv1 wgrad).
+_WGRAD_STREAM = os.environ.get("NIDT_AX_WGRAD_STREAM", "0") == "1"
+_WG2_EARLY = os.environ.get("NIDT_WG2_EARLY", "0") == "1"
 
 
 def _p(t):
@@ -125,6 +132,9 @@ class HipAlexNet3D:
                 if b["tri%d" % ci]:
                     b["stab%d" % ci] = e(self.m.conv3d_wgrad_tri_table_size(B, *sp, pad), dt=torch.int32)
                     self.m.conv3d_wgrad_tri_table(_p(b["stab%d" % ci]), B, *sp, pad, st0)
+            # the weight-gradient branch of this launch shape (one per shape: side lanes run shapes concurrently)
+            if d.type == "cuda":
+                b["wstream"] = torch.cuda.Stream(device=d)
         self._cache[key] = b
         return b
 
@@ -263,30 +273,50 @@ class HipAlexNet3D:
                      _p(theta), P, o["features.%d.weight" % bi], _p(grads), P, o["features.%d.weight" % bi],
                      o["features.%d.bias" % bi], o["features.%d.bias" % ci], _p(b["coef"]), _p(dy), ev, st)
 
+        # Weight gradients are off the critical path (nothing in the step reads them before the optimizer), so
+        # with a wgrad stream they run on a branch forked from the data-gradient chain: the one-block-per-CU
+        # conv3-5 grids fill each other's idle CUs, and the MFMA-bound conv2 wgrad runs beside the VALU-bound
+        # conv1 sparse wgrad.  All wgrads are ordered on that one branch, so they share ``wgpart``.
+        cur = torch.cuda.current_stream()
+        ws = b.get("wstream") if _WGRAD_STREAM else None
+        wst = ws.cuda_stream if ws is not None else st
+
+        def fork():
+            if ws is not None:
+                ws.wait_stream(cur)
+
         def wgrad(ci, x, xs, xt, dy, sp, cin, cout, pad):
             if b.get("tri%d" % ci) and xs is None:
                 m.conv3d_wgrad_tri(_p(x), _p(dy), _p(b["wgpart"]), _p(grads), P, o["features.%d.weight" % ci], G, B,
-                                   sp[0], sp[1], sp[2], cin, cout, pad, b["ns%d" % ci], 1.0, _p(b["stab%d" % ci]), st)
+                                   sp[0], sp[1], sp[2], cin, cout, pad, b["ns%d" % ci], 1.0, _p(b["stab%d" % ci]), wst)
                 return
             m.conv3d_wgrad(_p(x), _p(xs), _p(xt), _p(dy), _p(b["wgpart"]), _p(grads), P, o["features.%d.weight" % ci],
-                           G, B, sp[0], sp[1], sp[2], cin, cout, pad, b["ns%d" % ci], 1.0, _p(b["pt%d" % ci]), st)
+                           G, B, sp[0], sp[1], sp[2], cin, cout, pad, b["ns%d" % ci], 1.0, _p(b["pt%d" % ci]), wst)
 
         # layer 5: pool5 -> BN5 -> conv5
         bn_bwd(1, 14, 15, 128, (5, 7, 5), b["dp5"], b["p5"], b["a5"], b["dy5"], b["y5"])
+        fork()
         wgrad(14, b["h4"], None, None, b["dy5"], (5, 7, 5), 192, 128, 1)
         self._conv(b, "ksd14", b["dy5"], b["w14t"], None, b["dx5"], None, G, B, 5, 7, 5, 128, 192, 1, st)
         # layer 4
         bn_bwd(0, 11, 12, 192, (5, 7, 5), b["dx5"], None, None, b["dy4"], b["y4"])
+        fork()
         wgrad(11, b["h3"], None, None, b["dy4"], (5, 7, 5), 192, 192, 1)
         self._conv(b, "ksd11", b["dy4"], b["w11t"], None, b["dx4"], None, G, B, 5, 7, 5, 192, 192, 1, st)
         # layer 3
         bn_bwd(0, 8, 9, 192, (5, 7, 5), b["dx4"], None, None, b["dy3"], b["y3"])
+        fork()
         wgrad(8, b["p2"], None, None, b["dy3"], (5, 7, 5), 128, 192, 1)
         self._conv(b, "ksd8", b["dy3"], b["w8t"], None, b["dx3"], None, G, B, 5, 7, 5, 192, 128, 1, st)
         # layer 2: pool2 -> BN2 -> conv2
         bn_bwd(1, 4, 5, 128, (17, 21, 17), b["dx3"], b["p2"], b["a2"], b["dy2"], b["y2"])
-        wgrad(4, b["p1"], None, None, b["dy2"], (19, 23, 19), 64, 128, 0)
+        if ws is None or _WG2_EARLY:
+            fork()
+            wgrad(4, b["p1"], None, None, b["dy2"], (19, 23, 19), 64, 128, 0)
         self._conv(b, "ksd4", b["dy2"], b["w4t"], None, b["dp1"], None, G, B, 17, 21, 17, 128, 64, 2, st)
+        if ws is not None and not _WG2_EARLY:
+            fork()
+            wgrad(4, b["p1"], None, None, b["dy2"], (19, 23, 19), 64, 128, 0)
         # layer 1: sparse wgrad through pool1/ReLU/BN1 (closed form; eval mode: running mean minus the conv bias)
         emean = None
         if not bn_train:
@@ -296,6 +326,8 @@ class HipAlexNet3D:
                       _p(b["mu"]), _p(b["covw"]), _p(b["i1"]), _p(theta), P, o["features.1.weight"], _p(grads), P,
                       o["features.0.weight"], o["features.0.bias"], o["features.1.weight"], o["features.1.bias"],
                       1.0 / 255.0, _p(emean), st)
+        if ws is not None:
+            cur.wait_stream(ws)  # join: the optimizer reads every weight gradient
         return b["loss"]
 
     def eval_logits(self, theta, bufs, x8, idx, G, B):

@@ -31,6 +31,8 @@ same augmentation draws; the CPU tests compare it with per-client autograd throu
 """
 from __future__ import annotations
 
+import os
+
 import numpy as np
 import torch
 import torch.nn.functional as F
@@ -190,30 +192,41 @@ class GroupedConv:
         return y.view(B, G, self.cout, Ho, Wo).permute(1, 0, 3, 4, 2).reshape(N, Ho, Wo, self.cout)
 
     # ---------------------------------------------------------------- backward
-    def bwd(self, dy, x, theta, grads, G, need_dx, scratch=None):
+    def bwd(self, dy, x, theta, grads, G, need_dx, scratch=None, ws=None):
         """dW -> grads rows (PyTorch layout at ``off``); returns dX ``[N, H, W, cin_p]`` (or None).  For the 1x1
         stride-2 projection the returned gradient is the half-resolution one of the even pixels (``res_grad_s2``
-        adds it into the residual stream)."""
+        adds it into the residual stream).  ``ws``: stream of the step's weight-gradient branch — the wgrad is
+        forked onto it (the caller joins it before the optimizer) and only the data gradient stays on the chain."""
         if not self.hip:
             return self._torch_bwd(dy, x, theta, grads, G, need_dx)
-        m, st = ops.ext(), _stream()
+        m = ops.ext()
         N, H, W, _ = x.shape
         B = N // G
         Ho, Wo = dy.shape[1:3]
         dy = dy.contiguous()
         ns = m.conv_wgrad_nsplit_g(G, B, 1, H, W, self.cin_p, self.cout, self.kt, self.stride, self.pad, 0)
-        part = torch.empty(ns * G * self.cout * self.kt * self.cin_p, device=x.device, dtype=torch.float32)
         ptab = self._pos_table(B, H, W, Ho, Wo, x.device)
-        if self.cin_p == self.cin:
-            m.conv_wgrad_g(x.data_ptr(), dy.data_ptr(), part.data_ptr(), grads.data_ptr(), grads.stride(0), self.off,
-                           G, B, 1, H, W, self.cin_p, self.cout, self.kt, self.stride, self.pad, 0, ns, 1.0,
-                           ptab.data_ptr(), st)
-        else:  # channel-padded stem: full-width gradient, then the live input channels into the row
-            full = torch.empty(G, self.cout * self.cin_p * self.kt, device=x.device, dtype=torch.float32)
-            m.conv_wgrad_g(x.data_ptr(), dy.data_ptr(), part.data_ptr(), full.data_ptr(), full.stride(0), 0, G, B, 1,
-                           H, W, self.cin_p, self.cout, self.kt, self.stride, self.pad, 0, ns, 1.0, ptab.data_ptr(), st)
-            grads[:, self.off:self.off + self.numel].view(G, self.cout, self.cin, self.kt).copy_(
-                full.view(G, self.cout, self.cin_p, self.kt)[:, :, :self.cin])
+        cur = torch.cuda.current_stream()
+        if ws is not None:
+            ws.wait_stream(cur)
+            x.record_stream(ws)
+            dy.record_stream(ws)
+            ptab.record_stream(ws)
+        with torch.cuda.stream(ws if ws is not None else cur):
+            st = _stream()
+            part = torch.empty(ns * G * self.cout * self.kt * self.cin_p, device=x.device, dtype=torch.float32)
+            if self.cin_p == self.cin:
+                m.conv_wgrad_g(x.data_ptr(), dy.data_ptr(), part.data_ptr(), grads.data_ptr(), grads.stride(0),
+                               self.off, G, B, 1, H, W, self.cin_p, self.cout, self.kt, self.stride, self.pad, 0, ns,
+                               1.0, ptab.data_ptr(), st)
+            else:  # channel-padded stem: full-width gradient, then the live input channels into the row
+                full = torch.empty(G, self.cout * self.cin_p * self.kt, device=x.device, dtype=torch.float32)
+                m.conv_wgrad_g(x.data_ptr(), dy.data_ptr(), part.data_ptr(), full.data_ptr(), full.stride(0), 0, G, B,
+                               1, H, W, self.cin_p, self.cout, self.kt, self.stride, self.pad, 0, ns, 1.0,
+                               ptab.data_ptr(), st)
+                grads[:, self.off:self.off + self.numel].view(G, self.cout, self.cin, self.kt).copy_(
+                    full.view(G, self.cout, self.cin_p, self.kt)[:, :, :self.cin])
+        st = cur.cuda_stream
         if not need_dx:
             return None
         wt = self.wt
@@ -530,18 +543,21 @@ class GroupedResNet18GN:
         dpool = (dlog.view(G, B, self.ncls, 1) * lw.view(G, 1, self.ncls, self.feat)).sum(2).view(G * B, 1, self.feat)
         a = saved[-1][-1]
         N, H, W, C = a.shape
+        # NIDT_WGRAD_STREAM=1: weight gradients on a branch forked from the data-gradient chain (joined below); off by
+        # default: CIFAR SubAvg 1.077-1.087 vs 1.069-1.078 s/round, Tiny 2.82 vs 2.19 (profiles/r3_ab_wgrad_stream.txt)
+        ws = self._wgrad_stream(G, B)
         # bf16 residual-gradient stream on the HIP path (res_grad writes bf16; re-read by every GroupNorm backward)
         da = (dpool / float(H * W)).expand(N, H * W, C).reshape(N, H, W, C).to(self.act).contiguous()
         for blk, sv in zip(reversed(self.blocks), reversed(saved[1:])):
             xin, t1, s1, h1, t2, s2, ts, ss, a = sv
             dt2 = blk["n2"].bwd(da, a, t2, s2, theta, grads, G)
-            dh1 = blk["c2"].bwd(dt2, h1, theta, grads, G, True)
+            dh1 = blk["c2"].bwd(dt2, h1, theta, grads, G, True, ws=ws)
             dt1 = blk["n1"].bwd(dh1, h1, t1, s1, theta, grads, G)
-            dx1 = blk["c1"].bwd(dt1, xin, theta, grads, G, True)
+            dx1 = blk["c1"].bwd(dt1, xin, theta, grads, G, True, ws=ws)
             dx2 = None
             if "cs" in blk:
                 dts = blk["ns"].bwd(da, a, ts, ss, theta, grads, G)
-                dx2 = blk["cs"].bwd(dts, xin, theta, grads, G, True)
+                dx2 = blk["cs"].bwd(dts, xin, theta, grads, G, True, ws=ws)
             half = dx2 is not None and blk["cs"].stride == 2  # 1x1 stride-2 projection: even-pixel gradient
             if self.hip:
                 out = torch.empty(dx1.shape, device=dx1.device, dtype=torch.bfloat16)
@@ -562,8 +578,20 @@ class GroupedResNet18GN:
                 da = dx1.float() + (dx2.float() if dx2 is not None else da * (a > 0))
         x0, t0, st0, a0 = saved[0]
         dt0 = self.stem_gn.bwd(da, a0, t0, st0, theta, grads, G)
-        self.stem.bwd(dt0, x0, theta, grads, G, False)
+        self.stem.bwd(dt0, x0, theta, grads, G, False, ws=ws)
+        if ws is not None:
+            torch.cuda.current_stream().wait_stream(ws)  # join: the optimizer reads every weight gradient
         return losses.detach()
+
+    def _wgrad_stream(self, G, B):
+        """Weight-gradient branch stream of one launch shape (None on CPU or with NIDT_WGRAD_STREAM=0)."""
+        if not self.hip or os.environ.get("NIDT_WGRAD_STREAM", "0") != "1":
+            return None
+        if not hasattr(self, "_ws"):
+            self._ws = {}
+        if (G, B) not in self._ws:
+            self._ws[(G, B)] = torch.cuda.Stream(device=self.device)
+        return self._ws[(G, B)]
 
     def eval_logits(self, theta, x, G):
         logits, _, _ = self.forward(x, theta, G)

@@ -22,6 +22,8 @@ framework's config-5 model (``models/resnet3d.py``).
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn.functional as F
 
@@ -104,7 +106,9 @@ class GConv3:
                  self.kt, self.stride, self.pad, self.pad if self.kt == 27 else 0, x.device)
         return y
 
-    def bwd(self, dy, x, theta, grads, G, need_dx=True):
+    def bwd(self, dy, x, theta, grads, G, need_dx=True, ws=None):
+        """dW -> grads rows; returns dX (None without ``need_dx``).  ``ws``: stream of the step's weight-gradient
+        branch (the wgrad is forked onto it; the caller joins it before the optimizer)."""
         if not self.hip:
             w = theta[:, self.off:self.off + self.numel].detach().clone().requires_grad_(True)
             xx = x.detach().clone().requires_grad_(need_dx)
@@ -124,7 +128,6 @@ class GConv3:
         dy = dy.contiguous()
         padd = self.pad if self.kt == 27 else 0
         ns = m.conv_wgrad_nsplit_g(G, B, D, H, W, self.cin, self.cout, self.kt, self.stride, self.pad, padd)
-        part = torch.empty(ns * G * self.cout * self.kt * self.cin, device=x.device, dtype=torch.float32)
         key = (B, D, H, W)
         ptab = self._ptabs.get(key)
         if ptab is None:  # a function of the shape only: built once per (B, D, H, W)
@@ -132,9 +135,16 @@ class GConv3:
             m.conv_pos_table_g(ptab.data_ptr(), B, D, H, W, self.kt, self.stride, self.pad, padd, st)
             if not torch.cuda.is_current_stream_capturing():
                 self._ptabs[key] = ptab
-        m.conv_wgrad_g(x.data_ptr(), dy.data_ptr(), part.data_ptr(), grads.data_ptr(), grads.stride(0), self.off, G,
-                       B, D, H, W, self.cin, self.cout, self.kt, self.stride, self.pad, padd, ns, 1.0, ptab.data_ptr(),
-                       st)
+        cur = torch.cuda.current_stream()
+        if ws is not None:
+            ws.wait_stream(cur)
+            for t in (x, dy, ptab):
+                t.record_stream(ws)
+        with torch.cuda.stream(ws if ws is not None else cur):
+            part = torch.empty(ns * G * self.cout * self.kt * self.cin, device=x.device, dtype=torch.float32)
+            m.conv_wgrad_g(x.data_ptr(), dy.data_ptr(), part.data_ptr(), grads.data_ptr(), grads.stride(0), self.off,
+                           G, B, D, H, W, self.cin, self.cout, self.kt, self.stride, self.pad, padd, ns, 1.0,
+                           ptab.data_ptr(), _stream())
         if not need_dx:
             return None
         pk, self.wt = self.wt, None
@@ -437,18 +447,25 @@ class GroupedResNet3D:
         # the residual-stream gradient is kept in bf16 on the HIP path (res_grad writes bf16): it is re-read by the
         # BatchNorm backward of every block, where fp32 doubled the bytes
         da = dpool.expand(N, S, self.feat).reshape(a.shape).to(self.act).contiguous()
+        # NIDT_WGRAD_STREAM=1: weight gradients on a branch forked from the data-gradient chain (joined after the stem
+        # backward); off by default, as in the 2-D engine (profiles/r3_ab_wgrad_stream.txt)
+        ws = None
+        if self.hip and os.environ.get("NIDT_WGRAD_STREAM", "0") == "1":
+            if getattr(self, "_ws", None) is None:
+                self._ws = torch.cuda.Stream(device=self.device)
+            ws = self._ws
         for blk, sv in zip(reversed(self.blocks), reversed(saved)):
             xin, t1, s1, h1, t2, s2, h2, t3, s3, td, sd, a = sv
             dt3 = blk["n3"].bwd(da, a, t3, s3, theta, grads, G)
-            dh2 = blk["c3"].bwd(dt3, h2, theta, grads, G)
+            dh2 = blk["c3"].bwd(dt3, h2, theta, grads, G, ws=ws)
             dt2 = blk["n2"].bwd(dh2, h2, t2, s2, theta, grads, G)
-            dh1 = blk["c2"].bwd(dt2, h1, theta, grads, G)
+            dh1 = blk["c2"].bwd(dt2, h1, theta, grads, G, ws=ws)
             dt1 = blk["n1"].bwd(dh1, h1, t1, s1, theta, grads, G)
-            dx1 = blk["c1"].bwd(dt1, xin, theta, grads, G)
+            dx1 = blk["c1"].bwd(dt1, xin, theta, grads, G, ws=ws)
             dx2 = None
             if "cd" in blk:
                 dtd = blk["nd"].bwd(da, a, td, sd, theta, grads, G)
-                dx2 = blk["cd"].bwd(dtd, xin, theta, grads, G)
+                dx2 = blk["cd"].bwd(dtd, xin, theta, grads, G, ws=ws)
             half = dx2 is not None and blk["cd"].stride == 2  # 1x1x1 stride-2 projection: even-voxel gradient
             if self.hip:
                 out = torch.empty(dx1.shape, device=dx1.device, dtype=torch.bfloat16)
@@ -469,6 +486,8 @@ class GroupedResNet3D:
                 da = dx1.float() + (dx2.float() if dx2 is not None else da * (a > 0))
         if self.hip:
             self._stem_hip_bwd(stem, da, theta, grads, G)
+            if ws is not None:
+                torch.cuda.current_stream().wait_stream(ws)  # join: the optimizer reads every weight gradient
             return losses.detach()
         out, leaf = stem
         gw, gg, gb = torch.autograd.grad(out, leaf, da.to(out.dtype))
