@@ -39,6 +39,13 @@ int conv3d_fwd_tri_ok(int B, int D, int H, int W, int Cin, int Cout, int pad);
 int conv3d_union_umax(int B, int D, int H, int W, int pad, int P);
 int conv3d_fwd_tri_pick(int G, int B, int D, int H, int W, int Cin, int Cout, int pad);
 int conv3d_fwd_tri_table_size(int B, int D, int H, int W, int pad);
+int conv3d_fwd_slab_ok(int B, int D, int H, int W, int Cin, int Cout, int pad);
+int conv3d_slab_umax(int B, int D, int H, int W, int pad);
+int conv3d_fwd_slab_pick(int G, int B, int D, int H, int W, int Cin, int Cout, int pad);
+int conv3d_fwd_slab_table_size(int B, int D, int H, int W, int pad);
+void conv3d_fwd_slab_table(uintptr_t tab, int B, int D, int H, int W, int pad, uintptr_t stream);
+void conv3d_fwd_slab(uintptr_t x, uintptr_t w, uintptr_t bias, int64_t bias_ld, uintptr_t y, uintptr_t stats, int G,
+                     int B, int D, int H, int W, int Cin, int Cout, int pad, uintptr_t utab, uintptr_t stream);
 void conv3d_fwd_tri_table(uintptr_t tab, int B, int D, int H, int W, int pad, uintptr_t stream);
 void conv3d_fwd_tri(uintptr_t x, uintptr_t w, uintptr_t bias, int64_t bias_ld, uintptr_t y, uintptr_t stats, int G,
                     int B, int D, int H, int W, int Cin, int Cout, int pad, uintptr_t utab, uintptr_t stream);
@@ -194,6 +201,12 @@ PYBIND11_MODULE(_nidt_hip, m) {
   DEF(conv3d_fwd_tri_table_size);
   DEF(conv3d_fwd_tri_table);
   DEF(conv3d_fwd_tri);
+  DEF(conv3d_fwd_slab_ok);
+  DEF(conv3d_slab_umax);
+  DEF(conv3d_fwd_slab_pick);
+  DEF(conv3d_fwd_slab_table_size);
+  DEF(conv3d_fwd_slab_table);
+  DEF(conv3d_fwd_slab);
   DEF(conv3d_wgrad_tri_nsplit);
   DEF(conv3d_wgrad_tri_table);
   DEF(conv3d_wgrad_tri_ok);

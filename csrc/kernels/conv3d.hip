@@ -373,12 +373,27 @@ __global__ __launch_bounds__(64 * WM * WN, ((NST == 2 ? 8 : 4) / (WM * WN)) > 0 
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // uniform: LDS destinations stay in SGPRs
   const int wco = wid / WN, wp = wid % WN;
   const int Cin = a.Cin, nck = Cin / BK, nks = ntap * nck;
-  const int ks0 = nks * sp / a.ksplit, ks1 = nks * (sp + 1) / a.ksplit;  // this split's k-steps
+  int ks0 = nks * sp / a.ksplit, ks1 = nks * (sp + 1) / a.ksplit;  // this split's k-steps
   const int lrow = lane >> 3, slot = lane & 7;
+  const int S = a.Do * a.Ho * a.Wo;
+  if (a.kt == 27 && !a.nph && a.padd > 0) {
+    // depth taps kd that read only padding for EVERY position of this block are skipped (their B rows are all
+    // zeros): the conv2 data gradient (pad 2 over 17 dy planes) spends 27 % of its MACs on padding, and blocks
+    // inside the border output planes need only 1 or 2 of the 3 kd.  Positions of one sample only; a block that
+    // spans two samples keeps every kd.  The result is bitwise unchanged (only zero products are dropped).
+    const int m_lo = pb * BP, m_hi = min(m_lo + BP, a.Mg) - 1;
+    int od_lo = 0, od_hi = a.Do - 1;
+    if (m_lo / S == m_hi / S) {
+      od_lo = (m_lo % S) / (a.Ho * a.Wo);
+      od_hi = (m_hi % S) / (a.Ho * a.Wo);
+    }
+    const int kd_lo = max(0, a.padd - od_hi * a.st), kd_hi = min(2, a.D - 1 + a.padd - od_lo * a.st);
+    ks0 = max(ks0, 9 * kd_lo * nck);
+    ks1 = min(ks1, 9 * (kd_hi + 1) * nck);
+  }
 
   // ---- per-thread B rows: one per LDS-DMA instruction, fixed over the k loop (byte offsets in the client's input;
   // rows past the end and padding taps read out of range -> zeros) ----
-  const int S = a.Do * a.Ho * a.Wo;
   int roff[B_INSTR];
   uint32_t tmask[B_INSTR];
 #pragma unroll
@@ -428,6 +443,7 @@ __global__ __launch_bounds__(64 * WM * WN, ((NST == 2 ? 8 : 4) / (WM * WN)) > 0 
     for (int j = 0; j < TP; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int fr = lane & 15, fq = lane >> 4;
+  if (ks0 < ks1) {  // block-uniform; empty only for a split-K slice outside the block's live kd range
   // prologue: stages 0 .. NST-2 in flight, wait for stage 0 only
   DMA_ISSUE(ks0, 0)
 #pragma unroll
@@ -477,6 +493,7 @@ __global__ __launch_bounds__(64 * WM * WN, ((NST == 2 ? 8 : 4) / (WM * WN)) > 0 
     }
     __builtin_amdgcn_s_barrier();
     cur = cur + 1 == NST ? 0 : cur + 1;
+  }
   }
 #undef DMA_ISSUE
   if (a.ksplit > 1) {  // raw fp32 partials; bias, bf16 output and statistics come from k_fwd_splitk_fin
@@ -625,6 +642,143 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void k_conv_fwd_tri(ConvFwdArgs a,
     __builtin_amdgcn_s_barrier();
     if (kw == 2 && q + 1 < ntr) {  // every wave is done with this triplet's union: reload it for the next one
       issue_u(q + 1);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+    }
+  }
+  __syncthreads();
+  conv_fwd_epilogue<BCO, BP, WM, WN, BIAS, STATS, TCO, TP>(a, acc, reinterpret_cast<float*>(smem), g, pb, co0, wco, wp, fr,
+                                                         fq, tid);
+}
+
+// k_conv_fwd_slab — 3x3x3 stride-1 forward/dgrad with the B operand staged once per (kd, 64-channel chunk) slab for
+// all nine (kh, kw) taps.  k_conv_fwd_tri reloads a union per (kd, kh) triplet (3 x ~288 rows per kd for conv2); the
+// runs of a slab union are whole windows b(p) .. b(p) + 2 Wp + 2 of the padded input (k_union_table with
+// ext = 2 Wp + 2), so tap (kh, kw) of position p reads union row idx(p) + kh Wp + kw and one union of <= 384 rows
+// (~352 on average for conv2) serves 9 k-steps: 2.3x fewer B bytes than the triplet unions, 6x fewer than
+// per-tap tiles, and one exposed union reload per 9 k-steps instead of per 3.  The weight tile is double-buffered
+// per tap as in k_conv_fwd_tri; 256-position blocks and the k_conv_fwd_dma epilogue / statistics layout.  Depth taps
+// that read only padding for every position of a block (border output planes of the padded data gradient) are
+// skipped.  LDS: 48 KB union + 2 weight tiles (16 / 32 KB): two blocks per CU also at 128 output channels.
+template <int BCO, int WM, int WN, int U, bool PADDED, bool BIAS, bool STATS>
+__global__ __launch_bounds__(64 * WM * WN, 2) void k_conv_fwd_slab(ConvFwdArgs a, int nCO, const int* __restrict__ utab) {
+  constexpr int NW = WM * WN, BP = 64 * WN, BK = 64;
+  constexpr int WCO = BCO / WM, WP = 64, TCO = WCO / 16, TP = WP / 16;
+  constexpr int A_ELEMS = BCO * BK, ST = 2 * U + BP;
+  constexpr int A_INSTR = BCO / (8 * NW);
+  constexpr int UP = U / 8, UPW = (UP + NW - 1) / NW;  // union pieces (8 rows) per wave
+  static_assert(A_INSTR >= 1 && U % 8 == 0, "tile split");
+  __shared__ __attribute__((aligned(16))) uint16_t smem[2 * A_ELEMS + U * BK];
+  uint16_t* const sAb = smem;
+  uint16_t* const sU = smem + 2 * A_ELEMS;
+
+  const int nwg = gridDim.x;
+  const int id = xcd_remap(blockIdx.x, nwg);
+  const int cot = id % nCO, rest = id / nCO;
+  const int pb = rest % a.nPB, g = rest / a.nPB;
+  const int co0 = cot * BCO;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wco = wid / WN, wp = wid % WN;
+  const int Cin = a.Cin, nck = Cin / BK, Wp = a.W + 2 * a.pad;
+  // depth taps of this block (see k_conv_fwd_dma): slabs q = kd * nck + cc for kd in [kd_lo, kd_hi]
+  int kd_lo = 0, kd_hi = 2;
+  if (PADDED) {
+    const int S = a.Do * a.Ho * a.Wo, m_lo = pb * BP, m_hi = min(m_lo + BP, a.Mg) - 1;
+    if (m_lo / S == m_hi / S) {
+      const int od_lo = (m_lo % S) / (a.Ho * a.Wo), od_hi = (m_hi % S) / (a.Ho * a.Wo);
+      kd_lo = max(0, a.pad - od_hi);
+      kd_hi = min(2, a.D - 1 + a.pad - od_lo);
+    }
+  }
+  const int q0 = kd_lo * nck, nq = (kd_hi + 1) * nck - q0, nks = 9 * nq;
+  const int lrow = lane >> 3, slot = lane & 7;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int* ent = utab + (int64_t)pb * ST;
+  int uoff[UPW], ucode[UPW];
+#pragma unroll
+  for (int i = 0; i < UPW; ++i) {
+    const int u = 8 * (wid * UPW + i) + lrow;
+    uoff[i] = 0;
+    ucode[i] = 1023;
+    if (wid * UPW + i < UP) {
+      uoff[i] = ent[2 * u] * (Cin * 2) + ((slot ^ swz_un(u)) << 4);
+      ucode[i] = ent[2 * u + 1];
+    }
+  }
+  int hrow[TP];
+#pragma unroll
+  for (int j = 0; j < TP; ++j) hrow[j] = ent[2 * U + wp * WP + j * 16 + fr];
+  int aoff[A_INSTR];
+#pragma unroll
+  for (int i = 0; i < A_INSTR; ++i) {
+    const int row = 8 * (wid * A_INSTR + i) + lrow;
+    aoff[i] = ((co0 + row) * 27 * Cin + ((slot ^ swz_dma(row)) << 3)) * 2;
+  }
+  const int64_t xcl = (int64_t)a.B * a.D * a.H * a.W * Cin;
+  const i32x4_t rxs = make_rsrc(a.x + (int64_t)g * xcl, (uint32_t)(xcl * 2));
+  const i32x4_t rws = make_rsrc(a.w + (int64_t)g * a.Cout * 27 * Cin, (uint32_t)(a.Cout * 27 * Cin * 2));
+
+  auto issue_a = [&](int ks, int buf) {  // weight tile of tap (kd, t = kh * 3 + kw) of slab q0 + ks / 9
+    const int q = q0 + ks / 9, t = ks % 9, kd = q / nck, cc = q - kd * nck;
+    const int woff = ((kd * 9 + t) * Cin + cc * BK) * 2;
+    uint16_t* sA = sAb + buf * A_ELEMS;
+#pragma unroll
+    for (int i = 0; i < A_INSTR; ++i) blds16(rws, aoff[i] + woff, sA + (wid * A_INSTR + i) * 512);
+  };
+  auto issue_u = [&](int q) {  // union rows of slab q (its kd shift and 64-channel chunk)
+    const int kd = q / nck, cc = q - kd * nck;
+    const int add = kd * a.H * a.W * (Cin * 2) + cc * (BK * 2);
+    const int dlo = a.pad - kd;
+#pragma unroll
+    for (int i = 0; i < UPW; ++i) {
+      if (wid * UPW + i >= UP) continue;
+      const int c = ucode[i];
+      const bool ok = PADDED ? ((unsigned)((c & 1023) - dlo) < (unsigned)a.D &&
+                                (unsigned)(((c >> 10) & 1023) - a.pad) < (unsigned)a.H &&
+                                (unsigned)((c >> 20) - a.pad) < (unsigned)a.W)
+                             : (c & 1023) != 1023;
+      blds16(rxs, ok ? uoff[i] + add : kBufOOB, sU + (wid * UPW + i) * 512);
+    }
+  };
+
+  f32x4 acc[TCO][TP];
+#pragma unroll
+  for (int i = 0; i < TCO; ++i)
+#pragma unroll
+    for (int j = 0; j < TP; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  issue_u(q0);
+  issue_a(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  for (int ks = 0; ks < nks; ++ks) {
+    const int ql = ks / 9, t = ks - 9 * ql, kh = t / 3, kw = t - 3 * kh;
+    if (ks + 1 < nks) issue_a(ks + 1, (ks + 1) & 1);
+    const uint16_t* sA = sAb + (ks & 1) * A_ELEMS;
+    const int toff = kh * Wp + kw;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 fa[TCO], fb[TP];
+#pragma unroll
+      for (int i = 0; i < TCO; ++i) {
+        const int r = wco * WCO + i * 16 + fr;
+        fa[i] = *reinterpret_cast<const bf16x8*>(&sA[r * BK + (((4 * kk + fq) ^ swz_dma(r)) << 3)]);
+      }
+#pragma unroll
+      for (int j = 0; j < TP; ++j) {
+        const int r = hrow[j] + toff;
+        fb[j] = *reinterpret_cast<const bf16x8*>(&sU[r * BK + (((4 * kk + fq) ^ swz_un(r)) << 3)]);
+      }
+#pragma unroll
+      for (int i = 0; i < TCO; ++i)
+#pragma unroll
+        for (int j = 0; j < TP; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (t == 8 && ql + 1 < nq) {  // every wave is done with this slab's union: reload it for the next one
+      issue_u(q0 + ql + 1);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
     }
@@ -1042,8 +1196,8 @@ int conv3d_fwd_bp(int Cin, int Cout, int xf, int G, int Mg) {
   return 256;
 }
 
-static int union_umax(int B, int D, int H, int W, int pad, int P);
-__global__ void k_union_table(int* tab, int U, int P, int Mg, int D, int H, int W, int pad);
+static int union_umax(int B, int D, int H, int W, int pad, int P, int ext = 2);
+__global__ void k_union_table(int* tab, int U, int P, int Mg, int D, int H, int W, int pad, int ext);
 
 static inline int ft_ucap(int umax) { return umax <= 320 ? 320 : (umax <= 384 ? 384 : 0); }
 
@@ -1087,7 +1241,7 @@ void conv3d_fwd_tri_table(uintptr_t tab, int B, int D, int H, int W, int pad, ui
   NIDT_REQUIRE(U > 0, "conv3d_fwd_tri_table: shape not eligible");
   NIDT_REQUIRE(D + 2 * pad < 1024 && H + 2 * pad < 1024 && W + 2 * pad < 1024, "conv3d_fwd_tri_table: extents < 1024");
   hipLaunchKernelGGL(k_union_table, dim3(ceil_div(Mg, 256)), dim3(256), 0, as_stream(stream), ptr<int>(tab), U, 256, Mg,
-                     D, H, W, pad);
+                     D, H, W, pad, 2);
   NIDT_CHECK(hipGetLastError());
 }
 
@@ -1123,6 +1277,84 @@ void conv3d_fwd_tri(uintptr_t x, uintptr_t w, uintptr_t bias, int64_t bias_ld, u
 #undef NIDT_FT_U
 #undef NIDT_FT_B
 #undef NIDT_FT
+  NIDT_CHECK(hipGetLastError());
+}
+
+// ---- k_conv_fwd_slab host side (union rows <= 384 per 256-position band; ext = 2 Wp + 2) ----
+static inline int slab_ext(int W, int pad) { return 2 * (W + 2 * pad) + 2; }
+static inline int fs_ucap(int umax) { return umax <= 384 ? 384 : 0; }
+
+// largest kd-slab union (rows) of a 256-position band: exposed for host-side tests of the slab rule
+int conv3d_slab_umax(int B, int D, int H, int W, int pad) { return union_umax(B, D, H, W, pad, 256, slab_ext(W, pad)); }
+
+int conv3d_fwd_slab_ok(int B, int D, int H, int W, int Cin, int Cout, int pad) {
+  if (Cin % 64 != 0 || Cout % 64 != 0 || pad < 0 || pad > 2 || (int64_t)Cin * 27 > 27 * kMaxCin) return 0;
+  const int Mg = B * (D + 2 * pad - 2) * (H + 2 * pad - 2) * (W + 2 * pad - 2);
+  if (D + 2 * pad < 3 || H + 2 * pad < 3 || W + 2 * pad < 3 || Mg <= 0) return 0;
+  if (D + 2 * pad >= 1024 || H + 2 * pad >= 1024 || W + 2 * pad >= 1024) return 0;
+  return fs_ucap(union_umax(B, D, H, W, pad, 256, slab_ext(W, pad))) > 0 ? 1 : 0;
+}
+
+// Chosen for every eligible shape (measured, profiles/r3_ab_fwd_slab.txt, 64 clients: conv2 dgrad 3.60 -> 3.26 ms
+// against the per-tap kernel, conv2 fwd 2.65 -> 2.52 ms against k_conv_fwd_tri).  NIDT_FWD_SLAB=0 turns it off,
+// =1 keeps it to padded convs (A/B).
+int conv3d_fwd_slab_pick(int G, int B, int D, int H, int W, int Cin, int Cout, int pad) {
+  static const int env = [] {
+    const char* e = getenv("NIDT_FWD_SLAB");
+    return e ? atoi(e) : 2;
+  }();
+  if (!env || !conv3d_fwd_slab_ok(B, D, H, W, Cin, Cout, pad)) return 0;
+  const int Mg = B * (D + 2 * pad - 2) * (H + 2 * pad - 2) * (W + 2 * pad - 2);
+  if (conv3d_fwd_bp(Cin, Cout, 0, G, Mg) != 256 || conv3d_fwd_ksplit(Cin, Cout, G, Mg) > 1) return 0;
+  return (pad > 0 || env == 2) ? 1 : 0;
+}
+
+int conv3d_fwd_slab_table_size(int B, int D, int H, int W, int pad) {
+  const int Mg = B * (D + 2 * pad - 2) * (H + 2 * pad - 2) * (W + 2 * pad - 2);
+  const int U = fs_ucap(union_umax(B, D, H, W, pad, 256, slab_ext(W, pad)));
+  NIDT_REQUIRE(U > 0, "conv3d_fwd_slab_table_size: shape not eligible");
+  return ceil_div(Mg, 256) * (2 * U + 256);
+}
+
+void conv3d_fwd_slab_table(uintptr_t tab, int B, int D, int H, int W, int pad, uintptr_t stream) {
+  const int Mg = B * (D + 2 * pad - 2) * (H + 2 * pad - 2) * (W + 2 * pad - 2);
+  const int U = fs_ucap(union_umax(B, D, H, W, pad, 256, slab_ext(W, pad)));
+  NIDT_REQUIRE(U > 0, "conv3d_fwd_slab_table: shape not eligible");
+  hipLaunchKernelGGL(k_union_table, dim3(ceil_div(Mg, 256)), dim3(256), 0, as_stream(stream), ptr<int>(tab), U, 256, Mg,
+                     D, H, W, pad, slab_ext(W, pad));
+  NIDT_CHECK(hipGetLastError());
+}
+
+void conv3d_fwd_slab(uintptr_t x, uintptr_t w, uintptr_t bias, int64_t bias_ld, uintptr_t y, uintptr_t stats, int G,
+                     int B, int D, int H, int W, int Cin, int Cout, int pad, uintptr_t utab, uintptr_t stream) {
+  NIDT_REQUIRE(conv3d_fwd_slab_ok(B, D, H, W, Cin, Cout, pad) && utab != 0, "conv3d_fwd_slab: shape not supported");
+  NIDT_REQUIRE((int64_t)B * D * H * W * Cin * 2 < (1ll << 31), "conv3d_fwd_slab: per-client input below 2 GiB");
+  const bool hb = bias != 0, st = stats != 0;
+  NIDT_REQUIRE(!st || hb, "conv3d_fwd_slab: statistics require a bias");
+  ConvFwdArgs a;
+  a.x = ptr<const uint16_t>(x); a.w = ptr<const uint16_t>(w); a.bias = ptr<const float>(bias);
+  a.xs = nullptr; a.xt = nullptr; a.y = ptr<uint16_t>(y); a.stats = ptr<float>(stats);
+  a.B = B; a.D = D; a.H = H; a.W = W; a.Cin = Cin; a.Cout = Cout; a.pad = pad; a.padd = pad; a.kt = 27; a.st = 1;
+  a.Do = D + 2 * pad - 2; a.Ho = H + 2 * pad - 2; a.Wo = W + 2 * pad - 2;
+  a.Mg = B * a.Do * a.Ho * a.Wo;
+  a.nPB = ceil_div(a.Mg, 256);
+  a.G = G;
+  a.bias_ld = bias_ld;
+  const int bco = fwd_bco(Cout), nCO = Cout / bco;
+  const dim3 grid((unsigned)((int64_t)a.nPB * nCO * G));
+  hipStream_t s = as_stream(stream);
+  const int* tab = ptr<const int>(utab);
+#define NIDT_FS(BC, WM, PD, BI, STT) \
+  hipLaunchKernelGGL((k_conv_fwd_slab<BC, WM, 4, 384, PD, BI, STT>), grid, dim3(256 * WM), 0, s, a, nCO, tab)
+#define NIDT_FS_B(BC, WM, PD) \
+  if (st) NIDT_FS(BC, WM, PD, true, true); else if (hb) NIDT_FS(BC, WM, PD, true, false); else NIDT_FS(BC, WM, PD, false, false);
+  if (bco == 128) {
+    if (pad) { NIDT_FS_B(128, 2, true) } else { NIDT_FS_B(128, 2, false) }
+  } else {
+    if (pad) { NIDT_FS_B(64, 1, true) } else { NIDT_FS_B(64, 1, false) }
+  }
+#undef NIDT_FS_B
+#undef NIDT_FS
   NIDT_CHECK(hipGetLastError());
 }
 
@@ -1563,10 +1795,13 @@ static inline int wt_umax_cap(int umax) { return umax <= 80 ? 80 : (umax <= 96 ?
 
 // Union table of a 3x3x3 stride-1 conv (pad in every dimension), one entry per band of P consecutive output positions
 // of a client: int2 rows[U] = {voxel offset of the union row's (kd, kh) = (0, 0) source, padded (d, h, w) code},
-// int idx[P] = union row of each position's tap (0, 0, 0).  The union is the set of padded-input rows b(p) + kw
-// (kw = 0..2) over the band, in increasing order; rows past the union get a depth code that no range admits.
+// int idx[P] = union row of each position's tap (0, 0, 0).  The union is the set of padded-input rows b(p) + e
+// (e = 0..ext) over the band, in increasing order; rows past the union get a depth code that no range admits.
+// ext = 2: the three kw taps of one (kd, kh) (k_conv_fwd_tri, k_conv_wgrad_tri); ext = 2 Wp + 2: all nine (kh, kw)
+// taps of one kd, whose rows are idx(p) + kh Wp + kw because every run is whole (k_conv_fwd_slab).
 // One block of P threads per band (P <= 256); one thread merges the runs (allocation time only).
-__global__ __launch_bounds__(256) void k_union_table(int* tab, int U, int P, int Mg, int D, int H, int W, int pad) {
+__global__ __launch_bounds__(256) void k_union_table(int* tab, int U, int P, int Mg, int D, int H, int W, int pad,
+                                                      int ext) {
   __shared__ int b[256];
   const int Dp = D + 2 * pad, Hp = H + 2 * pad, Wp = W + 2 * pad, Do = Dp - 2, Ho = Hp - 2, Wo = Wp - 2;
   const int S = Do * Ho * Wo, VOL = Dp * Hp * Wp + 8;  // sample n's padded rows live at n * VOL + padded index
@@ -1588,7 +1823,7 @@ __global__ __launch_bounds__(256) void k_union_table(int* tab, int U, int P, int
     int first;
     if (cnt > 0 && bq <= last) { idx[q] = cnt - 1 - (last - bq); first = last + 1; }
     else { idx[q] = cnt; first = bq; }
-    for (int r = first; r <= bq + 2; ++r) {
+    for (int r = first; r <= bq + ext; ++r) {
       if (cnt < U) {
         const int n = r / VOL, l = r - n * VOL, dp = l / (Hp * Wp), l2 = l - dp * Hp * Wp, hp = l2 / Wp, wp = l2 - hp * Wp;
         rows[2 * cnt] = ((n * D + dp - pad) * H + hp - pad) * W + wp - pad;
@@ -1596,7 +1831,7 @@ __global__ __launch_bounds__(256) void k_union_table(int* tab, int U, int P, int
       }
       ++cnt;
     }
-    last = max(last, bq + 2);
+    last = max(last, bq + ext);
   }
   for (int u = cnt; u < U; ++u) {
     rows[2 * u] = 0;
@@ -1605,9 +1840,9 @@ __global__ __launch_bounds__(256) void k_union_table(int* tab, int U, int P, int
 }
 
 // largest union of one P-position band (same rule as k_union_table), cached per shape
-static int union_umax(int B, int D, int H, int W, int pad, int P) {
-  static std::map<std::array<int, 6>, int> cache;
-  const std::array<int, 6> key{B, D, H, W, pad, P};
+static int union_umax(int B, int D, int H, int W, int pad, int P, int ext) {
+  static std::map<std::array<int, 7>, int> cache;
+  const std::array<int, 7> key{B, D, H, W, pad, P, ext};
   auto it = cache.find(key);
   if (it != cache.end()) return it->second;
   const int Dp = D + 2 * pad, Hp = H + 2 * pad, Wp = W + 2 * pad, Do = Dp - 2, Ho = Hp - 2, Wo = Wp - 2;
@@ -1619,8 +1854,8 @@ static int union_umax(int B, int D, int H, int W, int pad, int P) {
       const int nl = m / S, r = m - nl * S, od = r / (Ho * Wo), r2 = r - od * Ho * Wo, oh = r2 / Wo, ow = r2 - oh * Wo;
       const int bq = nl * VOL + (od * Hp + oh) * Wp + ow;
       const int first = (cnt > 0 && bq <= last) ? last + 1 : bq;
-      cnt += std::max(0, bq + 3 - first);
-      last = std::max(last, bq + 2);
+      cnt += std::max(0, bq + ext + 1 - first);
+      last = std::max(last, bq + ext);
     }
     mx = std::max(mx, cnt);
   }
@@ -1807,7 +2042,7 @@ void conv3d_wgrad_tri_table(uintptr_t tab, int B, int D, int H, int W, int pad, 
   NIDT_REQUIRE(U > 0, "conv3d_wgrad_tri_table: shape not eligible");
   NIDT_REQUIRE(D + 2 * pad < 1024 && H + 2 * pad < 1024 && W + 2 * pad < 1024, "conv3d_wgrad_tri_table: extents < 1024");
   hipLaunchKernelGGL(k_union_table, dim3(ceil_div(Mg, 64)), dim3(64), 0, as_stream(stream), ptr<int>(tab), U, 64, Mg,
-                     D, H, W, pad);
+                     D, H, W, pad, 2);
   NIDT_CHECK(hipGetLastError());
 }
 

@@ -100,7 +100,12 @@ class HipAlexNet3D:
                 if tag == "d" and not train:
                     continue
                 kname = "ks%s%d" % (tag, ci)
-                if b[kname] <= 1 and self.m.conv3d_fwd_tri_pick(G, B, *vol, c_in, c_out, pd):
+                if b[kname] <= 1 and self.m.conv3d_fwd_slab_pick(G, B, *vol, c_in, c_out, pd):
+                    # kd-slab union staging (k_conv_fwd_slab): the padded conv2 data gradient
+                    tab = e(self.m.conv3d_fwd_slab_table_size(B, *vol, pd), dt=torch.int32)
+                    self.m.conv3d_fwd_slab_table(_p(tab), B, *vol, pd, st0)
+                    b["fs" + kname] = tab
+                elif b[kname] <= 1 and self.m.conv3d_fwd_tri_pick(G, B, *vol, c_in, c_out, pd):
                     tab = e(self.m.conv3d_fwd_tri_table_size(B, *vol, pd), dt=torch.int32)
                     self.m.conv3d_fwd_tri_table(_p(tab), B, *vol, pd, st0)
                     b["ft" + kname] = tab
@@ -142,14 +147,15 @@ class HipAlexNet3D:
         """conv3d_fwd, or its split-K form when ``b[key]`` (chosen at allocation) is > 1.  With ``theta`` the bias
         of conv ``ci`` is read straight from the flat parameter rows (row stride P), no per-step copy."""
         ks = b[key]
-        ft = b.get("ft" + key)
-        if ft is not None:  # union-staged B operand (k_conv_fwd_tri)
+        ft, fs = b.get("ft" + key), b.get("fs" + key)
+        if ft is not None or fs is not None:  # union-staged B operand (k_conv_fwd_slab / k_conv_fwd_tri)
             if theta is not None:
                 o = self.o["features.%d.bias" % ci]
                 bptr, bld = theta.data_ptr() + 4 * o, theta.stride(0)
             else:
                 bptr, bld = _p(bias), 0
-            self.m.conv3d_fwd_tri(_p(x), _p(w), bptr, bld, _p(y), _p(stats), G, B, D, H, W, cin, cout, pad, _p(ft), st)
+            fn = self.m.conv3d_fwd_slab if fs is not None else self.m.conv3d_fwd_tri
+            fn(_p(x), _p(w), bptr, bld, _p(y), _p(stats), G, B, D, H, W, cin, cout, pad, _p(fs if fs is not None else ft), st)
             return
         if theta is not None and ks <= 1:
             o = self.o["features.%d.bias" % ci]

@@ -1,5 +1,5 @@
 """Host-side rules of the union-staged conv kernels (``csrc/kernels/conv3d.hip``: ``k_conv_wgrad_tri``,
-``k_conv_fwd_tri``): the union size of a band of output positions (which decides eligibility and the kernel's U) against
+``k_conv_fwd_tri``, ``k_conv_fwd_slab``): the union size of a band of output positions (which decides eligibility and the kernel's U) against
 an independent Python model of the padded-input rows the three kw taps read, and the launch-choice rules measured in
 ``profiles/r2_ab_wgrad_tri.txt`` / ``profiles/r2_ab_fwd_tri.txt``.  Runs on the CPU (host functions of the built
 extension; skipped when it is not built)."""
@@ -14,8 +14,9 @@ def _ext():
         pytest.skip("HIP extension not built: %s" % e)
 
 
-def _union_rows(B, D, H, W, pad, P):
-    """Largest number of distinct padded-input rows {b(p) + kw} over the bands of P consecutive output positions."""
+def _union_rows(B, D, H, W, pad, P, slab=False):
+    """Largest number of distinct padded-input rows {b(p) + kw} (``slab``: the whole window b(p) .. b(p) + 2 Wp + 2)
+    over the bands of P consecutive output positions."""
     Dp, Hp, Wp = D + 2 * pad, H + 2 * pad, W + 2 * pad
     Do, Ho, Wo = Dp - 2, Hp - 2, Wp - 2
     S, vol = Do * Ho * Wo, Dp * Hp * Wp
@@ -28,7 +29,7 @@ def _union_rows(B, D, H, W, pad, P):
             od, r = divmod(r, Ho * Wo)
             oh, ow = divmod(r, Wo)
             base = n * vol + (od * Hp + oh) * Wp + ow
-            rows.update((base, base + 1, base + 2))
+            rows.update(range(base, base + (2 * Wp + 3 if slab else 3)))
         best = max(best, len(rows))
     return best
 
@@ -63,3 +64,43 @@ def test_union_kernel_choices():
     per = m.conv3d_wgrad_tri_table_size(16, 19, 23, 19, 0) // n_bands
     assert per * n_bands == m.conv3d_wgrad_tri_table_size(16, 19, 23, 19, 0)
     assert (per - 64) % 16 == 0 and (per - 64) // 2 >= m.conv3d_union_umax(16, 19, 23, 19, 0, 64)
+
+
+@pytest.mark.parametrize("shape", [(16, 19, 23, 19, 0), (16, 17, 21, 17, 2), (5, 10, 12, 11, 1), (16, 8, 14, 20, 1),
+                                   (3, 19, 23, 19, 0), (16, 5, 7, 5, 1)])
+def test_slab_union_matches_python_model(shape):
+    """kd-slab unions: size vs the Python model, and the addressing invariant the kernel relies on — every tap
+    (kh, kw) of a position reads union row idx(p) + kh Wp + kw (whole windows make the union contiguous there)."""
+    m = _ext()
+    B, D, H, W, pad = shape
+    um = _union_rows(*shape, 256, slab=True)
+    assert m.conv3d_slab_umax(*shape) == um
+    assert m.conv3d_fwd_slab_ok(B, D, H, W, 64, 64, pad) == (1 if um <= 384 else 0)
+    Dp, Hp, Wp = D + 2 * pad, H + 2 * pad, W + 2 * pad
+    Do, Ho, Wo = Dp - 2, Hp - 2, Wp - 2
+    S, vol = Do * Ho * Wo, Dp * Hp * Wp
+    for m0 in range(0, B * S, 256):
+        bases = []
+        for q in range(m0, min(m0 + 256, B * S)):
+            n, r = divmod(q, S)
+            od, r = divmod(r, Ho * Wo)
+            oh, ow = divmod(r, Wo)
+            bases.append(n * vol + (od * Hp + oh) * Wp + ow)
+        union = sorted({b + e for b in bases for e in range(2 * Wp + 3)})
+        pos = {r: i for i, r in enumerate(union)}
+        for b in bases:
+            for kh in range(3):
+                for kw in range(3):
+                    assert pos[b + kh * Wp + kw] == pos[b] + kh * Wp + kw
+
+
+def test_slab_kernel_choice():
+    m = _ext()
+    conv2 = (16, 19, 23, 19, 64, 128, 0)
+    conv2_dgrad = (16, 17, 21, 17, 128, 64, 2)
+    for G in (64, 8):
+        assert m.conv3d_fwd_slab_ok(*conv2) == 1 and m.conv3d_fwd_slab_ok(*conv2_dgrad) == 1
+        assert m.conv3d_fwd_slab_pick(G, *conv2_dgrad) == 1      # padded data gradient: the slab kernel
+    assert m.conv3d_fwd_slab_ok(16, 5, 7, 5, 192, 192, 1) == 0   # 5x7x5 bands: unions of ~470 rows
+    n_bands = -(-16 * 19 * 23 * 19 // 256)
+    assert m.conv3d_fwd_slab_table_size(16, 17, 21, 17, 2) == n_bands * (2 * 384 + 256)

@@ -107,6 +107,48 @@ def test_conv3d_fwd_stats(cin, cout, pad, sp, xf, G, B):
         assert (y3.float() - y.float()).abs().max() <= 1e-2 * y.float().abs().max()
         assert _relerr(st3, stats) < 1e-4
         assert _relerr(y4.float(), (yr.view(G, -1, cout) - bias.view(G, 1, cout)).view_as(yr)) < 1e-2
+    if not xf and bp == 256 and m.conv3d_fwd_slab_ok(B, *sp, cin, cout, pad):
+        # kd-slab union staging (k_conv_fwd_slab): same products as the per-tap kernel, slab-major k order
+        tab = torch.empty(m.conv3d_fwd_slab_table_size(B, *sp, pad), device=DEV, dtype=torch.int32)
+        m.conv3d_fwd_slab_table(tab.data_ptr(), B, *sp, pad, _st())
+        y5 = torch.empty_like(y)
+        st5 = torch.empty_like(stats)
+        m.conv3d_fwd_slab(x.data_ptr(), w.data_ptr(), bias.data_ptr(), 0, y5.data_ptr(), st5.data_ptr(), G, B, *sp,
+                          cin, cout, pad, tab.data_ptr(), _st())
+        torch.cuda.synchronize()
+        assert (y5.float() - y.float()).abs().max() <= 1e-2 * y.float().abs().max()
+        assert _relerr(st5, stats) < 1e-4
+
+
+@pytest.mark.parametrize("cin,cout,pad,sp", [(64, 128, 0, (19, 23, 19)), (128, 64, 2, (17, 21, 17)),
+                                             (64, 64, 1, (10, 12, 11)), (128, 128, 1, (8, 14, 20))])
+@pytest.mark.parametrize("G,B", [(2, 16), (3, 5)])
+def test_conv3d_fwd_slab_matches_fp32(cin, cout, pad, sp, G, B):
+    """kd-slab union forward / data gradient (k_conv_fwd_slab): bands crossing output rows, depth planes and
+    samples, padded geometries whose border planes skip depth taps, with and without bias — against fp32 conv3d."""
+    m = _m()
+    assert m.conv3d_fwd_slab_ok(B, *sp, cin, cout, pad)
+    torch.manual_seed(3)
+    x = torch.randn(G * B, *sp, cin, device=DEV).bfloat16()
+    w = (torch.randn(G, cout, 27, cin, device=DEV) * 0.05).bfloat16()
+    bias = torch.randn(G, cout, device=DEV)
+    Do, Ho, Wo = [s + 2 * pad - 2 for s in sp]
+    tab = torch.empty(m.conv3d_fwd_slab_table_size(B, *sp, pad), device=DEV, dtype=torch.int32)
+    m.conv3d_fwd_slab_table(tab.data_ptr(), B, *sp, pad, _st())
+    y = torch.empty(G * B, Do, Ho, Wo, cout, device=DEV, dtype=torch.bfloat16)
+    y0 = torch.empty_like(y)
+    m.conv3d_fwd_slab(x.data_ptr(), w.data_ptr(), bias.data_ptr(), 0, y.data_ptr(), 0, G, B, *sp, cin, cout, pad,
+                      tab.data_ptr(), _st())
+    m.conv3d_fwd_slab(x.data_ptr(), w.data_ptr(), 0, 0, y0.data_ptr(), 0, G, B, *sp, cin, cout, pad, tab.data_ptr(),
+                      _st())
+    torch.cuda.synchronize()
+    ys = []
+    for g in range(G):
+        wg = w[g].float().view(cout, 3, 3, 3, cin).permute(0, 4, 1, 2, 3)
+        ys.append(_cl(F.conv3d(_cf(x[g * B:(g + 1) * B].float()), wg, None, 1, pad)))
+    yr = torch.cat(ys, 0)
+    assert _relerr(y0.float(), yr) < 1e-2
+    assert _relerr(y.float(), (yr.view(G, -1, cout) + bias.view(G, 1, cout)).view_as(yr)) < 1e-2
 
 
 @pytest.mark.parametrize("cin,cout,G", [(128, 192, 16), (192, 192, 16), (192, 128, 24), (128, 192, 1), (192, 128, 2)])
