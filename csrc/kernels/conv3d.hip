@@ -1281,8 +1281,12 @@ void conv3d_fwd_tri(uintptr_t x, uintptr_t w, uintptr_t bias, int64_t bias_ld, u
 }
 
 // ---- k_conv_fwd_slab host side (union rows <= 384 per 256-position band; ext = 2 Wp + 2) ----
+// (512-position blocks, one 8-wave block per CU with 704-row unions, measured slower for the conv2 data gradient:
+// 3.79 vs 3.28 ms, profiles/r3_ab_fwd_slab.txt — not kept)
 static inline int slab_ext(int W, int pad) { return 2 * (W + 2 * pad) + 2; }
-static inline int fs_ucap(int umax) { return umax <= 384 ? 384 : 0; }
+static inline int slab_u(int B, int D, int H, int W, int pad) {
+  return union_umax(B, D, H, W, pad, 256, slab_ext(W, pad)) <= 384 ? 384 : 0;
+}
 
 // largest kd-slab union (rows) of a 256-position band: exposed for host-side tests of the slab rule
 int conv3d_slab_umax(int B, int D, int H, int W, int pad) { return union_umax(B, D, H, W, pad, 256, slab_ext(W, pad)); }
@@ -1292,7 +1296,7 @@ int conv3d_fwd_slab_ok(int B, int D, int H, int W, int Cin, int Cout, int pad) {
   const int Mg = B * (D + 2 * pad - 2) * (H + 2 * pad - 2) * (W + 2 * pad - 2);
   if (D + 2 * pad < 3 || H + 2 * pad < 3 || W + 2 * pad < 3 || Mg <= 0) return 0;
   if (D + 2 * pad >= 1024 || H + 2 * pad >= 1024 || W + 2 * pad >= 1024) return 0;
-  return fs_ucap(union_umax(B, D, H, W, pad, 256, slab_ext(W, pad))) > 0 ? 1 : 0;
+  return slab_u(B, D, H, W, pad) > 0 ? 1 : 0;
 }
 
 // Chosen for every eligible shape (measured, profiles/r3_ab_fwd_slab.txt, 64 clients: conv2 dgrad 3.60 -> 3.26 ms
@@ -1311,14 +1315,14 @@ int conv3d_fwd_slab_pick(int G, int B, int D, int H, int W, int Cin, int Cout, i
 
 int conv3d_fwd_slab_table_size(int B, int D, int H, int W, int pad) {
   const int Mg = B * (D + 2 * pad - 2) * (H + 2 * pad - 2) * (W + 2 * pad - 2);
-  const int U = fs_ucap(union_umax(B, D, H, W, pad, 256, slab_ext(W, pad)));
+  const int U = slab_u(B, D, H, W, pad);
   NIDT_REQUIRE(U > 0, "conv3d_fwd_slab_table_size: shape not eligible");
   return ceil_div(Mg, 256) * (2 * U + 256);
 }
 
 void conv3d_fwd_slab_table(uintptr_t tab, int B, int D, int H, int W, int pad, uintptr_t stream) {
   const int Mg = B * (D + 2 * pad - 2) * (H + 2 * pad - 2) * (W + 2 * pad - 2);
-  const int U = fs_ucap(union_umax(B, D, H, W, pad, 256, slab_ext(W, pad)));
+  const int U = slab_u(B, D, H, W, pad);
   NIDT_REQUIRE(U > 0, "conv3d_fwd_slab_table: shape not eligible");
   hipLaunchKernelGGL(k_union_table, dim3(ceil_div(Mg, 256)), dim3(256), 0, as_stream(stream), ptr<int>(tab), U, 256, Mg,
                      D, H, W, pad, slab_ext(W, pad));
@@ -1799,10 +1803,10 @@ static inline int wt_umax_cap(int umax) { return umax <= 80 ? 80 : (umax <= 96 ?
 // (e = 0..ext) over the band, in increasing order; rows past the union get a depth code that no range admits.
 // ext = 2: the three kw taps of one (kd, kh) (k_conv_fwd_tri, k_conv_wgrad_tri); ext = 2 Wp + 2: all nine (kh, kw)
 // taps of one kd, whose rows are idx(p) + kh Wp + kw because every run is whole (k_conv_fwd_slab).
-// One block of P threads per band (P <= 256); one thread merges the runs (allocation time only).
-__global__ __launch_bounds__(256) void k_union_table(int* tab, int U, int P, int Mg, int D, int H, int W, int pad,
+// One block of P threads per band (P <= 512); one thread merges the runs (allocation time only).
+__global__ __launch_bounds__(512) void k_union_table(int* tab, int U, int P, int Mg, int D, int H, int W, int pad,
                                                       int ext) {
-  __shared__ int b[256];
+  __shared__ int b[512];
   const int Dp = D + 2 * pad, Hp = H + 2 * pad, Wp = W + 2 * pad, Do = Dp - 2, Ho = Hp - 2, Wo = Wp - 2;
   const int S = Do * Ho * Wo, VOL = Dp * Hp * Wp + 8;  // sample n's padded rows live at n * VOL + padded index
   const int s = blockIdx.x, p = threadIdx.x, m = P * s + p;
