@@ -35,6 +35,14 @@ void conv3d_wgrad(uintptr_t x, uintptr_t xs, uintptr_t xt, uintptr_t dy, uintptr
 void conv3d_pos_table(uintptr_t tab, int B, int D, int H, int W, int pad, uintptr_t stream);
 int conv3d_wgrad_nsplit(int G, int B, int D, int H, int W, int Cin, int Cout, int pad);
 int conv3d_wgrad_tri_table_size(int B, int D, int H, int W, int pad);
+int conv3d_wgrad_slab_ok(int B, int D, int H, int W, int Cin, int Cout, int pad);
+int conv3d_wgrad_slab_pick(int G, int B, int D, int H, int W, int Cin, int Cout, int pad);
+int conv3d_wgrad_slab_nsplit(int G, int B, int D, int H, int W, int Cin, int Cout, int pad);
+int conv3d_wgrad_slab_table_size(int B, int D, int H, int W, int pad);
+void conv3d_wgrad_slab_table(uintptr_t tab, int B, int D, int H, int W, int pad, uintptr_t stream);
+void conv3d_wgrad_slab(uintptr_t x, uintptr_t dy, uintptr_t part, uintptr_t grad, int64_t ldg, int64_t off, int G,
+                       int B, int D, int H, int W, int Cin, int Cout, int pad, int nsplit, float scale, uintptr_t stab,
+                       uintptr_t stream);
 int conv3d_fwd_tri_ok(int B, int D, int H, int W, int Cin, int Cout, int pad);
 int conv3d_union_umax(int B, int D, int H, int W, int pad, int P);
 int conv3d_fwd_tri_pick(int G, int B, int D, int H, int W, int Cin, int Cout, int pad);
@@ -212,6 +220,12 @@ PYBIND11_MODULE(_nidt_hip, m) {
   DEF(conv3d_wgrad_tri_ok);
   DEF(conv3d_wgrad_tri_pick);
   DEF(conv3d_wgrad_tri);
+  DEF(conv3d_wgrad_slab_ok);
+  DEF(conv3d_wgrad_slab_pick);
+  DEF(conv3d_wgrad_slab_nsplit);
+  DEF(conv3d_wgrad_slab_table_size);
+  DEF(conv3d_wgrad_slab_table);
+  DEF(conv3d_wgrad_slab);
   DEF(conv3d_pos_table);
   DEF(pack_conv_w);
   DEF(bn_relu_apply);

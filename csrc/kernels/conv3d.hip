@@ -2007,6 +2007,145 @@ __global__ __launch_bounds__(192 * NCH, 2) void k_conv_wgrad_tri(ConvWgTriArgs a
   }
 }
 
+// k_conv_wgrad_slab — the weight gradient with one X union per (kd, 64-channel chunk) slab for all nine (kh, kw)
+// taps: per 64-position step the block stages the whole-window union of the step's positions (k_union_table with
+// ext = 2 Wp + 2, <= 152 rows for conv2 vs 3 x <= 80 for the three (kd, kh) triplets of k_conv_wgrad_tri) and the
+// step's dY tile, and 12 waves compute 64 co x 9 taps x 64 ci from them: 288 MFMAs per 27 KB of LDS-DMA instead of
+// 96 per 18 KB (k_conv_wgrad_tri, which the PMC shows waiting on those transfers).  Wave (kh, j) = (wid / 4,
+// wid % 4) owns ci tile j of taps (kh, 0..2) for all four co tiles: X row of tap (kh, kw) = idx(p) + kh Wp + kw.
+// Output: fp32 slabs per split (k_wgrad_reduce finishes), as k_conv_wgrad_tri.
+template <int U, bool PADDED>
+__global__ __launch_bounds__(768, 1) void k_conv_wgrad_slab(ConvWgTriArgs a) {
+  constexpr int NW = 12, XG = U * kWdRow, BUFE = XG + kWdGroup, ST = WtTab<U>::kST;
+  constexpr int XP = U / 8, XPW = (XP + NW - 1) / NW;   // union pieces (8 rows each) per wave
+  __shared__ __attribute__((aligned(16))) uint16_t smem[2 * BUFE];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int kh = wid >> 2, jt = wid & 3;
+  const int id = xcd_remap(blockIdx.x, gridDim.x);
+  const int kt = id % a.nKT, r1 = id / a.nKT;
+  const int ct = r1 % a.nCT, r2 = r1 / a.nCT;
+  const int sp = r2 % a.nsplit, g = r2 / a.nsplit;
+  const int Cin = a.Cin, nck = Cin / 64;
+  const int kd = kt / nck, cc = kt - kd * nck;
+  const int co0 = ct * 64, Wp = a.W + 2 * a.pad;
+  const int p_begin = sp * a.chunk, p_end = min(a.Mg, p_begin + a.chunk);
+  const i32x4_t rx = make_rsrc(a.x + (int64_t)g * a.xclient, (uint32_t)(a.xclient * 2));
+  const i32x4_t rd = make_rsrc(a.dy + (int64_t)g * a.Mg * a.Cout, (uint32_t)((int64_t)a.Mg * a.Cout * 2));
+  const i32x4_t rt = make_rsrc(a.stab, (uint32_t)a.nstab * ST * 4u);
+  const int lr = lane >> 3, ls = lane & 7;
+  const int xadd = kd * a.H * a.W;                          // voxel offset of tap (kd, 0, 0)
+  const int dlo = a.pad - kd;                               // depth code range of sources inside the volume
+  int xcol[XPW];
+#pragma unroll
+  for (int i = 0; i < XPW; ++i) {
+    const int u = 8 * (wid * XPW + i) + lr;
+    xcol[i] = (cc * 64 + ((ls ^ swz_wd(u)) << 3)) * 2;
+  }
+  const bool dload = wid < 8;                               // waves 0-7 stage dY slice wid (8 positions x 64 co)
+  const int dr = 8 * (wid & 7) + lr;
+  const int dcol = (dr * a.Cout + co0 + ((ls ^ swz_wd(dr)) << 3)) * 2;
+  const int gq = lane >> 4, li = lane & 15, qq = li >> 2, pp = li & 3;
+  const int rr0 = 8 * gq + qq, rr1 = rr0 + 4;
+  i32x2_t trow[XPW];
+  int tix[4], tixn[4];
+#define WS_FETCH_ROWS(S)                                                                                      \
+  {                                                                                                           \
+    _Pragma("unroll") for (int i_ = 0; i_ < XPW; ++i_)                                                        \
+      trow[i_] = nidt_raw_buffer_load_v2i32(rt, ((S) * ST + 2 * (8 * (wid * XPW + i_) + lr)) * 4, 0, 0);      \
+  }
+#define WS_FETCH_IDX(S, DST)                                                                                  \
+  {                                                                                                           \
+    _Pragma("unroll") for (int k_ = 0; k_ < 4; ++k_)                                                          \
+      DST[k_] = nidt_raw_buffer_load_i32(rt, ((S) * ST + 2 * U + 32 * (k_ >> 1) + ((k_ & 1) ? rr1 : rr0)) * 4, \
+                                         0, 0);                                                               \
+  }
+#define WS_ISSUE(S, BUFI)                                                                                     \
+  {                                                                                                           \
+    uint16_t* sX_ = smem + (BUFI) * BUFE;                                                                     \
+    _Pragma("unroll") for (int i_ = 0; i_ < XPW; ++i_)                                                        \
+      if (wid * XPW + i_ < XP) {                                                                              \
+        const int c_ = trow[i_].y;                                                                            \
+        const bool ok_ = PADDED ? ((unsigned)((c_ & 1023) - dlo) < (unsigned)a.D &&                            \
+                                   (unsigned)(((c_ >> 10) & 1023) - a.pad) < (unsigned)a.H &&                 \
+                                   (unsigned)((c_ >> 20) - a.pad) < (unsigned)a.W)                            \
+                                : (c_ & 1023) != 1023;                                                        \
+        blds16(rx, ok_ ? (trow[i_].x + xadd) * (2 * Cin) + xcol[i_] : kBufOOB, sX_ + (wid * XPW + i_) * 512);  \
+      }                                                                                                       \
+    if (dload) blds16(rd, (S) * 64 * (2 * a.Cout) + dcol, sX_ + XG + (wid & 7) * 512);                       \
+  }
+
+  f32x4 acc[3][4];
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int s0 = p_begin / 64, nsteps = (p_end - p_begin + 63) / 64;
+  if (nsteps > 0) {
+    WS_FETCH_ROWS(s0)
+    WS_FETCH_IDX(s0, tixn)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    WS_ISSUE(s0, 0)
+    if (nsteps > 1) WS_FETCH_ROWS(s0 + 1)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  const int toff = kh * Wp;
+  for (int st = 0; st < nsteps; ++st) {
+    const int cur = st & 1;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) tix[k] = tixn[k];
+    if (st + 1 < nsteps) {
+      WS_ISSUE(s0 + st + 1, cur ^ 1)
+      if (st + 2 < nsteps) WS_FETCH_ROWS(s0 + st + 2)
+      WS_FETCH_IDX(s0 + st + 1, tixn)
+    }
+    const uint16_t* sX = smem + cur * BUFE;
+    const uint16_t* sD = sX + XG;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int ra = 32 * kk + rr0, rb = 32 * kk + rr1;
+      bf16x8 fa[4], fb[3];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int c = 2 * i + (pp >> 1);
+        fa[i] = tr_pair(sD + ra * kWdRow + ((c ^ swz_wd(ra)) << 3) + (pp & 1) * 4,
+                        sD + rb * kWdRow + ((c ^ swz_wd(rb)) << 3) + (pp & 1) * 4);
+      }
+      const int c = 2 * jt + (pp >> 1);
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) {
+        const int xa = tix[2 * kk] + toff + kw, xb = tix[2 * kk + 1] + toff + kw;
+        fb[kw] = tr_pair(sX + xa * kWdRow + ((c ^ swz_wd(xa)) << 3) + (pp & 1) * 4,
+                         sX + xb * kWdRow + ((c ^ swz_wd(xb)) << 3) + (pp & 1) * 4);
+      }
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[kw][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[kw], acc[kw][i], 0, 0, 0);
+    }
+    // retire the next stage's LDS-DMA; the step-table loads issued after it (rows for st+2, idx for st+1) may stay
+    if (st + 2 < nsteps) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(XPW + 4) : "memory");
+    else if (st + 1 < nsteps) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+#undef WS_ISSUE
+#undef WS_FETCH_IDX
+#undef WS_FETCH_ROWS
+  const int fr = lane & 15, fq = lane >> 4;
+  float* out = a.part + (((int64_t)sp * a.G + g) * a.Cout + co0) * a.K;
+#pragma unroll
+  for (int kw = 0; kw < 3; ++kw) {
+    const int k = ((kd * 9 + kh * 3 + kw) * Cin) + cc * 64 + 16 * jt + fr;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) out[(int64_t)(16 * i + 4 * fq + r) * a.K + k] = acc[kw][i][r];
+  }
+}
+
 static inline int conv_out_n(int n, int pad) { return n + 2 * pad - 2; }
 
 // output channels per k_conv_wgrad_tri block: 64 (3 waves).  NIDT_WG_TRI_NCH=2 gives 128-channel blocks (6 waves)
@@ -2102,6 +2241,80 @@ void conv3d_wgrad_tri(uintptr_t x, uintptr_t dy, uintptr_t part, uintptr_t grad,
     if (U == 80) { NIDT_TRI(1, 80) } else { NIDT_TRI(1, 96) }
   }
 #undef NIDT_TRI
+  NIDT_CHECK(hipGetLastError());
+  hipLaunchKernelGGL(k_wgrad_reduce, dim3(Cout, G), dim3(256), 27 * (Cin + 1) * sizeof(float), s, ptr<const float>(part),
+                     nsplit, G, Cout, Cin, 27, ptr<float>(grad), ldg, off, scale);
+  NIDT_CHECK(hipGetLastError());
+}
+
+// ---- k_conv_wgrad_slab host side: 64-position steps, whole-window unions (ext = 2 Wp + 2) of <= 152 rows ----
+static inline int ws_u(int B, int D, int H, int W, int pad) {
+  return union_umax(B, D, H, W, pad, 64, 2 * (W + 2 * pad) + 2) <= 152 ? 152 : 0;
+}
+
+int conv3d_wgrad_slab_ok(int B, int D, int H, int W, int Cin, int Cout, int pad) {
+  if (pad < 0 || pad > 2 || Cin % 64 != 0 || Cout % 64 != 0) return 0;
+  if (conv_out_n(D, pad) < 1 || conv_out_n(H, pad) < 1 || conv_out_n(W, pad) < 1) return 0;
+  if (D + 2 * pad >= 1024 || H + 2 * pad >= 1024 || W + 2 * pad >= 1024) return 0;
+  return ws_u(B, D, H, W, pad) > 0 ? 1 : 0;
+}
+
+// Off by default (NIDT_WG_SLAB=1 opts in where k_conv_wgrad_tri would run): measured slower at 64 clients, conv2 wgrad
+// 3.83 vs 3.03 ms, conv3-5 0.44-0.63 vs 0.36-0.53 ms (profiles/r3_ab_wgrad_slab.txt) — one 12-wave block per CU
+// (114 VGPRs) re-reads the dY tile from LDS in every wave and waits at each step's barrier with no second block
+// to cover it; the triplet kernel's two 3-wave blocks per CU overlap those waits.
+int conv3d_wgrad_slab_pick(int G, int B, int D, int H, int W, int Cin, int Cout, int pad) {
+  static const int env = [] {
+    const char* e = getenv("NIDT_WG_SLAB");
+    return e ? atoi(e) : 0;
+  }();
+  if (!env || !conv3d_wgrad_slab_ok(B, D, H, W, Cin, Cout, pad)) return 0;
+  return conv3d_wgrad_tri_pick(G, B, D, H, W, Cin, Cout, pad) || env == 2 ? 1 : 0;
+}
+
+int conv3d_wgrad_slab_nsplit(int G, int B, int D, int H, int W, int Cin, int Cout, int pad) {
+  const int Mg = B * conv_out_n(D, pad) * conv_out_n(H, pad) * conv_out_n(W, pad);
+  // one 12-wave block per CU; ~3x the MFMAs of a k_conv_wgrad_tri step
+  return wgrad_nsplit_base(G * (Cout / 64) * 3 * (Cin / 64), G, Mg, 27 * Cin, Cout, 1.5, 0.0, 256.0);
+}
+
+int conv3d_wgrad_slab_table_size(int B, int D, int H, int W, int pad) {
+  const int Mg = B * conv_out_n(D, pad) * conv_out_n(H, pad) * conv_out_n(W, pad);
+  const int U = ws_u(B, D, H, W, pad);
+  NIDT_REQUIRE(U > 0, "conv3d_wgrad_slab_table_size: shape not eligible");
+  return ceil_div(Mg, 64) * (2 * U + 64);
+}
+
+void conv3d_wgrad_slab_table(uintptr_t tab, int B, int D, int H, int W, int pad, uintptr_t stream) {
+  const int Mg = B * conv_out_n(D, pad) * conv_out_n(H, pad) * conv_out_n(W, pad);
+  const int U = ws_u(B, D, H, W, pad);
+  NIDT_REQUIRE(U > 0, "conv3d_wgrad_slab_table: shape not eligible");
+  hipLaunchKernelGGL(k_union_table, dim3(ceil_div(Mg, 64)), dim3(64), 0, as_stream(stream), ptr<int>(tab), U, 64, Mg,
+                     D, H, W, pad, 2 * (W + 2 * pad) + 2);
+  NIDT_CHECK(hipGetLastError());
+}
+
+void conv3d_wgrad_slab(uintptr_t x, uintptr_t dy, uintptr_t part, uintptr_t grad, int64_t ldg, int64_t off, int G,
+                       int B, int D, int H, int W, int Cin, int Cout, int pad, int nsplit, float scale, uintptr_t stab,
+                       uintptr_t stream) {
+  NIDT_REQUIRE(conv3d_wgrad_slab_ok(B, D, H, W, Cin, Cout, pad), "conv3d_wgrad_slab: shape not eligible");
+  NIDT_REQUIRE(stab != 0 && nsplit >= 1, "conv3d_wgrad_slab: needs the step table");
+  ConvWgTriArgs d;
+  d.x = ptr<const uint16_t>(x); d.dy = ptr<const uint16_t>(dy); d.stab = ptr<const int>(stab); d.part = ptr<float>(part);
+  d.D = D; d.H = H; d.W = W; d.Cin = Cin; d.Cout = Cout; d.pad = pad;
+  d.Mg = B * conv_out_n(D, pad) * conv_out_n(H, pad) * conv_out_n(W, pad);
+  d.K = 27 * Cin; d.nsplit = nsplit; d.G = G;
+  d.chunk = ((ceil_div(d.Mg, nsplit) + 63) / 64) * 64;
+  d.nKT = 3 * (Cin / 64); d.nCT = Cout / 64;
+  d.nstab = ceil_div(d.Mg, 64);
+  d.xclient = (int64_t)B * D * H * W * Cin;
+  NIDT_REQUIRE(d.xclient * 2 < (1ll << 31) && (int64_t)d.Mg * Cout * 2 < (1ll << 31),
+               "conv3d_wgrad_slab: per-client tensors must stay below 2 GiB (32-bit buffer offsets)");
+  const int64_t nwg = (int64_t)d.nKT * d.nCT * nsplit * G;
+  NIDT_REQUIRE(nwg < (1ll << 31), "conv3d_wgrad_slab: grid too large");
+  hipStream_t s = as_stream(stream);
+  if (pad) hipLaunchKernelGGL((k_conv_wgrad_slab<152, true>), dim3((unsigned)nwg), dim3(768), 0, s, d);
+  else hipLaunchKernelGGL((k_conv_wgrad_slab<152, false>), dim3((unsigned)nwg), dim3(768), 0, s, d);
   NIDT_CHECK(hipGetLastError());
   hipLaunchKernelGGL(k_wgrad_reduce, dim3(Cout, G), dim3(256), 27 * (Cin + 1) * sizeof(float), s, ptr<const float>(part),
                      nsplit, G, Cout, Cin, 27, ptr<float>(grad), ldg, off, scale);

@@ -113,10 +113,14 @@ class HipAlexNet3D:
             for (ci, bi, cin, cout, pad, sp) in (L2, L3, L4, L5):
                 b["w%dt" % ci] = e(G, cin, 27, cout)
                 b["ns%d" % ci] = self.m.conv3d_wgrad_nsplit(G, B, sp[0], sp[1], sp[2], cin, cout, pad)
-            # wgrad with three-tap union staging (k_conv_wgrad_tri, its own split factor) where the shape allows
+            # wgrad with kd-slab (k_conv_wgrad_slab) or three-tap (k_conv_wgrad_tri) union staging, each with its own
+            # split factor, where the shape allows
             for (ci, bi, cin, cout, pad, sp) in (L2, L3, L4, L5):
-                b["tri%d" % ci] = bool(self.m.conv3d_wgrad_tri_pick(G, B, *sp, cin, cout, pad))
-                if b["tri%d" % ci]:
+                b["wslab%d" % ci] = bool(self.m.conv3d_wgrad_slab_pick(G, B, *sp, cin, cout, pad))
+                b["tri%d" % ci] = not b["wslab%d" % ci] and bool(self.m.conv3d_wgrad_tri_pick(G, B, *sp, cin, cout, pad))
+                if b["wslab%d" % ci]:
+                    b["ns%d" % ci] = self.m.conv3d_wgrad_slab_nsplit(G, B, *sp, cin, cout, pad)
+                elif b["tri%d" % ci]:
                     b["ns%d" % ci] = self.m.conv3d_wgrad_tri_nsplit(G, B, *sp, cin, cout, pad)
             wg_sz = max(b["ns%d" % ci] * G * cout * 27 * cin for (ci, bi, cin, cout, pad, sp) in (L2, L3, L4, L5))
             b.update(
@@ -134,7 +138,10 @@ class HipAlexNet3D:
                 b["pt%d" % ci] = e(mg, 2, dt=torch.int32)
                 self.m.conv3d_pos_table(_p(b["pt%d" % ci]), B, sp[0], sp[1], sp[2], pad, st0)
             for (ci, bi, cin, cout, pad, sp) in (L2, L3, L4, L5):
-                if b["tri%d" % ci]:
+                if b["wslab%d" % ci]:
+                    b["stab%d" % ci] = e(self.m.conv3d_wgrad_slab_table_size(B, *sp, pad), dt=torch.int32)
+                    self.m.conv3d_wgrad_slab_table(_p(b["stab%d" % ci]), B, *sp, pad, st0)
+                elif b["tri%d" % ci]:
                     b["stab%d" % ci] = e(self.m.conv3d_wgrad_tri_table_size(B, *sp, pad), dt=torch.int32)
                     self.m.conv3d_wgrad_tri_table(_p(b["stab%d" % ci]), B, *sp, pad, st0)
             # the weight-gradient branch of this launch shape (one per shape: side lanes run shapes concurrently)
@@ -292,6 +299,10 @@ class HipAlexNet3D:
                 ws.wait_stream(cur)
 
         def wgrad(ci, x, xs, xt, dy, sp, cin, cout, pad):
+            if b.get("wslab%d" % ci) and xs is None:
+                m.conv3d_wgrad_slab(_p(x), _p(dy), _p(b["wgpart"]), _p(grads), P, o["features.%d.weight" % ci], G, B,
+                                    sp[0], sp[1], sp[2], cin, cout, pad, b["ns%d" % ci], 1.0, _p(b["stab%d" % ci]), wst)
+                return
             if b.get("tri%d" % ci) and xs is None:
                 m.conv3d_wgrad_tri(_p(x), _p(dy), _p(b["wgpart"]), _p(grads), P, o["features.%d.weight" % ci], G, B,
                                    sp[0], sp[1], sp[2], cin, cout, pad, b["ns%d" % ci], 1.0, _p(b["stab%d" % ci]), wst)

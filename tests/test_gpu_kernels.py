@@ -282,6 +282,36 @@ def test_conv3d_wgrad_tri_matches_fp32(cin, cout, pad, sp):
         assert _relerr(grad[g, 5:5 + cout * cin * 27].view(cout, cin, 3, 3, 3), wref.grad) < 1e-4
 
 
+@pytest.mark.parametrize("cin,cout,pad,sp", [(64, 128, 0, (19, 23, 19)), (128, 192, 1, (5, 7, 5)),
+                                             (192, 128, 1, (5, 7, 5)), (64, 64, 1, (10, 12, 11))])
+@pytest.mark.parametrize("ns", [1, 3, 0])
+def test_conv3d_wgrad_slab_matches_fp32(cin, cout, pad, sp, ns):
+    """kd-slab union wgrad (k_conv_wgrad_slab: 12 waves, all nine (kh, kw) taps from one union per step) at B = 16
+    (steps crossing rows, depth slices and samples; padded geometries; split factors 1, 3 and the cost model's)
+    against the fp32 autograd weight gradient."""
+    m = _m()
+    G, B = 2, 16
+    assert m.conv3d_wgrad_slab_ok(B, *sp, cin, cout, pad)
+    torch.manual_seed(5)
+    x = torch.randn(G * B, *sp, cin, device=DEV).bfloat16()
+    Do, Ho, Wo = [s + 2 * pad - 2 for s in sp]
+    dy = torch.randn(G * B, Do, Ho, Wo, cout, device=DEV).bfloat16()
+    P = cout * cin * 27 + 5
+    stab = torch.empty(m.conv3d_wgrad_slab_table_size(B, *sp, pad), device=DEV, dtype=torch.int32)
+    m.conv3d_wgrad_slab_table(stab.data_ptr(), B, *sp, pad, _st())
+    ns = ns or m.conv3d_wgrad_slab_nsplit(G, B, *sp, cin, cout, pad)
+    part = torch.empty(ns * G * cout * 27 * cin, device=DEV)
+    grad = torch.zeros(G, P, device=DEV)
+    m.conv3d_wgrad_slab(x.data_ptr(), dy.data_ptr(), part.data_ptr(), grad.data_ptr(), P, 5, G, B, *sp, cin, cout,
+                        pad, ns, 1.0, stab.data_ptr(), _st())
+    torch.cuda.synchronize()
+    for g in range(G):
+        xin = _cf(x[g * B:(g + 1) * B].float())
+        wref = torch.zeros(cout, cin, 3, 3, 3, device=DEV, requires_grad=True)
+        F.conv3d(xin, wref, None, 1, pad).backward(_cf(dy[g * B:(g + 1) * B].float()))
+        assert _relerr(grad[g, 5:5 + cout * cin * 27].view(cout, cin, 3, 3, 3), wref.grad) < 1e-4
+
+
 def _signed_gamma(G, C):
     """gamma in (0.5, 1.5) with ~1/4 negative and a few ~0 entries (training can drive gamma through zero)."""
     g = torch.rand(G, C, device=DEV) + 0.5

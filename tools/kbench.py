@@ -88,6 +88,11 @@ def main():
             cout, pad, st), fl)
         add(name + "_dgrad", lambda ci=ci, sp=sp, cin=cin, cout=cout, pad=pad, Do=Do: net._conv(
             b, "ksd%d" % ci, b[dys[ci]], b["w%dt" % ci], None, b[dxs[ci]], None, G, B, *Do, cout, cin, 2 - pad, st), fl)
+        if b.get("wslab%d" % ci):  # the engine's kd-slab union wgrad
+            add(name + "_wgrad", lambda xin=xin, ci=ci, sp=sp, cin=cin, cout=cout, pad=pad: m.conv3d_wgrad_slab(
+                p(b[xin]), p(b[dys[ci]]), p(b["wgpart"]), p(grads), P, o["features.%d.weight" % ci], G, B, *sp, cin,
+                cout, pad, b["ns%d" % ci], 1.0, p(b["stab%d" % ci]), st), fl)
+            continue
         if b.get("tri%d" % ci):  # the engine's conv2 wgrad (three-tap union staging)
             add(name + "_wgrad", lambda xin=xin, ci=ci, sp=sp, cin=cin, cout=cout, pad=pad: m.conv3d_wgrad_tri(
                 p(b[xin]), p(b[dys[ci]]), p(b["wgpart"]), p(grads), P, o["features.%d.weight" % ci], G, B, *sp, cin,
