@@ -1,0 +1,13 @@
+#!/bin/bash
+# kd-slab union wgrad with 6-wave blocks (NIDT_WG_SLAB_NJ=2, two blocks per CU) vs the triplet wgrad: numerics + kbench
+set -o pipefail
+mkdir -p gpurun_out/r3z
+export PYTHONUNBUFFERED=1 KBENCH_EVAL=0
+timeout -k 10 300 python -u -m pytest tests/test_gpu_kernels.py -x -q --timeout 120 --timeout-method thread \
+  -k "wgrad_slab" > gpurun_out/r3z/pytest.txt 2>&1
+rc=$?; tail -1 gpurun_out/r3z/pytest.txt; if [ $rc -ne 0 ]; then exit $rc; fi
+for arm in 1 0 1 0; do
+  export NIDT_WG_SLAB=$arm
+  timeout -k 10 300 python -u tools/kbench.py 64 10 > gpurun_out/r3z/kbench_$arm.txt 2>&1 || exit 1
+  echo "arm $arm: $(grep -E 'full train step|_wgrad' gpurun_out/r3z/kbench_$arm.txt | tr -s ' ' | tr '\n' '|')"
+done
