@@ -405,7 +405,7 @@ __device__ __forceinline__ f16x8 c1_bfrag(const uint16_t* hb, int s, int ro, con
 
 // PF: B-fragment prefetch distance in k-steps; KS: k-steps per (dd, dh) row (7 or 4); OCC: blocks per CU the
 // register budget is cut for (2: 256 VGPRs; 3: 168, with spills — A/B NIDT_C1_OCC)
-template <int PF, int KS, int OCC = 2>
+template <int PF, int KS, int OCC = 2, int DDU = 1>
 __global__ __launch_bounds__(256, OCC) void k_conv1_fwd_pool_pipe(const uint8_t* __restrict__ x8,
                                                                 const int* __restrict__ idx,
                                                                 const uint16_t* __restrict__ w8,
@@ -521,7 +521,7 @@ __global__ __launch_bounds__(256, OCC) void k_conv1_fwd_pool_pipe(const uint8_t*
       for (int j = 0; j < 2; ++j)
 #pragma unroll
         for (int r = 0; r < 4; ++r) best[i][j][r] = -INFINITY;
-#pragma unroll 1
+#pragma unroll DDU
     for (int dd = 0; dd < 3; ++dd) {
       // 3 KS k-steps (3 dh rows x KS); the B fragments are read PF steps ahead of their MFMAs (a ring of PF + 1
       // register pairs), so an LDS read's latency is covered by PF steps of matrix work, not one
@@ -629,7 +629,18 @@ void conv1_fwd_pool(uintptr_t x8, uintptr_t idx, uintptr_t w8, uintptr_t scale, 
   hipLaunchKernelGGL((k_conv1_fwd_pool_pipe<PF, KSS>), dim3(kPD * NB), dim3(256), 0, as_stream(stream),           \
                      ptr<const uint8_t>(x8), ptr<const int>(idx), ptr<const uint16_t>(w8), ptr<const float>(scale),  \
                      ptr<const float>(shift), B, ptr<uint16_t>(out), ptr<uint8_t>(amax))
-  if (conv1_kslots() == 128) {
+  // the three dd rows of the 3^3 window unrolled: each row's pooling epilogue overlaps the next row's MFMAs and the
+  // body needs 208 instead of 248 VGPRs (4.30 -> 4.17 ms per 64-client step, profiles/r3_ab_conv1_fwd_ddu.txt);
+  // NIDT_C1_DDU=1 keeps the rolled loop (A/B)
+  static const int ddu = [] {
+    const char* e = getenv("NIDT_C1_DDU");
+    return e ? atoi(e) : 3;
+  }();
+  if (conv1_kslots() == 128 && ddu == 3 && pf == 2 && occ != 3) {
+    hipLaunchKernelGGL((k_conv1_fwd_pool_pipe<2, 4, 2, 3>), dim3(kPD * NB), dim3(256), 0, as_stream(stream),
+                       ptr<const uint8_t>(x8), ptr<const int>(idx), ptr<const uint16_t>(w8), ptr<const float>(scale),
+                       ptr<const float>(shift), B, ptr<uint16_t>(out), ptr<uint8_t>(amax));
+  } else if (conv1_kslots() == 128) {
     if (pf == 1) NIDT_C1(1, 4); else if (pf == 3) NIDT_C1(3, 4); else NIDT_C1(2, 4);
   } else {
     if (pf == 1) NIDT_C1(1, 7); else if (pf == 3) NIDT_C1(3, 7); else NIDT_C1(2, 7);
