@@ -2422,10 +2422,25 @@ __global__ __launch_bounds__(256) void k_pack_wp(const float* __restrict__ theta
   const int co = blockIdx.x, g = blockIdx.y;
   const int K = kt * Cin, Ks = kt * cin_src;  // source rows may carry fewer input channels (zero-padded here)
   const float* src = theta + (int64_t)g * ldt + off + (int64_t)co * Ks;
-  for (int e = threadIdx.x; e < K; e += 256) row[e] = e < Ks ? src[e] : 0.f;
+  if (Ks == K && (reinterpret_cast<uintptr_t>(src) & 15) == 0 && K % 4 == 0) {  // 16-B source loads
+    for (int e = 4 * threadIdx.x; e < K; e += 4 * 256)
+      *reinterpret_cast<float4*>(row + e) = *reinterpret_cast<const float4*>(src + e);
+  } else {
+    for (int e = threadIdx.x; e < K; e += 256) row[e] = e < Ks ? src[e] : 0.f;
+  }
   __syncthreads();
-  uint16_t* dst = wp + ((int64_t)g * Cout + co) * K;  // K even: 4-B aligned pairs
-  for (int e = 2 * threadIdx.x; e < K; e += 2 * 256) {  // e, e+1 share the tap (Cin even)
+  uint16_t* dst = wp + ((int64_t)g * Cout + co) * K;
+  if (Cin % 8 == 0) {  // 16-B stores: 8 channels of one tap per lane (K % 8 == 0: aligned)
+    for (int e = 8 * threadIdx.x; e < K; e += 8 * 256) {
+      const int t = e / Cin, ci = e - t * Cin;
+      const float* r = row + ci * kt + t;
+      *reinterpret_cast<uint4*>(dst + e) =
+          make_uint4(pack_bf16x2(r[0] * scale, r[kt] * scale), pack_bf16x2(r[2 * kt] * scale, r[3 * kt] * scale),
+                     pack_bf16x2(r[4 * kt] * scale, r[5 * kt] * scale), pack_bf16x2(r[6 * kt] * scale, r[7 * kt] * scale));
+    }
+    return;
+  }
+  for (int e = 2 * threadIdx.x; e < K; e += 2 * 256) {  // e, e+1 share the tap (Cin even); K even: 4-B aligned pairs
     const int t = e / Cin, ci = e - t * Cin;
     *reinterpret_cast<uint32_t*>(dst + e) = pack_bf16x2(row[ci * kt + t] * scale, row[(ci + 1) * kt + t] * scale);
   }
@@ -2433,18 +2448,29 @@ __global__ __launch_bounds__(256) void k_pack_wp(const float* __restrict__ theta
 
 __global__ __launch_bounds__(256) void k_pack_wt(const uint16_t* __restrict__ wp, int Cout, int Cin, int kt,
                                                  uint16_t* __restrict__ wt) {
-  __shared__ uint16_t tile[64][66];
+  // 16-B global pieces (8 channels per lane), transpose through a padded LDS tile (as pack.hip k_pack_trans)
+  __shared__ uint16_t tile[64][72];  // [co][ci]
   const int ci0 = blockIdx.x * 64, co0 = blockIdx.y * 64;
   const int g = blockIdx.z / kt, t = blockIdx.z - g * kt;
-  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
-  for (int r = ty; r < 64; r += 4) {  // r = co offset, tx = ci offset
-    const int co = co0 + r, ci = ci0 + tx;
-    tile[r][tx] = (co < Cout && ci < Cin) ? wp[(((int64_t)g * Cout + co) * kt + t) * Cin + ci] : 0;
+  const int q = threadIdx.x & 7, r0 = threadIdx.x >> 3;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int r = r0 + 32 * h, co = co0 + r, ci = ci0 + 8 * q;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (co < Cout && ci < Cin) v = *reinterpret_cast<const uint4*>(wp + (((int64_t)g * Cout + co) * kt + t) * Cin + ci);
+    *reinterpret_cast<uint4*>(&tile[r][8 * q]) = v;
   }
   __syncthreads();
-  for (int r = ty; r < 64; r += 4) {  // r = ci offset, tx = co offset
-    const int ci = ci0 + r, co = co0 + tx;
-    if (ci < Cin && co < Cout) wt[(((int64_t)g * Cin + ci) * kt + (kt - 1 - t)) * Cout + co] = tile[tx][r];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int r = r0 + 32 * h, ci = ci0 + r, co = co0 + 8 * q;
+    if (ci >= Cin || co >= Cout) continue;
+    uint32_t w[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      w[k] = (uint32_t)tile[8 * q + 2 * k][r] | ((uint32_t)tile[8 * q + 2 * k + 1][r] << 16);
+    *reinterpret_cast<uint4*>(wt + (((int64_t)g * Cin + ci) * kt + (kt - 1 - t)) * Cout + co) =
+        make_uint4(w[0], w[1], w[2], w[3]);
   }
 }
 
@@ -2455,6 +2481,7 @@ void pack_conv_wk(uintptr_t theta, int64_t ldt, int64_t off, int G, int Cout, in
   NIDT_REQUIRE((int64_t)Cin * kt <= 27 * kMaxCin && Cin % 2 == 0, "pack_conv_w: Cin even, taps x Cin <= 27 x 512");
   NIDT_REQUIRE(kt == 27 || kt == 9 || kt == 1, "pack_conv_w: taps 27, 9 or 1");
   NIDT_REQUIRE(cin_src >= 1 && cin_src <= Cin, "pack_conv_w: 1 <= cin_src <= Cin");
+  NIDT_REQUIRE(!wt || (Cin % 8 == 0 && Cout % 8 == 0), "pack_conv_w: the transposed image needs Cin, Cout % 8 == 0");
   hipStream_t s = as_stream(stream);
   hipLaunchKernelGGL(k_pack_wp, dim3(Cout, G), dim3(256), kt * Cin * sizeof(float), s, ptr<const float>(theta), ldt,
                      off, Cout, Cin, kt, cin_src, scale, ptr<uint16_t>(wp));

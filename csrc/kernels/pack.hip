@@ -38,9 +38,25 @@ __global__ __launch_bounds__(256) void k_pack_plain(const PackDesc* __restrict__
   const int co = blockIdx.x - d.blk_plain, g = blockIdx.y;
   const int Cin = d.cin_p, kt = d.kt, K = kt * Cin, Ks = kt * d.cin_src;
   const float* src = theta + (int64_t)g * ldt + d.src_off + (int64_t)co * Ks;
-  for (int e = threadIdx.x; e < Ks; e += 256) row[e] = src[e];
+  if ((reinterpret_cast<uintptr_t>(src) & 15) == 0 && Ks % 4 == 0) {  // 16-B source loads
+    for (int e = 4 * threadIdx.x; e < Ks; e += 4 * 256)
+      *reinterpret_cast<float4*>(row + e) = *reinterpret_cast<const float4*>(src + e);
+  } else {
+    for (int e = threadIdx.x; e < Ks; e += 256) row[e] = src[e];
+  }
   __syncthreads();
   uint16_t* dst = out + d.wp_off + ((int64_t)g * d.cout + co) * K;
+  if (Cin % 8 == 0 && (d.wp_off & 7) == 0) {  // 16-B stores: 8 channels of one tap per lane
+    for (int e = 8 * threadIdx.x; e < K; e += 8 * 256) {
+      const int t = e / Cin, ci = e - t * Cin;
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = ci + j < d.cin_src ? row[(ci + j) * kt + t] : 0.f;
+      *reinterpret_cast<uint4*>(dst + e) = make_uint4(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]),
+                                                      pack_bf16x2(v[4], v[5]), pack_bf16x2(v[6], v[7]));
+    }
+    return;
+  }
   for (int e = 2 * threadIdx.x; e < K; e += 2 * 256) {  // e, e+1: same tap (Cin even)
     const int t = e / Cin, ci = e - t * Cin;
     const float a = ci < d.cin_src ? row[ci * kt + t] : 0.f;
@@ -49,14 +65,16 @@ __global__ __launch_bounds__(256) void k_pack_plain(const PackDesc* __restrict__
   }
 }
 
-// transposed: block (64 ci x 64 co tile, tap t, client g) reads the plain image written by k_pack_plain
+// transposed: block (64 ci x 64 co tile, tap t, client g) reads the plain image written by k_pack_plain.  Global
+// traffic in 16-B pieces (8 channels per lane: a 64-wide tile row is 8 lanes), the transpose through a padded LDS tile
+// (2-B column reads there, where bandwidth is plentiful); 2-B global accesses ran at ~2 TB/s.
 __global__ __launch_bounds__(256) void k_pack_trans(const PackDesc* __restrict__ desc, int nd, int G,
                                                     uint16_t* __restrict__ out) {
-  __shared__ uint16_t tile[64][66];
+  __shared__ uint16_t tile[64][72];  // [co][ci], rows padded to 144 B (16-B aligned, staggered banks)
   const int li = find_layer(desc, nd, blockIdx.x, false);
   const PackDesc& d = desc[li];
   const int Cin = d.cin_p, Cout = d.cout, kt = d.kt;
-  const int nci = (Cin + 63) / 64, nco = (Cout + 63) / 64;
+  const int nci = (Cin + 63) / 64;
   int b = blockIdx.x - d.blk_t;
   const int t = b % kt;
   b /= kt;
@@ -64,20 +82,27 @@ __global__ __launch_bounds__(256) void k_pack_trans(const PackDesc* __restrict__
   const int g = blockIdx.y;
   const uint16_t* wp = out + d.wp_off + (int64_t)g * Cout * kt * Cin;
   uint16_t* wt = out + d.wt_off + (int64_t)g * Cin * kt * Cout;
-  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
-  for (int r = ty; r < 64; r += 4) {  // r = co offset, tx = ci offset
-    const int co = co0 + r, ci = ci0 + tx;
-    tile[r][tx] = (co < Cout && ci < Cin) ? wp[((int64_t)co * kt + t) * Cin + ci] : 0;
+  const int q = threadIdx.x & 7, r0 = threadIdx.x >> 3;  // 8-channel piece q of tile row r0 (+ 32)
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int r = r0 + 32 * h, co = co0 + r, ci = ci0 + 8 * q;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (co < Cout && ci < Cin) v = *reinterpret_cast<const uint4*>(wp + ((int64_t)co * kt + t) * Cin + ci);
+    *reinterpret_cast<uint4*>(&tile[r][8 * q]) = v;
   }
   __syncthreads();
   const int s = d.slot[t];
-  for (int r = ty; r < 64; r += 4) {  // r = ci offset, tx = co offset
-    const int ci = ci0 + r, co = co0 + tx;
-    if (ci < Cin && co < Cout) wt[((int64_t)ci * kt + s) * Cout + co] = tile[tx][r];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int r = r0 + 32 * h, ci = ci0 + r, co = co0 + 8 * q;  // output row ci, co piece q
+    if (ci >= Cin || co >= Cout) continue;
+    uint32_t w[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      w[k] = (uint32_t)tile[8 * q + 2 * k][r] | ((uint32_t)tile[8 * q + 2 * k + 1][r] << 16);
+    *reinterpret_cast<uint4*>(wt + ((int64_t)ci * kt + s) * Cout + co) = make_uint4(w[0], w[1], w[2], w[3]);
   }
-  (void)nco;
 }
-
 // desc: device table of nd PackDesc; nplain / ntrans: total blocks of the two grids; lds: bytes for the largest
 // plain source row (max kt * cin_src * 4)
 void pack_convs(uintptr_t desc, int nd, int nplain, int ntrans, int lds, uintptr_t theta, int64_t ldt, int G,

@@ -318,6 +318,7 @@ class WeightPacker:
             off += n_img
             vt = None
             if train and c.need_dgrad:
+                assert c.cin_p % 8 == 0 and c.cout % 8 == 0, "pack.hip k_pack_trans: 16-B channel pieces"
                 d["wt_off"] = off
                 vt = (off, (G, c.cin_p, c.kt, c.cout))
                 off += n_img

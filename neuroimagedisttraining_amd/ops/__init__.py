@@ -28,6 +28,9 @@ def _load():
     here = os.path.dirname(os.path.abspath(__file__))
     if here not in sys.path:
         sys.path.insert(0, here)
+    alt = os.environ.get("NIDT_EXT_DIR")  # A/B runs: load another build of _nidt_hip from this directory
+    if alt:
+        sys.path.insert(0, os.path.abspath(alt))
     try:
         _EXT = importlib.import_module("_nidt_hip")
     except Exception as e:  # noqa: BLE001
