@@ -1284,8 +1284,11 @@ void conv3d_fwd_tri(uintptr_t x, uintptr_t w, uintptr_t bias, int64_t bias_ld, u
 // (512-position blocks, one 8-wave block per CU with 704-row unions, measured slower for the conv2 data gradient:
 // 3.79 vs 3.28 ms, profiles/r3_ab_fwd_slab.txt — not kept)
 static inline int slab_ext(int W, int pad) { return 2 * (W + 2 * pad) + 2; }
+// union rows per band: 384, or 416 for 64-channel blocks (48 + 4 KB more LDS still leaves two blocks per CU: the
+// 31x37x31 layer-1 convs of the 3D ResNet need up to 408)
 static inline int slab_u(int B, int D, int H, int W, int pad) {
-  return union_umax(B, D, H, W, pad, 256, slab_ext(W, pad)) <= 384 ? 384 : 0;
+  const int um = union_umax(B, D, H, W, pad, 256, slab_ext(W, pad));
+  return um <= 384 ? 384 : (um <= 416 ? 416 : 0);
 }
 
 // largest kd-slab union (rows) of a 256-position band: exposed for host-side tests of the slab rule
@@ -1296,7 +1299,8 @@ int conv3d_fwd_slab_ok(int B, int D, int H, int W, int Cin, int Cout, int pad) {
   const int Mg = B * (D + 2 * pad - 2) * (H + 2 * pad - 2) * (W + 2 * pad - 2);
   if (D + 2 * pad < 3 || H + 2 * pad < 3 || W + 2 * pad < 3 || Mg <= 0) return 0;
   if (D + 2 * pad >= 1024 || H + 2 * pad >= 1024 || W + 2 * pad >= 1024) return 0;
-  return slab_u(B, D, H, W, pad) > 0 ? 1 : 0;
+  const int U = slab_u(B, D, H, W, pad);
+  return (U == 384 || (U == 416 && fwd_bco(Cout) == 64)) ? 1 : 0;
 }
 
 // Chosen for every eligible shape (measured, profiles/r3_ab_fwd_slab.txt, 64 clients: conv2 dgrad 3.60 -> 3.26 ms
@@ -1354,7 +1358,15 @@ void conv3d_fwd_slab(uintptr_t x, uintptr_t w, uintptr_t bias, int64_t bias_ld, 
   if (st) NIDT_FS(BC, WM, PD, true, true); else if (hb) NIDT_FS(BC, WM, PD, true, false); else NIDT_FS(BC, WM, PD, false, false);
   if (bco == 128) {
     if (pad) { NIDT_FS_B(128, 2, true) } else { NIDT_FS_B(128, 2, false) }
+  } else if (slab_u(B, D, H, W, pad) == 416) {
+#undef NIDT_FS
+#define NIDT_FS(BC, WM, PD, BI, STT) \
+  hipLaunchKernelGGL((k_conv_fwd_slab<BC, WM, 4, 416, PD, BI, STT>), grid, dim3(256 * WM), 0, s, a, nCO, tab)
+    if (pad) { NIDT_FS_B(64, 1, true) } else { NIDT_FS_B(64, 1, false) }
   } else {
+#undef NIDT_FS
+#define NIDT_FS(BC, WM, PD, BI, STT) \
+  hipLaunchKernelGGL((k_conv_fwd_slab<BC, WM, 4, 384, PD, BI, STT>), grid, dim3(256 * WM), 0, s, a, nCO, tab)
     if (pad) { NIDT_FS_B(64, 1, true) } else { NIDT_FS_B(64, 1, false) }
   }
 #undef NIDT_FS_B

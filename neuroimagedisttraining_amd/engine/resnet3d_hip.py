@@ -52,6 +52,26 @@ def conv_fwd(x_ptr, w_ptr, y_ptr, G, B, D, H, W, Cin, Cout, kt, st, pad, padd, d
     m.conv_fwd_gk(x_ptr, w_ptr, y_ptr, part.data_ptr(), ks, G, B, D, H, W, Cin, Cout, kt, st, pad, padd, _stream())
 
 
+_SLAB_TABS = {}
+
+
+def slab_conv(x_ptr, w_ptr, y_ptr, G, B, D, H, W, Cin, Cout, pad, device):
+    """3x3x3 stride-1 conv through the kd-slab union kernel (``k_conv_fwd_slab``) when the shape is eligible (its
+    band unions fit the kernel's LDS); returns False otherwise.  The union table is a function of the shape only and
+    is built once per (B, D, H, W, pad)."""
+    m = ops.ext()
+    if not m.conv3d_fwd_slab_pick(G, B, D, H, W, Cin, Cout, pad):
+        return False
+    key = (str(device), B, D, H, W, pad)
+    tab = _SLAB_TABS.get(key)
+    if tab is None:
+        tab = torch.empty(m.conv3d_fwd_slab_table_size(B, D, H, W, pad), device=device, dtype=torch.int32)
+        m.conv3d_fwd_slab_table(tab.data_ptr(), B, D, H, W, pad, _stream())
+        _SLAB_TABS[key] = tab
+    m.conv3d_fwd_slab(x_ptr, w_ptr, 0, 0, y_ptr, 0, G, B, D, H, W, Cin, Cout, pad, tab.data_ptr(), _stream())
+    return True
+
+
 class GConv3:
     """Client-grouped Conv3d (k = 1 or 3, stride 1/2, no bias) on channels-last ``[N, D, H, W, C]`` bf16.  Weight
     images come from the network's :class:`~.resnet2d_hip.WeightPacker` (two launches per step for all layers;
@@ -102,6 +122,9 @@ class GConv3:
             self.wt = (wt, G, theta.data_ptr()) if wt is not None else None
         wp = self.wp[0]
         y = torch.empty(N, Do, Ho, Wo, self.cout, device=x.device, dtype=torch.bfloat16)
+        if self.kt == 27 and self.stride == 1 and slab_conv(x.data_ptr(), wp.data_ptr(), y.data_ptr(), G, N // G, D,
+                                                            H, W, self.cin, self.cout, self.pad, x.device):
+            return y
         conv_fwd(x.data_ptr(), wp.data_ptr(), y.data_ptr(), G, N // G, D, H, W, self.cin, self.cout,
                  self.kt, self.stride, self.pad, self.pad if self.kt == 27 else 0, x.device)
         return y
@@ -152,6 +175,9 @@ class GConv3:
         if self.stride == 1:
             dx = torch.empty(N, D, H, W, self.cin, device=x.device, dtype=torch.bfloat16)
             p2 = self.k - 1 - self.pad
+            if self.kt == 27 and slab_conv(dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), G, B, Do, Ho, Wo, self.cout,
+                                           self.cin, p2, x.device):
+                return dx
             conv_fwd(dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), G, B, Do, Ho, Wo, self.cout, self.cin, self.kt,
                          1, p2, p2 if self.kt == 27 else 0, x.device)
             return dx

@@ -67,7 +67,7 @@ def test_union_kernel_choices():
 
 
 @pytest.mark.parametrize("shape", [(16, 19, 23, 19, 0), (16, 17, 21, 17, 2), (5, 10, 12, 11, 1), (16, 8, 14, 20, 1),
-                                   (3, 19, 23, 19, 0), (16, 5, 7, 5, 1)])
+                                   (3, 19, 23, 19, 0), (16, 5, 7, 5, 1), (4, 31, 37, 31, 1), (4, 16, 19, 16, 1)])
 def test_slab_union_matches_python_model(shape):
     """kd-slab unions: size vs the Python model, and the addressing invariant the kernel relies on — every tap
     (kh, kw) of a position reads union row idx(p) + kh Wp + kw (whole windows make the union contiguous there)."""
@@ -75,7 +75,8 @@ def test_slab_union_matches_python_model(shape):
     B, D, H, W, pad = shape
     um = _union_rows(*shape, 256, slab=True)
     assert m.conv3d_slab_umax(*shape) == um
-    assert m.conv3d_fwd_slab_ok(B, D, H, W, 64, 64, pad) == (1 if um <= 384 else 0)
+    assert m.conv3d_fwd_slab_ok(B, D, H, W, 64, 64, pad) == (1 if um <= 416 else 0)      # 64-channel blocks
+    assert m.conv3d_fwd_slab_ok(B, D, H, W, 64, 128, pad) == (1 if um <= 384 else 0)     # 128-channel blocks
     Dp, Hp, Wp = D + 2 * pad, H + 2 * pad, W + 2 * pad
     Do, Ho, Wo = Dp - 2, Hp - 2, Wp - 2
     S, vol = Do * Ho * Wo, Dp * Hp * Wp

@@ -121,7 +121,8 @@ def test_conv3d_fwd_stats(cin, cout, pad, sp, xf, G, B):
 
 
 @pytest.mark.parametrize("cin,cout,pad,sp", [(64, 128, 0, (19, 23, 19)), (128, 64, 2, (17, 21, 17)),
-                                             (64, 64, 1, (10, 12, 11)), (128, 128, 1, (8, 14, 20))])
+                                             (64, 64, 1, (10, 12, 11)), (128, 128, 1, (8, 14, 20)),
+                                             (64, 64, 1, (31, 37, 31))])
 @pytest.mark.parametrize("G,B", [(2, 16), (3, 5)])
 def test_conv3d_fwd_slab_matches_fp32(cin, cout, pad, sp, G, B):
     """kd-slab union forward / data gradient (k_conv_fwd_slab): bands crossing output rows, depth planes and
