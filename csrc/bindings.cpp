@@ -48,6 +48,10 @@ int conv3d_union_umax(int B, int D, int H, int W, int pad, int P);
 int conv3d_fwd_tri_pick(int G, int B, int D, int H, int W, int Cin, int Cout, int pad);
 int conv3d_fwd_tri_table_size(int B, int D, int H, int W, int pad);
 int conv3d_fwd_slab_ok(int B, int D, int H, int W, int Cin, int Cout, int pad);
+int conv2d_fwd_slab_ok(int B, int H, int W, int Cin, int Cout);
+int conv2d_fwd_slab_pick(int G, int B, int H, int W, int Cin, int Cout);
+void conv2d_fwd_slab(uintptr_t x, uintptr_t w, uintptr_t y, int G, int B, int H, int W, int Cin, int Cout,
+                     uintptr_t utab, uintptr_t stream);
 int conv3d_slab_umax(int B, int D, int H, int W, int pad);
 int conv3d_fwd_slab_pick(int G, int B, int D, int H, int W, int Cin, int Cout, int pad);
 int conv3d_fwd_slab_table_size(int B, int D, int H, int W, int pad);
@@ -215,6 +219,9 @@ PYBIND11_MODULE(_nidt_hip, m) {
   DEF(conv3d_fwd_slab_table_size);
   DEF(conv3d_fwd_slab_table);
   DEF(conv3d_fwd_slab);
+  DEF(conv2d_fwd_slab_ok);
+  DEF(conv2d_fwd_slab_pick);
+  DEF(conv2d_fwd_slab);
   DEF(conv3d_wgrad_tri_nsplit);
   DEF(conv3d_wgrad_tri_table);
   DEF(conv3d_wgrad_tri_ok);

@@ -713,15 +713,18 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void k_conv_fwd_slab(ConvFwdArgs a
 #pragma unroll
   for (int i = 0; i < A_INSTR; ++i) {
     const int row = 8 * (wid * A_INSTR + i) + lrow;
-    aoff[i] = ((co0 + row) * 27 * Cin + ((slot ^ swz_dma(row)) << 3)) * 2;
+    aoff[i] = ((co0 + row) * a.kt * Cin + ((slot ^ swz_dma(row)) << 3)) * 2;
   }
+  // a.kt = 27 (3-D) or 9: a 2-D 3x3 conv as a D = 1, pad 1 volume whose blocks all lie inside one sample, so the
+  // depth-tap skip above leaves kd = 1 only and that slab's weights are the 9-tap image itself
+  const int kdw = a.kt == 27 ? 9 : 0;
   const int64_t xcl = (int64_t)a.B * a.D * a.H * a.W * Cin;
   const i32x4_t rxs = make_rsrc(a.x + (int64_t)g * xcl, (uint32_t)(xcl * 2));
-  const i32x4_t rws = make_rsrc(a.w + (int64_t)g * a.Cout * 27 * Cin, (uint32_t)(a.Cout * 27 * Cin * 2));
+  const i32x4_t rws = make_rsrc(a.w + (int64_t)g * a.Cout * a.kt * Cin, (uint32_t)(a.Cout * a.kt * Cin * 2));
 
   auto issue_a = [&](int ks, int buf) {  // weight tile of tap (kd, t = kh * 3 + kw) of slab q0 + ks / 9
     const int q = q0 + ks / 9, t = ks % 9, kd = q / nck, cc = q - kd * nck;
-    const int woff = ((kd * 9 + t) * Cin + cc * BK) * 2;
+    const int woff = ((kd * kdw + t) * Cin + cc * BK) * 2;
     uint16_t* sA = sAb + buf * A_ELEMS;
 #pragma unroll
     for (int i = 0; i < A_INSTR; ++i) blds16(rws, aoff[i] + woff, sA + (wid * A_INSTR + i) * 512);
@@ -1333,8 +1336,9 @@ void conv3d_fwd_slab_table(uintptr_t tab, int B, int D, int H, int W, int pad, u
   NIDT_CHECK(hipGetLastError());
 }
 
-void conv3d_fwd_slab(uintptr_t x, uintptr_t w, uintptr_t bias, int64_t bias_ld, uintptr_t y, uintptr_t stats, int G,
-                     int B, int D, int H, int W, int Cin, int Cout, int pad, uintptr_t utab, uintptr_t stream) {
+static void fwd_slab_impl(uintptr_t x, uintptr_t w, uintptr_t bias, int64_t bias_ld, uintptr_t y, uintptr_t stats,
+                          int G, int B, int D, int H, int W, int Cin, int Cout, int pad, int kt, uintptr_t utab,
+                          uintptr_t stream) {
   NIDT_REQUIRE(conv3d_fwd_slab_ok(B, D, H, W, Cin, Cout, pad) && utab != 0, "conv3d_fwd_slab: shape not supported");
   NIDT_REQUIRE((int64_t)B * D * H * W * Cin * 2 < (1ll << 31), "conv3d_fwd_slab: per-client input below 2 GiB");
   const bool hb = bias != 0, st = stats != 0;
@@ -1342,7 +1346,7 @@ void conv3d_fwd_slab(uintptr_t x, uintptr_t w, uintptr_t bias, int64_t bias_ld, 
   ConvFwdArgs a;
   a.x = ptr<const uint16_t>(x); a.w = ptr<const uint16_t>(w); a.bias = ptr<const float>(bias);
   a.xs = nullptr; a.xt = nullptr; a.y = ptr<uint16_t>(y); a.stats = ptr<float>(stats);
-  a.B = B; a.D = D; a.H = H; a.W = W; a.Cin = Cin; a.Cout = Cout; a.pad = pad; a.padd = pad; a.kt = 27; a.st = 1;
+  a.B = B; a.D = D; a.H = H; a.W = W; a.Cin = Cin; a.Cout = Cout; a.pad = pad; a.padd = pad; a.kt = kt; a.st = 1;
   a.Do = D + 2 * pad - 2; a.Ho = H + 2 * pad - 2; a.Wo = W + 2 * pad - 2;
   a.Mg = B * a.Do * a.Ho * a.Wo;
   a.nPB = ceil_div(a.Mg, 256);
@@ -1372,6 +1376,40 @@ void conv3d_fwd_slab(uintptr_t x, uintptr_t w, uintptr_t bias, int64_t bias_ld, 
 #undef NIDT_FS_B
 #undef NIDT_FS
   NIDT_CHECK(hipGetLastError());
+}
+
+void conv3d_fwd_slab(uintptr_t x, uintptr_t w, uintptr_t bias, int64_t bias_ld, uintptr_t y, uintptr_t stats, int G,
+                     int B, int D, int H, int W, int Cin, int Cout, int pad, uintptr_t utab, uintptr_t stream) {
+  fwd_slab_impl(x, w, bias, bias_ld, y, stats, G, B, D, H, W, Cin, Cout, pad, 27, utab, stream);
+}
+
+// 2-D 3x3 stride-1 pad-1 convs (the CIFAR / Tiny ResNet-18 layers 1-2 and their data gradients) on the slab kernel:
+// one union per 64-channel chunk serves all nine taps.  Weights [G][Cout][9][Cin]; the union table is
+// conv3d_fwd_slab_table(B, 1, H, W, 1).  Eligible when every 256-position block lies inside one sample (H W % 256
+// == 0, so the depth-tap skip keeps kd = 1 only) and the band unions fit.
+int conv2d_fwd_slab_ok(int B, int H, int W, int Cin, int Cout) {
+  return (H * W) % 256 == 0 && conv3d_fwd_slab_ok(B, 1, H, W, Cin, Cout, 1) ? 1 : 0;
+}
+
+// Chosen (measured per layer, profiles/r3_ab_conv2d_slab.txt, B = 16): 64-channel blocks always (0.77-1.01 of the
+// per-tap kernel's time), 128-channel blocks once the grid has >= 160 of them (0.64-0.96; with 16-128 blocks the
+// slab's one-block-per-CU grid loses to the per-tap kernel's 64-position / split-K blocks: 1.09-1.56).
+// NIDT_2D_SLAB=0 turns it off, =2 forces it for every eligible shape (A/B).
+int conv2d_fwd_slab_pick(int G, int B, int H, int W, int Cin, int Cout) {
+  static const int env = [] {
+    const char* e = getenv("NIDT_2D_SLAB");
+    return e ? atoi(e) : 1;
+  }();
+  if (!env || !conv2d_fwd_slab_ok(B, H, W, Cin, Cout)) return 0;
+  const int bco = fwd_bco(Cout);
+  const int64_t blocks = (int64_t)ceil_div(B * H * W, 256) * (Cout / bco) * G;
+  return (env == 2 || bco == 64 || blocks >= 160) ? 1 : 0;
+}
+
+void conv2d_fwd_slab(uintptr_t x, uintptr_t w, uintptr_t y, int G, int B, int H, int W, int Cin, int Cout,
+                     uintptr_t utab, uintptr_t stream) {
+  NIDT_REQUIRE(conv2d_fwd_slab_ok(B, H, W, Cin, Cout), "conv2d_fwd_slab: shape not supported");
+  fwd_slab_impl(x, w, 0, 0, y, 0, G, B, 1, H, W, Cin, Cout, 1, 9, utab, stream);
 }
 
 int conv3d_fwd_nblocks(int B, int D, int H, int W, int pad, int bp) {

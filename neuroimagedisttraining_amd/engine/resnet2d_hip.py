@@ -109,6 +109,28 @@ def conv_fwd(x_ptr, w_ptr, y_ptr, G, B, D, H, W, Cin, Cout, kt, st, pad, padd, d
     m.conv_fwd_gk(x_ptr, w_ptr, y_ptr, part.data_ptr(), ks, G, B, D, H, W, Cin, Cout, kt, st, pad, padd, _stream())
 
 
+_SLAB_TABS = {}
+
+
+def slab_conv2d(x_ptr, w_ptr, y_ptr, G, B, H, W, Cin, Cout, device):
+    """3x3 stride-1 pad-1 conv through the kd-slab union kernel (``conv2d_fwd_slab``: one input union per 64-channel
+    chunk serves all nine taps) when the shape and grid qualify (``conv2d_fwd_slab_pick``; ``NIDT_2D_SLAB=0`` keeps
+    the per-tap kernels); returns False otherwise.  The union table depends on the shape only and is built once per
+    (B, H, W)."""
+    m = ops.ext()
+    if not m.conv2d_fwd_slab_pick(G, B, H, W, Cin, Cout):
+        return False
+    key = (str(device), B, H, W)
+    tab = _SLAB_TABS.get(key)
+    if tab is None:
+        tab = torch.empty(m.conv3d_fwd_slab_table_size(B, 1, H, W, 1), device=device, dtype=torch.int32)
+        m.conv3d_fwd_slab_table(tab.data_ptr(), B, 1, H, W, 1, _stream())
+        if not torch.cuda.is_current_stream_capturing():  # built inside a capture: that graph's memory, not cached
+            _SLAB_TABS[key] = tab
+    m.conv2d_fwd_slab(x_ptr, w_ptr, y_ptr, G, B, H, W, Cin, Cout, tab.data_ptr(), _stream())
+    return True
+
+
 def tap_slots(kt, stride):
     """Tap order of a layer's data-gradient weight image (``conv_tap_slots`` in conv3d.hip): stride 1 -> flipped,
     stride 2 (3x3) -> sub-pixel phase order, 1x1 -> identity."""
@@ -179,6 +201,9 @@ class GroupedConv:
             self.wt = (wt, G, theta.data_ptr()) if wt is not None else None
         wp = self.wp[0]
         y = torch.empty(N, Ho, Wo, self.cout, device=x.device, dtype=torch.bfloat16)
+        if self.kt == 9 and self.stride == 1 and self.pad == 1 and slab_conv2d(
+                x.data_ptr(), wp.data_ptr(), y.data_ptr(), G, N // G, H, W, self.cin_p, self.cout, x.device):
+            return y
         conv_fwd(x.data_ptr(), wp.data_ptr(), y.data_ptr(), G, N // G, 1, H, W, self.cin_p, self.cout,
                  self.kt, self.stride, self.pad, 0, x.device)
         return y
@@ -236,6 +261,9 @@ class GroupedConv:
         self.wt = None
         if self.stride == 1:
             dx = torch.empty(N, H, W, self.cin_p, device=x.device, dtype=torch.bfloat16)
+            if self.kt == 9 and self.pad == 1 and slab_conv2d(dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), G, B, Ho,
+                                                              Wo, self.cout, self.cin_p, x.device):
+                return dx
             conv_fwd(dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), G, B, 1, Ho, Wo, self.cout, self.cin_p, self.kt,
                      1, self.k - 1 - self.pad, 0, x.device)
             return dx

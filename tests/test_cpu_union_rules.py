@@ -105,3 +105,23 @@ def test_slab_kernel_choice():
     assert m.conv3d_fwd_slab_ok(16, 5, 7, 5, 192, 192, 1) == 0   # 5x7x5 bands: unions of ~470 rows
     n_bands = -(-16 * 19 * 23 * 19 // 256)
     assert m.conv3d_fwd_slab_table_size(16, 17, 21, 17, 2) == n_bands * (2 * 384 + 256)
+
+
+def test_conv2d_slab_choice():
+    """2-D 3x3 convs on the slab kernel (D = 1 volumes, pad 1): eligible when every 256-position block lies in one
+    sample and the band union fits; picked for 64-channel blocks always and 128-channel blocks from 160 blocks up."""
+    m = _ext()
+    assert m.conv3d_slab_umax(16, 1, 32, 32, 1) == _union_rows(16, 1, 32, 32, 1, 256, slab=True) == 340
+    assert m.conv3d_slab_umax(16, 1, 64, 64, 1) == 396                      # Tiny layer 1: the 416-row variant
+    assert m.conv2d_fwd_slab_ok(16, 32, 32, 64, 64) == 1
+    assert m.conv2d_fwd_slab_ok(16, 64, 64, 64, 64) == 1
+    assert m.conv2d_fwd_slab_ok(16, 64, 64, 128, 128) == 0                  # 416-row unions only for 64-ch blocks
+    assert m.conv2d_fwd_slab_ok(16, 8, 8, 256, 256) == 0                    # 64-position samples: blocks straddle
+    assert m.conv2d_fwd_slab_ok(16, 16, 16, 256, 256) == 1
+    assert m.conv2d_fwd_slab_pick(1, 16, 32, 32, 64, 64) == 1              # 64-channel blocks: any grid
+    assert m.conv2d_fwd_slab_pick(4, 16, 16, 16, 128, 128) == 0            # 64 blocks of 128 channels
+    assert m.conv2d_fwd_slab_pick(10, 16, 16, 16, 128, 128) == 1           # 160 blocks
+    assert m.conv2d_fwd_slab_pick(2, 16, 16, 16, 256, 256) == 0            # 64 blocks
+    assert m.conv2d_fwd_slab_pick(10, 16, 16, 16, 256, 256) == 1
+    n_bands = 16 * 32 * 32 // 256
+    assert m.conv3d_fwd_slab_table_size(16, 1, 32, 32, 1) == n_bands * (2 * 384 + 256)

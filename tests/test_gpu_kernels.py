@@ -152,6 +152,32 @@ def test_conv3d_fwd_slab_matches_fp32(cin, cout, pad, sp, G, B):
     assert _relerr(y.float(), (yr.view(G, -1, cout) + bias.view(G, 1, cout)).view_as(yr)) < 1e-2
 
 
+@pytest.mark.parametrize("cin,cout,hw", [(64, 64, (32, 32)), (128, 128, (16, 16)), (64, 128, (16, 32)),
+                                         (256, 256, (16, 16)), (64, 64, (64, 64)), (128, 64, (32, 32))])
+@pytest.mark.parametrize("G,B", [(1, 3), (3, 2)])
+def test_conv2d_fwd_slab_matches_fp32(cin, cout, hw, G, B):
+    """2-D 3x3 stride-1 pad-1 conv on the kd-slab kernel (conv2d_fwd_slab: 9-tap weights, one union per channel
+    chunk; the 64x64 shape takes the 416-row unions) against fp32 conv2d, per client."""
+    m = _m()
+    H, W = hw
+    assert m.conv2d_fwd_slab_ok(B, H, W, cin, cout)
+    torch.manual_seed(5)
+    x = torch.randn(G * B, H, W, cin, device=DEV).bfloat16()
+    w = (torch.randn(G, cout, 9, cin, device=DEV) * 0.05).bfloat16()
+    tab = torch.empty(m.conv3d_fwd_slab_table_size(B, 1, H, W, 1), device=DEV, dtype=torch.int32)
+    m.conv3d_fwd_slab_table(tab.data_ptr(), B, 1, H, W, 1, _st())
+    y = torch.full((G * B, H, W, cout), float("nan"), device=DEV, dtype=torch.bfloat16)
+    m.conv2d_fwd_slab(x.data_ptr(), w.data_ptr(), y.data_ptr(), G, B, H, W, cin, cout, tab.data_ptr(), _st())
+    torch.cuda.synchronize()
+    ys = []
+    for g in range(G):
+        wg = w[g].float().view(cout, 3, 3, cin).permute(0, 3, 1, 2)
+        ys.append(F.conv2d(x[g * B:(g + 1) * B].float().permute(0, 3, 1, 2), wg, None, 1, 1).permute(0, 2, 3, 1))
+    yr = torch.cat(ys, 0)
+    assert torch.isfinite(y.float()).all()
+    assert _relerr(y.float(), yr) < 1e-2
+
+
 @pytest.mark.parametrize("cin,cout,G", [(128, 192, 16), (192, 192, 16), (192, 128, 24), (128, 192, 1), (192, 128, 2)])
 @pytest.mark.parametrize("ksplit,stats_on", [(2, True), (3, True), (2, False), (4, True)])
 def test_conv3d_fwd_splitk(cin, cout, G, ksplit, stats_on):
