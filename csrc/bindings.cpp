@@ -153,6 +153,9 @@ void conv1_wgrad(uintptr_t x8, uintptr_t idx, uintptr_t dp, uintptr_t pout, uint
                  int64_t ldt, int64_t off_g, uintptr_t grad, int64_t ldg, int64_t goff_w, int64_t goff_bias,
                  int64_t goff_g, int64_t goff_b, float wscale, uintptr_t emean, uintptr_t stream);
 // head.hip
+void cls_head_train(uintptr_t a, uintptr_t theta, int64_t ldt, int64_t off_w, int64_t off_b, uintptr_t y, int G, int B,
+                    int HW, int C, int K, uintptr_t pooled, uintptr_t dlog, uintptr_t lossn, uintptr_t losses,
+                    uintptr_t grad, int64_t ldg, uintptr_t da, uintptr_t stream);
 void head(uintptr_t p5, uintptr_t theta, int64_t ldt, int64_t off_w1, int64_t off_b1, int64_t off_w2, int64_t off_b2,
           uintptr_t y, uintptr_t logits, uintptr_t loss, uintptr_t grad, int64_t ldg, uintptr_t dp5, int G, int B,
           int train, float keep, uint64_t seed, uintptr_t cids, uintptr_t seed_dev, uintptr_t stream);
@@ -272,6 +275,7 @@ PYBIND11_MODULE(_nidt_hip, m) {
   DEF(conv1_wgrad_nq);
   DEF(conv1_kslots);
   DEF(head);
+  DEF(cls_head_train);
   DEF(saliency_acc);
   DEF(radix_select_kth);
   DEF(threshold_mask);

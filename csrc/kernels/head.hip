@@ -155,4 +155,139 @@ void head(uintptr_t p5, uintptr_t theta, int64_t ldt, int64_t off_w1, int64_t of
   NIDT_CHECK(hipGetLastError());
 }
 
+// ------------------------------------------------------------------------------------------------
+// ResNet-18 classifier head + CrossEntropy, forward and backward (train step of the client-batched ResNet engine):
+// pooled = mean over the final H x W map, logits = pooled W^T + b, loss = -log softmax(logits)[y] (mean over the
+// client's batch), dlogits = (softmax - onehot) / B, dW / db rows, and the broadcast input gradient
+// da[n, hw, c] = (dlogits W)[c] / (H W) in bf16.  Reference: resnet.py ResNet.forward (avg_pool2d(4) / adaptive
+// pool, linear) with nn.CrossEntropyLoss in the trainers.  Two launches replace ~20 framework kernels per step.
+//
+// k_cls_head_fwd: one block per sample.  a: [N, HW, C] bf16; writes pooled [N, C], dlog [N, K] (already / B),
+// lossn [N] (per-sample CE) and da.
+constexpr int kCHT = 256;
+constexpr int kCHMaxC = 512, kCHMaxK = 256;
+__global__ __launch_bounds__(kCHT) void k_cls_head_fwd(const uint16_t* __restrict__ a, const float* __restrict__ theta,
+                                                       int64_t ldt, int64_t off_w, int64_t off_b,
+                                                       const int64_t* __restrict__ y, int B, int HW, int C, int K,
+                                                       float* __restrict__ pooled, float* __restrict__ dlog,
+                                                       float* __restrict__ lossn, uint16_t* __restrict__ da) {
+  __shared__ float sP[kCHMaxC];
+  __shared__ float sZ[kCHMaxK];
+  __shared__ float red[kCHT / 64];
+  const int n = blockIdx.x, g = n / B, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const float* W = theta + (int64_t)g * ldt + off_w;  // [K, C]
+  const float* bias = theta + (int64_t)g * ldt + off_b;
+  const uint16_t* an = a + (int64_t)n * HW * C;
+  const float inv_hw = 1.f / (float)HW;
+  for (int c = 2 * tid; c < C; c += 2 * kCHT) {  // pooled: channel pairs, one 4-B load per (hw, pair)
+    float s0 = 0.f, s1 = 0.f;
+    for (int hw = 0; hw < HW; ++hw) {
+      const uint32_t v = *reinterpret_cast<const uint32_t*>(an + (int64_t)hw * C + c);
+      s0 += bf16_to_f32((uint16_t)(v & 0xffffu));
+      s1 += bf16_to_f32((uint16_t)(v >> 16));
+    }
+    s0 *= inv_hw;
+    s1 *= inv_hw;
+    sP[c] = s0;
+    sP[c + 1] = s1;
+    pooled[(int64_t)n * C + c] = s0;
+    pooled[(int64_t)n * C + c + 1] = s1;
+  }
+  __syncthreads();
+  for (int k = wid; k < K; k += kCHT / 64) {  // logits: one wave per class row
+    float z = 0.f;
+    for (int c = lane; c < C; c += 64) z = fmaf(W[(int64_t)k * C + c], sP[c], z);
+    z = wave_sum(z);
+    if (lane == 0) sZ[k] = z + bias[k];
+  }
+  __syncthreads();
+  // softmax statistics (one wave; K <= 256)
+  if (wid == 0) {
+    float m = -INFINITY;
+    for (int k = lane; k < K; k += 64) m = fmaxf(m, sZ[k]);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+    float se = 0.f;
+    for (int k = lane; k < K; k += 64) se += expf(sZ[k] - m);
+    se = wave_sum(se);
+    if (lane == 0) {
+      red[0] = m;
+      red[1] = se;
+    }
+  }
+  __syncthreads();
+  const float m = red[0], se = red[1], lse = m + logf(se);
+  const int yy = (int)y[n];
+  if (tid == 0) lossn[n] = lse - sZ[yy];
+  __syncthreads();  // every thread has read sZ[yy] before it is overwritten below
+  const float invB = 1.f / (float)B;
+  for (int k = tid; k < K; k += kCHT) {
+    const float d = (expf(sZ[k] - m) / se - (k == yy ? 1.f : 0.f)) * invB;
+    sZ[k] = d;
+    dlog[(int64_t)n * K + k] = d;
+  }
+  __syncthreads();
+  for (int c = 2 * tid; c < C; c += 2 * kCHT) {  // dpool = dlog W, broadcast / HW over the map
+    float d0 = 0.f, d1 = 0.f;
+    for (int k = 0; k < K; ++k) {
+      const float2 w = *reinterpret_cast<const float2*>(W + (int64_t)k * C + c);
+      d0 = fmaf(sZ[k], w.x, d0);
+      d1 = fmaf(sZ[k], w.y, d1);
+    }
+    const uint32_t pk = pack_bf16x2(d0 * inv_hw, d1 * inv_hw);
+    for (int hw = 0; hw < HW; ++hw) *reinterpret_cast<uint32_t*>(da + ((int64_t)n * HW + hw) * C + c) = pk;
+  }
+}
+
+// k_cls_head_grad: dW[g][k][c] = sum_b dlog[g B + b][k] pooled[g B + b][c] into the grads rows (one thread per
+// (k, c), fixed order over b: deterministic); the extra block column (blockIdx.y == ncol) writes db and the client's
+// mean loss.
+__global__ __launch_bounds__(kCHT) void k_cls_head_grad(const float* __restrict__ pooled, const float* __restrict__ dlog,
+                                                        const float* __restrict__ lossn, int B, int C, int K,
+                                                        float* __restrict__ grad, int64_t ldg, int64_t off_w,
+                                                        int64_t off_b, float* __restrict__ losses) {
+  const int g = blockIdx.x, col = blockIdx.y, tid = threadIdx.x;
+  const int ncol = (K * C + kCHT - 1) / kCHT;
+  float* gr = grad + (int64_t)g * ldg;
+  const float* P = pooled + (int64_t)g * B * C;
+  const float* D = dlog + (int64_t)g * B * K;
+  if (col < ncol) {
+    const int e = col * kCHT + tid;
+    if (e >= K * C) return;
+    const int k = e / C, c = e - k * C;
+    float s = 0.f;
+    for (int b = 0; b < B; ++b) s = fmaf(D[(int64_t)b * K + k], P[(int64_t)b * C + c], s);
+    gr[off_w + e] = s;
+    return;
+  }
+  for (int k = tid; k < K; k += kCHT) {
+    float s = 0.f;
+    for (int b = 0; b < B; ++b) s += D[(int64_t)b * K + k];
+    gr[off_b + k] = s;
+  }
+  if (tid < 64) {
+    float l = 0.f;
+    for (int b = tid; b < B; b += 64) l += lossn[(int64_t)g * B + b];
+    l = wave_sum(l);
+    if (tid == 0) losses[g] = l / (float)B;
+  }
+}
+
+void cls_head_train(uintptr_t a, uintptr_t theta, int64_t ldt, int64_t off_w, int64_t off_b, uintptr_t y, int G, int B,
+                    int HW, int C, int K, uintptr_t pooled, uintptr_t dlog, uintptr_t lossn, uintptr_t losses,
+                    uintptr_t grad, int64_t ldg, uintptr_t da, uintptr_t stream) {
+  NIDT_REQUIRE(C % 2 == 0 && C <= kCHMaxC && K >= 1 && K <= kCHMaxK && B >= 1 && HW >= 1,
+               "cls_head_train: C even <= 512, 1 <= K <= 256");
+  NIDT_REQUIRE(off_w % 2 == 0 && ldt % 2 == 0, "cls_head_train: 8-B aligned weight rows");
+  hipStream_t s = as_stream(stream);
+  hipLaunchKernelGGL(k_cls_head_fwd, dim3(G * B), dim3(kCHT), 0, s, ptr<const uint16_t>(a), ptr<const float>(theta), ldt,
+                     off_w, off_b, ptr<const int64_t>(y), B, HW, C, K, ptr<float>(pooled), ptr<float>(dlog),
+                     ptr<float>(lossn), ptr<uint16_t>(da));
+  const int ncol = (K * C + kCHT - 1) / kCHT;
+  hipLaunchKernelGGL(k_cls_head_grad, dim3(G, ncol + 1), dim3(kCHT), 0, s, ptr<const float>(pooled),
+                     ptr<const float>(dlog), ptr<const float>(lossn), B, C, K, ptr<float>(grad), ldg, off_w, off_b,
+                     ptr<float>(losses));
+  NIDT_CHECK(hipGetLastError());
+}
+
 }  // namespace nidt

@@ -527,6 +527,19 @@ class GroupedResNet18GN:
 
     # ------------------------------------------------------------------ forward
     def forward(self, x, theta, G, train=False):
+        a, saved = self.features(x, theta, G, train)
+        N, H, W, C = a.shape
+        pooled = a.float().view(N, H * W, C).mean(1)  # avg_pool2d(4) on 4x4 (CIFAR) / adaptive 1x1 on 8x8 (Tiny)
+        B = N // G
+        lw = theta[:, self.lw_off:self.lw_off + self.ncls * self.feat].view(G, self.ncls, self.feat)
+        lb = theta[:, self.lb_off:self.lb_off + self.ncls]
+        # the 512 -> K head as broadcast multiply-reduce, not bmm: BLAS calls keep library workspaces that a
+        # replayed hipGraph would share with eager work
+        logits = (pooled.view(G, B, 1, C) * lw.view(G, 1, self.ncls, C)).sum(-1) + lb.view(G, 1, self.ncls)
+        return logits.view(N, self.ncls), pooled, saved
+
+    def features(self, x, theta, G, train=False):
+        """Stem + the four stages: the final activation map [N, H, W, 512] and the saved tensors of the backward."""
         saved = []
         packed = self.packer is not None
         if packed:
@@ -546,37 +559,53 @@ class GroupedResNet18GN:
                 ts, ss, ysc = None, None, xin
             a, s2 = blk["n2"].fwd(t2, theta, G, res=ysc, relu=True)
             saved.append((xin, t1, s1, h1, t2, s2, ts, ss, a))
+        return a, saved
+
+    def _fused_head(self, theta):
+        return (self.hip and self.lw_off % 2 == 0 and theta.stride(0) % 2 == 0 and self.ncls <= 256
+                and self.feat <= 512 and os.environ.get("NIDT_CLS_HEAD", "1") != "0")
+
+    def _head_train(self, a, theta, grads, y, G, B):
+        """Classifier head + CrossEntropy forward/backward: per-client mean losses [G], the head's gradient rows,
+        and the bf16 input gradient of the final map.  HIP: two launches (``head.hip`` ``cls_head_train``)."""
         N, H, W, C = a.shape
-        pooled = a.float().view(N, H * W, C).mean(1)  # avg_pool2d(4) on 4x4 (CIFAR) / adaptive 1x1 on 8x8 (Tiny)
-        B = N // G
+        if self._fused_head(theta):
+            dev = a.device
+            pooled = torch.empty(N, C, device=dev, dtype=torch.float32)
+            dlog = torch.empty(N, self.ncls, device=dev, dtype=torch.float32)
+            lossn = torch.empty(N, device=dev, dtype=torch.float32)
+            losses = torch.empty(G, device=dev, dtype=torch.float32)
+            da = torch.empty(N, H, W, C, device=dev, dtype=torch.bfloat16)
+            yl = y if y.dtype == torch.int64 else y.long()
+            ops.ext().cls_head_train(a.contiguous().data_ptr(), theta.data_ptr(), theta.stride(0), self.lw_off,
+                                     self.lb_off, yl.contiguous().data_ptr(), G, B, H * W, C, self.ncls,
+                                     pooled.data_ptr(), dlog.data_ptr(), lossn.data_ptr(), losses.data_ptr(),
+                                     grads.data_ptr(), grads.stride(0), da.data_ptr(), _stream())
+            return losses, da
+        pooled = a.float().view(N, H * W, C).mean(1)
         lw = theta[:, self.lw_off:self.lw_off + self.ncls * self.feat].view(G, self.ncls, self.feat)
         lb = theta[:, self.lb_off:self.lb_off + self.ncls]
-        # the 512 -> K head as broadcast multiply-reduce, not bmm: BLAS calls keep library workspaces that a
-        # replayed hipGraph would share with eager work
         logits = (pooled.view(G, B, 1, C) * lw.view(G, 1, self.ncls, C)).sum(-1) + lb.view(G, 1, self.ncls)
-        return logits.view(N, self.ncls), pooled, saved
-
-    # ------------------------------------------------------------------ train step
-    def train_step(self, theta, grads, x, y, G, B):
-        logits, pooled, saved = self.forward(x, theta, G, train=True)
-        lg = logits.view(G, B, self.ncls)
-        logp = torch.log_softmax(lg, dim=-1)
+        logp = torch.log_softmax(logits, dim=-1)
         yl = y.long().view(G, B)
         losses = -logp.gather(2, yl.unsqueeze(2)).squeeze(2).mean(1)
         # softmax - onehot (scatter, not F.one_hot: its range check syncs the host, which a graph capture forbids)
         dlog = logp.exp().scatter_add(2, yl.unsqueeze(2), torch.full_like(logp[..., :1], -1.0)) / B  # [G, B, K]
-        lw = theta[:, self.lw_off:self.lw_off + self.ncls * self.feat].view(G, self.ncls, self.feat)
         grads[:, self.lw_off:self.lw_off + self.ncls * self.feat].view(G, self.ncls, self.feat).copy_(
             (dlog.view(G, B, self.ncls, 1) * pooled.view(G, B, 1, self.feat)).sum(1))
         grads[:, self.lb_off:self.lb_off + self.ncls].copy_(dlog.sum(1))
         dpool = (dlog.view(G, B, self.ncls, 1) * lw.view(G, 1, self.ncls, self.feat)).sum(2).view(G * B, 1, self.feat)
-        a = saved[-1][-1]
-        N, H, W, C = a.shape
+        # bf16 residual-gradient stream on the HIP path (res_grad writes bf16; re-read by every GroupNorm backward)
+        da = (dpool / float(H * W)).expand(N, H * W, C).reshape(N, H, W, C).to(self.act).contiguous()
+        return losses, da
+
+    # ------------------------------------------------------------------ train step
+    def train_step(self, theta, grads, x, y, G, B):
+        a, saved = self.features(x, theta, G, train=True)
         # NIDT_WGRAD_STREAM=1: weight gradients on a branch forked from the data-gradient chain (joined below); off by
         # default: CIFAR SubAvg 1.077-1.087 vs 1.069-1.078 s/round, Tiny 2.82 vs 2.19 (profiles/r3_ab_wgrad_stream.txt)
         ws = self._wgrad_stream(G, B)
-        # bf16 residual-gradient stream on the HIP path (res_grad writes bf16; re-read by every GroupNorm backward)
-        da = (dpool / float(H * W)).expand(N, H * W, C).reshape(N, H, W, C).to(self.act).contiguous()
+        losses, da = self._head_train(a, theta, grads, y, G, B)
         for blk, sv in zip(reversed(self.blocks), reversed(saved[1:])):
             xin, t1, s1, h1, t2, s2, ts, ss, a = sv
             dt2 = blk["n2"].bwd(da, a, t2, s2, theta, grads, G)

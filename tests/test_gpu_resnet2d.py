@@ -280,3 +280,38 @@ def test_tiny_resnet18_train_step_matches_cpu_twin():
         assert cos > 0.98, (gi, cos)
     lg = hip.eval_logits(th_d, None, idx.to(dev), G, B)
     assert lg.shape == (G * B, 200) and torch.isfinite(lg).all()
+
+
+@pytest.mark.parametrize("hw,K,G,B", [(4, 10, 3, 16), (8, 200, 2, 5), (4, 100, 1, 7)])
+def test_fused_cls_head_matches_torch_head(hw, K, G, B, monkeypatch):
+    """``cls_head_train`` (pool + linear + CrossEntropy forward/backward, two launches) against the engine's torch
+    head on the same final map: per-client losses, dW / db rows and the bf16 input gradient."""
+    from neuroimagedisttraining_amd.engine import resnet2d_hip as R
+    from neuroimagedisttraining_amd.engine.flat import ParamLayout
+    from neuroimagedisttraining_amd.models import customized_resnet18
+    dev = _dev()
+    torch.manual_seed(K + B)
+    L = ParamLayout.from_tensors(list(customized_resnet18(class_num=K).named_parameters()))
+    net = R.GroupedResNet18GN(L, dev)
+    P = L.total
+    ld = (P + 63) // 64 * 64
+    theta = torch.zeros(G, ld, device=dev)[:, :P]
+    theta.copy_(torch.randn(G, P, device=dev) * 0.05)
+    a = torch.relu(torch.randn(G * B, hw, hw, 512, device=dev)).to(torch.bfloat16)
+    y = torch.randint(0, K, (G * B,), device=dev)
+    assert net._fused_head(theta)
+    g1 = torch.zeros(G, ld, device=dev)[:, :P]
+    l1, da1 = net._head_train(a, theta, g1, y, G, B)
+    monkeypatch.setenv("NIDT_CLS_HEAD", "0")
+    assert not net._fused_head(theta)
+    g0 = torch.zeros(G, ld, device=dev)[:, :P]
+    l0, da0 = net._head_train(a, theta, g0, y, G, B)
+    torch.cuda.synchronize()
+    assert _rel(l1, l0) < 1e-5
+    sl = slice(net.lw_off, net.lw_off + K * 512)
+    assert _rel(g1[:, sl], g0[:, sl]) < 1e-5
+    sb = slice(net.lb_off, net.lb_off + K)
+    assert _rel(g1[:, sb], g0[:, sb]) < 1e-5
+    assert da1.dtype == da0.dtype == torch.bfloat16 and da1.shape == da0.shape
+    assert _rel(da1, da0) < 1e-2
+    assert float(g1[:, :net.lw_off].abs().max()) == 0.0  # nothing outside the head rows written
