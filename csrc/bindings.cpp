@@ -49,6 +49,10 @@ int conv3d_fwd_tri_pick(int G, int B, int D, int H, int W, int Cin, int Cout, in
 int conv3d_fwd_tri_table_size(int B, int D, int H, int W, int pad);
 int conv3d_fwd_slab_ok(int B, int D, int H, int W, int Cin, int Cout, int pad);
 int conv2d_fwd_slab_ok(int B, int H, int W, int Cin, int Cout);
+int conv3d_fwd_vol_ok(int B, int D, int H, int W, int Cin, int Cout, int pad);
+int conv3d_fwd_vol_pick(int G, int B, int D, int H, int W, int Cin, int Cout, int pad);
+void conv3d_fwd_vol(uintptr_t x, uintptr_t w, uintptr_t bias, int64_t bias_ld, uintptr_t y, uintptr_t stats, int G,
+                    int B, int D, int H, int W, int Cin, int Cout, int pad, uintptr_t stream);
 int conv2d_fwd_slab_pick(int G, int B, int H, int W, int Cin, int Cout);
 void conv2d_fwd_slab(uintptr_t x, uintptr_t w, uintptr_t y, int G, int B, int H, int W, int Cin, int Cout,
                      uintptr_t utab, uintptr_t stream);
@@ -223,6 +227,9 @@ PYBIND11_MODULE(_nidt_hip, m) {
   DEF(conv3d_fwd_slab_table);
   DEF(conv3d_fwd_slab);
   DEF(conv2d_fwd_slab_ok);
+  DEF(conv3d_fwd_vol_ok);
+  DEF(conv3d_fwd_vol_pick);
+  DEF(conv3d_fwd_vol);
   DEF(conv2d_fwd_slab_pick);
   DEF(conv2d_fwd_slab);
   DEF(conv3d_wgrad_tri_nsplit);

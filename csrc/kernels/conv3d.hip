@@ -81,8 +81,13 @@ __device__ __forceinline__ uint4 xform8(uint4 v, const float* s, const float* t,
 template <int BCO, int BP, int WM, int WN, bool BIAS, bool STATS, int TCO, int TP>
 __device__ __forceinline__ void conv_fwd_epilogue(const ConvFwdArgs& a, f32x4 (&acc)[TCO][TP], float* red, int g,
                                                   int pb, int co0, int wco, int wp, int fr, int fq, int tid,
-                                                  int ph = 0) {
+                                                  int ph = 0, int mb = -1, int me = -1) {
+  // block positions [mb, me) of the client (default: [pb BP, min(pb BP + BP, Mg)), the fixed-size blocks)
   constexpr int WCO = BCO / WM, WP = BP / WN;
+  if (mb < 0) {
+    mb = pb * BP;
+    me = a.Mg;
+  }
   float bias_r[TCO][4];
 #pragma unroll
   for (int i = 0; i < TCO; ++i)
@@ -90,11 +95,11 @@ __device__ __forceinline__ void conv_fwd_epilogue(const ConvFwdArgs& a, f32x4 (&
     for (int r = 0; r < 4; ++r)
       bias_r[i][r] = BIAS ? a.bias[(int64_t)g * (a.bias_ld ? a.bias_ld : a.Cout) + co0 + wco * WCO + i * 16 + 4 * fq + r]
                           : 0.f;
-  const int posw = pb * BP + wp * WP + fr;
+  const int posw = mb + wp * WP + fr;
 #pragma unroll
   for (int j = 0; j < TP; ++j) {
     const int m = posw + j * 16;
-    if (m < a.Mg) {
+    if (m < me) {
       int64_t yo = (int64_t)g * a.Mg + m;
       if (a.nph) {  // phase output: scatter to the strided positions of the full-resolution gradient
         const int S = a.Do * a.Ho * a.Wo, nl = m / S, sr = m - nl * S;
@@ -117,7 +122,7 @@ __device__ __forceinline__ void conv_fwd_epilogue(const ConvFwdArgs& a, f32x4 (&
   if (STATS) {
     // pass 1: block sums per channel (valid positions only)
     // red: [WN (wp)][BCO] floats of LDS scratch
-    const int cnt = min(BP, a.Mg - pb * BP);
+    const int cnt = min(BP, me - mb);
     float s_[TCO][4];
 #pragma unroll
     for (int i = 0; i < TCO; ++i)
@@ -126,7 +131,7 @@ __device__ __forceinline__ void conv_fwd_epilogue(const ConvFwdArgs& a, f32x4 (&
         float s = 0.f;
 #pragma unroll
         for (int j = 0; j < TP; ++j)
-          if (posw + j * 16 < a.Mg) s += acc[i][j][r] + bias_r[i][r];
+          if (posw + j * 16 < me) s += acc[i][j][r] + bias_r[i][r];
         s += __shfl_xor(s, 1, 64);
         s += __shfl_xor(s, 2, 64);
         s += __shfl_xor(s, 4, 64);
@@ -160,7 +165,7 @@ __device__ __forceinline__ void conv_fwd_epilogue(const ConvFwdArgs& a, f32x4 (&
         float s = 0.f;
 #pragma unroll
         for (int j = 0; j < TP; ++j)
-          if (posw + j * 16 < a.Mg) {
+          if (posw + j * 16 < me) {
             const float d = acc[i][j][r] + bias_r[i][r] - mean_[i][r];
             s = fmaf(d, d, s);
           }
@@ -791,6 +796,133 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void k_conv_fwd_slab(ConvFwdArgs a
                                                          fq, tid);
 }
 
+// k_conv_fwd_vol — 3x3x3 stride-1 forward/dgrad of small volumes (the AlexNet3D 5x7x5 conv3-5 layers) with the B
+// operand of a whole padded SAMPLE staged once per 64-channel chunk for all 27 taps.  Blocks are (sample, output-
+// channel chunk) with BP = 64 WN >= Do Ho Wo positions; the padded sample (Dp Hp Wp <= U rows, padding rows read out of
+// the buffer range as zeros) is the union of every tap's rows, so tap (kd, kh, kw) of output p reads union row
+// idx(p) + kd Hp Wp + kh Wp + kw — no table.  Against the per-tap kernel (one B tile per tap) this moves 27x fewer B
+// bytes per k-step; weights double-buffered per tap as in k_conv_fwd_slab.  Per-sample BN statistics blocks
+// (nPB = B, block size Do Ho Wo).
+template <int BCO, int WM, int WN, int U, bool BIAS, bool STATS>
+__global__ __launch_bounds__(64 * WM * WN, 2) void k_conv_fwd_vol(ConvFwdArgs a, int nCO) {
+  constexpr int NW = WM * WN, BP = 64 * WN, BK = 64;
+  constexpr int WCO = BCO / WM, WP = 64, TCO = WCO / 16, TP = WP / 16;
+  constexpr int A_ELEMS = BCO * BK;
+  constexpr int AI = BCO / 8, AIW = (AI + NW - 1) / NW;   // weight-tile pieces (8 rows) and per wave
+  constexpr int UP = U / 8, UPW = (UP + NW - 1) / NW;     // union pieces and per wave
+  static_assert(U % 8 == 0 && TCO >= 1, "tile split");
+  __shared__ __attribute__((aligned(16))) uint16_t smem[2 * A_ELEMS + U * BK];
+  uint16_t* const sAb = smem;
+  uint16_t* const sU = smem + 2 * A_ELEMS;
+
+  const int nwg = gridDim.x;
+  const int id = xcd_remap(blockIdx.x, nwg);
+  const int cot = id % nCO, rest = id / nCO;
+  const int n = rest % a.B, g = rest / a.B;
+  const int co0 = cot * BCO;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wco = wid / WN, wp = wid % WN;
+  const int Cin = a.Cin, nck = Cin / BK, pad = a.pad;
+  const int Hp = a.H + 2 * pad, Wp = a.W + 2 * pad, HWp = Hp * Wp, R = (a.D + 2 * pad) * HWp;
+  const int S = a.Do * a.Ho * a.Wo, HoWo = a.Ho * a.Wo;
+  const int lrow = lane >> 3, slot = lane & 7;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int64_t vol = (int64_t)a.D * a.H * a.W;
+  // union pieces of this lane: padded row r -> source voxel of sample n (or out of range: zeros)
+  int uoff[UPW];
+#pragma unroll
+  for (int i = 0; i < UPW; ++i) {
+    const int u = 8 * (wid + NW * i) + lrow;
+    uoff[i] = kBufOOB;
+    if (wid + NW * i < UP && u < R) {
+      const int d = u / HWp - pad, h = (u / Wp) % Hp - pad, w = u % Wp - pad;
+      if ((unsigned)d < (unsigned)a.D && (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W)
+        uoff[i] = (int)(((n * vol + ((int64_t)d * a.H + h) * a.W + w) * Cin) * 2) + ((slot ^ swz_un(u)) << 4);
+    }
+  }
+  int hrow[TP];
+#pragma unroll
+  for (int j = 0; j < TP; ++j) {
+    int p = wp * WP + j * 16 + fr;
+    p = p < S ? p : 0;
+    const int od = p / HoWo, r2 = p - od * HoWo, oh = r2 / a.Wo, ow = r2 - oh * a.Wo;
+    hrow[j] = od * HWp + oh * Wp + ow;
+  }
+  int aoff[AIW];
+#pragma unroll
+  for (int i = 0; i < AIW; ++i) {
+    const int row = 8 * (wid + NW * i) + lrow;
+    aoff[i] = ((co0 + row) * 27 * Cin + ((slot ^ swz_dma(row)) << 3)) * 2;
+  }
+  const int64_t xcl = (int64_t)a.B * vol * Cin;
+  const i32x4_t rxs = make_rsrc(a.x + (int64_t)g * xcl, (uint32_t)(xcl * 2));
+  const i32x4_t rws = make_rsrc(a.w + (int64_t)g * a.Cout * 27 * Cin, (uint32_t)(a.Cout * 27 * Cin * 2));
+
+  auto issue_a = [&](int ks, int buf) {  // weight tile of tap t = ks % 27 of channel chunk ks / 27
+    const int cc = ks / 27, t = ks - 27 * cc;
+    const int woff = (t * Cin + cc * BK) * 2;
+    uint16_t* sA = sAb + buf * A_ELEMS;
+#pragma unroll
+    for (int i = 0; i < AIW; ++i)
+      if (wid + NW * i < AI) blds16(rws, aoff[i] + woff, sA + (wid + NW * i) * 512);
+  };
+  auto issue_u = [&](int cc) {
+#pragma unroll
+    for (int i = 0; i < UPW; ++i) {
+      if (wid + NW * i >= UP) continue;
+      const int o = uoff[i];
+      blds16(rxs, o == kBufOOB ? kBufOOB : o + cc * (BK * 2), sU + (wid + NW * i) * 512);
+    }
+  };
+
+  f32x4 acc[TCO][TP];
+#pragma unroll
+  for (int i = 0; i < TCO; ++i)
+#pragma unroll
+    for (int j = 0; j < TP; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nks = 27 * nck;
+  issue_u(0);
+  issue_a(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  for (int ks = 0; ks < nks; ++ks) {
+    const int cc = ks / 27, t = ks - 27 * cc, kd = t / 9, kh = (t / 3) % 3, kw = t % 3;
+    if (ks + 1 < nks) issue_a(ks + 1, (ks + 1) & 1);
+    const uint16_t* sA = sAb + (ks & 1) * A_ELEMS;
+    const int toff = kd * HWp + kh * Wp + kw;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 fa[TCO], fb[TP];
+#pragma unroll
+      for (int i = 0; i < TCO; ++i) {
+        const int r = wco * WCO + i * 16 + fr;
+        fa[i] = *reinterpret_cast<const bf16x8*>(&sA[r * BK + (((4 * kk + fq) ^ swz_dma(r)) << 3)]);
+      }
+#pragma unroll
+      for (int j = 0; j < TP; ++j) {
+        const int r = hrow[j] + toff;
+        fb[j] = *reinterpret_cast<const bf16x8*>(&sU[r * BK + (((4 * kk + fq) ^ swz_un(r)) << 3)]);
+      }
+#pragma unroll
+      for (int i = 0; i < TCO; ++i)
+#pragma unroll
+        for (int j = 0; j < TP; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (t == 26 && cc + 1 < nck) {  // every wave is done with this chunk's union: reload it for the next one
+      issue_u(cc + 1);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+    }
+  }
+  __syncthreads();
+  conv_fwd_epilogue<BCO, BP, WM, WN, BIAS, STATS, TCO, TP>(a, acc, reinterpret_cast<float*>(smem), g, n, co0, wco, wp, fr,
+                                                         fq, tid, 0, n * S, n * S + S);
+}
+
 // Finish of a split-K forward without bias / statistics: y = bf16(sum over the ksplit slabs), 4 values per thread
 __global__ __launch_bounds__(256) void k_fwd_splitk_sum(const float* __restrict__ part, int ksplit, int64_t n4,
                                                         uint16_t* __restrict__ y) {
@@ -1410,6 +1542,68 @@ void conv2d_fwd_slab(uintptr_t x, uintptr_t w, uintptr_t y, int G, int B, int H,
                      uintptr_t utab, uintptr_t stream) {
   NIDT_REQUIRE(conv2d_fwd_slab_ok(B, H, W, Cin, Cout), "conv2d_fwd_slab: shape not supported");
   fwd_slab_impl(x, w, 0, 0, y, 0, G, B, 1, H, W, Cin, Cout, 1, 9, utab, stream);
+}
+
+// ---- k_conv_fwd_vol host side (whole padded sample <= 448 rows, <= 256 output positions per sample) ----
+constexpr int kVolU = 448;
+int conv3d_fwd_vol_ok(int B, int D, int H, int W, int Cin, int Cout, int pad) {
+  if (Cin % 64 != 0 || Cout % 64 != 0 || pad < 0 || pad > 2 || Cin > kMaxCin || B < 1) return 0;
+  const int Do = D + 2 * pad - 2, Ho = H + 2 * pad - 2, Wo = W + 2 * pad - 2;
+  if (Do < 1 || Ho < 1 || Wo < 1 || Do * Ho * Wo > 256) return 0;
+  return (D + 2 * pad) * (H + 2 * pad) * (W + 2 * pad) <= kVolU ? 1 : 0;
+}
+
+// Opt-in (NIDT_FWD_VOL=1): measured slower than the per-tap kernel for the 5x7x5 conv3-5 at 64 clients (fwd + dgrad
+// 2.19 vs 1.71 ms per step: 3-wave blocks, one exposed weight-tile wait per tap) and within 1 % at 8 clients
+// (profiles/r3_ab_fwd_vol.txt).  When enabled: grids of >= NIDT_FWD_VOL_MINB (256) blocks without split-K.
+int conv3d_fwd_vol_pick(int G, int B, int D, int H, int W, int Cin, int Cout, int pad) {
+  static const int env = [] {
+    const char* e = getenv("NIDT_FWD_VOL");
+    return e ? atoi(e) : 0;
+  }();
+  static const int minb = [] {
+    const char* e = getenv("NIDT_FWD_VOL_MINB");
+    return e ? atoi(e) : 256;
+  }();
+  if (!env || !conv3d_fwd_vol_ok(B, D, H, W, Cin, Cout, pad)) return 0;
+  const int Mg = B * (D + 2 * pad - 2) * (H + 2 * pad - 2) * (W + 2 * pad - 2);
+  if (conv3d_fwd_ksplit(Cin, Cout, G, Mg) > 1) return 0;
+  return (int64_t)G * B * (Cout / 64) >= minb ? 1 : 0;
+}
+
+void conv3d_fwd_vol(uintptr_t x, uintptr_t w, uintptr_t bias, int64_t bias_ld, uintptr_t y, uintptr_t stats, int G,
+                    int B, int D, int H, int W, int Cin, int Cout, int pad, uintptr_t stream) {
+  NIDT_REQUIRE(conv3d_fwd_vol_ok(B, D, H, W, Cin, Cout, pad), "conv3d_fwd_vol: shape not supported");
+  NIDT_REQUIRE((int64_t)B * D * H * W * Cin * 2 < (1ll << 31), "conv3d_fwd_vol: per-client input below 2 GiB");
+  const bool hb = bias != 0, st = stats != 0;
+  NIDT_REQUIRE(!st || hb, "conv3d_fwd_vol: statistics require a bias");
+  ConvFwdArgs a;
+  a.x = ptr<const uint16_t>(x); a.w = ptr<const uint16_t>(w); a.bias = ptr<const float>(bias);
+  a.xs = nullptr; a.xt = nullptr; a.y = ptr<uint16_t>(y); a.stats = ptr<float>(stats);
+  a.B = B; a.D = D; a.H = H; a.W = W; a.Cin = Cin; a.Cout = Cout; a.pad = pad; a.padd = pad; a.kt = 27; a.st = 1;
+  a.Do = D + 2 * pad - 2; a.Ho = H + 2 * pad - 2; a.Wo = W + 2 * pad - 2;
+  a.Mg = B * a.Do * a.Ho * a.Wo;
+  a.nPB = B;  // statistics blocks = samples
+  a.G = G;
+  a.bias_ld = bias_ld;
+  const int S = a.Do * a.Ho * a.Wo, wn = ceil_div(S, 64), nCO = Cout / 64;
+  static const int wm = [] {
+    const char* e = getenv("NIDT_FWD_VOL_WM");
+    return e ? atoi(e) : 1;
+  }();
+  const dim3 grid((unsigned)((int64_t)G * B * nCO));
+  hipStream_t s = as_stream(stream);
+#define NIDT_FV(WM, WN, BI, STT) \
+  hipLaunchKernelGGL((k_conv_fwd_vol<64, WM, WN, kVolU, BI, STT>), grid, dim3(64 * WM * WN), 0, s, a, nCO)
+#define NIDT_FV_B(WM, WN) \
+  if (st) NIDT_FV(WM, WN, true, true); else if (hb) NIDT_FV(WM, WN, true, false); else NIDT_FV(WM, WN, false, false);
+#define NIDT_FV_N(WM) \
+  if (wn == 1) { NIDT_FV_B(WM, 1) } else if (wn == 2) { NIDT_FV_B(WM, 2) } else if (wn == 3) { NIDT_FV_B(WM, 3) } else { NIDT_FV_B(WM, 4) }
+  if (wm == 2) { NIDT_FV_N(2) } else { NIDT_FV_N(1) }
+#undef NIDT_FV_N
+#undef NIDT_FV_B
+#undef NIDT_FV
+  NIDT_CHECK(hipGetLastError());
 }
 
 int conv3d_fwd_nblocks(int B, int D, int H, int W, int pad, int bp) {

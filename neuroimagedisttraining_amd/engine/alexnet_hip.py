@@ -78,6 +78,8 @@ class HipAlexNet3D:
             mg = B * (sp[0] + 2 * pad - 2) * (sp[1] + 2 * pad - 2) * (sp[2] + 2 * pad - 2)
             bp = self.m.conv3d_fwd_bp(cin, cout, 0, G, mg)
             npb = self.m.conv3d_fwd_nblocks(B, sp[0], sp[1], sp[2], pad, bp)
+            if self.m.conv3d_fwd_vol_pick(G, B, *sp, cin, cout, pad):  # k_conv_fwd_vol: statistics per sample
+                bp, npb = mg // B, B
             b["st%d" % ci] = e(G, npb, cout, 2, dt=f32)
             b["npb%d" % ci] = npb
             b["bp%d" % ci] = bp
@@ -89,6 +91,9 @@ class HipAlexNet3D:
                 mg = B * (vol[0] + 2 * pd - 2) * (vol[1] + 2 * pd - 2) * (vol[2] + 2 * pd - 2)
                 ks = self.m.conv3d_fwd_ksplit(c_in, c_out, G, mg)
                 b["ks%s%d" % (tag, ci)] = ks
+                if (tag == "f" or train) and self.m.conv3d_fwd_vol_pick(G, B, *vol, c_in, c_out, pd):
+                    # whole-sample union staging (k_conv_fwd_vol): the 5x7x5 conv3-5 forward / data gradient
+                    b["fv%s%d" % (tag, ci)] = True
                 if ks > 1:
                     fp_sz = max(fp_sz, ks * G * mg * c_out)
         b["fpart"] = e(max(fp_sz, 1), dt=f32)
@@ -100,6 +105,8 @@ class HipAlexNet3D:
                 if tag == "d" and not train:
                     continue
                 kname = "ks%s%d" % (tag, ci)
+                if b.get("fv" + kname[2:]):
+                    continue
                 if b[kname] <= 1 and self.m.conv3d_fwd_slab_pick(G, B, *vol, c_in, c_out, pd):
                     # kd-slab union staging (k_conv_fwd_slab): the padded conv2 data gradient
                     tab = e(self.m.conv3d_fwd_slab_table_size(B, *vol, pd), dt=torch.int32)
@@ -154,6 +161,14 @@ class HipAlexNet3D:
         """conv3d_fwd, or its split-K form when ``b[key]`` (chosen at allocation) is > 1.  With ``theta`` the bias
         of conv ``ci`` is read straight from the flat parameter rows (row stride P), no per-step copy."""
         ks = b[key]
+        if b.get("fv" + key[2:]):  # whole-sample union B operand (k_conv_fwd_vol)
+            if theta is not None:
+                o = self.o["features.%d.bias" % ci]
+                bptr, bld = theta.data_ptr() + 4 * o, theta.stride(0)
+            else:
+                bptr, bld = _p(bias), 0
+            self.m.conv3d_fwd_vol(_p(x), _p(w), bptr, bld, _p(y), _p(stats), G, B, D, H, W, cin, cout, pad, st)
+            return
         ft, fs = b.get("ft" + key), b.get("fs" + key)
         if ft is not None or fs is not None:  # union-staged B operand (k_conv_fwd_slab / k_conv_fwd_tri)
             if theta is not None:

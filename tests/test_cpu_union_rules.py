@@ -125,3 +125,13 @@ def test_conv2d_slab_choice():
     assert m.conv2d_fwd_slab_pick(10, 16, 16, 16, 256, 256) == 1
     n_bands = 16 * 32 * 32 // 256
     assert m.conv3d_fwd_slab_table_size(16, 1, 32, 32, 1) == n_bands * (2 * 384 + 256)
+
+
+def test_vol_kernel_rule():
+    """Whole-sample union kernel (k_conv_fwd_vol): padded sample <= 448 rows and <= 256 output positions; opt-in."""
+    m = _ext()
+    assert m.conv3d_fwd_vol_ok(16, 5, 7, 5, 128, 192, 1) == 1      # AlexNet conv3: 7x9x7 = 441 rows, 175 positions
+    assert m.conv3d_fwd_vol_ok(16, 5, 7, 5, 192, 128, 1) == 1
+    assert m.conv3d_fwd_vol_ok(16, 6, 8, 7, 64, 64, 1) == 0        # 8x10x9 = 720 padded rows
+    assert m.conv3d_fwd_vol_ok(16, 5, 7, 5, 96, 128, 1) == 0       # channels not a multiple of 64
+    assert m.conv3d_fwd_vol_pick(64, 16, 5, 7, 5, 128, 192, 1) == 0  # off unless NIDT_FWD_VOL=1

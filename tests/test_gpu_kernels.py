@@ -152,6 +152,45 @@ def test_conv3d_fwd_slab_matches_fp32(cin, cout, pad, sp, G, B):
     assert _relerr(y.float(), (yr.view(G, -1, cout) + bias.view(G, 1, cout)).view_as(yr)) < 1e-2
 
 
+@pytest.mark.parametrize("cin,cout,pad,sp", [(128, 192, 1, (5, 7, 5)), (192, 192, 1, (5, 7, 5)),
+                                             (192, 128, 1, (5, 7, 5)), (64, 64, 0, (6, 8, 6)), (64, 128, 2, (3, 4, 3)),
+                                             (128, 64, 1, (4, 4, 4))])
+@pytest.mark.parametrize("G,B", [(2, 16), (3, 5)])
+def test_conv3d_fwd_vol_matches_fp32(cin, cout, pad, sp, G, B):
+    """Whole-sample union forward / data gradient (k_conv_fwd_vol: one padded sample per 64-channel chunk serves all
+    27 taps, per-sample statistics blocks): output with and without bias against fp32 conv3d, and the per-sample
+    (mean, M2) statistics against the oracle."""
+    m = _m()
+    assert m.conv3d_fwd_vol_ok(B, *sp, cin, cout, pad)
+    torch.manual_seed(7)
+    x = torch.randn(G * B, *sp, cin, device=DEV).bfloat16()
+    w = (torch.randn(G, cout, 27, cin, device=DEV) * 0.05).bfloat16()
+    bias = torch.randn(G, cout, device=DEV)
+    Do, Ho, Wo = [s + 2 * pad - 2 for s in sp]
+    S = Do * Ho * Wo
+    y = torch.full((G * B, Do, Ho, Wo, cout), float("nan"), device=DEV, dtype=torch.bfloat16)
+    y0 = torch.full_like(y, float("nan"))
+    stats = torch.full((G, B, cout, 2), float("nan"), device=DEV)
+    m.conv3d_fwd_vol(x.data_ptr(), w.data_ptr(), bias.data_ptr(), 0, y.data_ptr(), stats.data_ptr(), G, B, *sp, cin,
+                     cout, pad, _st())
+    m.conv3d_fwd_vol(x.data_ptr(), w.data_ptr(), 0, 0, y0.data_ptr(), 0, G, B, *sp, cin, cout, pad, _st())
+    torch.cuda.synchronize()
+    ys = []
+    for g in range(G):
+        wg = w[g].float().view(cout, 3, 3, 3, cin).permute(0, 4, 1, 2, 3)
+        ys.append(_cl(F.conv3d(_cf(x[g * B:(g + 1) * B].float()), wg, None, 1, pad)))
+    yr = torch.cat(ys, 0)
+    assert torch.isfinite(y.float()).all() and torch.isfinite(y0.float()).all()
+    assert _relerr(y0.float(), yr) < 1e-2
+    yb = (yr.view(G, -1, cout) + bias.view(G, 1, cout)).view_as(yr)
+    assert _relerr(y.float(), yb) < 1e-2
+    ys_ = yb.view(G, B, S, cout).double()
+    mean = ys_.mean(2)
+    m2 = ((ys_ - mean.unsqueeze(2)) ** 2).sum(2)
+    assert _relerr(stats[..., 0].double(), mean) < 1e-3
+    assert _relerr(stats[..., 1].double(), m2) < 1e-3
+
+
 @pytest.mark.parametrize("cin,cout,hw", [(64, 64, (32, 32)), (128, 128, (16, 16)), (64, 128, (16, 32)),
                                          (256, 256, (16, 16)), (64, 64, (64, 64)), (128, 64, (32, 32))])
 @pytest.mark.parametrize("G,B", [(1, 3), (3, 2)])
