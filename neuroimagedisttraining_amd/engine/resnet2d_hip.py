@@ -126,6 +126,8 @@ def slab_conv2d(x_ptr, w_ptr, y_ptr, G, B, H, W, Cin, Cout, device):
         tab = torch.empty(m.conv3d_fwd_slab_table_size(B, 1, H, W, 1), device=device, dtype=torch.int32)
         m.conv3d_fwd_slab_table(tab.data_ptr(), B, 1, H, W, 1, _stream())
         if not torch.cuda.is_current_stream_capturing():  # built inside a capture: that graph's memory, not cached
+            # the cached table is read by launches on other streams (side lanes): complete it before sharing it
+            torch.cuda.current_stream().synchronize()
             _SLAB_TABS[key] = tab
     m.conv2d_fwd_slab(x_ptr, w_ptr, y_ptr, G, B, H, W, Cin, Cout, tab.data_ptr(), _stream())
     return True
@@ -291,6 +293,7 @@ class GroupedConv:
             tab = torch.empty(B * Ho * Wo, 2, device=device, dtype=torch.int32)
             ops.ext().conv_pos_table_g(tab.data_ptr(), B, 1, H, W, self.kt, self.stride, self.pad, 0, _stream())
             if not torch.cuda.is_current_stream_capturing():
+                torch.cuda.current_stream().synchronize()  # shared with launches on other streams from now on
                 self._ptabs[key] = tab
         return tab
 
@@ -546,7 +549,8 @@ class GroupedResNet18GN:
             self.packer.pack(theta, G, train, key=(G, x.shape[0] // G, train))
         t = self.stem.fwd(x, theta, G, train, packed)
         a, st = self.stem_gn.fwd(t, theta, G, relu=True)
-        saved.append((x, t, st, a))
+        if train:  # evaluation keeps no activations alive (only the backward reads them)
+            saved.append((x, t, st, a))
         for blk in self.blocks:
             xin = a
             t1 = blk["c1"].fwd(xin, theta, G, train, packed)
@@ -558,7 +562,8 @@ class GroupedResNet18GN:
             else:
                 ts, ss, ysc = None, None, xin
             a, s2 = blk["n2"].fwd(t2, theta, G, res=ysc, relu=True)
-            saved.append((xin, t1, s1, h1, t2, s2, ts, ss, a))
+            if train:
+                saved.append((xin, t1, s1, h1, t2, s2, ts, ss, a))
         return a, saved
 
     def _fused_head(self, theta):

@@ -67,6 +67,10 @@ def slab_conv(x_ptr, w_ptr, y_ptr, G, B, D, H, W, Cin, Cout, pad, device):
     if tab is None:
         tab = torch.empty(m.conv3d_fwd_slab_table_size(B, D, H, W, pad), device=device, dtype=torch.int32)
         m.conv3d_fwd_slab_table(tab.data_ptr(), B, D, H, W, pad, _stream())
+        if torch.cuda.is_current_stream_capturing():  # built inside a capture: that graph's memory, not cached
+            m.conv3d_fwd_slab(x_ptr, w_ptr, 0, 0, y_ptr, 0, G, B, D, H, W, Cin, Cout, pad, tab.data_ptr(), _stream())
+            return True
+        torch.cuda.current_stream().synchronize()  # shared with launches on other streams from now on
         _SLAB_TABS[key] = tab
     m.conv3d_fwd_slab(x_ptr, w_ptr, 0, 0, y_ptr, 0, G, B, D, H, W, Cin, Cout, pad, tab.data_ptr(), _stream())
     return True
@@ -157,6 +161,7 @@ class GConv3:
             ptab = torch.empty(B * Do * Ho * Wo, 2, device=x.device, dtype=torch.int32)
             m.conv_pos_table_g(ptab.data_ptr(), B, D, H, W, self.kt, self.stride, self.pad, padd, st)
             if not torch.cuda.is_current_stream_capturing():
+                torch.cuda.current_stream().synchronize()  # shared with launches on other streams from now on
                 self._ptabs[key] = ptab
         cur = torch.cuda.current_stream()
         if ws is not None:

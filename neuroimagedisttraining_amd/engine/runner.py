@@ -32,6 +32,7 @@ The personalized / decentralized algorithms build on this class (``engine/person
 from __future__ import annotations
 
 import math
+import os
 import time
 from dataclasses import dataclass, replace
 
@@ -819,7 +820,91 @@ class FLRunner:
             out[js] = acc.cpu().numpy()
         return out
 
+    @staticmethod
+    def _pad_size(n):
+        """Evaluation bucket of a split of n samples: n rounded up to a multiple of 8 (n <= 64), else to the next
+        step of a 2^(1/4) ladder (<= 19 % padding, ~9 % on average)."""
+        if n <= 64:
+            return -(-n // 8) * 8
+        return int(math.ceil(2.0 ** (math.ceil(4.0 * math.log2(n) - 1e-9) / 4.0)))
+
     def eval_grouped(self, theta, bufs, rows, clients, which="test"):
+        """Model row rows[j] on client clients[j]'s split, per-client (correct, loss_sum, total).
+
+        Ragged splits (Dirichlet / site partitions give nearly every client its own size) are bucketed by padded
+        size (:meth:`_pad_size`) and each bucket's clients run as grouped launches of G rows x chunk samples, the
+        rows past a client's size repeating its first sample and masked out of the sums — a few launches instead
+        of one small latency-bound launch per distinct size (or per test_batch chunk of a large client).  Every
+        model is per-sample in eval mode (GroupNorm, BatchNorm on running statistics), so the padding cannot
+        change a valid sample's logits.  ``NIDT_EVAL_PAD=0`` keeps the exact-size grouping (A/B)."""
+        if os.environ.get("NIDT_EVAL_PAD", "1") == "0":
+            return self._eval_grouped_exact(theta, bufs, rows, clients, which)
+        out = np.zeros((len(clients), 3), dtype=np.float64)
+        splits = [self._split_of(c, which) for c in clients]
+        buckets = {}
+        for j, sp in enumerate(splits):
+            if len(sp):
+                buckets.setdefault(self._pad_size(len(sp)), []).append(j)
+        tb = self.cfg.test_batch
+        launches = []
+        for npad, js in sorted(buckets.items()):
+            # at most ~32 test batches of samples per launch (activation memory of the eval forward)
+            gcap = max(1, (32 * tb) // min(npad, tb))
+            for grp0 in self._groups(js):
+                for grp in [grp0[i:i + gcap] for i in range(0, len(grp0), gcap)]:
+                    top = max(len(splits[j]) for j in grp)  # padded to the group's largest split (equal sizes: none)
+                    for s0 in range(0, top, tb):
+                        launches.append((grp, s0, min(tb, top - s0)))
+        lanes = self._side_streams() if (self.device.type == "cuda" and len(launches) > 2) else None
+        main, used = (torch.cuda.current_stream(), set()) if lanes else (None, None)
+        fork = main.record_event() if lanes else None
+        pending = []
+        for grp, s0, ch in launches:
+            G = len(grp)
+            idx = np.empty((G, ch), dtype=np.int32)
+            valid = np.zeros(G, dtype=np.int64)
+            for k, j in enumerate(grp):
+                seg = np.asarray(splits[j][s0:s0 + ch])
+                valid[k] = len(seg)
+                idx[k, :len(seg)] = seg
+                idx[k, len(seg):] = splits[j][0]
+            st = self._lane(G, ch)[0] if lanes else None
+            if st is not None and st not in used:
+                st.wait_event(fork)
+                used.add(st)
+            with torch.cuda.stream(st) if st is not None else _nullctx():
+                rr = [rows[j] for j in grp]
+                if _contiguous(rr):
+                    th, bu = theta[rr[0]:rr[-1] + 1], bufs[rr[0]:rr[-1] + 1]
+                else:
+                    t = torch.tensor(rr, device=self.device)
+                    th, bu = gather_rows(theta, t), gather_rows(bufs, t)
+                # host->device through pinned buffers, enqueued before the forward: a pageable copy here would
+                # block the host until this launch's forward finished and serialise the launch sequence
+                idx_d = self._upload_i32(idx.reshape(-1))
+                valid_d = self._upload_i32(valid)
+                logits = self.e.eval_logits(th, bu, idx_d, G, ch).view(G, ch, -1)
+                y = self.e.labels.index_select(0, idx_d.long().to(self.e.labels.device)).to(logits.device).float()
+                correct, loss = self._eval_chunk_metrics(logits, y.view(G, ch))
+                valid_d = valid_d.to(logits.device)
+                if int(valid.min()) < ch:
+                    keep = (torch.arange(ch, device=logits.device).view(1, ch) < valid_d.view(G, 1)).float()
+                    correct, loss = correct * keep, loss * keep
+                res = torch.stack([correct.sum(1).double(), loss.sum(1).double(), valid_d.double()], 1)
+            if st is not None:
+                res.record_stream(main)
+            pending.append((grp, res))
+        for st in used or ():
+            main.wait_stream(st)
+        if pending:
+            host = torch.cat([r for _, r in pending], 0).cpu().numpy()
+            o = 0
+            for grp, _ in pending:
+                out[grp] += host[o:o + len(grp)]
+                o += len(grp)
+        return out
+
+    def _eval_grouped_exact(self, theta, bufs, rows, clients, which="test"):
         """Model row rows[j] on client clients[j]'s split: clients with equal split sizes are evaluated in grouped
         launches (G rows x n samples); one device->host copy at the end."""
         out = np.zeros((len(clients), 3), dtype=np.float64)

@@ -423,3 +423,38 @@ def test_balanced_owner_evens_the_sampled_load():
     assert load.max() - load.min() <= max(r.sizes[c] for c in sampled)
     assert all(own[c] == r.owner[c] for c in range(r.N) if c not in sampled)  # only sampled clients move
     assert np.array_equal(own, r.balanced_owner(sampled))                       # deterministic
+
+
+def test_padded_bucket_eval_equals_exact_grouping(monkeypatch):
+    """Ragged test splits evaluated in padded buckets (rows past a client's size repeat its first sample and are masked
+    out; chunks of test_batch across the group) give the same per-client (correct, loss_sum, total) as the exact-size
+    grouping, also for model rows shared by several clients."""
+    from neuroimagedisttraining_amd.engine.executor import ClientSplit, FLConfig, TorchEngine
+    from neuroimagedisttraining_amd.engine.personalized import make_runner
+    from neuroimagedisttraining_amd.parallel import runtime as rt
+    torch.manual_seed(0)
+    g = torch.Generator().manual_seed(9)
+    test_sizes = [3, 9, 17, 5, 30, 70, 9, 1]
+    splits, off = [], 0
+    for t in test_sizes:
+        tr = np.arange(off, off + 6)
+        splits.append(ClientSplit(tr, np.arange(off + 6, off + 6 + t), tr[:3]))
+        off += 6 + t
+    vols = torch.randint(0, 256, (off, 15, 15, 15), dtype=torch.uint8, generator=g)
+    labels = torch.randint(0, 2, (off,), generator=g).float()
+    model = Tiny3D()
+    eng = TorchEngine(model, vols, labels, "cpu")
+    info = rt.DistInfo(0, 1, 0, torch.device("cpu"), "none")
+    r = make_runner("fedavg", eng, splits, FLConfig(comm_round=1, epochs=1, batch_size=4, lr=0.05, seed=7,
+                                                    test_batch=16, group=3), info, model)
+    with torch.no_grad():
+        r.theta[:, :r.P].add_(torch.randn(r.theta.shape[0], r.P) * 0.05)
+    C = len(test_sizes)
+    for rows in (list(range(C)), [0] * C, [C - 1 - j for j in range(C)]):
+        monkeypatch.setenv("NIDT_EVAL_PAD", "1")
+        a = r.eval_grouped(r.theta, r.bufs, rows, list(range(C)))
+        monkeypatch.setenv("NIDT_EVAL_PAD", "0")
+        b = r.eval_grouped(r.theta, r.bufs, rows, list(range(C)))
+        assert np.array_equal(a[:, 2], np.array(test_sizes, dtype=np.float64))
+        assert np.allclose(a, b, rtol=1e-5, atol=1e-5), (a, b)
+    assert [r._pad_size(n) for n in (1, 8, 9, 64, 65, 100, 1000)] == [8, 8, 16, 64, 77, 108, 1024]
