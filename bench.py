@@ -1,7 +1,10 @@
 """Headline benchmark: FL rounds/sec (whole node), 64-client SalientGrads AlexNet3D on ABCD-shape synthetic volumes.
 
-Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N>1 it is launched with
-``torch.distributed.run`` (one rank per GPU, RCCL).  One *step* = one full federated round of the
+Contract (driver): ``python bench.py --gpus N --steps K --warmup W``, one rank per GPU over RCCL.  For N>1 it
+runs either under ``torch.distributed.run`` (the ranks come from RANK / WORLD_SIZE / LOCAL_RANK / MASTER_*, and
+``--gpus`` must equal WORLD_SIZE) or directly: with ``--gpus N > 1`` and no WORLD_SIZE in the environment the
+parent process spawns the N ranks itself (torchrun-style env, 127.0.0.1 rendezvous) BEFORE anything touches the
+GPU, forwards rank 0's JSON line and exits with the first failing rank's code.  One *step* = one full federated round of the
 reference's SalientGrads (``fedml_experiments/standalone/sailentgrads/main_sailentgrads.py`` defaults):
 all 64 clients (frac=1) train 2 local epochs of batch 16 over their 144-sample train split with
 SGD(lr 0.01 * 0.998^round, wd 5e-4) + clip_grad_norm(10) + global SNIP mask (dense_ratio 0.5), then
@@ -39,9 +42,10 @@ NAMES = {"salientgrads": "SalientGrads", "fedavg": "FedAvg", "fedprox": "FedProx
          "subavg": "SubAvg", "ditto": "Ditto", "dpsgd": "D-PSGD", "fedfomo": "FedFomo", "local": "Local"}
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs = ranks (default: WORLD_SIZE under torchrun, else 1); N>1 without torchrun self-launches")
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--clients", type=int, default=64)
@@ -65,11 +69,119 @@ def parse():
     ap.add_argument("--rebalance", type=int, default=0,
                     help="1: move sampled clients (state and samples) between ranks to even the per-round load "
                          "(off by default: no measurement has shown a net gain, profiles/r2_s2_rehearse_2ranks.txt)")
-    return ap.parse_args()
+    ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
+                    help="cpu: launcher/plumbing diagnostic only -- a tiny 3-D CNN on 15^3 volumes on the CPU twin "
+                         "engine with gloo collectives (NOT the headline config)")
+    return ap.parse_args(argv)
 
 
-def main():
-    args = parse()
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def self_launch(n, argv):
+    """Spawn ``n`` ranks of this script (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT, one per GPU).
+
+    Called before any GPU call in this process (``torch.cuda.device_count()`` does not initialise the GPU); the
+    children inherit stdout, so rank 0's JSON line is the only line printed.  When a rank fails the others are
+    terminated (they would otherwise wait in a collective until its timeout).  Returns the exit code."""
+    import signal
+    import subprocess
+    port = os.environ.get("MASTER_PORT") or str(_free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC (RCCL / cross-process tensors)
+        # stdout: rank 0's through a pipe (its JSON line is re-emitted on our stdout, anything else the libraries print
+        # there goes to stderr); the other ranks print nothing on stdout
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env,
+                                      stdout=subprocess.PIPE if r == 0 else sys.stderr, text=True, bufsize=1))
+
+    def forward(pipe):
+        for line in pipe:
+            out = sys.stdout if line.lstrip().startswith("{") else sys.stderr
+            out.write(line)
+            out.flush()
+
+    import threading
+    fwd = threading.Thread(target=forward, args=(procs[0].stdout,), daemon=True)
+    fwd.start()
+    rc = 0
+    try:
+        live = list(procs)
+        while live:
+            time.sleep(0.2)
+            for p in list(live):
+                code = p.poll()
+                if code is None:
+                    continue
+                live.remove(p)
+                if code != 0 and rc == 0:
+                    rc = code if code > 0 else 128 - code
+                    for q in live:
+                        q.send_signal(signal.SIGTERM)
+    finally:
+        deadline = time.time() + 30
+        for p in procs:
+            if p.poll() is None:
+                try:
+                    p.wait(timeout=max(0.1, deadline - time.time()))
+                except subprocess.TimeoutExpired:
+                    p.kill()
+                    p.wait()
+        fwd.join(timeout=10)
+    return rc
+
+
+def _cpu_tiny_setup(args, info):
+    """``--device cpu``: the same runner on the CPU twin engine (a small 3-D CNN, 15^3 uint8 volumes), so the
+    launcher and the gloo collectives can be checked without a GPU."""
+    import numpy as np
+    from torch import nn
+    from neuroimagedisttraining_amd.engine.executor import ClientSplit, TorchEngine
+
+    class Tiny3D(nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.features = nn.Sequential(nn.Conv3d(1, 4, 3, 2), nn.BatchNorm3d(4), nn.ReLU(inplace=True),
+                                          nn.Conv3d(4, 8, 3), nn.BatchNorm3d(8), nn.ReLU(inplace=True))
+            self.classifier = nn.Sequential(nn.Dropout(), nn.Linear(8, 1))
+
+        def forward(self, x):
+            return self.classifier(self.features(x).amax((2, 3, 4)))
+
+    per = args.train_per_client + args.test_per_client
+    g = torch.Generator().manual_seed(args.seed)
+    N = args.clients * per
+    vols = torch.randint(0, 256, (N, 15, 15, 15), dtype=torch.uint8, generator=g)
+    labels = torch.randint(0, 2, (N,), generator=g).float()
+    splits = [ClientSplit(np.arange(c * per, c * per + args.train_per_client),
+                          np.arange(c * per + args.train_per_client, (c + 1) * per)) for c in range(args.clients)]
+    torch.manual_seed(args.seed)
+    model = Tiny3D()
+    return model, TorchEngine(model, vols, labels, "cpu"), splits, [args.train_per_client] * args.clients
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else list(argv)
+    args = parse(argv)
+    world_env = os.environ.get("WORLD_SIZE")
+    if args.gpus is None:
+        args.gpus = int(world_env) if world_env else 1
+    if args.gpus > 1 and world_env is None:
+        if args.device == "cuda" and torch.cuda.device_count() < args.gpus:
+            sys.exit("bench.py: --gpus %d but only %d GPU(s) visible" % (args.gpus, torch.cuda.device_count()))
+        sys.exit(self_launch(args.gpus, argv))
+    run(args)
+
+
+def run(args):
     import numpy as np
     from neuroimagedisttraining_amd.parallel import runtime as rt
     from neuroimagedisttraining_amd.engine.executor import ClientSplit, FLConfig, HipEngine
@@ -77,51 +189,60 @@ def main():
     from neuroimagedisttraining_amd.data.synthetic_fl import build_fl_volumes, skewed_sizes, to_hip_store
     from neuroimagedisttraining_amd.models.alexnet3d import AlexNet3D_Dropout
 
-    info = rt.init_distributed(prefer_gpu=True)
-    assert info.device.type == "cuda", "bench.py needs a GPU"
+    info = rt.init_distributed(prefer_gpu=args.device == "cuda")
+    if info.world != args.gpus:
+        raise SystemExit("bench.py: --gpus %d but WORLD_SIZE=%d ranks" % (args.gpus, info.world))
+    cuda = args.device == "cuda"
+    if cuda:
+        assert info.device.type == "cuda", "bench.py needs a GPU (--device cpu: CPU plumbing diagnostic)"
+    sync = torch.cuda.synchronize if cuda else (lambda: None)
     torch.manual_seed(args.seed)
-    per = args.train_per_client + args.test_per_client
-    tot = skewed_sizes(args.clients, per, args.size_skew, seed=args.seed)
-    n_test = [max(1, int(round(t * args.test_per_client / per))) for t in tot]
-    n_train = [t - e for t, e in zip(tot, n_test)]
-    shards = rt.shard_clients(n_train, info.world)
     rebalance = bool(args.rebalance)
-    local = shards[info.rank]  # data is sharded like the clients (rebalancing moves a client's samples with it)
     t0 = time.perf_counter()
-    vol, labels, splits_local = build_fl_volumes(local, args.clients, n_train, n_test, info.device, seed=args.seed)
-    x8, mom = to_hip_store(vol)
-    del vol
-    nval = None
-    if args.algorithm == "fedfomo":  # validation split: 10 % of client 0's train size (data_val_loader.py:275)
-        nval = int(0.1 * n_train[0])
-        splits_local = {c: ClientSplit(s.train[nval:], s.test, s.train[:nval]) for c, s in splits_local.items()}
-        n_train = [n - nval for n in n_train]
-    torch.cuda.synchronize()
+    if cuda:
+        per = args.train_per_client + args.test_per_client
+        tot = skewed_sizes(args.clients, per, args.size_skew, seed=args.seed)
+        n_test = [max(1, int(round(t * args.test_per_client / per))) for t in tot]
+        n_train = [t - e for t, e in zip(tot, n_test)]
+        shards = rt.shard_clients(n_train, info.world)
+        local = shards[info.rank]  # data is sharded like the clients (rebalancing moves a client's samples with it)
+        vol, labels, splits_local = build_fl_volumes(local, args.clients, n_train, n_test, info.device,
+                                                     seed=args.seed)
+        x8, mom = to_hip_store(vol)
+        del vol
+        nval = None
+        if args.algorithm == "fedfomo":  # validation split: 10 % of client 0's train size (data_val_loader.py:275)
+            nval = int(0.1 * n_train[0])
+            splits_local = {c: ClientSplit(s.train[nval:], s.test, s.train[:nval]) for c, s in splits_local.items()}
+            n_train = [n - nval for n in n_train]
+        # splits indexed by global client id; non-local clients only need their sizes (sampling weights)
+        splits = [splits_local[c] if c in splits_local else
+                  ClientSplit(train=np.zeros(n_train[c], dtype=np.int64), test=np.zeros(n_test[c], dtype=np.int64),
+                              val=None if nval is None else np.zeros(nval, dtype=np.int64))
+                  for c in range(args.clients)]
+        model = AlexNet3D_Dropout(num_classes=1)
+        engine = HipEngine(model, x8, mom, labels, info.device)
+    else:
+        torch.set_num_threads(max(1, (os.cpu_count() or 1) // info.world))  # ranks share the host's cores
+        model, engine, splits, n_train = _cpu_tiny_setup(args, info)
+    sync()
     t_data = time.perf_counter() - t0
-
-    # splits indexed by global client id; non-local clients only need their sizes (sampling weights)
-    splits = [splits_local[c] if c in splits_local else
-              ClientSplit(train=np.zeros(n_train[c], dtype=np.int64), test=np.zeros(n_test[c], dtype=np.int64),
-                          val=None if nval is None else np.zeros(nval, dtype=np.int64))
-              for c in range(args.clients)]
-    model = AlexNet3D_Dropout(num_classes=1)
-    engine = HipEngine(model, x8, mom, labels, info.device)
     cfg = FLConfig(comm_round=args.warmup + args.steps, epochs=args.epochs, batch_size=args.batch,
                    dense_ratio=args.dense_ratio, seed=args.seed, group=args.group, frac=args.frac,
                    frequency_of_the_test=0 if args.no_eval else 1, aggregator=args.aggregator,
                    prox_mu=args.prox_mu if args.algorithm == "fedprox" else 0.0, cs=args.cs, final_round=False,
-                   rebalance=rebalance, step_streams=args.step_streams)
+                   rebalance=rebalance, step_streams=args.step_streams, hip_graphs=cuda)
     runner = make_runner(args.algorithm, engine, splits, cfg, info, model, logger=None)
     t0 = time.perf_counter()
     if runner.alg == "salientgrads":
         runner.generate_global_mask_snip()
-    torch.cuda.synchronize()
+    sync()
     t_snip = time.perf_counter() - t0
     for r in range(args.warmup):
         runner.run_round(r)
-    torch.cuda.synchronize()
+    sync()
     rt.barrier(info)
-    torch.cuda.synchronize()
+    sync()
     for k in runner.timers:
         runner.timers[k] = 0.0
     runner.record_train_events, runner.train_events = True, []
@@ -129,10 +250,10 @@ def main():
     res = None
     for r in range(args.warmup, args.warmup + args.steps):
         res = runner.run_round(r, sync_timers=args.phase_timers)
-    torch.cuda.synchronize()
+    sync()
     t_local = time.perf_counter() - t0   # this rank's own work (before waiting for the slowest rank)
     rt.barrier(info)
-    torch.cuda.synchronize()
+    sync()
     dt = time.perf_counter() - t0
     per_rank = rt.all_gather_cat(torch.tensor([t_local], dtype=torch.float64, device=info.device), info)
     per_rank = [round(float(x), 4) for x in per_rank.cpu()]
@@ -142,10 +263,11 @@ def main():
     per_rank_train = [round(float(x), 4) for x in per_rank_train.cpu()]
     dt = rt.max_over_ranks(dt, info)
     # caching-allocator peak of any rank (every engine buffer, incl. one scratch set per distinct (G, B) launch shape)
-    peak_gib = rt.max_over_ranks(torch.cuda.max_memory_allocated(info.device) / 2 ** 30, info)
+    peak_gib = rt.max_over_ranks(torch.cuda.max_memory_allocated(info.device) / 2 ** 30 if cuda else 0.0,
+                                info)
     ms = dt * 1000.0 / max(1, args.steps)
     value = args.steps / dt
-    headline = (args.algorithm == "salientgrads" and args.clients == 64 and args.aggregator == "fedavg"
+    headline = (cuda and args.algorithm == "salientgrads" and args.clients == 64 and args.aggregator == "fedavg"
                 and args.size_skew == 0 and args.frac == 1.0)
     if info.is_main:
         out = {
@@ -153,7 +275,8 @@ def main():
                        "FL rounds/sec (whole node), %d-client %s%s 3D-CNN on ABCD-shape synth%s"
                        % (args.clients, NAMES[args.algorithm],
                           "" if args.aggregator == "fedavg" else "+" + args.aggregator,
-                          "" if args.size_skew == 0 else " (size skew %.2f)" % args.size_skew)),
+                          "" if args.size_skew == 0 else " (size skew %.2f)" % args.size_skew)
+                       + ("" if cuda else " [CPU plumbing diagnostic: tiny 3-D CNN, 15^3 volumes]")),
             "value": round(value, 4),
             "unit": "rounds/s",
             "n_gpus": info.world,
@@ -164,12 +287,12 @@ def main():
             "scaling": "strong",
             "vs_baseline": (round(value / EAGER_BASELINE_ROUNDS_PER_S, 2) if headline else None),
             "vs_bf16_eager": (round(value / EAGER_BF16_BASELINE_ROUNDS_PER_S, 2) if headline else None),
-            "dtype": "bf16",
+            "dtype": "bf16" if cuda else "fp32",
             "data": "synthetic",
-            "config": {"model": "AlexNet3D_Dropout", "algorithm": NAMES[args.algorithm],
+            "config": {"model": "AlexNet3D_Dropout" if cuda else "Tiny3D (CPU diagnostic)", "algorithm": NAMES[args.algorithm],
                        "aggregator": args.aggregator, "clients": args.clients, "frac": args.frac,
                        "global_batch": args.batch * args.clients, "batch_per_client": args.batch,
-                       "seq_len": None, "input": "1x121x145x121", "epochs": args.epochs,
+                       "seq_len": None, "input": "1x121x145x121" if cuda else "1x15x15x15", "epochs": args.epochs,
                        "train_per_client": args.train_per_client, "test_per_client": args.test_per_client,
                        "size_skew": args.size_skew, "samples_train_total": int(sum(n_train)),
                        "dense_ratio": args.dense_ratio, "eval_every_round": not args.no_eval,
