@@ -19,6 +19,7 @@
 #include <cstdlib>
 
 #include "common.h"
+#include "conv1_wgrad_layout.h"
 
 namespace nidt {
 
@@ -1164,6 +1165,241 @@ __global__ __launch_bounds__(256, 2) void k_conv1_wgrad_dot(const uint8_t* __res
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// k_conv1_wgrad_smf — the same S[c][k] / D[c] slabs on 2:4-sparse MATRIX cores (v_smfmac_f32_32x32x32_bf16).
+//
+// S[c][k] = sum_pos dY[c][pos] X[2 pos + k] over the conv-output positions of the pooled region, with dY = dz at each
+// (cell, channel)'s argmax voxel and 0 elsewhere — an implicit-GEMM weight gradient with M = 64 channels (2 tiles of
+// 32), N = 125 taps (4 tiles of 32, 3 dummy columns), K = the conv positions x of one conv row (57 live, 2 k-steps of
+// 32).  Along x a group of 4 consecutive positions touches at most 2 pooling cells (cells are 3 wide) and a cell has
+// exactly ONE argmax per channel, so each group of 4 K of a channel's dY row holds <= 2 non-zeros: dY is exactly 2:4
+// structured-sparse, and smfmac computes the dense-equivalent product at twice the dense MFMA rate (the 32x32x32
+// smfmac issues at the cycles of the dense 32x32x16: profiles/r4_smfmac_probe.txt).  This replaces the per-(cell,
+// channel) gather on the VALU (k_conv1_wgrad_split: 0 MFMA, ~35 TF/s).
+//
+// Operand layouts (gfx950, measured with tools/probes/smfmac_probe.hip): B lane (n = l % 32, q = l / 32) holds the 16
+// consecutive K = 16 q .. 16 q + 15 of column n; A lane (m = l % 32, p = l / 32) holds 8 compressed values, element j
+// covering the 4-group at K = 16 (j >> 2) + 8 p + 4 ((j >> 1) & 1), its position in that group in bits 2j..2j+1 of
+// the index VGPR (abid 0).  With K = x, tap k = (kd, kh, kw)'s B fragment is 16 consecutive x of the input's phase
+// plane r(k) shifted by jw = kw >> 1.  Misaligned ds_read_b128 are exact on gfx950 but ~11x slower (probe), so the
+// stage holds three shifted copies J = jw of the bf16 phase planes (J = 2 only for rw = 0: 20 planes), laid out by
+// tools/probes/c1wg_layout_gen.py so that no ds_read_b128 lane group has two taps on one bank.
+//
+// A is built in registers: per stage each lane reads, for its 8 slots of each M-tile, the (dz, argmax) record of the
+// slot's cell from LDS and folds "argmax inside this 4-group" into a row key; per conv row a slot is dz if its key is
+// that row, else 0 (the position index word is row-independent).  Block = (sample, pd[, row range]), stage = pooled
+// row ph: wave w runs k-step w & 1 over 5 or 4 of the 9 conv rows (alternating per stage), 8 smfmac per row.  Slabs
+// are reduced across the 4 waves in a fixed order (deterministic), in the VALU kernel's part[slab][64][126] format.
+constexpr int kSmMetaOff = (kC1sBElems * 2 + 15) / 16 * 16;   // byte offset of the record table
+constexpr int kSmBytes = kSmMetaOff + kPW * kC1 * 4;
+static_assert(kSmBytes >= 4 * 32 * 128 * 4 + 4 * 64 * 4, "reduction scratch must fit in the stage buffers");
+
+typedef __bf16 bf16x16 __attribute__((ext_vector_type(16)));
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+
+__global__ __launch_bounds__(256, 2) void k_conv1_wgrad_smf(const uint8_t* __restrict__ x8, const int* __restrict__ idx,
+                                                           const uint16_t* __restrict__ dp,
+                                                           const uint16_t* __restrict__ pout,
+                                                           const uint8_t* __restrict__ amax, float* __restrict__ part,
+                                                           int nq) {
+  __shared__ __attribute__((aligned(16))) uint8_t smem[kSmBytes];
+  uint16_t* bsm = reinterpret_cast<uint16_t*>(smem);                    // the 20 phase-plane copies
+  uint32_t* meta = reinterpret_cast<uint32_t*>(smem + kSmMetaOff);      // [19 cells][64 c]: dz | x << 16 | row << 24
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int q = bid % nq, rest = bid / nq;
+  const int pd = rest % kPD, n = rest / kPD;
+  const int rq = ((kPH + nq - 1) / nq + kWgRows - 1) / kWgRows * kWgRows;
+  const int ph_begin = q * rq, ph_end = min(kPH, ph_begin + rq);
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const uint8_t* xs = x8 + (int64_t)idx[n] * kPZ * kPY * kPX * 8;
+  const int ks = wid & 1;  // this wave's k-step (x 0-31 or 32-63)
+  // B: this lane's column base per N-tile (plane copy J = jw of phase r, rows (jd, jh), x offset 16 q)
+  int bbase[4];
+#pragma unroll
+  for (int T = 0; T < 4; ++T) {
+    int k = kC1sSlotTap[32 * T + (lane & 31)];
+    k = k >= 1000 ? k - 1000 : k;
+    const int kd = k / 25, kh = (k / 5) % 5, kw = k % 5;
+    const int r = ((kd & 1) << 2) | ((kh & 1) << 1) | (kw & 1);
+    bbase[T] = kC1sPlaneBase[kC1sPlaneOf[kw >> 1][r]] + (kd >> 1) * kC1sZS + (kh >> 1) * kC1sRS + 16 * (lane >> 5) + 32 * ks;
+  }
+  // A: this lane's 8 slots (4-groups g = j >> 1 at x = Xg, slot j & 1 = the group's first cell or the next one)
+  const int pl = lane >> 5, ml = lane & 31;
+  int xg[4], mcell[8];
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    xg[g] = 32 * ks + 16 * (g >> 1) + 8 * pl + 4 * (g & 1);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int C = xg[g] / 3 + h;
+      mcell[2 * g + h] = C < kPW ? C * kC1 + ml : -1;
+    }
+  }
+  f32x16 acc[2][4];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int T = 0; T < 4; ++T)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[t][T][i] = 0.f;
+  float Dloc = 0.f;
+  const int rc = tid & 63, rcg = tid >> 6;  // record roles: channel, cell group
+  const int64_t rowbase = ((int64_t)n * kPD + pd) * kPH;
+  // B staging items: (input row zi * 5 + yi, 8-x chunk); the item needs voxels x0 .. x0 + 9
+  const int brow = tid >> 3, bx0 = 8 * (tid & 7);
+  const bool bact = tid < 200;
+  const int bzi = brow / 5, byi = brow - 5 * (brow / 5);
+  for (int ph = ph_begin; ph < ph_end; ++ph) {
+    // (1) global loads: this thread's 10 voxels and 5 records
+    uint2 vx[10];
+#pragma unroll
+    for (int v = 0; v < 10; ++v) {
+      const int x = bx0 + v;
+      vx[v] = make_uint2(0, 0);
+      if (bact && x < kPX)
+        vx[v] = *reinterpret_cast<const uint2*>(xs + (((int64_t)(3 * pd + bzi) * kPY + 3 * ph + byi) * kPX + x) * 8);
+    }
+    uint16_t rp[5], rg[5];
+    uint8_t ra[5];
+    const int64_t obase = (rowbase + ph) * kPW * kC1;
+#pragma unroll
+    for (int u = 0; u < 5; ++u) {
+      const int pw = rcg + 4 * u;
+      rp[u] = 0;
+      rg[u] = 0;
+      ra[u] = 0;
+      if (pw < kPW) {
+        rp[u] = pout[obase + pw * kC1 + rc];
+        rg[u] = dp[obase + pw * kC1 + rc];
+        ra[u] = amax[obase + pw * kC1 + rc];
+      }
+    }
+    __syncthreads();  // the previous stage's LDS reads are done
+    // (2) B planes: per phase r, 10 voxels -> bf16 (exact for uint8), packed for the copies J = 0, 1 (and 2 if rw = 0)
+    if (bact) {
+      const int roff = bzi * kC1sZS + byi * kC1sRS + bx0;
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        float f[10];
+#pragma unroll
+        for (int v = 0; v < 10; ++v) f[v] = u8f(r < 4 ? vx[v].x : vx[v].y, r & 3);
+        const uint32_t e0 = bf2_pack(f[0], f[1]), e1 = bf2_pack(f[2], f[3]), e2 = bf2_pack(f[4], f[5]);
+        const uint32_t e3 = bf2_pack(f[6], f[7]), e4 = bf2_pack(f[8], f[9]);
+        *reinterpret_cast<uint4*>(&bsm[kC1sPlaneBase[kC1sPlaneOf[0][r]] + roff]) = make_uint4(e0, e1, e2, e3);
+        *reinterpret_cast<uint4*>(&bsm[kC1sPlaneBase[kC1sPlaneOf[1][r]] + roff]) =
+            make_uint4(bf2_pack(f[1], f[2]), bf2_pack(f[3], f[4]), bf2_pack(f[5], f[6]), bf2_pack(f[7], f[8]));
+        if ((r & 1) == 0)
+          *reinterpret_cast<uint4*>(&bsm[kC1sPlaneBase[kC1sPlaneOf[2][r]] + roff]) = make_uint4(e1, e2, e3, e4);
+      }
+    }
+    // (3) records: dz (0 where the pooled value is ReLU-dead) | conv x of the argmax << 16 | its conv row << 24
+#pragma unroll
+    for (int u = 0; u < 5; ++u) {
+      const int pw = rcg + 4 * u;
+      const uint16_t dzb = bf16_to_f32(rp[u]) > 0.f ? rg[u] : (uint16_t)0;
+      Dloc += bf16_to_f32(dzb);
+      if (pw < kPW) {
+        const int a = ra[u];
+        const int ad = a / 9, ah = (a / 3) % 3, aw = a % 3;
+        meta[pw * kC1 + rc] = (uint32_t)dzb | ((uint32_t)(3 * pw + aw) << 16) | ((uint32_t)(ad * 3 + ah) << 24);
+      }
+    }
+    __syncthreads();
+    // (4) per-stage A operands of this wave's k-step: per 4-group g the two slots' dz values packed as one bf16 pair
+    // (W) and their conv rows as one-hot bits (row in the low half for slot 0, the high half for slot 1; none when
+    // the argmax falls outside the group); the index word holds each argmax's position in its group
+    uint32_t wv[2][4], oh[2][4], ix[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      ix[t] = 0;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        uint32_t w = 0, o = 0;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int j = 2 * g + h;
+          const uint32_t mw = mcell[j] >= 0 ? meta[mcell[j] + 32 * t] : 0u;
+          const uint32_t d = ((mw >> 16) & 0xffu) - (uint32_t)xg[g];
+          const bool in = d <= 3u && mcell[j] >= 0;
+          w |= (in ? (mw & 0xffffu) : 0u) << (16 * h);
+          o |= (in ? (1u << (mw >> 24)) : 0u) << (16 * h);
+          ix[t] |= (in ? d : 0u) << (2 * j);
+        }
+        wv[t][g] = w;
+        oh[t][g] = o;
+      }
+    }
+    // (5) smfmac over this wave's conv rows (the 5-row half alternates between the two waves of a k-step).  A of
+    // row rr: shifting the one-hot pair left by 15 - rr puts bit rr of each half into that half's sign bit, and a
+    // packed 16-bit arithmetic shift by 15 turns it into a 0xffff / 0 mask per slot (3 VALU per 4-group)
+    const int half = (wid >> 1) ^ ((ph - ph_begin) & 1);
+    const int rr0 = half ? 5 : 0, rr1 = half ? 9 : 5;
+    for (int rr = rr0; rr < rr1; ++rr) {
+      const int roff = (rr / 3) * kC1sZS + (rr % 3) * kC1sRS;
+      bf16x16 bv[4];
+#pragma unroll
+      for (int T = 0; T < 4; ++T) {
+        const uint16_t* bp = &bsm[bbase[T] + roff];
+        const bf16x8 lo = *reinterpret_cast<const bf16x8*>(bp);
+        const bf16x8 hi = *reinterpret_cast<const bf16x8*>(bp + 8);
+        bv[T] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15);
+      }
+      bf16x8 av[2];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        uint32_t w[4];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const s16x2 sh = __builtin_bit_cast(s16x2, oh[t][g] << (15 - rr));
+          const s16x2 m = sh >> (s16x2){15, 15};
+          w[g] = wv[t][g] & __builtin_bit_cast(uint32_t, m);
+        }
+        av[t] = __builtin_bit_cast(bf16x8, make_uint4(w[0], w[1], w[2], w[3]));
+      }
+#pragma unroll
+      for (int T = 0; T < 4; ++T) {
+        acc[0][T] = __builtin_amdgcn_smfmac_f32_32x32x32_bf16(av[0], bv[T], acc[0][T], (int)ix[0], 0, 0);
+        acc[1][T] = __builtin_amdgcn_smfmac_f32_32x32x32_bf16(av[1], bv[T], acc[1][T], (int)ix[1], 0, 0);
+      }
+    }
+  }
+  // (6) fixed-order reduction over the 4 waves, one M-tile (32 channels) at a time, and D over the 4 cell groups
+  float* red = reinterpret_cast<float*>(smem);           // [4 w][32 m][128 slot]
+  float* dred = red + 4 * 32 * 128;                      // [4 cg][64 c]
+  float* op = part + (int64_t)bid_slab(rest, q, nq) * kC1 * 126;
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    __syncthreads();
+#pragma unroll
+    for (int T = 0; T < 4; ++T)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int m = 8 * (i >> 2) + 4 * (lane >> 5) + (i & 3);
+        red[(wid * 32 + m) * 128 + 32 * T + (lane & 31)] = acc[t][T][i];
+      }
+    if (t == 0) dred[rcg * 64 + rc] = Dloc;
+    __syncthreads();
+    for (int e = tid; e < 32 * 126; e += 256) {
+      const int m = e / 126, k = e - 126 * (e / 126);
+      float v;
+      if (k < 125) {
+        const int sl = kC1sTapSlot[k];
+        v = red[(0 * 32 + m) * 128 + sl] + red[(1 * 32 + m) * 128 + sl];
+        v += red[(2 * 32 + m) * 128 + sl] + red[(3 * 32 + m) * 128 + sl];
+      } else {
+        const int c = 32 * t + m;
+        v = dred[0 * 64 + c] + dred[1 * 64 + c] + dred[2 * 64 + c] + dred[3 * 64 + c];
+      }
+      op[(32 * t + m) * 126 + k] = v;
+    }
+  }
+}
+
+// conv1 weight-gradient kernel: 0 = VALU gather (k_conv1_wgrad_split), 1 = 2:4 smfmac (k_conv1_wgrad_smf); -1 = the
+// NIDT_C1WG_SMF environment default
+static int g_c1wg_mode = -1;
+void conv1_wgrad_mode(int mode) { g_c1wg_mode = mode; }
+
 int conv1_wgrad_nq(int NB) { return (int64_t)NB * kPD < 4 * 256 * 4 ? 2 : 1; }
 
 void conv1_wgrad(uintptr_t x8, uintptr_t idx, uintptr_t dp, uintptr_t pout, uintptr_t amax, int NB, int B,
@@ -1187,7 +1423,16 @@ void conv1_wgrad(uintptr_t x8, uintptr_t idx, uintptr_t dp, uintptr_t pout, uint
   hipLaunchKernelGGL(k_conv1_wgrad_split<U>, dim3(kPD * NB * nq), dim3(256), 0, s, ptr<const uint8_t>(x8),          \
                      ptr<const int>(idx), ptr<const uint16_t>(dp), ptr<const uint16_t>(pout), ptr<const uint8_t>(amax), \
                      ptr<float>(part), nq)
-  if (dot)
+  static const int smf_env = [] {
+    const char* e = getenv("NIDT_C1WG_SMF");
+    return e ? atoi(e) : 0;
+  }();
+  const bool smf = g_c1wg_mode >= 0 ? g_c1wg_mode == 1 : smf_env == 1;
+  if (smf)
+    hipLaunchKernelGGL(k_conv1_wgrad_smf, dim3(kPD * NB * nq), dim3(256), 0, s, ptr<const uint8_t>(x8),
+                       ptr<const int>(idx), ptr<const uint16_t>(dp), ptr<const uint16_t>(pout),
+                       ptr<const uint8_t>(amax), ptr<float>(part), nq);
+  else if (dot)
     hipLaunchKernelGGL(k_conv1_wgrad_dot, dim3(kPD * NB * nq), dim3(256), 0, s, ptr<const uint8_t>(x8),
                        ptr<const int>(idx), ptr<const uint16_t>(dp), ptr<const uint16_t>(pout),
                        ptr<const uint8_t>(amax), ptr<float>(part), nq);

@@ -125,6 +125,25 @@ def init_stat_info(class_counts=None):
 class APIBase:
     """Common constructor: unpacks the dataset 8/9-tuple and builds one Client per client."""
 
+    def record_avg_inference_flops(self, w_global, mask_pers=None):
+        """Mean over clients of the sparse-aware inference FLOPs of ``w_global`` (under each client's personal
+        mask when given) — ``subavg_api.py:223-235``; counted with the trainer's forward-hook counter."""
+        tr = self.model_trainer
+        keep = tr.get_model_params()
+        flops = []
+        for c in range(self.args.client_num_in_total):
+            if mask_pers is None:
+                w = w_global
+            else:
+                w = {k: (v * mask_pers[c][k].to(v.device) if k in mask_pers[c] else v) for k, v in w_global.items()}
+            flops.append(tr.count_inference_flops(w))
+            if mask_pers is None:  # the same model for every client
+                flops = flops * self.args.client_num_in_total
+                break
+        tr.set_model_params(keep)
+        self.stat_info["avg_inference_flops"] = float(sum(flops) / len(flops))
+        return self.stat_info["avg_inference_flops"]
+
     def __init__(self, dataset, device, args, model_trainer, logger=None):
         self.logger = logger or log
         self.device = device

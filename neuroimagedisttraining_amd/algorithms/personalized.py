@@ -210,6 +210,7 @@ class SubAvgAPI(APIBase):
                 mask_pers[c] = m
             self.stat_info["round_time_s"].append(time.perf_counter() - t0)
         self.mask_pers, self.w_global = mask_pers, w_global
+        self.record_avg_inference_flops(w_global, mask_pers)  # subavg_api.py:91
         return w_global
 
 
@@ -229,10 +230,12 @@ class DittoAPI(APIBase):
             w_locals = []
             for c in idx:
                 client = self.client_list[c]
+                comm = tr.count_communication_params(w_global)  # ditto/client.py:43-49 (downlink + uplink)
                 tr.set_model_params(w_global)
                 tr.set_id(c)
                 tr.train(client.local_training_data, self.device, a, round_idx)
                 w_locals.append((client.get_sample_number(), tr.get_model_params()))
+                self.stat_info["sum_comm_params"] += int(comm + tr.count_communication_params(w_locals[-1][1]))
                 # personal model: proximal pull towards the round's global model (ditto/my_model_trainer.py:38-68)
                 tr.set_model_params(w_per[c])
                 tr.train(client.local_training_data, self.device, a, round_idx, prox_ref=w_global,
@@ -243,6 +246,7 @@ class DittoAPI(APIBase):
                 self._local_test_on_all_clients(w_per, round_idx, key="person_test_acc")
             self.stat_info["round_time_s"].append(time.perf_counter() - t0)
         self.w_global, self.w_per_mdls = w_global, w_per
+        self.record_avg_inference_flops(w_global)  # ditto_api.py:78
         return w_per
 
 

@@ -22,6 +22,18 @@ from .common import APIBase, model_sparsity
 from . import snip as S
 
 
+def _dataset_tensors(ds):
+    """(inputs, labels) tensors behind a TensorDataset / AugmentedTensorDataset (un-augmented); other datasets
+    fall back to item access."""
+    if hasattr(ds, "tensors"):
+        return ds.tensors[0], ds.tensors[1]
+    if hasattr(ds, "x") and hasattr(ds, "y"):
+        return ds.x, ds.y
+    items = [ds[i] for i in range(len(ds))]
+    return (torch.stack([torch.as_tensor(a) for a, _ in items]),
+            torch.as_tensor(np.asarray([np.asarray(b).reshape(-1)[0] for _, b in items])))
+
+
 class SailentGradsAPI(APIBase):
 
     def generate_global_mask_snip(self):
@@ -60,14 +72,15 @@ class SailentGradsAPI(APIBase):
         if store is not None and hasattr(loader, "indices"):  # ABCD IndexLoader: subject indices into a store
             idx = S.stratified_batch(loader.indices, loader._y, B, rng)
             return store.fetch(torch.from_numpy(idx.astype(np.float32)), device=self.device)
-        # generic DataLoader: stratify over the positions of its dataset
+        # generic DataLoader: stratify over the positions of its dataset.  Labels and images are read from the
+        # dataset's tensors, not through ds[i]: an augmenting dataset would run (and draw RNG for) a crop/flip per
+        # access, shifting later randomness and feeding SNIP an augmented batch the client-batched runner never sees
         ds = loader.dataset
-        ys = np.asarray([float(np.asarray(ds[i][1]).reshape(-1)[0]) for i in range(len(ds))])
+        xt, yt = _dataset_tensors(ds)
+        ys = np.asarray(yt.reshape(len(ds), -1)[:, 0], dtype=np.float64)
         pos = S.stratified_batch(np.arange(len(ds)), ys, B, rng)
-        xs, yl = zip(*(ds[int(i)] for i in pos))
-        x = torch.stack([torch.as_tensor(v) for v in xs]).to(self.device)
-        y = torch.as_tensor(np.asarray([np.asarray(v).reshape(-1)[0] for v in yl])).to(self.device)
-        return x, y
+        ix = torch.as_tensor(np.asarray(pos, dtype=np.int64))
+        return xt[ix].to(self.device), torch.as_tensor(yt)[ix].reshape(len(ix), -1)[:, 0].to(self.device)
 
     def train(self):
         mask = self.generate_global_mask_snip()

@@ -123,10 +123,14 @@ def add_args(parser, algo):
     a("--update_topk", type=float, default=0.0, help="send only the top-k fraction of each client's update")
     a("--group", type=int, default=0)
     a("--checkpoint_dir", type=str, default="")
-    a("--checkpoint_every", type=int, default=1, help="save every N rounds (and after the last round)")
+    a("--checkpoint_every", type=int, default=1,
+      help="save every N rounds (and after the last round); saves are written in the background and become the "
+           "resume point once written, so a crash loses at most N rounds plus the rounds one save takes to write")
     a("--keep_last", type=int, default=2, help="complete checkpoint rounds kept on disk (0 = all)")
     a("--resume", type=int, default=0)
     a("--log_dir", type=str, default="LOG")
+    a("--results_dir", type=str, default="results",
+      help="record_information target: <results_dir>/<dataset>/<identity>.json (+ .npz for large arrays)")
     return parser
 
 
@@ -479,8 +483,24 @@ def run_hip(args, algo, logger):
     if saver is not None:
         saver.close()
     runner.finish()
+    if info.is_main:
+        _record(args, algo, runner.stat_info, logger)
     rt.shutdown(info)
     return runner.stat_info
+
+
+# algorithms whose reference API persists stat_info at the end (subavg_api.py:92, fedfomo_api.py:118, local_api.py:84)
+RECORDED = ("subavg", "fedfomo", "local")
+
+
+def _record(args, algo, stat_info, logger):
+    """``record_information`` without pickle (JSON + npz), into a directory that is created (quirk Q13)."""
+    if algo not in RECORDED:
+        return None
+    from .utils.records import record_information
+    path = record_information(stat_info, args.results_dir, args.dataset, args.identity)
+    logger.info("stat_info recorded to %s", path)
+    return path
 
 
 def run_reference(args, algo, logger, device):
@@ -500,6 +520,7 @@ def run_reference(args, algo, logger, device):
            "local": PZ.LocalAPI}[algo]
     api = cls(dataset, device, args, trainer, logger)
     api.train()
+    _record(args, algo, api.stat_info, logger)
     return api.stat_info
 
 

@@ -111,7 +111,9 @@ def partition_data(y_train, partition, n_clients, alpha, n_cls, rng=None):
 def load_partition_data(dataset, data_dir, partition_method, partition_alpha, client_number, batch_size,
                         logger=None, n_train=None, n_test=None, seed=0, with_val=False, augment=True):
     """``augment``: the reference's train-time RandomCrop(pad 4) + RandomHorizontalFlip on the train loaders of the
-    image datasets (validation and test loaders are never augmented)."""
+    image datasets.  Test loaders are not augmented, as in the reference; validation loaders are not either, which
+    deviates from the reference's FedFomo validation loader (built with ``transform_train``,
+    ``cifar10/data_val_loader.py:248,309``) — see PARITY.md §2.5."""
     logger = logger or log
     aug = NORM.get(dataset) if augment else None
     xtr, ytr, xte, yte, n_cls = _load_arrays(dataset, data_dir, n_train, n_test, seed)

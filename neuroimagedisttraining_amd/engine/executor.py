@@ -117,6 +117,7 @@ class HipEngine:
         self._cid_cache = {}
 
     supports_graphs = True
+    input_shape = (1, 121, 145, 121)   # one sample as the model sees it (FLOP counting)
 
     def train_step(self, theta, bufs, grads, idx, G, B, keep, seed, cids=None, seed_dev=None, bn_train=True):
         y = self.labels.index_select(0, idx.long())
@@ -184,6 +185,11 @@ class TorchEngine:
         self.players = ParamLayout.from_tensors(list(self.model.named_parameters()))
         self.blayers = ParamLayout.from_tensors(list(self.model.named_buffers()))
         self.store, self.labels, self.device, self.loss, self.dtype = store, labels, torch.device(device), loss, dtype
+
+    @property
+    def input_shape(self):
+        shp = tuple(self.store.shape[1:])
+        return (1,) + shp if len(shp) == 3 else shp   # volumes without a channel dim get one (see _batch)
 
     def _views(self, row, layout):
         return {n: row[o:o + layout.numel(i)].view(layout.shapes[i])

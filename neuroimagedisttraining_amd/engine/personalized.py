@@ -136,14 +136,6 @@ class PersonalizedRunner(FLRunner):
             self.log.info({"%s_acc" % tag: acc, "%s_loss" % tag: loss})
         return acc, loss
 
-    def count_nonzero_rows(self, rs, rows):
-        """count_communication_params of whole states (params + buffers) per row (host ints)."""
-        if not rows:
-            return np.zeros(0, dtype=np.int64)
-        ix = torch.tensor(rows, device=self.device)
-        nz = torch.count_nonzero(rs.theta[ix], dim=1) + torch.count_nonzero(rs.bufs[ix], dim=1)
-        return nz.cpu().numpy().astype(np.int64)
-
     def local_masks_from(self, per_client_float):
         """list of N flat float masks [P] (host or device) -> this rank's bit rows [C, W]."""
         m = torch.stack([per_client_float[c].to(self.device) for c in self.local]) if self.C else \
@@ -159,7 +151,13 @@ class PersonalizedRunner(FLRunner):
                 out[lay.offsets[i]:lay.offsets[i] + lay.numel(i)] = named_masks[n].reshape(-1).float().cpu()
         return out
 
+    def end_of_training(self, round_idx, clients):
+        self.flush_round_log(round_idx, clients, comm_lines=False)
+        if self.log is not None or self.device.type != "cuda":
+            self.sync_stats()
+
     def finish(self):
+        self.sync_stats()
         return None
 
     def train(self):
@@ -183,6 +181,7 @@ class LocalRunner(PersonalizedRunner):
         t1 = time.perf_counter()
         self.timers["train"] += t1 - t0
         self.stat_info["sum_training_flops"] += int(self.cfg.epochs * sum(self.sizes[c] for c in sampled))
+        self.end_of_training(round_idx, sampled)
         r = self.eval_local(self.rowset, rows, loc)  # client.train tests right after training (local/client.py)
         acc, _ = self.log_test(r, "person_test_acc")
         self.timers["eval"] += time.perf_counter() - t1
@@ -206,6 +205,10 @@ class DittoRunner(PersonalizedRunner):
     def _row_state(self):
         return super()._row_state() + [("pers.theta", self.pers.theta), ("pers.bufs", self.pers.bufs)]
 
+    def finish(self):
+        self.record_avg_inference_flops()  # ditto_api.py:78: w_global for every client
+        return super().finish()
+
     def run_round(self, round_idx, sync_timers=False):
         t0 = time.perf_counter()
         self._round_start(round_idx)
@@ -219,6 +222,7 @@ class DittoRunner(PersonalizedRunner):
         t1 = time.perf_counter()
         self.aggregate(sampled)
         t2 = time.perf_counter()
+        self.end_of_training(round_idx, sampled)
         self.timers["train"] += t1 - t0
         self.timers["aggregate"] += t2 - t1
         res = None
@@ -281,6 +285,7 @@ class DPSGDRunner(PersonalizedRunner):
         self.timers["train"] += t1 - t0
         self.timers["aggregate"] += t2 - t1
         self.stat_info["sum_training_flops"] += int(self.cfg.epochs * self.sizes.sum())
+        self.end_of_training(round_idx, range(self.N))
         res = self.evaluate(round_idx)
         if round_idx % 100 == 99:  # fine-tune evaluation (dpsgd_api.py:89-101); state is unchanged
             self.finetune_round()
@@ -321,6 +326,7 @@ class FedFomoRunner(PersonalizedRunner):
         rows, loc = self.all_rows()
         self.train_rows(self.rowset, rows, loc, round_idx, self.cfg.epochs)
         self.stat_info["sum_training_flops"] += int(self.cfg.epochs * self.sizes.sum())
+        self.end_of_training(round_idx, range(self.N))
         t1 = time.perf_counter()
         after_train = self.eval_local(self.rowset, rows, loc)
         nei = {c: self.choose(c) for c in range(self.N)}  # same generator sequence on every rank
@@ -488,8 +494,9 @@ class DisPFLRunner(PersonalizedRunner):
             else:
                 self.mspace.select(MK.REGROW_RAND, None, self.mbits, k.to(self.device), cids=loc,
                                    seed=(cfg.seed << 20) + round_idx)
-        upd = self.count_nonzero_rows(RowSet(self.theta - w_old.theta, self.bufs - w_old.bufs), rows)
-        self.stat_info["sum_comm_params"] += int(self.count_nonzero_rows(w_old, rows).sum() + upd.sum())
+        upd = self.state_nonzeros(self.theta - w_old.theta, self.bufs - w_old.bufs, rows)
+        self.add_comm(self.state_nonzeros(w_old.theta, w_old.bufs, rows) + upd, loc)
+        self.end_of_training(round_idx, range(N))
         self.timers["train"] += t1 - t0
         t2 = time.perf_counter()
         acc, _ = self.log_test(after, "old_mask_test_acc")
@@ -547,6 +554,11 @@ class SubAvgRunner(PersonalizedRunner):
         names = self.e.players.names
         self.prune_names = [n for n in names if "weight" in n and "bn" not in n]  # prune_func.py:23
 
+    def finish(self):
+        # subavg_api.py:91: w_global under every client's personal mask (the whole federation, every rank's rows)
+        self.record_avg_inference_flops(self.mbits[:self.C] if self.C else self.mbits[:0])
+        return super().finish()
+
     def _real_prune_rows(self, rs, rows, bits_rows):
         ix = torch.tensor(rows, device=self.device)
         rs.theta[ix, :self.P] = rs.theta[ix, :self.P] * MK.unpack_bits(bits_rows, self.P)
@@ -565,9 +577,9 @@ class SubAvgRunner(PersonalizedRunner):
             self.theta[ix] = self.w_global.unsqueeze(0).expand(len(rows), -1)
             self.bufs[ix] = self.b_global.unsqueeze(0).expand(len(rows), -1)
             self._real_prune_rows(self.rowset, rows, old_bits)  # w_per = real_prune(w_global, mask)
-            nz = self.count_nonzero_rows(self.rowset, rows)
-            dense = nz / float(self.P + self.Q)  # print_pruning over the whole state
-            self.stat_info["sum_comm_params"] += int(nz.sum())
+            nz_dev = self.state_nonzeros(self.theta, self.bufs, rows)
+            dense = nz_dev.cpu().numpy() / float(self.P + self.Q)  # print_pruning over the whole state
+            self.add_comm(nz_dev)
 
             def hook(ep, view, clients):  # fake_prune after the first and the last epoch (the training masks)
                 if ep == 0:
@@ -592,8 +604,9 @@ class SubAvgRunner(PersonalizedRunner):
                     if met[q, 0] / max(1.0, met[q, 2]) > cfg.acc_thresh:
                         self.theta[rows[j], :self.P].copy_(pr.theta[q, :self.P])
                         final_bits[j] = m2[j]
-            self.stat_info["sum_comm_params"] += int(self.count_nonzero_rows(self.rowset, rows).sum())
+            self.add_comm(self.state_nonzeros(self.theta, self.bufs, rows))
         t1 = time.perf_counter()
+        self.end_of_training(round_idx, sampled)
         # masked average with the masks the clients trained with (subavg_api.py:123-139)
         s = torch.zeros(self.P, dtype=torch.float32, device=self.device)
         cnt = torch.zeros(self.P, dtype=torch.float32, device=self.device)

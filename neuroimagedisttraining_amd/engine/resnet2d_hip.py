@@ -668,6 +668,11 @@ class ResNetHipEngine:
     + RandomHorizontalFlip, drawn on device per (step, client, sample) and fused into the input stage."""
     sample_fields = ("x8", "labels")
 
+    @property
+    def input_shape(self):
+        n, h, w, c = self.x8.shape  # NHWC uint8 store
+        return (c, h, w)
+
     def __init__(self, template_model, images_u8, labels, device, hip=None, mean=None, std=None, augment=True):
         self.device = torch.device(device)
         self.players = ParamLayout.from_tensors(list(template_model.named_parameters()))

@@ -537,6 +537,10 @@ class ResNet3DHipEngine:
 
     supports_graphs = False  # launches here are few and large (seconds per step at config-5 shapes)
 
+    @property
+    def input_shape(self):
+        return (1,) + tuple(self.x8.shape[1:])
+
     def __init__(self, template_model, volumes_u8, labels, device, hip=None):
         self.device = torch.device(device)
         self.players = ParamLayout.from_tensors(list(template_model.named_parameters()))

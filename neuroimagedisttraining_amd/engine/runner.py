@@ -127,6 +127,7 @@ class FLRunner:
         self.mask = None              # SalientGrads global mask, float [P]
         self.mask_bits = None         # the same as one shared bit row [1, W]
         self.maskable = maskable_flat_mask(engine.players, snip_maskable_names(template_model)).to(self.device)
+        self.template = template_model   # layer structure for FLOP accounting (its weights are not used)
         self.stat_info = dict(sum_comm_params=0, sum_training_flops=0, global_test_acc=[], person_test_acc=[],
                               global_test_loss=[], person_test_loss=[], round_time=[])
         self.timers = {"train": 0.0, "aggregate": 0.0, "eval": 0.0, "snip": 0.0}
@@ -139,6 +140,15 @@ class FLRunner:
         self._lr_dev = self._seed_dev = None
         self._scratch = None
         self._eval_cache = None
+        # reference training log (``Client Index = c\tEpoch: e\tLoss: l``, ``my_model_trainer.py:234-235``) and the
+        # communication accounting (``count_communication_params``, ``sailentgrads/client.py:82,100``): per-step
+        # losses are summed into a device row buffer inside the (captured) step and snapshotted per epoch, the
+        # non-zero counts are device reductions — nothing syncs the host until a round's lines are logged
+        self.track_loss = logger is not None
+        self._loss_acc = None
+        self._loss_log = {}           # client -> [device tensor of per-epoch mean losses, one per training call]
+        self._comm_log = {}           # client -> device scalar (downlink + uplink non-zeros of this round)
+        self._comm_dev = None         # device int64 sum of every counted client (this rank)
 
     # ---------------------------------------------------------------------------------------------- helpers
     def _rng(self, *key):
@@ -278,6 +288,10 @@ class FLRunner:
             self._seed_dev = torch.zeros(1, dtype=torch.int64, device=self.device)
         self._lr_dev.fill_(lr)
         side = self._side_streams() if use_graphs else None
+        k = len(clients)
+        sums = [] if self.track_loss else None
+        if sums is not None:
+            self._loss_rows(k)[:k].zero_()
         for ep in range(epochs):
             plan, idx = self._plan(clients, self._epoch_chunks(round_idx, tag, ep))
             main, cur, lanes_used = torch.cuda.current_stream() if side else None, -1, set()
@@ -307,8 +321,18 @@ class FLRunner:
             for st in lanes_used:
                 main.wait_stream(st)
             self.concurrent_steps = getattr(self, "concurrent_steps", 0) + len(lanes_used)
+            if sums is not None:
+                sums.append(self._loss_acc[:k].clone())
+                self._loss_acc[:k].zero_()
             if epoch_hook is not None:
                 epoch_hook(ep, view, clients)
+        if sums:
+            B = cfg.batch_size
+            nb = torch.tensor([max(1, -(-len(self.splits[c].train) // B)) for c in clients], dtype=torch.float32,
+                              device=self.device)
+            means = torch.stack(sums, 1) / nb.view(-1, 1)   # mean batch loss per (client, epoch), as logged
+            for j, c in enumerate(clients):
+                self._loss_log.setdefault(int(c), []).append(means[j])
 
     def _side_streams(self):
         if self.cfg.step_streams <= 1:
@@ -317,6 +341,106 @@ class FLRunner:
             self._streams = [torch.cuda.Stream(device=self.device) for _ in range(self.cfg.step_streams)]
             self._lane_seed = [torch.zeros(1, dtype=torch.int64, device=self.device) for _ in self._streams]
         return self._streams
+
+    def _loss_rows(self, k):
+        """Device accumulator of the per-client training-loss sums of the current epoch (row = position in the
+        trained client list).  Captured steps add into it, so growing it drops the captured steps."""
+        if self._loss_acc is None or self._loss_acc.shape[0] < k:
+            self._loss_acc = torch.zeros(max(k, self.C, 1), dtype=torch.float32, device=self.device)
+            self._graphs = {}
+        return self._loss_acc
+
+    # ---------------------------------------------------------------------------------------------- statistics
+    def state_nonzeros(self, theta, bufs, rows):
+        """``count_communication_params`` of whole states (every state_dict entry: params and buffers) per row, as
+        a device int64 tensor."""
+        if not rows:
+            return torch.zeros(0, dtype=torch.int64, device=self.device)
+        if _contiguous(rows):
+            th, bu = theta[rows[0]:rows[-1] + 1, :self.P], bufs[rows[0]:rows[-1] + 1, :self.Q]
+        else:
+            ix = torch.tensor(rows, device=self.device)
+            th, bu = theta.index_select(0, ix)[:, :self.P], bufs.index_select(0, ix)[:, :self.Q]
+        return torch.count_nonzero(th, dim=1) + torch.count_nonzero(bu, dim=1)
+
+    def add_comm(self, per_client, clients=None):
+        """Add communication counts (device int64 per client, or a host int) to ``sum_comm_params`` — kept on
+        device and summed over ranks when the statistics are read (:meth:`sync_stats`)."""
+        if self._comm_dev is None:
+            self._comm_dev = torch.zeros((), dtype=torch.int64, device=self.device)
+        if torch.is_tensor(per_client):
+            self._comm_dev += per_client.sum().to(torch.int64)
+            if clients is not None and self.log is not None:
+                for j, c in enumerate(clients):
+                    self._comm_log[int(c)] = per_client[j]
+        else:
+            self._comm_dev += int(per_client)
+
+    def sync_stats(self):
+        """Fold the device-side counters into ``stat_info`` (a collective on multi-rank runs: every rank calls it
+        at the same points — the end of a logged round, ``finish``, checkpoints)."""
+        if self._comm_dev is None:
+            self._comm_dev = torch.zeros((), dtype=torch.int64, device=self.device)
+        t = self._comm_dev.view(1).clone()
+        rt.all_reduce_buckets(t, self.info)
+        self.stat_info["sum_comm_params"] += int(t.item())
+        self._comm_dev.zero_()
+        return self.stat_info
+
+    def record_avg_inference_flops(self, mask_bits=None):
+        """``stat_info["avg_inference_flops"]``: mean over ALL clients of the sparse-aware inference FLOPs of
+        ``w_global`` under each client's personal mask (``mask_bits`` [C, W] of this rank's clients; collective) or
+        of ``w_global`` alone (``subavg_api.py:223-235``, ``ditto/ditto_api.py:78,153``)."""
+        from ..utils.records import flop_coefficients, sparse_inference_flops
+        coef = flop_coefficients(self.template, input_shape=getattr(self.e, "input_shape", None))
+        lay = self.e.players
+        if mask_bits is None:  # every client runs w_global
+            avg = float(sparse_inference_flops(coef, lay, self.w_global.view(1, -1))[0])
+        else:
+            tot = torch.zeros(1, dtype=torch.float64, device=self.device)
+            for j in range(self.C):  # one client row at a time: [P] temporaries only
+                row = self.w_global.view(1, -1) * MK.unpack_bits(mask_bits[j:j + 1], self.P)
+                tot += sparse_inference_flops(coef, lay, row)
+            rt.all_reduce_buckets(tot, self.info)
+            avg = float(tot.item()) / self.N
+        self.stat_info["avg_inference_flops"] = avg
+        return avg
+
+    def flush_round_log(self, round_idx, clients, comm_lines=True):
+        """Emit the reference's per-client training lines for this round (rank 0, reference order):
+        ``@@@@@@@@@@@@@@@@ Training Client CM(r): c``, ``Client Index = c\tEpoch: e\tLoss: l`` per epoch and
+        ``communication parameters for search n`` (``sailentgrads_api.py:127``, ``my_model_trainer.py:234``,
+        ``client.py:101``).  No-op without a logger; one device->host copy (and one gather on multi-rank runs)."""
+        if self.log is None:
+            self._loss_log, self._comm_log = {}, {}
+            return
+        recs = []
+        for c in sorted(self._loss_log):
+            ls = torch.cat([v.view(-1) for v in self._loss_log[c]]).double()
+            cm = self._comm_log.get(c)
+            cm = cm.double().view(1) if cm is not None else torch.full((1,), -1.0, dtype=torch.float64,
+                                                                      device=self.device)
+            recs.append(torch.cat([torch.tensor([float(c), float(ls.numel())], dtype=torch.float64,
+                                                device=self.device), ls, cm]))
+        flat = torch.cat(recs) if recs else torch.zeros(0, dtype=torch.float64, device=self.device)
+        flat = rt.all_gather_cat(flat, self.info).cpu().numpy()
+        self._loss_log, self._comm_log = {}, {}
+        if not self.info.is_main:
+            return
+        per, o = {}, 0
+        while o < flat.size:
+            c, n = int(flat[o]), int(flat[o + 1])
+            per[c] = (flat[o + 2:o + 2 + n], flat[o + 2 + n])
+            o += 3 + n
+        for c in clients:
+            if int(c) not in per:
+                continue
+            losses, cm = per[int(c)]
+            self.log.info("@@@@@@@@@@@@@@@@ Training Client CM({}): {}".format(round_idx, int(c)))
+            for e, l in enumerate(losses):
+                self.log.info("Client Index = {}\tEpoch: {}\tLoss: {:.6f}".format(int(c), e, float(l)))
+            if comm_lines and cm >= 0:
+                self.log.info("communication parameters for search {}".format(int(cm)))
 
     def _lane(self, G, B):
         """Side stream (+ its own dropout-seed scalar) of a partial-batch launch shape.
@@ -336,8 +460,10 @@ class FLRunner:
         cfg = self.cfg
         gr = self.grads[r0:r0 + G]
         mo = self.mom_buf[r0:r0 + G] if self.mom_buf is not None else None
-        self.e.train_step(sub.theta, sub.bufs, gr, idx, G, B, cfg.dropout_keep, cfg.seed << 40, cids=cids,
-                          seed_dev=self._seed_dev if seed_dev is None else seed_dev)
+        loss = self.e.train_step(sub.theta, sub.bufs, gr, idx, G, B, cfg.dropout_keep, cfg.seed << 40, cids=cids,
+                                 seed_dev=self._seed_dev if seed_dev is None else seed_dev)
+        if self.track_loss and self._loss_acc is not None and loss is not None:
+            self._loss_acc[r0:r0 + G].add_(loss.view(-1).float())
         self.e.local_opt(sub.theta, gr, mo, spec, lr, cfg.wd, cfg.momentum, cfg.max_norm,
                          lr_dev=self._lr_dev if lr_dev is None else lr_dev)
 
@@ -624,8 +750,11 @@ class FLRunner:
             ix = torch.tensor(rows, device=self.device)
             self.theta[ix] = self.w_global.unsqueeze(0).expand(len(rows), -1)
             self.bufs[ix] = self.b_global.unsqueeze(0).expand(len(rows), -1)
+        # downlink: count_communication_params(w_global) per sampled client (the same state for all of them)
+        down = torch.count_nonzero(self.w_global) + torch.count_nonzero(self.b_global)
         self.train_rows(RowSet(self.theta, self.bufs), rows, loc, round_idx, self.cfg.epochs, self._fedavg_spec(),
                         lr=lr)
+        self.add_comm(down + self.state_nonzeros(self.theta, self.bufs, rows), loc)  # + uplink (the local model)
 
     def aggregate(self, sampled):
         if self.cfg.aggregator != "fedavg":
@@ -1051,6 +1180,7 @@ class FLRunner:
         self.timers["train"] += t1 - t0
         self.timers["aggregate"] += t2 - t1
         self.stat_info["sum_training_flops"] += int(self.cfg.epochs * sum(self.sizes[c] for c in sampled))
+        self.end_of_training(round_idx, sampled)
         res = None
         if self._eval_due(round_idx):
             res = self.evaluate(round_idx)
@@ -1058,6 +1188,14 @@ class FLRunner:
                 self._sync()
         self.stat_info["round_time"].append(time.perf_counter() - t0)
         return res
+
+    def end_of_training(self, round_idx, clients):
+        """Round bookkeeping after local training: the reference's per-client log lines and, when logging (or on
+        the CPU), ``sum_comm_params`` folded into ``stat_info``.  Timed GPU runs without a logger never sync here;
+        their counts are folded in by :meth:`finish` / :meth:`sync_stats`."""
+        self.flush_round_log(round_idx, clients, comm_lines=self.alg in ("salientgrads", "fedavg"))
+        if self.log is not None or self.device.type != "cuda":
+            self.sync_stats()
 
     def finetune_round(self):
         """FedAvg's final "fine-tune" pass (``fedavg_api.py:78-88``): every client trains one more local round from
@@ -1070,6 +1208,7 @@ class FLRunner:
         fin.theta.copy_(self.w_global.expand(self.C, -1))
         fin.bufs.copy_(self.b_global.expand(self.C, -1))
         self.train_rows(fin, rows, loc, -1, self.cfg.epochs, self._fedavg_spec(), tag=3)
+        self.flush_round_log(-1, loc, comm_lines=False)
         return self.evaluate(-1, fin.theta, fin.bufs)
 
     def train(self):
@@ -1083,6 +1222,7 @@ class FLRunner:
     def finish(self):
         """Reference round tail: SalientGrads re-evaluates (``sailentgrads_api.py:147``), FedAvg fine-tunes every
         client once more and evaluates (``fedavg_api.py:78-88``)."""
+        self.sync_stats()
         if not self.cfg.final_round:
             return None
         if self.alg == "salientgrads":

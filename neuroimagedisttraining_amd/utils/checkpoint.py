@@ -62,7 +62,7 @@ def _runner_state(runner):
     st = {}
     if hasattr(runner, "np_rng"):
         kind, keys, pos, has_gauss, cached = runner.np_rng.get_state()
-        st["np_rng_keys"] = torch.from_numpy(keys.astype(np.int64))
+        st["np_rng_keys"] = torch.from_numpy(np.array(keys, dtype=np.int64, copy=True))
         st["np_rng_meta"] = torch.tensor([pos, has_gauss], dtype=torch.int64)
         st["np_rng_cached"] = torch.tensor([cached], dtype=torch.float64)
     if hasattr(runner, "py_rng"):
@@ -72,8 +72,8 @@ def _runner_state(runner):
         if g is not None:
             st["py_rng_gauss"] = torch.tensor([g], dtype=torch.float64)
     for k in ("weights_locals", "p_choose", "dist_locals"):
-        if hasattr(runner, k):
-            st[k] = torch.from_numpy(np.asarray(getattr(runner, k), dtype=np.float64))
+        if hasattr(runner, k):  # a COPY: the writer thread may serialise it after the next round changed it in place
+            st[k] = torch.from_numpy(np.array(getattr(runner, k), dtype=np.float64, copy=True))
     return st
 
 
@@ -124,6 +124,8 @@ class Checkpointer:
 
     def _snapshot(self, runner, next_round):
         info = self.info
+        if hasattr(runner, "sync_stats"):
+            runner.sync_stats()  # device-side counters (sum_comm_params) into stat_info: collective, every rank
         C = runner.C
         shard = {"next_round": torch.tensor(next_round), "world": torch.tensor(info.world),
                  "rank": torch.tensor(info.rank), "ids": torch.tensor([int(c) for c in runner.local], dtype=torch.int64),
@@ -165,8 +167,21 @@ class Checkpointer:
             return
         next_round, fut = self._pending
         self._pending = None
+        err = None
         if fut is not None:
-            fut.result()
+            try:
+                fut.result()
+            except Exception as e:  # noqa: BLE001 - re-raised below on every rank together
+                err = e
+        # every rank learns whether every writer succeeded (a failed rank must not leave the others waiting in the
+        # barrier until the collective timeout), then all raise together
+        ok = torch.tensor([0.0 if err is not None else 1.0], dtype=torch.float64, device=self.info.device)
+        if self.info.enabled:
+            import torch.distributed as dist
+            dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        if float(ok.item()) < 1.0:
+            raise RuntimeError("checkpoint of round %d failed on %s" % (next_round, "this rank: %r" % (err,)
+                                                                          if err is not None else "another rank"))
         rt.barrier(self.info)
         if self.info.is_main:
             with open(os.path.join(self.dir, "latest.tmp"), "w") as f:
@@ -202,8 +217,19 @@ class Checkpointer:
             self._commit()
 
     def maybe_save(self, runner, next_round, last=False):
+        """Called after every round.  Besides saving every ``every``-th round it commits a background save whose
+        file writes finished (``latest`` advances then, not only at the next save: a crash loses at most ``every``
+        rounds plus the rounds a save takes to write).  The readiness test is agreed on by all ranks (collective)."""
         if (self.every > 0 and next_round % self.every == 0) or last:
             self.save(runner, next_round)
+        elif self._pending is not None:
+            done = self._pending[1] is None or self._pending[1].done()
+            flag = torch.tensor([1.0 if done else 0.0], dtype=torch.float64, device=self.info.device)
+            if self.info.enabled:
+                import torch.distributed as dist
+                dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+            if float(flag.item()) == 1.0:
+                self._commit()
 
     def close(self):
         """Commit any pending save (collective)."""
@@ -228,6 +254,9 @@ def load_runner(runner, directory):
         raise FileNotFoundError("no complete checkpoint in %s" % directory)
     rdir = os.path.join(directory, "round_%d" % r)
     g = torch.load(os.path.join(rdir, "global.pt"), map_location="cpu", weights_only=True)
+    if "index" not in g or "world" not in g:  # the earlier per-client-dict layout (no client index)
+        raise ValueError("checkpoint %s uses an unsupported (pre-index) format: it has no client index; re-run from "
+                         "scratch or convert it with the version that wrote it" % rdir)
     runner.w_global.copy_(g["w_global"].to(runner.device))
     runner.b_global.copy_(g["b_global"].to(runner.device))
     if g["mask"] is not None:
@@ -240,6 +269,8 @@ def load_runner(runner, directory):
     mats = _row_mats(runner)
     for s in shards:
         shard = torch.load(os.path.join(rdir, "clients_rank%d.pt" % s), map_location="cpu", weights_only=True)
+        if "ids" not in shard or "mats" not in shard:
+            raise ValueError("checkpoint shard %s uses an unsupported (pre-index) format" % rdir)
         if int(shard["next_round"]) != r or int(shard["world"]) != world or int(shard["rank"]) != s:
             raise ValueError("checkpoint shard %d of %s belongs to another save" % (s, rdir))
         ids = shard["ids"].tolist()

@@ -606,6 +606,45 @@ def test_conv1_fused_fwd_and_sparse_wgrad(signed):
         assert e_w < 2e-2 and e_g < 2e-2 and e_b < 2e-2, (e_w, e_g, e_b)
 
 
+@pytest.mark.parametrize("NB,B", [(4, 2), (256, 16)])  # nq = 2 row ranges per slab (few samples) and nq = 1
+def test_conv1_wgrad_smfmac_matches_valu_gather(NB, B):
+    """The 2:4-sparse matrix-core conv1 weight gradient (k_conv1_wgrad_smf) writes the same S / D slabs as the VALU
+    gather (k_conv1_wgrad_split) on random inputs: every argmax offset, ReLU-dead cells, signed bf16 gradients."""
+    m = _m()
+    g = torch.Generator(device=DEV).manual_seed(3)
+    x8 = torch.randint(0, 256, (NB, 61, 73, 61, 8), dtype=torch.uint8, device=DEV, generator=g)
+    idx = torch.randperm(NB, device=DEV, generator=g).int()
+    shp = (NB, 19, 23, 19, 64)
+    dp = torch.randn(shp, device=DEV, generator=g).bfloat16()
+    pout = torch.randn(shp, device=DEV, generator=g).bfloat16()           # ~half the cells ReLU-dead
+    amax = torch.randint(0, 27, shp, dtype=torch.uint8, device=DEV, generator=g)
+    G = NB // B
+    nq = m.conv1_wgrad_nq(NB)
+    parts, grads = [], []
+    P = 8000 + 64 * 4
+    for mode in (0, 1):
+        part = torch.full((NB * 19 * nq, 64, 126), float("nan"), device=DEV)
+        grad = torch.zeros(G, P, device=DEV)
+        theta = torch.ones(G, P, device=DEV)
+        w125 = torch.randn(G, 64, 125, device=DEV, generator=g) * 0 + 0.01
+        mu = torch.full((G, 125), 100.0, device=DEV)
+        covw = torch.full((G, 64, 125), 0.5, device=DEV)
+        inv = torch.full((G, 64), 2.0, device=DEV)
+        m.conv1_wgrad_mode(mode)
+        m.conv1_wgrad(x8.data_ptr(), idx.data_ptr(), dp.data_ptr(), pout.data_ptr(), amax.data_ptr(), NB, B,
+                      part.data_ptr(), w125.data_ptr(), mu.data_ptr(), covw.data_ptr(), inv.data_ptr(), theta.data_ptr(),
+                      P, 8000, grad.data_ptr(), P, 0, 8000 + 64, 8000 + 128, 8000 + 192, 1.0 / 255.0, 0, _st())
+        torch.cuda.synchronize()
+        parts.append(part)
+        grads.append(grad)
+    m.conv1_wgrad_mode(-1)
+    assert torch.isfinite(parts[1]).all()
+    # the slabs: fp32 sums of bf16 x uint8 products in two different orders
+    assert _relerr(parts[1], parts[0]) < 1e-5, _relerr(parts[1], parts[0])
+    assert float((parts[1] - parts[0]).abs().max()) <= 1e-4 * float(parts[0].abs().max())
+    assert _relerr(grads[1], grads[0]) < 1e-5
+
+
 @pytest.mark.parametrize("signed", [False, True])
 def test_alexnet_eval_matches_reference(signed):
     from neuroimagedisttraining_amd.engine.alexnet_hip import HipAlexNet3D

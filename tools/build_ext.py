@@ -41,7 +41,7 @@ def _compile(src, obj, extra):
 def build(force=False, verbose=True):
     os.makedirs(BUILD, exist_ok=True)
     inc = _includes()
-    common_m = os.path.getmtime(os.path.join(KDIR, "common.h"))
+    common_m = max(os.path.getmtime(os.path.join(KDIR, f)) for f in os.listdir(KDIR) if f.endswith(".h"))
     srcs = sorted(os.path.join(KDIR, f) for f in os.listdir(KDIR) if f.endswith(".hip"))
     srcs.append(os.path.join(ROOT, "csrc", "bindings.cpp"))
     jobs = []
