@@ -412,13 +412,18 @@ __global__ __launch_bounds__(256, OCC) void k_conv1_fwd_pool_pipe(const uint8_t*
                                                                 const uint16_t* __restrict__ w8,
                                                                 const float* __restrict__ scale,
                                                                 const float* __restrict__ shift, int B,
-                                                                uint16_t* __restrict__ out, uint8_t* __restrict__ amax) {
+                                                                uint16_t* __restrict__ out, uint8_t* __restrict__ amax,
+                                                                int nq) {
   constexpr int HX = 64;
   constexpr int HALO = 5 * 5 * HX * 8;  // f16 elements per buffer
   constexpr int NLD = (5 * 5 * HX + 255) / 256;  // 7 halo voxels per thread
   __shared__ __attribute__((aligned(16))) uint16_t halo[2 * HALO];
-  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  // block = (sample n, pd slab, row range q of nq): few clients per GPU split the 23 pooled rows of a slab over
+  // nq blocks (more, shorter blocks: a wider grid and a shorter tail of the last wave)
+  const int bid0 = xcd_remap(blockIdx.x, gridDim.x);
+  const int q = bid0 % nq, bid = bid0 / nq;
   const int pd = bid % kPD, n = bid / kPD;
+  const int ph_lo = (kPH * q) / nq, ph_hi = (kPH * (q + 1)) / nq;
   const int g = n / B;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const uint8_t* xs = x8 + (int64_t)idx[n] * kPZ * kPY * kPX * 8;
@@ -436,7 +441,7 @@ __global__ __launch_bounds__(256, OCC) void k_conv1_fwd_pool_pipe(const uint8_t*
     const int e_ = tid + 256 * u_;                                                                            \
     if (e_ < 5 * 5 * HX) *reinterpret_cast<uint4*>(&halo[(BUF) * HALO + e_ * 8]) = u8x8_to_f16magic(pre[u_]); \
   }
-  C1_LOAD(0)
+  C1_LOAD(ph_lo)
   const int fr = lane & 15, fq = lane >> 4;
   const int ch = wid & 1, op = wid >> 1;
   constexpr int KW = KS * 32;  // packed slots per channel row
@@ -511,9 +516,9 @@ __global__ __launch_bounds__(256, OCC) void k_conv1_fwd_pool_pipe(const uint8_t*
   const int wloc = fr / 3, dw = fr - 3 * wloc;
   C1_STORE(0)
   __syncthreads();
-  for (int ph = 0; ph < kPH; ++ph) {
-    const int cur = ph & 1;
-    if (ph + 1 < kPH) C1_LOAD(ph + 1)
+  for (int ph = ph_lo; ph < ph_hi; ++ph) {
+    const int cur = (ph - ph_lo) & 1;
+    if (ph + 1 < ph_hi) C1_LOAD(ph + 1)
     const uint16_t* hb = halo + cur * HALO;
     float best[2][2][4], pend[2][2][4];
 #pragma unroll
@@ -602,7 +607,7 @@ __global__ __launch_bounds__(256, OCC) void k_conv1_fwd_pool_pipe(const uint8_t*
         }
       }
     }
-    if (ph + 1 < kPH) C1_STORE(cur ^ 1)
+    if (ph + 1 < ph_hi) C1_STORE(cur ^ 1)
     __syncthreads();
   }
 #undef C1_LOAD
@@ -621,15 +626,21 @@ void conv1_fwd_pool(uintptr_t x8, uintptr_t idx, uintptr_t w8, uintptr_t scale, 
     const char* e = getenv("NIDT_C1_OCC");
     return e ? atoi(e) : 2;
   }();
+  // pooled-row split per slab: NIDT_C1_NQ (A/B), default 1
+  static const int nq_env = [] {
+    const char* e = getenv("NIDT_C1_NQ");
+    return e ? std::max(1, std::min(kPH, atoi(e))) : 1;
+  }();
+  const int nq = nq_env;
 #define NIDT_C1(PF, KSS)                                                                                       \
   if (occ == 3 && (PF) == 2 && (KSS) == 4)                                                                     \
-    hipLaunchKernelGGL((k_conv1_fwd_pool_pipe<2, 4, 3>), dim3(kPD * NB), dim3(256), 0, as_stream(stream),          \
+    hipLaunchKernelGGL((k_conv1_fwd_pool_pipe<2, 4, 3>), dim3(kPD * NB * nq), dim3(256), 0, as_stream(stream),     \
                        ptr<const uint8_t>(x8), ptr<const int>(idx), ptr<const uint16_t>(w8), ptr<const float>(scale), \
-                       ptr<const float>(shift), B, ptr<uint16_t>(out), ptr<uint8_t>(amax));                          \
+                       ptr<const float>(shift), B, ptr<uint16_t>(out), ptr<uint8_t>(amax), nq);                      \
   else                                                                                                         \
-  hipLaunchKernelGGL((k_conv1_fwd_pool_pipe<PF, KSS>), dim3(kPD * NB), dim3(256), 0, as_stream(stream),           \
+  hipLaunchKernelGGL((k_conv1_fwd_pool_pipe<PF, KSS>), dim3(kPD * NB * nq), dim3(256), 0, as_stream(stream),      \
                      ptr<const uint8_t>(x8), ptr<const int>(idx), ptr<const uint16_t>(w8), ptr<const float>(scale),  \
-                     ptr<const float>(shift), B, ptr<uint16_t>(out), ptr<uint8_t>(amax))
+                     ptr<const float>(shift), B, ptr<uint16_t>(out), ptr<uint8_t>(amax), nq)
   // the three dd rows of the 3^3 window unrolled: each row's pooling epilogue overlaps the next row's MFMAs and the
   // body needs 208 instead of 248 VGPRs (4.30 -> 4.17 ms per 64-client step, profiles/r3_ab_conv1_fwd_ddu.txt);
   // NIDT_C1_DDU=1 keeps the rolled loop (A/B)
@@ -638,9 +649,9 @@ void conv1_fwd_pool(uintptr_t x8, uintptr_t idx, uintptr_t w8, uintptr_t scale, 
     return e ? atoi(e) : 3;
   }();
   if (conv1_kslots() == 128 && ddu == 3 && pf == 2 && occ != 3) {
-    hipLaunchKernelGGL((k_conv1_fwd_pool_pipe<2, 4, 2, 3>), dim3(kPD * NB), dim3(256), 0, as_stream(stream),
+    hipLaunchKernelGGL((k_conv1_fwd_pool_pipe<2, 4, 2, 3>), dim3(kPD * NB * nq), dim3(256), 0, as_stream(stream),
                        ptr<const uint8_t>(x8), ptr<const int>(idx), ptr<const uint16_t>(w8), ptr<const float>(scale),
-                       ptr<const float>(shift), B, ptr<uint16_t>(out), ptr<uint8_t>(amax));
+                       ptr<const float>(shift), B, ptr<uint16_t>(out), ptr<uint8_t>(amax), nq);
   } else if (conv1_kslots() == 128) {
     if (pf == 1) NIDT_C1(1, 4); else if (pf == 3) NIDT_C1(3, 4); else NIDT_C1(2, 4);
   } else {

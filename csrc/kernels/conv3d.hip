@@ -2405,6 +2405,11 @@ static int wt_nch(int Cout) {
 
 // split factor of k_conv_wgrad_tri: the wgrad cost model over its own tiles (9 x Cin/64 triplets x co blocks x G)
 int conv3d_wgrad_tri_nsplit(int G, int B, int D, int H, int W, int Cin, int Cout, int pad) {
+  static const int ns_env = [] {  // NIDT_WG_TRI_NS=<n>: force the split of the unpadded (conv2) launch (A/B)
+    const char* e = getenv("NIDT_WG_TRI_NS");
+    return e ? atoi(e) : 0;
+  }();
+  if (ns_env > 0 && pad == 0) return ns_env;
   const int Mg = B * conv_out_n(D, pad) * conv_out_n(H, pad) * conv_out_n(W, pad);
   const int nch = wt_nch(Cout);
   // step cost ~1 us per block slot, no fixed term (128-channel blocks at 64 clients, conv2: ns 4 / 6 / 8 / 12 ->

@@ -787,31 +787,37 @@ class FLRunner:
         rows, loc = self._local_rows(sampled)
         rec = torch.zeros((len(rows), 1 + 2 * k), dtype=torch.float32, device=self.device)
         space = self._topk_space()
+        # per-row client ids and FedAvg weights: one pinned non-blocking upload (no host sync in the loop below)
+        meta = torch.tensor([[float(self.local[r]), self.sizes[self.local[r]] / n_tot] for r in rows],
+                            dtype=torch.float32).view(-1, 2)
+        meta = (meta.pin_memory().to(self.device, non_blocking=True) if self.device.type == "cuda" else meta)
         # chunks bound the [rows, P] temporaries: 8 x 46 M fp32 = 1.5 GB for the 3D ResNet-50
         chunk = max(1, min(len(rows), int(2e9 // (4 * max(1, self.P)))))
         for j0 in range(0, len(rows), chunk):
             rr = rows[j0:j0 + chunk]
-            ix = torch.tensor(rr, device=self.device)
-            d = padded_rows(len(rr), self.P, self.device)
-            torch.sub(self.theta.index_select(0, ix)[:, :self.P], self.w_global, out=d)
-            bits = torch.zeros((len(rr), self.W), dtype=torch.int32, device=self.device)
-            space.select(MK.REGROW_ABS, d, bits, torch.full((len(rr), 1), k, dtype=torch.int64))
-            top = MK.unpack_bits(bits, self.P, torch.bool).nonzero()[:, 1].view(len(rr), k)  # exactly k per row
-            wts = torch.tensor([self.sizes[self.local[r]] / n_tot for r in rr], dtype=torch.float32,
-                               device=self.device)
-            rec[j0:j0 + len(rr), 0] = torch.tensor([self.local[r] for r in rr], dtype=torch.float32,
-                                                   device=self.device)
-            rec[j0:j0 + len(rr), 1:1 + k] = d.gather(1, top) * wts[:, None]
-            rec[j0:j0 + len(rr), 1 + k:] = top.to(torch.int32).view(torch.float32)
+            n = len(rr)
+            d = padded_rows(n, self.P, self.device)
+            if _contiguous(rr):
+                torch.sub(self.theta[rr[0]:rr[-1] + 1, :self.P], self.w_global, out=d)
+            else:
+                torch.sub(self.theta.index_select(0, torch.tensor(rr, device=self.device))[:, :self.P], self.w_global,
+                          out=d)
+            bits = torch.zeros((n, self.W), dtype=torch.int32, device=self.device)
+            space.select(MK.REGROW_ABS, d, bits, torch.full((n, 1), k, dtype=torch.int64))
+            # exactly k set bits per row: a static-size compaction (no device->host size query)
+            top = torch.nonzero_static(MK.unpack_bits(bits, self.P, torch.bool), size=n * k)[:, 1].view(n, k)
+            rec[j0:j0 + n, 0] = meta[j0:j0 + n, 0]
+            rec[j0:j0 + n, 1:1 + k] = d.gather(1, top) * meta[j0:j0 + n, 1:2]
+            rec[j0:j0 + n, 1 + k:] = top.to(torch.int32).view(torch.float32)
         per_rank = [sum(1 for c in sampled if self.owner[c] == r) * (1 + 2 * k) for r in range(self.info.world)]
         g = rt.all_gather_sized(rec.view(-1), per_rank, self.info).view(-1, 1 + 2 * k)
         g = g.index_select(0, torch.argsort(g[:, 0]))  # fixed client order on every rank
         g_idx = g[:, 1 + k:].contiguous().view(torch.int32).to(torch.int64).reshape(1, -1)
         upd = torch.sparse_coo_tensor(g_idx, g[:, 1:1 + k].reshape(-1), (self.P,)).coalesce()
         self.w_global.index_add_(0, upd.indices()[0], upd.values())
-        bsum = torch.zeros(self.Q, dtype=torch.float32, device=self.device)
-        for r in rows:
-            bsum.add_(self.bufs[r, :self.Q], alpha=self.sizes[self.local[r]] / n_tot)
+        # BN buffers: dense weighted sum of the rows (one reduction, not one launch per client)
+        bsum = (meta[:, 1:2] * self.bufs[rows, :self.Q]).sum(0) if rows else \
+            torch.zeros(self.Q, dtype=torch.float32, device=self.device)
         rt.all_reduce_buckets(bsum, self.info)
         self.b_global.copy_(bsum)
         self.stat_info["aggregate_elems"] = int(2 * k * len(sampled))

@@ -67,3 +67,47 @@ def test_async_checkpoint_of_device_rows_round_trips(tmp_path):
     assert ck.load_runner(b, str(tmp_path)) == 2
     assert torch.equal(b.theta, a.theta) and not torch.equal(b.theta, keep)
     assert sorted(p.name for p in tmp_path.iterdir()) == ["latest", "round_2"]
+
+
+def test_hip_runner_training_log_with_graphs_equals_eager():
+    """AlexNet3D on the HIP engine: the per-client epoch losses the runner logs are accumulated on device inside the
+    captured hipGraph steps; they equal the eager (un-captured) run's, and sum_comm_params equals the formula."""
+    import logging
+    from neuroimagedisttraining_amd.data.synthetic_fl import build_fl_volumes, to_hip_store
+    from neuroimagedisttraining_amd.engine.executor import ClientSplit, FLConfig, FLRunner, HipEngine
+    from neuroimagedisttraining_amd.models.alexnet3d import AlexNet3D_Dropout
+    from neuroimagedisttraining_amd.parallel import runtime as rt
+    C, ntr, nte = 3, 6, 2
+    vol, labels, sp = build_fl_volumes(list(range(C)), C, ntr, nte, torch.device(DEV), seed=3)
+    x8, mom = to_hip_store(vol)
+    del vol
+    splits = [sp[c] for c in range(C)]
+    out = {}
+    for graphs in (True, False):
+        lines = []
+
+        class H(logging.Handler):
+            def emit(self, rec):
+                lines.append(rec.getMessage())
+        lg = logging.getLogger("nidt.gpu.log.%d" % graphs)
+        lg.handlers[:] = [H()]
+        lg.propagate = False
+        lg.setLevel(logging.INFO)
+        torch.manual_seed(0)
+        model = AlexNet3D_Dropout(num_classes=1)
+        eng = HipEngine(model, x8, mom, labels, torch.device(DEV))
+        info = rt.DistInfo(0, 1, 0, torch.device(DEV), "none")
+        cfg = FLConfig(comm_round=3, epochs=2, batch_size=4, seed=3, hip_graphs=graphs, frequency_of_the_test=0)
+        r = FLRunner(eng, splits, cfg, info, model, logger=lg)
+        r.generate_global_mask_snip()
+        comm = 0
+        for k in range(3):  # round 0 captures nothing new, round 1 captures, round 2 replays
+            down = int(torch.count_nonzero(r.w_global) + torch.count_nonzero(r.b_global))
+            r.run_round(k)
+            comm += C * down + sum(int(torch.count_nonzero(r.theta[j, :r.P]) + torch.count_nonzero(r.bufs[j, :r.Q]))
+                                   for j in range(r.C))
+        assert r.stat_info["sum_comm_params"] == comm
+        out[graphs] = [float(ln.split("Loss: ")[1]) for ln in lines if ln.startswith("Client Index")]
+    assert len(out[True]) == 3 * C * 2
+    assert all(np.isfinite(out[True])) and min(out[True]) > 0
+    assert np.allclose(out[True], out[False], rtol=1e-5, atol=1e-6), (out[True], out[False])
