@@ -158,23 +158,27 @@ void conv1_sample_moments(uintptr_t x8, int64_t N, uintptr_t mom, uintptr_t stre
 // 8 bytes) + H[fq] (phases 0,1,4,5: dwords 0 and 2); k-step 3 = W[fq] (phases 0,2,4,6: the low halves of the 4
 // dwords, two v_perm) + two 2-phase groups (or DHW) picked by one v_cndmask + v_perm each.  Only 3 of 128 slots are
 // empty (vs 99 of 224 in the 27 x 8 layout).
-__device__ constexpr int kC1F[8] = {0, 1, 3, 4, 9, 10, 12, 13};
-__device__ constexpr int kC1D[4] = {18, 19, 21, 22};
-__device__ constexpr int kC1H[4] = {6, 7, 15, 16};
+// [RO]: RO = 1 orders the groups of k-steps 0-2 so that the two lane quarters of each ds_read_b128 lane group (fq 0
+// with 1, fq 2 with 3) read tap groups of the same jw (their halo offsets then differ by whole 1-KB (dd, dh) rows:
+// the same banks for the same column, no conflict); RO = 0 is the original order (A/B, NIDT_C1_TAPORD=0)
+__device__ constexpr int kC1F2[2][8] = {{0, 1, 3, 4, 9, 10, 12, 13}, {0, 3, 1, 4, 9, 12, 10, 13}};
+__device__ constexpr int kC1D2[2][4] = {{18, 19, 21, 22}, {18, 21, 19, 22}};
+__device__ constexpr int kC1H2[2][4] = {{6, 7, 15, 16}, {6, 15, 7, 16}};
 __device__ constexpr int kC1W[4] = {2, 5, 11, 14};
 __device__ constexpr int kC1X1[4] = {24, 20, 8, 26};   // DH0, DW0, HW0, DHW
 __device__ constexpr int kC1X2[4] = {25, 23, 17, 26};  // DH1, DW1, HW1, (empty)
 __device__ constexpr int kC1XR[4][2] = {{0, 1}, {0, 2}, {0, 4}, {0, -1}};
 
 // (tap group, phase) of slot kk of the 128-slot layout, or t = -1 for an empty slot
+template <int RO>
 __device__ __forceinline__ void c1_slot128(int kk, int& t, int& r) {
   const int st = kk >> 5, fq = (kk >> 3) & 3, e = kk & 7;
   t = -1;
   r = 0;
-  if (st < 2) { t = kC1F[4 * st + fq]; r = e; return; }
+  if (st < 2) { t = kC1F2[RO][4 * st + fq]; r = e; return; }
   if (st == 2) {
-    if (e < 4) { t = kC1D[fq]; r = e; }
-    else { t = kC1H[fq]; r = (e - 4 < 2) ? e - 4 : e - 4 + 2; }
+    if (e < 4) { t = kC1D2[RO][fq]; r = e; }
+    else { t = kC1H2[RO][fq]; r = (e - 4 < 2) ? e - 4 : e - 4 + 2; }
     return;
   }
   if (e < 4) { t = kC1W[fq]; r = 2 * e; return; }
@@ -190,6 +194,7 @@ __device__ __forceinline__ void c1_slot128(int kk, int& t, int& r) {
 // A operand, against raw uint8 voxels; KS = 128 slots, or 224 = 27 x 8 for the legacy layout), w125 [G][64][125]
 // f32 = f16(w) * scale (scale = 1/255): the exact effective weights of conv(x / 255) that the moment math (BN
 // statistics) and the closed-form backward use.
+template <int RO>
 __global__ void k_pack_conv1_w(const float* __restrict__ theta, int64_t ldt, int64_t off, int64_t off_sign, int G,
                                float scale, int KS, uint16_t* __restrict__ w8, float* __restrict__ w125) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -197,7 +202,7 @@ __global__ void k_pack_conv1_w(const float* __restrict__ theta, int64_t ldt, int
   const int g = i / (kC1 * KS), rem = i - g * kC1 * KS, c = rem / KS, kk = rem - c * KS;
   int t, r;
   if (KS == 128) {
-    c1_slot128(kk, t, r);
+    c1_slot128<RO>(kk, t, r);
   } else {
     t = kk >> 3;
     r = kk & 7;
@@ -215,6 +220,15 @@ __global__ void k_pack_conv1_w(const float* __restrict__ theta, int64_t ldt, int
 }
 
 // K slots of the forward's packed weights: 128 (default) or the legacy 27 x 8 = 224 (NIDT_C1_K224=1, A/B)
+// tap-group order of the 128-slot forward layout (pack and forward must agree): NIDT_C1_TAPORD=0 keeps the original
+int conv1_tapord() {
+  static const int ro = [] {
+    const char* e = getenv("NIDT_C1_TAPORD");
+    return (e && atoi(e) == 0) ? 0 : 1;
+  }();
+  return ro;
+}
+
 int conv1_kslots() {
   static const int ks = [] {
     const char* e = getenv("NIDT_C1_K224");
@@ -227,8 +241,12 @@ void pack_conv1_w(uintptr_t theta, int64_t ldt, int64_t off, int64_t off_sign, i
                   uintptr_t w125, uintptr_t stream) {
   const int KS = conv1_kslots();
   // w125 entries of empty taps are never read; every valid (t, r) appears in exactly one slot of either layout
-  hipLaunchKernelGGL(k_pack_conv1_w, dim3(ceil_div(G * kC1 * KS, 256)), dim3(256), 0, as_stream(stream),
-                     ptr<const float>(theta), ldt, off, off_sign, G, scale, KS, ptr<uint16_t>(w8), ptr<float>(w125));
+  if (conv1_tapord())
+    hipLaunchKernelGGL(k_pack_conv1_w<1>, dim3(ceil_div(G * kC1 * KS, 256)), dim3(256), 0, as_stream(stream),
+                       ptr<const float>(theta), ldt, off, off_sign, G, scale, KS, ptr<uint16_t>(w8), ptr<float>(w125));
+  else
+    hipLaunchKernelGGL(k_pack_conv1_w<0>, dim3(ceil_div(G * kC1 * KS, 256)), dim3(256), 0, as_stream(stream),
+                       ptr<const float>(theta), ldt, off, off_sign, G, scale, KS, ptr<uint16_t>(w8), ptr<float>(w125));
   NIDT_CHECK(hipGetLastError());
 }
 
@@ -406,7 +424,7 @@ __device__ __forceinline__ f16x8 c1_bfrag(const uint16_t* hb, int s, int ro, con
 
 // PF: B-fragment prefetch distance in k-steps; KS: k-steps per (dd, dh) row (7 or 4); OCC: blocks per CU the
 // register budget is cut for (2: 256 VGPRs; 3: 168, with spills — A/B NIDT_C1_OCC)
-template <int PF, int KS, int OCC = 2, int DDU = 1>
+template <int PF, int KS, int OCC = 2, int DDU = 1, int RO = 1>
 __global__ __launch_bounds__(256, OCC) void k_conv1_fwd_pool_pipe(const uint8_t* __restrict__ x8,
                                                                 const int* __restrict__ idx,
                                                                 const uint16_t* __restrict__ w8,
@@ -501,11 +519,11 @@ __global__ __launch_bounds__(256, OCC) void k_conv1_fwd_pool_pipe(const uint8_t*
       toff[s] = goff(t);
     }
   } else {
-    toff[0] = goff(kC1F[fq]);
-    toff[1] = goff(kC1F[4 + fq]);
-    toff[2] = goff(kC1D[fq]);
+    toff[0] = goff(kC1F2[RO][fq]);
+    toff[1] = goff(kC1F2[RO][4 + fq]);
+    toff[2] = goff(kC1D2[RO][fq]);
     toff[3 % KS] = goff(kC1W[fq]);
-    gh = goff(kC1H[fq]);
+    gh = goff(kC1H2[RO][fq]);
     gx1 = goff(kC1X1[fq]);
     gx2 = goff(kC1X2[fq]);
     xsrc2 = fq == 2;
@@ -648,7 +666,11 @@ void conv1_fwd_pool(uintptr_t x8, uintptr_t idx, uintptr_t w8, uintptr_t scale, 
     const char* e = getenv("NIDT_C1_DDU");
     return e ? atoi(e) : 3;
   }();
-  if (conv1_kslots() == 128 && ddu == 3 && pf == 2 && occ != 3) {
+  if (conv1_kslots() == 128 && ddu == 3 && pf == 2 && occ != 3 && conv1_tapord() == 0) {
+    hipLaunchKernelGGL((k_conv1_fwd_pool_pipe<2, 4, 2, 3, 0>), dim3(kPD * NB * nq), dim3(256), 0, as_stream(stream),
+                       ptr<const uint8_t>(x8), ptr<const int>(idx), ptr<const uint16_t>(w8), ptr<const float>(scale),
+                       ptr<const float>(shift), B, ptr<uint16_t>(out), ptr<uint8_t>(amax), nq);
+  } else if (conv1_kslots() == 128 && ddu == 3 && pf == 2 && occ != 3) {
     hipLaunchKernelGGL((k_conv1_fwd_pool_pipe<2, 4, 2, 3>), dim3(kPD * NB * nq), dim3(256), 0, as_stream(stream),
                        ptr<const uint8_t>(x8), ptr<const int>(idx), ptr<const uint16_t>(w8), ptr<const float>(scale),
                        ptr<const float>(shift), B, ptr<uint16_t>(out), ptr<uint8_t>(amax), nq);
@@ -1201,51 +1223,104 @@ __global__ __launch_bounds__(256, 2) void k_conv1_wgrad_dot(const uint8_t* __res
 // that row, else 0 (the position index word is row-independent).  Block = (sample, pd[, row range]), stage = pooled
 // row ph: wave w runs k-step w & 1 over 5 or 4 of the 9 conv rows (alternating per stage), 8 smfmac per row.  Slabs
 // are reduced across the 4 waves in a fixed order (deterministic), in the VALU kernel's part[slab][64][126] format.
-constexpr int kSmMetaOff = (kC1sBElems * 2 + 15) / 16 * 16;   // byte offset of the record table
-constexpr int kSmBytes = kSmMetaOff + kPW * kC1 * 4;
+// Block = 8 waves, warp-specialised and double-buffered (one block per CU): waves 4-7 are producers — they issue the
+// global loads of stage s + 2, convert and store stage s + 1 (the 20 bf16 phase-plane copies and the record table)
+// into the other LDS buffer; waves 0-3 are consumers — each runs k-step w & 1 of stage s over 5 or 4 of its 9 conv
+// rows (8 smfmac per row, the next row's B fragments loaded under the current row's MFMAs).  One barrier per stage.
+constexpr int kSmBufBytes = (kC1sBElems * 2 + 15) / 16 * 16;        // one stage's B planes
+constexpr int kSmMetaBytes = kPW * kC1 * 4;                          // one stage's record table
+constexpr int kSmBytes = 2 * kSmBufBytes + 2 * kSmMetaBytes;
 static_assert(kSmBytes >= 4 * 32 * 128 * 4 + 4 * 64 * 4, "reduction scratch must fit in the stage buffers");
+static_assert(kSmBytes <= 160 * 1024, "LDS budget");
 
 typedef __bf16 bf16x16 __attribute__((ext_vector_type(16)));
 typedef short s16x2 __attribute__((ext_vector_type(2)));
 
-__global__ __launch_bounds__(256, 2) void k_conv1_wgrad_smf(const uint8_t* __restrict__ x8, const int* __restrict__ idx,
+// producer side: one stage's global data held in registers between its load and its LDS store
+struct C1sStage {
+  uint2 vx[10];        // 10 polyphase voxels (x0 .. x0 + 9) of this thread's staged input row
+  uint32_t rpg[5];     // pooled value | dL/dpooled << 16 of this thread's 5 records
+  uint32_t ra[5];      // argmax of the records
+};
+
+__device__ __forceinline__ void c1s_load(C1sStage& st, const uint8_t* xs, const uint16_t* dp, const uint16_t* pout,
+                                         const uint8_t* amax, int64_t rowbase, int pd, int ph, int ptid) {
+  const int brow = ptid >> 3, bx0 = 8 * (ptid & 7);
+  const int bzi = brow / 5, byi = brow - 5 * (brow / 5);
+#pragma unroll
+  for (int v = 0; v < 10; ++v) {
+    const int x = bx0 + v;
+    st.vx[v] = make_uint2(0, 0);
+    if (ptid < 200 && x < kPX)
+      st.vx[v] = *reinterpret_cast<const uint2*>(xs + (((int64_t)(3 * pd + bzi) * kPY + 3 * ph + byi) * kPX + x) * 8);
+  }
+  const int rc = ptid & 63, rcg = ptid >> 6;
+  const int64_t obase = (rowbase + ph) * kPW * kC1;
+#pragma unroll
+  for (int u = 0; u < 5; ++u) {
+    const int pw = rcg + 4 * u;
+    st.rpg[u] = 0;
+    st.ra[u] = 0;
+    if (pw < kPW) {
+      st.rpg[u] = (uint32_t)pout[obase + pw * kC1 + rc] | ((uint32_t)dp[obase + pw * kC1 + rc] << 16);
+      st.ra[u] = amax[obase + pw * kC1 + rc];
+    }
+  }
+}
+
+__device__ __forceinline__ void c1s_store(const C1sStage& st, uint16_t* bsm, uint32_t* meta, int ptid, float& Dloc) {
+  if (ptid < 200) {
+    const int brow = ptid >> 3, bx0 = 8 * (ptid & 7);
+    const int bzi = brow / 5, byi = brow - 5 * (brow / 5);
+    const int roff = bzi * kC1sZS + byi * kC1sRS + bx0;
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      float f[10];
+#pragma unroll
+      for (int v = 0; v < 10; ++v) f[v] = u8f(r < 4 ? st.vx[v].x : st.vx[v].y, r & 3);
+      const uint32_t e0 = bf2_pack(f[0], f[1]), e1 = bf2_pack(f[2], f[3]), e2 = bf2_pack(f[4], f[5]);
+      const uint32_t e3 = bf2_pack(f[6], f[7]), e4 = bf2_pack(f[8], f[9]);
+      *reinterpret_cast<uint4*>(&bsm[kC1sPlaneBase[kC1sPlaneOf[0][r]] + roff]) = make_uint4(e0, e1, e2, e3);
+      *reinterpret_cast<uint4*>(&bsm[kC1sPlaneBase[kC1sPlaneOf[1][r]] + roff]) =
+          make_uint4(bf2_pack(f[1], f[2]), bf2_pack(f[3], f[4]), bf2_pack(f[5], f[6]), bf2_pack(f[7], f[8]));
+      if ((r & 1) == 0)
+        *reinterpret_cast<uint4*>(&bsm[kC1sPlaneBase[kC1sPlaneOf[2][r]] + roff]) = make_uint4(e1, e2, e3, e4);
+    }
+  }
+  const int rc = ptid & 63, rcg = ptid >> 6;
+#pragma unroll
+  for (int u = 0; u < 5; ++u) {
+    const int pw = rcg + 4 * u;
+    const uint32_t dzb = bf16_to_f32((uint16_t)(st.rpg[u] & 0xffffu)) > 0.f ? (st.rpg[u] >> 16) : 0u;
+    Dloc += bf16_to_f32((uint16_t)dzb);
+    if (pw < kPW) {
+      const int a = st.ra[u];
+      const int ad = a / 9, ah = (a / 3) % 3, aw = a % 3;
+      meta[pw * kC1 + rc] = dzb | ((uint32_t)(3 * pw + aw) << 16) | ((uint32_t)(ad * 3 + ah) << 24);
+    }
+  }
+}
+
+__global__ __launch_bounds__(512, 1) void k_conv1_wgrad_smf(const uint8_t* __restrict__ x8, const int* __restrict__ idx,
                                                            const uint16_t* __restrict__ dp,
                                                            const uint16_t* __restrict__ pout,
                                                            const uint8_t* __restrict__ amax, float* __restrict__ part,
                                                            int nq) {
   __shared__ __attribute__((aligned(16))) uint8_t smem[kSmBytes];
-  uint16_t* bsm = reinterpret_cast<uint16_t*>(smem);                    // the 20 phase-plane copies
-  uint32_t* meta = reinterpret_cast<uint32_t*>(smem + kSmMetaOff);      // [19 cells][64 c]: dz | x << 16 | row << 24
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
   const int q = bid % nq, rest = bid / nq;
   const int pd = rest % kPD, n = rest / kPD;
   const int rq = ((kPH + nq - 1) / nq + kWgRows - 1) / kWgRows * kWgRows;
   const int ph_begin = q * rq, ph_end = min(kPH, ph_begin + rq);
+  const int nst = ph_end - ph_begin;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const bool producer = wid >= 4;
   const uint8_t* xs = x8 + (int64_t)idx[n] * kPZ * kPY * kPX * 8;
-  const int ks = wid & 1;  // this wave's k-step (x 0-31 or 32-63)
-  // B: this lane's column base per N-tile (plane copy J = jw of phase r, rows (jd, jh), x offset 16 q)
-  int bbase[4];
-#pragma unroll
-  for (int T = 0; T < 4; ++T) {
-    int k = kC1sSlotTap[32 * T + (lane & 31)];
-    k = k >= 1000 ? k - 1000 : k;
-    const int kd = k / 25, kh = (k / 5) % 5, kw = k % 5;
-    const int r = ((kd & 1) << 2) | ((kh & 1) << 1) | (kw & 1);
-    bbase[T] = kC1sPlaneBase[kC1sPlaneOf[kw >> 1][r]] + (kd >> 1) * kC1sZS + (kh >> 1) * kC1sRS + 16 * (lane >> 5) + 32 * ks;
-  }
-  // A: this lane's 8 slots (4-groups g = j >> 1 at x = Xg, slot j & 1 = the group's first cell or the next one)
-  const int pl = lane >> 5, ml = lane & 31;
-  int xg[4], mcell[8];
-#pragma unroll
-  for (int g = 0; g < 4; ++g) {
-    xg[g] = 32 * ks + 16 * (g >> 1) + 8 * pl + 4 * (g & 1);
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int C = xg[g] / 3 + h;
-      mcell[2 * g + h] = C < kPW ? C * kC1 + ml : -1;
-    }
-  }
+  const int64_t rowbase = ((int64_t)n * kPD + pd) * kPH;
+  auto bbuf = [&](int s) { return reinterpret_cast<uint16_t*>(smem + (s & 1) * kSmBufBytes); };
+  auto mbuf = [&](int s) { return reinterpret_cast<uint32_t*>(smem + 2 * kSmBufBytes + (s & 1) * kSmMetaBytes); };
+
+  float Dloc = 0.f;
   f32x16 acc[2][4];
 #pragma unroll
   for (int t = 0; t < 2; ++t)
@@ -1253,144 +1328,129 @@ __global__ __launch_bounds__(256, 2) void k_conv1_wgrad_smf(const uint8_t* __res
     for (int T = 0; T < 4; ++T)
 #pragma unroll
       for (int i = 0; i < 16; ++i) acc[t][T][i] = 0.f;
-  float Dloc = 0.f;
-  const int rc = tid & 63, rcg = tid >> 6;  // record roles: channel, cell group
-  const int64_t rowbase = ((int64_t)n * kPD + pd) * kPH;
-  // B staging items: (input row zi * 5 + yi, 8-x chunk); the item needs voxels x0 .. x0 + 9
-  const int brow = tid >> 3, bx0 = 8 * (tid & 7);
-  const bool bact = tid < 200;
-  const int bzi = brow / 5, byi = brow - 5 * (brow / 5);
-  for (int ph = ph_begin; ph < ph_end; ++ph) {
-    // (1) global loads: this thread's 10 voxels and 5 records
-    uint2 vx[10];
-#pragma unroll
-    for (int v = 0; v < 10; ++v) {
-      const int x = bx0 + v;
-      vx[v] = make_uint2(0, 0);
-      if (bact && x < kPX)
-        vx[v] = *reinterpret_cast<const uint2*>(xs + (((int64_t)(3 * pd + bzi) * kPY + 3 * ph + byi) * kPX + x) * 8);
-    }
-    uint16_t rp[5], rg[5];
-    uint8_t ra[5];
-    const int64_t obase = (rowbase + ph) * kPW * kC1;
-#pragma unroll
-    for (int u = 0; u < 5; ++u) {
-      const int pw = rcg + 4 * u;
-      rp[u] = 0;
-      rg[u] = 0;
-      ra[u] = 0;
-      if (pw < kPW) {
-        rp[u] = pout[obase + pw * kC1 + rc];
-        rg[u] = dp[obase + pw * kC1 + rc];
-        ra[u] = amax[obase + pw * kC1 + rc];
+
+  if (producer) {  // ------------------------------------------------------------------------------ producers
+    const int ptid = tid - 256;
+    C1sStage cur, nxt;
+    c1s_load(cur, xs, dp, pout, amax, rowbase, pd, ph_begin, ptid);
+    if (nst > 1) c1s_load(nxt, xs, dp, pout, amax, rowbase, pd, ph_begin + 1, ptid);
+    c1s_store(cur, bbuf(0), mbuf(0), ptid, Dloc);
+    __syncthreads();                                  // stage 0 ready
+    for (int s = 0; s < nst; ++s) {
+      if (s + 1 < nst) {
+        cur = nxt;
+        if (s + 2 < nst) c1s_load(nxt, xs, dp, pout, amax, rowbase, pd, ph_begin + s + 2, ptid);
+        c1s_store(cur, bbuf(s + 1), mbuf(s + 1), ptid, Dloc);
       }
+      __syncthreads();                                // stage s consumed, stage s + 1 ready
     }
-    __syncthreads();  // the previous stage's LDS reads are done
-    // (2) B planes: per phase r, 10 voxels -> bf16 (exact for uint8), packed for the copies J = 0, 1 (and 2 if rw = 0)
-    if (bact) {
-      const int roff = bzi * kC1sZS + byi * kC1sRS + bx0;
+  } else {  // ------------------------------------------------------------------------------------- consumers
+    const int ks = wid & 1;  // this wave's k-step (x 0-31 or 32-63)
+    int bbase[4];
 #pragma unroll
-      for (int r = 0; r < 8; ++r) {
-        float f[10];
-#pragma unroll
-        for (int v = 0; v < 10; ++v) f[v] = u8f(r < 4 ? vx[v].x : vx[v].y, r & 3);
-        const uint32_t e0 = bf2_pack(f[0], f[1]), e1 = bf2_pack(f[2], f[3]), e2 = bf2_pack(f[4], f[5]);
-        const uint32_t e3 = bf2_pack(f[6], f[7]), e4 = bf2_pack(f[8], f[9]);
-        *reinterpret_cast<uint4*>(&bsm[kC1sPlaneBase[kC1sPlaneOf[0][r]] + roff]) = make_uint4(e0, e1, e2, e3);
-        *reinterpret_cast<uint4*>(&bsm[kC1sPlaneBase[kC1sPlaneOf[1][r]] + roff]) =
-            make_uint4(bf2_pack(f[1], f[2]), bf2_pack(f[3], f[4]), bf2_pack(f[5], f[6]), bf2_pack(f[7], f[8]));
-        if ((r & 1) == 0)
-          *reinterpret_cast<uint4*>(&bsm[kC1sPlaneBase[kC1sPlaneOf[2][r]] + roff]) = make_uint4(e1, e2, e3, e4);
-      }
+    for (int T = 0; T < 4; ++T) {
+      int k = kC1sSlotTap[32 * T + (lane & 31)];
+      k = k >= 1000 ? k - 1000 : k;
+      const int kd = k / 25, kh = (k / 5) % 5, kw = k % 5;
+      const int r = ((kd & 1) << 2) | ((kh & 1) << 1) | (kw & 1);
+      bbase[T] = kC1sPlaneBase[kC1sPlaneOf[kw >> 1][r]] + (kd >> 1) * kC1sZS + (kh >> 1) * kC1sRS + 16 * (lane >> 5) +
+                 32 * ks;
     }
-    // (3) records: dz (0 where the pooled value is ReLU-dead) | conv x of the argmax << 16 | its conv row << 24
-#pragma unroll
-    for (int u = 0; u < 5; ++u) {
-      const int pw = rcg + 4 * u;
-      const uint16_t dzb = bf16_to_f32(rp[u]) > 0.f ? rg[u] : (uint16_t)0;
-      Dloc += bf16_to_f32(dzb);
-      if (pw < kPW) {
-        const int a = ra[u];
-        const int ad = a / 9, ah = (a / 3) % 3, aw = a % 3;
-        meta[pw * kC1 + rc] = (uint32_t)dzb | ((uint32_t)(3 * pw + aw) << 16) | ((uint32_t)(ad * 3 + ah) << 24);
-      }
-    }
-    __syncthreads();
-    // (4) per-stage A operands of this wave's k-step: per 4-group g the two slots' dz values packed as one bf16 pair
-    // (W) and their conv rows as one-hot bits (row in the low half for slot 0, the high half for slot 1; none when
-    // the argmax falls outside the group); the index word holds each argmax's position in its group
-    uint32_t wv[2][4], oh[2][4], ix[2];
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      ix[t] = 0;
+    // this lane's 4-groups g at x = xg (slot 0 = the group's first cell, slot 1 = the next one)
+    const int xg0 = 32 * ks + 8 * (lane >> 5);
+    __syncthreads();                                  // stage 0 ready
+    for (int s = 0; s < nst; ++s) {
+      const uint16_t* bsm = bbuf(s);
+      const uint32_t* meta = mbuf(s);
+      // per-stage A operands: per 4-group g the slots' dz values packed as one bf16 pair (W) and their conv rows as
+      // one-hot bits (low half slot 0, high half slot 1; none when the argmax falls outside the group); the index
+      // word holds each argmax's position in its group
+      uint32_t wv[2][4], oh[2][4], ix[2] = {0u, 0u};
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
-        uint32_t w = 0, o = 0;
+        const int xg = xg0 + 16 * (g >> 1) + 4 * (g & 1);
+        const int C0 = xg / 3;
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const int j = 2 * g + h;
-          const uint32_t mw = mcell[j] >= 0 ? meta[mcell[j] + 32 * t] : 0u;
-          const uint32_t d = ((mw >> 16) & 0xffu) - (uint32_t)xg[g];
-          const bool in = d <= 3u && mcell[j] >= 0;
-          w |= (in ? (mw & 0xffffu) : 0u) << (16 * h);
-          o |= (in ? (1u << (mw >> 24)) : 0u) << (16 * h);
-          ix[t] |= (in ? d : 0u) << (2 * j);
+        for (int t = 0; t < 2; ++t) {
+          uint32_t w = 0, o = 0;
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int C = C0 + h;
+            const uint32_t mw = C < kPW ? meta[C * kC1 + 32 * t + (lane & 31)] : 0u;
+            const uint32_t d = ((mw >> 16) & 0xffu) - (uint32_t)xg;
+            const bool in = d <= 3u && C < kPW;
+            w |= (in ? (mw & 0xffffu) : 0u) << (16 * h);
+            o |= (in ? (1u << (mw >> 24)) : 0u) << (16 * h);
+            ix[t] |= (in ? d : 0u) << (2 * (2 * g + h));
+          }
+          wv[t][g] = w;
+          oh[t][g] = o;
         }
-        wv[t][g] = w;
-        oh[t][g] = o;
       }
-    }
-    // (5) smfmac over this wave's conv rows (the 5-row half alternates between the two waves of a k-step).  A of
-    // row rr: shifting the one-hot pair left by 15 - rr puts bit rr of each half into that half's sign bit, and a
-    // packed 16-bit arithmetic shift by 15 turns it into a 0xffff / 0 mask per slot (3 VALU per 4-group)
-    const int half = (wid >> 1) ^ ((ph - ph_begin) & 1);
-    const int rr0 = half ? 5 : 0, rr1 = half ? 9 : 5;
-    for (int rr = rr0; rr < rr1; ++rr) {
-      const int roff = (rr / 3) * kC1sZS + (rr % 3) * kC1sRS;
-      bf16x16 bv[4];
+      const int half = (wid >> 1) ^ (s & 1);
+      const int rr0 = half ? 5 : 0, rr1 = half ? 9 : 5;
+      // B fragments of row rr: software-pipelined one row ahead
+      bf16x16 bv[4], bn[4];
+      auto loadB = [&](int rr, bf16x16 (&dst)[4]) {
+        const int roff = (rr / 3) * kC1sZS + (rr % 3) * kC1sRS;
 #pragma unroll
-      for (int T = 0; T < 4; ++T) {
-        const uint16_t* bp = &bsm[bbase[T] + roff];
-        const bf16x8 lo = *reinterpret_cast<const bf16x8*>(bp);
-        const bf16x8 hi = *reinterpret_cast<const bf16x8*>(bp + 8);
-        bv[T] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15);
-      }
-      bf16x8 av[2];
-#pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        uint32_t w[4];
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const s16x2 sh = __builtin_bit_cast(s16x2, oh[t][g] << (15 - rr));
-          const s16x2 m = sh >> (s16x2){15, 15};
-          w[g] = wv[t][g] & __builtin_bit_cast(uint32_t, m);
+        for (int T = 0; T < 4; ++T) {
+          const uint16_t* bp = &bsm[bbase[T] + roff];
+          const bf16x8 lo = *reinterpret_cast<const bf16x8*>(bp);
+          const bf16x8 hi = *reinterpret_cast<const bf16x8*>(bp + 8);
+          dst[T] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15);
         }
-        av[t] = __builtin_bit_cast(bf16x8, make_uint4(w[0], w[1], w[2], w[3]));
-      }
+      };
+      loadB(rr0, bv);
+      for (int rr = rr0; rr < rr1; ++rr) {
+        if (rr + 1 < rr1) loadB(rr + 1, bn);
+        // A of row rr: shifting a one-hot pair left by 15 - rr puts bit rr of each half into that half's sign bit;
+        // a packed 16-bit arithmetic shift by 15 makes it a 0xffff / 0 mask per slot (3 VALU per 4-group)
+        bf16x8 av[2];
 #pragma unroll
-      for (int T = 0; T < 4; ++T) {
-        acc[0][T] = __builtin_amdgcn_smfmac_f32_32x32x32_bf16(av[0], bv[T], acc[0][T], (int)ix[0], 0, 0);
-        acc[1][T] = __builtin_amdgcn_smfmac_f32_32x32x32_bf16(av[1], bv[T], acc[1][T], (int)ix[1], 0, 0);
+        for (int t = 0; t < 2; ++t) {
+          uint32_t w[4];
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const s16x2 sh = __builtin_bit_cast(s16x2, oh[t][g] << (15 - rr));
+            const s16x2 m = sh >> (s16x2){15, 15};
+            w[g] = wv[t][g] & __builtin_bit_cast(uint32_t, m);
+          }
+          av[t] = __builtin_bit_cast(bf16x8, make_uint4(w[0], w[1], w[2], w[3]));
+        }
+#pragma unroll
+        for (int T = 0; T < 4; ++T) {
+          acc[0][T] = __builtin_amdgcn_smfmac_f32_32x32x32_bf16(av[0], bv[T], acc[0][T], (int)ix[0], 0, 0);
+          acc[1][T] = __builtin_amdgcn_smfmac_f32_32x32x32_bf16(av[1], bv[T], acc[1][T], (int)ix[1], 0, 0);
+        }
+#pragma unroll
+        for (int T = 0; T < 4; ++T) bv[T] = bn[T];
       }
+      __syncthreads();                                // stage s consumed, stage s + 1 ready
     }
   }
-  // (6) fixed-order reduction over the 4 waves, one M-tile (32 channels) at a time, and D over the 4 cell groups
+  // fixed-order reduction over the 4 consumer waves, one M-tile (32 channels) at a time, and D over the producers'
+  // 4 cell groups
   float* red = reinterpret_cast<float*>(smem);           // [4 w][32 m][128 slot]
   float* dred = red + 4 * 32 * 128;                      // [4 cg][64 c]
   float* op = part + (int64_t)bid_slab(rest, q, nq) * kC1 * 126;
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
     __syncthreads();
+    if (!producer) {
 #pragma unroll
-    for (int T = 0; T < 4; ++T)
+      for (int T = 0; T < 4; ++T)
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int m = 8 * (i >> 2) + 4 * (lane >> 5) + (i & 3);
-        red[(wid * 32 + m) * 128 + 32 * T + (lane & 31)] = acc[t][T][i];
-      }
-    if (t == 0) dred[rcg * 64 + rc] = Dloc;
+        for (int i = 0; i < 16; ++i) {
+          const int m = 8 * (i >> 2) + 4 * (lane >> 5) + (i & 3);
+          red[(wid * 32 + m) * 128 + 32 * T + (lane & 31)] = acc[t][T][i];
+        }
+    } else if (t == 0) {
+      const int ptid = tid - 256;
+      dred[(ptid >> 6) * 64 + (ptid & 63)] = Dloc;
+    }
     __syncthreads();
-    for (int e = tid; e < 32 * 126; e += 256) {
+    for (int e = tid; e < 32 * 126; e += 512) {
       const int m = e / 126, k = e - 126 * (e / 126);
       float v;
       if (k < 125) {
@@ -1440,7 +1500,7 @@ void conv1_wgrad(uintptr_t x8, uintptr_t idx, uintptr_t dp, uintptr_t pout, uint
   }();
   const bool smf = g_c1wg_mode >= 0 ? g_c1wg_mode == 1 : smf_env == 1;
   if (smf)
-    hipLaunchKernelGGL(k_conv1_wgrad_smf, dim3(kPD * NB * nq), dim3(256), 0, s, ptr<const uint8_t>(x8),
+    hipLaunchKernelGGL(k_conv1_wgrad_smf, dim3(kPD * NB * nq), dim3(512), 0, s, ptr<const uint8_t>(x8),
                        ptr<const int>(idx), ptr<const uint16_t>(dp), ptr<const uint16_t>(pout),
                        ptr<const uint8_t>(amax), ptr<float>(part), nq);
   else if (dot)

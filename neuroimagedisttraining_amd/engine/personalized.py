@@ -525,20 +525,31 @@ class DisPFLRunner(PersonalizedRunner):
         MK.mix_rows(bplan, self.Q)
 
     def _all_bits(self, bits):
-        """[N, W] mask bit rows of every client (all-reduce of the zero-padded local rows)."""
-        out = torch.zeros((self.N, self.W), dtype=torch.int64, device=self.device)
-        if self.C:
-            out[torch.tensor(self.local, device=self.device)] = bits[:self.C].to(torch.int64)
-        rt.all_reduce_buckets(out, self.info)
-        return out.to(torch.int32)
+        """[N, W] int32 mask bit rows of every client: ONE all-gather of each rank's own rows (their per-rank counts
+        are known everywhere from the shard map, so no size exchange), placed by client id."""
+        out = torch.zeros((self.N, self.W), dtype=torch.int32, device=self.device)
+        mine = bits[:self.C].contiguous().view(-1) if self.C else torch.zeros(0, dtype=torch.int32, device=self.device)
+        if self.info.enabled:
+            sizes = [len(sh) * self.W for sh in self.shards]
+            flat = rt.all_gather_sized(mine, sizes, self.info).view(-1, self.W)
+            # each rank's rows are in its row order (size-sorted, ties by id: the rule of FLRunner.__init__/migrate)
+            order = [c for sh in self.shards for c in sorted(sh, key=lambda c: (-int(self.sizes[c]), c))]
+            out[torch.tensor(order, device=self.device)] = flat
+        elif self.C:
+            out[torch.tensor(self.local, device=self.device)] = mine.view(self.C, self.W)
+        return out
 
     def finish(self):
         all_bits = self._all_bits(self.mbits)
-        mat = []
-        for i in range(self.N):
-            d = self.mspace.hamming(all_bits[i:i + 1].expand(self.N, -1).contiguous(), all_bits).sum(1)
-            mat.append(d.cpu().tolist())
-        self.stat_info["mask_dis_matrix"] = mat
+        # [N, N] Hamming matrix on device, a chunk of rows per launch, one device->host copy at the end
+        N, ch = self.N, max(1, min(self.N, (1 << 26) // max(1, self.N * self.W)))
+        mat = torch.empty((N, N), dtype=torch.int64, device=self.device)
+        for i0 in range(0, N, ch):
+            i1 = min(N, i0 + ch)
+            a = all_bits[i0:i1].unsqueeze(1).expand(i1 - i0, N, self.W).reshape(-1, self.W)
+            b = all_bits.unsqueeze(0).expand(i1 - i0, N, self.W).reshape(-1, self.W)
+            mat[i0:i1] = self.mspace.hamming(a.contiguous(), b.contiguous()).sum(1).view(i1 - i0, N).to(torch.int64)
+        self.stat_info["mask_dis_matrix"] = mat.cpu().tolist()
         if self.cfg.save_masks:
             self.stat_info["final_masks"] = MK.unpack_bits(all_bits, self.P).bool().cpu()
         return None

@@ -11,9 +11,16 @@ if ROOT not in sys.path:
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) GPU and the built HIP extension")
     config.addinivalue_line("markers", "slow: long-running CPU test")
+    config.addinivalue_line("markers", "extended: extra shapes of a kernel family already covered by the default GPU "
+                                       "run (builder sessions: NIDT_EXTENDED_GPU_TESTS=1)")
 
 
 def pytest_collection_modifyitems(config, items):
+    if os.environ.get("NIDT_EXTENDED_GPU_TESTS", "0") != "1":
+        ext = pytest.mark.skip(reason="extended shape sweep (NIDT_EXTENDED_GPU_TESTS=1 runs it)")
+        for it in items:
+            if "extended" in it.keywords:
+                it.add_marker(ext)
     try:
         import torch
         has_gpu = torch.cuda.is_available()

@@ -1,9 +1,19 @@
 #!/bin/bash
-# G=8 (per-GPU load of the 8-GPU headline) A/B of the conv1 forward row split and the conv2 wgrad split-K, the Tiny /
-# CIFAR round-time diagnosis of round 3 (tools/gpu_r3_bc.sh), and the headline bench
+# smfmac conv1 wgrad v4 (warp-specialised, double-buffered): correctness vs the VALU gather, then kbench A/B
 set -o pipefail
+mkdir -p gpurun_out/r4i gpurun_out/r4h
 export PYTHONUNBUFFERED=1
-mkdir -p gpurun_out/r4h
+timeout -k 10 200 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_gpu_kernels.py \
+  -k "smfmac" > gpurun_out/r4i/pytest.txt 2>&1 || { tail -30 gpurun_out/r4i/pytest.txt; exit 1; }
+tail -2 gpurun_out/r4i/pytest.txt
+for mode in 0 1 0 1; do
+  NIDT_C1WG_SMF=$mode timeout -k 10 200 python tools/kbench.py 64 10 > gpurun_out/r4i/kbench_g64_smf$mode.txt 2>&1 || exit 1
+  echo "smf=$mode: $(grep -E 'full train' gpurun_out/r4i/kbench_g64_smf$mode.txt) $(grep -E '^conv1_wgrad' gpurun_out/r4i/kbench_g64_smf$mode.txt)"
+done
+for mode in 0 1; do
+  NIDT_C1WG_SMF=$mode timeout -k 10 200 python tools/kbench.py 8 10 > gpurun_out/r4i/kbench_g8_smf$mode.txt 2>&1 || exit 1
+  echo "g8 smf=$mode: $(grep -E 'full train' gpurun_out/r4i/kbench_g8_smf$mode.txt) $(grep -E '^conv1_wgrad' gpurun_out/r4i/kbench_g8_smf$mode.txt)"
+done
 kb() {  # name, env..., -- G
   local name=$1; shift; local envs=()
   while [ "$1" != "--" ]; do envs+=("$1"); shift; done; shift
@@ -29,5 +39,3 @@ timeout -k 10 300 python bench.py --clients 8 --steps 10 --warmup 3 > gpurun_out
 echo "bench 8 clients: $(grep -o '"value": [0-9.]*' gpurun_out/r4h/bench_c8.json)"
 timeout -k 10 300 python bench.py --steps 10 --warmup 3 > gpurun_out/r4h/bench.json 2>&1 || exit 1
 echo "bench 64 clients: $(grep -o '"value": [0-9.]*' gpurun_out/r4h/bench.json)"
-bash tools/gpu_r3_bc.sh 2>&1 | tee gpurun_out/r4h/r3bc.txt
-cp -r gpurun_out/r3bc gpurun_out/r4h/ 2>/dev/null
