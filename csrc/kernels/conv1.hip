@@ -160,7 +160,8 @@ void conv1_sample_moments(uintptr_t x8, int64_t N, uintptr_t mom, uintptr_t stre
 // empty (vs 99 of 224 in the 27 x 8 layout).
 // [RO]: RO = 1 orders the groups of k-steps 0-2 so that the two lane quarters of each ds_read_b128 lane group (fq 0
 // with 1, fq 2 with 3) read tap groups of the same jw (their halo offsets then differ by whole 1-KB (dd, dh) rows:
-// the same banks for the same column, no conflict); RO = 0 is the original order (A/B, NIDT_C1_TAPORD=0)
+// the same banks for the same column, no conflict); RO = 0 is the original order and the
+// default (RO = 1 measured slower, NIDT_C1_TAPORD=1 for A/B)
 __device__ constexpr int kC1F2[2][8] = {{0, 1, 3, 4, 9, 10, 12, 13}, {0, 3, 1, 4, 9, 12, 10, 13}};
 __device__ constexpr int kC1D2[2][4] = {{18, 19, 21, 22}, {18, 21, 19, 22}};
 __device__ constexpr int kC1H2[2][4] = {{6, 7, 15, 16}, {6, 15, 7, 16}};
@@ -220,11 +221,13 @@ __global__ void k_pack_conv1_w(const float* __restrict__ theta, int64_t ldt, int
 }
 
 // K slots of the forward's packed weights: 128 (default) or the legacy 27 x 8 = 224 (NIDT_C1_K224=1, A/B)
-// tap-group order of the 128-slot forward layout (pack and forward must agree): NIDT_C1_TAPORD=0 keeps the original
+// tap-group order of the 128-slot forward layout (pack and forward must agree): the original order by default;
+// NIDT_C1_TAPORD=1 selects the bank-paired order (slower at 64 clients: conv1 forward 4.38 vs 4.25 ms,
+// profiles/r4_kbench_g64.txt)
 int conv1_tapord() {
   static const int ro = [] {
     const char* e = getenv("NIDT_C1_TAPORD");
-    return (e && atoi(e) == 0) ? 0 : 1;
+    return (e && atoi(e) == 1) ? 1 : 0;
   }();
   return ro;
 }

@@ -2417,7 +2417,18 @@ int conv3d_wgrad_tri_nsplit(int G, int B, int D, int H, int W, int Cin, int Cout
   const int U = wt_umax_cap(wgrad_tri_umax(B, D, H, W, pad));
   const int lds = 2 * (U * 128 + nch * 8192);  // bytes per block; 4 waves per SIMD by registers
   const int per_cu = std::max(1, std::min(163840 / std::max(lds, 1), 16 / (3 * nch)));
-  return wgrad_nsplit_base(G * (Cout / (64 * nch)) * 9 * (Cin / 64), G, Mg, 27 * Cin, Cout, 1.0, 0.0, 256.0 * per_cu);
+  const int base = G * (Cout / (64 * nch)) * 9 * (Cin / 64);
+  const double slots = 256.0 * per_cu;
+  const int ns = wgrad_nsplit_base(base, G, Mg, 27 * Cin, Cout, 1.0, 0.0, slots);
+  // the unpadded launch runs on the wgrad side stream next to the dgrad: when the model's pick is a single wave
+  // (small lockstep groups) the side launch cannot fill around the dgrad; go about three waves deep instead
+  // (AlexNet conv2 at 8 clients: full step 3.62 -> 3.48 ms with 24 splits, 3.50 with 16, 3.58 with 8;
+  // profiles/r4_kbench_g8.txt)
+  if (pad == 0 && base * ns <= slots) {
+    const int deep = ceil_div((int)(3 * slots), base);
+    return std::max(ns, std::min(deep, std::max(1, std::min(64, Mg / 512))));
+  }
+  return ns;
 }
 
 // step table for k_conv_wgrad_tri: ceil(Mg / 64) entries of 2U + 64 ints
