@@ -129,8 +129,9 @@ def add_args(parser, algo):
     a("--keep_last", type=int, default=2, help="complete checkpoint rounds kept on disk (0 = all)")
     a("--resume", type=int, default=0)
     a("--log_dir", type=str, default="LOG")
-    a("--results_dir", type=str, default="results",
-      help="record_information target: <results_dir>/<dataset>/<identity>.json (+ .npz for large arrays)")
+    a("--results_dir", type=str, default=os.environ.get("NIDT_RESULTS_DIR", "results"),
+      help="record_information target: <results_dir>/<dataset>/<identity>.json (+ .npz for large arrays); "
+           "default $NIDT_RESULTS_DIR or ./results")
     return parser
 
 

@@ -6,6 +6,10 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
+# CLI runs inside tests record their stat_info into a scratch directory, not the working tree
+if "NIDT_RESULTS_DIR" not in os.environ:
+    import tempfile
+    os.environ["NIDT_RESULTS_DIR"] = tempfile.mkdtemp(prefix="nidt_results_")
 
 
 def pytest_configure(config):
