@@ -2420,10 +2420,10 @@ int conv3d_wgrad_tri_nsplit(int G, int B, int D, int H, int W, int Cin, int Cout
   const int base = G * (Cout / (64 * nch)) * 9 * (Cin / 64);
   const double slots = 256.0 * per_cu;
   const int ns = wgrad_nsplit_base(base, G, Mg, 27 * Cin, Cout, 1.0, 0.0, slots);
-  // the unpadded launch runs on the wgrad side stream next to the dgrad: when the model's pick is a single wave
-  // (small lockstep groups) the side launch cannot fill around the dgrad; go about three waves deep instead
-  // (AlexNet conv2 at 8 clients: full step 3.62 -> 3.48 ms with 24 splits, 3.50 with 16, 3.58 with 8;
-  // profiles/r4_kbench_g8.txt)
+  // a single-wave pick (small lockstep groups) ends with its slowest block: every block runs the whole launch, so
+  // uneven progress of co-resident blocks sets the time.  Going about three waves deep measured faster in the full
+  // step although the isolated launch is slower (AlexNet conv2 at 8 clients: step 3.62 -> 3.48 ms with 24 splits,
+  // 3.50 with 16, 3.58 with 8; isolated wgrad 0.363 -> 0.415 ms; profiles/r4_kbench_g8.txt)
   if (pad == 0 && base * ns <= slots) {
     const int deep = ceil_div((int)(3 * slots), base);
     return std::max(ns, std::min(deep, std::max(1, std::min(64, Mg / 512))));
