@@ -213,13 +213,16 @@ def load_data(args, dataset_name, logger=None):
 
 RESNET3D_NAMES = ("resnet3d_50", "3dresnet50")
 IMAGE_DATASETS = ("cifar10", "cifar100", "tiny")
+# the other image models of the reference entry points (main_subavg.py:143-158): client-batched via vmap
+ZOO2D_NAMES = ("lenet5", "cnn_cifar10", "cnn_cifar100", "vgg11", "vgg16")
 
 
 def hip_family(args):
     """Model family of the client-batched MI355X executor for these flags, or None (eager only):
     ``alexnet3d`` (3DCNN on ABCD: engine/executor.HipEngine), ``resnet2d`` (resnet18 = ResNet-18-GN on 32x32
     CIFAR-10/100 or 64x64 Tiny-ImageNet — ``customized_resnet18`` / ``tiny_resnet18``: engine/resnet2d_hip),
-    ``resnet3d`` (3D ResNet-50 on ABCD: engine/resnet3d_hip)."""
+    ``resnet3d`` (3D ResNet-50 on ABCD: engine/resnet3d_hip), ``batched2d`` (lenet5 / cnn_cifar10 / cnn_cifar100 /
+    vgg11 / vgg16 on CIFAR: engine/batched2d, clients vmapped into grouped library calls + the fused optimizer)."""
     model = args.model.lower()
     if args.dataset == "ABCD" and model in ("3dcnn", "alexnet3d", "alexnet3d_dropout"):
         # the AlexNet3D kernels are built for the ABCD volume (1x121x145x121: polyphase 61x73x61 store, conv1's
@@ -228,6 +231,8 @@ def hip_family(args):
         return "alexnet3d" if shape in (None, ABCD_SHAPE) else None
     if args.dataset in IMAGE_DATASETS and model == "resnet18":
         return "resnet2d"
+    if args.dataset in ("cifar10", "cifar100") and model in ZOO2D_NAMES:
+        return "batched2d"
     if args.dataset == "ABCD" and model in RESNET3D_NAMES:
         return "resnet3d"
     return None
@@ -254,8 +259,9 @@ def _use_hip(args, algo):
         shape = _cohort_shape(args) if args.dataset == "ABCD" else None
         why = ("the cohort's volumes are %s, the AlexNet3D kernels need %s" % (shape, ABCD_SHAPE)
                if shape not in (None, ABCD_SHAPE) else
-               "--engine hip supports --model 3DCNN / %s --dataset ABCD and --model resnet18 --dataset %s"
-               % (" / ".join(RESNET3D_NAMES), " / ".join(IMAGE_DATASETS)))
+               "--engine hip supports --model 3DCNN / %s --dataset ABCD, --model resnet18 --dataset %s and "
+               "--model %s --dataset cifar10 / cifar100"
+               % (" / ".join(RESNET3D_NAMES), " / ".join(IMAGE_DATASETS), " / ".join(ZOO2D_NAMES)))
         if args.engine == "hip":
             raise RuntimeError(why + "; use --engine torch")
         logging.getLogger(__name__).warning("running on the eager PyTorch engine: %s", why)
@@ -441,6 +447,17 @@ def build_hip_engine(args, algo, info, logger=None):
                                               len(splits))
         mean, std = NORM[args.dataset]
         eng = ResNetHipEngine(model, x8, y, info.device, mean=mean, std=std, augment=bool(getattr(args, "augment", 1)))
+        return eng, model, splits, desc
+    if fam == "batched2d":
+        from .data.images import NORM
+        from .engine.batched2d import BatchedModuleEngine
+        from .models import create_model
+        x8, y, splits, n_cls = image_cohort(args, info, with_val=algo == "fedfomo")
+        model = create_model(args.model, dataset=args.dataset, class_num=n_cls)
+        desc = "%s %s images (%d clients), %s vmapped over clients" % (
+            "synthetic" if not args.data_dir else args.data_dir, args.dataset, len(splits), args.model)
+        mean, std = NORM[args.dataset]
+        eng = BatchedModuleEngine(model, x8, y, info.device, mean, std, augment=bool(getattr(args, "augment", 1)))
         return eng, model, splits, desc
     if fam == "resnet3d":
         from .engine.resnet3d_hip import ResNet3DHipEngine
