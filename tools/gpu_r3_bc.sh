@@ -16,7 +16,9 @@ run tiny_default X=1 -- $T
 run tiny_evalpad0 NIDT_EVAL_PAD=0 -- $T
 run tiny_slab0 NIDT_2D_SLAB=0 -- $T
 run tiny_head0 NIDT_CLS_HEAD=0 -- $T
+run tiny_graphs0 NIDT_HIP_GRAPHS=0 -- $T
 run tiny_default2 X=1 -- $T
 run subavg_default X=1 -- $S
 run subavg_evalpad0 NIDT_EVAL_PAD=0 -- $S
+run subavg_graphs0 NIDT_HIP_GRAPHS=0 -- $S
 run subavg_default2 X=1 -- $S
