@@ -12,6 +12,8 @@ int64_t clip_sgd_mask_workspace(int64_t C, int64_t P);
 void clip_sgd_mask(uintptr_t w, uintptr_t g, uintptr_t buf, uintptr_t mask, uintptr_t part, uintptr_t coef_out,
                    uintptr_t wbf, int64_t C, int64_t P, int64_t stride, float lr, float wd, float mom, int first,
                    float max_norm, uintptr_t lr_dev, int keep_grad, uintptr_t stream);
+int64_t rows_nnz_blocks(int64_t P);
+void rows_nnz(uintptr_t rows, int64_t R, int64_t P, int64_t stride, uintptr_t part, uintptr_t stream);
 void weighted_rows_sum(uintptr_t rows, uintptr_t wts, int64_t C, int64_t P, int64_t stride, float beta, uintptr_t out,
                        uintptr_t stream);
 void broadcast_row(uintptr_t src, int64_t P, int64_t stride, int64_t C, uintptr_t dst, uintptr_t stream);
@@ -205,6 +207,8 @@ PYBIND11_MODULE(_nidt_hip, m) {
   DEF(clip_sgd_mask_workspace);
   DEF(clip_sgd_mask);
   DEF(weighted_rows_sum);
+  DEF(rows_nnz_blocks);
+  DEF(rows_nnz);
   DEF(broadcast_row);
   DEF(conv3d_fwd);
   DEF(conv3d_fwd_splitk);

@@ -364,6 +364,45 @@ void weighted_rows_sum(uintptr_t rows, uintptr_t wts, int64_t C, int64_t P, int6
   NIDT_CHECK(hipGetLastError());
 }
 
+// ---- non-zero count per row (the reference's count_communication_params, once per round per client) ----
+// grid (nblk, R): block b of row r counts [b * chunk, (b + 1) * chunk) with 16-B loads and writes one int32
+// partial (no atomics); the caller sums the [R, nblk] partials.  torch.count_nonzero(dim=1) ran at ~0.15 TB/s.
+__global__ __launch_bounds__(256) void k_rows_nnz(const float* __restrict__ rows, int64_t P, int64_t stride,
+                                                  int64_t chunk, int* __restrict__ part, int nblk) {
+  __shared__ int red[4];
+  const int r = blockIdx.y;
+  const float* row = rows + (int64_t)r * stride;
+  const int64_t s = (int64_t)blockIdx.x * chunk;
+  const int64_t e = s + chunk < P ? s + chunk : P;
+  int cnt = 0;
+  const int64_t e4 = s + ((e - s) & ~int64_t(3));
+  for (int64_t i = s + 4 * threadIdx.x; i < e4; i += 4 * 256) {
+    const float4 v = *reinterpret_cast<const float4*>(row + i);
+    cnt += (v.x != 0.f) + (v.y != 0.f) + (v.z != 0.f) + (v.w != 0.f);
+  }
+  for (int64_t i = e4 + threadIdx.x; i < e; i += 256) cnt += row[i] != 0.f;
+  for (int o = 32; o > 0; o >>= 1) cnt += __shfl_down(cnt, o);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = cnt;
+  __syncthreads();
+  if (threadIdx.x == 0) part[(int64_t)r * nblk + blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+}
+
+int64_t rows_nnz_blocks(int64_t P) {
+  int nb;
+  opt_chunk(P, &nb);
+  return nb;
+}
+
+void rows_nnz(uintptr_t rows, int64_t R, int64_t P, int64_t stride, uintptr_t part, uintptr_t stream) {
+  NIDT_REQUIRE(stride % 4 == 0 && (rows & 15) == 0, "rows_nnz: 16-byte aligned rows");
+  if (R == 0 || P == 0) return;
+  int nblk;
+  const int64_t chunk = opt_chunk(P, &nblk);
+  hipLaunchKernelGGL(k_rows_nnz, dim3(nblk, (unsigned)R), dim3(256), 0, as_stream(stream), ptr<const float>(rows), P,
+                     stride, chunk, ptr<int>(part), nblk);
+  NIDT_CHECK(hipGetLastError());
+}
+
 // ---- broadcast one row into C rows (round start: every client starts from w_global) ----
 __global__ void k_broadcast_row(const float* __restrict__ src, int64_t P, int64_t stride, int C, float* __restrict__ dst) {
   const int64_t i = 4 * ((int64_t)blockIdx.x * blockDim.x + threadIdx.x);

@@ -119,10 +119,13 @@ class HipEngine:
     supports_graphs = True
     input_shape = (1, 121, 145, 121)   # one sample as the model sees it (FLOP counting)
 
-    def train_step(self, theta, bufs, grads, idx, G, B, keep, seed, cids=None, seed_dev=None, bn_train=True):
+    accepts_cids_dev = True  # train_step(cids_dev=...): client ids from a device buffer (graph reuse across groups)
+
+    def train_step(self, theta, bufs, grads, idx, G, B, keep, seed, cids=None, seed_dev=None, bn_train=True,
+                   cids_dev=None):
         y = self.labels.index_select(0, idx.long())
-        ct = None
-        if cids is not None:
+        ct = cids_dev
+        if ct is None and cids is not None:
             key = tuple(int(c) for c in cids)
             ct = self._cid_cache.get(key)
             if ct is None:  # one upload per client group, reused by every step

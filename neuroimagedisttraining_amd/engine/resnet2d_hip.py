@@ -700,11 +700,14 @@ class ResNetHipEngine:
             self._cid_cache[key] = ct
         return ct
 
-    def train_step(self, theta, bufs, grads, idx, G, B, keep, seed, cids=None, seed_dev=None, bn_train=True):
+    accepts_cids_dev = True  # see HipEngine.train_step
+
+    def train_step(self, theta, bufs, grads, idx, G, B, keep, seed, cids=None, seed_dev=None, bn_train=True,
+                   cids_dev=None):
         aug = None
         if self.augment and seed_dev is not None:
             cids = list(range(G)) if cids is None else [int(c) for c in cids]
-            aug = (seed_dev, int(seed), self._cids_dev(cids), cids, B)
+            aug = (seed_dev, int(seed), cids_dev if cids_dev is not None else self._cids_dev(cids), cids, B)
         x = self.net.input(self.x8, idx, aug)
         y = self.labels.index_select(0, idx.long())
         return self.net.train_step(theta, grads, x, y, G, B)

@@ -132,6 +132,7 @@ class FLRunner:
                               global_test_loss=[], person_test_loss=[], round_time=[])
         self.timers = {"train": 0.0, "aggregate": 0.0, "eval": 0.0, "snip": 0.0}
         self._graphs = {}             # step key -> captured local step (None until the shape repeats, False = eager)
+        self.graph_stats = {}         # counts of first-seen (eager) / captured / replayed steps
         # captured steps kept (LRU); engines whose graphs own their activation memory (torch-allocated, e.g. the
         # ResNet engine) set a small limit, the AlexNet engine's graphs only reference its persistent buffers
         self.max_graphs = int(getattr(engine, "graph_cache_limit", 512))
@@ -289,6 +290,11 @@ class FLRunner:
             self._seed_dev = torch.zeros(1, dtype=torch.int64, device=self.device)
         self._lr_dev.fill_(lr)
         side = self._side_streams() if use_graphs else None
+        # client ids of the view's rows on the device: captured steps read a group's ids from a static buffer
+        # refilled before each replay, so a graph serves any clients at the same rows (sampled rounds reuse the
+        # previous rounds' captures instead of capturing every round)
+        cdev = (self._upload_i32([int(c) for c in clients])
+                if use_graphs and getattr(self.e, "accepts_cids_dev", False) else None)
         k = len(clients)
         sums = [] if self.track_loss else None
         if sums is not None:
@@ -313,9 +319,10 @@ class FLRunner:
                     with torch.cuda.stream(st):
                         sdev.fill_(seed)
                         self._graph_step(sub, r0, idx[off:off + n], G, B, spec.rows(r0, r1), cids, seed, fill=False,
-                                         seed_dev=sdev)
+                                         seed_dev=sdev, cids_dev=None if cdev is None else cdev[r0:r1])
                 elif use_graphs:
-                    self._graph_step(sub, r0, idx[off:off + n], G, B, spec.rows(r0, r1), cids, seed)
+                    self._graph_step(sub, r0, idx[off:off + n], G, B, spec.rows(r0, r1), cids, seed,
+                                     cids_dev=None if cdev is None else cdev[r0:r1])
                 else:
                     self._seed_dev.fill_(seed)
                     self._step(sub, r0, idx[off:off + n], G, B, spec.rows(r0, r1), cids, lr)
@@ -361,8 +368,20 @@ class FLRunner:
             th, bu = theta[rows[0]:rows[-1] + 1, :self.P], bufs[rows[0]:rows[-1] + 1, :self.Q]
         else:
             ix = torch.tensor(rows, device=self.device)
-            th, bu = theta.index_select(0, ix)[:, :self.P], bufs.index_select(0, ix)[:, :self.Q]
-        return torch.count_nonzero(th, dim=1) + torch.count_nonzero(bu, dim=1)
+            th, bu = gather_rows(theta, ix)[:, :self.P], gather_rows(bufs, ix)[:, :self.Q]
+        return self._rows_nnz(th) + self._rows_nnz(bu)
+
+    def _rows_nnz(self, mat):
+        """Non-zeros per row of a [R, K] fp32 row view: the HIP row counter on aligned device rows, else torch."""
+        R, K = mat.shape
+        if (self.device.type == "cuda" and R and K and mat.stride(1) == 1 and (R == 1 or mat.stride(0) % 4 == 0)
+                and mat.data_ptr() % 16 == 0 and mat.dtype == torch.float32):
+            m = ops.ext()
+            part = torch.empty((R, m.rows_nnz_blocks(K)), dtype=torch.int32, device=self.device)
+            m.rows_nnz(mat.data_ptr(), R, K, mat.stride(0) if R > 1 else (K + 3) // 4 * 4, part.data_ptr(),
+                       torch.cuda.current_stream().cuda_stream)
+            return part.sum(1, dtype=torch.int64)
+        return torch.count_nonzero(mat, dim=1)
 
     def add_comm(self, per_client, clients=None):
         """Add communication counts (device int64 per client, or a host int) to ``sum_comm_params`` — kept on
@@ -457,58 +476,71 @@ class FLRunner:
         k = hash((int(G), int(B))) % len(self._streams)
         return self._streams[k], self._lane_seed[k]
 
-    def _step(self, sub, r0, idx, G, B, spec, cids, lr, seed_dev=None, lr_dev=None):
+    def _step(self, sub, r0, idx, G, B, spec, cids, lr, seed_dev=None, lr_dev=None, cids_dev=None):
         cfg = self.cfg
         gr = self.grads[r0:r0 + G]
         mo = self.mom_buf[r0:r0 + G] if self.mom_buf is not None else None
+        kw = {} if cids_dev is None else {"cids_dev": cids_dev}
         loss = self.e.train_step(sub.theta, sub.bufs, gr, idx, G, B, cfg.dropout_keep, cfg.seed << 40, cids=cids,
-                                 seed_dev=self._seed_dev if seed_dev is None else seed_dev)
+                                 seed_dev=self._seed_dev if seed_dev is None else seed_dev, **kw)
         if self.track_loss and self._loss_acc is not None and loss is not None:
             self._loss_acc[r0:r0 + G].add_(loss.view(-1).float())
         self.e.local_opt(sub.theta, gr, mo, spec, lr, cfg.wd, cfg.momentum, cfg.max_norm,
                          lr_dev=self._lr_dev if lr_dev is None else lr_dev)
 
-    def _graph_step(self, sub, r0, idx, G, B, spec, cids, seed, fill=True, seed_dev=None):
+    def _graph_step(self, sub, r0, idx, G, B, spec, cids, seed, fill=True, seed_dev=None, cids_dev=None):
         """One lockstep local step (forward+backward of G clients + fused optimizer) as a replayed hipGraph.  The
         ~45 kernel launches of a step become one graph launch; everything that changes between steps lives in
         device memory the graph reads: the sample indices (copied into a static buffer), the dropout stream
         counter and the round's learning rate.  The first step of a shape runs eagerly (it also allocates every
         scratch buffer the graph will reuse), the second is captured and replayed, later ones only replay — same
-        kernels, same arguments, same results as the eager path."""
+        kernels, same arguments, same results as the eager path.  With ``cids_dev`` (engines that take the client
+        ids from device memory) the ids are one more refilled buffer and the key drops them."""
         sdev = self._seed_dev if seed_dev is None else seed_dev
-        key = (sub.theta.data_ptr(), r0, G, B, tuple(int(c) for c in cids), spec.key(), sdev.data_ptr())
+        ckey = tuple(int(c) for c in cids) if cids_dev is None else None
+        key = (sub.theta.data_ptr(), r0, G, B, ckey, spec.key(), sdev.data_ptr())
         ent = self._graphs.get(key, "new")
         if fill:
             sdev.fill_(seed)
+        st = self.graph_stats
         if ent == "new":
+            st["eager_first"] = st.get("eager_first", 0) + 1
             # bounded cache: with client sampling (frac < 1) every round brings new client groups; the oldest
             # captured graphs (and the memory pools they hold) are released first
             if len(self._graphs) >= self.max_graphs and getattr(self, "_streams", None):
                 torch.cuda.synchronize(self.device)  # an evicted graph may still run on a side stream
             while len(self._graphs) >= self.max_graphs:
                 self._graphs.pop(next(iter(self._graphs)))
-            self._step(sub, r0, idx, G, B, spec, cids, 0.0, seed_dev=sdev)
+            self._step(sub, r0, idx, G, B, spec, cids, 0.0, seed_dev=sdev, cids_dev=cids_dev)
             self._graphs[key] = None
             return
         if ent is None:
             idx_buf = torch.empty(G * B, dtype=torch.int32, device=self.device)
             idx_buf.copy_(idx)
+            cid_buf = None
+            if cids_dev is not None:
+                cid_buf = torch.empty(G, dtype=torch.int32, device=self.device)
+                cid_buf.copy_(cids_dev)
             torch.cuda.current_stream().synchronize()
             g = torch.cuda.CUDAGraph()
             try:
                 # thread_local: the RCCL watchdog thread of a multi-GPU run may query events during the capture
                 with torch.cuda.graph(g, capture_error_mode="thread_local"):
-                    self._step(sub, r0, idx_buf, G, B, spec, cids, 0.0, seed_dev=sdev)
+                    self._step(sub, r0, idx_buf, G, B, spec, cids, 0.0, seed_dev=sdev, cids_dev=cid_buf)
             except Exception:  # noqa: BLE001 - capture unsupported here: stay eager for this shape
                 self._graphs[key] = False
-                self._step(sub, r0, idx, G, B, spec, cids, 0.0, seed_dev=sdev)
+                self._step(sub, r0, idx, G, B, spec, cids, 0.0, seed_dev=sdev, cids_dev=cids_dev)
                 return
-            ent = self._graphs[key] = (g, idx_buf)
+            ent = self._graphs[key] = (g, idx_buf, cid_buf)
+            st["captured"] = st.get("captured", 0) + 1
         elif ent is False:
-            self._step(sub, r0, idx, G, B, spec, cids, 0.0, seed_dev=sdev)
+            self._step(sub, r0, idx, G, B, spec, cids, 0.0, seed_dev=sdev, cids_dev=cids_dev)
             return
-        g, idx_buf = ent
+        g, idx_buf, cid_buf = ent
+        st["replayed"] = st.get("replayed", 0) + 1
         idx_buf.copy_(idx)
+        if cid_buf is not None:
+            cid_buf.copy_(cids_dev)
         g.replay()
 
     def local_grad(self, rs, rows, clients, round_idx, bn_train=True, tag=11):
@@ -752,7 +784,7 @@ class FLRunner:
             self.theta[ix] = self.w_global.unsqueeze(0).expand(len(rows), -1)
             self.bufs[ix] = self.b_global.unsqueeze(0).expand(len(rows), -1)
         # downlink: count_communication_params(w_global) per sampled client (the same state for all of them)
-        down = torch.count_nonzero(self.w_global) + torch.count_nonzero(self.b_global)
+        down = self._rows_nnz(self.w_global.view(1, -1))[0] + self._rows_nnz(self.b_global.view(1, -1))[0]
         self.train_rows(RowSet(self.theta, self.bufs), rows, loc, round_idx, self.cfg.epochs, self._fedavg_spec(),
                         lr=lr)
         self.add_comm(down + self.state_nonzeros(self.theta, self.bufs, rows), loc)  # + uplink (the local model)

@@ -840,3 +840,18 @@ def test_modp_matmul_matches_numpy():
     got = TA.matmul_mod_device(A, B, p)
     assert np.array_equal(got, ref)
     assert np.array_equal(TA._matmul_mod(A, B, p), ref)  # dispatches to the device above the size threshold
+
+
+def test_rows_nnz_matches_count_nonzero():
+    """The per-row non-zero counter of the communication accounting (optim.hip rows_nnz) vs torch."""
+    from neuroimagedisttraining_amd.engine.runner import FLRunner
+    g = torch.Generator(device=DEV).manual_seed(3)
+    for R, K in ((5, 2570241), (1, 1001), (3, 7)):
+        m = padded_rows(R, K, DEV)
+        m.copy_(torch.randn(R, K, device=DEV, generator=g) * (torch.rand(R, K, device=DEV, generator=g) < 0.3))
+        m[0, :3] = torch.tensor([-0.0, float("nan"), 0.0], device=DEV)
+        stub = FLRunner.__new__(FLRunner)
+        stub.device = torch.device(DEV)
+        assert torch.equal(stub._rows_nnz(m), torch.count_nonzero(m, dim=1)), (R, K)
+        one = torch.zeros(K + 1, device=DEV)[1:]  # a [K] row at a 4-byte offset: torch fallback path
+        assert int(stub._rows_nnz(one.view(1, -1))[0]) == 0

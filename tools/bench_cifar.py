@@ -110,11 +110,13 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     res = None
+    each = []
     for r in range(args.warmup, args.warmup + args.rounds):
         t1 = time.perf_counter()
         res = runner.run_round(r)
         torch.cuda.synchronize()
-        print("round %d: %.2f s" % (r, time.perf_counter() - t1), flush=True)
+        each.append(time.perf_counter() - t1)
+        print("round %d: %.2f s" % (r, each[-1]), flush=True)
     rt.barrier(info)
     torch.cuda.synchronize()
     dt = rt.max_over_ranks(time.perf_counter() - t0, info)
@@ -127,6 +129,7 @@ def main():
             "value": round(value, 4), "unit": "rounds/s", "n_gpus": info.world, "rounds": args.rounds,
             "warmup": args.warmup, "s_per_round": round(dt / args.rounds, 3), "dtype": "bf16",
             "data": "synthetic", "setup_s": round(t_setup, 1), "warmup_round_s": [round(w, 2) for w in walls],
+            "s_round_each": [round(w, 3) for w in each], "graph_stats": dict(getattr(runner, "graph_stats", {})),
             "reference_v100": ({"bound": bound[0] + str(bound[1]), "source": bound[2],
                                 "vs_bound": round(value / bound[1], 1)} if (bound and not tiny) else None),
             "config": {"model": "resnet18 (GroupNorm32)", "clients": args.clients, "frac": args.frac,
