@@ -4,7 +4,9 @@ The default synthetic cohort is too easy to reveal a numerics regression (accura
 uses a weak label signal: the fp32 reference needs ~10 rounds to leave the majority-class plateau, and the HIP
 engine's global loss / accuracy trajectories must track it (round by round before the transition, without lagging
 after it).  6 clients, SalientGrads (SNIP mask + masked FedAvg), 20 rounds, every
-round evaluated."""
+round evaluated.  The fp32 side is the recorded trajectory of the fp32 engine on this cohort; the extended tier
+(``NIDT_EXTENDED_GPU_TESTS=1``) recomputes it and checks the record is current."""
+import json
 import os
 
 import numpy as np
@@ -39,14 +41,33 @@ def _trajectory(kind, vol, labels, splits):
     return np.array(r.stat_info["global_test_acc"]), np.array(r.stat_info["global_test_loss"])
 
 
-def test_hip_bf16_tracks_fp32_over_twenty_rounds():
+REF = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data", "convergence_fp32_reference.json")
+
+
+def _cohort():
     from neuroimagedisttraining_amd.data.synthetic_fl import build_fl_volumes
-    from neuroimagedisttraining_amd.engine.executor import ClientSplit
     C = 6
     vol, labels, local = build_fl_volumes(list(range(C)), C, 32, 16, DEV, seed=21, alpha=1.0, label_signal=0.25)
-    splits = [local[c] for c in range(C)]
+    return vol, labels, [local[c] for c in range(C)]
+
+
+def _reference():
+    with open(REF) as f:
+        d = json.load(f)
+    return np.array(d["acc"]), np.array(d["loss"])
+
+
+def test_hip_bf16_tracks_fp32_over_twenty_rounds():
+    """HIP bf16 trajectory against the fp32 engine's trajectory on the same cohort.  The fp32 run (~4-5 minutes of
+    MIOpen fp32 at full resolution) is the recorded one (``tests/data/convergence_fp32_reference.json``); the
+    extended tier recomputes it live (:func:`test_fp32_reference_trajectory_is_current` and
+    ``NIDT_CONVERGENCE_LIVE=1`` here)."""
+    vol, labels, splits = _cohort()
     acc_h, loss_h = _trajectory("hip", vol, labels, splits)
-    acc_t, loss_t = _trajectory("torch", vol, labels, splits)
+    if os.environ.get("NIDT_CONVERGENCE_LIVE", "0") == "1":
+        acc_t, loss_t = _trajectory("torch", vol, labels, splits)
+    else:
+        acc_t, loss_t = _reference()
     print("fp32 acc ", np.round(acc_t, 3).tolist())
     print("bf16 acc ", np.round(acc_h, 3).tolist())
     print("fp32 loss", np.round(loss_t, 4).tolist())
@@ -64,3 +85,14 @@ def test_hip_bf16_tracks_fp32_over_twenty_rounds():
     assert np.mean(acc_h[-5:]) >= np.mean(acc_t[-5:]) - 0.05                     # no accuracy lag
     assert abs(np.mean(acc_h[-5:]) - np.mean(acc_t[-5:])) <= 0.1
     assert np.mean(loss_h[-5:]) <= 1.05 * np.mean(loss_t[-5:])                   # no loss lag
+
+
+@pytest.mark.extended
+def test_fp32_reference_trajectory_is_current():
+    """The recorded fp32 trajectory is what the fp32 engine produces today: rounds 0-9 (before the chaotic
+    transition) within the run-to-run spread of fp32 itself (1.7 % under 1e-6 weight noise, r3 ablation)."""
+    vol, labels, splits = _cohort()
+    acc_t, loss_t = _trajectory("torch", vol, labels, splits)
+    acc_r, loss_r = _reference()
+    assert np.max(np.abs(loss_t[:10] - loss_r[:10]) / loss_r[:10]) <= 0.02
+    assert acc_t[-5:].max() > 0.85
