@@ -665,7 +665,16 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void k_conv_fwd_tri(ConvFwdArgs a,
 // per tap as in k_conv_fwd_tri; 256-position blocks and the k_conv_fwd_dma epilogue / statistics layout.  Depth taps
 // that read only padding for every position of a block (border output planes of the padded data gradient) are
 // skipped.  LDS: 48 KB union + 2 weight tiles (16 / 32 KB): two blocks per CU also at 128 output channels.
-template <int BCO, int WM, int WN, int U, bool PADDED, bool BIAS, bool STATS>
+// [LSWZ] the 16-B chunk swizzle of a union row is keyed by the row's output-space index L = (d Ho + h) Wo + w (its
+// padded coordinates of the kd = 0 union) instead of its union position u: the 16 positions of a B fragment read the
+// 16 CONSECUTIVE L values p + kh Wo + kw for every tap, across output-row and plane boundaries, where their union
+// positions jump by Wp - Wo + 1 (3 for a 3x3 window).  With the pair swizzle ((x >> 1) & 3) << 1 the rows of one
+// ds_read_b128 lane group then land on 16 distinct 4-bank slots; keyed by u, every fragment that crosses an output
+// row put two rows on one slot (modelled: 1.84 / 1.79 LDS cycles per B read for the AlexNet conv2 forward / data
+// gradient -> 1.00; measured 23-28 % LDS bank-conflict cycles, profiles/r3_s2_pmc_alexnet_g64.txt).
+__device__ __forceinline__ int swz_l(int l) { return ((l >> 1) & 3) << 1; }
+
+template <int BCO, int WM, int WN, int U, bool PADDED, bool BIAS, bool STATS, bool LSW = true>
 __global__ __launch_bounds__(64 * WM * WN, 2) void k_conv_fwd_slab(ConvFwdArgs a, int nCO, const int* __restrict__ utab) {
   constexpr int NW = WM * WN, BP = 64 * WN, BK = 64;
   constexpr int WCO = BCO / WM, WP = 64, TCO = WCO / 16, TP = WP / 16;
@@ -707,13 +716,20 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void k_conv_fwd_slab(ConvFwdArgs a
     uoff[i] = 0;
     ucode[i] = 1023;
     if (wid * UPW + i < UP) {
-      uoff[i] = ent[2 * u] * (Cin * 2) + ((slot ^ swz_un(u)) << 4);
-      ucode[i] = ent[2 * u + 1];
+      const int c = ent[2 * u + 1];
+      const int sw = LSW ? swz_l(((c & 1023) * a.Ho + ((c >> 10) & 1023)) * a.Wo + (c >> 20)) : swz_un(u);
+      uoff[i] = ent[2 * u] * (Cin * 2) + ((slot ^ sw) << 4);
+      ucode[i] = c;
     }
   }
-  int hrow[TP];
+  int hrow[TP], hl[TP];  // union row and output-space index L of tap (0, 0) of each fragment position
+  const int So = a.Do * a.Ho * a.Wo;
 #pragma unroll
-  for (int j = 0; j < TP; ++j) hrow[j] = ent[2 * U + wp * WP + j * 16 + fr];
+  for (int j = 0; j < TP; ++j) {
+    const int pl = wp * WP + j * 16 + fr;
+    hrow[j] = ent[2 * U + pl];
+    hl[j] = (pb * BP + pl) % So;
+  }
   int aoff[A_INSTR];
 #pragma unroll
   for (int i = 0; i < A_INSTR; ++i) {
@@ -764,7 +780,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void k_conv_fwd_slab(ConvFwdArgs a
     const int ql = ks / 9, t = ks - 9 * ql, kh = t / 3, kw = t - 3 * kh;
     if (ks + 1 < nks) issue_a(ks + 1, (ks + 1) & 1);
     const uint16_t* sA = sAb + (ks & 1) * A_ELEMS;
-    const int toff = kh * Wp + kw;
+    const int toff = kh * Wp + kw, loff = kh * a.Wo + kw;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       bf16x8 fa[TCO], fb[TP];
@@ -776,7 +792,8 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void k_conv_fwd_slab(ConvFwdArgs a
 #pragma unroll
       for (int j = 0; j < TP; ++j) {
         const int r = hrow[j] + toff;
-        fb[j] = *reinterpret_cast<const bf16x8*>(&sU[r * BK + (((4 * kk + fq) ^ swz_un(r)) << 3)]);
+        const int sw = LSW ? swz_l(hl[j] + loff) : swz_un(r);
+        fb[j] = *reinterpret_cast<const bf16x8*>(&sU[r * BK + (((4 * kk + fq) ^ sw) << 3)]);
       }
 #pragma unroll
       for (int i = 0; i < TCO; ++i)
@@ -1488,8 +1505,13 @@ static void fwd_slab_impl(uintptr_t x, uintptr_t w, uintptr_t bias, int64_t bias
   const dim3 grid((unsigned)((int64_t)a.nPB * nCO * G));
   hipStream_t s = as_stream(stream);
   const int* tab = ptr<const int>(utab);
+  static const int lswz = [] {  // NIDT_SLAB_LSWZ=0: union-position swizzle (A/B)
+    const char* e = getenv("NIDT_SLAB_LSWZ");
+    return e ? atoi(e) : 1;
+  }();
 #define NIDT_FS(BC, WM, PD, BI, STT) \
-  hipLaunchKernelGGL((k_conv_fwd_slab<BC, WM, 4, 384, PD, BI, STT>), grid, dim3(256 * WM), 0, s, a, nCO, tab)
+  if (lswz) hipLaunchKernelGGL((k_conv_fwd_slab<BC, WM, 4, 384, PD, BI, STT, true>), grid, dim3(256 * WM), 0, s, a, nCO, tab); \
+  else hipLaunchKernelGGL((k_conv_fwd_slab<BC, WM, 4, 384, PD, BI, STT, false>), grid, dim3(256 * WM), 0, s, a, nCO, tab)
 #define NIDT_FS_B(BC, WM, PD) \
   if (st) NIDT_FS(BC, WM, PD, true, true); else if (hb) NIDT_FS(BC, WM, PD, true, false); else NIDT_FS(BC, WM, PD, false, false);
   if (bco == 128) {
@@ -1497,12 +1519,14 @@ static void fwd_slab_impl(uintptr_t x, uintptr_t w, uintptr_t bias, int64_t bias
   } else if (slab_u(B, D, H, W, pad) == 416) {
 #undef NIDT_FS
 #define NIDT_FS(BC, WM, PD, BI, STT) \
-  hipLaunchKernelGGL((k_conv_fwd_slab<BC, WM, 4, 416, PD, BI, STT>), grid, dim3(256 * WM), 0, s, a, nCO, tab)
+  if (lswz) hipLaunchKernelGGL((k_conv_fwd_slab<BC, WM, 4, 416, PD, BI, STT, true>), grid, dim3(256 * WM), 0, s, a, nCO, tab); \
+  else hipLaunchKernelGGL((k_conv_fwd_slab<BC, WM, 4, 416, PD, BI, STT, false>), grid, dim3(256 * WM), 0, s, a, nCO, tab)
     if (pad) { NIDT_FS_B(64, 1, true) } else { NIDT_FS_B(64, 1, false) }
   } else {
 #undef NIDT_FS
 #define NIDT_FS(BC, WM, PD, BI, STT) \
-  hipLaunchKernelGGL((k_conv_fwd_slab<BC, WM, 4, 384, PD, BI, STT>), grid, dim3(256 * WM), 0, s, a, nCO, tab)
+  if (lswz) hipLaunchKernelGGL((k_conv_fwd_slab<BC, WM, 4, 384, PD, BI, STT, true>), grid, dim3(256 * WM), 0, s, a, nCO, tab); \
+  else hipLaunchKernelGGL((k_conv_fwd_slab<BC, WM, 4, 384, PD, BI, STT, false>), grid, dim3(256 * WM), 0, s, a, nCO, tab)
     if (pad) { NIDT_FS_B(64, 1, true) } else { NIDT_FS_B(64, 1, false) }
   }
 #undef NIDT_FS_B

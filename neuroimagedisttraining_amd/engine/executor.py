@@ -25,6 +25,7 @@ from __future__ import annotations
 import math
 import time
 from dataclasses import dataclass, field
+from typing import Optional
 
 import numpy as np
 import torch
@@ -72,7 +73,9 @@ class FLConfig:
     sparse_aggregate: bool = True  # SalientGrads: all-reduce only the coordinates kept by the global mask
     update_topk: float = 0.0      # >0: each client sends only its top-k |update| (values + int32 indices,
                                   # k = update_topk * P) through an RCCL all-gather (BASELINE config 5)
-    hip_graphs: bool = True       # capture each lockstep local step (train + optimizer) in a hipGraph and replay it
+    # capture each lockstep local step (train + optimizer) in a hipGraph and replay it: True / False force it,
+    # None = the engine's measured default (``graphs_default``: on for AlexNet3D, off for ResNet-18-GN)
+    hip_graphs: Optional[bool] = None
     step_streams: int = 4         # side HIP streams for the extra launches of one lockstep step (ragged clients)
     stratified_sampling: bool = False  # IterSNIP: label-stratified SNIP batches (sailentgrads/client.py:33-43)
     fix_eval_loss: bool = False   # evaluation loss on logits instead of the reference's sigmoid-then-BCEWithLogits (Q1)

@@ -688,6 +688,10 @@ class ResNetHipEngine:
         if self.net.hip:
             ops.ext()  # fail loudly on a GPU box without the extension
         self.supports_graphs = self.device.type == "cuda"
+        # replaying captured steps measured ~3 % slower than eager launches for this engine (CIFAR SubAvg 0.810 vs
+        # 0.786 s/round with the graphs reused across rounds, Tiny 1.969 vs 1.965 s; profiles/r4_graphs_ab.txt):
+        # eager unless FLConfig.hip_graphs=True
+        self.graphs_default = False
         self.graph_cache_limit = 24  # each captured step holds its own activation pool
         self._opt = None
         self._cid_cache = {}

@@ -283,7 +283,8 @@ class FLRunner:
         cfg = self.cfg
         lr = cfg.lr * (cfg.lr_decay ** round_idx) if lr is None else lr
         self._zero_mom(len(clients))
-        use_graphs = (cfg.hip_graphs and getattr(self.e, "supports_graphs", False) and self.device.type == "cuda"
+        hg = cfg.hip_graphs if cfg.hip_graphs is not None else getattr(self.e, "graphs_default", True)
+        use_graphs = (hg and getattr(self.e, "supports_graphs", False) and self.device.type == "cuda"
                       and os.environ.get("NIDT_HIP_GRAPHS", "1") != "0")  # NIDT_HIP_GRAPHS=0: eager steps (A/B)
         if self._lr_dev is None:
             self._lr_dev = torch.zeros(1, dtype=torch.float32, device=self.device)
