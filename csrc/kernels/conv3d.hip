@@ -671,7 +671,10 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void k_conv_fwd_tri(ConvFwdArgs a,
 // positions jump by Wp - Wo + 1 (3 for a 3x3 window).  With the pair swizzle ((x >> 1) & 3) << 1 the rows of one
 // ds_read_b128 lane group then land on 16 distinct 4-bank slots; keyed by u, every fragment that crosses an output
 // row put two rows on one slot (modelled: 1.84 / 1.79 LDS cycles per B read for the AlexNet conv2 forward / data
-// gradient -> 1.00; measured 23-28 % LDS bank-conflict cycles, profiles/r3_s2_pmc_alexnet_g64.txt).
+// gradient -> 1.00; measured 23-28 % LDS bank-conflict cycles, profiles/r3_s2_pmc_alexnet_g64.txt).  Measured
+// (profiles/r4_ab_lds_swizzle.txt): bank conflicts 23.4 / 28.3 % -> 0.1 %, but conv2 forward / data gradient time
+// unchanged (2.55 / 3.30 vs 2.55 / 3.25 ms) — the B reads are not what these blocks wait on.  Opt-in
+// (NIDT_SLAB_LSWZ=1); the union-position swizzle stays the default.
 __device__ __forceinline__ int swz_l(int l) { return ((l >> 1) & 3) << 1; }
 
 template <int BCO, int WM, int WN, int U, bool PADDED, bool BIAS, bool STATS, bool LSW = true>
@@ -1505,9 +1508,9 @@ static void fwd_slab_impl(uintptr_t x, uintptr_t w, uintptr_t bias, int64_t bias
   const dim3 grid((unsigned)((int64_t)a.nPB * nCO * G));
   hipStream_t s = as_stream(stream);
   const int* tab = ptr<const int>(utab);
-  static const int lswz = [] {  // NIDT_SLAB_LSWZ=0: union-position swizzle (A/B)
+  static const int lswz = [] {  // NIDT_SLAB_LSWZ=1: output-space swizzle (A/B: no gain measured, see [LSWZ])
     const char* e = getenv("NIDT_SLAB_LSWZ");
-    return e ? atoi(e) : 1;
+    return e ? atoi(e) : 0;
   }();
 #define NIDT_FS(BC, WM, PD, BI, STT) \
   if (lswz) hipLaunchKernelGGL((k_conv_fwd_slab<BC, WM, 4, 384, PD, BI, STT, true>), grid, dim3(256 * WM), 0, s, a, nCO, tab); \
@@ -2140,7 +2143,13 @@ static int wgrad_tri_umax(int B, int D, int H, int W, int pad) { return union_um
 // largest union (rows) of a P-position band: exposed for host-side tests of the union rule
 int conv3d_union_umax(int B, int D, int H, int W, int pad, int P) { return union_umax(B, D, H, W, pad, P); }
 
-template <int NCH, int U, bool PADDED>
+// [LSW] as k_conv_fwd_slab: the X union rows' chunk swizzle is keyed by their output-space index L = (d Ho + h) Wo + w
+// (the positions of one ds_read_b64_tr_b16 read L = p + kw for 8 positions p, consecutive within the step except at
+// the 32-position kk halves, where the union rows jump at output-row ends; modelled for conv2: 1.52 LDS cycles per X
+// read -> 1.00).  The dY rows are the step's positions themselves and keep swz_wd of their row.  Measured: conflicts
+// 20.8 / 33.2 % -> 0.1 / 1.7 % (conv2 / conv3-5) but conv2 2.92-2.98 -> 3.22-3.29 ms (the per-step swizzle of the
+// DMA addresses sits on the issue path); opt-in NIDT_WGTRI_LSWZ=1 (profiles/r4_ab_lds_swizzle.txt).
+template <int NCH, int U, bool PADDED, bool LSW = true>
 __global__ __launch_bounds__(192 * NCH, 2) void k_conv_wgrad_tri(ConvWgTriArgs a) {
   constexpr int NW = 3 * NCH, XG = U * kWdRow, BUFE = XG + NCH * kWdGroup, ST = WtTab<U>::kST;
   constexpr int XP = U / 8, XPW = (XP + NW - 1) / NW;       // union pieces (8 rows each) per wave
@@ -2168,8 +2177,9 @@ __global__ __launch_bounds__(192 * NCH, 2) void k_conv_wgrad_tri(ConvWgTriArgs a
 #pragma unroll
   for (int i = 0; i < XPW; ++i) {
     const int u = 8 * (wid * XPW + i) + lr;
-    xcol[i] = (cc * 64 + ((ls ^ swz_wd(u)) << 3)) * 2;
+    xcol[i] = (cc * 64 + (LSW ? 0 : ((ls ^ swz_wd(u)) << 3))) * 2;
   }
+  const int Ho = a.H + 2 * a.pad - 2, Wo = a.W + 2 * a.pad - 2, So = (a.D + 2 * a.pad - 2) * Ho * Wo;
 #pragma unroll
   for (int i = 0; i < DPW; ++i) {
     const int dp = min(wid * DPW + i, DP - 1), h = dp >> 3, sl = dp & 7, r = 8 * sl + lr;
@@ -2202,7 +2212,8 @@ __global__ __launch_bounds__(192 * NCH, 2) void k_conv_wgrad_tri(ConvWgTriArgs a
                                    (unsigned)(((c_ >> 10) & 1023) - hlo) < (unsigned)a.H &&                   \
                                    (unsigned)((c_ >> 20) - a.pad) < (unsigned)a.W)                            \
                                 : (c_ & 1023) != 1023;                                                        \
-        blds16(rx, ok_ ? (trow[i_].x + xadd) * (2 * Cin) + xcol[i_] : kBufOOB, sX_ + (wid * XPW + i_) * 512);  \
+        const int sw_ = LSW ? ((ls ^ swz_wd(((c_ & 1023) * Ho + ((c_ >> 10) & 1023)) * Wo + (c_ >> 20))) << 4) : 0; \
+        blds16(rx, ok_ ? (trow[i_].x + xadd) * (2 * Cin) + xcol[i_] + sw_ : kBufOOB, sX_ + (wid * XPW + i_) * 512); \
       }                                                                                                       \
     _Pragma("unroll") for (int i_ = 0; i_ < DPW; ++i_)                                                        \
       if (wid * DPW + i_ < DP) blds16(rd, (S) * 64 * (2 * a.Cout) + dcol[i_], sD_ + dls[i_]);               \
@@ -2215,6 +2226,10 @@ __global__ __launch_bounds__(192 * NCH, 2) void k_conv_wgrad_tri(ConvWgTriArgs a
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int s0 = p_begin / 64, nsteps = (p_end - p_begin + 63) / 64;
+  // output-space index (within the sample) of the four fragment positions of this lane, advanced by 64 per step
+  int lpos[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) lpos[k] = (s0 * 64 + 32 * (k >> 1) + ((k & 1) ? rr1 : rr0)) % So;
   if (nsteps > 0) {
     WT_FETCH_ROWS(s0)
     WT_FETCH_IDX(s0, tixn)
@@ -2239,19 +2254,25 @@ __global__ __launch_bounds__(192 * NCH, 2) void k_conv_wgrad_tri(ConvWgTriArgs a
     for (int kk = 0; kk < 2; ++kk) {
       const int ra = 32 * kk + rr0, rb = 32 * kk + rr1;
       const int xa = tix[2 * kk] + kw, xb = tix[2 * kk + 1] + kw;
+      const int sxa = swz_wd(LSW ? lpos[2 * kk] + kw : xa), sxb = swz_wd(LSW ? lpos[2 * kk + 1] + kw : xb);
       bf16x8 fa[4], fb[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int c = 2 * i + (pp >> 1);
         fa[i] = tr_pair(sD + ra * kWdRow + ((c ^ swz_wd(ra)) << 3) + (pp & 1) * 4,
                         sD + rb * kWdRow + ((c ^ swz_wd(rb)) << 3) + (pp & 1) * 4);
-        fb[i] = tr_pair(sX + xa * kWdRow + ((c ^ swz_wd(xa)) << 3) + (pp & 1) * 4,
-                        sX + xb * kWdRow + ((c ^ swz_wd(xb)) << 3) + (pp & 1) * 4);
+        fb[i] = tr_pair(sX + xa * kWdRow + ((c ^ sxa) << 3) + (pp & 1) * 4,
+                        sX + xb * kWdRow + ((c ^ sxb) << 3) + (pp & 1) * 4);
       }
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      lpos[k] += 64;
+      lpos[k] -= lpos[k] >= So ? So : 0;  // So >= 64 for every eligible shape (host check)
     }
     // retire the next stage's LDS-DMA; the step-table loads issued after it (rows for st+2, idx for st+1) may stay
     if (st + 2 < nsteps) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(XPW + 4) : "memory");
@@ -2516,9 +2537,19 @@ void conv3d_wgrad_tri(uintptr_t x, uintptr_t dy, uintptr_t part, uintptr_t grad,
   NIDT_REQUIRE(nwg < (1ll << 31), "conv3d_wgrad_tri: grid too large");
   hipStream_t s = as_stream(stream);
   const dim3 grid((unsigned)nwg);
+  static const int lsw_env = [] {  // NIDT_WGTRI_LSWZ=1: output-space swizzle of the X rows (A/B: slower, see [LSW])
+    const char* e = getenv("NIDT_WGTRI_LSWZ");
+    return e ? atoi(e) : 0;
+  }();
+  const bool lsw = lsw_env && d.Mg / B >= 64;  // the kernel advances its output-space indices by 64 per step
 #define NIDT_TRI(NC, UU)                                                                                       \
-  if (pad) hipLaunchKernelGGL((k_conv_wgrad_tri<NC, UU, true>), grid, dim3(192 * NC), 0, s, d);                \
-  else hipLaunchKernelGGL((k_conv_wgrad_tri<NC, UU, false>), grid, dim3(192 * NC), 0, s, d);
+  if (lsw) {                                                                                                   \
+    if (pad) hipLaunchKernelGGL((k_conv_wgrad_tri<NC, UU, true, true>), grid, dim3(192 * NC), 0, s, d);        \
+    else hipLaunchKernelGGL((k_conv_wgrad_tri<NC, UU, false, true>), grid, dim3(192 * NC), 0, s, d);           \
+  } else {                                                                                                     \
+    if (pad) hipLaunchKernelGGL((k_conv_wgrad_tri<NC, UU, true, false>), grid, dim3(192 * NC), 0, s, d);       \
+    else hipLaunchKernelGGL((k_conv_wgrad_tri<NC, UU, false, false>), grid, dim3(192 * NC), 0, s, d);          \
+  }
   if (nch == 2) {
     if (U == 80) { NIDT_TRI(2, 80) } else { NIDT_TRI(2, 96) }
   } else {
