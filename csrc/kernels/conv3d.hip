@@ -677,7 +677,10 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void k_conv_fwd_tri(ConvFwdArgs a,
 // (NIDT_SLAB_LSWZ=1); the union-position swizzle stays the default.
 __device__ __forceinline__ int swz_l(int l) { return ((l >> 1) & 3) << 1; }
 
-template <int BCO, int WM, int WN, int U, bool PADDED, bool BIAS, bool STATS, bool LSW = true>
+// [NA] weight-tile stages: 2 = double buffer (the tile of k-step ks + 1 lands under k-step ks), 3 = two tiles in
+// flight (the 64-channel blocks: 3 x 8 KB + the union still leave two blocks per CU).  Measured not faster (conv2
+// data gradient 3.32-3.35 vs 3.25 ms, profiles/r4_ab_slab_stages.txt): NA = 3 is opt-in (NIDT_SLAB_NA=3).
+template <int BCO, int WM, int WN, int U, bool PADDED, bool BIAS, bool STATS, bool LSW = true, int NA = 2>
 __global__ __launch_bounds__(64 * WM * WN, 2) void k_conv_fwd_slab(ConvFwdArgs a, int nCO, const int* __restrict__ utab) {
   constexpr int NW = WM * WN, BP = 64 * WN, BK = 64;
   constexpr int WCO = BCO / WM, WP = 64, TCO = WCO / 16, TP = WP / 16;
@@ -685,9 +688,10 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void k_conv_fwd_slab(ConvFwdArgs a
   constexpr int A_INSTR = BCO / (8 * NW);
   constexpr int UP = U / 8, UPW = (UP + NW - 1) / NW;  // union pieces (8 rows) per wave
   static_assert(A_INSTR >= 1 && U % 8 == 0, "tile split");
-  __shared__ __attribute__((aligned(16))) uint16_t smem[2 * A_ELEMS + U * BK];
+  static_assert(NA == 2 || NA == 3, "weight stages");
+  __shared__ __attribute__((aligned(16))) uint16_t smem[NA * A_ELEMS + U * BK];
   uint16_t* const sAb = smem;
-  uint16_t* const sU = smem + 2 * A_ELEMS;
+  uint16_t* const sU = smem + NA * A_ELEMS;
 
   const int nwg = gridDim.x;
   const int id = xcd_remap(blockIdx.x, nwg);
@@ -777,12 +781,20 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void k_conv_fwd_slab(ConvFwdArgs a
 
   issue_u(q0);
   issue_a(0, 0);
+  if (NA == 3 && nks > 1) issue_a(1, 1);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
+  int bcur = 0;  // buffer of k-step ks (ks % NA)
   for (int ks = 0; ks < nks; ++ks) {
     const int ql = ks / 9, t = ks - 9 * ql, kh = t / 3, kw = t - 3 * kh;
-    if (ks + 1 < nks) issue_a(ks + 1, (ks + 1) & 1);
-    const uint16_t* sA = sAb + (ks & 1) * A_ELEMS;
+    const int bnext = bcur + 1 == NA ? 0 : bcur + 1;
+    if (NA == 2) {
+      if (ks + 1 < nks) issue_a(ks + 1, bnext);
+    } else if (ks + 2 < nks) {
+      issue_a(ks + 2, bnext + 1 == NA ? 0 : bnext + 1);
+    }
+    const uint16_t* sA = sAb + bcur * A_ELEMS;
+    bcur = bnext;
     const int toff = kh * Wp + kw, loff = kh * a.Wo + kw;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
@@ -803,7 +815,9 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void k_conv_fwd_slab(ConvFwdArgs a
 #pragma unroll
         for (int j = 0; j < TP; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
     }
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    // the tile of k-step ks + 1 must have landed; with three stages the one of ks + 2 may stay in flight
+    if (NA == 3 && ks + 2 < nks) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(A_INSTR) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     if (t == 8 && ql + 1 < nq) {  // every wave is done with this slab's union: reload it for the next one
       issue_u(q0 + ql + 1);
@@ -1512,28 +1526,29 @@ static void fwd_slab_impl(uintptr_t x, uintptr_t w, uintptr_t bias, int64_t bias
     const char* e = getenv("NIDT_SLAB_LSWZ");
     return e ? atoi(e) : 0;
   }();
-#define NIDT_FS(BC, WM, PD, BI, STT) \
-  if (lswz) hipLaunchKernelGGL((k_conv_fwd_slab<BC, WM, 4, 384, PD, BI, STT, true>), grid, dim3(256 * WM), 0, s, a, nCO, tab); \
-  else hipLaunchKernelGGL((k_conv_fwd_slab<BC, WM, 4, 384, PD, BI, STT, false>), grid, dim3(256 * WM), 0, s, a, nCO, tab)
-#define NIDT_FS_B(BC, WM, PD) \
-  if (st) NIDT_FS(BC, WM, PD, true, true); else if (hb) NIDT_FS(BC, WM, PD, true, false); else NIDT_FS(BC, WM, PD, false, false);
+  static const int na3 = [] {  // NIDT_SLAB_NA=3: three weight-tile stages for the 64-channel blocks (A/B)
+    const char* e = getenv("NIDT_SLAB_NA");
+    return e ? (atoi(e) == 3) : 0;
+  }();
+#define NIDT_FS_U(BC, WM, UU, PD, BI, STT)                                                                         \
+  if (lswz) hipLaunchKernelGGL((k_conv_fwd_slab<BC, WM, 4, UU, PD, BI, STT, true>), grid, dim3(256 * WM), 0, s, a,   \
+                               nCO, tab);                                                                          \
+  else if (na3 && BC == 64)                                                                                        \
+    hipLaunchKernelGGL((k_conv_fwd_slab<BC, WM, 4, UU, PD, BI, STT, false, (BC == 64 ? 3 : 2)>), grid,            \
+                       dim3(256 * WM), 0, s, a, nCO, tab);                                                         \
+  else hipLaunchKernelGGL((k_conv_fwd_slab<BC, WM, 4, UU, PD, BI, STT, false>), grid, dim3(256 * WM), 0, s, a, nCO, tab)
+#define NIDT_FS_B(BC, WM, UU, PD)                                                                                  \
+  if (st) NIDT_FS_U(BC, WM, UU, PD, true, true); else if (hb) NIDT_FS_U(BC, WM, UU, PD, true, false);            \
+  else NIDT_FS_U(BC, WM, UU, PD, false, false);
   if (bco == 128) {
-    if (pad) { NIDT_FS_B(128, 2, true) } else { NIDT_FS_B(128, 2, false) }
+    if (pad) { NIDT_FS_B(128, 2, 384, true) } else { NIDT_FS_B(128, 2, 384, false) }
   } else if (slab_u(B, D, H, W, pad) == 416) {
-#undef NIDT_FS
-#define NIDT_FS(BC, WM, PD, BI, STT) \
-  if (lswz) hipLaunchKernelGGL((k_conv_fwd_slab<BC, WM, 4, 416, PD, BI, STT, true>), grid, dim3(256 * WM), 0, s, a, nCO, tab); \
-  else hipLaunchKernelGGL((k_conv_fwd_slab<BC, WM, 4, 416, PD, BI, STT, false>), grid, dim3(256 * WM), 0, s, a, nCO, tab)
-    if (pad) { NIDT_FS_B(64, 1, true) } else { NIDT_FS_B(64, 1, false) }
+    if (pad) { NIDT_FS_B(64, 1, 416, true) } else { NIDT_FS_B(64, 1, 416, false) }
   } else {
-#undef NIDT_FS
-#define NIDT_FS(BC, WM, PD, BI, STT) \
-  if (lswz) hipLaunchKernelGGL((k_conv_fwd_slab<BC, WM, 4, 384, PD, BI, STT, true>), grid, dim3(256 * WM), 0, s, a, nCO, tab); \
-  else hipLaunchKernelGGL((k_conv_fwd_slab<BC, WM, 4, 384, PD, BI, STT, false>), grid, dim3(256 * WM), 0, s, a, nCO, tab)
-    if (pad) { NIDT_FS_B(64, 1, true) } else { NIDT_FS_B(64, 1, false) }
+    if (pad) { NIDT_FS_B(64, 1, 384, true) } else { NIDT_FS_B(64, 1, 384, false) }
   }
 #undef NIDT_FS_B
-#undef NIDT_FS
+#undef NIDT_FS_U
   NIDT_CHECK(hipGetLastError());
 }
 
