@@ -24,7 +24,7 @@ def _args(algo, argv):
     ("subavg", [], "resnet2d"),
     ("ditto", ["--dataset", "cifar100"], "resnet2d"),
     ("fedavg", ["--model", "resnet3d_50"], "resnet3d"),
-    ("subavg", ["--model", "vgg11"], None),
+    ("subavg", ["--model", "vgg11"], "batched2d"),  # the other CIFAR models: vmapped client batches
     ("local", ["--dataset", "tiny"], "resnet2d"),  # tiny_resnet18 (64x64, 200 classes) on the same engine
     ("local", ["--dataset", "tiny", "--model", "vgg16"], None),
 ])
