@@ -79,13 +79,18 @@ def main():
     rt.barrier(info)
     t0 = time.perf_counter()
     res = None
-    per_round = []
+    per_round, peaks, phases = [], [], []
     for r in range(args.rounds):
+        if dev.type == "cuda":
+            torch.cuda.reset_peak_memory_stats()
+        t_before = dict(runner.timers)
         tr = time.perf_counter()
-        res = runner.run_round(r)
+        res = runner.run_round(r, sync_timers=True)
         if dev.type == "cuda":
             torch.cuda.synchronize()
+            peaks.append(round(torch.cuda.max_memory_allocated() / 2 ** 30, 1))
         per_round.append(rt.max_over_ranks(time.perf_counter() - tr, info))
+        phases.append({k: round(v - t_before.get(k, 0.0), 3) for k, v in runner.timers.items()})
     dt = rt.max_over_ranks(time.perf_counter() - t0, info)
     peak = torch.cuda.max_memory_allocated() / 2 ** 30 if dev.type == "cuda" else 0.0
     if info.is_main:
@@ -97,7 +102,8 @@ def main():
                           "steady_s_per_round": (round(float(np.mean(per_round[args.warmup:])), 2)
                                                  if args.rounds > args.warmup else None),
                           "s_round_each": [round(x, 2) for x in per_round], "hip_convs": n_hip,
-                          "peak_hbm_gib_rank0": round(peak, 1),
+                          "peak_hbm_gib_rank0": round(peak, 1), "peak_gib_each_round": peaks,
+                          "phase_s_each_round": phases,
                           "update_topk": args.topk, "aggregate_elems": runner.stat_info.get("aggregate_elems"),
                           "metrics": res}), flush=True)
     rt.shutdown(info)

@@ -30,6 +30,18 @@ def main(db, top=30, out=None, window_ms=None):
         lines.append("%-90s %8d %12.3f %10.2f %6.2f" % (name[:90], n, s / 1e6, s / n / 1e3, 100.0 * s / tot))
     lines.append("TOTAL kernel time %.3f ms over %d kernels (%d dispatches)" % (tot / 1e6, len(rows), len(ev)))
     if ev:
+        # the largest gaps with the kernels around them (host-side stalls show up as long gaps)
+        sev = sorted(ev, key=lambda x: x[1])
+        ctx, end_max, prev = [], sev[0][2], sev[0][0]
+        for k in range(1, len(sev)):
+            gap = sev[k][1] - end_max
+            if gap > 0:
+                ctx.append((gap, prev, sev[k][0], (sev[k][1] - sev[0][1]) / 1e6))
+            if sev[k][2] > end_max:
+                end_max, prev = sev[k][2], sev[k][0]
+        ctx.sort(reverse=True)
+        for gap, a, b, at in ctx[:6]:
+            lines.append("GAP %.3f ms at +%.1f ms: after %s -> before %s" % (gap / 1e6, at, a[:70], b[:70]))
         iv = sorted((s, e) for _, s, e in ev)
         busy, gaps = 0, []
         cs, ce = iv[0]
