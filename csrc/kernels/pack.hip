@@ -16,66 +16,52 @@ struct PackDesc {
   int64_t wp_off;    // element offset of wp (all G clients) in the packed buffer
   int64_t wt_off;    // ... of wt, or -1 (no dgrad image)
   int cout, cin_p, cin_src, kt;
-  int blk_plain;     // first block of this layer in the plain grid (Cout x ceil(Cin_p / 64) blocks per layer)
+  int blk_plain;     // first block of this layer in the plain grid (Cout blocks per layer)
   int blk_t;         // first block in the transpose grid (ceil(Cin_p/64) * ceil(Cout/64) * kt blocks per layer)
   int slot[27];
 };
 static_assert(sizeof(PackDesc) % 8 == 0, "PackDesc alignment");
 
-// layer of block b: binary search over the prefix block counts (log2 of ~60 layers, uniform per block)
 __device__ __forceinline__ int find_layer(const PackDesc* d, int n, int b, bool plain) {
-  int lo = 0, hi = n - 1;
-  while (lo < hi) {
-    const int mid = (lo + hi + 1) >> 1;
-    if ((plain ? d[mid].blk_plain : d[mid].blk_t) <= b) lo = mid;
-    else hi = mid - 1;
-  }
-  return lo;
+  int i = 0;
+  while (i + 1 < n && (plain ? d[i + 1].blk_plain : d[i + 1].blk_t) <= b) ++i;
+  return i;
 }
 
-// plain: block (layer row co, 64-channel chunk cc, client g): the chunk's fp32 source rows [64][kt] (contiguous in
-// the PyTorch layout) are staged in LDS and written as kt runs of 64 bf16 channels.  Chunked so that a block stages
-// at most 64 kt floats (6.9 KB for 3x3x3) instead of a whole [cin][kt] row: the launch's dynamic LDS is sized by its
-// largest block, and whole 512-channel rows (55 KB) held the 3D ResNet's pack to two blocks per CU (~1.2 TB/s).
+// plain: block (layer row co, client g); the fp32 source row [cin_src][kt] is staged in LDS
 __global__ __launch_bounds__(256) void k_pack_plain(const PackDesc* __restrict__ desc, int nd,
                                                     const float* __restrict__ theta, int64_t ldt, int G,
                                                     uint16_t* __restrict__ out) {
   extern __shared__ float row[];
   const int li = find_layer(desc, nd, blockIdx.x, true);
   const PackDesc& d = desc[li];
+  const int co = blockIdx.x - d.blk_plain, g = blockIdx.y;
   const int Cin = d.cin_p, kt = d.kt, K = kt * Cin, Ks = kt * d.cin_src;
-  const int nci = (Cin + 63) >> 6;
-  const int b = blockIdx.x - d.blk_plain, co = b / nci, c0 = (b - co * nci) * 64, g = blockIdx.y;
-  const int nc = min(64, Cin - c0);                       // output channels of this chunk
-  const int ns = max(0, min(64, d.cin_src - c0));         // source channels present in it (the rest are zero)
-  const float* src = theta + (int64_t)g * ldt + d.src_off + (int64_t)co * Ks + (int64_t)c0 * kt;
-  const int n = ns * kt;
-  if ((reinterpret_cast<uintptr_t>(src) & 15) == 0 && n % 4 == 0) {  // 16-B source loads
-    for (int e = 4 * threadIdx.x; e < n; e += 4 * 256)
+  const float* src = theta + (int64_t)g * ldt + d.src_off + (int64_t)co * Ks;
+  if ((reinterpret_cast<uintptr_t>(src) & 15) == 0 && Ks % 4 == 0) {  // 16-B source loads
+    for (int e = 4 * threadIdx.x; e < Ks; e += 4 * 256)
       *reinterpret_cast<float4*>(row + e) = *reinterpret_cast<const float4*>(src + e);
   } else {
-    for (int e = threadIdx.x; e < n; e += 256) row[e] = src[e];
+    for (int e = threadIdx.x; e < Ks; e += 256) row[e] = src[e];
   }
   __syncthreads();
-  uint16_t* dst = out + d.wp_off + ((int64_t)g * d.cout + co) * K + c0;
-  if (Cin % 8 == 0 && nc % 8 == 0 && (d.wp_off & 7) == 0) {  // 16-B stores: 8 channels of one tap per lane
-    const int n8 = nc >> 3;
-    for (int it = threadIdx.x; it < kt * n8; it += 256) {
-      const int t = it / n8, j0 = (it - t * n8) * 8;
+  uint16_t* dst = out + d.wp_off + ((int64_t)g * d.cout + co) * K;
+  if (Cin % 8 == 0 && (d.wp_off & 7) == 0) {  // 16-B stores: 8 channels of one tap per lane
+    for (int e = 8 * threadIdx.x; e < K; e += 8 * 256) {
+      const int t = e / Cin, ci = e - t * Cin;
       float v[8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = j0 + j < ns ? row[(j0 + j) * kt + t] : 0.f;
-      *reinterpret_cast<uint4*>(dst + t * Cin + j0) = make_uint4(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]),
-                                                                 pack_bf16x2(v[4], v[5]), pack_bf16x2(v[6], v[7]));
+      for (int j = 0; j < 8; ++j) v[j] = ci + j < d.cin_src ? row[(ci + j) * kt + t] : 0.f;
+      *reinterpret_cast<uint4*>(dst + e) = make_uint4(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]),
+                                                      pack_bf16x2(v[4], v[5]), pack_bf16x2(v[6], v[7]));
     }
     return;
   }
-  const int n2 = (nc + 1) >> 1;  // channel pairs (Cin even: a pair never straddles a tap)
-  for (int it = threadIdx.x; it < kt * n2; it += 256) {
-    const int t = it / n2, j = (it - t * n2) * 2;
-    const float a = j < ns ? row[j * kt + t] : 0.f;
-    const float c = j + 1 < ns ? row[(j + 1) * kt + t] : 0.f;
-    *reinterpret_cast<uint32_t*>(dst + t * Cin + j) = pack_bf16x2(a, c);
+  for (int e = 2 * threadIdx.x; e < K; e += 2 * 256) {  // e, e+1: same tap (Cin even)
+    const int t = e / Cin, ci = e - t * Cin;
+    const float a = ci < d.cin_src ? row[ci * kt + t] : 0.f;
+    const float b = ci + 1 < d.cin_src ? row[(ci + 1) * kt + t] : 0.f;
+    *reinterpret_cast<uint32_t*>(dst + e) = pack_bf16x2(a, b);
   }
 }
 
@@ -118,7 +104,7 @@ __global__ __launch_bounds__(256) void k_pack_trans(const PackDesc* __restrict__
   }
 }
 // desc: device table of nd PackDesc; nplain / ntrans: total blocks of the two grids; lds: bytes for the largest
-// plain block (max kt * min(64, cin_src) * 4)
+// plain source row (max kt * cin_src * 4)
 void pack_convs(uintptr_t desc, int nd, int nplain, int ntrans, int lds, uintptr_t theta, int64_t ldt, int G,
                 uintptr_t out, uintptr_t stream) {
   NIDT_REQUIRE(nd > 0 && G > 0 && lds > 0 && lds <= 160 * 1024, "pack_convs: bad table");

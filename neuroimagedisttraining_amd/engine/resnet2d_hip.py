@@ -342,7 +342,7 @@ class WeightPacker:
             d = desc[i]
             d["src_off"], d["cout"], d["cin_p"], d["cin_src"], d["kt"] = c.off, c.cout, c.cin_p, c.cin, c.kt
             d["blk_plain"], d["blk_t"] = nplain, ntrans
-            nplain += c.cout * ((c.cin_p + 63) // 64)  # pack.hip k_pack_plain: (row, 64-channel chunk) blocks
+            nplain += c.cout
             n_img = G * c.cout * c.kt * c.cin_p
             d["wp_off"] = off
             vp = (off, (G, c.cout, c.kt, c.cin_p))
@@ -358,7 +358,7 @@ class WeightPacker:
                 d["wt_off"] = -1
             d["slot"][:c.kt] = c.slots
             views.append((vp, vt))
-        lds = max(c.kt * min(64, c.cin) * 4 for c in self.convs)
+        lds = max(c.kt * c.cin * 4 for c in self.convs)
         buf = torch.empty(max(1, off), dtype=torch.bfloat16, device=self.device)
         tab = torch.from_numpy(desc.view(np.uint8).copy()).to(self.device)
         plan = (tab, nplain, ntrans, lds, buf, views)

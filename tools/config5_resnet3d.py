@@ -74,6 +74,21 @@ def main():
                    test_batch=args.test_batch or (16 if args.engine == "hip" else 8),
                    group=args.group if args.engine == "hip" else 0)
     runner = FLRunner(eng, splits, cfg, info, model, algorithm="fedavg")
+    memlog = []
+    if dev.type == "cuda":  # per-phase memory: allocated after, and the peak during, each phase of a round
+        def _wrap(name):
+            fn = getattr(runner, name)
+
+            def w(*a, **k):
+                torch.cuda.reset_peak_memory_stats()
+                out = fn(*a, **k)
+                memlog.append((name, round(torch.cuda.memory_allocated() / 2 ** 30, 1),
+                               round(torch.cuda.max_memory_allocated() / 2 ** 30, 1),
+                               round(torch.cuda.memory_reserved() / 2 ** 30, 1)))
+                return out
+            setattr(runner, name, w)
+        for nm in ("local_train", "aggregate", "evaluate"):
+            _wrap(nm)
     if dev.type == "cuda":
         torch.cuda.synchronize()
     rt.barrier(info)
@@ -81,14 +96,12 @@ def main():
     res = None
     per_round, peaks, phases = [], [], []
     for r in range(args.rounds):
-        if dev.type == "cuda":
-            torch.cuda.reset_peak_memory_stats()
         t_before = dict(runner.timers)
         tr = time.perf_counter()
         res = runner.run_round(r, sync_timers=True)
         if dev.type == "cuda":
             torch.cuda.synchronize()
-            peaks.append(round(torch.cuda.max_memory_allocated() / 2 ** 30, 1))
+            peaks.append(max((m[2] for m in memlog[-3:]), default=0.0))
         per_round.append(rt.max_over_ranks(time.perf_counter() - tr, info))
         phases.append({k: round(v - t_before.get(k, 0.0), 3) for k, v in runner.timers.items()})
     dt = rt.max_over_ranks(time.perf_counter() - t0, info)
@@ -103,7 +116,7 @@ def main():
                                                  if args.rounds > args.warmup else None),
                           "s_round_each": [round(x, 2) for x in per_round], "hip_convs": n_hip,
                           "peak_hbm_gib_rank0": round(peak, 1), "peak_gib_each_round": peaks,
-                          "phase_s_each_round": phases,
+                          "phase_s_each_round": phases, "mem_gib_phase_alloc_peak_reserved": memlog,
                           "update_topk": args.topk, "aggregate_elems": runner.stat_info.get("aggregate_elems"),
                           "metrics": res}), flush=True)
     rt.shutdown(info)
