@@ -1,10 +1,9 @@
 """Client-batched 3D ResNet (BASELINE config 5: Bottleneck ResNet-50 on full-resolution 1x121x145x121 volumes) on the
 gfx950 kernels: G clients' local steps in one lockstep pass over rows of the flat ``[C, P]`` parameter matrix.
 
-* the 1x1x1 stride-1 convolutions (forward and data gradient, and the stride-2 projections' data gradient) are
-  plain per-client GEMMs on channels-last rows: batched hipBLASLt GEMMs (:func:`gemm_1x1`);
-* every other bottleneck convolution — 3x3x3 at stride 1 and 2, the 1x1x1 stride-2 projections — runs on the
-  client-grouped LDS-DMA implicit-GEMM kernels of ``conv3d.hip`` (the weight gradients of all of them too), with
+* every bottleneck convolution — 1x1x1 (the GEMM path: ``conv_fwd_g`` with one tap; batched library GEMMs opt-in,
+  :func:`gemm_1x1`), 3x3x3 at stride 1 and 2, the 1x1x1 stride-2 projections — runs on the client-grouped LDS-DMA
+  implicit-GEMM kernels of ``conv3d.hip``, with
   every layer's bf16 MFMA images packed in two launches per step (``pack.hip``); data gradients: stride 1 = the
   same kernels on tap-flipped transposed weights, 3x3x3 stride 2 = eight sub-pixel phase convs over the dy grid
   written straight into dX (``conv_dgrad_s2_g``: 8x fewer MACs than the zero-upsampled form, no memset or crop),
@@ -56,17 +55,22 @@ def conv_fwd(x_ptr, w_ptr, y_ptr, G, B, D, H, W, Cin, Cout, kt, st, pad, padd, d
 
 _SLAB_TABS = {}
 # 1x1x1 stride-1 convs (forward and data gradient) are plain per-client GEMMs [M, Cin] x [Cin, Cout] on channels-last
-# rows: batched hipBLASLt GEMMs (torch.bmm) instead of the general LDS-DMA conv kernel, which spends ~7 VALU per MFMA
-# on per-tap addressing it does not need here (14 % MFMA busy, profiles/r4_pmc_config5.txt).  NIDT_R3D_BLAS=0: the HIP
-# kernel (A/B).
-_BLAS_1X1 = os.environ.get("NIDT_R3D_BLAS", "1") != "0"
+# rows; NIDT_R3D_BLAS=1 runs them as batched library GEMMs (torch.bmm) instead of the general LDS-DMA conv kernel
+# (which spends ~7 VALU per MFMA on per-tap addressing, 14 % MFMA busy, profiles/r4_pmc_config5.txt).  OFF by
+# default: at config-5 scale (32 clients x 142 k positions x 256 channels, > 2^31 elements per batched operand) the
+# run hung with the GPU left in a memory-fault state (profiles/r4_blas_1x1_fault.txt); the engine tests at small
+# shapes pass.  Operands below 2^31 bytes only, even when enabled.
+_BLAS_1X1 = os.environ.get("NIDT_R3D_BLAS", "0") == "1"
 
 
 def gemm_1x1(x, w, out, G):
     """out[g] = x[g] @ w[g]^T for channels-last x [G*B, D, H, W, K] and a packed image w [G, N, 1, K] (bf16, fp32
-    accumulation), written into out [G*B, D, H, W, N]."""
+    accumulation), written into out [G*B, D, H, W, N].  False (nothing launched) when an operand reaches 2^31 bytes."""
     K, N = x.shape[-1], out.shape[-1]
+    if max(x.numel(), out.numel()) * 2 >= (1 << 31):
+        return False
     torch.bmm(x.view(G, -1, K), w.view(G, N, K).transpose(1, 2), out=out.view(G, -1, N))
+    return True
 
 
 def slab_conv(x_ptr, w_ptr, y_ptr, G, B, D, H, W, Cin, Cout, pad, device):
@@ -140,8 +144,7 @@ class GConv3:
             self.wt = (wt, G, theta.data_ptr()) if wt is not None else None
         wp = self.wp[0]
         y = torch.empty(N, Do, Ho, Wo, self.cout, device=x.device, dtype=torch.bfloat16)
-        if self.kt == 1 and self.stride == 1 and _BLAS_1X1:
-            gemm_1x1(x, wp, y, G)
+        if self.kt == 1 and self.stride == 1 and _BLAS_1X1 and gemm_1x1(x, wp, y, G):
             return y
         if self.kt == 27 and self.stride == 1 and slab_conv(x.data_ptr(), wp.data_ptr(), y.data_ptr(), G, N // G, D,
                                                             H, W, self.cin, self.cout, self.pad, x.device):
@@ -197,8 +200,7 @@ class GConv3:
         if self.stride == 1:
             dx = torch.empty(N, D, H, W, self.cin, device=x.device, dtype=torch.bfloat16)
             p2 = self.k - 1 - self.pad
-            if self.kt == 1 and _BLAS_1X1:
-                gemm_1x1(dy, wt, dx, G)
+            if self.kt == 1 and _BLAS_1X1 and gemm_1x1(dy, wt, dx, G):
                 return dx
             if self.kt == 27 and slab_conv(dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), G, B, Do, Ho, Wo, self.cout,
                                            self.cin, p2, x.device):
@@ -216,8 +218,7 @@ class GConv3:
             return dx
         # 1x1 stride 2: the half-resolution W^T dY of the even voxels (res_grad_s2 adds it into the residual stream)
         sub = torch.empty(N, Do, Ho, Wo, self.cin, device=x.device, dtype=torch.bfloat16)
-        if _BLAS_1X1:
-            gemm_1x1(dy, wt, sub, G)
+        if _BLAS_1X1 and gemm_1x1(dy, wt, sub, G):
             return sub
         conv_fwd(dy.data_ptr(), wt.data_ptr(), sub.data_ptr(), G, B, Do, Ho, Wo, self.cout, self.cin, 1, 1, 0, 0,
                  x.device)

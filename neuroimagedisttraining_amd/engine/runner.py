@@ -959,9 +959,10 @@ class FLRunner:
         correct = ((pred >= 0.5).float() == y).float()
         return correct, loss
 
-    def _eval_rows(self, theta, bufs, clients, per_client_rows, which="test"):
+    def _eval_rows(self, theta, bufs, clients, per_client_rows, which="test", chunk=None):
         """Per-client (correct, loss_sum, total) with reference test semantics (Q1).  Clients that share a
-        model row are evaluated together in chunks of ``test_batch`` samples (one launch sequence each)."""
+        model row are evaluated together in chunks of ``chunk`` (default ``test_batch``) samples, balanced so the
+        last launch is not a small tail (one launch sequence each)."""
         out = np.zeros((len(clients), 3), dtype=np.float64)
         by_row = {}
         for j, r in enumerate(per_client_rows):
@@ -973,7 +974,8 @@ class FLRunner:
             if allidx.size == 0:
                 continue
             th, bu = theta[r:r + 1], bufs[r:r + 1]
-            tb = self.cfg.test_batch
+            cap = chunk or self.cfg.test_batch
+            tb = -(-allidx.size // -(-allidx.size // cap))  # ceil(n / ceil(n / cap))
             acc = torch.zeros((len(js), 3), dtype=torch.float64, device=self.device)
             own_t = torch.from_numpy(owner).to(self.device)
             all_t = self._upload_i32(allidx)
@@ -1130,20 +1132,23 @@ class FLRunner:
         return th[:k], bu[:k]
 
     def _eval_global_and_personal(self, theta=None, bufs=None):
-        """Global model and every local client's personal model on that client's test split, in ONE grouped
-        launch sequence of 2C model rows (C personal rows + C copies of the global model) — full-client kernel
-        shapes instead of a G = 1 global evaluation."""
+        """Global model and every local client's personal model on that client's test split, as grouped launches:
+        the personal rows straight from the row matrix, the global model from K = min(C, 64) staged copies that
+        every group of clients reuses (rows j mod K).  (Staging copies of all C personal rows next to C copies of
+        the global model took a 2C-row buffer: 94 GB for config 5's 256 x 46 M parameters, which pushed its peak to
+        260 GiB and the allocator into a synchronous cache flush every round.)  Per-client launch shapes stay those
+        of the grouped evaluation: the engines' per-client tensors keep their 32-bit offsets."""
         C = self.C
         theta = self.theta if theta is None else theta
         bufs = self.bufs if bufs is None else bufs
-        th, bu = self._eval_buffers(2 * C)
+        pers = self.eval_grouped(theta, bufs, list(range(C)), self.local)
+        K = min(C, 64)
+        th, bu = self._eval_buffers(K)
         with torch.no_grad():
-            th[:C].copy_(theta[:C])
-            th[C:].copy_(self.w_global.expand(C, -1))
-            bu[:C].copy_(bufs[:C])
-            bu[C:].copy_(self.b_global.expand(C, -1))
-        res = self.eval_grouped(th, bu, list(range(2 * C)), self.local + self.local)
-        return res[C:], res[:C]
+            th.copy_(self.w_global.expand(K, -1))
+            bu.copy_(self.b_global.expand(K, -1))
+        glob = self.eval_grouped(th, bu, [j % K for j in range(C)], self.local)
+        return glob, pers
 
     def gather_metrics(self, clients, arr):
         """Per-client metric rows of this rank's clients -> [N, k] numpy on every rank (one all-reduce)."""
