@@ -134,9 +134,9 @@ class GConv3:
 
     def fwd(self, x, theta, G, train=False, packed=False):
         N, D, H, W, C = x.shape
-        assert C == self.cin and N % G == 0 and x.is_contiguous()
-        if not self.hip:
+        if not self.hip:  # CPU twin (its BN output may be a permuted view)
             return self._torch_fwd(x, theta[:, self.off:self.off + self.numel], G)
+        assert C == self.cin and N % G == 0 and x.is_contiguous()
         Do, Ho, Wo = self.out_dims(D, H, W)
         if not packed:
             wp, wt = self._wp(theta, G, train)
@@ -452,7 +452,8 @@ class GroupedResNet3D:
             bufs[:, self.boff["bn1.running_var"]:self.boff["bn1.running_var"] + C].copy_(rv.view(G, C))
             if "bn1.num_batches_tracked" in self.boff:
                 bufs[:, self.boff["bn1.num_batches_tracked"]] += 1
-        return out.to(self.act).contiguous(), (out, leaf)
+        # downstream layers get a detached activation (the stem's own backward is autograd.grad(out, leaf, da))
+        return out.detach().to(self.act).contiguous(), (out, leaf)
 
     # ------------------------------------------------------------------ forward
     def forward(self, x8, theta, bufs, G, train, idx=None):
@@ -597,18 +598,25 @@ class ResNet3DHipEngine:
             logits, _, _, _ = self.net.forward(x, theta, bufs, G, False, idx=sel)
         return logits.float()
 
+    def _opt_cls(self):
+        from .executor import HipEngine, TorchEngine
+        return HipEngine if theta_on_gpu(self) else TorchEngine  # fused HIP optimizer, or its torch twin on CPU
+
     def _delegate(self):
         if self._opt is None:
-            from .executor import HipEngine
-            self._opt = HipEngine.__new__(HipEngine)
-            self._opt.m = ops.ext()
+            cls = self._opt_cls()
+            self._opt = cls.__new__(cls)
+            if theta_on_gpu(self):
+                self._opt.m = ops.ext()
         return self._opt
 
     def local_opt(self, theta, grads, mom_buf, spec, lr, wd, momentum, max_norm, lr_dev=None, keep_grad=False):
-        from .executor import HipEngine
-        HipEngine.local_opt(self._delegate(), theta, grads, mom_buf, spec, lr, wd, momentum, max_norm, lr_dev=lr_dev,
-                            keep_grad=keep_grad)
+        self._opt_cls().local_opt(self._delegate(), theta, grads, mom_buf, spec, lr, wd, momentum, max_norm,
+                                  lr_dev=lr_dev, keep_grad=keep_grad)
 
     def saliency_acc(self, theta, grads, score, alpha):
-        from .executor import HipEngine
-        HipEngine.saliency_acc(self._delegate(), theta, grads, score, alpha)
+        self._opt_cls().saliency_acc(self._delegate(), theta, grads, score, alpha)
+
+
+def theta_on_gpu(engine):
+    return torch.device(engine.device).type == "cuda"

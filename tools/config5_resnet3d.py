@@ -104,6 +104,8 @@ def main():
             peaks.append(max((m[2] for m in memlog[-3:]), default=0.0))
         per_round.append(rt.max_over_ranks(time.perf_counter() - tr, info))
         phases.append({k: round(v - t_before.get(k, 0.0), 3) for k, v in runner.timers.items()})
+        if info.is_main:
+            print("round %d: %.2f s %s" % (r, per_round[-1], phases[-1]), flush=True)  # progress
     dt = rt.max_over_ranks(time.perf_counter() - t0, info)
     peak = torch.cuda.max_memory_allocated() / 2 ** 30 if dev.type == "cuda" else 0.0
     if info.is_main:
