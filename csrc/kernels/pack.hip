@@ -16,24 +16,36 @@ struct PackDesc {
   int64_t wp_off;    // element offset of wp (all G clients) in the packed buffer
   int64_t wt_off;    // ... of wt, or -1 (no dgrad image)
   int cout, cin_p, cin_src, kt;
-  int blk_plain;     // first block of this layer in the plain grid (Cout blocks per layer)
+  int blk_plain;     // first block of this layer in the plain grid (Cout blocks per layer; 0 blocks for 1x1 layers
+                     // packed by k_pack_plain1)
   int blk_t;         // first block in the transpose grid (ceil(Cin_p/64) * ceil(Cout/64) * kt blocks per layer)
+  int blk_plain1;    // first block in the 1x1 grid (ceil(Cout / pack1_rows(Cin_p)) blocks; 0 for the other layers)
   int slot[27];
 };
 static_assert(sizeof(PackDesc) % 8 == 0, "PackDesc alignment");
 
-__device__ __forceinline__ int find_layer(const PackDesc* d, int n, int b, bool plain) {
-  int i = 0;
-  while (i + 1 < n && (plain ? d[i + 1].blk_plain : d[i + 1].blk_t) <= b) ++i;
-  return i;
+// layer of block b in one of the three grids: the last layer whose prefix block count is <= b (prefixes are
+// non-decreasing; layers without blocks in a grid repeat the running count and are never the last such layer)
+__device__ __forceinline__ int find_layer(const PackDesc* d, int n, int b, int grid) {
+  int lo = 0, hi = n - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    const int p = grid == 0 ? d[mid].blk_plain : (grid == 1 ? d[mid].blk_t : d[mid].blk_plain1);
+    if (p <= b) lo = mid;
+    else hi = mid - 1;
+  }
+  return lo;
 }
+
+// rows per block of the 1x1 grid: about 8 K elements per block (host twin: resnet2d_hip.WeightPacker)
+__host__ __device__ constexpr int pack1_rows(int cin_p) { return cin_p >= 8192 ? 1 : 8192 / cin_p; }
 
 // plain: block (layer row co, client g); the fp32 source row [cin_src][kt] is staged in LDS
 __global__ __launch_bounds__(256) void k_pack_plain(const PackDesc* __restrict__ desc, int nd,
                                                     const float* __restrict__ theta, int64_t ldt, int G,
                                                     uint16_t* __restrict__ out) {
   extern __shared__ float row[];
-  const int li = find_layer(desc, nd, blockIdx.x, true);
+  const int li = find_layer(desc, nd, blockIdx.x, 0);
   const PackDesc& d = desc[li];
   const int co = blockIdx.x - d.blk_plain, g = blockIdx.y;
   const int Cin = d.cin_p, kt = d.kt, K = kt * Cin, Ks = kt * d.cin_src;
@@ -65,13 +77,44 @@ __global__ __launch_bounds__(256) void k_pack_plain(const PackDesc* __restrict__
   }
 }
 
+// plain image of the 1x1 layers (kt = 1: the PyTorch row [cin] is already the image row [1][Cin_p] up to the zero
+// channels): no transpose and no LDS; block (layer, R = pack1_rows consecutive rows, client g) converts R x Cin_p
+// elements, 8 per lane (two 16-B loads, one 16-B store).  The per-row kernel above staged each of these short rows
+// in an LDS buffer sized for the largest 3x3x3 row, which held the whole pack to two blocks per CU.
+__global__ __launch_bounds__(256) void k_pack_plain1(const PackDesc* __restrict__ desc, int nd,
+                                                     const float* __restrict__ theta, int64_t ldt, int G,
+                                                     uint16_t* __restrict__ out) {
+  const int li = find_layer(desc, nd, blockIdx.x, 2);
+  const PackDesc& d = desc[li];
+  const int Cin = d.cin_p, cs = d.cin_src, R = pack1_rows(Cin);
+  const int r0 = (blockIdx.x - d.blk_plain1) * R, nr = min(R, d.cout - r0), g = blockIdx.y;
+  const float* src = theta + (int64_t)g * ldt + d.src_off + (int64_t)r0 * cs;
+  uint16_t* dst = out + d.wp_off + ((int64_t)g * d.cout + r0) * Cin;
+  const int n8 = nr * (Cin >> 3);
+  const bool vec = cs == Cin && (reinterpret_cast<uintptr_t>(src) & 15) == 0;
+  for (int e = threadIdx.x; e < n8; e += 256) {
+    const int row = e / (Cin >> 3), c = (e - row * (Cin >> 3)) * 8;
+    float v[8];
+    if (vec) {
+      const float4 lo = *reinterpret_cast<const float4*>(src + (int64_t)row * cs + c);
+      const float4 hi = *reinterpret_cast<const float4*>(src + (int64_t)row * cs + c + 4);
+      v[0] = lo.x; v[1] = lo.y; v[2] = lo.z; v[3] = lo.w; v[4] = hi.x; v[5] = hi.y; v[6] = hi.z; v[7] = hi.w;
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = c + j < cs ? src[(int64_t)row * cs + c + j] : 0.f;
+    }
+    *reinterpret_cast<uint4*>(dst + (int64_t)row * Cin + c) =
+        make_uint4(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]), pack_bf16x2(v[4], v[5]), pack_bf16x2(v[6], v[7]));
+  }
+}
+
 // transposed: block (64 ci x 64 co tile, tap t, client g) reads the plain image written by k_pack_plain.  Global
 // traffic in 16-B pieces (8 channels per lane: a 64-wide tile row is 8 lanes), the transpose through a padded LDS tile
 // (2-B column reads there, where bandwidth is plentiful); 2-B global accesses ran at ~2 TB/s.
 __global__ __launch_bounds__(256) void k_pack_trans(const PackDesc* __restrict__ desc, int nd, int G,
                                                     uint16_t* __restrict__ out) {
   __shared__ uint16_t tile[64][72];  // [co][ci], rows padded to 144 B (16-B aligned, staggered banks)
-  const int li = find_layer(desc, nd, blockIdx.x, false);
+  const int li = find_layer(desc, nd, blockIdx.x, 1);
   const PackDesc& d = desc[li];
   const int Cin = d.cin_p, Cout = d.cout, kt = d.kt;
   const int nci = (Cin + 63) / 64;
@@ -103,15 +146,23 @@ __global__ __launch_bounds__(256) void k_pack_trans(const PackDesc* __restrict__
     *reinterpret_cast<uint4*>(wt + ((int64_t)ci * kt + s) * Cout + co) = make_uint4(w[0], w[1], w[2], w[3]);
   }
 }
-// desc: device table of nd PackDesc; nplain / ntrans: total blocks of the two grids; lds: bytes for the largest
-// plain source row (max kt * cin_src * 4)
-void pack_convs(uintptr_t desc, int nd, int nplain, int ntrans, int lds, uintptr_t theta, int64_t ldt, int G,
-                uintptr_t out, uintptr_t stream) {
-  NIDT_REQUIRE(nd > 0 && G > 0 && lds > 0 && lds <= 160 * 1024, "pack_convs: bad table");
+// desc: device table of nd PackDesc; nplain / nplain1 / ntrans: total blocks of the three grids; lds: bytes for the
+// largest row of the per-row plain grid (max kt * cin_src * 4 over its layers)
+void pack_convs(uintptr_t desc, int nd, int nplain, int nplain1, int ntrans, int lds, uintptr_t theta, int64_t ldt,
+                int G, uintptr_t out, uintptr_t stream) {
+  NIDT_REQUIRE(nd > 0 && G > 0 && lds > 0 && lds <= 160 * 1024 && nplain >= 0 && nplain1 >= 0,
+               "pack_convs: bad table");
   hipStream_t s = as_stream(stream);
-  hipLaunchKernelGGL(k_pack_plain, dim3(nplain, G), dim3(256), lds, s, ptr<const PackDesc>(desc), nd,
-                     ptr<const float>(theta), ldt, G, ptr<uint16_t>(out));
-  NIDT_CHECK(hipGetLastError());
+  if (nplain > 0) {
+    hipLaunchKernelGGL(k_pack_plain, dim3(nplain, G), dim3(256), lds, s, ptr<const PackDesc>(desc), nd,
+                       ptr<const float>(theta), ldt, G, ptr<uint16_t>(out));
+    NIDT_CHECK(hipGetLastError());
+  }
+  if (nplain1 > 0) {
+    hipLaunchKernelGGL(k_pack_plain1, dim3(nplain1, G), dim3(256), 0, s, ptr<const PackDesc>(desc), nd,
+                       ptr<const float>(theta), ldt, G, ptr<uint16_t>(out));
+    NIDT_CHECK(hipGetLastError());
+  }
   if (ntrans > 0) {
     hipLaunchKernelGGL(k_pack_trans, dim3(ntrans, G), dim3(256), 0, s, ptr<const PackDesc>(desc), nd, G,
                        ptr<uint16_t>(out));
@@ -120,5 +171,6 @@ void pack_convs(uintptr_t desc, int nd, int nplain, int ntrans, int lds, uintptr
 }
 
 int pack_desc_bytes() { return (int)sizeof(PackDesc); }
+int pack1_rows_host(int cin_p) { return pack1_rows(cin_p); }
 
 }  // namespace nidt

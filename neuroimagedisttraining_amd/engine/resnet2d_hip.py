@@ -313,11 +313,14 @@ class GroupedConv:
 
 
 # descriptor of pack.hip (PackDesc): int64 src_off, wp_off, wt_off; int32 cout, cin_p, cin_src, kt, blk_plain, blk_t,
-# slot[27]; 160 bytes with the struct's 8-B alignment
+# blk_plain1, slot[27]; 160 bytes with the struct's 8-B alignment
 _PACK_DTYPE = np.dtype({"names": ["src_off", "wp_off", "wt_off", "cout", "cin_p", "cin_src", "kt", "blk_plain",
-                                  "blk_t", "slot"],
-                        "formats": ["<i8", "<i8", "<i8", "<i4", "<i4", "<i4", "<i4", "<i4", "<i4", ("<i4", 27)],
-                        "offsets": [0, 8, 16, 24, 28, 32, 36, 40, 44, 48], "itemsize": 160})
+                                  "blk_t", "blk_plain1", "slot"],
+                        "formats": ["<i8", "<i8", "<i8", "<i4", "<i4", "<i4", "<i4", "<i4", "<i4", "<i4",
+                                    ("<i4", 27)],
+                        "offsets": [0, 8, 16, 24, 28, 32, 36, 40, 44, 48, 52], "itemsize": 160})
+# 1x1 layers on the no-LDS row-batched pack (pack.hip k_pack_plain1); NIDT_PACK1=0: the per-row kernel (A/B)
+_PACK1 = os.environ.get("NIDT_PACK1", "1") != "0"
 
 
 class WeightPacker:
@@ -336,13 +339,18 @@ class WeightPacker:
         if ops.ext().pack_desc_bytes() != _PACK_DTYPE.itemsize:
             raise RuntimeError("pack.hip PackDesc layout changed")
         desc = np.zeros(len(self.convs), dtype=_PACK_DTYPE)
-        off = nplain = ntrans = 0
+        off = nplain = nplain1 = ntrans = 0
         views = []
+        m = ops.ext()
         for i, c in enumerate(self.convs):
             d = desc[i]
             d["src_off"], d["cout"], d["cin_p"], d["cin_src"], d["kt"] = c.off, c.cout, c.cin_p, c.cin, c.kt
-            d["blk_plain"], d["blk_t"] = nplain, ntrans
-            nplain += c.cout
+            d["blk_plain"], d["blk_t"], d["blk_plain1"] = nplain, ntrans, nplain1
+            if _PACK1 and c.kt == 1 and c.cin_p % 8 == 0:
+                rows = m.pack1_rows_host(c.cin_p)
+                nplain1 += (c.cout + rows - 1) // rows
+            else:
+                nplain += c.cout
             n_img = G * c.cout * c.kt * c.cin_p
             d["wp_off"] = off
             vp = (off, (G, c.cout, c.kt, c.cin_p))
@@ -358,26 +366,26 @@ class WeightPacker:
                 d["wt_off"] = -1
             d["slot"][:c.kt] = c.slots
             views.append((vp, vt))
-        lds = max(c.kt * c.cin * 4 for c in self.convs)
+        lds = max([c.kt * c.cin * 4 for c in self.convs if not (_PACK1 and c.kt == 1 and c.cin_p % 8 == 0)] + [4])
         buf = torch.empty(max(1, off), dtype=torch.bfloat16, device=self.device)
         tab = torch.from_numpy(desc.view(np.uint8).copy()).to(self.device)
-        plan = (tab, nplain, ntrans, lds, buf, views)
+        plan = (tab, (nplain, nplain1), ntrans, lds, buf, views)
         self._plans[key] = plan
         return plan
 
     def pack(self, theta, G, train, key=None):
         """Pack every layer for this step and hand each conv its views (``conv.wp`` / ``conv.wt``)."""
-        tab, nplain, ntrans, lds, buf, views = self._plan(G, train, key)
-        ops.ext().pack_convs(tab.data_ptr(), len(self.convs), nplain, ntrans, lds, theta.data_ptr(), theta.stride(0),
-                             G, buf.data_ptr(), _stream())
+        tab, (nplain, nplain1), ntrans, lds, buf, views = self._plan(G, train, key)
+        ops.ext().pack_convs(tab.data_ptr(), len(self.convs), nplain, nplain1, ntrans, lds, theta.data_ptr(),
+                             theta.stride(0), G, buf.data_ptr(), _stream())
         for c, (vp, vt) in zip(self.convs, views):
             c.wp = (buf[vp[0]:vp[0] + int(np.prod(vp[1]))].view(vp[1]), G, theta.data_ptr())
             c.wt = (buf[vt[0]:vt[0] + int(np.prod(vt[1]))].view(vt[1]), G, theta.data_ptr()) if vt else None
 
     def pack_into(self, theta, G, wp, wt):
         """Single-layer packing into caller-provided tensors (tests, standalone layers)."""
-        tab, nplain, ntrans, lds, buf, views = self._plan(G, wt is not None, key=("one", G, wt is not None))
-        ops.ext().pack_convs(tab.data_ptr(), 1, nplain, ntrans, lds, theta.data_ptr(), theta.stride(0), G,
+        tab, (nplain, nplain1), ntrans, lds, buf, views = self._plan(G, wt is not None, key=("one", G, wt is not None))
+        ops.ext().pack_convs(tab.data_ptr(), 1, nplain, nplain1, ntrans, lds, theta.data_ptr(), theta.stride(0), G,
                              buf.data_ptr(), _stream())
         (vp, vt), = views
         wp.copy_(buf[vp[0]:vp[0] + wp.numel()].view(wp.shape))

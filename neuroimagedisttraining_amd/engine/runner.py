@@ -1137,16 +1137,14 @@ class FLRunner:
         every group of clients reuses (rows j mod K).  (Staging copies of all C personal rows next to C copies of
         the global model took a 2C-row buffer: 94 GB for config 5's 256 x 46 M parameters, which pushed its peak to
         260 GiB and the allocator into a synchronous cache flush every round.)  Per-client launch shapes stay those
-        of the grouped evaluation: the engines' per-client tensors keep their 32-bit offsets.  Models whose 2C-row
-        copy stays below 8 GB keep the single launch sequence over that copy (``NIDT_EVAL_STAGE=1`` / ``0`` force
-        either form)."""
+        of the grouped evaluation: the engines' per-client tensors keep their 32-bit offsets.  At the AlexNet3D
+        headline it is also slightly faster than one launch sequence over the 2C-row copy (2.2055 vs 2.196-2.200
+        rounds/s, interleaved, profiles/r4_ab_eval_forms.txt; ``NIDT_EVAL_STAGE=1`` selects that form)."""
         C = self.C
         theta = self.theta if theta is None else theta
         bufs = self.bufs if bufs is None else bufs
-        stage = os.environ.get("NIDT_EVAL_STAGE")
-        if stage == "1" or (stage is None and 2 * C * (self.P + self.Q) * 4 <= (8 << 30)):
-            # small models: one grouped launch sequence over a 2C-row copy (C personal + C global rows) keeps the
-            # launches twice as wide (AlexNet3D at 64 clients: 128 rows x 36 samples per launch)
+        if os.environ.get("NIDT_EVAL_STAGE") == "1":
+            # the previous form (A/B): one grouped launch sequence over a 2C-row copy (C personal + C global rows)
             th, bu = self._eval_buffers(2 * C)
             with torch.no_grad():
                 th[:C].copy_(theta[:C])
