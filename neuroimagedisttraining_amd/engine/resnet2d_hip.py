@@ -319,8 +319,9 @@ _PACK_DTYPE = np.dtype({"names": ["src_off", "wp_off", "wt_off", "cout", "cin_p"
                         "formats": ["<i8", "<i8", "<i8", "<i4", "<i4", "<i4", "<i4", "<i4", "<i4", "<i4",
                                     ("<i4", 27)],
                         "offsets": [0, 8, 16, 24, 28, 32, 36, 40, 44, 48, 52], "itemsize": 160})
-# 1x1 layers on the no-LDS row-batched pack (pack.hip k_pack_plain1) with NIDT_PACK1=1 (A/B; default: the per-row kernel)
-_PACK1 = os.environ.get("NIDT_PACK1", "0") == "1"
+# 1x1 layers on the no-LDS row-batched pack (pack.hip k_pack_plain1; config 5 12.48 -> 12.24 s/round,
+# profiles/r4_ab_pack1.txt); NIDT_PACK1=0: the per-row kernel (A/B)
+_PACK1 = os.environ.get("NIDT_PACK1", "1") != "0"
 
 
 class WeightPacker:
