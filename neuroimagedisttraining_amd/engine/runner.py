@@ -1138,13 +1138,16 @@ class FLRunner:
         the global model took a 2C-row buffer: 94 GB for config 5's 256 x 46 M parameters, which pushed its peak to
         260 GiB and the allocator into a synchronous cache flush every round.)  Per-client launch shapes stay those
         of the grouped evaluation: the engines' per-client tensors keep their 32-bit offsets.  At the AlexNet3D
-        headline it is also slightly faster than one launch sequence over the 2C-row copy (2.2055 vs 2.196-2.200
-        rounds/s, interleaved, profiles/r4_ab_eval_forms.txt; ``NIDT_EVAL_STAGE=1`` selects that form)."""
+        headline (64 clients) it is also slightly faster than one launch sequence over the 2C-row copy (2.2055 vs
+        2.196-2.200 rounds/s); with up to 32 clients (small models) the copy's twice-as-wide launches win and are
+        used (``NIDT_EVAL_STAGE=1`` / ``0`` force either form; profiles/r4_ab_eval_forms.txt)."""
         C = self.C
         theta = self.theta if theta is None else theta
         bufs = self.bufs if bufs is None else bufs
-        if os.environ.get("NIDT_EVAL_STAGE") == "1":
-            # the previous form (A/B): one grouped launch sequence over a 2C-row copy (C personal + C global rows)
+        stage = os.environ.get("NIDT_EVAL_STAGE")
+        if stage == "1" or (stage is None and C <= 32 and 2 * C * (self.P + self.Q) * 4 <= (8 << 30)):
+            # few clients: one grouped launch sequence over a 2C-row copy (C personal + C global rows) keeps the
+            # launches twice as wide (8 clients: 14.78-14.84 vs 14.64-14.73 rounds/s, profiles/r4_ab_eval_forms.txt)
             th, bu = self._eval_buffers(2 * C)
             with torch.no_grad():
                 th[:C].copy_(theta[:C])
