@@ -33,6 +33,9 @@ NM = 125 + 125 * 125
 # NIDT_WG2_EARLY=1 forks the conv2 wgrad before the conv2 dgrad instead of after it (beside the conv1 wgrad).
 _WGRAD_STREAM = os.environ.get("NIDT_AX_WGRAD_STREAM", "0") == "1"
 _WG2_EARLY = os.environ.get("NIDT_WG2_EARLY", "0") == "1"
+# conv2-5 weight packs batched into two pack.hip launches per step instead of eight: 8 clients per GPU +0.3%,
+# 64 within noise (profiles/r4_ab_alexnet_bpack.txt); NIDT_AX_BPACK=0: the per-layer packs (A/B)
+_BPACK = os.environ.get("NIDT_AX_BPACK", "1") != "0"
 
 
 def _p(t):
@@ -154,8 +157,46 @@ class HipAlexNet3D:
             # the weight-gradient branch of this launch shape (one per shape: side lanes run shapes concurrently)
             if d.type == "cuda":
                 b["wstream"] = torch.cuda.Stream(device=d)
+        if _BPACK:
+            self._batched_pack_plan(G, b, train)
         self._cache[key] = b
         return b
+
+    def _batched_pack_plan(self, G, b, train):
+        """conv2-5 weight images of all G clients in one buffer, packed by two launches per step (``pack.hip``
+        ``pack_convs``: a plain grid over the four layers, then a transpose grid) instead of two per layer;
+        ``b["w%dp"]`` / ``b["w%dt"]`` become views of that buffer."""
+        import numpy as np
+
+        from .resnet2d_hip import _PACK_DTYPE
+        if self.m.pack_desc_bytes() != _PACK_DTYPE.itemsize:
+            raise RuntimeError("pack.hip PackDesc layout changed")
+        desc = np.zeros(4, dtype=_PACK_DTYPE)
+        off = nplain = ntrans = 0
+        views = []
+        for i, (ci, bi, cin, cout, pad, sp) in enumerate((L2, L3, L4, L5)):
+            dd = desc[i]
+            dd["src_off"] = self.o["features.%d.weight" % ci]
+            dd["cout"], dd["cin_p"], dd["cin_src"], dd["kt"] = cout, cin, cin, 27
+            dd["blk_plain"], dd["blk_t"], dd["blk_plain1"] = nplain, ntrans, 0
+            dd["slot"][:] = np.arange(26, -1, -1)  # stride 1: the flipped kernel
+            n = G * cout * 27 * cin
+            dd["wp_off"], off, nplain = off, off + n, nplain + cout
+            vt = None
+            if train:
+                dd["wt_off"], vt, off = off, off, off + n
+                ntrans += ((cin + 63) // 64) * ((cout + 63) // 64) * 27
+            else:
+                dd["wt_off"] = -1
+            views.append((ci, cin, cout, int(dd["wp_off"]), vt))
+        buf = torch.empty(off, dtype=torch.bfloat16, device=self.dev)
+        for ci, cin, cout, op, ot in views:
+            n = G * cout * 27 * cin
+            b["w%dp" % ci] = buf[op:op + n].view(G, cout, 27, cin)
+            if ot is not None:
+                b["w%dt" % ci] = buf[ot:ot + n].view(G, cin, 27, cout)
+        lds = max(27 * L[2] * 4 for L in (L2, L3, L4, L5))
+        b["bpack"] = (torch.from_numpy(desc.view(np.uint8).copy()).to(self.dev), nplain, ntrans, lds, buf)
 
     def _conv(self, b, key, x, w, bias, y, stats, G, B, D, H, W, cin, cout, pad, st, theta=None, ci=None):
         """conv3d_fwd, or its split-K form when ``b[key]`` (chosen at allocation) is > 1.  With ``theta`` the bias
@@ -199,6 +240,10 @@ class HipAlexNet3D:
         P = theta.stride(0)
         m.pack_conv1_w(_p(theta), P, self.o["features.0.weight"], self.o["features.1.weight"], G, 1.0 / 255.0,
                        _p(b["w1p"]), _p(b["w125"]), st)
+        if "bpack" in b:
+            tab, nplain, ntrans, lds, buf = b["bpack"]
+            m.pack_convs(_p(tab), 4, nplain, 0, ntrans, lds, _p(theta), P, G, _p(buf), st)
+            return
         for (ci, bi, cin, cout, pad, sp) in (L2, L3, L4, L5):
             m.pack_conv_w(_p(theta), P, self.o["features.%d.weight" % ci], G, cout, cin, 1.0, _p(b["w%dp" % ci]),
                           _p(b["w%dt" % ci]) if train else 0, st)
