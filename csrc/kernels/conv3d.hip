@@ -351,7 +351,42 @@ __device__ __forceinline__ void blds16(i32x4_t rsrc, int voffset, uint16_t* lds_
   nidt_raw_buffer_load_lds(rsrc, (__attribute__((address_space(3))) uint32_t*)(lds_wave_base), 16, voffset, 0, 0, 0);
 }
 
-template <int BCO, int WM, int WN, int NST, bool BIAS, bool STATS>
+// [SCHED] one 64-deep k-step (two 32-deep MFMA halves) of a wave's TCO x TP fragment tile with every fragment in its
+// own registers: the second half's LDS reads issue between the first half's MFMAs, so the wave waits on LDS about
+// once per k-step.  The compiler's own schedule of the same loop re-reads each weight fragment into one register set
+// (an LDS round trip per TP MFMAs), which two waves per SIMD cannot cover.  fa_at(kk, i) / fb_at(kk, j) read the
+// fragments.  The closing sched_barrier keeps the MFMAs ahead of the caller's wait + barrier: hoisted above it, they
+// would leave the next k-step's tile loads only a few MFMAs to land in.
+template <int TCO, int TP, class FA, class FB>
+__device__ __forceinline__ void kstep_sched(f32x4 (&acc)[TCO][TP], FA fa_at, FB fb_at) {
+  bf16x8 fa[2][TCO], fb[2][TP];
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk) {
+#pragma unroll
+    for (int i = 0; i < TCO; ++i) fa[kk][i] = fa_at(kk, i);
+#pragma unroll
+    for (int j = 0; j < TP; ++j) fb[kk][j] = fb_at(kk, j);
+  }
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+    for (int i = 0; i < TCO; ++i)
+#pragma unroll
+      for (int j = 0; j < TP; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[kk][i], fb[kk][j], acc[i][j], 0, 0, 0);
+  __builtin_amdgcn_sched_group_barrier(0x100, TCO + TP, 0);  // DS_READ: first half's fragments
+#pragma unroll
+  for (int x = 0; x < TCO + TP; ++x) {
+    __builtin_amdgcn_sched_group_barrier(0x8, 1, 0);    // MFMA
+    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS_READ of the second half
+  }
+  __builtin_amdgcn_sched_group_barrier(0x8, 2 * TCO * TP - (TCO + TP), 0);
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+// [SCHED] on the 64-channel (one wave per channel block, two waves per SIMD) forward blocks: NIDT_DMA_SCHED=0 turns
+// it off (A/B)
+template <int BCO, int WM, int WN, int NST, bool BIAS, bool STATS, bool SCHED = false>
 __global__ __launch_bounds__(64 * WM * WN, ((NST == 2 ? 8 : 4) / (WM * WN)) > 0 ? (NST == 2 ? 8 : 4) / (WM * WN) : 1) void k_conv_fwd_dma(ConvFwdArgs a, int nCO) {
   // waves: WM (co) x WN (positions); each wave owns (BCO/WM) co x 64 positions
   constexpr int NW = WM * WN, BP = 64 * WN, BK = 64;
@@ -470,6 +505,18 @@ __global__ __launch_bounds__(64 * WM * WN, ((NST == 2 ? 8 : 4) / (WM * WN)) > 0 
     }
     const uint16_t* sA = smem + cur * BUF;
     const uint16_t* sB = sA + A_ELEMS;
+    if constexpr (SCHED) {
+      kstep_sched<TCO, TP>(
+          acc,
+          [&](int kk, int i) {
+            const int r = wco * WCO + i * 16 + fr;
+            return *reinterpret_cast<const bf16x8*>(&sA[r * BK + (((4 * kk + fq) ^ swz_dma(r)) << 3)]);
+          },
+          [&](int kk, int j) {
+            const int r = wp * WP + j * 16 + fr;
+            return *reinterpret_cast<const bf16x8*>(&sB[r * BK + (((4 * kk + fq) ^ swz_dma(r)) << 3)]);
+          });
+    } else {
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       bf16x8 fa[TCO], fb[TP];
@@ -487,6 +534,7 @@ __global__ __launch_bounds__(64 * WM * WN, ((NST == 2 ? 8 : 4) / (WM * WN)) > 0 
       for (int i = 0; i < TCO; ++i)
 #pragma unroll
         for (int j = 0; j < TP; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    }
     }
     // retire stage ks+1 (this wave's own glds), keep the younger stages in flight, then one barrier so
     // every wave's part of stage ks+1 has landed and every wave is done reading stage ks.
@@ -680,7 +728,8 @@ __device__ __forceinline__ int swz_l(int l) { return ((l >> 1) & 3) << 1; }
 // [NA] weight-tile stages: 2 = double buffer (the tile of k-step ks + 1 lands under k-step ks), 3 = two tiles in
 // flight (the 64-channel blocks: 3 x 8 KB + the union still leave two blocks per CU).  Measured not faster (conv2
 // data gradient 3.32-3.35 vs 3.25 ms, profiles/r4_ab_slab_stages.txt): NA = 3 is opt-in (NIDT_SLAB_NA=3).
-template <int BCO, int WM, int WN, int U, bool PADDED, bool BIAS, bool STATS, bool LSW = true, int NA = 2>
+template <int BCO, int WM, int WN, int U, bool PADDED, bool BIAS, bool STATS, bool LSW = true, int NA = 2,
+          bool SCHED = false>
 __global__ __launch_bounds__(64 * WM * WN, 2) void k_conv_fwd_slab(ConvFwdArgs a, int nCO, const int* __restrict__ utab) {
   constexpr int NW = WM * WN, BP = 64 * WN, BK = 64;
   constexpr int WCO = BCO / WM, WP = 64, TCO = WCO / 16, TP = WP / 16;
@@ -796,6 +845,19 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void k_conv_fwd_slab(ConvFwdArgs a
     const uint16_t* sA = sAb + bcur * A_ELEMS;
     bcur = bnext;
     const int toff = kh * Wp + kw, loff = kh * a.Wo + kw;
+    if constexpr (SCHED) {  // [SCHED] (kstep_sched)
+      kstep_sched<TCO, TP>(
+          acc,
+          [&](int kk, int i) {
+            const int r = wco * WCO + i * 16 + fr;
+            return *reinterpret_cast<const bf16x8*>(&sA[r * BK + (((4 * kk + fq) ^ swz_dma(r)) << 3)]);
+          },
+          [&](int kk, int j) {
+            const int r = hrow[j] + toff;
+            const int sw = LSW ? swz_l(hl[j] + loff) : swz_un(r);
+            return *reinterpret_cast<const bf16x8*>(&sU[r * BK + (((4 * kk + fq) ^ sw) << 3)]);
+          });
+    } else {
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       bf16x8 fa[TCO], fb[TP];
@@ -814,6 +876,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void k_conv_fwd_slab(ConvFwdArgs a
       for (int i = 0; i < TCO; ++i)
 #pragma unroll
         for (int j = 0; j < TP; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    }
     }
     // the tile of k-step ks + 1 must have landed; with three stages the one of ks + 2 may stay in flight
     if (NA == 3 && ks + 2 < nks) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(A_INSTR) : "memory");
@@ -1053,9 +1116,29 @@ __global__ __launch_bounds__(1024) void k_fwd_splitk_fin(const float* __restrict
 int conv3d_fwd_bp(int Cin, int Cout, int xf, int G, int Mg);
 
 // launch one k_conv_fwd_dma variant; the 3-stage pipeline only where 3 LDS stages fit in 160 KB
+static int dma_sched() {
+  static const int env = [] {
+    const char* e = getenv("NIDT_DMA_SCHED");
+    return e ? atoi(e) : 1;
+  }();
+  return env;
+}
+
 template <int BC, int WM, int WN, bool BI, bool ST>
 static void launch_fwd_dma(int nst, dim3 g, hipStream_t s, const ConvFwdArgs& a, int nCO) {
   constexpr int kStageBytes = (BC + 64 * WN) * 64 * 2;
+  if constexpr (BC == 64 && WM == 1) {
+    if (dma_sched()) {
+      if constexpr (3 * kStageBytes <= 160 * 1024) {
+        if (nst == 3) {
+          hipLaunchKernelGGL((k_conv_fwd_dma<BC, WM, WN, 3, BI, ST, true>), g, dim3(64 * WM * WN), 0, s, a, nCO);
+          return;
+        }
+      }
+      hipLaunchKernelGGL((k_conv_fwd_dma<BC, WM, WN, 2, BI, ST, true>), g, dim3(64 * WM * WN), 0, s, a, nCO);
+      return;
+    }
+  }
   if constexpr (3 * kStageBytes <= 160 * 1024) {
     if (nst == 3) {
       hipLaunchKernelGGL((k_conv_fwd_dma<BC, WM, WN, 3, BI, ST>), g, dim3(64 * WM * WN), 0, s, a, nCO);
@@ -1530,16 +1613,28 @@ static void fwd_slab_impl(uintptr_t x, uintptr_t w, uintptr_t bias, int64_t bias
     const char* e = getenv("NIDT_SLAB_NA");
     return e ? (atoi(e) == 3) : 0;
   }();
-#define NIDT_FS_U(BC, WM, UU, PD, BI, STT)                                                                         \
+  // [SCHED] fragment schedule for the 64-channel blocks (AlexNet conv2 data gradient 3.25 -> 3.00 ms at 64 clients,
+  // profiles/r4_ab_slab_sched.txt; the 128-channel blocks would need > 128 VGPRs and lose their second block per CU:
+  // conv2 forward 2.55 -> 3.23 ms).  NIDT_SLAB_SCHED=0: the compiler's schedule (A/B)
+  static const int sched = [] {
+    const char* e = getenv("NIDT_SLAB_SCHED");
+    return e ? atoi(e) : 1;
+  }();
+#define NIDT_FS_U(BC, WM, UU, PD, BI, STT)                                                                        \
   if (lswz) hipLaunchKernelGGL((k_conv_fwd_slab<BC, WM, 4, UU, PD, BI, STT, true>), grid, dim3(256 * WM), 0, s, a,   \
                                nCO, tab);                                                                          \
   else if (na3 && BC == 64)                                                                                        \
     hipLaunchKernelGGL((k_conv_fwd_slab<BC, WM, 4, UU, PD, BI, STT, false, (BC == 64 ? 3 : 2)>), grid,            \
                        dim3(256 * WM), 0, s, a, nCO, tab);                                                         \
+  else if (sched && BC == 64)                                                                                      \
+    hipLaunchKernelGGL((k_conv_fwd_slab<BC, WM, 4, UU, PD, BI, STT, false, 2, BC == 64>), grid, dim3(256 * WM), 0, s, \
+                       a, nCO, tab);                                                                               \
   else hipLaunchKernelGGL((k_conv_fwd_slab<BC, WM, 4, UU, PD, BI, STT, false>), grid, dim3(256 * WM), 0, s, a, nCO, tab)
 #define NIDT_FS_B(BC, WM, UU, PD)                                                                                  \
   if (st) NIDT_FS_U(BC, WM, UU, PD, true, true); else if (hb) NIDT_FS_U(BC, WM, UU, PD, true, false);            \
   else NIDT_FS_U(BC, WM, UU, PD, false, false);
+  // (8-wave 64-channel blocks, two 32-channel halves: conv2 data gradient 3.49 vs 3.25 ms — more VALU per MFMA from
+  // the duplicated B addressing; profiles/r4_ab_slab_sched.txt, not kept)
   if (bco == 128) {
     if (pad) { NIDT_FS_B(128, 2, 384, true) } else { NIDT_FS_B(128, 2, 384, false) }
   } else if (slab_u(B, D, H, W, pad) == 416) {
