@@ -384,9 +384,30 @@ __device__ __forceinline__ void kstep_sched(f32x4 (&acc)[TCO][TP], FA fa_at, FB 
   __builtin_amdgcn_sched_barrier(0);
 }
 
+// [SCHED-half] the register-lean form for blocks at four waves per SIMD (<= 128 VGPRs): one 32-deep half's
+// fragments at a time, all of its reads ahead of its MFMAs
+template <int TCO, int TP, class FA, class FB>
+__device__ __forceinline__ void kstep_sched_half(f32x4 (&acc)[TCO][TP], FA fa_at, FB fb_at) {
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk) {
+    bf16x8 fa[TCO], fb[TP];
+#pragma unroll
+    for (int i = 0; i < TCO; ++i) fa[i] = fa_at(kk, i);
+#pragma unroll
+    for (int j = 0; j < TP; ++j) fb[j] = fb_at(kk, j);
+#pragma unroll
+    for (int i = 0; i < TCO; ++i)
+#pragma unroll
+      for (int j = 0; j < TP; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_sched_group_barrier(0x100, TCO + TP, 0);
+    __builtin_amdgcn_sched_group_barrier(0x8, TCO * TP, 0);
+  }
+  __builtin_amdgcn_sched_barrier(0);
+}
+
 // [SCHED] on the 64-channel (one wave per channel block, two waves per SIMD) forward blocks: NIDT_DMA_SCHED=0 turns
 // it off (A/B)
-template <int BCO, int WM, int WN, int NST, bool BIAS, bool STATS, bool SCHED = false>
+template <int BCO, int WM, int WN, int NST, bool BIAS, bool STATS, int SCHED = 0>
 __global__ __launch_bounds__(64 * WM * WN, ((NST == 2 ? 8 : 4) / (WM * WN)) > 0 ? (NST == 2 ? 8 : 4) / (WM * WN) : 1) void k_conv_fwd_dma(ConvFwdArgs a, int nCO) {
   // waves: WM (co) x WN (positions); each wave owns (BCO/WM) co x 64 positions
   constexpr int NW = WM * WN, BP = 64 * WN, BK = 64;
@@ -505,17 +526,18 @@ __global__ __launch_bounds__(64 * WM * WN, ((NST == 2 ? 8 : 4) / (WM * WN)) > 0 
     }
     const uint16_t* sA = smem + cur * BUF;
     const uint16_t* sB = sA + A_ELEMS;
-    if constexpr (SCHED) {
-      kstep_sched<TCO, TP>(
-          acc,
-          [&](int kk, int i) {
-            const int r = wco * WCO + i * 16 + fr;
-            return *reinterpret_cast<const bf16x8*>(&sA[r * BK + (((4 * kk + fq) ^ swz_dma(r)) << 3)]);
-          },
-          [&](int kk, int j) {
-            const int r = wp * WP + j * 16 + fr;
-            return *reinterpret_cast<const bf16x8*>(&sB[r * BK + (((4 * kk + fq) ^ swz_dma(r)) << 3)]);
-          });
+    auto fa_at = [&](int kk, int i) {
+      const int r = wco * WCO + i * 16 + fr;
+      return *reinterpret_cast<const bf16x8*>(&sA[r * BK + (((4 * kk + fq) ^ swz_dma(r)) << 3)]);
+    };
+    auto fb_at = [&](int kk, int j) {
+      const int r = wp * WP + j * 16 + fr;
+      return *reinterpret_cast<const bf16x8*>(&sB[r * BK + (((4 * kk + fq) ^ swz_dma(r)) << 3)]);
+    };
+    if constexpr (SCHED == 1) {
+      kstep_sched<TCO, TP>(acc, fa_at, fb_at);
+    } else if constexpr (SCHED == 2) {
+      kstep_sched_half<TCO, TP>(acc, fa_at, fb_at);
     } else {
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
@@ -729,7 +751,7 @@ __device__ __forceinline__ int swz_l(int l) { return ((l >> 1) & 3) << 1; }
 // flight (the 64-channel blocks: 3 x 8 KB + the union still leave two blocks per CU).  Measured not faster (conv2
 // data gradient 3.32-3.35 vs 3.25 ms, profiles/r4_ab_slab_stages.txt): NA = 3 is opt-in (NIDT_SLAB_NA=3).
 template <int BCO, int WM, int WN, int U, bool PADDED, bool BIAS, bool STATS, bool LSW = true, int NA = 2,
-          bool SCHED = false>
+          int SCHED = 0>
 __global__ __launch_bounds__(64 * WM * WN, 2) void k_conv_fwd_slab(ConvFwdArgs a, int nCO, const int* __restrict__ utab) {
   constexpr int NW = WM * WN, BP = 64 * WN, BK = 64;
   constexpr int WCO = BCO / WM, WP = 64, TCO = WCO / 16, TP = WP / 16;
@@ -845,18 +867,19 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void k_conv_fwd_slab(ConvFwdArgs a
     const uint16_t* sA = sAb + bcur * A_ELEMS;
     bcur = bnext;
     const int toff = kh * Wp + kw, loff = kh * a.Wo + kw;
-    if constexpr (SCHED) {  // [SCHED] (kstep_sched)
-      kstep_sched<TCO, TP>(
-          acc,
-          [&](int kk, int i) {
-            const int r = wco * WCO + i * 16 + fr;
-            return *reinterpret_cast<const bf16x8*>(&sA[r * BK + (((4 * kk + fq) ^ swz_dma(r)) << 3)]);
-          },
-          [&](int kk, int j) {
-            const int r = hrow[j] + toff;
-            const int sw = LSW ? swz_l(hl[j] + loff) : swz_un(r);
-            return *reinterpret_cast<const bf16x8*>(&sU[r * BK + (((4 * kk + fq) ^ sw) << 3)]);
-          });
+    auto fa_at = [&](int kk, int i) {
+      const int r = wco * WCO + i * 16 + fr;
+      return *reinterpret_cast<const bf16x8*>(&sA[r * BK + (((4 * kk + fq) ^ swz_dma(r)) << 3)]);
+    };
+    auto fb_at = [&](int kk, int j) {
+      const int r = hrow[j] + toff;
+      const int sw = LSW ? swz_l(hl[j] + loff) : swz_un(r);
+      return *reinterpret_cast<const bf16x8*>(&sU[r * BK + (((4 * kk + fq) ^ sw) << 3)]);
+    };
+    if constexpr (SCHED == 1) {  // [SCHED] (kstep_sched)
+      kstep_sched<TCO, TP>(acc, fa_at, fb_at);
+    } else if constexpr (SCHED == 2) {  // [SCHED-half]
+      kstep_sched_half<TCO, TP>(acc, fa_at, fb_at);
     } else {
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
@@ -1131,11 +1154,17 @@ static void launch_fwd_dma(int nst, dim3 g, hipStream_t s, const ConvFwdArgs& a,
     if (dma_sched()) {
       if constexpr (3 * kStageBytes <= 160 * 1024) {
         if (nst == 3) {
-          hipLaunchKernelGGL((k_conv_fwd_dma<BC, WM, WN, 3, BI, ST, true>), g, dim3(64 * WM * WN), 0, s, a, nCO);
+          hipLaunchKernelGGL((k_conv_fwd_dma<BC, WM, WN, 3, BI, ST, 1>), g, dim3(64 * WM * WN), 0, s, a, nCO);
           return;
         }
       }
-      hipLaunchKernelGGL((k_conv_fwd_dma<BC, WM, WN, 2, BI, ST, true>), g, dim3(64 * WM * WN), 0, s, a, nCO);
+      hipLaunchKernelGGL((k_conv_fwd_dma<BC, WM, WN, 2, BI, ST, 1>), g, dim3(64 * WM * WN), 0, s, a, nCO);
+      return;
+    }
+  }
+  if constexpr (BC == 128 && WM == 2 && WN == 4) {  // NIDT_DMA_SCHED=2: [SCHED] on the 128-channel blocks too (A/B)
+    if (dma_sched() == 2 && nst == 2) {
+      hipLaunchKernelGGL((k_conv_fwd_dma<BC, WM, WN, 2, BI, ST, 1>), g, dim3(64 * WM * WN), 0, s, a, nCO);
       return;
     }
   }
@@ -1615,7 +1644,8 @@ static void fwd_slab_impl(uintptr_t x, uintptr_t w, uintptr_t bias, int64_t bias
   }();
   // [SCHED] fragment schedule for the 64-channel blocks (AlexNet conv2 data gradient 3.25 -> 3.00 ms at 64 clients,
   // profiles/r4_ab_slab_sched.txt; the 128-channel blocks would need > 128 VGPRs and lose their second block per CU:
-  // conv2 forward 2.55 -> 3.23 ms).  NIDT_SLAB_SCHED=0: the compiler's schedule (A/B)
+  // conv2 forward 2.55 -> 3.23 ms).  NIDT_SLAB_SCHED=0: the compiler's schedule (A/B); =2 adds [SCHED-half] on the
+  // 128-channel blocks (A/B)
   static const int sched = [] {
     const char* e = getenv("NIDT_SLAB_SCHED");
     return e ? atoi(e) : 1;
@@ -1627,8 +1657,11 @@ static void fwd_slab_impl(uintptr_t x, uintptr_t w, uintptr_t bias, int64_t bias
     hipLaunchKernelGGL((k_conv_fwd_slab<BC, WM, 4, UU, PD, BI, STT, false, (BC == 64 ? 3 : 2)>), grid,            \
                        dim3(256 * WM), 0, s, a, nCO, tab);                                                         \
   else if (sched && BC == 64)                                                                                      \
-    hipLaunchKernelGGL((k_conv_fwd_slab<BC, WM, 4, UU, PD, BI, STT, false, 2, BC == 64>), grid, dim3(256 * WM), 0, s, \
-                       a, nCO, tab);                                                                               \
+    hipLaunchKernelGGL((k_conv_fwd_slab<BC, WM, 4, UU, PD, BI, STT, false, 2, (BC == 64 ? 1 : 0)>), grid,         \
+                       dim3(256 * WM), 0, s, a, nCO, tab);                                                         \
+  else if (sched == 2 && BC == 128 && !PD)                                                                         \
+    hipLaunchKernelGGL((k_conv_fwd_slab<BC, WM, 4, UU, PD, BI, STT, false, 2, (BC == 128 && !PD ? 2 : 0)>), grid, \
+                       dim3(256 * WM), 0, s, a, nCO, tab);                                                         \
   else hipLaunchKernelGGL((k_conv_fwd_slab<BC, WM, 4, UU, PD, BI, STT, false>), grid, dim3(256 * WM), 0, s, a, nCO, tab)
 #define NIDT_FS_B(BC, WM, UU, PD)                                                                                  \
   if (st) NIDT_FS_U(BC, WM, UU, PD, true, true); else if (hb) NIDT_FS_U(BC, WM, UU, PD, true, false);            \
