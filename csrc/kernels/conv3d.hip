@@ -355,9 +355,10 @@ __device__ __forceinline__ void blds16(i32x4_t rsrc, int voffset, uint16_t* lds_
 // own registers: the second half's LDS reads issue between the first half's MFMAs, so the wave waits on LDS about
 // once per k-step.  The compiler's own schedule of the same loop re-reads each weight fragment into one register set
 // (an LDS round trip per TP MFMAs), which two waves per SIMD cannot cover.  fa_at(kk, i) / fb_at(kk, j) read the
-// fragments.  The closing sched_barrier keeps the MFMAs ahead of the caller's wait + barrier: hoisted above it, they
-// would leave the next k-step's tile loads only a few MFMAs to land in.
-template <int TCO, int TP, class FA, class FB>
+// fragments with RPF LDS read instructions each (2 for the transposed-read pairs of the weight-gradient kernels).  The
+// closing sched_barrier keeps the MFMAs ahead of the caller's wait + barrier: hoisted above it, they would leave the
+// next k-step's tile loads only a few MFMAs to land in.
+template <int TCO, int TP, int RPF = 1, class FA, class FB>
 __device__ __forceinline__ void kstep_sched(f32x4 (&acc)[TCO][TP], FA fa_at, FB fb_at) {
   bf16x8 fa[2][TCO], fb[2][TP];
 #pragma unroll
@@ -374,11 +375,11 @@ __device__ __forceinline__ void kstep_sched(f32x4 (&acc)[TCO][TP], FA fa_at, FB 
 #pragma unroll
       for (int j = 0; j < TP; ++j)
         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[kk][i], fb[kk][j], acc[i][j], 0, 0, 0);
-  __builtin_amdgcn_sched_group_barrier(0x100, TCO + TP, 0);  // DS_READ: first half's fragments
+  __builtin_amdgcn_sched_group_barrier(0x100, RPF * (TCO + TP), 0);  // DS_READ: first half's fragments
 #pragma unroll
   for (int x = 0; x < TCO + TP; ++x) {
-    __builtin_amdgcn_sched_group_barrier(0x8, 1, 0);    // MFMA
-    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS_READ of the second half
+    __builtin_amdgcn_sched_group_barrier(0x8, 1, 0);      // MFMA
+    __builtin_amdgcn_sched_group_barrier(0x100, RPF, 0);  // DS_READ of the second half
   }
   __builtin_amdgcn_sched_group_barrier(0x8, 2 * TCO * TP - (TCO + TP), 0);
   __builtin_amdgcn_sched_barrier(0);
@@ -2063,7 +2064,7 @@ __device__ __forceinline__ int swz_wd(int r) { return (r & 2) | ((r >> 1) & 4); 
 // the X tile of a k-step feeds twice the MFMAs, 48 KB of LDS-DMA per 256 MFMAs instead of 40 KB per 128).
 // Wave (wc, wk) = (wid / 4, wid % 4) computes co half wc x X group wk; it stages 8/NCH of group wk's 8 X
 // instructions and dY half wc's slices 2wk, 2wk+1.
-template <int NCH>
+template <int NCH, bool SCHED = false>
 __global__ __launch_bounds__(256 * NCH, 2 / NCH) void k_conv_wgrad_dma(ConvWgDmaArgs a) {
   constexpr int BUFE = (4 + NCH) * kWdGroup;  // elements per stage: 4 X groups + NCH dY halves
   constexpr int XI = 8 / NCH;                  // X instructions per wave per stage
@@ -2141,6 +2142,15 @@ __global__ __launch_bounds__(256 * NCH, 2 / NCH) void k_conv_wgrad_dma(ConvWgDma
     }
     const uint16_t* sX = smem + cur * BUFE + wk * kWdGroup;
     const uint16_t* sD = smem + cur * BUFE + (4 + wc) * kWdGroup;
+    if constexpr (SCHED) {  // [SCHED] (kstep_sched)
+      auto frag = [&](const uint16_t* base, int kk, int i) {
+        const int ra = 32 * kk + rr0, rb = 32 * kk + rr1, c = 2 * i + (pp >> 1);
+        return tr_pair(base + ra * kWdRow + ((c ^ swz_wd(ra)) << 3) + (pp & 1) * 4,
+                       base + rb * kWdRow + ((c ^ swz_wd(rb)) << 3) + (pp & 1) * 4);
+      };
+      kstep_sched<4, 4, 2>(acc, [&](int kk, int i) { return frag(sD, kk, i); },
+                           [&](int kk, int j) { return frag(sX, kk, j); });
+    } else {
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {  // two 32-position MFMA k-steps
       const int ra = 32 * kk + rr0, rb = 32 * kk + rr1;
@@ -2157,6 +2167,7 @@ __global__ __launch_bounds__(256 * NCH, 2 / NCH) void k_conv_wgrad_dma(ConvWgDma
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    }
     }
     // retire this step's LDS-DMA (next stage) but leave the XI position-table loads for step st+2 in flight: they
     // are the youngest vector-memory ops and are only consumed by the next step's DMA issue
@@ -2292,7 +2303,7 @@ int conv3d_union_umax(int B, int D, int H, int W, int pad, int P) { return union
 // read -> 1.00).  The dY rows are the step's positions themselves and keep swz_wd of their row.  Measured: conflicts
 // 20.8 / 33.2 % -> 0.1 / 1.7 % (conv2 / conv3-5) but conv2 2.92-2.98 -> 3.22-3.29 ms (the per-step swizzle of the
 // DMA addresses sits on the issue path); opt-in NIDT_WGTRI_LSWZ=1 (profiles/r4_ab_lds_swizzle.txt).
-template <int NCH, int U, bool PADDED, bool LSW = true>
+template <int NCH, int U, bool PADDED, bool LSW = true, bool SCHED = false>
 __global__ __launch_bounds__(192 * NCH, 2) void k_conv_wgrad_tri(ConvWgTriArgs a) {
   constexpr int NW = 3 * NCH, XG = U * kWdRow, BUFE = XG + NCH * kWdGroup, ST = WtTab<U>::kST;
   constexpr int XP = U / 8, XPW = (XP + NW - 1) / NW;       // union pieces (8 rows each) per wave
@@ -2393,6 +2404,21 @@ __global__ __launch_bounds__(192 * NCH, 2) void k_conv_wgrad_tri(ConvWgTriArgs a
     }
     const uint16_t* sX = smem + cur * BUFE;
     const uint16_t* sD = sX + XG + wc * kWdGroup;
+    if constexpr (SCHED) {  // [SCHED] (kstep_sched)
+      kstep_sched<4, 4, 2>(
+          acc,
+          [&](int kk, int i) {
+            const int ra = 32 * kk + rr0, rb = 32 * kk + rr1, c = 2 * i + (pp >> 1);
+            return tr_pair(sD + ra * kWdRow + ((c ^ swz_wd(ra)) << 3) + (pp & 1) * 4,
+                           sD + rb * kWdRow + ((c ^ swz_wd(rb)) << 3) + (pp & 1) * 4);
+          },
+          [&](int kk, int j) {
+            const int xa = tix[2 * kk] + kw, xb = tix[2 * kk + 1] + kw, c = 2 * j + (pp >> 1);
+            const int sxa = swz_wd(LSW ? lpos[2 * kk] + kw : xa), sxb = swz_wd(LSW ? lpos[2 * kk + 1] + kw : xb);
+            return tr_pair(sX + xa * kWdRow + ((c ^ sxa) << 3) + (pp & 1) * 4,
+                           sX + xb * kWdRow + ((c ^ sxb) << 3) + (pp & 1) * 4);
+          });
+    } else {
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       const int ra = 32 * kk + rr0, rb = 32 * kk + rr1;
@@ -2411,6 +2437,7 @@ __global__ __launch_bounds__(192 * NCH, 2) void k_conv_wgrad_tri(ConvWgTriArgs a
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    }
     }
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -2685,8 +2712,15 @@ void conv3d_wgrad_tri(uintptr_t x, uintptr_t dy, uintptr_t part, uintptr_t grad,
     return e ? atoi(e) : 0;
   }();
   const bool lsw = lsw_env && d.Mg / B >= 64;  // the kernel advances its output-space indices by 64 per step
+  static const int tsched = [] {  // NIDT_WGT_SCHED=1: [SCHED] k-step schedule (kstep_sched), A/B
+    const char* e = getenv("NIDT_WGT_SCHED");
+    return e ? atoi(e) : 0;
+  }();
 #define NIDT_TRI(NC, UU)                                                                                       \
-  if (lsw) {                                                                                                   \
+  if (tsched && !lsw) {                                                                                        \
+    if (pad) hipLaunchKernelGGL((k_conv_wgrad_tri<NC, UU, true, false, true>), grid, dim3(192 * NC), 0, s, d); \
+    else hipLaunchKernelGGL((k_conv_wgrad_tri<NC, UU, false, false, true>), grid, dim3(192 * NC), 0, s, d);    \
+  } else if (lsw) {                                                                                            \
     if (pad) hipLaunchKernelGGL((k_conv_wgrad_tri<NC, UU, true, true>), grid, dim3(192 * NC), 0, s, d);        \
     else hipLaunchKernelGGL((k_conv_wgrad_tri<NC, UU, false, true>), grid, dim3(192 * NC), 0, s, d);           \
   } else {                                                                                                     \
@@ -2839,8 +2873,18 @@ static void conv_wgrad_impl(uintptr_t x, uintptr_t xs, uintptr_t xt, uintptr_t d
                  "conv3d_wgrad: per-client tensors must stay below 2 GiB (32-bit buffer offsets)");
     const int64_t nwg = (int64_t)d.nKT * d.nCT * nsplit * G;
     NIDT_REQUIRE(nwg < (1ll << 31), "conv3d_wgrad: grid too large");
-    if (nch == 2) hipLaunchKernelGGL(k_conv_wgrad_dma<2>, dim3((unsigned)nwg), dim3(512), 0, s, d);
-    else hipLaunchKernelGGL(k_conv_wgrad_dma<1>, dim3((unsigned)nwg), dim3(256), 0, s, d);
+    static const int wsched = [] {  // NIDT_WGD_SCHED=1: [SCHED] k-step schedule (kstep_sched), A/B
+      const char* e = getenv("NIDT_WGD_SCHED");
+      return e ? atoi(e) : 0;
+    }();
+    if (wsched) {
+      if (nch == 2) hipLaunchKernelGGL((k_conv_wgrad_dma<2, true>), dim3((unsigned)nwg), dim3(512), 0, s, d);
+      else hipLaunchKernelGGL((k_conv_wgrad_dma<1, true>), dim3((unsigned)nwg), dim3(256), 0, s, d);
+    } else if (nch == 2) {
+      hipLaunchKernelGGL(k_conv_wgrad_dma<2>, dim3((unsigned)nwg), dim3(512), 0, s, d);
+    } else {
+      hipLaunchKernelGGL(k_conv_wgrad_dma<1>, dim3((unsigned)nwg), dim3(256), 0, s, d);
+    }
   } else {
     dim3 grid(ceil_div(a.K, kWgKC), Cout / kWgCO, G * nsplit);
     if (xs) hipLaunchKernelGGL((k_conv_wgrad<true>), grid, dim3(256), 0, s, a);
