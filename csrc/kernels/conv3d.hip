@@ -2712,9 +2712,11 @@ void conv3d_wgrad_tri(uintptr_t x, uintptr_t dy, uintptr_t part, uintptr_t grad,
     return e ? atoi(e) : 0;
   }();
   const bool lsw = lsw_env && d.Mg / B >= 64;  // the kernel advances its output-space indices by 64 per step
-  static const int tsched = [] {  // NIDT_WGT_SCHED=1: [SCHED] k-step schedule (kstep_sched), A/B
+  // [SCHED] k-step schedule (kstep_sched): AlexNet conv2-5 weight gradients at 64 clients 4.28 -> 4.24 ms
+  // (profiles/r4_ab_sched_more.txt); NIDT_WGT_SCHED=0: the compiler's schedule (A/B)
+  static const int tsched = [] {
     const char* e = getenv("NIDT_WGT_SCHED");
-    return e ? atoi(e) : 0;
+    return e ? atoi(e) : 1;
   }();
 #define NIDT_TRI(NC, UU)                                                                                       \
   if (tsched && !lsw) {                                                                                        \
@@ -2873,9 +2875,11 @@ static void conv_wgrad_impl(uintptr_t x, uintptr_t xs, uintptr_t xt, uintptr_t d
                  "conv3d_wgrad: per-client tensors must stay below 2 GiB (32-bit buffer offsets)");
     const int64_t nwg = (int64_t)d.nKT * d.nCT * nsplit * G;
     NIDT_REQUIRE(nwg < (1ll << 31), "conv3d_wgrad: grid too large");
-    static const int wsched = [] {  // NIDT_WGD_SCHED=1: [SCHED] k-step schedule (kstep_sched), A/B
+    // [SCHED] k-step schedule (kstep_sched): AlexNet conv3-5 weight gradients at 8 clients -2.7 %, config 5 12.16 ->
+    // 12.10 s/round (profiles/r4_ab_sched_more.txt); NIDT_WGD_SCHED=0: the compiler's schedule (A/B)
+    static const int wsched = [] {
       const char* e = getenv("NIDT_WGD_SCHED");
-      return e ? atoi(e) : 0;
+      return e ? atoi(e) : 1;
     }();
     if (wsched) {
       if (nch == 2) hipLaunchKernelGGL((k_conv_wgrad_dma<2, true>), dim3((unsigned)nwg), dim3(512), 0, s, d);
