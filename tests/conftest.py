@@ -10,6 +10,14 @@ if ROOT not in sys.path:
 if "NIDT_RESULTS_DIR" not in os.environ:
     import tempfile
     os.environ["NIDT_RESULTS_DIR"] = tempfile.mkdtemp(prefix="nidt_results_")
+# pytest-xdist workers share the machine's cores: give each worker its share of intra-op threads (and the gloo ranks
+# it spawns inherit the variable).  Unbounded, 6 workers x all-core OpenMP pools on 8 CPUs stalled small autograd
+# graphs past the 900 s test timeout.
+_XW = os.environ.get("PYTEST_XDIST_WORKER_COUNT")
+if _XW and "OMP_NUM_THREADS" not in os.environ:
+    os.environ["OMP_NUM_THREADS"] = str(max(1, (os.cpu_count() or 8) // max(1, int(_XW))))
+    if "torch" in sys.modules:
+        sys.modules["torch"].set_num_threads(int(os.environ["OMP_NUM_THREADS"]))
 
 
 def pytest_configure(config):
