@@ -406,8 +406,7 @@ __device__ __forceinline__ void kstep_sched_half(f32x4 (&acc)[TCO][TP], FA fa_at
   __builtin_amdgcn_sched_barrier(0);
 }
 
-// [SCHED] on the 64-channel (one wave per channel block, two waves per SIMD) forward blocks: NIDT_DMA_SCHED=0 turns
-// it off (A/B)
+// [SCHED] on the forward blocks (dma_sched: NIDT_DMA_SCHED)
 template <int BCO, int WM, int WN, int NST, bool BIAS, bool STATS, int SCHED = 0>
 __global__ __launch_bounds__(64 * WM * WN, ((NST == 2 ? 8 : 4) / (WM * WN)) > 0 ? (NST == 2 ? 8 : 4) / (WM * WN) : 1) void k_conv_fwd_dma(ConvFwdArgs a, int nCO) {
   // waves: WM (co) x WN (positions); each wave owns (BCO/WM) co x 64 positions
@@ -1140,10 +1139,13 @@ __global__ __launch_bounds__(1024) void k_fwd_splitk_fin(const float* __restrict
 int conv3d_fwd_bp(int Cin, int Cout, int xf, int G, int Mg);
 
 // launch one k_conv_fwd_dma variant; the 3-stage pipeline only where 3 LDS stages fit in 160 KB
+// [SCHED] on the per-tap forward blocks: 1 = the 64-channel blocks, 2 (default) = the 128-channel blocks too (each of
+// the three A/Bs the same sign: 8-client step -0.6 %, 8-client round 15.25 -> 15.29 rounds/s, config 5 12.16 ->
+// 12.12 s/round; profiles/r4_ab_dma_sched.txt, r4_ab_sched_more.txt, r4_ab_dma_sched128.txt); 0 = off (A/B)
 static int dma_sched() {
   static const int env = [] {
     const char* e = getenv("NIDT_DMA_SCHED");
-    return e ? atoi(e) : 1;
+    return e ? atoi(e) : 2;
   }();
   return env;
 }
@@ -1163,8 +1165,14 @@ static void launch_fwd_dma(int nst, dim3 g, hipStream_t s, const ConvFwdArgs& a,
       return;
     }
   }
-  if constexpr (BC == 128 && WM == 2 && WN == 4) {  // NIDT_DMA_SCHED=2: [SCHED] on the 128-channel blocks too (A/B)
-    if (dma_sched() == 2 && nst == 2) {
+  if constexpr (BC == 128 && WM == 2) {
+    if (dma_sched() == 2) {
+      if constexpr (3 * kStageBytes <= 160 * 1024) {
+        if (nst == 3) {
+          hipLaunchKernelGGL((k_conv_fwd_dma<BC, WM, WN, 3, BI, ST, 1>), g, dim3(64 * WM * WN), 0, s, a, nCO);
+          return;
+        }
+      }
       hipLaunchKernelGGL((k_conv_fwd_dma<BC, WM, WN, 2, BI, ST, 1>), g, dim3(64 * WM * WN), 0, s, a, nCO);
       return;
     }
