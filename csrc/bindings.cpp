@@ -154,6 +154,7 @@ void conv1_bnstats(uintptr_t mom, uintptr_t idx, int B, int G, uintptr_t Mb, uin
 void conv1_fwd_pool(uintptr_t x8, uintptr_t idx, uintptr_t w8, uintptr_t scale, uintptr_t shift, int NB, int B,
                     uintptr_t out, uintptr_t amax, uintptr_t stream);
 int conv1_wgrad_nq(int NB);
+int conv1_wgrad_mx_npb(int NB);
 void conv1_wgrad_mode(int mode);
 int conv1_kslots();
 void conv1_wgrad(uintptr_t x8, uintptr_t idx, uintptr_t dp, uintptr_t pout, uintptr_t amax, int NB, int B,
@@ -287,6 +288,7 @@ PYBIND11_MODULE(_nidt_hip, m) {
   DEF(conv1_fwd_pool);
   DEF(conv1_wgrad);
   DEF(conv1_wgrad_nq);
+  DEF(conv1_wgrad_mx_npb);
   DEF(conv1_wgrad_mode);
   DEF(conv1_kslots);
   DEF(head);

@@ -17,9 +17,11 @@
 //      dw = gamma invstd (S - D mu - dgamma invstd Cov w),  db = 0
 //    which is exactly the gradient autograd computes through conv -> BN(train) -> ReLU -> pool.
 #include <cstdlib>
+#include <type_traits>
 
 #include "common.h"
 #include "conv1_wgrad_layout.h"
+#include "conv1_mx_layout.h"
 
 namespace nidt {
 
@@ -710,7 +712,7 @@ __device__ __forceinline__ int bid_slab(int n_pd, int q, int nq) { return n_pd *
 // clients per GPU there are only 64*G blocks to cover the L2/HBM latency), merged through LDS in a fixed order
 // (deterministic), then threads 0..127 (k) apply the closed form.
 constexpr int kFinW = 16;
-__global__ __launch_bounds__(64 * kFinW) void k_conv1_wgrad_fin(const float* __restrict__ part, int B,
+__global__ __launch_bounds__(64 * kFinW) void k_conv1_wgrad_fin(const float* __restrict__ part, int nslab,
                                                          const float* __restrict__ w125, const float* __restrict__ mu,
                                                          const float* __restrict__ covw,
                                                          const float* __restrict__ invstd, const float* theta,
@@ -721,7 +723,6 @@ __global__ __launch_bounds__(64 * kFinW) void k_conv1_wgrad_fin(const float* __r
   __shared__ double sD, sdg;
   __shared__ double wpart[kFinW][128];
   const int c = blockIdx.x, g = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int nslab = B * kPD;
   {
     const float* base = part + ((int64_t)g * nslab * kC1 + c) * 126;
     const int64_t sst = (int64_t)kC1 * 126;  // slab stride
@@ -1469,8 +1470,392 @@ __global__ __launch_bounds__(512, 1) void k_conv1_wgrad_smf(const uint8_t* __res
   }
 }
 
-// conv1 weight-gradient kernel: 0 = VALU gather (k_conv1_wgrad_split), 1 = 2:4 smfmac (k_conv1_wgrad_smf); -1 = the
-// NIDT_C1WG_SMF environment default
+// ------------------------------------------------------------------------------------------------
+// k_conv1_wgrad_mx — the conv1 weight-gradient slabs on 2:4-sparse matrix cores with the argmax ROW in the sparsity
+// index (v_smfmac_f32_32x32x32_bf16).
+//
+// K of S[c][k] = sum_pos dY[c][pos] X[2 pos + k] is ordered (dh, x, dd): a 4-group of K is the three conv positions
+// dd = 0, 1, 2 of one pooling-window column (dh, x) plus a pad slot.  A window column holds at most one argmax per
+// channel (a cell has one argmax, at (dd, dh, dw)), so every 4-group of a channel's dY row has <= 1 non-zero — legal
+// 2:4 — and its position in the group IS the argmax's dd.  Hence:
+//  * A (dY, 32 channels x 32 K per M-tile) is the same for the three dh of a pooled row: element 2i = dz of the
+//    cell covering the lane's x (dY = dz only where the argmax column is x: aw == x mod 3), element 2i + 1 = 0.  Only
+//    the 2-bit indices change with dh: dd where the argmax is in row dh, else 3 (the pad slot, whose B value is 0).
+//    The three index words come from ONE 32-bit OR per (channel, x) and stage — fields at bits 4i (dh 0), 16 + 4i
+//    (dh 1, read with abid 1) and 4i + 2 (dh 2: the dead element's field, read after a 2-bit shift) — instead of a
+//    per-row value mask (k_conv1_wgrad_smf: 23 VALU per smfmac);
+//  * B (input, 32 K x 32 taps per N-tile) comes from "dd-slot images": per jd = kd >> 1 an image of 4-slot groups
+//    [z' = 3 pd + jd + dd for dd = 0..2, 0] per (y', phase r, x'), so a tap's 16 K (4 groups at x' = x + jw) are 32
+//    contiguous bytes, 8-B aligned for every jw: no shifted copies, four ds_read_b64 per fragment, and all 125 taps
+//    share one A (4 N-tiles).
+// The images keep y' rows in an 8-slot ring (3 new rows per pooled row, 5 at a new pd slab); per-plane offsets and the
+// tap -> column order (conv1_mx_layout.h, tools/probes/c1mx_layout_gen.py) put the 32 taps of every N-tile on 32
+// distinct LDS bank pairs.  Cost: 4/3 of the minimal K (the pad slot) = 192 smfmac per pooled row and sample.
+//
+// Block = 8 waves, one per CU by LDS = (sample, range of pd slabs); wave w owns x = 8w .. 8w + 7 (one 32-K k-step per
+// dh) for all 64 channels (2 M-tiles) x 128 tap columns (4 N-tiles): 24 smfmac per pooled row, 128 accumulators.  The
+// next pooled row's staging (3 y' rows: uint8 -> bf16 into the three images; the row's (dz, argmax) records) is
+// loaded into registers before this row's MFMAs and stored after them: one barrier per pooled row.  Output
+// part[block][64][126] (125 S + D), summed per client by k_conv1_wgrad_fin.
+constexpr int kMxRing = 8;                         // y' ring slots (+ 2 mirrors of slots 0, 1: see below)
+constexpr int kMxSS8 = kMxSS * 8;                  // bytes per slot
+constexpr int kMxImgBytes = (kMxRing + 2) * kMxSS8;
+constexpr int kMxRecCells = kPW + 1;               // + a zero cell for the x beyond the pooled region
+constexpr int kMxRecBytes = kMxRecCells * kC1 * 8;
+constexpr int kMxLdsBytes = 135168;                // also the [8 waves][32][128] fp32 reduction scratch
+static_assert(kMxImgBytes + 2 * kMxRecBytes + 32 * 4 <= kMxLdsBytes, "LDS budget");
+static_assert(8 * 32 * 128 * 4 <= kMxLdsBytes && kMxLdsBytes <= 163840, "reduction scratch");
+static_assert(2 * kMxSS8 + 24 < 65536, "dh offsets must fit the ds_read immediate");
+constexpr int kMxRecItems = kPW * 16;              // (cell, channel quad) record items of a pooled row
+
+struct MxRec { uint2 pv, gv; uint32_t av; };      // 4 channels of one cell: pooled, dL/dpooled (bf16), argmax
+
+// y' row task (row, phase half H) of one wave: lane = x' (< 61); the 5 (H = 0) or 4 (H = 1) z' = 3 pd + z bytes
+template <int H>
+__device__ __forceinline__ void mx_load_row(uint32_t (&v)[5], const uint8_t* xs, int pd, int y, int xp) {
+  // lanes x' >= 61 read x' = 60 (their stores are skipped): unpredicated loads
+  const uint8_t* src = xs + (((int64_t)(3 * pd) * kPY + y) * kPX + min(xp, kPX - 1)) * 8 + 4 * H;
+  constexpr int64_t zs = (int64_t)kPY * kPX * 8;
+#pragma unroll
+  for (int z = 0; z < 5; ++z) v[z] = (H == 0 || z < 4) ? *reinterpret_cast<const uint32_t*>(src + z * zs) : 0u;
+}
+
+// into the images at ring slot s (wave-uniform; and its mirror s + 8 for s < 2): group [z' jd, jd + 1, jd + 2, 0] of
+// plane 8 jd + r, straight-line stores with immediate plane offsets
+template <int H>
+__device__ __forceinline__ void mx_store_row(const uint32_t (&v)[5], uint8_t* img, int s, int xp) {
+  constexpr int NJ = H == 0 ? 3 : 2;
+  uint2 g[NJ][4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    float f[5];
+#pragma unroll
+    for (int z = 0; z < NJ + 2; ++z) f[z] = u8f(v[z], r);
+#pragma unroll
+    for (int jd = 0; jd < NJ; ++jd) g[jd][r] = make_uint2(bf2_pack(f[jd], f[jd + 1]), __float_as_uint(f[jd + 2]) >> 16);
+  }
+  if (xp >= kPX) return;  // x' >= 61 stays the zero of the initialisation
+  uint8_t* base = img + s * kMxSS8 + xp * 8;
+#pragma unroll
+  for (int jd = 0; jd < NJ; ++jd)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) *reinterpret_cast<uint2*>(base + kMxPO[8 * jd + 4 * H + r] * 8) = g[jd][r];
+  if (s < 2) {
+    base += 8 * kMxSS8;
+#pragma unroll
+    for (int jd = 0; jd < NJ; ++jd)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) *reinterpret_cast<uint2*>(base + kMxPO[8 * jd + 4 * H + r] * 8) = g[jd][r];
+  }
+}
+
+__device__ __forceinline__ void mx_load_rec(MxRec& st, const uint16_t* dp, const uint16_t* pout, const uint8_t* amax,
+                                            int n, int pd, int ph, int item) {
+  const int pw = item >> 4, cq = item & 15;
+  const int64_t o = ((((int64_t)n * kPD + pd) * kPH + ph) * kPW + pw) * kC1 + 4 * cq;
+  st.pv = *reinterpret_cast<const uint2*>(pout + o);
+  st.gv = *reinterpret_cast<const uint2*>(dp + o);
+  st.av = *reinterpret_cast<const uint32_t*>(amax + o);
+}
+
+// record = (dz as bf16 in the low half, lut[argmax]): dz = dL/dpooled where the pooled value is > 0 (ReLU), else 0
+__device__ __forceinline__ void mx_store_rec(const MxRec& st, uint8_t* rec, const uint32_t* lut, int item) {
+  const int pw = item >> 4, cq = item & 15;
+  uint32_t o[8];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const uint32_t pw2 = j < 2 ? st.pv.x : st.pv.y, gw2 = j < 2 ? st.gv.x : st.gv.y;
+    const uint32_t p16 = (pw2 >> (16 * (j & 1))) & 0xffffu, g16 = (gw2 >> (16 * (j & 1))) & 0xffffu;
+    o[2 * j] = (int16_t)p16 > 0 ? g16 : 0u;
+    o[2 * j + 1] = lut[(st.av >> (8 * j)) & 0xffu];
+  }
+  uint4* d = reinterpret_cast<uint4*>(rec + (pw * kC1 + 4 * cq) * 8);
+  d[0] = make_uint4(o[0], o[1], o[2], o[3]);
+  d[1] = make_uint4(o[4], o[5], o[6], o[7]);
+}
+
+// stage S of a block (flat over its pd slabs x 23 pooled rows): slab, pooled row, ring offset (+5 per slab: the
+// first 5 rows of a new slab go to slots the last stage of the old one leaves free / frees at its end)
+struct MxStage {
+  int pd, ph, ro;
+};
+__device__ __forceinline__ MxStage mx_stage(int pd0, int S) {
+  const int sl = S / kPH;
+  return MxStage{pd0 + sl, S - sl * kPH, (5 * sl) & 7};
+}
+
+template <int DBG>
+__global__ __launch_bounds__(512, 1) void k_conv1_wgrad_mx(const uint8_t* __restrict__ x8, const int* __restrict__ idx,
+                                                          const uint16_t* __restrict__ dp,
+                                                          const uint16_t* __restrict__ pout,
+                                                          const uint8_t* __restrict__ amax, float* __restrict__ part,
+                                                          int npb, int nblk) {
+  __shared__ __attribute__((aligned(16))) uint8_t smem[kMxLdsBytes];
+  uint8_t* img = smem;
+  uint8_t* recb = smem + kMxImgBytes;
+  uint32_t* lut = reinterpret_cast<uint32_t*>(smem + kMxImgBytes + 2 * kMxRecBytes);
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int n = bid / nblk, jb = bid - n * nblk;
+  const int pd0 = jb * npb, pd1 = min(kPD, pd0 + npb);
+  const int nstage = (pd1 - pd0) * kPH;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int m = lane & 31, q = lane >> 5;
+  const uint8_t* xs = x8 + (int64_t)idx[n] * kPZ * kPY * kPX * 8;
+
+  // ---- initialisation: zero images (x' >= 61, pads), the constant ones plane [1, 1, 1, 0] of every slot, the zero
+  // cell of both record buffers, and the argmax lut: a -> the dd ^ 3 index field at the bit of its row dh (0: bit 0,
+  // 1: bit 16, 2: bit 2; "no argmax here" = 0 -> index 3 after the final NOT) and its column aw in bits 30-31
+  for (int e = tid; e < kMxImgBytes / 16; e += 512) reinterpret_cast<uint4*>(img)[e] = make_uint4(0, 0, 0, 0);
+  __syncthreads();
+  for (int e = tid; e < (kMxRing + 2) * 66; e += 512) {
+    const int s = e / 66, xp = e - 66 * s;
+    *reinterpret_cast<uint2*>(img + s * kMxSS8 + (kMxPO[20] + xp) * 8) = make_uint2(0x3f803f80u, 0x3f80u);
+  }
+  if (tid < 27) {
+    const int ad = tid / 9, ah = (tid / 3) % 3, aw = tid % 3;
+    lut[tid] = ((uint32_t)(ad ^ 3) << (ah == 0 ? 0 : ah == 1 ? 16 : 2)) | ((uint32_t)aw << 30);
+  }
+  if (tid >= 64 && tid < 64 + 2 * kC1) {
+    const int b = (tid - 64) / kC1, c = (tid - 64) % kC1;
+    *reinterpret_cast<uint2*>(recb + b * kMxRecBytes + (kPW * kC1 + c) * 8) = make_uint2(0, 0);
+  }
+
+  // ---- per-lane constants of the MFMA part (wave w = k-step: x = 8 w .. 8 w + 7)
+  int roff[4], awi[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int gi = (i & 1) + 2 * q + 4 * (i >> 1);  // A element 2i covers 4-group gi = 2q, 2q + 1, 4 + 2q, 5 + 2q
+    const int x = 8 * w + gi;
+    const int cell = x < 3 * kPW ? x / 3 : kPW;
+    roff[i] = (cell * kC1 + m) * 8;
+    awi[i] = x % 3;
+  }
+  int col8[4], jhT[4];
+#pragma unroll
+  for (int T = 0; T < 4; ++T) {
+    int k = kMxTap[32 * T + m];
+    if (k == 999) {  // the ones column: D = sum of dz (any slot, any x)
+      col8[T] = (kMxPO[20] + 8 * w + 4 * q) * 8;
+      jhT[T] = 0;
+      continue;
+    }
+    k = k >= 1000 ? k - 1000 : k;
+    const int kd = k / 25, kh = (k / 5) % 5, kw = k % 5;
+    const int p = 8 * (kd >> 1) + 4 * (kd & 1) + 2 * (kh & 1) + (kw & 1);
+    col8[T] = (kMxPO[p] + 8 * w + 4 * q + (kw >> 1)) * 8;
+    jhT[T] = kh >> 1;
+  }
+
+  // ---- staging roles.  The two waves of a SIMD (w, w + 4) run in opposite phases: waves 0-3 stage the NEXT pooled
+  // row after their MFMAs (loads issued at the start of the row), waves 4-7 before them (loaded one row earlier), so
+  // one wave's conversion VALU runs beside the other's matrix work.  Waves 0-2 / 4-6: y' row tasks (row, half) 0-2 /
+  // 3-5 of the 3 new rows; waves 3 / 7: record items {l, 128 + l, 256 + l} / {64 + l, 192 + l}.  At a new slab its
+  // rows 0, 1 (tasks 6-9) are written by waves 0-3 after the last barrier of the old slab.  Each role runs its own
+  // copy of the loop with unconditional (index-clamped) loads: loads under role branches made the compiler copy the
+  // loaded registers at the joins behind a vmcnt(0) wait, exposing the HBM latency before every row's MFMAs.
+  const int wu = __builtin_amdgcn_readfirstlane(w);
+  const int wl = wu & 3;
+
+  // prologue: stage 0 (its 5 rows and records) by every wave
+  __syncthreads();  // lut, zeros
+  {
+    const MxStage st = mx_stage(pd0, 0);
+    for (int t = wu; t < 10; t += 8) {
+      uint32_t v[5];
+      if ((t & 1) == 0) {
+        mx_load_row<0>(v, xs, st.pd, t >> 1, lane);
+        mx_store_row<0>(v, img, ((t >> 1) + st.ro) & 7, lane);
+      } else {
+        mx_load_row<1>(v, xs, st.pd, t >> 1, lane);
+        mx_store_row<1>(v, img, ((t >> 1) + st.ro) & 7, lane);
+      }
+    }
+    for (int it = tid; it < kMxRecItems; it += 512) {
+      MxRec r;
+      mx_load_rec(r, dp, pout, amax, n, st.pd, st.ph, it);
+      mx_store_rec(r, recb, lut, it);
+    }
+  }
+
+  f32x16 acc[2][4];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int T = 0; T < 4; ++T)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[t][T][e] = 0.f;
+
+  auto run = [&](auto early_c, auto meta_c) {
+    constexpr bool EARLY = decltype(early_c)::value, META = decltype(meta_c)::value;
+    constexpr int NREC = META ? (EARLY ? 2 : 3) : 0;
+    const int rec0 = EARLY ? 64 : 0;
+    const int bt = META ? 0 : (EARLY ? 3 : 0) + wl;  // y' row task: row bt >> 1 of the new rows, phase half bt & 1
+    const int bh = bt & 1;
+    // two register sets, alternating per pooled row, so a row's staging data is loaded two rows before it is stored
+    // (one row of MFMA work did not cover the HBM latency: the same kernel ran 3.60 vs 2.43 ms with the loads
+    // redirected to L2-resident rows).  The row loop is unrolled by 2 so the sets never need register copies.
+    struct Set {
+      uint32_t bv[5], xv[5];
+      MxRec rv[NREC > 0 ? NREC : 1];
+    };
+    Set sa, sb;
+    auto load_stage = [&](Set& X, int S) {  // S clamped to a valid stage: the loads never sit under a branch
+      S = min(S, nstage - 1);
+      const MxStage st = mx_stage(pd0, DBG ? 0 : S);  // DBG: diagnostic, every row re-reads stage 0 (L2 hits)
+      if constexpr (META) {
+#pragma unroll
+        for (int k = 0; k < NREC; ++k)
+          mx_load_rec(X.rv[k], dp, pout, amax, n, st.pd, st.ph, min(rec0 + 128 * k + lane, kMxRecItems - 1));
+      } else {
+        const uint8_t* src = xs + (((int64_t)(3 * st.pd) * kPY + 3 * st.ph + 2 + (bt >> 1)) * kPX +
+                                   min(lane, kPX - 1)) * 8 + 4 * bh;
+#pragma unroll
+        for (int z = 0; z < 5; ++z) X.bv[z] = *reinterpret_cast<const uint32_t*>(src + z * (int64_t)kPY * kPX * 8);
+      }
+      if constexpr (!EARLY) {  // rows 0, 1 of S's slab (used only when S starts a new slab)
+        const uint8_t* src = xs + (((int64_t)(3 * st.pd) * kPY + (wl >> 1)) * kPX + min(lane, kPX - 1)) * 8 + 4 * (wl & 1);
+#pragma unroll
+        for (int z = 0; z < 5; ++z) X.xv[z] = *reinterpret_cast<const uint32_t*>(src + z * (int64_t)kPY * kPX * 8);
+      }
+    };
+    auto store_stage = [&](const Set& X, int S) {
+      const MxStage st = mx_stage(pd0, S);
+      if constexpr (META) {
+#pragma unroll
+        for (int k = 0; k < NREC; ++k)
+          if (rec0 + 128 * k + lane < kMxRecItems)
+            mx_store_rec(X.rv[k], recb + (S & 1) * kMxRecBytes, lut, rec0 + 128 * k + lane);
+      } else {
+        const int sl = (3 * st.ph + 2 + (bt >> 1) + st.ro) & 7;
+        if (bh == 0) mx_store_row<0>(X.bv, img, sl, lane);
+        else mx_store_row<1>(X.bv, img, sl, lane);
+      }
+    };
+    // row s: early waves store row s + 1 from set X (loaded at row s - 2) and reload X with row s + 3; late waves load
+    // row s + 2 into X and store row s + 1 from Y (loaded at row s - 1) after their MFMAs
+    auto body = [&](int s, Set& X, Set& Y) {
+      const MxStage cur = mx_stage(pd0, s);
+      if constexpr (EARLY) {
+        if (s + 1 < nstage) store_stage(X, s + 1);
+        load_stage(X, s + 3);
+      } else {
+        load_stage(X, s + 2);
+      }
+      // ---- A of this pooled row (both M-tiles): values and the three index words
+      const uint8_t* rb = recb + (s & 1) * kMxRecBytes;
+      uint32_t av[2][4], om[2] = {0u, 0u};
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const uint64_t r = *((lds_u64*)(rb + roff[i] + 256 * t));
+          const uint32_t rx = (uint32_t)r, ry = (uint32_t)(r >> 32);
+          av[t][i] = rx;
+          om[t] |= ((ry >> 30) == (uint32_t)awi[i]) ? (ry << (4 * i)) : 0u;
+        }
+      bf16x8 A[2];
+      int W0[2], W2[2];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        A[t] = __builtin_bit_cast(bf16x8, make_uint4(av[t][0], av[t][1], av[t][2], av[t][3]));
+        W0[t] = (int)~om[t];
+        W2[t] = (int)(~om[t] >> 2);
+      }
+      // B base of each N-tile at dh = 0: ring slot of y' = 3 ph + jh; dh = 1, 2 are +1, +2 slots (immediate
+      // offsets; the mirrors 8, 9 of slots 0, 1 make that valid across the ring's end)
+      int bb[4];
+#pragma unroll
+      for (int T = 0; T < 4; ++T) bb[T] = ((3 * cur.ph + cur.ro + jhT[T]) & 7) * kMxSS8 + col8[T];
+#pragma unroll
+      for (int dh = 0; dh < 3; ++dh) {
+        bf16x16 B[4];
+#pragma unroll
+        for (int T = 0; T < 4; ++T) {
+          lds_u64* bp = (lds_u64*)(img + bb[T] + dh * kMxSS8);
+          typedef uint64_t u64x4 __attribute__((ext_vector_type(4)));
+          const u64x4 bq = {bp[0], bp[1], bp[2], bp[3]};
+          B[T] = __builtin_bit_cast(bf16x16, bq);
+        }
+#pragma unroll
+        for (int T = 0; T < 4; ++T)
+#pragma unroll
+          for (int t = 0; t < 2; ++t) {
+            if (dh == 0) acc[t][T] = __builtin_amdgcn_smfmac_f32_32x32x32_bf16(A[t], B[T], acc[t][T], W0[t], 0, 0);
+            else if (dh == 1) acc[t][T] = __builtin_amdgcn_smfmac_f32_32x32x32_bf16(A[t], B[T], acc[t][T], W0[t], 0, 1);
+            else acc[t][T] = __builtin_amdgcn_smfmac_f32_32x32x32_bf16(A[t], B[T], acc[t][T], W2[t], 0, 0);
+          }
+      }
+      if constexpr (!EARLY)
+        if (s + 1 < nstage) store_stage(Y, s + 1);
+      __syncthreads();
+      if (s + 1 < nstage) {
+        const MxStage nx = mx_stage(pd0, s + 1);
+        if (nx.ph == 0) {  // rows 0, 1 of the new slab take the slots rows 69, 70 of the old one just released
+          if constexpr (!EARLY) {
+            const int sl = ((wl >> 1) + nx.ro) & 7;
+            if ((wl & 1) == 0) mx_store_row<0>(Y.xv, img, sl, lane);
+            else mx_store_row<1>(Y.xv, img, sl, lane);
+          }
+          __syncthreads();
+        }
+      }
+    };
+    if constexpr (EARLY) {
+      load_stage(sa, 1);
+      load_stage(sb, 2);
+    } else {
+      load_stage(sb, 1);
+    }
+    __syncthreads();
+    int s = 0;
+    for (; s + 1 < nstage; s += 2) {
+      body(s, sa, sb);
+      body(s + 1, sb, sa);
+    }
+    if (s < nstage) body(s, sa, sb);
+  };
+  using T1 = std::integral_constant<bool, true>;
+  using F1 = std::integral_constant<bool, false>;
+  if (wu >= 4) {
+    if (wl == 3) run(T1{}, T1{});
+    else run(T1{}, F1{});
+  } else {
+    if (wl == 3) run(F1{}, T1{});
+    else run(F1{}, F1{});
+  }
+
+  // ---- fixed-order reduction over the 8 waves (one M-tile at a time through the whole LDS); column 999 = D
+  float* red = reinterpret_cast<float*>(smem);
+  float* op = part + (int64_t)bid * kC1 * 126;
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    __syncthreads();
+#pragma unroll
+    for (int T = 0; T < 4; ++T)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int mm = 8 * (e >> 2) + 4 * q + (e & 3);
+        red[(w * 32 + mm) * 128 + 32 * T + m] = acc[t][T][e];
+      }
+    __syncthreads();
+    for (int e = tid; e < 32 * 128; e += 512) {
+      const int mm = e >> 7, col = e & 127;
+      int k = kMxTap[col];
+      if (k >= 1000) continue;
+      float v = 0.f;
+#pragma unroll
+      for (int ww = 0; ww < 8; ++ww) v += red[(ww * 32 + mm) * 128 + col];
+      op[(32 * t + mm) * 126 + (k == 999 ? 125 : k)] = v;
+    }
+  }
+}
+
+// pd slabs per block: the whole sample when there are >= 4 samples per CU (one reduction per sample), else fewer so
+// the grid still covers the chip ~4 times
+int conv1_wgrad_mx_npb(int NB) { return std::max(1, std::min(kPD, NB * kPD / (4 * 256))); }
+
+// conv1 weight-gradient kernel: 0 = VALU gather (k_conv1_wgrad_split), 1 = 2:4 smfmac (k_conv1_wgrad_smf),
+// 2 = 2:4 smfmac with the argmax row in the index (k_conv1_wgrad_mx); -1 = the environment default
 static int g_c1wg_mode = -1;
 void conv1_wgrad_mode(int mode) { g_c1wg_mode = mode; }
 
@@ -1501,8 +1886,31 @@ void conv1_wgrad(uintptr_t x8, uintptr_t idx, uintptr_t dp, uintptr_t pout, uint
     const char* e = getenv("NIDT_C1WG_SMF");
     return e ? atoi(e) : 0;
   }();
-  const bool smf = g_c1wg_mode >= 0 ? g_c1wg_mode == 1 : smf_env == 1;
-  if (smf)
+  // NIDT_C1WG_MX=0 falls back from the argmax-row smfmac kernel (default) to the VALU gather
+  static const int mx_env = [] {
+    const char* e = getenv("NIDT_C1WG_MX");
+    return e ? atoi(e) : 1;
+  }();
+  const int mode = g_c1wg_mode >= 0 ? g_c1wg_mode : (smf_env == 1 ? 1 : mx_env == 1 ? 2 : 0);
+  const bool smf = mode == 1;
+  int nslab = B * kPD * nq;  // part slabs per client
+  if (mode == 2) {
+    const int npb = conv1_wgrad_mx_npb(NB), nblk = (kPD + npb - 1) / npb;
+    NIDT_REQUIRE(nblk <= kPD * nq, "conv1_wgrad: part buffer");
+    static const int dbg = [] {
+      const char* e = getenv("NIDT_C1WG_DBG");
+      return e ? atoi(e) : 0;
+    }();
+    if (dbg)
+      hipLaunchKernelGGL(k_conv1_wgrad_mx<1>, dim3(NB * nblk), dim3(512), 0, s, ptr<const uint8_t>(x8),
+                         ptr<const int>(idx), ptr<const uint16_t>(dp), ptr<const uint16_t>(pout),
+                         ptr<const uint8_t>(amax), ptr<float>(part), npb, nblk);
+    else
+      hipLaunchKernelGGL(k_conv1_wgrad_mx<0>, dim3(NB * nblk), dim3(512), 0, s, ptr<const uint8_t>(x8),
+                         ptr<const int>(idx), ptr<const uint16_t>(dp), ptr<const uint16_t>(pout),
+                         ptr<const uint8_t>(amax), ptr<float>(part), npb, nblk);
+    nslab = B * nblk;
+  } else if (smf)
     hipLaunchKernelGGL(k_conv1_wgrad_smf, dim3(kPD * NB * nq), dim3(512), 0, s, ptr<const uint8_t>(x8),
                        ptr<const int>(idx), ptr<const uint16_t>(dp), ptr<const uint16_t>(pout),
                        ptr<const uint8_t>(amax), ptr<float>(part), nq);
@@ -1514,8 +1922,8 @@ void conv1_wgrad(uintptr_t x8, uintptr_t idx, uintptr_t dp, uintptr_t pout, uint
 #undef NIDT_C1WG
   NIDT_CHECK(hipGetLastError());
   const int G = NB / B;
-  // client g's slabs are contiguous: B samples x 19 pd x nq row ranges
-  hipLaunchKernelGGL(k_conv1_wgrad_fin, dim3(kC1, G), dim3(64 * kFinW), 0, s, ptr<const float>(part), B * nq,
+  // client g's slabs are contiguous: B samples x (19 pd x nq row ranges | nblk pd ranges)
+  hipLaunchKernelGGL(k_conv1_wgrad_fin, dim3(kC1, G), dim3(64 * kFinW), 0, s, ptr<const float>(part), nslab,
                      ptr<const float>(w125), ptr<const float>(mu), ptr<const float>(covw), ptr<const float>(invstd),
                      ptr<const float>(theta), ldt, off_g, ptr<float>(grad), ldg, goff_w, goff_bias, goff_g, goff_b,
                      wscale, ptr<const float>(emean));

@@ -26,7 +26,7 @@ import numpy as np
 import torch
 
 from ..core import partition as P
-from .volumes import ABCD_SHAPE, VolumeStore, make_synthetic_abcd
+from .volumes import ABCD_SHAPE, VolumeStore, make_synthetic_abcd, quantize_cohort_volumes
 
 log = logging.getLogger(__name__)
 
@@ -116,18 +116,26 @@ def load_partition_data_abcd_synthetic(client_number=64, partition_method="dir",
 
 
 def _read_h5(path):
+    """``X`` (as uint8, quantised chunk-wise from the stored dtype: :func:`quantize_cohort_volumes`), ``y``, ``site``."""
     import h5py  # optional dependency
     with h5py.File(path, "r") as f:
         y = f["y"][()]
         site = f["site"][()]
-        X = f["X"][()] if "X" in f else None
+        X = quantize_cohort_volumes(f["X"]) if "X" in f else None
     return X, y, site
+
+
+def _cohort_store(X, y, site, device):
+    X = quantize_cohort_volumes(X)  # no-op copy for uint8; refuses non-/255 floats instead of truncating them
+    return VolumeStore(torch.from_numpy(X).to(device),
+                       torch.from_numpy(np.asarray(y, np.float32)).to(device),
+                       torch.from_numpy(np.asarray(site, np.float32)).to(device))
 
 
 def load_partition_data_abcd(data_dir, partition_method="site", partition_alpha=0.3, client_number=21,
                              batch_size=16, logger=None, max_clients=21, device="cpu", shape=ABCD_SHAPE):
-    """Reference entry point.  ``data_dir`` may be an HDF5 file (keys ``X`` uint8 volumes, ``y``,
-    ``site``) or a directory containing ``alldatain8bitsnormalized.h5``.  Falls back to a synthetic
+    """Reference entry point.  ``data_dir`` may be an HDF5 file (keys ``X`` volumes — uint8, or the reference's
+    float k/255 maps, quantised exactly — ``y``, ``site``) or a directory containing ``alldatain8bitsnormalized.h5``.  Falls back to a synthetic
     cohort (and says so) when ``h5py`` or the file is unavailable."""
     path = data_dir
     if path and os.path.isdir(path):
@@ -149,9 +157,7 @@ def load_partition_data_abcd(data_dir, partition_method="site", partition_alpha=
                                                   logger=logger)
     if X is None:
         raise ValueError("HDF5 file has no 'X' volumes")
-    store = VolumeStore(torch.from_numpy(np.ascontiguousarray(X)).to(torch.uint8).to(device),
-                        torch.from_numpy(np.asarray(y, np.float32)).to(device),
-                        torch.from_numpy(np.asarray(site, np.float32)).to(device))
+    store = _cohort_store(X, y, site, device)
     train, test, _ = P.partition_by_site(np.asarray(site), max_clients=max_clients)
     return _assemble(store, train, test, batch_size, 2, logger)
 
@@ -187,6 +193,4 @@ def _load_store(data_dir, device="cpu", logger=None):
     except Exception as e:  # noqa: BLE001
         (logger or log).warning("ABCD cohort unavailable (%s); using a synthetic ABCD-shape cohort", e)
         return make_synthetic_abcd(21 * 40, seed=0, device=device)
-    return VolumeStore(torch.from_numpy(np.ascontiguousarray(X)).to(torch.uint8).to(device),
-                       torch.from_numpy(np.asarray(y, np.float32)).to(device),
-                       torch.from_numpy(np.asarray(site, np.float32)).to(device))
+    return _cohort_store(X, y, site, device)

@@ -24,6 +24,7 @@ import sys
 
 import numpy as np
 import torch
+from .volumes import quantize_cohort_volumes
 
 MAGIC = b"NIDTVOL1"
 HEADER = 128
@@ -55,8 +56,8 @@ def write_volume_file(path, volumes, labels, sites=None, chunk=64):
         for s in range(0, n, chunk):
             v = volumes[s:s + chunk]
             v = v.cpu().numpy() if torch.is_tensor(v) else np.asarray(v)
-            if v.dtype != np.uint8:
-                raise TypeError("volumes must be uint8 (quantise like the reference's preprocessing first)")
+            if v.dtype != np.uint8:  # the reference's float k/255 maps quantise exactly; anything else raises
+                v = quantize_cohort_volumes(v)
             f.write(np.ascontiguousarray(v).tobytes())
         f.write(lab.tobytes())
         f.write(sit.tobytes())

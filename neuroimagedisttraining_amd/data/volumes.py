@@ -56,6 +56,45 @@ class VolumeStore:
         return x, y
 
 
+def quantize_cohort_volumes(X, chunk=64, atol=1e-3):
+    """Cohort volumes ``X`` ([N, D, H, W], numpy array / tensor / h5py dataset) -> uint8 numpy array, without ever
+    silently zeroing the data.
+
+    * uint8 is taken as is; other integer dtypes must lie in [0, 255];
+    * float volumes are accepted only in the reference's stored form, the 8-bit quantised maps divided by 255
+      (``Preprocess_ABCD.ipynb``: ``eight_bit_data = (...).astype(np.uint8) / 255.0``, read back as float32 by
+      ``sailentgrads/my_model_trainer.py:194-197``): ``round(X * 255)`` is kept when every ``|X*255 - round(X*255)|``
+      is below ``atol`` and the result lies in [0, 255];
+    * anything else raises ``ValueError`` naming the dtype and range.
+    Processed ``chunk`` subjects at a time, so an HDF5 dataset is never materialised as floats."""
+    n = int(X.shape[0])
+    out = np.empty(tuple(int(s) for s in X.shape), dtype=np.uint8)
+    for s in range(0, n, chunk):
+        v = X[s:s + chunk]
+        v = v.cpu().numpy() if torch.is_tensor(v) else np.asarray(v)
+        if v.dtype == np.uint8:
+            out[s:s + len(v)] = v
+            continue
+        if np.issubdtype(v.dtype, np.integer) or v.dtype == np.bool_:
+            lo, hi = int(v.min()), int(v.max())
+            if lo < 0 or hi > 255:
+                raise ValueError("cohort X (dtype %s) has integer values in [%d, %d], outside uint8" % (v.dtype, lo, hi))
+            out[s:s + len(v)] = v.astype(np.uint8)
+            continue
+        if not np.issubdtype(v.dtype, np.floating):
+            raise ValueError("cohort X has unsupported dtype %s" % v.dtype)
+        x = v.astype(np.float64) * 255.0
+        q = np.rint(x)
+        err = float(np.abs(x - q).max()) if x.size else 0.0
+        lo, hi = float(v.min()), float(v.max())
+        if not np.isfinite(err) or err >= atol or q.min() < 0 or q.max() > 255:
+            raise ValueError("cohort X (dtype %s, range [%g, %g]) is not 8-bit data stored as k/255 (max |X*255 - "
+                             "round(X*255)| = %g): quantise it like Preprocess_ABCD.ipynb before loading"
+                             % (v.dtype, lo, hi, err))
+        out[s:s + len(v)] = q.astype(np.uint8)
+    return out
+
+
 def _smooth_field(gen, n, coarse, shape, device):
     """Low-frequency random field: coarse normal noise trilinearly upsampled to ``shape``."""
     z = torch.randn((n, 1) + tuple(coarse), generator=gen, device=device)

@@ -606,10 +606,13 @@ def test_conv1_fused_fwd_and_sparse_wgrad(signed):
         assert e_w < 2e-2 and e_g < 2e-2 and e_b < 2e-2, (e_w, e_g, e_b)
 
 
-@pytest.mark.parametrize("NB,B", [(4, 2), (256, 16)])  # nq = 2 row ranges per slab (few samples) and nq = 1
-def test_conv1_wgrad_smfmac_matches_valu_gather(NB, B):
-    """The 2:4-sparse matrix-core conv1 weight gradient (k_conv1_wgrad_smf) writes the same S / D slabs as the VALU
-    gather (k_conv1_wgrad_split) on random inputs: every argmax offset, ReLU-dead cells, signed bf16 gradients."""
+@pytest.mark.parametrize("mode", [1, 2])
+@pytest.mark.parametrize("NB,B", [(4, 2), (256, 16)])  # few samples (row / slab splits) and many
+def test_conv1_wgrad_smfmac_matches_valu_gather(NB, B, mode):
+    """The 2:4-sparse matrix-core conv1 weight gradients — k_conv1_wgrad_smf (mode 1, x-ordered K) and k_conv1_wgrad_mx
+    (mode 2, the default: argmax row in the sparsity index, blocks over pd-slab ranges) — give the same per-client S / D
+    sums and gradients as the VALU gather (k_conv1_wgrad_split) on random inputs: every argmax offset, ReLU-dead cells,
+    signed bf16 gradients."""
     m = _m()
     g = torch.Generator(device=DEV).manual_seed(3)
     x8 = torch.randint(0, 256, (NB, 61, 73, 61, 8), dtype=torch.uint8, device=DEV, generator=g)
@@ -620,9 +623,11 @@ def test_conv1_wgrad_smfmac_matches_valu_gather(NB, B):
     amax = torch.randint(0, 27, shp, dtype=torch.uint8, device=DEV, generator=g)
     G = NB // B
     nq = m.conv1_wgrad_nq(NB)
+    npb = m.conv1_wgrad_mx_npb(NB)
+    nblk = (19 + npb - 1) // npb
     parts, grads = [], []
     P = 8000 + 64 * 4
-    for mode in (0, 1):
+    for mode in (0, mode):
         part = torch.full((NB * 19 * nq, 64, 126), float("nan"), device=DEV)
         grad = torch.zeros(G, P, device=DEV)
         theta = torch.ones(G, P, device=DEV)
@@ -635,11 +640,13 @@ def test_conv1_wgrad_smfmac_matches_valu_gather(NB, B):
                       part.data_ptr(), w125.data_ptr(), mu.data_ptr(), covw.data_ptr(), inv.data_ptr(), theta.data_ptr(),
                       P, 8000, grad.data_ptr(), P, 0, 8000 + 64, 8000 + 128, 8000 + 192, 1.0 / 255.0, 0, _st())
         torch.cuda.synchronize()
-        parts.append(part)
+        nsl = B * 19 * nq if mode != 2 else B * nblk  # slabs per client
+        part = part[:G * nsl]
+        assert torch.isfinite(part).all()
+        parts.append(part.view(G, nsl, 64, 126).double().sum(1))
         grads.append(grad)
     m.conv1_wgrad_mode(-1)
-    assert torch.isfinite(parts[1]).all()
-    # the slabs: fp32 sums of bf16 x uint8 products in two different orders
+    # per-client slab sums: fp32 sums of bf16 x uint8 products in two different orders
     assert _relerr(parts[1], parts[0]) < 1e-5, _relerr(parts[1], parts[0])
     assert float((parts[1] - parts[0]).abs().max()) <= 1e-4 * float(parts[0].abs().max())
     assert _relerr(grads[1], grads[0]) < 1e-5
