@@ -552,7 +552,7 @@ class DisPFLRunner(PersonalizedRunner):
         self.stat_info["mask_dis_matrix"] = mat.cpu().tolist()
         if self.cfg.save_masks:
             self.stat_info["final_masks"] = MK.unpack_bits(all_bits, self.P).bool().cpu()
-        return None
+        return super().finish()  # folds the device-side counters (sum_comm_params) into stat_info
 
 
 # ================================================================================================== SubAvg

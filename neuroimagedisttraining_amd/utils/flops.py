@@ -1,6 +1,6 @@
 """Analytic FLOP counting (reference ``fedml_api/utils/main_flops_counter.py:30-163``).
 
-Forward hooks count multiply-adds of Conv1d/2d/3d and Linear layers (sparse-aware: only non-zero weights unless
+Forward hooks count the FLOPs (2 per multiply-add) of Conv1d/2d/3d and Linear layers (sparse-aware: only non-zero weights unless
 ``full=True``); training = 3x inference (the reference's rule).  Unlike the reference (quirk Q15) Conv3d is
 counted and each dataset uses its true input shape (ABCD: 1x121x145x121 rather than 1x32x32).
 """
@@ -14,19 +14,21 @@ INPUT_SHAPES = {"emnist": (1, 28, 28), "mnist": (1, 28, 28), "cifar10": (3, 32, 
 
 
 def count_model_param_flops(model, dataset="ABCD", full=False, input_shape=None):
+    """The reference counter with ``multiply_adds=True`` (its default, ``main_flops_counter.py:38``): a conv adds
+    ``(2 * nnz(weight) + bias * Cout) * H_out * W_out`` (``:58-66``), a linear layer
+    ``batch * (2 * nnz(weight) + nnz(bias))`` (``:71-80``; ``full`` counts every element instead of the non-zeros)."""
     counts = []
 
     def conv_hook(m, inp, out):
-        k = m.weight.numel() // m.out_channels if full else int(torch.count_nonzero(m.weight)) / m.out_channels
-        k = k  # weights per output channel (incl. groups)
+        nnz = m.weight.numel() if full else int(torch.count_nonzero(m.weight))
         bias = 1 if m.bias is not None else 0
-        counts.append((k + bias) * out.numel())
+        counts.append((2.0 * nnz / m.out_channels + bias) * out.numel())
 
     def linear_hook(m, inp, out):
         w = m.weight.numel() if full else int(torch.count_nonzero(m.weight))
-        bias = m.bias.numel() if m.bias is not None else 0
+        bias = 0 if m.bias is None else (m.bias.numel() if full else int(torch.count_nonzero(m.bias)))
         batch = out.numel() // m.out_features
-        counts.append((w + bias) * batch)
+        counts.append((2 * w + bias) * batch)
 
     handles = []
     for m in model.modules():

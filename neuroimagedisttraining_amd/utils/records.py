@@ -9,8 +9,8 @@ small array, large arrays (final masks, mask-distance matrices of big federation
 ``record_avg_inference_flops`` (``subavg_api.py:223-235``, ``ditto/ditto_api.py:78,153``) averages the sparse-aware
 inference FLOPs of every client's model (``w_global`` under the client's personal mask for SubAvg, ``w_global``
 alone for Ditto).  The counter's per-layer cost is affine in the layer's non-zero weight count
-(``(nnz + bias * C_out) * spatial`` for a conv, ``(nnz + bias) * batch`` for a linear layer,
-``utils/flops.py``), so the coefficients are measured with ONE forward of the template model and each client's
+(``(2 nnz + bias * C_out) * spatial`` for a conv, ``(2 nnz(weight) + nnz(bias)) * batch`` for a linear layer: the
+reference's ``multiply_adds=True``, ``main_flops_counter.py:58-80``; ``utils/flops.py``), so the coefficients are measured with ONE forward of the template model and each client's
 count is a dot product with its per-layer non-zero counts — no per-client forward pass.
 """
 from __future__ import annotations
@@ -85,20 +85,23 @@ def load_information(path):
 
 
 def flop_coefficients(model, dataset="ABCD", input_shape=None):
-    """{weight parameter name: (a, b)} such that the counter's FLOPs of that layer = a * nnz(weight) + b.
-    One forward of ``model`` on a ``(1,) + input`` tensor (the counter's batch of one)."""
+    """{parameter name: (a, b)} such that the counter's FLOPs = sum over names of a * nnz(parameter) + b
+    (:func:`..utils.flops.count_model_param_flops`: conv weight ``(2 * spatial, bias * Cout * spatial)``, linear weight
+    ``(2 * batch, 0)`` and its bias, counted by its non-zeros like the reference, ``(batch, 0)``).  One forward of
+    ``model`` on a ``(1,) + input`` tensor (the counter's batch of one)."""
     coef = {}
     names = {m: n for n, m in model.named_modules()}
 
     def conv_hook(m, inp, out):
         spatial = out.numel() // m.out_channels
         bias = m.out_channels if m.bias is not None else 0
-        coef[names[m] + ".weight"] = (float(spatial), float(bias * spatial))
+        coef[names[m] + ".weight"] = (2.0 * spatial, float(bias * spatial))
 
     def linear_hook(m, inp, out):
         batch = out.numel() // m.out_features
-        bias = m.bias.numel() if m.bias is not None else 0
-        coef[names[m] + ".weight"] = (float(batch), float(bias * batch))
+        coef[names[m] + ".weight"] = (2.0 * batch, 0.0)
+        if m.bias is not None:
+            coef[names[m] + ".bias"] = (float(batch), 0.0)
 
     hs = []
     for m in model.modules():

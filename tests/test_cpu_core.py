@@ -370,3 +370,40 @@ def test_heartbeat_failure_detector_reports_silent_rank():
     finally:
         for m in mons:
             m.stop()
+
+
+def test_flops_match_reference_multiply_adds_by_hand():
+    """The reference counter with its default ``multiply_adds=True`` (``main_flops_counter.py:58-80``): a conv is
+    ``(2 * nnz(W) + Cout) * H_out * W_out`` with a bias, a linear layer ``2 * nnz(W) + nnz(b)`` at batch 1; computed
+    here by hand for a small CIFAR-shape net with some zeroed weights and bias entries."""
+    import torch.nn as nn
+    from neuroimagedisttraining_amd.utils.flops import count_inference_flops
+    from neuroimagedisttraining_amd.utils.records import flop_coefficients
+
+    class Net(nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.conv = nn.Conv2d(3, 4, 3, padding=1)             # 32x32 out
+            self.conv2 = nn.Conv2d(4, 2, 3, stride=2, bias=False)  # 15x15 out
+            self.fc = nn.Linear(2 * 15 * 15, 10)
+
+        def forward(self, x):
+            return self.fc(torch.flatten(self.conv2(self.conv(x)), 1))
+
+    torch.manual_seed(0)
+    m = Net()
+    with torch.no_grad():
+        m.conv.weight[0].zero_()     # 27 zeros
+        m.fc.weight[:, :7].zero_()   # 70 zeros
+        m.fc.bias[:3].zero_()        # 3 zero biases
+    nnz_c1 = 4 * 27 - 27
+    nnz_c2 = 2 * 36
+    nnz_fc = 10 * 450 - 70
+    want = (2 * nnz_c1 + 4) * 32 * 32 + (2 * nnz_c2) * 15 * 15 + (2 * nnz_fc + 7)
+    assert count_inference_flops(m, input_shape=(3, 32, 32)) == want
+    full = (2 * 108 + 4) * 32 * 32 + (2 * 72) * 15 * 15 + (2 * 4500 + 10)
+    assert count_inference_flops(m, input_shape=(3, 32, 32), full=True) == full
+    coef = flop_coefficients(m, input_shape=(3, 32, 32))
+    sd = dict(m.named_parameters())
+    got = sum(a * int(torch.count_nonzero(sd[n])) + b for n, (a, b) in coef.items())
+    assert got == want

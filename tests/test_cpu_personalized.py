@@ -151,6 +151,7 @@ def _collect(r):
     bits = {c: r.mbits[r.row_of[c]].clone() for c in r.local} if getattr(r, "mbits", None) is not None else {}
     pers = {c: r.pers.theta[r.row_of[c], :r.P].clone() for c in r.local} if hasattr(r, "pers") else {}
     return {"rows": rows, "bits": bits, "pers": pers, "w": r.w_global.clone(),
+            "comm": int(r.stat_info.get("sum_comm_params", 0)),
             "stats": {k: v for k, v in r.stat_info.items() if isinstance(v, list) and v and
                       isinstance(v[0], float) and "time" not in k}}
 
@@ -216,7 +217,7 @@ def _spawn(world, out, algo, kw, ckpt=None):
         for key in ("rows", "bits", "pers"):
             got[key].update(d[key])
         if rk == 0:
-            got["w"], got["stats"] = d["w"], d["stats"]
+            got["w"], got["stats"], got["comm"] = d["w"], d["stats"], d["comm"]
     return got
 
 
@@ -228,6 +229,8 @@ def _same(got, ref, n, algo, atol=1e-5):
         if ref["pers"]:
             assert torch.allclose(got["pers"][c], ref["pers"][c], atol=atol), (algo, c)
     assert torch.allclose(got["w"], ref["w"], atol=atol)
+    if algo == "dispfl":  # finish() folds the device-side communication counter (summed over ranks)
+        assert ref["comm"] > 0 and got.get("comm", ref["comm"]) == ref["comm"], (got.get("comm"), ref["comm"])
     for k, v in ref["stats"].items():
         assert np.allclose(got["stats"][k], v, atol=1e-6), (algo, k)
 
@@ -395,7 +398,7 @@ def test_rebalancing_moves_samples_with_clients_on_sharded_stores(algo, world, k
         for key in ("rows", "bits", "pers"):
             got[key].update(d[key])
         if rk == 0:
-            got["w"], got["stats"] = d["w"], d["stats"]
+            got["w"], got["stats"], got["comm"] = d["w"], d["stats"], d["comm"]
         total += d["held"][1]
     n_all = sum(s + 4 + 3 for s in kw["sizes"])  # train + test + val rows of every client (_runner: val = 3)
     assert total == n_all  # the stores partition the cohort after migration

@@ -6,6 +6,7 @@ engine's global loss / accuracy trajectories must track it (round by round befor
 after it).  6 clients, SalientGrads (SNIP mask + masked FedAvg), 20 rounds, every
 round evaluated.  The fp32 side is the recorded trajectory of the fp32 engine on this cohort; the extended tier
 (``NIDT_EXTENDED_GPU_TESTS=1``) recomputes it and checks the record is current."""
+import hashlib
 import json
 import os
 
@@ -57,14 +58,40 @@ def _reference():
     return np.array(d["acc"]), np.array(d["loss"])
 
 
+def _fingerprint(vol, labels, splits):
+    """Hash of the cohort the recorded fp32 trajectory belongs to: labels, client splits, per-subject voxel sums and a
+    strided voxel sample.  A change of build_fl_volumes / the synthetic RNG shows up here instead of silently
+    comparing the bf16 run against a stale trajectory."""
+    h = hashlib.sha256()
+    h.update(labels.detach().float().cpu().numpy().tobytes())
+    for sp in splits:
+        for part in (getattr(sp, "train", None), getattr(sp, "test", None)):
+            h.update(np.asarray(part if part is not None else sp, dtype=np.int64).tobytes())
+    h.update(vol.reshape(vol.shape[0], -1).to(torch.int64).sum(1).cpu().numpy().tobytes())
+    h.update(vol.reshape(-1)[::9973].cpu().numpy().tobytes())
+    return h.hexdigest()[:16]
+
+
+def _check_fingerprint(vol, labels, splits):
+    with open(REF) as f:
+        want = json.load(f).get("fingerprint")
+    got = _fingerprint(vol, labels, splits)
+    print("cohort fingerprint", got, flush=True)
+    assert want is not None, "record the cohort fingerprint %s in %s" % (got, REF)
+    assert got == want, "cohort changed (%s != recorded %s): re-record the fp32 trajectory (extended tier)" % (got, want)
+
+
 def test_hip_bf16_tracks_fp32_over_twenty_rounds():
     """HIP bf16 trajectory against the fp32 engine's trajectory on the same cohort.  The fp32 run (~4-5 minutes of
     MIOpen fp32 at full resolution) is the recorded one (``tests/data/convergence_fp32_reference.json``); the
     extended tier recomputes it live (:func:`test_fp32_reference_trajectory_is_current` and
     ``NIDT_CONVERGENCE_LIVE=1`` here)."""
     vol, labels, splits = _cohort()
+    live = os.environ.get("NIDT_CONVERGENCE_LIVE", "0") == "1"
+    if not live:
+        _check_fingerprint(vol, labels, splits)
     acc_h, loss_h = _trajectory("hip", vol, labels, splits)
-    if os.environ.get("NIDT_CONVERGENCE_LIVE", "0") == "1":
+    if live:
         acc_t, loss_t = _trajectory("torch", vol, labels, splits)
     else:
         acc_t, loss_t = _reference()
@@ -92,6 +119,7 @@ def test_fp32_reference_trajectory_is_current():
     """The recorded fp32 trajectory is what the fp32 engine produces today: rounds 0-9 (before the chaotic
     transition) within the run-to-run spread of fp32 itself (1.7 % under 1e-6 weight noise, r3 ablation)."""
     vol, labels, splits = _cohort()
+    _check_fingerprint(vol, labels, splits)
     acc_t, loss_t = _trajectory("torch", vol, labels, splits)
     acc_r, loss_r = _reference()
     assert np.max(np.abs(loss_t[:10] - loss_r[:10]) / loss_r[:10]) <= 0.02

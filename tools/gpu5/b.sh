@@ -3,7 +3,7 @@
 set -o pipefail
 export PYTHONUNBUFFERED=1 KBENCH_EVAL=0
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-OUT=gpurun_out/r5d; mkdir -p $OUT
+OUT=gpurun_out/r5i; mkdir -p $OUT
 RE='k_conv1_wgrad_mx'
 i=0
 for C in "SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE" \
