@@ -534,9 +534,9 @@ class DisPFLRunner(PersonalizedRunner):
             flat = rt.all_gather_sized(mine, sizes, self.info).view(-1, self.W)
             # each rank's rows are in its row order (size-sorted, ties by id: the rule of FLRunner.__init__/migrate)
             order = [c for sh in self.shards for c in sorted(sh, key=lambda c: (-int(self.sizes[c]), c))]
-            out[torch.tensor(order, device=self.device)] = flat
+            out[self._to_dev(order)] = flat
         elif self.C:
-            out[torch.tensor(self.local, device=self.device)] = mine.view(self.C, self.W)
+            out[self._to_dev(self.local)] = mine.view(self.C, self.W)
         return out
 
     def finish(self):
@@ -571,7 +571,7 @@ class SubAvgRunner(PersonalizedRunner):
         return super().finish()
 
     def _real_prune_rows(self, rs, rows, bits_rows):
-        ix = torch.tensor(rows, device=self.device)
+        ix = self._to_dev(rows)
         rs.theta[ix, :self.P] = rs.theta[ix, :self.P] * MK.unpack_bits(bits_rows, self.P)
 
     def run_round(self, round_idx, sync_timers=False):
@@ -583,7 +583,7 @@ class SubAvgRunner(PersonalizedRunner):
         rows, loc = self._local_rows(sampled)
         hooks = {}
         if rows:
-            ix = torch.tensor(rows, device=self.device)
+            ix = self._to_dev(rows)
             old_bits = self.mbits[ix].clone()
             self.theta[ix] = self.w_global.unsqueeze(0).expand(len(rows), -1)
             self.bufs[ix] = self.b_global.unsqueeze(0).expand(len(rows), -1)

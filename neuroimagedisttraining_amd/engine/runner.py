@@ -36,6 +36,8 @@ import os
 import time
 from dataclasses import dataclass, replace
 
+from collections.abc import Mapping
+
 import numpy as np
 import torch
 import torch.nn.functional as F
@@ -78,6 +80,72 @@ class RowSet:
 
     def rows(self, lo, hi):
         return RowSet(self.theta[lo:hi], self.bufs[lo:hi])
+
+
+class StatInfo(dict):
+    """``stat_info`` whose evaluation lists may trail the device by a round: reads first fold in the evaluations
+    still in flight (:meth:`FLRunner._flush_metrics`), so every consumer sees the complete, ordered lists while a timed
+    GPU loop never waits for a metric."""
+
+    DEFERRED = ("global_test_acc", "global_test_loss", "person_test_acc", "person_test_loss")
+
+    def __init__(self, flush, *a, **kw):
+        super().__init__(*a, **kw)
+        self._flush = flush
+
+    def __getitem__(self, k):
+        if k in self.DEFERRED:  # other keys (round_time, counters) never wait for the device
+            self._flush()
+        return super().__getitem__(k)
+
+    def get(self, k, default=None):
+        if k in self.DEFERRED:
+            self._flush()
+        return super().get(k, default)
+
+    def items(self):
+        self._flush()
+        return super().items()
+
+    def values(self):
+        self._flush()
+        return super().values()
+
+    def __iter__(self):
+        self._flush()
+        return super().__iter__()
+
+    def copy(self):
+        self._flush()
+        return dict(super().items())
+
+    def __reduce__(self):
+        self._flush()
+        return (dict, (dict(super().items()),))
+
+
+class LazyMetrics(Mapping):
+    """A round's evaluation result that is read from the device only when looked at."""
+
+    def __init__(self, runner, holder):
+        self._runner, self._holder = runner, holder
+
+    def _d(self):
+        if "res" not in self._holder:
+            self._runner._flush_metrics()
+        return self._holder["res"]
+
+    def __getitem__(self, k):
+        return self._d()[k]
+
+    def __iter__(self):
+        return iter(self._d())
+
+    def __len__(self):
+        return len(self._d())
+
+    def __repr__(self):
+        return repr(self._d())
 
 
 def _nullctx():
@@ -128,8 +196,10 @@ class FLRunner:
         self.mask_bits = None         # the same as one shared bit row [1, W]
         self.maskable = maskable_flat_mask(engine.players, snip_maskable_names(template_model)).to(self.device)
         self.template = template_model   # layer structure for FLOP accounting (its weights are not used)
-        self.stat_info = dict(sum_comm_params=0, sum_training_flops=0, global_test_acc=[], person_test_acc=[],
-                              global_test_loss=[], person_test_loss=[], round_time=[])
+        self._pending_metrics = []     # deferred evaluations: (round, pinned host rows, event, result holder)
+        self._pinned_free = []
+        self.stat_info = StatInfo(self._flush_metrics, sum_comm_params=0, sum_training_flops=0, global_test_acc=[],
+                                  person_test_acc=[], global_test_loss=[], person_test_loss=[], round_time=[])
         self.timers = {"train": 0.0, "aggregate": 0.0, "eval": 0.0, "snip": 0.0}
         self._graphs = {}             # step key -> captured local step (None until the shape repeats, False = eager)
         self.graph_stats = {}         # counts of first-seen (eager) / captured / replayed steps
@@ -162,6 +232,15 @@ class FLRunner:
     def _upload_i32(self, arr):
         """int32 host array -> device tensor through pinned memory, without blocking the host."""
         t = torch.from_numpy(np.ascontiguousarray(arr, dtype=np.int32))
+        if self.device.type != "cuda":
+            return t
+        return t.pin_memory().to(self.device, non_blocking=True)
+
+    def _to_dev(self, arr, dtype=torch.int64):
+        """Small host list / array -> device tensor through pinned memory, without blocking the host.  (A plain
+        ``torch.tensor(..., device=cuda)`` copies from pageable memory and synchronises the stream: the host then
+        waits for all queued GPU work, e.g. the whole local training before the aggregation is enqueued.)"""
+        t = torch.as_tensor(np.asarray(arr), dtype=dtype)
         if self.device.type != "cuda":
             return t
         return t.pin_memory().to(self.device, non_blocking=True)
@@ -263,7 +342,7 @@ class FLRunner:
             lo, hi = rows[0], rows[-1] + 1
             self._train_view(rs.rows(lo, hi), clients, round_idx, epochs, spec.rows(lo, hi), tag, epoch_hook, lr)
             return
-        ix = torch.tensor(rows, device=self.device)
+        ix = self._to_dev(rows)
         k = len(rows)
         sc = self._scratch_rows(k)
         view = sc.rows(0, k)
@@ -337,8 +416,7 @@ class FLRunner:
                 epoch_hook(ep, view, clients)
         if sums:
             B = cfg.batch_size
-            nb = torch.tensor([max(1, -(-len(self.splits[c].train) // B)) for c in clients], dtype=torch.float32,
-                              device=self.device)
+            nb = self._to_dev([max(1, -(-len(self.splits[c].train) // B)) for c in clients], torch.float32)
             means = torch.stack(sums, 1) / nb.view(-1, 1)   # mean batch loss per (client, epoch), as logged
             for j, c in enumerate(clients):
                 self._loss_log.setdefault(int(c), []).append(means[j])
@@ -368,7 +446,7 @@ class FLRunner:
         if _contiguous(rows):
             th, bu = theta[rows[0]:rows[-1] + 1, :self.P], bufs[rows[0]:rows[-1] + 1, :self.Q]
         else:
-            ix = torch.tensor(rows, device=self.device)
+            ix = self._to_dev(rows)
             th, bu = gather_rows(theta, ix)[:, :self.P], gather_rows(bufs, ix)[:, :self.Q]
         return self._rows_nnz(th) + self._rows_nnz(bu)
 
@@ -551,7 +629,7 @@ class FLRunner:
         plan, idx = self._plan(clients, self._epoch_chunks(round_idx, tag, 0, n_batches=1))
         seed_dev = self._seed_dev_or_zero()
         for r0, r1, s, off, n, G, B in plan:
-            t = torch.tensor(rows[r0:r1], device=self.device)
+            t = self._to_dev(rows[r0:r1])
             th, bu = gather_rows(rs.theta, t), gather_rows(rs.bufs, t)
             seed_dev.fill_(self._step_seed(round_idx, tag, 0, s))
             self.e.train_step(th, bu, self.grads[r0:r1], idx[off:off + n], G, B, self.cfg.dropout_keep,
@@ -687,8 +765,8 @@ class FLRunner:
                 torch.zeros((n, width), dtype=t.dtype, device=self.device)
             keep = [(i, self.row_of[c]) for i, c in enumerate(new_local) if c in self.row_of]
             if keep:
-                di = torch.tensor([i for i, _ in keep], device=self.device)
-                si = torch.tensor([j for _, j in keep], device=self.device)
+                di = self._to_dev([i for i, _ in keep])
+                si = self._to_dev([j for _, j in keep])
                 nt[di] = t[si]
             for i, c in enumerate(new_local):
                 if c not in self.row_of:
@@ -781,7 +859,7 @@ class FLRunner:
             self.theta[rows[0]:rows[-1] + 1].copy_(self.w_global.expand(len(rows), -1))
             self.bufs[rows[0]:rows[-1] + 1].copy_(self.b_global.expand(len(rows), -1))
         else:
-            ix = torch.tensor(rows, device=self.device)
+            ix = self._to_dev(rows)
             self.theta[ix] = self.w_global.unsqueeze(0).expand(len(rows), -1)
             self.bufs[ix] = self.b_global.unsqueeze(0).expand(len(rows), -1)
         # downlink: count_communication_params(w_global) per sampled client (the same state for all of them)
@@ -834,7 +912,7 @@ class FLRunner:
             if _contiguous(rr):
                 torch.sub(self.theta[rr[0]:rr[-1] + 1, :self.P], self.w_global, out=d)
             else:
-                torch.sub(self.theta.index_select(0, torch.tensor(rr, device=self.device))[:, :self.P], self.w_global,
+                torch.sub(self.theta.index_select(0, self._to_dev(rr))[:, :self.P], self.w_global,
                           out=d)
             bits = torch.zeros((n, self.W), dtype=torch.int32, device=self.device)
             space.select(MK.REGROW_ABS, d, bits, torch.full((n, 1), k, dtype=torch.int64))
@@ -874,7 +952,7 @@ class FLRunner:
         Pp = (self.P + 63) // 64 * 64  # keep the buffer section 16-B aligned for the vectorised kernel
         buf = torch.zeros(Pp + self.Q, dtype=torch.float32, device=self.device)
         if rows:
-            w = torch.tensor(weights, dtype=torch.float32, device=self.device)
+            w = self._to_dev(weights, torch.float32)
             if self.device.type == "cuda" and _contiguous(rows):
                 m, st = ops.ext(), torch.cuda.current_stream().cuda_stream
                 lo = rows[0]
@@ -884,7 +962,7 @@ class FLRunner:
                     m.weighted_rows_sum(bufs[lo].data_ptr(), w.data_ptr(), len(rows), self.Q, bufs.stride(0), 0.0,
                                         buf[Pp:].data_ptr(), st)
             else:
-                ix = torch.tensor(rows, device=self.device)
+                ix = self._to_dev(rows)
                 buf[:self.P] = (w.view(-1, 1) * theta[ix]).sum(0)
                 buf[Pp:] = (w.view(-1, 1) * bufs[ix]).sum(0)
         return buf, Pp
@@ -918,7 +996,7 @@ class FLRunner:
         for Krum and are coordinate-aggregated otherwise."""
         from ..core import robustness as R
         rows, loc = self._local_rows(sampled)
-        ids = torch.tensor(loc, dtype=torch.float32, device=self.device)
+        ids = self._to_dev(loc, torch.float32)
         W = self.P + self.Q
         lm = torch.cat([self.theta[rows, :self.P], self.bufs[rows, :self.Q]], 1) if rows else \
             torch.zeros((0, W), device=self.device)
@@ -977,7 +1055,7 @@ class FLRunner:
             cap = chunk or self.cfg.test_batch
             tb = -(-allidx.size // -(-allidx.size // cap))  # ceil(n / ceil(n / cap))
             acc = torch.zeros((len(js), 3), dtype=torch.float64, device=self.device)
-            own_t = torch.from_numpy(owner).to(self.device)
+            own_t = self._to_dev(owner)
             all_t = self._upload_i32(allidx)
             for s in range(0, allidx.size, tb):
                 idx = all_t[s:s + tb]
@@ -999,7 +1077,7 @@ class FLRunner:
             return -(-n // 8) * 8
         return int(math.ceil(2.0 ** (math.ceil(4.0 * math.log2(n) - 1e-9) / 4.0)))
 
-    def eval_grouped(self, theta, bufs, rows, clients, which="test"):
+    def eval_grouped(self, theta, bufs, rows, clients, which="test", device_out=False):
         """Model row rows[j] on client clients[j]'s split, per-client (correct, loss_sum, total).
 
         Ragged splits (Dirichlet / site partitions give nearly every client its own size) are bucketed by padded
@@ -1007,9 +1085,11 @@ class FLRunner:
         rows past a client's size repeating its first sample and masked out of the sums — a few launches instead
         of one small latency-bound launch per distinct size (or per test_batch chunk of a large client).  Every
         model is per-sample in eval mode (GroupNorm, BatchNorm on running statistics), so the padding cannot
-        change a valid sample's logits.  ``NIDT_EVAL_PAD=0`` keeps the exact-size grouping (A/B)."""
+        change a valid sample's logits.  ``NIDT_EVAL_PAD=0`` keeps the exact-size grouping (A/B).  ``device_out``:
+        the [len(clients), 3] float64 result stays on the device (no host synchronisation)."""
         if os.environ.get("NIDT_EVAL_PAD", "1") == "0":
-            return self._eval_grouped_exact(theta, bufs, rows, clients, which)
+            r = self._eval_grouped_exact(theta, bufs, rows, clients, which)
+            return torch.from_numpy(r).to(self.device) if device_out else r
         out = np.zeros((len(clients), 3), dtype=np.float64)
         splits = [self._split_of(c, which) for c in clients]
         buckets = {}
@@ -1048,7 +1128,7 @@ class FLRunner:
                 if _contiguous(rr):
                     th, bu = theta[rr[0]:rr[-1] + 1], bufs[rr[0]:rr[-1] + 1]
                 else:
-                    t = torch.tensor(rr, device=self.device)
+                    t = self._to_dev(rr)
                     th, bu = gather_rows(theta, t), gather_rows(bufs, t)
                 # host->device through pinned buffers, enqueued before the forward: a pageable copy here would
                 # block the host until this launch's forward finished and serialise the launch sequence
@@ -1067,6 +1147,12 @@ class FLRunner:
             pending.append((grp, res))
         for st in used or ():
             main.wait_stream(st)
+        if device_out:  # accumulate on the device: no host wait (the deferred-metrics path)
+            od = torch.zeros((len(clients), 3), dtype=torch.float64, device=self.device)
+            if pending:
+                pos = self._upload_i32(np.concatenate([np.asarray(g, dtype=np.int32) for g, _ in pending]))
+                od.index_add_(0, pos.long(), torch.cat([r for _, r in pending], 0).to(self.device))
+            return od
         if pending:
             host = torch.cat([r for _, r in pending], 0).cpu().numpy()
             o = 0
@@ -1104,7 +1190,7 @@ class FLRunner:
                     if _contiguous(rr):
                         th, bu = theta[rr[0]:rr[-1] + 1], bufs[rr[0]:rr[-1] + 1]
                     else:
-                        t = torch.tensor(rr, device=self.device)
+                        t = self._to_dev(rr)
                         th, bu = gather_rows(theta, t), gather_rows(bufs, t)
                     idx = self._upload_i32(np.concatenate([self._split_of(clients[j], which) for j in grp]))
                     logits = self.e.eval_logits(th, bu, idx, len(grp), n).view(len(grp), n, -1)
@@ -1131,7 +1217,7 @@ class FLRunner:
         th, bu = self._eval_cache
         return th[:k], bu[:k]
 
-    def _eval_global_and_personal(self, theta=None, bufs=None):
+    def _eval_global_and_personal(self, theta=None, bufs=None, device_out=False):
         """Global model and every local client's personal model on that client's test split, as grouped launches:
         the personal rows straight from the row matrix, the global model from K = min(C, 64) staged copies that
         every group of clients reuses (rows j mod K).  (Staging copies of all C personal rows next to C copies of
@@ -1154,26 +1240,28 @@ class FLRunner:
                 th[C:].copy_(self.w_global.expand(C, -1))
                 bu[:C].copy_(bufs[:C])
                 bu[C:].copy_(self.b_global.expand(C, -1))
-            res = self.eval_grouped(th, bu, list(range(2 * C)), self.local + self.local)
+            res = self.eval_grouped(th, bu, list(range(2 * C)), self.local + self.local, device_out=device_out)
             return res[C:], res[:C]
-        pers = self.eval_grouped(theta, bufs, list(range(C)), self.local)
+        pers = self.eval_grouped(theta, bufs, list(range(C)), self.local, device_out=device_out)
         K = min(C, 64)
         th, bu = self._eval_buffers(K)
         with torch.no_grad():
             th.copy_(self.w_global.expand(K, -1))
             bu.copy_(self.b_global.expand(K, -1))
-        glob = self.eval_grouped(th, bu, [j % K for j in range(C)], self.local)
+        glob = self.eval_grouped(th, bu, [j % K for j in range(C)], self.local, device_out=device_out)
         return glob, pers
 
-    def gather_metrics(self, clients, arr):
-        """Per-client metric rows of this rank's clients -> [N, k] numpy on every rank (one all-reduce)."""
+    def gather_metrics(self, clients, arr, device_out=False):
+        """Per-client metric rows of this rank's clients -> [N, k] on every rank (one all-reduce): numpy, or with
+        ``device_out`` a device tensor (``arr`` may then be a device tensor too: nothing waits for the device)."""
         k = arr.shape[1] if arr.ndim == 2 else 1
         res = torch.zeros((self.N, k), dtype=torch.float64, device=self.device)
         if len(clients):
-            res[torch.tensor(list(clients), device=self.device)] = torch.from_numpy(
-                np.asarray(arr, dtype=np.float64).reshape(len(clients), k)).to(self.device)
+            src = arr if torch.is_tensor(arr) else torch.from_numpy(np.asarray(arr, dtype=np.float64))
+            res.index_copy_(0, self._upload_i32(list(clients)).to(self.device).long(),
+                            src.to(self.device, torch.float64).reshape(len(clients), k))
         rt.all_reduce_buckets(res, self.info)
-        return res.cpu().numpy()
+        return res if device_out else res.cpu().numpy()
 
     @staticmethod
     def mean_acc_loss(r, cols=(0, 1, 2)):
@@ -1182,22 +1270,71 @@ class FLRunner:
             return 0.0, 0.0
         return float(np.mean(r[ok, cols[0]] / r[ok, cols[2]])), float(np.mean(r[ok, cols[1]] / r[ok, cols[2]]))
 
-    def evaluate(self, round_idx, theta=None, bufs=None):
-        t0 = time.perf_counter()
-        glob, pers = self._eval_global_and_personal(theta, bufs) if self.C else (np.zeros((0, 3)), np.zeros((0, 3)))
-        r = self.gather_metrics(self.local, np.concatenate([glob, pers], 1))
+    def _defer_metrics(self):
+        """Timed GPU runs without a logger read a round's metrics one round later (pinned copy + event) instead of
+        waiting for the device at the end of every round; with a logger (reference log order) or on the CPU they are
+        read at once.  ``NIDT_DEFER_METRICS=0`` disables the deferral."""
+        env = os.environ.get("NIDT_DEFER_METRICS", "1")
+        return env == "force" or (self.device.type == "cuda" and self.log is None and env != "0")
+
+    def _flush_metrics(self, ready_only=False):
+        """Fold the evaluations still in flight into ``stat_info`` (in round order); ``ready_only``: only those whose
+        device result has already arrived (never waits)."""
+        while self._pending_metrics:
+            if ready_only and self._pending_metrics[0][2] is not None and not self._pending_metrics[0][2].query():
+                break
+            round_idx, host, ev, holder = self._pending_metrics.pop(0)
+            if ev is not None:
+                ev.synchronize()
+            holder["res"] = self._record_metrics(round_idx, host.numpy().copy())
+            if ev is not None:
+                self._pinned_free.append(host)
+
+    def _record_metrics(self, round_idx, r):
+        sl = dict.__getitem__  # the raw lists: this IS the flush
         g_acc, g_loss = self.mean_acc_loss(r, (0, 1, 2))
         p_acc, p_loss = self.mean_acc_loss(r, (3, 4, 5))
-        self.stat_info["global_test_acc"].append(g_acc)
-        self.stat_info["global_test_loss"].append(g_loss)
-        self.stat_info["person_test_acc"].append(p_acc)
-        self.stat_info["person_test_loss"].append(p_loss)
+        sl(self.stat_info, "global_test_acc").append(g_acc)
+        sl(self.stat_info, "global_test_loss").append(g_loss)
+        sl(self.stat_info, "person_test_acc").append(p_acc)
+        sl(self.stat_info, "person_test_loss").append(p_loss)
         if self.log is not None and self.info.is_main:
             self.log.info("################global_test_on_all_clients : {}".format(round_idx))
             self.log.info({"global_test_acc": g_acc, "global_test_loss": g_loss})
             self.log.info({"person_test_acc": p_acc, "person_test_loss": p_loss})
-        self.timers["eval"] += time.perf_counter() - t0
         return dict(global_test_acc=g_acc, global_test_loss=g_loss, person_test_acc=p_acc, person_test_loss=p_loss)
+
+    def evaluate(self, round_idx, theta=None, bufs=None):
+        t0 = time.perf_counter()
+        if self._defer_metrics():
+            self._flush_metrics(ready_only=True)  # earlier rounds whose copies have landed: no wait
+            if self.C:
+                glob, pers = self._eval_global_and_personal(theta, bufs, device_out=True)
+                loc = torch.cat([glob, pers], 1)
+            else:
+                loc = torch.zeros((0, 6), dtype=torch.float64, device=self.device)
+            r = self.gather_metrics(self.local, loc, device_out=True)
+            if self.device.type == "cuda":
+                host = next((h for h in self._pinned_free if h.shape == r.shape), None)
+                if host is not None:
+                    self._pinned_free.remove(host)
+                else:
+                    host = torch.empty(r.shape, dtype=r.dtype, pin_memory=True)
+                host.copy_(r, non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record()
+            else:  # NIDT_DEFER_METRICS=force on the CPU (tests of the deferred bookkeeping)
+                host, ev = r.clone(), None
+            holder = {}
+            self._pending_metrics.append((round_idx, host, ev, holder))
+            self.timers["eval"] += time.perf_counter() - t0
+            return LazyMetrics(self, holder)
+        glob, pers = self._eval_global_and_personal(theta, bufs) if self.C else (np.zeros((0, 3)), np.zeros((0, 3)))
+        r = self.gather_metrics(self.local, np.concatenate([glob, pers], 1))
+        self._flush_metrics()
+        res = self._record_metrics(round_idx, r)
+        self.timers["eval"] += time.perf_counter() - t0
+        return res
 
     # ---------------------------------------------------------------------------------------------- driver
     def _heartbeat(self):

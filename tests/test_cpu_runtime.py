@@ -57,7 +57,8 @@ def test_volume_file_validation(tmp_path):
     trunc.write_bytes(open(p, "rb").read()[:5000])
     with pytest.raises(RuntimeError, match="truncated"):
         VolumeFile(str(trunc))
-    with pytest.raises(TypeError):
+    # floats are accepted only in the reference's k/255 form (quantised exactly); raw 0..255 floats are refused
+    with pytest.raises(ValueError, match="k/255"):
         write_volume_file(str(tmp_path / "f.nidtvol"), X.astype(np.float32), y)
 
 
