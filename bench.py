@@ -252,6 +252,8 @@ def run(args):
     res = None
     for r in range(args.warmup, args.warmup + args.steps):
         res = runner.run_round(r, sync_timers=args.phase_timers)
+    if hasattr(runner, "_flush_metrics"):
+        runner._flush_metrics()   # the last round's deferred evaluation metrics land on the host inside the timing
     sync()
     t_local = time.perf_counter() - t0   # this rank's own work (before waiting for the slowest rank)
     rt.barrier(info)
@@ -309,7 +311,7 @@ def run(args):
             "rank_imbalance": (round(max(per_rank_train) / (sum(per_rank_train) / len(per_rank_train)), 3)
                                if per_rank_train and sum(per_rank_train) > 0 else None),
             "peak_hbm_gib": round(peak_gib, 2),
-            "last_round_metrics": res,
+            "last_round_metrics": None if res is None else dict(res),
         }
         if args.phase_timers:
             out["phase_s"] = {k: round(v, 3) for k, v in runner.timers.items()}

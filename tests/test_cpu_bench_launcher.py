@@ -50,12 +50,28 @@ def _port():
 
 def test_self_launch_four_ranks_matches_one_process():
     one = _json(_run([sys.executable, BENCH, "--gpus", "1"] + TINY))
-    four = _json(_run([sys.executable, BENCH, "--gpus", "4"] + TINY))
+    env = _env()
+    env["NIDT_DEFER_METRICS"] = "force"   # the GPU default: metrics read back one round late (pinned copy + event)
+    four = _json(_run([sys.executable, BENCH, "--gpus", "4"] + TINY, env=env))
     assert one["n_gpus"] == 1 and four["n_gpus"] == 4
     assert four["config"]["parallelism"].endswith("dp4") and len(four["rank_wall_s"]) == 4
     assert four["metric"] == one["metric"]
     for k, v in one["last_round_metrics"].items():
         assert np.isclose(four["last_round_metrics"][k], v, rtol=1e-5, atol=1e-6), (k, v, four["last_round_metrics"])
+
+
+def test_eight_ranks_headline_layout_matches_one_process():
+    """The headline layout of the driver's 8-GPU scaling run: 64 clients, 8 per rank, deferred metrics."""
+    big = ["--device", "cpu", "--clients", "64", "--train-per-client", "4", "--test-per-client", "2", "--batch", "4",
+           "--steps", "1", "--warmup", "1"]
+    one = _json(_run([sys.executable, BENCH, "--gpus", "1"] + big))
+    env = _env()
+    env["NIDT_DEFER_METRICS"] = "force"
+    eight = _json(_run([sys.executable, BENCH, "--gpus", "8"] + big, env=env))
+    assert eight["n_gpus"] == 8 and len(eight["rank_wall_s"]) == 8
+    assert eight["config"]["parallelism"].endswith("dp8") and eight["config"]["clients"] == 64
+    for k, v in one["last_round_metrics"].items():
+        assert np.isclose(eight["last_round_metrics"][k], v, rtol=1e-5, atol=1e-6), (k, v, eight["last_round_metrics"])
 
 
 def test_torchrun_launch_shape_still_works():

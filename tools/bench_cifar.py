@@ -136,7 +136,7 @@ def main():
                        "epochs": args.epochs, "batch": args.batch, "lr": args.lr, "dense_ratio": args.dense_ratio,
                        "partition": "dir 0.3", "train_images": args.n_train, "eval_every_round": not args.no_eval,
                        "dataset": args.dataset, "augment": not args.no_augment},
-            "last_round_metrics": res}), flush=True)
+            "last_round_metrics": None if res is None else dict(res)}), flush=True)
     rt.shutdown(info)
 
 

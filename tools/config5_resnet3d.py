@@ -120,7 +120,7 @@ def main():
                           "peak_hbm_gib_rank0": round(peak, 1), "peak_gib_each_round": peaks,
                           "phase_s_each_round": phases, "mem_gib_phase_alloc_peak_reserved": memlog,
                           "update_topk": args.topk, "aggregate_elems": runner.stat_info.get("aggregate_elems"),
-                          "metrics": res}), flush=True)
+                          "metrics": None if res is None else dict(res)}), flush=True)
     rt.shutdown(info)
 
 
