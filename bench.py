@@ -189,7 +189,9 @@ def run(args):
     from neuroimagedisttraining_amd.data.synthetic_fl import build_fl_volumes, skewed_sizes, to_hip_store
     from neuroimagedisttraining_amd.models.alexnet3d import AlexNet3D_Dropout
 
-    if args.device == "cuda" and args.gpus > 1 and torch.cuda.device_count() < args.gpus:
+    # NIDT_DIST_BACKEND=gloo rehearses the multi-rank layout with every rank on the one visible GPU (not a scaling run)
+    if (args.device == "cuda" and args.gpus > 1 and torch.cuda.device_count() < args.gpus
+            and os.environ.get("NIDT_DIST_BACKEND") != "gloo"):
         raise SystemExit("bench.py: --gpus %d but only %d GPU(s) visible" % (args.gpus, torch.cuda.device_count()))
     info = rt.init_distributed(prefer_gpu=args.device == "cuda")
     if info.world != args.gpus:
