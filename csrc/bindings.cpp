@@ -156,6 +156,7 @@ void conv1_fwd_pool(uintptr_t x8, uintptr_t idx, uintptr_t w8, uintptr_t scale, 
 int conv1_wgrad_nq(int NB);
 int conv1_wgrad_mx_npb(int NB);
 void conv1_wgrad_mode(int mode);
+void conv1_fwd_mode(int mode);
 int conv1_kslots();
 void conv1_wgrad(uintptr_t x8, uintptr_t idx, uintptr_t dp, uintptr_t pout, uintptr_t amax, int NB, int B,
                  uintptr_t part, uintptr_t w125, uintptr_t mu, uintptr_t covw, uintptr_t invstd, uintptr_t theta,
@@ -290,6 +291,7 @@ PYBIND11_MODULE(_nidt_hip, m) {
   DEF(conv1_wgrad_nq);
   DEF(conv1_wgrad_mx_npb);
   DEF(conv1_wgrad_mode);
+  DEF(conv1_fwd_mode);
   DEF(conv1_kslots);
   DEF(head);
   DEF(cls_head_train);

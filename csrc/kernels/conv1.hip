@@ -637,9 +637,240 @@ __global__ __launch_bounds__(256, OCC) void k_conv1_fwd_pool_pipe(const uint8_t*
 #undef C1_STORE
 }
 
+// max over the 3 columns of a pooling window = this lane and the next two of its 16-lane row: two VOP2 DPP maxes
+// (the lanes whose window leaves the row are not writers and keep garbage); one s_nop 1 covers the VALU -> DPP
+// read hazard of all four inputs
+__device__ __forceinline__ void pool3_dpp4(const float (&b)[4], float (&m)[4]) {
+  asm volatile(
+      "s_nop 1\n\t"
+      "v_max_f32_dpp %0, %4, %4 row_shl:1 row_mask:0xf bank_mask:0xf\n\t"
+      "v_max_f32_dpp %1, %5, %5 row_shl:1 row_mask:0xf bank_mask:0xf\n\t"
+      "v_max_f32_dpp %2, %6, %6 row_shl:1 row_mask:0xf bank_mask:0xf\n\t"
+      "v_max_f32_dpp %3, %7, %7 row_shl:1 row_mask:0xf bank_mask:0xf\n\t"
+      "v_max_f32_dpp %0, %4, %0 row_shl:2 row_mask:0xf bank_mask:0xf\n\t"
+      "v_max_f32_dpp %1, %5, %1 row_shl:2 row_mask:0xf bank_mask:0xf\n\t"
+      "v_max_f32_dpp %2, %6, %2 row_shl:2 row_mask:0xf bank_mask:0xf\n\t"
+      "v_max_f32_dpp %3, %7, %3 row_shl:2 row_mask:0xf bank_mask:0xf"
+      : "=&v"(m[0]), "=&v"(m[1]), "=&v"(m[2]), "=&v"(m[3])
+      : "v"(b[0]), "v"(b[1]), "v"(b[2]), "v"(b[3]));
+}
+
+// Wave-tile variant of the fused forward (k_conv1_fwd_w64): each wave owns ALL 64 output channels of one group of
+// 15 conv columns (op = wave), instead of 32 channels x 2 column groups.  The B fragment of a (dd, dh, k-step) is
+// then read and assembled once for 4 MFMAs instead of twice for 2 each, which halves the LDS traffic (the pipe
+// kernel's LDS array time was ~80 % of its MFMA time before its 34 % bank conflicts) and the B-assembly VALU
+// (v_perm / v_cndmask / v_mov of k-steps 2-3).  The A operand (64 x 128 f16) stays in 64 VGPRs.  Halo loads are
+// unconditional (columns >= 61 clamp to 60: they only feed conv columns >= 59, which no pooled cell reads) with a
+// scalar row base and a per-thread 32-bit offset; the max-pool starts from the first candidate pair instead of -inf.
+template <int PF>
+__global__ __launch_bounds__(256, 2) void k_conv1_fwd_w64(const uint8_t* __restrict__ x8, const int* __restrict__ idx,
+                                                          const uint16_t* __restrict__ w8,
+                                                          const float* __restrict__ scale,
+                                                          const float* __restrict__ shift, int B,
+                                                          uint16_t* __restrict__ out, uint8_t* __restrict__ amax,
+                                                          int nq) {
+  constexpr int HX = 64, KS = 4, KW = KS * 32;
+  constexpr int HALO = 5 * 5 * HX * 8;           // f16 elements per buffer
+  constexpr int NV = 5 * 5 * HX;                 // 1600 halo voxels
+  constexpr int NLD = (NV + 255) / 256;          // 7 per thread (the 7th: wave 0 only)
+  __shared__ __attribute__((aligned(16))) uint16_t halo[2 * HALO];
+  __shared__ __attribute__((aligned(16))) float scsh[2][kC1];  // |scale| / 255 and shift (read by the epilogue)
+  const int bid0 = xcd_remap(blockIdx.x, gridDim.x);
+  const int q = bid0 % nq, bid = bid0 / nq;
+  const int pd = bid % kPD, n = bid / kPD;
+  const int ph_lo = (kPH * q) / nq, ph_hi = (kPH * (q + 1)) / nq;
+  const int g = n / B;
+  const int tid = threadIdx.x, lane = tid & 63, op = tid >> 6;
+  if (tid < kC1) {
+    scsh[0][tid] = fabsf(scale[g * kC1 + tid]) * (1.0f / 255.0f);
+    scsh[1][tid] = shift[g * kC1 + tid];
+  }
+  const uint8_t* xs = x8 + ((int64_t)idx[n] * kPZ * kPY * kPX + (int64_t)(3 * pd) * kPY * kPX) * 8;
+  int lofs[NLD];
+#pragma unroll
+  for (int u = 0; u < NLD; ++u) {
+    const int e = min(tid + 256 * u, NV - 1);
+    const int xh = min(e & (HX - 1), kPX - 1), yz = e >> 6, yh = yz % 5, zh = yz / 5;
+    lofs[u] = ((zh * kPY + yh) * kPX + xh) * 8;
+  }
+  uint2 pre[NLD];
+  auto load_row = [&](int ph) {
+    const uint8_t* rp = xs + (int64_t)(3 * ph) * kPX * 8;
+#pragma unroll
+    for (int u = 0; u < NLD; ++u) pre[u] = *reinterpret_cast<const uint2*>(rp + lofs[u]);
+  };
+  auto store_row = [&](int buf) {
+#pragma unroll
+    for (int u = 0; u < NLD; ++u) {
+      const int e = tid + 256 * u;
+      if (u < NLD - 1 || e < NV) *reinterpret_cast<uint4*>(&halo[buf * HALO + e * 8]) = u8x8_to_f16magic(pre[u]);
+    }
+  };
+  load_row(ph_lo);
+  const int fr = lane & 15, fq = lane >> 4;
+  f16x8 fa[4][KS];
+  const uint16_t* wg = w8 + (int64_t)g * kC1 * KW;
+  float rs[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      fa[i][s] = *reinterpret_cast<const f16x8*>(wg + (16 * i + fr) * KW + 32 * s + 8 * fq);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) rs[i] += (float)fa[i][s][e];
+    }
+  f32x4 cinit[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    rs[i] += __shfl_xor(rs[i], 16, 64);
+    rs[i] += __shfl_xor(rs[i], 32, 64);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) cinit[i][r] = -1024.f * __shfl(rs[i], 4 * fq + r, 64);
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+#pragma unroll
+    for (int s = 0; s < KS; ++s) asm volatile("" : "+v"(fa[i][s]));
+#pragma unroll
+    for (int r = 0; r < 4; ++r) asm volatile("" : "+v"(cinit[i][r]));
+  }
+  auto goff = [](int t) { return (((t / 9) * 5 + (t / 3) % 3) * HX + (t % 3)) * 8; };
+  int toff[KS];
+  toff[0] = goff(kC1F2[0][fq]);
+  toff[1] = goff(kC1F2[0][4 + fq]);
+  toff[2] = goff(kC1D2[0][fq]);
+  toff[3] = goff(kC1W[fq]);
+  const int gh = goff(kC1H2[0][fq]), gx1 = goff(kC1X1[fq]), gx2 = goff(kC1X2[fq]);
+  const bool xsrc2 = fq == 2;
+  const uint32_t xsel1 = fq == 0 ? 0x03020100u : fq == 3 ? 0x0c0c0100u : 0x05040100u;
+  const uint32_t xsel2 = fq == 0 ? 0x03020100u : fq == 3 ? 0x0c0c0c0cu : 0x05040100u;
+  // k-step 3's two 2-phase groups: the second dword of each is picked by address (dword 2 for the HW groups of
+  // fq = 2, dword 1 otherwise) instead of a v_cndmask after a 16-B read
+  const int gx1s = gx1 + (xsrc2 ? 4 : 2), gx2s = gx2 + (xsrc2 ? 4 : 2);
+  auto bfrag = [&](const uint16_t* hb, int s, int ro) -> f16x8 {
+    if (s < 3) return c1_bfrag<KS>(hb, s, ro, toff, gh, gx1, gx2, xsrc2, xsel1, xsel2);
+    const uint4 w = *reinterpret_cast<const uint4*>(&hb[ro + toff[3]]);
+    const uint32_t a0 = *reinterpret_cast<const uint32_t*>(&hb[ro + gx1]);
+    const uint32_t a1 = *reinterpret_cast<const uint32_t*>(&hb[ro + gx1s]);
+    const uint32_t b0 = *reinterpret_cast<const uint32_t*>(&hb[ro + gx2]);
+    const uint32_t b1 = *reinterpret_cast<const uint32_t*>(&hb[ro + gx2s]);
+    uint4 v;
+    v.x = __builtin_amdgcn_perm(w.y, w.x, 0x05040100u);  // phases 0, 2 (low halves)
+    v.y = __builtin_amdgcn_perm(w.w, w.z, 0x05040100u);  // phases 4, 6
+    v.z = __builtin_amdgcn_perm(a1, a0, xsel1);
+    v.w = __builtin_amdgcn_perm(b1, b0, xsel2);
+    return __builtin_bit_cast(f16x8, v);
+  };
+  const int colbase = (15 * op + fr) * 8;
+  const int wloc = fr / 3, dw = fr - 3 * wloc;
+  const int pw = 5 * op + wloc;
+  const bool writer = (dw == 0) && (fr < 15) && (pw < kPW);
+  store_row(0);
+  __syncthreads();
+  for (int ph = ph_lo; ph < ph_hi; ++ph) {
+    const int cur = (ph - ph_lo) & 1;
+    if (ph + 1 < ph_hi) load_row(ph + 1);
+    const uint16_t* hb = halo + cur * HALO + colbase;
+    float best[4][4], pend[4][4], pend2[4][4];
+#pragma unroll
+    for (int dd = 0; dd < 3; ++dd) {
+      constexpr int NQ = 3 * KS;
+      f16x8 rb[PF + 1];
+#pragma unroll
+      for (int p = 0; p < PF; ++p)
+        rb[p] = bfrag(hb, p % KS, ((dd * 5 + p / KS) * HX) * 8);
+      f32x4 acc[4];
+#pragma unroll
+      for (int qq = 0; qq < NQ; ++qq) {
+        const int dh = qq / KS, s = qq % KS;
+        if (qq + PF < NQ) {
+          const int qn = qq + PF;
+          rb[qn % (PF + 1)] = bfrag(hb, qn % KS, ((dd * 5 + qn / KS) * HX) * 8);
+        }
+        const f16x8 fb = rb[qq % (PF + 1)];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[i][s], fb, s == 0 ? cinit[i] : acc[i], 0, 0, 0);
+        if (PF > 1) asm volatile("" ::: "memory");
+        if (s != KS - 1) continue;
+        // the 9 (dd, dh) candidates of a lane fold into the running max with 4 v_max3: k = 0, 1 wait, k = 2 starts
+        // the max, then every even k folds itself and the odd one before it
+        const uint32_t tag = (uint32_t)(dd * 9 + dh * 3 + dw);
+        const int k = dd * 3 + dh;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float e = tag_idx(acc[i][r], tag);
+            if (k == 0) pend2[i][r] = e;
+            else if (k & 1) pend[i][r] = e;
+            else if (k == 2) best[i][r] = vmax3(pend2[i][r], pend[i][r], e);
+            else best[i][r] = vmax3(best[i][r], pend[i][r], e);
+          }
+      }
+    }
+    const int64_t o = ((((int64_t)n * kPD + pd) * kPH + ph) * kPW + pw) * kC1 + 4 * fq;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float m[4];
+      pool3_dpp4(best[i], m);
+      const f32x4 scv = *reinterpret_cast<const f32x4*>(&scsh[0][16 * i + 4 * fq]);
+      const f32x4 shv = *reinterpret_cast<const f32x4*>(&scsh[1][16 * i + 4 * fq]);
+      uint32_t u[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) u[r] = __float_as_uint(m[r]);
+      // argmax tags: the low byte of each candidate, gathered by two v_perm, then masked to 5 bits
+      const uint32_t t01 = __builtin_amdgcn_perm(u[1], u[0], 0x0c0c0400u);
+      const uint32_t t23 = __builtin_amdgcn_perm(u[3], u[2], 0x04000c0cu);
+      const uint32_t ab = (t01 | t23) & 0x1f1f1f1fu;
+      f32x2 v01 = {__uint_as_float(u[0] & ~31u), __uint_as_float(u[1] & ~31u)};
+      f32x2 v23 = {__uint_as_float(u[2] & ~31u), __uint_as_float(u[3] & ~31u)};
+      const f32x2 s01 = {scv[0], scv[1]}, s23 = {scv[2], scv[3]}, h01 = {shv[0], shv[1]}, h23 = {shv[2], shv[3]};
+      v01 = v01 * s01 + h01;
+      v23 = v23 * s23 + h23;
+      // relu on the packed bf16 pair: a signed 16-bit max with 0 zeroes exactly the negative values (and -0)
+      typedef short s16x2 __attribute__((ext_vector_type(2)));
+      const s16x2 z = {0, 0};
+      const s16x2 p01 = __builtin_elementwise_max(__builtin_bit_cast(s16x2, pack_bf16x2(v01[0], v01[1])), z);
+      const s16x2 p23 = __builtin_elementwise_max(__builtin_bit_cast(s16x2, pack_bf16x2(v23[0], v23[1])), z);
+      if (writer) {
+        *reinterpret_cast<uint2*>(out + o + 16 * i) =
+            make_uint2(__builtin_bit_cast(uint32_t, p01), __builtin_bit_cast(uint32_t, p23));
+        *reinterpret_cast<uint32_t*>(amax + o + 16 * i) = ab;
+      }
+    }
+    if (ph + 1 < ph_hi) store_row(cur ^ 1);
+    __syncthreads();
+  }
+}
+
+// forward variant: NIDT_C1_FWD=1 (default) the wave-tile kernel (k_conv1_fwd_w64: 4.20 -> 3.33 ms per 64-client
+// step, 0.59 -> 0.47 ms at 8 clients, profiles/r5_c1fwd_w64.txt), 0 the channel-split pipe kernel;
+// conv1_fwd_mode(m) overrides it at run time (tests: m = 0 / 1, -1 back to the environment / default)
+static int g_c1fwd_mode = -1;
+void conv1_fwd_mode(int mode) { g_c1fwd_mode = mode; }
+int conv1_fwd_variant() {
+  static const int v = [] {
+    const char* e = getenv("NIDT_C1_FWD");
+    return e ? atoi(e) : 1;
+  }();
+  return g_c1fwd_mode >= 0 ? g_c1fwd_mode : v;
+}
+
 void conv1_fwd_pool(uintptr_t x8, uintptr_t idx, uintptr_t w8, uintptr_t scale, uintptr_t shift, int NB, int B,
                     uintptr_t out, uintptr_t amax, uintptr_t stream) {
   NIDT_REQUIRE(NB % B == 0, "conv1_fwd_pool: NB % B");
+  if (conv1_fwd_variant() == 1 && conv1_kslots() == 128 && conv1_tapord() == 0) {
+    static const int nq1 = [] {
+      const char* e = getenv("NIDT_C1_NQ");
+      return e ? std::max(1, std::min(kPH, atoi(e))) : 1;
+    }();
+    hipLaunchKernelGGL((k_conv1_fwd_w64<2>), dim3(kPD * NB * nq1), dim3(256), 0, as_stream(stream),
+                       ptr<const uint8_t>(x8), ptr<const int>(idx), ptr<const uint16_t>(w8), ptr<const float>(scale),
+                       ptr<const float>(shift), B, ptr<uint16_t>(out), ptr<uint8_t>(amax), nq1);
+    NIDT_CHECK(hipGetLastError());
+    return;
+  }
   // B-fragment prefetch distance (k-steps); NIDT_C1_PF=1/2/3 selects it (A/B), default 2
   static const int pf = [] {
     const char* e = getenv("NIDT_C1_PF");

@@ -606,6 +606,38 @@ def test_conv1_fused_fwd_and_sparse_wgrad(signed):
         assert e_w < 2e-2 and e_g < 2e-2 and e_b < 2e-2, (e_w, e_g, e_b)
 
 
+@pytest.mark.parametrize("NB,B", [(4, 2), (128, 16)])
+def test_conv1_fwd_wave_tile_matches_pipe(NB, B):
+    """The wave-tile fused forward (k_conv1_fwd_w64: a wave owns all 64 channels of 15 columns, DPP pooling, packed
+    epilogue) computes every conv output with the same MFMA chains as the channel-split pipe kernel, so the pooled
+    bf16 outputs and the argmax bytes are bit-identical (random volumes, signed scales, per-client weights)."""
+    m = _m()
+    g = torch.Generator(device=DEV).manual_seed(5)
+    G = NB // B
+    x8 = torch.randint(0, 256, (NB, 61, 73, 61, 8), dtype=torch.uint8, device=DEV, generator=g)
+    idx = torch.randperm(NB, device=DEV, generator=g).int()
+    # packed weights: f16 bits of w in the 128-slot layout, the 3 empty slots zero
+    w = (torch.randn(G, 64, 128, device=DEV, generator=g) * 0.05).half()
+    w[:, :, 125:] = 0
+    w8 = w.view(torch.int16)
+    scale = torch.randn(G, 64, device=DEV, generator=g) * 0.02
+    shift = torch.randn(G, 64, device=DEV, generator=g)
+    outs = []
+    for mode in (0, 1):
+        p1 = torch.full((NB, 19, 23, 19, 64), float("nan"), device=DEV).bfloat16()
+        a1 = torch.full((NB, 19, 23, 19, 64), 255, dtype=torch.uint8, device=DEV)
+        m.conv1_fwd_mode(mode)
+        m.conv1_fwd_pool(x8.data_ptr(), idx.data_ptr(), w8.data_ptr(), scale.data_ptr(), shift.data_ptr(), NB, B,
+                         p1.data_ptr(), a1.data_ptr(), _st())
+        torch.cuda.synchronize()
+        outs.append((p1, a1))
+    m.conv1_fwd_mode(-1)
+    (p0, a0), (p1, a1) = outs
+    assert torch.isfinite(p1.float()).all() and int(a1.max()) < 27
+    assert torch.equal(p0.view(torch.int16), p1.view(torch.int16))
+    assert torch.equal(a0, a1)
+
+
 @pytest.mark.parametrize("mode", [1, 2])
 @pytest.mark.parametrize("NB,B", [(4, 2), (256, 16)])  # few samples (row / slab splits) and many
 def test_conv1_wgrad_smfmac_matches_valu_gather(NB, B, mode):
