@@ -662,7 +662,7 @@ __device__ __forceinline__ void pool3_dpp4(const float (&b)[4], float (&m)[4]) {
 // (v_perm / v_cndmask / v_mov of k-steps 2-3).  The A operand (64 x 128 f16) stays in 64 VGPRs.  Halo loads are
 // unconditional (columns >= 61 clamp to 60: they only feed conv columns >= 59, which no pooled cell reads) with a
 // scalar row base and a per-thread 32-bit offset; the max-pool starts from the first candidate pair instead of -inf.
-template <int PF>
+template <int PF, int RO>
 __global__ __launch_bounds__(256, 2) void k_conv1_fwd_w64(const uint8_t* __restrict__ x8, const int* __restrict__ idx,
                                                           const uint16_t* __restrict__ w8,
                                                           const float* __restrict__ scale,
@@ -736,11 +736,11 @@ __global__ __launch_bounds__(256, 2) void k_conv1_fwd_w64(const uint8_t* __restr
   }
   auto goff = [](int t) { return (((t / 9) * 5 + (t / 3) % 3) * HX + (t % 3)) * 8; };
   int toff[KS];
-  toff[0] = goff(kC1F2[0][fq]);
-  toff[1] = goff(kC1F2[0][4 + fq]);
-  toff[2] = goff(kC1D2[0][fq]);
+  toff[0] = goff(kC1F2[RO][fq]);
+  toff[1] = goff(kC1F2[RO][4 + fq]);
+  toff[2] = goff(kC1D2[RO][fq]);
   toff[3] = goff(kC1W[fq]);
-  const int gh = goff(kC1H2[0][fq]), gx1 = goff(kC1X1[fq]), gx2 = goff(kC1X2[fq]);
+  const int gh = goff(kC1H2[RO][fq]), gx1 = goff(kC1X1[fq]), gx2 = goff(kC1X2[fq]);
   const bool xsrc2 = fq == 2;
   const uint32_t xsel1 = fq == 0 ? 0x03020100u : fq == 3 ? 0x0c0c0100u : 0x05040100u;
   const uint32_t xsel2 = fq == 0 ? 0x03020100u : fq == 3 ? 0x0c0c0c0cu : 0x05040100u;
@@ -860,14 +860,19 @@ int conv1_fwd_variant() {
 void conv1_fwd_pool(uintptr_t x8, uintptr_t idx, uintptr_t w8, uintptr_t scale, uintptr_t shift, int NB, int B,
                     uintptr_t out, uintptr_t amax, uintptr_t stream) {
   NIDT_REQUIRE(NB % B == 0, "conv1_fwd_pool: NB % B");
-  if (conv1_fwd_variant() == 1 && conv1_kslots() == 128 && conv1_tapord() == 0) {
+  if (conv1_fwd_variant() == 1 && conv1_kslots() == 128) {
     static const int nq1 = [] {
       const char* e = getenv("NIDT_C1_NQ");
       return e ? std::max(1, std::min(kPH, atoi(e))) : 1;
     }();
-    hipLaunchKernelGGL((k_conv1_fwd_w64<2>), dim3(kPD * NB * nq1), dim3(256), 0, as_stream(stream),
-                       ptr<const uint8_t>(x8), ptr<const int>(idx), ptr<const uint16_t>(w8), ptr<const float>(scale),
-                       ptr<const float>(shift), B, ptr<uint16_t>(out), ptr<uint8_t>(amax), nq1);
+    if (conv1_tapord() == 1)
+      hipLaunchKernelGGL((k_conv1_fwd_w64<2, 1>), dim3(kPD * NB * nq1), dim3(256), 0, as_stream(stream),
+                         ptr<const uint8_t>(x8), ptr<const int>(idx), ptr<const uint16_t>(w8), ptr<const float>(scale),
+                         ptr<const float>(shift), B, ptr<uint16_t>(out), ptr<uint8_t>(amax), nq1);
+    else
+      hipLaunchKernelGGL((k_conv1_fwd_w64<2, 0>), dim3(kPD * NB * nq1), dim3(256), 0, as_stream(stream),
+                         ptr<const uint8_t>(x8), ptr<const int>(idx), ptr<const uint16_t>(w8), ptr<const float>(scale),
+                         ptr<const float>(shift), B, ptr<uint16_t>(out), ptr<uint8_t>(amax), nq1);
     NIDT_CHECK(hipGetLastError());
     return;
   }
