@@ -157,6 +157,8 @@ int conv1_wgrad_nq(int NB);
 int conv1_wgrad_mx_npb(int NB);
 void conv1_wgrad_mode(int mode);
 void conv1_fwd_mode(int mode);
+int gemm1x1_ok(int K, int N);
+void gemm1x1_g(uintptr_t x, uintptr_t w, uintptr_t y, int G, int64_t Mg, int K, int N, uintptr_t stream);
 int conv1_kslots();
 void conv1_wgrad(uintptr_t x8, uintptr_t idx, uintptr_t dp, uintptr_t pout, uintptr_t amax, int NB, int B,
                  uintptr_t part, uintptr_t w125, uintptr_t mu, uintptr_t covw, uintptr_t invstd, uintptr_t theta,
@@ -292,6 +294,8 @@ PYBIND11_MODULE(_nidt_hip, m) {
   DEF(conv1_wgrad_mx_npb);
   DEF(conv1_wgrad_mode);
   DEF(conv1_fwd_mode);
+  DEF(gemm1x1_ok);
+  DEF(gemm1x1_g);
   DEF(conv1_kslots);
   DEF(head);
   DEF(cls_head_train);

@@ -63,6 +63,23 @@ _SLAB_TABS = {}
 _BLAS_1X1 = os.environ.get("NIDT_R3D_BLAS", "0") == "1"
 
 
+# 1x1x1 stride-1 convs (forward, data gradient, and the stride-2 projection's half-resolution data gradient) on the
+# streaming per-client GEMM kernel gemm1x1.hip (K <= 512); NIDT_R3D_G1=0 keeps them on the general conv kernel (A/B)
+_G1 = os.environ.get("NIDT_R3D_G1", "1") != "0"
+
+
+def g1_gemm(x, w, out, G, K, N):
+    """out[g] = x[g] @ w[g]^T on channels-last rows with the hand-written streaming GEMM (``gemm1x1.hip``); False
+    (nothing launched) when the shape has no kernel (K >= 1024) or the switch is off."""
+    m = ops.ext()
+    if not _G1 or not m.gemm1x1_ok(K, N):
+        return False
+    Mg = x.numel() // (G * K)
+    assert x.numel() == G * Mg * K and out.numel() == G * Mg * N and x.is_contiguous() and out.is_contiguous()
+    m.gemm1x1_g(x.data_ptr(), w.data_ptr(), out.data_ptr(), G, Mg, K, N, _stream())
+    return True
+
+
 def gemm_1x1(x, w, out, G):
     """out[g] = x[g] @ w[g]^T for channels-last x [G*B, D, H, W, K] and a packed image w [G, N, 1, K] (bf16, fp32
     accumulation), written into out [G*B, D, H, W, N].  False (nothing launched) when an operand reaches 2^31 bytes."""
@@ -144,6 +161,8 @@ class GConv3:
             self.wt = (wt, G, theta.data_ptr()) if wt is not None else None
         wp = self.wp[0]
         y = torch.empty(N, Do, Ho, Wo, self.cout, device=x.device, dtype=torch.bfloat16)
+        if self.kt == 1 and self.stride == 1 and g1_gemm(x, wp, y, G, self.cin, self.cout):
+            return y
         if self.kt == 1 and self.stride == 1 and _BLAS_1X1 and gemm_1x1(x, wp, y, G):
             return y
         if self.kt == 27 and self.stride == 1 and slab_conv(x.data_ptr(), wp.data_ptr(), y.data_ptr(), G, N // G, D,
@@ -200,6 +219,8 @@ class GConv3:
         if self.stride == 1:
             dx = torch.empty(N, D, H, W, self.cin, device=x.device, dtype=torch.bfloat16)
             p2 = self.k - 1 - self.pad
+            if self.kt == 1 and g1_gemm(dy, wt, dx, G, self.cout, self.cin):
+                return dx
             if self.kt == 1 and _BLAS_1X1 and gemm_1x1(dy, wt, dx, G):
                 return dx
             if self.kt == 27 and slab_conv(dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), G, B, Do, Ho, Wo, self.cout,
@@ -218,6 +239,8 @@ class GConv3:
             return dx
         # 1x1 stride 2: the half-resolution W^T dY of the even voxels (res_grad_s2 adds it into the residual stream)
         sub = torch.empty(N, Do, Ho, Wo, self.cin, device=x.device, dtype=torch.bfloat16)
+        if g1_gemm(dy, wt, sub, G, self.cout, self.cin):
+            return sub
         if _BLAS_1X1 and gemm_1x1(dy, wt, sub, G):
             return sub
         conv_fwd(dy.data_ptr(), wt.data_ptr(), sub.data_ptr(), G, B, Do, Ho, Wo, self.cout, self.cin, 1, 1, 0, 0,

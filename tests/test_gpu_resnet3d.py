@@ -65,6 +65,54 @@ def test_gconv3_fwd_dgrad_wgrad(cin, cout, k, stride, dims):
     assert _rel(dx.permute(0, 4, 1, 2, 3), xr.grad) < 2e-2
 
 
+G1_SHAPES = [(64, 256), (64, 128), (64, 64), (128, 256), (128, 128), (128, 64), (256, 128), (256, 64), (512, 64),
+             (512, 128), (256, 1024)]
+
+
+@pytest.mark.parametrize("K,N", G1_SHAPES)
+def test_gemm1x1_matches_fp32(K, N):
+    """gemm1x1.hip (every tile configuration) against a per-client fp32 matmul of the same bf16 operands, with a
+    row count that leaves a partial last m-tile and blocks with different tile counts."""
+    from neuroimagedisttraining_amd import ops
+    dev = _dev()
+    m = ops.ext()
+    assert m.gemm1x1_ok(K, N)
+    torch.manual_seed(K + N)
+    G, Mg = 3, 2 * 64 * 9 + 37
+    x = torch.randn(G, Mg, K, device=dev).to(torch.bfloat16)
+    w = (torch.randn(G, N, K, device=dev) * K ** -0.5).to(torch.bfloat16)
+    y = torch.full((G, Mg, N), float("nan"), device=dev).to(torch.bfloat16)
+    m.gemm1x1_g(x.data_ptr(), w.data_ptr(), y.data_ptr(), G, Mg, K, N, torch.cuda.current_stream().cuda_stream)
+    ref = torch.bmm(x.float(), w.float().transpose(1, 2))
+    torch.cuda.synchronize()
+    assert torch.isfinite(y.float()).all()
+    assert _rel(y, ref) < 5e-3
+    assert float((y.float() - ref).abs().max()) <= 2 ** -7 * float(ref.abs().max())
+
+
+def test_gemm1x1_operand_above_2_31_elements():
+    """An X operand of more than 2^31 elements (64-bit client bases): the last client's last rows — the largest
+    offsets — against a chunked fp32 reference."""
+    from neuroimagedisttraining_amd import ops
+    dev = _dev()
+    m = ops.ext()
+    G, Mg, K, N = 32, 270001, 256, 64
+    assert G * Mg * K > 2 ** 31
+    gen = torch.Generator(device=dev).manual_seed(4)
+    x = torch.empty(G, Mg, K, device=dev, dtype=torch.bfloat16)
+    for g in range(G):  # chunked fill: no fp32 temporary of the whole operand
+        x[g].copy_(torch.randn(Mg, K, device=dev, generator=gen))
+    w = (torch.randn(G, N, K, device=dev, generator=gen) * K ** -0.5).to(torch.bfloat16)
+    y = torch.empty(G, Mg, N, device=dev, dtype=torch.bfloat16)
+    m.gemm1x1_g(x.data_ptr(), w.data_ptr(), y.data_ptr(), G, Mg, K, N, torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    for g, rows in ((G - 1, slice(Mg - 4096, Mg)), (G // 2, slice(0, 4096)), (0, slice(Mg - 100, Mg))):
+        ref = x[g, rows].float() @ w[g].float().t()
+        assert _rel(y[g, rows], ref) < 5e-3, g
+    del x, y
+    torch.cuda.empty_cache()
+
+
 @pytest.mark.parametrize("dims", [(9, 11, 9), (8, 10, 8)])
 def test_res_grad_s2_3d_matches_torch(dims):
     from neuroimagedisttraining_amd import ops
