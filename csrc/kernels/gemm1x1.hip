@@ -34,6 +34,18 @@ __device__ __forceinline__ void g1_wait_vm() {
   __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | ((N >> 4) << 14));
 }
 
+// The tile loop's VMEM traffic — the LDS-DMA of X / W and the Y stores — is issued from inline asm, invisible to the
+// compiler's waitcnt pass, and ordered only by the kernel's own counted waits (g1_wait_vm): with the intrinsic DMA
+// and plain stores the pass put a vmcnt(1) at the head of every tile (wait for every VMEM op but the DMA just issued,
+// i.e. the next tile's DMA and the previous tile's stores), which left one tile in flight and cut the K = 64, N = 256
+// shape to ~3 TB/s.  No other code in the kernel uses M0 (the DMA's LDS base).
+template <class T>
+__device__ __forceinline__ void g1_dma16(i32x4_t rsrc, int voffset, T* lds_wave_base) {
+  const uint32_t m0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) T*)lds_wave_base;
+  asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds" ::"s"(m0), "v"(voffset), "s"(rsrc)
+               : "memory");
+}
+
 template <int BN, int NKC, int BM>
 __global__ __launch_bounds__(512, 1) void k_gemm1x1(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w,
                                                      uint16_t* __restrict__ y, int G, int Mg, int N, int nNT,
@@ -73,7 +85,7 @@ __global__ __launch_bounds__(512, 1) void k_gemm1x1(const uint16_t* __restrict__
   for (int i = 0; i < NIW; ++i) {
     const int j = wid * NIW + i, kc = j / (BN / 8), rg = j % (BN / 8);
     const int r = rg * 8 + lrow;
-    blds16(rw, ((n0 + r) * K + kc * 64 + ((slot ^ swz_g1(r)) << 3)) * 2, sW + kc * BN * 64 + rg * 512);
+    g1_dma16(rw, ((n0 + r) * K + kc * 64 + ((slot ^ swz_g1(r)) << 3)) * 2, sW + kc * BN * 64 + rg * 512);
   }
   // X stage of m-tile t into stage array sb
   auto issue_x = [&](int t, uint16_t* sb) {
@@ -83,7 +95,7 @@ __global__ __launch_bounds__(512, 1) void k_gemm1x1(const uint16_t* __restrict__
       const int j = wid * NIX + i, kc = j / (BM / 8), rg = j % (BM / 8);
       const int r = rg * 8 + lrow;
       const int m = m0 + r;
-      blds16(rx, m < Mg ? (m * K + kc * 64 + ((slot ^ swz_g1(r)) << 3)) * 2 : kBufOOB, sb + kc * BM * 64 + rg * 512);
+      g1_dma16(rx, m < Mg ? (m * K + kc * 64 + ((slot ^ swz_g1(r)) << 3)) * 2 : kBufOOB, sb + kc * BM * 64 + rg * 512);
     }
   };
   // every tile issues the DMA of tile t + 2, past the block's last tile as all-out-of-range loads (zeros, no HBM
@@ -131,8 +143,10 @@ __global__ __launch_bounds__(512, 1) void k_gemm1x1(const uint16_t* __restrict__
         uint16_t* yp = y + ((int64_t)g * Mg + m) * N + n0 + wn * WN + 4 * fq;
 #pragma unroll
         for (int i = 0; i < NSUB; ++i)
-          *reinterpret_cast<uint2*>(yp + 16 * i) =
-              make_uint2(pack_bf16x2(acc[i][j][0], acc[i][j][1]), pack_bf16x2(acc[i][j][2], acc[i][j][3]));
+        {
+          const uint2 v = make_uint2(pack_bf16x2(acc[i][j][0], acc[i][j][1]), pack_bf16x2(acc[i][j][2], acc[i][j][3]));
+          asm volatile("global_store_dwordx2 %0, %1, off" ::"v"(yp + 16 * i), "v"(v) : "memory");
+        }
       }
     }
     // stage t + 1 landed (younger: the stage t + 2 DMA and this tile's stores; only the client's partial last m-tile,

@@ -40,40 +40,47 @@ __device__ __forceinline__ int find_layer(const PackDesc* d, int n, int b, int g
 // rows per block of the 1x1 grid: about 8 K elements per block (host twin: resnet2d_hip.WeightPacker)
 __host__ __device__ constexpr int pack1_rows(int cin_p) { return cin_p >= 8192 ? 1 : 8192 / cin_p; }
 
-// plain: block (layer row co, client g); the fp32 source row [cin_src][kt] is staged in LDS
+// plain: block (layer row co, 64-channel chunk, client g).  The chunk's fp32 source [64 ci][kt] (contiguous in the
+// PyTorch row) is staged in LDS and written as kt runs of 64 image channels (16-B stores).  The round-4 kernel staged
+// a whole row per block (kt x Cin x 4 B: 55 KB for a 512-channel 3x3x3 layer), which held it to two blocks per CU and
+// ~1.2 TB/s (7.2 ms per config-5 pack); 64-channel chunks need 7 KB (kt = 27) and give Cout x Cin/64 blocks per layer.
+constexpr int kPackCC = 64;
 __global__ __launch_bounds__(256) void k_pack_plain(const PackDesc* __restrict__ desc, int nd,
                                                     const float* __restrict__ theta, int64_t ldt, int G,
                                                     uint16_t* __restrict__ out) {
-  extern __shared__ float row[];
+  extern __shared__ float row[];  // [kPackCC][kt]
   const int li = find_layer(desc, nd, blockIdx.x, 0);
   const PackDesc& d = desc[li];
-  const int co = blockIdx.x - d.blk_plain, g = blockIdx.y;
-  const int Cin = d.cin_p, kt = d.kt, K = kt * Cin, Ks = kt * d.cin_src;
-  const float* src = theta + (int64_t)g * ldt + d.src_off + (int64_t)co * Ks;
-  if ((reinterpret_cast<uintptr_t>(src) & 15) == 0 && Ks % 4 == 0) {  // 16-B source loads
-    for (int e = 4 * threadIdx.x; e < Ks; e += 4 * 256)
+  const int Cin = d.cin_p, kt = d.kt, cs = d.cin_src, K = kt * Cin;
+  const int nch = (Cin + kPackCC - 1) / kPackCC;
+  const int b = blockIdx.x - d.blk_plain, co = b / nch, ci0 = (b - co * nch) * kPackCC, g = blockIdx.y;
+  const int cw = min(kPackCC, Cin - ci0);          // image channels of this chunk
+  const int cc = max(0, min(kPackCC, cs - ci0));   // source channels of this chunk
+  const int n = cc * kt;
+  const float* src = theta + (int64_t)g * ldt + d.src_off + ((int64_t)co * cs + ci0) * kt;
+  if ((reinterpret_cast<uintptr_t>(src) & 15) == 0 && n % 4 == 0) {  // 16-B source loads
+    for (int e = 4 * threadIdx.x; e < n; e += 4 * 256)
       *reinterpret_cast<float4*>(row + e) = *reinterpret_cast<const float4*>(src + e);
   } else {
-    for (int e = threadIdx.x; e < Ks; e += 256) row[e] = src[e];
+    for (int e = threadIdx.x; e < n; e += 256) row[e] = src[e];
   }
   __syncthreads();
-  uint16_t* dst = out + d.wp_off + ((int64_t)g * d.cout + co) * K;
+  uint16_t* dst = out + d.wp_off + ((int64_t)g * d.cout + co) * K + ci0;
   if (Cin % 8 == 0 && (d.wp_off & 7) == 0) {  // 16-B stores: 8 channels of one tap per lane
-    for (int e = 8 * threadIdx.x; e < K; e += 8 * 256) {
-      const int t = e / Cin, ci = e - t * Cin;
+    const int nq = cw / 8;
+    for (int e = threadIdx.x; e < kt * nq; e += 256) {
+      const int t = e / nq, c = (e - t * nq) * 8;
       float v[8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = ci + j < d.cin_src ? row[(ci + j) * kt + t] : 0.f;
-      *reinterpret_cast<uint4*>(dst + e) = make_uint4(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]),
-                                                      pack_bf16x2(v[4], v[5]), pack_bf16x2(v[6], v[7]));
+      for (int j = 0; j < 8; ++j) v[j] = c + j < cc ? row[(c + j) * kt + t] : 0.f;
+      *reinterpret_cast<uint4*>(dst + (int64_t)t * Cin + c) = make_uint4(
+          pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]), pack_bf16x2(v[4], v[5]), pack_bf16x2(v[6], v[7]));
     }
     return;
   }
-  for (int e = 2 * threadIdx.x; e < K; e += 2 * 256) {  // e, e+1: same tap (Cin even)
-    const int t = e / Cin, ci = e - t * Cin;
-    const float a = ci < d.cin_src ? row[ci * kt + t] : 0.f;
-    const float b = ci + 1 < d.cin_src ? row[(ci + 1) * kt + t] : 0.f;
-    *reinterpret_cast<uint32_t*>(dst + e) = pack_bf16x2(a, b);
+  for (int e = threadIdx.x; e < kt * cw; e += 256) {
+    const int t = e / cw, c = e - t * cw;
+    dst[(int64_t)t * Cin + c] = f32_to_bf16(c < cc ? row[c * kt + t] : 0.f);
   }
 }
 
@@ -146,8 +153,8 @@ __global__ __launch_bounds__(256) void k_pack_trans(const PackDesc* __restrict__
     *reinterpret_cast<uint4*>(wt + ((int64_t)ci * kt + s) * Cout + co) = make_uint4(w[0], w[1], w[2], w[3]);
   }
 }
-// desc: device table of nd PackDesc; nplain / nplain1 / ntrans: total blocks of the three grids; lds: bytes for the
-// largest row of the per-row plain grid (max kt * cin_src * 4 over its layers)
+// desc: device table of nd PackDesc; nplain / nplain1 / ntrans: total blocks of the three grids (the plain grid has
+// Cout x ceil(Cin_p / 64) blocks per layer); lds: bytes of one plain-grid chunk (64 x max kt x 4 over its layers)
 void pack_convs(uintptr_t desc, int nd, int nplain, int nplain1, int ntrans, int lds, uintptr_t theta, int64_t ldt,
                 int G, uintptr_t out, uintptr_t stream) {
   NIDT_REQUIRE(nd > 0 && G > 0 && lds > 0 && lds <= 160 * 1024 && nplain >= 0 && nplain1 >= 0,
@@ -172,5 +179,6 @@ void pack_convs(uintptr_t desc, int nd, int nplain, int nplain1, int ntrans, int
 
 int pack_desc_bytes() { return (int)sizeof(PackDesc); }
 int pack1_rows_host(int cin_p) { return pack1_rows(cin_p); }
+int pack_plain_chunks(int cin_p) { return (cin_p + kPackCC - 1) / kPackCC; }
 
 }  // namespace nidt

@@ -65,6 +65,40 @@ def test_gconv3_fwd_dgrad_wgrad(cin, cout, k, stride, dims):
     assert _rel(dx.permute(0, 4, 1, 2, 3), xr.grad) < 2e-2
 
 
+def test_weight_packer_images_exact():
+    """pack.hip (chunked plain grid, 1x1 grid, transpose grid) for a mix of layers — 3x3x3 at 64/192/512 input
+    channels (one, three, eight 64-channel chunks), a channel-padded 2-D stem (cin 3 -> 64), 3x3 and 1x1 — against the
+    permuted fp32 rows rounded to bf16, bit for bit; the dgrad image with the taps in each layer's slot order."""
+    from neuroimagedisttraining_amd.engine.resnet2d_hip import GroupedConv, WeightPacker
+    from neuroimagedisttraining_amd.engine.resnet3d_hip import GConv3
+    dev = _dev()
+    specs = [("3", 128, 64, 3, 1), ("3", 64, 192, 3, 1), ("3", 64, 512, 3, 2), ("3", 256, 128, 1, 1),
+             ("2", 64, 3, 3, 1), ("2", 128, 64, 3, 2), ("2", 128, 64, 1, 2)]
+    convs, off = [], 0
+    for kind, cout, cin, k, st in specs:
+        c = GConv3(off, cout, cin, k, st, (k - 1) // 2) if kind == "3" else \
+            GroupedConv(off, cout, cin, k, st, (k - 1) // 2, True)
+        convs.append(c)
+        off += c.numel + 3  # unaligned layer offsets exercise the scalar source path
+    G = 3
+    theta = torch.randn(G, off + 64, device=dev)[:, :off]
+    pk = WeightPacker(convs, dev)
+    pk.pack(theta, G, True)
+    torch.cuda.synchronize()
+    for c in convs:
+        w = theta[:, c.off:c.off + c.numel].reshape(G, c.cout, c.cin, c.kt)
+        ref = torch.zeros(G, c.cout, c.kt, c.cin_p, device=dev)
+        ref[..., :c.cin] = w.permute(0, 1, 3, 2)
+        ref = ref.to(torch.bfloat16)
+        assert torch.equal(c.wp[0].view(torch.int16), ref.view(torch.int16)), (c.cout, c.cin, c.kt)
+        if c.wt is not None:
+            slots = list(c.slots)
+            rt = torch.empty(G, c.cin_p, c.kt, c.cout, device=dev, dtype=torch.bfloat16)
+            for t in range(c.kt):
+                rt[:, :, slots[t], :] = ref[:, :, t, :].transpose(1, 2)
+            assert torch.equal(c.wt[0].view(torch.int16), rt.view(torch.int16)), (c.cout, c.cin, c.kt)
+
+
 G1_SHAPES = [(64, 256), (64, 128), (64, 64), (128, 256), (128, 128), (128, 64), (256, 128), (256, 64), (512, 64),
              (512, 128), (256, 1024)]
 
