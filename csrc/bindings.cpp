@@ -159,6 +159,11 @@ int conv1_wgrad_mx_npb(int NB);
 void conv1_wgrad_mode(int mode);
 void conv1_fwd_mode(int mode);
 int gemm1x1_ok(int K, int N);
+void conv2d_any_fwd(uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t y, int G, int B, int H, int W, int cin, int cs,
+                    int cout, int k, int pad, uintptr_t stream);
+int conv2d_any_wgrad_chunks(int B, int Ho, int Wo);
+void conv2d_any_wgrad(uintptr_t x, uintptr_t dy, uintptr_t part, int G, int B, int H, int W, int cin, int cs, int cout,
+                      int k, int pad, uintptr_t stream);
 void gemm1x1_g(uintptr_t x, uintptr_t w, uintptr_t y, int G, int64_t Mg, int K, int N, uintptr_t stream);
 int conv1_kslots();
 void conv1_wgrad(uintptr_t x8, uintptr_t idx, uintptr_t dp, uintptr_t pout, uintptr_t amax, int NB, int B,
@@ -297,6 +302,9 @@ PYBIND11_MODULE(_nidt_hip, m) {
   DEF(conv1_wgrad_mode);
   DEF(conv1_fwd_mode);
   DEF(gemm1x1_ok);
+  DEF(conv2d_any_fwd);
+  DEF(conv2d_any_wgrad_chunks);
+  DEF(conv2d_any_wgrad);
   DEF(gemm1x1_g);
   DEF(conv1_kslots);
   DEF(head);

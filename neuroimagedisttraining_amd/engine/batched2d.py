@@ -19,6 +19,8 @@ from __future__ import annotations
 import torch
 import torch.nn.functional as F
 
+import os
+
 from .flat import ParamLayout
 from .resnet2d_hip import AUG_PAD
 
@@ -94,6 +96,20 @@ class BatchedModuleEngine:
         self._shift = (-torch.tensor(mean, dtype=torch.float32, device=self.device)
                        / torch.tensor(std, dtype=torch.float32, device=self.device)).view(1, c, 1, 1)
         self._opt = None
+        # GPU: the hand-written grouped layers (conv2d_hip.py: conv2d_any.hip convolutions, batched GEMM linears,
+        # grouped GroupNorm) over group-stacked tensors instead of vmapped library convolutions; NIDT_B2D_HIP=0 keeps
+        # the vmap path (the CPU always uses it)
+        self._grouped = None
+        if self.device.type == "cuda" and os.environ.get("NIDT_B2D_HIP", "1") != "0":
+            from . import conv2d_hip
+            if conv2d_hip.supports(self.model):
+                from .. import ops
+                ops.ext()  # fail loudly without the extension
+                self._grouped = conv2d_hip.grouped_model(self.model)
+
+    @property
+    def uses_hip_layers(self):
+        return self._grouped is not None
 
     @property
     def input_shape(self):
@@ -111,6 +127,47 @@ class BatchedModuleEngine:
     def _params(self, theta, G):
         return {n: theta[:G, o:o + self.players.numel(i)].view((G,) + tuple(self.players.shapes[i]))
                 for i, (n, o) in enumerate(zip(self.players.names, self.players.offsets))}
+
+    def _grouped_forward(self, theta, G, x):
+        """Group-stacked forward through the grouped twins (``x`` [G*B, C, H, W]); the parameter views of theta's
+        rows are leaves when ``theta`` requires no grad, returned for the caller's backward."""
+        gm, grp = self._grouped
+        grp.G = G
+        grp.params = {n: theta[:G, o:o + self.players.numel(i)].view((G,) + tuple(self.players.shapes[i]))
+                      for i, (n, o) in enumerate(zip(self.players.names, self.players.offsets))}
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=self.amp):
+            out = gm(x.contiguous(memory_format=torch.channels_last))
+        out = out[0] if isinstance(out, (list, tuple)) else out
+        return out.float(), grp.params
+
+    def _grouped_train(self, theta, grads, x, y, G, B, keep):
+        gm, grp = self._grouped
+        gm.train(True)
+        if keep >= 1.0:
+            for mod in gm.modules():
+                if isinstance(mod, torch.nn.Dropout):
+                    mod.eval()
+        leaves = theta.detach()
+        gm_params = {}
+        for i, (n, o) in enumerate(zip(self.players.names, self.players.offsets)):
+            gm_params[n] = leaves[:G, o:o + self.players.numel(i)].view((G,) + tuple(self.players.shapes[i])) \
+                .requires_grad_(True)
+        grp.G, grp.params = G, gm_params
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=self.amp):
+            out = gm(x.reshape((G * B,) + self.input_shape).contiguous(memory_format=torch.channels_last))
+        out = (out[0] if isinstance(out, (list, tuple)) else out).float().view(G, B, -1)
+        if out.shape[-1] == 1:
+            loss = F.binary_cross_entropy_with_logits(out.view(G, B), y.float(), reduction="none").mean(1)
+        else:
+            loss = F.cross_entropy(out.reshape(G * B, -1), y.long().reshape(-1), reduction="none").view(G, B).mean(1)
+        names = list(gm_params)
+        gs = torch.autograd.grad(loss.sum(), [gm_params[n] for n in names])
+        with torch.no_grad():
+            for n, gr in zip(names, gs):
+                i = self.players.names.index(n)
+                o, k = self.players.offsets[i], self.players.numel(i)
+                grads[:G, o:o + k].copy_(gr.reshape(G, k))
+        return loss.detach()
 
     def _forward_fn(self):
         from torch.func import functional_call
@@ -132,6 +189,8 @@ class BatchedModuleEngine:
             aug = aug_draws_t(seed_dev.to(torch.int64).view(()) + int(seed), cl, B)
         x = self._input(idx, aug).view((G, B) + self.input_shape)
         y = self.labels.index_select(0, idx.long()).view(G, B)
+        if self._grouped is not None:
+            return self._grouped_train(theta, grads, x, y, G, B, keep)
         fwd = self._forward_fn()
         self.model.train(True)
         if keep >= 1.0:
@@ -154,6 +213,11 @@ class BatchedModuleEngine:
 
     def eval_logits(self, theta, bufs, idx, G, B):
         from torch.func import vmap
+        if self._grouped is not None:
+            self._grouped[0].eval()
+            with torch.no_grad():
+                out, _ = self._grouped_forward(theta, G, self._input(idx))
+            return out.reshape(G * B, -1)
         self.model.eval()
         with torch.no_grad():
             x = self._input(idx).view((G, B) + self.input_shape)
