@@ -100,13 +100,14 @@ def test_batched2d_hip_layers_match_vmap_and_issue_no_library_conv(name, ds, mon
     y = torch.randint(0, 10, (G * B,))
     mean, std = ((0.1307,), (0.3081,)) if c == 1 else (CIFAR_MEAN, CIFAR_STD)
     out = {}
+    flat = torch.cat([p.detach().reshape(-1) for p in model.parameters()]).cuda()
+    rows = flat.expand(G, -1) + torch.randn(G, flat.numel(), device="cuda") * 0.01  # one draw for both paths
     for hip in ("1", "0"):
         monkeypatch.setenv("NIDT_B2D_HIP", hip)
         eng = BatchedModuleEngine(create_model(name, dataset=ds, class_num=10), x8, y, "cuda", mean, std)
         assert eng.uses_hip_layers == (hip == "1")
         theta = padded_rows(G, eng.players.total, "cuda")
-        theta.copy_(torch.cat([p.detach().reshape(-1) for p in model.parameters()]).cuda().expand(G, -1))
-        theta.add_(torch.randn_like(theta) * 0.01)
+        theta.copy_(rows)
         grads = padded_rows(G, eng.players.total, "cuda")
         idx = torch.arange(G * B, dtype=torch.int32, device="cuda")
         if hip == "1":

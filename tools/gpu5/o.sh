@@ -1,0 +1,13 @@
+#!/bin/bash
+set -o pipefail
+export PYTHONUNBUFFERED=1
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+OUT=gpurun_out/r5o; mkdir -p $OUT
+timeout -k 10 500 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_gpu_batched2d.py tests/test_gpu_cli.py > $OUT/t.txt 2>&1 || { grep -E "PASS|FAIL|Error|assert|error" $OUT/t.txt | tail -40; exit 1; }
+grep -E "passed|failed" $OUT/t.txt | tail -1
+timeout -k 10 300 python -u tools/bench_cifar.py --algorithm subavg --rounds 3 --warmup 1 > $OUT/subavg.txt 2>&1 || { tail -20 $OUT/subavg.txt; exit 1; }
+grep -E "^round|^warmup" $OUT/subavg.txt; tail -1 $OUT/subavg.txt | cut -c1-300
+timeout -k 10 400 rocprofv3 --kernel-trace -d /tmp/cifarprof -o run -- python3 -u tools/bench_cifar.py --algorithm subavg --rounds 2 --warmup 1 > $OUT/subavg_prof.txt 2>&1 || { tail -20 $OUT/subavg_prof.txt; exit 1; }
+db=$(find /tmp/cifarprof -name "*.db" | head -1)
+python3 tools/prof_summary.py "$db" $OUT/subavg_round_kernels.txt --top 45 --window-ms 1500 > /dev/null 2>&1
+head -40 $OUT/subavg_round_kernels.txt | cut -c1-140; grep TIMELINE $OUT/subavg_round_kernels.txt
