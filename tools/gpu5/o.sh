@@ -11,3 +11,9 @@ timeout -k 10 400 rocprofv3 --kernel-trace -d /tmp/cifarprof -o run -- python3 -
 db=$(find /tmp/cifarprof -name "*.db" | head -1)
 python3 tools/prof_summary.py "$db" $OUT/subavg_round_kernels.txt --top 45 --window-ms 1500 > /dev/null 2>&1
 head -40 $OUT/subavg_round_kernels.txt | cut -c1-140; grep TIMELINE $OUT/subavg_round_kernels.txt
+timeout -k 10 400 python -u tools/bench_cifar.py --algorithm dispfl --rounds 1 --warmup 1 > $OUT/dispfl.txt 2>&1 || { tail -20 $OUT/dispfl.txt; exit 1; }
+grep -E "^round|^warmup" $OUT/dispfl.txt; tail -1 $OUT/dispfl.txt | cut -c1-300
+timeout -k 10 500 rocprofv3 --kernel-trace -d /tmp/dprof -o run -- python3 -u tools/bench_cifar.py --algorithm dispfl --rounds 1 --warmup 1 > $OUT/dispfl_prof.txt 2>&1 || { tail -20 $OUT/dispfl_prof.txt; exit 1; }
+db=$(find /tmp/dprof -name "*.db" | head -1)
+python3 tools/prof_summary.py "$db" $OUT/dispfl_round_kernels.txt --top 45 --window-ms 4500 > /dev/null 2>&1
+head -30 $OUT/dispfl_round_kernels.txt | cut -c1-140; grep -E "TIMELINE|GAP" $OUT/dispfl_round_kernels.txt
