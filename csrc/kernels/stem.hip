@@ -262,11 +262,23 @@ __global__ void k_stem_pool(StemDims d, const uint16_t* __restrict__ y, const fl
       best[q] = -INFINITY;
       arg[q] = 0;
     }
+    // all 27 window loads are issued before the max (clamped addresses + a validity mask; the round-4 loop's
+    // per-voxel bounds `continue` made them 27 dependent round trips: 2.2 ms per config-5 step)
+    uint4 raw[27];
+    uint32_t valid = 0;
+    const uint16_t* yn = y + (int64_t)n * d.OD * d.OH * d.OW * kSC + cg * 8;
+#pragma unroll
     for (int a = 0; a < 27; ++a) {
       const int zd = 2 * pz - 1 + a / 9, zh = 2 * py - 1 + (a / 3) % 3, zw = 2 * px - 1 + a % 3;
-      if (zd < 0 || zd >= d.OD || zh < 0 || zh >= d.OH || zw < 0 || zw >= d.OW) continue;
-      const uint4 raw = *reinterpret_cast<const uint4*>(y + ((((int64_t)n * d.OD + zd) * d.OH + zh) * d.OW + zw) * kSC + cg * 8);
-      const uint32_t u[4] = {raw.x, raw.y, raw.z, raw.w};
+      const bool ok = zd >= 0 && zd < d.OD && zh >= 0 && zh < d.OH && zw >= 0 && zw < d.OW;
+      valid |= (uint32_t)ok << a;
+      const int cd = min(max(zd, 0), d.OD - 1), ch = min(max(zh, 0), d.OH - 1), cw = min(max(zw, 0), d.OW - 1);
+      raw[a] = *reinterpret_cast<const uint4*>(yn + (((int64_t)cd * d.OH + ch) * d.OW + cw) * kSC);
+    }
+#pragma unroll
+    for (int a = 0; a < 27; ++a) {
+      if (!((valid >> a) & 1u)) continue;
+      const uint32_t u[4] = {raw[a].x, raw[a].y, raw[a].z, raw[a].w};
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
         const float yv = __uint_as_float((q & 1) ? (u[q >> 1] & 0xffff0000u) : (u[q >> 1] << 16));
@@ -306,31 +318,39 @@ __global__ __launch_bounds__(256) void k_stem_unpool(StemDims d, const uint16_t*
     float dv[8];
 #pragma unroll
     for (int q = 0; q < 8; ++q) dv[q] = 0.f;
-    for (int qd = qd0; qd <= qd1 && qd < d.QD; ++qd) {
-      const int ad = od - (2 * qd - 1);
-      for (int qh = oh >> 1; qh <= ((oh + 1) >> 1) && qh < d.QH; ++qh) {
-        const int ah = oh - (2 * qh - 1);
-        for (int qw = ow >> 1; qw <= ((ow + 1) >> 1) && qw < d.QW; ++qw) {
-          const int aw = ow - (2 * qw - 1);
-          const int a = ad * 9 + ah * 3 + aw;
-          const int64_t qo = ((((int64_t)n * d.QD + qd) * d.QH + qh) * d.QW + qw) * kSC + cg * 8;
-          const uint2 am = *reinterpret_cast<const uint2*>(amax + qo);
-          const uint4 gr = *reinterpret_cast<const uint4*>(dpool + qo);  // bf16 (the engine's residual stream)
-          const uint32_t gu[4] = {gr.x, gr.y, gr.z, gr.w};
-          float gv[8];
-#pragma unroll
-          for (int q = 0; q < 8; ++q)
-            gv[q] = __uint_as_float((q & 1) ? (gu[q >> 1] & 0xffff0000u) : (gu[q >> 1] << 16));
-#pragma unroll
-          for (int q = 0; q < 8; ++q) {
-            const int aq = (int)(((q < 4 ? am.x : am.y) >> (8 * (q & 3))) & 0xffu);
-            if (aq == a) dv[q] += gv[q];
-          }
-        }
-      }
-    }
+    // the (<= 8) pooling windows containing this voxel: windows qd in {od >> 1, (od + 1) >> 1} (one when od is even),
+    // likewise qh, qw; their argmax bytes and gradients are loaded before any is used (clamped addresses, validity
+    // bits) instead of one dependent round trip per window, and summed in the round-4 loop's (qd, qh, qw) order
+    const int qh0 = oh >> 1, qh1 = (oh + 1) >> 1, qw0 = ow >> 1, qw1 = (ow + 1) >> 1;
     const int64_t yo = ((((int64_t)n * d.OD + od) * d.OH + oh) * d.OW + ow) * kSC + cg * 8;
     const uint4 raw = *reinterpret_cast<const uint4*>(y + yo);
+    uint2 am[8];
+    uint4 gr[8];
+    uint32_t wvalid = 0;
+#pragma unroll
+    for (int w8 = 0; w8 < 8; ++w8) {
+      const int qd = (w8 & 4) ? qd1 : qd0, qh = (w8 & 2) ? qh1 : qh0, qw = (w8 & 1) ? qw1 : qw0;
+      const bool ok = ((w8 & 4) == 0 || qd1 != qd0) && ((w8 & 2) == 0 || qh1 != qh0) && ((w8 & 1) == 0 || qw1 != qw0) &&
+                      qd < d.QD && qh < d.QH && qw < d.QW;
+      wvalid |= (uint32_t)ok << w8;
+      const int64_t qo = ((((int64_t)n * d.QD + min(qd, d.QD - 1)) * d.QH + min(qh, d.QH - 1)) * d.QW +
+                          min(qw, d.QW - 1)) * kSC + cg * 8;
+      am[w8] = *reinterpret_cast<const uint2*>(amax + qo);
+      gr[w8] = *reinterpret_cast<const uint4*>(dpool + qo);  // bf16 (the engine's residual stream)
+    }
+#pragma unroll
+    for (int w8 = 0; w8 < 8; ++w8) {
+      if (!((wvalid >> w8) & 1u)) continue;
+      const int qd = (w8 & 4) ? qd1 : qd0, qh = (w8 & 2) ? qh1 : qh0, qw = (w8 & 1) ? qw1 : qw0;
+      const int a = (od - (2 * qd - 1)) * 9 + (oh - (2 * qh - 1)) * 3 + (ow - (2 * qw - 1));
+      const uint32_t gu[4] = {gr[w8].x, gr[w8].y, gr[w8].z, gr[w8].w};
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const float gv = __uint_as_float((q & 1) ? (gu[q >> 1] & 0xffff0000u) : (gu[q >> 1] << 16));
+        const int aq = (int)(((q < 4 ? am[w8].x : am[w8].y) >> (8 * (q & 3))) & 0xffu);
+        if (aq == a) dv[q] += gv;
+      }
+    }
     const uint32_t u[4] = {raw.x, raw.y, raw.z, raw.w};
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
