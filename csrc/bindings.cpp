@@ -108,7 +108,8 @@ void img_input(uintptr_t src, uintptr_t idx, uintptr_t out, int N, int H, int W,
 void pack_convs(uintptr_t desc, int nd, int nplain, int nplain1, int ntrans, int lds, uintptr_t theta, int64_t ldt,
                 int G, uintptr_t out, uintptr_t stream);
 int pack1_rows_host(int cin_p);
-int pack_plain_chunks(int cin_p);
+int pack_plain_chunks(int cin_p, int kt);
+int pack_plain_lds(int cin_p, int kt);
 int pack_desc_bytes();
 // conv3d.hip (sub-pixel stride-2 data gradient)
 void conv_dgrad_s2_g(uintptr_t dy, uintptr_t w, uintptr_t dx, int G, int B, int D, int H, int W, int Cin, int Cout,
@@ -278,6 +279,7 @@ PYBIND11_MODULE(_nidt_hip, m) {
   DEF(pack_convs);
   DEF(pack1_rows_host);
   DEF(pack_plain_chunks);
+  DEF(pack_plain_lds);
   DEF(pack_desc_bytes);
   DEF(conv_dgrad_s2_g);
   DEF(conv_tap_slots);

@@ -40,22 +40,28 @@ __device__ __forceinline__ int find_layer(const PackDesc* d, int n, int b, int g
 // rows per block of the 1x1 grid: about 8 K elements per block (host twin: resnet2d_hip.WeightPacker)
 __host__ __device__ constexpr int pack1_rows(int cin_p) { return cin_p >= 8192 ? 1 : 8192 / cin_p; }
 
-// plain: block (layer row co, 64-channel chunk, client g).  The chunk's fp32 source [64 ci][kt] (contiguous in the
-// PyTorch row) is staged in LDS and written as kt runs of 64 image channels (16-B stores).  The round-4 kernel staged
+// plain: block (layer row co, channel chunk of pack_cc channels, client g).  The chunk's fp32 source [cc][kt]
+// (contiguous in the PyTorch row) is staged in LDS and written as kt runs of image channels (16-B stores).  The round-4 kernel staged
 // a whole row per block (kt x Cin x 4 B: 55 KB for a 512-channel 3x3x3 layer), which held it to two blocks per CU and
 // ~1.2 TB/s (7.2 ms per config-5 pack); 64-channel chunks need 7 KB (kt = 27) and give Cout x Cin/64 blocks per layer.
-constexpr int kPackCC = 64;
+// chunk width: as many 64-channel groups as keep the staged chunk within 8 K floats (32 KB), at least one — whole
+// rows for the 3x3 layers of the 2-D ResNet (a 64-channel chunk there is 2.3 KB, and the 4096 blocks per 512x512
+// layer per client made the pack 5x slower than the per-row kernel), 256 channels for a 512-channel 3x3x3 layer
+__host__ __device__ inline int pack_cc(int cin_p, int kt) {
+  const int cc = ((8192 / kt) / 64) * 64;
+  return cc < 64 ? 64 : (cc > cin_p ? cin_p : cc);
+}
 __global__ __launch_bounds__(256) void k_pack_plain(const PackDesc* __restrict__ desc, int nd,
                                                     const float* __restrict__ theta, int64_t ldt, int G,
                                                     uint16_t* __restrict__ out) {
-  extern __shared__ float row[];  // [kPackCC][kt]
+  extern __shared__ float row[];  // [CC][kt]
   const int li = find_layer(desc, nd, blockIdx.x, 0);
   const PackDesc& d = desc[li];
   const int Cin = d.cin_p, kt = d.kt, cs = d.cin_src, K = kt * Cin;
-  const int nch = (Cin + kPackCC - 1) / kPackCC;
-  const int b = blockIdx.x - d.blk_plain, co = b / nch, ci0 = (b - co * nch) * kPackCC, g = blockIdx.y;
-  const int cw = min(kPackCC, Cin - ci0);          // image channels of this chunk
-  const int cc = max(0, min(kPackCC, cs - ci0));   // source channels of this chunk
+  const int CC = pack_cc(Cin, kt), nch = (Cin + CC - 1) / CC;
+  const int b = blockIdx.x - d.blk_plain, co = b / nch, ci0 = (b - co * nch) * CC, g = blockIdx.y;
+  const int cw = min(CC, Cin - ci0);          // image channels of this chunk
+  const int cc = max(0, min(CC, cs - ci0));   // source channels of this chunk
   const int n = cc * kt;
   const float* src = theta + (int64_t)g * ldt + d.src_off + ((int64_t)co * cs + ci0) * kt;
   if ((reinterpret_cast<uintptr_t>(src) & 15) == 0 && n % 4 == 0) {  // 16-B source loads
@@ -179,6 +185,7 @@ void pack_convs(uintptr_t desc, int nd, int nplain, int nplain1, int ntrans, int
 
 int pack_desc_bytes() { return (int)sizeof(PackDesc); }
 int pack1_rows_host(int cin_p) { return pack1_rows(cin_p); }
-int pack_plain_chunks(int cin_p) { return (cin_p + kPackCC - 1) / kPackCC; }
+int pack_plain_chunks(int cin_p, int kt) { const int cc = pack_cc(cin_p, kt); return (cin_p + cc - 1) / cc; }
+int pack_plain_lds(int cin_p, int kt) { return pack_cc(cin_p, kt) * kt * 4; }
 
 }  // namespace nidt

@@ -181,7 +181,7 @@ class HipAlexNet3D:
             dd["blk_plain"], dd["blk_t"], dd["blk_plain1"] = nplain, ntrans, 0
             dd["slot"][:] = np.arange(26, -1, -1)  # stride 1: the flipped kernel
             n = G * cout * 27 * cin
-            dd["wp_off"], off, nplain = off, off + n, nplain + cout * self.m.pack_plain_chunks(cin)
+            dd["wp_off"], off, nplain = off, off + n, nplain + cout * self.m.pack_plain_chunks(cin, 27)
             vt = None
             if train:
                 dd["wt_off"], vt, off = off, off, off + n
@@ -195,7 +195,7 @@ class HipAlexNet3D:
             b["w%dp" % ci] = buf[op:op + n].view(G, cout, 27, cin)
             if ot is not None:
                 b["w%dt" % ci] = buf[ot:ot + n].view(G, cin, 27, cout)
-        lds = 64 * 27 * 4  # one 64-channel chunk of a 3x3x3 row (pack.hip k_pack_plain)
+        lds = max(self.m.pack_plain_lds(L[2], 27) for L in (L2, L3, L4, L5))  # one channel chunk of a 3x3x3 row
         b["bpack"] = (torch.from_numpy(desc.view(np.uint8).copy()).to(self.dev), nplain, ntrans, lds, buf)
 
     def _conv(self, b, key, x, w, bias, y, stats, G, B, D, H, W, cin, cout, pad, st, theta=None, ci=None):

@@ -351,7 +351,7 @@ class WeightPacker:
                 rows = m.pack1_rows_host(c.cin_p)
                 nplain1 += (c.cout + rows - 1) // rows
             else:
-                nplain += c.cout * m.pack_plain_chunks(c.cin_p)
+                nplain += c.cout * m.pack_plain_chunks(c.cin_p, c.kt)
             n_img = G * c.cout * c.kt * c.cin_p
             d["wp_off"] = off
             vp = (off, (G, c.cout, c.kt, c.cin_p))
@@ -367,7 +367,8 @@ class WeightPacker:
                 d["wt_off"] = -1
             d["slot"][:c.kt] = c.slots
             views.append((vp, vt))
-        lds = max([64 * c.kt * 4 for c in self.convs if not (_PACK1 and c.kt == 1 and c.cin_p % 8 == 0)] + [4])
+        lds = max([m.pack_plain_lds(c.cin_p, c.kt) for c in self.convs
+                   if not (_PACK1 and c.kt == 1 and c.cin_p % 8 == 0)] + [4])
         buf = torch.empty(max(1, off), dtype=torch.bfloat16, device=self.device)
         tab = torch.from_numpy(desc.view(np.uint8).copy()).to(self.device)
         plan = (tab, (nplain, nplain1), ntrans, lds, buf, views)
