@@ -262,28 +262,34 @@ __global__ void k_stem_pool(StemDims d, const uint16_t* __restrict__ y, const fl
       best[q] = -INFINITY;
       arg[q] = 0;
     }
-    // all 27 window loads are issued before the max (clamped addresses + a validity mask; the round-4 loop's
-    // per-voxel bounds `continue` made them 27 dependent round trips: 2.2 ms per config-5 step)
-    uint4 raw[27];
-    uint32_t valid = 0;
+    // the window's 9 voxels of one depth plane are loaded before their max (clamped addresses + a validity mask): the
+    // round-4 loop's per-voxel bounds `continue` made the 27 loads dependent round trips; all 27 at once held 108
+    // VGPRs and ran slower (5.5 vs 2.2 ms per config-5 step)
     const uint16_t* yn = y + (int64_t)n * d.OD * d.OH * d.OW * kSC + cg * 8;
+    for (int kd = 0; kd < 3; ++kd) {
+      const int zd = 2 * pz - 1 + kd;
+      if (zd < 0 || zd >= d.OD) continue;
+      uint4 raw[9];
+      uint32_t valid = 0;
 #pragma unroll
-    for (int a = 0; a < 27; ++a) {
-      const int zd = 2 * pz - 1 + a / 9, zh = 2 * py - 1 + (a / 3) % 3, zw = 2 * px - 1 + a % 3;
-      const bool ok = zd >= 0 && zd < d.OD && zh >= 0 && zh < d.OH && zw >= 0 && zw < d.OW;
-      valid |= (uint32_t)ok << a;
-      const int cd = min(max(zd, 0), d.OD - 1), ch = min(max(zh, 0), d.OH - 1), cw = min(max(zw, 0), d.OW - 1);
-      raw[a] = *reinterpret_cast<const uint4*>(yn + (((int64_t)cd * d.OH + ch) * d.OW + cw) * kSC);
-    }
+      for (int a9 = 0; a9 < 9; ++a9) {
+        const int zh = 2 * py - 1 + a9 / 3, zw = 2 * px - 1 + a9 % 3;
+        const bool ok = zh >= 0 && zh < d.OH && zw >= 0 && zw < d.OW;
+        valid |= (uint32_t)ok << a9;
+        const int ch = min(max(zh, 0), d.OH - 1), cw = min(max(zw, 0), d.OW - 1);
+        raw[a9] = *reinterpret_cast<const uint4*>(yn + (((int64_t)zd * d.OH + ch) * d.OW + cw) * kSC);
+      }
 #pragma unroll
-    for (int a = 0; a < 27; ++a) {
-      if (!((valid >> a) & 1u)) continue;
-      const uint32_t u[4] = {raw[a].x, raw[a].y, raw[a].z, raw[a].w};
+      for (int a9 = 0; a9 < 9; ++a9) {
+        if (!((valid >> a9) & 1u)) continue;
+        const int a = kd * 9 + a9;
+        const uint32_t u[4] = {raw[a9].x, raw[a9].y, raw[a9].z, raw[a9].w};
 #pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const float yv = __uint_as_float((q & 1) ? (u[q >> 1] & 0xffff0000u) : (u[q >> 1] << 16));
-        const float z = fmaxf(fmaf(yv, sc[q], sf[q]), 0.f);
-        if (z > best[q]) { best[q] = z; arg[q] = a; }
+        for (int q = 0; q < 8; ++q) {
+          const float yv = __uint_as_float((q & 1) ? (u[q >> 1] & 0xffff0000u) : (u[q >> 1] << 16));
+          const float z = fmaxf(fmaf(yv, sc[q], sf[q]), 0.f);
+          if (z > best[q]) { best[q] = z; arg[q] = a; }
+        }
       }
     }
     const int64_t o = e * 8;
