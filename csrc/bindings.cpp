@@ -165,7 +165,11 @@ void conv2d_any_fwd(uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t y, int G
 int conv2d_any_wgrad_chunks(int B, int Ho, int Wo);
 void conv2d_any_wgrad(uintptr_t x, uintptr_t dy, uintptr_t part, int G, int B, int H, int W, int cin, int cs, int cout,
                       int k, int pad, uintptr_t stream);
-void gemm1x1_g(uintptr_t x, uintptr_t w, uintptr_t y, int G, int64_t Mg, int K, int N, uintptr_t stream);
+int gemm1x1_chunks(int G, int64_t Mg, int K, int N);
+void gemm1x1_g(uintptr_t x, uintptr_t w, uintptr_t y, int G, int64_t Mg, int K, int N, uintptr_t part,
+               uintptr_t stream);
+void bnr_finalize_part(uintptr_t part, int nchunk, int G, int64_t M, int C, float eps, float mom, uintptr_t stats,
+                       uintptr_t bufs, int64_t ldb, int64_t off_rm, int64_t off_rv, int64_t off_nbt, uintptr_t stream);
 int conv1_kslots();
 void conv1_wgrad(uintptr_t x8, uintptr_t idx, uintptr_t dp, uintptr_t pout, uintptr_t amax, int NB, int B,
                  uintptr_t part, uintptr_t w125, uintptr_t mu, uintptr_t covw, uintptr_t invstd, uintptr_t theta,
@@ -308,6 +312,8 @@ PYBIND11_MODULE(_nidt_hip, m) {
   DEF(conv2d_any_wgrad_chunks);
   DEF(conv2d_any_wgrad);
   DEF(gemm1x1_g);
+  DEF(gemm1x1_chunks);
+  DEF(bnr_finalize_part);
   DEF(conv1_kslots);
   DEF(head);
   DEF(cls_head_train);

@@ -304,6 +304,17 @@ void bnr_stats(uintptr_t t, int G, int64_t M, int C, float eps, float mom, uintp
   NIDT_CHECK(hipGetLastError());
 }
 
+// training-mode statistics from precomputed chunk partials part [nchunk][G][C][2] (e.g. gemm1x1.hip's [STATS]
+// epilogue) -> stats [G][C][2] (+ running stats); the k_bnr_partial pass over t is skipped
+void bnr_finalize_part(uintptr_t part, int nchunk, int G, int64_t M, int C, float eps, float mom, uintptr_t stats,
+                       uintptr_t bufs, int64_t ldb, int64_t off_rm, int64_t off_rv, int64_t off_nbt, uintptr_t stream) {
+  bnr_check(G, M, C, "bnr_finalize_part");
+  NIDT_REQUIRE(nchunk > 0, "bnr_finalize_part: nchunk");
+  hipLaunchKernelGGL(k_bnr_finalize, dim3(G), dim3(256), 0, as_stream(stream), ptr<const float>(part), nchunk, G, C,
+                     (int)M, eps, mom, ptr<float>(stats), ptr<float>(bufs), ldb, off_rm, off_rv, off_nbt);
+  NIDT_CHECK(hipGetLastError());
+}
+
 void bnr_eval_stats(int G, int C, float eps, uintptr_t bufs, int64_t ldb, int64_t off_rm, int64_t off_rv,
                     uintptr_t stats, uintptr_t stream) {
   hipLaunchKernelGGL(k_bnr_eval_stats, dim3(G), dim3(256), 0, as_stream(stream), G, C, eps, ptr<const float>(bufs), ldb,

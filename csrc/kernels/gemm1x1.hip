@@ -46,10 +46,14 @@ __device__ __forceinline__ void g1_dma16(i32x4_t rsrc, int voffset, T* lds_wave_
                : "memory");
 }
 
-template <int BN, int NKC, int BM>
+// [STATS] the following BatchNorm's training statistics from the epilogue: per-lane sums of the stored (bf16)
+// outputs and their squares over every row the block writes, reduced over the 16 row lanes (DPP/shuffle) and the two
+// m-half waves (LDS) into part[mb][g][N][2] = the chunk partials of bnr.hip's k_bnr_finalize (nchunk = nMB), which
+// replaces that layer's k_bnr_partial pass over the whole output (a 2.33 GB read per layer-1 conv3 at config 5)
+template <int BN, int NKC, int BM, bool STATS>
 __global__ __launch_bounds__(512, 1) void k_gemm1x1(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w,
                                                      uint16_t* __restrict__ y, int G, int Mg, int N, int nNT,
-                                                     int nMB) {
+                                                     int nMB, float* __restrict__ part) {
   constexpr int K = 64 * NKC;
   constexpr int W_ELEMS = NKC * BN * 64, X_ELEMS = NKC * BM * 64;
   constexpr int NIW = NKC * BN / 64;           // weight DMA instructions per wave
@@ -77,7 +81,16 @@ __global__ __launch_bounds__(512, 1) void k_gemm1x1(const uint16_t* __restrict__
   const int wn = wid & 3, wm = wid >> 2;
   const int lrow = lane >> 3, slot = lane & 7;
 
-  if (T == 0) return;  // block-uniform
+  if (T == 0) {  // block-uniform
+    if (STATS)
+      for (int c = tid; c < 2 * BN; c += 512) part[(((int64_t)mb * G + g) * N + n0) * 2 + c] = 0.f;
+    return;
+  }
+  float s1[NSUB][4], s2[NSUB][4];
+#pragma unroll
+  for (int i = 0; i < NSUB; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) s1[i][r] = s2[i][r] = 0.f;
   const i32x4_t rx = make_rsrc(x + (int64_t)g * Mg * K, (uint32_t)Mg * K * 2);
   const i32x4_t rw = make_rsrc(w + (int64_t)g * N * K, (uint32_t)N * K * 2);
   // weight tile: instruction j = (k chunk, 8-row group) of [NKC][BN][64]
@@ -146,6 +159,15 @@ __global__ __launch_bounds__(512, 1) void k_gemm1x1(const uint16_t* __restrict__
         {
           const uint2 v = make_uint2(pack_bf16x2(acc[i][j][0], acc[i][j][1]), pack_bf16x2(acc[i][j][2], acc[i][j][3]));
           asm volatile("global_store_dwordx2 %0, %1, off" ::"v"(yp + 16 * i), "v"(v) : "memory");
+          if (STATS) {
+            const float q[4] = {__uint_as_float(v.x << 16), __uint_as_float(v.x & 0xffff0000u),
+                                __uint_as_float(v.y << 16), __uint_as_float(v.y & 0xffff0000u)};
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              s1[i][r] += q[r];
+              s2[i][r] = fmaf(q[r], q[r], s2[i][r]);
+            }
+          }
         }
       }
     }
@@ -162,6 +184,31 @@ __global__ __launch_bounds__(512, 1) void k_gemm1x1(const uint16_t* __restrict__
   }
   if (t < T) tile(t, sX0, sX2);
   if (t + 1 < T) tile(t + 1, sX1, sX0);
+  if (STATS) {
+#pragma unroll
+    for (int i = 0; i < NSUB; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+          s1[i][r] += __shfl_xor(s1[i][r], o, 64);
+          s2[i][r] += __shfl_xor(s2[i][r], o, 64);
+        }
+    float* red = reinterpret_cast<float*>(sX0);  // [2 m halves][BN][2]; every wave is past the last tile's barrier
+    if (fr == 0) {
+#pragma unroll
+      for (int i = 0; i < NSUB; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int c = wn * WN + 16 * i + 4 * fq + r;
+          red[(wm * BN + c) * 2] = s1[i][r];
+          red[(wm * BN + c) * 2 + 1] = s2[i][r];
+        }
+    }
+    __syncthreads();
+    for (int c = tid; c < 2 * BN; c += 512)
+      part[(((int64_t)mb * G + g) * N + n0) * 2 + c] = red[c] + red[2 * BN + c];
+  }
 }
 
 // (BN, NKC, BM) of a (K, N) shape, or 0 when the weight tile does not fit (K >= 1024: the general conv kernel)
@@ -181,23 +228,37 @@ int gemm1x1_ok(int K, int N) {
   return g1_cfg(K, N, BN, NKC, BM);
 }
 
-void gemm1x1_g(uintptr_t x, uintptr_t w, uintptr_t y, int G, int64_t Mg, int K, int N, uintptr_t stream) {
+// m-tile groups per (client, n-tile): about two blocks per CU in all (one resident per CU at the large LDS
+// configs) — enough tiles per block to keep the DMA ring full, enough blocks to fill the 256 CUs.  Also the chunk
+// count of the [STATS] partials.
+int gemm1x1_chunks(int G, int64_t Mg, int K, int N) {
+  int BN, NKC, BM;
+  NIDT_REQUIRE(g1_cfg(K, N, BN, NKC, BM), "gemm1x1_chunks: unsupported (K, N)");
+  const int nNT = N / BN;
+  const int nmt = (int)((Mg + BM - 1) / BM);
+  const int target = 512;
+  return std::max(1, std::min(nmt, (target + G * nNT - 1) / (G * nNT)));
+}
+
+// part: 0, or [gemm1x1_chunks][G][N][2] fp32 BatchNorm partial sums of the output (see [STATS])
+void gemm1x1_g(uintptr_t x, uintptr_t w, uintptr_t y, int G, int64_t Mg, int K, int N, uintptr_t part,
+               uintptr_t stream) {
   int BN, NKC, BM;
   NIDT_REQUIRE(g1_cfg(K, N, BN, NKC, BM), "gemm1x1_g: unsupported (K, N)");
   NIDT_REQUIRE(Mg > 0 && Mg * K * 2 < (int64_t(1) << 31) && Mg * N * 2 < (int64_t(1) << 31),
                "gemm1x1_g: a client's rows must stay below 2 GB (32-bit in-client offsets)");
   const int nNT = N / BN;
-  const int nmt = (int)((Mg + BM - 1) / BM);
-  // about two blocks per CU in all (one resident per CU at the large LDS configs): enough tiles per block to
-  // keep the DMA ring full, enough blocks to fill the 256 CUs
-  const int target = 512;
-  const int nMB = std::max(1, std::min(nmt, (target + G * nNT - 1) / (G * nNT)));
+  const int nMB = gemm1x1_chunks(G, Mg, K, N);
   const dim3 grid(G * nNT * nMB), block(512);
   hipStream_t s = as_stream(stream);
 #define G1(BN_, NKC_, BM_)                                                                                     \
   if (BN == BN_ && NKC == NKC_ && BM == BM_) {                                                                 \
-    hipLaunchKernelGGL((k_gemm1x1<BN_, NKC_, BM_>), grid, block, 0, s, ptr<const uint16_t>(x),                 \
-                       ptr<const uint16_t>(w), ptr<uint16_t>(y), G, (int)Mg, N, nNT, nMB);                      \
+    if (part)                                                                                                  \
+      hipLaunchKernelGGL((k_gemm1x1<BN_, NKC_, BM_, true>), grid, block, 0, s, ptr<const uint16_t>(x),         \
+                         ptr<const uint16_t>(w), ptr<uint16_t>(y), G, (int)Mg, N, nNT, nMB, ptr<float>(part)); \
+    else                                                                                                       \
+      hipLaunchKernelGGL((k_gemm1x1<BN_, NKC_, BM_, false>), grid, block, 0, s, ptr<const uint16_t>(x),        \
+                         ptr<const uint16_t>(w), ptr<uint16_t>(y), G, (int)Mg, N, nNT, nMB, nullptr);          \
     NIDT_CHECK(hipGetLastError());                                                                             \
     return;                                                                                                    \
   }

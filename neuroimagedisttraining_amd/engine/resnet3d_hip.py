@@ -68,16 +68,27 @@ _BLAS_1X1 = os.environ.get("NIDT_R3D_BLAS", "0") == "1"
 _G1 = os.environ.get("NIDT_R3D_G1", "1") != "0"
 
 
-def g1_gemm(x, w, out, G, K, N):
+# NIDT_R3D_G1STATS=0: the following BatchNorm reads its training statistics in a pass of its own (k_bnr_partial)
+# instead of from the GEMM epilogue (A/B)
+_G1STATS = os.environ.get("NIDT_R3D_G1STATS", "1") != "0"
+
+
+def g1_gemm(x, w, out, G, K, N, stats=False):
     """out[g] = x[g] @ w[g]^T on channels-last rows with the hand-written streaming GEMM (``gemm1x1.hip``); False
-    (nothing launched) when the shape has no kernel (K >= 1024) or the switch is off."""
+    (nothing launched) when the shape has no kernel (K >= 1024) or the switch is off.  ``stats``: also the BatchNorm
+    chunk partials of ``out`` (returned as ``(part, nchunk)`` instead of True)."""
     m = ops.ext()
     if not _G1 or not m.gemm1x1_ok(K, N):
         return False
     Mg = x.numel() // (G * K)
     assert x.numel() == G * Mg * K and out.numel() == G * Mg * N and x.is_contiguous() and out.is_contiguous()
-    m.gemm1x1_g(x.data_ptr(), w.data_ptr(), out.data_ptr(), G, Mg, K, N, _stream())
-    return True
+    part = None
+    if stats and _G1STATS:
+        nch = m.gemm1x1_chunks(G, Mg, K, N)
+        part = (torch.empty(nch, G, N, 2, device=x.device, dtype=torch.float32), nch)
+    m.gemm1x1_g(x.data_ptr(), w.data_ptr(), out.data_ptr(), G, Mg, K, N, part[0].data_ptr() if part else 0,
+                _stream())
+    return part if part else True
 
 
 def gemm_1x1(x, w, out, G):
@@ -127,6 +138,13 @@ class GConv3:
         self.slots = list(ops.ext().conv_tap_slots(self.kt, stride)) if hip else None
         self.wp = self.wt = None
         self._ptabs = {}
+        self._part = None  # BatchNorm partials of the last forward output (fwd(stats=True) on the GEMM path)
+
+    def take_part(self):
+        """The BatchNorm chunk partials of the last ``fwd(stats=True)`` output, or None (then the BN computes its
+        own); cleared by the call."""
+        p, self._part = self._part, None
+        return p
 
     def out_dims(self, d, h, w):
         f = lambda n: (n + 2 * self.pad - self.k) // self.stride + 1  # noqa: E731
@@ -149,7 +167,8 @@ class GConv3:
                      padding=self.pad, groups=G)
         return y.view(B, G, self.cout, *y.shape[2:]).permute(1, 0, 3, 4, 5, 2).reshape(N, *y.shape[2:], self.cout)
 
-    def fwd(self, x, theta, G, train=False, packed=False):
+    def fwd(self, x, theta, G, train=False, packed=False, stats=False):
+        self._part = None
         N, D, H, W, C = x.shape
         if not self.hip:  # CPU twin (its BN output may be a permuted view)
             return self._torch_fwd(x, theta[:, self.off:self.off + self.numel], G)
@@ -161,8 +180,11 @@ class GConv3:
             self.wt = (wt, G, theta.data_ptr()) if wt is not None else None
         wp = self.wp[0]
         y = torch.empty(N, Do, Ho, Wo, self.cout, device=x.device, dtype=torch.bfloat16)
-        if self.kt == 1 and self.stride == 1 and g1_gemm(x, wp, y, G, self.cin, self.cout):
-            return y
+        if self.kt == 1 and self.stride == 1:
+            r = g1_gemm(x, wp, y, G, self.cin, self.cout, stats=stats)
+            if r is not False:
+                self._part = r if isinstance(r, tuple) else None
+                return y
         if self.kt == 1 and self.stride == 1 and _BLAS_1X1 and gemm_1x1(x, wp, y, G):
             return y
         if self.kt == 27 and self.stride == 1 and slab_conv(x.data_ptr(), wp.data_ptr(), y.data_ptr(), G, N // G, D,
@@ -283,14 +305,20 @@ class GBN3:
             y = torch.relu(y)
         return y.to(t.dtype), torch.stack([mean, rstd], -1)
 
-    def fwd(self, t, theta, bufs, G, train, res=None, relu=False):
+    def fwd(self, t, theta, bufs, G, train, res=None, relu=False, part=None):
+        """``part``: (chunk partials [n][G][C][2], n) of ``t`` computed by the producing GEMM's epilogue (training
+        mode): only the finalize runs, no statistics pass over ``t``."""
         if not self.hip:
             return self._torch_fwd(t, theta, bufs, G, train, res, relu)
         m, st = ops.ext(), _stream()
         N = t.shape[0]
         M = t.numel() // (self.C * G)
         stats = torch.empty(G, self.C, 2, device=t.device, dtype=torch.float32)
-        if train:
+        if train and part is not None:
+            m.bnr_finalize_part(part[0].data_ptr(), part[1], G, M, self.C, BN_EPS, BN_MOM, stats.data_ptr(),
+                                bufs.data_ptr() if bufs is not None else 0, bufs.stride(0) if bufs is not None else 0,
+                                self.off_rm, self.off_rv, self.off_nbt, st)
+        elif train:
             ws = torch.empty(m.bnr_workspace(G, M, self.C), device=t.device, dtype=torch.float32)
             m.bnr_stats(t.data_ptr(), G, M, self.C, BN_EPS, BN_MOM, ws.data_ptr(), stats.data_ptr(),
                         bufs.data_ptr() if bufs is not None else 0, bufs.stride(0) if bufs is not None else 0,
@@ -488,17 +516,19 @@ class GroupedResNet3D:
         saved = []
         for blk in self.blocks:
             xin = a
-            t1 = blk["c1"].fwd(xin, theta, G, train, packed)
-            h1, s1 = blk["n1"].fwd(t1, theta, bufs, G, train, relu=True)
+            # the 1x1x1 GEMMs hand their outputs' BatchNorm partials to the next BN (training mode)
+            t1 = blk["c1"].fwd(xin, theta, G, train, packed, stats=train)
+            h1, s1 = blk["n1"].fwd(t1, theta, bufs, G, train, relu=True, part=blk["c1"].take_part())
             t2 = blk["c2"].fwd(h1, theta, G, train, packed)
             h2, s2 = blk["n2"].fwd(t2, theta, bufs, G, train, relu=True)
-            t3 = blk["c3"].fwd(h2, theta, G, train, packed)
+            t3 = blk["c3"].fwd(h2, theta, G, train, packed, stats=train)
+            p3 = blk["c3"].take_part()
             if "cd" in blk:
-                td = blk["cd"].fwd(xin, theta, G, train, packed)
-                yd, sd = blk["nd"].fwd(td, theta, bufs, G, train)
+                td = blk["cd"].fwd(xin, theta, G, train, packed, stats=train)
+                yd, sd = blk["nd"].fwd(td, theta, bufs, G, train, part=blk["cd"].take_part())
             else:
                 td, sd, yd = None, None, xin
-            a, s3 = blk["n3"].fwd(t3, theta, bufs, G, train, res=yd, relu=True)
+            a, s3 = blk["n3"].fwd(t3, theta, bufs, G, train, res=yd, relu=True, part=p3)
             if train:
                 saved.append((xin, t1, s1, h1, t2, s2, h2, t3, s3, td, sd, a))
         N = a.shape[0]

@@ -116,12 +116,23 @@ def test_gemm1x1_matches_fp32(K, N):
     x = torch.randn(G, Mg, K, device=dev).to(torch.bfloat16)
     w = (torch.randn(G, N, K, device=dev) * K ** -0.5).to(torch.bfloat16)
     y = torch.full((G, Mg, N), float("nan"), device=dev).to(torch.bfloat16)
-    m.gemm1x1_g(x.data_ptr(), w.data_ptr(), y.data_ptr(), G, Mg, K, N, torch.cuda.current_stream().cuda_stream)
+    nch = m.gemm1x1_chunks(G, Mg, K, N)
+    part = torch.full((nch, G, N, 2), float("nan"), device=dev)
+    m.gemm1x1_g(x.data_ptr(), w.data_ptr(), y.data_ptr(), G, Mg, K, N, part.data_ptr(),
+                torch.cuda.current_stream().cuda_stream)
     ref = torch.bmm(x.float(), w.float().transpose(1, 2))
     torch.cuda.synchronize()
     assert torch.isfinite(y.float()).all()
     assert _rel(y, ref) < 5e-3
     assert float((y.float() - ref).abs().max()) <= 2 ** -7 * float(ref.abs().max())
+    # [STATS] epilogue: per-client channel sums of the stored bf16 outputs and of their squares
+    ps = part.double().sum(0)
+    yf = y.double()
+    assert _rel(ps[..., 0], yf.sum(1)) < 1e-5 and _rel(ps[..., 1], (yf * yf).sum(1)) < 1e-5
+    y2 = torch.empty_like(y)
+    m.gemm1x1_g(x.data_ptr(), w.data_ptr(), y2.data_ptr(), G, Mg, K, N, 0, torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    assert torch.equal(y2.view(torch.int16), y.view(torch.int16))  # the statistics do not change the output
 
 
 def test_gemm1x1_operand_above_2_31_elements():
@@ -138,7 +149,7 @@ def test_gemm1x1_operand_above_2_31_elements():
         x[g].copy_(torch.randn(Mg, K, device=dev, generator=gen))
     w = (torch.randn(G, N, K, device=dev, generator=gen) * K ** -0.5).to(torch.bfloat16)
     y = torch.empty(G, Mg, N, device=dev, dtype=torch.bfloat16)
-    m.gemm1x1_g(x.data_ptr(), w.data_ptr(), y.data_ptr(), G, Mg, K, N, torch.cuda.current_stream().cuda_stream)
+    m.gemm1x1_g(x.data_ptr(), w.data_ptr(), y.data_ptr(), G, Mg, K, N, 0, torch.cuda.current_stream().cuda_stream)
     torch.cuda.synchronize()
     for g, rows in ((G - 1, slice(Mg - 4096, Mg)), (G // 2, slice(0, 4096)), (0, slice(Mg - 100, Mg))):
         ref = x[g, rows].float() @ w[g].float().t()

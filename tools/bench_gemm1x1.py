@@ -44,7 +44,7 @@ def main():
                                             st))
         line = "K=%4d N=%4d Mg=%6d  conv_fwd_g %7.3f ms" % (K, N, Mg, t_old)
         if m.gemm1x1_ok(K, N):
-            t_new = timeit(lambda: m.gemm1x1_g(x.data_ptr(), w.data_ptr(), y.data_ptr(), G, Mg, K, N, st))
+            t_new = timeit(lambda: m.gemm1x1_g(x.data_ptr(), w.data_ptr(), y.data_ptr(), G, Mg, K, N, 0, st))
             gb = G * Mg * (K + N) * 2 / 1e9
             tf = 2.0 * G * Mg * K * N / 1e12
             err = float((y.float() - y2.float()).norm() / y2.float().norm())
