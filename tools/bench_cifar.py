@@ -130,6 +130,7 @@ def main():
             "warmup": args.warmup, "s_per_round": round(dt / args.rounds, 3), "dtype": "bf16",
             "data": "synthetic", "setup_s": round(t_setup, 1), "warmup_round_s": [round(w, 2) for w in walls],
             "s_round_each": [round(w, 3) for w in each], "graph_stats": dict(getattr(runner, "graph_stats", {})),
+            "phase_s_total": {k: round(v, 3) for k, v in runner.timers.items()},
             "reference_v100": ({"bound": bound[0] + str(bound[1]), "source": bound[2],
                                 "vs_bound": round(value / bound[1], 1)} if (bound and not tiny) else None),
             "config": {"model": "resnet18 (GroupNorm32)", "clients": args.clients, "frac": args.frac,
