@@ -56,6 +56,7 @@ struct ConvFwdArgs {
   // 2oh + bit1(poff), 2ow + bit0(poff)) of the [Dx][Hx][Wx] output (positions outside are skipped)
   int nph = 0, Dx = 0, Hx = 0, Wx = 0;
   unsigned char pnt[8] = {0}, pt0[8] = {0}, poff[8] = {0}, ptap[28] = {0};
+  int dbg = 0;          // timing diagnostics only (NIDT_SLAB_DBG): 1 = k_conv_fwd_slab keeps its first union
 };
 
 constexpr int kFwdBP = 128;  // positions per block
@@ -878,7 +879,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void k_conv_fwd_slab(ConvFwdArgs a
     if (NA == 3 && ks + 2 < nks) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(A_INSTR) : "memory");
     else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    if (t == 8 && ql + 1 < nq) {  // every wave is done with this slab's union: reload it for the next one
+    if (t == 8 && ql + 1 < nq && a.dbg != 1) {  // every wave is done with this slab's union: reload it for the next one
       issue_u(q0 + ql + 1);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
@@ -1612,6 +1613,11 @@ static void fwd_slab_impl(uintptr_t x, uintptr_t w, uintptr_t bias, int64_t bias
   a.nPB = ceil_div(a.Mg, 256);
   a.G = G;
   a.bias_ld = bias_ld;
+  static const int slab_dbg = [] {  // timing diagnostics only (wrong results): NIDT_SLAB_DBG=1 skips union reloads
+    const char* e = getenv("NIDT_SLAB_DBG");
+    return e ? atoi(e) : 0;
+  }();
+  a.dbg = slab_dbg;
   const int bco = fwd_bco(Cout), nCO = Cout / bco;
   const dim3 grid((unsigned)((int64_t)a.nPB * nCO * G));
   hipStream_t s = as_stream(stream);
@@ -2020,6 +2026,12 @@ struct ConvWgDmaArgs {
   float* part;          // [nsplit, G, Cout, K]
   int D, H, W, Cin, Cout, Mg, K, nsplit, chunk, G, nKT, nCT;
   int64_t xclient;      // elements per client in x (B*D*H*W*Cin)
+  // nsplit == 1: the epilogue writes the PyTorch-layout gradient rows itself (grad[g][off + (co*Cin + ci)*kt + t],
+  // times scale) and k_wgrad_reduce is skipped; null -> fp32 slabs into part
+  float* grad;
+  int64_t ldg, off;
+  float scale;
+  int kt;
 };
 
 __global__ void k_conv_pos_table(int2* tab, int Mg, int D, int H, int W, int Do, int Ho, int Wo, int st, int padd,
@@ -2159,6 +2171,21 @@ __global__ __launch_bounds__(256 * NCH, 2 / NCH) void k_conv_wgrad_dma(ConvWgDma
 #undef WD_ISSUE
 #undef WD_FETCH
   const int fr = lane & 15, fq = lane >> 4;
+  if (a.grad) {  // single split: final layout straight from the accumulators (this wave's group is one tap)
+    float* out = a.grad + (int64_t)g * a.ldg + a.off + (int64_t)(co0 + 64 * wc) * a.K;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int k = kc0 + 64 * wk + 16 * j + fr;
+      if (k < a.K) {
+        const int dk = (k - gtap * Cin) * a.kt + gtap;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) out[(int64_t)(16 * i + 4 * fq + r) * a.K + dk] = acc[i][j][r] * a.scale;
+      }
+    }
+    return;
+  }
   float* out = a.part + (((int64_t)sp * a.G + g) * a.Cout + co0 + 64 * wc) * a.K;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
@@ -2837,6 +2864,7 @@ static void conv_wgrad_impl(uintptr_t x, uintptr_t xs, uintptr_t xt, uintptr_t d
   a.nsplit = nsplit;
   a.chunk = ((ceil_div(a.Mg, nsplit) + 31) / 32) * 32;
   hipStream_t s = as_stream(stream);
+  bool direct = false;
   if (ptab && !xs) {
     ConvWgDmaArgs d;
     d.x = a.x; d.dy = a.dy; d.ptab = ptr<const int2>(ptab); d.part = a.part;
@@ -2852,6 +2880,15 @@ static void conv_wgrad_impl(uintptr_t x, uintptr_t xs, uintptr_t xt, uintptr_t d
     const int nch = (Cout % 128 == 0 && nch_env == 2) ? 2 : 1;
     d.nKT = ceil_div(a.K, kWgKC); d.nCT = Cout / (kWgCO * nch);
     d.xclient = (int64_t)B * D * H * W * Cin;
+    // [WG-DIRECT] one split: the kernel writes the gradient rows (no fp32 slab round trip, no reduce launch).
+    // NIDT_WG_DIRECT=0 keeps slab + k_wgrad_reduce (A/B; the results are bitwise equal)
+    static const int direct_env = [] {
+      const char* e = getenv("NIDT_WG_DIRECT");
+      return e ? atoi(e) : 1;
+    }();
+    direct = direct_env && nsplit == 1;
+    d.grad = direct ? ptr<float>(grad) : nullptr;
+    d.ldg = ldg; d.off = off; d.scale = scale; d.kt = kt;
     NIDT_REQUIRE(d.xclient * 2 < (1ll << 31) && (int64_t)a.Mg * Cout * 2 < (1ll << 31),
                  "conv3d_wgrad: per-client tensors must stay below 2 GiB (32-bit buffer offsets)");
     const int64_t nwg = (int64_t)d.nKT * d.nCT * nsplit * G;
@@ -2876,6 +2913,7 @@ static void conv_wgrad_impl(uintptr_t x, uintptr_t xs, uintptr_t xt, uintptr_t d
     else hipLaunchKernelGGL((k_conv_wgrad<false>), grid, dim3(256), 0, s, a);
   }
   NIDT_CHECK(hipGetLastError());
+  if (direct) return;
   hipLaunchKernelGGL(k_wgrad_reduce, dim3(Cout, G), dim3(256), kt * (Cin + 1) * sizeof(float), s,
                      ptr<const float>(part), nsplit, G, Cout, Cin, kt,
                      ptr<float>(grad), ldg, off, scale);

@@ -16,6 +16,10 @@ __device__ int nidt_raw_buffer_load_i32(i32x4_t rsrc, int voffset, int soffset, 
 __device__ void nidt_raw_buffer_load_lds(i32x4_t rsrc, __attribute__((address_space(3))) uint32_t* lds, int size,
                                          int voffset, int soffset, int offset, int aux)
     __asm("llvm.amdgcn.raw.buffer.load.lds");
+__device__ i32x4_t nidt_raw_buffer_load_v4i32(i32x4_t rsrc, int voffset, int soffset, int aux)
+    __asm("llvm.amdgcn.raw.buffer.load.v4i32");
+__device__ void nidt_raw_buffer_store_v4i32(i32x4_t data, i32x4_t rsrc, int voffset, int soffset, int aux)
+    __asm("llvm.amdgcn.raw.buffer.store.v4i32");
 constexpr int kBufOOB = (int)0x80000000u;
 
 __device__ __forceinline__ i32x4_t make_rsrc(const void* base, uint32_t bytes) {

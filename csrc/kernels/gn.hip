@@ -12,6 +12,7 @@
 // dy*gamma*xhat, and writes dt in bf16; k_gn_param_grads sums the per-sample partials of each client into its
 // gradient row.
 #include "common.h"
+#include "dma.h"
 
 namespace nidt {
 
@@ -53,35 +54,83 @@ __device__ __forceinline__ void gn_reduce_groups(const float* part, float* sm, f
   __syncthreads();
 }
 
+// Per-channel totals over the block of this thread's 8 channel partials p (channels 8j .. 8j+7 of chunk column
+// j = tid % nch): the lanes of a wave sharing j by xor shuffles over the lane bits >= log2(nch), then the 8 waves in
+// a fixed order through LDS (deterministic).  red: LDS [8][512]; out: LDS [C] (valid after the call; p is clobbered).
+__device__ __forceinline__ void gn_chan_sums(float* p, float* red, float* out, int C, int nch) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  for (int o = nch; o < 64; o <<= 1)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) p[e] += __shfl_xor(p[e], o, 64);
+  if (lane < nch) {
+    float4* r = reinterpret_cast<float4*>(red + w * 512 + 8 * lane);
+    r[0] = make_float4(p[0], p[1], p[2], p[3]);
+    r[1] = make_float4(p[4], p[5], p[6], p[7]);
+  }
+  __syncthreads();
+  for (int c = tid; c < C; c += kGnThreads) {
+    float s = 0.f;
+#pragma unroll
+    for (int q = 0; q < kGnThreads / 64; ++q) s += red[q * 512 + c];
+    out[c] = s;
+  }
+  __syncthreads();
+}
+
+__device__ __forceinline__ uint4 as_u4(i32x4_t v) {
+  return make_uint4((uint32_t)v.x, (uint32_t)v.y, (uint32_t)v.z, (uint32_t)v.w);
+}
+
+// Opaque redefinition of the held chunks between passes: the compiler may not keep a pass's unpacked fp32 copies
+// alive for the next pass (2x the registers of the packed bf16 chunks).
+template <int NV>
+__device__ __forceinline__ void gn_fence(i32x4_t (&v)[NV]) {
+#pragma unroll
+  for (int k = 0; k < NV; ++k) asm volatile("" : "+v"(v[k]));
+}
+
+// [GN-REG] Register-resident forward: the sample's 16-B chunks are read once through a raw buffer resource (a 32-bit
+// VGPR offset per chunk row; rows past the sample read zeros and their stores are dropped by the range check, so no
+// 64-bit address per chunk stays live) and kept packed; <= 128 VGPRs at NV = 16 -> two 512-thread blocks per CU (the
+// global-pointer version needed 184 VGPRs: one block per CU, its load / reduce / store phases never overlapped).
 template <int NV, bool RES, bool RELU>
-__global__ __launch_bounds__(kGnThreads) void k_gn_fwd(const uint16_t* __restrict__ t, const uint16_t* __restrict__ res,
-                                                       const float* __restrict__ theta, int64_t ldt, int64_t off_w,
-                                                       int64_t off_b, uint16_t* __restrict__ y,
-                                                       float* __restrict__ stats, int B, int S, int C) {
-  __shared__ float sm[kGnThreads * 9];
+__global__ __launch_bounds__(kGnThreads, 4) void k_gn_fwd(const uint16_t* __restrict__ t,
+                                                          const uint16_t* __restrict__ res,
+                                                          const float* __restrict__ theta, int64_t ldt, int64_t off_w,
+                                                          int64_t off_b, uint16_t* __restrict__ y,
+                                                          float* __restrict__ stats, int B, int S, int C) {
+  __shared__ __attribute__((aligned(16))) float red[kGnThreads / 64 * 512];
   __shared__ float chs[512];
-  __shared__ float grp[kGnGroups], gmean[kGnGroups], grstd[kGnGroups];
+  __shared__ float gmean[kGnGroups], grstd[kGnGroups];
   const int n = blockIdx.x, g = n / B, tid = threadIdx.x;
   const int nch = C >> 3, nchunk = S * nch;
   const int64_t base = (int64_t)n * S * C;
+  const uint32_t bytes = (uint32_t)S * C * 2;
   const int j = tid % nch;  // this thread's channel chunk (512 % nch == 0)
   const int cg = C / kGnGroups;
-  uint4 v[NV];
+  const int vo = tid * 16;
+  const i32x4_t rt = make_rsrc(t + base, bytes);
+  i32x4_t v[NV];
+#pragma unroll
+  for (int k = 0; k < NV; ++k) v[k] = nidt_raw_buffer_load_v4i32(rt, vo + k * kGnThreads * 16, 0, 0);
   float part[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) part[e] = 0.f;
 #pragma unroll
-  for (int k = 0; k < NV; ++k) {
-    const int q = tid + k * kGnThreads;
-    v[k] = q < nchunk ? *reinterpret_cast<const uint4*>(t + base + (int64_t)q * 8) : make_uint4(0, 0, 0, 0);
+  for (int k = 0; k < NV; ++k) {  // rows past the sample read zeros: no guard in the sum
     float f[8];
-    unpack8(v[k], f);
+    unpack8(as_u4(v[k]), f);
 #pragma unroll
     for (int e = 0; e < 8; ++e) part[e] += f[e];
   }
-  gn_reduce_groups(part, sm, chs, grp, C, nch);
-  if (tid < kGnGroups) gmean[tid] = grp[tid] / (float)(S * cg);
+  gn_chan_sums(part, red, chs, C, nch);
+  if (tid < kGnGroups) {
+    float s = 0.f;
+    for (int i = 0; i < cg; ++i) s += chs[tid * cg + i];
+    gmean[tid] = s / (float)(S * cg);
+  }
   __syncthreads();
+  gn_fence(v);
   float mu[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
@@ -90,10 +139,9 @@ __global__ __launch_bounds__(kGnThreads) void k_gn_fwd(const uint16_t* __restric
   }
 #pragma unroll
   for (int k = 0; k < NV; ++k) {
-    const int q = tid + k * kGnThreads;
-    if (q < nchunk) {
+    if (tid + k * kGnThreads < nchunk) {
       float f[8];
-      unpack8(v[k], f);
+      unpack8(as_u4(v[k]), f);
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         const float d = f[e] - mu[e];
@@ -101,9 +149,11 @@ __global__ __launch_bounds__(kGnThreads) void k_gn_fwd(const uint16_t* __restric
       }
     }
   }
-  gn_reduce_groups(part, sm, chs, grp, C, nch);
+  gn_chan_sums(part, red, chs, C, nch);
   if (tid < kGnGroups) {
-    const float rs = rsqrtf(grp[tid] / (float)(S * cg) + kGnEps);
+    float s = 0.f;
+    for (int i = 0; i < cg; ++i) s += chs[tid * cg + i];
+    const float rs = rsqrtf(s / (float)(S * cg) + kGnEps);
     grstd[tid] = rs;
     stats[((int64_t)n * kGnGroups + tid) * 2] = gmean[tid];
     stats[((int64_t)n * kGnGroups + tid) * 2 + 1] = rs;
@@ -115,52 +165,57 @@ __global__ __launch_bounds__(kGnThreads) void k_gn_fwd(const uint16_t* __restric
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
     const int c = 8 * j + e;
-    const float rs = grstd[c / cg];
-    sc[e] = gw[c] * rs;
+    sc[e] = gw[c] * grstd[c / cg];
     sh[e] = gb[c] - mu[e] * sc[e];
   }
+  gn_fence(v);
+  const i32x4_t ry = make_rsrc(y + base, bytes);
+  i32x4_t rr;
+  if (RES) rr = make_rsrc(res + base, bytes);
 #pragma unroll
   for (int k = 0; k < NV; ++k) {
-    const int q = tid + k * kGnThreads;
-    if (q < nchunk) {
-      float f[8], r[8];
-      unpack8(v[k], f);
-      if (RES) unpack8(*reinterpret_cast<const uint4*>(res + base + (int64_t)q * 8), r);
-      uint32_t o[4];
+    float f[8], r[8];
+    unpack8(as_u4(v[k]), f);
+    if (RES) unpack8(as_u4(nidt_raw_buffer_load_v4i32(rr, vo + k * kGnThreads * 16, 0, 0)), r);
+    i32x4_t o;
+    int* op = reinterpret_cast<int*>(&o);
 #pragma unroll
-      for (int e = 0; e < 8; e += 2) {
-        float a0 = fmaf(f[e], sc[e], sh[e]), a1 = fmaf(f[e + 1], sc[e + 1], sh[e + 1]);
-        if (RES) {
-          a0 += r[e];
-          a1 += r[e + 1];
-        }
-        if (RELU) {
-          a0 = fmaxf(a0, 0.f);
-          a1 = fmaxf(a1, 0.f);
-        }
-        o[e >> 1] = pack_bf16x2(a0, a1);
+    for (int e = 0; e < 8; e += 2) {
+      float a0 = fmaf(f[e], sc[e], sh[e]), a1 = fmaf(f[e + 1], sc[e + 1], sh[e + 1]);
+      if (RES) {
+        a0 += r[e];
+        a1 += r[e + 1];
       }
-      *reinterpret_cast<uint4*>(y + base + (int64_t)q * 8) = make_uint4(o[0], o[1], o[2], o[3]);
+      if (RELU) {
+        a0 = fmaxf(a0, 0.f);
+        a1 = fmaxf(a1, 0.f);
+      }
+      op[e >> 1] = (int)pack_bf16x2(a0, a1);
     }
+    nidt_raw_buffer_store_v4i32(o, ry, vo + k * kGnThreads * 16, 0, 0);  // rows past the sample: dropped
   }
 }
 
-// dy: fp32 (DYB = false) or bf16; mask (optional, bf16 post-ReLU activation): dy *= (mask > 0)
-template <int NV, bool DYB, bool MASK>
-__global__ __launch_bounds__(kGnThreads) void k_gn_bwd(const void* __restrict__ dyv, const uint16_t* __restrict__ mask,
+// dy: fp32 (DYB = false) or bf16; mask (optional, bf16 post-ReLU activation): dy *= (mask > 0).
+// [GN-REG] HOLD (bf16 dy): t and the masked dy are read once and held packed; otherwise t is held and dy (and the
+// mask) are read again by the apply pass (fewer registers: more resident blocks for the 16-row samples).
+template <int NV, bool DYB, bool MASK, bool HOLD>
+__global__ __launch_bounds__(kGnThreads, (HOLD || NV >= 16) ? 2 : 4) void k_gn_bwd(const void* __restrict__ dyv, const uint16_t* __restrict__ mask,
                                                        const uint16_t* __restrict__ t, const float* __restrict__ stats,
                                                        const float* __restrict__ theta, int64_t ldt, int64_t off_w,
                                                        uint16_t* __restrict__ dt, float* __restrict__ part_out, int B,
                                                        int S, int C) {
-  __shared__ float sm[kGnThreads * 9];
-  __shared__ float chs[512];
-  __shared__ float grp[kGnGroups], gm1[kGnGroups], gm2[kGnGroups];
-  __shared__ float chA[512];
+  static_assert(!HOLD || DYB, "k_gn_bwd: held dy is bf16");
+  __shared__ __attribute__((aligned(16))) float red[kGnThreads / 64 * 512];
+  __shared__ float chA[512], chB[512];
+  __shared__ float gm1[kGnGroups], gm2[kGnGroups];
   const int n = blockIdx.x, g = n / B, tid = threadIdx.x;
   const int nch = C >> 3, nchunk = S * nch;
   const int64_t base = (int64_t)n * S * C;
+  const uint32_t bytes = (uint32_t)S * C * 2;
   const int j = tid % nch;
   const int cg = C / kGnGroups;
+  const int vo = tid * 16;
   float mu[8], rs[8], gw[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
@@ -169,34 +224,73 @@ __global__ __launch_bounds__(kGnThreads) void k_gn_bwd(const void* __restrict__ 
     rs[e] = stats[((int64_t)n * kGnGroups + c / cg) * 2 + 1];
     gw[e] = theta[(int64_t)g * ldt + off_w + c];
   }
-  auto load_dy = [&](int q, float* d) {
-    if (DYB) {
-      unpack8(*reinterpret_cast<const uint4*>(reinterpret_cast<const uint16_t*>(dyv) + base + (int64_t)q * 8), d);
-    } else {
+  const i32x4_t rt = make_rsrc(t + base, bytes);
+  i32x4_t rm, rd;
+  if (MASK) rm = make_rsrc(mask + base, bytes);
+  if (DYB) rd = make_rsrc(reinterpret_cast<const uint16_t*>(dyv) + base, bytes);
+  auto mask_bits = [&](i32x4_t dvk, i32x4_t mk) {  // keep the dy halves whose mask value is > 0
+    float m[8];
+    unpack8(as_u4(mk), m);
+    int* dp = reinterpret_cast<int*>(&dvk);
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+      const uint32_t u = (uint32_t)dp[h];
+      dp[h] = (int)((m[2 * h] > 0.f ? (u & 0xffffu) : 0u) | (m[2 * h + 1] > 0.f ? (u & 0xffff0000u) : 0u));
+    }
+    return dvk;
+  };
+  auto load_d = [&](int k, float* d) {  // dy row k (masked), not held
+    const int q = tid + k * kGnThreads;
+    if constexpr (DYB) {
+      i32x4_t x = nidt_raw_buffer_load_v4i32(rd, vo + k * kGnThreads * 16, 0, 0);
+      if (MASK) x = mask_bits(x, nidt_raw_buffer_load_v4i32(rm, vo + k * kGnThreads * 16, 0, 0));
+      unpack8(as_u4(x), d);
+    } else if (q < nchunk) {
       const float4* p = reinterpret_cast<const float4*>(reinterpret_cast<const float*>(dyv) + base + (int64_t)q * 8);
       const float4 a = p[0], b = p[1];
       d[0] = a.x; d[1] = a.y; d[2] = a.z; d[3] = a.w; d[4] = b.x; d[5] = b.y; d[6] = b.z; d[7] = b.w;
-    }
-    if (MASK) {
-      float m[8];
-      unpack8(*reinterpret_cast<const uint4*>(mask + base + (int64_t)q * 8), m);
+      if (MASK) {
+        float m[8];
+        unpack8(*reinterpret_cast<const uint4*>(mask + base + (int64_t)q * 8), m);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) d[e] = m[e] > 0.f ? d[e] : 0.f;
+        for (int e = 0; e < 8; ++e) d[e] = m[e] > 0.f ? d[e] : 0.f;
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) d[e] = 0.f;
     }
   };
-  uint4 v[NV];
+  i32x4_t v[NV];
+  i32x4_t dv[HOLD ? NV : 1];
+#pragma unroll
+  for (int k = 0; k < NV; ++k) v[k] = nidt_raw_buffer_load_v4i32(rt, vo + k * kGnThreads * 16, 0, 0);
+  if constexpr (HOLD) {
+    constexpr int KB = NV < 4 ? NV : 4;  // dy + mask in batches of 4 rows (bounded in-flight registers)
+#pragma unroll
+    for (int k0 = 0; k0 < NV; k0 += KB) {
+      i32x4_t mk[KB];
+#pragma unroll
+      for (int k = k0; k < k0 + KB; ++k) {
+        dv[k] = nidt_raw_buffer_load_v4i32(rd, vo + k * kGnThreads * 16, 0, 0);
+        if (MASK) mk[k - k0] = nidt_raw_buffer_load_v4i32(rm, vo + k * kGnThreads * 16, 0, 0);
+      }
+      if (MASK) {
+#pragma unroll
+        for (int k = k0; k < k0 + KB; ++k) dv[k] = mask_bits(dv[k], mk[k - k0]);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
   float pa[8], pb[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) pa[e] = pb[e] = 0.f;
 #pragma unroll
   for (int k = 0; k < NV; ++k) {
-    const int q = tid + k * kGnThreads;
-    v[k] = make_uint4(0, 0, 0, 0);
-    if (q < nchunk) {
-      v[k] = *reinterpret_cast<const uint4*>(t + base + (int64_t)q * 8);
-      float f[8], d[8];
-      unpack8(v[k], f);
-      load_dy(q, d);
+    float f[8], d[8];
+    unpack8(as_u4(v[k]), f);
+    if constexpr (HOLD) unpack8(as_u4(dv[k]), d);
+    else load_d(k, d);
+    if (tid + k * kGnThreads < nchunk) {  // rows past the sample: dy reads zero, but (f - mu) does not
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         pa[e] += d[e];
@@ -205,16 +299,11 @@ __global__ __launch_bounds__(kGnThreads) void k_gn_bwd(const void* __restrict__ 
     }
   }
   // per-channel A_c (= dbeta partial) and B_c (= dgamma partial); group sums of gamma-weighted values
-  gn_reduce_groups(pa, sm, chs, grp, C, nch);
-  for (int c = tid; c < C; c += kGnThreads) chA[c] = chs[c];
-  __syncthreads();
-  float pbw[8];
-#pragma unroll
-  for (int e = 0; e < 8; ++e) pbw[e] = pb[e];
-  gn_reduce_groups(pbw, sm, chs, grp, C, nch);  // chs = B_c
+  gn_chan_sums(pa, red, chA, C, nch);
+  gn_chan_sums(pb, red, chB, C, nch);
   for (int c = tid; c < C; c += kGnThreads) {
     part_out[((int64_t)n * C + c) * 2] = chA[c];
-    part_out[((int64_t)n * C + c) * 2 + 1] = chs[c];
+    part_out[((int64_t)n * C + c) * 2 + 1] = chB[c];
   }
   if (tid < kGnGroups) {
     float s1 = 0.f, s2 = 0.f;
@@ -222,7 +311,7 @@ __global__ __launch_bounds__(kGnThreads) void k_gn_bwd(const void* __restrict__ 
     for (int i = 0; i < cg; ++i) {
       const int c = tid * cg + i;
       s1 = fmaf(gwr[c], chA[c], s1);
-      s2 = fmaf(gwr[c], chs[c], s2);
+      s2 = fmaf(gwr[c], chB[c], s2);
     }
     gm1[tid] = s1 / (float)(S * cg);
     gm2[tid] = s2 / (float)(S * cg);
@@ -234,23 +323,25 @@ __global__ __launch_bounds__(kGnThreads) void k_gn_bwd(const void* __restrict__ 
     m1[e] = gm1[(8 * j + e) / cg];
     m2[e] = gm2[(8 * j + e) / cg];
   }
+  gn_fence(v);
+  if constexpr (HOLD) gn_fence(dv);
+  const i32x4_t rdt = make_rsrc(dt + base, bytes);
 #pragma unroll
   for (int k = 0; k < NV; ++k) {
-    const int q = tid + k * kGnThreads;
-    if (q < nchunk) {
-      float f[8], d[8];
-      unpack8(v[k], f);
-      load_dy(q, d);
-      uint32_t o[4];
+    float f[8], d[8];
+    unpack8(as_u4(v[k]), f);
+    if constexpr (HOLD) unpack8(as_u4(dv[k]), d);
+    else load_d(k, d);
+    i32x4_t o;
+    int* op = reinterpret_cast<int*>(&o);
 #pragma unroll
-      for (int e = 0; e < 8; e += 2) {
-        const float x0 = (f[e] - mu[e]) * rs[e], x1 = (f[e + 1] - mu[e + 1]) * rs[e + 1];
-        const float r0 = rs[e] * (d[e] * gw[e] - m1[e] - x0 * m2[e]);
-        const float r1 = rs[e + 1] * (d[e + 1] * gw[e + 1] - m1[e + 1] - x1 * m2[e + 1]);
-        o[e >> 1] = pack_bf16x2(r0, r1);
-      }
-      *reinterpret_cast<uint4*>(dt + base + (int64_t)q * 8) = make_uint4(o[0], o[1], o[2], o[3]);
+    for (int e = 0; e < 8; e += 2) {
+      const float x0 = (f[e] - mu[e]) * rs[e], x1 = (f[e + 1] - mu[e + 1]) * rs[e + 1];
+      const float r0 = rs[e] * (d[e] * gw[e] - m1[e] - x0 * m2[e]);
+      const float r1 = rs[e + 1] * (d[e + 1] * gw[e + 1] - m1[e + 1] - x1 * m2[e + 1]);
+      op[e >> 1] = (int)pack_bf16x2(r0, r1);
     }
+    nidt_raw_buffer_store_v4i32(o, rdt, vo + k * kGnThreads * 16, 0, 0);  // rows past the sample: dropped
   }
 }
 
@@ -624,8 +715,18 @@ void gn_bwd(uintptr_t dy, int dy_bf16, uintptr_t mask, uintptr_t t, uintptr_t st
     return;
   }
   const int nv = gn_nv(S, C);
+  // [GN-REG] hold the bf16 dy in registers up to NIDT_GN_HOLD rows per thread (default 4: at 8 rows holding costs the
+  // second resident block, at 16 it spills; A/B with NIDT_GN_HOLD=8)
+  static const int hold_max = [] {
+    const char* e = getenv("NIDT_GN_HOLD");
+    return e ? atoi(e) : 4;
+  }();
+  const bool hold = dy_bf16 && nv <= hold_max;
 #define GNB(NVV, DB, M)                                                                                        \
-  hipLaunchKernelGGL((k_gn_bwd<NVV, DB, M>), dim3(N), dim3(kGnThreads), 0, s, ptr<const void>(dy),              \
+  if (DB && hold) hipLaunchKernelGGL((k_gn_bwd<NVV, DB, M, DB>), dim3(N), dim3(kGnThreads), 0, s,               \
+                     ptr<const void>(dy), ptr<const uint16_t>(mask), ptr<const uint16_t>(t), ptr<const float>(stats), \
+                     ptr<const float>(theta), ldt, off_w, ptr<uint16_t>(dt), ptr<float>(part), B, S, C);        \
+  else hipLaunchKernelGGL((k_gn_bwd<NVV, DB, M, false>), dim3(N), dim3(kGnThreads), 0, s, ptr<const void>(dy),  \
                      ptr<const uint16_t>(mask), ptr<const uint16_t>(t), ptr<const float>(stats),               \
                      ptr<const float>(theta), ldt, off_w, ptr<uint16_t>(dt), ptr<float>(part), B, S, C)
 #define GNB_DM(NVV)                                                                                            \

@@ -56,7 +56,7 @@ def matmul_mod_device(A, B, p, device="cuda"):
     B = torch.as_tensor(np.asarray(B, dtype=np.int64) % p).to(device).contiguous()
     C = torch.empty((A.shape[0], B.shape[1]), dtype=torch.int64, device=device)
     ops.ext().modp_matmul(A.data_ptr(), B.data_ptr(), C.data_ptr(), A.shape[0], A.shape[1], B.shape[1], int(p),
-                          torch.cuda.current_stream().cuda_stream)
+                          ops.stream())
     return C.cpu().numpy()
 
 

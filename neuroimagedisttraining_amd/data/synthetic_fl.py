@@ -74,7 +74,7 @@ def to_hip_store(vol_u8, chunk=512):
     dev = vol_u8.device
     x8 = torch.empty((N, 61, 73, 61, 8), dtype=torch.uint8, device=dev)
     mom = torch.empty((N, 125 + 125 * 125), dtype=torch.float64, device=dev)
-    st = torch.cuda.current_stream().cuda_stream
+    st = ops.stream()
     for s in range(0, N, chunk):
         e = min(N, s + chunk)
         src = vol_u8[s:e].contiguous()

@@ -101,7 +101,7 @@ class HipAlexNet3D:
                     fp_sz = max(fp_sz, ks * G * mg * c_out)
         b["fpart"] = e(max(fp_sz, 1), dt=f32)
         # forward / dgrad convs with the three-tap union B staging (k_conv_fwd_tri) and their union tables
-        st0 = torch.cuda.current_stream().cuda_stream
+        st0 = ops.stream()
         for (ci, bi, cin, cout, pad, sp) in (L2, L3, L4, L5):
             out = tuple(d + 2 * pad - 2 for d in sp)
             for tag, (c_in, c_out, vol, pd) in (("f", (cin, cout, sp, pad)), ("d", (cout, cin, out, 2 - pad))):
@@ -142,7 +142,7 @@ class HipAlexNet3D:
                 c1part=e(NB * 19 * self.m.conv1_wgrad_nq(NB), 64, 126, dt=f32),
             )
             # per-layer output-position tables for the LDS-DMA wgrad kernel (shared by all clients and steps)
-            st0 = torch.cuda.current_stream().cuda_stream
+            st0 = ops.stream()
             for (ci, bi, cin, cout, pad, sp) in (L2, L3, L4, L5):
                 mg = B * (sp[0] + 2 * pad - 2) * (sp[1] + 2 * pad - 2) * (sp[2] + 2 * pad - 2)
                 b["pt%d" % ci] = e(mg, 2, dt=torch.int32)
@@ -236,7 +236,7 @@ class HipAlexNet3D:
 
     # ---------------------------------------------------------------------------------------------
     def _pack(self, theta, G, b, train):
-        m, st = self.m, torch.cuda.current_stream().cuda_stream
+        m, st = self.m, ops.stream()
         P = theta.stride(0)
         m.pack_conv1_w(_p(theta), P, self.o["features.0.weight"], self.o["features.1.weight"], G, 1.0 / 255.0,
                        _p(b["w1p"]), _p(b["w125"]), st)
@@ -251,7 +251,7 @@ class HipAlexNet3D:
     def _bn(self, ci, bi, C, G, B, sp, theta, bufs, b, train):
         """BN coefficients for conv ``ci`` (train: from the conv epilogue stats; eval: running stats, which also
         leaves the running mean / invstd in ``m``/``i`` for an eval-mode backward)."""
-        m, st = self.m, torch.cuda.current_stream().cuda_stream
+        m, st = self.m, ops.stream()
         P, Q = theta.stride(0), bufs.stride(0)
         og, ob = self.o["features.%d.weight" % bi], self.o["features.%d.bias" % bi]
         orm, orv = self.ob["features.%d.running_mean" % bi], self.ob["features.%d.running_var" % bi]
@@ -273,7 +273,7 @@ class HipAlexNet3D:
         assert theta.shape[1] == self.P and bufs.shape[1] == self.Q and theta.dtype == torch.float32
         assert idx.dtype == torch.int32 and idx.numel() == G * B and x8.dtype == torch.uint8
         assert x8.dim() == 5 and tuple(x8.shape[1:]) == (61, 73, 61, 8) and x8.is_contiguous()
-        m, st = self.m, torch.cuda.current_stream().cuda_stream
+        m, st = self.m, ops.stream()
         b = self._bufs(G, B, train)
         NB = G * B
         P, Q = theta.stride(0), bufs.stride(0)
@@ -327,7 +327,7 @@ class HipAlexNet3D:
         update) — DisPFL's ``screen_gradients`` (``DisPFL/my_model_trainer.py:166-189``)."""
         assert grads.shape == theta.shape and grads.stride(1) == 1 and grads.stride(0) == theta.stride(0)
         assert labels.dtype == torch.float32 and labels.numel() == G * B and B <= 32
-        m, st = self.m, torch.cuda.current_stream().cuda_stream
+        m, st = self.m, ops.stream()
         if not bn_train:
             keep = 1.0
         ev = 0 if bn_train else 1
@@ -409,7 +409,7 @@ class HipAlexNet3D:
 
     def eval_logits(self, theta, bufs, x8, idx, G, B):
         """Eval-mode (running-stat BN, no dropout) logits [G*B] for client g's samples idx[g*B:(g+1)*B]."""
-        m, st = self.m, torch.cuda.current_stream().cuda_stream
+        m, st = self.m, ops.stream()
         b = self.forward(theta, bufs, x8, None, idx, G, B, False)
         P = theta.stride(0)
         o = self.o

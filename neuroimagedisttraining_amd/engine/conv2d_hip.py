@@ -25,8 +25,7 @@ import torch.nn.functional as F
 from .. import ops
 
 
-def _stream():
-    return torch.cuda.current_stream().cuda_stream
+_stream = ops.stream
 
 
 def _nhwc_bf16(x):

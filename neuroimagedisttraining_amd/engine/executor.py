@@ -169,12 +169,12 @@ class HipEngine:
                          pref.stride(0) if (pref is not None and pref.dim() == 2) else 0, float(spec.lamda),
                          ows.data_ptr(), G, P, float(lr), float(wd), float(momentum), float(max_norm),
                          lr_dev.data_ptr() if lr_dev is not None else 0, int(keep_grad),
-                         torch.cuda.current_stream().cuda_stream)
+                         ops.stream())
 
     def saliency_acc(self, theta, grads, score, alpha):
         G, P = theta.shape
         self.m.saliency_acc(theta.data_ptr(), grads.data_ptr(), theta.stride(0), P, G, float(alpha),
-                            score.data_ptr(), score.stride(0), torch.cuda.current_stream().cuda_stream)
+                            score.data_ptr(), score.stride(0), ops.stream())
 
 
 class TorchEngine:

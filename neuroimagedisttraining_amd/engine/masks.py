@@ -34,7 +34,7 @@ def _hip(t):
 
 
 def _st():
-    return torch.cuda.current_stream().cuda_stream
+    return ops.stream()
 
 
 def mask_words(P):

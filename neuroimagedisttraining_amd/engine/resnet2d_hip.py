@@ -49,8 +49,7 @@ GN_GROUPS = 32
 GN_EPS = 1e-5
 
 
-def _stream():
-    return torch.cuda.current_stream().cuda_stream
+_stream = ops.stream
 
 
 # ------------------------------------------------------------------------------------------------ augmentation
@@ -233,27 +232,16 @@ class GroupedConv:
         dy = dy.contiguous()
         ns = m.conv_wgrad_nsplit_g(G, B, 1, H, W, self.cin_p, self.cout, self.kt, self.stride, self.pad, 0)
         ptab = self._pos_table(B, H, W, Ho, Wo, x.device)
-        cur = torch.cuda.current_stream()
-        if ws is not None:
-            ws.wait_stream(cur)
+        if ws is None:  # no branch: the whole backward on the current stream (no stream objects per launch)
+            self._wgrad(m, x, dy, grads, G, B, H, W, ns, ptab, _stream())
+        else:
+            ws.wait_stream(torch.cuda.current_stream())
             x.record_stream(ws)
             dy.record_stream(ws)
             ptab.record_stream(ws)
-        with torch.cuda.stream(ws if ws is not None else cur):
-            st = _stream()
-            part = torch.empty(ns * G * self.cout * self.kt * self.cin_p, device=x.device, dtype=torch.float32)
-            if self.cin_p == self.cin:
-                m.conv_wgrad_g(x.data_ptr(), dy.data_ptr(), part.data_ptr(), grads.data_ptr(), grads.stride(0),
-                               self.off, G, B, 1, H, W, self.cin_p, self.cout, self.kt, self.stride, self.pad, 0, ns,
-                               1.0, ptab.data_ptr(), st)
-            else:  # channel-padded stem: full-width gradient, then the live input channels into the row
-                full = torch.empty(G, self.cout * self.cin_p * self.kt, device=x.device, dtype=torch.float32)
-                m.conv_wgrad_g(x.data_ptr(), dy.data_ptr(), part.data_ptr(), full.data_ptr(), full.stride(0), 0, G, B,
-                               1, H, W, self.cin_p, self.cout, self.kt, self.stride, self.pad, 0, ns, 1.0,
-                               ptab.data_ptr(), st)
-                grads[:, self.off:self.off + self.numel].view(G, self.cout, self.cin, self.kt).copy_(
-                    full.view(G, self.cout, self.cin_p, self.kt)[:, :, :self.cin])
-        st = cur.cuda_stream
+            with torch.cuda.stream(ws):
+                self._wgrad(m, x, dy, grads, G, B, H, W, ns, ptab, _stream())
+        st = _stream()
         if not need_dx:
             return None
         wt = self.wt
@@ -283,6 +271,20 @@ class GroupedConv:
         conv_fwd(dy.data_ptr(), wt.data_ptr(), sub.data_ptr(), G, B, 1, Ho, Wo, self.cout, self.cin_p, 1, 1,
                  0, 0, x.device)
         return sub
+
+    def _wgrad(self, m, x, dy, grads, G, B, H, W, ns, ptab, st):
+        part = torch.empty(ns * G * self.cout * self.kt * self.cin_p, device=x.device, dtype=torch.float32)
+        if self.cin_p == self.cin:
+            m.conv_wgrad_g(x.data_ptr(), dy.data_ptr(), part.data_ptr(), grads.data_ptr(), grads.stride(0),
+                           self.off, G, B, 1, H, W, self.cin_p, self.cout, self.kt, self.stride, self.pad, 0, ns,
+                           1.0, ptab.data_ptr(), st)
+        else:  # channel-padded stem: full-width gradient, then the live input channels into the row
+            full = torch.empty(G, self.cout * self.cin_p * self.kt, device=x.device, dtype=torch.float32)
+            m.conv_wgrad_g(x.data_ptr(), dy.data_ptr(), part.data_ptr(), full.data_ptr(), full.stride(0), 0, G, B,
+                           1, H, W, self.cin_p, self.cout, self.kt, self.stride, self.pad, 0, ns, 1.0,
+                           ptab.data_ptr(), st)
+            grads[:, self.off:self.off + self.numel].view(G, self.cout, self.cin, self.kt).copy_(
+                full.view(G, self.cout, self.cin_p, self.kt)[:, :, :self.cin])
 
     def _pos_table(self, B, H, W, Ho, Wo, device):
         """Output-position table of the wgrad kernel: a function of the shape only, built once per (B, H, W) outside

@@ -35,8 +35,7 @@ BN_EPS = 1e-5
 BN_MOM = 0.1
 
 
-def _stream():
-    return torch.cuda.current_stream().cuda_stream
+_stream = ops.stream
 
 
 def conv_fwd(x_ptr, w_ptr, y_ptr, G, B, D, H, W, Cin, Cout, kt, st, pad, padd, device):

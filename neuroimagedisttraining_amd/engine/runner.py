@@ -458,7 +458,7 @@ class FLRunner:
             m = ops.ext()
             part = torch.empty((R, m.rows_nnz_blocks(K)), dtype=torch.int32, device=self.device)
             m.rows_nnz(mat.data_ptr(), R, K, mat.stride(0) if R > 1 else (K + 3) // 4 * 4, part.data_ptr(),
-                       torch.cuda.current_stream().cuda_stream)
+                       ops.stream())
             return part.sum(1, dtype=torch.int64)
         return torch.count_nonzero(mat, dim=1)
 
@@ -679,10 +679,10 @@ class FLRunner:
                 hist = torch.empty(256, dtype=torch.int32, device=self.device)
                 sel = sel.contiguous()
                 m.radix_select_kth(sel.data_ptr(), sel.numel(), k, st.data_ptr(), hist.data_ptr(),
-                                   torch.cuda.current_stream().cuda_stream)
+                                   ops.stream())
                 keep = torch.empty_like(sel)
                 m.threshold_mask(sel.data_ptr(), sel.numel(), st.data_ptr(), keep.data_ptr(),
-                                 torch.cuda.current_stream().cuda_stream)
+                                 ops.stream())
             else:
                 thr = torch.topk(sel, k, sorted=True).values[-1]
                 keep = (sel >= thr).float()
@@ -954,7 +954,7 @@ class FLRunner:
         if rows:
             w = self._to_dev(weights, torch.float32)
             if self.device.type == "cuda" and _contiguous(rows):
-                m, st = ops.ext(), torch.cuda.current_stream().cuda_stream
+                m, st = ops.ext(), ops.stream()
                 lo = rows[0]
                 m.weighted_rows_sum(theta[lo].data_ptr(), w.data_ptr(), len(rows), self.P, theta.stride(0), 0.0,
                                     buf.data_ptr(), st)

@@ -61,6 +61,14 @@ def require(device) -> bool:
     return True
 
 
+def stream() -> int:
+    """Raw ``hipStream_t`` of the current stream on the current device (honours ``torch.cuda.stream(...)``
+    contexts and graph capture).  ``torch.cuda.current_stream()`` builds a Python stream object per call
+    (~8 us); the small-model engines launch ~10^5 kernels per round, so every launch site uses this instead."""
+    import torch
+    return torch._C._cuda_getCurrentRawStream(torch._C._cuda_getDevice())
+
+
 def ext_path():
     m = _load()
     return getattr(m, "__file__", None) if m is not None else None

@@ -20,12 +20,12 @@ from __future__ import annotations
 import torch
 
 from . import ext
+from . import stream as _raw_stream
 
 _LIB = "nidt"
 
 
-def _stream():
-    return torch.cuda.current_stream().cuda_stream
+_stream = _raw_stream
 
 
 def _check_conv(x, w, bias, pad):

@@ -4,6 +4,7 @@ from __future__ import annotations
 import torch
 
 from . import ext
+from . import stream as _raw_stream
 
 
 def kth_largest(v: torch.Tensor, k: int) -> torch.Tensor:
@@ -19,7 +20,7 @@ def kth_largest(v: torch.Tensor, k: int) -> torch.Tensor:
     st = torch.empty(4, dtype=torch.int32, device=v.device)
     hist = torch.empty(256, dtype=torch.int32, device=v.device)
     m.radix_select_kth(x.data_ptr(), x.numel(), int(k), st.data_ptr(), hist.data_ptr(),
-                       torch.cuda.current_stream().cuda_stream)
+                       _raw_stream())
     return st[3:4].view(torch.float32)[0].clone()
 
 

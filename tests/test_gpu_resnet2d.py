@@ -167,7 +167,7 @@ def test_resnet18gn_hip_runners_graphs_match_eager():
         assert torch.equal(outs[0], outs[1]), alg
 
 
-@pytest.mark.parametrize("hw,C", [(32, 64), (16, 128), (8, 256), (4, 512), (64, 64), (32, 128)])
+@pytest.mark.parametrize("hw,C", [(32, 64), (16, 128), (8, 256), (4, 512), (64, 64), (32, 128), (6, 64), (7, 128)])
 @pytest.mark.parametrize("res,dy_bf16", [(False, True), (True, False)])
 def test_groupnorm_kernels_match_torch(hw, C, res, dy_bf16):
     """gn.hip forward (affine + residual + ReLU) and backward (ReLU mask, dgamma/dbeta rows) vs the fp32 CPU

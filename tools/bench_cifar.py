@@ -106,6 +106,26 @@ def main():
         torch.cuda.synchronize()
         walls.append(time.perf_counter() - t1)
         print("warmup round %d: %.2f s" % (r, walls[-1]), flush=True)
+    if os.environ.get("NIDT_CIFAR_EVAL_PROBE") in ("1", "exit") and hasattr(runner, "_eval_buffers"):
+        # diagnostics: time the per-round personal evaluation of every client alone (SubAvg's eval block)
+        from neuroimagedisttraining_amd.engine import masks as MK
+        from neuroimagedisttraining_amd.engine.personalized import RowSet
+        for rep in range(3):
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            th, bu = runner._eval_buffers(max(1, runner.C))
+            th.copy_(runner.w_global.expand_as(th))
+            bu.copy_(runner.b_global.expand_as(bu))
+            th[:runner.C, :runner.P].mul_(MK.unpack_bits(runner.mbits[:runner.C], runner.P))
+            torch.cuda.synchronize()
+            t2 = time.perf_counter()
+            r = runner.eval_local(RowSet(th, bu), *runner.all_rows())
+            torch.cuda.synchronize()
+            print("eval probe %d: prepare %.1f ms, eval_local %.1f ms (%d clients, %d test samples)"
+                  % (rep, (t2 - t1) * 1e3, (time.perf_counter() - t2) * 1e3, runner.C,
+                     int(sum(len(sp.test) for sp in splits))), flush=True)
+        if os.environ.get("NIDT_CIFAR_EVAL_PROBE") == "exit":
+            return
     rt.barrier(info)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
