@@ -2880,13 +2880,16 @@ static void conv_wgrad_impl(uintptr_t x, uintptr_t xs, uintptr_t xt, uintptr_t d
     const int nch = (Cout % 128 == 0 && nch_env == 2) ? 2 : 1;
     d.nKT = ceil_div(a.K, kWgKC); d.nCT = Cout / (kWgCO * nch);
     d.xclient = (int64_t)B * D * H * W * Cin;
-    // [WG-DIRECT] one split: the kernel writes the gradient rows (no fp32 slab round trip, no reduce launch).
-    // NIDT_WG_DIRECT=0 keeps slab + k_wgrad_reduce (A/B; the results are bitwise equal)
+    // [WG-DIRECT] one split: the kernel writes the gradient rows (no fp32 slab round trip, no reduce launch).  The
+    // rows are [Cout][Cin][kt] and a block owns 1-4 taps of a channel slice, so for kt > 1 its stores are 4-B
+    // scatters at a kt-float stride: CIFAR DisPFL (100 clients) -70 ms/round net, SubAvg (10 clients) +10 ms
+    // (profiles/r5_pack_fuse_wg_direct.txt).  NIDT_WG_DIRECT=1 (default): 1x1 layers only (contiguous rows), 2: every layer,
+    // 0: off (A/B; the results are bitwise equal either way)
     static const int direct_env = [] {
       const char* e = getenv("NIDT_WG_DIRECT");
       return e ? atoi(e) : 1;
     }();
-    direct = direct_env && nsplit == 1;
+    direct = nsplit == 1 && (direct_env == 2 || (direct_env == 1 && kt == 1));
     d.grad = direct ? ptr<float>(grad) : nullptr;
     d.ldg = ldg; d.off = off; d.scale = scale; d.kt = kt;
     NIDT_REQUIRE(d.xclient * 2 < (1ll << 31) && (int64_t)a.Mg * Cout * 2 < (1ll << 31),

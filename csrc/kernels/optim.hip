@@ -13,6 +13,7 @@
 // g^2 written to a [C, nblk] slab; (2) every block of client c re-reduces that client's nblk
 // partials (<= 1024 floats, L2-resident) and updates its chunk with 16-B vector accesses.
 #include "common.h"
+#include "pack.h"
 
 namespace nidt {
 
@@ -225,19 +226,21 @@ __global__ __launch_bounds__(kOptThreads) void k_local_sqnorm(LocalOpt a, int64_
   if (threadIdx.x == 0) part[(int64_t)c * nblk + blockIdx.x] = t;
 }
 
-template <int MASK, bool HAS_MOM>
-__global__ __launch_bounds__(kOptThreads) void k_local_step(LocalOpt a, const float* __restrict__ part, int nblk,
-                                                            int64_t P, int64_t chunk) {
-  __shared__ float red[kOptThreads / 64];
-  const int c = blockIdx.y;
-  const float lr = a.lr_dev ? *a.lr_dev : a.lr;
+// clip coefficient of client row c from its sqnorm partials (every thread of the block takes part)
+__device__ __forceinline__ float opt_coef(const LocalOpt& a, const float* __restrict__ part, int nblk, int c,
+                                          float* red) {
   float t = 0.f;
   for (int i = threadIdx.x; i < nblk; i += kOptThreads) t += part[(int64_t)c * nblk + i];
   t = block_sum(t, red);
-  float coef = a.max_norm / (sqrtf(t) + 1e-6f);
-  coef = coef < 1.f ? coef : 1.f;
-  const int64_t s = (int64_t)blockIdx.x * chunk;
-  const int64_t e = s + chunk < P ? s + chunk : P;
+  const float coef = a.max_norm / (sqrtf(t) + 1e-6f);
+  return coef < 1.f ? coef : 1.f;
+}
+
+// the step on elements [s, e) of client row c (16-B accesses on the 4-aligned body, scalars at the ends); stage
+// (optional, LDS): the updated weights at stage[i - s]
+template <int MASK, bool HAS_MOM>
+__device__ __forceinline__ void opt_range(const LocalOpt& a, int c, float coef, float lr, int64_t s, int64_t e,
+                                          float* stage) {
   float* wr = a.w + (int64_t)c * a.ld;
   float* gr = a.g + (int64_t)c * a.ld;
   float* br = HAS_MOM ? a.buf + (int64_t)c * a.ld : nullptr;
@@ -258,8 +261,20 @@ __global__ __launch_bounds__(kOptThreads) void k_local_step(LocalOpt a, const fl
     if (pr) ww = fmaf(-pull, ww - pv, ww);
     if (MASK == kMaskWeight && !m) ww = 0.f;
   };
-  const int64_t e4 = s + ((e - s) & ~int64_t(3));
-  for (int64_t i = s + 4 * threadIdx.x; i < e4; i += 4 * kOptThreads) {
+  auto scalar = [&](int64_t i) {
+    float ww = wr[i], gg = gr[i], bb = HAS_MOM ? br[i] : 0.f;
+    const bool m = MASK == kMaskNone ? true : ((a.mbits[(int64_t)c * a.mstride + (i >> 5)] >> (i & 31)) & 1u);
+    one(ww, gg, bb, rr ? rr[i] : 0.f, pr ? pr[i] : 0.f, m);
+    if (a.keep_grad) gr[i] = gg;
+    wr[i] = ww;
+    if (HAS_MOM) br[i] = bb;
+    if (stage) stage[i - s] = ww;
+  };
+  int64_t s4 = (s + 3) & ~int64_t(3);
+  if (s4 > e) s4 = e;
+  const int64_t e4 = s4 + ((e - s4) & ~int64_t(3));
+  for (int64_t i = s + threadIdx.x; i < s4; i += kOptThreads) scalar(i);
+  for (int64_t i = s4 + 4 * threadIdx.x; i < e4; i += 4 * kOptThreads) {
     const float4 gv = *reinterpret_cast<const float4*>(gr + i);
     const float4 wv = *reinterpret_cast<const float4*>(wr + i);
     float gg[4] = {gv.x, gv.y, gv.z, gv.w}, ww[4] = {wv.x, wv.y, wv.z, wv.w};
@@ -282,15 +297,56 @@ __global__ __launch_bounds__(kOptThreads) void k_local_step(LocalOpt a, const fl
     if (a.keep_grad) *reinterpret_cast<float4*>(gr + i) = make_float4(gg[0], gg[1], gg[2], gg[3]);
     *reinterpret_cast<float4*>(wr + i) = make_float4(ww[0], ww[1], ww[2], ww[3]);
     if (HAS_MOM) *reinterpret_cast<float4*>(br + i) = make_float4(bb[0], bb[1], bb[2], bb[3]);
+    if (stage) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) stage[i - s + j] = ww[j];
+    }
   }
-  for (int64_t i = e4 + threadIdx.x; i < e; i += kOptThreads) {
-    float ww = wr[i], gg = gr[i], bb = HAS_MOM ? br[i] : 0.f;
-    const bool m = MASK == kMaskNone ? true : ((a.mbits[(int64_t)c * a.mstride + (i >> 5)] >> (i & 31)) & 1u);
-    one(ww, gg, bb, rr ? rr[i] : 0.f, pr ? pr[i] : 0.f, m);
-    if (a.keep_grad) gr[i] = gg;
-    wr[i] = ww;
-    if (HAS_MOM) br[i] = bb;
+  for (int64_t i = e4 + threadIdx.x; i < e; i += kOptThreads) scalar(i);
+}
+
+template <int MASK, bool HAS_MOM>
+__global__ __launch_bounds__(kOptThreads) void k_local_step(LocalOpt a, const float* __restrict__ part, int nblk,
+                                                            int64_t P, int64_t chunk) {
+  __shared__ float red[kOptThreads / 64];
+  const int c = blockIdx.y;
+  const float lr = a.lr_dev ? *a.lr_dev : a.lr;
+  const float coef = opt_coef(a, part, nblk, c, red);
+  const int64_t s = (int64_t)blockIdx.x * chunk;
+  const int64_t e = s + chunk < P ? s + chunk : P;
+  opt_range<MASK, HAS_MOM>(a, c, coef, lr, s, e, nullptr);
+}
+
+// [PACK-FUSE] The step with the next forward's bf16 weight images written from the updated values (no k_pack_plain
+// re-read of the fp32 rows).  Blocks [0, nconv): one plain-grid chunk of a conv layer each (desc: blk_plain prefixes
+// over every conv layer, 1x1 included), updated into LDS and written as image rows (pack.h pack_image_chunk);
+// blocks [nconv, nconv + nrest): the ranges of the other parameters (rest: {start, length} pairs).
+template <int MASK, bool HAS_MOM>
+__global__ __launch_bounds__(kOptThreads) void k_local_step_pack(LocalOpt a, const float* __restrict__ part, int nblk,
+                                                                 const PackDesc* __restrict__ desc, int nd, int nconv,
+                                                                 const int64_t* __restrict__ rest,
+                                                                 uint16_t* __restrict__ out) {
+  extern __shared__ float row[];
+  __shared__ float red[kOptThreads / 64];
+  const int c = blockIdx.y;
+  const float lr = a.lr_dev ? *a.lr_dev : a.lr;
+  const float coef = opt_coef(a, part, nblk, c, red);
+  if ((int)blockIdx.x >= nconv) {
+    const int64_t* r = rest + 2 * ((int64_t)blockIdx.x - nconv);
+    opt_range<MASK, HAS_MOM>(a, c, coef, lr, r[0], r[0] + r[1], nullptr);
+    return;
   }
+  const int li = find_layer(desc, nd, blockIdx.x, 0);
+  const PackDesc& d = desc[li];
+  const int Cin = d.cin_p, kt = d.kt, cs = d.cin_src;
+  const int CC = pack_cc(Cin, kt), nch = (Cin + CC - 1) / CC;
+  const int b = blockIdx.x - d.blk_plain, co = b / nch, ci0 = (b - co * nch) * CC;
+  const int cw = min(CC, Cin - ci0);
+  const int cc = max(0, min(CC, cs - ci0));
+  const int64_t s = d.src_off + ((int64_t)co * cs + ci0) * kt;
+  opt_range<MASK, HAS_MOM>(a, c, coef, lr, s, s + (int64_t)cc * kt, row);
+  __syncthreads();
+  pack_image_chunk(d, row, out, c, co, ci0, cw, cc);
 }
 
 void local_opt(uintptr_t w, uintptr_t g, uintptr_t buf, int64_t ld, uintptr_t mbits, int64_t mstride, int mask_mode,
@@ -327,6 +383,50 @@ void local_opt(uintptr_t w, uintptr_t g, uintptr_t buf, int64_t ld, uintptr_t mb
     default: NIDT_REQUIRE(false, "local_opt: mask_mode");
   }
 #undef NIDT_LS
+  NIDT_CHECK(hipGetLastError());
+}
+
+// local_opt + the forward images of the conv layers (k_local_step_pack): desc / nd / nconv = the fused plain grid,
+// rest / nrest = the other parameter ranges, lds = bytes of the largest chunk, out = the packed image buffer
+void local_opt_pack(uintptr_t w, uintptr_t g, uintptr_t buf, int64_t ld, uintptr_t mbits, int64_t mstride,
+                    int mask_mode, uintptr_t ref, int64_t ref_ld, float mu, uintptr_t pref, int64_t pref_ld,
+                    float lamda, uintptr_t part, int64_t C, int64_t P, float lr, float wd, float mom, float max_norm,
+                    uintptr_t lr_dev, int keep_grad, uintptr_t desc, int nd, int nconv, uintptr_t rest, int nrest,
+                    int lds, uintptr_t out, uintptr_t stream) {
+  NIDT_REQUIRE(ld % 4 == 0 && ld >= P, "local_opt_pack: row stride must be >= P and a multiple of 4");
+  NIDT_REQUIRE((w & 15) == 0 && (g & 15) == 0 && (buf & 15) == 0, "local_opt_pack: 16-byte alignment");
+  NIDT_REQUIRE(mask_mode == kMaskNone || (mbits != 0 && mstride % 4 == 0 && (mbits & 15) == 0), "local_opt_pack: mask");
+  NIDT_REQUIRE(mu == 0.f || (ref != 0 && ref_ld % 4 == 0 && (ref & 15) == 0), "local_opt_pack: prox reference");
+  NIDT_REQUIRE(lamda == 0.f || (pref != 0 && pref_ld % 4 == 0 && (pref & 15) == 0), "local_opt_pack: pull reference");
+  NIDT_REQUIRE(desc != 0 && nd > 0 && nconv > 0 && nrest >= 0 && (nrest == 0 || rest != 0) && out != 0 && lds > 0 &&
+               lds <= 64 * 1024, "local_opt_pack: bad pack plan");
+  if (C == 0) return;
+  LocalOpt a{ptr<float>(w), ptr<float>(g), ptr<float>(buf), ld, ptr<const uint32_t>(mbits), mstride,
+             ptr<const float>(ref), ref_ld, mu, ptr<const float>(pref), pref_ld, lamda, lr, wd, mom, max_norm,
+             ptr<const float>(lr_dev), keep_grad};
+  int nblk;
+  const int64_t chunk = opt_chunk(P, &nblk);
+  hipStream_t st = as_stream(stream);
+  const dim3 grid(nblk, (unsigned)C);
+  if (mask_mode == kMaskGrad)
+    hipLaunchKernelGGL(k_local_sqnorm<kMaskGrad>, grid, dim3(kOptThreads), 0, st, a, P, chunk, ptr<float>(part), nblk);
+  else
+    hipLaunchKernelGGL(k_local_sqnorm<kMaskNone>, grid, dim3(kOptThreads), 0, st, a, P, chunk, ptr<float>(part), nblk);
+  const bool hm = buf != 0 && mom != 0.f;
+  const dim3 pgrid((unsigned)(nconv + nrest), (unsigned)C);
+#define NIDT_LSP(M, MO)                                                                                        \
+  hipLaunchKernelGGL((k_local_step_pack<M, MO>), pgrid, dim3(kOptThreads), lds, st, a, ptr<const float>(part), nblk, \
+                     ptr<const PackDesc>(desc), nd, nconv, ptr<const int64_t>(rest), ptr<uint16_t>(out))
+  switch (mask_mode * 2 + (hm ? 1 : 0)) {
+    case 0: NIDT_LSP(kMaskNone, false); break;
+    case 1: NIDT_LSP(kMaskNone, true); break;
+    case 2: NIDT_LSP(kMaskWeight, false); break;
+    case 3: NIDT_LSP(kMaskWeight, true); break;
+    case 4: NIDT_LSP(kMaskGrad, false); break;
+    case 5: NIDT_LSP(kMaskGrad, true); break;
+    default: NIDT_REQUIRE(false, "local_opt_pack: mask_mode");
+  }
+#undef NIDT_LSP
   NIDT_CHECK(hipGetLastError());
 }
 

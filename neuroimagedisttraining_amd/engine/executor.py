@@ -144,6 +144,19 @@ class HipEngine:
         """Fused per-client step (``optim.hip`` ``local_opt``): masks (shared or per-row bits, weight or gradient
         mode), FedProx proximal gradient, clip(10), SGD(wd, momentum), Ditto pull — one norm pass + one update
         pass over the rows.  The clipped gradient is written back only with ``keep_grad``."""
+        self.m.local_opt(*self._opt_args(theta, grads, mom_buf, spec, lr, wd, momentum, max_norm, lr_dev,
+                                         keep_grad), ops.stream())
+
+    def local_opt_pack(self, theta, grads, mom_buf, spec, lr, wd, momentum, max_norm, plan, lr_dev=None,
+                       keep_grad=False):
+        """:meth:`local_opt` that also writes the conv layers' bf16 forward images of the next step from the updated
+        weights (``optim.hip`` ``local_opt_pack``; ``plan`` = :meth:`.resnet2d_hip.WeightPacker.fused_plan`)."""
+        tab, nd, nconv, rest, nrest, lds, buf = plan
+        self.m.local_opt_pack(*self._opt_args(theta, grads, mom_buf, spec, lr, wd, momentum, max_norm, lr_dev,
+                                              keep_grad), tab.data_ptr(), nd, nconv,
+                              rest.data_ptr() if nrest else 0, nrest, lds, buf.data_ptr(), ops.stream())
+
+    def _opt_args(self, theta, grads, mom_buf, spec, lr, wd, momentum, max_norm, lr_dev, keep_grad):
         G, P = theta.shape
         # one workspace per row group, never freed or shared: captured graphs keep its address, and the launches of
         # one step may run concurrently on side streams (runner step_streams)
@@ -161,15 +174,14 @@ class HipEngine:
         mstride = 0 if (bits is None or spec.shared) else bits.stride(0)
         ref = spec.ref if spec.prox_mu else None
         pref = spec.pref if spec.lamda else None
-        self.m.local_opt(theta.data_ptr(), grads.data_ptr(), mom_buf.data_ptr() if mom_buf is not None else 0,
-                         theta.stride(0), bits.data_ptr() if (bits is not None and spec.mask_mode) else 0, mstride,
-                         int(spec.mask_mode), ref.data_ptr() if ref is not None else 0,
-                         ref.stride(0) if (ref is not None and ref.dim() == 2) else 0, float(spec.prox_mu),
-                         pref.data_ptr() if pref is not None else 0,
-                         pref.stride(0) if (pref is not None and pref.dim() == 2) else 0, float(spec.lamda),
-                         ows.data_ptr(), G, P, float(lr), float(wd), float(momentum), float(max_norm),
-                         lr_dev.data_ptr() if lr_dev is not None else 0, int(keep_grad),
-                         ops.stream())
+        return (theta.data_ptr(), grads.data_ptr(), mom_buf.data_ptr() if mom_buf is not None else 0,
+                theta.stride(0), bits.data_ptr() if (bits is not None and spec.mask_mode) else 0, mstride,
+                int(spec.mask_mode), ref.data_ptr() if ref is not None else 0,
+                ref.stride(0) if (ref is not None and ref.dim() == 2) else 0, float(spec.prox_mu),
+                pref.data_ptr() if pref is not None else 0,
+                pref.stride(0) if (pref is not None and pref.dim() == 2) else 0, float(spec.lamda),
+                ows.data_ptr(), G, P, float(lr), float(wd), float(momentum), float(max_norm),
+                lr_dev.data_ptr() if lr_dev is not None else 0, int(keep_grad))
 
     def saliency_acc(self, theta, grads, score, alpha):
         G, P = theta.shape

@@ -324,6 +324,8 @@ _PACK_DTYPE = np.dtype({"names": ["src_off", "wp_off", "wt_off", "cout", "cin_p"
 # 1x1 layers on the no-LDS row-batched pack (pack.hip k_pack_plain1; config 5 12.48 -> 12.24 s/round,
 # profiles/r4_ab_pack1.txt); NIDT_PACK1=0: the per-row kernel (A/B)
 _PACK1 = os.environ.get("NIDT_PACK1", "1") != "0"
+# NIDT_PACK_FUSE=0: the optimizer never writes the forward images (k_pack_plain every step; A/B)
+_PACK_FUSE = os.environ.get("NIDT_PACK_FUSE", "1") != "0"
 
 
 class WeightPacker:
@@ -334,6 +336,9 @@ class WeightPacker:
     def __init__(self, convs, device):
         self.convs, self.device = list(convs), torch.device(device)
         self._plans = {}
+        self._descs = {}
+        self.last = None   # (key, theta data_ptr, row stride) of the last pack() call
+        self.fresh = {}    # key -> (theta data_ptr, theta._version) whose forward images the optimizer wrote
 
     def _plan(self, G, train, key=None):
         key = (G, train) if key is None else key
@@ -375,13 +380,52 @@ class WeightPacker:
         tab = torch.from_numpy(desc.view(np.uint8).copy()).to(self.device)
         plan = (tab, (nplain, nplain1), ntrans, lds, buf, views)
         self._plans[key] = plan
+        self._descs[key] = desc
+        return plan
+
+    def fused_plan(self, key, P):
+        """Plan of the optimizer step that writes ``key``'s forward images itself (``optim.hip`` ``local_opt_pack``):
+        (descriptor table with plain-grid prefixes over every conv layer, its length, conv blocks, {start, length}
+        table of the other parameter ranges of a P-wide row, its length, LDS bytes, the image buffer)."""
+        fk = ("fused", key, int(P))
+        plan = self._plans.get(fk)
+        if plan is not None:
+            return plan
+        m = ops.ext()
+        desc = self._descs[key].copy()
+        nconv, spans = 0, []
+        for i, c in enumerate(self.convs):
+            desc[i]["blk_plain"] = nconv
+            nconv += c.cout * m.pack_plain_chunks(c.cin_p, c.kt)
+            spans.append((c.off, c.off + c.numel))
+        rest, pos = [], 0
+        for a, b in sorted(spans) + [(int(P), int(P))]:
+            while pos < a:  # the parameters between conv layers, 4096 per block
+                n = min(4096, a - pos)
+                rest.append((pos, n))
+                pos += n
+            pos = max(pos, b)
+        lds = max(m.pack_plain_lds(c.cin_p, c.kt) for c in self.convs)
+        tab = torch.from_numpy(desc.view(np.uint8).copy()).to(self.device)
+        rt = torch.tensor(rest if rest else [(0, 0)], dtype=torch.int64).to(self.device)
+        plan = (tab, len(self.convs), nconv, rt, len(rest), lds, self._plans[key][4])
+        self._plans[fk] = plan
         return plan
 
     def pack(self, theta, G, train, key=None):
-        """Pack every layer for this step and hand each conv its views (``conv.wp`` / ``conv.wt``)."""
+        """Pack every layer for this step and hand each conv its views (``conv.wp`` / ``conv.wt``).  When the previous
+        optimizer step wrote this key's forward images from these rows (``fresh``, see :meth:`fused_plan`; the rows
+        unchanged since by torch ops: same ``_version``), only the dgrad transposes run."""
+        key = (G, train) if key is None else key
         tab, (nplain, nplain1), ntrans, lds, buf, views = self._plan(G, train, key)
-        ops.ext().pack_convs(tab.data_ptr(), len(self.convs), nplain, nplain1, ntrans, lds, theta.data_ptr(),
-                             theta.stride(0), G, buf.data_ptr(), _stream())
+        f = self.fresh.pop(key, None)
+        if f is not None and f == (theta.data_ptr(), theta._version) and not torch.cuda.is_current_stream_capturing():
+            nplain = nplain1 = 0
+        self.fresh.clear()  # an image is only ever reused by the very next pack
+        self.last = (key, theta.data_ptr(), theta.stride(0)) if train else None
+        if nplain or nplain1 or ntrans:
+            ops.ext().pack_convs(tab.data_ptr(), len(self.convs), nplain, nplain1, ntrans, lds, theta.data_ptr(),
+                                 theta.stride(0), G, buf.data_ptr(), _stream())
         for c, (vp, vt) in zip(self.convs, views):
             c.wp = (buf[vp[0]:vp[0] + int(np.prod(vp[1]))].view(vp[1]), G, theta.data_ptr())
             c.wt = (buf[vt[0]:vt[0] + int(np.prod(vt[1]))].view(vt[1]), G, theta.data_ptr()) if vt else None
@@ -730,6 +774,8 @@ class ResNetHipEngine:
 
     def eval_logits(self, theta, bufs, idx, G, B):
         with torch.no_grad():
+            if self.net.packer is not None:
+                self.net.packer.fresh.clear()
             x = self.net.input(self.x8, idx)
             return self.net.eval_logits(theta, x, G).float()
 
@@ -741,14 +787,32 @@ class ResNetHipEngine:
                 self._opt.m = ops.ext()
         return self._opt
 
-    def local_opt(self, theta, grads, mom_buf, spec, lr, wd, momentum, max_norm, lr_dev=None, keep_grad=False):
+    # [PACK-FUSE] the runner may ask the optimizer step to write the next step's forward images (pack_next: the same
+    # rows train again right after, with nothing else touching them in between)
+    fused_pack = True
+
+    def local_opt(self, theta, grads, mom_buf, spec, lr, wd, momentum, max_norm, lr_dev=None, keep_grad=False,
+                  pack_next=False):
         from .executor import HipEngine, TorchEngine
+        pk = self.net.packer
+        if (pack_next and pk is not None and pk.last is not None and _PACK_FUSE
+                and pk.last[1:] == (theta.data_ptr(), theta.stride(0)) and pk.last[0][0] == theta.shape[0]
+                and not torch.cuda.is_current_stream_capturing()):
+            key = pk.last[0]
+            HipEngine.local_opt_pack(self._delegate(), theta, grads, mom_buf, spec, lr, wd, momentum, max_norm,
+                                     pk.fused_plan(key, theta.shape[1]), lr_dev=lr_dev, keep_grad=keep_grad)
+            pk.fresh = {key: (theta.data_ptr(), theta._version)}
+            return
+        if pk is not None:
+            pk.fresh.clear()
         cls = HipEngine if self.net.hip else TorchEngine
         cls.local_opt(self._delegate(), theta, grads, mom_buf, spec, lr, wd, momentum, max_norm, lr_dev=lr_dev,
                       keep_grad=keep_grad)
 
     def saliency_acc(self, theta, grads, score, alpha):
         from .executor import HipEngine, TorchEngine
+        if self.net.packer is not None:
+            self.net.packer.fresh.clear()
         cls = HipEngine if self.net.hip else TorchEngine
         cls.saliency_acc(self._delegate(), theta, grads, score, alpha)
 

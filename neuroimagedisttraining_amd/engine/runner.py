@@ -383,7 +383,8 @@ class FLRunner:
             plan, idx = self._plan(clients, self._epoch_chunks(round_idx, tag, ep))
             main, cur, lanes_used = torch.cuda.current_stream() if side else None, -1, set()
             partial_steps = {it[2] for it in plan if it[6] < cfg.batch_size} if side else ()
-            for r0, r1, s, off, n, G, B in plan:
+            pnext = self._pack_next(plan) if not use_graphs else None
+            for pi, (r0, r1, s, off, n, G, B) in enumerate(plan):
                 if s != cur:  # fork point of this step: main has enqueued every earlier step
                     cur = s
                     fork = main.record_event() if s in partial_steps else None
@@ -405,7 +406,8 @@ class FLRunner:
                                      cids_dev=None if cdev is None else cdev[r0:r1])
                 else:
                     self._seed_dev.fill_(seed)
-                    self._step(sub, r0, idx[off:off + n], G, B, spec.rows(r0, r1), cids, lr)
+                    self._step(sub, r0, idx[off:off + n], G, B, spec.rows(r0, r1), cids, lr,
+                               pack_next=bool(pnext and pnext[pi]))
             for st in lanes_used:
                 main.wait_stream(st)
             self.concurrent_steps = getattr(self, "concurrent_steps", 0) + len(lanes_used)
@@ -555,7 +557,24 @@ class FLRunner:
         k = hash((int(G), int(B))) % len(self._streams)
         return self._streams[k], self._lane_seed[k]
 
-    def _step(self, sub, r0, idx, G, B, spec, cids, lr, seed_dev=None, lr_dev=None, cids_dev=None):
+    def _pack_next(self, plan):
+        """Per plan entry: may its optimizer step write the next step's packed weight images (engines with
+        ``fused_pack``)?  Only when the same rows train again next in this epoch at the same launch shape and no other
+        row group shares that shape (groups of one shape share the image buffer)."""
+        if not getattr(self.e, "fused_pack", False):
+            return None
+        groups = {}
+        for it in plan:
+            groups.setdefault((it[5], it[6]), set()).add(it[0])
+        out, last = [False] * len(plan), {}
+        for i, it in enumerate(plan):
+            j = last.get(it[0])
+            if j is not None:
+                out[j] = plan[j][6] == it[6] and plan[j][1] == it[1] and len(groups[(it[5], it[6])]) == 1
+            last[it[0]] = i
+        return out
+
+    def _step(self, sub, r0, idx, G, B, spec, cids, lr, seed_dev=None, lr_dev=None, cids_dev=None, pack_next=False):
         cfg = self.cfg
         gr = self.grads[r0:r0 + G]
         mo = self.mom_buf[r0:r0 + G] if self.mom_buf is not None else None
@@ -564,8 +583,9 @@ class FLRunner:
                                  seed_dev=self._seed_dev if seed_dev is None else seed_dev, **kw)
         if self.track_loss and self._loss_acc is not None and loss is not None:
             self._loss_acc[r0:r0 + G].add_(loss.view(-1).float())
+        kw = {"pack_next": True} if pack_next else {}
         self.e.local_opt(sub.theta, gr, mo, spec, lr, cfg.wd, cfg.momentum, cfg.max_norm,
-                         lr_dev=self._lr_dev if lr_dev is None else lr_dev)
+                         lr_dev=self._lr_dev if lr_dev is None else lr_dev, **kw)
 
     def _graph_step(self, sub, r0, idx, G, B, spec, cids, seed, fill=True, seed_dev=None, cids_dev=None):
         """One lockstep local step (forward+backward of G clients + fused optimizer) as a replayed hipGraph.  The

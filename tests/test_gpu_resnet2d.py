@@ -315,3 +315,57 @@ def test_fused_cls_head_matches_torch_head(hw, K, G, B, monkeypatch):
     assert da1.dtype == da0.dtype == torch.bfloat16 and da1.shape == da0.shape
     assert _rel(da1, da0) < 1e-2
     assert float(g1[:, :net.lw_off].abs().max()) == 0.0  # nothing outside the head rows written
+
+
+@pytest.mark.parametrize("mask_mode", [0, 1])
+def test_optimizer_written_images_equal_pack(mask_mode):
+    """[PACK-FUSE] local_opt(pack_next=True) (optim.hip k_local_step_pack) updates theta, momentum and gradients bit for
+    bit like the plain step, writes the forward images k_pack_plain would write from the updated rows, and the next
+    step (which skips the plain pack) gives the same loss and gradients."""
+    from neuroimagedisttraining_amd.engine import masks as MK
+    from neuroimagedisttraining_amd.engine.executor import padded_rows
+    from neuroimagedisttraining_amd.engine.resnet2d_hip import ResNetHipEngine, synthetic_cifar
+    from neuroimagedisttraining_amd.engine.runner import StepSpec
+    from neuroimagedisttraining_amd.models import customized_resnet18
+    dev = _dev()
+    torch.manual_seed(3)
+    G, B = 3, 8
+    m = customized_resnet18(class_num=10)
+    x8, y = synthetic_cifar(G * B, seed=2)
+    flat = torch.cat([p.detach().reshape(-1) for p in m.parameters()]).to(dev)
+    out = {}
+    for fused in (False, True):
+        eng = ResNetHipEngine(m, x8, y, dev)
+        P = eng.players.total
+        theta = padded_rows(G, P, dev)
+        theta.copy_(flat.expand(G, -1) + 0.01 * torch.randn(G, P, device=dev, generator=torch.Generator(dev).manual_seed(5)))
+        grads, mom = padded_rows(G, P, dev), padded_rows(G, P, dev)
+        spec = StepSpec()
+        if mask_mode:
+            keep = (torch.rand(G, P, device=dev, generator=torch.Generator(dev).manual_seed(7)) < 0.4).float()
+            spec = StepSpec(mask_mode=1, bits=MK.pack_bits(keep))
+            theta.mul_(keep)
+        idx = torch.arange(G * B, dtype=torch.int32, device=dev)
+        seed = torch.tensor([11], dtype=torch.int64, device=dev)
+        losses = []
+        for step in range(3):
+            losses.append(eng.train_step(theta, None, grads, idx, G, B, 1.0, 1 << 40, seed_dev=seed).clone())
+            eng.local_opt(theta, grads, mom, spec, 0.05, 5e-4, 0.9, 10.0, pack_next=fused and step < 2)
+            if fused and step == 0:  # step 1 then runs on the images written by step 0's optimizer (checked here)
+                pk = eng.net.packer
+                key = pk.last[0]
+                assert key in pk.fresh
+                buf, views = pk._plans[key][4], pk._plans[key][5]
+                fwd = [buf[o:o + int(np.prod(shp))] for (o, shp), _ in views]  # the forward images (not the dgrad)
+                got = [v.clone() for v in fwd]
+                pk.fresh.clear()
+                pk.pack(theta, G, True, key=key)  # the plain pack from the updated rows
+                torch.cuda.synchronize()
+                for li, (a, b) in enumerate(zip(got, fwd)):
+                    assert torch.equal(a, b), (step, li)
+                pk.fresh[key] = (theta.data_ptr(), theta._version)  # restore: the next step reuses the images
+        torch.cuda.synchronize()
+        out[fused] = (theta.clone(), mom.clone(), torch.stack(losses))
+    assert torch.equal(out[False][0], out[True][0])
+    assert torch.equal(out[False][1], out[True][1])
+    assert torch.equal(out[False][2], out[True][2])
