@@ -160,6 +160,8 @@ class GroupedConv:
     """One conv layer of the client-grouped network (weights = rows of theta at ``off``, PyTorch layout
     ``[Cout, cin, k, k]``).  ``cin_p`` = channels of the activation tensor (cin zero-padded to 64)."""
 
+    _keep = []  # tensors read by the weight-gradient branch of the step in flight (released at its join)
+
     def __init__(self, off, cout, cin, k, stride, pad, hip):
         self.off, self.cout, self.cin, self.k, self.stride, self.pad = off, cout, cin, k, stride, pad
         self.kt = k * k
@@ -236,9 +238,9 @@ class GroupedConv:
             self._wgrad(m, x, dy, grads, G, B, H, W, ns, ptab, _stream())
         else:
             ws.wait_stream(torch.cuda.current_stream())
-            x.record_stream(ws)
-            dy.record_stream(ws)
-            ptab.record_stream(ws)
+            # the branch reads x / dy / ptab: they stay referenced until the caller joins the branch (no
+            # record_stream: its deferred frees are not capturable and pile up on large steps)
+            self._keep.extend((x, dy, ptab))
             with torch.cuda.stream(ws):
                 self._wgrad(m, x, dy, grads, G, B, H, W, ns, ptab, _stream())
         st = _stream()
@@ -663,9 +665,8 @@ class GroupedResNet18GN:
     # ------------------------------------------------------------------ train step
     def train_step(self, theta, grads, x, y, G, B):
         a, saved = self.features(x, theta, G, train=True)
-        # NIDT_WGRAD_STREAM=1: weight gradients on a branch forked from the data-gradient chain (joined below); off by
-        # default: CIFAR SubAvg 1.077-1.087 vs 1.069-1.078 s/round, Tiny 2.82 vs 2.19 (profiles/r3_ab_wgrad_stream.txt)
-        ws = self._wgrad_stream(G, B)
+        # weight gradients on a branch forked from the data-gradient chain (joined below), see _wgrad_stream
+        ws = self._wgrad_stream(G, B, x.shape[1] * x.shape[2])
         losses, da = self._head_train(a, theta, grads, y, G, B)
         for blk, sv in zip(reversed(self.blocks), reversed(saved[1:])):
             xin, t1, s1, h1, t2, s2, ts, ss, a = sv
@@ -700,11 +701,22 @@ class GroupedResNet18GN:
         self.stem.bwd(dt0, x0, theta, grads, G, False, ws=ws)
         if ws is not None:
             torch.cuda.current_stream().wait_stream(ws)  # join: the optimizer reads every weight gradient
+            GroupedConv._keep.clear()  # later reuse of their memory on this stream is ordered after the branch
         return losses.detach()
 
-    def _wgrad_stream(self, G, B):
-        """Weight-gradient branch stream of one launch shape (None on CPU or with NIDT_WGRAD_STREAM=0)."""
-        if not self.hip or os.environ.get("NIDT_WGRAD_STREAM", "0") != "1":
+    def _wgrad_stream(self, G, B, HW):
+        """Weight-gradient branch stream of one launch shape, or None (CPU; NIDT_WGRAD_STREAM=0; large steps).
+
+        Measured per shape (profiles/r5_wgrad_stream.txt): with the per-launch host costs gone the overlap pays at
+        CIFAR SubAvg (0.749 -> 0.724 s/round), CIFAR DisPFL (3.785 -> 3.630) and Tiny SubAvg (2.544 -> 2.43), but Tiny
+        DisPFL (100 clients x 16 x 64x64) went 18.6 -> 26-28 s: the branch keeps every step's activations alive until
+        it joins, and at that size the allocator falls back to device frees (measured with record_stream; the branch
+        now holds plain references until the join).  Default: on up to 2^21
+        input positions per step (G*B*H*W); NIDT_WGRAD_STREAM=1 forces it on, =0 off."""
+        env = os.environ.get("NIDT_WGRAD_STREAM", "auto")
+        if not self.hip or env == "0" or (env != "1" and G * B * HW > (1 << 21)):
+            return None
+        if torch.cuda.is_current_stream_capturing():  # captured steps: one stream
             return None
         if not hasattr(self, "_ws"):
             self._ws = {}
