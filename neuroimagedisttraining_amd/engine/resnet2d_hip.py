@@ -414,7 +414,7 @@ class WeightPacker:
         self._plans[fk] = plan
         return plan
 
-    def pack(self, theta, G, train, key=None):
+    def pack(self, theta, G, train, key=None, side=None):
         """Pack every layer for this step and hand each conv its views (``conv.wp`` / ``conv.wt``).  When the previous
         optimizer step wrote this key's forward images from these rows (``fresh``, see :meth:`fused_plan`; the rows
         unchanged since by torch ops: same ``_version``), only the dgrad transposes run."""
@@ -425,7 +425,15 @@ class WeightPacker:
             nplain = nplain1 = 0
         self.fresh.clear()  # an image is only ever reused by the very next pack
         self.last = (key, theta.data_ptr(), theta.stride(0)) if train else None
-        if nplain or nplain1 or ntrans:
+        if side is not None and ntrans:  # forward images here, dgrad transposes on the side stream (caller joins)
+            if nplain or nplain1:
+                ops.ext().pack_convs(tab.data_ptr(), len(self.convs), nplain, nplain1, 0, lds, theta.data_ptr(),
+                                     theta.stride(0), G, buf.data_ptr(), _stream())
+            side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(side):
+                ops.ext().pack_convs(tab.data_ptr(), len(self.convs), 0, 0, ntrans, lds, theta.data_ptr(),
+                                     theta.stride(0), G, buf.data_ptr(), _stream())
+        elif nplain or nplain1 or ntrans:
             ops.ext().pack_convs(tab.data_ptr(), len(self.convs), nplain, nplain1, ntrans, lds, theta.data_ptr(),
                                  theta.stride(0), G, buf.data_ptr(), _stream())
         for c, (vp, vt) in zip(self.convs, views):
@@ -479,9 +487,10 @@ class GroupNormG:
             y = torch.relu(y)
         return y.to(t.dtype), (mean, rstd)
 
-    def bwd(self, dy, mask, t, saved, theta, grads, G):
+    def bwd(self, dy, mask, t, saved, theta, grads, G, ws=None):
         """dy [N, H, W, C] (fp32 or bf16), times (mask > 0) if a mask is given; writes the dgamma/dbeta rows,
-        returns dt in t's dtype."""
+        returns dt in t's dtype.  ``ws``: the step's weight-gradient branch stream — the per-client dgamma/dbeta sum
+        (off the data-gradient chain) is forked onto it."""
         N, H, W, C = t.shape
         B = N // G
         if self.hip:
@@ -493,8 +502,15 @@ class GroupNormG:
             ops.ext().gn_bwd(dy.data_ptr(), int(dy.dtype == torch.bfloat16), m.data_ptr() if m is not None else 0,
                              t.data_ptr(), saved.data_ptr(), theta.data_ptr(), theta.stride(0), self.off_w,
                              dt.data_ptr(), part.data_ptr(), N, B, H * W, C, _stream())
-            ops.ext().gn_param_grads(part.data_ptr(), G, B, C, grads.data_ptr(), grads.stride(0), self.off_w,
-                                     self.off_b, _stream())
+            if ws is None:
+                ops.ext().gn_param_grads(part.data_ptr(), G, B, C, grads.data_ptr(), grads.stride(0), self.off_w,
+                                         self.off_b, _stream())
+                return dt
+            ws.wait_stream(torch.cuda.current_stream())
+            GroupedConv._keep.append(part)
+            with torch.cuda.stream(ws):
+                ops.ext().gn_param_grads(part.data_ptr(), G, B, C, grads.data_ptr(), grads.stride(0), self.off_w,
+                                         self.off_b, _stream())
             return dt
         mean, rstd = saved
         cg = C // GN_GROUPS
@@ -599,12 +615,12 @@ class GroupedResNet18GN:
         logits = (pooled.view(G, B, 1, C) * lw.view(G, 1, self.ncls, C)).sum(-1) + lb.view(G, 1, self.ncls)
         return logits.view(N, self.ncls), pooled, saved
 
-    def features(self, x, theta, G, train=False):
+    def features(self, x, theta, G, train=False, side=None):
         """Stem + the four stages: the final activation map [N, H, W, 512] and the saved tensors of the backward."""
         saved = []
         packed = self.packer is not None
         if packed:
-            self.packer.pack(theta, G, train, key=(G, x.shape[0] // G, train))
+            self.packer.pack(theta, G, train, key=(G, x.shape[0] // G, train), side=side)
         t = self.stem.fwd(x, theta, G, train, packed)
         a, st = self.stem_gn.fwd(t, theta, G, relu=True)
         if train:  # evaluation keeps no activations alive (only the backward reads them)
@@ -664,19 +680,21 @@ class GroupedResNet18GN:
 
     # ------------------------------------------------------------------ train step
     def train_step(self, theta, grads, x, y, G, B):
-        a, saved = self.features(x, theta, G, train=True)
-        # weight gradients on a branch forked from the data-gradient chain (joined below), see _wgrad_stream
+        # the branch stream (see _wgrad_stream) also takes the dgrad-image transposes, overlapped with the forward
         ws = self._wgrad_stream(G, B, x.shape[1] * x.shape[2])
+        a, saved = self.features(x, theta, G, train=True, side=ws)
         losses, da = self._head_train(a, theta, grads, y, G, B)
+        if ws is not None:
+            torch.cuda.current_stream().wait_stream(ws)  # the dgrad images (pack_trans on the branch)
         for blk, sv in zip(reversed(self.blocks), reversed(saved[1:])):
             xin, t1, s1, h1, t2, s2, ts, ss, a = sv
-            dt2 = blk["n2"].bwd(da, a, t2, s2, theta, grads, G)
+            dt2 = blk["n2"].bwd(da, a, t2, s2, theta, grads, G, ws=ws)
             dh1 = blk["c2"].bwd(dt2, h1, theta, grads, G, True, ws=ws)
-            dt1 = blk["n1"].bwd(dh1, h1, t1, s1, theta, grads, G)
+            dt1 = blk["n1"].bwd(dh1, h1, t1, s1, theta, grads, G, ws=ws)
             dx1 = blk["c1"].bwd(dt1, xin, theta, grads, G, True, ws=ws)
             dx2 = None
             if "cs" in blk:
-                dts = blk["ns"].bwd(da, a, ts, ss, theta, grads, G)
+                dts = blk["ns"].bwd(da, a, ts, ss, theta, grads, G, ws=ws)
                 dx2 = blk["cs"].bwd(dts, xin, theta, grads, G, True, ws=ws)
             half = dx2 is not None and blk["cs"].stride == 2  # 1x1 stride-2 projection: even-pixel gradient
             if self.hip:
@@ -697,7 +715,7 @@ class GroupedResNet18GN:
             else:
                 da = dx1.float() + (dx2.float() if dx2 is not None else da * (a > 0))
         x0, t0, st0, a0 = saved[0]
-        dt0 = self.stem_gn.bwd(da, a0, t0, st0, theta, grads, G)
+        dt0 = self.stem_gn.bwd(da, a0, t0, st0, theta, grads, G, ws=ws)
         self.stem.bwd(dt0, x0, theta, grads, G, False, ws=ws)
         if ws is not None:
             torch.cuda.current_stream().wait_stream(ws)  # join: the optimizer reads every weight gradient
@@ -705,16 +723,15 @@ class GroupedResNet18GN:
         return losses.detach()
 
     def _wgrad_stream(self, G, B, HW):
-        """Weight-gradient branch stream of one launch shape, or None (CPU; NIDT_WGRAD_STREAM=0; large steps).
+        """Weight-gradient branch stream of one launch shape, or None (CPU; NIDT_WGRAD_STREAM=0; graph capture).
+        The branch takes the weight gradients, the GroupNorm parameter sums and the dgrad-image transposes (those
+        overlapped with the forward), i.e. everything off the data-gradient chain.
 
-        Measured per shape (profiles/r5_wgrad_stream.txt): with the per-launch host costs gone the overlap pays at
-        CIFAR SubAvg (0.749 -> 0.724 s/round), CIFAR DisPFL (3.785 -> 3.630) and Tiny SubAvg (2.544 -> 2.43), but Tiny
-        DisPFL (100 clients x 16 x 64x64) went 18.6 -> 26-28 s: the branch keeps every step's activations alive until
-        it joins, and at that size the allocator falls back to device frees (measured with record_stream; the branch
-        now holds plain references until the join).  Default: on up to 2^21
-        input positions per step (G*B*H*W); NIDT_WGRAD_STREAM=1 forces it on, =0 off."""
-        env = os.environ.get("NIDT_WGRAD_STREAM", "auto")
-        if not self.hip or env == "0" or (env != "1" and G * B * HW > (1 << 21)):
+        Measured (profiles/r5_wgrad_stream.txt): CIFAR SubAvg 0.749 -> 0.714 s/round, CIFAR DisPFL 3.785 -> 3.59,
+        Tiny SubAvg 2.544 -> 2.435, Tiny DisPFL 18.6 -> 18.4.  (A first version pinned the branch's inputs with
+        record_stream: Tiny DisPFL went to 26-28 s as the deferred frees piled up; the branch now holds plain
+        references until its join.)"""
+        if not self.hip or os.environ.get("NIDT_WGRAD_STREAM", "1") == "0":
             return None
         if torch.cuda.is_current_stream_capturing():  # captured steps: one stream
             return None
