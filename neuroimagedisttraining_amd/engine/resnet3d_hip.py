@@ -37,6 +37,8 @@ BN_MOM = 0.1
 
 _stream = ops.stream
 
+_BRANCH_KEEP = []  # tensors read by the weight-gradient branch of the step in flight (released at its join)
+
 
 def conv_fwd(x_ptr, w_ptr, y_ptr, G, B, D, H, W, Cin, Cout, kt, st, pad, padd, device):
     """Client-grouped conv forward (``conv_fwd_g``), split over the reduction when the output grid is too small to
@@ -226,8 +228,7 @@ class GConv3:
         cur = torch.cuda.current_stream()
         if ws is not None:
             ws.wait_stream(cur)
-            for t in (x, dy, ptab):
-                t.record_stream(ws)
+            _BRANCH_KEEP.extend((x, dy, ptab))  # referenced until the branch joins (no record_stream)
         with torch.cuda.stream(ws if ws is not None else cur):
             part = torch.empty(ns * G * self.cout * self.kt * self.cin, device=x.device, dtype=torch.float32)
             m.conv_wgrad_g(x.data_ptr(), dy.data_ptr(), part.data_ptr(), grads.data_ptr(), grads.stride(0), self.off,
@@ -558,7 +559,7 @@ class GroupedResNet3D:
         # NIDT_WGRAD_STREAM=1: weight gradients on a branch forked from the data-gradient chain (joined after the stem
         # backward); off by default, as in the 2-D engine (profiles/r3_ab_wgrad_stream.txt)
         ws = None
-        if self.hip and os.environ.get("NIDT_WGRAD_STREAM", "0") == "1":
+        if self.hip and os.environ.get("NIDT_WGRAD_STREAM", "0") == "1" and not torch.cuda.is_current_stream_capturing():
             if getattr(self, "_ws", None) is None:
                 self._ws = torch.cuda.Stream(device=self.device)
             ws = self._ws
@@ -596,6 +597,7 @@ class GroupedResNet3D:
             self._stem_hip_bwd(stem, da, theta, grads, G)
             if ws is not None:
                 torch.cuda.current_stream().wait_stream(ws)  # join: the optimizer reads every weight gradient
+                _BRANCH_KEEP.clear()
             return losses.detach()
         out, leaf = stem
         gw, gg, gb = torch.autograd.grad(out, leaf, da.to(out.dtype))
