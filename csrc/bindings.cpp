@@ -60,6 +60,13 @@ int conv3d_fwd_vol_ok(int B, int D, int H, int W, int Cin, int Cout, int pad);
 int conv3d_fwd_vol_pick(int G, int B, int D, int H, int W, int Cin, int Cout, int pad);
 void conv3d_fwd_vol(uintptr_t x, uintptr_t w, uintptr_t bias, int64_t bias_ld, uintptr_t y, uintptr_t stats, int G,
                     int B, int D, int H, int W, int Cin, int Cout, int pad, uintptr_t stream);
+void stream_fork(uintptr_t src, uintptr_t dst);
+int conv2d_fwd_slab_bd_ok(int B, int H, int W, int Cin, int Cout);
+int conv2d_fwd_slab_bd_pick(int G, int B, int H, int W, int Cin, int Cout);
+int conv2d_fwd_slab_bd_table_size(int B, int H, int W);
+void conv2d_fwd_slab_bd_table(uintptr_t tab, int B, int H, int W, uintptr_t stream);
+void conv2d_fwd_slab_bd(uintptr_t x, uintptr_t w, uintptr_t y, int G, int B, int H, int W, int Cin, int Cout,
+                        uintptr_t utab, uintptr_t stream);
 int conv2d_fwd_slab_pick(int G, int B, int H, int W, int Cin, int Cout);
 void conv2d_fwd_slab(uintptr_t x, uintptr_t w, uintptr_t y, int G, int B, int H, int W, int Cin, int Cout,
                      uintptr_t utab, uintptr_t stream);
@@ -256,6 +263,12 @@ PYBIND11_MODULE(_nidt_hip, m) {
   DEF(conv3d_fwd_vol_ok);
   DEF(conv3d_fwd_vol_pick);
   DEF(conv3d_fwd_vol);
+  DEF(stream_fork);
+  DEF(conv2d_fwd_slab_bd_ok);
+  DEF(conv2d_fwd_slab_bd_pick);
+  DEF(conv2d_fwd_slab_bd_table_size);
+  DEF(conv2d_fwd_slab_bd_table);
+  DEF(conv2d_fwd_slab_bd);
   DEF(conv2d_fwd_slab_pick);
   DEF(conv2d_fwd_slab);
   DEF(conv3d_wgrad_tri_nsplit);

@@ -56,6 +56,7 @@ struct ConvFwdArgs {
   // 2oh + bit1(poff), 2ow + bit0(poff)) of the [Dx][Hx][Wx] output (positions outside are skipped)
   int nph = 0, Dx = 0, Hx = 0, Wx = 0;
   unsigned char pnt[8] = {0}, pt0[8] = {0}, poff[8] = {0}, ptap[28] = {0};
+  int kd1 = 0;          // k_conv_fwd_slab: depth tap kd = 1 only (2-D maps batched along depth, conv2d_fwd_slab_bd)
   int dbg = 0;          // timing diagnostics only (NIDT_SLAB_DBG): 1 = k_conv_fwd_slab keeps its first union
 };
 
@@ -757,6 +758,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void k_conv_fwd_slab(ConvFwdArgs a
       kd_hi = min(2, a.D - 1 + a.pad - od_lo);
     }
   }
+  if (a.kd1) kd_lo = kd_hi = 1;
   const int q0 = kd_lo * nck, nq = (kd_hi + 1) * nck - q0, nks = 9 * nq;
   const int lrow = lane >> 3, slot = lane & 7;
   const int fr = lane & 15, fq = lane >> 4;
@@ -1597,10 +1599,13 @@ void conv3d_fwd_slab_table(uintptr_t tab, int B, int D, int H, int W, int pad, u
   NIDT_CHECK(hipGetLastError());
 }
 
+static int slab_bd_u(int B, int H, int W);
+
 static void fwd_slab_impl(uintptr_t x, uintptr_t w, uintptr_t bias, int64_t bias_ld, uintptr_t y, uintptr_t stats,
                           int G, int B, int D, int H, int W, int Cin, int Cout, int pad, int kt, uintptr_t utab,
-                          uintptr_t stream) {
-  NIDT_REQUIRE(conv3d_fwd_slab_ok(B, D, H, W, Cin, Cout, pad) && utab != 0, "conv3d_fwd_slab: shape not supported");
+                          uintptr_t stream, int kd1 = 0) {
+  NIDT_REQUIRE((kd1 ? slab_bd_u(D, H, W) > 0 : conv3d_fwd_slab_ok(B, D, H, W, Cin, Cout, pad)) && utab != 0,
+               "conv3d_fwd_slab: shape not supported");
   NIDT_REQUIRE((int64_t)B * D * H * W * Cin * 2 < (1ll << 31), "conv3d_fwd_slab: per-client input below 2 GiB");
   const bool hb = bias != 0, st = stats != 0;
   NIDT_REQUIRE(!st || hb, "conv3d_fwd_slab: statistics require a bias");
@@ -1618,7 +1623,8 @@ static void fwd_slab_impl(uintptr_t x, uintptr_t w, uintptr_t bias, int64_t bias
     return e ? atoi(e) : 0;
   }();
   a.dbg = slab_dbg;
-  const int bco = fwd_bco(Cout), nCO = Cout / bco;
+  a.kd1 = kd1;
+  const int bco = (kd1 && slab_u(B, D, H, W, pad) == 416) ? 64 : fwd_bco(Cout), nCO = Cout / bco;
   const dim3 grid((unsigned)((int64_t)a.nPB * nCO * G));
   hipStream_t s = as_stream(stream);
   const int* tab = ptr<const int>(utab);
@@ -1700,6 +1706,45 @@ void conv2d_fwd_slab(uintptr_t x, uintptr_t w, uintptr_t y, int G, int B, int H,
                      uintptr_t utab, uintptr_t stream) {
   NIDT_REQUIRE(conv2d_fwd_slab_ok(B, H, W, Cin, Cout), "conv2d_fwd_slab: shape not supported");
   fwd_slab_impl(x, w, 0, 0, y, 0, G, B, 1, H, W, Cin, Cout, 1, 9, utab, stream);
+}
+
+// [SLAB-BD] 2-D 3x3 stride-1 pad-1 convs on maps whose 256-position blocks span several samples (8x8: four samples
+// per block; the CIFAR / Tiny ResNet-18 layer 3 and the 16x16 / 8x8 maps of the Tiny layers): the client's B samples
+// are the depth planes of ONE volume [1][B][H][W] and the conv is the 3-D slab conv restricted to depth tap kd = 1
+// (k_conv_fwd_slab with a.kd1): plane d reads only plane d, i.e. each sample's own 2-D conv, and one union of
+// consecutive whole padded planes (4 x 100 rows for 8x8 maps) serves the block's nine taps.  Eligible when the union
+// fits (416 rows: 64-channel blocks).
+static int slab_bd_u(int B, int H, int W) {
+  if (B + 2 >= 1024 || H + 2 >= 1024 || W + 2 >= 1024) return 0;
+  return slab_u(1, B, H, W, 1);
+}
+
+int conv2d_fwd_slab_bd_ok(int B, int H, int W, int Cin, int Cout) {
+  return (Cin % 64 == 0 && Cout % 64 == 0 && Cin <= kMaxCin && (H * W) % 256 != 0 && slab_bd_u(B, H, W) > 0) ? 1 : 0;
+}
+
+// Chosen for every eligible shape: CIFAR layer-3 convs 0.158 -> 0.129 ms at 100 clients x 16, 0.625 -> 0.502 ms at
+// 100 x 62 (764 -> 934 TF/s), 0.032 -> 0.031 at 10 x 16 (tools/bench_conv2d.py, profiles/r5_slab_bd.txt).
+// NIDT_2D_SLAB_BD=0 keeps the per-tap kernel (A/B)
+int conv2d_fwd_slab_bd_pick(int G, int B, int H, int W, int Cin, int Cout) {
+  static const int env = [] {
+    const char* e = getenv("NIDT_2D_SLAB_BD");
+    return e ? atoi(e) : 1;
+  }();
+  (void)G;
+  return env && conv2d_fwd_slab_bd_ok(B, H, W, Cin, Cout) ? 1 : 0;
+}
+
+int conv2d_fwd_slab_bd_table_size(int B, int H, int W) { return conv3d_fwd_slab_table_size(1, B, H, W, 1); }
+
+void conv2d_fwd_slab_bd_table(uintptr_t tab, int B, int H, int W, uintptr_t stream) {
+  conv3d_fwd_slab_table(tab, 1, B, H, W, 1, stream);
+}
+
+void conv2d_fwd_slab_bd(uintptr_t x, uintptr_t w, uintptr_t y, int G, int B, int H, int W, int Cin, int Cout,
+                        uintptr_t utab, uintptr_t stream) {
+  NIDT_REQUIRE(conv2d_fwd_slab_bd_ok(B, H, W, Cin, Cout), "conv2d_fwd_slab_bd: shape not supported");
+  fwd_slab_impl(x, w, 0, 0, y, 0, G, 1, B, H, W, Cin, Cout, 1, 9, utab, stream, 1);
 }
 
 // ---- k_conv_fwd_vol host side (whole padded sample <= 448 rows, <= 256 output positions per sample) ----

@@ -570,6 +570,15 @@ class SubAvgRunner(PersonalizedRunner):
         self.record_avg_inference_flops(self.mbits[:self.C] if self.C else self.mbits[:0])
         return super().finish()
 
+    def _record_subavg(self, round_idx, r):
+        sl = dict.__getitem__  # the raw lists (called from the metric flush too)
+        acc, loss = self.mean_acc_loss(r)
+        sl(self.stat_info, "test_acc").append(acc)
+        sl(self.stat_info, "person_test_acc").append(acc)
+        if self.log is not None and self.info.is_main:
+            self.log.info({"test_acc": acc, "test_loss": loss})
+        return {"test_acc": acc, "test_loss": loss}
+
     def _real_prune_rows(self, rs, rows, bits_rows):
         ix = self._to_dev(rows)
         rs.theta[ix, :self.P] = rs.theta[ix, :self.P] * MK.unpack_bits(bits_rows, self.P)
@@ -588,8 +597,7 @@ class SubAvgRunner(PersonalizedRunner):
             self.theta[ix] = self.w_global.unsqueeze(0).expand(len(rows), -1)
             self.bufs[ix] = self.b_global.unsqueeze(0).expand(len(rows), -1)
             self._real_prune_rows(self.rowset, rows, old_bits)  # w_per = real_prune(w_global, mask)
-            nz_dev = self.state_nonzeros(self.theta, self.bufs, rows)
-            dense = nz_dev.cpu().numpy() / float(self.P + self.Q)  # print_pruning over the whole state
+            nz_dev = self.state_nonzeros(self.theta, self.bufs, rows)  # print_pruning over the whole state
             self.add_comm(nz_dev)
 
             def hook(ep, view, clients):  # fake_prune after the first and the last epoch (the training masks)
@@ -602,7 +610,9 @@ class SubAvgRunner(PersonalizedRunner):
             spec = StepSpec(mask_mode=MASK_GRAD, bits=self.mbits)
             self.train_rows(self.rowset, rows, loc, round_idx, cfg.epochs, spec, epoch_hook=hook)
             m1, m2 = hooks["m1"], hooks["m2"]
-            ham = self.mspace.hamming(m1, m2).double().cpu().numpy()
+            # one host read after training for both (a read before it drained the device at every round start)
+            hd = torch.cat([nz_dev.double().view(-1, 1), self.mspace.hamming(m1, m2).double()], 1).cpu().numpy()
+            dense, ham = hd[:, 0] / float(self.P + self.Q), hd[:, 1:]
             dist = (ham / self.mspace.seg_len[None, :]).mean(1)  # mean over every parameter (scipy hamming)
             cand = [j for j in range(len(rows)) if dist[j] > cfg.dist_thresh and dense[j] > cfg.dense_ratio]
             final_bits = old_bits.clone()
@@ -643,10 +653,15 @@ class SubAvgRunner(PersonalizedRunner):
             bu.copy_(self.b_global.expand_as(bu))
             if self.C:
                 th[:self.C, :self.P].mul_(MK.unpack_bits(self.mbits[:self.C], self.P))
-            r = self.eval_local(RowSet(th, bu), *self.all_rows())
-            acc, loss = self.log_test(r, "test_acc")
-            self.stat_info["person_test_acc"].append(acc)
-            res = {"test_acc": acc, "test_loss": loss}
+            if self._defer_metrics():  # read one round late (no end-of-round device drain; see FLRunner.evaluate)
+                self._flush_metrics(ready_only=True)
+                rows_e, clients_e = self.all_rows()
+                loc = (self.eval_grouped(th, bu, rows_e, clients_e, "test", device_out=True) if rows_e
+                       else torch.zeros((0, 3), dtype=torch.float64, device=self.device))
+                res = self._defer_result(round_idx, self.gather_metrics(clients_e, loc, device_out=True),
+                                         self._record_subavg)
+            else:
+                res = self._record_subavg(round_idx, self.eval_local(RowSet(th, bu), *self.all_rows()))
         if rows:
             self.mbits[ix] = final_bits
         self.timers["train"] += t1 - t0

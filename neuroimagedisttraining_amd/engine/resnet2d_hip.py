@@ -50,6 +50,23 @@ GN_EPS = 1e-5
 
 
 _stream = ops.stream
+_EXT = {}
+
+
+def _external(ptr):
+    """torch stream object of a raw handle (cached): for the few torch ops a side branch issues."""
+    s = _EXT.get(ptr)
+    if s is None:
+        s = _EXT[ptr] = torch.cuda.ExternalStream(ptr)
+    return s
+
+
+class _nullctx:
+    def __enter__(self):
+        return None
+
+    def __exit__(self, *a):
+        return False
 
 
 # ------------------------------------------------------------------------------------------------ augmentation
@@ -118,7 +135,19 @@ def slab_conv2d(x_ptr, w_ptr, y_ptr, G, B, H, W, Cin, Cout, device):
     (B, H, W)."""
     m = ops.ext()
     if not m.conv2d_fwd_slab_pick(G, B, H, W, Cin, Cout):
-        return False
+        if not m.conv2d_fwd_slab_bd_pick(G, B, H, W, Cin, Cout):
+            return False
+        # [SLAB-BD] maps whose blocks span several samples: the samples as the depth planes of one volume
+        key = ("bd", str(device), B, H, W)
+        tab = _SLAB_TABS.get(key)
+        if tab is None:
+            tab = torch.empty(m.conv2d_fwd_slab_bd_table_size(B, H, W), device=device, dtype=torch.int32)
+            m.conv2d_fwd_slab_bd_table(tab.data_ptr(), B, H, W, _stream())
+            if not torch.cuda.is_current_stream_capturing():
+                torch.cuda.current_stream().synchronize()
+                _SLAB_TABS[key] = tab
+        m.conv2d_fwd_slab_bd(x_ptr, w_ptr, y_ptr, G, B, H, W, Cin, Cout, tab.data_ptr(), _stream())
+        return True
     key = (str(device), B, H, W)
     tab = _SLAB_TABS.get(key)
     if tab is None:
@@ -223,7 +252,7 @@ class GroupedConv:
     def bwd(self, dy, x, theta, grads, G, need_dx, scratch=None, ws=None):
         """dW -> grads rows (PyTorch layout at ``off``); returns dX ``[N, H, W, cin_p]`` (or None).  For the 1x1
         stride-2 projection the returned gradient is the half-resolution one of the even pixels (``res_grad_s2``
-        adds it into the residual stream).  ``ws``: stream of the step's weight-gradient branch — the wgrad is
+        adds it into the residual stream).  ``ws``: raw handle of the step's weight-gradient branch stream — the wgrad is
         forked onto it (the caller joins it before the optimizer) and only the data gradient stays on the chain."""
         if not self.hip:
             return self._torch_bwd(dy, x, theta, grads, G, need_dx)
@@ -234,15 +263,14 @@ class GroupedConv:
         dy = dy.contiguous()
         ns = m.conv_wgrad_nsplit_g(G, B, 1, H, W, self.cin_p, self.cout, self.kt, self.stride, self.pad, 0)
         ptab = self._pos_table(B, H, W, Ho, Wo, x.device)
-        if ws is None:  # no branch: the whole backward on the current stream (no stream objects per launch)
+        if ws is None:  # no branch: the whole backward on the current stream
             self._wgrad(m, x, dy, grads, G, B, H, W, ns, ptab, _stream())
         else:
-            ws.wait_stream(torch.cuda.current_stream())
-            # the branch reads x / dy / ptab: they stay referenced until the caller joins the branch (no
+            # the branch (raw stream ws) reads x / dy / ptab: they stay referenced until the caller joins it (no
             # record_stream: its deferred frees are not capturable and pile up on large steps)
+            m.stream_fork(_stream(), ws)
             self._keep.extend((x, dy, ptab))
-            with torch.cuda.stream(ws):
-                self._wgrad(m, x, dy, grads, G, B, H, W, ns, ptab, _stream())
+            self._wgrad(m, x, dy, grads, G, B, H, W, ns, ptab, ws)
         st = _stream()
         if not need_dx:
             return None
@@ -275,7 +303,10 @@ class GroupedConv:
         return sub
 
     def _wgrad(self, m, x, dy, grads, G, B, H, W, ns, ptab, st):
+        branch = st != _stream()
         part = torch.empty(ns * G * self.cout * self.kt * self.cin_p, device=x.device, dtype=torch.float32)
+        if branch:  # allocated on the main stream's pool, used on the branch: held until the join
+            self._keep.append(part)
         if self.cin_p == self.cin:
             m.conv_wgrad_g(x.data_ptr(), dy.data_ptr(), part.data_ptr(), grads.data_ptr(), grads.stride(0),
                            self.off, G, B, 1, H, W, self.cin_p, self.cout, self.kt, self.stride, self.pad, 0, ns,
@@ -285,8 +316,11 @@ class GroupedConv:
             m.conv_wgrad_g(x.data_ptr(), dy.data_ptr(), part.data_ptr(), full.data_ptr(), full.stride(0), 0, G, B,
                            1, H, W, self.cin_p, self.cout, self.kt, self.stride, self.pad, 0, ns, 1.0,
                            ptab.data_ptr(), st)
-            grads[:, self.off:self.off + self.numel].view(G, self.cout, self.cin, self.kt).copy_(
-                full.view(G, self.cout, self.cin_p, self.kt)[:, :, :self.cin])
+            if branch:
+                self._keep.append(full)
+            with torch.cuda.stream(_external(st)) if branch else _nullctx():
+                grads[:, self.off:self.off + self.numel].view(G, self.cout, self.cin, self.kt).copy_(
+                    full.view(G, self.cout, self.cin_p, self.kt)[:, :, :self.cin])
 
     def _pos_table(self, B, H, W, Ho, Wo, device):
         """Output-position table of the wgrad kernel: a function of the shape only, built once per (B, H, W) outside
@@ -429,10 +463,9 @@ class WeightPacker:
             if nplain or nplain1:
                 ops.ext().pack_convs(tab.data_ptr(), len(self.convs), nplain, nplain1, 0, lds, theta.data_ptr(),
                                      theta.stride(0), G, buf.data_ptr(), _stream())
-            side.wait_stream(torch.cuda.current_stream())
-            with torch.cuda.stream(side):
-                ops.ext().pack_convs(tab.data_ptr(), len(self.convs), 0, 0, ntrans, lds, theta.data_ptr(),
-                                     theta.stride(0), G, buf.data_ptr(), _stream())
+            ops.ext().stream_fork(_stream(), side)
+            ops.ext().pack_convs(tab.data_ptr(), len(self.convs), 0, 0, ntrans, lds, theta.data_ptr(),
+                                 theta.stride(0), G, buf.data_ptr(), side)
         elif nplain or nplain1 or ntrans:
             ops.ext().pack_convs(tab.data_ptr(), len(self.convs), nplain, nplain1, ntrans, lds, theta.data_ptr(),
                                  theta.stride(0), G, buf.data_ptr(), _stream())
@@ -489,7 +522,7 @@ class GroupNormG:
 
     def bwd(self, dy, mask, t, saved, theta, grads, G, ws=None):
         """dy [N, H, W, C] (fp32 or bf16), times (mask > 0) if a mask is given; writes the dgamma/dbeta rows,
-        returns dt in t's dtype.  ``ws``: the step's weight-gradient branch stream — the per-client dgamma/dbeta sum
+        returns dt in t's dtype.  ``ws``: raw handle of the weight-gradient branch stream — the per-client dgamma/dbeta sum
         (off the data-gradient chain) is forked onto it."""
         N, H, W, C = t.shape
         B = N // G
@@ -506,11 +539,10 @@ class GroupNormG:
                 ops.ext().gn_param_grads(part.data_ptr(), G, B, C, grads.data_ptr(), grads.stride(0), self.off_w,
                                          self.off_b, _stream())
                 return dt
-            ws.wait_stream(torch.cuda.current_stream())
+            ops.ext().stream_fork(_stream(), ws)
             GroupedConv._keep.append(part)
-            with torch.cuda.stream(ws):
-                ops.ext().gn_param_grads(part.data_ptr(), G, B, C, grads.data_ptr(), grads.stride(0), self.off_w,
-                                         self.off_b, _stream())
+            ops.ext().gn_param_grads(part.data_ptr(), G, B, C, grads.data_ptr(), grads.stride(0), self.off_w,
+                                     self.off_b, ws)
             return dt
         mean, rstd = saved
         cg = C // GN_GROUPS
@@ -685,7 +717,7 @@ class GroupedResNet18GN:
         a, saved = self.features(x, theta, G, train=True, side=ws)
         losses, da = self._head_train(a, theta, grads, y, G, B)
         if ws is not None:
-            torch.cuda.current_stream().wait_stream(ws)  # the dgrad images (pack_trans on the branch)
+            ops.ext().stream_fork(ws, _stream())  # the dgrad images (pack_trans on the branch)
         for blk, sv in zip(reversed(self.blocks), reversed(saved[1:])):
             xin, t1, s1, h1, t2, s2, ts, ss, a = sv
             dt2 = blk["n2"].bwd(da, a, t2, s2, theta, grads, G, ws=ws)
@@ -718,7 +750,7 @@ class GroupedResNet18GN:
         dt0 = self.stem_gn.bwd(da, a0, t0, st0, theta, grads, G, ws=ws)
         self.stem.bwd(dt0, x0, theta, grads, G, False, ws=ws)
         if ws is not None:
-            torch.cuda.current_stream().wait_stream(ws)  # join: the optimizer reads every weight gradient
+            ops.ext().stream_fork(ws, _stream())  # join: the optimizer reads every weight gradient
             GroupedConv._keep.clear()  # later reuse of their memory on this stream is ordered after the branch
         return losses.detach()
 
@@ -739,7 +771,7 @@ class GroupedResNet18GN:
             self._ws = {}
         if (G, B) not in self._ws:
             self._ws[(G, B)] = torch.cuda.Stream(device=self.device)
-        return self._ws[(G, B)]
+        return self._ws[(G, B)].cuda_stream  # raw handle: forks / joins through ops.stream_fork
 
     def eval_logits(self, theta, x, G):
         logits, _, _ = self.forward(x, theta, G)

@@ -87,7 +87,7 @@ class StatInfo(dict):
     still in flight (:meth:`FLRunner._flush_metrics`), so every consumer sees the complete, ordered lists while a timed
     GPU loop never waits for a metric."""
 
-    DEFERRED = ("global_test_acc", "global_test_loss", "person_test_acc", "person_test_loss")
+    DEFERRED = ("global_test_acc", "global_test_loss", "person_test_acc", "person_test_loss", "test_acc")
 
     def __init__(self, flush, *a, **kw):
         super().__init__(*a, **kw)
@@ -1303,12 +1303,30 @@ class FLRunner:
         while self._pending_metrics:
             if ready_only and self._pending_metrics[0][2] is not None and not self._pending_metrics[0][2].query():
                 break
-            round_idx, host, ev, holder = self._pending_metrics.pop(0)
+            round_idx, host, ev, holder, *rec = self._pending_metrics.pop(0)
             if ev is not None:
                 ev.synchronize()
-            holder["res"] = self._record_metrics(round_idx, host.numpy().copy())
+            holder["res"] = (rec[0] if rec else self._record_metrics)(round_idx, host.numpy().copy())
             if ev is not None:
                 self._pinned_free.append(host)
+
+    def _defer_result(self, round_idx, r, recorder=None):
+        """Queue the device metric matrix ``r`` of a round: a pinned copy + event now, folded into ``stat_info`` by
+        ``recorder(round_idx, host_matrix)`` (default :meth:`_record_metrics`) when first looked at."""
+        if self.device.type == "cuda":
+            host = next((h for h in self._pinned_free if h.shape == r.shape), None)
+            if host is not None:
+                self._pinned_free.remove(host)
+            else:
+                host = torch.empty(r.shape, dtype=r.dtype, pin_memory=True)
+            host.copy_(r, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+        else:  # NIDT_DEFER_METRICS=force on the CPU (tests of the deferred bookkeeping)
+            host, ev = r.clone(), None
+        holder = {}
+        self._pending_metrics.append((round_idx, host, ev, holder) + ((recorder,) if recorder else ()))
+        return LazyMetrics(self, holder)
 
     def _record_metrics(self, round_idx, r):
         sl = dict.__getitem__  # the raw lists: this IS the flush
@@ -1334,21 +1352,8 @@ class FLRunner:
             else:
                 loc = torch.zeros((0, 6), dtype=torch.float64, device=self.device)
             r = self.gather_metrics(self.local, loc, device_out=True)
-            if self.device.type == "cuda":
-                host = next((h for h in self._pinned_free if h.shape == r.shape), None)
-                if host is not None:
-                    self._pinned_free.remove(host)
-                else:
-                    host = torch.empty(r.shape, dtype=r.dtype, pin_memory=True)
-                host.copy_(r, non_blocking=True)
-                ev = torch.cuda.Event()
-                ev.record()
-            else:  # NIDT_DEFER_METRICS=force on the CPU (tests of the deferred bookkeeping)
-                host, ev = r.clone(), None
-            holder = {}
-            self._pending_metrics.append((round_idx, host, ev, holder))
             self.timers["eval"] += time.perf_counter() - t0
-            return LazyMetrics(self, holder)
+            return self._defer_result(round_idx, r)
         glob, pers = self._eval_global_and_personal(theta, bufs) if self.C else (np.zeros((0, 3)), np.zeros((0, 3)))
         r = self.gather_metrics(self.local, np.concatenate([glob, pers], 1))
         self._flush_metrics()

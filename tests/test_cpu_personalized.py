@@ -461,3 +461,19 @@ def test_padded_bucket_eval_equals_exact_grouping(monkeypatch):
         assert np.array_equal(a[:, 2], np.array(test_sizes, dtype=np.float64))
         assert np.allclose(a, b, rtol=1e-5, atol=1e-5), (a, b)
     assert [r._pad_size(n) for n in (1, 8, 9, 64, 65, 100, 1000)] == [8, 8, 16, 64, 77, 108, 1024]
+
+
+def test_subavg_deferred_metrics_match_immediate(monkeypatch):
+    """SubAvg's evaluation read one round late (NIDT_DEFER_METRICS=force on the CPU) gives the same rounds' results,
+    stat_info lists and model rows as the immediate read."""
+    out = {}
+    for mode in ("0", "force"):
+        monkeypatch.setenv("NIDT_DEFER_METRICS", mode)
+        r = _runner("subavg")
+        res = [r.run_round(k) for k in range(2)]
+        out[mode] = ([dict(x) if x is not None else None for x in res], _collect(r))
+    (ra, ca), (rb, cb) = out["0"], out["force"]
+    assert ra == rb
+    assert ca["stats"] == cb["stats"] and ca["stats"].get("test_acc")
+    for c in ca["rows"]:
+        assert torch.equal(ca["rows"][c], cb["rows"][c])

@@ -33,6 +33,13 @@ def main():
             res["pertap"] = timeit(lambda: R.conv_fwd(x.data_ptr(), w.data_ptr(), y.data_ptr(), G, B, 1, H, H, C, C, 9,
                                                       1, 1, 0, dev))
             ref = y.clone()
+            if m.conv2d_fwd_slab_bd_ok(B, H, H, C, C):  # samples as depth planes (tools: always timed when eligible)
+                tab = torch.empty(m.conv2d_fwd_slab_bd_table_size(B, H, H), device=dev, dtype=torch.int32)
+                m.conv2d_fwd_slab_bd_table(tab.data_ptr(), B, H, H, ops.stream())
+                y.zero_()
+                res["slab_bd"] = timeit(lambda: m.conv2d_fwd_slab_bd(x.data_ptr(), w.data_ptr(), y.data_ptr(), G, B, H, H,
+                                                                     C, C, tab.data_ptr(), ops.stream()))
+                row += "  [bd vs pertap rel %.1e]" % float((y.float() - ref.float()).norm() / ref.float().norm())
             res["any"] = timeit(lambda: m.conv2d_any_fwd(x.data_ptr(), w.data_ptr(), 0, y.data_ptr(), G, B, H, H, C, C,
                                                          C, 3, 1, ops.stream()))
             err = float((y.float() - ref.float()).norm() / ref.float().norm())

@@ -1,0 +1,17 @@
+#!/bin/bash
+# raw-stream branch forks + batched-depth slab default: resnet2d GPU tests, CIFAR benches, SubAvg round timeline
+set -o pipefail
+export PYTHONUNBUFFERED=1
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+OUT=gpurun_out/r5m2; mkdir -p $OUT
+timeout -k 10 400 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_resnet2d.py > $OUT/pytest.txt 2>&1 || { grep -E "Error|assert|FAILED|passed|failed" $OUT/pytest.txt | tail -20; exit 1; }
+tail -1 $OUT/pytest.txt
+for cfg in "cifar10 subavg" "cifar10 dispfl"; do
+  set -- $cfg
+  timeout -k 10 400 python -u tools/bench_cifar.py --dataset $1 --algorithm $2 --rounds 2 --warmup 1 > $OUT/$1_$2.txt 2>&1 || { tail -20 $OUT/$1_$2.txt; exit 1; }
+  echo "== $1 $2 $(tail -1 $OUT/$1_$2.txt | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["s_round_each"], d.get("last_round_metrics"))')"
+done
+timeout -k 10 400 rocprofv3 --kernel-trace -d /tmp/sprof -o run -- python3 -u tools/bench_cifar.py --algorithm subavg --rounds 1 --warmup 1 > $OUT/subavg_prof.txt 2>&1 || { tail -20 $OUT/subavg_prof.txt; exit 1; }
+db=$(find /tmp/sprof -name "*.db" | head -1)
+python3 tools/prof_summary.py "$db" $OUT/subavg_kernels.txt --top 45 --window-ms 700 > /dev/null 2>&1
+grep -E "TOTAL|TIMELINE" $OUT/subavg_kernels.txt
