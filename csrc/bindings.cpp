@@ -63,8 +63,8 @@ void conv3d_fwd_vol(uintptr_t x, uintptr_t w, uintptr_t bias, int64_t bias_ld, u
 void stream_fork(uintptr_t src, uintptr_t dst);
 int conv2d_fwd_slab_bd_ok(int B, int H, int W, int Cin, int Cout);
 int conv2d_fwd_slab_bd_pick(int G, int B, int H, int W, int Cin, int Cout);
-int conv2d_fwd_slab_bd_table_size(int B, int H, int W);
-void conv2d_fwd_slab_bd_table(uintptr_t tab, int B, int H, int W, uintptr_t stream);
+int conv2d_fwd_slab_bd_table_size(int B, int H, int W, int Cin, int Cout);
+void conv2d_fwd_slab_bd_table(uintptr_t tab, int B, int H, int W, int Cin, int Cout, uintptr_t stream);
 void conv2d_fwd_slab_bd(uintptr_t x, uintptr_t w, uintptr_t y, int G, int B, int H, int W, int Cin, int Cout,
                         uintptr_t utab, uintptr_t stream);
 int conv2d_fwd_slab_pick(int G, int B, int H, int W, int Cin, int Cout);

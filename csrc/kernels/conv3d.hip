@@ -1599,13 +1599,15 @@ void conv3d_fwd_slab_table(uintptr_t tab, int B, int D, int H, int W, int pad, u
   NIDT_CHECK(hipGetLastError());
 }
 
-static int slab_bd_u(int B, int H, int W);
+static int slab_bd_u(int B, int H, int W, int bp = 256);
 
 static void fwd_slab_impl(uintptr_t x, uintptr_t w, uintptr_t bias, int64_t bias_ld, uintptr_t y, uintptr_t stats,
                           int G, int B, int D, int H, int W, int Cin, int Cout, int pad, int kt, uintptr_t utab,
-                          uintptr_t stream, int kd1 = 0) {
-  NIDT_REQUIRE((kd1 ? slab_bd_u(D, H, W) > 0 : conv3d_fwd_slab_ok(B, D, H, W, Cin, Cout, pad)) && utab != 0,
+                          uintptr_t stream, int kd1 = 0, int bp = 256) {
+  NIDT_REQUIRE((kd1 ? slab_bd_u(D, H, W, bp) > 0 : conv3d_fwd_slab_ok(B, D, H, W, Cin, Cout, pad)) && utab != 0,
                "conv3d_fwd_slab: shape not supported");
+  NIDT_REQUIRE(bp == 256 || (bp == 128 && kd1 && !bias && !stats && Cout % 128 == 0),
+               "conv3d_fwd_slab: 128-position blocks only for the depth-batched 2-D form, 128-channel blocks");
   NIDT_REQUIRE((int64_t)B * D * H * W * Cin * 2 < (1ll << 31), "conv3d_fwd_slab: per-client input below 2 GiB");
   const bool hb = bias != 0, st = stats != 0;
   NIDT_REQUIRE(!st || hb, "conv3d_fwd_slab: statistics require a bias");
@@ -1615,7 +1617,7 @@ static void fwd_slab_impl(uintptr_t x, uintptr_t w, uintptr_t bias, int64_t bias
   a.B = B; a.D = D; a.H = H; a.W = W; a.Cin = Cin; a.Cout = Cout; a.pad = pad; a.padd = pad; a.kt = kt; a.st = 1;
   a.Do = D + 2 * pad - 2; a.Ho = H + 2 * pad - 2; a.Wo = W + 2 * pad - 2;
   a.Mg = B * a.Do * a.Ho * a.Wo;
-  a.nPB = ceil_div(a.Mg, 256);
+  a.nPB = ceil_div(a.Mg, bp);
   a.G = G;
   a.bias_ld = bias_ld;
   static const int slab_dbg = [] {  // timing diagnostics only (wrong results): NIDT_SLAB_DBG=1 skips union reloads
@@ -1624,6 +1626,14 @@ static void fwd_slab_impl(uintptr_t x, uintptr_t w, uintptr_t bias, int64_t bias
   }();
   a.dbg = slab_dbg;
   a.kd1 = kd1;
+  if (bp == 128) {  // [SLAB-BD] 128-position bands (4x4 maps: 8 padded samples = 288 union rows)
+    const int nCO = Cout / 128;
+    const dim3 grid((unsigned)((int64_t)a.nPB * nCO * G));
+    hipLaunchKernelGGL((k_conv_fwd_slab<128, 2, 2, 384, true, false, false, false>), grid, dim3(256), 0,
+                       as_stream(stream), a, nCO, ptr<const int>(utab));
+    NIDT_CHECK(hipGetLastError());
+    return;
+  }
   const int bco = (kd1 && slab_u(B, D, H, W, pad) == 416) ? 64 : fwd_bco(Cout), nCO = Cout / bco;
   const dim3 grid((unsigned)((int64_t)a.nPB * nCO * G));
   hipStream_t s = as_stream(stream);
@@ -1714,37 +1724,67 @@ void conv2d_fwd_slab(uintptr_t x, uintptr_t w, uintptr_t y, int G, int B, int H,
 // (k_conv_fwd_slab with a.kd1): plane d reads only plane d, i.e. each sample's own 2-D conv, and one union of
 // consecutive whole padded planes (4 x 100 rows for 8x8 maps) serves the block's nine taps.  Eligible when the union
 // fits (416 rows: 64-channel blocks).
-static int slab_bd_u(int B, int H, int W) {
+// bp = 256: the slab kernel's union sizes (384 / 416 rows); bp = 128 (4x4 maps, 128-channel blocks): <= 384 rows
+static int slab_bd_u(int B, int H, int W, int bp) {
   if (B + 2 >= 1024 || H + 2 >= 1024 || W + 2 >= 1024) return 0;
+  if (bp == 128) return union_umax(1, B, H, W, 1, 128, slab_ext(W, 1)) <= 384 ? 384 : 0;
   return slab_u(1, B, H, W, 1);
 }
 
-int conv2d_fwd_slab_bd_ok(int B, int H, int W, int Cin, int Cout) {
-  return (Cin % 64 == 0 && Cout % 64 == 0 && Cin <= kMaxCin && (H * W) % 256 != 0 && slab_bd_u(B, H, W) > 0) ? 1 : 0;
+// block positions of the depth-batched form for a shape (256, 128, or 0 = not eligible)
+static int slab_bd_bp(int B, int H, int W, int Cin, int Cout) {
+  if (Cin % 64 != 0 || Cout % 64 != 0 || Cin > kMaxCin || (H * W) % 256 == 0) return 0;
+  if (slab_bd_u(B, H, W, 256) > 0) return 256;
+  return (Cout % 128 == 0 && slab_bd_u(B, H, W, 128) > 0) ? 128 : 0;
 }
 
-// Chosen for every eligible shape: CIFAR layer-3 convs 0.158 -> 0.129 ms at 100 clients x 16, 0.625 -> 0.502 ms at
-// 100 x 62 (764 -> 934 TF/s), 0.032 -> 0.031 at 10 x 16 (tools/bench_conv2d.py, profiles/r5_slab_bd.txt).
+int conv2d_fwd_slab_bd_ok(int B, int H, int W, int Cin, int Cout) { return slab_bd_bp(B, H, W, Cin, Cout) > 0 ? 1 : 0; }
+
+// Chosen for every eligible 256-position shape: CIFAR layer-3 convs 0.158 -> 0.129 ms at 100 clients x 16, 0.625 ->
+// 0.502 ms at 100 x 62 (764 -> 934 TF/s), 0.032 -> 0.031 at 10 x 16; the 128-position form (4x4 maps) from 512 blocks
+// (tools/bench_conv2d.py, profiles/r5_slab_bd.txt).
 // NIDT_2D_SLAB_BD=0 keeps the per-tap kernel (A/B)
 int conv2d_fwd_slab_bd_pick(int G, int B, int H, int W, int Cin, int Cout) {
   static const int env = [] {
     const char* e = getenv("NIDT_2D_SLAB_BD");
     return e ? atoi(e) : 1;
   }();
-  (void)G;
-  return env && conv2d_fwd_slab_bd_ok(B, H, W, Cin, Cout) ? 1 : 0;
+  const int bp = env ? slab_bd_bp(B, H, W, Cin, Cout) : 0;
+  if (bp == 128) {  // one 8-wave block per band and 128 channels: small grids lose to the per-tap kernel's split-K
+    // (4x4 maps at 10 clients x 16: 0.041 -> 0.062 ms; at 100 x 16: 0.193 -> 0.177; 100 x 62: 0.615 -> 0.548)
+    const int64_t blocks = (int64_t)ceil_div(B * H * W, 128) * (Cout / 128) * G;
+    return blocks >= 512 ? 1 : 0;
+  }
+  return bp > 0 ? 1 : 0;
 }
 
-int conv2d_fwd_slab_bd_table_size(int B, int H, int W) { return conv3d_fwd_slab_table_size(1, B, H, W, 1); }
+// union tables per (B, H, W, block positions): the caller passes the Cin / Cout of the layer so the same blocking is
+// chosen here and in conv2d_fwd_slab_bd
+int conv2d_fwd_slab_bd_table_size(int B, int H, int W, int Cin, int Cout) {
+  const int bp = slab_bd_bp(B, H, W, Cin, Cout);
+  NIDT_REQUIRE(bp > 0, "conv2d_fwd_slab_bd_table_size: shape not eligible");
+  if (bp == 256) return conv3d_fwd_slab_table_size(1, B, H, W, 1);
+  return ceil_div(B * H * W, 128) * (2 * 384 + 128);
+}
 
-void conv2d_fwd_slab_bd_table(uintptr_t tab, int B, int H, int W, uintptr_t stream) {
-  conv3d_fwd_slab_table(tab, 1, B, H, W, 1, stream);
+void conv2d_fwd_slab_bd_table(uintptr_t tab, int B, int H, int W, int Cin, int Cout, uintptr_t stream) {
+  const int bp = slab_bd_bp(B, H, W, Cin, Cout);
+  NIDT_REQUIRE(bp > 0, "conv2d_fwd_slab_bd_table: shape not eligible");
+  if (bp == 256) {
+    conv3d_fwd_slab_table(tab, 1, B, H, W, 1, stream);
+    return;
+  }
+  const int Mg = B * H * W;
+  hipLaunchKernelGGL(k_union_table, dim3(ceil_div(Mg, 128)), dim3(256), 0, as_stream(stream), ptr<int>(tab), 384, 128,
+                     Mg, B, H, W, 1, slab_ext(W, 1));
+  NIDT_CHECK(hipGetLastError());
 }
 
 void conv2d_fwd_slab_bd(uintptr_t x, uintptr_t w, uintptr_t y, int G, int B, int H, int W, int Cin, int Cout,
                         uintptr_t utab, uintptr_t stream) {
-  NIDT_REQUIRE(conv2d_fwd_slab_bd_ok(B, H, W, Cin, Cout), "conv2d_fwd_slab_bd: shape not supported");
-  fwd_slab_impl(x, w, 0, 0, y, 0, G, 1, B, H, W, Cin, Cout, 1, 9, utab, stream, 1);
+  const int bp = slab_bd_bp(B, H, W, Cin, Cout);
+  NIDT_REQUIRE(bp > 0, "conv2d_fwd_slab_bd: shape not supported");
+  fwd_slab_impl(x, w, 0, 0, y, 0, G, 1, B, H, W, Cin, Cout, 1, 9, utab, stream, 1, bp);
 }
 
 // ---- k_conv_fwd_vol host side (whole padded sample <= 448 rows, <= 256 output positions per sample) ----

@@ -138,11 +138,11 @@ def slab_conv2d(x_ptr, w_ptr, y_ptr, G, B, H, W, Cin, Cout, device):
         if not m.conv2d_fwd_slab_bd_pick(G, B, H, W, Cin, Cout):
             return False
         # [SLAB-BD] maps whose blocks span several samples: the samples as the depth planes of one volume
-        key = ("bd", str(device), B, H, W)
+        key = ("bd", str(device), B, H, W, Cin, Cout)  # the block size (256 / 128 positions) depends on the channels
         tab = _SLAB_TABS.get(key)
         if tab is None:
-            tab = torch.empty(m.conv2d_fwd_slab_bd_table_size(B, H, W), device=device, dtype=torch.int32)
-            m.conv2d_fwd_slab_bd_table(tab.data_ptr(), B, H, W, _stream())
+            tab = torch.empty(m.conv2d_fwd_slab_bd_table_size(B, H, W, Cin, Cout), device=device, dtype=torch.int32)
+            m.conv2d_fwd_slab_bd_table(tab.data_ptr(), B, H, W, Cin, Cout, _stream())
             if not torch.cuda.is_current_stream_capturing():
                 torch.cuda.current_stream().synchronize()
                 _SLAB_TABS[key] = tab

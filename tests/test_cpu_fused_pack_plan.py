@@ -62,9 +62,10 @@ def test_pack_next_plan_rules():
     assert r._pack_next(plan) is None
 
 
-@pytest.mark.parametrize("B,hw,c,ok", [(16, 8, 256, 1), (250, 8, 256, 1), (16, 4, 512, 0), (16, 16, 128, 0),
-                                       (1022, 8, 64, 0)])
+@pytest.mark.parametrize("B,hw,c,ok", [(16, 8, 256, 1), (250, 8, 256, 1), (16, 4, 512, 1), (16, 4, 64, 0),
+                                       (16, 16, 128, 0), (1022, 8, 64, 0)])
 def test_slab_batched_depth_eligibility(B, hw, c, ok):
-    """8x8 maps fit the 416-row union (4 padded samples); 4x4 maps do not (16 x 36 rows); 16x16 maps take the
-    per-sample slab; the depth extent must stay below the 10-bit plane code."""
+    """8x8 maps fit the 416-row union of 256-position blocks (4 padded samples); 4x4 maps take 128-position blocks
+    (8 x 36 rows, 128-channel blocks only); 16x16 maps take the per-sample slab; the depth extent must stay below the
+    10-bit plane code."""
     assert ops.ext().conv2d_fwd_slab_bd_ok(B, hw, hw, c, c) == ok

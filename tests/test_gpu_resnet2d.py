@@ -371,7 +371,8 @@ def test_optimizer_written_images_equal_pack(mask_mode):
     assert torch.equal(out[False][2], out[True][2])
 
 
-@pytest.mark.parametrize("B,hw,cin,cout", [(6, 8, 64, 64), (5, 8, 256, 256), (3, 8, 128, 256), (4, 6, 64, 128)])
+@pytest.mark.parametrize("B,hw,cin,cout", [(6, 8, 64, 64), (5, 8, 256, 256), (3, 8, 128, 256), (4, 6, 64, 128),
+                                           (16, 4, 512, 512), (13, 4, 256, 512), (9, 4, 512, 128)])
 def test_slab_batched_depth_matches_fp32(B, hw, cin, cout):
     """[SLAB-BD] 2-D 3x3 convs whose blocks span several samples, as the depth planes of one volume restricted to
     depth tap 1 (conv2d_fwd_slab_bd), against fp32 F.conv2d per client on the same bf16 operands."""
@@ -385,8 +386,8 @@ def test_slab_batched_depth_matches_fp32(B, hw, cin, cout):
     x = torch.randn(G * B, hw, hw, cin, device=dev).to(torch.bfloat16)
     w = (torch.randn(G, cout, 9, cin, device=dev) * (9 * cin) ** -0.5).to(torch.bfloat16)
     y = torch.empty(G * B, hw, hw, cout, device=dev, dtype=torch.bfloat16)
-    tab = torch.empty(m.conv2d_fwd_slab_bd_table_size(B, hw, hw), device=dev, dtype=torch.int32)
-    m.conv2d_fwd_slab_bd_table(tab.data_ptr(), B, hw, hw, ops.stream())
+    tab = torch.empty(m.conv2d_fwd_slab_bd_table_size(B, hw, hw, cin, cout), device=dev, dtype=torch.int32)
+    m.conv2d_fwd_slab_bd_table(tab.data_ptr(), B, hw, hw, cin, cout, ops.stream())
     m.conv2d_fwd_slab_bd(x.data_ptr(), w.data_ptr(), y.data_ptr(), G, B, hw, hw, cin, cout, tab.data_ptr(), ops.stream())
     torch.cuda.synchronize()
     for g in range(G):

@@ -34,8 +34,8 @@ def main():
                                                       1, 1, 0, dev))
             ref = y.clone()
             if m.conv2d_fwd_slab_bd_ok(B, H, H, C, C):  # samples as depth planes (tools: always timed when eligible)
-                tab = torch.empty(m.conv2d_fwd_slab_bd_table_size(B, H, H), device=dev, dtype=torch.int32)
-                m.conv2d_fwd_slab_bd_table(tab.data_ptr(), B, H, H, ops.stream())
+                tab = torch.empty(m.conv2d_fwd_slab_bd_table_size(B, H, H, C, C), device=dev, dtype=torch.int32)
+                m.conv2d_fwd_slab_bd_table(tab.data_ptr(), B, H, H, C, C, ops.stream())
                 y.zero_()
                 res["slab_bd"] = timeit(lambda: m.conv2d_fwd_slab_bd(x.data_ptr(), w.data_ptr(), y.data_ptr(), G, B, H, H,
                                                                      C, C, tab.data_ptr(), ops.stream()))

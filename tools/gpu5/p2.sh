@@ -1,0 +1,16 @@
+#!/bin/bash
+# 128-position depth-batched slab (4x4 maps): correctness, kernel bench, resnet2d tests, CIFAR benches
+set -o pipefail
+export PYTHONUNBUFFERED=1
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+OUT=gpurun_out/r5p2; mkdir -p $OUT
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_resnet2d.py -k "slab_batched_depth" > $OUT/pytest_bd.txt 2>&1 || { grep -E "Error|assert|FAILED|passed|failed" $OUT/pytest_bd.txt | tail -20; exit 1; }
+tail -1 $OUT/pytest_bd.txt
+timeout -k 10 300 python -u tools/bench_conv2d.py > $OUT/conv2d.txt 2>&1 || { tail -20 $OUT/conv2d.txt; exit 1; }
+grep "4x4\|8x8" $OUT/conv2d.txt
+timeout -k 10 400 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_resnet2d.py > $OUT/pytest.txt 2>&1 || { grep -E "Error|assert|FAILED|passed|failed" $OUT/pytest.txt | tail -20; exit 1; }
+tail -1 $OUT/pytest.txt
+for alg in subavg dispfl; do
+  timeout -k 10 300 python -u tools/bench_cifar.py --algorithm $alg --rounds 2 --warmup 1 > $OUT/$alg.txt 2>&1 || { tail -20 $OUT/$alg.txt; exit 1; }
+  echo "== $alg $(tail -1 $OUT/$alg.txt | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["s_round_each"], d.get("last_round_metrics"))')"
+done
