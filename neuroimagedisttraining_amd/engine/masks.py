@@ -62,6 +62,24 @@ def unpack_bits(bits, P, dtype=torch.float32):
     return (b & 1).view(R, W * 32)[:, :P].to(dtype)
 
 
+def masked_rows(dst, bits, src=None, P=None):
+    """``dst[c, :P] = (src if given else dst[c, :P]) * mask_c`` with ``bits`` ``[C, W]`` (or ``[1, W]``: one mask for
+    every row); ``dst`` ``[C, >= P]`` fp32 rows, ``src`` a ``[P]`` row.  HIP: one pass (``optim.hip`` ``k_masked_rows``)."""
+    C = dst.shape[0]
+    if P is None:
+        P = src.numel() if src is not None else min(dst.shape[1], bits.shape[1] * 32)
+    if _hip(dst) and dst.dtype == torch.float32 and dst.stride(1) == 1 and dst.stride(0) % 4 == 0 and C:
+        b = bits.contiguous()
+        s = src.contiguous() if src is not None else None
+        ops.ext().masked_rows(s.data_ptr() if s is not None else 0, b.data_ptr(), 0 if b.shape[0] == 1 else b.stride(0),
+                              C, P, dst.stride(0), dst.data_ptr(), _st())
+        return dst
+    m = unpack_bits(bits, P)
+    base = src.view(1, -1).expand(C, -1) if src is not None else dst[:, :P]
+    dst[:, :P] = base * m
+    return dst
+
+
 # ------------------------------------------------------------------------------------------------ hash (regrow_rand)
 def _mix_hash_np(seed, a, b):
     """numpy twin of ``mix_hash`` in sparse.hip (uint64 splitmix finaliser)."""

@@ -441,7 +441,7 @@ class DisPFLRunner(PersonalizedRunner):
         self.shared_bits = self.mbits.clone()  # mask_pers_shared: the mask each client last trained with
         # w_per = w_global * mask (every parameter is masked)
         if self.C:
-            self.theta[:self.C].mul_(MK.unpack_bits(self.mbits[:self.C], self.P))
+            MK.masked_rows(self.theta[:self.C], self.mbits[:self.C], P=self.P)
         self.dist_locals = np.zeros((N, N))
 
     def benefit_choose(self, c, active):
@@ -581,7 +581,8 @@ class SubAvgRunner(PersonalizedRunner):
 
     def _real_prune_rows(self, rs, rows, bits_rows):
         ix = self._to_dev(rows)
-        rs.theta[ix, :self.P] = rs.theta[ix, :self.P] * MK.unpack_bits(bits_rows, self.P)
+        t = rs.theta[ix]
+        rs.theta[ix] = MK.masked_rows(t, bits_rows, P=self.P)
 
     def run_round(self, round_idx, sync_timers=False):
         cfg = self.cfg
@@ -619,7 +620,7 @@ class SubAvgRunner(PersonalizedRunner):
             if cand:
                 pr = self.pool([(self.theta[rows[j]], self.bufs[rows[j]]) for j in cand])
                 cb = torch.stack([m2[j] for j in cand])
-                pr.theta[:len(cand), :self.P].mul_(MK.unpack_bits(cb, self.P))
+                MK.masked_rows(pr.theta[:len(cand)], cb, P=self.P)
                 met = self.eval_grouped(pr.theta, pr.bufs, list(range(len(cand))), [loc[j] for j in cand], "train")
                 for q, j in enumerate(cand):
                     if met[q, 0] / max(1.0, met[q, 2]) > cfg.acc_thresh:
@@ -649,10 +650,12 @@ class SubAvgRunner(PersonalizedRunner):
         if self._eval_due(round_idx):  # every client tests real_prune(w_global, its current mask)
             er = self._eval_buffers(max(1, self.C))
             th, bu = er
-            th.copy_(self.w_global.expand_as(th))
             bu.copy_(self.b_global.expand_as(bu))
-            if self.C:
-                th[:self.C, :self.P].mul_(MK.unpack_bits(self.mbits[:self.C], self.P))
+            if self.C:  # w_global * mask_c in one pass (masks.masked_rows)
+                MK.masked_rows(th[:self.C], self.mbits[:self.C], src=self.w_global[:self.P])
+                if th.shape[1] > self.P:
+                    th[:self.C, self.P:].copy_(self.w_global[self.P:].expand(self.C, -1))
+            th[self.C:].copy_(self.w_global.expand_as(th[self.C:]))
             if self._defer_metrics():  # read one round late (no end-of-round device drain; see FLRunner.evaluate)
                 self._flush_metrics(ready_only=True)
                 rows_e, clients_e = self.all_rows()

@@ -395,3 +395,22 @@ def test_slab_batched_depth_matches_fp32(B, hw, cin, cout):
         wr = w[g].float().view(cout, 3, 3, cin).permute(0, 3, 1, 2)
         ref = F.conv2d(xr, wr, padding=1).permute(0, 2, 3, 1)
         assert _rel(y[g * B:(g + 1) * B].float(), ref) < 1e-2, g
+
+
+@pytest.mark.parametrize("P,shared,src", [(1000, False, False), (1000, True, True), (4103, False, True), (37, False, False)])
+def test_masked_rows_matches_unpack(P, shared, src):
+    """masks.masked_rows (optim.hip k_masked_rows) == the torch unpack-and-multiply, tails and shared masks included."""
+    from neuroimagedisttraining_amd.engine import masks as MK
+    from neuroimagedisttraining_amd.engine.executor import padded_rows
+    dev = _dev()
+    C = 5
+    torch.manual_seed(P)
+    rows = padded_rows(C, P, dev)
+    rows[:, :P] = torch.randn(C, P, device=dev)
+    keep = torch.rand(1 if shared else C, P, device=dev) < 0.4
+    bits = MK.pack_bits(keep)
+    s = torch.randn(P, device=dev) if src else None
+    ref = ((s.view(1, -1) if src else rows[:, :P]) * keep.float()).clone()
+    out = MK.masked_rows(rows, bits, src=s, P=P)
+    torch.cuda.synchronize()
+    assert torch.equal(out[:, :P], ref.expand(C, -1))

@@ -1,0 +1,13 @@
+#!/bin/bash
+set -o pipefail
+export PYTHONUNBUFFERED=1
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+OUT=gpurun_out/r5r2; mkdir -p $OUT
+timeout -k 10 400 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_resnet2d.py > $OUT/pytest.txt 2>&1 || { grep -E "Error|assert|FAILED|passed|failed" $OUT/pytest.txt | tail -20; exit 1; }
+tail -1 $OUT/pytest.txt
+NIDT_CIFAR_EVAL_PROBE=1 timeout -k 10 300 python -u tools/bench_cifar.py --algorithm subavg --rounds 1 --warmup 1 > $OUT/probe.txt 2>&1 || { tail -20 $OUT/probe.txt; exit 1; }
+grep -E "probe" $OUT/probe.txt | head -2
+for alg in subavg dispfl; do
+  timeout -k 10 300 python -u tools/bench_cifar.py --algorithm $alg --rounds 3 --warmup 1 > $OUT/$alg.txt 2>&1 || { tail -20 $OUT/$alg.txt; exit 1; }
+  echo "== $alg $(tail -1 $OUT/$alg.txt | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["s_round_each"], d.get("last_round_metrics"))')"
+done
