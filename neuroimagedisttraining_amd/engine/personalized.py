@@ -29,6 +29,7 @@ from __future__ import annotations
 
 import math
 import random
+import os
 import time
 from dataclasses import replace
 
@@ -601,16 +602,26 @@ class SubAvgRunner(PersonalizedRunner):
             nz_dev = self.state_nonzeros(self.theta, self.bufs, rows)  # print_pruning over the whole state
             self.add_comm(nz_dev)
 
+            late = os.environ.get("NIDT_SUBAVG_LATE_PRUNE", "1") != "0"
+
             def hook(ep, view, clients):  # fake_prune after the first and the last epoch (the training masks)
-                if ep == 0:
+                if ep == 0 and cfg.epochs > 1 and not late:
                     hooks["m1"] = self.mspace.percentile_prune(view.theta, old_bits, cfg.each_prune_ratio,
                                                                self.prune_names)
+                elif ep == 0 and cfg.epochs > 1:
+                    # the first epoch's weights are kept and pruned after training: the percentile search reads
+                    # its thresholds on the host, which in mid-training drained the device between epochs
+                    hooks["t1"] = view.theta.clone()
                 if ep == cfg.epochs - 1:
                     hooks["m2"] = self.mspace.percentile_prune(view.theta, old_bits, cfg.each_prune_ratio,
                                                                self.prune_names)
             spec = StepSpec(mask_mode=MASK_GRAD, bits=self.mbits)
             self.train_rows(self.rowset, rows, loc, round_idx, cfg.epochs, spec, epoch_hook=hook)
-            m1, m2 = hooks["m1"], hooks["m2"]
+            m2 = hooks["m2"]
+            m1 = hooks.get("m1")
+            if m1 is None:
+                m1 = (self.mspace.percentile_prune(hooks.pop("t1"), old_bits, cfg.each_prune_ratio, self.prune_names)
+                      if cfg.epochs > 1 else m2)
             # one host read after training for both (a read before it drained the device at every round start)
             hd = torch.cat([nz_dev.double().view(-1, 1), self.mspace.hamming(m1, m2).double()], 1).cpu().numpy()
             dense, ham = hd[:, 0] / float(self.P + self.Q), hd[:, 1:]
