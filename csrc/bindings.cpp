@@ -60,6 +60,7 @@ int conv3d_fwd_vol_ok(int B, int D, int H, int W, int Cin, int Cout, int pad);
 int conv3d_fwd_vol_pick(int G, int B, int D, int H, int W, int Cin, int Cout, int pad);
 void conv3d_fwd_vol(uintptr_t x, uintptr_t w, uintptr_t bias, int64_t bias_ld, uintptr_t y, uintptr_t stats, int G,
                     int B, int D, int H, int W, int Cin, int Cout, int pad, uintptr_t stream);
+void unpack_bits_dev(uintptr_t bits, int64_t mstride, int64_t R, int64_t P, int f32, uintptr_t out, uintptr_t stream);
 void masked_rows(uintptr_t src, uintptr_t bits, int64_t mstride, int64_t C, int64_t P, int64_t ld, uintptr_t dst,
                  uintptr_t stream);
 void stream_fork(uintptr_t src, uintptr_t dst);
@@ -265,6 +266,7 @@ PYBIND11_MODULE(_nidt_hip, m) {
   DEF(conv3d_fwd_vol_ok);
   DEF(conv3d_fwd_vol_pick);
   DEF(conv3d_fwd_vol);
+  DEF(unpack_bits_dev);
   DEF(masked_rows);
   DEF(stream_fork);
   DEF(conv2d_fwd_slab_bd_ok);

@@ -548,6 +548,45 @@ __global__ __launch_bounds__(256) void k_masked_rows(const float* __restrict__ s
   }
 }
 
+// ---- bit rows -> [R, P] 0/1 rows (uint8 for bool, or fp32): 4 elements per thread (one nibble of a mask word),
+// consecutive threads on consecutive elements: 4-B / 16-B coalesced stores ----
+template <bool F32>
+__global__ __launch_bounds__(256) void k_unpack_bits(const uint32_t* __restrict__ bits, int64_t mstride, int64_t P,
+                                                     void* __restrict__ out) {
+  const int r = blockIdx.y;
+  const int64_t i = 4 * ((int64_t)blockIdx.x * blockDim.x + threadIdx.x);
+  if (i >= P) return;
+  const uint32_t nib = (bits[(int64_t)r * mstride + (i >> 5)] >> (i & 31)) & 0xfu;
+  if (F32) {
+    float* o = reinterpret_cast<float*>(out) + (int64_t)r * P + i;
+    const float v[4] = {(float)(nib & 1u), (float)((nib >> 1) & 1u), (float)((nib >> 2) & 1u), (float)(nib >> 3)};
+    if (i + 3 < P && (P & 3) == 0) {
+      *reinterpret_cast<float4*>(o) = make_float4(v[0], v[1], v[2], v[3]);
+    } else {
+      for (int j = 0; j < 4 && i + j < P; ++j) o[j] = v[j];
+    }
+  } else {
+    uint8_t* o = reinterpret_cast<uint8_t*>(out) + (int64_t)r * P + i;
+    if (i + 3 < P && (P & 3) == 0) {
+      *reinterpret_cast<uint32_t*>(o) = (nib & 1u) | (((nib >> 1) & 1u) << 8) | (((nib >> 2) & 1u) << 16) | ((nib >> 3) << 24);
+    } else {
+      for (int j = 0; j < 4 && i + j < P; ++j) o[j] = (uint8_t)((nib >> j) & 1u);
+    }
+  }
+}
+
+void unpack_bits_dev(uintptr_t bits, int64_t mstride, int64_t R, int64_t P, int f32, uintptr_t out, uintptr_t stream) {
+  NIDT_REQUIRE(bits != 0 && out != 0 && R > 0 && P > 0 && (out & 15) == 0, "unpack_bits_dev: arguments");
+  const dim3 grid((unsigned)ceil_div((P + 3) / 4, 256), (unsigned)R);
+  if (f32)
+    hipLaunchKernelGGL(k_unpack_bits<true>, grid, dim3(256), 0, as_stream(stream), ptr<const uint32_t>(bits), mstride, P,
+                       ptr<void>(out));
+  else
+    hipLaunchKernelGGL(k_unpack_bits<false>, grid, dim3(256), 0, as_stream(stream), ptr<const uint32_t>(bits), mstride,
+                       P, ptr<void>(out));
+  NIDT_CHECK(hipGetLastError());
+}
+
 void masked_rows(uintptr_t src, uintptr_t bits, int64_t mstride, int64_t C, int64_t P, int64_t ld, uintptr_t dst,
                  uintptr_t stream) {
   NIDT_REQUIRE(ld % 4 == 0 && (dst & 15) == 0 && (src & 15) == 0 && bits != 0 && C > 0 && P > 0 && ld >= P,

@@ -56,8 +56,14 @@ def pack_bits(m):
 
 
 def unpack_bits(bits, P, dtype=torch.float32):
-    """``[R, W]`` int32 bit rows -> ``[R, P]`` 0/1 tensor."""
+    """``[R, W]`` int32 bit rows -> ``[R, P]`` 0/1 tensor (HIP: ``optim.hip`` ``k_unpack_bits`` for bool / fp32 — the
+    torch form goes through an int64 [R, 32 W] temporary, 8 bytes per element, several passes)."""
     R, W = bits.shape
+    if _hip(bits) and dtype in (torch.bool, torch.float32) and R and P:
+        b = bits.contiguous()
+        out = torch.empty((R, P), dtype=dtype, device=bits.device)
+        ops.ext().unpack_bits_dev(b.data_ptr(), b.stride(0), R, P, int(dtype == torch.float32), out.data_ptr(), _st())
+        return out
     b = (bits.to(torch.int64) & 0xffffffff).unsqueeze(-1) >> torch.arange(32, device=bits.device, dtype=torch.int64)
     return (b & 1).view(R, W * 32)[:, :P].to(dtype)
 

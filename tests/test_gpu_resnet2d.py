@@ -414,3 +414,17 @@ def test_masked_rows_matches_unpack(P, shared, src):
     out = MK.masked_rows(rows, bits, src=s, P=P)
     torch.cuda.synchronize()
     assert torch.equal(out[:, :P], ref.expand(C, -1))
+
+
+@pytest.mark.parametrize("P", [1000, 4103, 37, 64])
+def test_unpack_bits_kernel_matches_torch(P):
+    """masks.unpack_bits on the device (k_unpack_bits, bool and fp32) == the torch bit arithmetic on the CPU."""
+    from neuroimagedisttraining_amd.engine import masks as MK
+    dev = _dev()
+    torch.manual_seed(P)
+    keep = torch.rand(3, P) < 0.3
+    bits = MK.pack_bits(keep)
+    for dt in (torch.bool, torch.float32):
+        got = MK.unpack_bits(bits.to(dev), P, dt).cpu()
+        assert torch.equal(got, MK.unpack_bits(bits, P, dt)), dt
+        assert torch.equal(got.bool(), keep)

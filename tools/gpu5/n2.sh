@@ -3,7 +3,7 @@
 set -o pipefail
 export PYTHONUNBUFFERED=1
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-OUT=gpurun_out/r5n2; mkdir -p $OUT
+OUT=gpurun_out/r5n3; mkdir -p $OUT
 timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests -m gpu > $OUT/pytest_gpu.txt 2>&1 \
   || { grep -E "FAILED|Error|passed|failed" $OUT/pytest_gpu.txt | tail -20; exit 1; }
 tail -2 $OUT/pytest_gpu.txt
