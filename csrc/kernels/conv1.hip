@@ -171,20 +171,35 @@ __device__ constexpr int kC1W[4] = {2, 5, 11, 14};
 __device__ constexpr int kC1X1[4] = {24, 20, 8, 26};   // DH0, DW0, HW0, DHW
 __device__ constexpr int kC1X2[4] = {25, 23, 17, 26};  // DH1, DW1, HW1, (empty)
 __device__ constexpr int kC1XR[4][2] = {{0, 1}, {0, 2}, {0, 4}, {0, -1}};
+// RO = 2 (the w64 default): every B operand is one conflict-free ds_read_b128.  A ds_read_b128 is served in 16-lane
+// groups {fq0 fr0-3,12-15 + fq1 fr4-11} (and the fq2/fq3 mirror): when the two lane quarters of a group read tap
+// groups of the same jw, their 16 lanes touch 16 distinct 16-B slots of the 256-B bank row.  k-steps 0-2 take the
+// RO = 1 order (paired jw); k-step 3 holds W[fq] (phases 0,2,4,6) + X1[fq] (phases 0,2: DW0, DW1, DHW, empty) +
+// X2[fq] (phases 0,1 for DH0/DH1, 0,4 for HW0/HW1).  Only X2 of the fq0/fq1 quarters (DH0: jw 0 vs DH1: jw 1) is
+// 2-way.  The narrow reads of RO = 0/1 (ds_read_b64 / b32 at a 16-B lane stride: 2- and 4-way) were the kernel's
+// 45.7 % LDS bank conflicts (profiles/r5_c1fwd_w64_pmc.txt).
+__device__ constexpr int kC1X1b[4] = {20, 23, 26, -1};  // DW0, DW1, DHW, empty
+__device__ constexpr int kC1X2b[4] = {24, 25, 8, 17};   // DH0, DH1, HW0, HW1
 
 // (tap group, phase) of slot kk of the 128-slot layout, or t = -1 for an empty slot
 template <int RO>
 __device__ __forceinline__ void c1_slot128(int kk, int& t, int& r) {
+  constexpr int R1 = RO ? 1 : 0;
   const int st = kk >> 5, fq = (kk >> 3) & 3, e = kk & 7;
   t = -1;
   r = 0;
-  if (st < 2) { t = kC1F2[RO][4 * st + fq]; r = e; return; }
+  if (st < 2) { t = kC1F2[R1][4 * st + fq]; r = e; return; }
   if (st == 2) {
-    if (e < 4) { t = kC1D2[RO][fq]; r = e; }
-    else { t = kC1H2[RO][fq]; r = (e - 4 < 2) ? e - 4 : e - 4 + 2; }
+    if (e < 4) { t = kC1D2[R1][fq]; r = e; }
+    else { t = kC1H2[R1][fq]; r = (e - 4 < 2) ? e - 4 : e - 4 + 2; }
     return;
   }
   if (e < 4) { t = kC1W[fq]; r = 2 * e; return; }
+  if (RO == 2) {
+    if (e < 6) { t = kC1X1b[fq]; r = e == 4 ? 0 : 2; }  // DHW's phase 2 is invalid: tp_valid zeroes its weight
+    else { t = kC1X2b[fq]; r = e == 6 ? 0 : (fq < 2 ? 1 : 4); }
+    return;
+  }
   const int x = (e - 4) >> 1, h = e & 1;
   if (x == 1 && fq == 3) return;
   const int rr = kC1XR[fq][h];
@@ -226,12 +241,16 @@ __global__ void k_pack_conv1_w(const float* __restrict__ theta, int64_t ldt, int
 // tap-group order of the 128-slot forward layout (pack and forward must agree): the original order by default;
 // NIDT_C1_TAPORD=1 selects the bank-paired order (slower at 64 clients: conv1 forward 4.38 vs 4.25 ms,
 // profiles/r4_kbench_g64.txt)
+// (the w64 forward defaults to RO = 2, the all-b128 layout; the pipe kernel knows RO = 0 / 1 only)
+int conv1_kslots();
+int conv1_fwd_variant();
 int conv1_tapord() {
-  static const int ro = [] {
+  static const int env = [] {
     const char* e = getenv("NIDT_C1_TAPORD");
-    return (e && atoi(e) == 1) ? 1 : 0;
+    return e ? atoi(e) : -1;
   }();
-  return ro;
+  if (conv1_fwd_variant() == 1 && conv1_kslots() == 128) return env >= 0 && env <= 2 ? env : 2;
+  return env == 1 ? 1 : 0;
 }
 
 int conv1_kslots() {
@@ -246,7 +265,11 @@ void pack_conv1_w(uintptr_t theta, int64_t ldt, int64_t off, int64_t off_sign, i
                   uintptr_t w125, uintptr_t stream) {
   const int KS = conv1_kslots();
   // w125 entries of empty taps are never read; every valid (t, r) appears in exactly one slot of either layout
-  if (conv1_tapord())
+  const int ro = conv1_tapord();
+  if (ro == 2)
+    hipLaunchKernelGGL(k_pack_conv1_w<2>, dim3(ceil_div(G * kC1 * KS, 256)), dim3(256), 0, as_stream(stream),
+                       ptr<const float>(theta), ldt, off, off_sign, G, scale, KS, ptr<uint16_t>(w8), ptr<float>(w125));
+  else if (ro == 1)
     hipLaunchKernelGGL(k_pack_conv1_w<1>, dim3(ceil_div(G * kC1 * KS, 256)), dim3(256), 0, as_stream(stream),
                        ptr<const float>(theta), ldt, off, off_sign, G, scale, KS, ptr<uint16_t>(w8), ptr<float>(w125));
   else
@@ -735,19 +758,46 @@ __global__ __launch_bounds__(256, 2) void k_conv1_fwd_w64(const uint8_t* __restr
     for (int r = 0; r < 4; ++r) asm volatile("" : "+v"(cinit[i][r]));
   }
   auto goff = [](int t) { return (((t / 9) * 5 + (t / 3) % 3) * HX + (t % 3)) * 8; };
+  constexpr int R1 = RO ? 1 : 0;
   int toff[KS];
-  toff[0] = goff(kC1F2[RO][fq]);
-  toff[1] = goff(kC1F2[RO][4 + fq]);
-  toff[2] = goff(kC1D2[RO][fq]);
+  toff[0] = goff(kC1F2[R1][fq]);
+  toff[1] = goff(kC1F2[R1][4 + fq]);
+  toff[2] = goff(kC1D2[R1][fq]);
   toff[3] = goff(kC1W[fq]);
-  const int gh = goff(kC1H2[RO][fq]), gx1 = goff(kC1X1[fq]), gx2 = goff(kC1X2[fq]);
+  const int gh = goff(kC1H2[R1][fq]);
+  // RO = 2: the empty X1 quarter (fq 3) reads the DHW group of its jw-paired quarter (zero weights)
+  const int gx1 = RO == 2 ? goff(kC1X1b[fq < 3 ? fq : 2]) : goff(kC1X1[fq]);
+  const int gx2 = RO == 2 ? goff(kC1X2b[fq]) : goff(kC1X2[fq]);
   const bool xsrc2 = fq == 2;
   const uint32_t xsel1 = fq == 0 ? 0x03020100u : fq == 3 ? 0x0c0c0100u : 0x05040100u;
-  const uint32_t xsel2 = fq == 0 ? 0x03020100u : fq == 3 ? 0x0c0c0c0cu : 0x05040100u;
+  const uint32_t xsel2 = RO == 2 ? (fq < 2 ? 0x03020100u : 0x05040100u)
+                                 : fq == 0 ? 0x03020100u : fq == 3 ? 0x0c0c0c0cu : 0x05040100u;
   // k-step 3's two 2-phase groups: the second dword of each is picked by address (dword 2 for the HW groups of
   // fq = 2, dword 1 otherwise) instead of a v_cndmask after a 16-B read
   const int gx1s = gx1 + (xsrc2 ? 4 : 2), gx2s = gx2 + (xsrc2 ? 4 : 2);
+  // a whole 16-B read whose value is only partly used: the opaque asm keeps all four dwords live, so the load is
+  // not narrowed back to a conflicting ds_read_b64 / ds_read2_b32
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  auto rd128 = [](const uint16_t* p) -> uint4 {
+    u32x4 v = *reinterpret_cast<const u32x4*>(p);
+    asm("" : "+v"(v));
+    return make_uint4(v[0], v[1], v[2], v[3]);
+  };
   auto bfrag = [&](const uint16_t* hb, int s, int ro) -> f16x8 {
+    if (RO == 2) {
+      if (s < 2) return *reinterpret_cast<const f16x8*>(&hb[ro + toff[s]]);
+      if (s == 2) {
+        const uint4 d = rd128(&hb[ro + toff[2]]), h = rd128(&hb[ro + gh]);
+        return __builtin_bit_cast(f16x8, make_uint4(d.x, d.y, h.x, h.z));  // D: phases 0-3, H: phases 0,1,4,5
+      }
+      const uint4 w = rd128(&hb[ro + toff[3]]), a = rd128(&hb[ro + gx1]), b = rd128(&hb[ro + gx2]);
+      uint4 v;
+      v.x = __builtin_amdgcn_perm(w.y, w.x, 0x05040100u);  // W: phases 0, 2
+      v.y = __builtin_amdgcn_perm(w.w, w.z, 0x05040100u);  // W: phases 4, 6
+      v.z = __builtin_amdgcn_perm(a.y, a.x, 0x05040100u);  // X1: phases 0, 2
+      v.w = __builtin_amdgcn_perm(b.z, b.x, xsel2);        // X2: phases 0, 1 (DH) or 0, 4 (HW)
+      return __builtin_bit_cast(f16x8, v);
+    }
     if (s < 3) return c1_bfrag<KS>(hb, s, ro, toff, gh, gx1, gx2, xsrc2, xsel1, xsel2);
     const uint4 w = *reinterpret_cast<const uint4*>(&hb[ro + toff[3]]);
     const uint32_t a0 = *reinterpret_cast<const uint32_t*>(&hb[ro + gx1]);
@@ -865,7 +915,24 @@ void conv1_fwd_pool(uintptr_t x8, uintptr_t idx, uintptr_t w8, uintptr_t scale, 
       const char* e = getenv("NIDT_C1_NQ");
       return e ? std::max(1, std::min(kPH, atoi(e))) : 1;
     }();
-    if (conv1_tapord() == 1)
+    // B-fragment prefetch distance of the RO = 2 kernel in k-steps (NIDT_C1_WPF, A/B), default 2
+    static const int wpf = [] {
+      const char* e = getenv("NIDT_C1_WPF");
+      return e ? atoi(e) : 2;
+    }();
+    if (conv1_tapord() == 2 && wpf == 3)
+      hipLaunchKernelGGL((k_conv1_fwd_w64<3, 2>), dim3(kPD * NB * nq1), dim3(256), 0, as_stream(stream),
+                         ptr<const uint8_t>(x8), ptr<const int>(idx), ptr<const uint16_t>(w8), ptr<const float>(scale),
+                         ptr<const float>(shift), B, ptr<uint16_t>(out), ptr<uint8_t>(amax), nq1);
+    else if (conv1_tapord() == 2 && wpf == 4)
+      hipLaunchKernelGGL((k_conv1_fwd_w64<4, 2>), dim3(kPD * NB * nq1), dim3(256), 0, as_stream(stream),
+                         ptr<const uint8_t>(x8), ptr<const int>(idx), ptr<const uint16_t>(w8), ptr<const float>(scale),
+                         ptr<const float>(shift), B, ptr<uint16_t>(out), ptr<uint8_t>(amax), nq1);
+    else if (conv1_tapord() == 2)
+      hipLaunchKernelGGL((k_conv1_fwd_w64<2, 2>), dim3(kPD * NB * nq1), dim3(256), 0, as_stream(stream),
+                         ptr<const uint8_t>(x8), ptr<const int>(idx), ptr<const uint16_t>(w8), ptr<const float>(scale),
+                         ptr<const float>(shift), B, ptr<uint16_t>(out), ptr<uint8_t>(amax), nq1);
+    else if (conv1_tapord() == 1)
       hipLaunchKernelGGL((k_conv1_fwd_w64<2, 1>), dim3(kPD * NB * nq1), dim3(256), 0, as_stream(stream),
                          ptr<const uint8_t>(x8), ptr<const int>(idx), ptr<const uint16_t>(w8), ptr<const float>(scale),
                          ptr<const float>(shift), B, ptr<uint16_t>(out), ptr<uint8_t>(amax), nq1);

@@ -194,7 +194,11 @@ __global__ __launch_bounds__(512, 1) void k_gemm1x1(const uint16_t* __restrict__
           s1[i][r] += __shfl_xor(s1[i][r], o, 64);
           s2[i][r] += __shfl_xor(s2[i][r], o, 64);
         }
-    float* red = reinterpret_cast<float*>(sX0);  // [2 m halves][BN][2]; every wave is past the last tile's barrier
+    // [2 m halves][BN][2] in sX0.  The last tile issued (out-of-range) DMAs for tiles T and T + 1, one of which can
+    // target sX0 (T % 3 == 2) and land late: drain every wave's DMAs and meet at a barrier before the first write
+    g1_wait_vm<0>();
+    __builtin_amdgcn_s_barrier();
+    float* red = reinterpret_cast<float*>(sX0);
     if (fr == 0) {
 #pragma unroll
       for (int i = 0; i < NSUB; ++i)

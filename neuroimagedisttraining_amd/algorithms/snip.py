@@ -113,3 +113,59 @@ def mask_from_scores(model, scores, keep_ratio, use_kernel=True):
     for pname, p in model.named_parameters():
         final[pname] = keep[wnames[pname]].to(p.device) if pname in wnames else torch.ones_like(p)
     return keep, final
+
+
+# ------------------------------------------------------------------------------------------------
+# The reference's public SNIP functions with their signatures (``sailentgrads/snip.py:9-164``), imported by its
+# ``sailentgrads_api.py:16`` and ``client.py:12``.  ``self`` is any object with a ``.model`` (the reference's
+# client / trainer).  They delegate to the functions above; the scores are the same |dL/dmask| at mask = 1.
+
+def snip_forward_conv3d(self, x):
+    """Forward of a Conv3d whose weight is multiplied by a learnable ``weight_mask`` (``snip.py:9-12``)."""
+    return F.conv3d(x, self.weight * self.weight_mask, self.bias, self.stride, self.padding, self.dilation,
+                    self.groups)
+
+
+def snip_forward_linear(self, x):
+    """Forward of a Linear whose weight is multiplied by a learnable ``weight_mask`` (``snip.py:15-16``)."""
+    return F.linear(x, self.weight * self.weight_mask, self.bias)
+
+
+def get_snip_scores(self, mini_batch, re_init=False):
+    """``snip.py:21-79``: ``mini_batch = (inputs, targets, site_info)`` with channel-less volumes (a channel axis is
+    added), BCE-with-logits loss, scores of every Conv3d / Linear as a list of ``(module name, |dL/dmask|)``.
+    ``re_init`` re-initialises the scored copy's weights with Xavier-normal first, as the reference does."""
+    model = self.model
+    device = next(iter(model.parameters())).device
+    inputs, targets = mini_batch[0], mini_batch[1]
+    inputs = torch.as_tensor(inputs).to(device).unsqueeze(1)
+    targets = torch.as_tensor(targets).to(device)
+    cp = copy.deepcopy(model)
+    if re_init:
+        for m in cp.modules():
+            if isinstance(m, (nn.Conv3d, nn.Linear)):
+                nn.init.xavier_normal_(m.weight)
+    scores = snip_scores(cp, inputs.float(), targets.float(), loss="bce")
+    del cp
+    return [(n, scores[n]) for n in scores]
+
+
+def get_mask_from_grads(self, grads_abs, keep_ratio, params):
+    """``snip.py:84-129``: global top-``keep_ratio`` of the sum-normalised scores (ties kept).  Returns
+    ``(keep_masks{module name}, mask_key_layer{module}, final_weight_mask{parameter name})``; biases and norm
+    parameters get all-ones masks.  ``params`` is unused, as in the reference."""
+    del params
+    keep, final = mask_from_scores(self.model, dict(grads_abs), keep_ratio, use_kernel=False)
+    mods = dict(self.model.named_modules())
+    mask_key_layer = {mods[n]: keep[n] for n in keep if n in mods}
+    return keep, mask_key_layer, final
+
+
+def get_mean_snip_scores(grads_gathered):
+    """``snip.py:133-155``: element-wise mean of a list of score dicts (or lists of ``(name, score)`` pairs)."""
+    return mean_scores([dict(g) for g in grads_gathered])
+
+
+def get_mean_sailency_scores(final_sailency_list):
+    """``snip.py:158-179`` (IterSNIP): element-wise mean of a list of saliency dicts."""
+    return mean_scores([dict(g) for g in final_sailency_list])

@@ -54,3 +54,15 @@ def count_inference_flops(model, dataset="ABCD", full=False, input_shape=None):
 
 def count_training_flops(model, dataset="ABCD", full=False, input_shape=None):
     return 3.0 * count_model_param_flops(model, dataset, full, input_shape)
+
+
+def print_model_param_nums(model=None):
+    """``main_flops_counter.py:24-28``: prints (and returns) the number of non-zero entries of the 4-D and 2-D
+    parameters (2-D conv kernels and linear weights — the reference's rule, so 3-D conv kernels are not counted).
+    The reference's default model is torchvision's AlexNet; torchvision is not a dependency here, so a model is
+    required."""
+    if model is None:
+        raise ValueError("print_model_param_nums: pass a model (the torchvision AlexNet default is not available)")
+    total = sum(int((p != 0).sum()) for p in model.parameters() if p.dim() in (2, 4))
+    print('  + Number of params: %.2f' % (total))
+    return total

@@ -120,3 +120,83 @@ def test_cnn_dropout_complexity_script():
     from fedml_api.model.cv.cnn import CNN_DropOut
     flops, params = mod.complexity(CNN_DropOut())
     assert params == 1199882 and flops > 0
+
+
+def test_every_reference_import_line_resolves():
+    """Each ``from fedml_api|fedml_core ... import ...`` line of the reference (tests/data/reference_imports.txt)
+    imports against this repo, so the reference's scripts and modules find every public name they use."""
+    path = os.path.join(os.path.dirname(__file__), "data", "reference_imports.txt")
+    lines = [ln.strip() for ln in open(path) if ln.strip() and not ln.startswith("#")]
+    assert len(lines) >= 60
+    bad = []
+    for ln in lines:
+        try:
+            exec(ln, {})
+        except Exception as e:  # noqa: BLE001
+            bad.append("%s -> %r" % (ln, e))
+    assert not bad, "\n".join(bad)
+
+
+def test_reference_snip_functions_match_monkeypatched_masks():
+    """get_snip_scores / get_mask_from_grads / get_mean_snip_scores with the reference signatures: the scores equal
+    |dL/dmask| of the reference's weight_mask monkey-patch (snip_forward_conv3d / snip_forward_linear), and the mask
+    keeps the global top keep_ratio of the sum-normalised scores."""
+    import copy
+    import types
+    from fedml_api.standalone.sailentgrads.snip import (
+        get_mask_from_grads, get_mean_snip_scores, get_snip_scores, snip_forward_conv3d, snip_forward_linear)
+
+    class Net(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.features = torch.nn.Sequential(torch.nn.Conv3d(1, 4, 3), torch.nn.ReLU())
+            self.classifier = torch.nn.Linear(4 * 4 * 4 * 4, 1)
+
+        def forward(self, x):
+            return self.classifier(self.features(x).flatten(1))
+
+    torch.manual_seed(0)
+    owner = types.SimpleNamespace(model=Net())
+    x, y = torch.randn(5, 6, 6, 6), torch.randint(0, 2, (5,))
+    scores = get_snip_scores(owner, (x, y, None))
+    # the reference's mechanism on a copy
+    cp = copy.deepcopy(owner.model)
+    for layer in cp.modules():
+        if isinstance(layer, (torch.nn.Conv3d, torch.nn.Linear)):
+            layer.weight_mask = torch.nn.Parameter(torch.ones_like(layer.weight))
+            layer.weight.requires_grad = False
+            f = snip_forward_conv3d if isinstance(layer, torch.nn.Conv3d) else snip_forward_linear
+            layer.forward = types.MethodType(f, layer)
+    loss = torch.nn.BCEWithLogitsLoss()(cp(x.unsqueeze(1)), y.unsqueeze(1).float())
+    loss.backward()
+    ref = [(n, m.weight_mask.grad.abs()) for n, m in cp.named_modules() if hasattr(m, "weight_mask")]
+    assert [n for n, _ in scores] == [n for n, _ in ref]
+    for (_, a), (_, b) in zip(scores, ref):
+        assert torch.allclose(a, b, rtol=1e-5, atol=1e-8)
+    mean = get_mean_snip_scores([scores, scores])
+    keep, by_layer, final = get_mask_from_grads(owner, mean, 0.3, None)
+    flat = torch.cat([v.flatten() for v in mean.values()])
+    flat = flat / flat.sum()
+    thr = torch.topk(flat, int(flat.numel() * 0.3)).values[-1]
+    assert int(sum(int(v.sum()) for v in keep.values())) == int((flat >= thr).sum())
+    assert set(final) == {n for n, _ in owner.model.named_parameters()}
+    assert torch.equal(final["features.0.bias"], torch.ones(4))
+    assert len(by_layer) == 2
+
+
+def test_reference_helper_names():
+    """dispflAPI / FEDFOMOAPI class names, slim_util.cosine_annealing(args, round) and print_model_param_nums."""
+    import types
+    from fedml_api.standalone.DisPFL.dispfl_api import dispflAPI
+    from fedml_api.standalone.DisPFL.slim_util import cosine_annealing
+    from fedml_api.standalone.fedfomo.fedfomo_api import FEDFOMOAPI
+    from fedml_api.utils.main_flops_counter import print_model_param_nums
+    from neuroimagedisttraining_amd.algorithms.personalized import DisPFLAPI, FedFomoAPI
+    assert dispflAPI is DisPFLAPI and FEDFOMOAPI is FedFomoAPI
+    args = types.SimpleNamespace(anneal_factor=0.5, comm_round=10)
+    assert abs(cosine_annealing(args, 0) - 0.5) < 1e-12 and abs(cosine_annealing(args, 10)) < 1e-12
+    assert abs(cosine_annealing(args, 5) - 0.25) < 1e-12
+    net = torch.nn.Sequential(torch.nn.Conv2d(1, 2, 3), torch.nn.Conv3d(1, 2, 3), torch.nn.Linear(3, 4))
+    with torch.no_grad():
+        net[0].weight[0] = 0
+    assert print_model_param_nums(net) == 9 + 12

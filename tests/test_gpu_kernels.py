@@ -609,33 +609,37 @@ def test_conv1_fused_fwd_and_sparse_wgrad(signed):
 @pytest.mark.parametrize("NB,B", [(4, 2), (128, 16)])
 def test_conv1_fwd_wave_tile_matches_pipe(NB, B):
     """The wave-tile fused forward (k_conv1_fwd_w64: a wave owns all 64 channels of 15 columns, DPP pooling, packed
-    epilogue) computes every conv output with the same MFMA chains as the channel-split pipe kernel, so the pooled
-    bf16 outputs and the argmax bytes are bit-identical (random volumes, signed scales, per-client weights)."""
+    epilogue, and its own all-b128 k-slot layout RO = 2) against the channel-split pipe kernel (RO = 0 layout): each
+    mode packs the same fp32 weights with pack_conv1_w into its own slot order, so the MFMA k order differs and the
+    fp32 sums agree to rounding: the pooled bf16 outputs within 1 bf16 ulp of the output scale, the argmax bytes
+    equal except at near-ties (random volumes, signed scales, per-client weights)."""
     m = _m()
     g = torch.Generator(device=DEV).manual_seed(5)
     G = NB // B
     x8 = torch.randint(0, 256, (NB, 61, 73, 61, 8), dtype=torch.uint8, device=DEV, generator=g)
     idx = torch.randperm(NB, device=DEV, generator=g).int()
-    # packed weights: f16 bits of w in the 128-slot layout, the 3 empty slots zero
-    w = (torch.randn(G, 64, 128, device=DEV, generator=g) * 0.05).half()
-    w[:, :, 125:] = 0
-    w8 = w.view(torch.int16)
+    theta = torch.randn(G, 8000, device=DEV, generator=g) * 0.05
     scale = torch.randn(G, 64, device=DEV, generator=g) * 0.02
     shift = torch.randn(G, 64, device=DEV, generator=g)
     outs = []
     for mode in (0, 1):
+        m.conv1_fwd_mode(mode)
+        w8 = torch.zeros(G, 64, 128, dtype=torch.int16, device=DEV)
+        w125 = torch.zeros(G, 64, 125, device=DEV)
+        m.pack_conv1_w(theta.data_ptr(), 8000, 0, -1, G, 1.0 / 255.0, w8.data_ptr(), w125.data_ptr(), _st())
         p1 = torch.full((NB, 19, 23, 19, 64), float("nan"), device=DEV).bfloat16()
         a1 = torch.full((NB, 19, 23, 19, 64), 255, dtype=torch.uint8, device=DEV)
-        m.conv1_fwd_mode(mode)
         m.conv1_fwd_pool(x8.data_ptr(), idx.data_ptr(), w8.data_ptr(), scale.data_ptr(), shift.data_ptr(), NB, B,
                          p1.data_ptr(), a1.data_ptr(), _st())
         torch.cuda.synchronize()
-        outs.append((p1, a1))
+        outs.append((p1, a1, w125))
     m.conv1_fwd_mode(-1)
-    (p0, a0), (p1, a1) = outs
+    (p0, a0, w0), (p1, a1, w1) = outs
+    assert torch.equal(w0, w1)  # the effective weights do not depend on the slot order
     assert torch.isfinite(p1.float()).all() and int(a1.max()) < 27
-    assert torch.equal(p0.view(torch.int16), p1.view(torch.int16))
-    assert torch.equal(a0, a1)
+    d = (p0.float() - p1.float()).abs()
+    assert float(d.max()) <= float(p0.float().abs().max()) * 2 ** -7, float(d.max())
+    assert float((a0 != a1).float().mean()) < 1e-3
 
 
 @pytest.mark.parametrize("mode", [1, 2])

@@ -112,7 +112,22 @@ def test_gemm1x1_matches_fp32(K, N):
     m = ops.ext()
     assert m.gemm1x1_ok(K, N)
     torch.manual_seed(K + N)
-    G, Mg = 3, 2 * 64 * 9 + 37
+    G = 3
+    # a row count with a partial last m-tile, and one where some block's tile count T has T % 3 == 2 (its last tile's
+    # out-of-range DMA targets the stage array the [STATS] reduction reuses: the drain before that reduction)
+    bm = 32 if K == 512 else 64
+    mgs = [2 * 64 * 9 + 37]
+    for mg in range(64 * 3, 64 * 400, 64 * 7 + 11):
+        nch, nmt = m.gemm1x1_chunks(G, mg, K, N), (mg + bm - 1) // bm
+        if any(((nmt - 1 - mb) // nch + 1) % 3 == 2 for mb in range(min(nch, nmt))):
+            mgs.append(mg)
+            break
+    assert len(mgs) == 2
+    for Mg in mgs:
+        _gemm1x1_case(m, dev, G, Mg, K, N)
+
+
+def _gemm1x1_case(m, dev, G, Mg, K, N):
     x = torch.randn(G, Mg, K, device=dev).to(torch.bfloat16)
     w = (torch.randn(G, N, K, device=dev) * K ** -0.5).to(torch.bfloat16)
     y = torch.full((G, Mg, N), float("nan"), device=dev).to(torch.bfloat16)

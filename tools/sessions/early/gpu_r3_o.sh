@@ -1,7 +1,7 @@
 #!/bin/bash
 # r3_n (bf16 residual gradient: tests, config 5 timeline, CIFAR benches), then conv1 fwd occupancy A/B, then the
 # chaos-control cosines of the HIP-vs-fp32 runner comparison
-bash tools/gpu_r3_n.sh; rc=$?
+bash tools/sessions/early/gpu_r3_n.sh; rc=$?
 echo "r3_n rc=$rc"
 if [ $rc -gt 1 ]; then exit $rc; fi
 mkdir -p gpurun_out/r3o

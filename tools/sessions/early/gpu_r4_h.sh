@@ -1,6 +1,6 @@
 #!/bin/bash
 # G=8 (per-GPU load of the 8-GPU headline) A/B of the conv1 forward row split and the conv2 wgrad split-K, the Tiny /
-# CIFAR round-time diagnosis of round 3 (tools/gpu_r3_bc.sh), and the headline bench
+# CIFAR round-time diagnosis of round 3 (tools/sessions/early/gpu_r3_bc.sh), and the headline bench
 set -o pipefail
 export PYTHONUNBUFFERED=1
 mkdir -p gpurun_out/r4h
@@ -29,5 +29,5 @@ timeout -k 10 300 python bench.py --clients 8 --steps 10 --warmup 3 > gpurun_out
 echo "bench 8 clients: $(grep -o '"value": [0-9.]*' gpurun_out/r4h/bench_c8.json)"
 timeout -k 10 300 python bench.py --steps 10 --warmup 3 > gpurun_out/r4h/bench.json 2>&1 || exit 1
 echo "bench 64 clients: $(grep -o '"value": [0-9.]*' gpurun_out/r4h/bench.json)"
-bash tools/gpu_r3_bc.sh 2>&1 | tee gpurun_out/r4h/r3bc.txt
+bash tools/sessions/early/gpu_r3_bc.sh 2>&1 | tee gpurun_out/r4h/r3bc.txt
 cp -r gpurun_out/r3bc gpurun_out/r4h/ 2>/dev/null

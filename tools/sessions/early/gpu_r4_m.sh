@@ -1,7 +1,7 @@
 #!/bin/bash
 # New defaults (conv1 forward original tap order; 3-wave conv2 wgrad split at small groups): conv1/AlexNet numerics,
 # kbench G=8 / G=64, 8-client round kernel timeline, headline bench; then the Tiny / SubAvg regression switches
-# (tools/gpu_r3_bc.sh)
+# (tools/sessions/early/gpu_r3_bc.sh)
 set -o pipefail
 export PYTHONUNBUFFERED=1
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
@@ -23,4 +23,4 @@ timeout -k 10 300 python bench.py --clients 8 --steps 10 --warmup 3 > $OUT/bench
 echo "bench 8 clients: $(grep -o '"value": [0-9.]*' $OUT/bench_c8_noprof.json)"
 timeout -k 10 300 python bench.py --steps 10 --warmup 3 > $OUT/bench.json 2>&1 || exit 1
 echo "bench 64 clients: $(grep -o '"value": [0-9.]*' $OUT/bench.json)"
-bash tools/gpu_r3_bc.sh
+bash tools/sessions/early/gpu_r3_bc.sh
