@@ -64,6 +64,9 @@ def parse(argv=None):
     ap.add_argument("--prox-mu", type=float, default=0.01)
     ap.add_argument("--cs", default="ring", help="D-PSGD topology")
     ap.add_argument("--phase-timers", action="store_true", help="synchronised per-phase timers (adds syncs)")
+    ap.add_argument("--dump-rows", default="", help="after the run, save this rank's client rows (each client's "
+                    "last locally trained params, i.e. the rows before the last aggregation) to <prefix>.rank<r>.pt "
+                    "(sharding-parity checks: tools/compare_rows.py)")
     ap.add_argument("--step-streams", type=int, default=4,
                     help="side streams for the extra (ragged) launches of one lockstep step (1 = serial)")
     ap.add_argument("--rebalance", type=int, default=0,
@@ -318,6 +321,10 @@ def run(args):
         if args.phase_timers:
             out["phase_s"] = {k: round(v, 3) for k, v in runner.timers.items()}
         print(json.dumps(out), flush=True)
+    if args.dump_rows:
+        rows, loc = runner._local_rows(range(args.clients))
+        torch.save({int(c): runner.theta[r, :runner.P].detach().cpu() for r, c in zip(rows, loc)},
+                   "%s.rank%d.pt" % (args.dump_rows, info.rank))
     rt.shutdown(info)
 
 

@@ -63,6 +63,8 @@ def add_args(parser, algo):
     a("--model", type=str, default=d["model"])
     a("--dataset", type=str, default=d["dataset"])
     a("--data_dir", type=str, default="")
+    # Tiny-ImageNet: reproduce the reference loader's reshape(-1, 3, 64, 64) pixel scramble (PARITY.md §2.5)
+    a("--tiny_ref_pixel_order", type=int, default=0)
     a("--partition_method", type=str, default=d.get("partition_method", "dir"))
     a("--partition_alpha", type=float, default=0.3)
     a("--batch_size", type=int, default=d["batch_size"])
@@ -205,7 +207,8 @@ def load_data(args, dataset_name, logger=None):
         return images.load_partition_data(dataset_name, args.data_dir, args.partition_method, args.partition_alpha,
                                           args.client_num_in_total, args.batch_size, logger, seed=args.seed,
                                           with_val=getattr(args, "algo", "") == "fedfomo", n_train=n,
-                                          n_test=n // 5 if n else None, augment=bool(getattr(args, "augment", 1)))
+                                          n_test=n // 5 if n else None, augment=bool(getattr(args, "augment", 1)),
+                                          ref_pixel_order=bool(getattr(args, "tiny_ref_pixel_order", 0)))
     if dataset_name == "synthetic":
         return images.load_partition_data_synthetic_tabular(args.client_num_in_total, args.batch_size)
     raise ValueError(dataset_name)
@@ -387,20 +390,17 @@ def image_cohort(args, info, with_val=False):
     ``+n_train``), split exactly as the eager loaders do (``data/images.load_partition_data``: same partitioner, same
     RandomState stream, per-client test sets drawn from the train label histogram, FedFomo's 10 % validation split).
 
-    Pixels: an ``.npz`` (``--data_dir``) holding uint8 HWC images is used as is (the engine applies the dataset's
-    mean/std normalisation, ``images.NORM``); float images (the synthetic loader's, or a float ``.npz``) are taken
-    to be normalised NCHW tensors and mapped back to uint8 pixels."""
+    Pixels: uint8 HWC images (the reference's dataset directories, ``data/image_files.py``, or a uint8 ``.npz``) are
+    used as is (the engine applies the dataset's mean/std normalisation on device, as the eager loaders do on the
+    host, ``images.NORM``); float images (the synthetic loader's, or a float ``.npz``) are taken to be normalised
+    NCHW tensors and mapped back to uint8 pixels."""
     from .core import partition as PT
     from .data import images
     from .engine.executor import ClientSplit
     MEAN, STD = images.NORM[args.dataset]
     n = getattr(args, "synthetic_size", 0) or None
-    xtr, ytr, xte, yte, n_cls = images._load_arrays(args.dataset, args.data_dir, n, n // 5 if n else None,
-                                                     args.seed)
-    if args.data_dir and args.data_dir.endswith(".npz"):
-        d = np.load(args.data_dir, allow_pickle=False)
-        if d["x_train"].dtype == np.uint8 and d["x_train"].shape[-1] == 3:
-            xtr, xte = torch.from_numpy(d["x_train"]), torch.from_numpy(d["x_test"])
+    xtr, ytr, xte, yte, n_cls = images.load_raw(args.dataset, args.data_dir, n, n // 5 if n else None, args.seed,
+                                                 bool(getattr(args, "tiny_ref_pixel_order", 0)))
 
     def to_u8(x):
         if x.dtype == torch.uint8:

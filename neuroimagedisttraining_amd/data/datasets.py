@@ -2,12 +2,12 @@
 datasets.py:36-92`` ``CIFAR10_truncated`` / ``CIFAR100_truncated`` and ``tiny_imagenet/datasets.py:20-270``
 ``tiny`` / ``tiny_truncated``).
 
-The reference wraps torchvision datasets (downloaded from the network) and decodes Tiny-ImageNet JPEGs into a
-pickle cache.  Neither is possible here (no network, no torchvision, and pickles are never loaded), so the
-backing arrays come from, in order: an explicit ``cache_data_set`` object with ``.data`` / ``.targets``
-(the reference's in-memory cache argument), an ``.npz`` at ``root`` (``x_train, y_train, x_test, y_test``,
-loaded with ``allow_pickle=False``), or the synthetic class-conditional images of ``data/images.py`` of the
-dataset's real shape.  ``.data`` is HWC like torchvision's, so transforms written for the reference keep
+The reference wraps torchvision datasets and decodes Tiny-ImageNet JPEGs into a pickle cache.  Here (no
+network, no torchvision, nothing unpickled) the backing arrays come from, in order: an explicit
+``cache_data_set`` object with ``.data`` / ``.targets`` (the reference's in-memory cache argument), an ``.npz``
+at ``root`` (``x_train, y_train, x_test, y_test``, loaded with ``allow_pickle=False``), the reference's dataset
+directory at ``root`` (CIFAR binary batches, Tiny-ImageNet list files + JPEGs: ``data/image_files.py``), or —
+only when ``root`` is empty — the synthetic class-conditional images of ``data/images.py``.  ``.data`` is HWC like torchvision's, so transforms written for the reference keep
 working; without a transform an item is a CHW float tensor.
 """
 from __future__ import annotations
@@ -29,8 +29,10 @@ class ArrayData:
         self.targets = list(np.asarray(targets).tolist())
 
 
-def load_arrays(name, root, train=True, n=None, seed=0):
-    """(data [N,H,W,C] float32, targets [N] int64) for ``name`` in {cifar10, cifar100, tiny}."""
+def load_arrays(name, root, train=True, n=None, seed=0, ref_pixel_order=False):
+    """(data [N,H,W,C], targets [N] int64) for ``name`` in {cifar10, cifar100, tiny}: uint8 pixels from the
+    reference's dataset directories (``data/image_files.py``) or an ``.npz``; synthetic float images only without a
+    ``root`` (a ``root`` with no dataset files raises)."""
     shape, n_cls, ntr, nte = SPECS[name]
     if root and os.path.isfile(root) and root.endswith(".npz"):
         d = np.load(root, allow_pickle=False)
@@ -39,6 +41,9 @@ def load_arrays(name, root, train=True, n=None, seed=0):
         if x.ndim == 4 and x.shape[1] in (1, 3) and x.shape[-1] not in (1, 3):
             x = np.transpose(x, (0, 2, 3, 1))
         return np.ascontiguousarray(x), np.asarray(y, dtype=np.int64)
+    if root:
+        from .image_files import read_image_split
+        return read_image_split(name, root, train, ref_pixel_order)
     n = n or (ntr if train else nte)
     x, y = synthetic_images(n, shape, n_cls, seed=seed + (0 if train else 1))
     return x.permute(0, 2, 3, 1).contiguous().numpy(), y.numpy()
@@ -98,8 +103,9 @@ class tiny_truncated(TruncatedDataset):  # noqa: N801
 
 class tiny(Dataset):  # noqa: N801
     """Whole Tiny-ImageNet split (``tiny_imagenet/datasets.py:20-210``): 200 classes of 3x64x64.  The reference
-    decodes ``root/{train,val}`` JPEGs once and caches a pickle; here the split comes from an ``.npz`` at
-    ``root`` or is synthesised, and nothing is cached or unpickled."""
+    decodes ``root/tiny-imagenet-200/{train,val}_list.txt`` JPEGs once and caches a pickle; here the same files are
+    decoded with PIL and cached as an ``.npz`` (``data/image_files.py``), or the split comes from an ``.npz`` at
+    ``root`` or is synthesised (empty ``root``)."""
 
     def __init__(self, root, train=True, transform=None, target_transform=None, n=None):
         self.root, self.train = root, train

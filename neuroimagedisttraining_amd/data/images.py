@@ -1,9 +1,11 @@
 """CIFAR-10 / CIFAR-100 / Tiny-ImageNet / tabular federated loaders (reference
 ``fedml_api/data_preprocessing/{cifar10,cifar100,tiny_imagenet}/{data_loader,data_val_loader}.py``).
 
-There is no network and no dataset files in this environment, so each loader builds a synthetic dataset of the
-real shape and class count (class-conditional smooth patterns + noise, learnable), unless ``data_dir`` holds an
-``.npz`` with ``x_train, y_train, x_test, y_test`` (loaded with ``allow_pickle=False``).  Partitioning and the
+Images come from ``data_dir``: the reference's dataset directories (Tiny-ImageNet list files + JPEGs, the CIFAR
+binary batches: ``data/image_files.py``) or an ``.npz`` with ``x_train, y_train, x_test, y_test`` (loaded with
+``allow_pickle=False``); uint8 pixels are normalised with the reference loader's mean/std.  Without a
+``data_dir`` each loader builds a synthetic dataset of the real shape and class count (class-conditional smooth
+patterns + noise, learnable); a ``data_dir`` that holds no dataset files raises.  Partitioning and the
 per-client test / validation construction follow the reference exactly:
 
 * train split: ``partition_method`` in {dir, n_cls, my_part, homo, hetero};
@@ -47,17 +49,56 @@ def synthetic_images(n, shape, n_cls, seed=0, noise=0.6, template_seed=12345):
     return x.float(), y.long()
 
 
-def _load_arrays(dataset, data_dir, n_train=None, n_test=None, seed=0):
+def _as_hwc(x):
+    x = np.asarray(x)
+    if x.ndim == 4 and x.shape[1] in (1, 3) and x.shape[-1] not in (1, 3):
+        x = np.transpose(x, (0, 2, 3, 1))
+    return np.ascontiguousarray(x)
+
+
+def load_raw(dataset, data_dir, n_train=None, n_test=None, seed=0, ref_pixel_order=False):
+    """``(x_train, y_train, x_test, y_test, n_cls)`` of ``dataset`` as the files hold them: uint8 ``[N, H, W, C]``
+    pixels for the reference's dataset directories (``data/image_files.py``) and uint8 ``.npz`` files; normalised
+    float ``[N, C, H, W]`` for a float ``.npz`` and for the synthetic images, which are only made when no
+    ``data_dir`` is given — a ``data_dir`` without dataset files raises."""
     shape, n_cls, ntr, nte = SPECS[dataset]
-    if data_dir and os.path.isfile(data_dir) and data_dir.endswith(".npz"):
-        d = np.load(data_dir, allow_pickle=False)
-        return (torch.from_numpy(d["x_train"]).float(), torch.from_numpy(d["y_train"]).long(),
-                torch.from_numpy(d["x_test"]).float(), torch.from_numpy(d["y_test"]).long(), n_cls)
+    if data_dir:
+        if os.path.isfile(data_dir) and data_dir.endswith(".npz"):
+            d = np.load(data_dir, allow_pickle=False)
+            xs = [d["x_train"], d["x_test"]]
+            if xs[0].dtype == np.uint8:
+                xs = [torch.from_numpy(_as_hwc(x)) for x in xs]
+            else:
+                xs = [torch.from_numpy(np.asarray(x)).float() for x in xs]
+            return xs[0], torch.from_numpy(d["y_train"]).long(), xs[1], torch.from_numpy(d["y_test"]).long(), n_cls
+        from .image_files import read_image_split
+        xtr, ytr = read_image_split(dataset, data_dir, True, ref_pixel_order)
+        xte, yte = read_image_split(dataset, data_dir, False, ref_pixel_order)
+        return torch.from_numpy(xtr), torch.from_numpy(ytr), torch.from_numpy(xte), torch.from_numpy(yte), n_cls
     ntr = n_train or ntr
     nte = n_test or nte
     xtr, ytr = synthetic_images(ntr, shape, n_cls, seed)
     xte, yte = synthetic_images(nte, shape, n_cls, seed + 1)
-    log.info("%s: no data files, using synthetic %s images (%d train / %d test)", dataset, shape, ntr, nte)
+    log.info("%s: no --data_dir, using synthetic %s images (%d train / %d test)", dataset, shape, ntr, nte)
+    return xtr, ytr, xte, yte, n_cls
+
+
+def normalise_u8(x, dataset):
+    """uint8 ``[N, H, W, C]`` pixels -> float ``[N, C, H, W]``: ``ToTensor`` (/255) then the reference loader's
+    ``Normalize(mean, std)`` (``NORM``; datasets without one stop after ``ToTensor``)."""
+    f = x.permute(0, 3, 1, 2).float().div_(255.0)
+    if dataset in NORM:
+        mean, std = NORM[dataset]
+        f.sub_(torch.tensor(mean).view(1, -1, 1, 1)).div_(torch.tensor(std).view(1, -1, 1, 1))
+    return f.contiguous()
+
+
+def _load_arrays(dataset, data_dir, n_train=None, n_test=None, seed=0, ref_pixel_order=False):
+    """The eager loaders' arrays: normalised float NCHW images (uint8 pixels are normalised here, as the HIP image
+    engine normalises them on device) and int64 labels."""
+    xtr, ytr, xte, yte, n_cls = load_raw(dataset, data_dir, n_train, n_test, seed, ref_pixel_order)
+    if xtr.dtype == torch.uint8:
+        xtr, xte = normalise_u8(xtr, dataset), normalise_u8(xte, dataset)
     return xtr, ytr, xte, yte, n_cls
 
 
@@ -109,14 +150,15 @@ def partition_data(y_train, partition, n_clients, alpha, n_cls, rng=None):
 
 
 def load_partition_data(dataset, data_dir, partition_method, partition_alpha, client_number, batch_size,
-                        logger=None, n_train=None, n_test=None, seed=0, with_val=False, augment=True):
+                        logger=None, n_train=None, n_test=None, seed=0, with_val=False, augment=True,
+                        ref_pixel_order=False):
     """``augment``: the reference's train-time RandomCrop(pad 4) + RandomHorizontalFlip on the train loaders of the
     image datasets.  Test loaders are not augmented, as in the reference; validation loaders are not either, which
     deviates from the reference's FedFomo validation loader (built with ``transform_train``,
     ``cifar10/data_val_loader.py:248,309``) — see PARITY.md §2.5."""
     logger = logger or log
     aug = NORM.get(dataset) if augment else None
-    xtr, ytr, xte, yte, n_cls = _load_arrays(dataset, data_dir, n_train, n_test, seed)
+    xtr, ytr, xte, yte, n_cls = _load_arrays(dataset, data_dir, n_train, n_test, seed, ref_pixel_order)
     rng = np.random.RandomState(seed)
     train_map = partition_data(ytr.numpy(), partition_method, client_number, partition_alpha, n_cls, rng)
     test_map = P.per_client_test_indices(ytr.numpy(), yte.numpy(), train_map, n_cls=n_cls, rng=rng)

@@ -1016,14 +1016,15 @@ class FLRunner:
         for Krum and are coordinate-aggregated otherwise."""
         from ..core import robustness as R
         rows, loc = self._local_rows(sampled)
-        ids = self._to_dev(loc, torch.float32)
         W = self.P + self.Q
-        lm = torch.cat([self.theta[rows, :self.P], self.bufs[rows, :self.Q]], 1) if rows else \
-            torch.zeros((0, W), device=self.device)
-        allrows = rt.all_gather_cat(lm.reshape(-1).contiguous(), self.info).view(-1, W)
-        allids = rt.all_gather_cat(ids, self.info).long()
-        order = torch.argsort(allids)  # deterministic client order on every rank
-        M = allrows.index_select(0, order)
+        # one record per client: [id, params, buffers]; every rank knows how many sampled clients each rank owns,
+        # so the gather needs no size exchange (no host round trip)
+        lm = torch.cat([self._to_dev(loc, torch.float32).view(-1, 1), self.theta[rows, :self.P],
+                        self.bufs[rows, :self.Q]], 1) if rows else torch.zeros((0, 1 + W), device=self.device)
+        per_rank = [sum(1 for c in sampled if self.owner[c] == r) * (1 + W) for r in range(self.info.world)]
+        allrows = rt.all_gather_sized(lm.reshape(-1).contiguous(), per_rank, self.info).view(-1, 1 + W)
+        order = torch.argsort(allrows[:, 0])  # deterministic client order on every rank
+        M = allrows[:, 1:].index_select(0, order)
         kind = self.cfg.aggregator
         if kind in ("krum", "multikrum"):
             m = 1 if kind == "krum" else (self.cfg.multikrum_m or max(1, M.shape[0] - self.cfg.byzantine_f))

@@ -93,12 +93,14 @@ def test_truncated_datasets():
     assert len(ds) == 3 and list(ds.target) == [1, 2, 2]
     x, y = ds[0]
     assert x.shape == (3, 32, 32) and y == 1 and torch.allclose(x, torch.from_numpy(data[7]).permute(2, 0, 1))
-    ds2 = CIFAR10_truncated("unused", dataidxs=[0, 1], n=16, transform=lambda im: torch.as_tensor(im).mean())
+    ds2 = CIFAR10_truncated("", dataidxs=[0, 1], n=16, transform=lambda im: torch.as_tensor(im).mean())
     assert len(ds2) == 2 and ds2[1][0].dim() == 0
-    t = tiny("unused", n=8)
+    t = tiny("", n=8)  # no root: synthetic images of the real shape
     assert len(t) == 8 and t[0][0].shape == (3, 64, 64)
-    tt = tiny_truncated("unused", dataidxs=[1, 3], n=8)
+    tt = tiny_truncated("", dataidxs=[1, 3], n=8)
     assert len(tt) == 2
+    with pytest.raises(FileNotFoundError):  # a root without dataset files is an error, not silent noise
+        tiny("no/such/dir", n=8)
 
 
 def test_genotype_dot_export(tmp_path):

@@ -150,6 +150,48 @@ def test_two_rank_gloo_matches_single_process(tmp_path, cfg_kw):
     assert np.allclose(got["acc"], r.stat_info["global_test_acc"])
 
 
+def _rows_worker(rank, world, port, out):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.save(_trained_rows(rank, world), "%s.%d" % (out, rank))
+    dist.destroy_process_group()
+
+
+def _trained_rows(rank=0, world=1):
+    """Each local client's row after round 0's local training (before the first aggregation)."""
+    r = _runner(rank, world)
+    r.generate_global_mask_snip()
+    r._round_start(0)
+    sampled = r.sample_clients(0)
+    r.local_train(0, sampled)
+    rows, loc = r._local_rows(range(r.N))
+    return {int(c): r.theta[i].clone() for i, c in zip(rows, loc)}
+
+
+def test_sharded_rows_bit_identical_to_single_process(tmp_path):
+    """A client's local training does not depend on which rank trains it: after the SNIP mask and round 0's local
+    training, every client row of 2 gloo ranks is bit-identical to the same client's row in one process.  (Later
+    rounds start from an all-reduced global model, whose summation order differs across layouts: the two-rank test
+    above checks that at fp32 rounding.)"""
+    import socket
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    out = str(tmp_path / "rows")
+    mp.start_processes(_rows_worker, args=(2, port, out), nprocs=2, join=True, start_method="spawn")
+    got = {}
+    for k in range(2):
+        got.update(torch.load("%s.%d" % (out, k), weights_only=True))
+    ref = _trained_rows()
+    assert set(got) == set(ref) and len(ref) > 2
+    bad = [c for c in ref if not torch.equal(got[c], ref[c])]
+    assert not bad, bad
+
+
 def test_executor_robust_aggregation_rejects_outlier():
     from neuroimagedisttraining_amd.core import robustness as R
     for kind in ("krum", "multikrum", "median", "trimmed_mean"):
