@@ -915,10 +915,11 @@ void conv1_fwd_pool(uintptr_t x8, uintptr_t idx, uintptr_t w8, uintptr_t scale, 
       const char* e = getenv("NIDT_C1_NQ");
       return e ? std::max(1, std::min(kPH, atoi(e))) : 1;
     }();
-    // B-fragment prefetch distance of the RO = 2 kernel in k-steps (NIDT_C1_WPF, A/B), default 2
+    // B-fragment prefetch distance of the RO = 2 kernel in k-steps (NIDT_C1_WPF, A/B), default 4 (3.28 ms per
+    // 64-client step vs 3.35 at 2; the RO = 0 kernel, 45.7 % bank conflicts, also 3.28: profiles/r6_conv1_b128.txt)
     static const int wpf = [] {
       const char* e = getenv("NIDT_C1_WPF");
-      return e ? atoi(e) : 2;
+      return e ? atoi(e) : 4;
     }();
     if (conv1_tapord() == 2 && wpf == 3)
       hipLaunchKernelGGL((k_conv1_fwd_w64<3, 2>), dim3(kPD * NB * nq1), dim3(256), 0, as_stream(stream),

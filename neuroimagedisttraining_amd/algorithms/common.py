@@ -12,6 +12,7 @@ Reference behaviours reproduced (SURVEY.md §2.2 "Shared algorithm behaviors"):
 from __future__ import annotations
 
 import copy
+import functools
 import logging
 
 import numpy as np
@@ -123,7 +124,32 @@ def init_stat_info(class_counts=None):
 
 
 class APIBase:
-    """Common constructor: unpacks the dataset 8/9-tuple and builds one Client per client."""
+    """Common constructor: unpacks the dataset 8/9-tuple and builds one Client per client.
+
+    ``train()`` of every subclass first offers the run to the client-batched MI355X executor
+    (``algorithms/hip_dispatch.py``: a GPU device, the built extension and a supported model / data layout); the
+    eager, sequential-client loop of the subclass is the fallback and the test oracle (``args.engine = "torch"``
+    or ``NIDT_API_ENGINE=torch`` forces it).  ``engine_used`` says which one ran."""
+
+    engine_used = None
+
+    def __init_subclass__(cls, **kw):
+        super().__init_subclass__(**kw)
+        if "train" not in cls.__dict__:
+            return
+        eager = cls.__dict__["train"]
+
+        @functools.wraps(eager)
+        def train(self, *a, **k):
+            if not getattr(self, "_hip_offered", False):
+                self._hip_offered = True
+                from .hip_dispatch import try_train_on_hip
+                if try_train_on_hip(self):
+                    return None
+                self.engine_used = "eager"
+            return eager(self, *a, **k)
+
+        cls.train = train
 
     def record_avg_inference_flops(self, w_global, mask_pers=None):
         """Mean over clients of the sparse-aware inference FLOPs of ``w_global`` (under each client's personal

@@ -33,6 +33,7 @@ def test_fedavg_logistic_regression_two_clients_learns():
     tr = ClassificationTrainer(LogisticRegression(20, 5), args)
     api = FedAvgAPI(ds, torch.device("cpu"), args, tr)
     api.train()
+    assert api.engine_used == "eager"  # a CPU device keeps the eager loop (the HIP dispatch needs a GPU)
     acc = api.stat_info["global_test_acc"]
     assert acc[-1] > 0.5 and acc[-1] >= acc[0]
 
