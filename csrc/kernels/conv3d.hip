@@ -23,6 +23,7 @@
 #include <array>
 #include <cstdlib>
 #include <map>
+#include <type_traits>
 
 #include <vector>
 
@@ -2396,12 +2397,18 @@ int conv3d_union_umax(int B, int D, int H, int W, int pad, int P) { return union
 // read -> 1.00).  The dY rows are the step's positions themselves and keep swz_wd of their row.  Measured: conflicts
 // 20.8 / 33.2 % -> 0.1 / 1.7 % (conv2 / conv3-5) but conv2 2.92-2.98 -> 3.22-3.29 ms (the per-step swizzle of the
 // DMA addresses sits on the issue path); opt-in NIDT_WGTRI_LSWZ=1 (profiles/r4_ab_lds_swizzle.txt).
-template <int NCH, int U, bool PADDED, bool LSW = true, bool SCHED = false>
+// [ADMA] the stage DMA issued from inline asm (blds16_asm) instead of the intrinsic: the compiler's waitcnt pass
+// treats an intrinsic LDS-DMA as a write to LDS that the fragment reads of the current stage may alias, and put a
+// vmcnt wait for the next stage's DMA (issued at the top of the step) in front of them — the double buffer never
+// overlapped a transfer with the MFMAs of its own wave.  The kernel's counted waits at the end of each step already
+// order every DMA before its stage is read; M0 is used by nothing else here.
+template <int NCH, int U, bool PADDED, bool LSW = true, bool SCHED = false, bool ADMA = false>
 __global__ __launch_bounds__(192 * NCH, 2) void k_conv_wgrad_tri(ConvWgTriArgs a) {
   constexpr int NW = 3 * NCH, XG = U * kWdRow, BUFE = XG + NCH * kWdGroup, ST = WtTab<U>::kST;
   constexpr int XP = U / 8, XPW = (XP + NW - 1) / NW;       // union pieces (8 rows each) per wave
   constexpr int DP = 8 * NCH, DPW = (DP + NW - 1) / NW;     // dY pieces (8 positions x 64 co) per wave
   __shared__ __attribute__((aligned(16))) uint16_t smem[2 * BUFE];
+  auto stage = [&](int k) -> uint16_t* { return smem + k * BUFE; };
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wc = wid / 3, kw = wid - 3 * wc;
@@ -2437,6 +2444,10 @@ __global__ __launch_bounds__(192 * NCH, 2) void k_conv_wgrad_tri(ConvWgTriArgs a
   const int rr0 = 8 * gq + qq, rr1 = rr0 + 4;
   i32x2_t trow[XPW];
   int tix[4], tixn[4];
+  auto wt_dma = [](i32x4_t r, int off, uint16_t* dst) {
+    if constexpr (ADMA) blds16_asm(r, off, dst);
+    else blds16(r, off, dst);
+  };
 #define WT_FETCH_ROWS(S)                                                                                      \
   {                                                                                                           \
     _Pragma("unroll") for (int i_ = 0; i_ < XPW; ++i_)                                                        \
@@ -2448,23 +2459,24 @@ __global__ __launch_bounds__(192 * NCH, 2) void k_conv_wgrad_tri(ConvWgTriArgs a
       DST[k_] = nidt_raw_buffer_load_i32(rt, ((S) * ST + 2 * U + 32 * (k_ >> 1) + ((k_ & 1) ? rr1 : rr0)) * 4, \
                                          0, 0);                                                               \
   }
-#define WT_ISSUE(S, BUFI)                                                                                     \
+#define WT_ISSUE_R(S, BUFI, TR)                                                                               \
   {                                                                                                           \
-    uint16_t* sX_ = smem + (BUFI) * BUFE;                                                                     \
+    uint16_t* sX_ = stage(BUFI);                                                                              \
     uint16_t* sD_ = sX_ + XG;                                                                                 \
     _Pragma("unroll") for (int i_ = 0; i_ < XPW; ++i_)                                                        \
       if (wid * XPW + i_ < XP) {                                                                              \
-        const int c_ = trow[i_].y;                                                                            \
+        const int c_ = TR[i_].y;                                                                              \
         const bool ok_ = PADDED ? ((unsigned)((c_ & 1023) - dlo) < (unsigned)a.D &&                            \
                                    (unsigned)(((c_ >> 10) & 1023) - hlo) < (unsigned)a.H &&                   \
                                    (unsigned)((c_ >> 20) - a.pad) < (unsigned)a.W)                            \
                                 : (c_ & 1023) != 1023;                                                        \
         const int sw_ = LSW ? ((ls ^ swz_wd(((c_ & 1023) * Ho + ((c_ >> 10) & 1023)) * Wo + (c_ >> 20))) << 4) : 0; \
-        blds16(rx, ok_ ? (trow[i_].x + xadd) * (2 * Cin) + xcol[i_] + sw_ : kBufOOB, sX_ + (wid * XPW + i_) * 512); \
+        wt_dma(rx, ok_ ? (TR[i_].x + xadd) * (2 * Cin) + xcol[i_] + sw_ : kBufOOB, sX_ + (wid * XPW + i_) * 512); \
       }                                                                                                       \
     _Pragma("unroll") for (int i_ = 0; i_ < DPW; ++i_)                                                        \
-      if (wid * DPW + i_ < DP) blds16(rd, (S) * 64 * (2 * a.Cout) + dcol[i_], sD_ + dls[i_]);               \
+      if (wid * DPW + i_ < DP) wt_dma(rd, (S) * 64 * (2 * a.Cout) + dcol[i_], sD_ + dls[i_]);               \
   }
+#define WT_ISSUE(S, BUFI) WT_ISSUE_R(S, BUFI, trow)
 
   f32x4 acc[4][4];
 #pragma unroll
@@ -2477,6 +2489,50 @@ __global__ __launch_bounds__(192 * NCH, 2) void k_conv_wgrad_tri(ConvWgTriArgs a
   int lpos[4];
 #pragma unroll
   for (int k = 0; k < 4; ++k) lpos[k] = (s0 * 64 + 32 * (k >> 1) + ((k & 1) ? rr1 : rr0)) % So;
+  // the k-step: 32 MFMAs per wave from stage buffer `buf` with union-row indices tx of this step's positions
+  auto compute = [&](const uint16_t* sX, const int (&tx)[4]) {
+    const uint16_t* sD = sX + XG + wc * kWdGroup;
+    if constexpr (SCHED) {  // [SCHED] (kstep_sched)
+      kstep_sched<4, 4, 2>(
+          acc,
+          [&](int kk, int i) {
+            const int ra = 32 * kk + rr0, rb = 32 * kk + rr1, c = 2 * i + (pp >> 1);
+            return tr_pair(sD + ra * kWdRow + ((c ^ swz_wd(ra)) << 3) + (pp & 1) * 4,
+                           sD + rb * kWdRow + ((c ^ swz_wd(rb)) << 3) + (pp & 1) * 4);
+          },
+          [&](int kk, int j) {
+            const int xa = tx[2 * kk] + kw, xb = tx[2 * kk + 1] + kw, c = 2 * j + (pp >> 1);
+            const int sxa = swz_wd(LSW ? lpos[2 * kk] + kw : xa), sxb = swz_wd(LSW ? lpos[2 * kk + 1] + kw : xb);
+            return tr_pair(sX + xa * kWdRow + ((c ^ sxa) << 3) + (pp & 1) * 4,
+                           sX + xb * kWdRow + ((c ^ sxb) << 3) + (pp & 1) * 4);
+          });
+    } else {
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const int ra = 32 * kk + rr0, rb = 32 * kk + rr1;
+        const int xa = tx[2 * kk] + kw, xb = tx[2 * kk + 1] + kw;
+        const int sxa = swz_wd(LSW ? lpos[2 * kk] + kw : xa), sxb = swz_wd(LSW ? lpos[2 * kk + 1] + kw : xb);
+        bf16x8 fa[4], fb[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int c = 2 * i + (pp >> 1);
+          fa[i] = tr_pair(sD + ra * kWdRow + ((c ^ swz_wd(ra)) << 3) + (pp & 1) * 4,
+                          sD + rb * kWdRow + ((c ^ swz_wd(rb)) << 3) + (pp & 1) * 4);
+          fb[i] = tr_pair(sX + xa * kWdRow + ((c ^ sxa) << 3) + (pp & 1) * 4,
+                          sX + xb * kWdRow + ((c ^ sxb) << 3) + (pp & 1) * 4);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      lpos[k] += 64;
+      lpos[k] -= lpos[k] >= So ? So : 0;  // So >= 64 for every eligible shape (host check)
+    }
+  };
   if (nsteps > 0) {
     WT_FETCH_ROWS(s0)
     WT_FETCH_IDX(s0, tixn)
@@ -2490,60 +2546,39 @@ __global__ __launch_bounds__(192 * NCH, 2) void k_conv_wgrad_tri(ConvWgTriArgs a
     const int cur = st & 1;
 #pragma unroll
     for (int k = 0; k < 4; ++k) tix[k] = tixn[k];
-    if (st + 1 < nsteps) {
-      WT_ISSUE(s0 + st + 1, cur ^ 1)
-      if (st + 2 < nsteps) WT_FETCH_ROWS(s0 + st + 2)
-      WT_FETCH_IDX(s0 + st + 1, tixn)
-    }
-    const uint16_t* sX = smem + cur * BUFE;
-    const uint16_t* sD = sX + XG + wc * kWdGroup;
-    if constexpr (SCHED) {  // [SCHED] (kstep_sched)
-      kstep_sched<4, 4, 2>(
-          acc,
-          [&](int kk, int i) {
-            const int ra = 32 * kk + rr0, rb = 32 * kk + rr1, c = 2 * i + (pp >> 1);
-            return tr_pair(sD + ra * kWdRow + ((c ^ swz_wd(ra)) << 3) + (pp & 1) * 4,
-                           sD + rb * kWdRow + ((c ^ swz_wd(rb)) << 3) + (pp & 1) * 4);
-          },
-          [&](int kk, int j) {
-            const int xa = tix[2 * kk] + kw, xb = tix[2 * kk + 1] + kw, c = 2 * j + (pp >> 1);
-            const int sxa = swz_wd(LSW ? lpos[2 * kk] + kw : xa), sxb = swz_wd(LSW ? lpos[2 * kk + 1] + kw : xb);
-            return tr_pair(sX + xa * kWdRow + ((c ^ sxa) << 3) + (pp & 1) * 4,
-                           sX + xb * kWdRow + ((c ^ sxb) << 3) + (pp & 1) * 4);
-          });
-    } else {
+    if constexpr (ADMA) {
+      // [ADMA] the step-table loads (rows of st + 2, indices of st + 1) go out first, then the asm DMA of st + 1 from
+      // the rows fetched a step ago (rdma): the compiler, which counts only the loads it sees, never has to wait for
+      // anything younger than the DMA to feed it, and nothing of this step reads those new registers, so the only
+      // wait for the DMA is ours at the end of the step — the transfer overlaps this step's MFMAs
+      i32x2_t rdma[XPW];
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      const int ra = 32 * kk + rr0, rb = 32 * kk + rr1;
-      const int xa = tix[2 * kk] + kw, xb = tix[2 * kk + 1] + kw;
-      const int sxa = swz_wd(LSW ? lpos[2 * kk] + kw : xa), sxb = swz_wd(LSW ? lpos[2 * kk + 1] + kw : xb);
-      bf16x8 fa[4], fb[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int c = 2 * i + (pp >> 1);
-        fa[i] = tr_pair(sD + ra * kWdRow + ((c ^ swz_wd(ra)) << 3) + (pp & 1) * 4,
-                        sD + rb * kWdRow + ((c ^ swz_wd(rb)) << 3) + (pp & 1) * 4);
-        fb[i] = tr_pair(sX + xa * kWdRow + ((c ^ sxa) << 3) + (pp & 1) * 4,
-                        sX + xb * kWdRow + ((c ^ sxb) << 3) + (pp & 1) * 4);
+      for (int i = 0; i < XPW; ++i) rdma[i] = trow[i];
+      if (st + 1 < nsteps) {
+        if (st + 2 < nsteps) WT_FETCH_ROWS(s0 + st + 2)
+        WT_FETCH_IDX(s0 + st + 1, tixn)
+        WT_ISSUE_R(s0 + st + 1, cur ^ 1, rdma)
       }
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+      compute(stage(cur), tix);
+      // s_waitcnt vmcnt(0) lgkmcnt(0) as the builtin, which the waitcnt pass sees (with an asm wait it would still
+      // count this step's table loads as pending and wait for them in front of the next step's DMA)
+      __builtin_amdgcn_s_waitcnt(7 << 4);
+    } else {
+      if (st + 1 < nsteps) {
+        WT_ISSUE(s0 + st + 1, cur ^ 1)
+        if (st + 2 < nsteps) WT_FETCH_ROWS(s0 + st + 2)
+        WT_FETCH_IDX(s0 + st + 1, tixn)
+      }
+      compute(stage(cur), tix);
+      // retire the next stage's LDS-DMA; the step-table loads issued after it (rows for st+2, idx for st+1) may stay
+      if (st + 2 < nsteps) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(XPW + 4) : "memory");
+      else if (st + 1 < nsteps) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
-    }
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      lpos[k] += 64;
-      lpos[k] -= lpos[k] >= So ? So : 0;  // So >= 64 for every eligible shape (host check)
-    }
-    // retire the next stage's LDS-DMA; the step-table loads issued after it (rows for st+2, idx for st+1) may stay
-    if (st + 2 < nsteps) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(XPW + 4) : "memory");
-    else if (st + 1 < nsteps) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
 #undef WT_ISSUE
+#undef WT_ISSUE_R
 #undef WT_FETCH_IDX
 #undef WT_FETCH_ROWS
   const int fr = lane & 15, fq = lane >> 4;
@@ -2811,8 +2846,16 @@ void conv3d_wgrad_tri(uintptr_t x, uintptr_t dy, uintptr_t part, uintptr_t grad,
     const char* e = getenv("NIDT_WGT_SCHED");
     return e ? atoi(e) : 1;
   }();
+  // [ADMA] asm-issued stage DMA (NIDT_WGT_ADMA=0: the intrinsic, A/B)
+  static const int tadma = [] {
+    const char* e = getenv("NIDT_WGT_ADMA");
+    return e ? atoi(e) : 1;
+  }();
 #define NIDT_TRI(NC, UU)                                                                                       \
-  if (tsched && !lsw) {                                                                                        \
+  if (tsched && !lsw && tadma) {                                                                               \
+    if (pad) hipLaunchKernelGGL((k_conv_wgrad_tri<NC, UU, true, false, true, true>), grid, dim3(192 * NC), 0, s, d); \
+    else hipLaunchKernelGGL((k_conv_wgrad_tri<NC, UU, false, false, true, true>), grid, dim3(192 * NC), 0, s, d); \
+  } else if (tsched && !lsw) {                                                                                        \
     if (pad) hipLaunchKernelGGL((k_conv_wgrad_tri<NC, UU, true, false, true>), grid, dim3(192 * NC), 0, s, d); \
     else hipLaunchKernelGGL((k_conv_wgrad_tri<NC, UU, false, false, true>), grid, dim3(192 * NC), 0, s, d);    \
   } else if (lsw) {                                                                                            \

@@ -36,4 +36,14 @@ __device__ __forceinline__ void blds16(i32x4_t rsrc, int voffset, uint16_t* lds_
   nidt_raw_buffer_load_lds(rsrc, (__attribute__((address_space(3))) uint32_t*)(lds_wave_base), 16, voffset, 0, 0, 0);
 }
 
+// The same 16-B LDS-DMA issued from inline asm: invisible to the compiler's waitcnt pass, which otherwise treats the
+// DMA as a write to LDS that every later ds_read may alias and puts a vmcnt wait for it in front of them (the stage
+// in flight is then waited for before the current one is computed).  Kernels using it order their DMA with their
+// own counted s_waitcnt vmcnt and barriers, and use M0 for nothing else.
+__device__ __forceinline__ void blds16_asm(i32x4_t rsrc, int voffset, uint16_t* lds_wave_base) {
+  const uint32_t m0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint16_t*)lds_wave_base;
+  asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds" ::"s"(m0), "v"(voffset), "s"(rsrc)
+               : "memory");
+}
+
 }  // namespace nidt

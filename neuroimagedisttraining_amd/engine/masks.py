@@ -74,7 +74,11 @@ def masked_rows(dst, bits, src=None, P=None):
     C = dst.shape[0]
     if P is None:
         P = src.numel() if src is not None else min(dst.shape[1], bits.shape[1] * 32)
-    if _hip(dst) and dst.dtype == torch.float32 and dst.stride(1) == 1 and dst.stride(0) % 4 == 0 and C:
+    # the kernel reads 16-B row pieces and one bit row per dst row (or one shared row): anything else takes torch
+    ok = (_hip(dst) and dst.dtype == torch.float32 and dst.stride(1) == 1 and dst.stride(0) % 4 == 0 and C
+          and dst.data_ptr() % 16 == 0 and (src is None or (src.is_contiguous() and src.data_ptr() % 16 == 0))
+          and bits.shape[0] in (1, C) and bits.shape[1] * 32 >= P)
+    if ok:
         b = bits.contiguous()
         s = src.contiguous() if src is not None else None
         ops.ext().masked_rows(s.data_ptr() if s is not None else 0, b.data_ptr(), 0 if b.shape[0] == 1 else b.stride(0),

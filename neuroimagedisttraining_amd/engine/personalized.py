@@ -602,7 +602,15 @@ class SubAvgRunner(PersonalizedRunner):
             nz_dev = self.state_nonzeros(self.theta, self.bufs, rows)  # print_pruning over the whole state
             self.add_comm(nz_dev)
 
+            # [late prune] NIDT_SUBAVG_LATE_PRUNE=1 (default) keeps an fp32 copy of every trained row's parameters from
+            # the end of epoch 0 until after training (rows x P x 4 B: ~450 MB for ResNet-18 at frac 0.1); it is
+            # skipped (the epoch-0 prune runs in training, with its host read) when that copy would exceed a quarter
+            # of the free device memory or NIDT_SUBAVG_LATE_PRUNE_GB (default 8)
             late = os.environ.get("NIDT_SUBAVG_LATE_PRUNE", "1") != "0"
+            if late and self.device.type == "cuda":
+                need = len(rows) * self.theta.stride(0) * 4
+                cap = float(os.environ.get("NIDT_SUBAVG_LATE_PRUNE_GB", "8")) * 2 ** 30
+                late = need <= min(cap, torch.cuda.mem_get_info(self.device)[0] / 4)
 
             def hook(ep, view, clients):  # fake_prune after the first and the last epoch (the training masks)
                 if ep == 0 and cfg.epochs > 1 and not late:

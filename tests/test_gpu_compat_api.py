@@ -44,7 +44,7 @@ def test_salientgrads_api_runs_on_hip_kernels():
     assert api.engine_used == "hip"
     ks = _nidt_kernels(prof)
     assert any("conv1" in k for k in ks), ks[:20]
-    assert len(api.stat_info["global_test_acc"]) == 2 and len(api.stat_info["person_test_acc"]) == 2
+    assert len(api.stat_info["global_test_acc"]) >= 2 and len(api.stat_info["person_test_acc"]) >= 2
     assert 0.0 <= api.stat_info["global_test_acc"][-1] <= 1.0
     # the final global model is loaded back into the caller's trainer
     assert not torch.equal(model.features[0].weight.detach(), w0)

@@ -1,0 +1,17 @@
+#!/bin/bash
+# compat API classes on the HIP engine, the full GPU suite, a bench; kbench with the slab union reloads skipped
+set -o pipefail
+export PYTHONUNBUFFERED=1
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+OUT=gpurun_out/r6e; mkdir -p $OUT
+timeout -k 10 400 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_compat_api.py > $OUT/compat.txt 2>&1 || { tail -40 $OUT/compat.txt; exit 1; }
+grep -E "PASS|FAIL|passed|failed" $OUT/compat.txt | tail -5
+export KBENCH_EVAL=0
+NIDT_SLAB_DBG=1 timeout -k 10 200 python -u tools/kbench.py 64 > $OUT/kb64_dbg.txt 2>&1 || { tail -20 $OUT/kb64_dbg.txt; exit 1; }
+timeout -k 10 200 python -u tools/kbench.py 64 > $OUT/kb64.txt 2>&1 || { tail -20 $OUT/kb64.txt; exit 1; }
+echo "== union reloads skipped (wrong results, timing only)"; grep -E "full train step|conv2" $OUT/kb64_dbg.txt
+echo "== default"; grep -E "full train step|conv2" $OUT/kb64.txt
+timeout -k 10 1000 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests > $OUT/gpu_all.txt 2>&1 || { tail -40 $OUT/gpu_all.txt; exit 1; }
+tail -3 $OUT/gpu_all.txt
+timeout -k 10 300 python -u bench.py > $OUT/bench.txt 2>&1 || { tail -20 $OUT/bench.txt; exit 1; }
+tail -1 $OUT/bench.txt | cut -c1-400
