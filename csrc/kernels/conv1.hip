@@ -171,7 +171,7 @@ __device__ constexpr int kC1W[4] = {2, 5, 11, 14};
 __device__ constexpr int kC1X1[4] = {24, 20, 8, 26};   // DH0, DW0, HW0, DHW
 __device__ constexpr int kC1X2[4] = {25, 23, 17, 26};  // DH1, DW1, HW1, (empty)
 __device__ constexpr int kC1XR[4][2] = {{0, 1}, {0, 2}, {0, 4}, {0, -1}};
-// RO = 2 (the w64 default): every B operand is one conflict-free ds_read_b128.  A ds_read_b128 is served in 16-lane
+// RO = 2 (opt-in, NIDT_C1_TAPORD=2): every B operand is one conflict-free ds_read_b128.  A ds_read_b128 is served in 16-lane
 // groups {fq0 fr0-3,12-15 + fq1 fr4-11} (and the fq2/fq3 mirror): when the two lane quarters of a group read tap
 // groups of the same jw, their 16 lanes touch 16 distinct 16-B slots of the 256-B bank row.  k-steps 0-2 take the
 // RO = 1 order (paired jw); k-step 3 holds W[fq] (phases 0,2,4,6) + X1[fq] (phases 0,2: DW0, DW1, DHW, empty) +
@@ -241,15 +241,18 @@ __global__ void k_pack_conv1_w(const float* __restrict__ theta, int64_t ldt, int
 // tap-group order of the 128-slot forward layout (pack and forward must agree): the original order by default;
 // NIDT_C1_TAPORD=1 selects the bank-paired order (slower at 64 clients: conv1 forward 4.38 vs 4.25 ms,
 // profiles/r4_kbench_g64.txt)
-// (the w64 forward defaults to RO = 2, the all-b128 layout; the pipe kernel knows RO = 0 / 1 only)
+// NIDT_C1_TAPORD=2 (A/B, the w64 forward only): the all-b128 layout [RO = 2]: LDS bank conflicts 45.7 % -> 0.0 %
+// with the forward's time unchanged (3.28 ms per 64-client step either way, profiles/r6_conv1_b128.txt) — the
+// conflicts are not what the kernel waits on.  Its fp32 sums differ from RO = 0 by rounding (another k order), which
+// flips near-tie max-pool / ReLU decisions downstream; RO = 0 stays the default.  The pipe kernel knows RO 0 / 1.
 int conv1_kslots();
 int conv1_fwd_variant();
 int conv1_tapord() {
   static const int env = [] {
     const char* e = getenv("NIDT_C1_TAPORD");
-    return e ? atoi(e) : -1;
+    return e ? atoi(e) : 0;
   }();
-  if (conv1_fwd_variant() == 1 && conv1_kslots() == 128) return env >= 0 && env <= 2 ? env : 2;
+  if (conv1_fwd_variant() == 1 && conv1_kslots() == 128) return env >= 0 && env <= 2 ? env : 0;
   return env == 1 ? 1 : 0;
 }
 

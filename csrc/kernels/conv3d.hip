@@ -2143,7 +2143,8 @@ __device__ __forceinline__ int swz_wd(int r) { return (r & 2) | ((r >> 1) & 4); 
 // the X tile of a k-step feeds twice the MFMAs, 48 KB of LDS-DMA per 256 MFMAs instead of 40 KB per 128).
 // Wave (wc, wk) = (wid / 4, wid % 4) computes co half wc x X group wk; it stages 8/NCH of group wk's 8 X
 // instructions and dY half wc's slices 2wk, 2wk+1.
-template <int NCH, bool SCHED = false>
+// [ADMA] as k_conv_wgrad_tri: the stage DMA from inline asm, the position-table loads issued before it
+template <int NCH, bool SCHED = false, bool ADMA = false>
 __global__ __launch_bounds__(256 * NCH, 2 / NCH) void k_conv_wgrad_dma(ConvWgDmaArgs a) {
   constexpr int BUFE = (4 + NCH) * kWdGroup;  // elements per stage: 4 X groups + NCH dY halves
   constexpr int XI = 8 / NCH;                  // X instructions per wave per stage
@@ -2183,17 +2184,22 @@ __global__ __launch_bounds__(256 * NCH, 2 / NCH) void k_conv_wgrad_dma(ConvWgDma
     _Pragma("unroll") for (int i_ = 0; i_ < XI; ++i_)                                                         \
       tn[i_] = nidt_raw_buffer_load_v2i32(rt, ((P0) + 8 * (xi0 + i_) + lr) * 8, 0, 0);                        \
   }
-#define WD_ISSUE(P0, BUFI)                                                                                    \
+  auto wd_dma = [](i32x4_t r, int off, uint16_t* dst) {
+    if constexpr (ADMA) blds16_asm(r, off, dst);
+    else blds16(r, off, dst);
+  };
+#define WD_ISSUE_T(P0, BUFI, TN)                                                                              \
   {                                                                                                           \
     uint16_t* sX_ = smem + (BUFI) * BUFE + wk * kWdGroup;                                                     \
     uint16_t* sD_ = smem + (BUFI) * BUFE + (4 + wc) * kWdGroup;                                               \
     _Pragma("unroll") for (int i_ = 0; i_ < XI; ++i_) {                                                       \
-      const bool ok_ = (tn[i_].y >> gtap) & 1;                                                                \
-      blds16(rx, ok_ ? tn[i_].x * (2 * Cin) + xcol[i_] : kBufOOB, sX_ + (xi0 + i_) * 512);                    \
+      const bool ok_ = (TN[i_].y >> gtap) & 1;                                                                \
+      wd_dma(rx, ok_ ? TN[i_].x * (2 * Cin) + xcol[i_] : kBufOOB, sX_ + (xi0 + i_) * 512);                    \
     }                                                                                                         \
     _Pragma("unroll") for (int i_ = 0; i_ < 2; ++i_)                                                          \
-      blds16(rd, (P0) * (2 * a.Cout) + dcol[i_], sD_ + (2 * wk + i_) * 512);                                  \
+      wd_dma(rd, (P0) * (2 * a.Cout) + dcol[i_], sD_ + (2 * wk + i_) * 512);                                  \
   }
+#define WD_ISSUE(P0, BUFI) WD_ISSUE_T(P0, BUFI, tn)
 
   f32x4 acc[4][4];
 #pragma unroll
@@ -2215,7 +2221,15 @@ __global__ __launch_bounds__(256 * NCH, 2 / NCH) void k_conv_wgrad_dma(ConvWgDma
   }
   for (int st = 0; st < nsteps; ++st) {
     const int cur = st & 1;
-    if (st + 1 < nsteps) {
+    if constexpr (ADMA) {
+      i32x2_t tdma[XI];  // the table entries of step st + 1, fetched a step ago
+#pragma unroll
+      for (int i = 0; i < XI; ++i) tdma[i] = tn[i];
+      if (st + 1 < nsteps) {
+        if (st + 2 < nsteps) WD_FETCH(p_begin + kWdPos * (st + 2))
+        WD_ISSUE_T(p_begin + kWdPos * (st + 1), cur ^ 1, tdma)
+      }
+    } else if (st + 1 < nsteps) {
       WD_ISSUE(p_begin + kWdPos * (st + 1), cur ^ 1)
       if (st + 2 < nsteps) WD_FETCH(p_begin + kWdPos * (st + 2))
     }
@@ -2248,13 +2262,18 @@ __global__ __launch_bounds__(256 * NCH, 2 / NCH) void k_conv_wgrad_dma(ConvWgDma
         for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
     }
     }
-    // retire this step's LDS-DMA (next stage) but leave the XI position-table loads for step st+2 in flight: they
-    // are the youngest vector-memory ops and are only consumed by the next step's DMA issue
-    if (st + 2 < nsteps) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(XI) : "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if constexpr (ADMA) {
+      __builtin_amdgcn_s_waitcnt(7 << 4);  // vmcnt(0) lgkmcnt(0), visible to the waitcnt pass (k_conv_wgrad_tri)
+    } else {
+      // retire this step's LDS-DMA (next stage) but leave the XI position-table loads for step st+2 in flight: they
+      // are the youngest vector-memory ops and are only consumed by the next step's DMA issue
+      if (st + 2 < nsteps) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(XI) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     __syncthreads();
   }
 #undef WD_ISSUE
+#undef WD_ISSUE_T
 #undef WD_FETCH
   const int fr = lane & 15, fq = lane >> 4;
   if (a.grad) {  // single split: final layout straight from the accumulators (this wave's group is one tap)
@@ -3030,7 +3049,15 @@ static void conv_wgrad_impl(uintptr_t x, uintptr_t xs, uintptr_t xt, uintptr_t d
       const char* e = getenv("NIDT_WGD_SCHED");
       return e ? atoi(e) : 1;
     }();
-    if (wsched) {
+    // [ADMA] asm-issued stage DMA (k_conv_wgrad_tri); NIDT_WGD_ADMA=0: the intrinsic (A/B)
+    static const int wadma = [] {
+      const char* e = getenv("NIDT_WGD_ADMA");
+      return e ? atoi(e) : 1;
+    }();
+    if (wsched && wadma) {
+      if (nch == 2) hipLaunchKernelGGL((k_conv_wgrad_dma<2, true, true>), dim3((unsigned)nwg), dim3(512), 0, s, d);
+      else hipLaunchKernelGGL((k_conv_wgrad_dma<1, true, true>), dim3((unsigned)nwg), dim3(256), 0, s, d);
+    } else if (wsched) {
       if (nch == 2) hipLaunchKernelGGL((k_conv_wgrad_dma<2, true>), dim3((unsigned)nwg), dim3(512), 0, s, d);
       else hipLaunchKernelGGL((k_conv_wgrad_dma<1, true>), dim3((unsigned)nwg), dim3(256), 0, s, d);
     } else if (nch == 2) {
