@@ -323,8 +323,10 @@ def run(args):
         print(json.dumps(out), flush=True)
     if args.dump_rows:
         rows, loc = runner._local_rows(range(args.clients))
-        torch.save({int(c): runner.theta[r, :runner.P].detach().cpu() for r, c in zip(rows, loc)},
-                   "%s.rank%d.pt" % (args.dump_rows, info.rank))
+        dump = {int(c): runner.theta[r, :runner.P].detach().cpu() for r, c in zip(rows, loc)}
+        if getattr(runner, "mask", None) is not None:
+            dump[-1] = runner.mask.detach().float().cpu()  # the global SNIP mask the rows trained under
+        torch.save(dump, "%s.rank%d.pt" % (args.dump_rows, info.rank))
     rt.shutdown(info)
 
 

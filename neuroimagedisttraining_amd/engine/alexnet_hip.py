@@ -235,15 +235,19 @@ class HipAlexNet3D:
             self.m.conv3d_fwd(_p(x), _p(w), _p(bias), 0, 0, _p(y), _p(stats), G, B, D, H, W, cin, cout, pad, st)
 
     # ---------------------------------------------------------------------------------------------
-    def _pack(self, theta, G, b, train):
+    def _pack(self, theta, G, b, train, prepacked=False):
+        """Weight images of this step.  ``prepacked``: the previous optimizer step already wrote the conv2-5 forward
+        images from these rows (``fused_plan``), so only conv1's pack and the data-gradient transposes run."""
         m, st = self.m, ops.stream()
         P = theta.stride(0)
         m.pack_conv1_w(_p(theta), P, self.o["features.0.weight"], self.o["features.1.weight"], G, 1.0 / 255.0,
                        _p(b["w1p"]), _p(b["w125"]), st)
         if "bpack" in b:
             tab, nplain, ntrans, lds, buf = b["bpack"]
-            m.pack_convs(_p(tab), 4, nplain, 0, ntrans, lds, _p(theta), P, G, _p(buf), st)
+            if nplain and not prepacked or ntrans:
+                m.pack_convs(_p(tab), 4, 0 if prepacked else nplain, 0, ntrans, lds, _p(theta), P, G, _p(buf), st)
             return
+        assert not prepacked, "prepacked weight images need the batched pack plan (NIDT_AX_BPACK=1)"
         for (ci, bi, cin, cout, pad, sp) in (L2, L3, L4, L5):
             m.pack_conv_w(_p(theta), P, self.o["features.%d.weight" % ci], G, cout, cin, 1.0, _p(b["w%dp" % ci]),
                           _p(b["w%dt" % ci]) if train else 0, st)
@@ -265,7 +269,32 @@ class HipAlexNet3D:
             m.bn_eval(G, C, _p(theta), P, og, ob, _p(bufs), Q, orm, orv, BN_EPS, _p(b["s%d" % ci]),
                       _p(b["t%d" % ci]), _p(b["m%d" % ci]), _p(b["i%d" % ci]), st)
 
-    def forward(self, theta, bufs, x8, mom, idx, G, B, train, bn_train=None):
+    def fused_plan(self, G, B, P):
+        """Plan of the optimizer step that writes the conv2-5 forward images of the next (G, B) train step itself
+        (``optim.hip`` ``local_opt_pack``, as the 2-D engine's ``WeightPacker.fused_plan``): the batched pack's
+        descriptor table (plain-grid block prefixes over the four layers), its plain block count, the {start, length}
+        table of the other parameter ranges of a P-wide row (4096 per block), LDS bytes, the image buffer."""
+        key = ("fused", G, B, int(P))
+        plan = self._cache.get(key)
+        if plan is not None:
+            return plan
+        b = self._bufs(G, B, True)
+        tab, nplain, ntrans, lds, buf = b["bpack"]
+        spans = sorted((self.o["features.%d.weight" % L[0]], self.o["features.%d.weight" % L[0]] + L[3] * 27 * L[2])
+                       for L in (L2, L3, L4, L5))
+        rest, pos = [], 0
+        for a_, b_ in spans + [(int(P), int(P))]:
+            while pos < a_:
+                n = min(4096, a_ - pos)
+                rest.append((pos, n))
+                pos += n
+            pos = max(pos, b_)
+        rt_ = torch.tensor(rest if rest else [(0, 0)], dtype=torch.int64).to(self.dev)
+        plan = (tab, 4, nplain, rt_, len(rest), lds, buf)
+        self._cache[key] = plan
+        return plan
+
+    def forward(self, theta, bufs, x8, mom, idx, G, B, train, bn_train=None, prepacked=False):
         """Runs the forward; returns the scratch dict (logits in ``b['logits']``).  ``train`` keeps what the backward
         needs; ``bn_train`` (default = ``train``) selects batch statistics (+ running-stat update) vs running stats."""
         bn_train = train if bn_train is None else bn_train
@@ -277,7 +306,7 @@ class HipAlexNet3D:
         b = self._bufs(G, B, train)
         NB = G * B
         P, Q = theta.stride(0), bufs.stride(0)
-        self._pack(theta, G, b, train)
+        self._pack(theta, G, b, train, prepacked)
         # ---- conv1 + BN1 + ReLU + pool1 ----
         if bn_train:
             assert mom is not None and mom.dtype == torch.float64 and mom.shape[1] == NM
@@ -319,7 +348,7 @@ class HipAlexNet3D:
 
     # ---------------------------------------------------------------------------------------------
     def train_step(self, theta, bufs, grads, x8, mom, idx, labels, G, B, keep=0.5, seed=0, cids=None, seed_dev=None,
-                   bn_train=True):
+                   bn_train=True, prepacked=False):
         """Forward + backward for G clients; writes ``grads`` [G,P], updates BN running stats in ``bufs``.
         Returns the per-client mean loss tensor [G] (device).  ``seed_dev`` (int64 device scalar, optional) is
         added to ``seed`` inside the kernel, so a captured hipGraph can advance the dropout stream on device.
@@ -331,7 +360,7 @@ class HipAlexNet3D:
         if not bn_train:
             keep = 1.0
         ev = 0 if bn_train else 1
-        b = self.forward(theta, bufs, x8, mom, idx, G, B, True, bn_train=bn_train)
+        b = self.forward(theta, bufs, x8, mom, idx, G, B, True, bn_train=bn_train, prepacked=prepacked)
         NB = G * B
         P = theta.stride(0)
         o = self.o

@@ -23,6 +23,7 @@ Round semantics reproduced from the reference (SURVEY.md §2.2 "Shared algorithm
 from __future__ import annotations
 
 import math
+import os
 import time
 from dataclasses import dataclass, field
 from typing import Optional
@@ -124,8 +125,14 @@ class HipEngine:
 
     accepts_cids_dev = True  # train_step(cids_dev=...): client ids from a device buffer (graph reuse across groups)
 
+    # [PACK-FUSE] the optimizer step may write the next train step's conv2-5 forward images (runner: pack_next /
+    # prepacked, also inside captured steps: the two variants are separate graphs).  NIDT_AX_PACK_FUSE=0: off (A/B)
+    fused_pack = os.environ.get("NIDT_AX_PACK_FUSE", "1") != "0"
+    fused_pack_graphs = fused_pack
+
     def train_step(self, theta, bufs, grads, idx, G, B, keep, seed, cids=None, seed_dev=None, bn_train=True,
-                   cids_dev=None):
+                   cids_dev=None, prepacked=False):
+        self._last_gb = (G, B)
         y = self.labels.index_select(0, idx.long())
         ct = cids_dev
         if ct is None and cids is not None:
@@ -135,15 +142,23 @@ class HipEngine:
                 ct = torch.tensor(key, dtype=torch.int32, device=self.device)
                 self._cid_cache[key] = ct
         return self.net.train_step(theta, bufs, grads, self.x8, self.mom, idx, y, G, B, keep, seed, ct, seed_dev,
-                                   bn_train=bn_train)
+                                   bn_train=bn_train, prepacked=prepacked)
 
     def eval_logits(self, theta, bufs, idx, G, B):
         return self.net.eval_logits(theta, bufs, self.x8, idx, G, B)
 
-    def local_opt(self, theta, grads, mom_buf, spec, lr, wd, momentum, max_norm, lr_dev=None, keep_grad=False):
+    def local_opt(self, theta, grads, mom_buf, spec, lr, wd, momentum, max_norm, lr_dev=None, keep_grad=False,
+                  pack_next=False):
         """Fused per-client step (``optim.hip`` ``local_opt``): masks (shared or per-row bits, weight or gradient
         mode), FedProx proximal gradient, clip(10), SGD(wd, momentum), Ditto pull — one norm pass + one update
-        pass over the rows.  The clipped gradient is written back only with ``keep_grad``."""
+        pass over the rows.  The clipped gradient is written back only with ``keep_grad``.  ``pack_next``: the same
+        rows train again next at this step's shape, so the update also writes their conv2-5 forward images (the next
+        train step then runs with ``prepacked``)."""
+        gb = getattr(self, "_last_gb", None)
+        if pack_next and self.fused_pack and gb is not None and gb[0] == theta.shape[0]:
+            self.local_opt_pack(theta, grads, mom_buf, spec, lr, wd, momentum, max_norm,
+                                self.net.fused_plan(gb[0], gb[1], theta.shape[1]), lr_dev=lr_dev, keep_grad=keep_grad)
+            return
         self.m.local_opt(*self._opt_args(theta, grads, mom_buf, spec, lr, wd, momentum, max_norm, lr_dev,
                                          keep_grad), ops.stream())
 

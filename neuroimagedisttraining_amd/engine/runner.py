@@ -383,8 +383,17 @@ class FLRunner:
             plan, idx = self._plan(clients, self._epoch_chunks(round_idx, tag, ep))
             main, cur, lanes_used = torch.cuda.current_stream() if side else None, -1, set()
             partial_steps = {it[2] for it in plan if it[6] < cfg.batch_size} if side else ()
-            pnext = self._pack_next(plan) if not use_graphs else None
+            # [PACK-FUSE] engines whose optimizer can write the next step's weight images: eager steps always, captured
+            # steps when the engine keeps the two variants (prepacked or not) as separate graphs
+            pnext = (self._pack_next(plan) if not use_graphs or getattr(self.e, "fused_pack_graphs", False)
+                     else None)
+            fresh = set()  # row groups whose previous step (this epoch) wrote their images
             for pi, (r0, r1, s, off, n, G, B) in enumerate(plan):
+                pn = bool(pnext and pnext[pi])
+                pre = r0 in fresh
+                fresh.discard(r0)
+                if pn:
+                    fresh.add(r0)
                 if s != cur:  # fork point of this step: main has enqueued every earlier step
                     cur = s
                     fork = main.record_event() if s in partial_steps else None
@@ -403,11 +412,11 @@ class FLRunner:
                                          seed_dev=sdev, cids_dev=None if cdev is None else cdev[r0:r1])
                 elif use_graphs:
                     self._graph_step(sub, r0, idx[off:off + n], G, B, spec.rows(r0, r1), cids, seed,
-                                     cids_dev=None if cdev is None else cdev[r0:r1])
+                                     cids_dev=None if cdev is None else cdev[r0:r1], prepacked=pre, pack_next=pn)
                 else:
                     self._seed_dev.fill_(seed)
-                    self._step(sub, r0, idx[off:off + n], G, B, spec.rows(r0, r1), cids, lr,
-                               pack_next=bool(pnext and pnext[pi]))
+                    self._step(sub, r0, idx[off:off + n], G, B, spec.rows(r0, r1), cids, lr, pack_next=pn,
+                               prepacked=pre)
             for st in lanes_used:
                 main.wait_stream(st)
             self.concurrent_steps = getattr(self, "concurrent_steps", 0) + len(lanes_used)
@@ -574,11 +583,14 @@ class FLRunner:
             last[it[0]] = i
         return out
 
-    def _step(self, sub, r0, idx, G, B, spec, cids, lr, seed_dev=None, lr_dev=None, cids_dev=None, pack_next=False):
+    def _step(self, sub, r0, idx, G, B, spec, cids, lr, seed_dev=None, lr_dev=None, cids_dev=None, pack_next=False,
+              prepacked=False):
         cfg = self.cfg
         gr = self.grads[r0:r0 + G]
         mo = self.mom_buf[r0:r0 + G] if self.mom_buf is not None else None
         kw = {} if cids_dev is None else {"cids_dev": cids_dev}
+        if prepacked and getattr(self.e, "fused_pack_graphs", False):  # (the 2-D engine tracks its images itself)
+            kw["prepacked"] = True
         loss = self.e.train_step(sub.theta, sub.bufs, gr, idx, G, B, cfg.dropout_keep, cfg.seed << 40, cids=cids,
                                  seed_dev=self._seed_dev if seed_dev is None else seed_dev, **kw)
         if self.track_loss and self._loss_acc is not None and loss is not None:
@@ -587,7 +599,8 @@ class FLRunner:
         self.e.local_opt(sub.theta, gr, mo, spec, lr, cfg.wd, cfg.momentum, cfg.max_norm,
                          lr_dev=self._lr_dev if lr_dev is None else lr_dev, **kw)
 
-    def _graph_step(self, sub, r0, idx, G, B, spec, cids, seed, fill=True, seed_dev=None, cids_dev=None):
+    def _graph_step(self, sub, r0, idx, G, B, spec, cids, seed, fill=True, seed_dev=None, cids_dev=None,
+                    prepacked=False, pack_next=False):
         """One lockstep local step (forward+backward of G clients + fused optimizer) as a replayed hipGraph.  The
         ~45 kernel launches of a step become one graph launch; everything that changes between steps lives in
         device memory the graph reads: the sample indices (copied into a static buffer), the dropout stream
@@ -597,7 +610,8 @@ class FLRunner:
         ids from device memory) the ids are one more refilled buffer and the key drops them."""
         sdev = self._seed_dev if seed_dev is None else seed_dev
         ckey = tuple(int(c) for c in cids) if cids_dev is None else None
-        key = (sub.theta.data_ptr(), r0, G, B, ckey, spec.key(), sdev.data_ptr())
+        key = (sub.theta.data_ptr(), r0, G, B, ckey, spec.key(), sdev.data_ptr(), prepacked, pack_next)
+        pk = {"prepacked": prepacked, "pack_next": pack_next}
         ent = self._graphs.get(key, "new")
         if fill:
             sdev.fill_(seed)
@@ -610,7 +624,7 @@ class FLRunner:
                 torch.cuda.synchronize(self.device)  # an evicted graph may still run on a side stream
             while len(self._graphs) >= self.max_graphs:
                 self._graphs.pop(next(iter(self._graphs)))
-            self._step(sub, r0, idx, G, B, spec, cids, 0.0, seed_dev=sdev, cids_dev=cids_dev)
+            self._step(sub, r0, idx, G, B, spec, cids, 0.0, seed_dev=sdev, cids_dev=cids_dev, **pk)
             self._graphs[key] = None
             return
         if ent is None:
@@ -625,15 +639,15 @@ class FLRunner:
             try:
                 # thread_local: the RCCL watchdog thread of a multi-GPU run may query events during the capture
                 with torch.cuda.graph(g, capture_error_mode="thread_local"):
-                    self._step(sub, r0, idx_buf, G, B, spec, cids, 0.0, seed_dev=sdev, cids_dev=cid_buf)
+                    self._step(sub, r0, idx_buf, G, B, spec, cids, 0.0, seed_dev=sdev, cids_dev=cid_buf, **pk)
             except Exception:  # noqa: BLE001 - capture unsupported here: stay eager for this shape
                 self._graphs[key] = False
-                self._step(sub, r0, idx, G, B, spec, cids, 0.0, seed_dev=sdev, cids_dev=cids_dev)
+                self._step(sub, r0, idx, G, B, spec, cids, 0.0, seed_dev=sdev, cids_dev=cids_dev, **pk)
                 return
             ent = self._graphs[key] = (g, idx_buf, cid_buf)
             st["captured"] = st.get("captured", 0) + 1
         elif ent is False:
-            self._step(sub, r0, idx, G, B, spec, cids, 0.0, seed_dev=sdev, cids_dev=cids_dev)
+            self._step(sub, r0, idx, G, B, spec, cids, 0.0, seed_dev=sdev, cids_dev=cids_dev, **pk)
             return
         g, idx_buf, cid_buf = ent
         st["replayed"] = st.get("replayed", 0) + 1

@@ -609,10 +609,10 @@ def test_conv1_fused_fwd_and_sparse_wgrad(signed):
 @pytest.mark.parametrize("NB,B", [(4, 2), (128, 16)])
 def test_conv1_fwd_wave_tile_matches_pipe(NB, B):
     """The wave-tile fused forward (k_conv1_fwd_w64: a wave owns all 64 channels of 15 columns, DPP pooling, packed
-    epilogue, and its own all-b128 k-slot layout RO = 2) against the channel-split pipe kernel (RO = 0 layout): each
-    mode packs the same fp32 weights with pack_conv1_w into its own slot order, so the MFMA k order differs and the
-    fp32 sums agree to rounding: the pooled bf16 outputs within 1 bf16 ulp of the output scale, the argmax bytes
-    equal except at near-ties (random volumes, signed scales, per-client weights)."""
+    epilogue) against the channel-split pipe kernel: each mode packs the same fp32 weights with pack_conv1_w into the
+    slot order it reads (both the RO = 0 layout by default; NIDT_C1_TAPORD=2 gives w64 the all-b128 layout, another
+    MFMA k order), so the pooled bf16 outputs agree within 1 bf16 ulp of the output scale and the argmax bytes except
+    at near-ties (random volumes, signed scales, per-client weights)."""
     m = _m()
     g = torch.Generator(device=DEV).manual_seed(5)
     G = NB // B

@@ -273,6 +273,28 @@ def test_runner_hip_graphs_bit_identical_to_eager(algo):
         assert a.stat_info[k] == b.stat_info[k], k
 
 
+@pytest.mark.parametrize("algo", ["salientgrads", "dispfl", "subavg"])
+@pytest.mark.parametrize("graphs", [True, False])
+def test_alexnet_pack_fuse_bit_identical(algo, graphs, monkeypatch):
+    """[PACK-FUSE] the optimizer step writing the next step's conv2-5 forward images (and that step skipping their
+    pack; captured as a separate graph) == packing every step, bit for bit (ragged groups, per-row masks)."""
+    from neuroimagedisttraining_amd.engine.executor import HipEngine
+    fed = _fed(SIZES, n_test=[6, 4, 7, 5, 6, 3, 8, 5])
+    outs = []
+    for fuse in (True, False):
+        monkeypatch.setattr(HipEngine, "fused_pack", fuse)
+        monkeypatch.setattr(HipEngine, "fused_pack_graphs", fuse)
+        r, _ = _run(algo, "hip", fed, hip_graphs=graphs, dropout_keep=0.5, **_extra(algo))
+        outs.append(r)
+    a, b = outs
+    if graphs:
+        assert any(isinstance(k, tuple) and k[-1] for k in a._graphs), "no pack-writing step was captured"
+    assert torch.equal(a.theta, b.theta) and torch.equal(a.bufs, b.bufs)
+    assert torch.equal(a.w_global, b.w_global)
+    for k in ("global_test_acc", "person_test_acc"):
+        assert a.stat_info[k] == b.stat_info[k], k
+
+
 @pytest.mark.parametrize("algo", ALGOS)
 def test_runner_hip_tracks_torch_engine(algo):
     """HIP engine (bf16 MFMA operands) vs the same runner on the fp32 PyTorch engine: 8 clients of unequal sizes

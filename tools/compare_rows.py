@@ -17,6 +17,9 @@ def load(prefix):
 def main():
     a, b = load(sys.argv[1]), load(sys.argv[2])
     assert a and set(a) == set(b), (len(a), len(b))
+    if -1 in a:  # the global masks (key -1): a different mask explains every row difference
+        ma, mb = a.pop(-1), b.pop(-1)
+        print("global mask: %d of %d entries differ" % (int((ma != mb).sum()), ma.numel()))
     same = [c for c in a if torch.equal(a[c], b[c])]
     diff = {c: float((a[c] - b[c]).abs().max()) for c in a if c not in same}
     print("clients %d  bit-identical %d  differing %d  max|diff| %.3e" %
