@@ -277,9 +277,9 @@ def test_runner_hip_graphs_bit_identical_to_eager(algo):
 @pytest.mark.parametrize("graphs", [True, False])
 def test_alexnet_pack_fuse_bit_identical(algo, graphs, monkeypatch):
     """[PACK-FUSE] the optimizer step writing the next step's conv2-5 forward images (and that step skipping their
-    pack; captured as a separate graph) == packing every step, bit for bit (ragged groups, per-row masks)."""
+    pack; captured as a separate graph) == packing every step, bit for bit (per-row masks, grad masks)."""
     from neuroimagedisttraining_amd.engine.executor import HipEngine
-    fed = _fed(SIZES, n_test=[6, 4, 7, 5, 6, 3, 8, 5])
+    fed = _fed([24] * 6)  # equal sizes: every epoch is 3 full lockstep steps of one row group (2 of them fusable)
     outs = []
     for fuse in (True, False):
         monkeypatch.setattr(HipEngine, "fused_pack", fuse)
