@@ -2828,8 +2828,12 @@ int conv3d_wgrad_tri_ok(int B, int D, int H, int W, int Cin, int Cout, int pad) 
 // 0.37/0.52/0.36 ms; at 8 clients the 4-tap kernel is as fast or faster, 0.074/0.079/0.074 vs 0.076/0.090/0.074)
 int conv3d_wgrad_tri_pick(int G, int B, int D, int H, int W, int Cin, int Cout, int pad) {
   if (!conv3d_wgrad_tri_ok(B, D, H, W, Cin, Cout, pad)) return 0;
+  static const int64_t minpos = [] {  // NIDT_WG_TRI_MINPOS: the padded-conv threshold (A/B)
+    const char* e = getenv("NIDT_WG_TRI_MINPOS");
+    return e ? (int64_t)atoll(e) : (int64_t)65536;
+  }();
   const int64_t pos = (int64_t)G * B * conv_out_n(D, pad) * conv_out_n(H, pad) * conv_out_n(W, pad);
-  return (pad == 0 || pos >= 65536) ? 1 : 0;
+  return (pad == 0 || pos >= minpos) ? 1 : 0;
 }
 
 void conv3d_wgrad_tri(uintptr_t x, uintptr_t dy, uintptr_t part, uintptr_t grad, int64_t ldg, int64_t off, int G, int B,

@@ -31,6 +31,7 @@ The personalized / decentralized algorithms build on this class (``engine/person
 """
 from __future__ import annotations
 
+import gc
 import math
 import os
 import time
@@ -636,6 +637,10 @@ class FLRunner:
                 cid_buf.copy_(cids_dev)
             torch.cuda.current_stream().synchronize()
             g = torch.cuda.CUDAGraph()
+            # no garbage collection inside the capture: a dead reference cycle of an earlier run (its captured
+            # graphs, tensors freed with events on other streams) released mid-capture aborts the HIP runtime
+            gc_on = gc.isenabled()
+            gc.disable()
             try:
                 # thread_local: the RCCL watchdog thread of a multi-GPU run may query events during the capture
                 with torch.cuda.graph(g, capture_error_mode="thread_local"):
@@ -644,6 +649,9 @@ class FLRunner:
                 self._graphs[key] = False
                 self._step(sub, r0, idx, G, B, spec, cids, 0.0, seed_dev=sdev, cids_dev=cids_dev, **pk)
                 return
+            finally:
+                if gc_on:
+                    gc.enable()
             ent = self._graphs[key] = (g, idx_buf, cid_buf)
             st["captured"] = st.get("captured", 0) + 1
         elif ent is False:
