@@ -175,6 +175,10 @@ int conv1_wgrad_mx_npb(int NB);
 void conv1_wgrad_mode(int mode);
 void conv1_fwd_mode(int mode);
 int gemm1x1_ok(int K, int N);
+int wgrad1x1_ok(int N, int K);
+int wgrad1x1_chunks(int G, int64_t Mg, int N, int K);
+void wgrad1x1_g(uintptr_t x, uintptr_t dy, uintptr_t part, uintptr_t grad, int64_t ldg, int64_t off, int G, int64_t Mg,
+                int N, int K, int nMB, float scale, uintptr_t stream);
 void conv2d_any_fwd(uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t y, int G, int B, int H, int W, int cin, int cs,
                     int cout, int k, int pad, uintptr_t stream);
 int conv2d_any_wgrad_chunks(int B, int Ho, int Wo);
@@ -331,6 +335,9 @@ PYBIND11_MODULE(_nidt_hip, m) {
   DEF(conv1_wgrad_mode);
   DEF(conv1_fwd_mode);
   DEF(gemm1x1_ok);
+  DEF(wgrad1x1_ok);
+  DEF(wgrad1x1_chunks);
+  DEF(wgrad1x1_g);
   DEF(conv2d_any_fwd);
   DEF(conv2d_any_wgrad_chunks);
   DEF(conv2d_any_wgrad);

@@ -2032,6 +2032,27 @@ __global__ __launch_bounds__(256) void k_wgrad_reduce(const float* __restrict__ 
   }
 }
 
+void k_wgrad_reduce_launch(const float* part, int nsplit, int G, int Cout, int Cin, int kt, float* grad, int64_t ldg,
+                           int64_t off, float scale, hipStream_t s) {
+  hipLaunchKernelGGL(k_wgrad_reduce, dim3(Cout, G), dim3(256), kt * (Cin + 1) * sizeof(float), s, part, nsplit, G, Cout,
+                     Cin, kt, grad, ldg, off, scale);
+  NIDT_CHECK(hipGetLastError());
+}
+
+// 1x1x1 stride-1 weight gradients on the streaming kernel of wgrad1x1.hip (default); NIDT_WG1X1=0 keeps them on
+// k_conv_wgrad_dma (A/B)
+int wgrad1x1_ok(int N, int K);
+int wgrad1x1_chunks(int G, int64_t Mg, int N, int K);
+void wgrad1x1_g(uintptr_t x, uintptr_t dy, uintptr_t part, uintptr_t grad, int64_t ldg, int64_t off, int G, int64_t Mg,
+                int N, int K, int nMB, float scale, uintptr_t stream);
+static bool wg1x1_on(int Cin, int Cout, int kt, int st) {
+  static const bool on = [] {
+    const char* e = getenv("NIDT_WG1X1");
+    return !(e && e[0] == '0');
+  }();
+  return on && kt == 1 && st == 1 && wgrad1x1_ok(Cout, Cin);
+}
+
 // Split-K factor for the wgrad: blocks are equally long (chunk positions each), so the run time is
 // waves x block time with waves = ceil(blocks / slots), slots = 256 CUs x 2 resident blocks (80 KB LDS each),
 // plus the fp32 slab traffic (ns x G x Cout x K, written once and read once by k_wgrad_reduce).  The model
@@ -2047,6 +2068,7 @@ int conv3d_wgrad_nsplit(int G, int B, int D, int H, int W, int Cin, int Cout, in
 int conv_wgrad_nsplit_g(int G, int B, int D, int H, int W, int Cin, int Cout, int kt, int st, int pad, int padd) {
   const int kd = kt == 27 ? 3 : 1, khw = kt == 1 ? 1 : 3;
   const int Mg = B * conv_out_dim(D, kd, st, padd) * conv_out_dim(H, khw, st, pad) * conv_out_dim(W, khw, st, pad);
+  if (wg1x1_on(Cin, Cout, kt, st) && pad == 0) return wgrad1x1_chunks(G, Mg, Cout, Cin);
   return wgrad_nsplit_mk(G, Mg, kt * Cin, Cout);
 }
 
@@ -2824,13 +2846,15 @@ int conv3d_wgrad_tri_ok(int B, int D, int H, int W, int Cin, int Cout, int pad) 
 }
 
 // k_conv_wgrad_tri is the faster choice for this layer and client count: always for unpadded convs (conv2); padded
-// convs only with >= 64 K output positions per launch (the 5x7x5 conv3-5 at 64 clients: 0.47/0.64/0.45 ->
-// 0.37/0.52/0.36 ms; at 8 clients the 4-tap kernel is as fast or faster, 0.074/0.079/0.074 vs 0.076/0.090/0.074)
+// convs with >= 8 K output positions per launch (the 5x7x5 conv3-5 at 64 clients: 0.47/0.64/0.45 -> 0.37/0.52/0.36
+// ms).  Since its stage DMA overlaps the MFMAs ([ADMA]) it also wins at 8 clients (22 K positions): conv3 / conv5
+// 0.076 -> 0.059 / 0.060 ms, conv4 0.081 -> 0.085 (kbench 8: step 3.07-3.15 -> 3.01 ms, profiles/r6_g8_sweep.txt);
+// the threshold was 64 K before [ADMA]
 int conv3d_wgrad_tri_pick(int G, int B, int D, int H, int W, int Cin, int Cout, int pad) {
   if (!conv3d_wgrad_tri_ok(B, D, H, W, Cin, Cout, pad)) return 0;
   static const int64_t minpos = [] {  // NIDT_WG_TRI_MINPOS: the padded-conv threshold (A/B)
     const char* e = getenv("NIDT_WG_TRI_MINPOS");
-    return e ? (int64_t)atoll(e) : (int64_t)65536;
+    return e ? (int64_t)atoll(e) : (int64_t)8192;
   }();
   const int64_t pos = (int64_t)G * B * conv_out_n(D, pad) * conv_out_n(H, pad) * conv_out_n(W, pad);
   return (pad == 0 || pos >= minpos) ? 1 : 0;
@@ -3001,6 +3025,10 @@ static void conv_wgrad_impl(uintptr_t x, uintptr_t xs, uintptr_t xt, uintptr_t d
   NIDT_REQUIRE((ptab && !xs) ? (int64_t)Cin * kt <= 27 * kMaxCin : Cin <= 192,
                "conv3d_wgrad: taps x Cin <= 27 x 512 (LDS-DMA path with a position table), else Cin <= 192");
   NIDT_REQUIRE(Cout % kWgCO == 0, "conv3d_wgrad: Cout must be a multiple of 64");
+  if (wg1x1_on(Cin, Cout, kt, st) && pad == 0 && padd == 0 && !xs) {  // rows of X and dY are the same positions
+    wgrad1x1_g(x, dy, part, grad, ldg, off, G, (int64_t)B * D * H * W, Cout, Cin, nsplit, scale, stream);
+    return;
+  }
   ConvWgArgs a;
   a.x = ptr<const uint16_t>(x); a.xs = ptr<const float>(xs); a.xt = ptr<const float>(xt);
   a.dy = ptr<const uint16_t>(dy); a.part = ptr<float>(part);

@@ -150,6 +150,36 @@ def _gemm1x1_case(m, dev, G, Mg, K, N):
     assert torch.equal(y2.view(torch.int16), y.view(torch.int16))  # the statistics do not change the output
 
 
+W1_SHAPES = [(64, 64), (256, 64), (64, 256), (128, 128), (128, 256), (256, 128), (512, 128), (128, 512),
+             (1024, 2048)]
+
+
+@pytest.mark.parametrize("N,K", W1_SHAPES)
+def test_wgrad1x1_matches_fp32(N, K):
+    """wgrad1x1.hip (every tile configuration; one chunk = gradient rows written by the kernel, several = partials +
+    k_wgrad_reduce) against a per-client fp32 dY^T X of the same bf16 operands, with a partial last m-tile; the rows
+    around each client's gradient slice stay untouched."""
+    from neuroimagedisttraining_amd import ops
+    dev = _dev()
+    m = ops.ext()
+    assert m.wgrad1x1_ok(N, K)
+    torch.manual_seed(N + K)
+    G, Mg = 3, 64 * 37 + 21
+    x = torch.randn(G, Mg, K, device=dev).to(torch.bfloat16)
+    dy = torch.randn(G, Mg, N, device=dev).to(torch.bfloat16)
+    ref = torch.bmm(dy.float().transpose(1, 2), x.float()) * 0.5
+    off, ld = 7, N * K + 19
+    for nmb in sorted({1, 3, m.wgrad1x1_chunks(G, Mg, N, K)}):
+        rows = torch.full((G, ld), -3.0, device=dev)
+        part = torch.empty(max(nmb, 1) * G * N * K, device=dev)
+        m.wgrad1x1_g(x.data_ptr(), dy.data_ptr(), part.data_ptr(), rows.data_ptr(), ld, off, G, Mg, N, K, nmb, 0.5,
+                     torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        got = rows[:, off:off + N * K].view(G, N, K)
+        assert _rel(got, ref) < 1e-5, nmb
+        assert float(rows[:, :off].sub(-3.0).abs().max()) == 0 and float(rows[:, off + N * K:].sub(-3.0).abs().max()) == 0
+
+
 def test_gemm1x1_operand_above_2_31_elements():
     """An X operand of more than 2^31 elements (64-bit client bases): the last client's last rows — the largest
     offsets — against a chunked fp32 reference."""
