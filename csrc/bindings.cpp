@@ -115,6 +115,10 @@ void res_grad(uintptr_t out, uintptr_t dx1, uintptr_t dx2, uintptr_t da, uintptr
               uintptr_t stream);
 void res_grad_s2(uintptr_t out, uintptr_t dx1, uintptr_t dx2s, int N, int D, int H, int W, int C, int out_bf16,
                  uintptr_t stream);
+void res_grad_om(uintptr_t out, uintptr_t dx1, uintptr_t dx2, uintptr_t da, uintptr_t mask, uintptr_t omask, int64_t n,
+                 int flags, uintptr_t stream);
+void res_grad_s2_om(uintptr_t out, uintptr_t dx1, uintptr_t dx2s, uintptr_t omask, int N, int D, int H, int W, int C,
+                    int out_bf16, uintptr_t stream);
 // img.hip
 void img_input(uintptr_t src, uintptr_t idx, uintptr_t out, int N, int H, int W, int CP, float m0, float m1, float m2,
                float s0, float s1, float s2, int aug, int pad, uintptr_t seed_dev, int64_t seed_base, uintptr_t cids,
@@ -304,6 +308,8 @@ PYBIND11_MODULE(_nidt_hip, m) {
   DEF(gn_fwd);
   DEF(gn_bwd);
   DEF(gn_param_grads);
+  DEF(res_grad_om);
+  DEF(res_grad_s2_om);
   DEF(res_grad);
   DEF(res_grad_s2);
   DEF(img_input);

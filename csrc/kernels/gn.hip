@@ -555,9 +555,14 @@ __device__ __forceinline__ void store8(void* out, int64_t q, const float (&v)[8]
   }
 }
 
+// [OMASK] omask (optional): the output is also multiplied by [omask > 0] — the ReLU mask of the previous block's
+// output, so the stream handed on is the gradient at that block's BatchNorm output (pre-ReLU) and its BN backward
+// and identity shortcut read no mask (config 5: two fewer passes over the widest tensor per block).  mask == null
+// with dx2 == null: da is already masked.
 template <bool OB, bool DB>
 __global__ void k_res_grad(void* __restrict__ out, const uint16_t* __restrict__ dx1, const uint16_t* __restrict__ dx2,
-                           const void* __restrict__ da, const uint16_t* __restrict__ mask, int64_t n8) {
+                           const void* __restrict__ da, const uint16_t* __restrict__ mask,
+                           const uint16_t* __restrict__ omask, int64_t n8) {
   for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n8; q += (int64_t)gridDim.x * blockDim.x) {
     float a[8], b[8];
     unpack8(*reinterpret_cast<const uint4*>(dx1 + q * 8), a);
@@ -565,7 +570,12 @@ __global__ void k_res_grad(void* __restrict__ out, const uint16_t* __restrict__ 
       unpack8(*reinterpret_cast<const uint4*>(dx2 + q * 8), b);
     } else {
       float m[8], d[8];
-      unpack8(*reinterpret_cast<const uint4*>(mask + q * 8), m);
+      if (mask) {
+        unpack8(*reinterpret_cast<const uint4*>(mask + q * 8), m);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) m[e] = 1.f;
+      }
       if (DB) {
         unpack8(*reinterpret_cast<const uint4*>(reinterpret_cast<const uint16_t*>(da) + q * 8), d);
       } else {
@@ -579,20 +589,27 @@ __global__ void k_res_grad(void* __restrict__ out, const uint16_t* __restrict__ 
     float v[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) v[e] = a[e] + b[e];
+    if (omask) {
+      float om[8];
+      unpack8(*reinterpret_cast<const uint4*>(omask + q * 8), om);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = om[e] > 0.f ? v[e] : 0.f;
+    }
     store8(out, q, v, OB);
   }
 }
 
-// flags: bit 0 = out bf16, bit 1 = da bf16
-void res_grad(uintptr_t out, uintptr_t dx1, uintptr_t dx2, uintptr_t da, uintptr_t mask, int64_t n, int flags,
-              uintptr_t stream) {
-  NIDT_REQUIRE(n % 8 == 0 && (dx2 || (da && mask)), "res_grad: n % 8 == 0 and (dx2 or da+mask)");
+// flags: bit 0 = out bf16, bit 1 = da bf16.  res_grad_om: with the [OMASK] output mask (and mask optional)
+void res_grad_om(uintptr_t out, uintptr_t dx1, uintptr_t dx2, uintptr_t da, uintptr_t mask, uintptr_t omask, int64_t n,
+                 int flags, uintptr_t stream) {
+  NIDT_REQUIRE(n % 8 == 0 && (dx2 || da), "res_grad: n % 8 == 0 and (dx2 or da)");
   const int64_t n8 = n / 8;
   const dim3 grid((unsigned)std::min<int64_t>(8192, (n8 + 255) / 256));
   hipStream_t s = as_stream(stream);
 #define RG(OB, DB)                                                                                             \
   hipLaunchKernelGGL((k_res_grad<OB, DB>), grid, dim3(256), 0, s, ptr<void>(out), ptr<const uint16_t>(dx1),     \
-                     ptr<const uint16_t>(dx2), ptr<const void>(da), ptr<const uint16_t>(mask), n8)
+                     ptr<const uint16_t>(dx2), ptr<const void>(da), ptr<const uint16_t>(mask),                  \
+                     ptr<const uint16_t>(omask), n8)
   switch (flags & 3) {
     case 0: RG(false, false); break;
     case 1: RG(true, false); break;
@@ -603,12 +620,19 @@ void res_grad(uintptr_t out, uintptr_t dx1, uintptr_t dx2, uintptr_t da, uintptr
   NIDT_CHECK(hipGetLastError());
 }
 
+void res_grad(uintptr_t out, uintptr_t dx1, uintptr_t dx2, uintptr_t da, uintptr_t mask, int64_t n, int flags,
+              uintptr_t stream) {
+  NIDT_REQUIRE(dx2 || (da && mask), "res_grad: dx2 or da+mask");
+  res_grad_om(out, dx1, dx2, da, mask, 0, n, flags, stream);
+}
+
 // Residual-stream gradient of a downsampling block: out = dx1 + (dx2 at the even pixels), with the 1x1(x1) stride-2
 // shortcut's data gradient given at half resolution (dx2s [N][Do][Ho][Wo][C], Ho = ceil(H/2); D = 1 for 2-D maps):
 // the shortcut conv read only the even positions, so no full-size zero-filled scatter of its gradient is needed.
 template <bool OB>
 __global__ void k_res_grad_s2(void* __restrict__ out, const uint16_t* __restrict__ dx1,
-                              const uint16_t* __restrict__ dx2s, int64_t n8, int D, int H, int W, int C) {
+                              const uint16_t* __restrict__ dx2s, const uint16_t* __restrict__ omask, int64_t n8, int D,
+                              int H, int W, int C) {
   const int C8 = C / 8, Do = D > 1 ? (D + 1) / 2 : 1, Ho = (H + 1) / 2, Wo = (W + 1) / 2;
   for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n8; q += (int64_t)gridDim.x * blockDim.x) {
     const int c8 = (int)(q % C8);
@@ -632,22 +656,33 @@ __global__ void k_res_grad_s2(void* __restrict__ out, const uint16_t* __restrict
     float v[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) v[e] = a[e] + b[e];
+    if (omask) {  // [OMASK]
+      float om[8];
+      unpack8(*reinterpret_cast<const uint4*>(omask + q * 8), om);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = om[e] > 0.f ? v[e] : 0.f;
+    }
     store8(out, q, v, OB);
   }
 }
 
-void res_grad_s2(uintptr_t out, uintptr_t dx1, uintptr_t dx2s, int N, int D, int H, int W, int C, int out_bf16,
-                 uintptr_t stream) {
+void res_grad_s2_om(uintptr_t out, uintptr_t dx1, uintptr_t dx2s, uintptr_t omask, int N, int D, int H, int W, int C,
+                    int out_bf16, uintptr_t stream) {
   NIDT_REQUIRE(C % 8 == 0 && D >= 1, "res_grad_s2: C % 8 == 0");
   const int64_t n8 = (int64_t)N * D * H * W * C / 8;
   const dim3 grid((unsigned)std::min<int64_t>(8192, (n8 + 255) / 256));
   if (out_bf16)
     hipLaunchKernelGGL(k_res_grad_s2<true>, grid, dim3(256), 0, as_stream(stream), ptr<void>(out),
-                       ptr<const uint16_t>(dx1), ptr<const uint16_t>(dx2s), n8, D, H, W, C);
+                       ptr<const uint16_t>(dx1), ptr<const uint16_t>(dx2s), ptr<const uint16_t>(omask), n8, D, H, W, C);
   else
     hipLaunchKernelGGL(k_res_grad_s2<false>, grid, dim3(256), 0, as_stream(stream), ptr<void>(out),
-                       ptr<const uint16_t>(dx1), ptr<const uint16_t>(dx2s), n8, D, H, W, C);
+                       ptr<const uint16_t>(dx1), ptr<const uint16_t>(dx2s), ptr<const uint16_t>(omask), n8, D, H, W, C);
   NIDT_CHECK(hipGetLastError());
+}
+
+void res_grad_s2(uintptr_t out, uintptr_t dx1, uintptr_t dx2s, int N, int D, int H, int W, int C, int out_bf16,
+                 uintptr_t stream) {
+  res_grad_s2_om(out, dx1, dx2s, 0, N, D, H, W, C, out_bf16, stream);
 }
 
 static int gn_nv(int S, int C) {

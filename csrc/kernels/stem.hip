@@ -525,6 +525,148 @@ __global__ __launch_bounds__(256, 2) void k_stem_wgrad(StemDims d, const uint8_t
       for (int r = 0; r < 4; ++r) sp[(32 * chh + 16 * i + 4 * fq + r) * 128 + 64 * shh + 16 * j + fr] = acc[i][j][r];
 }
 
+// [WG4] k_stem_wgrad with the four depth tap groups jd in ONE block.  k_stem_wgrad is a block per (sample, od chunk,
+// jd): every one of the four builds the same dy tile from dz and y, so the two 64-channel bf16 tensors (4.45 GB each
+// at config 5) were read four times — 35.6 GB, the kernel ran at ~4.3 TB/s and 8.3 ms per step
+// (profiles/r5_config5_steady.txt).  Here 8 waves = jd (w >> 1) x slot half (w & 1), 64 channels x 64 slots each, share
+// one dy tile per output row; the input rows of the four planes z' = od + jd live in per-jd rings of 4 y' rows
+// (row oh reads y' = oh .. oh + 3 and writes oh + 3 into the slot row oh - 1 read last).  Software-pipelined: the dz / y
+// chunk and the raw input bytes of row oh + 1 are loaded into registers while the MFMAs of row oh run; one barrier
+// after the LDS writes, one after the MFMAs.  Same slab layout as k_stem_wgrad (k_stem_wgrad_fin unchanged).
+constexpr int kW4Ring = 4;
+__global__ __launch_bounds__(512, 2) void k_stem_wgrad4(StemDims d, const uint8_t* __restrict__ xq,
+                                                        const uint16_t* __restrict__ dz, const uint16_t* __restrict__ y,
+                                                        const float* __restrict__ coef, int B, float* __restrict__ slab) {
+  __shared__ __attribute__((aligned(16))) uint16_t bq[4 * kW4Ring * 8 * 4 * 64];  // [jd][ring][r][jw][64 pos]
+  __shared__ __attribute__((aligned(16))) uint16_t dyt[64 * 64];                  // [pos][c]
+  const int nchunk = (d.OD + kWgOD - 1) / kWgOD;
+  const int bid = blockIdx.x;
+  const int oc = bid % nchunk, n = bid / nchunk, g = n / B;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int jdw = wid >> 1, shh = wid & 1;
+  const int64_t vox = (int64_t)d.PZ * d.PY * d.PX;
+  // dy item: position pt, channel chunk cg
+  const int cg = tid & 7, pt = tid >> 3;
+  float ca[8], cb[8], cd[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const int c = g * kSC + cg * 8 + q;
+    ca[q] = coef[c * 3]; cb[q] = coef[c * 3 + 1]; cd[q] = coef[c * 3 + 2];
+  }
+  // staging items it = tid + 512 h: (jd, r, jw, 8-position group)
+  int s_jd[2], s_r[2], s_jw[2], s_p0[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int it = tid + 512 * h;
+    s_jd[h] = it >> 8; s_r[h] = (it >> 5) & 7; s_jw[h] = (it >> 3) & 3; s_p0[h] = (it & 7) * 8;
+  }
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  uint2 rlo[2], rhi[2];  // raw input bytes p0 .. p0 + 15 of the staged row, per item
+  uint4 zr, yr;          // dz / y chunk of the dy item
+  auto ld_raw = [&](int od, int yrow) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      rlo[h] = rhi[h] = make_uint2(0, 0);
+      if (yrow < d.PY) {
+        const uint8_t* row = xq + ((int64_t)n * 8 + s_r[h]) * vox + ((int64_t)(od + s_jd[h]) * d.PY + yrow) * d.PX;
+        rlo[h] = *reinterpret_cast<const uint2*>(row + s_p0[h]);
+        if (s_p0[h] + 8 < d.PX) rhi[h] = *reinterpret_cast<const uint2*>(row + s_p0[h] + 8);
+      }
+    }
+  };
+  auto st_raw = [&](int yrow) {  // the 4 x-shifted bf16 copies of the loaded row into ring slot yrow % kW4Ring
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const uint64_t lo = ((uint64_t)rlo[h].y << 32) | rlo[h].x, hi = ((uint64_t)rhi[h].y << 32) | rhi[h].x;
+      const int sh = 8 * s_jw[h];
+      const uint64_t v = sh ? (lo >> sh) | (hi << (64 - sh)) : lo;
+      *reinterpret_cast<uint4*>(&bq[((((s_jd[h] * kW4Ring + yrow % kW4Ring) * 8 + s_r[h]) * 4 + s_jw[h]) * 64) +
+                                    s_p0[h]]) = u8x8_to_bf16(make_uint2((uint32_t)v, (uint32_t)(v >> 32)));
+    }
+  };
+  auto ld_dy = [&](int od, int oh) {
+    zr = yr = make_uint4(0, 0, 0, 0);
+    if (pt < d.OW) {
+      const int64_t yo = ((((int64_t)n * d.OD + od) * d.OH + oh) * d.OW + pt) * kSC + cg * 8;
+      zr = *reinterpret_cast<const uint4*>(dz + yo);
+      yr = *reinterpret_cast<const uint4*>(y + yo);
+    }
+  };
+  auto st_dy = [&]() {
+    uint4 o = make_uint4(0, 0, 0, 0);
+    if (pt < d.OW) {
+      const uint32_t zu[4] = {zr.x, zr.y, zr.z, zr.w}, yu[4] = {yr.x, yr.y, yr.z, yr.w};
+      float v[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const float zv = __uint_as_float((q & 1) ? (zu[q >> 1] & 0xffff0000u) : (zu[q >> 1] << 16));
+        const float yv = __uint_as_float((q & 1) ? (yu[q >> 1] & 0xffff0000u) : (yu[q >> 1] << 16));
+        v[q] = fmaf(ca[q], zv, fmaf(cb[q], yv, cd[q]));
+      }
+      o = make_uint4(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]), pack_bf16x2(v[4], v[5]), pack_bf16x2(v[6], v[7]));
+    }
+    *reinterpret_cast<uint4*>(&dyt[pt * 64 + cg * 8]) = o;
+  };
+
+  const int od0 = oc * kWgOD, od1 = min(d.OD, od0 + kWgOD);
+  const uint16_t* bqw = bq + jdw * kW4Ring * 8 * 4 * 64;
+  for (int od = od0; od < od1; ++od) {
+    for (int yy = 0; yy < 3; ++yy) {  // ring rows 0..2 (the previous plane's last MFMAs are behind a barrier)
+      ld_raw(od, yy);
+      st_raw(yy);
+    }
+    ld_dy(od, 0);
+    ld_raw(od, 3);
+    for (int oh = 0; oh < d.OH; ++oh) {
+      st_dy();
+      st_raw(oh + 3);
+      __syncthreads();
+      if (oh + 1 < d.OH) {  // next row's operands in flight under this row's MFMAs
+        ld_dy(od, oh + 1);
+        ld_raw(od, oh + 4);
+      }
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        bf16x8 fa[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int q = fr >> 2, pp = fr & 3;
+          const uint16_t* a0 = &dyt[(32 * ks + 8 * fq + q) * 64 + 16 * i + 4 * pp];
+          const uint16_t* a1 = &dyt[(32 * ks + 8 * fq + 4 + q) * 64 + 16 * i + 4 * pp];
+          const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)a0);
+          const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)a1);
+          typedef short s16x8 __attribute__((ext_vector_type(8)));
+          const s16x8 f = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          fa[i] = __builtin_bit_cast(bf16x8, f);
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int sl = 64 * shh + 16 * j + fr;
+          const int jh = sl >> 5, jw = (sl >> 3) & 3, r = sl & 7;
+          const bf16x8 fb = *reinterpret_cast<const bf16x8*>(
+              &bqw[((((oh + jh) % kW4Ring) * 8 + r) * 4 + jw) * 64 + 32 * ks + 8 * fq]);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb, acc[i][j], 0, 0, 0);
+        }
+      }
+      __syncthreads();
+    }
+  }
+  float* sp = slab + ((int64_t)bid * 4 + jdw) * kSC * 128;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) sp[(16 * i + 4 * fq + r) * 128 + 64 * shh + 16 * j + fr] = acc[i][j][r];
+}
+
 // per (g, c, tap k): sum of the client's slabs at the tap's slot, / 255 (the input scale), PyTorch layout [64][343]
 __global__ void k_stem_wgrad_fin(StemDims d, const float* __restrict__ slab, int B, int G, float* __restrict__ grad, int64_t ldg,
                                  int64_t goff) {
@@ -597,8 +739,18 @@ void stem_bwd(uintptr_t dpool, uintptr_t amax, uintptr_t y, uintptr_t xq, uintpt
                      ptr<float>(grad), ldg, goff_g, goff_b, ptr<float>(coef));
   NIDT_CHECK(hipGetLastError());
   const int nchunk = (d.OD + kWgOD - 1) / kWgOD;
-  hipLaunchKernelGGL(k_stem_wgrad, dim3(N * nchunk * 4), dim3(256), 0, s, d, ptr<const uint8_t>(xq),
-                     ptr<const uint16_t>(dz), ptr<const uint16_t>(y), ptr<const float>(coef), B, ptr<float>(slab));
+  // [WG4] one block per (sample, od chunk) for all four jd (NIDT_STEM_WG4=0: k_stem_wgrad, A/B); its raw-row loads
+  // are 8-byte words, so the polyphase rows must be a multiple of 8 bytes (64 at the ABCD shape)
+  static const bool wg4 = [] {
+    const char* e = getenv("NIDT_STEM_WG4");
+    return !(e && e[0] == '0');
+  }();
+  if (wg4 && d.PX % 8 == 0)
+    hipLaunchKernelGGL(k_stem_wgrad4, dim3(N * nchunk), dim3(512), 0, s, d, ptr<const uint8_t>(xq),
+                       ptr<const uint16_t>(dz), ptr<const uint16_t>(y), ptr<const float>(coef), B, ptr<float>(slab));
+  else
+    hipLaunchKernelGGL(k_stem_wgrad, dim3(N * nchunk * 4), dim3(256), 0, s, d, ptr<const uint8_t>(xq),
+                       ptr<const uint16_t>(dz), ptr<const uint16_t>(y), ptr<const float>(coef), B, ptr<float>(slab));
   NIDT_CHECK(hipGetLastError());
   hipLaunchKernelGGL(k_stem_wgrad_fin, dim3(ceil_div(G * kSC * kSK, 256)), dim3(256), 0, s, d, ptr<const float>(slab), B,
                      G, ptr<float>(grad), ldg, goff_w);

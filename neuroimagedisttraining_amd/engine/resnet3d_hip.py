@@ -563,9 +563,15 @@ class GroupedResNet3D:
             if getattr(self, "_ws", None) is None:
                 self._ws = torch.cuda.Stream(device=self.device)
             ws = self._ws
-        for blk, sv in zip(reversed(self.blocks), reversed(saved)):
+        # [OMASK] HIP: the residual-gradient kernel of a block also applies the ReLU mask of the previous block's
+        # output (its input xin), so that block's BN3 / downsample-BN backward and identity shortcut take the stream
+        # pre-masked (no mask reads); NIDT_R3D_OMASK=0 keeps the masks in the BN backward (A/B)
+        omask_on = self.hip and os.environ.get("NIDT_R3D_OMASK", "1") != "0"
+        da_masked = False
+        for bi, (blk, sv) in enumerate(zip(reversed(self.blocks), reversed(saved))):
             xin, t1, s1, h1, t2, s2, h2, t3, s3, td, sd, a = sv
-            dt3 = blk["n3"].bwd(da, a, t3, s3, theta, grads, G)
+            amask = None if da_masked else a
+            dt3 = blk["n3"].bwd(da, amask, t3, s3, theta, grads, G)
             dh2 = blk["c3"].bwd(dt3, h2, theta, grads, G, ws=ws)
             dt2 = blk["n2"].bwd(dh2, h2, t2, s2, theta, grads, G)
             dh1 = blk["c2"].bwd(dt2, h1, theta, grads, G, ws=ws)
@@ -573,21 +579,25 @@ class GroupedResNet3D:
             dx1 = blk["c1"].bwd(dt1, xin, theta, grads, G, ws=ws)
             dx2 = None
             if "cd" in blk:
-                dtd = blk["nd"].bwd(da, a, td, sd, theta, grads, G)
+                dtd = blk["nd"].bwd(da, amask, td, sd, theta, grads, G)
                 dx2 = blk["cd"].bwd(dtd, xin, theta, grads, G, ws=ws)
             half = dx2 is not None and blk["cd"].stride == 2  # 1x1x1 stride-2 projection: even-voxel gradient
             if self.hip:
                 out = torch.empty(dx1.shape, device=dx1.device, dtype=torch.bfloat16)
+                # the input of the network's first block is the stem output (its backward applies its own masks)
+                om = xin if (omask_on and bi + 1 < len(self.blocks)) else None
+                omp = om.data_ptr() if om is not None else 0
                 if half:
                     Nn, Dd, Hh, Ww, Cc = dx1.shape
-                    ops.ext().res_grad_s2(out.data_ptr(), dx1.data_ptr(), dx2.data_ptr(), Nn, Dd, Hh, Ww, Cc, 1,
-                                          _stream())
+                    ops.ext().res_grad_s2_om(out.data_ptr(), dx1.data_ptr(), dx2.data_ptr(), omp, Nn, Dd, Hh, Ww, Cc,
+                                             1, _stream())
                 else:
-                    ops.ext().res_grad(out.data_ptr(), dx1.data_ptr(), dx2.data_ptr() if dx2 is not None else 0,
-                                       0 if dx2 is not None else da.data_ptr(),
-                                       0 if dx2 is not None else a.data_ptr(), out.numel(),
-                                       1 | (2 if da.dtype == torch.bfloat16 else 0), _stream())
+                    ops.ext().res_grad_om(out.data_ptr(), dx1.data_ptr(), dx2.data_ptr() if dx2 is not None else 0,
+                                          0 if dx2 is not None else da.data_ptr(),
+                                          0 if (dx2 is not None or amask is None) else amask.data_ptr(), omp,
+                                          out.numel(), 1 | (2 if da.dtype == torch.bfloat16 else 0), _stream())
                 da = out
+                da_masked = om is not None
             elif half:
                 da = dx1.float().clone()
                 da[:, ::2, ::2, ::2] += dx2.float()

@@ -360,12 +360,48 @@ def test_resnet3d_lockstep_step_matches_per_client_autograd():
     assert lg.shape == (G * B, 1) and torch.isfinite(lg).all()
 
 
-@pytest.mark.parametrize("G,B,dims", [(2, 1, (121, 145, 121)), (2, 2, (21, 26, 22)), (3, 1, (9, 128, 13))])
+def test_resnet3d_omask_bit_identical(monkeypatch):
+    """[OMASK]: the residual-gradient kernel applying the previous block's ReLU mask (BN3 / downsample-BN backward and
+    identity shortcuts then read no mask) gives bit-identical gradients, losses and running statistics to masking in
+    the BN backward — identity and projection blocks, stride-2 projections."""
+    from neuroimagedisttraining_amd.engine.executor import padded_rows
+    from neuroimagedisttraining_amd.engine.resnet3d_hip import ResNet3DHipEngine
+    from neuroimagedisttraining_amd.models.resnet3d import Bottleneck, ResNet3D
+    dev = _dev()
+    torch.manual_seed(3)
+    G, B = 2, 2
+    vol = torch.randint(0, 256, (G * B, 40, 44, 40), dtype=torch.uint8, device=dev)
+    lab = torch.tensor([0.0, 1.0, 1.0, 0.0], device=dev)
+    m = ResNet3D(Bottleneck, [2, 2, 1, 1], 1)
+    eng = ResNet3DHipEngine(m, vol, lab, dev)
+    L, Lb = eng.players, eng.blayers
+    flat = torch.cat([p.detach().reshape(-1) for p in m.parameters()]).to(dev)
+    bflat = torch.cat([b.detach().float().reshape(-1) for b in m.buffers()]).to(dev)
+    idx = torch.arange(G * B, dtype=torch.int32, device=dev)
+    outs = []
+    for om in ("0", "1"):
+        monkeypatch.setenv("NIDT_R3D_OMASK", om)
+        th, gr, bu = padded_rows(G, L.total, dev), padded_rows(G, L.total, dev), padded_rows(G, Lb.total, dev)
+        th.copy_(flat.expand(G, -1) + 0.01 * torch.randn(G, L.total, device=dev, generator=torch.Generator(
+            device=dev).manual_seed(1)))
+        bu.copy_(bflat.expand(G, -1))
+        gr.zero_()
+        losses = eng.train_step(th, bu, gr, idx, G, B, 1.0, 0)
+        torch.cuda.synchronize()
+        outs.append((losses.clone(), gr.clone(), bu.clone()))
+    (l0, g0, b0), (l1, g1, b1) = outs
+    assert torch.equal(l0, l1) and torch.equal(b0, b1)
+    assert float(g0.abs().sum()) > 0 and torch.equal(g0, g1)
+
+
+@pytest.mark.parametrize("G,B,dims", [(2, 1, (121, 145, 121)), (2, 2, (21, 26, 22)), (3, 1, (9, 128, 13)),
+                                        (2, 2, (15, 20, 10))])
 def test_stem_hip_fwd_bwd_match_torch(G, B, dims):
     """stem.hip (polyphase 7^3/s2 conv on MFMA + BN statistics, BN+ReLU+3^3/s2 max-pool, the backward with the MFMA
     weight gradient) against fp32 PyTorch autograd of Conv3d(1, 64, 7, 2, 3) -> BatchNorm3d -> ReLU -> MaxPool3d,
-    per client; full ABCD extents and odd/even small ones.  The reference rounds the weights and the conv output
-    to bf16 where the HIP path stores them."""
+    per client; full ABCD extents and odd/even small ones (the ABCD and 15 x 20 x 10 extents, 8-byte polyphase rows,
+    take the one-block-for-all-jd weight gradient k_stem_wgrad4, the others k_stem_wgrad).  The reference rounds the
+    weights and the conv output to bf16 where the HIP path stores them."""
     from neuroimagedisttraining_amd.engine.resnet3d_hip import GroupedResNet3D
     from neuroimagedisttraining_amd.engine.executor import padded_rows
     from neuroimagedisttraining_amd.engine.flat import ParamLayout
