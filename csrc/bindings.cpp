@@ -147,6 +147,9 @@ void bnr_apply(uintptr_t t, uintptr_t res, uintptr_t stats, uintptr_t theta, int
 void bnr_bwd(uintptr_t t, uintptr_t dy, int dy_bf16, uintptr_t mask, uintptr_t stats, uintptr_t theta, int64_t ldt,
              int64_t off_w, int64_t off_b, uintptr_t grads, int64_t ldg, uintptr_t ws, uintptr_t coef, uintptr_t dt,
              int G, int64_t M, int C, int eval_mode, uintptr_t stream);
+void bnr_bwd_tm(uintptr_t t, uintptr_t dy, int dy_bf16, uintptr_t mask, uintptr_t stats, uintptr_t theta, int64_t ldt,
+                int64_t off_w, int64_t off_b, uintptr_t grads, int64_t ldg, uintptr_t ws, uintptr_t coef, uintptr_t dt,
+                int G, int64_t M, int C, int eval_mode, int tmask, uintptr_t stream);
 // bn.hip
 void bn_finalize(uintptr_t stats, int nPB, int BP, int Mg, int G, int C, uintptr_t theta, int64_t ldt, int64_t off_g,
                  int64_t off_b, uintptr_t bufs, int64_t ldb, int64_t off_rm, int64_t off_rv, int64_t off_nbt,
@@ -325,6 +328,7 @@ PYBIND11_MODULE(_nidt_hip, m) {
   DEF(bnr_stats);
   DEF(bnr_eval_stats);
   DEF(bnr_apply);
+  DEF(bnr_bwd_tm);
   DEF(bnr_bwd);
   DEF(bn_finalize);
   DEF(bn_eval);

@@ -25,26 +25,42 @@ __device__ __forceinline__ void bnr_unpack8(const uint4 v, float* f) {
   }
 }
 
+// [TMASK] the BN affine of the forward apply, written so that every kernel computes it bit-identically (explicit
+// fmaf, no contraction choices): sc = gamma rstd, sf = beta - mu sc, x = t sc + sf.  The backward of a BN + ReLU
+// without residual (the Bottleneck's bn1 / bn2) then recomputes the ReLU mask of the stored output from t instead of
+// reading that bf16 tensor: mask = bf16(relu(x)) > 0, exactly the stored value's test.
+__device__ __forceinline__ void bnr_affine(float gamma, float beta, float mu, float rs, float& sc, float& sf) {
+  sc = gamma * rs;
+  sf = fmaf(-mu, sc, beta);
+}
+__device__ __forceinline__ bool bnr_relu_live(float t, float sc, float sf) {
+  return __uint_as_float((uint32_t)f32_to_bf16(fmaxf(fmaf(t, sc, sf), 0.f)) << 16) > 0.f;
+}
+
 // MODE 0: part = (sum t, sum t^2); MODE 1: part = (sum dy', sum dy' * xhat) with dy' = dy * (mask > 0) (mask optional),
 // xhat = (t - mean) * rstd from stats [G][C][2].  dy: fp32 (DYB false) or bf16.
-template <int MODE, bool DYB>
+// TM: the mask from t ([TMASK]; theta rows give gamma / beta)
+template <int MODE, bool DYB, bool TM = false>
 __global__ __launch_bounds__(kBnrThreads) void k_bnr_partial(const uint16_t* __restrict__ t, const void* __restrict__ dyv,
                                                              const uint16_t* __restrict__ mask,
                                                              const float* __restrict__ stats, int M, int C,
-                                                             float* __restrict__ part) {
+                                                             float* __restrict__ part, const float* __restrict__ theta = nullptr,
+                                                             int64_t ldt = 0, int64_t off_w = 0, int64_t off_b = 0) {
   __shared__ float sm[kBnrThreads * 17];
   const int chunk = blockIdx.x, g = blockIdx.y, nchunk = gridDim.x, tid = threadIdx.x;
   const int nch = C >> 3, rows = kBnrThreads / nch;
   const int j = tid % nch, r = tid / nch;
   const int p0 = chunk * kBnrChunk, p1 = min(M, p0 + kBnrChunk);
   const int64_t base = (int64_t)g * M * C;
-  float a[8], b[8], mu[8], rs[8];
+  float a[8], b[8], mu[8], rs[8], tsc[8], tsf[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
     a[e] = b[e] = 0.f;
     if (MODE == 1) {
       mu[e] = stats[((int64_t)g * C + 8 * j + e) * 2];
       rs[e] = stats[((int64_t)g * C + 8 * j + e) * 2 + 1];
+      if (TM) bnr_affine(theta[(int64_t)g * ldt + off_w + 8 * j + e], theta[(int64_t)g * ldt + off_b + 8 * j + e], mu[e],
+                         rs[e], tsc[e], tsf[e]);
     }
   }
   // per position: the t chunk, and for MODE 1 the dy / mask chunks; four positions' loads are issued before
@@ -64,7 +80,7 @@ __global__ __launch_bounds__(kBnrThreads) void k_bnr_partial(const uint16_t* __r
         v.d0 = q[0];
         v.d1 = q[1];
       }
-      if (mask) v.m = *reinterpret_cast<const uint4*>(mask + o);
+      if (!TM && mask) v.m = *reinterpret_cast<const uint4*>(mask + o);
     }
     return v;
   };
@@ -86,7 +102,10 @@ __global__ __launch_bounds__(kBnrThreads) void k_bnr_partial(const uint16_t* __r
 #pragma unroll
         for (int e = 0; e < 8; ++e) d[e] = __uint_as_float(u[e]);
       }
-      if (mask) {
+      if (TM) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) d[e] = bnr_relu_live(f[e], tsc[e], tsf[e]) ? d[e] : 0.f;
+      } else if (mask) {
         float mk[8];
         bnr_unpack8(v.m, mk);
 #pragma unroll
@@ -185,8 +204,7 @@ __global__ __launch_bounds__(256) void k_bnr_apply(const uint16_t* __restrict__ 
   for (int e = 0; e < 8; ++e) {
     const int c = 8 * j + e;
     const float mu = stats[((int64_t)g * C + c) * 2], rs = stats[((int64_t)g * C + c) * 2 + 1];
-    sc[e] = theta[(int64_t)g * ldt + off_w + c] * rs;
-    sf[e] = theta[(int64_t)g * ldt + off_b + c] - mu * sc[e];
+    bnr_affine(theta[(int64_t)g * ldt + off_w + c], theta[(int64_t)g * ldt + off_b + c], mu, rs, sc[e], sf[e]);
   }
   for (int64_t q = q0; q < per; q += (int64_t)gridDim.x * blockDim.x) {
     const int64_t o = ((int64_t)g * M * nch + q) * 8;
@@ -229,12 +247,12 @@ __global__ void k_bnr_bwd_fin(const float* __restrict__ part, int nchunk, int G,
 }
 
 // dt = rstd * gamma * (dy' - mean(dy') - xhat * mean(dy' xhat))   (eval mode: coef = 0 -> rstd * gamma * dy')
-template <bool DYB>
+template <bool DYB, bool TM = false>
 __global__ __launch_bounds__(256) void k_bnr_bwd_apply(const uint16_t* __restrict__ t, const void* __restrict__ dyv,
                                                        const uint16_t* __restrict__ mask,
                                                        const float* __restrict__ stats, const float* __restrict__ coef,
                                                        const float* __restrict__ theta, int64_t ldt, int64_t off_w,
-                                                       uint16_t* __restrict__ dt, int64_t M, int C) {
+                                                       uint16_t* __restrict__ dt, int64_t M, int C, int64_t off_b = 0) {
   const int nch = C >> 3;
   const int64_t per = M * nch;
   const int g = blockIdx.y;
@@ -242,11 +260,12 @@ __global__ __launch_bounds__(256) void k_bnr_bwd_apply(const uint16_t* __restric
   // K2 = -A rstd m2, K1 = -A m1 - K2 mu
   const int64_t q0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int j = (int)(q0 % nch);
-  float A[8], K1[8], K2[8];
+  float A[8], K1[8], K2[8], tsc[8], tsf[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
     const int c = 8 * j + e;
     const float mu = stats[((int64_t)g * C + c) * 2], rs = stats[((int64_t)g * C + c) * 2 + 1];
+    if (TM) bnr_affine(theta[(int64_t)g * ldt + off_w + c], theta[(int64_t)g * ldt + off_b + c], mu, rs, tsc[e], tsf[e]);
     const float m1 = coef ? coef[((int64_t)g * C + c) * 2] : 0.f;
     const float m2 = coef ? coef[((int64_t)g * C + c) * 2 + 1] : 0.f;
     A[e] = rs * theta[(int64_t)g * ldt + off_w + c];
@@ -264,7 +283,10 @@ __global__ __launch_bounds__(256) void k_bnr_bwd_apply(const uint16_t* __restric
       const float4 x0 = p[0], x1 = p[1];
       d[0] = x0.x; d[1] = x0.y; d[2] = x0.z; d[3] = x0.w; d[4] = x1.x; d[5] = x1.y; d[6] = x1.z; d[7] = x1.w;
     }
-    if (mask) {
+    if (TM) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) d[e] = bnr_relu_live(f[e], tsc[e], tsf[e]) ? d[e] : 0.f;
+    } else if (mask) {
       float mk[8];
       bnr_unpack8(*reinterpret_cast<const uint4*>(mask + o), mk);
 #pragma unroll
@@ -342,13 +364,31 @@ void bnr_apply(uintptr_t t, uintptr_t res, uintptr_t stats, uintptr_t theta, int
 }
 
 // backward: dgamma/dbeta rows (train mode) and dt.  eval_mode: BN used running stats (no statistics gradient).
-void bnr_bwd(uintptr_t t, uintptr_t dy, int dy_bf16, uintptr_t mask, uintptr_t stats, uintptr_t theta, int64_t ldt,
-             int64_t off_w, int64_t off_b, uintptr_t grads, int64_t ldg, uintptr_t ws, uintptr_t coef, uintptr_t dt,
-             int G, int64_t M, int C, int eval_mode, uintptr_t stream) {
+// bnr_bwd_tm with tmask: the ReLU mask recomputed from t ([TMASK]; the forward was bnr_apply with relu, no residual,
+// and the same stats / theta rows); mask must be null then.
+void bnr_bwd_tm(uintptr_t t, uintptr_t dy, int dy_bf16, uintptr_t mask, uintptr_t stats, uintptr_t theta, int64_t ldt,
+                int64_t off_w, int64_t off_b, uintptr_t grads, int64_t ldg, uintptr_t ws, uintptr_t coef, uintptr_t dt,
+                int G, int64_t M, int C, int eval_mode, int tmask, uintptr_t stream) {
   bnr_check(G, M, C, "bnr_bwd");
   NIDT_REQUIRE(C / 8 <= kBnrThreads, "bnr_bwd: C <= 2048");
+  NIDT_REQUIRE(!tmask || (!mask && dy_bf16), "bnr_bwd: tmask replaces the mask tensor (bf16 dy)");
   hipStream_t s = as_stream(stream);
   const int nc = bnr_nchunk(M);
+  if (tmask) {
+    hipLaunchKernelGGL((k_bnr_partial<1, true, true>), dim3(nc, G), dim3(kBnrThreads), 0, s, ptr<const uint16_t>(t),
+                       ptr<const void>(dy), nullptr, ptr<const float>(stats), (int)M, C, ptr<float>(ws),
+                       ptr<const float>(theta), ldt, off_w, off_b);
+    NIDT_CHECK(hipGetLastError());
+    hipLaunchKernelGGL(k_bnr_bwd_fin, dim3(G), dim3(256), 0, s, ptr<const float>(ws), nc, G, C, (int)M,
+                       ptr<float>(grads), ldg, off_w, off_b, ptr<float>(coef));
+    NIDT_CHECK(hipGetLastError());
+    hipLaunchKernelGGL((k_bnr_bwd_apply<true, true>), bnr_grid(G, M, C), dim3(256), 0, s, ptr<const uint16_t>(t),
+                       ptr<const void>(dy), nullptr, ptr<const float>(stats),
+                       eval_mode ? nullptr : ptr<const float>(coef), ptr<const float>(theta), ldt, off_w,
+                       ptr<uint16_t>(dt), M, C, off_b);
+    NIDT_CHECK(hipGetLastError());
+    return;
+  }
   if (dy_bf16)
     hipLaunchKernelGGL((k_bnr_partial<1, true>), dim3(nc, G), dim3(kBnrThreads), 0, s, ptr<const uint16_t>(t),
                        ptr<const void>(dy), ptr<const uint16_t>(mask), ptr<const float>(stats), (int)M, C, ptr<float>(ws));
@@ -370,6 +410,13 @@ void bnr_bwd(uintptr_t t, uintptr_t dy, int dy_bf16, uintptr_t mask, uintptr_t s
                        ptr<const uint16_t>(mask), ptr<const float>(stats), cf, ptr<const float>(theta), ldt, off_w,
                        ptr<uint16_t>(dt), M, C);
   NIDT_CHECK(hipGetLastError());
+}
+
+void bnr_bwd(uintptr_t t, uintptr_t dy, int dy_bf16, uintptr_t mask, uintptr_t stats, uintptr_t theta, int64_t ldt,
+             int64_t off_w, int64_t off_b, uintptr_t grads, int64_t ldg, uintptr_t ws, uintptr_t coef, uintptr_t dt,
+             int G, int64_t M, int C, int eval_mode, uintptr_t stream) {
+  bnr_bwd_tm(t, dy, dy_bf16, mask, stats, theta, ldt, off_w, off_b, grads, ldg, ws, coef, dt, G, M, C, eval_mode, 0,
+             stream);
 }
 
 }  // namespace nidt

@@ -333,7 +333,9 @@ class GBN3:
         assert N % G == 0
         return y, stats
 
-    def bwd(self, dy, mask, t, stats, theta, grads, G, eval_mode=False):
+    def bwd(self, dy, mask, t, stats, theta, grads, G, eval_mode=False, tmask=False):
+        """``tmask`` (HIP): the forward was ``fwd(relu=True)`` without residual and ``mask`` is its output; the kernels
+        recompute that ReLU mask from ``t`` bit-exactly instead of reading the mask tensor ([TMASK], ``bnr.hip``)."""
         if not self.hip:
             C = self.C
             d = dy.float().reshape(G, -1, C)
@@ -357,10 +359,11 @@ class GBN3:
         ws = torch.empty(m.bnr_workspace(G, M, self.C), device=t.device, dtype=torch.float32)
         coef = torch.empty(G, self.C, 2, device=t.device, dtype=torch.float32)
         dt = torch.empty_like(t)
-        m.bnr_bwd(t.data_ptr(), dy.data_ptr(), int(dy.dtype == torch.bfloat16),
-                  mask.data_ptr() if mask is not None else 0, stats.data_ptr(), theta.data_ptr(), theta.stride(0),
-                  self.off_w, self.off_b, grads.data_ptr(), grads.stride(0), ws.data_ptr(), coef.data_ptr(),
-                  dt.data_ptr(), G, M, self.C, int(eval_mode), st)
+        tm = bool(tmask) and mask is not None and dy.dtype == torch.bfloat16
+        m.bnr_bwd_tm(t.data_ptr(), dy.data_ptr(), int(dy.dtype == torch.bfloat16),
+                     mask.data_ptr() if (mask is not None and not tm) else 0, stats.data_ptr(), theta.data_ptr(),
+                     theta.stride(0), self.off_w, self.off_b, grads.data_ptr(), grads.stride(0), ws.data_ptr(),
+                     coef.data_ptr(), dt.data_ptr(), G, M, self.C, int(eval_mode), int(tm), st)
         return dt
 
 
@@ -567,15 +570,17 @@ class GroupedResNet3D:
         # output (its input xin), so that block's BN3 / downsample-BN backward and identity shortcut take the stream
         # pre-masked (no mask reads); NIDT_R3D_OMASK=0 keeps the masks in the BN backward (A/B)
         omask_on = self.hip and os.environ.get("NIDT_R3D_OMASK", "1") != "0"
+        # [TMASK] bn1 / bn2 backward recompute their ReLU mask from t (no h1 / h2 reads); NIDT_R3D_TMASK=0: A/B
+        tm = self.hip and os.environ.get("NIDT_R3D_TMASK", "1") != "0"
         da_masked = False
         for bi, (blk, sv) in enumerate(zip(reversed(self.blocks), reversed(saved))):
             xin, t1, s1, h1, t2, s2, h2, t3, s3, td, sd, a = sv
             amask = None if da_masked else a
             dt3 = blk["n3"].bwd(da, amask, t3, s3, theta, grads, G)
             dh2 = blk["c3"].bwd(dt3, h2, theta, grads, G, ws=ws)
-            dt2 = blk["n2"].bwd(dh2, h2, t2, s2, theta, grads, G)
+            dt2 = blk["n2"].bwd(dh2, h2, t2, s2, theta, grads, G, tmask=tm)
             dh1 = blk["c2"].bwd(dt2, h1, theta, grads, G, ws=ws)
-            dt1 = blk["n1"].bwd(dh1, h1, t1, s1, theta, grads, G)
+            dt1 = blk["n1"].bwd(dh1, h1, t1, s1, theta, grads, G, tmask=tm)
             dx1 = blk["c1"].bwd(dt1, xin, theta, grads, G, ws=ws)
             dx2 = None
             if "cd" in blk:

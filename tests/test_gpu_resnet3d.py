@@ -360,10 +360,12 @@ def test_resnet3d_lockstep_step_matches_per_client_autograd():
     assert lg.shape == (G * B, 1) and torch.isfinite(lg).all()
 
 
-def test_resnet3d_omask_bit_identical(monkeypatch):
+@pytest.mark.parametrize("env", ["NIDT_R3D_OMASK", "NIDT_R3D_TMASK"])
+def test_resnet3d_omask_bit_identical(monkeypatch, env):
     """[OMASK]: the residual-gradient kernel applying the previous block's ReLU mask (BN3 / downsample-BN backward and
     identity shortcuts then read no mask) gives bit-identical gradients, losses and running statistics to masking in
-    the BN backward — identity and projection blocks, stride-2 projections."""
+    the BN backward — identity and projection blocks, stride-2 projections.  [TMASK]: bn1 / bn2 backward recomputing
+    their ReLU mask from the pre-BN tensor, likewise bit-identical to reading the stored output."""
     from neuroimagedisttraining_amd.engine.executor import padded_rows
     from neuroimagedisttraining_amd.engine.resnet3d_hip import ResNet3DHipEngine
     from neuroimagedisttraining_amd.models.resnet3d import Bottleneck, ResNet3D
@@ -380,7 +382,7 @@ def test_resnet3d_omask_bit_identical(monkeypatch):
     idx = torch.arange(G * B, dtype=torch.int32, device=dev)
     outs = []
     for om in ("0", "1"):
-        monkeypatch.setenv("NIDT_R3D_OMASK", om)
+        monkeypatch.setenv(env, om)
         th, gr, bu = padded_rows(G, L.total, dev), padded_rows(G, L.total, dev), padded_rows(G, Lb.total, dev)
         th.copy_(flat.expand(G, -1) + 0.01 * torch.randn(G, L.total, device=dev, generator=torch.Generator(
             device=dev).manual_seed(1)))
