@@ -123,6 +123,44 @@ def slab_conv(x_ptr, w_ptr, y_ptr, G, B, D, H, W, Cin, Cout, pad, device):
     return True
 
 
+# 3x3x3 stride-1 weight gradients with the union-staged B operand of the AlexNet3D conv2-5 kernels (k_conv_wgrad_slab:
+# one kd-slab union per 64 channels, or k_conv_wgrad_tri: one three-tap union per (kd, kh)) where the shape is eligible;
+# NIDT_R3D_WG_UNION=0 keeps every layer on the position-table kernel k_conv_wgrad_dma (A/B)
+_WG_UNION = os.environ.get("NIDT_R3D_WG_UNION", "1") != "0"
+_WG_TABS = {}
+
+
+def union_wgrad(x, dy, grads, off, G, B, D, H, W, cin, cout, pad):
+    """dW of a 3x3x3 stride-1 conv into the gradient rows through k_conv_wgrad_slab / k_conv_wgrad_tri; False
+    (nothing launched) when neither applies."""
+    m = ops.ext()
+    if not _WG_UNION:
+        return False
+    if m.conv3d_wgrad_slab_pick(G, B, D, H, W, cin, cout, pad):
+        kind, ns = "slab", m.conv3d_wgrad_slab_nsplit(G, B, D, H, W, cin, cout, pad)
+    elif m.conv3d_wgrad_tri_pick(G, B, D, H, W, cin, cout, pad):
+        kind, ns = "tri", m.conv3d_wgrad_tri_nsplit(G, B, D, H, W, cin, cout, pad)
+    else:
+        return False
+    key = (kind, str(x.device), B, D, H, W, pad)
+    tab = _WG_TABS.get(key)
+    if tab is None:
+        size = (m.conv3d_wgrad_slab_table_size if kind == "slab" else m.conv3d_wgrad_tri_table_size)(B, D, H, W, pad)
+        tab = torch.empty(size, device=x.device, dtype=torch.int32)
+        (m.conv3d_wgrad_slab_table if kind == "slab" else m.conv3d_wgrad_tri_table)(tab.data_ptr(), B, D, H, W, pad,
+                                                                                     _stream())
+        if not torch.cuda.is_current_stream_capturing():
+            torch.cuda.current_stream().synchronize()  # shared with launches on other streams from now on
+            _WG_TABS[key] = tab
+        else:
+            _BRANCH_KEEP.append(tab)
+    part = torch.empty(ns * G * cout * 27 * cin, device=x.device, dtype=torch.float32)
+    fn = m.conv3d_wgrad_slab if kind == "slab" else m.conv3d_wgrad_tri
+    fn(x.data_ptr(), dy.data_ptr(), part.data_ptr(), grads.data_ptr(), grads.stride(0), off, G, B, D, H, W, cin, cout,
+       pad, ns, 1.0, tab.data_ptr(), _stream())
+    return True
+
+
 class GConv3:
     """Client-grouped Conv3d (k = 1 or 3, stride 1/2, no bias) on channels-last ``[N, D, H, W, C]`` bf16.  Weight
     images come from the network's :class:`~.resnet2d_hip.WeightPacker` (two launches per step for all layers;
@@ -230,10 +268,13 @@ class GConv3:
             ws.wait_stream(cur)
             _BRANCH_KEEP.extend((x, dy, ptab))  # referenced until the branch joins (no record_stream)
         with torch.cuda.stream(ws if ws is not None else cur):
-            part = torch.empty(ns * G * self.cout * self.kt * self.cin, device=x.device, dtype=torch.float32)
-            m.conv_wgrad_g(x.data_ptr(), dy.data_ptr(), part.data_ptr(), grads.data_ptr(), grads.stride(0), self.off,
-                           G, B, D, H, W, self.cin, self.cout, self.kt, self.stride, self.pad, padd, ns, 1.0,
-                           ptab.data_ptr(), _stream())
+            union = self.kt == 27 and self.stride == 1 and union_wgrad(x, dy, grads, self.off, G, B, D, H, W,
+                                                                       self.cin, self.cout, self.pad)
+            if not union:
+                part = torch.empty(ns * G * self.cout * self.kt * self.cin, device=x.device, dtype=torch.float32)
+                m.conv_wgrad_g(x.data_ptr(), dy.data_ptr(), part.data_ptr(), grads.data_ptr(), grads.stride(0),
+                               self.off, G, B, D, H, W, self.cin, self.cout, self.kt, self.stride, self.pad, padd, ns,
+                               1.0, ptab.data_ptr(), _stream())
         if not need_dx:
             return None
         pk, self.wt = self.wt, None
