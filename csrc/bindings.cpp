@@ -150,6 +150,12 @@ void bnr_bwd(uintptr_t t, uintptr_t dy, int dy_bf16, uintptr_t mask, uintptr_t s
 void bnr_bwd_tm(uintptr_t t, uintptr_t dy, int dy_bf16, uintptr_t mask, uintptr_t stats, uintptr_t theta, int64_t ldt,
                 int64_t off_w, int64_t off_b, uintptr_t grads, int64_t ldg, uintptr_t ws, uintptr_t coef, uintptr_t dt,
                 int G, int64_t M, int C, int eval_mode, int tmask, uintptr_t stream);
+void bnr_res_partial(uintptr_t out, uintptr_t dx1, uintptr_t dx2, uintptr_t da, uintptr_t mask, uintptr_t omask,
+                     uintptr_t t3, uintptr_t s3, uintptr_t ws3, uintptr_t td, uintptr_t sd, uintptr_t wsd, int G,
+                     int64_t M, int C, uintptr_t stream);
+void bnr_bwd_part(uintptr_t t, uintptr_t dy, uintptr_t stats, uintptr_t theta, int64_t ldt, int64_t off_w,
+                  int64_t off_b, uintptr_t grads, int64_t ldg, uintptr_t ws, uintptr_t coef, uintptr_t dt, int G,
+                  int64_t M, int C, uintptr_t stream);
 // bn.hip
 void bn_finalize(uintptr_t stats, int nPB, int BP, int Mg, int G, int C, uintptr_t theta, int64_t ldt, int64_t off_g,
                  int64_t off_b, uintptr_t bufs, int64_t ldb, int64_t off_rm, int64_t off_rv, int64_t off_nbt,
@@ -328,6 +334,8 @@ PYBIND11_MODULE(_nidt_hip, m) {
   DEF(bnr_stats);
   DEF(bnr_eval_stats);
   DEF(bnr_apply);
+  DEF(bnr_res_partial);
+  DEF(bnr_bwd_part);
   DEF(bnr_bwd_tm);
   DEF(bnr_bwd);
   DEF(bn_finalize);

@@ -149,6 +149,117 @@ __global__ __launch_bounds__(kBnrThreads) void k_bnr_partial(const uint16_t* __r
   (void)nchunk;
 }
 
+// [RESBN] the residual-stream gradient of a Bottleneck (res_grad with the [OMASK] output mask) fused with the
+// backward statistics of the BatchNorms that consume it next: the previous block's bn3 and, when that block has a
+// projection, its downsample BN.  out = (dx1 + (dx2 | da [mask > 0])) [omask > 0] is the gradient at their outputs
+// (bf16), and this pass also reduces part3 = (sum out, sum out xhat3) and partd = (sum out, sum out xhatd) per chunk
+// of kBnrChunk positions, the layout k_bnr_partial writes — so their backward runs k_bnr_bwd_fin + k_bnr_bwd_apply
+// only, without its own pass over (t, dy).  Sums of the stored (bf16-rounded) out, as the unfused path sums it.
+template <bool HAS_D>
+__global__ __launch_bounds__(kBnrThreads) void k_bnr_res_partial(
+    uint16_t* __restrict__ out, const uint16_t* __restrict__ dx1, const uint16_t* __restrict__ dx2,
+    const uint16_t* __restrict__ da, const uint16_t* __restrict__ mask, const uint16_t* __restrict__ omask,
+    const uint16_t* __restrict__ t3, const float* __restrict__ s3, float* __restrict__ part3,
+    const uint16_t* __restrict__ td, const float* __restrict__ sd, float* __restrict__ partd, int M, int C) {
+  __shared__ float sm[kBnrThreads * 25];
+  const int chunk = blockIdx.x, g = blockIdx.y, tid = threadIdx.x;
+  const int nch = C >> 3, rows = kBnrThreads / nch;
+  const int j = tid % nch, r = tid / nch;
+  const int p0 = chunk * kBnrChunk, p1 = min(M, p0 + kBnrChunk);
+  const int64_t base = (int64_t)g * M * C;
+  float a[8], b3[8], bd[8], mu3[8], rs3[8], mud[8], rsd[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    a[e] = b3[e] = bd[e] = 0.f;
+    mu3[e] = s3[((int64_t)g * C + 8 * j + e) * 2];
+    rs3[e] = s3[((int64_t)g * C + 8 * j + e) * 2 + 1];
+    if (HAS_D) {
+      mud[e] = sd[((int64_t)g * C + 8 * j + e) * 2];
+      rsd[e] = sd[((int64_t)g * C + 8 * j + e) * 2 + 1];
+    }
+  }
+  // loads of four positions are issued before their arithmetic (k_bnr_partial)
+  struct Ld {
+    uint4 x1, x2, mk, om, t3, td;
+  };
+  auto load = [&](int p) {
+    Ld v;
+    const int64_t o = base + (int64_t)p * C + 8 * j;
+    v.x1 = *reinterpret_cast<const uint4*>(dx1 + o);
+    v.x2 = *reinterpret_cast<const uint4*>((dx2 ? dx2 : da) + o);
+    if (!dx2 && mask) v.mk = *reinterpret_cast<const uint4*>(mask + o);
+    v.om = *reinterpret_cast<const uint4*>(omask + o);
+    v.t3 = *reinterpret_cast<const uint4*>(t3 + o);
+    if (HAS_D) v.td = *reinterpret_cast<const uint4*>(td + o);
+    return v;
+  };
+  auto step = [&](int p, const Ld& v) {
+    const int64_t o = base + (int64_t)p * C + 8 * j;
+    float x1[8], x2[8], om[8], f3[8], fd[8];
+    bnr_unpack8(v.x1, x1);
+    bnr_unpack8(v.x2, x2);
+    if (!dx2 && mask) {
+      float mk[8];
+      bnr_unpack8(v.mk, mk);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) x2[e] = mk[e] > 0.f ? x2[e] : 0.f;
+    }
+    bnr_unpack8(v.om, om);
+    bnr_unpack8(v.t3, f3);
+    if (HAS_D) bnr_unpack8(v.td, fd);
+    uint32_t w[4];
+#pragma unroll
+    for (int e = 0; e < 8; e += 2) {
+      const float v0 = om[e] > 0.f ? x1[e] + x2[e] : 0.f, v1 = om[e + 1] > 0.f ? x1[e + 1] + x2[e + 1] : 0.f;
+      w[e >> 1] = pack_bf16x2(v0, v1);
+    }
+    *reinterpret_cast<uint4*>(out + o) = make_uint4(w[0], w[1], w[2], w[3]);
+    float d[8];
+    bnr_unpack8(make_uint4(w[0], w[1], w[2], w[3]), d);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      a[e] += d[e];
+      b3[e] = fmaf(d[e], (f3[e] - mu3[e]) * rs3[e], b3[e]);
+      if (HAS_D) bd[e] = fmaf(d[e], (fd[e] - mud[e]) * rsd[e], bd[e]);
+    }
+  };
+  if (r < rows) {
+    int p = p0 + r;
+    for (; p + 3 * rows < p1; p += 4 * rows) {
+      const Ld v0 = load(p), v1 = load(p + rows), v2 = load(p + 2 * rows), v3 = load(p + 3 * rows);
+      step(p, v0);
+      step(p + rows, v1);
+      step(p + 2 * rows, v2);
+      step(p + 3 * rows, v3);
+    }
+    for (; p < p1; p += rows) step(p, load(p));
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    sm[tid * 25 + e] = a[e];
+    sm[tid * 25 + 8 + e] = b3[e];
+    sm[tid * 25 + 16 + e] = bd[e];
+  }
+  __syncthreads();
+  for (int c = tid; c < C; c += kBnrThreads) {
+    const int jj = c >> 3, e = c & 7;
+    float sa = 0.f, sb = 0.f, sdd = 0.f;
+    for (int rr = 0; rr < rows; ++rr) {
+      sa += sm[(rr * nch + jj) * 25 + e];
+      sb += sm[(rr * nch + jj) * 25 + 8 + e];
+      sdd += sm[(rr * nch + jj) * 25 + 16 + e];
+    }
+    float* o3 = part3 + (((int64_t)chunk * gridDim.y + g) * C + c) * 2;
+    o3[0] = sa;
+    o3[1] = sb;
+    if (HAS_D) {
+      float* od = partd + (((int64_t)chunk * gridDim.y + g) * C + c) * 2;
+      od[0] = sa;
+      od[1] = sdd;
+    }
+  }
+}
+
 // per (client, channel): stats = (mean, rstd); running stats rows updated (train mode)
 __global__ void k_bnr_finalize(const float* __restrict__ part, int nchunk, int G, int C, int M, float eps, float mom,
                                float* __restrict__ stats, float* bufs, int64_t ldb, int64_t off_rm, int64_t off_rv,
@@ -417,6 +528,46 @@ void bnr_bwd(uintptr_t t, uintptr_t dy, int dy_bf16, uintptr_t mask, uintptr_t s
              int G, int64_t M, int C, int eval_mode, uintptr_t stream) {
   bnr_bwd_tm(t, dy, dy_bf16, mask, stats, theta, ldt, off_w, off_b, grads, ldg, ws, coef, dt, G, M, C, eval_mode, 0,
              stream);
+}
+
+// [RESBN] host side: out and the chunk partials of bn3 (ws3) and, with td, of the downsample BN (wsd); flags bit 1:
+// da bf16 (required: the engines keep the stream in bf16)
+void bnr_res_partial(uintptr_t out, uintptr_t dx1, uintptr_t dx2, uintptr_t da, uintptr_t mask, uintptr_t omask,
+                     uintptr_t t3, uintptr_t s3, uintptr_t ws3, uintptr_t td, uintptr_t sd, uintptr_t wsd, int G,
+                     int64_t M, int C, uintptr_t stream) {
+  bnr_check(G, M, C, "bnr_res_partial");
+  NIDT_REQUIRE(C / 8 <= kBnrThreads && omask && t3 && s3 && ws3 && (dx2 || da) && (!td || (sd && wsd)),
+               "bnr_res_partial: operands");
+  hipStream_t s = as_stream(stream);
+  const dim3 grid(bnr_nchunk(M), G);
+  if (td)
+    hipLaunchKernelGGL(k_bnr_res_partial<true>, grid, dim3(kBnrThreads), 0, s, ptr<uint16_t>(out),
+                       ptr<const uint16_t>(dx1), ptr<const uint16_t>(dx2), ptr<const uint16_t>(da),
+                       ptr<const uint16_t>(mask), ptr<const uint16_t>(omask), ptr<const uint16_t>(t3),
+                       ptr<const float>(s3), ptr<float>(ws3), ptr<const uint16_t>(td), ptr<const float>(sd),
+                       ptr<float>(wsd), (int)M, C);
+  else
+    hipLaunchKernelGGL(k_bnr_res_partial<false>, grid, dim3(kBnrThreads), 0, s, ptr<uint16_t>(out),
+                       ptr<const uint16_t>(dx1), ptr<const uint16_t>(dx2), ptr<const uint16_t>(da),
+                       ptr<const uint16_t>(mask), ptr<const uint16_t>(omask), ptr<const uint16_t>(t3),
+                       ptr<const float>(s3), ptr<float>(ws3), nullptr, nullptr, nullptr, (int)M, C);
+  NIDT_CHECK(hipGetLastError());
+}
+
+// backward from precomputed chunk partials ws [nchunk][G][C][2] of (sum dy', sum dy' xhat) (k_bnr_res_partial):
+// dgamma / dbeta rows and dt, no statistics pass; dy bf16, no mask (the partials' producer applied it)
+void bnr_bwd_part(uintptr_t t, uintptr_t dy, uintptr_t stats, uintptr_t theta, int64_t ldt, int64_t off_w,
+                  int64_t off_b, uintptr_t grads, int64_t ldg, uintptr_t ws, uintptr_t coef, uintptr_t dt, int G,
+                  int64_t M, int C, uintptr_t stream) {
+  bnr_check(G, M, C, "bnr_bwd_part");
+  hipStream_t s = as_stream(stream);
+  hipLaunchKernelGGL(k_bnr_bwd_fin, dim3(G), dim3(256), 0, s, ptr<const float>(ws), bnr_nchunk(M), G, C, (int)M,
+                     ptr<float>(grads), ldg, off_w, off_b, ptr<float>(coef));
+  NIDT_CHECK(hipGetLastError());
+  hipLaunchKernelGGL((k_bnr_bwd_apply<true, false>), bnr_grid(G, M, C), dim3(256), 0, s, ptr<const uint16_t>(t),
+                     ptr<const void>(dy), nullptr, ptr<const float>(stats), ptr<const float>(coef),
+                     ptr<const float>(theta), ldt, off_w, ptr<uint16_t>(dt), M, C, (int64_t)0);
+  NIDT_CHECK(hipGetLastError());
 }
 
 }  // namespace nidt

@@ -374,7 +374,7 @@ class GBN3:
         assert N % G == 0
         return y, stats
 
-    def bwd(self, dy, mask, t, stats, theta, grads, G, eval_mode=False, tmask=False):
+    def bwd(self, dy, mask, t, stats, theta, grads, G, eval_mode=False, tmask=False, part=None):
         """``tmask`` (HIP): the forward was ``fwd(relu=True)`` without residual and ``mask`` is its output; the kernels
         recompute that ReLU mask from ``t`` bit-exactly instead of reading the mask tensor ([TMASK], ``bnr.hip``)."""
         if not self.hip:
@@ -397,9 +397,15 @@ class GBN3:
         m, st = ops.ext(), _stream()
         M = t.numel() // (self.C * G)
         dy = dy.contiguous()
-        ws = torch.empty(m.bnr_workspace(G, M, self.C), device=t.device, dtype=torch.float32)
         coef = torch.empty(G, self.C, 2, device=t.device, dtype=torch.float32)
         dt = torch.empty_like(t)
+        if part is not None:  # [RESBN] statistics from the residual-gradient pass that produced dy
+            assert mask is None and not eval_mode and dy.dtype == torch.bfloat16
+            m.bnr_bwd_part(t.data_ptr(), dy.data_ptr(), stats.data_ptr(), theta.data_ptr(), theta.stride(0),
+                           self.off_w, self.off_b, grads.data_ptr(), grads.stride(0), part.data_ptr(), coef.data_ptr(),
+                           dt.data_ptr(), G, M, self.C, st)
+            return dt
+        ws = torch.empty(m.bnr_workspace(G, M, self.C), device=t.device, dtype=torch.float32)
         tm = bool(tmask) and mask is not None and dy.dtype == torch.bfloat16
         m.bnr_bwd_tm(t.data_ptr(), dy.data_ptr(), int(dy.dtype == torch.bfloat16),
                      mask.data_ptr() if (mask is not None and not tm) else 0, stats.data_ptr(), theta.data_ptr(),
@@ -613,11 +619,15 @@ class GroupedResNet3D:
         omask_on = self.hip and os.environ.get("NIDT_R3D_OMASK", "1") != "0"
         # [TMASK] bn1 / bn2 backward recompute their ReLU mask from t (no h1 / h2 reads); NIDT_R3D_TMASK=0: A/B
         tm = self.hip and os.environ.get("NIDT_R3D_TMASK", "1") != "0"
+        # [RESBN] with [OMASK], the residual-gradient pass also reduces the backward statistics of the previous block's
+        # bn3 (and downsample BN): their backward skips its own pass over (t, dy); NIDT_R3D_RESBN=0: A/B
+        resbn = omask_on and os.environ.get("NIDT_R3D_RESBN", "1") != "0"
+        pre3 = pred = None
         da_masked = False
         for bi, (blk, sv) in enumerate(zip(reversed(self.blocks), reversed(saved))):
             xin, t1, s1, h1, t2, s2, h2, t3, s3, td, sd, a = sv
             amask = None if da_masked else a
-            dt3 = blk["n3"].bwd(da, amask, t3, s3, theta, grads, G)
+            dt3 = blk["n3"].bwd(da, amask, t3, s3, theta, grads, G, part=pre3)
             dh2 = blk["c3"].bwd(dt3, h2, theta, grads, G, ws=ws)
             dt2 = blk["n2"].bwd(dh2, h2, t2, s2, theta, grads, G, tmask=tm)
             dh1 = blk["c2"].bwd(dt2, h1, theta, grads, G, ws=ws)
@@ -625,7 +635,7 @@ class GroupedResNet3D:
             dx1 = blk["c1"].bwd(dt1, xin, theta, grads, G, ws=ws)
             dx2 = None
             if "cd" in blk:
-                dtd = blk["nd"].bwd(da, amask, td, sd, theta, grads, G)
+                dtd = blk["nd"].bwd(da, amask, td, sd, theta, grads, G, part=pred)
                 dx2 = blk["cd"].bwd(dtd, xin, theta, grads, G, ws=ws)
             half = dx2 is not None and blk["cd"].stride == 2  # 1x1x1 stride-2 projection: even-voxel gradient
             if self.hip:
@@ -633,7 +643,23 @@ class GroupedResNet3D:
                 # the input of the network's first block is the stem output (its backward applies its own masks)
                 om = xin if (omask_on and bi + 1 < len(self.blocks)) else None
                 omp = om.data_ptr() if om is not None else 0
-                if half:
+                pre3 = pred = None
+                if resbn and om is not None and not half:
+                    psv = saved[len(saved) - 2 - bi]  # the previous block (next in this backward walk)
+                    t3p, s3p, tdp, sdp = psv[7], psv[8], psv[9], psv[10]
+                    Cc = out.shape[-1]
+                    Mm = out.numel() // (Cc * G)
+                    mm = ops.ext()
+                    pre3 = torch.empty(mm.bnr_workspace(G, Mm, Cc), device=out.device, dtype=torch.float32)
+                    pred = torch.empty_like(pre3) if tdp is not None else None
+                    mm.bnr_res_partial(out.data_ptr(), dx1.data_ptr(), dx2.data_ptr() if dx2 is not None else 0,
+                                       0 if dx2 is not None else da.data_ptr(),
+                                       0 if (dx2 is not None or amask is None) else amask.data_ptr(), omp,
+                                       t3p.data_ptr(), s3p.data_ptr(), pre3.data_ptr(),
+                                       tdp.data_ptr() if tdp is not None else 0,
+                                       sdp.data_ptr() if tdp is not None else 0,
+                                       pred.data_ptr() if pred is not None else 0, G, Mm, Cc, _stream())
+                elif half:
                     Nn, Dd, Hh, Ww, Cc = dx1.shape
                     ops.ext().res_grad_s2_om(out.data_ptr(), dx1.data_ptr(), dx2.data_ptr(), omp, Nn, Dd, Hh, Ww, Cc,
                                              1, _stream())

@@ -360,12 +360,13 @@ def test_resnet3d_lockstep_step_matches_per_client_autograd():
     assert lg.shape == (G * B, 1) and torch.isfinite(lg).all()
 
 
-@pytest.mark.parametrize("env", ["NIDT_R3D_OMASK", "NIDT_R3D_TMASK"])
+@pytest.mark.parametrize("env", ["NIDT_R3D_OMASK", "NIDT_R3D_TMASK", "NIDT_R3D_RESBN"])
 def test_resnet3d_omask_bit_identical(monkeypatch, env):
     """[OMASK]: the residual-gradient kernel applying the previous block's ReLU mask (BN3 / downsample-BN backward and
     identity shortcuts then read no mask) gives bit-identical gradients, losses and running statistics to masking in
     the BN backward — identity and projection blocks, stride-2 projections.  [TMASK]: bn1 / bn2 backward recomputing
-    their ReLU mask from the pre-BN tensor, likewise bit-identical to reading the stored output."""
+    their ReLU mask from the pre-BN tensor, likewise bit-identical to reading the stored output.  [RESBN]: the
+    residual-gradient pass reducing the next bn3 / downsample-BN backward statistics, bit-identical to their own pass."""
     from neuroimagedisttraining_amd.engine.executor import padded_rows
     from neuroimagedisttraining_amd.engine.resnet3d_hip import ResNet3DHipEngine
     from neuroimagedisttraining_amd.models.resnet3d import Bottleneck, ResNet3D
