@@ -159,6 +159,11 @@ __global__ __launch_bounds__(256) void k_seg_ties(const Tile* __restrict__ tiles
 
 // Apply the selection: thread = one 32-bit mask word of the tile; ties are taken in index order (block scan of the
 // per-word tie counts, running base across the tile, base of the tile = ties of the segment's earlier tiles).
+// [COAL] the keys are computed lane-contiguous: wave w of the block owns words w0 + 64 w .. + 63 (2048 elements);
+// in pass j its lanes read elements 64 j + lane of that range (256 contiguous bytes per load instead of a 128-B
+// stride per lane) and two ballots give words 2 j and 2 j + 1, which lanes 2 j / 2 j + 1 keep — each thread ends
+// with the (gt, eq) bits of its own word, as before.  The mask words are fetched once per lane and shuffled.
+// (config 5's sparse update selection: 5.3 ms per call at 1.1 TB/s, profiles/r6_config5_steady.txt)
 template <int MODE>
 __global__ __launch_bounds__(256) void k_seg_apply(const Tile* __restrict__ tiles, const int* __restrict__ tile_first,
                                                    const float* __restrict__ v, int64_t ldv,
@@ -172,28 +177,40 @@ __global__ __launch_bounds__(256) void k_seg_apply(const Tile* __restrict__ tile
   const uint32_t T = state[sid * 4 + 3];
   const int krem = (int)state[sid * 4 + 2];
   if (krem == 0) return;
-  int prior = 0;
-  for (int j = tile_first[blockIdx.x]; j < (int)blockIdx.x; ++j) prior += ties[j];
+  (void)tile_first;
+  const int prior = ties[blockIdx.x];  // ties of the segment's earlier tiles (k_seg_ties_scan)
   int quota = krem - prior;  // ties this tile may still take
   const uint32_t cid = cids ? (uint32_t)cids[t.row] : (uint32_t)t.row;
   const float* vr = v + (int64_t)t.row * ldv;
   uint32_t* br = bits + (int64_t)t.row * mstride;
   int wb, we;
   tile_words(t, wb, we);
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   if (threadIdx.x == 0) base_s = 0;
   for (int w0 = wb; w0 < we; w0 += blockDim.x) {
     const int w = w0 + threadIdx.x;
+    const uint32_t word = w < we ? br[w] : 0u;  // this thread's mask word (read before any write of this pass)
+    const int wbase = w0 + 64 * wv;             // first word of this wave
     uint32_t gt = 0, eq = 0;
-    if (w < we) {
-      const uint32_t rm = word_range_mask(w, t.begin, t.end);
-      const uint32_t word = br[w];
+    if (wbase < we) {  // wave-uniform
       for (int j = 0; j < 32; ++j) {
-        if (!((rm >> j) & 1u)) continue;
-        const int e = (w << 5) + j;
-        const uint32_t key = sel_key<MODE>(MODE == kRegrowRand ? 0.f : vr[e], (word >> j) & 1u, seed, cid,
-                                           (uint32_t)e);
-        if (key > T) gt |= 1u << j;
-        else if (key == T && key != 0u) eq |= 1u << j;
+        const int e = (wbase << 5) + 64 * j + lane;
+        const uint32_t wj = __shfl(word, 2 * j + (lane >> 5), 64);
+        bool g = false, q = false;
+        if (e >= t.begin && e < t.end) {
+          const uint32_t key = sel_key<MODE>(MODE == kRegrowRand ? 0.f : vr[e], (wj >> (lane & 31)) & 1u, seed, cid,
+                                             (uint32_t)e);
+          g = key > T;
+          q = key == T && key != 0u;
+        }
+        const uint64_t bg = __ballot(g), bq = __ballot(q);
+        if (lane == 2 * j) {
+          gt = (uint32_t)bg;
+          eq = (uint32_t)bq;
+        } else if (lane == 2 * j + 1) {
+          gt = (uint32_t)(bg >> 32);
+          eq = (uint32_t)(bq >> 32);
+        }
       }
     }
     const int my = __popc(eq);
@@ -222,6 +239,20 @@ __global__ __launch_bounds__(256) void k_seg_apply(const Tile* __restrict__ tile
     __syncthreads();
     if (threadIdx.x == 255) base_s += scan[255];
     __syncthreads();
+  }
+}
+
+// [TSCAN] per-tile tie counts -> the exclusive prefix over the segment's earlier tiles, in place: one thread per
+// segment start walks its tiles.  k_seg_apply summed ties[tile_first .. b) itself — O(tiles^2) loads per segment,
+// 5.3 ms per call for config 5's whole-row update segments (thousands of tiles each)
+__global__ void k_seg_ties_scan(const int* __restrict__ tile_first, int* __restrict__ ties, int ntiles) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= ntiles || tile_first[b] != b) return;
+  int acc = 0;
+  for (int j = b; j < ntiles && tile_first[j] == b; ++j) {
+    const int c = ties[j];
+    ties[j] = acc;
+    acc += c;
   }
 }
 
@@ -256,6 +287,8 @@ void seg_select(uintptr_t tiles, uintptr_t tile_first, int ntiles, uintptr_t v, 
     hipLaunchKernelGGL(k_seg_ties<M>, dim3(ntiles), dim3(256), 0, st, tl, ptr<const float>(v), ldv,              \
                        ptr<const uint32_t>(bits), mstride, ptr<const int>(cids), seed, S,                        \
                        ptr<const uint32_t>(state), ptr<int>(ties));                                              \
+    hipLaunchKernelGGL(k_seg_ties_scan, dim3(ceil_div(ntiles, 256)), dim3(256), 0, st, ptr<const int>(tile_first),   \
+                       ptr<int>(ties), ntiles);                                                                  \
     hipLaunchKernelGGL(k_seg_apply<M>, dim3(ntiles), dim3(256), 0, st, tl, ptr<const int>(tile_first),           \
                        ptr<const float>(v), ldv, ptr<uint32_t>(bits), mstride, ptr<const int>(cids), seed, S,    \
                        ptr<const uint32_t>(state), ptr<const int>(ties));                                        \
