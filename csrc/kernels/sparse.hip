@@ -242,17 +242,27 @@ __global__ __launch_bounds__(256) void k_seg_apply(const Tile* __restrict__ tile
   }
 }
 
-// [TSCAN] per-tile tie counts -> the exclusive prefix over the segment's earlier tiles, in place: one thread per
-// segment start walks its tiles.  k_seg_apply summed ties[tile_first .. b) itself — O(tiles^2) loads per segment,
-// 5.3 ms per call for config 5's whole-row update segments (thousands of tiles each)
+// [TSCAN] per-tile tie counts -> the exclusive prefix over the segment's earlier tiles, in place: one wave per
+// segment start walks its tiles 64 at a time (wave prefix sum + running base).  k_seg_apply summed
+// ties[tile_first .. b) itself — O(tiles^2) loads per segment, 5.3 ms per call for config 5's whole-row update
+// segments (thousands of tiles each)
 __global__ void k_seg_ties_scan(const int* __restrict__ tile_first, int* __restrict__ ties, int ntiles) {
-  const int b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= ntiles || tile_first[b] != b) return;
-  int acc = 0;
-  for (int j = b; j < ntiles && tile_first[j] == b; ++j) {
-    const int c = ties[j];
-    ties[j] = acc;
-    acc += c;
+  const int b = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (b >= ntiles || tile_first[b] != b) return;  // wave-uniform
+  int base = 0;
+  for (int j0 = b; j0 < ntiles; j0 += 64) {
+    const int j = j0 + lane;
+    const bool in = j < ntiles && tile_first[j] == b;
+    const int c = in ? ties[j] : 0;
+    int inc = c;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int u = __shfl_up(inc, o, 64);
+      if (lane >= o) inc += u;
+    }
+    if (in) ties[j] = base + inc - c;
+    base += __shfl(inc, 63, 64);
+    if (!__all(in)) break;  // the segment ended inside this group of 64
   }
 }
 
@@ -287,7 +297,7 @@ void seg_select(uintptr_t tiles, uintptr_t tile_first, int ntiles, uintptr_t v, 
     hipLaunchKernelGGL(k_seg_ties<M>, dim3(ntiles), dim3(256), 0, st, tl, ptr<const float>(v), ldv,              \
                        ptr<const uint32_t>(bits), mstride, ptr<const int>(cids), seed, S,                        \
                        ptr<const uint32_t>(state), ptr<int>(ties));                                              \
-    hipLaunchKernelGGL(k_seg_ties_scan, dim3(ceil_div(ntiles, 256)), dim3(256), 0, st, ptr<const int>(tile_first),   \
+    hipLaunchKernelGGL(k_seg_ties_scan, dim3(ceil_div(ntiles, 4)), dim3(256), 0, st, ptr<const int>(tile_first),     \
                        ptr<int>(ties), ntiles);                                                                  \
     hipLaunchKernelGGL(k_seg_apply<M>, dim3(ntiles), dim3(256), 0, st, tl, ptr<const int>(tile_first),           \
                        ptr<const float>(v), ldv, ptr<uint32_t>(bits), mstride, ptr<const int>(cids), seed, S,    \

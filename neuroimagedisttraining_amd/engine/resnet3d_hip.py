@@ -102,10 +102,11 @@ def gemm_1x1(x, w, out, G):
     return True
 
 
-def slab_conv(x_ptr, w_ptr, y_ptr, G, B, D, H, W, Cin, Cout, pad, device):
+def slab_conv(x_ptr, w_ptr, y_ptr, G, B, D, H, W, Cin, Cout, pad, device, bias=0, stats=0):
     """3x3x3 stride-1 conv through the kd-slab union kernel (``k_conv_fwd_slab``) when the shape is eligible (its
     band unions fit the kernel's LDS); returns False otherwise.  The union table is a function of the shape only and
-    is built once per (B, D, H, W, pad)."""
+    is built once per (B, D, H, W, pad).  ``stats``: [G, nPB, Cout, 2] per-256-position-block BatchNorm statistics
+    of the output from the epilogue (needs a ``bias`` [G, Cout], zeros for the bias-free ResNet convs)."""
     m = ops.ext()
     if not m.conv3d_fwd_slab_pick(G, B, D, H, W, Cin, Cout, pad):
         return False
@@ -115,12 +116,27 @@ def slab_conv(x_ptr, w_ptr, y_ptr, G, B, D, H, W, Cin, Cout, pad, device):
         tab = torch.empty(m.conv3d_fwd_slab_table_size(B, D, H, W, pad), device=device, dtype=torch.int32)
         m.conv3d_fwd_slab_table(tab.data_ptr(), B, D, H, W, pad, _stream())
         if torch.cuda.is_current_stream_capturing():  # built inside a capture: that graph's memory, not cached
-            m.conv3d_fwd_slab(x_ptr, w_ptr, 0, 0, y_ptr, 0, G, B, D, H, W, Cin, Cout, pad, tab.data_ptr(), _stream())
+            m.conv3d_fwd_slab(x_ptr, w_ptr, bias, 0, y_ptr, stats, G, B, D, H, W, Cin, Cout, pad, tab.data_ptr(),
+                              _stream())
             return True
         torch.cuda.current_stream().synchronize()  # shared with launches on other streams from now on
         _SLAB_TABS[key] = tab
-    m.conv3d_fwd_slab(x_ptr, w_ptr, 0, 0, y_ptr, 0, G, B, D, H, W, Cin, Cout, pad, tab.data_ptr(), _stream())
+    m.conv3d_fwd_slab(x_ptr, w_ptr, bias, 0, y_ptr, stats, G, B, D, H, W, Cin, Cout, pad, tab.data_ptr(), _stream())
     return True
+
+
+# [SLAB-STATS] the BatchNorm after a slab-kernel 3x3x3 conv takes its training statistics from the conv epilogue
+# (per-block mean / M2, merged by bn.hip's finalize) instead of a k_bnr_partial pass; NIDT_R3D_SLAB_STATS=0: A/B
+_SLAB_STATS = os.environ.get("NIDT_R3D_SLAB_STATS", "1") != "0"
+_ZERO_BIAS = {}
+
+
+def _zero_bias(G, C, device):
+    key = (G, C, str(device))
+    z = _ZERO_BIAS.get(key)
+    if z is None:
+        z = _ZERO_BIAS[key] = torch.zeros(G, C, device=device, dtype=torch.float32)
+    return z
 
 
 # 3x3x3 stride-1 weight gradients with the union-staged B operand of the AlexNet3D conv2-5 kernels (k_conv_wgrad_slab:
@@ -178,6 +194,12 @@ class GConv3:
         self.wp = self.wt = None
         self._ptabs = {}
         self._part = None  # BatchNorm partials of the last forward output (fwd(stats=True) on the GEMM path)
+        self._bstats = None  # ... on the slab path: (per-block stats, nPB, block size, positions per client)
+
+    def take_bstats(self):
+        """The per-block BatchNorm statistics of the last ``fwd(stats=True)`` output on the slab path, or None."""
+        p, self._bstats = self._bstats, None
+        return p
 
     def take_part(self):
         """The BatchNorm chunk partials of the last ``fwd(stats=True)`` output, or None (then the BN computes its
@@ -208,6 +230,7 @@ class GConv3:
 
     def fwd(self, x, theta, G, train=False, packed=False, stats=False):
         self._part = None
+        self._bstats = None
         N, D, H, W, C = x.shape
         if not self.hip:  # CPU twin (its BN output may be a permuted view)
             return self._torch_fwd(x, theta[:, self.off:self.off + self.numel], G)
@@ -226,9 +249,17 @@ class GConv3:
                 return y
         if self.kt == 1 and self.stride == 1 and _BLAS_1X1 and gemm_1x1(x, wp, y, G):
             return y
-        if self.kt == 27 and self.stride == 1 and slab_conv(x.data_ptr(), wp.data_ptr(), y.data_ptr(), G, N // G, D,
-                                                            H, W, self.cin, self.cout, self.pad, x.device):
-            return y
+        if self.kt == 27 and self.stride == 1:
+            bst, bias = None, 0
+            if stats and _SLAB_STATS:
+                Mg = (N // G) * Do * Ho * Wo
+                npb = (Mg + 255) // 256
+                bst = (torch.empty(G, npb, self.cout, 2, device=x.device, dtype=torch.float32), npb, 256, Mg)
+                bias = _zero_bias(G, self.cout, x.device).data_ptr()
+            if slab_conv(x.data_ptr(), wp.data_ptr(), y.data_ptr(), G, N // G, D, H, W, self.cin, self.cout, self.pad,
+                         x.device, bias=bias, stats=bst[0].data_ptr() if bst is not None else 0):
+                self._bstats = bst
+                return y
         conv_fwd(x.data_ptr(), wp.data_ptr(), y.data_ptr(), G, N // G, D, H, W, self.cin, self.cout,
                  self.kt, self.stride, self.pad, self.pad if self.kt == 27 else 0, x.device)
         return y
@@ -346,7 +377,7 @@ class GBN3:
             y = torch.relu(y)
         return y.to(t.dtype), torch.stack([mean, rstd], -1)
 
-    def fwd(self, t, theta, bufs, G, train, res=None, relu=False, part=None):
+    def fwd(self, t, theta, bufs, G, train, res=None, relu=False, part=None, bstats=None):
         """``part``: (chunk partials [n][G][C][2], n) of ``t`` computed by the producing GEMM's epilogue (training
         mode): only the finalize runs, no statistics pass over ``t``."""
         if not self.hip:
@@ -355,7 +386,16 @@ class GBN3:
         N = t.shape[0]
         M = t.numel() // (self.C * G)
         stats = torch.empty(G, self.C, 2, device=t.device, dtype=torch.float32)
-        if train and part is not None:
+        if train and bstats is not None and bufs is not None and self.off_nbt >= 0:
+            # [SLAB-STATS] per-block (mean, M2) of the conv epilogue, merged with the running-stat update
+            bst, npb, bp, Mg = bstats
+            assert Mg == M
+            co = torch.empty(4, G * self.C, device=t.device, dtype=torch.float32)  # scale, shift, mean, invstd
+            m.bn_finalize(bst.data_ptr(), npb, bp, Mg, G, self.C, theta.data_ptr(), theta.stride(0), self.off_w,
+                          self.off_b, bufs.data_ptr(), bufs.stride(0), self.off_rm, self.off_rv, self.off_nbt, BN_MOM,
+                          BN_EPS, co[0].data_ptr(), co[1].data_ptr(), co[2].data_ptr(), co[3].data_ptr(), 1, st)
+            stats.copy_(co[2:4].t().reshape(G, self.C, 2))
+        elif train and part is not None:
             m.bnr_finalize_part(part[0].data_ptr(), part[1], G, M, self.C, BN_EPS, BN_MOM, stats.data_ptr(),
                                 bufs.data_ptr() if bufs is not None else 0, bufs.stride(0) if bufs is not None else 0,
                                 self.off_rm, self.off_rv, self.off_nbt, st)
@@ -569,8 +609,8 @@ class GroupedResNet3D:
             # the 1x1x1 GEMMs hand their outputs' BatchNorm partials to the next BN (training mode)
             t1 = blk["c1"].fwd(xin, theta, G, train, packed, stats=train)
             h1, s1 = blk["n1"].fwd(t1, theta, bufs, G, train, relu=True, part=blk["c1"].take_part())
-            t2 = blk["c2"].fwd(h1, theta, G, train, packed)
-            h2, s2 = blk["n2"].fwd(t2, theta, bufs, G, train, relu=True)
+            t2 = blk["c2"].fwd(h1, theta, G, train, packed, stats=train)
+            h2, s2 = blk["n2"].fwd(t2, theta, bufs, G, train, relu=True, bstats=blk["c2"].take_bstats())
             t3 = blk["c3"].fwd(h2, theta, G, train, packed, stats=train)
             p3 = blk["c3"].take_part()
             if "cd" in blk:
