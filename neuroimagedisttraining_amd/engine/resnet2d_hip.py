@@ -375,6 +375,10 @@ class WeightPacker:
         self._descs = {}
         self.last = None   # (key, theta data_ptr, row stride) of the last pack() call
         self.fresh = {}    # key -> (theta data_ptr, theta._version) whose forward images the optimizer wrote
+        # keys own their buffers (the 3-D engine's per-row-group training keys): an image stays fresh across other
+        # keys' packs; otherwise only the very next pack may reuse one
+        self.keep_other_fresh = False
+        self.fresh_hits = 0  # packs that reused optimizer-written forward images
 
     def _plan(self, G, train, key=None):
         key = (G, train) if key is None else key
@@ -457,7 +461,9 @@ class WeightPacker:
         f = self.fresh.pop(key, None)
         if f is not None and f == (theta.data_ptr(), theta._version) and not torch.cuda.is_current_stream_capturing():
             nplain = nplain1 = 0
-        self.fresh.clear()  # an image is only ever reused by the very next pack
+            self.fresh_hits += 1
+        if not self.keep_other_fresh:
+            self.fresh.clear()  # an image is only ever reused by the very next pack
         self.last = (key, theta.data_ptr(), theta.stride(0)) if train else None
         if side is not None and ntrans:  # forward images here, dgrad transposes on the side stream (caller joins)
             if nplain or nplain1:

@@ -498,6 +498,7 @@ class GroupedResNet3D:
             from .resnet2d_hip import WeightPacker
             self.packer = WeightPacker([b[k] for b in self.blocks for k in ("c1", "c2", "c3", "cd") if k in b],
                                        self.device)
+            self.packer.keep_other_fresh = _PACK_FUSE_G
         else:
             self.packer = None
 
@@ -601,7 +602,10 @@ class GroupedResNet3D:
         packed = self.packer is not None
         N = x8.shape[0] if idx is None else idx.numel()
         if packed:  # every bottleneck layer's MFMA images for this step, two launches
-            self.packer.pack(theta, G, train, key=(G, N // G, train))
+            # [PACK-FUSE-G] training images per row group (keyed by the rows' address): the runner's step-major plan
+            # interleaves the row groups, and the optimizer of a group writes that group's next-step images
+            key = (G, N // G, train, theta.data_ptr()) if (train and _PACK_FUSE_G) else (G, N // G, train)
+            self.packer.pack(theta, G, train, key=key)
         a, stem = self._stem(x8, theta, bufs, G, train, idx)
         saved = []
         for blk in self.blocks:
@@ -731,12 +735,20 @@ class GroupedResNet3D:
         return losses.detach()
 
 
+# [PACK-FUSE-G] the optimizer step writes the next step's forward weight images (``optim.hip`` ``local_opt_pack``,
+# the 2-D engine's fusion) with one image buffer per training row group (8 x 5.9 GB at config 5: the HBM is sized
+# for it); NIDT_R3D_PACK_FUSE=0: every step packs from theta (A/B)
+_PACK_FUSE_G = os.environ.get("NIDT_R3D_PACK_FUSE", "1") != "0"
+
+
 class ResNet3DHipEngine:
     """Engine API (train_step / eval_logits / local_opt / saliency_acc) of the client-batched 3D ResNet on uint8
     ABCD-shape volumes ``[N, D, H, W]`` (labels {0, 1}, BCE head with one logit)."""
     sample_fields = ("x8", "labels")
 
     supports_graphs = False  # launches here are few and large (seconds per step at config-5 shapes)
+    fused_pack = _PACK_FUSE_G   # runner: local_opt(pack_next=True) where the same rows train next at this shape
+    images_per_group = True     # ... also when several row groups share the launch shape (separate image buffers)
 
     @property
     def input_shape(self):
@@ -786,7 +798,19 @@ class ResNet3DHipEngine:
                 self._opt.m = ops.ext()
         return self._opt
 
-    def local_opt(self, theta, grads, mom_buf, spec, lr, wd, momentum, max_norm, lr_dev=None, keep_grad=False):
+    def local_opt(self, theta, grads, mom_buf, spec, lr, wd, momentum, max_norm, lr_dev=None, keep_grad=False,
+                  pack_next=False):
+        pk = self.net.packer
+        if (pack_next and _PACK_FUSE_G and pk is not None and pk.last is not None
+                and pk.last[1:] == (theta.data_ptr(), theta.stride(0)) and pk.last[0][0] == theta.shape[0]):
+            from .executor import HipEngine
+            key = pk.last[0]
+            HipEngine.local_opt_pack(self._delegate(), theta, grads, mom_buf, spec, lr, wd, momentum, max_norm,
+                                     pk.fused_plan(key, theta.shape[1]), lr_dev=lr_dev, keep_grad=keep_grad)
+            pk.fresh[key] = (theta.data_ptr(), theta._version)
+            return
+        if pk is not None and pk.last is not None:  # these rows change without their images
+            pk.fresh.pop(pk.last[0], None)
         self._opt_cls().local_opt(self._delegate(), theta, grads, mom_buf, spec, lr, wd, momentum, max_norm,
                                   lr_dev=lr_dev, keep_grad=keep_grad)
 

@@ -570,7 +570,8 @@ class FLRunner:
     def _pack_next(self, plan):
         """Per plan entry: may its optimizer step write the next step's packed weight images (engines with
         ``fused_pack``)?  Only when the same rows train again next in this epoch at the same launch shape and no other
-        row group shares that shape (groups of one shape share the image buffer)."""
+        row group shares that shape (groups of one shape share the image buffer), unless the engine keeps images per
+        row group (``images_per_group``)."""
         if not getattr(self.e, "fused_pack", False):
             return None
         groups = {}
@@ -580,7 +581,8 @@ class FLRunner:
         for i, it in enumerate(plan):
             j = last.get(it[0])
             if j is not None:
-                out[j] = plan[j][6] == it[6] and plan[j][1] == it[1] and len(groups[(it[5], it[6])]) == 1
+                out[j] = (plan[j][6] == it[6] and plan[j][1] == it[1]
+                          and (len(groups[(it[5], it[6])]) == 1 or getattr(self.e, "images_per_group", False)))
             last[it[0]] = i
         return out
 

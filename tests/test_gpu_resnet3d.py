@@ -397,6 +397,41 @@ def test_resnet3d_omask_bit_identical(monkeypatch, env):
     assert float(g0.abs().sum()) > 0 and torch.equal(g0, g1)
 
 
+def test_resnet3d_pack_fuse_per_group_bit_identical(monkeypatch):
+    """[PACK-FUSE-G]: FedAvg rounds through the runner with two row groups of one launch shape (step-major plan: the
+    groups' steps interleave), the optimizer writing each group's next-step weight images into that group's buffer,
+    give bit-identical client rows and global model to packing every step from theta."""
+    import numpy as np
+    from neuroimagedisttraining_amd.engine import resnet3d_hip as R3
+    from neuroimagedisttraining_amd.engine.executor import ClientSplit, FLConfig, FLRunner
+    from neuroimagedisttraining_amd.models.resnet3d import Bottleneck, ResNet3D
+    from neuroimagedisttraining_amd.parallel import runtime as rt
+    dev = _dev()
+    torch.manual_seed(5)
+    nc, ntr, nte = 4, 8, 2
+    vol = torch.randint(0, 256, (nc * (ntr + nte), 40, 44, 40), dtype=torch.uint8, device=dev)
+    lab = torch.randint(0, 2, (nc * (ntr + nte),), device=dev).float()
+    splits = [ClientSplit(np.arange(c * 10, c * 10 + ntr), np.arange(c * 10 + ntr, c * 10 + 10)) for c in range(nc)]
+    model = ResNet3D(Bottleneck, [1, 1, 1, 1], 1)
+    out = []
+    for fuse in (False, True):
+        monkeypatch.setattr(R3, "_PACK_FUSE_G", fuse)
+        monkeypatch.setattr(R3.ResNet3DHipEngine, "fused_pack", fuse)
+        eng = R3.ResNet3DHipEngine(model, vol, lab, dev)
+        info = rt.DistInfo(0, 1, 0, torch.device(dev), "none")
+        r = FLRunner(eng, splits, FLConfig(comm_round=2, epochs=1, batch_size=2, lr=0.01, seed=3, frac=1.0, group=2),
+                     info, model)
+        for k in range(2):
+            r.run_round(k)
+        torch.cuda.synchronize()
+        if fuse:
+            assert any(len(k) == 4 for k in eng.net.packer._plans), "no per-group image buffer was used"
+            assert eng.net.packer.fresh_hits > 0, "no step reused optimizer-written images"
+        out.append((r.theta.clone(), r.w_global.clone()))
+    (t0, w0), (t1, w1) = out
+    assert torch.equal(t0, t1) and torch.equal(w0, w1)
+
+
 @pytest.mark.parametrize("G,B,dims", [(2, 1, (121, 145, 121)), (2, 2, (21, 26, 22)), (3, 1, (9, 128, 13)),
                                         (2, 2, (15, 20, 10))])
 def test_stem_hip_fwd_bwd_match_torch(G, B, dims):
