@@ -2642,7 +2642,8 @@ __global__ __launch_bounds__(192 * NCH, 2) void k_conv_wgrad_tri(ConvWgTriArgs a
 // 96 per 18 KB (k_conv_wgrad_tri, which the PMC shows waiting on those transfers).  Wave (kh, j) = (wid / 4,
 // wid % 4) owns ci tile j of taps (kh, 0..2) for all four co tiles: X row of tap (kh, kw) = idx(p) + kh Wp + kw.
 // Output: fp32 slabs per split (k_wgrad_reduce finishes), as k_conv_wgrad_tri.
-template <int U, bool PADDED>
+// [ADMA] as k_conv_wgrad_tri: the stage DMA from inline asm, the step-table loads issued before it, the builtin wait
+template <int U, bool PADDED, bool ADMA = false>
 __global__ __launch_bounds__(768, 1) void k_conv_wgrad_slab(ConvWgTriArgs a) {
   constexpr int NW = 12, XG = U * kWdRow, BUFE = XG + kWdGroup, ST = WtTab<U>::kST;
   constexpr int XP = U / 8, XPW = (XP + NW - 1) / NW;   // union pieces (8 rows each) per wave
@@ -2688,20 +2689,25 @@ __global__ __launch_bounds__(768, 1) void k_conv_wgrad_slab(ConvWgTriArgs a) {
       DST[k_] = nidt_raw_buffer_load_i32(rt, ((S) * ST + 2 * U + 32 * (k_ >> 1) + ((k_ & 1) ? rr1 : rr0)) * 4, \
                                          0, 0);                                                               \
   }
-#define WS_ISSUE(S, BUFI)                                                                                     \
+  auto ws_dma = [](i32x4_t r, int off, uint16_t* dst) {
+    if constexpr (ADMA) blds16_asm(r, off, dst);
+    else blds16(r, off, dst);
+  };
+#define WS_ISSUE_R(S, BUFI, TR)                                                                               \
   {                                                                                                           \
     uint16_t* sX_ = smem + (BUFI) * BUFE;                                                                     \
     _Pragma("unroll") for (int i_ = 0; i_ < XPW; ++i_)                                                        \
       if (wid * XPW + i_ < XP) {                                                                              \
-        const int c_ = trow[i_].y;                                                                            \
+        const int c_ = TR[i_].y;                                                                              \
         const bool ok_ = PADDED ? ((unsigned)((c_ & 1023) - dlo) < (unsigned)a.D &&                            \
                                    (unsigned)(((c_ >> 10) & 1023) - a.pad) < (unsigned)a.H &&                 \
                                    (unsigned)((c_ >> 20) - a.pad) < (unsigned)a.W)                            \
                                 : (c_ & 1023) != 1023;                                                        \
-        blds16(rx, ok_ ? (trow[i_].x + xadd) * (2 * Cin) + xcol[i_] : kBufOOB, sX_ + (wid * XPW + i_) * 512);  \
+        ws_dma(rx, ok_ ? (TR[i_].x + xadd) * (2 * Cin) + xcol[i_] : kBufOOB, sX_ + (wid * XPW + i_) * 512);    \
       }                                                                                                       \
-    if (dload) blds16(rd, (S) * 64 * (2 * a.Cout) + dcol, sX_ + XG + (wid & 7) * 512);                       \
+    if (dload) ws_dma(rd, (S) * 64 * (2 * a.Cout) + dcol, sX_ + XG + (wid & 7) * 512);                       \
   }
+#define WS_ISSUE(S, BUFI) WS_ISSUE_R(S, BUFI, trow)
 
   f32x4 acc[3][4];
 #pragma unroll
@@ -2724,7 +2730,16 @@ __global__ __launch_bounds__(768, 1) void k_conv_wgrad_slab(ConvWgTriArgs a) {
     const int cur = st & 1;
 #pragma unroll
     for (int k = 0; k < 4; ++k) tix[k] = tixn[k];
-    if (st + 1 < nsteps) {
+    if constexpr (ADMA) {
+      i32x2_t rdma[XPW];
+#pragma unroll
+      for (int i = 0; i < XPW; ++i) rdma[i] = trow[i];
+      if (st + 1 < nsteps) {
+        if (st + 2 < nsteps) WS_FETCH_ROWS(s0 + st + 2)
+        WS_FETCH_IDX(s0 + st + 1, tixn)
+        WS_ISSUE_R(s0 + st + 1, cur ^ 1, rdma)
+      }
+    } else if (st + 1 < nsteps) {
       WS_ISSUE(s0 + st + 1, cur ^ 1)
       if (st + 2 < nsteps) WS_FETCH_ROWS(s0 + st + 2)
       WS_FETCH_IDX(s0 + st + 1, tixn)
@@ -2753,13 +2768,18 @@ __global__ __launch_bounds__(768, 1) void k_conv_wgrad_slab(ConvWgTriArgs a) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) acc[kw][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[kw], acc[kw][i], 0, 0, 0);
     }
-    // retire the next stage's LDS-DMA; the step-table loads issued after it (rows for st+2, idx for st+1) may stay
-    if (st + 2 < nsteps) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(XPW + 4) : "memory");
-    else if (st + 1 < nsteps) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if constexpr (ADMA) {
+      __builtin_amdgcn_s_waitcnt(7 << 4);  // vmcnt(0) lgkmcnt(0), visible to the waitcnt pass (k_conv_wgrad_tri)
+    } else {
+      // retire the next stage's LDS-DMA; the step-table loads issued after it (rows for st+2, idx for st+1) may stay
+      if (st + 2 < nsteps) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(XPW + 4) : "memory");
+      else if (st + 1 < nsteps) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     __syncthreads();
   }
 #undef WS_ISSUE
+#undef WS_ISSUE_R
 #undef WS_FETCH_IDX
 #undef WS_FETCH_ROWS
   const int fr = lane & 15, fq = lane >> 4;
@@ -2990,8 +3010,19 @@ void conv3d_wgrad_slab(uintptr_t x, uintptr_t dy, uintptr_t part, uintptr_t grad
   const int64_t nwg = (int64_t)d.nKT * d.nCT * nsplit * G;
   NIDT_REQUIRE(nwg < (1ll << 31), "conv3d_wgrad_slab: grid too large");
   hipStream_t s = as_stream(stream);
-  if (pad) hipLaunchKernelGGL((k_conv_wgrad_slab<152, true>), dim3((unsigned)nwg), dim3(768), 0, s, d);
-  else hipLaunchKernelGGL((k_conv_wgrad_slab<152, false>), dim3((unsigned)nwg), dim3(768), 0, s, d);
+  // [ADMA] asm-issued stage DMA (k_conv_wgrad_tri); NIDT_WGS_ADMA=0: the intrinsic (A/B)
+  static const int sadma = [] {
+    const char* e = getenv("NIDT_WGS_ADMA");
+    return e ? atoi(e) : 1;
+  }();
+  if (sadma) {
+    if (pad) hipLaunchKernelGGL((k_conv_wgrad_slab<152, true, true>), dim3((unsigned)nwg), dim3(768), 0, s, d);
+    else hipLaunchKernelGGL((k_conv_wgrad_slab<152, false, true>), dim3((unsigned)nwg), dim3(768), 0, s, d);
+  } else if (pad) {
+    hipLaunchKernelGGL((k_conv_wgrad_slab<152, true>), dim3((unsigned)nwg), dim3(768), 0, s, d);
+  } else {
+    hipLaunchKernelGGL((k_conv_wgrad_slab<152, false>), dim3((unsigned)nwg), dim3(768), 0, s, d);
+  }
   NIDT_CHECK(hipGetLastError());
   hipLaunchKernelGGL(k_wgrad_reduce, dim3(Cout, G), dim3(256), 27 * (Cin + 1) * sizeof(float), s, ptr<const float>(part),
                      nsplit, G, Cout, Cin, 27, ptr<float>(grad), ldg, off, scale);
