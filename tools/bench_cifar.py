@@ -48,6 +48,8 @@ def main():
     ap.add_argument("--no-eval", action="store_true")
     ap.add_argument("--dataset", default="cifar10", choices=["cifar10", "tiny"])
     ap.add_argument("--no-augment", action="store_true")
+    ap.add_argument("--graphs", default="default", choices=["default", "on", "off"],
+                    help="captured hipGraph local steps (FLConfig.hip_graphs; default = the engine's choice)")
     args = ap.parse_args()
     tiny = args.dataset == "tiny"
     if tiny and args.n_train == 50000:
@@ -93,7 +95,8 @@ def main():
     engine = ResNetHipEngine(model, x8, y, info.device, augment=not args.no_augment)
     cfg = FLConfig(comm_round=args.warmup + args.rounds, epochs=args.epochs, batch_size=args.batch, lr=args.lr,
                    lr_decay=0.998, dense_ratio=args.dense_ratio, seed=args.seed, frac=args.frac,
-                   frequency_of_the_test=0 if args.no_eval else 1, final_round=False)
+                   frequency_of_the_test=0 if args.no_eval else 1, final_round=False,
+                   hip_graphs={"default": None, "on": True, "off": False}[args.graphs])
     runner = make_runner(args.algorithm, engine, splits, cfg, info, model, logger=None)
     torch.cuda.synchronize()
     t_setup = time.perf_counter() - t0
