@@ -52,8 +52,10 @@ def test_union_kernel_choices():
         assert m.conv3d_fwd_tri_ok(*conv2_dgrad) == 1           # supported ...
         assert m.conv3d_fwd_tri_pick(G, *conv2_dgrad) == 0      # ... but not chosen (no consistent gain)
     assert m.conv3d_fwd_tri_pick(64, *conv2) == 1
-    assert m.conv3d_wgrad_tri_pick(64, *conv4) == 1             # padded wgrad: only with >= 64 K positions
-    assert m.conv3d_wgrad_tri_pick(8, *conv4) == 0
+    # padded wgrad: only with >= 8 K output positions per launch (64 K before the overlapped stage DMA, [ADMA])
+    assert m.conv3d_wgrad_tri_pick(64, *conv4) == 1
+    assert m.conv3d_wgrad_tri_pick(8, *conv4) == 1              # 22 K positions
+    assert m.conv3d_wgrad_tri_pick(1, *conv4) == 0              # 2.8 K positions
     assert m.conv3d_fwd_tri_pick(64, *conv4) == 0               # padded forwards stay on the per-tap kernel
     # split factors stay within the model's bounds and keep >= 8 steps per block
     for G in (64, 8, 1):
