@@ -224,20 +224,23 @@ def partition_labels(method, labels, n_clients, alpha, n_cls=None, rng=None):
 
 def per_client_test_indices(train_labels, test_labels, train_map, n_cls=None, rng=None):
     """Per-client test sets drawn proportionally to each client's train label histogram:
-    for class c, ``ceil(count_c / total * ceil(|test| / C))`` random test indices of class c
-    (``cifar10/data_loader.py:221-236``).  Test sets may overlap across clients."""
+    for class c, ``ceil(count_c / total * ceil(|test| / C))`` random test indices of class c, C = the number of
+    clients (``tmp_tst_num`` of ``cifar10/data_loader.py:226-236``, the same in the cifar100 / tiny_imagenet / ABCD
+    loaders): about |test| / C samples per client (100 for CIFAR-10 with 100 clients).  Test sets may overlap across
+    clients.  (Rounds 1-5 divided by the class count instead: CIFAR-10 clients got ~1000 test samples each, ten
+    times the reference's evaluation work.)"""
     r = _rs(rng)
     train_labels, test_labels = np.asarray(train_labels), np.asarray(test_labels)
     n_cls = int(max(train_labels.max(), test_labels.max())) + 1 if n_cls is None else n_cls
     by_cls = [np.where(test_labels == c)[0] for c in range(n_cls)]
-    per_cls = math.ceil(len(test_labels) / n_cls)
+    per_client = math.ceil(len(test_labels) / max(1, len(train_map)))
     out = {}
     for i, idx in train_map.items():
         hist = np.bincount(train_labels[idx], minlength=n_cls)
         tot = max(1, hist.sum())
         pick = []
         for c in range(n_cls):
-            n = math.ceil(hist[c] / tot * per_cls)
+            n = math.ceil(hist[c] / tot * per_client)
             if n > 0 and len(by_cls[c]) > 0:
                 pick.append(r.choice(by_cls[c], min(n, len(by_cls[c])), replace=False))
         out[i] = np.concatenate(pick).astype(np.int64) if pick else np.zeros(0, np.int64)

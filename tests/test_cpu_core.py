@@ -44,6 +44,21 @@ def test_dir_partition_is_non_iid():
     assert np.mean(ent) < 0.8 * np.log(10)
 
 
+def test_per_client_test_sets_follow_reference_sizes():
+    """cifar10/data_loader.py:226-236: tmp_tst_num = ceil(|test| / client_number); class c gets
+    ceil(count_c / total * tmp_tst_num) samples, drawn from the test images of class c."""
+    y = _labels(5000)
+    yte = _labels(10000)[::-1].copy()
+    m = P.partition_dir(y, 100, 0.3, n_cls=10, rng=np.random.RandomState(3))
+    te = P.per_client_test_indices(y, yte, m, n_cls=10, rng=np.random.RandomState(4))
+    for c, ix in m.items():
+        h = np.bincount(y[ix], minlength=10)
+        want = sum(int(np.ceil(h[k] / h.sum() * 100)) for k in range(10))
+        assert len(te[c]) == want and 100 <= want <= 110
+        assert np.array_equal(np.bincount(yte[te[c]], minlength=10) > 0, h > 0)
+        assert len(set(te[c].tolist())) == len(te[c])
+
+
 def test_homo_and_site_partition():
     m = P.partition_homo(103, 4, rng=np.random.RandomState(0))
     assert sorted(np.concatenate(list(m.values())).tolist()) == list(range(103))
