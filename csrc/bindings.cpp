@@ -123,6 +123,9 @@ void res_grad_s2_om(uintptr_t out, uintptr_t dx1, uintptr_t dx2s, uintptr_t omas
 void img_input(uintptr_t src, uintptr_t idx, uintptr_t out, int N, int H, int W, int CP, float m0, float m1, float m2,
                float s0, float s1, float s2, int aug, int pad, uintptr_t seed_dev, int64_t seed_base, uintptr_t cids,
                int B, uintptr_t stream);
+void img_input_fold(uintptr_t src, uintptr_t idx, uintptr_t out, int N, int H, int W, int CP, float m0, float m1,
+                    float m2, float s0, float s1, float s2, int aug, int pad, uintptr_t seed_dev, int64_t seed_base,
+                    uintptr_t cids, int B, uintptr_t stream);
 // pack.hip
 void pack_convs(uintptr_t desc, int nd, int nplain, int nplain1, int ntrans, int lds, uintptr_t theta, int64_t ldt,
                 int G, uintptr_t out, uintptr_t stream);
@@ -322,6 +325,7 @@ PYBIND11_MODULE(_nidt_hip, m) {
   DEF(res_grad);
   DEF(res_grad_s2);
   DEF(img_input);
+  DEF(img_input_fold);
   DEF(pack_convs);
   DEF(pack1_rows_host);
   DEF(pack_plain_chunks);

@@ -13,7 +13,8 @@ client of a launch group is a row of the flat ``[C, P]`` parameter matrix and ea
   in two launches per step (``pack.hip``);
 * every convolution (3x3 stride 1/2, the 1x1 stride-2 projection shortcuts, the stem) is the client-grouped
   LDS-DMA implicit-GEMM kernel of ``conv3d.hip`` run on D = 1 volumes with 9 taps (``conv_fwd_g``); the stem's
-  3 input channels are zero-padded to 64 (one more layer-1-sized GEMM instead of a separate kernel);
+  3x3 window is folded into the input channels by the input stage (27 live of 64), so it runs as a 1x1 conv
+  ([STEM-FOLD]: 9x fewer MACs than nine channel-padded taps, forward and weight gradient);
 * data gradients: stride 1 = the same kernel on tap-flipped transposed weights; stride 2 (3x3) = four sub-pixel
   phase convs over the dy grid with 1/2/2/4 taps written straight into the interleaved dX positions
   (``conv_dgrad_s2_g``: 4x fewer MACs than a conv over the zero-upsampled gradient, no memset); 1x1 stride 2 = the
@@ -110,6 +111,19 @@ def augment_u8(img, oy, ox, flip, pad=AUG_PAD):
     return out
 
 
+def fold_window(x, cin=3, cp=None):
+    """The [STEM-FOLD] input from a channel-padded image [N, H, W, C] (channels < cin live): channel 3 t + c of pixel
+    (y, x) = channel c of pixel (y + kh - 1, x + kw - 1), t = 3 kh + kw, zero outside (twin of img.hip k_img_fold)."""
+    N, H, W, C = x.shape
+    cp = C if cp is None else cp
+    xp = F.pad(x[..., :cin].float(), (0, 0, 1, 1, 1, 1))
+    out = torch.zeros(N, H, W, cp, dtype=torch.float32, device=x.device)
+    for t in range(9):
+        kh, kw = divmod(t, 3)
+        out[..., cin * t:cin * (t + 1)] = xp[:, kh:kh + H, kw:kw + W]
+    return out.to(x.dtype)
+
+
 # ------------------------------------------------------------------------------------------------ convolutions
 def conv_fwd(x_ptr, w_ptr, y_ptr, G, B, D, H, W, Cin, Cout, kt, st, pad, padd, device):
     """Client-grouped conv forward (``conv_fwd_g``), split over the reduction when the output grid is too small to
@@ -201,6 +215,25 @@ class GroupedConv:
         self.slots = tap_slots(self.kt, stride)
         self.wp = self.wt = None  # packed images of the current step (WeightPacker.pack)
         self._ptabs = {}  # wgrad output-position tables per (B, H, W)
+        # [STEM-FOLD] (set by the network for its 3-channel stem, HIP only): the input arrives with the 3x3 window
+        # folded into its channels (img.hip k_img_fold, channel 3 t + c), so the layer runs as a 1x1 conv over
+        # K = 27 (padded to cin_p) with the folded weight image [Cout][27 -> cin_p]
+        self.fold = False
+        self._wf = {}  # folded weight image per G (persistent: its zero tail is written once)
+
+    def geometry(self):
+        """(taps, stride, pad) of the launches: the folded stem is a 1x1 stride-1 conv."""
+        return (1, 1, 0) if self.fold else (self.kt, self.stride, self.pad)
+
+    def _fold_w(self, wp, G):
+        """[G, Cout, 1, cin_p] folded image from the step's 9-tap image wp [G, Cout, 9, cin_p] (channels < 3 live):
+        wf[g, co, 3 t + c] = wp[g, co, t, c] (one strided copy; the 27 .. cin_p-1 tail stays zero)."""
+        wf = self._wf.get(G)
+        if wf is None:
+            wf = self._wf[G] = torch.zeros(G, self.cout, 1, self.cin_p, device=wp.device, dtype=torch.bfloat16)
+        wf.view(G, self.cout, self.cin_p)[:, :, :self.kt * self.cin].view(G, self.cout, self.kt, self.cin).copy_(
+            wp.view(G, self.cout, self.kt, self.cin_p)[..., :self.cin])
+        return wf
 
     def out_hw(self, h, w):
         return ((h + 2 * self.pad - self.k) // self.stride + 1, (w + 2 * self.pad - self.k) // self.stride + 1)
@@ -233,6 +266,10 @@ class GroupedConv:
             self.wt = (wt, G, theta.data_ptr()) if wt is not None else None
         wp = self.wp[0]
         y = torch.empty(N, Ho, Wo, self.cout, device=x.device, dtype=torch.bfloat16)
+        if self.fold:
+            conv_fwd(x.data_ptr(), self._fold_w(wp, G).data_ptr(), y.data_ptr(), G, N // G, 1, H, W, self.cin_p,
+                     self.cout, 1, 1, 0, 0, x.device)
+            return y
         if self.kt == 9 and self.stride == 1 and self.pad == 1 and slab_conv2d(
                 x.data_ptr(), wp.data_ptr(), y.data_ptr(), G, N // G, H, W, self.cin_p, self.cout, x.device):
             return y
@@ -261,7 +298,8 @@ class GroupedConv:
         B = N // G
         Ho, Wo = dy.shape[1:3]
         dy = dy.contiguous()
-        ns = m.conv_wgrad_nsplit_g(G, B, 1, H, W, self.cin_p, self.cout, self.kt, self.stride, self.pad, 0)
+        kt, st_, pd = self.geometry()
+        ns = m.conv_wgrad_nsplit_g(G, B, 1, H, W, self.cin_p, self.cout, kt, st_, pd, 0)
         ptab = self._pos_table(B, H, W, Ho, Wo, x.device)
         if ws is None:  # no branch: the whole backward on the current stream
             self._wgrad(m, x, dy, grads, G, B, H, W, ns, ptab, _stream())
@@ -304,23 +342,28 @@ class GroupedConv:
 
     def _wgrad(self, m, x, dy, grads, G, B, H, W, ns, ptab, st):
         branch = st != _stream()
-        part = torch.empty(ns * G * self.cout * self.kt * self.cin_p, device=x.device, dtype=torch.float32)
+        kt, st_, pd = self.geometry()
+        part = torch.empty(ns * G * self.cout * kt * self.cin_p, device=x.device, dtype=torch.float32)
         if branch:  # allocated on the main stream's pool, used on the branch: held until the join
             self._keep.append(part)
         if self.cin_p == self.cin:
             m.conv_wgrad_g(x.data_ptr(), dy.data_ptr(), part.data_ptr(), grads.data_ptr(), grads.stride(0),
-                           self.off, G, B, 1, H, W, self.cin_p, self.cout, self.kt, self.stride, self.pad, 0, ns,
+                           self.off, G, B, 1, H, W, self.cin_p, self.cout, kt, st_, pd, 0, ns,
                            1.0, ptab.data_ptr(), st)
         else:  # channel-padded stem: full-width gradient, then the live input channels into the row
-            full = torch.empty(G, self.cout * self.cin_p * self.kt, device=x.device, dtype=torch.float32)
+            full = torch.empty(G, self.cout * self.cin_p * kt, device=x.device, dtype=torch.float32)
             m.conv_wgrad_g(x.data_ptr(), dy.data_ptr(), part.data_ptr(), full.data_ptr(), full.stride(0), 0, G, B,
-                           1, H, W, self.cin_p, self.cout, self.kt, self.stride, self.pad, 0, ns, 1.0,
+                           1, H, W, self.cin_p, self.cout, kt, st_, pd, 0, ns, 1.0,
                            ptab.data_ptr(), st)
             if branch:
                 self._keep.append(full)
             with torch.cuda.stream(_external(st)) if branch else _nullctx():
-                grads[:, self.off:self.off + self.numel].view(G, self.cout, self.cin, self.kt).copy_(
-                    full.view(G, self.cout, self.cin_p, self.kt)[:, :, :self.cin])
+                dst = grads[:, self.off:self.off + self.numel].view(G, self.cout, self.cin, self.kt)
+                if self.fold:  # folded column 3 t + c -> PyTorch [co][c][t]
+                    dst.copy_(full.view(G, self.cout, self.cin_p)[:, :, :self.kt * self.cin]
+                              .view(G, self.cout, self.kt, self.cin).transpose(2, 3))
+                else:
+                    dst.copy_(full.view(G, self.cout, self.cin_p, self.kt)[:, :, :self.cin])
 
     def _pos_table(self, B, H, W, Ho, Wo, device):
         """Output-position table of the wgrad kernel: a function of the shape only, built once per (B, H, W) outside
@@ -328,8 +371,9 @@ class GroupedConv:
         key = (B, H, W)
         tab = self._ptabs.get(key)
         if tab is None:
+            kt, st_, pd = self.geometry()
             tab = torch.empty(B * Ho * Wo, 2, device=device, dtype=torch.int32)
-            ops.ext().conv_pos_table_g(tab.data_ptr(), B, 1, H, W, self.kt, self.stride, self.pad, 0, _stream())
+            ops.ext().conv_pos_table_g(tab.data_ptr(), B, 1, H, W, kt, st_, pd, 0, _stream())
             if not torch.cuda.is_current_stream_capturing():
                 torch.cuda.current_stream().synchronize()  # shared with launches on other streams from now on
                 self._ptabs[key] = tab
@@ -362,6 +406,9 @@ _PACK_DTYPE = np.dtype({"names": ["src_off", "wp_off", "wt_off", "cout", "cin_p"
 _PACK1 = os.environ.get("NIDT_PACK1", "1") != "0"
 # NIDT_PACK_FUSE=0: the optimizer never writes the forward images (k_pack_plain every step; A/B)
 _PACK_FUSE = os.environ.get("NIDT_PACK_FUSE", "1") != "0"
+# [STEM-FOLD] the 3-channel stem as a 1x1 conv over the window-folded input (img.hip k_img_fold); NIDT_STEM_FOLD=0:
+# the channel-padded 9-tap conv (A/B)
+_STEM_FOLD = os.environ.get("NIDT_STEM_FOLD", "1") != "0"
 
 
 class WeightPacker:
@@ -588,6 +635,8 @@ class GroupedResNet18GN:
             return GroupNormG(off[prefix + ".weight"], off[prefix + ".bias"], shp[prefix + ".weight"][0], self.hip)
 
         self.stem = conv("conv1.weight", 1, 1)
+        self.stem.fold = (self.hip and _STEM_FOLD and self.stem.k == 3 and self.stem.stride == 1 and self.stem.pad == 1
+                          and self.stem.cin * self.stem.kt <= self.stem.cin_p)
         self.stem_gn = gn("bn1")
         self.blocks = []
         for li in range(1, 5):
@@ -621,14 +670,14 @@ class GroupedResNet18GN:
         if self.hip:
             out = torch.empty(N, H, W, cp, device=self.device, dtype=torch.bfloat16)
             idx32 = idx if idx.dtype == torch.int32 else idx.int()
+            fn = ops.ext().img_input_fold if self.stem.fold else ops.ext().img_input  # [STEM-FOLD]
             if aug is not None:
                 seed_dev, seed_base, cids_dev, _, B = aug
-                ops.ext().img_input(x8.data_ptr(), idx32.data_ptr(), out.data_ptr(), N, H, W, cp, *self.mean,
-                                    *self.std, 1, AUG_PAD, seed_dev.data_ptr(), int(seed_base), cids_dev.data_ptr(),
-                                    B, _stream())
+                fn(x8.data_ptr(), idx32.data_ptr(), out.data_ptr(), N, H, W, cp, *self.mean, *self.std, 1, AUG_PAD,
+                   seed_dev.data_ptr(), int(seed_base), cids_dev.data_ptr(), B, _stream())
             else:
-                ops.ext().img_input(x8.data_ptr(), idx32.data_ptr(), out.data_ptr(), N, H, W, cp, *self.mean,
-                                    *self.std, 0, AUG_PAD, 0, 0, 0, 1, _stream())
+                fn(x8.data_ptr(), idx32.data_ptr(), out.data_ptr(), N, H, W, cp, *self.mean, *self.std, 0, AUG_PAD, 0,
+                   0, 0, 1, _stream())
             return out
         img = x8.index_select(0, idx.long().to(x8.device))
         if aug is not None:

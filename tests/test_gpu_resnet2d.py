@@ -237,14 +237,56 @@ def test_fused_input_stage_matches_twin(hw):
     seed_dev = torch.tensor([123456], dtype=torch.int64, device=dev)
     cids = [7, 2, 11]
     cids_dev = torch.tensor(cids, dtype=torch.int32, device=dev)
-    xa = hip.input(x8.to(dev), idx.to(dev), (seed_dev, 5 << 40, cids_dev, cids, B))
+    assert hip.stem.fold  # [STEM-FOLD] is the default on the HIP path
     xc = cpu.input(x8, idx, (seed_dev.cpu(), 5 << 40, None, cids, B))
-    torch.cuda.synchronize()
-    assert xa.shape == (G * B, hw, hw, 64) and float(xa[..., 3:].float().abs().max()) == 0.0
-    assert torch.allclose(xa.cpu().float(), xc.float(), atol=2e-2, rtol=0)
-    xp = hip.input(x8.to(dev), idx.to(dev))
-    assert torch.allclose(xp.cpu().float(), cpu.input(x8, idx).float(), atol=2e-2, rtol=0)
-    assert not torch.allclose(xa.float(), xp.float(), atol=0.1)
+    xcp = cpu.input(x8, idx)
+    for fold in (False, True):
+        hip.stem.fold = fold
+        xa = hip.input(x8.to(dev), idx.to(dev), (seed_dev, 5 << 40, cids_dev, cids, B))
+        xp = hip.input(x8.to(dev), idx.to(dev))
+        torch.cuda.synchronize()
+        ea, ep = (R.fold_window(xc), R.fold_window(xcp)) if fold else (xc, xcp)
+        live = 27 if fold else 3
+        assert xa.shape == (G * B, hw, hw, 64) and float(xa[..., live:].float().abs().max()) == 0.0
+        assert torch.allclose(xa.cpu().float(), ea.float(), atol=2e-2, rtol=0), fold
+        assert torch.allclose(xp.cpu().float(), ep.float(), atol=2e-2, rtol=0), fold
+        assert not torch.allclose(xa.float(), xp.float(), atol=0.1)
+
+
+def test_stem_fold_matches_padded_stem():
+    """[STEM-FOLD]: the stem as a 1x1 conv over the window-folded input == the channel-padded 9-tap stem (forward
+    output and the stem's weight-gradient row), same weights, same augmented batch."""
+    from neuroimagedisttraining_amd.engine import resnet2d_hip as R
+    from neuroimagedisttraining_amd.engine.executor import padded_rows
+    from neuroimagedisttraining_amd.engine.flat import ParamLayout
+    from neuroimagedisttraining_amd.models import customized_resnet18
+    dev = _dev()
+    torch.manual_seed(1)
+    G, B, hw = 3, 4, 32
+    m = customized_resnet18(class_num=10)
+    L = ParamLayout.from_tensors(list(m.named_parameters()))
+    net = R.GroupedResNet18GN(L, dev)
+    P = L.total
+    th = padded_rows(G, P, dev)
+    th.copy_(torch.randn(G, P, device=dev) * 0.1)
+    x8 = torch.from_numpy(np.random.default_rng(2).integers(0, 256, size=(G * B, hw, hw, 3)).astype(np.uint8)).to(dev)
+    idx = torch.arange(G * B, dtype=torch.int32, device=dev)
+    st = net.stem
+    outs = []
+    for fold in (False, True):
+        st.fold = fold
+        x = net.input(x8, idx)
+        net.packer.pack(th, G, True, key=("t", fold))
+        y = st.fwd(x, th, G, train=True, packed=True)
+        dy = (torch.randn(y.shape, device=dev, generator=torch.Generator(device=dev).manual_seed(3))).to(y.dtype)
+        gr = padded_rows(G, P, dev)
+        gr.zero_()
+        st.bwd(dy, x, th, gr, G, False)
+        torch.cuda.synchronize()
+        outs.append((y.float(), gr[:, st.off:st.off + st.numel].clone()))
+    (y0, g0), (y1, g1) = outs
+    assert _rel(y1, y0) < 1e-2
+    assert _rel(g1, g0) < 1e-3
 
 
 def test_tiny_resnet18_train_step_matches_cpu_twin():
