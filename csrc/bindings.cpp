@@ -26,6 +26,13 @@ void local_opt_pack(uintptr_t w, uintptr_t g, uintptr_t buf, int64_t ld, uintptr
                     float lamda, uintptr_t part, int64_t C, int64_t P, float lr, float wd, float mom, float max_norm,
                     uintptr_t lr_dev, int keep_grad, uintptr_t desc, int nd, int nconv, uintptr_t rest, int nrest,
                     int lds, uintptr_t out, uintptr_t stream);
+void local_opt_pack_wt(uintptr_t w, uintptr_t g, uintptr_t buf, int64_t ld, uintptr_t mbits, int64_t mstride,
+                       int mask_mode, uintptr_t ref, int64_t ref_ld, float mu, uintptr_t pref, int64_t pref_ld,
+                       float lamda, uintptr_t part, int64_t C, int64_t P, float lr, float wd, float mom, float max_norm,
+                       uintptr_t lr_dev, int keep_grad, uintptr_t desc, int nd, int nconv, uintptr_t rest, int nrest,
+                       int lds, uintptr_t out, uintptr_t stream);
+int wt_tiles(int cout, int cin_p);
+int wt_tile_lds(int kt);
 // conv3d.hip
 void conv3d_fwd(uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t xs, uintptr_t xt, uintptr_t y, uintptr_t stats,
                 int G, int B, int D, int H, int W, int Cin, int Cout, int pad, uintptr_t stream);
@@ -375,6 +382,9 @@ PYBIND11_MODULE(_nidt_hip, m) {
   DEF(mask_stats);
   DEF(local_opt);
   DEF(local_opt_pack);
+  DEF(local_opt_pack_wt);
+  DEF(wt_tiles);
+  DEF(wt_tile_lds);
   DEF(seg_count);
   DEF(seg_select);
   DEF(seg_prune);

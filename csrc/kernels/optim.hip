@@ -349,6 +349,118 @@ __global__ __launch_bounds__(kOptThreads) void k_local_step_pack(LocalOpt a, con
   pack_image_chunk(d, row, out, c, co, ci0, cw, cc);
 }
 
+// [PACK-WT] The step writing BOTH bf16 images of the next training step: the forward image wp[g][Cout][kt][Cin_p] and
+// the data-gradient image wt[g][Cin_p][slot(t)][Cout] (pack.hip's layouts), so no k_pack_trans pass re-reads wp and
+// writes wt in the next step.  Conv blocks are tiles of kWtCo output x kWtCi input channels x all taps: the tile's
+// updated weights go to LDS as bf16 in PyTorch order ([co][ci][t]: 72 KB at kt = 9, two blocks per CU), the forward
+// image is written in 128-B runs (64 input channels of one (co, t)) and the transposed image in 128-B runs (64 output
+// channels of one (ci, slot)) — bit-identical to k_pack_plain + k_pack_trans.  Opt-in (NIDT_PACK_WT=1): measured
+// slower than k_pack_trans overlapped on the side stream, with 16- and 64-channel tiles (profiles/r6_pack_wt.txt).  Blocks
+// [nconv, nconv + nrest): the other parameter ranges, as k_local_step_pack.  desc.blk_plain = this tiled grid's
+// prefixes (host: wt_tiles).
+constexpr int kWtCo = 64, kWtCi = 64;
+int wt_tiles(int cout, int cin_p) { return ((cout + kWtCo - 1) / kWtCo) * ((cin_p + kWtCi - 1) / kWtCi); }
+int wt_tile_lds(int kt) { return kWtCo * kWtCi * kt * 2; }
+
+template <int MASK, bool HAS_MOM>
+__global__ __launch_bounds__(kOptThreads) void k_local_step_pack_wt(LocalOpt a, const float* __restrict__ part,
+                                                                    int nblk, const PackDesc* __restrict__ desc, int nd,
+                                                                    int nconv, const int64_t* __restrict__ rest,
+                                                                    uint16_t* __restrict__ out) {
+  extern __shared__ uint16_t rowh[];
+  __shared__ float red[kOptThreads / 64];
+  const int c = blockIdx.y;
+  const float lr = a.lr_dev ? *a.lr_dev : a.lr;
+  const float coef = opt_coef(a, part, nblk, c, red);
+  if ((int)blockIdx.x >= nconv) {
+    const int64_t* r = rest + 2 * ((int64_t)blockIdx.x - nconv);
+    opt_range<MASK, HAS_MOM>(a, c, coef, lr, r[0], r[0] + r[1], nullptr);
+    return;
+  }
+  const int li = find_layer(desc, nd, blockIdx.x, 0);
+  const PackDesc& d = desc[li];
+  const int Cin = d.cin_p, kt = d.kt, cs = d.cin_src, Cout = d.cout;
+  const int nci = (Cin + kWtCi - 1) / kWtCi;
+  const int b = blockIdx.x - d.blk_plain, co0 = (b / nci) * kWtCo, ci0 = (b - (b / nci) * nci) * kWtCi;
+  const int nco = min(kWtCo, Cout - co0), cw = min(kWtCi, Cin - ci0), cc = max(0, min(kWtCi, cs - ci0));
+  const int RS = kWtCi * kt;  // LDS elements per output channel of the tile
+  const int L = cc * kt;      // live elements per output channel (contiguous in the PyTorch row)
+  const int64_t base = d.src_off + (int64_t)co0 * cs * kt + (int64_t)ci0 * kt, rstr = (int64_t)cs * kt;
+  float* wr = a.w + (int64_t)c * a.ld;
+  float* gr = a.g + (int64_t)c * a.ld;
+  float* br = HAS_MOM ? a.buf + (int64_t)c * a.ld : nullptr;
+  const float* rr = a.mu != 0.f ? a.ref + (int64_t)c * a.ref_ld : nullptr;
+  const float* pr = a.lamda != 0.f ? a.pref + (int64_t)c * a.pref_ld : nullptr;
+  const float pull = lr * a.lamda;
+  auto step1 = [&](float& ww, float& gg, float& bb, int64_t gi, bool m) {  // the element step of opt_range
+    float gj = (MASK == kMaskGrad && !m) ? 0.f : gg;
+    if (rr) gj = fmaf(a.mu, ww - rr[gi], gj);
+    gj *= coef;
+    gg = gj;
+    float dd = fmaf(a.wd, ww, gj);
+    if (HAS_MOM) {
+      bb = fmaf(a.mom, bb, dd);
+      dd = bb;
+    }
+    ww = fmaf(-lr, dd, ww);
+    if (pr) ww = fmaf(-pull, ww - pr[gi], ww);
+    if (MASK == kMaskWeight && !m) ww = 0.f;
+  };
+  if (L % 4 == 0 && (base & 3) == 0 && (rstr & 3) == 0) {  // the tile's rows as one flat loop of 16-B accesses
+    const int L4 = L >> 2;
+    for (int e = threadIdx.x; e < nco * L4; e += kOptThreads) {
+      const int r = e / L4, i = (e - r * L4) * 4;
+      const int64_t gi = base + r * rstr + i;
+      const float4 gv = *reinterpret_cast<const float4*>(gr + gi), wv = *reinterpret_cast<const float4*>(wr + gi);
+      float gg[4] = {gv.x, gv.y, gv.z, gv.w}, ww[4] = {wv.x, wv.y, wv.z, wv.w}, bb[4] = {0.f, 0.f, 0.f, 0.f};
+      if (HAS_MOM) {
+        const float4 v = *reinterpret_cast<const float4*>(br + gi);
+        bb[0] = v.x; bb[1] = v.y; bb[2] = v.z; bb[3] = v.w;
+      }
+      const uint32_t m = mask4<MASK>(a, c, gi);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) step1(ww[j], gg[j], bb[j], gi + j, (m >> j) & 1u);
+      if (a.keep_grad) *reinterpret_cast<float4*>(gr + gi) = make_float4(gg[0], gg[1], gg[2], gg[3]);
+      *reinterpret_cast<float4*>(wr + gi) = make_float4(ww[0], ww[1], ww[2], ww[3]);
+      if (HAS_MOM) *reinterpret_cast<float4*>(br + gi) = make_float4(bb[0], bb[1], bb[2], bb[3]);
+      *reinterpret_cast<uint2*>(rowh + r * RS + i) = make_uint2(pack_bf16x2(ww[0], ww[1]), pack_bf16x2(ww[2], ww[3]));
+    }
+  } else {  // unaligned rows (the 3-channel stem): element by element
+    for (int e = threadIdx.x; e < nco * L; e += kOptThreads) {
+      const int r = e / L, i = e - r * L;
+      const int64_t gi = base + r * rstr + i;
+      float ww = wr[gi], gg = gr[gi], bb = HAS_MOM ? br[gi] : 0.f;
+      const bool m = MASK == kMaskNone ? true : ((a.mbits[(int64_t)c * a.mstride + (gi >> 5)] >> (gi & 31)) & 1u);
+      step1(ww, gg, bb, gi, m);
+      if (a.keep_grad) gr[gi] = gg;
+      wr[gi] = ww;
+      if (HAS_MOM) br[gi] = bb;
+      rowh[r * RS + i] = f32_to_bf16(ww);
+    }
+  }
+  __syncthreads();
+  auto w_at = [&](int r, int ci, int t) -> uint32_t { return ci < cc ? (uint32_t)rowh[r * RS + ci * kt + t] : 0u; };
+  uint16_t* wp = out + d.wp_off + (int64_t)c * Cout * kt * Cin;
+  const int nq = cw >> 3;
+  for (int e = threadIdx.x; e < nco * kt * nq; e += kOptThreads) {
+    const int q = e % nq, rt = e / nq, t = rt % kt, r = rt / kt;
+    uint32_t w[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) w[k] = w_at(r, 8 * q + 2 * k, t) | (w_at(r, 8 * q + 2 * k + 1, t) << 16);
+    *reinterpret_cast<uint4*>(wp + ((int64_t)(co0 + r) * kt + t) * Cin + ci0 + 8 * q) = make_uint4(w[0], w[1], w[2], w[3]);
+  }
+  if (d.wt_off < 0) return;
+  uint16_t* wt = out + d.wt_off + (int64_t)c * Cin * kt * Cout;
+  const int nq2 = nco >> 3;
+  for (int e = threadIdx.x; e < cw * kt * nq2; e += kOptThreads) {
+    const int q = e % nq2, rt = e / nq2, t = rt % kt, ci = rt / kt;
+    uint32_t w[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) w[k] = w_at(8 * q + 2 * k, ci, t) | (w_at(8 * q + 2 * k + 1, ci, t) << 16);
+    *reinterpret_cast<uint4*>(wt + ((int64_t)(ci0 + ci) * kt + d.slot[t]) * Cout + co0 + 8 * q) = make_uint4(w[0], w[1], w[2], w[3]);
+  }
+}
+
 void local_opt(uintptr_t w, uintptr_t g, uintptr_t buf, int64_t ld, uintptr_t mbits, int64_t mstride, int mask_mode,
                uintptr_t ref, int64_t ref_ld, float mu, uintptr_t pref, int64_t pref_ld, float lamda, uintptr_t part,
                int64_t C, int64_t P, float lr, float wd, float mom, float max_norm, uintptr_t lr_dev, int keep_grad,
@@ -388,18 +500,19 @@ void local_opt(uintptr_t w, uintptr_t g, uintptr_t buf, int64_t ld, uintptr_t mb
 
 // local_opt + the forward images of the conv layers (k_local_step_pack): desc / nd / nconv = the fused plain grid,
 // rest / nrest = the other parameter ranges, lds = bytes of the largest chunk, out = the packed image buffer
-void local_opt_pack(uintptr_t w, uintptr_t g, uintptr_t buf, int64_t ld, uintptr_t mbits, int64_t mstride,
-                    int mask_mode, uintptr_t ref, int64_t ref_ld, float mu, uintptr_t pref, int64_t pref_ld,
-                    float lamda, uintptr_t part, int64_t C, int64_t P, float lr, float wd, float mom, float max_norm,
-                    uintptr_t lr_dev, int keep_grad, uintptr_t desc, int nd, int nconv, uintptr_t rest, int nrest,
-                    int lds, uintptr_t out, uintptr_t stream) {
+static void local_opt_pack_impl(uintptr_t w, uintptr_t g, uintptr_t buf, int64_t ld, uintptr_t mbits,
+                                int64_t mstride, int mask_mode, uintptr_t ref, int64_t ref_ld, float mu,
+                                uintptr_t pref, int64_t pref_ld, float lamda, uintptr_t part, int64_t C, int64_t P,
+                                float lr, float wd, float mom, float max_norm, uintptr_t lr_dev, int keep_grad,
+                                uintptr_t desc, int nd, int nconv, uintptr_t rest, int nrest, int lds, uintptr_t out,
+                                uintptr_t stream, bool wt) {
   NIDT_REQUIRE(ld % 4 == 0 && ld >= P, "local_opt_pack: row stride must be >= P and a multiple of 4");
   NIDT_REQUIRE((w & 15) == 0 && (g & 15) == 0 && (buf & 15) == 0, "local_opt_pack: 16-byte alignment");
   NIDT_REQUIRE(mask_mode == kMaskNone || (mbits != 0 && mstride % 4 == 0 && (mbits & 15) == 0), "local_opt_pack: mask");
   NIDT_REQUIRE(mu == 0.f || (ref != 0 && ref_ld % 4 == 0 && (ref & 15) == 0), "local_opt_pack: prox reference");
   NIDT_REQUIRE(lamda == 0.f || (pref != 0 && pref_ld % 4 == 0 && (pref & 15) == 0), "local_opt_pack: pull reference");
   NIDT_REQUIRE(desc != 0 && nd > 0 && nconv > 0 && nrest >= 0 && (nrest == 0 || rest != 0) && out != 0 && lds > 0 &&
-               lds <= 64 * 1024, "local_opt_pack: bad pack plan");
+               lds <= (wt ? 80 : 64) * 1024, "local_opt_pack: bad pack plan");
   if (C == 0) return;
   LocalOpt a{ptr<float>(w), ptr<float>(g), ptr<float>(buf), ld, ptr<const uint32_t>(mbits), mstride,
              ptr<const float>(ref), ref_ld, mu, ptr<const float>(pref), pref_ld, lamda, lr, wd, mom, max_norm,
@@ -415,8 +528,14 @@ void local_opt_pack(uintptr_t w, uintptr_t g, uintptr_t buf, int64_t ld, uintptr
   const bool hm = buf != 0 && mom != 0.f;
   const dim3 pgrid((unsigned)(nconv + nrest), (unsigned)C);
 #define NIDT_LSP(M, MO)                                                                                        \
-  hipLaunchKernelGGL((k_local_step_pack<M, MO>), pgrid, dim3(kOptThreads), lds, st, a, ptr<const float>(part), nblk, \
-                     ptr<const PackDesc>(desc), nd, nconv, ptr<const int64_t>(rest), ptr<uint16_t>(out))
+  if (wt) {                                                                                                    \
+    NIDT_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_local_step_pack_wt<M, MO>),                   \
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, lds));                            \
+    hipLaunchKernelGGL((k_local_step_pack_wt<M, MO>), pgrid, dim3(kOptThreads), lds, st, a, ptr<const float>(part), \
+                       nblk, ptr<const PackDesc>(desc), nd, nconv, ptr<const int64_t>(rest), ptr<uint16_t>(out));  \
+  } else                                                                                                       \
+    hipLaunchKernelGGL((k_local_step_pack<M, MO>), pgrid, dim3(kOptThreads), lds, st, a, ptr<const float>(part), \
+                       nblk, ptr<const PackDesc>(desc), nd, nconv, ptr<const int64_t>(rest), ptr<uint16_t>(out))
   switch (mask_mode * 2 + (hm ? 1 : 0)) {
     case 0: NIDT_LSP(kMaskNone, false); break;
     case 1: NIDT_LSP(kMaskNone, true); break;
@@ -428,6 +547,26 @@ void local_opt_pack(uintptr_t w, uintptr_t g, uintptr_t buf, int64_t ld, uintptr
   }
 #undef NIDT_LSP
   NIDT_CHECK(hipGetLastError());
+}
+
+void local_opt_pack(uintptr_t w, uintptr_t g, uintptr_t buf, int64_t ld, uintptr_t mbits, int64_t mstride,
+                    int mask_mode, uintptr_t ref, int64_t ref_ld, float mu, uintptr_t pref, int64_t pref_ld,
+                    float lamda, uintptr_t part, int64_t C, int64_t P, float lr, float wd, float mom, float max_norm,
+                    uintptr_t lr_dev, int keep_grad, uintptr_t desc, int nd, int nconv, uintptr_t rest, int nrest,
+                    int lds, uintptr_t out, uintptr_t stream) {
+  local_opt_pack_impl(w, g, buf, ld, mbits, mstride, mask_mode, ref, ref_ld, mu, pref, pref_ld, lamda, part, C, P, lr,
+                      wd, mom, max_norm, lr_dev, keep_grad, desc, nd, nconv, rest, nrest, lds, out, stream, false);
+}
+
+// [PACK-WT] local_opt_pack over the tiled grid (desc.blk_plain = wt_tiles prefixes; lds = wt_tile_lds(max kt)), also
+// writing the data-gradient images of the layers with wt_off >= 0 (every layer: Cout % 16 == 0, Cin_p % 8 == 0)
+void local_opt_pack_wt(uintptr_t w, uintptr_t g, uintptr_t buf, int64_t ld, uintptr_t mbits, int64_t mstride,
+                       int mask_mode, uintptr_t ref, int64_t ref_ld, float mu, uintptr_t pref, int64_t pref_ld,
+                       float lamda, uintptr_t part, int64_t C, int64_t P, float lr, float wd, float mom, float max_norm,
+                       uintptr_t lr_dev, int keep_grad, uintptr_t desc, int nd, int nconv, uintptr_t rest, int nrest,
+                       int lds, uintptr_t out, uintptr_t stream) {
+  local_opt_pack_impl(w, g, buf, ld, mbits, mstride, mask_mode, ref, ref_ld, mu, pref, pref_ld, lamda, part, C, P, lr,
+                      wd, mom, max_norm, lr_dev, keep_grad, desc, nd, nconv, rest, nrest, lds, out, stream, true);
 }
 
 // ---- weighted reduction over the client axis: out[p] = sum_c wts[c] * rows[c, p] (+ beta*out) ----

@@ -163,13 +163,14 @@ class HipEngine:
                                          keep_grad), ops.stream())
 
     def local_opt_pack(self, theta, grads, mom_buf, spec, lr, wd, momentum, max_norm, plan, lr_dev=None,
-                       keep_grad=False):
+                       keep_grad=False, wt=False):
         """:meth:`local_opt` that also writes the conv layers' bf16 forward images of the next step from the updated
-        weights (``optim.hip`` ``local_opt_pack``; ``plan`` = :meth:`.resnet2d_hip.WeightPacker.fused_plan`)."""
+        weights (``optim.hip`` ``local_opt_pack``; ``plan`` = :meth:`.resnet2d_hip.WeightPacker.fused_plan`).
+        ``wt``: the plan is the tiled one and the step writes the data-gradient images too (``local_opt_pack_wt``)."""
         tab, nd, nconv, rest, nrest, lds, buf = plan
-        self.m.local_opt_pack(*self._opt_args(theta, grads, mom_buf, spec, lr, wd, momentum, max_norm, lr_dev,
-                                              keep_grad), tab.data_ptr(), nd, nconv,
-                              rest.data_ptr() if nrest else 0, nrest, lds, buf.data_ptr(), ops.stream())
+        fn = self.m.local_opt_pack_wt if wt else self.m.local_opt_pack
+        fn(*self._opt_args(theta, grads, mom_buf, spec, lr, wd, momentum, max_norm, lr_dev, keep_grad),
+           tab.data_ptr(), nd, nconv, rest.data_ptr() if nrest else 0, nrest, lds, buf.data_ptr(), ops.stream())
 
     def _opt_args(self, theta, grads, mom_buf, spec, lr, wd, momentum, max_norm, lr_dev, keep_grad):
         G, P = theta.shape

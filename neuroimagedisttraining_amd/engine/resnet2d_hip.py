@@ -406,6 +406,11 @@ _PACK_DTYPE = np.dtype({"names": ["src_off", "wp_off", "wt_off", "cout", "cin_p"
 _PACK1 = os.environ.get("NIDT_PACK1", "1") != "0"
 # NIDT_PACK_FUSE=0: the optimizer never writes the forward images (k_pack_plain every step; A/B)
 _PACK_FUSE = os.environ.get("NIDT_PACK_FUSE", "1") != "0"
+# [PACK-WT] NIDT_PACK_WT=1: the optimizer also writes the next step's data-gradient images (optim.hip
+# k_local_step_pack_wt over 64 x 64-channel tiles, bit-identical), so the step runs no k_pack_trans.  Off by default:
+# slower than k_pack_trans overlapped on the weight-gradient side stream (CIFAR SubAvg -2.4 %, DisPFL -4.5 %; with
+# 16-channel tiles -0.3 / -2.8 %; profiles/r6_pack_wt.txt) — the optimizer is on the critical path, the transposes are not
+_PACK_WT = os.environ.get("NIDT_PACK_WT", "0") == "1"
 # [STEM-FOLD] the 3-channel stem as a 1x1 conv over the window-folded input (img.hip k_img_fold); NIDT_STEM_FOLD=0:
 # the channel-padded 9-tap conv (A/B)
 _STEM_FOLD = os.environ.get("NIDT_STEM_FOLD", "1") != "0"
@@ -421,7 +426,9 @@ class WeightPacker:
         self._plans = {}
         self._descs = {}
         self.last = None   # (key, theta data_ptr, row stride) of the last pack() call
-        self.fresh = {}    # key -> (theta data_ptr, theta._version) whose forward images the optimizer wrote
+        # key -> (theta data_ptr, theta._version, wt) whose forward images (and with wt the data-gradient images too)
+        # the optimizer wrote
+        self.fresh = {}
         # keys own their buffers (the 3-D engine's per-row-group training keys): an image stays fresh across other
         # keys' packs; otherwise only the very next pack may reuse one
         self.keep_other_fresh = False
@@ -470,11 +477,17 @@ class WeightPacker:
         self._descs[key] = desc
         return plan
 
-    def fused_plan(self, key, P):
+    def wt_ok(self):
+        """[PACK-WT] applies: every layer's channels fit the tiled step's 16-B runs and its LDS tile."""
+        return _PACK_WT and all(c.cout % 16 == 0 and c.cin_p % 8 == 0 and c.kt <= 9 for c in self.convs)
+
+    def fused_plan(self, key, P, wt=False):
         """Plan of the optimizer step that writes ``key``'s forward images itself (``optim.hip`` ``local_opt_pack``):
         (descriptor table with plain-grid prefixes over every conv layer, its length, conv blocks, {start, length}
-        table of the other parameter ranges of a P-wide row, its length, LDS bytes, the image buffer)."""
-        fk = ("fused", key, int(P))
+        table of the other parameter ranges of a P-wide row, its length, LDS bytes, the image buffer).  ``wt``: the
+        tiled grid of ``local_opt_pack_wt`` (16 output x 64 input channels x all taps per block), which also writes
+        the data-gradient images of ``key``'s layers."""
+        fk = ("fused", key, int(P), bool(wt))
         plan = self._plans.get(fk)
         if plan is not None:
             return plan
@@ -483,7 +496,7 @@ class WeightPacker:
         nconv, spans = 0, []
         for i, c in enumerate(self.convs):
             desc[i]["blk_plain"] = nconv
-            nconv += c.cout * m.pack_plain_chunks(c.cin_p, c.kt)
+            nconv += m.wt_tiles(c.cout, c.cin_p) if wt else c.cout * m.pack_plain_chunks(c.cin_p, c.kt)
             spans.append((c.off, c.off + c.numel))
         rest, pos = [], 0
         for a, b in sorted(spans) + [(int(P), int(P))]:
@@ -492,7 +505,7 @@ class WeightPacker:
                 rest.append((pos, n))
                 pos += n
             pos = max(pos, b)
-        lds = max(m.pack_plain_lds(c.cin_p, c.kt) for c in self.convs)
+        lds = max((m.wt_tile_lds(c.kt) if wt else m.pack_plain_lds(c.cin_p, c.kt)) for c in self.convs)
         tab = torch.from_numpy(desc.view(np.uint8).copy()).to(self.device)
         rt = torch.tensor(rest if rest else [(0, 0)], dtype=torch.int64).to(self.device)
         plan = (tab, len(self.convs), nconv, rt, len(rest), lds, self._plans[key][4])
@@ -506,8 +519,11 @@ class WeightPacker:
         key = (G, train) if key is None else key
         tab, (nplain, nplain1), ntrans, lds, buf, views = self._plan(G, train, key)
         f = self.fresh.pop(key, None)
-        if f is not None and f == (theta.data_ptr(), theta._version) and not torch.cuda.is_current_stream_capturing():
+        if (f is not None and f[:2] == (theta.data_ptr(), theta._version)
+                and not torch.cuda.is_current_stream_capturing()):
             nplain = nplain1 = 0
+            if len(f) > 2 and f[2]:  # [PACK-WT] the data-gradient images too
+                ntrans = 0
             self.fresh_hits += 1
         if not self.keep_other_fresh:
             self.fresh.clear()  # an image is only ever reused by the very next pack
@@ -915,9 +931,11 @@ class ResNetHipEngine:
                 and pk.last[1:] == (theta.data_ptr(), theta.stride(0)) and pk.last[0][0] == theta.shape[0]
                 and not torch.cuda.is_current_stream_capturing()):
             key = pk.last[0]
+            wt = pk.wt_ok()
             HipEngine.local_opt_pack(self._delegate(), theta, grads, mom_buf, spec, lr, wd, momentum, max_norm,
-                                     pk.fused_plan(key, theta.shape[1]), lr_dev=lr_dev, keep_grad=keep_grad)
-            pk.fresh = {key: (theta.data_ptr(), theta._version)}
+                                     pk.fused_plan(key, theta.shape[1], wt=wt), lr_dev=lr_dev, keep_grad=keep_grad,
+                                     wt=wt)
+            pk.fresh = {key: (theta.data_ptr(), theta._version, wt)}
             return
         if pk is not None:
             pk.fresh.clear()

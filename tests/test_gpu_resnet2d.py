@@ -360,10 +360,14 @@ def test_fused_cls_head_matches_torch_head(hw, K, G, B, monkeypatch):
 
 
 @pytest.mark.parametrize("mask_mode", [0, 1])
-def test_optimizer_written_images_equal_pack(mask_mode):
+@pytest.mark.parametrize("wt", [False, True])
+def test_optimizer_written_images_equal_pack(mask_mode, wt, monkeypatch):
     """[PACK-FUSE] local_opt(pack_next=True) (optim.hip k_local_step_pack) updates theta, momentum and gradients bit for
     bit like the plain step, writes the forward images k_pack_plain would write from the updated rows, and the next
-    step (which skips the plain pack) gives the same loss and gradients."""
+    step (which skips the plain pack) gives the same loss and gradients.  [PACK-WT] (wt): the tiled step
+    (k_local_step_pack_wt) also writes the data-gradient images, bit for bit those of k_pack_trans."""
+    from neuroimagedisttraining_amd.engine import resnet2d_hip as R
+    monkeypatch.setattr(R, "_PACK_WT", wt)
     from neuroimagedisttraining_amd.engine import masks as MK
     from neuroimagedisttraining_amd.engine.executor import padded_rows
     from neuroimagedisttraining_amd.engine.resnet2d_hip import ResNetHipEngine, synthetic_cifar
@@ -396,16 +400,18 @@ def test_optimizer_written_images_equal_pack(mask_mode):
             if fused and step == 0:  # step 1 then runs on the images written by step 0's optimizer (checked here)
                 pk = eng.net.packer
                 key = pk.last[0]
-                assert key in pk.fresh
+                assert key in pk.fresh and pk.fresh[key][2] == wt
                 buf, views = pk._plans[key][4], pk._plans[key][5]
-                fwd = [buf[o:o + int(np.prod(shp))] for (o, shp), _ in views]  # the forward images (not the dgrad)
+                fwd = [buf[o:o + int(np.prod(shp))] for (o, shp), _ in views]  # the forward images
+                if wt:  # ... and the data-gradient images
+                    fwd += [buf[vt[0]:vt[0] + int(np.prod(vt[1]))] for _, vt in views if vt is not None]
                 got = [v.clone() for v in fwd]
                 pk.fresh.clear()
                 pk.pack(theta, G, True, key=key)  # the plain pack from the updated rows
                 torch.cuda.synchronize()
                 for li, (a, b) in enumerate(zip(got, fwd)):
                     assert torch.equal(a, b), (step, li)
-                pk.fresh[key] = (theta.data_ptr(), theta._version)  # restore: the next step reuses the images
+                pk.fresh[key] = (theta.data_ptr(), theta._version, wt)  # restore: the next step reuses the images
         torch.cuda.synchronize()
         out[fused] = (theta.clone(), mom.clone(), torch.stack(losses))
     assert torch.equal(out[False][0], out[True][0])
