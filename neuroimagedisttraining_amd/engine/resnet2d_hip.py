@@ -286,11 +286,13 @@ class GroupedConv:
         return y.view(B, G, self.cout, Ho, Wo).permute(1, 0, 3, 4, 2).reshape(N, Ho, Wo, self.cout)
 
     # ---------------------------------------------------------------- backward
-    def bwd(self, dy, x, theta, grads, G, need_dx, scratch=None, ws=None):
+    def bwd(self, dy, x, theta, grads, G, need_dx, scratch=None, ws=None, defer=None):
         """dW -> grads rows (PyTorch layout at ``off``); returns dX ``[N, H, W, cin_p]`` (or None).  For the 1x1
         stride-2 projection the returned gradient is the half-resolution one of the even pixels (``res_grad_s2``
         adds it into the residual stream).  ``ws``: raw handle of the step's weight-gradient branch stream — the wgrad is
-        forked onto it (the caller joins it before the optimizer) and only the data gradient stays on the chain."""
+        forked onto it (the caller joins it before the optimizer) and only the data gradient stays on the chain.
+        ``defer`` (a list, with ``ws``): the wgrad launch is appended to it instead, for the caller to issue on ws
+        after ONE fork for several layers ([FORK-GROUP])."""
         if not self.hip:
             return self._torch_bwd(dy, x, theta, grads, G, need_dx)
         m = ops.ext()
@@ -306,9 +308,12 @@ class GroupedConv:
         else:
             # the branch (raw stream ws) reads x / dy / ptab: they stay referenced until the caller joins it (no
             # record_stream: its deferred frees are not capturable and pile up on large steps)
-            m.stream_fork(_stream(), ws)
             self._keep.extend((x, dy, ptab))
-            self._wgrad(m, x, dy, grads, G, B, H, W, ns, ptab, ws)
+            if defer is not None:
+                defer.append(lambda: self._wgrad(m, x, dy, grads, G, B, H, W, ns, ptab, ws))
+            else:
+                m.stream_fork(_stream(), ws)
+                self._wgrad(m, x, dy, grads, G, B, H, W, ns, ptab, ws)
         st = _stream()
         if not need_dx:
             return None
@@ -411,6 +416,9 @@ _PACK_FUSE = os.environ.get("NIDT_PACK_FUSE", "1") != "0"
 # slower than k_pack_trans overlapped on the weight-gradient side stream (CIFAR SubAvg -2.4 %, DisPFL -4.5 %; with
 # 16-channel tiles -0.3 / -2.8 %; profiles/r6_pack_wt.txt) — the optimizer is on the critical path, the transposes are not
 _PACK_WT = os.environ.get("NIDT_PACK_WT", "0") == "1"
+# [FORK-GROUP] NIDT_FORK_GROUP=1: one fork of the weight-gradient branch per residual block (its wgrads and GroupNorm
+# parameter sums issued together after the block's data-gradient chain) instead of one per layer (A/B)
+_FORK_GROUP = os.environ.get("NIDT_FORK_GROUP", "1") == "1"
 # [STEM-FOLD] the 3-channel stem as a 1x1 conv over the window-folded input (img.hip k_img_fold); NIDT_STEM_FOLD=0:
 # the channel-padded 9-tap conv (A/B)
 _STEM_FOLD = os.environ.get("NIDT_STEM_FOLD", "1") != "0"
@@ -589,7 +597,7 @@ class GroupNormG:
             y = torch.relu(y)
         return y.to(t.dtype), (mean, rstd)
 
-    def bwd(self, dy, mask, t, saved, theta, grads, G, ws=None):
+    def bwd(self, dy, mask, t, saved, theta, grads, G, ws=None, defer=None):
         """dy [N, H, W, C] (fp32 or bf16), times (mask > 0) if a mask is given; writes the dgamma/dbeta rows,
         returns dt in t's dtype.  ``ws``: raw handle of the weight-gradient branch stream — the per-client dgamma/dbeta sum
         (off the data-gradient chain) is forked onto it."""
@@ -608,10 +616,16 @@ class GroupNormG:
                 ops.ext().gn_param_grads(part.data_ptr(), G, B, C, grads.data_ptr(), grads.stride(0), self.off_w,
                                          self.off_b, _stream())
                 return dt
-            ops.ext().stream_fork(_stream(), ws)
             GroupedConv._keep.append(part)
-            ops.ext().gn_param_grads(part.data_ptr(), G, B, C, grads.data_ptr(), grads.stride(0), self.off_w,
-                                     self.off_b, ws)
+
+            def side():
+                ops.ext().gn_param_grads(part.data_ptr(), G, B, C, grads.data_ptr(), grads.stride(0), self.off_w,
+                                         self.off_b, ws)
+            if defer is not None:  # [FORK-GROUP] issued by the caller after its one fork
+                defer.append(side)
+            else:
+                ops.ext().stream_fork(_stream(), ws)
+                side()
             return dt
         mean, rstd = saved
         cg = C // GN_GROUPS
@@ -791,14 +805,19 @@ class GroupedResNet18GN:
             ops.ext().stream_fork(ws, _stream())  # the dgrad images (pack_trans on the branch)
         for blk, sv in zip(reversed(self.blocks), reversed(saved[1:])):
             xin, t1, s1, h1, t2, s2, ts, ss, a = sv
-            dt2 = blk["n2"].bwd(da, a, t2, s2, theta, grads, G, ws=ws)
-            dh1 = blk["c2"].bwd(dt2, h1, theta, grads, G, True, ws=ws)
-            dt1 = blk["n1"].bwd(dh1, h1, t1, s1, theta, grads, G, ws=ws)
-            dx1 = blk["c1"].bwd(dt1, xin, theta, grads, G, True, ws=ws)
+            dfr = [] if (ws is not None and _FORK_GROUP) else None
+            dt2 = blk["n2"].bwd(da, a, t2, s2, theta, grads, G, ws=ws, defer=dfr)
+            dh1 = blk["c2"].bwd(dt2, h1, theta, grads, G, True, ws=ws, defer=dfr)
+            dt1 = blk["n1"].bwd(dh1, h1, t1, s1, theta, grads, G, ws=ws, defer=dfr)
+            dx1 = blk["c1"].bwd(dt1, xin, theta, grads, G, True, ws=ws, defer=dfr)
             dx2 = None
             if "cs" in blk:
-                dts = blk["ns"].bwd(da, a, ts, ss, theta, grads, G, ws=ws)
-                dx2 = blk["cs"].bwd(dts, xin, theta, grads, G, True, ws=ws)
+                dts = blk["ns"].bwd(da, a, ts, ss, theta, grads, G, ws=ws, defer=dfr)
+                dx2 = blk["cs"].bwd(dts, xin, theta, grads, G, True, ws=ws, defer=dfr)
+            if dfr:  # [FORK-GROUP] the block's weight-gradient work: one fork, then every launch on the branch
+                ops.ext().stream_fork(_stream(), ws)
+                for f in dfr:
+                    f()
             half = dx2 is not None and blk["cs"].stride == 2  # 1x1 stride-2 projection: even-pixel gradient
             if self.hip:
                 out = torch.empty(dx1.shape, device=dx1.device, dtype=torch.bfloat16)
