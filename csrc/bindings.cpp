@@ -114,6 +114,9 @@ void pack_conv_wk(uintptr_t theta, int64_t ldt, int64_t off, int G, int Cout, in
 // gn.hip
 void gn_fwd(uintptr_t t, uintptr_t res, uintptr_t theta, int64_t ldt, int64_t off_w, int64_t off_b, uintptr_t y,
             uintptr_t stats, int N, int B, int S, int C, int relu, uintptr_t stream);
+void gn_bwd_rm(uintptr_t dy, int dy_bf16, uintptr_t t, uintptr_t stats, uintptr_t theta, int64_t ldt, int64_t off_w,
+               int64_t off_b, uintptr_t dt, uintptr_t part, int N, int B, int S, int C, uintptr_t stream);
+int gn_rm_ok(int S, int C);
 void gn_bwd(uintptr_t dy, int dy_bf16, uintptr_t mask, uintptr_t t, uintptr_t stats, uintptr_t theta, int64_t ldt,
             int64_t off_w, uintptr_t dt, uintptr_t part, int N, int B, int S, int C, uintptr_t stream);
 void gn_param_grads(uintptr_t part, int G, int B, int C, uintptr_t grads, int64_t ldg, int64_t off_w, int64_t off_b,
@@ -326,6 +329,8 @@ PYBIND11_MODULE(_nidt_hip, m) {
   DEF(pack_conv_wk);
   DEF(gn_fwd);
   DEF(gn_bwd);
+  DEF(gn_bwd_rm);
+  DEF(gn_rm_ok);
   DEF(gn_param_grads);
   DEF(res_grad_om);
   DEF(res_grad_s2_om);

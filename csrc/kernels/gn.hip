@@ -199,13 +199,17 @@ __global__ __launch_bounds__(kGnThreads, 4) void k_gn_fwd(const uint16_t* __rest
 // dy: fp32 (DYB = false) or bf16; mask (optional, bf16 post-ReLU activation): dy *= (mask > 0).
 // [GN-REG] HOLD (bf16 dy): t and the masked dy are read once and held packed; otherwise t is held and dy (and the
 // mask) are read again by the apply pass (fewer registers: more resident blocks for the 16-row samples).
-template <int NV, bool DYB, bool MASK, bool HOLD>
+// [GN-RMASK] RM: the ReLU mask of a GroupNorm WITHOUT residual (y = relu(gamma xhat + beta)) recomputed from the held t
+// and the saved statistics with the forward's own arithmetic (sc = gamma rstd, sh = beta - mu sc, y > 0 <=>
+// fma(t, sc, sh) > 0): no mask tensor read, the same dt bit for bit (off_b = the beta offset).
+template <int NV, bool DYB, bool MASK, bool HOLD, bool RM = false>
 __global__ __launch_bounds__(kGnThreads, (HOLD || NV >= 16) ? 2 : 4) void k_gn_bwd(const void* __restrict__ dyv, const uint16_t* __restrict__ mask,
                                                        const uint16_t* __restrict__ t, const float* __restrict__ stats,
                                                        const float* __restrict__ theta, int64_t ldt, int64_t off_w,
                                                        uint16_t* __restrict__ dt, float* __restrict__ part_out, int B,
-                                                       int S, int C) {
+                                                       int S, int C, int64_t off_b = 0) {
   static_assert(!HOLD || DYB, "k_gn_bwd: held dy is bf16");
+  static_assert(!(RM && MASK), "k_gn_bwd: one mask source");
   __shared__ __attribute__((aligned(16))) float red[kGnThreads / 64 * 512];
   __shared__ float chA[512], chB[512];
   __shared__ float gm1[kGnGroups], gm2[kGnGroups];
@@ -216,14 +220,24 @@ __global__ __launch_bounds__(kGnThreads, (HOLD || NV >= 16) ? 2 : 4) void k_gn_b
   const int j = tid % nch;
   const int cg = C / kGnGroups;
   const int vo = tid * 16;
-  float mu[8], rs[8], gw[8];
+  float mu[8], rs[8], gw[8], msc[8], msh[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
     const int c = 8 * j + e;
     mu[e] = stats[((int64_t)n * kGnGroups + c / cg) * 2];
     rs[e] = stats[((int64_t)n * kGnGroups + c / cg) * 2 + 1];
     gw[e] = theta[(int64_t)g * ldt + off_w + c];
+    if (RM) {  // k_gn_fwd's coefficients, same expressions
+      msc[e] = gw[e] * rs[e];
+      msh[e] = theta[(int64_t)g * ldt + off_b + c] - mu[e] * msc[e];
+    }
   }
+  auto rmask = [&](const float* f, float* d) {  // [GN-RMASK] dy *= (relu input > 0)
+    if (RM) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) d[e] = fmaf(f[e], msc[e], msh[e]) > 0.f ? d[e] : 0.f;
+    }
+  };
   const i32x4_t rt = make_rsrc(t + base, bytes);
   i32x4_t rm, rd;
   if (MASK) rm = make_rsrc(mask + base, bytes);
@@ -290,6 +304,7 @@ __global__ __launch_bounds__(kGnThreads, (HOLD || NV >= 16) ? 2 : 4) void k_gn_b
     unpack8(as_u4(v[k]), f);
     if constexpr (HOLD) unpack8(as_u4(dv[k]), d);
     else load_d(k, d);
+    rmask(f, d);
     if (tid + k * kGnThreads < nchunk) {  // rows past the sample: dy reads zero, but (f - mu) does not
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
@@ -332,6 +347,7 @@ __global__ __launch_bounds__(kGnThreads, (HOLD || NV >= 16) ? 2 : 4) void k_gn_b
     unpack8(as_u4(v[k]), f);
     if constexpr (HOLD) unpack8(as_u4(dv[k]), d);
     else load_d(k, d);
+    rmask(f, d);
     i32x4_t o;
     int* op = reinterpret_cast<int*>(&o);
 #pragma unroll
@@ -776,6 +792,40 @@ void gn_bwd(uintptr_t dy, int dy_bf16, uintptr_t mask, uintptr_t t, uintptr_t st
   }
 #undef GNB_DM
 #undef GNB
+  NIDT_CHECK(hipGetLastError());
+}
+
+// [GN-RMASK] gn_bwd of a GroupNorm + ReLU without residual, the ReLU mask recomputed from t (no mask tensor); the
+// register-resident shapes only (gn_rm_ok), the streaming ones keep the mask tensor
+int gn_rm_ok(int S, int C) { return gn_streaming(S, C) ? 0 : 1; }
+
+void gn_bwd_rm(uintptr_t dy, int dy_bf16, uintptr_t t, uintptr_t stats, uintptr_t theta, int64_t ldt, int64_t off_w,
+               int64_t off_b, uintptr_t dt, uintptr_t part, int N, int B, int S, int C, uintptr_t stream) {
+  gn_check(N, B, S, C, "gn_bwd_rm");
+  NIDT_REQUIRE(!gn_streaming(S, C), "gn_bwd_rm: register-resident shapes only (gn_rm_ok)");
+  hipStream_t s = as_stream(stream);
+  const int nv = gn_nv(S, C);
+  static const int hold_max = [] {
+    const char* e = getenv("NIDT_GN_HOLD");
+    return e ? atoi(e) : 4;
+  }();
+  const bool hold = dy_bf16 && nv <= hold_max;
+#define GNR(NVV, DB, H)                                                                                        \
+  hipLaunchKernelGGL((k_gn_bwd<NVV, DB, false, H, true>), dim3(N), dim3(kGnThreads), 0, s, ptr<const void>(dy), \
+                     nullptr, ptr<const uint16_t>(t), ptr<const float>(stats), ptr<const float>(theta), ldt, off_w,  \
+                     ptr<uint16_t>(dt), ptr<float>(part), B, S, C, off_b)
+#define GNR_D(NVV)                                                                                             \
+  if (dy_bf16) { if (hold) GNR(NVV, true, true); else GNR(NVV, true, false); }                                 \
+  else GNR(NVV, false, false);
+  switch (nv) {
+    case 1: GNR_D(1) break;
+    case 2: GNR_D(2) break;
+    case 4: GNR_D(4) break;
+    case 8: GNR_D(8) break;
+    default: GNR_D(16) break;
+  }
+#undef GNR_D
+#undef GNR
   NIDT_CHECK(hipGetLastError());
 }
 

@@ -419,6 +419,11 @@ _PACK_WT = os.environ.get("NIDT_PACK_WT", "0") == "1"
 # [FORK-GROUP] NIDT_FORK_GROUP=1: one fork of the weight-gradient branch per residual block (its wgrads and GroupNorm
 # parameter sums issued together after the block's data-gradient chain) instead of one per layer (A/B)
 _FORK_GROUP = os.environ.get("NIDT_FORK_GROUP", "1") == "1"
+# [GN-RMASK] the GroupNorm+ReLU backward of each block's first norm recomputes its ReLU mask from t (no mask read);
+# [OMASK] the residual-gradient pass applies the previous block's output ReLU mask, so the block's second norm and
+# shortcut norm backward read none either.  NIDT_GN_RMASK=0 / NIDT_OMASK2D=0: the mask tensors (A/B)
+_GN_RMASK = os.environ.get("NIDT_GN_RMASK", "1") != "0"
+_OMASK2D = os.environ.get("NIDT_OMASK2D", "1") != "0"
 # [STEM-FOLD] the 3-channel stem as a 1x1 conv over the window-folded input (img.hip k_img_fold); NIDT_STEM_FOLD=0:
 # the channel-padded 9-tap conv (A/B)
 _STEM_FOLD = os.environ.get("NIDT_STEM_FOLD", "1") != "0"
@@ -597,10 +602,11 @@ class GroupNormG:
             y = torch.relu(y)
         return y.to(t.dtype), (mean, rstd)
 
-    def bwd(self, dy, mask, t, saved, theta, grads, G, ws=None, defer=None):
+    def bwd(self, dy, mask, t, saved, theta, grads, G, ws=None, defer=None, rmask=False):
         """dy [N, H, W, C] (fp32 or bf16), times (mask > 0) if a mask is given; writes the dgamma/dbeta rows,
         returns dt in t's dtype.  ``ws``: raw handle of the weight-gradient branch stream — the per-client dgamma/dbeta sum
-        (off the data-gradient chain) is forked onto it."""
+        (off the data-gradient chain) is forked onto it.  ``rmask``: ``mask`` is this GroupNorm's own ReLU output
+        (no residual), so the HIP kernel recomputes it from t and the statistics instead of reading it ([GN-RMASK])."""
         N, H, W, C = t.shape
         B = N // G
         if self.hip:
@@ -608,10 +614,15 @@ class GroupNormG:
             assert dy.dtype in (torch.float32, torch.bfloat16)
             dt = torch.empty_like(t)
             part = torch.empty(N, C, 2, device=t.device, dtype=torch.float32)
-            m = mask.contiguous() if mask is not None else None
-            ops.ext().gn_bwd(dy.data_ptr(), int(dy.dtype == torch.bfloat16), m.data_ptr() if m is not None else 0,
-                             t.data_ptr(), saved.data_ptr(), theta.data_ptr(), theta.stride(0), self.off_w,
-                             dt.data_ptr(), part.data_ptr(), N, B, H * W, C, _stream())
+            if rmask and mask is not None and _GN_RMASK and ops.ext().gn_rm_ok(H * W, C):
+                ops.ext().gn_bwd_rm(dy.data_ptr(), int(dy.dtype == torch.bfloat16), t.data_ptr(), saved.data_ptr(),
+                                    theta.data_ptr(), theta.stride(0), self.off_w, self.off_b, dt.data_ptr(),
+                                    part.data_ptr(), N, B, H * W, C, _stream())
+            else:
+                m = mask.contiguous() if mask is not None else None
+                ops.ext().gn_bwd(dy.data_ptr(), int(dy.dtype == torch.bfloat16), m.data_ptr() if m is not None else 0,
+                                 t.data_ptr(), saved.data_ptr(), theta.data_ptr(), theta.stride(0), self.off_w,
+                                 dt.data_ptr(), part.data_ptr(), N, B, H * W, C, _stream())
             if ws is None:
                 ops.ext().gn_param_grads(part.data_ptr(), G, B, C, grads.data_ptr(), grads.stride(0), self.off_w,
                                          self.off_b, _stream())
@@ -803,16 +814,20 @@ class GroupedResNet18GN:
         losses, da = self._head_train(a, theta, grads, y, G, B)
         if ws is not None:
             ops.ext().stream_fork(ws, _stream())  # the dgrad images (pack_trans on the branch)
+        # [OMASK] dm: da is already multiplied by this block's output ReLU mask (a > 0) — the previous residual-gradient
+        # pass applied it — so the block's n2 / shortcut GroupNorm backward read no mask tensor
+        dm = False
         for blk, sv in zip(reversed(self.blocks), reversed(saved[1:])):
             xin, t1, s1, h1, t2, s2, ts, ss, a = sv
+            am = None if dm else a
             dfr = [] if (ws is not None and _FORK_GROUP) else None
-            dt2 = blk["n2"].bwd(da, a, t2, s2, theta, grads, G, ws=ws, defer=dfr)
+            dt2 = blk["n2"].bwd(da, am, t2, s2, theta, grads, G, ws=ws, defer=dfr)
             dh1 = blk["c2"].bwd(dt2, h1, theta, grads, G, True, ws=ws, defer=dfr)
-            dt1 = blk["n1"].bwd(dh1, h1, t1, s1, theta, grads, G, ws=ws, defer=dfr)
+            dt1 = blk["n1"].bwd(dh1, h1, t1, s1, theta, grads, G, ws=ws, defer=dfr, rmask=True)
             dx1 = blk["c1"].bwd(dt1, xin, theta, grads, G, True, ws=ws, defer=dfr)
             dx2 = None
             if "cs" in blk:
-                dts = blk["ns"].bwd(da, a, ts, ss, theta, grads, G, ws=ws, defer=dfr)
+                dts = blk["ns"].bwd(da, am, ts, ss, theta, grads, G, ws=ws, defer=dfr)
                 dx2 = blk["cs"].bwd(dts, xin, theta, grads, G, True, ws=ws, defer=dfr)
             if dfr:  # [FORK-GROUP] the block's weight-gradient work: one fork, then every launch on the branch
                 ops.ext().stream_fork(_stream(), ws)
@@ -821,23 +836,25 @@ class GroupedResNet18GN:
             half = dx2 is not None and blk["cs"].stride == 2  # 1x1 stride-2 projection: even-pixel gradient
             if self.hip:
                 out = torch.empty(dx1.shape, device=dx1.device, dtype=torch.bfloat16)
+                om = xin.data_ptr() if _OMASK2D else 0  # [OMASK] the previous block's (or the stem's) ReLU output
                 if half:
                     Nn, Hh, Ww, Cc = dx1.shape
-                    ops.ext().res_grad_s2(out.data_ptr(), dx1.data_ptr(), dx2.data_ptr(), Nn, 1, Hh, Ww, Cc, 1,
-                                          _stream())
+                    ops.ext().res_grad_s2_om(out.data_ptr(), dx1.data_ptr(), dx2.data_ptr(), om, Nn, 1, Hh, Ww, Cc, 1,
+                                             _stream())
                 else:
-                    ops.ext().res_grad(out.data_ptr(), dx1.data_ptr(), dx2.data_ptr() if dx2 is not None else 0,
-                                       0 if dx2 is not None else da.data_ptr(),
-                                       0 if dx2 is not None else a.data_ptr(), out.numel(),
-                                       1 | (2 if da.dtype == torch.bfloat16 else 0), _stream())
+                    ops.ext().res_grad_om(out.data_ptr(), dx1.data_ptr(), dx2.data_ptr() if dx2 is not None else 0,
+                                          0 if dx2 is not None else da.data_ptr(),
+                                          0 if (dx2 is not None or dm) else a.data_ptr(), om, out.numel(),
+                                          1 | (2 if da.dtype == torch.bfloat16 else 0), _stream())
                 da = out
+                dm = bool(om)
             elif half:
                 da = dx1.float().clone()
                 da[:, ::2, ::2] += dx2.float()
             else:
                 da = dx1.float() + (dx2.float() if dx2 is not None else da * (a > 0))
         x0, t0, st0, a0 = saved[0]
-        dt0 = self.stem_gn.bwd(da, a0, t0, st0, theta, grads, G, ws=ws)
+        dt0 = self.stem_gn.bwd(da, None if dm else a0, t0, st0, theta, grads, G, ws=ws)
         self.stem.bwd(dt0, x0, theta, grads, G, False, ws=ws)
         if ws is not None:
             ops.ext().stream_fork(ws, _stream())  # join: the optimizer reads every weight gradient

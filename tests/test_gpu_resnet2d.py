@@ -476,3 +476,36 @@ def test_unpack_bits_kernel_matches_torch(P):
         got = MK.unpack_bits(bits.to(dev), P, dt).cpu()
         assert torch.equal(got, MK.unpack_bits(bits, P, dt)), dt
         assert torch.equal(got.bool(), keep)
+
+
+def test_gn_recomputed_masks_bit_identical(monkeypatch):
+    """[GN-RMASK] + [OMASK]: the block's first GroupNorm backward recomputing its ReLU mask from t, and the residual
+    gradient carrying the previous block's output mask (so the second / shortcut norms read no mask), give the same
+    loss and gradient rows bit for bit as the mask-tensor backward (CIFAR and Tiny map sizes)."""
+    from neuroimagedisttraining_amd.engine import resnet2d_hip as R
+    from neuroimagedisttraining_amd.engine.executor import padded_rows
+    from neuroimagedisttraining_amd.models import customized_resnet18
+    dev = _dev()
+    for hw in (32, 64):
+        G, B = 3, 4
+        g = np.random.default_rng(hw)
+        x8 = torch.from_numpy(g.integers(0, 256, size=(G * B, hw, hw, 3)).astype(np.uint8))
+        y = torch.from_numpy(g.integers(0, 10, size=G * B))
+        m = customized_resnet18(class_num=10)
+        P = sum(p.numel() for p in m.parameters())
+        flat = torch.cat([p.detach().reshape(-1) for p in m.parameters()]).to(dev)
+        res = []
+        for on in (False, True):
+            monkeypatch.setattr(R, "_GN_RMASK", on)
+            monkeypatch.setattr(R, "_OMASK2D", on)
+            eng = R.ResNetHipEngine(m, x8, y, dev)
+            th, gr = padded_rows(G, P, dev), padded_rows(G, P, dev)
+            th.copy_(flat.expand(G, -1))
+            gr.zero_()
+            idx = torch.arange(G * B, dtype=torch.int32, device=dev)
+            loss = eng.train_step(th, None, gr, idx, G, B, 1.0, 0)
+            torch.cuda.synchronize()
+            res.append((loss.clone(), gr.clone()))
+        assert torch.equal(res[0][0], res[1][0]), hw
+        assert torch.isfinite(res[1][1]).all() and float(res[1][1].abs().sum()) > 0
+        assert torch.equal(res[0][1], res[1][1]), (hw, float((res[0][1] - res[1][1]).abs().max()))
