@@ -766,11 +766,12 @@ void gn_bwd(uintptr_t dy, int dy_bf16, uintptr_t mask, uintptr_t t, uintptr_t st
     return;
   }
   const int nv = gn_nv(S, C);
-  // [GN-REG] hold the bf16 dy in registers up to NIDT_GN_HOLD rows per thread (default 4: at 8 rows holding costs the
-  // second resident block, at 16 it spills; A/B with NIDT_GN_HOLD=8)
+  // [GN-REG] hold the bf16 dy in registers up to NIDT_GN_HOLD rows per thread (round 5: 4 — at 8 rows holding cost
+  // the second resident block; round 6, with the ReLU masks no longer read here ([GN-RMASK], [OMASK]): 16, CIFAR SubAvg
+  // +0.8 %, DisPFL +0.2 % vs 4, profiles/r6_gn_masks.txt)
   static const int hold_max = [] {
     const char* e = getenv("NIDT_GN_HOLD");
-    return e ? atoi(e) : 4;
+    return e ? atoi(e) : 16;
   }();
   const bool hold = dy_bf16 && nv <= hold_max;
 #define GNB(NVV, DB, M)                                                                                        \
@@ -807,7 +808,7 @@ void gn_bwd_rm(uintptr_t dy, int dy_bf16, uintptr_t t, uintptr_t stats, uintptr_
   const int nv = gn_nv(S, C);
   static const int hold_max = [] {
     const char* e = getenv("NIDT_GN_HOLD");
-    return e ? atoi(e) : 4;
+    return e ? atoi(e) : 16;
   }();
   const bool hold = dy_bf16 && nv <= hold_max;
 #define GNR(NVV, DB, H)                                                                                        \
