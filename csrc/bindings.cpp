@@ -78,6 +78,10 @@ void conv2d_fwd_slab_bd_table(uintptr_t tab, int B, int H, int W, int Cin, int C
 void conv2d_fwd_slab_bd(uintptr_t x, uintptr_t w, uintptr_t y, int G, int B, int H, int W, int Cin, int Cout,
                         uintptr_t utab, uintptr_t stream);
 int conv2d_fwd_slab_pick(int G, int B, int H, int W, int Cin, int Cout);
+void conv2d_fwd_slab_stats(uintptr_t x, uintptr_t w, uintptr_t zb, uintptr_t y, uintptr_t stats, int G, int B, int H,
+                           int W, int Cin, int Cout, uintptr_t utab, uintptr_t stream);
+void gn_apply(uintptr_t t, uintptr_t res, uintptr_t part, int nb, int bp, uintptr_t theta, int64_t ldt, int64_t off_w,
+              int64_t off_b, uintptr_t y, uintptr_t stats, int N, int B, int S, int C, int relu, uintptr_t stream);
 void conv2d_fwd_slab(uintptr_t x, uintptr_t w, uintptr_t y, int G, int B, int H, int W, int Cin, int Cout,
                      uintptr_t utab, uintptr_t stream);
 int conv3d_slab_umax(int B, int D, int H, int W, int pad);
@@ -306,6 +310,8 @@ PYBIND11_MODULE(_nidt_hip, m) {
   DEF(conv2d_fwd_slab_bd);
   DEF(conv2d_fwd_slab_pick);
   DEF(conv2d_fwd_slab);
+  DEF(conv2d_fwd_slab_stats);
+  DEF(gn_apply);
   DEF(conv3d_wgrad_tri_nsplit);
   DEF(conv3d_wgrad_tri_table);
   DEF(conv3d_wgrad_tri_ok);

@@ -1719,6 +1719,16 @@ void conv2d_fwd_slab(uintptr_t x, uintptr_t w, uintptr_t y, int G, int B, int H,
   fwd_slab_impl(x, w, 0, 0, y, 0, G, B, 1, H, W, Cin, Cout, 1, 9, utab, stream);
 }
 
+// [GN-EPI] the same conv with the per-block channel statistics (mean, M2 over the block's 256 positions, from the fp32
+// accumulators) written to stats [G][nPB][Cout][2] by the shared epilogue: every block lies inside one sample (H W %
+// 256 == 0), so a sample's blocks pb = n (H W / 256) .. are its GroupNorm partials (gn.hip gn_apply).  The epilogue's
+// statistics need its bias path: zb is a [G][Cout] zero bias (the ResNet convs have none)
+void conv2d_fwd_slab_stats(uintptr_t x, uintptr_t w, uintptr_t zb, uintptr_t y, uintptr_t stats, int G, int B, int H,
+                           int W, int Cin, int Cout, uintptr_t utab, uintptr_t stream) {
+  NIDT_REQUIRE(conv2d_fwd_slab_ok(B, H, W, Cin, Cout) && zb != 0 && stats != 0, "conv2d_fwd_slab_stats: shape");
+  fwd_slab_impl(x, w, zb, 0, y, stats, G, B, 1, H, W, Cin, Cout, 1, 9, utab, stream);
+}
+
 // [SLAB-BD] 2-D 3x3 stride-1 pad-1 convs on maps whose 256-position blocks span several samples (8x8: four samples
 // per block; the CIFAR / Tiny ResNet-18 layer 3 and the 16x16 / 8x8 maps of the Tiny layers): the client's B samples
 // are the depth planes of ONE volume [1][B][H][W] and the conv is the 3-D slab conv restricted to depth tap kd = 1

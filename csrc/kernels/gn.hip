@@ -796,6 +796,98 @@ void gn_bwd(uintptr_t dy, int dy_bf16, uintptr_t mask, uintptr_t t, uintptr_t st
   NIDT_CHECK(hipGetLastError());
 }
 
+// [GN-EPI] GroupNorm forward from the producing conv's epilogue statistics: part [N * nb][C][2] = (mean, M2) of each
+// channel over each of the sample's nb blocks of bp positions (conv2d_fwd_slab_stats).  The sample's 32 group
+// statistics are combined from them (Chan: mean = the mean of the block means, M2 = sum M2 + bp sum (block mean -
+// mean)^2, population variance as k_gn_fwd), then normalisation + affine (+ residual) (+ ReLU) is a pure streaming
+// pass over many blocks per sample: no reduction phases between the sample's load and store, the grid fills the chip
+// (k_gn_fwd: one block per sample, its phases serialised).  Block (sample n, chunk range); block 0 of a sample writes
+// the saved (mean, rstd).  sc / sh exactly as k_gn_fwd (the backward's [GN-RMASK] recomputes them).
+constexpr int kGnApplyThreads = 256, kGnApplyChunks = 4;  // 16-B chunks per thread
+template <bool RES, bool RELU>
+__global__ __launch_bounds__(kGnApplyThreads) void k_gn_apply(const uint16_t* __restrict__ t,
+                                                              const uint16_t* __restrict__ res,
+                                                              const float* __restrict__ part, int nb, float bp,
+                                                              const float* __restrict__ theta, int64_t ldt,
+                                                              int64_t off_w, int64_t off_b, uint16_t* __restrict__ y,
+                                                              float* __restrict__ stats, int B, int S, int C, int nblk) {
+  __shared__ float gmean[kGnGroups], grstd[kGnGroups];
+  const int n = blockIdx.x / nblk, q = blockIdx.x - n * nblk, g = n / B, tid = threadIdx.x;
+  const int cg = C / kGnGroups;
+  if (tid < kGnGroups) {  // group statistics of sample n (fixed order: deterministic)
+    const float* pp = part + (int64_t)n * nb * C * 2;
+    const int k = nb * cg;
+    float m = 0.f;
+    for (int b = 0; b < nb; ++b)
+      for (int i = 0; i < cg; ++i) m += pp[((int64_t)b * C + tid * cg + i) * 2];
+    m /= (float)k;
+    float m2 = 0.f;
+    for (int b = 0; b < nb; ++b)
+      for (int i = 0; i < cg; ++i) {
+        const float* e = pp + ((int64_t)b * C + tid * cg + i) * 2;
+        const float d = e[0] - m;
+        m2 += e[1] + bp * d * d;
+      }
+    const float rs = rsqrtf(m2 / (bp * (float)k) + kGnEps);
+    gmean[tid] = m;
+    grstd[tid] = rs;
+    if (q == 0) {
+      stats[((int64_t)n * kGnGroups + tid) * 2] = m;
+      stats[((int64_t)n * kGnGroups + tid) * 2 + 1] = rs;
+    }
+  }
+  __syncthreads();
+  const int nch = C >> 3;
+  const int64_t base = (int64_t)n * S * C;
+  const int nchunk = S * nch;
+  const float* gw = theta + (int64_t)g * ldt + off_w;
+  const float* gb = theta + (int64_t)g * ldt + off_b;
+#pragma unroll
+  for (int k = 0; k < kGnApplyChunks; ++k) {
+    const int ch = (q * kGnApplyChunks + k) * kGnApplyThreads + tid;  // 16-B chunk of the sample
+    if (ch >= nchunk) break;
+    const int j = ch % nch;  // 8-channel column
+    float f[8], r[8];
+    unpack8(*reinterpret_cast<const uint4*>(t + base + (int64_t)ch * 8), f);
+    if (RES) unpack8(*reinterpret_cast<const uint4*>(res + base + (int64_t)ch * 8), r);
+    uint32_t o[4];
+#pragma unroll
+    for (int e = 0; e < 8; e += 2) {
+      float v[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int c = 8 * j + e + h;
+        const float mu = gmean[c / cg];
+        const float sc = gw[c] * grstd[c / cg];
+        const float sh = gb[c] - mu * sc;
+        float a = fmaf(f[e + h], sc, sh);
+        if (RES) a += r[e + h];
+        if (RELU) a = fmaxf(a, 0.f);
+        v[h] = a;
+      }
+      o[e >> 1] = pack_bf16x2(v[0], v[1]);
+    }
+    *reinterpret_cast<uint4*>(y + base + (int64_t)ch * 8) = make_uint4(o[0], o[1], o[2], o[3]);
+  }
+}
+
+void gn_apply(uintptr_t t, uintptr_t res, uintptr_t part, int nb, int bp, uintptr_t theta, int64_t ldt, int64_t off_w,
+              int64_t off_b, uintptr_t y, uintptr_t stats, int N, int B, int S, int C, int relu, uintptr_t stream) {
+  gn_check(N, B, S, C, "gn_apply");
+  NIDT_REQUIRE(nb >= 1 && bp >= 1 && (int64_t)nb * bp == S && part != 0, "gn_apply: partials must tile the sample");
+  const int nchunk = S * (C >> 3);
+  const int nblk = ceil_div(nchunk, kGnApplyThreads * kGnApplyChunks);
+  hipStream_t s = as_stream(stream);
+#define GNA(R, L)                                                                                              \
+  hipLaunchKernelGGL((k_gn_apply<R, L>), dim3((unsigned)((int64_t)N * nblk)), dim3(kGnApplyThreads), 0, s,       \
+                     ptr<const uint16_t>(t), ptr<const uint16_t>(res), ptr<const float>(part), nb, (float)bp,    \
+                     ptr<const float>(theta), ldt, off_w, off_b, ptr<uint16_t>(y), ptr<float>(stats), B, S, C, nblk)
+  if (res) { if (relu) GNA(true, true); else GNA(true, false); }
+  else { if (relu) GNA(false, true); else GNA(false, false); }
+#undef GNA
+  NIDT_CHECK(hipGetLastError());
+}
+
 // [GN-RMASK] gn_bwd of a GroupNorm + ReLU without residual, the ReLU mask recomputed from t (no mask tensor); the
 // register-resident shapes only (gn_rm_ok), the streaming ones keep the mask tensor
 int gn_rm_ok(int S, int C) { return gn_streaming(S, C) ? 0 : 1; }

@@ -142,11 +142,12 @@ def conv_fwd(x_ptr, w_ptr, y_ptr, G, B, D, H, W, Cin, Cout, kt, st, pad, padd, d
 _SLAB_TABS = {}
 
 
-def slab_conv2d(x_ptr, w_ptr, y_ptr, G, B, H, W, Cin, Cout, device):
+def slab_conv2d(x_ptr, w_ptr, y_ptr, G, B, H, W, Cin, Cout, device, stats=None):
     """3x3 stride-1 pad-1 conv through the kd-slab union kernel (``conv2d_fwd_slab``: one input union per 64-channel
     chunk serves all nine taps) when the shape and grid qualify (``conv2d_fwd_slab_pick``; ``NIDT_2D_SLAB=0`` keeps
     the per-tap kernels); returns False otherwise.  The union table depends on the shape only and is built once per
-    (B, H, W)."""
+    (B, H, W).  ``stats`` = (zero-bias ptr, partials ptr): [GN-EPI] the 256-position slab form also writes the
+    per-block channel statistics (returns 2 then; the depth-batched form has blocks spanning samples and writes none)."""
     m = ops.ext()
     if not m.conv2d_fwd_slab_pick(G, B, H, W, Cin, Cout):
         if not m.conv2d_fwd_slab_bd_pick(G, B, H, W, Cin, Cout):
@@ -171,6 +172,10 @@ def slab_conv2d(x_ptr, w_ptr, y_ptr, G, B, H, W, Cin, Cout, device):
             # the cached table is read by launches on other streams (side lanes): complete it before sharing it
             torch.cuda.current_stream().synchronize()
             _SLAB_TABS[key] = tab
+    if stats is not None:
+        m.conv2d_fwd_slab_stats(x_ptr, w_ptr, stats[0], y_ptr, stats[1], G, B, H, W, Cin, Cout, tab.data_ptr(),
+                                _stream())
+        return 2
     m.conv2d_fwd_slab(x_ptr, w_ptr, y_ptr, G, B, H, W, Cin, Cout, tab.data_ptr(), _stream())
     return True
 
@@ -220,6 +225,8 @@ class GroupedConv:
         # K = 27 (padded to cin_p) with the folded weight image [Cout][27 -> cin_p]
         self.fold = False
         self._wf = {}  # folded weight image per G (persistent: its zero tail is written once)
+        self._zb = {}  # [GN-EPI] zero bias per G (the statistics epilogue runs on the bias path)
+        self.gn_part = None
 
     def geometry(self):
         """(taps, stride, pad) of the launches: the folded stem is a 1x1 stride-1 conv."""
@@ -252,9 +259,13 @@ class GroupedConv:
         return theta[:, self.off:self.off + self.numel].reshape(G * self.cout, self.cin, self.k, self.k)
 
     # ---------------------------------------------------------------- forward
-    def fwd(self, x, theta, G, train=False, packed=False):
+    def fwd(self, x, theta, G, train=False, packed=False, gn_stats=False):
         """``packed``: the network's WeightPacker has packed this step's images (``self.wp`` / ``self.wt``);
-        otherwise (standalone layer) the layer packs its own, incl. the dgrad image when ``train``."""
+        otherwise (standalone layer) the layer packs its own, incl. the dgrad image when ``train``.  ``gn_stats``
+        ([GN-EPI]): when the layer runs on the 256-position slab kernel, its epilogue also writes the per-block channel
+        statistics of the output for the GroupNorm that follows (``self.gn_part`` = (partials, blocks per sample,
+        positions per block), else None)."""
+        self.gn_part = None
         N, H, W, C = x.shape
         assert C == self.cin_p and N % G == 0, (x.shape, self.cin_p, G)
         Ho, Wo = self.out_hw(H, W)
@@ -270,9 +281,20 @@ class GroupedConv:
             conv_fwd(x.data_ptr(), self._fold_w(wp, G).data_ptr(), y.data_ptr(), G, N // G, 1, H, W, self.cin_p,
                      self.cout, 1, 1, 0, 0, x.device)
             return y
-        if self.kt == 9 and self.stride == 1 and self.pad == 1 and slab_conv2d(
-                x.data_ptr(), wp.data_ptr(), y.data_ptr(), G, N // G, H, W, self.cin_p, self.cout, x.device):
-            return y
+        if self.kt == 9 and self.stride == 1 and self.pad == 1:
+            st = None
+            if gn_stats and (H * W) % 256 == 0:
+                zb = self._zb.get(G)
+                if zb is None:
+                    zb = self._zb[G] = torch.zeros(G, self.cout, device=x.device, dtype=torch.float32)
+                part = torch.empty(N * (H * W // 256) * self.cout * 2, device=x.device, dtype=torch.float32)
+                st = (zb.data_ptr(), part.data_ptr())
+            r = slab_conv2d(x.data_ptr(), wp.data_ptr(), y.data_ptr(), G, N // G, H, W, self.cin_p, self.cout,
+                            x.device, stats=st)
+            if r == 2:
+                self.gn_part = (part, H * W // 256, 256)
+            if r:
+                return y
         conv_fwd(x.data_ptr(), wp.data_ptr(), y.data_ptr(), G, N // G, 1, H, W, self.cin_p, self.cout,
                  self.kt, self.stride, self.pad, 0, x.device)
         return y
@@ -424,6 +446,12 @@ _FORK_GROUP = os.environ.get("NIDT_FORK_GROUP", "1") == "1"
 # shortcut norm backward read none either.  NIDT_GN_RMASK=0 / NIDT_OMASK2D=0: the mask tensors (A/B)
 _GN_RMASK = os.environ.get("NIDT_GN_RMASK", "1") != "0"
 _OMASK2D = os.environ.get("NIDT_OMASK2D", "1") != "0"
+# [GN-EPI] NIDT_GN_EPI=1: GroupNorm statistics from the epilogue of the slab conv that produces its input (layers whose
+# 256-position conv blocks lie inside one sample: the 32x32 / 16x16 CIFAR maps, 64x64 / 32x32 Tiny), then a streaming
+# apply pass (gn.hip k_gn_apply, 4.7-6.2 TB/s) instead of the one-block-per-sample k_gn_fwd.  Off by default: the
+# statistics epilogue adds more to the conv (64-channel slab blocks 261 -> 331 us at DisPFL's 100 clients) than the
+# apply pass saves (CIFAR SubAvg -1.7 %, DisPFL -1.8 %; profiles/r6_gn_epi.txt)
+_GN_EPI = os.environ.get("NIDT_GN_EPI", "0") == "1"
 # [STEM-FOLD] the 3-channel stem as a 1x1 conv over the window-folded input (img.hip k_img_fold); NIDT_STEM_FOLD=0:
 # the channel-padded 9-tap conv (A/B)
 _STEM_FOLD = os.environ.get("NIDT_STEM_FOLD", "1") != "0"
@@ -577,14 +605,21 @@ class GroupNormG:
     def _affine(self, theta):
         return theta[:, self.off_w:self.off_w + self.C], theta[:, self.off_b:self.off_b + self.C]
 
-    def fwd(self, t, theta, G, res=None, relu=False):
-        """t [N, H, W, C] -> (relu?(gn(t) + res) in t's dtype, saved statistics)."""
+    def fwd(self, t, theta, G, res=None, relu=False, part=None):
+        """t [N, H, W, C] -> (relu?(gn(t) + res) in t's dtype, saved statistics).  ``part`` ([GN-EPI]): the producing
+        conv's per-block statistics (``GroupedConv.gn_part``): a streaming apply pass instead of the per-sample kernel."""
         N, H, W, C = t.shape
         if self.hip:
             t = t.contiguous()
             y = torch.empty_like(t)
             stats = torch.empty(N, GN_GROUPS, 2, device=t.device, dtype=torch.float32)
             r = res.contiguous() if res is not None else None
+            if part is not None:
+                pt, nb, bp = part
+                ops.ext().gn_apply(t.data_ptr(), r.data_ptr() if r is not None else 0, pt.data_ptr(), nb, bp,
+                                   theta.data_ptr(), theta.stride(0), self.off_w, self.off_b, y.data_ptr(),
+                                   stats.data_ptr(), N, N // G, H * W, C, int(relu), _stream())
+                return y, stats
             ops.ext().gn_fwd(t.data_ptr(), r.data_ptr() if r is not None else 0, theta.data_ptr(), theta.stride(0),
                              self.off_w, self.off_b, y.data_ptr(), stats.data_ptr(), N, N // G, H * W, C, int(relu),
                              _stream())
@@ -755,15 +790,15 @@ class GroupedResNet18GN:
             saved.append((x, t, st, a))
         for blk in self.blocks:
             xin = a
-            t1 = blk["c1"].fwd(xin, theta, G, train, packed)
-            h1, s1 = blk["n1"].fwd(t1, theta, G, relu=True)
-            t2 = blk["c2"].fwd(h1, theta, G, train, packed)
+            t1 = blk["c1"].fwd(xin, theta, G, train, packed, gn_stats=_GN_EPI)
+            h1, s1 = blk["n1"].fwd(t1, theta, G, relu=True, part=blk["c1"].gn_part)
+            t2 = blk["c2"].fwd(h1, theta, G, train, packed, gn_stats=_GN_EPI)
             if "cs" in blk:
                 ts = blk["cs"].fwd(xin, theta, G, train, packed)
                 ysc, ss = blk["ns"].fwd(ts, theta, G)
             else:
                 ts, ss, ysc = None, None, xin
-            a, s2 = blk["n2"].fwd(t2, theta, G, res=ysc, relu=True)
+            a, s2 = blk["n2"].fwd(t2, theta, G, res=ysc, relu=True, part=blk["c2"].gn_part)
             if train:
                 saved.append((xin, t1, s1, h1, t2, s2, ts, ss, a))
         return a, saved

@@ -509,3 +509,52 @@ def test_gn_recomputed_masks_bit_identical(monkeypatch):
         assert torch.equal(res[0][0], res[1][0]), hw
         assert torch.isfinite(res[1][1]).all() and float(res[1][1].abs().sum()) > 0
         assert torch.equal(res[0][1], res[1][1]), (hw, float((res[0][1] - res[1][1]).abs().max()))
+
+
+@pytest.mark.parametrize("hw", [32, 64])
+def test_gn_epilogue_statistics_match_gn_kernel(hw, monkeypatch):
+    """[GN-EPI]: GroupNorm forward from the slab conv epilogue's per-block statistics (conv2d_fwd_slab_stats +
+    k_gn_apply) against the per-sample k_gn_fwd on the same conv output: the normalised activations agree to bf16
+    rounding, the saved (mean, rstd) to fp32 rounding of the pre-/post-bf16 sums, and a whole train step's loss and
+    gradient rows stay close to the k_gn_fwd path (the statistics come from the fp32 accumulators, not the bf16 t)."""
+    from neuroimagedisttraining_amd.engine import resnet2d_hip as R
+    from neuroimagedisttraining_amd.engine.executor import padded_rows
+    from neuroimagedisttraining_amd.models import customized_resnet18
+    dev = _dev()
+    torch.manual_seed(hw)
+    G, B, C = 3, 4, 64
+    conv = R.GroupedConv(0, C, C, 3, 1, 1, hip=True)
+    gn = R.GroupNormG(conv.numel, conv.numel + C, C, hip=True)
+    P = conv.numel + 2 * C
+    theta = torch.zeros(G, (P + 63) // 64 * 64, device=dev)[:, :P]
+    theta[:, :conv.numel] = torch.randn(G, conv.numel, device=dev) * (2.0 / (9 * C)) ** 0.5
+    theta[:, conv.numel:] = torch.randn(G, 2 * C, device=dev)
+    x = torch.randn(G * B, hw, hw, C, device=dev).to(torch.bfloat16)
+    t = conv.fwd(x, theta, G, gn_stats=True)
+    assert conv.gn_part is not None and conv.gn_part[1] == hw * hw // 256
+    r = torch.randn_like(t.float()).to(torch.bfloat16)
+    y1, s1 = gn.fwd(t, theta, G, res=r, relu=True, part=conv.gn_part)
+    y0, s0 = gn.fwd(t, theta, G, res=r, relu=True)
+    torch.cuda.synchronize()
+    assert _rel(y1, y0) < 1e-2
+    assert torch.allclose(s1[..., 0], s0[..., 0], atol=2e-2) and torch.allclose(s1[..., 1], s0[..., 1], rtol=1e-2)
+    # whole step
+    m = customized_resnet18(class_num=10)
+    g = np.random.default_rng(hw)
+    x8 = torch.from_numpy(g.integers(0, 256, size=(G * B, hw, hw, 3)).astype(np.uint8))
+    yl = torch.from_numpy(g.integers(0, 10, size=G * B))
+    Pm = sum(p.numel() for p in m.parameters())
+    flat = torch.cat([p.detach().reshape(-1) for p in m.parameters()]).to(dev)
+    res = []
+    for on in (False, True):
+        monkeypatch.setattr(R, "_GN_EPI", on)
+        eng = R.ResNetHipEngine(m, x8, yl, dev)
+        th, gr = padded_rows(G, Pm, dev), padded_rows(G, Pm, dev)
+        th.copy_(flat.expand(G, -1))
+        loss = eng.train_step(th, None, gr, torch.arange(G * B, dtype=torch.int32, device=dev), G, B, 1.0, 0)
+        torch.cuda.synchronize()
+        res.append((loss.clone(), gr.clone()))
+    assert torch.allclose(res[0][0], res[1][0], atol=2e-2), (res[0][0], res[1][0])
+    for gi in range(G):
+        a, b = res[0][1][gi], res[1][1][gi]
+        assert float(a @ b / (a.norm() * b.norm())) > 0.99
