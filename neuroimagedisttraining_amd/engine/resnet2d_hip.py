@@ -224,7 +224,10 @@ class GroupedConv:
         # folded into its channels (img.hip k_img_fold, channel 3 t + c), so the layer runs as a 1x1 conv over
         # K = 27 (padded to cin_p) with the folded weight image [Cout][27 -> cin_p]
         self.fold = False
-        self._wf = {}  # folded weight image per G (persistent: its zero tail is written once)
+        # folded weight image per packed-image buffer (persistent: its zero tail is written once).  Keyed by the
+        # buffer, not by G: launches of different shapes with the same G (a partial-batch step on a side lane beside
+        # a full-batch step, concurrent evaluation lanes) must not share one
+        self._wf = {}
         self._zb = {}  # [GN-EPI] zero bias per G (the statistics epilogue runs on the bias path)
         self.gn_part = None
 
@@ -235,9 +238,10 @@ class GroupedConv:
     def _fold_w(self, wp, G):
         """[G, Cout, 1, cin_p] folded image from the step's 9-tap image wp [G, Cout, 9, cin_p] (channels < 3 live):
         wf[g, co, 3 t + c] = wp[g, co, t, c] (one strided copy; the 27 .. cin_p-1 tail stays zero)."""
-        wf = self._wf.get(G)
+        key = (wp.data_ptr(), G)
+        wf = self._wf.get(key)
         if wf is None:
-            wf = self._wf[G] = torch.zeros(G, self.cout, 1, self.cin_p, device=wp.device, dtype=torch.bfloat16)
+            wf = self._wf[key] = torch.zeros(G, self.cout, 1, self.cin_p, device=wp.device, dtype=torch.bfloat16)
         wf.view(G, self.cout, self.cin_p)[:, :, :self.kt * self.cin].view(G, self.cout, self.kt, self.cin).copy_(
             wp.view(G, self.cout, self.kt, self.cin_p)[..., :self.cin])
         return wf
