@@ -124,10 +124,12 @@ __device__ __forceinline__ void conv_fwd_epilogue(const ConvFwdArgs& a, f32x4 (&
     }
   }
   if (STATS) {
-    // pass 1: block sums per channel (valid positions only)
-    // red: [WN (wp)][BCO] floats of LDS scratch
-    const int cnt = min(BP, me - mb);
-    float s_[TCO][4];
+    // [WSTATS] each wave's (mean, M2) per channel over its own WP positions (two passes, shuffles only: the wave mean
+    // needs no block-wide round), then ONE LDS round: the WN wave partials merged per channel (Chan: mean = count-
+    // weighted mean of the wave means, M2 = sum M2 + sum cnt (wave mean - mean)^2).  Two barriers instead of four.
+    // red: [WN (wp)][BCO][2] floats of LDS scratch
+    const int cntw = max(0, min(WP, me - (mb + wp * WP)));  // valid positions of this wave (uniform)
+    float m_[TCO][4], q_[TCO][4];
 #pragma unroll
     for (int i = 0; i < TCO; ++i)
 #pragma unroll
@@ -140,69 +142,52 @@ __device__ __forceinline__ void conv_fwd_epilogue(const ConvFwdArgs& a, f32x4 (&
         s += __shfl_xor(s, 2, 64);
         s += __shfl_xor(s, 4, 64);
         s += __shfl_xor(s, 8, 64);
-        s_[i][r] = s;
-      }
-    __syncthreads();
-    if (fr == 0) {
-#pragma unroll
-      for (int i = 0; i < TCO; ++i)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) red[wp * BCO + wco * WCO + i * 16 + 4 * fq + r] = s_[i][r];
-    }
-    __syncthreads();
-    float mean_[TCO][4];
-#pragma unroll
-    for (int i = 0; i < TCO; ++i)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int c = wco * WCO + i * 16 + 4 * fq + r;
-        float t = 0.f;
-#pragma unroll
-        for (int q = 0; q < WN; ++q) t += red[q * BCO + c];
-        mean_[i][r] = t / (float)cnt;
-      }
-    __syncthreads();
-#pragma unroll
-    for (int i = 0; i < TCO; ++i)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        float s = 0.f;
+        const float mw = cntw > 0 ? s / (float)cntw : 0.f;
+        float q = 0.f;
 #pragma unroll
         for (int j = 0; j < TP; ++j)
           if (posw + j * 16 < me) {
-            const float d = acc[i][j][r] + bias_r[i][r] - mean_[i][r];
-            s = fmaf(d, d, s);
+            const float d = acc[i][j][r] + bias_r[i][r] - mw;
+            q = fmaf(d, d, q);
           }
-        s += __shfl_xor(s, 1, 64);
-        s += __shfl_xor(s, 2, 64);
-        s += __shfl_xor(s, 4, 64);
-        s += __shfl_xor(s, 8, 64);
-        s_[i][r] = s;
+        q += __shfl_xor(q, 1, 64);
+        q += __shfl_xor(q, 2, 64);
+        q += __shfl_xor(q, 4, 64);
+        q += __shfl_xor(q, 8, 64);
+        m_[i][r] = mw;
+        q_[i][r] = q;
       }
+    __syncthreads();  // red aliases the operand staging
     if (fr == 0) {
-#pragma unroll
-      for (int i = 0; i < TCO; ++i)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) red[wp * BCO + wco * WCO + i * 16 + 4 * fq + r] = s_[i][r];
-    }
-    __syncthreads();
-    for (int c = tid; c < BCO; c += (int)blockDim.x) {
-      float* st = a.stats + (((int64_t)g * a.nPB + pb) * a.Cout + co0 + c) * 2;
-      // recompute mean for this channel from the first pass is not available here; store via second array
-      float t = 0.f;
-#pragma unroll
-      for (int q = 0; q < WN; ++q) t += red[q * BCO + c];
-      st[1] = t;
-    }
-    // means: write by the owning lanes (every (wco, i, fq, r) channel is owned by the fr==0, wp==0 lanes)
-    if (fr == 0 && wp == 0) {
 #pragma unroll
       for (int i = 0; i < TCO; ++i)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int c = wco * WCO + i * 16 + 4 * fq + r;
-          a.stats[(((int64_t)g * a.nPB + pb) * a.Cout + co0 + c) * 2] = mean_[i][r];
+          float* e = red + 2 * (wp * BCO + wco * WCO + i * 16 + 4 * fq + r);
+          e[0] = m_[i][r];
+          e[1] = q_[i][r];
         }
+    }
+    __syncthreads();
+    for (int c = tid; c < BCO; c += (int)blockDim.x) {
+      float n = 0.f, sm = 0.f;
+#pragma unroll
+      for (int w = 0; w < WN; ++w) {
+        const float cw = (float)max(0, min(WP, me - (mb + w * WP)));
+        n += cw;
+        sm = fmaf(cw, red[2 * (w * BCO + c)], sm);
+      }
+      const float mean = n > 0.f ? sm / n : 0.f;
+      float m2 = 0.f;
+#pragma unroll
+      for (int w = 0; w < WN; ++w) {
+        const float cw = (float)max(0, min(WP, me - (mb + w * WP)));
+        const float d = red[2 * (w * BCO + c)] - mean;
+        m2 += red[2 * (w * BCO + c) + 1] + cw * d * d;
+      }
+      float* st = a.stats + (((int64_t)g * a.nPB + pb) * a.Cout + co0 + c) * 2;
+      st[0] = mean;
+      st[1] = m2;
     }
   }
 }
