@@ -80,6 +80,21 @@ __device__ __forceinline__ uint4 xform8(uint4 v, const float* s, const float* t,
   return make_uint4(u[0], u[1], u[2], u[3]);
 }
 
+// [DPP-SUM] sum over the 16 lanes of a DPP row, every lane getting the same total: quad swaps (lane ^ 1, lane ^ 2),
+// then the half-row and row mirrors — four v_add_f32 with a DPP source operand instead of four __shfl_xor
+// (ds_bpermute_b32: an LDS-pipeline round trip each; profiles/r6_dpp_stats.txt).
+template <int CTRL>
+__device__ __forceinline__ float dpp_f32(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xf, 0xf, false));
+}
+__device__ __forceinline__ float row_sum16(float s) {
+  s += dpp_f32<0xB1>(s);   // quad_perm [1, 0, 3, 2]
+  s += dpp_f32<0x4E>(s);   // quad_perm [2, 3, 0, 1]
+  s += dpp_f32<0x141>(s);  // row_half_mirror: lane i <- 7 - i within each 8
+  s += dpp_f32<0x140>(s);  // row_mirror: lane i <- 15 - i
+  return s;
+}
+
 // Shared epilogue of the forward kernels: bias, bf16 store, per-block BN statistics (block mean + M2 per
 // channel).  C layout (16x16x32): C[row = 4*fq + r][col = fr]; rows = co, cols = positions.
 template <int BCO, int BP, int WM, int WN, bool BIAS, bool STATS, int TCO, int TP>
@@ -138,10 +153,7 @@ __device__ __forceinline__ void conv_fwd_epilogue(const ConvFwdArgs& a, f32x4 (&
 #pragma unroll
         for (int j = 0; j < TP; ++j)
           if (posw + j * 16 < me) s += acc[i][j][r] + bias_r[i][r];
-        s += __shfl_xor(s, 1, 64);
-        s += __shfl_xor(s, 2, 64);
-        s += __shfl_xor(s, 4, 64);
-        s += __shfl_xor(s, 8, 64);
+        s = row_sum16(s);
         const float mw = cntw > 0 ? s / (float)cntw : 0.f;
         float q = 0.f;
 #pragma unroll
@@ -150,10 +162,7 @@ __device__ __forceinline__ void conv_fwd_epilogue(const ConvFwdArgs& a, f32x4 (&
             const float d = acc[i][j][r] + bias_r[i][r] - mw;
             q = fmaf(d, d, q);
           }
-        q += __shfl_xor(q, 1, 64);
-        q += __shfl_xor(q, 2, 64);
-        q += __shfl_xor(q, 4, 64);
-        q += __shfl_xor(q, 8, 64);
+        q = row_sum16(q);
         m_[i][r] = mw;
         q_[i][r] = q;
       }
