@@ -139,7 +139,7 @@ __device__ __forceinline__ void conv_fwd_epilogue(const ConvFwdArgs& a, f32x4 (&
     }
   }
   if (STATS) {
-    // [WSTATS] each wave's (mean, M2) per channel over its own WP positions (two passes, shuffles only: the wave mean
+    // [WSTATS] each wave's (mean, M2) per channel over its own WP positions (one pass, DPP only: the wave mean
     // needs no block-wide round), then ONE LDS round: the WN wave partials merged per channel (Chan: mean = count-
     // weighted mean of the wave means, M2 = sum M2 + sum cnt (wave mean - mean)^2).  Two barriers instead of four.
     // red: [WN (wp)][BCO][2] floats of LDS scratch
@@ -149,22 +149,22 @@ __device__ __forceinline__ void conv_fwd_epilogue(const ConvFwdArgs& a, f32x4 (&
     for (int i = 0; i < TCO; ++i)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        float s = 0.f;
-#pragma unroll
-        for (int j = 0; j < TP; ++j)
-          if (posw + j * 16 < me) s += acc[i][j][r] + bias_r[i][r];
-        s = row_sum16(s);
-        const float mw = cntw > 0 ? s / (float)cntw : 0.f;
-        float q = 0.f;
+        // [ONEPASS] sum and sum of squares of the bias-free accumulators in one sweep (the bias is uniform over the
+        // 16 reduced lanes, so it only shifts the mean); the two DPP chains are independent and interleave.  A wave
+        // covers <= 64 positions, so the fp32 cancellation in q - s*mean stays ~1e-6 relative for |mean|/std < 30.
+        float s = 0.f, q = 0.f;
 #pragma unroll
         for (int j = 0; j < TP; ++j)
           if (posw + j * 16 < me) {
-            const float d = acc[i][j][r] + bias_r[i][r] - mw;
-            q = fmaf(d, d, q);
+            const float v = acc[i][j][r];
+            s += v;
+            q = fmaf(v, v, q);
           }
+        s = row_sum16(s);
         q = row_sum16(q);
-        m_[i][r] = mw;
-        q_[i][r] = q;
+        const float mw = cntw > 0 ? s / (float)cntw : 0.f;
+        m_[i][r] = mw + bias_r[i][r];
+        q_[i][r] = fmaxf(q - s * mw, 0.f);
       }
     __syncthreads();  // red aliases the operand staging
     if (fr == 0) {
