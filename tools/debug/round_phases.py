@@ -50,21 +50,30 @@ wrap(MK.MaskSpace, "hamming")
 wrap(RU.FLRunner, "state_nonzeros")
 wrap(PE.SubAvgRunner, "_real_prune_rows")
 wrap(RU.FLRunner, "end_of_training")
-orig_round = PE.SubAvgRunner.run_round
+# DisPFL's round (personalized.py DisPFLRunner.run_round)
+wrap(PE.PersonalizedRunner, "eval_local")
+wrap(PE.PersonalizedRunner, "snapshot")
+wrap(RU.FLRunner, "local_grad")
+wrap(MK.MaskSpace, "select")
+wrap(MK.MaskSpace, "popcount")
+wrap(PE.DisPFLRunner, "_aggregate_neighbours")
 rounds = []
 
 
-def run_round(self, *a, **k):
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    before = dict(tot)
-    r = orig_round(self, *a, **k)
-    torch.cuda.synchronize()
-    rounds.append((time.perf_counter() - t0, {kk: tot[kk] - before.get(kk, 0.0) for kk in tot}))
-    return r
+def timed_round(orig_round):
+    def run_round(self, *a, **k):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        before = dict(tot)
+        r = orig_round(self, *a, **k)
+        torch.cuda.synchronize()
+        rounds.append((time.perf_counter() - t0, {kk: tot[kk] - before.get(kk, 0.0) for kk in tot}))
+        return r
+    return run_round
 
 
-PE.SubAvgRunner.run_round = run_round
+for cls in (PE.SubAvgRunner, PE.DisPFLRunner):
+    cls.run_round = timed_round(cls.run_round)
 sys.argv = ["bench_cifar.py"] + sys.argv[1:]
 try:
     runpy.run_path(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "bench_cifar.py"),
