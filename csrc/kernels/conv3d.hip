@@ -149,22 +149,25 @@ __device__ __forceinline__ void conv_fwd_epilogue(const ConvFwdArgs& a, f32x4 (&
     for (int i = 0; i < TCO; ++i)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        // [ONEPASS] sum and sum of squares of the bias-free accumulators in one sweep (the bias is uniform over the
-        // 16 reduced lanes, so it only shifts the mean); the two DPP chains are independent and interleave.  A wave
-        // covers <= 64 positions, so the fp32 cancellation in q - s*mean stays ~1e-6 relative for |mean|/std < 30.
+        // [ONEPASS] sum and sum of squares in one sweep, shifted by one sample of the channel (the row's lane 0,
+        // first position: row_newbcast:0 hands it to the 16 reduced lanes; valid whenever cntw > 0), so q - s^2/n
+        // cancels only at the channel's spread, not its mean (exact shifted-data variance; the bias only moves the
+        // mean).  The two DPP chains are independent and interleave.
+        const float k0 = __int_as_float(
+            __builtin_amdgcn_update_dpp(0, __float_as_int(acc[i][0][r]), 0x150, 0xf, 0xf, false));
         float s = 0.f, q = 0.f;
 #pragma unroll
         for (int j = 0; j < TP; ++j)
           if (posw + j * 16 < me) {
-            const float v = acc[i][j][r];
+            const float v = acc[i][j][r] - k0;
             s += v;
             q = fmaf(v, v, q);
           }
         s = row_sum16(s);
         q = row_sum16(q);
-        const float mw = cntw > 0 ? s / (float)cntw : 0.f;
-        m_[i][r] = mw + bias_r[i][r];
-        q_[i][r] = fmaxf(q - s * mw, 0.f);
+        const float dw = cntw > 0 ? s / (float)cntw : 0.f;
+        m_[i][r] = (cntw > 0 ? k0 + dw : 0.f) + bias_r[i][r];
+        q_[i][r] = fmaxf(q - s * dw, 0.f);
       }
     __syncthreads();  // red aliases the operand staging
     if (fr == 0) {

@@ -92,32 +92,75 @@ def test_conv3d_fwd_stats(cin, cout, pad, sp, xf, G, B):
     assert _relerr(mean, yr_g.mean(1)) < 1e-3
     assert _relerr(var, yr_g.var(1, unbiased=False)) < 1e-3
     if not xf and bp == 256 and m.conv3d_fwd_tri_ok(B, *sp, cin, cout, pad):
-        # union-staged B operand (k_conv_fwd_tri) against the per-tap kernel and, without bias, the fp32 oracle
-        tab = torch.empty(m.conv3d_fwd_tri_table_size(B, *sp, pad), device=DEV, dtype=torch.int32)
-        m.conv3d_fwd_tri_table(tab.data_ptr(), B, *sp, pad, _st())
-        y3 = torch.empty_like(y)
-        st3 = torch.empty_like(stats)
-        m.conv3d_fwd_tri(x.data_ptr(), w.data_ptr(), bias.data_ptr(), 0, y3.data_ptr(), st3.data_ptr(), G, B, *sp, cin,
-                         cout, pad, tab.data_ptr(), _st())
-        y4 = torch.empty_like(y)  # no bias / statistics (the dgrad form)
-        m.conv3d_fwd_tri(x.data_ptr(), w.data_ptr(), 0, 0, y4.data_ptr(), 0, G, B, *sp, cin, cout, pad, tab.data_ptr(),
-                         _st())
-        torch.cuda.synchronize()
-        # same products; the k order differs when Cin > 64 (triplet-major vs tap-major) -> fp32 rounding only
-        assert (y3.float() - y.float()).abs().max() <= 1e-2 * y.float().abs().max()
-        assert _relerr(st3, stats) < 1e-4
-        assert _relerr(y4.float(), (yr.view(G, -1, cout) - bias.view(G, 1, cout)).view_as(yr)) < 1e-2
+        _check_tri(m, x, w, bias, y, yr, stats, G, B, sp, cin, cout, pad)
     if not xf and bp == 256 and m.conv3d_fwd_slab_ok(B, *sp, cin, cout, pad):
-        # kd-slab union staging (k_conv_fwd_slab): same products as the per-tap kernel, slab-major k order
-        tab = torch.empty(m.conv3d_fwd_slab_table_size(B, *sp, pad), device=DEV, dtype=torch.int32)
-        m.conv3d_fwd_slab_table(tab.data_ptr(), B, *sp, pad, _st())
-        y5 = torch.empty_like(y)
-        st5 = torch.empty_like(stats)
-        m.conv3d_fwd_slab(x.data_ptr(), w.data_ptr(), bias.data_ptr(), 0, y5.data_ptr(), st5.data_ptr(), G, B, *sp,
-                          cin, cout, pad, tab.data_ptr(), _st())
-        torch.cuda.synchronize()
-        assert (y5.float() - y.float()).abs().max() <= 1e-2 * y.float().abs().max()
-        assert _relerr(st5, stats) < 1e-4
+        _check_slab(m, x, w, bias, y, stats, G, B, sp, cin, cout, pad)
+
+
+@pytest.mark.parametrize("cin,cout,pad,sp,G,B", [(192, 128, 0, (7, 9, 7), 2, 3), (192, 128, 0, (7, 9, 7), 8, 16),
+                                                 (64, 128, 0, (19, 23, 19), 2, 2)])
+def test_conv3d_fwd_stats_large_mean(cin, cout, pad, sp, G, B):
+    """Conv outputs whose channel mean is 50-100x their spread (positive inputs and weights, no padding, so every
+    output sums the same number of taps): the one-pass statistics epilogue must not lose the variance to fp32
+    cancellation (its sums are shifted by a sample of the channel)."""
+    m = _m()
+    torch.manual_seed(3)
+    x = (torch.rand(G * B, *sp, cin, device=DEV) + 0.5).bfloat16()
+    w = (torch.rand(G, cout, 27, cin, device=DEV) * 0.05).bfloat16()
+    bias = torch.randn(G, cout, device=DEV) * 0.1
+    Do, Ho, Wo = [s + 2 * pad - 2 for s in sp]
+    y = torch.empty(G * B, Do, Ho, Wo, cout, device=DEV, dtype=torch.bfloat16)
+    Mg = B * Do * Ho * Wo
+    bp = m.conv3d_fwd_bp(cin, cout, 0, G, Mg)
+    npb = m.conv3d_fwd_nblocks(B, *sp, pad, bp)
+    stats = torch.empty(G, npb, cout, 2, device=DEV)
+    m.conv3d_fwd(x.data_ptr(), w.data_ptr(), bias.data_ptr(), 0, 0, y.data_ptr(), stats.data_ptr(), G, B, *sp, cin,
+                 cout, pad, _st())
+    torch.cuda.synchronize()
+    ys = []
+    for g in range(G):
+        wg = w[g].double().view(cout, 3, 3, 3, cin).permute(0, 4, 1, 2, 3)
+        ys.append(_cl(F.conv3d(_cf(x[g * B:(g + 1) * B].double()), wg, bias[g].double(), 1, pad)))
+    yr_g = torch.cat(ys, 0).view(G, Mg, cout)
+    cnt = torch.tensor([min(bp, Mg - b * bp) for b in range(npb)], device=DEV, dtype=torch.float64)
+    mean_b, m2_b = stats[..., 0].double(), stats[..., 1].double()
+    mean = (mean_b * cnt.view(1, -1, 1)).sum(1) / Mg
+    var = (m2_b + cnt.view(1, -1, 1) * (mean_b - mean.unsqueeze(1)) ** 2).sum(1) / Mg
+    vr = yr_g.var(1, unbiased=False)
+    assert float((yr_g.mean(1).abs() / vr.sqrt()).median()) > 50  # the regime this test is for
+    assert _relerr(mean, yr_g.mean(1)) < 1e-5
+    assert _relerr(var, vr) < 2e-3
+
+
+def _check_tri(m, x, w, bias, y, yr, stats, G, B, sp, cin, cout, pad):
+    # union-staged B operand (k_conv_fwd_tri) against the per-tap kernel and, without bias, the fp32 oracle
+    tab = torch.empty(m.conv3d_fwd_tri_table_size(B, *sp, pad), device=DEV, dtype=torch.int32)
+    m.conv3d_fwd_tri_table(tab.data_ptr(), B, *sp, pad, _st())
+    y3 = torch.empty_like(y)
+    st3 = torch.empty_like(stats)
+    m.conv3d_fwd_tri(x.data_ptr(), w.data_ptr(), bias.data_ptr(), 0, y3.data_ptr(), st3.data_ptr(), G, B, *sp, cin,
+                     cout, pad, tab.data_ptr(), _st())
+    y4 = torch.empty_like(y)  # no bias / statistics (the dgrad form)
+    m.conv3d_fwd_tri(x.data_ptr(), w.data_ptr(), 0, 0, y4.data_ptr(), 0, G, B, *sp, cin, cout, pad, tab.data_ptr(),
+                     _st())
+    torch.cuda.synchronize()
+    # same products; the k order differs when Cin > 64 (triplet-major vs tap-major) -> fp32 rounding only
+    assert (y3.float() - y.float()).abs().max() <= 1e-2 * y.float().abs().max()
+    assert _relerr(st3, stats) < 1e-4
+    assert _relerr(y4.float(), (yr.view(G, -1, cout) - bias.view(G, 1, cout)).view_as(yr)) < 1e-2
+
+
+def _check_slab(m, x, w, bias, y, stats, G, B, sp, cin, cout, pad):
+    # kd-slab union staging (k_conv_fwd_slab): same products as the per-tap kernel, slab-major k order
+    tab = torch.empty(m.conv3d_fwd_slab_table_size(B, *sp, pad), device=DEV, dtype=torch.int32)
+    m.conv3d_fwd_slab_table(tab.data_ptr(), B, *sp, pad, _st())
+    y5 = torch.empty_like(y)
+    st5 = torch.empty_like(stats)
+    m.conv3d_fwd_slab(x.data_ptr(), w.data_ptr(), bias.data_ptr(), 0, y5.data_ptr(), st5.data_ptr(), G, B, *sp,
+                      cin, cout, pad, tab.data_ptr(), _st())
+    torch.cuda.synchronize()
+    assert (y5.float() - y.float()).abs().max() <= 1e-2 * y.float().abs().max()
+    assert _relerr(st5, stats) < 1e-4
 
 
 @pytest.mark.parametrize("cin,cout,pad,sp", [(64, 128, 0, (19, 23, 19)), (128, 64, 2, (17, 21, 17)),
