@@ -238,7 +238,8 @@ def run(args):
                    dense_ratio=args.dense_ratio, seed=args.seed, group=args.group, frac=args.frac,
                    frequency_of_the_test=0 if args.no_eval else 1, aggregator=args.aggregator,
                    prox_mu=args.prox_mu if args.algorithm == "fedprox" else 0.0, cs=args.cs, final_round=False,
-                   rebalance=rebalance, step_streams=args.step_streams, hip_graphs=cuda)
+                   rebalance=rebalance, step_streams=args.step_streams,
+                   hip_graphs=None if cuda else False)  # None: the engine's per-launch-size default
     runner = make_runner(args.algorithm, engine, splits, cfg, info, model, logger=None)
     t0 = time.perf_counter()
     if runner.alg == "salientgrads":

@@ -28,10 +28,26 @@ L3 = (8, 9, 128, 192, 1, (5, 7, 5))
 L4 = (11, 12, 192, 192, 1, (5, 7, 5))
 L5 = (14, 15, 192, 128, 1, (5, 7, 5))
 NM = 125 + 125 * 125
-# weight gradients on a forked branch of the step (see train_step) with NIDT_AX_WGRAD_STREAM=1: measured no faster
-# (kbench 23.3 vs 23.2 ms per 64-client step, bench 2.08-2.10 vs 2.10-2.11 r/s: profiles/r3_ab_wgrad_stream.txt).
+# [EAGER-BRANCH] weight gradients on a forked branch of the step (see train_step).  Captured steps run without it
+# (64 clients: no faster, profiles/r3_ab_wgrad_stream.txt; 8 clients captured with the branch -1.0 %).  Launches of
+# <= NIDT_AX_EAGER_MAXG clients (default 32: the per-GPU loads of the 2-, 4- and 8-GPU strong-scaling bench) run
+# EAGER steps with the branch instead: 8 / 16 / 32 clients +1.7 / +2.9 / +2.0 % over captured steps without it,
+# 64 clients -4.2 % (stays captured) (profiles/r6_eager_branch.txt).  HipEngine.graphs_default_for picks the mode
+# per trained row set; NIDT_AX_WGRAD_STREAM=0 / 1 forces the branch off / on for every launch.
 # NIDT_WG2_EARLY=1 forks the conv2 wgrad before the conv2 dgrad instead of after it (beside the conv1 wgrad).
-_WGRAD_STREAM = os.environ.get("NIDT_AX_WGRAD_STREAM", "0") == "1"
+_WS_ENV = os.environ.get("NIDT_AX_WGRAD_STREAM")
+_EAGER_MAXG = int(os.environ.get("NIDT_AX_EAGER_MAXG", "32"))
+
+
+def eager_branch(G):
+    """Launches of G clients train in eager steps with the weight-gradient branch ([EAGER-BRANCH])."""
+    return G <= _EAGER_MAXG
+
+
+def _wgrad_branch(G):
+    if _WS_ENV is not None:
+        return _WS_ENV == "1"
+    return eager_branch(G) and not torch.cuda.is_current_stream_capturing()
 _WG2_EARLY = os.environ.get("NIDT_WG2_EARLY", "0") == "1"
 # conv2-5 weight packs batched into two pack.hip launches per step instead of eight: 8 clients per GPU +0.3%,
 # 64 within noise (profiles/r4_ab_alexnet_bpack.txt); NIDT_AX_BPACK=0: the per-layer packs (A/B)
@@ -380,7 +396,7 @@ class HipAlexNet3D:
         # conv3-5 grids fill each other's idle CUs, and the MFMA-bound conv2 wgrad runs beside the VALU-bound
         # conv1 sparse wgrad.  All wgrads are ordered on that one branch, so they share ``wgpart``.
         cur = torch.cuda.current_stream()
-        ws = b.get("wstream") if _WGRAD_STREAM else None
+        ws = b.get("wstream") if _wgrad_branch(G) else None
         wst = ws.cuda_stream if ws is not None else st
 
         def fork():

@@ -123,6 +123,13 @@ class HipEngine:
     supports_graphs = True
     input_shape = (1, 121, 145, 121)   # one sample as the model sees it (FLOP counting)
 
+    @staticmethod
+    def graphs_default_for(k):
+        """Captured steps for row sets of more than NIDT_AX_EAGER_MAXG clients, eager steps with the weight-gradient
+        branch below ([EAGER-BRANCH], alexnet_hip.py)."""
+        from .alexnet_hip import eager_branch
+        return not eager_branch(k)
+
     accepts_cids_dev = True  # train_step(cids_dev=...): client ids from a device buffer (graph reuse across groups)
 
     # [PACK-FUSE] the optimizer step may write the next train step's conv2-5 forward images (runner: pack_next /

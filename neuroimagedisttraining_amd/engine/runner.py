@@ -363,7 +363,10 @@ class FLRunner:
         cfg = self.cfg
         lr = cfg.lr * (cfg.lr_decay ** round_idx) if lr is None else lr
         self._zero_mom(len(clients))
-        hg = cfg.hip_graphs if cfg.hip_graphs is not None else getattr(self.e, "graphs_default", True)
+        hg = cfg.hip_graphs
+        if hg is None:  # the engine's measured default, per trained row set where it depends on the launch size
+            f = getattr(self.e, "graphs_default_for", None)
+            hg = f(len(clients)) if f is not None else getattr(self.e, "graphs_default", True)
         use_graphs = (hg and getattr(self.e, "supports_graphs", False) and self.device.type == "cuda"
                       and os.environ.get("NIDT_HIP_GRAPHS", "1") != "0")  # NIDT_HIP_GRAPHS=0: eager steps (A/B)
         if self._lr_dev is None:

@@ -422,3 +422,20 @@ def test_flops_match_reference_multiply_adds_by_hand():
     sd = dict(m.named_parameters())
     got = sum(a * int(torch.count_nonzero(sd[n])) + b for n, (a, b) in coef.items())
     assert got == want
+
+
+def test_alexnet_step_mode_follows_launch_size(monkeypatch):
+    """[EAGER-BRANCH]: row sets of <= 32 clients (the per-GPU loads of the 2/4/8-GPU bench) train in eager steps with
+    the weight-gradient branch, larger ones in captured steps; FLConfig.hip_graphs still overrides in the runner."""
+    from neuroimagedisttraining_amd.engine import alexnet_hip as AX
+    from neuroimagedisttraining_amd.engine.executor import HipEngine
+    assert [HipEngine.graphs_default_for(k) for k in (1, 8, 16, 32, 33, 64)] == [False] * 4 + [True] * 2
+    monkeypatch.setattr(AX, "_WS_ENV", None)
+    monkeypatch.setattr(AX.torch.cuda, "is_current_stream_capturing", lambda: False)
+    assert AX._wgrad_branch(8) and not AX._wgrad_branch(64)
+    monkeypatch.setattr(AX.torch.cuda, "is_current_stream_capturing", lambda: True)
+    assert not AX._wgrad_branch(8)  # a captured step never forks the branch
+    monkeypatch.setattr(AX, "_WS_ENV", "0")
+    assert not AX._wgrad_branch(8)
+    monkeypatch.setattr(AX, "_WS_ENV", "1")
+    assert AX._wgrad_branch(64)
