@@ -34,8 +34,11 @@ NM = 125 + 125 * 125
 # EAGER steps with the branch instead: 8 / 16 / 32 clients +1.7 / +2.9 / +2.0 % over captured steps without it,
 # 64 clients -4.2 % (stays captured) (profiles/r6_eager_branch.txt).  HipEngine.graphs_default_for picks the mode
 # per trained row set; NIDT_AX_WGRAD_STREAM=0 / 1 forces the branch off / on for every launch.
-# NIDT_WG2_EARLY=1 forks the conv2 wgrad before the conv2 dgrad instead of after it (beside the conv1 wgrad).
+# [WG2-EARLY] with the branch, the conv2 wgrad is forked before the conv2 dgrad (beside it) for launches of <= 8
+# clients, after it (beside the conv1 wgrad) above: 8 clients +0.9 %, 16 / 32 clients -2.1 / -1.6 %
+# (profiles/r6_eager_branch.txt); NIDT_WG2_EARLY=0 / 1 forces it.
 _WS_ENV = os.environ.get("NIDT_AX_WGRAD_STREAM")
+_WG2_EARLY_ENV = os.environ.get("NIDT_WG2_EARLY")
 _EAGER_MAXG = int(os.environ.get("NIDT_AX_EAGER_MAXG", "32"))
 
 
@@ -44,11 +47,14 @@ def eager_branch(G):
     return G <= _EAGER_MAXG
 
 
+def _wg2_early(G):
+    return _WG2_EARLY_ENV == "1" if _WG2_EARLY_ENV is not None else G <= 8
+
+
 def _wgrad_branch(G):
     if _WS_ENV is not None:
         return _WS_ENV == "1"
     return eager_branch(G) and not torch.cuda.is_current_stream_capturing()
-_WG2_EARLY = os.environ.get("NIDT_WG2_EARLY", "0") == "1"
 # conv2-5 weight packs batched into two pack.hip launches per step instead of eight: 8 clients per GPU +0.3%,
 # 64 within noise (profiles/r4_ab_alexnet_bpack.txt); NIDT_AX_BPACK=0: the per-layer packs (A/B)
 _BPACK = os.environ.get("NIDT_AX_BPACK", "1") != "0"
@@ -432,11 +438,12 @@ class HipAlexNet3D:
         self._conv(b, "ksd8", b["dy3"], b["w8t"], None, b["dx3"], None, G, B, 5, 7, 5, 192, 128, 1, st)
         # layer 2: pool2 -> BN2 -> conv2
         bn_bwd(1, 4, 5, 128, (17, 21, 17), b["dx3"], b["p2"], b["a2"], b["dy2"], b["y2"])
-        if ws is None or _WG2_EARLY:
+        early = _wg2_early(G)
+        if ws is None or early:
             fork()
             wgrad(4, b["p1"], None, None, b["dy2"], (19, 23, 19), 64, 128, 0)
         self._conv(b, "ksd4", b["dy2"], b["w4t"], None, b["dp1"], None, G, B, 17, 21, 17, 128, 64, 2, st)
-        if ws is not None and not _WG2_EARLY:
+        if ws is not None and not early:
             fork()
             wgrad(4, b["p1"], None, None, b["dy2"], (19, 23, 19), 64, 128, 0)
         # layer 1: sparse wgrad through pool1/ReLU/BN1 (closed form; eval mode: running mean minus the conv bias)

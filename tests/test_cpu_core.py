@@ -439,3 +439,7 @@ def test_alexnet_step_mode_follows_launch_size(monkeypatch):
     assert not AX._wgrad_branch(8)
     monkeypatch.setattr(AX, "_WS_ENV", "1")
     assert AX._wgrad_branch(64)
+    monkeypatch.setattr(AX, "_WG2_EARLY_ENV", None)
+    assert AX._wg2_early(8) and not AX._wg2_early(16)
+    monkeypatch.setattr(AX, "_WG2_EARLY_ENV", "0")
+    assert not AX._wg2_early(8)
